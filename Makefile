@@ -1,0 +1,26 @@
+# Build of the MI355X (gfx950) hot-path library and the CPU oracle.
+#   make            -> sp-slam_amd/libspslam_gpu.so  and  oracle/liboracle.so
+# hipcc cross-compiles for gfx950 in the build container (no GPU needed).
+HIPCC ?= /opt/rocm/bin/hipcc
+OFFLOAD_ARCH ?= gfx950
+HIPFLAGS ?= --offload-arch=$(OFFLOAD_ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -fno-fast-math -Wall -Wno-unused-result
+
+PKG := sp-slam_amd
+CSRC := $(PKG)/csrc
+GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/spslam_capi.cpp
+GPU_HDRS := $(CSRC)/orb_geom.h $(CSRC)/orb_launch.h include/spslam_gpu.h include/spslam_brief_pattern.inc
+
+all: $(PKG)/libspslam_gpu.so oracle/liboracle.so
+
+$(PKG)/libspslam_gpu.so: $(GPU_SRCS) $(GPU_HDRS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip -x hip $(CSRC)/spslam_capi.cpp
+
+oracle/liboracle.so:
+	$(MAKE) -C oracle liboracle.so
+
+clean:
+	rm -f $(PKG)/libspslam_gpu.so
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle/liboracle.so

@@ -1,0 +1,169 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/liboracle.so, the CPU restatement of the reference
+hot path.  Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg (as the checker / CPU baseline, never as the product).
+Parity status: unpinned against the reference binary -- see orb_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import pathlib
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = HERE / "liboracle.so"
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(str(LIB_PATH))
+        vp, ip = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)
+        L.oracle_orb_new.restype = vp
+        L.oracle_orb_new.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_orb_free.argtypes = [vp]
+        for name in ("oracle_orb_features_per_level", "oracle_orb_umax"):
+            getattr(L, name).argtypes = [vp, ip]
+        L.oracle_orb_scale_tables.argtypes = [vp] + [ctypes.POINTER(ctypes.c_float)] * 4
+        L.oracle_orb_extract.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ip]
+        L.oracle_orb_pyramid.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_orb_level_size.argtypes = [vp, ctypes.c_int, ip, ip]
+        L.oracle_orb_level_image.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_orb_level_blurred.argtypes = [vp, ctypes.c_int, vp]
+        L.oracle_orb_level_candidates.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ip]
+        L.oracle_orb_level_keypoints.argtypes = [vp, ctypes.c_int, vp, ctypes.c_int, ip]
+        L.oracle_resize_linear.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ctypes.c_int]
+        L.oracle_gaussian_blur.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_fast.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ip]
+        for name in ("oracle_fast_atan2",):
+            getattr(L, name).restype = ctypes.c_float
+            getattr(L, name).argtypes = [ctypes.c_float, ctypes.c_float]
+        for name in ("oracle_sinf", "oracle_cosf"):
+            getattr(L, name).restype = ctypes.c_float
+            getattr(L, name).argtypes = [ctypes.c_float]
+        L.oracle_descriptor.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                        ctypes.c_float, vp]
+        _lib = L
+    return _lib
+
+
+class OrbOracle:
+    """CPU restatement of ORB_SLAM2::ORBextractor (src/ORBextractor.cc)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7):
+        self.L = lib()
+        self.h = self.L.oracle_orb_new(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast)
+        self.nlevels = nlevels
+
+    def __del__(self):
+        try:
+            self.L.oracle_orb_free(self.h)
+        except Exception:
+            pass
+
+    def features_per_level(self):
+        out = (ctypes.c_int * self.nlevels)()
+        self.L.oracle_orb_features_per_level(self.h, out)
+        return np.array(out[:])
+
+    def scale_tables(self):
+        arrs = [(ctypes.c_float * self.nlevels)() for _ in range(4)]
+        self.L.oracle_orb_scale_tables(self.h, *arrs)
+        return [np.array(a[:]) for a in arrs]
+
+    def umax(self):
+        out = (ctypes.c_int * 16)()
+        self.L.oracle_orb_umax(self.h, out)
+        return np.array(out[:])
+
+    def extract(self, gray: np.ndarray, cap: int = 8192):
+        gray = np.ascontiguousarray(gray, np.uint8)
+        h, w = gray.shape if gray.size else (0, 0)
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        rc = self.L.oracle_orb_extract(self.h, gray.ctypes.data if gray.size else None, w, h, w, kps.ctypes.data,
+                                       desc.ctypes.data, cap, ctypes.byref(n))
+        assert rc == 0
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def pyramid(self, gray: np.ndarray):
+        gray = np.ascontiguousarray(gray, np.uint8)
+        self.L.oracle_orb_pyramid(self.h, gray.ctypes.data, gray.shape[1], gray.shape[0], gray.shape[1])
+
+    def level_size(self, level):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        self.L.oracle_orb_level_size(self.h, level, ctypes.byref(w), ctypes.byref(h))
+        return w.value, h.value
+
+    def level_image(self, level):
+        w, h = self.level_size(level)
+        out = np.zeros((h, w), np.uint8)
+        self.L.oracle_orb_level_image(self.h, level, out.ctypes.data)
+        return out
+
+    def level_blurred(self, level):
+        w, h = self.level_size(level)
+        out = np.zeros((h, w), np.uint8)
+        self.L.oracle_orb_level_blurred(self.h, level, out.ctypes.data)
+        return out
+
+    def _kps(self, fn, level, cap=1 << 20):
+        out = np.zeros(cap, KEYPOINT_DTYPE)
+        n = ctypes.c_int()
+        assert fn(self.h, level, out.ctypes.data, cap, ctypes.byref(n)) == 0
+        return out[:n.value].copy()
+
+    def level_candidates(self, level):
+        return self._kps(self.L.oracle_orb_level_candidates, level)
+
+    def level_keypoints(self, level):
+        return self._kps(self.L.oracle_orb_level_keypoints, level, 8192)
+
+
+def resize_linear(src: np.ndarray, dw: int, dh: int) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib().oracle_resize_linear(src.ctypes.data, src.shape[1], src.shape[0], out.ctypes.data, dw, dh)
+    return out
+
+
+def gaussian_blur(src: np.ndarray) -> np.ndarray:
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros_like(src)
+    lib().oracle_gaussian_blur(src.ctypes.data, src.shape[1], src.shape[0], out.ctypes.data)
+    return out
+
+
+def fast(img: np.ndarray, thr: int, cap: int = 1 << 16):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros(cap, KEYPOINT_DTYPE)
+    n = ctypes.c_int()
+    assert lib().oracle_fast(img.ctypes.data, img.shape[1], img.shape[0], thr, out.ctypes.data, cap,
+                             ctypes.byref(n)) == 0
+    return out[:n.value].copy()
+
+
+def fast_atan2(y: float, x: float) -> float:
+    return lib().oracle_fast_atan2(y, x)
+
+
+def sinf(x: float) -> float:
+    return lib().oracle_sinf(x)
+
+
+def cosf(x: float) -> float:
+    return lib().oracle_cosf(x)
+
+
+def descriptor(img: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros(32, np.uint8)
+    lib().oracle_descriptor(img.ctypes.data, img.shape[1], img.shape[0], x, y, angle, out.ctypes.data)
+    return out

@@ -1,0 +1,54 @@
+// Level geometry of the ORB pyramid, shared by the host launcher and the
+// gfx950 kernels.  All derived sizes follow src/ORBextractor.cc exactly:
+// level size (:1111-1112), FAST cell grid (:769-787), per-level feature
+// quota (:435-446), scaled patch size (:837).
+#pragma once
+#include <cstdint>
+
+namespace spslam {
+
+constexpr int kMaxLevels = 8;
+constexpr int kEdgeThreshold = 19;     // src/ORBextractor.cc:74
+constexpr int kMinBorder = kEdgeThreshold - 3;
+constexpr int kCellCap = 512;          // max FAST survivors of one cell window (checked on host)
+constexpr int kCellWinMax = 72;        // max cell window side (LDS tile pitch)
+constexpr int kNodeCap = 1024;         // max DistributeOctTree list length (checked on host)
+
+struct LevelGeom {
+    int w, h;                 // level image size
+    int stride;               // row pitch in bytes of the level image
+    int pad_;
+    long long frame_stride;   // bytes between frames of this level
+    const uint8_t* img;       // level image, frame 0
+    uint8_t* blur;            // blurred level, frame 0 (pitch = w, frame stride = blur_frame_stride)
+    long long blur_frame_stride;
+    int maxBorderX, maxBorderY;
+    int nCols, nRows, wCell, hCell;
+    int cell_base;            // first cell of this level in the per-frame cell array
+    int nfeat;                // mnFeaturesPerLevel[level]
+    int kp_cap;               // per-level keypoint slot capacity
+    int kp_base;              // offset of the level's slot in the per-frame level-keypoint array
+    int key_base;             // offset of the level's key scratch (in keys) per frame
+    int patch_size;           // (int)(PATCH_SIZE * mvScaleFactor[level])
+    float scale;              // mvScaleFactor[level]
+    int pad2_;
+};
+
+struct OrbGeom {
+    LevelGeom lv[kMaxLevels];
+    int nlevels;
+    int cells_per_frame;
+    int lvl_kp_per_frame;     // sum of kp_cap over levels
+    int keys_per_frame;       // sum of ncells*kCellCap over levels
+    int blur_tiles_per_frame;
+    int pad_[3];
+};
+
+// Intermediate per-level keypoint (DistributeOctTree output, level coordinates).
+struct LevelKp {
+    uint16_t x, y;            // level pixel coordinates (integral in the reference)
+    uint16_t response;        // FAST score
+    uint16_t pad;
+};
+
+}  // namespace spslam

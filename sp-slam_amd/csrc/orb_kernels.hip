@@ -1,0 +1,715 @@
+// gfx950 kernels for SP-SLAM's ORB extractor (reference: src/ORBextractor.cc).
+//
+// One batched pass over B frames is five kernel kinds:
+//   resize_level_kernel   x7  pyramid level l from level l-1 (OpenCV INTER_LINEAR
+//                             8U fixed point, :1107-1132)
+//   fast_cells_kernel     x1  one wave per 30x30 FAST cell of every level: window
+//                             in LDS, FAST-9/16 score, 3x3 NMS at iniThFAST, retry
+//                             at minThFAST if the cell came back empty (:789-829)
+//   blur_kernel           x1  7x7 sigma-2 Gaussian of every level (:1085-1086)
+//   octree_kernel         x1  one workgroup per (frame, level): DistributeOctTree
+//                             (:539-763) as data-parallel passes over the keys
+//   desc_kernel           x1  one wave per keypoint: IC_Angle (:77-104) + rotated
+//                             BRIEF (:107-147), output assembly (:1075-1104)
+//
+// Floating point: built with -ffp-contract=off and correctly rounded fp32
+// division; the only fused multiply-adds are the explicit ones reproducing the
+// reference build's contraction of the BRIEF sample expression.
+#include <hip/hip_runtime.h>
+
+#include "../../include/spslam_gpu.h"
+#include "orb_launch.h"
+
+namespace spslam {
+
+__constant__ int8_t c_pattern[1024] = {
+#include "../../include/spslam_brief_pattern.inc"
+};
+__constant__ int c_umax[16];
+
+__device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
+
+// ---------------------------------------------------------------------------
+// Pyramid: OpenCV resize INTER_LINEAR on 8U (classic fixed-point path).
+// One thread per destination pixel; the per-column / per-row coefficients are
+// recomputed from the same double/float expressions OpenCV uses.
+__global__ __launch_bounds__(256) void resize_level_kernel(const uint8_t* __restrict__ src, int sw, int sh,
+                                                           int sstride, long long sfs, uint8_t* __restrict__ dst,
+                                                           int dw, int dh, int dstride, long long dfs) {
+    const int f = blockIdx.y;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= dw * dh) return;
+    const int dy = idx / dw, dx = idx - dy * dw;
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    bool tail = false;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= sw) {
+        tail = true;
+        if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    }
+    const int a0 = (short)cv_round((1.f - fx) * 2048.f), a1 = (short)cv_round(fx * 2048.f);
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = (int)floorf(fy);
+    fy -= sy;
+    const int b0 = (short)cv_round((1.f - fy) * 2048.f), b1 = (short)cv_round(fy * 2048.f);
+    const int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
+    const uint8_t* s = src + f * sfs;
+    const uint8_t* r0p = s + (size_t)y0 * sstride + sx;
+    const uint8_t* r1p = s + (size_t)y1 * sstride + sx;
+    int r0, r1;
+    if (!tail) {
+        r0 = r0p[0] * a0 + r0p[1] * a1;
+        r1 = r1p[0] * a0 + r1p[1] * a1;
+    } else {
+        r0 = r0p[0] * 2048;
+        r1 = r1p[0] * 2048;
+    }
+    dst[f * dfs + (size_t)dy * dstride + dx] =
+        (uint8_t)((((b0 * (r0 >> 4)) >> 16) + ((b1 * (r1 >> 4)) >> 16) + 2) >> 2);
+}
+
+// ---------------------------------------------------------------------------
+// FAST-9/16.  Score = max over the 16 contiguous 9-arcs of min(v - x) and of
+// min(x - v), minus 1; equals OpenCV cornerScore<16> for every corner, and
+// "corner at threshold t" <=> score >= t.
+__device__ __forceinline__ int fast_score(const uint8_t* p, int P) {
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * P];       d[1] = v - p[3 * P + 1];   d[2] = v - p[2 * P + 2];  d[3] = v - p[P + 3];
+    d[4] = v - p[3];           d[5] = v - p[-P + 3];      d[6] = v - p[-2 * P + 2]; d[7] = v - p[-3 * P + 1];
+    d[8] = v - p[-3 * P];      d[9] = v - p[-3 * P - 1];  d[10] = v - p[-2 * P - 2]; d[11] = v - p[-P - 3];
+    d[12] = v - p[-3];         d[13] = v - p[P - 3];      d[14] = v - p[2 * P - 2]; d[15] = v - p[3 * P - 1];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
+    int mn4[16], mx4[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
+    int best = -1000, worst = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
+        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
+        best = max(best, mn9);
+        worst = min(worst, mx9);
+    }
+    return max(best, -worst) - 1;
+}
+
+__device__ __forceinline__ int level_of_cell(const OrbGeom& g, int cid) {
+    int l = 0;
+    for (int k = 1; k < g.nlevels; k++)
+        if (cid >= g.lv[k].cell_base) l = k;
+    return l;
+}
+
+// One 64-lane wave per FAST cell.  Candidates are written in the reference's
+// order (row-major inside the cell), packed x | y << 12 | score << 24 with
+// (x, y) relative to (minBorderX, minBorderY) as at src/ORBextractor.cc:822-823.
+__global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
+                                                        uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
+    __shared__ uint8_t win[kCellWinMax * kCellWinMax];
+    __shared__ uint8_t sc[kCellWinMax * kCellWinMax];
+    const int cid = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+    const int l = level_of_cell(g, cid);
+    const LevelGeom& L = g.lv[l];
+    const int local = cid - L.cell_base;
+    const int ci = local / L.nCols, cj = local - ci * L.nCols;
+    const size_t cell_slot = (size_t)f * g.cells_per_frame + cid;
+    uint32_t* out = cand + cell_slot * kCellCap;
+    const int iniY = kMinBorder + ci * L.hCell, iniX = kMinBorder + cj * L.wCell;
+    if (iniY >= L.maxBorderY - 3 || iniX >= L.maxBorderX - 6) {
+        if (lane == 0) cand_cnt[cell_slot] = 0;
+        return;
+    }
+    const int maxY = min(iniY + L.hCell + 6, L.maxBorderY), maxX = min(iniX + L.wCell + 6, L.maxBorderX);
+    const int ww = maxX - iniX, wh = maxY - iniY;
+    const uint8_t* img = L.img + f * L.frame_stride + (size_t)iniY * L.stride + iniX;
+    for (int t = lane; t < ww * wh; t += 64) {
+        const int r = t / ww, c = t - r * ww;
+        win[r * kCellWinMax + c] = img[(size_t)r * L.stride + c];
+    }
+    __syncthreads();
+    const int R = wh - 6, C = ww - 6;
+    const int npx = (R > 0 && C > 0) ? R * C : 0;
+    for (int p = lane; p < npx; p += 64) {
+        const int r = 3 + p / C, c = 3 + p % C;
+        const int s = fast_score(&win[r * kCellWinMax + c], kCellWinMax);
+        sc[r * kCellWinMax + c] = (uint8_t)max(s, 0);
+    }
+    __syncthreads();
+    int base = 0;
+    for (int pass = 0; pass < 2; pass++) {
+        const int thr = pass == 0 ? iniTh : minTh;
+        base = 0;
+        for (int p0 = 0; p0 < npx; p0 += 64) {
+            const int p = p0 + lane;
+            bool keep = false;
+            int r = 0, c = 0, s = 0;
+            if (p < npx) {
+                r = 3 + p / C; c = 3 + p % C;
+                s = sc[r * kCellWinMax + c];
+                if (s >= thr) {
+                    keep = true;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; dx++) {
+                            if (!dy && !dx) continue;
+                            const int rr = r + dy, cc = c + dx;
+                            int n = 0;
+                            if (rr >= 3 && rr < wh - 3 && cc >= 3 && cc < ww - 3) n = sc[rr * kCellWinMax + cc];
+                            if (n < thr) n = 0;
+                            keep = keep && (s > n);
+                        }
+                }
+            }
+            const unsigned long long mask = __ballot(keep);
+            if (keep) {
+                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
+                out[pos] = (uint32_t)(c + cj * L.wCell) | ((uint32_t)(r + ci * L.hCell) << 12) | ((uint32_t)s << 24);
+            }
+            base += __popcll(mask);
+        }
+        if (base > 0) break;
+    }
+    if (lane == 0) cand_cnt[cell_slot] = (uint16_t)base;
+}
+
+// ---------------------------------------------------------------------------
+// GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, OpenCV 8U bit-exact fixed
+// point: out = (sum_ij k_i k_j p + 2^15) >> 16 with k = [18,34,48,56,48,34,18].
+constexpr int kBlurTW = 64, kBlurTH = 16;
+__device__ __forceinline__ int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+__global__ __launch_bounds__(256) void blur_kernel(OrbGeom g) {
+    __shared__ uint8_t tin[kBlurTH + 6][kBlurTW + 8];
+    __shared__ int th[kBlurTH + 6][kBlurTW];
+    const int f = blockIdx.y;
+    int tile = blockIdx.x, l = 0;
+    for (; l < g.nlevels; l++) {
+        const LevelGeom& L = g.lv[l];
+        const int nt = ((L.w + kBlurTW - 1) / kBlurTW) * ((L.h + kBlurTH - 1) / kBlurTH);
+        if (tile < nt) break;
+        tile -= nt;
+    }
+    const LevelGeom& L = g.lv[l];
+    const int tx = (L.w + kBlurTW - 1) / kBlurTW;
+    const int x0 = (tile % tx) * kBlurTW, y0 = (tile / tx) * kBlurTH;
+    const uint8_t* img = L.img + f * L.frame_stride;
+    for (int t = threadIdx.x; t < (kBlurTH + 6) * (kBlurTW + 6); t += 256) {
+        const int r = t / (kBlurTW + 6), c = t - r * (kBlurTW + 6);
+        const int y = reflect101(y0 + r - 3, L.h), x = reflect101(min(x0 + c - 3, L.w + 2), L.w);
+        tin[r][c] = img[(size_t)y * L.stride + x];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < (kBlurTH + 6) * kBlurTW; t += 256) {
+        const int r = t / kBlurTW, c = t - r * kBlurTW;
+        const uint8_t* p = &tin[r][c];
+        th[r][c] = 18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3];
+    }
+    __syncthreads();
+    uint8_t* out = L.blur + f * L.blur_frame_stride;
+    for (int t = threadIdx.x; t < kBlurTH * kBlurTW; t += 256) {
+        const int r = t / kBlurTW, c = t - r * kBlurTW;
+        const int y = y0 + r, x = x0 + c;
+        if (y >= L.h || x >= L.w) continue;
+        const int s = 18 * (th[r][c] + th[r + 6][c]) + 34 * (th[r + 1][c] + th[r + 5][c]) +
+                      48 * (th[r + 2][c] + th[r + 4][c]) + 56 * th[r + 3][c];
+        out[(size_t)y * L.w + x] = (uint8_t)min(255, (s + (1 << 15)) >> 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// DistributeOctTree (src/ORBextractor.cc:539-763) for one (frame, level) per
+// 256-thread workgroup.
+//
+// The reference walks a std::list, dividing nodes one at a time.  All
+// divisions of one main-loop pass are independent, so a pass is done as: one
+// sweep over the keys counting each divided node's four children (atomics in
+// LDS), block scans that place every child where the reference's push_front
+// sequence would put it, and one sweep re-pointing each key at its new node.
+// The node table always *is* the list (entry i = i-th list element).  The
+// final phase (:673-737) sorts the expandable nodes by (size, creation
+// sequence) -- the creation sequence stands in for the reference's pointer
+// tie-break, see DESIGN.md -- and finds the division after which the list
+// reaches N with one scan instead of one division at a time.
+constexpr int kFlagNoMore = 1, kFlagToExp = 2;
+
+struct OctShared {
+    short x0[2][kNodeCap], y0[2][kNodeCap], x1[2][kNodeCap], y1[2][kNodeCap];
+    int cnt[2][kNodeCap];
+    int seq[2][kNodeCap];
+    uint8_t flags[2][kNodeCap];
+    uint8_t div[kNodeCap];
+    int c4[kNodeCap][4];   // child counts, then child positions (-1 = empty)
+    int sa[kNodeCap];      // scan scratch
+    int sb[kNodeCap];      // scan scratch / remap
+    int sc[kNodeCap];      // scan scratch / sort
+    int cand[kNodeCap];
+    int cellpre[2048];
+    int wsum[4];
+    int misc[8];
+};
+
+// Exclusive scan of a[0..n) in place (n <= 2048), returns the total.
+__device__ int block_scan(int* a, int n, int* wsum) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int v[8], local = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int i = 8 * t + k;
+        v[k] = i < n ? a[i] : 0;
+        local += v[k];
+    }
+    int x = local;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int wbase = 0;
+    for (int j = 0; j < w; j++) wbase += wsum[j];
+    const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    int run = wbase + x - local;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int i = 8 * t + k;
+        if (i < n) a[i] = run;
+        run += v[k];
+    }
+    __syncthreads();
+    return total;
+}
+
+__device__ __forceinline__ int quadrant(int kx, int ky, int x0, int y0, int x1, int y1) {
+    const int hx = (int)ceilf((float)(x1 - x0) / 2), hy = (int)ceilf((float)(y1 - y0) / 2);
+    const bool left = kx < x0 + hx, top = ky < y0 + hy;
+    return left ? (top ? 0 : 2) : (top ? 1 : 3);
+}
+
+__device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1, short& cx0, short& cy0, short& cx1,
+                                           short& cy1) {
+    const int hx = (int)ceilf((float)(x1 - x0) / 2), hy = (int)ceilf((float)(y1 - y0) / 2);
+    cx0 = (short)((q & 1) ? x0 + hx : x0);
+    cx1 = (short)((q & 1) ? x1 : x0 + hx);
+    cy0 = (short)((q & 2) ? y0 + hy : y0);
+    cy1 = (short)((q & 2) ? y1 : y0 + hy);
+}
+
+// Rebuild the list after dividing the nodes flagged in S.div (proc rank of a
+// divided node in S.sb[node] = position in division order, P_c prefix in
+// S.sa[node]).  T = number of children pushed.  Returns the new length.
+__device__ int rebuild_list(OctShared& S, int cur, int L, int T, int seqc, const uint32_t* keys, uint16_t* keynode,
+                            int C) {
+    const int nb = cur ^ 1;
+    // rank of non-divided nodes in list order
+    for (int i = threadIdx.x; i < L; i += 256) S.sc[i] = S.div[i] ? 0 : 1;
+    __syncthreads();
+    const int ND = block_scan(S.sc, L, S.wsum);
+    for (int i = threadIdx.x; i < L; i += 256) {
+        if (S.div[i]) {
+            const int pc = S.sa[i];
+            int r = 0;
+            for (int q = 0; q < 4; q++) {
+                const int n = S.c4[i][q];
+                if (n > 0) {
+                    const int pos = T - pc - 1 - r;
+                    short a, b, c, d;
+                    child_rect(q, S.x0[cur][i], S.y0[cur][i], S.x1[cur][i], S.y1[cur][i], a, b, c, d);
+                    S.x0[nb][pos] = a; S.y0[nb][pos] = b; S.x1[nb][pos] = c; S.y1[nb][pos] = d;
+                    S.cnt[nb][pos] = n;
+                    S.seq[nb][pos] = seqc + pc + r;
+                    S.flags[nb][pos] = (uint8_t)((n == 1 ? kFlagNoMore : 0) | (n > 1 ? kFlagToExp : 0));
+                    S.c4[i][q] = pos;
+                    r++;
+                } else {
+                    S.c4[i][q] = -1;
+                }
+            }
+        } else {
+            const int pos = T + S.sc[i];
+            S.x0[nb][pos] = S.x0[cur][i]; S.y0[nb][pos] = S.y0[cur][i];
+            S.x1[nb][pos] = S.x1[cur][i]; S.y1[nb][pos] = S.y1[cur][i];
+            S.cnt[nb][pos] = S.cnt[cur][i];
+            S.seq[nb][pos] = S.seq[cur][i];
+            S.flags[nb][pos] = (uint8_t)(S.flags[cur][i] & kFlagNoMore);
+            S.sb[i] = pos;
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < C; k += 256) {
+        const int n = keynode[k];
+        if (S.div[n]) {
+            const uint32_t key = keys[k];
+            const int q = quadrant(key & 0xFFF, (key >> 12) & 0xFFF, S.x0[cur][n], S.y0[cur][n], S.x1[cur][n],
+                                   S.y1[cur][n]);
+            keynode[k] = (uint16_t)S.c4[n][q];
+        } else {
+            keynode[k] = (uint16_t)S.sb[n];
+        }
+    }
+    __syncthreads();
+    return T + ND;
+}
+
+// Count the four children of every node with S.div set.
+__device__ void count_children(OctShared& S, int cur, int L, const uint32_t* keys, const uint16_t* keynode, int C) {
+    for (int i = threadIdx.x; i < L; i += 256) S.c4[i][0] = S.c4[i][1] = S.c4[i][2] = S.c4[i][3] = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < C; k += 256) {
+        const int n = keynode[k];
+        if (S.div[n]) {
+            const uint32_t key = keys[k];
+            const int q = quadrant(key & 0xFFF, (key >> 12) & 0xFFF, S.x0[cur][n], S.y0[cur][n], S.x1[cur][n],
+                                   S.y1[cur][n]);
+            atomicAdd(&S.c4[n][q], 1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* __restrict__ cand,
+                                                     const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
+                                                     uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
+                                                     int* __restrict__ lvl_cnt) {
+    __shared__ OctShared S;
+    const int l = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+    const LevelGeom& Lg = g.lv[l];
+    const int ncells = Lg.nRows * Lg.nCols;
+    uint32_t* keys = keys_all + (size_t)f * g.keys_per_frame + Lg.key_base;
+    uint16_t* keynode = keynode_all + (size_t)f * g.keys_per_frame + Lg.key_base;
+    const size_t cell0 = (size_t)f * g.cells_per_frame + Lg.cell_base;
+
+    // --- gather candidates in cell order (vToDistributeKeys, :818-826)
+    for (int c = t; c < ncells; c += 256) S.cellpre[c] = cand_cnt[cell0 + c];
+    __syncthreads();
+    const int C = block_scan(S.cellpre, ncells, S.wsum);
+    for (int c = t >> 6; c < ncells; c += 4) {
+        const int n = (int)cand_cnt[cell0 + c], o = S.cellpre[c];
+        const uint32_t* src = cand + (cell0 + c) * kCellCap;
+        for (int j = t & 63; j < n; j += 64) keys[o + j] = src[j];
+    }
+    __threadfence_block();
+    __syncthreads();
+
+    // --- initial nodes (:542-585)
+    const int minX = kMinBorder, maxX = Lg.maxBorderX, minY = kMinBorder, maxY = Lg.maxBorderY;
+    const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
+    const float hX = (float)(maxX - minX) / nIni;
+    int cur = 0;
+    if (t < 4 * nIni) S.sa[t] = 0;
+    __syncthreads();
+    for (int k = t; k < C; k += 256) {
+        const int i = (int)((float)(keys[k] & 0xFFF) / hX);
+        keynode[k] = (uint16_t)i;
+        atomicAdd(&S.sa[i], 1);
+    }
+    __syncthreads();
+    if (t == 0) {
+        int L = 0;
+        for (int i = 0; i < nIni; i++) {
+            S.sb[i] = -1;
+            if (S.sa[i] == 0) continue;
+            S.x0[0][L] = (short)(int)(hX * (float)i); S.y0[0][L] = 0;
+            S.x1[0][L] = (short)(int)(hX * (float)(i + 1)); S.y1[0][L] = (short)(maxY - minY);
+            S.cnt[0][L] = S.sa[i];
+            S.seq[0][L] = i;
+            S.flags[0][L] = (uint8_t)(S.sa[i] == 1 ? kFlagNoMore : 0);
+            S.sb[i] = L++;
+        }
+        S.misc[0] = L;
+    }
+    __syncthreads();
+    int L = S.misc[0];
+    for (int k = t; k < C; k += 256) keynode[k] = (uint16_t)S.sb[keynode[k]];
+    __syncthreads();
+    int seqc = nIni;
+    const int N = Lg.nfeat;
+
+    bool finish = (L == 0);
+    while (!finish) {
+        // ---- main-loop pass (:596-665): divide every node that is not bNoMore
+        const int prevSize = L;
+        for (int i = t; i < L; i += 256) S.div[i] = (S.flags[cur][i] & kFlagNoMore) ? 0 : 1;
+        __syncthreads();
+        count_children(S, cur, L, keys, keynode, C);
+        for (int i = t; i < L; i += 256) {
+            int nc = 0, nm = 0;
+            if (S.div[i])
+                for (int q = 0; q < 4; q++) { nc += S.c4[i][q] > 0; nm += S.c4[i][q] > 1; }
+            S.sa[i] = nc;
+            S.sb[i] = nm;
+        }
+        __syncthreads();
+        const int nToExpand = block_scan(S.sb, L, S.wsum);
+        const int T = block_scan(S.sa, L, S.wsum);
+        L = rebuild_list(S, cur, L, T, seqc, keys, keynode, C);
+        seqc += T;
+        cur ^= 1;
+        if (L >= N || L == prevSize) {
+            finish = true;
+        } else if (L + nToExpand * 3 > N) {
+            // ---- final phase (:673-737)
+            while (!finish) {
+                const int prev2 = L;
+                // candidates = nodes pushed last step with > 1 key
+                for (int i = t; i < L; i += 256) S.sc[i] = (S.flags[cur][i] & kFlagToExp) ? 1 : 0;
+                __syncthreads();
+                const int M = block_scan(S.sc, L, S.wsum);
+                for (int i = t; i < L; i += 256)
+                    if (S.flags[cur][i] & kFlagToExp) S.cand[S.sc[i]] = i;
+                __syncthreads();
+                // processing rank: descending (size, seq)
+                for (int a = t; a < M; a += 256) {
+                    const int ia = S.cand[a], ca = S.cnt[cur][ia], sa = S.seq[cur][ia];
+                    int rank = 0;
+                    for (int b = 0; b < M; b++) {
+                        const int ib = S.cand[b], cb = S.cnt[cur][ib], sb = S.seq[cur][ib];
+                        rank += (cb < ca) || (cb == ca && sb < sa);
+                    }
+                    S.sc[M - 1 - rank] = ia;  // sc[p] = node processed p-th
+                }
+                for (int i = t; i < L; i += 256) S.div[i] = (S.flags[cur][i] & kFlagToExp) ? 1 : 0;
+                __syncthreads();
+                count_children(S, cur, L, keys, keynode, C);
+                // deltas in processing order
+                for (int p = t; p < M; p += 256) {
+                    const int i = S.sc[p];
+                    int nc = 0;
+                    for (int q = 0; q < 4; q++) nc += S.c4[i][q] > 0;
+                    S.sa[p] = nc - 1;
+                    S.cand[p] = nc;
+                }
+                if (t == 0) S.misc[1] = M - 1;
+                __syncthreads();
+                block_scan(S.sa, M, S.wsum);  // exclusive prefix of deltas
+                for (int p = t; p < M; p += 256)
+                    if (L + S.sa[p] + (S.cand[p] - 1) >= N) atomicMin(&S.misc[1], p);
+                __syncthreads();
+                const int kstar = S.misc[1];
+                // divided = first kstar+1 in processing order; P_c over processing order
+                for (int i = t; i < L; i += 256) S.div[i] = 0;
+                __syncthreads();
+                for (int p = t; p < M; p += 256) {
+                    S.sa[p] = p <= kstar ? S.cand[p] : 0;
+                    if (p <= kstar) S.div[S.sc[p]] = 1;
+                }
+                __syncthreads();
+                const int T2 = block_scan(S.sa, M, S.wsum);
+                // move P_c from processing slot to node slot (sb is free here)
+                for (int p = t; p <= kstar; p += 256) S.sb[S.sc[p]] = S.sa[p];
+                __syncthreads();
+                for (int i = t; i < L; i += 256)
+                    if (S.div[i]) S.sa[i] = S.sb[i];
+                __syncthreads();
+                L = rebuild_list(S, cur, L, T2, seqc, keys, keynode, C);
+                seqc += T2;
+                cur ^= 1;
+                if (L >= N || L == prev2) finish = true;
+            }
+        }
+    }
+
+    // --- retain the best key of each node (:741-760): first max in key order
+    for (int i = t; i < L; i += 256) S.sa[i] = 0;
+    __syncthreads();
+    for (int k = t; k < C; k += 256) {
+        const uint32_t key = keys[k];
+        atomicMax(&S.sa[keynode[k]], (int)(((key >> 24) << 23) | (0x7FFFFF - k)));
+    }
+    __syncthreads();
+    LevelKp* out = lvl_kp + (size_t)f * g.lvl_kp_per_frame + Lg.kp_base;
+    const int nout = min(L, Lg.kp_cap);
+    for (int i = t; i < nout; i += 256) {
+        const int k = 0x7FFFFF - (S.sa[i] & 0x7FFFFF);
+        const uint32_t key = keys[k];
+        LevelKp kp;
+        kp.x = (uint16_t)((key & 0xFFF) + minX);
+        kp.y = (uint16_t)(((key >> 12) & 0xFFF) + minY);
+        kp.response = (uint16_t)(key >> 24);
+        kp.pad = 0;
+        out[i] = kp;
+    }
+    if (t == 0) lvl_cnt[f * kMaxLevels + l] = nout;
+}
+
+// ---------------------------------------------------------------------------
+// glibc sinf/cosf (|y| < 120) restated; bit-identical to the system libm the
+// reference calls at src/ORBextractor.cc:113 over all ORB angles.
+struct SinCosT { double sign[4]; double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3; };
+__constant__ SinCosT c_sincos[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+__device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+__device__ __forceinline__ float sincos_poly(double x, double x2, const SinCosT* p, int n) {
+    if ((n & 1) == 0) {
+        const double x3 = x * x2, s1 = p->s2 + x2 * p->s3, x7 = x3 * x2, s = x + x3 * p->s1;
+        return (float)(s + x7 * s1);
+    }
+    const double x4 = x2 * x2, c2 = p->c3 + x2 * p->c4, c1 = p->c0 + x2 * p->c1, x6 = x4 * x2, c = c1 + x4 * p->c2;
+    return (float)(c + x6 * c2);
+}
+__device__ void glibc_sincosf(float y, float* sn, float* cs) {
+    const double x = y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        if (abstop12(y) < abstop12(0x1p-12f)) { *sn = y; *cs = 1.0f; return; }
+        *sn = sincos_poly(x, x * x, &c_sincos[0], 0);
+        *cs = sincos_poly(x, x * x, &c_sincos[0], 1);
+        return;
+    }
+    const double r = x * c_sincos[0].hpi_inv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    const double xr = x - n * c_sincos[0].hpi;
+    const double s = c_sincos[0].sign[n & 3];
+    const SinCosT* p = (n & 2) ? &c_sincos[1] : &c_sincos[0];
+    *sn = sincos_poly(xr * s, xr * xr, p, n);
+    *cs = sincos_poly(xr * s, xr * xr, p, n ^ 1);
+}
+
+// OpenCV cv::fastAtan2 (degrees).
+__device__ float fast_atan2(float y, float x) {
+    const float k = (float)(180 / M_PI);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k, p5 = 0.1555786518463281f * k,
+                p7 = -0.04432655554792128f * k;
+    const float eps = (float)2.220446049250313e-16;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps); c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps); c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// One wave per keypoint slot: orientation on the level image, rotated BRIEF
+// on the blurred level, final scaling/placement in reference order.
+__global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __restrict__ lvl_kp,
+                                                   const int* __restrict__ lvl_cnt, spslam_keypoint* __restrict__ out_kp,
+                                                   uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt,
+                                                   int cap_per_frame) {
+    const int f = blockIdx.y, lane = threadIdx.x & 63;
+    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (slot >= g.lvl_kp_per_frame) return;
+    int l = 0;
+    for (int k = 1; k < g.nlevels; k++)
+        if (slot >= g.lv[k].kp_base) l = k;
+    const LevelGeom& L = g.lv[l];
+    const int i = slot - L.kp_base;
+    const int* cnt = lvl_cnt + f * kMaxLevels;
+    int off = 0, total = 0;
+    for (int k = 0; k < g.nlevels; k++) {
+        if (k < l) off += cnt[k];
+        total += cnt[k];
+    }
+    if (slot == 0 && lane == 0) out_cnt[f] = min(total, cap_per_frame);
+    if (i >= cnt[l] || off + i >= cap_per_frame) return;
+    const LevelKp kp = lvl_kp[(size_t)f * g.lvl_kp_per_frame + slot];
+    // IC_Angle (:77-104) on the un-blurred level
+    const uint8_t* img = L.img + f * L.frame_stride;
+    const int P = L.stride;
+    const uint8_t* center = img + (size_t)kp.y * P + kp.x;
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        const int u = lane - 15;
+        m10 = u * center[u];
+        for (int v = 1; v <= 15; v++) {
+            if (abs(u) > c_umax[v]) continue;
+            const int vp = center[u + v * P], vm = center[u - v * P];
+            m01 += v * (vp - vm);
+            m10 += u * (vp + vm);
+        }
+    }
+#pragma unroll
+    for (int off2 = 32; off2 >= 1; off2 >>= 1) {
+        m10 += __shfl_xor(m10, off2);
+        m01 += __shfl_xor(m01, off2);
+    }
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // rotated BRIEF (:107-147) on the blurred level
+    const float factorPI = (float)(M_PI / 180.f);
+    float sb, ca;
+    glibc_sincosf(angle * factorPI, &sb, &ca);
+    const uint8_t* bimg = L.blur + f * L.blur_frame_stride;
+    const uint8_t* bc = bimg + (size_t)kp.y * L.w + kp.x;
+    const size_t o = (size_t)f * cap_per_frame + off + i;
+    uint64_t* dd = reinterpret_cast<uint64_t*>(out_desc + o * 32);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int tst = lane + 64 * k;
+        int val[2];
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const float x = (float)c_pattern[4 * tst + 2 * e], y = (float)c_pattern[4 * tst + 2 * e + 1];
+            const int r = cv_round(__builtin_fmaf(x, sb, y * ca));
+            const int c = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
+            val[e] = bc[r * L.w + c];
+        }
+        const unsigned long long m = __ballot(val[0] < val[1]);
+        if (lane == 0) dd[k] = m;
+    }
+    if (lane == 0) {
+        spslam_keypoint r;
+        float x = (float)kp.x, y = (float)kp.y;
+        if (l != 0) { x = x * L.scale; y = y * L.scale; }
+        r.x = x; r.y = y;
+        r.size = (float)L.patch_size;
+        r.angle = angle;
+        r.response = (float)kp.response;
+        r.octave = l;
+        r.class_id = -1;
+        out_kp[o] = r;
+    }
+}
+
+}  // namespace spslam
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (called from spslam_capi.cpp).
+namespace spslam {
+
+hipError_t orb_upload_tables(const int umax[16]) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, 16 * sizeof(int));
+}
+
+
+
+// Enqueue the whole ORB pass for n frames on `s`.  g.lv[0].img/stride/
+// frame_stride must already point at the caller's gray frames.
+hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, int minTh, spslam_keypoint* kps,
+                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s) {
+    for (int l = 1; l < g.nlevels; l++) {
+        const LevelGeom& P = g.lv[l - 1];
+        const LevelGeom& D = g.lv[l];
+        dim3 grid((D.w * D.h + 255) / 256, n);
+        hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P.img, P.w, P.h, P.stride, P.frame_stride,
+                           const_cast<uint8_t*>(D.img), D.w, D.h, D.stride, D.frame_stride);
+    }
+    hipLaunchKernelGGL(fast_cells_kernel, dim3(g.cells_per_frame, n), dim3(64), 0, s, g, b.cand, b.cand_cnt, iniTh,
+                       minTh);
+    hipLaunchKernelGGL(blur_kernel, dim3(g.blur_tiles_per_frame, n), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
+                       b.lvl_kp, b.lvl_cnt);
+    hipLaunchKernelGGL(desc_kernel, dim3((g.lvl_kp_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.lvl_kp, b.lvl_cnt,
+                       kps, desc, counts, cap_per_frame);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

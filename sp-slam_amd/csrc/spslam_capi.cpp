@@ -1,0 +1,382 @@
+// C ABI (include/spslam_gpu.h) over the gfx950 ORB kernels.
+//
+// The context owns: the level tables of ORBextractor (src/ORBextractor.cc:
+// 410-470), the pyramid geometry, device scratch for `max_batch` frames and a
+// HIP stream.  Nothing here falls back to a CPU path: if the HIP runtime or
+// the gfx950 code object is unusable every entry point returns SPSLAM_ERR_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/spslam_gpu.h"
+#include "orb_launch.h"
+
+using namespace spslam;
+
+struct spslam_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    spslam_orb_params p{};
+    std::string err;
+    // ORBextractor tables
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nfeat;
+    int umax[16]{};
+    OrbGeom geom{};
+    long long pyr_frame_stride = 0, blur_frame_stride = 0;
+    int max_kp = 0;
+    // device buffers
+    uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;
+    OrbBuffers b{};
+    uint8_t* d_in = nullptr;
+    spslam_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int* d_cnt = nullptr;
+    // last call (debug stage access)
+    const uint8_t* last_gray = nullptr;
+    size_t last_frame_stride = 0;
+    int last_stride = 0, last_frames = 0;
+};
+
+namespace {
+
+int fail(spslam_ctx* c, int code, const char* fmt, const char* what = "") {
+    if (c) {
+        char buf[512];
+        std::snprintf(buf, sizeof buf, fmt, what);
+        c->err = buf;
+    }
+    return code;
+}
+#define HIP_CHECK(ctx, expr)                                                                  \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(ctx, SPSLAM_ERR_HIP, #expr ": %s", hipGetErrorString(e_)); \
+    } while (0)
+
+int cv_round(float v) { return (int)std::nearbyint(v); }
+
+// ORBextractor::ORBextractor tables, src/ORBextractor.cc:415-469.
+void build_tables(spslam_ctx* c) {
+    const int nl = c->p.nlevels;
+    const double scaleFactor = c->p.scale_factor;  // member is double, ctor arg float
+    c->scale.assign(nl, 1.f); c->sigma2.assign(nl, 1.f);
+    for (int i = 1; i < nl; i++) {
+        c->scale[i] = (float)(c->scale[i - 1] * scaleFactor);
+        c->sigma2[i] = c->scale[i] * c->scale[i];
+    }
+    c->inv_scale.resize(nl); c->inv_sigma2.resize(nl);
+    for (int i = 0; i < nl; i++) {
+        c->inv_scale[i] = 1.0f / c->scale[i];
+        c->inv_sigma2[i] = 1.0f / c->sigma2[i];
+    }
+    c->nfeat.assign(nl, 0);
+    float factor = (float)(1.0f / scaleFactor);
+    float nDesired = c->p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    int sum = 0;
+    for (int l = 0; l < nl - 1; l++) {
+        c->nfeat[l] = cv_round(nDesired);
+        sum += c->nfeat[l];
+        nDesired *= factor;
+    }
+    c->nfeat[nl - 1] = std::max(c->p.nfeatures - sum, 0);
+    const int HP = 15;
+    int v, v0, vmax = (int)std::floor(HP * std::sqrt(2.f) / 2 + 1), vmin = (int)std::ceil(HP * std::sqrt(2.f) / 2);
+    const double hp2 = HP * HP;
+    for (v = 0; v <= vmax; ++v) c->umax[v] = (int)std::nearbyint(std::sqrt(hp2 - v * v));
+    for (v = HP, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+}
+
+// Pyramid + FAST-cell geometry (src/ORBextractor.cc:769-787, 1111-1112) and
+// scratch layout.  Returns an error string for unsupported shapes.
+const char* build_geom(spslam_ctx* c) {
+    OrbGeom& g = c->geom;
+    std::memset(&g, 0, sizeof g);
+    g.nlevels = c->p.nlevels;
+    long long pyr = 0, blur = 0;
+    int cells = 0, kpb = 0, keyb = 0, tiles = 0;
+    for (int l = 0; l < g.nlevels; l++) {
+        LevelGeom& L = g.lv[l];
+        L.w = cv_round((float)c->p.width * c->inv_scale[l]);
+        L.h = cv_round((float)c->p.height * c->inv_scale[l]);
+        if (L.w > 4095 || L.h > 4095) return "level wider/taller than 4095 px";
+        L.maxBorderX = L.w - kEdgeThreshold + 3;
+        L.maxBorderY = L.h - kEdgeThreshold + 3;
+        const float width = (float)(L.maxBorderX - kMinBorder), height = (float)(L.maxBorderY - kMinBorder);
+        L.nCols = (int)(width / 30.f);
+        L.nRows = (int)(height / 30.f);
+        if (L.nCols < 1 || L.nRows < 1) return "pyramid level smaller than one FAST cell (reference divides by zero)";
+        L.wCell = (int)std::ceil(width / L.nCols);
+        L.hCell = (int)std::ceil(height / L.nRows);
+        if (L.wCell + 6 > kCellWinMax || L.hCell + 6 > kCellWinMax) return "FAST cell window exceeds LDS tile";
+        if (((L.wCell + 1) / 2) * ((L.hCell + 1) / 2) > kCellCap) return "FAST cell survivor bound exceeds kCellCap";
+        const int nIni = (int)std::round(width / height);
+        if (nIni < 1 || 4 * nIni > 64) return "unsupported aspect ratio for DistributeOctTree";
+        L.cell_base = cells;
+        cells += L.nCols * L.nRows;
+        if (L.nCols * L.nRows > 2048) return "too many FAST cells per level";
+        L.nfeat = c->nfeat[l];
+        L.kp_cap = std::max(L.nfeat + 16, 4 * nIni + 4);
+        if (L.kp_cap > kNodeCap) return "nfeatures per level exceeds DistributeOctTree node capacity";
+        L.kp_base = kpb;
+        kpb += L.kp_cap;
+        L.key_base = keyb;
+        keyb += L.nCols * L.nRows * kCellCap;
+        L.scale = c->scale[l];
+        L.patch_size = (int)(31 * c->scale[l]);
+        if (l > 0) {
+            L.stride = L.w;
+            L.img = reinterpret_cast<const uint8_t*>(pyr);  // offset, rebased after allocation
+            pyr += (long long)L.w * L.h;
+        }
+        L.blur = reinterpret_cast<uint8_t*>(blur);
+        blur += (long long)L.w * L.h;
+        tiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+    }
+    c->pyr_frame_stride = (pyr + 255) / 256 * 256;
+    c->blur_frame_stride = (blur + 255) / 256 * 256;
+    g.cells_per_frame = cells;
+    g.lvl_kp_per_frame = kpb;
+    g.keys_per_frame = keyb;
+    g.blur_tiles_per_frame = tiles;
+    c->max_kp = kpb;
+    return nullptr;
+}
+
+void free_all(spslam_ctx* c) {
+    void* ptrs[] = {c->d_pyr, c->d_blur, c->b.cand, c->b.cand_cnt, c->b.keys, c->b.keynode,
+                    c->b.lvl_kp, c->b.lvl_cnt, c->d_in, c->d_kps, c->d_desc, c->d_cnt};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// Point level 0 at the caller's frames and levels >= 1 at the context pyramid.
+void bind_frames(spslam_ctx* c, const uint8_t* d_gray, size_t frame_stride, int stride) {
+    OrbGeom& g = c->geom;
+    g.lv[0].img = d_gray;
+    g.lv[0].stride = stride;
+    g.lv[0].frame_stride = (long long)frame_stride;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spslam_create(int device, const spslam_orb_params* params, spslam_ctx** out) {
+    if (!params || !out) return SPSLAM_ERR_ARG;
+    *out = nullptr;
+    spslam_ctx* c = new (std::nothrow) spslam_ctx();
+    if (!c) return SPSLAM_ERR_ARG;
+    c->device = device;
+    c->p = *params;
+    if (c->p.nlevels < 1 || c->p.nlevels > SPSLAM_MAX_LEVELS || c->p.nfeatures < 1 || c->p.scale_factor <= 1.f ||
+        c->p.width < 64 || c->p.height < 64 || c->p.max_batch < 1) {
+        delete c;
+        return SPSLAM_ERR_ARG;
+    }
+    build_tables(c);
+    if (const char* e = build_geom(c)) {
+        delete c;
+        std::fprintf(stderr, "spslam_create: %s\n", e);
+        return SPSLAM_ERR_ARG;
+    }
+    int rc = SPSLAM_OK;
+    auto hip_ok = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == SPSLAM_OK) {
+            rc = fail(c, SPSLAM_ERR_HIP, "%s", what);
+            c->err += std::string(": ") + hipGetErrorString(e);
+        }
+        return e == hipSuccess;
+    };
+    if (!hip_ok(hipSetDevice(device), "hipSetDevice") ||
+        !hip_ok(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate") ||
+        !hip_ok(orb_upload_tables(c->umax), "upload tables")) {
+        std::fprintf(stderr, "spslam_create: %s\n", c->err.c_str());
+        free_all(c);
+        delete c;
+        return SPSLAM_ERR_HIP;
+    }
+    const size_t B = (size_t)c->p.max_batch;
+    const OrbGeom& g = c->geom;
+    hip_ok(hipMalloc(&c->d_pyr, B * c->pyr_frame_stride), "alloc pyramid");
+    hip_ok(hipMalloc(&c->d_blur, B * c->blur_frame_stride), "alloc blur");
+    hip_ok(hipMalloc(&c->b.cand, B * g.cells_per_frame * kCellCap * sizeof(uint32_t)), "alloc cand");
+    hip_ok(hipMalloc(&c->b.cand_cnt, B * g.cells_per_frame * sizeof(uint16_t)), "alloc cand_cnt");
+    hip_ok(hipMalloc(&c->b.keys, B * g.keys_per_frame * sizeof(uint32_t)), "alloc keys");
+    hip_ok(hipMalloc(&c->b.keynode, B * g.keys_per_frame * sizeof(uint16_t)), "alloc keynode");
+    hip_ok(hipMalloc(&c->b.lvl_kp, B * g.lvl_kp_per_frame * sizeof(LevelKp)), "alloc lvl_kp");
+    hip_ok(hipMalloc(&c->b.lvl_cnt, B * kMaxLevels * sizeof(int)), "alloc lvl_cnt");
+    hip_ok(hipMalloc(&c->d_in, (size_t)c->p.width * c->p.height), "alloc input");
+    hip_ok(hipMalloc(&c->d_kps, (size_t)c->max_kp * sizeof(spslam_keypoint)), "alloc kps");
+    hip_ok(hipMalloc(&c->d_desc, (size_t)c->max_kp * 32), "alloc desc");
+    hip_ok(hipMalloc(&c->d_cnt, sizeof(int) * 4), "alloc cnt");
+    if (rc != SPSLAM_OK) {
+        std::fprintf(stderr, "spslam_create: %s\n", c->err.c_str());
+        free_all(c);
+        delete c;
+        return rc;
+    }
+    // rebase level offsets onto the allocations
+    OrbGeom& gm = c->geom;
+    for (int l = 0; l < gm.nlevels; l++) {
+        LevelGeom& L = gm.lv[l];
+        if (l > 0) {
+            L.img = c->d_pyr + reinterpret_cast<long long>(L.img);
+            L.frame_stride = c->pyr_frame_stride;
+        }
+        L.blur = c->d_blur + reinterpret_cast<long long>(L.blur);
+        L.blur_frame_stride = c->blur_frame_stride;
+    }
+    *out = c;
+    return SPSLAM_OK;
+}
+
+void spslam_destroy(spslam_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    free_all(ctx);
+    delete ctx;
+}
+
+const char* spslam_last_error(const spslam_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int spslam_orb_tables(const spslam_ctx* c, int* nlevels, float* scale, float* inv_scale, float* sigma2,
+                      float* inv_sigma2, int* fpl) {
+    if (!c) return SPSLAM_ERR_ARG;
+    const int nl = c->p.nlevels;
+    if (nlevels) *nlevels = nl;
+    for (int l = 0; l < nl; l++) {
+        if (scale) scale[l] = c->scale[l];
+        if (inv_scale) inv_scale[l] = c->inv_scale[l];
+        if (sigma2) sigma2[l] = c->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = c->inv_sigma2[l];
+        if (fpl) fpl[l] = c->nfeat[l];
+    }
+    return SPSLAM_OK;
+}
+
+int spslam_orb_max_keypoints(const spslam_ctx* c) { return c ? c->max_kp : SPSLAM_ERR_ARG; }
+
+int spslam_orb_level_size(const spslam_ctx* c, int level, int* w, int* h) {
+    if (!c || level < 0 || level >= c->p.nlevels) return SPSLAM_ERR_ARG;
+    *w = c->geom.lv[level].w;
+    *h = c->geom.lv[level].h;
+    return SPSLAM_OK;
+}
+
+int spslam_orb_extract_batch_device(spslam_ctx* c, const uint8_t* d_gray, int n_frames, size_t frame_stride,
+                                    int stride, spslam_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
+                                    int cap_per_frame, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!d_gray || !d_kps || !d_desc || !d_counts || n_frames < 1 || n_frames > c->p.max_batch ||
+        stride < c->p.width || (n_frames > 1 && frame_stride < (size_t)stride * c->p.height) || cap_per_frame < 1)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_orb_extract_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    bind_frames(c, d_gray, frame_stride, stride);
+    HIP_CHECK(c, orb_launch(c->geom, c->b, n_frames, c->p.ini_th_fast, c->p.min_th_fast, d_kps, d_desc, d_counts,
+                            cap_per_frame, s));
+    c->last_gray = d_gray;
+    c->last_frame_stride = frame_stride;
+    c->last_stride = stride;
+    c->last_frames = n_frames;
+    return SPSLAM_OK;
+}
+
+int spslam_orb_extract(spslam_ctx* c, const uint8_t* gray, int w, int h, int stride, spslam_keypoint* kps,
+                       uint8_t* desc, int cap, int* n) {
+    if (!c || !n) return SPSLAM_ERR_ARG;
+    if (w == 0 || h == 0 || !gray) {  // reference: empty image -> return, outputs untouched
+        *n = 0;
+        return SPSLAM_OK;
+    }
+    if (w != c->p.width || h != c->p.height || stride < w)
+        return fail(c, SPSLAM_ERR_ARG, "image size does not match the context%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipMemcpy2DAsync(c->d_in, w, gray, stride, w, h, hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_orb_extract_batch_device(c, c->d_in, 1, (size_t)w * h, w, c->d_kps, c->d_desc, c->d_cnt,
+                                             c->max_kp, c->stream);
+    if (rc) return rc;
+    int cnt = 0;
+    HIP_CHECK(c, hipMemcpyAsync(&cnt, c->d_cnt, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    *n = cnt;
+    if (cnt > cap) return fail(c, SPSLAM_ERR_CAPACITY, "keypoint buffer too small%s", "");
+    if (cnt > 0) {
+        if (kps) HIP_CHECK(c, hipMemcpy(kps, c->d_kps, cnt * sizeof(spslam_keypoint), hipMemcpyDeviceToHost));
+        if (desc) HIP_CHECK(c, hipMemcpy(desc, c->d_desc, (size_t)cnt * 32, hipMemcpyDeviceToHost));
+    }
+    return SPSLAM_OK;
+}
+
+int spslam_orb_debug_stage(spslam_ctx* c, int frame, int level, int stage, void* out, int cap, int* n) {
+    if (!c || !out || level < 0 || level >= c->p.nlevels) return SPSLAM_ERR_ARG;
+    if (!c->last_frames || frame < 0 || frame >= c->last_frames)
+        return fail(c, SPSLAM_ERR_NOT_READY, "no such frame in the last call%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    HIP_CHECK(c, hipDeviceSynchronize());
+    const LevelGeom& L = c->geom.lv[level];
+    if (stage == 0 || stage == 1) {
+        const uint8_t* src;
+        size_t pitch;
+        if (stage == 0) {
+            src = (level == 0 ? c->last_gray : L.img) +
+                  (size_t)frame * (level == 0 ? c->last_frame_stride : (size_t)L.frame_stride);
+            pitch = level == 0 ? c->last_stride : L.stride;
+        } else {
+            src = L.blur + (size_t)frame * L.blur_frame_stride;
+            pitch = L.w;
+        }
+        HIP_CHECK(c, hipMemcpy2D(out, L.w, src, pitch, L.w, L.h, hipMemcpyDeviceToHost));
+        if (n) *n = L.w * L.h;
+        return SPSLAM_OK;
+    }
+    spslam_keypoint* o = (spslam_keypoint*)out;
+    if (stage == 2) {
+        const int ncells = L.nRows * L.nCols;
+        std::vector<uint16_t> cnt(ncells);
+        std::vector<uint32_t> cand((size_t)ncells * kCellCap);
+        const size_t cell0 = (size_t)frame * c->geom.cells_per_frame + L.cell_base;
+        HIP_CHECK(c, hipMemcpy(cnt.data(), c->b.cand_cnt + cell0, ncells * sizeof(uint16_t), hipMemcpyDeviceToHost));
+        HIP_CHECK(c, hipMemcpy(cand.data(), c->b.cand + cell0 * kCellCap, cand.size() * 4, hipMemcpyDeviceToHost));
+        int k = 0;
+        for (int ci = 0; ci < ncells; ci++)
+            for (int j = 0; j < cnt[ci]; j++, k++) {
+                if (k >= cap) continue;
+                const uint32_t v = cand[(size_t)ci * kCellCap + j];
+                o[k] = spslam_keypoint{(float)(v & 0xFFF), (float)((v >> 12) & 0xFFF), 7.f, -1.f, (float)(v >> 24), 0, -1};
+            }
+        *n = k;
+        return k > cap ? SPSLAM_ERR_CAPACITY : SPSLAM_OK;
+    }
+    if (stage == 3) {
+        int cnt = 0;
+        HIP_CHECK(c, hipMemcpy(&cnt, c->b.lvl_cnt + frame * kMaxLevels + level, sizeof(int), hipMemcpyDeviceToHost));
+        std::vector<LevelKp> v(cnt);
+        if (cnt)
+            HIP_CHECK(c, hipMemcpy(v.data(), c->b.lvl_kp + (size_t)frame * c->geom.lvl_kp_per_frame + L.kp_base,
+                                   cnt * sizeof(LevelKp), hipMemcpyDeviceToHost));
+        for (int i = 0; i < cnt && i < cap; i++)
+            o[i] = spslam_keypoint{(float)v[i].x, (float)v[i].y, (float)L.patch_size, -1.f, (float)v[i].response,
+                                   level, -1};
+        *n = cnt;
+        return cnt > cap ? SPSLAM_ERR_CAPACITY : SPSLAM_OK;
+    }
+    return fail(c, SPSLAM_ERR_ARG, "unknown stage%s", "");
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+"""ctypes binding of the C ABI in include/spslam_gpu.h (the gfx950 hot path).
+
+This is the Python side of the drop-in boundary: the same entry points a
+cgo/JNI/ctypes binding of the reference would call.  The
+library is built in-tree (`make` -> sp-slam_amd/libspslam_gpu.so); there is
+no CPU fallback -- if the library or a HIP device is missing, constructing
+`OrbExtractor` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+_HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = _HERE / "libspslam_gpu.so"
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
+                ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int), ("width", ctypes.c_int),
+                ("height", ctypes.c_int), ("max_batch", ctypes.c_int)]
+
+
+EXPORTED = [
+    "spslam_create", "spslam_destroy", "spslam_last_error", "spslam_orb_tables", "spslam_orb_max_keypoints",
+    "spslam_orb_extract", "spslam_orb_extract_batch_device", "spslam_orb_debug_stage", "spslam_orb_level_size",
+]
+
+_lib = None
+
+
+def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
+    """Load libspslam_gpu.so (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    lib = ctypes.CDLL(str(path or LIB_PATH))
+    vp, ip, fp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)
+    lib.spslam_create.argtypes = [ctypes.c_int, ctypes.POINTER(OrbParams), ctypes.POINTER(vp)]
+    lib.spslam_destroy.argtypes = [vp]
+    lib.spslam_destroy.restype = None
+    lib.spslam_last_error.argtypes = [vp]
+    lib.spslam_last_error.restype = ctypes.c_char_p
+    lib.spslam_orb_tables.argtypes = [vp, ip, fp, fp, fp, fp, ip]
+    lib.spslam_orb_max_keypoints.argtypes = [vp]
+    lib.spslam_orb_extract.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int, ip]
+    lib.spslam_orb_extract_batch_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_size_t, ctypes.c_int, vp, vp, vp,
+                                                    ctypes.c_int, vp]
+    lib.spslam_orb_debug_stage.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ip]
+    lib.spslam_orb_level_size.argtypes = [vp, ctypes.c_int, ip, ip]
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class SpslamError(RuntimeError):
+    pass
+
+
+class OrbExtractor:
+    """GPU ORB extractor; mirrors ORB_SLAM2::ORBextractor (include/ORBextractor.h:45-111)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7,
+                 width=640, height=480, max_batch=1, device=0):
+        self.lib = load_library()
+        self.params = OrbParams(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast, width, height, max_batch)
+        self.ctx = ctypes.c_void_p()
+        rc = self.lib.spslam_create(device, ctypes.byref(self.params), ctypes.byref(self.ctx))
+        if rc != 0:
+            raise SpslamError(f"spslam_create failed ({rc})")
+        self.width, self.height, self.nlevels = width, height, nlevels
+        self.max_kp = self.lib.spslam_orb_max_keypoints(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self.lib.spslam_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise SpslamError(f"rc={rc}: {self.lib.spslam_last_error(self.ctx).decode()}")
+
+    # --- ORBextractor getters (include/ORBextractor.h:63-83)
+    def tables(self):
+        n = ctypes.c_int()
+        arr = [(ctypes.c_float * 8)() for _ in range(4)]
+        fpl = (ctypes.c_int * 8)()
+        self._check(self.lib.spslam_orb_tables(self.ctx, ctypes.byref(n), *arr, fpl))
+        k = n.value
+        return dict(nlevels=k, scale=np.array(arr[0][:k]), inv_scale=np.array(arr[1][:k]),
+                    sigma2=np.array(arr[2][:k]), inv_sigma2=np.array(arr[3][:k]), features=np.array(fpl[:k]))
+
+    def level_size(self, level):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.spslam_orb_level_size(self.ctx, level, ctypes.byref(w), ctypes.byref(h)))
+        return w.value, h.value
+
+    # --- ORBextractor::operator() (host buffers)
+    def __call__(self, gray: np.ndarray):
+        gray = np.ascontiguousarray(gray, dtype=np.uint8)
+        h, w = gray.shape if gray.size else (0, 0)
+        kps = np.zeros(self.max_kp, KEYPOINT_DTYPE)
+        desc = np.zeros((self.max_kp, 32), np.uint8)
+        n = ctypes.c_int()
+        self._check(self.lib.spslam_orb_extract(self.ctx, gray.ctypes.data if gray.size else None, w, h, w,
+                                                kps.ctypes.data, desc.ctypes.data, self.max_kp, ctypes.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    # --- batched, device resident
+    def extract_batch_device(self, gray_ptr: int, n_frames: int, frame_stride: int, stride: int,
+                             kps_ptr: int, desc_ptr: int, counts_ptr: int, cap_per_frame: int, stream: int = 0):
+        self._check(self.lib.spslam_orb_extract_batch_device(self.ctx, gray_ptr, n_frames, frame_stride, stride,
+                                                             kps_ptr, desc_ptr, counts_ptr, cap_per_frame,
+                                                             stream or None))
+
+    # --- stage access for parity tests
+    def debug_stage(self, frame: int, level: int, stage: int):
+        w, h = self.level_size(level)
+        n = ctypes.c_int()
+        if stage in (0, 1):
+            out = np.zeros((h, w), np.uint8)
+            self._check(self.lib.spslam_orb_debug_stage(self.ctx, frame, level, stage, out.ctypes.data, out.size,
+                                                        ctypes.byref(n)))
+            return out
+        cap = 1 << 20 if stage == 2 else 4096
+        out = np.zeros(cap, KEYPOINT_DTYPE)
+        self._check(self.lib.spslam_orb_debug_stage(self.ctx, frame, level, stage, out.ctypes.data, cap,
+                                                    ctypes.byref(n)))
+        return out[:n.value].copy()

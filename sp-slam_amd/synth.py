@@ -1,0 +1,162 @@
+"""Synthetic RGB-D sequences for parity tests and the throughput bench.
+
+The reference datasets (TUM fr1/fr3, ICL-NUIM) are not available in the build
+container or on the GPU box, so every test/bench input is generated here
+("Synthetic inputs"):
+
+* a textured room (6 planes) plus axis-aligned boxes on the floor (each box
+  face is an extra plane; the C5-style dense scene uses >= 10 visible planes),
+* random-block texture on every face, blurred (sigma 1.5 texels) and stretched
+  to [10, 245] so FAST finds corners at iniThFAST = 20,
+* a smooth camera trajectory (about 0.3 m/s, 15 deg/s at 30 Hz),
+* depth as u16 = round(z * 5000) with N(0, 1 mm) noise and 2 % dropout to 0,
+* TUM3 intrinsics (zero distortion) by default.
+
+Everything is a pure function of (seq_id, frame index) through
+numpy.random.Generator(PCG64(0x5EED0000 + seq_id)).
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+TUM3 = dict(fx=535.4, fy=539.2, cx=320.1, cy=247.6, bf=40.0, depth_factor=5000.0, th_depth=40.0)
+
+
+@dataclasses.dataclass
+class Face:
+    axis: int          # normal axis 0/1/2 (world)
+    offset: float      # plane: X[axis] = offset
+    lo: np.ndarray     # bounds on the two other axes (in axis order)
+    hi: np.ndarray
+    tex: int           # texture index
+
+
+def _texture(rng: np.random.Generator, size: int = 1024) -> np.ndarray:
+    cells = rng.integers(0, 256, size=(size // 8, size // 8)).astype(np.float32)
+    img = np.kron(cells, np.ones((8, 8), np.float32))
+    # random dots
+    n = size * size // 200
+    ys, xs = rng.integers(2, size - 2, n), rng.integers(2, size - 2, n)
+    vals = rng.integers(0, 256, n).astype(np.float32)
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            img[ys + dy, xs + dx] = vals
+    # separable gaussian blur sigma 1.5 texels
+    r = np.arange(-4, 5, dtype=np.float32)
+    k = np.exp(-r * r / (2 * 1.5 ** 2)); k /= k.sum()
+    pad = np.pad(img, 4, mode="wrap")
+    tmp = sum(k[i] * pad[:, i:i + size] for i in range(9))
+    img = sum(k[i] * tmp[i:i + size, :] for i in range(9))
+    lo, hi = np.percentile(img, 0.5), np.percentile(img, 99.5)
+    return np.clip(10 + (img - lo) * (235.0 / max(hi - lo, 1e-3)), 10, 245).astype(np.float32)
+
+
+class Scene:
+    """Room 5 x 2.6 x 4 m (x right, y down, z forward) plus boxes on the floor."""
+
+    def __init__(self, seq_id: int = 0, n_boxes: int = 3, texel: float = 0.006):
+        self.rng = np.random.Generator(np.random.PCG64(0x5EED0000 + seq_id))
+        self.texel = texel
+        X0, X1, Y0, Y1, Z0, Z1 = -2.5, 2.5, -1.3, 1.3, -1.0, 3.0
+        faces = [
+            Face(0, X0, np.array([Y0, Z0]), np.array([Y1, Z1]), 0),
+            Face(0, X1, np.array([Y0, Z0]), np.array([Y1, Z1]), 1),
+            Face(1, Y0, np.array([X0, Z0]), np.array([X1, Z1]), 2),
+            Face(1, Y1, np.array([X0, Z0]), np.array([X1, Z1]), 3),
+            Face(2, Z0, np.array([X0, Y0]), np.array([X1, Y1]), 4),
+            Face(2, Z1, np.array([X0, Y0]), np.array([X1, Y1]), 5),
+        ]
+        ntex = 6
+        for b in range(n_boxes):
+            sx, sy, sz = self.rng.uniform(0.4, 0.9), self.rng.uniform(0.4, 1.0), self.rng.uniform(0.4, 0.9)
+            cx = self.rng.uniform(-1.8, 1.8)
+            cz = self.rng.uniform(1.4, 2.5)
+            lo = np.array([cx - sx / 2, Y1 - sy, cz - sz / 2])
+            hi = np.array([cx + sx / 2, Y1, cz + sz / 2])
+            for axis in range(3):
+                o = [a for a in range(3) if a != axis]
+                for off in (lo[axis], hi[axis]):
+                    faces.append(Face(axis, float(off), lo[o].copy(), hi[o].copy(), ntex))
+                    ntex += 1
+        self.faces = faces
+        self.textures = [_texture(self.rng) for _ in range(ntex)]
+
+    def pose(self, i: int) -> np.ndarray:
+        """Camera-to-world 4x4 at frame i (30 Hz)."""
+        t = i / 30.0
+        yaw = 0.26 * np.sin(0.5 * t)
+        pitch = 0.08 * np.sin(0.7 * t + 0.3)
+        roll = 0.05 * np.sin(0.9 * t + 1.0)
+        cy, sy = np.cos(yaw), np.sin(yaw)
+        cp, sp = np.cos(pitch), np.sin(pitch)
+        cr, sr = np.cos(roll), np.sin(roll)
+        Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+        Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+        Rz = np.array([[cr, -sr, 0], [sr, cr, 0], [0, 0, 1]])
+        T = np.eye(4)
+        T[:3, :3] = Ry @ Rx @ Rz
+        T[:3, 3] = [0.4 * np.sin(0.3 * t), 0.1 * np.sin(0.5 * t), -0.2 + 0.3 * np.sin(0.2 * t)]
+        return T
+
+    def render(self, Twc: np.ndarray, w: int = 640, h: int = 480, K=TUM3, noise_seed: int = 0,
+               depth_noise: float = 0.001, dropout: float = 0.02, gray_noise: float = 1.0):
+        """Returns (gray u8 HxW, depth u16 HxW, plane id int16 HxW)."""
+        fx, fy, cx, cy = K["fx"], K["fy"], K["cx"], K["cy"]
+        if w != 640:  # scaled intrinsics for other resolutions
+            s = w / 640.0
+            fx, fy, cx, cy = fx * s, fy * s, cx * s, cy * s
+        u, v = np.meshgrid(np.arange(w, dtype=np.float64), np.arange(h, dtype=np.float64))
+        dc = np.stack([(u - cx) / fx, (v - cy) / fy, np.ones_like(u)], -1)
+        R, o = Twc[:3, :3], Twc[:3, 3]
+        dw = dc @ R.T
+        best = np.full((h, w), np.inf)
+        fid = np.full((h, w), -1, np.int32)
+        for k, f in enumerate(self.faces):
+            den = dw[..., f.axis]
+            with np.errstate(divide="ignore", invalid="ignore"):
+                t = (f.offset - o[f.axis]) / den
+            ok = (t > 1e-6) & (t < best)
+            oth = [a for a in range(3) if a != f.axis]
+            for j, a in enumerate(oth):
+                pa = o[a] + t * dw[..., a]
+                ok &= (pa >= f.lo[j] - 1e-9) & (pa <= f.hi[j] + 1e-9)
+            best = np.where(ok, t, best)
+            fid = np.where(ok, k, fid)
+        z = np.where(np.isfinite(best), best, 0.0)  # dc has unit z, so t == camera depth
+        P = o + dw * z[..., None]
+        gray = np.zeros((h, w), np.float32)
+        for k, f in enumerate(self.faces):
+            m = fid == k
+            if not m.any():
+                continue
+            oth = [a for a in range(3) if a != f.axis]
+            tu = P[..., oth[0]][m] / self.texel + 300.0
+            tv = P[..., oth[1]][m] / self.texel + 300.0
+            tex = self.textures[f.tex]
+            n = tex.shape[0]
+            iu, iv = np.floor(tu), np.floor(tv)
+            au, av = (tu - iu).astype(np.float32), (tv - iv).astype(np.float32)
+            iu = iu.astype(np.int64) % n
+            iv = iv.astype(np.int64) % n
+            iu1, iv1 = (iu + 1) % n, (iv + 1) % n
+            val = ((1 - au) * (1 - av) * tex[iv, iu] + au * (1 - av) * tex[iv, iu1]
+                   + (1 - au) * av * tex[iv1, iu] + au * av * tex[iv1, iu1])
+            gray[m] = val
+        nrng = np.random.Generator(np.random.PCG64(0x5EED0000 + 7919 * (noise_seed + 1)))
+        gray = np.clip(np.rint(gray + nrng.normal(0, gray_noise, gray.shape)), 0, 255).astype(np.uint8)
+        zn = z + nrng.normal(0, depth_noise, z.shape)
+        depth = np.clip(np.rint(zn * K["depth_factor"]), 0, 65535).astype(np.uint16)
+        depth[nrng.random(z.shape) < dropout] = 0
+        depth[fid < 0] = 0
+        return gray, depth, fid.astype(np.int16)
+
+
+def sequence(seq_id: int, n_frames: int, w: int = 640, h: int = 480, n_boxes: int = 3):
+    """Yields (Twc, gray, depth_u16) for n_frames frames of sequence seq_id."""
+    sc = Scene(seq_id, n_boxes=n_boxes)
+    for i in range(n_frames):
+        T = sc.pose(i)
+        g, d, _ = sc.render(T, w, h, noise_seed=seq_id * 100003 + i)
+        yield T, g, d
