@@ -41,6 +41,14 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7.  If
+    # torch is importable, load it first so our DT_NEEDED libamdhip64.so.7
+    # binds to the already-loaded copy instead of a second runtime from
+    # /opt/rocm (two runtimes in one process cannot share the device).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(str(path or LIB_PATH))
     vp, ip, fp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)
     lib.spslam_create.argtypes = [ctypes.c_int, ctypes.POINTER(OrbParams), ctypes.POINTER(vp)]
