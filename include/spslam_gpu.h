@@ -104,6 +104,15 @@ int spslam_orb_extract_batch_device(spslam_ctx* ctx, const uint8_t* d_gray, int 
 int spslam_orb_debug_stage(spslam_ctx* ctx, int frame, int level, int stage, void* out, int cap, int* n);
 int spslam_orb_level_size(const spslam_ctx* ctx, int level, int* w, int* h);
 
+/* Measurement: when enabled, every kernel kind launched by this context is
+ * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
+ * per kind, the summed event time (ms) and number of timed launches since the
+ * last spslam_set_timing call (it waits for the recorded events).  Returns the
+ * number of kinds written; spslam_kernel_name(kind) names the kernel. */
+int spslam_set_timing(spslam_ctx* ctx, int enable);
+int spslam_kernel_times(spslam_ctx* ctx, double* total_ms, long long* launches, int max_kinds);
+const char* spslam_kernel_name(int kind);
+
 #ifdef __cplusplus
 }
 #endif

@@ -693,8 +693,17 @@ hipError_t orb_upload_tables(const int umax[16]) {
 
 // Enqueue the whole ORB pass for n frames on `s`.  g.lv[0].img/stride/
 // frame_stride must already point at the caller's gray frames.
+const char* kernel_kind_name(int kind) {
+    static const char* names[kNumKernelKinds] = {"resize_level_kernel", "fast_cells_kernel", "blur_kernel",
+                                                 "octree_kernel", "desc_kernel"};
+    return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
+}
+
 hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, int minTh, spslam_keypoint* kps,
-                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s) {
+                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer) {
+    auto B = [&](int k) { if (timer) timer->begin(k, s); };
+    auto E = [&](int k) { if (timer) timer->end(k, s); };
+    B(kKindResize);
     for (int l = 1; l < g.nlevels; l++) {
         const LevelGeom& P = g.lv[l - 1];
         const LevelGeom& D = g.lv[l];
@@ -702,13 +711,22 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
         hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P.img, P.w, P.h, P.stride, P.frame_stride,
                            const_cast<uint8_t*>(D.img), D.w, D.h, D.stride, D.frame_stride);
     }
+    E(kKindResize);
+    B(kKindFast);
     hipLaunchKernelGGL(fast_cells_kernel, dim3(g.cells_per_frame, n), dim3(64), 0, s, g, b.cand, b.cand_cnt, iniTh,
                        minTh);
+    E(kKindFast);
+    B(kKindBlur);
     hipLaunchKernelGGL(blur_kernel, dim3(g.blur_tiles_per_frame, n), dim3(256), 0, s, g);
+    E(kKindBlur);
+    B(kKindOctree);
     hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
                        b.lvl_kp, b.lvl_cnt);
+    E(kKindOctree);
+    B(kKindDesc);
     hipLaunchKernelGGL(desc_kernel, dim3((g.lvl_kp_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.lvl_kp, b.lvl_cnt,
                        kps, desc, counts, cap_per_frame);
+    E(kKindDesc);
     return hipGetLastError();
 }
 

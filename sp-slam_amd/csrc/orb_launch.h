@@ -16,8 +16,20 @@ struct OrbBuffers {
     int* lvl_cnt;        // [frames][kMaxLevels]
 };
 
+// Kernel kinds for the per-kind HIP-event timers (spslam_kernel_times).
+enum KernelKind { kKindResize = 0, kKindFast, kKindBlur, kKindOctree, kKindDesc, kNumKernelKinds };
+const char* kernel_kind_name(int kind);
+
+// Optional timer: begin/end are called on the launch stream around each kernel
+// kind (the resize kind spans its per-level launches).
+struct KernelTimer {
+    virtual void begin(int kind, hipStream_t s) = 0;
+    virtual void end(int kind, hipStream_t s) = 0;
+    virtual ~KernelTimer() = default;
+};
+
 hipError_t orb_upload_tables(const int umax[16]);
 hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, int minTh, spslam_keypoint* kps,
-                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s);
+                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer);
 
 }  // namespace spslam

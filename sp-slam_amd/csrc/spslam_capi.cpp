@@ -19,6 +19,45 @@
 
 using namespace spslam;
 
+// HIP-event timer per kernel kind; events recorded on the launch stream.
+struct EventTimer : KernelTimer {
+    struct Pair { int kind; hipEvent_t e0, e1; };
+    std::vector<Pair> pending;
+    std::vector<hipEvent_t> pool;
+    double total_ms[kNumKernelKinds] = {};
+    long long count[kNumKernelKinds] = {};
+    hipEvent_t cur[kNumKernelKinds] = {};
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void begin(int kind, hipStream_t s) override { cur[kind] = get(); (void)hipEventRecord(cur[kind], s); }
+    void end(int kind, hipStream_t s) override {
+        hipEvent_t e1 = get();
+        (void)hipEventRecord(e1, s);
+        pending.push_back(Pair{kind, cur[kind], e1});
+    }
+    void collect() {
+        for (auto& p : pending) {
+            float ms = 0.f;
+            if (hipEventSynchronize(p.e1) == hipSuccess && hipEventElapsedTime(&ms, p.e0, p.e1) == hipSuccess) {
+                total_ms[p.kind] += ms;
+                count[p.kind] += 1;
+            }
+            pool.push_back(p.e0);
+            pool.push_back(p.e1);
+        }
+        pending.clear();
+    }
+    void reset() { collect(); for (int k = 0; k < kNumKernelKinds; k++) { total_ms[k] = 0; count[k] = 0; } }
+    ~EventTimer() override {
+        for (auto& p : pending) { (void)hipEventDestroy(p.e0); (void)hipEventDestroy(p.e1); }
+        for (auto e : pool) (void)hipEventDestroy(e);
+    }
+};
+
 struct spslam_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -43,6 +82,7 @@ struct spslam_ctx {
     const uint8_t* last_gray = nullptr;
     size_t last_frame_stride = 0;
     int last_stride = 0, last_frames = 0;
+    EventTimer* timer = nullptr;
 };
 
 namespace {
@@ -160,6 +200,8 @@ void free_all(spslam_ctx* c) {
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c->timer;
+    c->timer = nullptr;
 }
 
 // Point level 0 at the caller's frames and levels >= 1 at the context pyramid.
@@ -288,7 +330,7 @@ int spslam_orb_extract_batch_device(spslam_ctx* c, const uint8_t* d_gray, int n_
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
     bind_frames(c, d_gray, frame_stride, stride);
     HIP_CHECK(c, orb_launch(c->geom, c->b, n_frames, c->p.ini_th_fast, c->p.min_th_fast, d_kps, d_desc, d_counts,
-                            cap_per_frame, s));
+                            cap_per_frame, s, c->timer));
     c->last_gray = d_gray;
     c->last_frame_stride = frame_stride;
     c->last_stride = stride;
@@ -321,6 +363,28 @@ int spslam_orb_extract(spslam_ctx* c, const uint8_t* gray, int w, int h, int str
     }
     return SPSLAM_OK;
 }
+
+int spslam_set_timing(spslam_ctx* c, int enable) {
+    if (!c) return SPSLAM_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    if (enable && !c->timer) c->timer = new EventTimer();
+    if (!enable && c->timer) { delete c->timer; c->timer = nullptr; }
+    if (c->timer) c->timer->reset();
+    return SPSLAM_OK;
+}
+
+int spslam_kernel_times(spslam_ctx* c, double* total_ms, long long* launches, int max_kinds) {
+    if (!c) return SPSLAM_ERR_ARG;
+    const int n = std::min(max_kinds, (int)kNumKernelKinds);
+    if (c->timer) c->timer->collect();
+    for (int k = 0; k < n; k++) {
+        if (total_ms) total_ms[k] = c->timer ? c->timer->total_ms[k] : 0.0;
+        if (launches) launches[k] = c->timer ? c->timer->count[k] : 0;
+    }
+    return n;
+}
+
+const char* spslam_kernel_name(int kind) { return kernel_kind_name(kind); }
 
 int spslam_orb_debug_stage(spslam_ctx* c, int frame, int level, int stage, void* out, int cap, int* n) {
     if (!c || !out || level < 0 || level >= c->p.nlevels) return SPSLAM_ERR_ARG;

@@ -31,6 +31,7 @@ class OrbParams(ctypes.Structure):
 EXPORTED = [
     "spslam_create", "spslam_destroy", "spslam_last_error", "spslam_orb_tables", "spslam_orb_max_keypoints",
     "spslam_orb_extract", "spslam_orb_extract_batch_device", "spslam_orb_debug_stage", "spslam_orb_level_size",
+    "spslam_set_timing", "spslam_kernel_times", "spslam_kernel_name",
 ]
 
 _lib = None
@@ -63,6 +64,11 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
                                                     ctypes.c_int, vp]
     lib.spslam_orb_debug_stage.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, ip]
     lib.spslam_orb_level_size.argtypes = [vp, ctypes.c_int, ip, ip]
+    lib.spslam_set_timing.argtypes = [vp, ctypes.c_int]
+    lib.spslam_kernel_times.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong),
+                                        ctypes.c_int]
+    lib.spslam_kernel_name.argtypes = [ctypes.c_int]
+    lib.spslam_kernel_name.restype = ctypes.c_char_p
     if path is None:
         _lib = lib
     return lib
@@ -133,6 +139,17 @@ class OrbExtractor:
         self._check(self.lib.spslam_orb_extract_batch_device(self.ctx, gray_ptr, n_frames, frame_stride, stride,
                                                              kps_ptr, desc_ptr, counts_ptr, cap_per_frame,
                                                              stream or None))
+
+    # --- measurement
+    def set_timing(self, enable: bool):
+        self._check(self.lib.spslam_set_timing(self.ctx, int(enable)))
+
+    def kernel_times(self):
+        """{kernel name: (total ms, launches)} since set_timing(True)."""
+        tot = (ctypes.c_double * 32)()
+        cnt = (ctypes.c_longlong * 32)()
+        n = self.lib.spslam_kernel_times(self.ctx, tot, cnt, 32)
+        return {self.lib.spslam_kernel_name(k).decode(): (tot[k], cnt[k]) for k in range(n)}
 
     # --- stage access for parity tests
     def debug_stage(self, frame: int, level: int, stage: int):
