@@ -15,6 +15,8 @@
  * Reference interfaces replaced (paths relative to the reference tree):
  *   spslam_orb_*        ORB_SLAM2::ORBextractor (include/ORBextractor.h:45-111,
  *                       src/ORBextractor.cc:410-470, 1043-1132)
+ *   spslam_pose_*       Optimizer::PoseOptimization (include/Optimizer.h:47,
+ *                       src/Optimizer.cc:519-1152) with g2oAddition plane edges
  */
 #ifndef SPSLAM_GPU_H
 #define SPSLAM_GPU_H
@@ -103,6 +105,85 @@ int spslam_orb_extract_batch_device(spslam_ctx* ctx, const uint8_t* d_gray, int 
  *            orientation; count in *n). */
 int spslam_orb_debug_stage(spslam_ctx* ctx, int frame, int level, int stage, void* out, int cap, int* n);
 int spslam_orb_level_size(const spslam_ctx* ctx, int level, int* w, int* h);
+
+/* ------------------------------------------------------------------------
+ * PoseOptimization (src/Optimizer.cc:519-1152; include/Optimizer.h:47).
+ *
+ * The reference builds a g2o graph from Frame/MapPoint/MapPlane members; at
+ * this boundary the caller passes those members flattened:
+ *   - one spslam_point_obs per keypoint i with mvpMapPoints[i] != NULL, in
+ *     increasing i (the reference's edge insertion order, :561-647);
+ *   - one spslam_plane_obs per plane edge, all kind 0 (mvpMapPlanes) first,
+ *     then kind 1 (mvpParallelPlanes), then kind 2 (mvpVerticalPlanes), each
+ *     in increasing plane index (:700-859).  world = MapPlane::GetWorldPos(),
+ *     meas = Frame::mvPlaneCoefficients[i]; map_plane_id = MapPlane::mnId
+ *     (only used for the vertex-id bookkeeping the reference does).
+ * Results: the optimized Tcw (what Frame::SetPose receives, :1149-1150), the
+ * returned inlier count (:1151; 0 when fewer than 3 point correspondences,
+ * :653), and the per-observation outlier flags (mvbOutlier, mvbPlaneOutlier,
+ * mvbParPlaneOutlier, mvbVerPlaneOutlier). */
+typedef struct spslam_point_obs {
+    float u, v;        /* mvKeysUn[i].pt */
+    float ur;          /* mvuRight[i]; < 0 -> monocular edge */
+    float inv_sigma2;  /* mvInvLevelSigma2[mvKeysUn[i].octave] */
+    float xw[3];       /* MapPoint::GetWorldPos() */
+    int32_t kp_index;  /* i (informational) */
+} spslam_point_obs;
+
+#define SPSLAM_PLANE_EDGE 0      /* g2o::EdgePlane          (3-D error) */
+#define SPSLAM_PARALLEL_EDGE 1   /* g2o::EdgeParallelPlane  (2-D error) */
+#define SPSLAM_VERTICAL_EDGE 2   /* g2o::EdgeVerticalPlane  (2-D error) */
+
+typedef struct spslam_plane_obs {
+    float meas[4];     /* frame plane coefficients (a,b,c,d) */
+    float world[4];    /* map plane world coefficients */
+    int32_t kind;      /* SPSLAM_*_EDGE */
+    int32_t plane_index;
+    int32_t map_plane_id;
+    int32_t pad;
+} spslam_plane_obs;
+
+/* Config keys read by PoseOptimization (src/Optimizer.cc:681-693; YAML
+ * Plane.AngleInfo/DistanceInfo/ParallelInfo/VerticalInfo/Chi/VPChi). */
+typedef struct spslam_plane_config {
+    double angle_info, distance_info, parallel_info, vertical_info, chi, vp_chi;
+} spslam_plane_config;
+
+typedef struct spslam_pose_problem {
+    float Tcw[16];      /* Frame::mTcw, row-major 4x4 */
+    float fx, fy, cx, cy, bf;
+    int32_t n_points;   /* observations [point_offset, point_offset + n_points) */
+    int32_t n_planes;
+    int32_t point_offset;
+    int32_t plane_offset;
+    int32_t pad;
+} spslam_pose_problem;
+
+typedef struct spslam_pose_result {
+    float Tcw[16];      /* optimized pose (unchanged input if n_inliers == 0 by the <3 rule) */
+    int32_t n_inliers;  /* PoseOptimization return value */
+    int32_t lm_iterations;  /* total LM iterations run (diagnostic) */
+    int32_t pad[2];
+} spslam_pose_result;
+
+/* Drop-in for Optimizer::PoseOptimization(Frame*) on host buffers, one frame.
+ * point_outlier / plane_outlier (n_points / n_planes bytes) receive the
+ * outlier flags. */
+int spslam_pose_optimize(spslam_ctx* ctx, const spslam_pose_problem* problem, const spslam_point_obs* points,
+                         const spslam_plane_obs* planes, const spslam_plane_config* cfg, spslam_pose_result* result,
+                         uint8_t* point_outlier, uint8_t* plane_outlier);
+
+/* Batched, device resident: n problems, one workgroup each.  Observation
+ * arrays are indexed through each problem's point/plane offsets; the outlier
+ * flag arrays share those offsets.  If d_init_from is non-NULL, problem p
+ * starts from d_init_from[p].Tcw instead of its own Tcw (used to chain the
+ * motion-model and local-map optimizations of one frame on the device).
+ * Asynchronous on hip_stream (NULL = context stream). */
+int spslam_pose_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_pose_problem* d_problems,
+                                      const spslam_point_obs* d_points, const spslam_plane_obs* d_planes,
+                                      const spslam_plane_config* cfg, const spslam_pose_result* d_init_from,
+                                      spslam_pose_result* d_results, uint8_t* d_point_outlier,
+                                      uint8_t* d_plane_outlier, void* hip_stream);
 
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,

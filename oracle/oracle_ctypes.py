@@ -167,3 +167,20 @@ def descriptor(img: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
     out = np.zeros(32, np.uint8)
     lib().oracle_descriptor(img.ctypes.data, img.shape[1], img.shape[0], x, y, angle, out.ctypes.data)
     return out
+
+
+def pose_optimize(problem, points, planes, cfg=None):
+    """Oracle Optimizer::PoseOptimization.  Same arrays/dtypes as spslam_gpu.pose_optimize."""
+    import spslam_gpu as G  # dtypes/config only (no GPU call)
+    L = lib()
+    L.oracle_pose_optimize.argtypes = [ctypes.c_void_p] * 7
+    cfg = cfg or G.PlaneConfig.tum()
+    problem = np.ascontiguousarray(problem, G.POSE_PROBLEM_DTYPE).reshape(())
+    points = np.ascontiguousarray(points, G.POINT_OBS_DTYPE)
+    planes = np.ascontiguousarray(planes, G.PLANE_OBS_DTYPE)
+    res = np.zeros((), G.POSE_RESULT_DTYPE)
+    po = np.zeros(max(len(points), 1), np.uint8)
+    plo = np.zeros(max(len(planes), 1), np.uint8)
+    L.oracle_pose_optimize(problem.ctypes.data, points.ctypes.data, planes.ctypes.data, ctypes.addressof(cfg),
+                           res.ctypes.data, po.ctypes.data, plo.ctypes.data)
+    return res, po[:len(points)].astype(bool), plo[:len(planes)].astype(bool)

@@ -1,0 +1,538 @@
+// ORACLE -- TEST INFRASTRUCTURE ONLY (see orb_oracle.h for the rules).
+//
+// CPU restatement of Optimizer::PoseOptimization (src/Optimizer.cc:519-1152)
+// on top of a minimal restatement of the vendored g2o pieces it uses:
+//   SparseOptimizer::initializeOptimization/optimize/activeRobustChi2
+//     (Thirdparty/g2o/g2o/core/sparse_optimizer.cpp:100-114,199-267,354-420)
+//   OptimizationAlgorithmLevenberg::solve / computeLambdaInit / computeScale
+//     (core/optimization_algorithm_levenberg.cpp:61-189)
+//   BlockSolver::buildSystem/setLambda (core/block_solver.hpp:502-590),
+//   LinearSolverDense (Eigen LDLT, solvers/linear_solver_dense.h:65-115)
+//   RobustKernelHuber (core/robust_kernel_impl.cpp:78-91), robustInformation
+//     (core/base_edge.h:96-102), quadratic forms (base_unary_edge.hpp:43-72,
+//     base_binary_edge.hpp:55-120), numeric Jacobian (base_binary_edge.hpp:130-205)
+//   SE3Quat / VertexSE3Expmap (types/se3quat.h, types_six_dof_expmap.h:73-76)
+//   EdgeSE3ProjectXYZOnlyPose / EdgeStereoSE3ProjectXYZOnlyPose
+//     (types_six_dof_expmap.h:143-202, .cpp:266-364)
+//   g2oAddition Plane3D / EdgePlane / EdgeParallelPlane / EdgeVerticalPlane
+// and the Eigen 3 routines they call (Quaternion(Matrix3), toRotationMatrix,
+// quaternion product and vector rotation, AngleAxis, LDLT with diagonal
+// pivoting).  All arithmetic is double, like the reference.
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "../include/spslam_gpu.h"
+
+namespace oracle {
+namespace {
+
+struct V3 { double x, y, z; };
+inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+inline double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline V3 cross(V3 a, V3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline double norm(V3 a) { return std::sqrt(dot(a, a)); }
+
+struct M3 { double m[3][3]; };
+inline V3 mul(const M3& R, V3 v) {
+    return {R.m[0][0] * v.x + R.m[0][1] * v.y + R.m[0][2] * v.z, R.m[1][0] * v.x + R.m[1][1] * v.y + R.m[1][2] * v.z,
+            R.m[2][0] * v.x + R.m[2][1] * v.y + R.m[2][2] * v.z};
+}
+inline M3 transpose(const M3& R) {
+    M3 T;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T.m[i][j] = R.m[j][i];
+    return T;
+}
+inline M3 mul(const M3& A, const M3& B) {
+    M3 C;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C.m[i][j] = A.m[i][0] * B.m[0][j] + A.m[i][1] * B.m[1][j] + A.m[i][2] * B.m[2][j];
+    return C;
+}
+
+struct Quat { double w, x, y, z; };
+// Eigen::Quaternion(const Matrix3&) (Eigen/src/Geometry/Quaternion.h quaternionbase_assign_impl)
+Quat quat_from_rot(const M3& R) {
+    Quat q;
+    double t = R.m[0][0] + R.m[1][1] + R.m[2][2];
+    if (t > 0) {
+        t = std::sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (R.m[2][1] - R.m[1][2]) * t;
+        q.y = (R.m[0][2] - R.m[2][0]) * t;
+        q.z = (R.m[1][0] - R.m[0][1]) * t;
+    } else {
+        int i = 0;
+        if (R.m[1][1] > R.m[0][0]) i = 1;
+        if (R.m[2][2] > R.m[i][i]) i = 2;
+        int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(R.m[i][i] - R.m[j][j] - R.m[k][k] + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (R.m[k][j] - R.m[j][k]) * t;
+        c[j] = (R.m[j][i] + R.m[i][j]) * t;
+        c[k] = (R.m[k][i] + R.m[i][k]) * t;
+        q.x = c[0]; q.y = c[1]; q.z = c[2];
+    }
+    return q;
+}
+M3 quat_to_rot(const Quat& q) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    M3 R;
+    R.m[0][0] = 1 - (tyy + tzz); R.m[0][1] = txy - twz; R.m[0][2] = txz + twy;
+    R.m[1][0] = txy + twz; R.m[1][1] = 1 - (txx + tzz); R.m[1][2] = tyz - twx;
+    R.m[2][0] = txz - twy; R.m[2][1] = tyz + twx; R.m[2][2] = 1 - (txx + tyy);
+    return R;
+}
+Quat quat_mul(const Quat& a, const Quat& b) {
+    return {a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+            a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z, a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x};
+}
+// Eigen QuaternionBase::_transformVector
+V3 quat_rotate(const Quat& q, V3 v) {
+    V3 qv{q.x, q.y, q.z};
+    V3 uv = cross(qv, v);
+    uv = uv + uv;
+    return v + q.w * uv + cross(qv, uv);
+}
+void quat_normalize_rotation(Quat& q) {  // SE3Quat::normalizeRotation
+    if (q.w < 0) { q.w = -q.w; q.x = -q.x; q.y = -q.y; q.z = -q.z; }
+    double n = std::sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+    q.w /= n; q.x /= n; q.y /= n; q.z /= n;
+}
+
+struct SE3 {
+    Quat r{1, 0, 0, 0};
+    V3 t{0, 0, 0};
+    static SE3 from_Rt(const M3& R, V3 t) { SE3 s; s.r = quat_from_rot(R); s.t = t; quat_normalize_rotation(s.r); return s; }
+    V3 map(V3 X) const { return quat_rotate(r, X) + t; }
+    SE3 operator*(const SE3& b) const {
+        SE3 res = *this;
+        res.t = res.t + quat_rotate(r, b.t);
+        res.r = quat_mul(res.r, b.r);
+        quat_normalize_rotation(res.r);
+        return res;
+    }
+    // SE3Quat::exp, types/se3quat.h:223-257
+    static SE3 exp(const double u[6]) {
+        V3 w{u[0], u[1], u[2]}, ups{u[3], u[4], u[5]};
+        double theta = norm(w);
+        M3 O{{{0, -w.z, w.y}, {w.z, 0, -w.x}, {-w.y, w.x, 0}}};
+        M3 R, V;
+        if (theta < 0.00001) {
+            M3 O2 = mul(O, O);
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) R.m[i][j] = (i == j ? 1.0 : 0.0) + O.m[i][j] + O2.m[i][j];
+            V = R;
+        } else {
+            M3 O2 = mul(O, O);
+            double a = std::sin(theta) / theta, b = (1 - std::cos(theta)) / (theta * theta),
+                   c = (theta - std::sin(theta)) / std::pow(theta, 3);
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++) {
+                    R.m[i][j] = (i == j ? 1.0 : 0.0) + a * O.m[i][j] + b * O2.m[i][j];
+                    V.m[i][j] = (i == j ? 1.0 : 0.0) + b * O.m[i][j] + c * O2.m[i][j];
+                }
+        }
+        SE3 s;
+        s.r = quat_from_rot(R);
+        s.t = mul(V, ups);
+        quat_normalize_rotation(s.r);
+        return s;
+    }
+};
+
+// --- g2oAddition/Plane3D.h -------------------------------------------------
+struct Plane {
+    double c[4];
+    V3 normal() const { return {c[0], c[1], c[2]}; }
+    double distance() const { return -c[3]; }
+    static void normalize(double* v) {
+        double n = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        for (int i = 0; i < 4; i++) v[i] = v[i] * (1. / n);
+        if (v[3] < 0.0)
+            for (int i = 0; i < 4; i++) v[i] = -v[i];
+    }
+    static Plane from(const double* v) { Plane p; std::memcpy(p.c, v, sizeof p.c); normalize(p.c); return p; }
+};
+double azimuth(V3 v) { return std::atan2(v.y, v.x); }
+double elevation(V3 v) { return std::atan2(v.z, std::sqrt(v.x * v.x + v.y * v.y)); }
+Quat aa_quat(double angle, V3 axis) {  // Eigen Quaternion(AngleAxis)
+    double ha = 0.5 * angle, s = std::sin(ha);
+    return {std::cos(ha), s * axis.x, s * axis.y, s * axis.z};
+}
+M3 aa_rot(double angle, V3 a) {  // Eigen AngleAxis::toRotationMatrix
+    V3 sa = std::sin(angle) * a;
+    double c = std::cos(angle);
+    V3 c1 = (1 - c) * a;
+    M3 r;
+    double tmp;
+    tmp = c1.x * a.y; r.m[0][1] = tmp - sa.z; r.m[1][0] = tmp + sa.z;
+    tmp = c1.x * a.z; r.m[0][2] = tmp + sa.y; r.m[2][0] = tmp - sa.y;
+    tmp = c1.y * a.z; r.m[1][2] = tmp - sa.x; r.m[2][1] = tmp + sa.x;
+    r.m[0][0] = c1.x * a.x + c; r.m[1][1] = c1.y * a.y + c; r.m[2][2] = c1.z * a.z + c;
+    return r;
+}
+M3 plane_rotation(V3 v) {  // Plane3D::rotation
+    Quat q = quat_mul(aa_quat(azimuth(v), {0, 0, 1}), aa_quat(-elevation(v), {0, 1, 0}));
+    return quat_to_rot(q);
+}
+// operator*(Isometry3D, Plane3D)
+Plane transform(const SE3& T, const Plane& p) {
+    M3 R = quat_to_rot(T.r);
+    V3 n2 = mul(R, p.normal());
+    double v2[4] = {n2.x, n2.y, n2.z, p.c[3] - dot(T.t, n2)};
+    if (v2[3] < 0.0)
+        for (double& e : v2) e = -e;
+    return Plane::from(v2);
+}
+void ominus(const Plane& a, const Plane& b, double* e) {
+    M3 R = transpose(plane_rotation(a.normal()));
+    V3 n = mul(R, b.normal());
+    e[0] = azimuth(n); e[1] = elevation(n); e[2] = a.distance() - b.distance();
+}
+void ominus_par(const Plane& a, const Plane& b, double* e) {
+    V3 nor = a.normal();
+    if (dot(b.normal(), nor) < 0) nor = -1.0 * nor;
+    M3 R = transpose(plane_rotation(nor));
+    V3 n = mul(R, b.normal());
+    e[0] = azimuth(n); e[1] = elevation(n);
+}
+void ominus_ver(const Plane& a, const Plane& b, double* e) {
+    V3 v = cross(a.normal(), b.normal());
+    V3 ax = (1.0 / norm(v)) * v;
+    V3 bb = mul(aa_rot(M_PI / 2, ax), a.normal());
+    M3 R = transpose(plane_rotation(bb));
+    V3 n = mul(R, b.normal());
+    e[0] = azimuth(n); e[1] = elevation(n);
+}
+
+// --- edges -------------------------------------------------------------------
+struct Huber {
+    bool on = true;
+    double delta = 0, dsqr = 0;
+    void set(double d) { delta = d; dsqr = d * d; }
+    void robustify(double e, double rho[3]) const {
+        if (e <= dsqr) { rho[0] = e; rho[1] = 1.; rho[2] = 0.; }
+        else { double s = std::sqrt(e); rho[0] = 2 * s * delta - dsqr; rho[1] = delta / s; rho[2] = -0.5 * rho[1] / e; }
+    }
+};
+
+struct Edge {
+    int type;   // 0 mono, 1 stereo, 2 plane, 3 parallel, 4 vertical
+    int dim;
+    int level = 0;
+    Huber rk;
+    double info[3];   // diagonal information
+    double meas[3];   // point measurements
+    V3 Xw;
+    Plane world, mplane;
+    double err[3] = {0, 0, 0};
+    double chi2() const { double s = 0; for (int i = 0; i < dim; i++) s += err[i] * info[i] * err[i]; return s; }
+};
+
+struct Cam { double fx, fy, cx, cy, bf; };
+
+void compute_error(Edge& e, const SE3& T, const Cam& c) {
+    if (e.type == 0) {
+        V3 p = T.map(e.Xw);
+        double px = p.x / p.z, py = p.y / p.z;
+        e.err[0] = e.meas[0] - (px * c.fx + c.cx);
+        e.err[1] = e.meas[1] - (py * c.fy + c.cy);
+    } else if (e.type == 1) {
+        V3 p = T.map(e.Xw);
+        const float invz = (float)(1.0f / p.z);
+        double r0 = p.x * invz * c.fx + c.cx, r1 = p.y * invz * c.fy + c.cy, r2 = r0 - c.bf * invz;
+        e.err[0] = e.meas[0] - r0; e.err[1] = e.meas[1] - r1; e.err[2] = e.meas[2] - r2;
+    } else {
+        Plane local = transform(T, e.world);
+        if (e.type == 2) ominus(local, e.mplane, e.err);
+        else if (e.type == 3) ominus_par(local, e.mplane, e.err);
+        else ominus_ver(local, e.mplane, e.err);
+    }
+}
+
+// Jacobian wrt the pose update (rows = e.dim, cols 6).
+void jacobian(Edge& e, const SE3& T, const Cam& c, double J[3][6]) {
+    if (e.type <= 1) {
+        V3 p = T.map(e.Xw);
+        double x = p.x, y = p.y, invz = 1.0 / p.z, invz_2 = invz * invz;
+        J[0][0] = x * y * invz_2 * c.fx; J[0][1] = -(1 + (x * x * invz_2)) * c.fx; J[0][2] = y * invz * c.fx;
+        J[0][3] = -invz * c.fx; J[0][4] = 0; J[0][5] = x * invz_2 * c.fx;
+        J[1][0] = (1 + y * y * invz_2) * c.fy; J[1][1] = -x * y * invz_2 * c.fy; J[1][2] = -x * invz * c.fy;
+        J[1][3] = 0; J[1][4] = -invz * c.fy; J[1][5] = y * invz_2 * c.fy;
+        if (e.type == 1) {
+            J[2][0] = J[0][0] - c.bf * y * invz_2; J[2][1] = J[0][1] + c.bf * x * invz_2; J[2][2] = J[0][2];
+            J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - c.bf * invz_2;
+        }
+        return;
+    }
+    // numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205)
+    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    double bak[3], save[3];
+    std::memcpy(save, e.err, sizeof save);
+    for (int d = 0; d < 6; d++) {
+        double add[6] = {0, 0, 0, 0, 0, 0};
+        add[d] = delta;
+        SE3 Tp = SE3::exp(add) * T;
+        compute_error(e, Tp, c);
+        for (int i = 0; i < e.dim; i++) bak[i] = e.err[i];
+        add[d] = -delta;
+        SE3 Tm = SE3::exp(add) * T;
+        compute_error(e, Tm, c);
+        for (int i = 0; i < e.dim; i++) J[i][d] = scalar * (bak[i] - e.err[i]);
+    }
+    std::memcpy(e.err, save, sizeof save);
+}
+
+// Eigen::LDLT<MatrixXd> compute (diagonal pivoting, lower storage) + solve.
+bool ldlt_solve(double A[6][6], const double b[6], double x[6]) {
+    const int n = 6;
+    double m[6][6];
+    std::memcpy(m, A, sizeof m);
+    int tr[6];
+    int sign = 0;  // 0 zero, 1 possemidef, 2 negsemidef, 3 indefinite
+    bool ret = true, found_zero = false;
+    double temp[6];
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = std::fabs(m[k][k]);
+        for (int i = k + 1; i < n; i++)
+            if (std::fabs(m[i][i]) > bv) { bv = std::fabs(m[i][i]); big = i; }
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; j++) std::swap(m[k][j], m[big][j]);
+            for (int i = big + 1; i < n; i++) std::swap(m[i][k], m[i][big]);
+            std::swap(m[k][k], m[big][big]);
+            for (int i = k + 1; i < big; ++i) { double t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
+        }
+        const int rs = n - k - 1;
+        if (k > 0) {
+            for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
+            double s = 0;
+            for (int j = 0; j < k; j++) s += m[k][j] * temp[j];
+            m[k][k] -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += m[i][j] * temp[j];
+                m[i][k] -= t;
+            }
+        }
+        const double akk = m[k][k];
+        const bool valid = std::fabs(akk) > 0;
+        if (k == 0 && !valid) { sign = 0; return false; }
+        if (rs > 0 && valid)
+            for (int i = k + 1; i < n; i++) m[i][k] /= akk;
+        if (found_zero && valid) ret = false;
+        else if (!valid) found_zero = true;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    (void)ret;
+    const bool positive = sign == 1 || sign == 0;
+    if (!positive) return false;
+    // solve: P b, L y = Pb, D z = y (pseudo-inverse), L^T w = z, x = P^T w
+    double y[6];
+    std::memcpy(y, b, sizeof y);
+    for (int k = 0; k < n; k++) std::swap(y[k], y[tr[k]]);
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) y[i] -= m[i][j] * y[j];
+    double maxd = 0;
+    for (int i = 0; i < n; i++) maxd = std::max(maxd, std::fabs(m[i][i]));
+    const double tol = std::numeric_limits<double>::min();  // Eigen: RealScalar(1)/NumTraits::highest()
+    (void)maxd;
+    for (int i = 0; i < n; i++) y[i] = std::fabs(m[i][i]) > tol ? y[i] / m[i][i] : 0.0;
+    for (int i = n - 1; i >= 0; i--)
+        for (int j = i + 1; j < n; j++) y[i] -= m[j][i] * y[j];
+    for (int k = n - 1; k >= 0; k--) std::swap(y[k], y[tr[k]]);
+    std::memcpy(x, y, sizeof y);
+    return true;
+}
+
+struct LM {
+    double lambda = -1, ni = 2;
+    int nBad = 0;
+};
+
+double robust_chi2(const std::vector<Edge*>& active) {
+    double chi = 0;
+    for (Edge* e : active) {
+        if (e->rk.on) { double rho[3]; e->rk.robustify(e->chi2(), rho); chi += rho[0]; }
+        else chi += e->chi2();
+    }
+    return chi;
+}
+
+// SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg.
+int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
+    LM lm;
+    int its = 0;
+    for (int it = 0; it < iterations; it++) {
+        for (Edge* e : active) compute_error(*e, T, c);
+        double currentChi = robust_chi2(active), tempChi = currentChi, iniChi = currentChi;
+        // buildSystem
+        double H[6][6] = {}, b[6] = {};
+        for (Edge* e : active) {
+            double J[3][6];
+            jacobian(*e, T, c, J);
+            double w = 1.0;
+            if (e->rk.on) { double rho[3]; e->rk.robustify(e->chi2(), rho); w = rho[1]; }
+            for (int r = 0; r < e->dim; r++) {
+                const double oe = e->info[r] * e->err[r];
+                for (int i = 0; i < 6; i++) {
+                    b[i] -= w * J[r][i] * oe;
+                    for (int j = 0; j < 6; j++) H[i][j] += J[r][i] * (w * e->info[r]) * J[r][j];
+                }
+            }
+        }
+        if (it == 0) {
+            double maxDiag = 0;
+            for (int j = 0; j < 6; j++) maxDiag = std::max(std::fabs(H[j][j]), maxDiag);
+            lm.lambda = 1e-5 * maxDiag;
+            lm.ni = 2;
+            lm.nBad = 0;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            SE3 backup = T;
+            double Hl[6][6];
+            std::memcpy(Hl, H, sizeof Hl);
+            for (int j = 0; j < 6; j++) Hl[j][j] += lm.lambda;
+            double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten (rejected step)
+            bool ok2 = ldlt_solve(Hl, b, x);
+            T = SE3::exp(x) * T;
+            for (Edge* e : active) compute_error(*e, T, c);
+            tempChi = robust_chi2(active);
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            rho = currentChi - tempChi;
+            double scale = 0;
+            for (int j = 0; j < 6; j++) scale += x[j] * (lm.lambda * x[j] + b[j]);
+            scale += 1e-3;
+            rho /= scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                double sf = std::max(1. / 3., alpha);
+                lm.lambda *= sf;
+                lm.ni = 2;
+                currentChi = tempChi;
+            } else {
+                lm.lambda *= lm.ni;
+                lm.ni *= 2;
+                T = backup;
+            }
+            qmax++;
+        } while (rho < 0 && qmax < 10);
+        its++;
+        if (qmax == 10 || rho == 0) break;
+        if ((iniChi - currentChi) * 1e3 < iniChi) lm.nBad++;
+        else lm.nBad = 0;
+        if (lm.nBad >= 3) break;
+    }
+    return its;
+}
+
+}  // namespace
+}  // namespace oracle
+
+using namespace oracle;
+
+extern "C" int oracle_pose_optimize(const spslam_pose_problem* P, const spslam_point_obs* pts,
+                                    const spslam_plane_obs* pls, const spslam_plane_config* cfg,
+                                    spslam_pose_result* out, uint8_t* pout, uint8_t* plout) {
+    M3 R;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) R.m[i][j] = P->Tcw[4 * i + j];
+    const SE3 T0 = SE3::from_Rt(R, {P->Tcw[3], P->Tcw[7], P->Tcw[11]});
+    const Cam cam{P->fx, P->fy, P->cx, P->cy, P->bf};
+    const float deltaMono = std::sqrt(5.991), deltaStereo = std::sqrt(7.815);
+    std::vector<Edge> edges;
+    edges.reserve(P->n_points + P->n_planes);
+    int nInitial = 0;
+    for (int i = 0; i < P->n_points; i++) {
+        const spslam_point_obs& o = pts[i];
+        Edge e;
+        e.Xw = {o.xw[0], o.xw[1], o.xw[2]};
+        e.meas[0] = o.u; e.meas[1] = o.v;
+        if (o.ur < 0) { e.type = 0; e.dim = 2; e.rk.set(deltaMono); }
+        else { e.type = 1; e.dim = 3; e.meas[2] = o.ur; e.rk.set(deltaStereo); }
+        for (int k = 0; k < 3; k++) e.info[k] = (double)o.inv_sigma2;
+        edges.push_back(e);
+        nInitial++;
+        pout[i] = 0;
+    }
+    std::memcpy(out->Tcw, P->Tcw, sizeof out->Tcw);
+    out->lm_iterations = 0;
+    if (nInitial < 3) { out->n_inliers = 0; for (int i = 0; i < P->n_planes; i++) plout[i] = 0; return 0; }
+    const double angleInfo = 3282.8 / (cfg->angle_info * cfg->angle_info);
+    const double disInfo = cfg->distance_info * cfg->distance_info;
+    const double parInfo = 3282.8 / (cfg->parallel_info * cfg->parallel_info);
+    const double verInfo = 3282.8 / (cfg->vertical_info * cfg->vertical_info);
+    const double planeChi = cfg->chi, VPplaneChi = cfg->vp_chi;
+    const float deltaPlane = std::sqrt(planeChi), VPdeltaPlane = std::sqrt(VPplaneChi);
+    for (int i = 0; i < P->n_planes; i++) {
+        const spslam_plane_obs& o = pls[i];
+        Edge e;
+        e.type = 2 + o.kind;
+        e.dim = o.kind == 0 ? 3 : 2;
+        double w[4], m[4];
+        for (int k = 0; k < 4; k++) { w[k] = o.world[k]; m[k] = o.meas[k]; }
+        if (o.world[3] < 0.0f) for (double& v : w) v = -v;   // Converter::toPlane3D
+        if (o.meas[3] < 0.0f) for (double& v : m) v = -v;
+        e.world = Plane::from(w);
+        e.mplane = Plane::from(m);
+        if (o.kind == 0) { e.info[0] = e.info[1] = angleInfo; e.info[2] = disInfo; e.rk.set(deltaPlane); }
+        else { const double inf = o.kind == 1 ? parInfo : verInfo; e.info[0] = e.info[1] = inf; e.info[2] = 0; e.rk.set(VPdeltaPlane); }
+        edges.push_back(e);
+        nInitial++;
+        plout[i] = 0;
+    }
+    SE3 T = T0;
+    int nBad = 0, total_its = 0;
+    for (int it = 0; it < 4; it++) {
+        T = T0;
+        std::vector<Edge*> active;
+        for (Edge& e : edges)
+            if (e.level == 0) active.push_back(&e);
+        total_its += optimize(active, T, cam, 10);
+        nBad = 0;
+        for (size_t k = 0; k < edges.size(); k++) {
+            Edge& e = edges[k];
+            const bool is_point = e.type <= 1;
+            uint8_t& flag = is_point ? pout[k] : plout[k - P->n_points];
+            if (flag) compute_error(e, T, cam);
+            const float chi2 = (float)e.chi2();
+            bool bad;
+            if (e.type == 0) bad = chi2 > 5.991f;
+            else if (e.type == 1) bad = chi2 > 7.815f;
+            else if (e.type == 2) bad = chi2 > planeChi;
+            else bad = chi2 > VPplaneChi;
+            flag = bad ? 1 : 0;
+            e.level = bad ? 1 : 0;
+            nBad += bad;
+            if (it == 2) e.rk.on = false;
+        }
+        if (edges.size() < 10) break;
+    }
+    // Converter::toCvMat(SE3Quat): to_homogeneous_matrix -> float
+    M3 Rr = quat_to_rot(T.r);
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) out->Tcw[4 * i + j] = (float)Rr.m[i][j];
+    }
+    out->Tcw[3] = (float)T.t.x; out->Tcw[7] = (float)T.t.y; out->Tcw[11] = (float)T.t.z;
+    out->Tcw[12] = 0.f; out->Tcw[13] = 0.f; out->Tcw[14] = 0.f; out->Tcw[15] = 1.f;
+    out->n_inliers = nInitial - nBad;
+    out->lm_iterations = total_its;
+    return out->n_inliers;
+}

@@ -695,7 +695,7 @@ hipError_t orb_upload_tables(const int umax[16]) {
 // frame_stride must already point at the caller's gray frames.
 const char* kernel_kind_name(int kind) {
     static const char* names[kNumKernelKinds] = {"resize_level_kernel", "fast_cells_kernel", "blur_kernel",
-                                                 "octree_kernel", "desc_kernel"};
+                                                 "octree_kernel", "desc_kernel", "pose_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

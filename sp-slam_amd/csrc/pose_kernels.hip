@@ -1,0 +1,577 @@
+// gfx950 PoseOptimization (reference: src/Optimizer.cc:519-1152 on the
+// vendored g2o Levenberg-Marquardt + g2oAddition plane edges).
+//
+// One 256-thread workgroup per frame problem runs all 4 rounds x <= 10 LM
+// iterations (x <= 10 trials) with no host round trip.  Per LM iteration:
+//   pass A  (all threads)  per-edge error, Huber weight and Jacobian, local
+//                          sums of robust chi2, J^T W J (21 terms), J^T W e (6)
+//   reduce                 wave shuffles + LDS, fp64
+//   solve   (thread 0)     (H + lambda I) x = b by LDLT with diagonal pivoting
+//                          (Eigen::LDLT, solvers/linear_solver_dense.h:103-110)
+//   pass B  (all threads)  robust chi2 at exp(x) * T, accept/reject, lambda
+// Outlier relabeling after each round reproduces the reference's use of the
+// errors cached by the LAST computeActiveErrors (which may belong to a
+// rejected trial): those errors are recomputed at that trial pose.
+// All arithmetic is fp64 like g2o/Eigen; reductions are tree-ordered, so the
+// result matches the reference to rounding, not bitwise.
+#include <hip/hip_runtime.h>
+
+#include "../../include/spslam_gpu.h"
+#include "pose_launch.h"
+
+namespace spslam {
+namespace pose {
+
+struct V3 { double x, y, z; };
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+struct Q { double w, x, y, z; };
+struct SE3 { Q r; V3 t; };
+struct M3 { double a[9]; };  // row-major
+
+__device__ __forceinline__ V3 mv(const M3& R, V3 v) {
+    return {R.a[0] * v.x + R.a[1] * v.y + R.a[2] * v.z, R.a[3] * v.x + R.a[4] * v.y + R.a[5] * v.z,
+            R.a[6] * v.x + R.a[7] * v.y + R.a[8] * v.z};
+}
+__device__ __forceinline__ V3 mtv(const M3& R, V3 v) {  // R^T v
+    return {R.a[0] * v.x + R.a[3] * v.y + R.a[6] * v.z, R.a[1] * v.x + R.a[4] * v.y + R.a[7] * v.z,
+            R.a[2] * v.x + R.a[5] * v.y + R.a[8] * v.z};
+}
+
+// Eigen Quaternion(Matrix3)
+__device__ Q q_from_rot(const M3& R) {
+    Q q;
+    double t = R.a[0] + R.a[4] + R.a[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (R.a[7] - R.a[5]) * t;
+        q.y = (R.a[2] - R.a[6]) * t;
+        q.z = (R.a[3] - R.a[1]) * t;
+    } else {
+        int i = 0;
+        if (R.a[4] > R.a[0]) i = 1;
+        if (R.a[8] > R.a[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(R.a[4 * i] - R.a[4 * j] - R.a[4 * k] + 1.0);
+        double c[3];
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (R.a[3 * k + j] - R.a[3 * j + k]) * t;
+        c[j] = (R.a[3 * j + i] + R.a[3 * i + j]) * t;
+        c[k] = (R.a[3 * k + i] + R.a[3 * i + k]) * t;
+        q.x = c[0]; q.y = c[1]; q.z = c[2];
+    }
+    return q;
+}
+__device__ M3 q_to_rot(const Q& q) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    return M3{{1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx, txz - twy, tyz + twx,
+               1 - (txx + tyy)}};
+}
+__device__ __forceinline__ Q q_mul(const Q& a, const Q& b) {
+    return {a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+            a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z, a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ V3 q_rot(const Q& q, V3 v) {  // Eigen _transformVector
+    const V3 qv{q.x, q.y, q.z};
+    V3 uv = cross(qv, v);
+    uv = uv + uv;
+    return v + q.w * uv + cross(qv, uv);
+}
+__device__ __forceinline__ void q_normalize(Q& q) {  // SE3Quat::normalizeRotation
+    if (q.w < 0) { q.w = -q.w; q.x = -q.x; q.y = -q.y; q.z = -q.z; }
+    const double n = sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+    q.w /= n; q.x /= n; q.y /= n; q.z /= n;
+}
+__device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
+    SE3 r = a;
+    r.t = r.t + q_rot(a.r, b.t);
+    r.r = q_mul(r.r, b.r);
+    q_normalize(r.r);
+    return r;
+}
+// SE3Quat::exp (types/se3quat.h:223-257)
+__device__ SE3 se3_exp(const double* u) {
+    const V3 w{u[0], u[1], u[2]}, ups{u[3], u[4], u[5]};
+    const double theta = sqrt(dot(w, w));
+    const double O[9] = {0, -w.z, w.y, w.z, 0, -w.x, -w.y, w.x, 0};
+    double O2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+    M3 R, V;
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; k++) R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
+        V = R;
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta),
+                     c = (theta - sin(theta)) / pow(theta, 3);
+        for (int k = 0; k < 9; k++) {
+            R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
+            V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
+        }
+    }
+    SE3 s;
+    s.r = q_from_rot(R);
+    s.t = mv(V, ups);
+    q_normalize(s.r);
+    return s;
+}
+
+// ---- g2oAddition/Plane3D.h ------------------------------------------------
+struct P4 { double c[4]; };
+__device__ __forceinline__ void p_normalize(double* v) {
+    const double n = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    for (int i = 0; i < 4; i++) v[i] = v[i] * (1. / n);
+    if (v[3] < 0.0)
+        for (int i = 0; i < 4; i++) v[i] = -v[i];
+}
+__device__ __forceinline__ double azimuth(V3 v) { return atan2(v.y, v.x); }
+__device__ __forceinline__ double elevation(V3 v) { return atan2(v.z, sqrt(v.x * v.x + v.y * v.y)); }
+// Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
+__device__ M3 p_rotation(V3 v) {
+    const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
+    const Q a{cos(ha), 0.0 * sin(ha), 0.0 * sin(ha), 1.0 * sin(ha)};
+    const Q e{cos(he), 0.0 * sin(he), 1.0 * sin(he), 0.0 * sin(he)};
+    return q_to_rot(q_mul(a, e));
+}
+// Eigen AngleAxis::toRotationMatrix() * v
+__device__ V3 aa_apply(double ang, V3 ax, V3 v) {
+    const V3 sa = sin(ang) * ax;
+    const double c = cos(ang);
+    const V3 c1 = (1 - c) * ax;
+    M3 r;
+    double tmp;
+    tmp = c1.x * ax.y; r.a[1] = tmp - sa.z; r.a[3] = tmp + sa.z;
+    tmp = c1.x * ax.z; r.a[2] = tmp + sa.y; r.a[6] = tmp - sa.y;
+    tmp = c1.y * ax.z; r.a[5] = tmp - sa.x; r.a[7] = tmp + sa.x;
+    r.a[0] = c1.x * ax.x + c; r.a[4] = c1.y * ax.y + c; r.a[8] = c1.z * ax.z + c;
+    return mv(r, v);
+}
+
+// plane-edge error: (T * world).ominus{,_par,_ver}(meas)
+__device__ void plane_error(int kind, const SE3& T, const P4& world, const P4& meas, double* e) {
+    const M3 R = q_to_rot(T.r);
+    const V3 n2 = mv(R, V3{world.c[0], world.c[1], world.c[2]});
+    double v[4] = {n2.x, n2.y, n2.z, world.c[3] - dot(T.t, n2)};
+    if (v[3] < 0.0)
+        for (int i = 0; i < 4; i++) v[i] = -v[i];
+    p_normalize(v);
+    const V3 ln{v[0], v[1], v[2]}, mn{meas.c[0], meas.c[1], meas.c[2]};
+    V3 ref = ln;
+    if (kind == 1) {
+        if (dot(mn, ln) < 0) ref = -1.0 * ln;
+    } else if (kind == 2) {
+        const V3 a = cross(ln, mn);
+        ref = aa_apply(M_PI / 2, (1.0 / sqrt(dot(a, a))) * a, ln);
+    }
+    const V3 n = mtv(p_rotation(ref), mn);
+    e[0] = azimuth(n);
+    e[1] = elevation(n);
+    if (kind == 0) e[2] = (-v[3]) - (-meas.c[3]);
+}
+
+struct Cam { double fx, fy, cx, cy, bf; };
+
+__device__ __forceinline__ void point_error(const spslam_point_obs& o, const SE3& T, const Cam& c, double* e,
+                                            V3* pc) {
+    const V3 p = q_rot(T.r, V3{(double)o.xw[0], (double)o.xw[1], (double)o.xw[2]}) + T.t;
+    if (pc) *pc = p;
+    if (o.ur < 0) {
+        e[0] = (double)o.u - (p.x / p.z * c.fx + c.cx);
+        e[1] = (double)o.v - (p.y / p.z * c.fy + c.cy);
+    } else {
+        const float invz = (float)(1.0f / p.z);  // float reciprocal, types_six_dof_expmap.cpp:300
+        const double r0 = p.x * invz * c.fx + c.cx, r1 = p.y * invz * c.fy + c.cy;
+        e[0] = (double)o.u - r0;
+        e[1] = (double)o.v - r1;
+        e[2] = (double)o.ur - (r0 - c.bf * invz);
+    }
+}
+
+// Eigen::LDLT (lower, diagonal pivoting) + solve.  Returns false when the
+// factor is not positive (LinearSolverDense::solve returns false, x unchanged).
+__device__ bool ldlt_solve(double m[6][6], const double* b, double* x) {
+    const int n = 6;
+    int tr[6];
+    int sign = 0;
+    double temp[6];
+    for (int k = 0; k < n; ++k) {
+        int big = k;
+        double bv = fabs(m[k][k]);
+        for (int i = k + 1; i < n; i++)
+            if (fabs(m[i][i]) > bv) { bv = fabs(m[i][i]); big = i; }
+        tr[k] = big;
+        if (k != big) {
+            for (int j = 0; j < k; j++) { double t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
+            for (int i = big + 1; i < n; i++) { double t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
+            { double t = m[k][k]; m[k][k] = m[big][big]; m[big][big] = t; }
+            for (int i = k + 1; i < big; ++i) { double t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
+        }
+        if (k > 0) {
+            for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
+            double s = 0;
+            for (int j = 0; j < k; j++) s += m[k][j] * temp[j];
+            m[k][k] -= s;
+            for (int i = k + 1; i < n; i++) {
+                double t = 0;
+                for (int j = 0; j < k; j++) t += m[i][j] * temp[j];
+                m[i][k] -= t;
+            }
+        }
+        const double akk = m[k][k];
+        const bool valid = fabs(akk) > 0;
+        if (k == 0 && !valid) return false;
+        if (k + 1 < n && valid)
+            for (int i = k + 1; i < n; i++) m[i][k] /= akk;
+        if (sign == 1) { if (akk < 0) sign = 3; }
+        else if (sign == 2) { if (akk > 0) sign = 3; }
+        else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
+    }
+    if (!(sign == 1 || sign == 0)) return false;
+    double y[6];
+    for (int i = 0; i < n; i++) y[i] = b[i];
+    for (int k = 0; k < n; k++) { double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < i; j++) y[i] -= m[i][j] * y[j];
+    for (int i = 0; i < n; i++) y[i] = fabs(m[i][i]) > 2.2250738585072014e-308 ? y[i] / m[i][i] : 0.0;
+    for (int i = n - 1; i >= 0; i--)
+        for (int j = i + 1; j < n; j++) y[i] -= m[j][i] * y[j];
+    for (int k = n - 1; k >= 0; k--) { double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+    for (int i = 0; i < n; i++) x[i] = y[i];
+    return true;
+}
+
+constexpr int kThreads = 256;
+constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
+
+struct Shared {
+    double red[kThreads / 64][kRed];
+    double H[6][6], b[6], x[6];
+    double lambda, ni, currentChi, iniChi, tempChi;
+    SE3 T, T0, Ttrial, Tlast;
+    int nBad, stop, active_any;
+    int count[kThreads / 64];
+};
+
+// Block reduction of `n` doubles per thread (v[0..n)) into S.red[0][0..n).
+template <int NV>
+__device__ void block_reduce(double (&v)[NV], int n, Shared& S) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int k = 0; k < n; k++) {
+        double x = v[k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+        if (lane == 0) S.red[w][k] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < n) {
+        double s = 0;
+        for (int j = 0; j < kThreads / 64; j++) s += S.red[j][threadIdx.x];
+        S.red[0][threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void huber(double chi, double delta, bool on, double* rho0, double* rho1) {
+    const double dsqr = delta * delta;
+    if (!on || chi <= dsqr) { *rho0 = chi; *rho1 = 1.0; return; }
+    const double s = sqrt(chi);
+    *rho0 = 2 * s * delta - dsqr;
+    *rho1 = delta / s;
+}
+
+}  // namespace pose
+
+using namespace pose;
+
+__global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+                                                   const spslam_point_obs* __restrict__ pts_all,
+                                                   const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
+                                                   const spslam_pose_result* __restrict__ init_from,
+                                                   spslam_pose_result* __restrict__ results,
+                                                   uint8_t* __restrict__ pout_all, uint8_t* __restrict__ plout_all) {
+    __shared__ Shared S;
+    const int t = threadIdx.x;
+    const spslam_pose_problem P = probs[blockIdx.x];
+    const spslam_point_obs* pts = pts_all + P.point_offset;
+    const spslam_plane_obs* pls = pls_all + P.plane_offset;
+    uint8_t* pout = pout_all + P.point_offset;
+    uint8_t* plout = plout_all + P.plane_offset;
+    spslam_pose_result* res = results + blockIdx.x;
+    const float* Tin = init_from ? init_from[blockIdx.x].Tcw : P.Tcw;
+    const int np = P.n_points, nl = P.n_planes, ne = np + nl;
+    const Cam cam{P.fx, P.fy, P.cx, P.cy, P.bf};
+
+    for (int i = t; i < np; i += kThreads) pout[i] = 0;
+    for (int i = t; i < nl; i += kThreads) plout[i] = 0;
+    if (np < 3) {  // nInitialCorrespondences < 3 (:653): no SetPose
+        if (t < 16) res->Tcw[t] = Tin[t];
+        if (t == 0) { res->n_inliers = 0; res->lm_iterations = 0; }
+        return;
+    }
+    if (t == 0) {
+        M3 R;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) R.a[3 * i + j] = Tin[4 * i + j];
+        S.T0.r = q_from_rot(R);
+        S.T0.t = V3{Tin[3], Tin[7], Tin[11]};
+        q_normalize(S.T0.r);
+    }
+    __syncthreads();
+
+    // edge e < np: point e; else plane e - np.  Per-edge info/delta:
+    auto edge_info = [&](int e, double* info, double* delta, int* dim) {
+        if (e < np) {
+            const spslam_point_obs& o = pts[e];
+            info[0] = info[1] = info[2] = (double)o.inv_sigma2;
+            *dim = o.ur < 0 ? 2 : 3;
+            *delta = o.ur < 0 ? K.delta_mono : K.delta_stereo;
+        } else {
+            const int kind = pls[e - np].kind;
+            if (kind == 0) { info[0] = info[1] = K.angle_info; info[2] = K.dis_info; *delta = K.delta_plane; *dim = 3; }
+            else { info[0] = info[1] = kind == 1 ? K.par_info : K.ver_info; info[2] = 0; *delta = K.delta_vp; *dim = 2; }
+        }
+    };
+    auto plane_of = [&](int e, P4& w, P4& m) {
+        const spslam_plane_obs& o = pls[e - np];
+        for (int k = 0; k < 4; k++) { w.c[k] = o.world[k]; m.c[k] = o.meas[k]; }
+        if (o.world[3] < 0.0f) for (int k = 0; k < 4; k++) w.c[k] = -w.c[k];  // Converter::toPlane3D
+        if (o.meas[3] < 0.0f) for (int k = 0; k < 4; k++) m.c[k] = -m.c[k];
+        p_normalize(w.c);
+        p_normalize(m.c);
+    };
+    auto error_at = [&](int e, const SE3& T, double* err, V3* pc) {
+        if (e < np) point_error(pts[e], T, cam, err, pc);
+        else {
+            P4 w, m;
+            plane_of(e, w, m);
+            plane_error(pls[e - np].kind, T, w, m, err);
+        }
+    };
+    auto is_outlier = [&](int e) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
+
+    bool robust = true;
+    int nBad = 0, total_its = 0;
+    for (int round = 0; round < 4; round++) {
+        if (t == 0) S.T = S.T0;
+        // any active edge?
+        int act = 0;
+        for (int e = t; e < ne; e += kThreads) act |= !is_outlier(e);
+        act = __syncthreads_or(act);
+        if (act) {
+            for (int it = 0; it < 10; it++) {
+                // ---- pass A: errors, robust chi2, quadratic form at T
+                double v[kRed];
+                for (int k = 0; k < kRed; k++) v[k] = 0;
+                const SE3 T = S.T;
+                for (int e = t; e < ne; e += kThreads) {
+                    if (is_outlier(e)) continue;
+                    double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
+                    int dim;
+                    edge_info(e, info, &delta, &dim);
+                    V3 pc;
+                    error_at(e, T, err, &pc);
+                    double chi = 0;
+                    for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
+                    double rho0, rho1;
+                    huber(chi, delta, robust, &rho0, &rho1);
+                    v[0] += rho0;
+                    if (e < np) {
+                        const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
+                        J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+                        J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
+                        J[0][5] = x * invz_2 * cam.fx;
+                        J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
+                        J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
+                        J[1][5] = y * invz_2 * cam.fy;
+                        if (dim == 3) {
+                            J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
+                            J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
+                        }
+                    } else {
+                        // numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205)
+                        const double dl = 1e-9, scalar = 1.0 / (2 * dl);
+                        for (int d = 0; d < 6; d++) {
+                            double add[6] = {0, 0, 0, 0, 0, 0}, ep[3] = {0, 0, 0}, em[3] = {0, 0, 0};
+                            add[d] = dl;
+                            error_at(e, se3_mul(se3_exp(add), T), ep, nullptr);
+                            add[d] = -dl;
+                            error_at(e, se3_mul(se3_exp(add), T), em, nullptr);
+                            for (int r = 0; r < dim; r++) J[r][d] = scalar * (ep[r] - em[r]);
+                        }
+                    }
+                    int k = 1;
+                    for (int i = 0; i < 6; i++)
+                        for (int j = i; j < 6; j++, k++) {
+                            double s = 0;
+                            for (int r = 0; r < dim; r++) s += J[r][i] * (rho1 * info[r]) * J[r][j];
+                            v[k] += s;
+                        }
+                    for (int i = 0; i < 6; i++) {
+                        double s = 0;
+                        for (int r = 0; r < dim; r++) s += rho1 * J[r][i] * (info[r] * err[r]);
+                        v[22 + i] -= s;
+                    }
+                }
+                block_reduce(v, kRed, S);
+                if (t == 0) {
+                    S.Tlast = S.T;
+                    S.currentChi = S.red[0][0];
+                    S.iniChi = S.currentChi;
+                    int k = 1;
+                    for (int i = 0; i < 6; i++)
+                        for (int j = i; j < 6; j++, k++) S.H[i][j] = S.H[j][i] = S.red[0][k];
+                    for (int i = 0; i < 6; i++) S.b[i] = S.red[0][22 + i];
+                    if (it == 0) {
+                        double md = 0;
+                        for (int j = 0; j < 6; j++) md = fmax(fabs(S.H[j][j]), md);
+                        S.lambda = 1e-5 * md;
+                        S.ni = 2;
+                        S.nBad = 0;
+                    }
+                    for (int j = 0; j < 6; j++) S.x[j] = 0;
+                }
+                __syncthreads();
+                // ---- trials
+                double rho = 0;
+                int qmax = 0;
+                bool ok2 = true;
+                do {
+                    if (t == 0) {
+                        double Hl[6][6];
+                        for (int i = 0; i < 6; i++)
+                            for (int j = 0; j < 6; j++) Hl[i][j] = S.H[i][j] + (i == j ? S.lambda : 0.0);
+                        double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten
+                        S.stop = ldlt_solve(Hl, S.b, x) ? 1 : 0;
+                        for (int j = 0; j < 6; j++) S.x[j] = x[j];
+                        S.Ttrial = se3_mul(se3_exp(x), S.T);
+                    }
+                    __syncthreads();
+                    ok2 = S.stop != 0;
+                    const SE3 Tt = S.Ttrial;
+                    double c[1] = {0};
+                    for (int e = t; e < ne; e += kThreads) {
+                        if (is_outlier(e)) continue;
+                        double info[3], delta, err[3] = {0, 0, 0};
+                        int dim;
+                        edge_info(e, info, &delta, &dim);
+                        error_at(e, Tt, err, nullptr);
+                        double chi = 0;
+                        for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
+                        double rho0, rho1;
+                        huber(chi, delta, robust, &rho0, &rho1);
+                        c[0] += rho0;
+                    }
+                    block_reduce(c, 1, S);
+                    if (t == 0) {
+                        S.Tlast = S.Ttrial;
+                        double tempChi = S.red[0][0];
+                        if (!ok2) tempChi = 1.7976931348623157e308;
+                        double r = S.currentChi - tempChi;
+                        double scale = 0;
+                        for (int j = 0; j < 6; j++) scale += S.x[j] * (S.lambda * S.x[j] + S.b[j]);
+                        scale += 1e-3;
+                        r /= scale;
+                        if (r > 0 && isfinite(tempChi)) {
+                            double alpha = 1. - pow((2 * r - 1), 3);
+                            alpha = fmin(alpha, 2. / 3.);
+                            S.lambda *= fmax(1. / 3., alpha);
+                            S.ni = 2;
+                            S.currentChi = tempChi;
+                            S.T = S.Ttrial;
+                        } else {
+                            S.lambda *= S.ni;
+                            S.ni *= 2;
+                        }
+                        S.tempChi = r;  // broadcast rho
+                    }
+                    __syncthreads();
+                    rho = S.tempChi;
+                    qmax++;
+                } while (rho < 0 && qmax < 10);
+                total_its++;
+                if (qmax == 10 || rho == 0) break;
+                int stop = 0;
+                if (t == 0) {
+                    if ((S.iniChi - S.currentChi) * 1e3 < S.iniChi) S.nBad++;
+                    else S.nBad = 0;
+                    S.stop = S.nBad >= 3;
+                }
+                __syncthreads();
+                stop = S.stop;
+                __syncthreads();
+                if (stop) break;
+            }
+        }
+        // ---- relabel (:925-1140)
+        const SE3 T = S.T, Tl = S.Tlast;
+        int bad = 0;
+        for (int e = t; e < ne; e += kThreads) {
+            double info[3], delta, err[3] = {0, 0, 0};
+            int dim;
+            edge_info(e, info, &delta, &dim);
+            const bool was_out = is_outlier(e);
+            error_at(e, was_out ? T : Tl, err, nullptr);
+            double chi = 0;
+            for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
+            const float chi2 = (float)chi;
+            bool b;
+            if (e < np) b = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
+            else b = pls[e - np].kind == 0 ? (double)chi2 > K.plane_chi : (double)chi2 > K.vp_chi;
+            bad += b;
+            if (e < np) pout[e] = b;
+            else plout[e - np] = b;
+        }
+        // wave-sum then LDS
+        for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
+        if ((t & 63) == 0) S.count[t >> 6] = bad;
+        __syncthreads();
+        nBad = S.count[0] + S.count[1] + S.count[2] + S.count[3];
+        __syncthreads();
+        if (round == 2) robust = false;
+        if (ne < 10) break;
+    }
+    if (t == 0) {
+        const M3 R = q_to_rot(S.T.r);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) res->Tcw[4 * i + j] = (float)R.a[3 * i + j];
+        res->Tcw[3] = (float)S.T.t.x; res->Tcw[7] = (float)S.T.t.y; res->Tcw[11] = (float)S.T.t.z;
+        res->Tcw[12] = 0.f; res->Tcw[13] = 0.f; res->Tcw[14] = 0.f; res->Tcw[15] = 1.f;
+        res->n_inliers = ne - nBad;
+        res->lm_iterations = total_its;
+    }
+}
+
+PoseConsts make_pose_consts(const spslam_plane_config& c) {
+    PoseConsts K;
+    K.delta_mono = (double)(float)sqrt(5.991);
+    K.delta_stereo = (double)(float)sqrt(7.815);
+    K.angle_info = 3282.8 / (c.angle_info * c.angle_info);
+    K.dis_info = c.distance_info * c.distance_info;
+    K.par_info = 3282.8 / (c.parallel_info * c.parallel_info);
+    K.ver_info = 3282.8 / (c.vertical_info * c.vertical_info);
+    K.plane_chi = c.chi;
+    K.vp_chi = c.vp_chi;
+    K.delta_plane = (double)(float)sqrt(c.chi);
+    K.delta_vp = (double)(float)sqrt(c.vp_chi);
+    return K;
+}
+
+hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_point_obs* pts,
+                       const spslam_plane_obs* pls, const PoseConsts& K, const spslam_pose_result* init_from,
+                       spslam_pose_result* res, uint8_t* pout, uint8_t* plout, hipStream_t s) {
+    hipLaunchKernelGGL(pose_kernel, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

@@ -16,6 +16,7 @@
 
 #include "../../include/spslam_gpu.h"
 #include "orb_launch.h"
+#include "pose_launch.h"
 
 using namespace spslam;
 
@@ -83,6 +84,9 @@ struct spslam_ctx {
     size_t last_frame_stride = 0;
     int last_stride = 0, last_frames = 0;
     EventTimer* timer = nullptr;
+    // drop-in PoseOptimization staging
+    uint8_t* d_pose_scratch = nullptr;
+    size_t pose_scratch_bytes = 0;
 };
 
 namespace {
@@ -196,7 +200,7 @@ const char* build_geom(spslam_ctx* c) {
 
 void free_all(spslam_ctx* c) {
     void* ptrs[] = {c->d_pyr, c->d_blur, c->b.cand, c->b.cand_cnt, c->b.keys, c->b.keynode,
-                    c->b.lvl_kp, c->b.lvl_cnt, c->d_in, c->d_kps, c->d_desc, c->d_cnt};
+                    c->b.lvl_kp, c->b.lvl_cnt, c->d_in, c->d_kps, c->d_desc, c->d_cnt, c->d_pose_scratch};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -361,6 +365,66 @@ int spslam_orb_extract(spslam_ctx* c, const uint8_t* gray, int w, int h, int str
         if (kps) HIP_CHECK(c, hipMemcpy(kps, c->d_kps, cnt * sizeof(spslam_keypoint), hipMemcpyDeviceToHost));
         if (desc) HIP_CHECK(c, hipMemcpy(desc, c->d_desc, (size_t)cnt * 32, hipMemcpyDeviceToHost));
     }
+    return SPSLAM_OK;
+}
+
+int spslam_pose_optimize_batch_device(spslam_ctx* c, int n, const spslam_pose_problem* d_problems,
+                                      const spslam_point_obs* d_points, const spslam_plane_obs* d_planes,
+                                      const spslam_plane_config* cfg, const spslam_pose_result* d_init_from,
+                                      spslam_pose_result* d_results, uint8_t* d_point_outlier,
+                                      uint8_t* d_plane_outlier, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n < 0 || !cfg || (n > 0 && (!d_problems || !d_points || !d_results || !d_point_outlier)))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_pose_optimize_batch_device");
+    if (n == 0) return SPSLAM_OK;
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    const PoseConsts K = make_pose_consts(*cfg);
+    if (c->timer) c->timer->begin(kKindPose, s);
+    HIP_CHECK(c, pose_launch(n, d_problems, d_points, d_planes, K, d_init_from, d_results, d_point_outlier,
+                             d_plane_outlier, s));
+    if (c->timer) c->timer->end(kKindPose, s);
+    return SPSLAM_OK;
+}
+
+int spslam_pose_optimize(spslam_ctx* c, const spslam_pose_problem* problem, const spslam_point_obs* points,
+                         const spslam_plane_obs* planes, const spslam_plane_config* cfg, spslam_pose_result* result,
+                         uint8_t* point_outlier, uint8_t* plane_outlier) {
+    if (!c || !problem || !cfg || !result) return SPSLAM_ERR_ARG;
+    const int np = problem->n_points, nl = problem->n_planes;
+    if (np < 0 || nl < 0 || (np && (!points || !point_outlier)) || (nl && (!planes || !plane_outlier)))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_pose_optimize");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t need = sizeof(spslam_pose_problem) + sizeof(spslam_pose_result) +
+                        (size_t)np * (sizeof(spslam_point_obs) + 1) + (size_t)nl * (sizeof(spslam_plane_obs) + 1) +
+                        256;
+    if (need > c->pose_scratch_bytes) {
+        if (c->d_pose_scratch) (void)hipFree(c->d_pose_scratch);
+        c->d_pose_scratch = nullptr;
+        c->pose_scratch_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_pose_scratch, need * 2));
+        c->pose_scratch_bytes = need * 2;
+    }
+    uint8_t* base = c->d_pose_scratch;
+    auto carve = [&](size_t bytes) { uint8_t* p = base; base += (bytes + 15) / 16 * 16; return p; };
+    auto* d_prob = (spslam_pose_problem*)carve(sizeof(spslam_pose_problem));
+    auto* d_res = (spslam_pose_result*)carve(sizeof(spslam_pose_result));
+    auto* d_pts = (spslam_point_obs*)carve((size_t)np * sizeof(spslam_point_obs));
+    auto* d_pls = (spslam_plane_obs*)carve((size_t)nl * sizeof(spslam_plane_obs));
+    auto* d_po = carve((size_t)np + 1);
+    auto* d_plo = carve((size_t)nl + 1);
+    spslam_pose_problem prob = *problem;
+    prob.point_offset = 0;
+    prob.plane_offset = 0;
+    HIP_CHECK(c, hipMemcpyAsync(d_prob, &prob, sizeof prob, hipMemcpyHostToDevice, c->stream));
+    if (np) HIP_CHECK(c, hipMemcpyAsync(d_pts, points, np * sizeof(spslam_point_obs), hipMemcpyHostToDevice, c->stream));
+    if (nl) HIP_CHECK(c, hipMemcpyAsync(d_pls, planes, nl * sizeof(spslam_plane_obs), hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_pose_optimize_batch_device(c, 1, d_prob, d_pts, d_pls, cfg, nullptr, d_res, d_po, d_plo, c->stream);
+    if (rc) return rc;
+    HIP_CHECK(c, hipMemcpyAsync(result, d_res, sizeof *result, hipMemcpyDeviceToHost, c->stream));
+    if (np) HIP_CHECK(c, hipMemcpyAsync(point_outlier, d_po, np, hipMemcpyDeviceToHost, c->stream));
+    if (nl) HIP_CHECK(c, hipMemcpyAsync(plane_outlier, d_plo, nl, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return SPSLAM_OK;
 }
 

@@ -165,3 +165,66 @@ class OrbExtractor:
         self._check(self.lib.spslam_orb_debug_stage(self.ctx, frame, level, stage, out.ctypes.data, cap,
                                                     ctypes.byref(n)))
         return out[:n.value].copy()
+
+
+# ---------------------------------------------------------------------------
+# PoseOptimization (include/spslam_gpu.h, spslam_pose_*)
+POINT_OBS_DTYPE = np.dtype([("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("inv_sigma2", "<f4"), ("xw", "<f4", 3),
+                            ("kp_index", "<i4")])
+PLANE_OBS_DTYPE = np.dtype([("meas", "<f4", 4), ("world", "<f4", 4), ("kind", "<i4"), ("plane_index", "<i4"),
+                            ("map_plane_id", "<i4"), ("pad", "<i4")])
+POSE_PROBLEM_DTYPE = np.dtype([("Tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                               ("bf", "<f4"), ("n_points", "<i4"), ("n_planes", "<i4"), ("point_offset", "<i4"),
+                               ("plane_offset", "<i4"), ("pad", "<i4")])
+POSE_RESULT_DTYPE = np.dtype([("Tcw", "<f4", 16), ("n_inliers", "<i4"), ("lm_iterations", "<i4"),
+                              ("pad", "<i4", 2)])
+assert POINT_OBS_DTYPE.itemsize == 32 and PLANE_OBS_DTYPE.itemsize == 48
+assert POSE_PROBLEM_DTYPE.itemsize == 104 and POSE_RESULT_DTYPE.itemsize == 80
+
+
+class PlaneConfig(ctypes.Structure):
+    """Plane.* YAML keys read by PoseOptimization (TUM1.yaml defaults)."""
+    _fields_ = [("angle_info", ctypes.c_double), ("distance_info", ctypes.c_double),
+                ("parallel_info", ctypes.c_double), ("vertical_info", ctypes.c_double), ("chi", ctypes.c_double),
+                ("vp_chi", ctypes.c_double)]
+
+    @classmethod
+    def tum(cls):
+        return cls(1.0, 100.0, 0.5, 0.5, 300.0, 300.0)
+
+
+def _bind_pose(lib):
+    vp = ctypes.c_void_p
+    lib.spslam_pose_optimize.argtypes = [vp, vp, vp, vp, ctypes.POINTER(PlaneConfig), vp, vp, vp]
+    lib.spslam_pose_optimize_batch_device.argtypes = [vp, ctypes.c_int, vp, vp, vp, ctypes.POINTER(PlaneConfig), vp,
+                                                      vp, vp, vp, vp]
+
+
+EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device"]
+
+
+def pose_optimize(ex: OrbExtractor, problem, points, planes, cfg: PlaneConfig | None = None):
+    """Optimizer::PoseOptimization drop-in on host arrays (one frame).
+
+    Returns (result record, point outlier flags, plane outlier flags)."""
+    _bind_pose(ex.lib)
+    cfg = cfg or PlaneConfig.tum()
+    problem = np.ascontiguousarray(problem, POSE_PROBLEM_DTYPE).reshape(())
+    points = np.ascontiguousarray(points, POINT_OBS_DTYPE)
+    planes = np.ascontiguousarray(planes, PLANE_OBS_DTYPE)
+    res = np.zeros((), POSE_RESULT_DTYPE)
+    po = np.zeros(max(len(points), 1), np.uint8)
+    plo = np.zeros(max(len(planes), 1), np.uint8)
+    ex._check(ex.lib.spslam_pose_optimize(ex.ctx, problem.ctypes.data, points.ctypes.data if len(points) else None,
+                                          planes.ctypes.data if len(planes) else None, ctypes.byref(cfg),
+                                          res.ctypes.data, po.ctypes.data, plo.ctypes.data))
+    return res, po[:len(points)].astype(bool), plo[:len(planes)].astype(bool)
+
+
+def pose_optimize_batch_device(ex: OrbExtractor, n, problems_ptr, points_ptr, planes_ptr, results_ptr,
+                               pout_ptr, plout_ptr, init_from_ptr=0, cfg: PlaneConfig | None = None, stream=0):
+    _bind_pose(ex.lib)
+    cfg = cfg or PlaneConfig.tum()
+    ex._check(ex.lib.spslam_pose_optimize_batch_device(ex.ctx, n, problems_ptr, points_ptr, planes_ptr,
+                                                       ctypes.byref(cfg), init_from_ptr or None, results_ptr,
+                                                       pout_ptr, plout_ptr, stream or None))

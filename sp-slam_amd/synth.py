@@ -160,3 +160,98 @@ def sequence(seq_id: int, n_frames: int, w: int = 640, h: int = 480, n_boxes: in
         T = sc.pose(i)
         g, d, _ = sc.render(T, w, h, noise_seed=seq_id * 100003 + i)
         yield T, g, d
+
+
+# ---------------------------------------------------------------------------
+# PoseOptimization problems.  In the reference, the inputs of
+# Optimizer::PoseOptimization come from ORBmatcher::SearchByProjection and
+# Map::AssociatePlanesByBoundary (both outside this hot path).
+# Here they are synthesized from the scene ground truth: each ORB keypoint of
+# the frame gets a map point (its back-projection with the true depth, 5 mm
+# noise, a fraction replaced by gross outliers), each visible face gets a
+# plane edge, and some faces a parallel / perpendicular edge to another face.
+
+def face_plane(face: Face) -> np.ndarray:
+    """World plane (a, b, c, d) of a face with the reference's d >= 0 sign."""
+    n = np.zeros(3)
+    n[face.axis] = 1.0
+    p = np.array([*n, -face.offset])
+    return -p if p[3] < 0 else p
+
+
+def transform_plane(Tcw: np.ndarray, p: np.ndarray) -> np.ndarray:
+    R, t = Tcw[:3, :3], Tcw[:3, 3]
+    n = R @ p[:3]
+    out = np.array([*n, p[3] - t @ n])
+    return -out if out[3] < 0 else out
+
+
+def _rot(axis_angle):
+    th = np.linalg.norm(axis_angle)
+    if th < 1e-12:
+        return np.eye(3)
+    k = axis_angle / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def pose_problem(scene: Scene, frame: int, kps, depth_u16, fid, inv_level_sigma2, rng, K=TUM3,
+                 match_frac=0.8, outlier_frac=0.08, rot_noise_deg=1.0, trans_noise=0.03,
+                 with_planes=True, min_face_px=4000):
+    """Returns (problem record, point obs, plane obs, Tcw_gt) with the dtypes of spslam_gpu."""
+    import spslam_gpu as G
+    Twc = scene.pose(frame)
+    Tcw = np.linalg.inv(Twc)
+    fx, fy, cx, cy, bf = K["fx"], K["fy"], K["cx"], K["cy"], K["bf"]
+    h, w = depth_u16.shape
+    if w != 640:
+        s = w / 640.0
+        fx, fy, cx, cy = fx * s, fy * s, cx * s, cy * s
+    pts = []
+    for i, kp in enumerate(kps):
+        if rng.random() > match_frac:
+            continue
+        u, v = float(kp["x"]), float(kp["y"])
+        d = depth_u16[int(v), int(u)] / K["depth_factor"]
+        ur = u - bf / d if d > 0 else -1.0
+        # true depth along the ray from the noise-free scene
+        ray = np.array([(u - cx) / fx, (v - cy) / fy, 1.0])
+        zt = d if d > 0 else 2.0
+        Xc = ray * (zt + rng.normal(0, 0.005))
+        Xw = Twc[:3, :3] @ Xc + Twc[:3, 3]
+        if rng.random() < outlier_frac:
+            Xw = Xw + rng.normal(0, 0.3, 3)
+        pts.append((u, v, ur, inv_level_sigma2[int(kp["octave"])], Xw.astype(np.float32), i))
+    points = np.array(pts, G.POINT_OBS_DTYPE) if pts else np.zeros(0, G.POINT_OBS_DTYPE)
+    planes = []
+    if with_planes:
+        counts = np.bincount(fid[fid >= 0].ravel(), minlength=len(scene.faces))
+        vis = [k for k in range(len(scene.faces)) if counts[k] >= min_face_px]
+        edges = {0: [], 1: [], 2: []}
+        for j, k in enumerate(vis):
+            wp = face_plane(scene.faces[k])
+            cp = transform_plane(Tcw, wp)
+            Rn = _rot(rng.normal(0, np.deg2rad(0.3), 3))
+            meas = np.array([*(Rn @ cp[:3]), cp[3] + rng.normal(0, 0.005)])
+            edges[0].append((meas, wp, j, k))
+            par = [m for m in range(len(scene.faces)) if m != k and scene.faces[m].axis == scene.faces[k].axis]
+            ver = [m for m in range(len(scene.faces)) if scene.faces[m].axis != scene.faces[k].axis]
+            if par and rng.random() < 0.5:
+                m = par[rng.integers(len(par))]
+                edges[1].append((meas, face_plane(scene.faces[m]), j, m))
+            if ver and rng.random() < 0.5:
+                m = ver[rng.integers(len(ver))]
+                edges[2].append((meas, face_plane(scene.faces[m]), j, m))
+        for kind in (0, 1, 2):
+            for meas, wp, j, mid in edges[kind]:
+                planes.append((meas.astype(np.float32), wp.astype(np.float32), kind, j, mid, 0))
+    planes = np.array(planes, G.PLANE_OBS_DTYPE) if planes else np.zeros(0, G.PLANE_OBS_DTYPE)
+    # motion-model initial guess: perturbed ground truth
+    T0 = Tcw.copy()
+    T0[:3, :3] = _rot(rng.normal(0, np.deg2rad(rot_noise_deg), 3)) @ Tcw[:3, :3]
+    T0[:3, 3] = Tcw[:3, 3] + rng.normal(0, trans_noise, 3)
+    prob = np.zeros((), G.POSE_PROBLEM_DTYPE)
+    prob["Tcw"] = T0.astype(np.float32).ravel()
+    prob["fx"], prob["fy"], prob["cx"], prob["cy"], prob["bf"] = fx, fy, cx, cy, bf
+    prob["n_points"], prob["n_planes"] = len(points), len(planes)
+    return prob, points, planes, Tcw

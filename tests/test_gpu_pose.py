@@ -1,0 +1,130 @@
+"""GPU parity: PoseOptimization (src/Optimizer.cc:519-1152) vs the CPU oracle.
+
+Bar (BASELINE.json north_star): pose within 1e-4 relative; inlier count and
+every outlier flag identical.  Problems are synthesized from the scene ground
+truth (synth.pose_problem) on top of real ORB keypoints of the frame.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+POSE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import spslam_gpu
+    ex = spslam_gpu.OrbExtractor(max_batch=1)
+    yield ex
+    ex.close()
+
+
+@pytest.fixture(scope="module")
+def problems(synth_frames):
+    import oracle_ctypes
+    import synth
+    sc = synth.Scene(0)
+    orb = oracle_ctypes.OrbOracle()
+    invs2 = orb.scale_tables()[3]
+    out = []
+    for k, fi in enumerate((0, 7, 19, 40)):
+        g, d, fid = sc.render(sc.pose(fi), noise_seed=fi)
+        kps, _ = orb.extract(g)
+        for variant in range(3):
+            rng = np.random.default_rng(100 * k + variant)
+            kw = [dict(), dict(match_frac=0.5, outlier_frac=0.2, rot_noise_deg=3.0, trans_noise=0.08),
+                  dict(with_planes=False, outlier_frac=0.0)][variant]
+            out.append(synth.pose_problem(sc, fi, kps, d, fid, invs2, rng, **kw))
+    return out
+
+
+def pose_close(Ta, Tb, tol=POSE_TOL):
+    Ta, Tb = Ta.reshape(4, 4).astype(np.float64), Tb.reshape(4, 4).astype(np.float64)
+    dr = np.abs(Ta[:3, :3] - Tb[:3, :3]).max()
+    dt = np.linalg.norm(Ta[:3, 3] - Tb[:3, 3]) / max(np.linalg.norm(Tb[:3, 3]), 1.0)
+    return dr <= tol and dt <= tol, (dr, dt)
+
+
+def test_pose_matches_oracle(gpu, problems):
+    import oracle_ctypes
+    import spslam_gpu
+    for k, (prob, pts, pls, Tgt) in enumerate(problems):
+        rg, pog, plog = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
+        ro, poo, ploo = oracle_ctypes.pose_optimize(prob, pts, pls)
+        ok, err = pose_close(rg["Tcw"], ro["Tcw"])
+        assert ok, f"problem {k}: pose differs {err}"
+        assert int(rg["n_inliers"]) == int(ro["n_inliers"]), f"problem {k}"
+        assert np.array_equal(pog, poo), f"problem {k}: point outliers differ at {np.nonzero(pog != poo)[0][:10]}"
+        assert np.array_equal(plog, ploo), f"problem {k}: plane outliers differ"
+        # and the optimizer actually converged to the ground truth
+        ok_gt, err_gt = pose_close(rg["Tcw"], Tgt.astype(np.float32), tol=2e-2)
+        assert ok_gt, f"problem {k}: far from ground truth {err_gt}"
+
+
+def test_fewer_than_three_points_returns_zero(gpu, problems):
+    import spslam_gpu
+    prob, pts, pls, _ = problems[0]
+    p = prob.copy()
+    p["n_points"] = 2
+    r, po, plo = spslam_gpu.pose_optimize(gpu, p, pts[:2], pls)
+    assert r["n_inliers"] == 0
+    assert np.array_equal(r["Tcw"], prob["Tcw"])  # SetPose is not called (:653-654)
+
+
+def test_few_edges_single_round(gpu, problems):
+    """< 10 edges: the reference breaks after the first round (:1142-1143)."""
+    import oracle_ctypes
+    import spslam_gpu
+    prob, pts, pls, _ = problems[2]
+    p = prob.copy()
+    p["n_points"], p["n_planes"] = 6, 0
+    rg, pog, _ = spslam_gpu.pose_optimize(gpu, p, pts[:6], pls[:0])
+    ro, poo, _ = oracle_ctypes.pose_optimize(p, pts[:6], pls[:0])
+    ok, err = pose_close(rg["Tcw"], ro["Tcw"])
+    assert ok, err
+    assert np.array_equal(pog, poo) and rg["n_inliers"] == ro["n_inliers"]
+
+
+def test_batch_device_chained(gpu, problems):
+    """Batched device entry: all problems in one launch, then a second launch
+    chained from the first results (motion model -> local map, :982, :1061)."""
+    torch = pytest.importorskip("torch")
+    import oracle_ctypes
+    import spslam_gpu as G
+    n = len(problems)
+    probs = np.zeros(n, G.POSE_PROBLEM_DTYPE)
+    pts_all, pls_all = [], []
+    po_off = pl_off = 0
+    for i, (prob, pts, pls, _) in enumerate(problems):
+        probs[i] = prob
+        probs[i]["point_offset"], probs[i]["plane_offset"] = po_off, pl_off
+        po_off += len(pts)
+        pl_off += len(pls)
+        pts_all.append(pts)
+        pls_all.append(pls)
+    pts_all = np.concatenate(pts_all)
+    pls_all = np.concatenate(pls_all)
+    dev = lambda a: torch.from_numpy(a.view(np.uint8).copy()).cuda()
+    d_probs, d_pts, d_pls = dev(probs), dev(pts_all), dev(pls_all)
+    d_res1 = torch.zeros(n * G.POSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    d_res2 = torch.zeros_like(d_res1)
+    d_po = torch.zeros(len(pts_all), dtype=torch.uint8, device="cuda")
+    d_plo = torch.zeros(max(len(pls_all), 1), dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    G.pose_optimize_batch_device(gpu, n, d_probs.data_ptr(), d_pts.data_ptr(), d_pls.data_ptr(), d_res1.data_ptr(),
+                                 d_po.data_ptr(), d_plo.data_ptr(), stream=s)
+    G.pose_optimize_batch_device(gpu, n, d_probs.data_ptr(), d_pts.data_ptr(), d_pls.data_ptr(), d_res2.data_ptr(),
+                                 d_po.data_ptr(), d_plo.data_ptr(), init_from_ptr=d_res1.data_ptr(), stream=s)
+    torch.cuda.synchronize()
+    res1 = d_res1.cpu().numpy().view(G.POSE_RESULT_DTYPE)
+    res2 = d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE)
+    for i, (prob, pts, pls, _) in enumerate(problems):
+        r1, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
+        ok, err = pose_close(res1[i]["Tcw"], r1["Tcw"])
+        assert ok, (i, err)
+        p2 = prob.copy()
+        p2["Tcw"] = res1[i]["Tcw"]
+        r2, _, _ = oracle_ctypes.pose_optimize(p2, pts, pls)
+        ok, err = pose_close(res2[i]["Tcw"], r2["Tcw"])
+        assert ok, (i, err)
