@@ -185,6 +185,61 @@ int spslam_pose_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_pose_
                                       spslam_pose_result* d_results, uint8_t* d_point_outlier,
                                       uint8_t* d_plane_outlier, void* hip_stream);
 
+/* ------------------------------------------------------------------------
+ * Plane extraction: Frame::ComputePlanesFromOrganizedPointCloud
+ * (include/Frame.h:120, src/Frame.cc:854-936) with the PCL 1.8
+ * IntegralImageNormalEstimation + OrganizedMultiPlaneSegmentation it calls.
+ *
+ * Input: the float depth image in meters the RGB-D Frame constructor
+ * receives (imDepth, CV_32F, src/Tracking.cc:230-231).  Output per frame:
+ * the planes Frame appends to mvPlaneCoefficients (d >= 0, PlaneNotSeen
+ * de-duplicated, in the reference's order) with, per plane, the
+ * organized-cloud indices of its inliers (mvPlanePoints) and of its contour
+ * (mvBoundaryPoints).  The organized cloud itself (points (x, y, z), row-major
+ * ceil(h/dis) x ceil(w/dis)) is available through spslam_planes_cloud. */
+typedef struct spslam_plane_params {
+    int cloud_dis;            /* Cloud.Dis (3) */
+    int min_size;             /* Plane.MinSize (500) */
+    float angle_threshold;    /* Plane.AngleThreshold, degrees (3.0) */
+    float distance_threshold; /* Plane.DistanceThreshold (0.05) */
+    float fx, fy, cx, cy;     /* static Frame::fx, fy, cx, cy */
+    int width, height;        /* depth image size */
+} spslam_plane_params;
+
+typedef struct spslam_plane {
+    float coef[4];            /* mvPlaneCoefficients entry */
+    int32_t n_inliers;        /* mvPlanePoints size */
+    int32_t inlier_offset;    /* into the frame's inlier index buffer */
+    int32_t n_contour;        /* mvBoundaryPoints size */
+    int32_t contour_offset;   /* into the frame's contour index buffer */
+} spslam_plane;
+
+/* Configure (and allocate scratch for max_batch frames) the plane stage. */
+int spslam_planes_configure(spslam_ctx* ctx, const spslam_plane_params* params);
+
+/* Capacities the caller must provide per frame: planes, inlier indices,
+ * contour indices. */
+int spslam_planes_capacity(const spslam_ctx* ctx, int* planes_cap, int* inlier_cap, int* contour_cap);
+
+/* Drop-in for one frame, host buffers.  *n_planes receives the plane count;
+ * inliers / contours receive the index lists referenced by planes[]. */
+int spslam_planes_extract(spslam_ctx* ctx, const float* depth, int w, int h, int stride_floats,
+                          spslam_plane* planes, int planes_cap, int* n_planes, int32_t* inliers, int32_t* contours);
+
+/* Batched, device resident: frame f's depth at d_depth + f*frame_stride
+ * floats (rows stride_floats apart).  Per frame f: counts[f] planes at
+ * d_planes + f*planes_cap, indices at d_inliers + f*inlier_cap and
+ * d_contours + f*contour_cap (capacities from spslam_planes_capacity). */
+int spslam_planes_extract_batch_device(spslam_ctx* ctx, const float* d_depth, int n_frames, size_t frame_stride,
+                                       int stride_floats, spslam_plane* d_planes, int* d_counts,
+                                       int32_t* d_inliers, int32_t* d_contours, void* hip_stream);
+
+/* Stage access for parity tests, frame `frame` of the last batch:
+ * what 0 = organized cloud (3*N floats, x,y,z per point), 1 = normals
+ * (3*N floats, NaN = invalid), 2 = distance map (N floats), 3 = labels after
+ * connected components (N uint32, PCL label ids). */
+int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_points);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

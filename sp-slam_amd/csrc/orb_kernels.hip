@@ -695,7 +695,10 @@ hipError_t orb_upload_tables(const int umax[16]) {
 // frame_stride must already point at the caller's gray frames.
 const char* kernel_kind_name(int kind) {
     static const char* names[kNumKernelKinds] = {"resize_level_kernel", "fast_cells_kernel", "blur_kernel",
-                                                 "octree_kernel", "desc_kernel", "pose_kernel"};
+                                                 "octree_kernel", "desc_kernel", "pose_kernel",
+                                                 "plane_cloud_kernel", "plane_distance_kernel",
+                                                 "plane_integral_kernel", "plane_normal_kernel",
+                                                 "plane_segment_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

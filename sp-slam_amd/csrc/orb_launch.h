@@ -17,7 +17,11 @@ struct OrbBuffers {
 };
 
 // Kernel kinds for the per-kind HIP-event timers (spslam_kernel_times).
-enum KernelKind { kKindResize = 0, kKindFast, kKindBlur, kKindOctree, kKindDesc, kKindPose, kNumKernelKinds };
+enum KernelKind {
+    kKindResize = 0, kKindFast, kKindBlur, kKindOctree, kKindDesc, kKindPose,
+    kKindPlaneCloud, kKindPlaneDist, kKindPlaneIntegral, kKindPlaneNormal, kKindPlaneSegment,
+    kNumKernelKinds
+};
 const char* kernel_kind_name(int kind);
 
 // Optional timer: begin/end are called on the launch stream around each kernel

@@ -16,6 +16,7 @@
 
 #include "../../include/spslam_gpu.h"
 #include "orb_launch.h"
+#include "plane_launch.h"
 #include "pose_launch.h"
 
 using namespace spslam;
@@ -87,6 +88,17 @@ struct spslam_ctx {
     // drop-in PoseOptimization staging
     uint8_t* d_pose_scratch = nullptr;
     size_t pose_scratch_bytes = 0;
+    // plane stage
+    bool planes_ready = false;
+    PlaneGeom pg{};
+    PlaneBuffers pb{};
+    void* d_plane_scratch = nullptr;
+    float* d_depth_in = nullptr;
+    spslam_plane* d_planes1 = nullptr;
+    int* d_plane_cnt1 = nullptr;
+    int32_t* d_inl1 = nullptr;
+    int32_t* d_con1 = nullptr;
+    int plane_last_frames = 0;
 };
 
 namespace {
@@ -199,8 +211,10 @@ const char* build_geom(spslam_ctx* c) {
 }
 
 void free_all(spslam_ctx* c) {
-    void* ptrs[] = {c->d_pyr, c->d_blur, c->b.cand, c->b.cand_cnt, c->b.keys, c->b.keynode,
-                    c->b.lvl_kp, c->b.lvl_cnt, c->d_in, c->d_kps, c->d_desc, c->d_cnt, c->d_pose_scratch};
+    void* ptrs[] = {c->d_pyr,    c->d_blur,   c->b.cand,          c->b.cand_cnt,     c->b.keys,
+                    c->b.keynode, c->b.lvl_kp, c->b.lvl_cnt,       c->d_in,           c->d_kps,
+                    c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
+                    c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -426,6 +440,142 @@ int spslam_pose_optimize(spslam_ctx* c, const spslam_pose_problem* problem, cons
     if (nl) HIP_CHECK(c, hipMemcpyAsync(plane_outlier, d_plo, nl, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return SPSLAM_OK;
+}
+
+int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
+    if (!c || !p) return SPSLAM_ERR_ARG;
+    if (p->cloud_dis < 1 || p->width < 1 || p->height < 1 || p->fx == 0.f || p->fy == 0.f)
+        return fail(c, SPSLAM_ERR_ARG, "bad plane parameters%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    PlaneGeom& g = c->pg;
+    g.w = p->width;
+    g.h = p->height;
+    g.ds = p->cloud_dis;
+    g.W = (int)std::ceil(p->width / (float)p->cloud_dis);
+    g.H = (int)std::ceil(p->height / (float)p->cloud_dis);
+    g.N = g.W * g.H;
+    if (g.H > 512) return fail(c, SPSLAM_ERR_ARG, "organized cloud taller than 512 rows%s", "");
+    if (g.N > 160000) return fail(c, SPSLAM_ERR_ARG, "organized cloud larger than the LDS state map%s", "");
+    g.fx = p->fx; g.fy = p->fy; g.cx = p->cx; g.cy = p->cy;
+    g.min_size = p->min_size;
+    g.ang_cos = std::cos((float)(0.017453 * p->angle_threshold));  // cosf(static_cast<float>(0.017453*AngTh))
+    g.dist_th = p->distance_threshold;
+    g.inlier_cap = g.N;
+    g.contour_cap = 4 * g.N;
+    const long long N = g.N, F = c->p.max_batch, IWH = (long long)(g.W + 1) * (g.H + 1);
+    PlaneBuffers& b = c->pb;
+    b.cloud_fs = 3 * N; b.dist_fs = N; b.integral_fs = 6 * IWH; b.normal_fs = 3 * N; b.pd_fs = N;
+    b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N;
+    const size_t bytes = F * (sizeof(float) * (b.cloud_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
+                              sizeof(double) * b.integral_fs + sizeof(uint32_t) * b.labels_fs +
+                              sizeof(int) * (b.work_fs + 2 * b.grown_fs)) + 4096;
+    if (c->d_plane_scratch) (void)hipFree(c->d_plane_scratch);
+    c->d_plane_scratch = nullptr;
+    HIP_CHECK(c, hipMalloc(&c->d_plane_scratch, bytes));
+    uint8_t* q = (uint8_t*)c->d_plane_scratch;
+    auto carve = [&](size_t n) { uint8_t* r = q; q += (n + 255) / 256 * 256; return r; };
+    b.integral = (double*)carve(F * b.integral_fs * sizeof(double));
+    b.cloud = (float*)carve(F * b.cloud_fs * 4);
+    b.dist = (float*)carve(F * b.dist_fs * 4);
+    b.normal = (float*)carve(F * b.normal_fs * 4);
+    b.pd = (float*)carve(F * b.pd_fs * 4);
+    b.labels = (uint32_t*)carve(F * b.labels_fs * 4);
+    b.work = (int*)carve(F * b.work_fs * 4);
+    b.grown = (int*)carve(F * b.grown_fs * 4);
+    b.grown_model = (int*)carve(F * b.grown_fs * 4);
+    void* olds[] = {c->d_depth_in, c->d_planes1, c->d_plane_cnt1, c->d_inl1, c->d_con1};
+    for (void* o : olds)
+        if (o) (void)hipFree(o);
+    HIP_CHECK(c, hipMalloc(&c->d_depth_in, (size_t)g.w * g.h * sizeof(float)));
+    HIP_CHECK(c, hipMalloc(&c->d_planes1, kMaxPlanesPerFrame * sizeof(spslam_plane)));
+    HIP_CHECK(c, hipMalloc(&c->d_plane_cnt1, 16));
+    HIP_CHECK(c, hipMalloc(&c->d_inl1, (size_t)g.inlier_cap * 4));
+    HIP_CHECK(c, hipMalloc(&c->d_con1, (size_t)g.contour_cap * 4));
+    c->planes_ready = true;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_capacity(const spslam_ctx* c, int* planes_cap, int* inlier_cap, int* contour_cap) {
+    if (!c || !c->planes_ready) return SPSLAM_ERR_NOT_READY;
+    if (planes_cap) *planes_cap = kMaxPlanesPerFrame;
+    if (inlier_cap) *inlier_cap = c->pg.inlier_cap;
+    if (contour_cap) *contour_cap = c->pg.contour_cap;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_extract_batch_device(spslam_ctx* c, const float* d_depth, int n_frames, size_t frame_stride,
+                                       int stride_floats, spslam_plane* d_planes, int* d_counts,
+                                       int32_t* d_inliers, int32_t* d_contours, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
+    if (!d_depth || !d_planes || !d_counts || !d_inliers || !d_contours || n_frames < 1 ||
+        n_frames > c->p.max_batch || stride_floats < c->pg.w)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_extract_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIP_CHECK(c, plane_launch(c->pg, c->pb, n_frames, d_depth, (long long)frame_stride, stride_floats, d_planes,
+                              d_counts, kMaxPlanesPerFrame, d_inliers, d_contours, s, c->timer));
+    c->plane_last_frames = n_frames;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_extract(spslam_ctx* c, const float* depth, int w, int h, int stride_floats, spslam_plane* planes,
+                          int planes_cap, int* n_planes, int32_t* inliers, int32_t* contours) {
+    if (!c || !n_planes) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
+    if (!depth || w != c->pg.w || h != c->pg.h || stride_floats < w)
+        return fail(c, SPSLAM_ERR_ARG, "depth size does not match the plane configuration%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipMemcpy2DAsync(c->d_depth_in, (size_t)w * 4, depth, (size_t)stride_floats * 4, (size_t)w * 4, h,
+                                  hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_planes_extract_batch_device(c, c->d_depth_in, 1, (size_t)w * h, w, c->d_planes1, c->d_plane_cnt1,
+                                                c->d_inl1, c->d_con1, c->stream);
+    if (rc) return rc;
+    int n = 0;
+    spslam_plane tmp[kMaxPlanesPerFrame];
+    HIP_CHECK(c, hipMemcpyAsync(&n, c->d_plane_cnt1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(tmp, c->d_planes1, sizeof tmp, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    *n_planes = n;
+    if (n > planes_cap) return fail(c, SPSLAM_ERR_CAPACITY, "plane buffer too small%s", "");
+    int ni = 0, nc = 0;
+    for (int k = 0; k < n; k++) {
+        planes[k] = tmp[k];
+        ni = std::max(ni, tmp[k].inlier_offset + tmp[k].n_inliers);
+        nc = std::max(nc, tmp[k].contour_offset + tmp[k].n_contour);
+    }
+    if (inliers && ni) HIP_CHECK(c, hipMemcpy(inliers, c->d_inl1, (size_t)ni * 4, hipMemcpyDeviceToHost));
+    if (contours && nc) HIP_CHECK(c, hipMemcpy(contours, c->d_con1, (size_t)nc * 4, hipMemcpyDeviceToHost));
+    return SPSLAM_OK;
+}
+
+int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_points) {
+    if (!c || !out) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready || frame < 0 || frame >= c->plane_last_frames)
+        return fail(c, SPSLAM_ERR_NOT_READY, "no plane data for that frame%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipDeviceSynchronize());
+    const PlaneBuffers& b = c->pb;
+    const long long N = c->pg.N;
+    if (n_points) *n_points = (int)N;
+    if (what == 0 || what == 1) {  // SoA on device -> AoS x,y,z
+        const float* src = what == 0 ? b.cloud + frame * b.cloud_fs : b.normal + frame * b.normal_fs;
+        std::vector<float> soa(3 * N);
+        HIP_CHECK(c, hipMemcpy(soa.data(), src, 3 * N * 4, hipMemcpyDeviceToHost));
+        float* o = (float*)out;
+        for (long long i = 0; i < N; i++) { o[3 * i] = soa[i]; o[3 * i + 1] = soa[N + i]; o[3 * i + 2] = soa[2 * N + i]; }
+        return SPSLAM_OK;
+    }
+    if (what == 2) {
+        HIP_CHECK(c, hipMemcpy(out, b.dist + frame * b.dist_fs, N * 4, hipMemcpyDeviceToHost));
+        return SPSLAM_OK;
+    }
+    if (what == 3) {
+        HIP_CHECK(c, hipMemcpy(out, b.labels + frame * b.labels_fs, N * 4, hipMemcpyDeviceToHost));
+        return SPSLAM_OK;
+    }
+    return fail(c, SPSLAM_ERR_ARG, "unknown debug stage%s", "");
 }
 
 int spslam_set_timing(spslam_ctx* c, int enable) {

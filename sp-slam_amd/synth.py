@@ -59,7 +59,7 @@ class Scene:
     def __init__(self, seq_id: int = 0, n_boxes: int = 3, texel: float = 0.006):
         self.rng = np.random.Generator(np.random.PCG64(0x5EED0000 + seq_id))
         self.texel = texel
-        X0, X1, Y0, Y1, Z0, Z1 = -2.5, 2.5, -1.3, 1.3, -1.0, 3.0
+        X0, X1, Y0, Y1, Z0, Z1 = -2.5, 2.5, -1.3, 1.3, -2.0, 3.5
         faces = [
             Face(0, X0, np.array([Y0, Z0]), np.array([Y1, Z1]), 0),
             Face(0, X1, np.array([Y0, Z0]), np.array([Y1, Z1]), 1),
@@ -72,7 +72,7 @@ class Scene:
         for b in range(n_boxes):
             sx, sy, sz = self.rng.uniform(0.4, 0.9), self.rng.uniform(0.4, 1.0), self.rng.uniform(0.4, 0.9)
             cx = self.rng.uniform(-1.8, 1.8)
-            cz = self.rng.uniform(1.4, 2.5)
+            cz = self.rng.uniform(0.6, 2.6)
             lo = np.array([cx - sx / 2, Y1 - sy, cz - sz / 2])
             hi = np.array([cx + sx / 2, Y1, cz + sz / 2])
             for axis in range(3):
@@ -87,7 +87,7 @@ class Scene:
         """Camera-to-world 4x4 at frame i (30 Hz)."""
         t = i / 30.0
         yaw = 0.26 * np.sin(0.5 * t)
-        pitch = 0.08 * np.sin(0.7 * t + 0.3)
+        pitch = -0.32 + 0.08 * np.sin(0.7 * t + 0.3)  # looking down at the floor and boxes
         roll = 0.05 * np.sin(0.9 * t + 1.0)
         cy, sy = np.cos(yaw), np.sin(yaw)
         cp, sp = np.cos(pitch), np.sin(pitch)
@@ -97,12 +97,17 @@ class Scene:
         Rz = np.array([[cr, -sr, 0], [sr, cr, 0], [0, 0, 1]])
         T = np.eye(4)
         T[:3, :3] = Ry @ Rx @ Rz
-        T[:3, 3] = [0.4 * np.sin(0.3 * t), 0.1 * np.sin(0.5 * t), -0.2 + 0.3 * np.sin(0.2 * t)]
+        T[:3, 3] = [0.4 * np.sin(0.3 * t), -0.3 + 0.1 * np.sin(0.5 * t), -1.2 + 0.3 * np.sin(0.2 * t)]
         return T
 
     def render(self, Twc: np.ndarray, w: int = 640, h: int = 480, K=TUM3, noise_seed: int = 0,
-               depth_noise: float = 0.001, dropout: float = 0.02, gray_noise: float = 1.0):
-        """Returns (gray u8 HxW, depth u16 HxW, plane id int16 HxW)."""
+               depth_noise: float = 0.0012, dropout: float = 0.0005, gray_noise: float = 1.0,
+               holes: int = 12):
+        """Returns (gray u8 HxW, depth u16 HxW, plane id int16 HxW).
+
+        Depth noise is Kinect-like, N(0, depth_noise * z^2); invalid depth (0)
+        appears as salt (`dropout`), at occlusion edges, and in `holes` random
+        blobs of 2-8 px radius."""
         fx, fy, cx, cy = K["fx"], K["fy"], K["cx"], K["cy"]
         if w != 640:  # scaled intrinsics for other resolutions
             s = w / 640.0
@@ -146,9 +151,19 @@ class Scene:
             gray[m] = val
         nrng = np.random.Generator(np.random.PCG64(0x5EED0000 + 7919 * (noise_seed + 1)))
         gray = np.clip(np.rint(gray + nrng.normal(0, gray_noise, gray.shape)), 0, 255).astype(np.uint8)
-        zn = z + nrng.normal(0, depth_noise, z.shape)
+        zn = z + nrng.normal(0, 1.0, z.shape) * depth_noise * z * z
         depth = np.clip(np.rint(zn * K["depth_factor"]), 0, 65535).astype(np.uint16)
         depth[nrng.random(z.shape) < dropout] = 0
+        # occlusion-edge shadows (1 px band where depth jumps by > 10 cm)
+        jump = np.zeros(z.shape, bool)
+        jump[:, 1:] |= np.abs(np.diff(z, axis=1)) > 0.1
+        jump[1:, :] |= np.abs(np.diff(z, axis=0)) > 0.1
+        depth[jump & (nrng.random(z.shape) < 0.7)] = 0
+        yy, xx = np.mgrid[0:h, 0:w]
+        for _ in range(holes):
+            r = nrng.uniform(2, 8)
+            hy, hx = nrng.uniform(0, h), nrng.uniform(0, w)
+            depth[(yy - hy) ** 2 + (xx - hx) ** 2 < r * r] = 0
         depth[fid < 0] = 0
         return gray, depth, fid.astype(np.int16)
 
