@@ -3,16 +3,18 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c5]
 
-A "step" is one pass of the hot path over one batch of B synthetic frames that
-are already resident in HBM (one process per GPU; for N > 1 launch through
-torch.distributed.run, each rank runs its own independent sequences -- the
-path shards with no data-path collective; one all-reduce aggregates timing).
+A "step" is one pass of the hot path -- ORB extraction, plane extraction and
+two chained PoseOptimizations (motion model, then local map) -- over one
+batch of B synthetic RGB-D frames already resident in HBM (sp-slam_amd/
+pipeline.py).  One process per GPU; for N > 1 launch through
+torch.distributed.run: every rank runs its own independent sequence (the path
+shards with no data-path collective; one all-reduce takes the max time).
 
-Rank 0 prints ONE JSON line.  `value` = frames processed by all ranks / the
-max over ranks of the timed region.  `roofline` is computed for the kernel
-with the largest share of the timed region, from HIP events recorded on its
-launch stream during the timed steps; `cpu_baseline` is the CPU oracle
-(single core) on a bounded sample of the same workload.
+Rank 0 prints ONE JSON line.  `value` = frames processed by all ranks / max
+over ranks of the timed region.  `roofline` is computed for the kernel with
+the largest share of the timed region, from HIP events recorded on its launch
+stream during the timed steps; `cpu_baseline` is the CPU oracle (one core) on
+a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -27,12 +29,13 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "sp-slam_amd"))
 
 CONFIGS = {
-    # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, nFeatures=1000, 8 levels
+    # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, ORB + planes + PoseOptimization
     "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=3,
-               workload="C2: synthetic 640x480 RGB-D stream, ORB nFeatures=1000, 8-level pyramid"),
+               workload="C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud "
+                        "plane extraction + 2x PoseOptimization (point+plane+parallel+perpendicular edges), no LBA"),
     # configs[4]: 1280x960, nFeatures=4000, dense-plane scene
-    "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=6,
-               workload="C5: synthetic 1280x960 RGB-D, nFeatures=4000, dense-plane scene"),
+    "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8,
+               workload="C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + 2x PoseOptimization"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -50,33 +53,55 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return out
 
 
-def algorithmic_bytes(cfg, n_kp):
-    """Compulsory bytes per frame for each kernel kind ("Roofline")."""
+def algorithmic_bytes(cfg, n_kp, n_pts, n_pls):
+    """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
+    W, H = -(-cfg["width"] // 3), -(-cfg["height"] // 3)
+    N = W * H
+    IWH = (W + 1) * (H + 1)
     return {
-        "resize_level_kernel": sum(px[:-1]) + sum(px[1:]),     # read level l-1, write level l
-        "fast_cells_kernel": sum(px),                           # every level pixel read once
-        "blur_kernel": 2 * sum(px),                             # read + write every level
-        "octree_kernel": 0,                                     # latency/serial bound: no streamed bytes
-        "desc_kernel": n_kp * (28 + 32),                        # keypoint + descriptor out
+        "resize_level_kernel": sum(px[:-1]) + sum(px[1:]),   # read level l-1, write level l
+        "fast_cells_kernel": sum(px),                         # every level pixel read once
+        "blur_kernel": 2 * sum(px),                           # read + write every level
+        "octree_kernel": 0,                                   # serial list algorithm, no streamed bytes
+        "desc_kernel": n_kp * (28 + 32),                      # keypoint + descriptor out
+        "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call
+        "plane_cloud_kernel": 4 * N + 12 * N,                 # depth samples in, xyz out
+        "plane_distance_kernel": 4 * N + 4 * N,               # z in, distance map out
+        "plane_integral_kernel": 12 * N + 48 * IWH,           # xyz in, 6 fp64 integral images out
+        "plane_normal_kernel": 16 * N + 48 * IWH + 16 * N,    # xyz+dist, integral, normal+plane_d out
+        "plane_segment_kernel": 28 * N + 4 * N,               # xyz+normal+plane_d in, labels out
     }
 
 
-def cpu_baseline(frames, cfg, budget_s=12.0):
-    """Oracle (CPU restatement) single-core frames/s on a bounded sample."""
+def cpu_baseline(hp, budget_s=12.0):
+    """CPU restatement (oracle) of the same per-frame work, one core, bounded sample."""
     sys.path.insert(0, str(ROOT / "oracle"))
+    import numpy as np
     import oracle_ctypes
-    orb = oracle_ctypes.OrbOracle(nfeatures=cfg["nfeatures"])
+    import oracle_planes
+    orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
+    po = oracle_planes.PlaneOracle()
     n = 0
+    U = len(hp.frames)
+    depth_f = [f[2].astype(np.float32) * np.float32(np.float32(1.0) / np.float32(5000.0)) for f in hp.frames]
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        orb.extract(frames[n % len(frames)], cap=20000)
+        i = n % U
+        orb.extract(hp.frames[i][1], cap=20000)
+        po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
+        pa, pts, pls, _ = hp.probA[i]
+        r1, _, _ = oracle_ctypes.pose_optimize(pa, pts, pls)
+        pb, pts2, pls2, _ = hp.probB[i]
+        pb = pb.copy()
+        pb["Tcw"] = r1["Tcw"]
+        oracle_ctypes.pose_optimize(pb, pts2, pls2)
         n += 1
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
-                sample=f"{n} frames of the same synthetic {cfg['width']}x{cfg['height']} stream, "
-                       f"{dt:.1f}s, one core, oracle/liboracle.so (-O3 x86-64-v3)")
+                sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
+                       f"2x PoseOptimization), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -94,7 +119,6 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -102,55 +126,48 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    import spslam_gpu
-    import synth
-
-    W, H, B = cfg["width"], cfg["height"], args.batch
-    sc = synth.Scene(seq_id=rank, n_boxes=cfg["n_boxes"])
-    uniq = [sc.render(sc.pose(i * 3), W, H, noise_seed=rank * 1000 + i)[0] for i in range(args.unique_frames)]
-    host = np.stack([uniq[i % len(uniq)] for i in range(B)])
-    gray = torch.from_numpy(host).to("cuda")
-    ex = spslam_gpu.OrbExtractor(nfeatures=cfg["nfeatures"], width=W, height=H, max_batch=B, device=local)
-    cap = ex.max_kp
-    kps = torch.empty((B, cap, 7), dtype=torch.float32, device="cuda")
-    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
-    cnt = torch.empty(B, dtype=torch.int32, device="cuda")
-    stream = torch.cuda.current_stream().cuda_stream
-
-    def step():
-        ex.extract_batch_device(gray.data_ptr(), B, W * H, W, kps.data_ptr(), desc.data_ptr(), cnt.data_ptr(),
-                                cap, stream)
-
+    import pipeline
+    hp = pipeline.HotPath(args.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"], seq_id=rank,
+                          unique_frames=args.unique_frames, device=local)
     for _ in range(args.warmup):
-        step()
+        hp.step()
     torch.cuda.synchronize()
-    ex.set_timing(True)
+    hp.ex.set_timing(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        hp.step()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    times = ex.kernel_times()
-    n_kp = float(cnt.float().mean().item())
+    times = {k: v for k, v in hp.ex.kernel_times().items() if v[1] > 0}
+    res = hp.results()
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    frames = world * B * args.steps
+    frames = world * args.batch * args.steps
     value = frames / elapsed
     total_kernel_ms = sum(v[0] for v in times.values())
     dom, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
-    alg = algorithmic_bytes(cfg, n_kp)
-    launches_per_step = {"resize_level_kernel": 1}  # the resize kind is one timed group of 7 launches
+    n_pts = (hp.dA["n_points"] + hp.dB["n_points"]) / args.batch
+    n_pls = (hp.dA["n_planes"] + hp.dB["n_planes"]) / args.batch
+    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls)
+    launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
-    bytes_per_launch = alg[dom] * B
+    bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step
     achieved = bytes_per_launch / avg_launch_s / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{args.config}_b{args.batch}.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get(dom)
+        except Exception:
+            traffic = None
     result = {
         "metric": "RGB-D frames/sec (track+planes+poseOpt) at 640x480; ATE vs CPU ref",
         "value": value,
@@ -162,22 +179,25 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (in-repo textured-room RGB-D renderer, sp-slam_amd/synth.py)",
-        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": B, "stages": ["orb"],
-                   "parallelism": f"shard{world}", "mean_keypoints": n_kp},
-        "kernels_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in times.items()},
+        "dtype": "u8+f32+f64",
+        "data": "synthetic (in-repo textured-room RGB-D renderer sp-slam_amd/synth.py; pose correspondences "
+                "synthesized from scene ground truth)",
+        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": args.batch,
+                   "parallelism": f"shard{world}", "mean_keypoints": hp.mean_keypoints,
+                   "mean_planes": float(res["plane_counts"].mean()),
+                   "pose_edges_per_frame": n_pts + n_pls},
+        "kernels_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in sorted(times.items())},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_launch_s * 1e3,
                      "share_of_kernel_time": dom_ms / max(total_kernel_ms, 1e-9)},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(uniq, cfg)
+        result["cpu_baseline"] = cpu_baseline(hp)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    ex.close()
+    hp.close()
     if dist:
         dist.destroy_process_group()
 

@@ -1,0 +1,139 @@
+"""Batched per-frame tracking hot path on one GPU (the throughput step of bench.py).
+
+One step = for each of B frames resident in HBM (gray u8 + depth f32):
+  ORBextractor::operator()                      (spslam_orb_extract_batch_device)
+  Frame::ComputePlanesFromOrganizedPointCloud   (spslam_planes_extract_batch_device)
+  Optimizer::PoseOptimization, motion model     (spslam_pose_optimize_batch_device)
+  Optimizer::PoseOptimization, local map,       (same, chained on the device from
+      starting from the motion-model pose        the first call's results)
+mirroring Tracking::Track's per-frame sequence (src/Tracking.cc:233, 982, 1061).
+
+The correspondences PoseOptimization consumes come from ORBmatcher /
+Map::AssociatePlanesByBoundary in the reference (outside this path,
+SURVEY.md 8(f)); here they are synthesized once per frame from the scene
+ground truth and the frame's own keypoints (synth.pose_problem) and kept in
+HBM.  All launches go to one HIP stream; nothing returns to the host inside
+a step.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import spslam_gpu as G
+import spslam_planes
+import synth
+
+
+class HotPath:
+    def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
+                 device=0, K=synth.TUM3, oracle_kps=None):
+        import torch
+        self.torch = torch
+        self.B, self.W, self.H = B, width, height
+        s = width / 640.0
+        self.fx, self.fy, self.cx, self.cy = K["fx"] * s, K["fy"] * s, K["cx"] * s, K["cy"] * s
+        self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
+        self.ex = G.OrbExtractor(nfeatures=nfeatures, width=width, height=height, max_batch=B, device=device)
+        self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height)
+        # --- unique synthetic frames
+        U = min(unique_frames, B)
+        self.frames = []
+        for i in range(U):
+            fi = 3 * i
+            g, d, fid = self.scene.render(self.scene.pose(fi), width, height, noise_seed=seq_id * 1000 + fi)
+            self.frames.append((fi, g, d, fid))
+        gray = np.stack([self.frames[i % U][1] for i in range(B)])
+        depth = np.stack([self.frames[i % U][2] for i in range(B)]).astype(np.float32) * \
+            np.float32(np.float32(1.0) / np.float32(K["depth_factor"]))
+        dev = "cuda"
+        self.d_gray = torch.from_numpy(gray).to(dev)
+        self.d_depth = torch.from_numpy(depth).to(dev)
+        cap = self.ex.max_kp
+        self.kp_cap = cap
+        self.d_kps = torch.zeros((B, cap, 7), dtype=torch.float32, device=dev)
+        self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+        self.d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        pe = self.pe
+        self.d_planes = torch.zeros(B * pe.planes_cap * 8, dtype=torch.int32, device=dev)
+        self.d_pcnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_inl = torch.zeros(B * pe.inlier_cap, dtype=torch.int32, device=dev)
+        self.d_con = torch.zeros(B * pe.contour_cap, dtype=torch.int32, device=dev)
+        # --- pose problems: run one ORB pass to get each unique frame's keypoints
+        self.stream = torch.cuda.current_stream().cuda_stream
+        self.orb()
+        torch.cuda.synchronize()
+        kps = self.d_kps.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(B, cap)
+        cnts = self.d_cnt.cpu().numpy()
+        invs2 = self.ex.tables()["inv_sigma2"]
+        probA, probB = [], []
+        for i in range(U):
+            fi, g, d, fid = self.frames[i]
+            k = kps[i, :cnts[i]]
+            rng = np.random.default_rng(seq_id * 7919 + i)
+            probA.append(synth.pose_problem(self.scene, fi, k, d, fid, invs2, rng, K=K, match_frac=0.6))
+            probB.append(synth.pose_problem(self.scene, fi, k, d, fid, invs2, rng, K=K, match_frac=0.85,
+                                            rot_noise_deg=0.3, trans_noise=0.01))
+        self.probA = [probA[i % U] for i in range(B)]
+        self.probB = [probB[i % U] for i in range(B)]
+        self.dA = self._upload(self.probA)
+        self.dB = self._upload(self.probB)
+        self.d_res1 = torch.zeros(B * G.POSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        self.d_res2 = torch.zeros_like(self.d_res1)
+        self.mean_keypoints = float(cnts.mean())
+
+    def _upload(self, probs):
+        torch = self.torch
+        n = len(probs)
+        P = np.zeros(n, G.POSE_PROBLEM_DTYPE)
+        pts, pls = [], []
+        po = pl = 0
+        for i, (prob, p, q, _) in enumerate(probs):
+            P[i] = prob
+            P[i]["point_offset"], P[i]["plane_offset"] = po, pl
+            po += len(p)
+            pl += len(q)
+            pts.append(p)
+            pls.append(q)
+        pts = np.concatenate(pts)
+        pls = np.concatenate(pls) if pl else np.zeros(1, G.PLANE_OBS_DTYPE)
+        dev = lambda a: torch.from_numpy(a.view(np.uint8).copy()).cuda()
+        return dict(P=dev(P), pts=dev(pts), pls=dev(pls),
+                    pout=torch.zeros(max(po, 1), dtype=torch.uint8, device="cuda"),
+                    plout=torch.zeros(max(pl, 1), dtype=torch.uint8, device="cuda"), n_points=po, n_planes=pl)
+
+    # --- stages
+    def orb(self):
+        self.ex.extract_batch_device(self.d_gray.data_ptr(), self.B, self.W * self.H, self.W, self.d_kps.data_ptr(),
+                                     self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, self.stream)
+
+    def planes(self):
+        self.pe.extract_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
+                                     self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_inl.data_ptr(),
+                                     self.d_con.data_ptr(), self.stream)
+
+    def pose(self):
+        A, Bp = self.dA, self.dB
+        G.pose_optimize_batch_device(self.ex, self.B, A["P"].data_ptr(), A["pts"].data_ptr(), A["pls"].data_ptr(),
+                                     self.d_res1.data_ptr(), A["pout"].data_ptr(), A["plout"].data_ptr(),
+                                     stream=self.stream)
+        G.pose_optimize_batch_device(self.ex, self.B, Bp["P"].data_ptr(), Bp["pts"].data_ptr(), Bp["pls"].data_ptr(),
+                                     self.d_res2.data_ptr(), Bp["pout"].data_ptr(), Bp["plout"].data_ptr(),
+                                     init_from_ptr=self.d_res1.data_ptr(), stream=self.stream)
+
+    def step(self):
+        self.orb()
+        self.planes()
+        self.pose()
+
+    def results(self):
+        torch = self.torch
+        torch.cuda.synchronize()
+        return dict(
+            kps=self.d_kps.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(self.B, self.kp_cap),
+            kp_counts=self.d_cnt.cpu().numpy(),
+            plane_counts=self.d_pcnt.cpu().numpy(),
+            pose1=self.d_res1.cpu().numpy().view(G.POSE_RESULT_DTYPE),
+            pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE))
+
+    def close(self):
+        self.ex.close()

@@ -1,0 +1,41 @@
+"""Regenerate the golden fixtures in tests/golden/ from the CPU oracle.
+
+The reference ships no fixtures for this path, so these
+pin the restatement against regressions; they are data (inputs are
+reproducible from sp-slam_amd/synth.py; outputs are oracle results).
+    python tools/make_golden.py
+"""
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT / "sp-slam_amd"), str(ROOT / "oracle")]
+import oracle_ctypes as O  # noqa: E402
+import oracle_planes as OP  # noqa: E402
+import synth  # noqa: E402
+
+out = ROOT / "tests" / "golden"
+out.mkdir(parents=True, exist_ok=True)
+sc = synth.Scene(0)
+g, d, fid = sc.render(sc.pose(5), noise_seed=5)
+orb = O.OrbOracle()
+kps, desc = orb.extract(g)
+np.savez_compressed(out / "orb_seq0_f5.npz", kps=kps, desc=desc, gray_sum=np.int64(g.astype(np.int64).sum()))
+# planes
+df = OP.depth_to_float(d)
+po = OP.PlaneOracle()
+K = synth.TUM3
+res = po.extract(df, K["fx"], K["fy"], K["cx"], K["cy"])
+np.savez_compressed(out / "planes_seq0_f5.npz", coef=np.array(res["coef"]), n_inliers=np.array([len(i) for i in res["inliers"]]),
+                    inliers=np.concatenate(res["inliers"]) if res["inliers"] else np.zeros(0, np.int32),
+                    depth_sum=np.int64(d.astype(np.int64).sum()))
+# pose
+invs2 = orb.scale_tables()[3]
+rng = np.random.default_rng(11)
+prob, pts, pls, Tgt = synth.pose_problem(sc, 5, kps, d, fid, invs2, rng)
+r, pout, plout = O.pose_optimize(prob, pts, pls)
+np.savez_compressed(out / "pose_seq0_f5.npz", prob=prob, pts=pts, pls=pls, Tcw=r["Tcw"], n_inliers=r["n_inliers"],
+                    pout=pout, plout=plout, Tgt=Tgt)
+print("wrote", sorted(p.name for p in out.iterdir()))
