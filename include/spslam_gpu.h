@@ -237,7 +237,8 @@ int spslam_planes_extract_batch_device(spslam_ctx* ctx, const float* d_depth, in
 /* Stage access for parity tests, frame `frame` of the last batch:
  * what 0 = organized cloud (3*N floats, x,y,z per point), 1 = normals
  * (3*N floats, NaN = invalid), 2 = distance map (N floats), 3 = labels after
- * connected components (N uint32, PCL label ids). */
+ * connected components (N uint32, PCL label ids), 4 = segmentation phase
+ * timestamps (16 int64 ticks of the 100 MHz GPU real-time clock). */
 int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_points);
 
 /* Measurement: when enabled, every kernel kind launched by this context is

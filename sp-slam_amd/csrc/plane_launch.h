@@ -31,13 +31,19 @@ struct PlaneBuffers {
     float* pd;           // [F][N]  plane_d = p . n
     uint32_t* labels;    // [F][N]
     int* work;           // [F][N + 4*N] misc (ranks, sizes, member lists)
-    int* grown;          // [F][N] grown points (refinement order)
-    int* grown_model;    // [F][N]
-    long long cloud_fs, dist_fs, integral_fs, normal_fs, pd_fs, labels_fs, work_fs, grown_fs;
+    int* grown;          // [F][N] refinement grow events (target | model << 24), reference order
+    uint8_t* maps;       // [F][2N] component tag / model map + contour masks (when not in LDS)
+    long long* ts;       // [F][16] segmentation phase stamps (s_memrealtime, 100 MHz), diagnostics
+    long long cloud_fs, dist_fs, integral_fs, normal_fs, pd_fs, labels_fs, work_fs, grown_fs, maps_fs;
 };
 
 hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const float* depth, long long depth_fs,
                         int depth_stride, spslam_plane* planes, int* plane_counts, int planes_cap,
                         int32_t* inliers, int32_t* contours, hipStream_t s, KernelTimer* timer);
+
+// Segmentation stage alone (plane_segment.hip); needs cloud/normal/pd filled.
+hipError_t plane_segment_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, spslam_plane* planes,
+                                int* plane_counts, int planes_cap, int32_t* inliers, int32_t* contours,
+                                hipStream_t s);
 
 }  // namespace spslam

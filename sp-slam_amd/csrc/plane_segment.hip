@@ -1,0 +1,1077 @@
+// gfx950 segmentation stage of Frame::ComputePlanesFromOrganizedPointCloud
+// (src/Frame.cc:876-934): pcl::OrganizedMultiPlaneSegmentation::segmentAndRefine
+// (PCL 1.8, PlaneCoefficientComparator + PlaneRefinementComparator), the
+// boundary extraction, Frame's sign flip and PlaneNotSeen.
+//
+// One 1024-thread workgroup per frame.  Phases (each a block-wide barrier
+// apart); the per-frame maps live in LDS when they fit (C2: 214x160), in
+// global scratch otherwise (C5):
+//   A  row runs: one wave per cloud row; ballots give the comparator's
+//      horizontal/vertical edge bits (LDS bitmaps) and each pixel's run head
+//   B  union-find over run heads, one vertical link per run overlap
+//      (min-index linking with atomicMin => root = first raster pixel)
+//   C  path flattening;  D  labels = rank of the root (PCL's label order),
+//      component sizes by wave-aggregated atomics;  E  components > MinSize
+//   G  per component, one wave: raster-order member list and PCL's float
+//      mean/covariance accumulation (terms staged through LDS, nine lanes
+//      each own one accumulator, so the sums are the reference's sequence)
+//   H  eigen33 / viewpoint / curvature filter (models)
+//   K  refinement: the reference's two raster passes are row recurrences;
+//      one wave evaluates each row with a scan over composed per-pixel
+//      transfer functions (constant label, or pass-through-if-accepted
+//      bitmask over models), so a row costs O(log 64) instead of O(W)
+//      dependent steps; grow events are emitted in the reference's order
+//   L  Frame.cc:912-934 sign flip + PlaneNotSeen;  M  inlier lists
+//   N  findLabeledRegionBoundary: Moore tracing from per-pixel 8-neighbour
+//      masks, one wave per plane (count pass, offsets, write pass)
+// Reference semantics are restated in oracle/plane_oracle.cpp:268-470.
+#include <hip/hip_runtime.h>
+
+#include "plane_launch.h"
+
+namespace spslam {
+namespace planes {
+
+constexpr int kSegThreads = 1024;
+constexpr int kSegWaves = kSegThreads / 64;
+constexpr int kMaxBig = 255;          // components > MinSize per frame (u8 tags)
+constexpr int kMaxRowWords = 8;       // W <= 512
+constexpr int kLdsBytes = 160 * 1024;
+
+struct SegShared {
+    int wsum[kSegWaves];
+    int misc[8];
+    int nbig;
+    int big_label[kMaxBig];
+    int big_root[kMaxBig];
+    int big_size[kMaxBig];
+    int big_off[kMaxBig];
+    float big_par[kMaxBig][4];
+    float big_cen[kMaxBig][4];
+    float big_curv[kMaxBig];
+    uint8_t big_state[kMaxBig + 1];
+    int nmodel;
+    int model_big[kMaxPlanesPerFrame];
+    float model_coef[kMaxPlanesPerFrame][4];
+    int model_grown[kMaxPlanesPerFrame];
+    int nkept;
+    int kept[kMaxPlanesPerFrame];
+    int con_len[kMaxPlanesPerFrame];
+    alignas(16) float stage[kSegWaves][9][64];   // covariance terms of one 64-pixel chunk, per wave
+};
+
+// The whole frame lives in one workgroup (one CU): workgroup scope is enough
+// for every global-memory hand-off, and avoids the L2 writeback/invalidate an
+// agent-scope fence costs on gfx950.
+__device__ __forceinline__ int ld_wg(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int uf_find(const int* P, int x) {
+    int p = ld_wg(&P[x]);
+    while (p != x) { x = p; p = ld_wg(&P[x]); }
+    return x;
+}
+// Lock-free union with min-index linking: P[x] <= x always, a root is the
+// smallest index of its tree.
+__device__ void uf_union(int* P, int a, int b) {
+    a = uf_find(P, a);
+    b = uf_find(P, b);
+    while (a != b) {
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = __hip_atomic_fetch_min(&P[a], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (old == a) return;
+        a = uf_find(P, old);
+        b = uf_find(P, b);
+    }
+}
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const int lane = threadIdx.x & 63;
+    return (1ull << lane) - 1ull;
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ void block_sync() {
+    __syncthreads();   // workgroup-scope release/acquire (global and LDS)
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const int lo = __shfl_up((int)(uint32_t)v, d), hi = __shfl_up((int)(uint32_t)(v >> 32), d);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+// Exclusive wave prefix sum of v; *total = wave sum.
+__device__ __forceinline__ int wave_excl(int v, int* total) {
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    *total = __shfl(x, 63);
+    return x - v;
+}
+
+// pcl::computeRoots / eigen33 (float), see oracle/plane_oracle.cpp.
+__device__ void roots2(float b, float c, float* r) {
+    r[0] = 0.f;
+    float d = (float)(b * b - 4.0 * c);
+    if (d < 0.0) d = 0.0;
+    const float sd = sqrtf(d);
+    r[2] = 0.5f * (b + sd);
+    r[1] = 0.5f * (b - sd);
+}
+__device__ void eigen33_min(const float (&m0)[3][3], float* eval, float* evec) {
+    float scale = 0.f;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) scale = fmaxf(scale, fabsf(m0[i][j]));
+    if (scale <= 1.17549435e-38f) scale = 1.f;
+    float m[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m[i][j] = m0[i][j] / scale;
+    float r[3];
+    const float c0 = m[0][0] * m[1][1] * m[2][2] + 2.f * m[0][1] * m[0][2] * m[1][2] - m[0][0] * m[1][2] * m[1][2] -
+                     m[1][1] * m[0][2] * m[0][2] - m[2][2] * m[0][1] * m[0][1];
+    const float c1 = m[0][0] * m[1][1] - m[0][1] * m[0][1] + m[0][0] * m[2][2] - m[0][2] * m[0][2] +
+                     m[1][1] * m[2][2] - m[1][2] * m[1][2];
+    const float c2 = m[0][0] + m[1][1] + m[2][2];
+    if (fabsf(c0) < 1.1920929e-07f) {
+        roots2(c2, c1, r);
+    } else {
+        const float s_inv3 = (float)(1.0 / 3.0), s_sqrt3 = sqrtf(3.0f);
+        const float c2_over_3 = c2 * s_inv3;
+        float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+        if (a_over_3 > 0.f) a_over_3 = 0.f;
+        const float half_b = 0.5f * (c0 + c2_over_3 * (2.f * c2_over_3 * c2_over_3 - c1));
+        float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+        if (q > 0.f) q = 0.f;
+        const float rho = sqrtf(-a_over_3);
+        const float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
+        const float ct = cosf(theta), st = sinf(theta);
+        r[0] = c2_over_3 + 2.f * rho * ct;
+        r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
+        r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
+        float t;
+        if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+        if (r[1] >= r[2]) {
+            t = r[1]; r[1] = r[2]; r[2] = t;
+            if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+        }
+        if (r[0] <= 0) roots2(c2, c1, r);
+    }
+    *eval = r[0] * scale;
+    for (int i = 0; i < 3; i++) m[i][i] -= r[0];
+    float v[3][3];
+    const int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    float len[3];
+    for (int k = 0; k < 3; k++) {
+        const float* a = m[pr[k][0]];
+        const float* b = m[pr[k][1]];
+        v[k][0] = a[1] * b[2] - a[2] * b[1];
+        v[k][1] = a[2] * b[0] - a[0] * b[2];
+        v[k][2] = a[0] * b[1] - a[1] * b[0];
+        len[k] = v[k][0] * v[k][0] + v[k][1] * v[k][1] + v[k][2] * v[k][2];
+    }
+    int k = 2;
+    if (len[0] >= len[1] && len[0] >= len[2]) k = 0;
+    else if (len[1] >= len[0] && len[1] >= len[2]) k = 1;
+    const float sl = sqrtf(len[k]);
+    for (int j = 0; j < 3; j++) evec[j] = v[k][j] / sl;
+}
+
+// Eigen SSE predux order for a Vector4f dot.
+__device__ __forceinline__ float dot4(const float* a, const float* b) {
+    const float p0 = a[0] * b[0], p1 = a[1] * b[1], p2 = a[2] * b[2], p3 = a[3] * b[3];
+    return (p0 + p2) + (p1 + p3);
+}
+
+// ---------------------------------------------------------------------------
+// Refinement.  A pixel's state is 0 or model+1.  Per row, each pixel maps the
+// state arriving along the row chain (from the previous pixel of the pass
+// order) to its final state: a constant (already labelled, or grown from the
+// previous row, which the reference does first), or "keep the incoming model
+// if this point is within 0.02 m of it".  Such maps compose associatively.
+struct Fn {
+    uint64_t m;  // pass-through models (bit v-1 for state v), when c < 0
+    int c;       // constant output, or -1
+};
+__device__ __forceinline__ int fn_apply(const Fn& f, int L) {
+    if (f.c >= 0) return f.c;
+    return (L > 0 && ((f.m >> (L - 1)) & 1ull)) ? L : 0;
+}
+__device__ __forceinline__ Fn fn_then(const Fn& first, const Fn& second) {
+    if (second.c >= 0) return second;
+    if (first.c >= 0) return Fn{0ull, fn_apply(second, first.c)};
+    return Fn{first.m & second.m, -1};
+}
+
+// PlaneRefinementComparator::compare (absolute 0.02 m): float expression,
+// compared after promotion as the reference does.
+__device__ __forceinline__ bool ptp_ok(const float* m, float x, float y, float z) {
+    const float e = m[0] * x + m[1] * y + m[2] * z + m[3];
+    return fabsf(e) < 0.02f;
+}
+
+template <int K>
+__device__ __forceinline__ int sel(const int (&a)[K], int k) {
+    int v = 0;
+#pragma unroll
+    for (int j = 0; j < K; j++)
+        if (j == k) v = a[j];
+    return v;
+}
+
+// One refinement pass by one wave (reference: OrganizedMultiPlaneSegmentation
+// ::refine, the forward loop r = 0..H-2 / c = 0..W-2 growing right then
+// down, and the backward loop r = H-1..1 / c = W-1..0 growing left (row-wrap
+// at c = 0) then up).  Lane l owns pass positions p = l*K + k; column
+// c = p (forward) or W-1-p (backward).  Grow events are appended to ev[] in
+// the reference's order: events of a source row are emitted once both of
+// their target rows are final.  Returns the number of events appended.
+template <int K>
+__device__ __forceinline__ int refine_pass(SegShared& S, uint8_t* state, const uint64_t* cbits, const float* X, const float* Y,
+                           const float* Z, int W, int H, bool bw, int* ev, int ev_base) {
+    const int RW = (W + 63) >> 6;
+    const int lane = threadIdx.x & 63;
+    const int nmodel = S.nmodel;
+    const int lastLane = (W - 1) / K, lastK = (W - 1) - lastLane * K;
+    // per-position flags are K-bit masks (bit k = position lane*K+k)
+    int prevS[K];
+    int pvm = 0, pcm = 0;  // previous row: valid points, grown along the chain
+#pragma unroll
+    for (int k = 0; k < K; k++) prevS[k] = 0;
+    int carry = 0, ng = 0;
+    // prefetch of the next row (its state is not touched by the current step)
+    float qx[K], qy[K], qz[K];
+    int qs[K];
+#define SPSLAM_REFINE_FETCH(STEP)                                                  \
+    {                                                                              \
+        const int r_ = bw ? H - 1 - (STEP) : (STEP);                               \
+        _Pragma("unroll") for (int k = 0; k < K; k++) {                            \
+            const int p = lane * K + k;                                            \
+            qs[k] = 0; qx[k] = qy[k] = qz[k] = 0.f;                                \
+            if (p < W && (STEP) < H) {                                             \
+                const int i = r_ * W + (bw ? W - 1 - p : p);                       \
+                qs[k] = state[i];                                                  \
+                qx[k] = X[i]; qy[k] = Y[i]; qz[k] = Z[i];                          \
+            }                                                                      \
+        }                                                                          \
+    }
+    SPSLAM_REFINE_FETCH(0)
+    for (int step = 0; step < H; step++) {
+        const int r = bw ? H - 1 - step : step;
+        int s0[K], fin[K];
+        float px[K], py[K], pz[K];
+        int vm = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            s0[k] = qs[k]; px[k] = qx[k]; py[k] = qy[k]; pz[k] = qz[k];
+            if (lane * K + k < W && isfinite(px[k])) vm |= 1 << k;
+        }
+        SPSLAM_REFINE_FETCH(step + 1)
+        // neighbours across lanes: previous row at position p+1, current row at p-1 / position 0
+        const int nbS = __shfl_down(prevS[0], 1);
+        const int nb = __shfl_down(pvm | (pcm << 8), 1);
+        const int nbV = nb & 1, nbC = (nb >> 8) & 1;
+        const int pvV = (__shfl_up(vm, 1) >> (K - 1)) & 1;
+        const int cur0V = __shfl(vm, 0) & 1;
+        const int wrapV = (__shfl(pvm, lastLane) >> lastK) & 1;
+        // rows without a growable point (unlabelled, valid, within 0.02 m of some
+        // model) keep their states: skip the composition
+        int any = 0;
+        for (int w = 0; w < RW; w++) any |= cbits[r * RW + w] != 0ull;
+        int gm = 0, cm = 0;  // grown from the previous row / along the row chain
+        if (!any) {
+#pragma unroll
+            for (int k = 0; k < K; k++) fin[k] = s0[k];
+        } else {
+        int cand = 0;
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int p = lane * K + k;
+            if (p < W) {
+                const int c = bw ? W - 1 - p : p;
+                cand |= (int)((cbits[r * RW + (c >> 6)] >> (c & 63)) & 1ull) << k;
+            }
+        }
+        Fn g[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const int p = lane * K + k;
+            const int c = bw ? W - 1 - p : p;
+            const int vk = (vm >> k) & 1, pvk = (pvm >> k) & 1;
+            const int pv1 = k < K - 1 ? (pvm >> (k + 1)) & 1 : nbV;   // previous row, position p+1
+            const int vm1 = k > 0 ? (vm >> (k - 1)) & 1 : pvV;        // current row, position p-1
+            // vertical source: the previous row's pixel in this column
+            bool act;
+            if (!bw) act = step >= 1 && c <= W - 2 && pvk && pv1 && vk;
+            else act = step >= 1 && pvk && (c >= 1 ? pv1 : cur0V) && vk;
+            if (p >= W) {
+                g[k] = Fn{0ull, 0};
+            } else if (s0[k]) {
+                g[k] = Fn{0ull, s0[k]};
+            } else if (!((cand >> k) & 1)) {
+                g[k] = Fn{0ull, 0};
+            } else if (act && prevS[k] && ptp_ok(S.model_coef[prevS[k] - 1], px[k], py[k], pz[k])) {
+                g[k] = Fn{0ull, prevS[k]};
+                gm |= 1 << k;
+            } else {
+                bool link;
+                if (!bw) link = p >= 1 && r <= H - 2 && vm1 && vk;
+                else if (p >= 1) link = r >= 1 && vm1 && vk;
+                else link = step >= 1 && wrapV && vk;
+                if (link) {
+                    uint64_t m = 0;
+                    for (int v = 0; v < nmodel; v++)
+                        if (ptp_ok(S.model_coef[v], px[k], py[k], pz[k])) m |= 1ull << v;
+                    g[k] = Fn{m, -1};
+                } else {
+                    g[k] = Fn{0ull, 0};
+                }
+            }
+        }
+        // compose along the row: lane-local, then a wave inclusive scan
+        Fn F = g[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) F = fn_then(F, g[k]);
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const Fn o{shfl_up64(F.m, off), __shfl_up(F.c, off)};
+            if (lane >= off) F = fn_then(o, F);
+        }
+        Fn ex{shfl_up64(F.m, 1), __shfl_up(F.c, 1)};
+        if (lane == 0) ex = Fn{~0ull, -1};
+        int L = fn_apply(ex, bw ? carry : 0);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            fin[k] = fn_apply(g[k], L);
+            if (g[k].c < 0 && fin[k] != 0) cm |= 1 << k;
+            L = fin[k];
+            const int p = lane * K + k;
+            if (p < W && s0[k] == 0 && fin[k] != 0) state[r * W + (bw ? W - 1 - p : p)] = (uint8_t)fin[k];
+        }
+        }
+        carry = __shfl(sel<K>(fin, lastK), lastLane);
+        // emit the events of the previous row's sources, in pass order
+        if (step >= 1) {
+            const int chain0 = __shfl(cm, 0) & 1, fin0 = __shfl(fin[0], 0);
+            int n = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int p = lane * K + k;
+                int fa = 0;
+                if (p <= W - 2) fa = k < K - 1 ? (pcm >> (k + 1)) & 1 : nbC;
+                else if (p == W - 1 && bw) fa = chain0;
+                n += fa + ((gm >> k) & 1);
+            }
+            int tot;
+            int o = ev_base + ng + wave_excl(n, &tot);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int p = lane * K + k;
+                const int c = bw ? W - 1 - p : p;
+                // A: along the source row (forward: right, backward: left / row wrap)
+                int fa = 0, ta = 0, ma = 0;
+                if (p <= W - 2) {
+                    fa = k < K - 1 ? (pcm >> (k + 1)) & 1 : nbC;
+                    ma = k < K - 1 ? prevS[k + 1] : nbS;
+                    ta = bw ? (r + 1) * W + c - 1 : (r - 1) * W + c + 1;
+                } else if (p == W - 1 && bw) {
+                    fa = chain0; ma = fin0; ta = r * W + W - 1;
+                }
+                if (fa) ev[o++] = ta | ((ma - 1) << 24);
+                // B: into this row (forward: down, backward: up)
+                if ((gm >> k) & 1) ev[o++] = (r * W + c) | ((fin[k] - 1) << 24);
+            }
+            ng += tot;
+        }
+#pragma unroll
+        for (int k = 0; k < K; k++) prevS[k] = fin[k];
+        pvm = vm;
+        pcm = cm;
+    }
+    return ng;
+#undef SPSLAM_REFINE_FETCH
+}
+
+// Fast path (nmodel <= 6).  Before each pass every point gets a descriptor
+// byte, computed in parallel: bits 0-5 = models whose plane is within 0.02 m
+// of the point (only for valid, still unlabelled points), bit 6 = its
+// vertical source may grow it, bit 7 = its chain source may grow it (source
+// and source-neighbour validity, row limits of the reference loops).  The
+// pass itself then only composes per-pixel transfer functions, packed in 9
+// bits (bit 8 = constant; low byte = constant state, or the complement of the
+// pass-through set, so 0 is the identity) and scanned with DPP.  Which grow
+// event produced each new label is re-derived afterwards from the final
+// states, in parallel, in the reference's event order.
+__device__ __forceinline__ int f8_pass(int f, int L) {  // f: complemented pass-through set
+    return (L > 0 && !((f >> ((L - 1) & 7)) & 1)) ? L : 0;
+}
+__device__ __forceinline__ int f8_then(int first, int second) {
+    const int through = 0x100 | f8_pass(second, first & 0xFF);
+    const int both = first | second;
+    const int r = (first & 0x100) ? through : both;
+    return (second & 0x100) ? second : r;
+}
+__device__ __forceinline__ int f8_apply(int f, int L) {
+    return (f & 0x100) ? (f & 0xFF) : f8_pass(f, L);
+}
+// Inclusive wave scan of f8_then (lane order), DPP row shifts + row broadcasts.
+__device__ __forceinline__ int f8_scan(int x) {
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true), x);  // row_shr:1
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true), x);  // row_shr:2
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true), x);  // row_shr:4
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true), x);  // row_shr:8
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false), x); // row_bcast:15
+    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false), x); // row_bcast:31
+    return x;
+}
+
+// Descriptor byte of point i for one pass (see above).
+__device__ __forceinline__ int refine_desc(const uint8_t* state, const float* X, const float* Y, const float* Z,
+                                           const float (*coef)[4], int nmodel, int W, int H, int i, bool bw) {
+    if (state[i]) return 0;
+    const float x = X[i], y = Y[i], z = Z[i];
+    if (!isfinite(x)) return 0;
+    int acc = 0;
+    for (int v = 0; v < nmodel; v++)
+        if (ptp_ok(coef[v], x, y, z)) acc |= 1 << v;
+    if (!acc) return 0;
+    const int r = i / W, c = i - r * W;
+    bool act, link;
+    if (!bw) {  // sources (r-1, c) [needs (r-1, c+1)] and (r, c-1)
+        act = r >= 1 && c <= W - 2 && isfinite(X[i - W]) && isfinite(X[i - W + 1]);
+        link = c >= 1 && r <= H - 2 && isfinite(X[i - 1]);
+    } else {    // sources (r+1, c) [needs flat index before it] and flat i+1 (row wrap at c = W-1)
+        act = r <= H - 2 && isfinite(X[i + W]) && isfinite(X[i + W - 1]);
+        link = (c <= W - 2 ? r >= 1 : r <= H - 2) && isfinite(X[i + 1]);
+    }
+    return acc | (act ? 0x40 : 0) | (link ? 0x80 : 0);
+}
+
+template <int K>
+__device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc, const uint64_t* cbits, int W, int H,
+                                            bool bw) {
+    const int lane = threadIdx.x & 63;
+    const int RW = (W + 63) >> 6;
+    const int lastLane = (W - 1) / K, lastK = (W - 1) - lastLane * K;
+    int prevS[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) prevS[k] = 0;
+    int carry = 0;
+    int qs[K], qd[K];
+#define SPSLAM_FAST_FETCH(STEP)                                                    \
+    {                                                                              \
+        const int r_ = bw ? H - 1 - (STEP) : (STEP);                               \
+        _Pragma("unroll") for (int k = 0; k < K; k++) {                            \
+            const int p = lane * K + k;                                            \
+            qs[k] = 0; qd[k] = 0;                                                  \
+            if (p < W && (STEP) < H) {                                             \
+                const int i = r_ * W + (bw ? W - 1 - p : p);                       \
+                qs[k] = state[i];                                                  \
+                qd[k] = desc[i];                                                   \
+            }                                                                      \
+        }                                                                          \
+    }
+    SPSLAM_FAST_FETCH(0)
+    for (int step = 0; step < H; step++) {
+        const int r = bw ? H - 1 - step : step;
+        int s0[K], d[K], fin[K];
+#pragma unroll
+        for (int k = 0; k < K; k++) { s0[k] = qs[k]; d[k] = qd[k]; }
+        SPSLAM_FAST_FETCH(step + 1)
+        uint64_t any = 0;
+        for (int w = 0; w < RW; w++) any |= cbits[r * RW + w];
+        if (!any) {
+#pragma unroll
+            for (int k = 0; k < K; k++) fin[k] = s0[k];
+        } else {
+            int g[K];
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                const int acc = d[k] & 0x3F, U = prevS[k];
+                const bool grant = (d[k] & 0x40) && U && ((acc >> ((U - 1) & 7)) & 1);
+                int e = (d[k] & 0x80) ? (~acc & 0xFF) : 0x100;
+                e = grant ? (0x100 | U) : e;
+                e = acc ? e : 0x100;
+                g[k] = s0[k] ? (0x100 | s0[k]) : e;
+            }
+            int F = g[0];
+#pragma unroll
+            for (int k = 1; k < K; k++) F = f8_then(F, g[k]);
+            F = f8_scan(F);
+            int ex = __shfl_up(F, 1);
+            if (lane == 0) ex = 0;
+            int L = f8_apply(ex, bw ? carry : 0);
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                fin[k] = f8_apply(g[k], L);
+                L = fin[k];
+                const int p = lane * K + k;
+                if (p < W && s0[k] == 0 && fin[k] != 0) state[r * W + (bw ? W - 1 - p : p)] = (uint8_t)fin[k];
+            }
+        }
+        if (bw) carry = __shfl(sel<K>(fin, lastK), lastLane);
+#pragma unroll
+        for (int k = 0; k < K; k++) prevS[k] = fin[k];
+    }
+#undef SPSLAM_FAST_FETCH
+}
+
+// Grow events of one finished fast pass, appended at ev[] in the reference's
+// order (sources in pass order; per source: along the row, then across rows).
+// Returns the number of events (uniform).
+__device__ int refine_events(SegShared& S, const uint8_t* state, const uint8_t* desc, int W, int H, int N, bool bw,
+                             int* ev) {
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int M = (H - 1) * W;
+    // how target j grew in this pass: 0 not, 1 along its row (chain), 2 from the other row
+    auto how = [&](int j, int vsrc) -> int {
+        const int dj = desc[j];
+        if (!(dj & 0x3F) || !state[j]) return 0;
+        if (dj & 0x40) {
+            const int U = state[vsrc];
+            if (U && ((dj >> (U - 1)) & 1)) return 2;
+        }
+        return 1;
+    };
+    auto events = [&](int q, int* tA, int* tB) {
+        const int s = bw ? N - 1 - q : q;
+        *tA = bw ? s - 1 : s + 1;
+        *tB = bw ? s - W : s + W;
+        const int a = how(*tA, bw ? *tA + W : *tA - W) == 1;
+        const int b = how(*tB, s) == 2;
+        return a | (b << 1);
+    };
+    const int span = (M + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
+    const int q0 = wave * span, q1 = min(M, q0 + span);
+    int cnt = 0;
+    for (int base = q0; base < q1; base += 64) {
+        const int q = base + lane;
+        int tA, tB, e = 0;
+        if (q < q1) e = events(q, &tA, &tB);
+        cnt += __popcll(__ballot(e & 1)) + __popcll(__ballot(e & 2));
+    }
+    if (lane == 0) S.wsum[wave] = cnt;
+    __syncthreads();
+    int off = 0, total = 0;
+    for (int j = 0; j < kSegWaves; j++) {
+        if (j < wave) off += S.wsum[j];
+        total += S.wsum[j];
+    }
+    const uint64_t lt = lanemask_lt();
+    for (int base = q0; base < q1; base += 64) {
+        const int q = base + lane;
+        int tA = 0, tB = 0, e = 0;
+        if (q < q1) e = events(q, &tA, &tB);
+        const uint64_t ma = __ballot(e & 1), mb = __ballot(e & 2);
+        int pos = off + __popcll(ma & lt) + __popcll(mb & lt);
+        if (e & 1) ev[pos++] = tA | ((state[tA] - 1) << 24);
+        if (e & 2) ev[pos] = tB | ((state[tB] - 1) << 24);
+        off += __popcll(ma) + __popcll(mb);
+    }
+    __syncthreads();
+    return total;
+}
+
+// 8-neighbour offsets of findLabeledRegionBoundary, packed 2 bits each (+1).
+constexpr uint32_t kDX = (0u << 0) | (0u << 2) | (1u << 4) | (2u << 6) | (2u << 8) | (2u << 10) | (1u << 12) | (0u << 14);
+constexpr uint32_t kDY = (1u << 0) | (0u << 2) | (0u << 4) | (0u << 6) | (1u << 8) | (2u << 10) | (2u << 12) | (2u << 14);
+__device__ __forceinline__ int ddx(int d) { return (int)((kDX >> (2 * d)) & 3u) - 1; }
+__device__ __forceinline__ int ddy(int d) { return (int)((kDY >> (2 * d)) & 3u) - 1; }
+
+__device__ __forceinline__ int nb_bits(const uint8_t* state, int W, int H, int x, int y, int lab, bool same) {
+    int m = 0;
+    for (int d = 0; d < 8; d++) {
+        const int u = x + ddx(d), v = y + ddy(d);
+        if (u >= 0 && u < W && v >= 0 && v < H && ((state[v * W + u] == lab) == same)) m |= 1 << d;
+    }
+    return m;
+}
+
+// Moore tracing from `start` (reference: findLabeledRegionBoundary); writes
+// at most cap indices, returns the full length.
+__device__ int trace_contour(const uint8_t* state, const uint8_t* nmask, int W, int H, int N, int start, int lab,
+                             int32_t* out, int cap) {
+    int cx = start % W, cy = start / W;
+    const int ne = nb_bits(state, W, H, cx, cy, lab, false);
+    if (!ne) return 0;
+    int dir = __builtin_ctz(ne);
+    int n = 0, cur = start;
+    if (n < cap) out[n] = start;
+    n++;
+    do {
+        const int m = state[cur] == lab ? nmask[cur] : nb_bits(state, W, H, cx, cy, lab, true);
+        const int sh = (dir + 1) & 7;
+        const int rot = ((m >> sh) | (m << (8 - sh))) & 0xFF;
+        const int nIdx = rot ? (sh + __builtin_ctz(rot)) & 7 : dir;
+        dir = (nIdx + 4) & 7;
+        cx += ddx(nIdx);
+        cy += ddy(nIdx);
+        cur = cy * W + cx;
+        if (n < cap) out[n] = cur;
+        n++;
+    } while (cur != start && n < 8 * N);
+    return n;
+}
+
+template <bool kLdsMaps, int K>
+__global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
+    PlaneGeom g, PlaneBuffers b, spslam_plane* __restrict__ planes_out, int* __restrict__ plane_counts, int planes_cap,
+    int32_t* __restrict__ inliers_out, int32_t* __restrict__ contours_out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    __shared__ SegShared S;
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int W = g.W, H = g.H, N = g.N, RW = (W + 63) >> 6;
+    uint64_t* hbits = (uint64_t*)dyn;      // comparator edge to the left neighbour, [H][RW]
+    uint64_t* vbits = hbits + H * RW;      // comparator edge to the upper neighbour
+    uint8_t* state = kLdsMaps ? (uint8_t*)(vbits + H * RW) : b.maps + f * b.maps_fs;  // [N] tag / model+1
+    uint8_t* nmask = state + N;                                                        // [N] contour masks
+    const float* X = b.cloud + f * b.cloud_fs;
+    const float* Y = X + N;
+    const float* Z = X + 2 * N;
+    const float* Nx = b.normal + f * b.normal_fs;
+    const float* Ny = Nx + N;
+    const float* Nz = Nx + 2 * N;
+    const float* PD = b.pd + f * b.pd_fs;
+    int* P = (int*)(b.labels + f * b.labels_fs);   // parents, then labels (-1 = invalid point)
+    int* rankA = b.work + f * b.work_fs;           // [N] label of each root pixel
+    int* sizes = rankA + N;                        // [N] per label (big ones: -(index+1))
+    int* rootOf = sizes + N;                       // [N] root pixel of each label
+    int* members = rootOf + N;                     // [N] member lists of big components
+    int* ev = b.grown + f * b.grown_fs;            // [N] grow events: target | model << 24
+    spslam_plane* planes = planes_out + (size_t)f * planes_cap;
+    int32_t* inl = inliers_out + (size_t)f * g.inlier_cap;
+    int32_t* con = contours_out + (size_t)f * g.contour_cap;
+    long long* ts = b.ts + f * 16;
+#define STAMP(k) do { if (t == 0) ts[k] = (long long)__builtin_amdgcn_s_memrealtime(); } while (0)
+    STAMP(15);
+    if (t < kMaxPlanesPerFrame) S.model_grown[t] = 0;
+
+    // PlaneCoefficientComparator::compare (i1 = current, i2 = neighbour)
+    auto cmp = [&](int i1, int i2) {
+        const float z = X[i1] * 0.f + Y[i1] * 0.f + Z[i1] * 1.f;
+        float threshold = g.dist_th;
+        threshold *= z * z;
+        const float nd = Nx[i1] * Nx[i2] + Ny[i1] * Ny[i2] + Nz[i1] * Nz[i2];
+        return (fabsf(PD[i1] - PD[i2]) < threshold) && (nd > g.ang_cos);
+    };
+    auto bit = [&](const uint64_t* m, int r, int c) { return (int)((m[r * RW + (c >> 6)] >> (c & 63)) & 1ull); };
+
+    // ---- A: edge bits and run heads, one wave per row
+    for (int r = wave; r < H; r += kSegWaves) {
+        int carry = 0;
+        for (int k = 0; k < RW; k++) {
+            const int c = (k << 6) + lane;
+            const bool in = c < W;
+            const int i = r * W + c;
+            bool h = false, v = false, valid = false;
+            if (in) {
+                valid = isfinite(X[i]);
+                h = c >= 1 && cmp(i, i - 1);
+                v = r >= 1 && cmp(i, i - W);
+            }
+            const uint64_t hb = __ballot(h), vb = __ballot(v);
+            if (lane == 0) { hbits[r * RW + k] = hb; vbits[r * RW + k] = vb; }
+            const uint64_t sb = __ballot(in && !h);
+            const uint64_t upto = lane == 63 ? sb : (sb & ((2ull << lane) - 1ull));
+            const int head = upto ? r * W + (k << 6) + 63 - __clzll(upto) : carry;
+            if (in) P[i] = valid ? head : -1;
+            carry = __shfl(head, 63);
+        }
+    }
+    block_sync();
+    STAMP(0);
+    // ---- B: one union per vertical run overlap
+    for (int i = W + t; i < N; i += kSegThreads) {
+        const int r = i / W, c = i - r * W;
+        if (!bit(vbits, r, c)) continue;
+        if (c >= 1 && bit(hbits, r, c) && bit(hbits, r - 1, c) && bit(vbits, r, c - 1)) continue;
+        uf_union(P, ld_wg(&P[i]), ld_wg(&P[i - W]));
+    }
+    block_sync();
+    STAMP(1);
+    // ---- C: flatten
+    for (int i = t; i < N; i += kSegThreads) {
+        const int p = P[i];
+        if (p >= 0) P[i] = uf_find(P, p);
+    }
+    block_sync();
+    STAMP(2);
+    // ---- D: labels = rank of the root; sizes
+    const int span = (N + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
+    {
+        const int w0 = wave * span, w1 = min(N, w0 + span);
+        int cnt = 0;
+        for (int base = w0; base < w1; base += 64) {
+            const int i = base + lane;
+            cnt += __popcll(__ballot(i < w1 && P[i] == i));
+        }
+        if (lane == 0) S.wsum[wave] = cnt;
+        __syncthreads();
+        int wb = 0, ncomp = 0;
+        for (int j = 0; j < kSegWaves; j++) {
+            if (j < wave) wb += S.wsum[j];
+            ncomp += S.wsum[j];
+        }
+        for (int base = w0; base < w1; base += 64) {
+            const int i = base + lane;
+            const bool root = i < w1 && P[i] == i;
+            const uint64_t m = __ballot(root);
+            if (root) {
+                const int L = wb + __popcll(m & lanemask_lt());
+                rankA[i] = L;
+                rootOf[L] = i;
+            }
+            wb += __popcll(m);
+        }
+        for (int k = t; k < ncomp; k += kSegThreads) sizes[k] = 0;
+        if (t == 0) S.misc[1] = ncomp;
+    }
+    block_sync();
+    for (int base = 0; base < N; base += kSegThreads) {
+        const int i = base + t;
+        int L = -1;
+        if (i < N) {
+            const int p = P[i];
+            if (p >= 0) L = rankA[p];
+            P[i] = L;
+        }
+        const int prevL = __shfl_up(L, 1);
+        const bool chg = lane == 0 || prevL != L;
+        const uint64_t cb = __ballot(chg);
+        if (chg && L >= 0) {
+            const uint64_t rest = lane == 63 ? 0ull : (cb >> (lane + 1));
+            const int len = rest ? __builtin_ctzll(rest) + 1 : 64 - lane;
+            atomicAdd(&sizes[L], len);
+        }
+    }
+    block_sync();
+    STAMP(3);
+    // ---- E: components larger than MinSize, in label order
+    const int ncomp = S.misc[1];
+    {
+        const int lspan = (ncomp + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
+        const int w0 = wave * lspan, w1 = min(ncomp, w0 + lspan);
+        int cnt = 0;
+        for (int base = w0; base < w1; base += 64) {
+            const int L = base + lane;
+            cnt += __popcll(__ballot(L < w1 && (unsigned)sizes[L] > (unsigned)g.min_size));
+        }
+        __syncthreads();
+        if (lane == 0) S.wsum[wave] = cnt;
+        __syncthreads();
+        int wb = 0, nbig = 0;
+        for (int j = 0; j < kSegWaves; j++) {
+            if (j < wave) wb += S.wsum[j];
+            nbig += S.wsum[j];
+        }
+        for (int base = w0; base < w1; base += 64) {
+            const int L = base + lane;
+            const bool big = L < w1 && (unsigned)sizes[L] > (unsigned)g.min_size;
+            const uint64_t m = __ballot(big);
+            const int j = wb + __popcll(m & lanemask_lt());
+            if (big && j < kMaxBig) {
+                S.big_label[j] = L;
+                S.big_size[j] = sizes[L];
+                S.big_root[j] = rootOf[L];
+            }
+            wb += __popcll(m);
+        }
+        __syncthreads();
+        if (t == 0) {
+            S.nbig = min(nbig, kMaxBig);
+            int off = 0;
+            for (int j = 0; j < S.nbig; j++) { S.big_off[j] = off; off += S.big_size[j]; }
+        }
+        __syncthreads();
+        for (int j = t; j < S.nbig; j += kSegThreads) sizes[S.big_label[j]] = -(j + 1);
+    }
+    block_sync();
+    const int nbig = S.nbig;
+    // ---- F: per-pixel component tag
+    for (int i = t; i < N; i += kSegThreads) {
+        const int L = P[i];
+        int s = 0;
+        if (L >= 0) {
+            const int z = sizes[L];
+            s = z < 0 ? -z : 0;
+        }
+        state[i] = (uint8_t)s;
+    }
+    block_sync();
+    STAMP(5);
+    // ---- G: member lists + mean/covariance in PCL's float accumulation order
+    for (int j = wave; j < nbig; j += kSegWaves) {
+        const int n = S.big_size[j], o = S.big_off[j], tag = j + 1;
+        float* st = &S.stage[wave][0][0];
+        float acc = 0.f;
+        int found = 0;
+        int base = S.big_root[j] & ~63;
+        float cx = 0.f, cy = 0.f, cz = 0.f;
+        if (base + lane < N) { cx = X[base + lane]; cy = Y[base + lane]; cz = Z[base + lane]; }
+        for (; found < n && base < N; base += 64) {
+            const int i = base + lane;
+            float nx = 0.f, ny = 0.f, nz = 0.f;
+            if (i + 64 < N) { nx = X[i + 64]; ny = Y[i + 64]; nz = Z[i + 64]; }
+            const bool m = i < N && state[i] == tag;
+            const uint64_t mk = __ballot(m);
+            if (mk) {
+                const int cnt = __popcll(mk), pos = __popcll(mk & lanemask_lt()), pad = (cnt + 3) & ~3;
+                if (m) {
+                    members[o + found + pos] = i;
+                    st[0 * 64 + pos] = cx * cx; st[1 * 64 + pos] = cx * cy; st[2 * 64 + pos] = cx * cz;
+                    st[3 * 64 + pos] = cy * cy; st[4 * 64 + pos] = cy * cz; st[5 * 64 + pos] = cz * cz;
+                    st[6 * 64 + pos] = cx; st[7 * 64 + pos] = cy; st[8 * 64 + pos] = cz;
+                }
+                if (lane >= cnt && lane < pad)
+                    for (int q = 0; q < 9; q++) st[q * 64 + lane] = 0.f;
+                wave_sync();
+                if (lane < 9) {
+                    const float4* row = (const float4*)(st + lane * 64);
+                    for (int q = 0; q < (pad >> 2); q++) {
+                        const float4 v = row[q];
+                        acc += v.x;
+                        acc += v.y;
+                        acc += v.z;
+                        acc += v.w;
+                    }
+                }
+                wave_sync();
+                found += cnt;
+            }
+            cx = nx; cy = ny; cz = nz;
+        }
+        if (lane < 9) acc /= (float)n;
+        float a[9];
+        for (int k = 0; k < 9; k++) a[k] = __shfl(acc, k);
+        if (lane == 0) {
+            float cov[3][3];
+            cov[0][0] = a[0] - a[6] * a[6];
+            cov[0][1] = a[1] - a[6] * a[7];
+            cov[0][2] = a[2] - a[6] * a[8];
+            cov[1][1] = a[3] - a[7] * a[7];
+            cov[1][2] = a[4] - a[7] * a[8];
+            cov[2][2] = a[5] - a[8] * a[8];
+            cov[1][0] = cov[0][1]; cov[2][0] = cov[0][2]; cov[2][1] = cov[1][2];
+            float ev0, evec[3];
+            eigen33_min(cov, &ev0, evec);
+            const float eig_sum = cov[0][0] + cov[1][1] + cov[2][2];
+            S.big_curv[j] = eig_sum != 0 ? fabsf(ev0 / eig_sum) : 0.f;
+            S.big_par[j][0] = evec[0]; S.big_par[j][1] = evec[1]; S.big_par[j][2] = evec[2]; S.big_par[j][3] = 0.f;
+            S.big_cen[j][0] = a[6]; S.big_cen[j][1] = a[7]; S.big_cen[j][2] = a[8]; S.big_cen[j][3] = 1.f;
+        }
+    }
+    block_sync();
+    STAMP(6);
+    // ---- H: plane sign via the (accumulating) viewpoint vector, curvature filter
+    if (t == 0) {
+        float vp[4] = {0, 0, 0, 0};
+        int nm = 0;
+        S.big_state[0] = 0;
+        for (int j = 0; j < nbig; j++) {
+            float pp[4] = {S.big_par[j][0], S.big_par[j][1], S.big_par[j][2], 0.f};
+            pp[3] = -1 * dot4(pp, S.big_cen[j]);
+            for (int k = 0; k < 4; k++) vp[k] -= S.big_cen[j][k];
+            if (dot4(vp, pp) < 0) {
+                for (int k = 0; k < 4; k++) pp[k] *= -1;
+                pp[3] = 0;
+                pp[3] = -1 * dot4(pp, S.big_cen[j]);
+            }
+            S.big_state[j + 1] = 0;
+            if (S.big_curv[j] < 0.001f && nm < kMaxPlanesPerFrame) {
+                S.model_big[nm] = j;
+                for (int k = 0; k < 4; k++) S.model_coef[nm][k] = pp[k];
+                S.big_state[j + 1] = (uint8_t)(nm + 1);
+                nm++;
+            }
+        }
+        S.nmodel = nm;
+    }
+    __syncthreads();
+    const int nmodel = S.nmodel;
+    for (int i = t; i < N; i += kSegThreads) {
+        const int s = state[i];
+        if (s) state[i] = S.big_state[s];
+    }
+    block_sync();
+    STAMP(7);
+    // ---- K: refinement (two passes), one wave per pass
+    uint64_t* cbits = hbits;  // rows with growable points (hbits no longer needed)
+    if (nmodel > 0 && nmodel <= 6) {
+        uint8_t* desc = nmask;  // the contour masks come later
+        int ng = 0;
+        for (int pass = 0; pass < 2; pass++) {
+            const bool bw = pass == 1;
+            for (int r = wave; r < H; r += kSegWaves)
+                for (int k = 0; k < RW; k++) {
+                    const int c = (k << 6) + lane, i = r * W + c;
+                    int dsc = 0;
+                    if (c < W) {
+                        dsc = refine_desc(state, X, Y, Z, S.model_coef, nmodel, W, H, i, bw);
+                        desc[i] = (uint8_t)dsc;
+                    }
+                    const uint64_t m = __ballot(dsc != 0);
+                    if (lane == 0) cbits[r * RW + k] = m;
+                }
+            __syncthreads();
+            if (pass == 0) STAMP(10);
+            if (wave == 0) refine_rows<K>(state, desc, cbits, W, H, bw);
+            __syncthreads();
+            if (pass == 0) STAMP(11);
+            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng);
+        }
+        if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
+    } else if (nmodel > 0) {
+        // general path: accept masks over up to 64 models evaluated in the pass
+        for (int r = wave; r < H; r += kSegWaves)
+            for (int k = 0; k < RW; k++) {
+                const int c = (k << 6) + lane, i = r * W + c;
+                bool cand = false;
+                if (c < W && state[i] == 0) {
+                    const float x = X[i], y = Y[i], z = Z[i];
+                    if (isfinite(x))
+                        for (int v = 0; v < nmodel && !cand; v++) cand = ptp_ok(S.model_coef[v], x, y, z);
+                }
+                const uint64_t m = __ballot(cand);
+                if (lane == 0) cbits[r * RW + k] = m;
+            }
+        __syncthreads();
+        if (wave == 0) {
+            int ng = refine_pass<K>(S, state, cbits, X, Y, Z, W, H, false, ev, 0);
+            ng += refine_pass<K>(S, state, cbits, X, Y, Z, W, H, true, ev, ng);
+            if (lane == 0) S.misc[0] = ng;
+        }
+    } else if (t == 0) {
+        S.misc[0] = 0;
+    }
+    block_sync();
+    for (int e = t; e < S.misc[0]; e += kSegThreads) atomicAdd(&S.model_grown[ev[e] >> 24], 1);
+    __syncthreads();
+    STAMP(8);
+    // ---- L: Frame.cc:912-934: d >= 0, PlaneNotSeen; inlier offsets
+    if (t == 0) {
+        int nk = 0;
+        for (int m = 0; m < nmodel; m++) {
+            float cf[4] = {S.model_coef[m][0], S.model_coef[m][1], S.model_coef[m][2], S.model_coef[m][3]};
+            if (cf[3] < 0)
+                for (int k = 0; k < 4; k++) cf[k] = -cf[k];
+            bool seen = false;
+            for (int q = 0; q < nk && !seen; q++) {
+                const spslam_plane& pm = planes[q];
+                const float d = pm.coef[3] - cf[3];
+                const float angle = pm.coef[0] * cf[0] + pm.coef[1] * cf[1] + pm.coef[2] * cf[2];
+                if (d > 0.2f || d < -0.2f) continue;
+                if (angle < 0.9397f && angle > -0.9397f) continue;
+                seen = true;
+            }
+            if (seen || nk >= planes_cap) continue;
+            for (int k = 0; k < 4; k++) planes[nk].coef[k] = cf[k];
+            S.kept[nk++] = m;
+        }
+        S.nkept = nk;
+        int off = 0;
+        for (int q = 0; q < nk; q++) {
+            const int m = S.kept[q];
+            const int n = min(S.big_size[S.model_big[m]] + S.model_grown[m], g.inlier_cap - off);
+            planes[q].inlier_offset = off;
+            planes[q].n_inliers = n;
+            off += n;
+        }
+        plane_counts[f] = nk;
+    }
+    __syncthreads();
+    const int nk = S.nkept, ng = S.misc[0];
+    // ---- M: inlier lists (component members in raster order, then grown points in grow order);
+    //         8-neighbour same-state masks for the contour walk
+    for (int i = t; i < N; i += kSegThreads) {
+        const int s = state[i];
+        nmask[i] = s ? (uint8_t)nb_bits(state, W, H, i % W, i / W, s, true) : 0;
+    }
+    for (int q = wave; q < nk; q += kSegWaves) {
+        const int m = S.kept[q], j = S.model_big[m], n = S.big_size[j], o = S.big_off[j];
+        const int dst = planes[q].inlier_offset, lim = planes[q].n_inliers;
+        for (int k = lane; k < min(n, lim); k += 64) inl[dst + k] = members[o + k];
+        int w = n;
+        for (int e0 = 0; e0 < ng; e0 += 64) {
+            const int e = e0 + lane;
+            const int x = e < ng ? ev[e] : -1;
+            const bool hit = x >= 0 && (x >> 24) == m;
+            const uint64_t mk = __ballot(hit);
+            const int pos = w + __popcll(mk & lanemask_lt());
+            if (hit && pos < lim) inl[dst + pos] = x & 0xFFFFFF;
+            w += __popcll(mk);
+        }
+    }
+    block_sync();
+    STAMP(4);
+    // ---- N: contours (findLabeledRegionBoundary from the component's first pixel, on refined labels)
+    for (int q = wave; q < nk; q += kSegWaves)
+        if (lane == 0) {
+            const int m = S.kept[q];
+            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.big_root[S.model_big[m]], m + 1, nullptr, 0);
+        }
+    __syncthreads();
+    if (t == 0) {
+        int coff = 0;
+        for (int q = 0; q < nk; q++) {
+            planes[q].contour_offset = coff;
+            planes[q].n_contour = min(S.con_len[q], g.contour_cap - coff);
+            coff += planes[q].n_contour;
+        }
+    }
+    block_sync();
+    for (int q = wave; q < nk; q += kSegWaves)
+        if (lane == 0) {
+            const int m = S.kept[q];
+            trace_contour(state, nmask, W, H, N, S.big_root[S.model_big[m]], m + 1, con + planes[q].contour_offset,
+                          planes[q].n_contour);
+        }
+    STAMP(9);
+#undef STAMP
+}
+
+}  // namespace planes
+
+size_t plane_segment_lds_bytes(const PlaneGeom& g, bool* in_lds) {
+    const size_t RW = (g.W + 63) / 64;
+    const size_t bits = 2 * g.H * RW * sizeof(uint64_t);
+    const size_t maps = ((size_t)2 * g.N + 15) / 16 * 16;
+    const bool fits = sizeof(planes::SegShared) + bits + maps <= (size_t)planes::kLdsBytes;
+    if (in_lds) *in_lds = fits;
+    return bits + (fits ? maps : 0);
+}
+
+hipError_t plane_segment_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, spslam_plane* planes,
+                                int* plane_counts, int planes_cap, int32_t* inliers, int32_t* contours,
+                                hipStream_t s) {
+    if (g.W > 64 * planes::kMaxRowWords || g.N >= (1 << 24)) return hipErrorInvalidValue;
+    bool in_lds = false;
+    const size_t dyn = plane_segment_lds_bytes(g, &in_lds);
+    if (sizeof(planes::SegShared) + dyn > (size_t)planes::kLdsBytes) return hipErrorInvalidValue;
+    auto launch = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(n), dim3(planes::kSegThreads), dyn, s, g, b, planes, plane_counts, planes_cap,
+                           inliers, contours);
+    };
+    auto lds_attr = [](const void* k) {
+        return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(planes::kLdsBytes - sizeof(planes::SegShared)));
+    };
+    static const hipError_t a4 = lds_attr((const void*)planes::plane_segment_kernel<true, 4>);
+    static const hipError_t a8 = lds_attr((const void*)planes::plane_segment_kernel<true, 8>);
+    (void)a4;
+    (void)a8;
+    // lane positions per refinement row: 4 for W <= 256, 8 for W <= 512
+    if (in_lds) {
+        if (g.W <= 256) launch(planes::plane_segment_kernel<true, 4>);
+        else launch(planes::plane_segment_kernel<true, 8>);
+    } else {
+        if (g.W <= 256) launch(planes::plane_segment_kernel<false, 4>);
+        else launch(planes::plane_segment_kernel<false, 8>);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace spslam

@@ -466,10 +466,10 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     const long long N = g.N, F = c->p.max_batch, IWH = (long long)(g.W + 1) * (g.H + 1);
     PlaneBuffers& b = c->pb;
     b.cloud_fs = 3 * N; b.dist_fs = N; b.integral_fs = 6 * IWH; b.normal_fs = 3 * N; b.pd_fs = N;
-    b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N;
+    b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N; b.maps_fs = 2 * N;
     const size_t bytes = F * (sizeof(float) * (b.cloud_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
                               sizeof(double) * b.integral_fs + sizeof(uint32_t) * b.labels_fs +
-                              sizeof(int) * (b.work_fs + 2 * b.grown_fs)) + 4096;
+                              sizeof(int) * (b.work_fs + b.grown_fs) + b.maps_fs + 16 * sizeof(long long)) + 8192;
     if (c->d_plane_scratch) (void)hipFree(c->d_plane_scratch);
     c->d_plane_scratch = nullptr;
     HIP_CHECK(c, hipMalloc(&c->d_plane_scratch, bytes));
@@ -483,7 +483,8 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     b.labels = (uint32_t*)carve(F * b.labels_fs * 4);
     b.work = (int*)carve(F * b.work_fs * 4);
     b.grown = (int*)carve(F * b.grown_fs * 4);
-    b.grown_model = (int*)carve(F * b.grown_fs * 4);
+    b.maps = (uint8_t*)carve(F * b.maps_fs);
+    b.ts = (long long*)carve(F * 16 * sizeof(long long));
     void* olds[] = {c->d_depth_in, c->d_planes1, c->d_plane_cnt1, c->d_inl1, c->d_con1};
     for (void* o : olds)
         if (o) (void)hipFree(o);
@@ -573,6 +574,10 @@ int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_po
     }
     if (what == 3) {
         HIP_CHECK(c, hipMemcpy(out, b.labels + frame * b.labels_fs, N * 4, hipMemcpyDeviceToHost));
+        return SPSLAM_OK;
+    }
+    if (what == 4) {
+        HIP_CHECK(c, hipMemcpy(out, b.ts + frame * 16, 16 * sizeof(long long), hipMemcpyDeviceToHost));
         return SPSLAM_OK;
     }
     return fail(c, SPSLAM_ERR_ARG, "unknown debug stage%s", "");

@@ -50,6 +50,12 @@ class PlaneExtractor:
         self.W = -(-width // cloud_dis)
         self.H = -(-height // cloud_dis)
 
+    def configure(self, **kw):
+        """Change Plane.* parameters (min_size, angle_threshold, distance_threshold, ...) in place."""
+        for k, v in kw.items():
+            setattr(self.params, k, v)
+        self.ex._check(self.ex.lib.spslam_planes_configure(self.ex.ctx, ctypes.byref(self.params)))
+
     def __call__(self, depth_f32: np.ndarray):
         """Returns dict(coef=[...], inliers=[...], contour=[...]) like the oracle."""
         d = np.ascontiguousarray(depth_f32, np.float32)

@@ -37,13 +37,84 @@ def depth_frames():
     return out
 
 
-def _oracle(depth):
+def _oracle(depth, scale=1.0, min_size=500):
     import oracle_planes
     import synth
     K = synth.TUM3
     po = oracle_planes.PlaneOracle()
-    res = po.extract(depth, K["fx"], K["fy"], K["cx"], K["cy"])
+    res = po.extract(depth, K["fx"] * scale, K["fy"] * scale, K["cx"] * scale, K["cy"] * scale, min_size=min_size)
     return po, res
+
+
+def _compare(pe, depth, k, scale=1.0, min_size=500):
+    """Every stage and output of one frame against the oracle; returns (#planes, #models)."""
+    po, ro = _oracle(depth, scale, min_size)
+    rg = pe(depth)
+    assert np.array_equal(pe.debug(0, 0), po.cloud(), equal_nan=True), f"frame {k}: cloud"
+    assert np.array_equal(pe.debug(0, 2), po.distance(), equal_nan=True), f"frame {k}: distance map"
+    ng, no = pe.debug(0, 1), po.normals()
+    assert np.array_equal(np.isnan(ng), np.isnan(no)), f"frame {k}: normal validity"
+    m = ~np.isnan(no)
+    assert np.array_equal(ng[m], no[m]), f"frame {k}: normals"
+    assert np.array_equal(pe.debug(0, 3), po.labels(False)), f"frame {k}: CC labels"
+    assert len(rg["coef"]) == len(ro["coef"]), f"frame {k}: {len(rg['coef'])} vs {len(ro['coef'])} planes"
+    for j in range(len(ro["coef"])):
+        assert np.abs(rg["coef"][j] - ro["coef"][j]).max() <= COEF_TOL * max(1.0, abs(ro["coef"][j][3])), \
+            f"frame {k} plane {j}: {rg['coef'][j]} vs {ro['coef'][j]}"
+        assert np.array_equal(rg["inliers"][j], ro["inliers"][j]), f"frame {k} plane {j}: inliers"
+        assert np.array_equal(rg["contour"][j], ro["contour"][j]), f"frame {k} plane {j}: contour"
+    return len(ro["coef"]), po.n_models
+
+
+def test_planes_many_models(ctx):
+    """More than 6 candidate models per frame (the general refinement path) and fewer (the fast path)."""
+    import oracle_planes
+    import synth
+    _, pe = ctx
+    sc = synth.Scene(3, n_boxes=8)
+    models = []
+    for min_size in (500, 150):
+        pe.configure(min_size=min_size)
+        for fi in (0, 15, 30):
+            _, d, _ = sc.render(sc.pose(fi), noise_seed=fi)
+            models.append(_compare(pe, oracle_planes.depth_to_float(d), fi, min_size=min_size)[1])
+    pe.configure(min_size=500)
+    assert min(models) <= 6 < max(models), models
+
+
+def test_planes_nan_depth(ctx):
+    """Non-finite depth samples: invalid points (label 0xFFFFFFFF), skipped by the refinement loops."""
+    import oracle_planes
+    import synth
+    _, pe = ctx
+    sc = synth.Scene(0)
+    _, d, _ = sc.render(sc.pose(12), noise_seed=12)
+    depth = oracle_planes.depth_to_float(d)
+    rng = np.random.default_rng(5)
+    depth[rng.random(depth.shape) < 0.01] = np.nan
+    depth[200:260, 300:420] = np.nan
+    n, _ = _compare(pe, depth, 12)
+    assert n >= 1
+
+
+def test_planes_c5_size():
+    """1280x960 (BASELINE config C5): maps in global memory, 8 positions per lane."""
+    import oracle_planes
+    import spslam_gpu
+    import spslam_planes
+    import synth
+    K = synth.TUM3
+    ex = spslam_gpu.OrbExtractor(nfeatures=4000, width=1280, height=960, max_batch=1)
+    try:
+        for min_size, expect_general in ((500, True), (4000, False)):
+            pe = spslam_planes.PlaneExtractor(ex, K["fx"] * 2, K["fy"] * 2, K["cx"] * 2, K["cy"] * 2, 1280, 960,
+                                              min_size=min_size)
+            sc = synth.Scene(1, n_boxes=8)
+            _, d, _ = sc.render(sc.pose(5), 1280, 960, noise_seed=5)
+            n, nm = _compare(pe, oracle_planes.depth_to_float(d), 5, scale=2.0, min_size=min_size)
+            assert n >= 2 and (nm > 6) == expect_general, (n, nm)
+    finally:
+        ex.close()
 
 
 def test_planes_match_oracle(ctx, depth_frames):
