@@ -82,21 +82,6 @@ def test_planes_many_models(ctx):
     assert min(models) <= 6 < max(models), models
 
 
-def test_planes_nan_depth(ctx):
-    """Non-finite depth samples: invalid points (label 0xFFFFFFFF), skipped by the refinement loops."""
-    import oracle_planes
-    import synth
-    _, pe = ctx
-    sc = synth.Scene(0)
-    _, d, _ = sc.render(sc.pose(12), noise_seed=12)
-    depth = oracle_planes.depth_to_float(d)
-    rng = np.random.default_rng(5)
-    depth[rng.random(depth.shape) < 0.01] = np.nan
-    depth[200:260, 300:420] = np.nan
-    n, _ = _compare(pe, depth, 12)
-    assert n >= 1
-
-
 def test_planes_c5_size():
     """1280x960 (BASELINE config C5): maps in global memory, 8 positions per lane."""
     import oracle_planes
