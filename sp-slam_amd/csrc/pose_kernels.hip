@@ -60,13 +60,14 @@ __device__ Q q_from_rot(const M3& R) {
         if (R.a[8] > R.a[4 * i]) i = 2;
         const int j = (i + 1) % 3, k = (j + 1) % 3;
         t = sqrt(R.a[4 * i] - R.a[4 * j] - R.a[4 * k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
+        const double ci = 0.5 * t;
         t = 0.5 / t;
         q.w = (R.a[3 * k + j] - R.a[3 * j + k]) * t;
-        c[j] = (R.a[3 * j + i] + R.a[3 * i + j]) * t;
-        c[k] = (R.a[3 * k + i] + R.a[3 * i + k]) * t;
-        q.x = c[0]; q.y = c[1]; q.z = c[2];
+        const double cj = (R.a[3 * j + i] + R.a[3 * i + j]) * t;
+        const double ck = (R.a[3 * k + i] + R.a[3 * i + k]) * t;
+        q.x = i == 0 ? ci : (j == 0 ? cj : ck);
+        q.y = i == 1 ? ci : (j == 1 ? cj : ck);
+        q.z = i == 2 ? ci : (j == 2 ? cj : ck);
     }
     return q;
 }
@@ -200,11 +201,11 @@ __device__ __forceinline__ void point_error(const spslam_point_obs& o, const SE3
 
 // Eigen::LDLT (lower, diagonal pivoting) + solve.  Returns false when the
 // factor is not positive (LinearSolverDense::solve returns false, x unchanged).
-__device__ bool ldlt_solve(double m[6][6], const double* b, double* x) {
+// m, tr, temp and y live in LDS (dynamic pivot indexing would otherwise spill to scratch).
+__device__ __forceinline__ bool ldlt_solve(double (*m)[6], const double* b, double* x, int* tr, double* temp,
+                                           double* y) {
     const int n = 6;
-    int tr[6];
     int sign = 0;
-    double temp[6];
     for (int k = 0; k < n; ++k) {
         int big = k;
         double bv = fabs(m[k][k]);
@@ -238,7 +239,6 @@ __device__ bool ldlt_solve(double m[6][6], const double* b, double* x) {
         else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
     if (!(sign == 1 || sign == 0)) return false;
-    double y[6];
     for (int i = 0; i < n; i++) y[i] = b[i];
     for (int k = 0; k < n; k++) { double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
     for (int i = 0; i < n; i++)
@@ -253,10 +253,16 @@ __device__ bool ldlt_solve(double m[6][6], const double* b, double* x) {
 
 constexpr int kThreads = 256;
 constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
+constexpr int kPlaneChunk = 64;  // plane edges whose 12 perturbed errors are evaluated together
 
 struct Shared {
     double red[kThreads / 64][kRed];
+    SE3 Eadd[12];                    // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
+    SE3 Tp[12];                      // exp(+-1e-9 e_d) * T for the current iterate
+    double perr[kPlaneChunk][12][3]; // plane errors at the 12 perturbed poses
     double H[6][6], b[6], x[6];
+    double Hl[6][6], ly[6], ltemp[6];
+    int ltr[6];
     double lambda, ni, currentChi, iniChi, tempChi;
     SE3 T, T0, Ttrial, Tlast;
     int nBad, stop, active_any;
@@ -319,6 +325,11 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
         if (t == 0) { res->n_inliers = 0; res->lm_iterations = 0; }
         return;
     }
+    if (t < 12 && nl > 0) {
+        double add[6] = {0, 0, 0, 0, 0, 0};
+        add[t >> 1] = (t & 1) ? -1e-9 : 1e-9;
+        S.Eadd[t] = se3_exp(add);
+    }
     if (t == 0) {
         M3 R;
         for (int i = 0; i < 3; i++)
@@ -372,55 +383,90 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
             for (int it = 0; it < 10; it++) {
                 // ---- pass A: errors, robust chi2, quadratic form at T
                 double v[kRed];
+#pragma unroll
                 for (int k = 0; k < kRed; k++) v[k] = 0;
                 const SE3 T = S.T;
-                for (int e = t; e < ne; e += kThreads) {
-                    if (is_outlier(e)) continue;
+                // accumulate one edge's robust chi2, J^T W J and -J^T W e
+                auto accumulate = [&](const double (&J)[3][6], const double* err, const double* info, int dim,
+                                      double delta) {
+                    // rows beyond dim carry zero error and Jacobian: their terms add exact zeros
+                    (void)dim;
+                    double chi = 0;
+#pragma unroll
+                    for (int r = 0; r < 3; r++) chi += err[r] * info[r] * err[r];
+                    double rho0, rho1;
+                    huber(chi, delta, robust, &rho0, &rho1);
+                    v[0] += rho0;
+#pragma unroll
+                    for (int i = 0; i < 6; i++)
+#pragma unroll
+                        for (int j = i; j < 6; j++) {
+                            double s = 0;
+#pragma unroll
+                            for (int r = 0; r < 3; r++) s += J[r][i] * (rho1 * info[r]) * J[r][j];
+                            v[1 + i * 6 - i * (i - 1) / 2 + (j - i)] += s;
+                        }
+#pragma unroll
+                    for (int i = 0; i < 6; i++) {
+                        double s = 0;
+#pragma unroll
+                        for (int r = 0; r < 3; r++) s += rho1 * J[r][i] * (info[r] * err[r]);
+                        v[22 + i] -= s;
+                    }
+                };
+                for (int e = t; e < np; e += kThreads) {
+                    if (pout[e]) continue;
                     double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
                     int dim;
                     edge_info(e, info, &delta, &dim);
                     V3 pc;
                     error_at(e, T, err, &pc);
-                    double chi = 0;
-                    for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
-                    double rho0, rho1;
-                    huber(chi, delta, robust, &rho0, &rho1);
-                    v[0] += rho0;
-                    if (e < np) {
-                        const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
-                        J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-                        J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
-                        J[0][5] = x * invz_2 * cam.fx;
-                        J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
-                        J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
-                        J[1][5] = y * invz_2 * cam.fy;
-                        if (dim == 3) {
-                            J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
-                            J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
-                        }
+                    const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
+                    J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+                    J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
+                    J[0][5] = x * invz_2 * cam.fx;
+                    J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
+                    J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
+                    J[1][5] = y * invz_2 * cam.fy;
+                    if (dim == 3) {
+                        J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
+                        J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
                     } else {
-                        // numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205)
-                        const double dl = 1e-9, scalar = 1.0 / (2 * dl);
-                        for (int d = 0; d < 6; d++) {
-                            double add[6] = {0, 0, 0, 0, 0, 0}, ep[3] = {0, 0, 0}, em[3] = {0, 0, 0};
-                            add[d] = dl;
-                            error_at(e, se3_mul(se3_exp(add), T), ep, nullptr);
-                            add[d] = -dl;
-                            error_at(e, se3_mul(se3_exp(add), T), em, nullptr);
-                            for (int r = 0; r < dim; r++) J[r][d] = scalar * (ep[r] - em[r]);
-                        }
+#pragma unroll
+                        for (int d = 0; d < 6; d++) J[2][d] = 0;
                     }
-                    int k = 1;
-                    for (int i = 0; i < 6; i++)
-                        for (int j = i; j < 6; j++, k++) {
-                            double s = 0;
-                            for (int r = 0; r < dim; r++) s += J[r][i] * (rho1 * info[r]) * J[r][j];
-                            v[k] += s;
+                    accumulate(J, err, info, dim, delta);
+                }
+                // plane edges: numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205);
+                // the 12 perturbed evaluations of each edge run on 12 threads
+                if (nl > 0) {
+                    if (t < 12) S.Tp[t] = se3_mul(S.Eadd[t], T);
+                    __syncthreads();
+                    for (int base = 0; base < nl; base += kPlaneChunk) {
+                        const int cnt = min(kPlaneChunk, nl - base);
+                        for (int w = t; w < cnt * 12; w += kThreads) {
+                            const int j = w / 12, q = w - j * 12, e = np + base + j;
+                            double err[3] = {0, 0, 0};
+                            if (!plout[e - np]) error_at(e, S.Tp[q], err, nullptr);
+                            S.perr[j][q][0] = err[0]; S.perr[j][q][1] = err[1]; S.perr[j][q][2] = err[2];
                         }
-                    for (int i = 0; i < 6; i++) {
-                        double s = 0;
-                        for (int r = 0; r < dim; r++) s += rho1 * J[r][i] * (info[r] * err[r]);
-                        v[22 + i] -= s;
+                        __syncthreads();
+                        for (int j = t; j < cnt; j += kThreads) {
+                            const int e = np + base + j;
+                            if (plout[e - np]) continue;
+                            double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
+                            int dim;
+                            edge_info(e, info, &delta, &dim);
+                            error_at(e, T, err, nullptr);
+                            const double scalar = 1.0 / (2 * 1e-9);
+#pragma unroll
+                            for (int d = 0; d < 6; d++)
+#pragma unroll
+                                for (int r = 0; r < 3; r++)
+                                    J[r][d] = scalar * (S.perr[j][2 * d][r] - S.perr[j][2 * d + 1][r]);
+                            accumulate(J, err, info, dim, delta);
+                        }
+                        __syncthreads();
                     }
                 }
                 block_reduce(v, kRed, S);
@@ -448,11 +494,10 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                 bool ok2 = true;
                 do {
                     if (t == 0) {
-                        double Hl[6][6];
                         for (int i = 0; i < 6; i++)
-                            for (int j = 0; j < 6; j++) Hl[i][j] = S.H[i][j] + (i == j ? S.lambda : 0.0);
+                            for (int j = 0; j < 6; j++) S.Hl[i][j] = S.H[i][j] + (i == j ? S.lambda : 0.0);
                         double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten
-                        S.stop = ldlt_solve(Hl, S.b, x) ? 1 : 0;
+                        S.stop = ldlt_solve(S.Hl, S.b, x, S.ltr, S.ltemp, S.ly) ? 1 : 0;
                         for (int j = 0; j < 6; j++) S.x[j] = x[j];
                         S.Ttrial = se3_mul(se3_exp(x), S.T);
                     }
