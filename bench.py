@@ -61,9 +61,9 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls):
     N = W * H
     IWH = (W + 1) * (H + 1)
     return {
-        "resize_level_kernel": sum(px[:-1]) + sum(px[1:]),   # read level l-1, write level l
-        "fast_cells_kernel": sum(px),                         # every level pixel read once
-        "blur_kernel": 2 * sum(px),                           # read + write every level
+        # level l-1 (or the input frame) read; level image (l >= 1), blur and FAST score map written
+        "level_kernel": px[0] + sum(px[:-1]) + sum(px[1:]) + 2 * sum(px),
+        "fast_cells_kernel": sum(px),                         # score maps read once
         "octree_kernel": 0,                                   # serial list algorithm, no streamed bytes
         "desc_kernel": n_kp * (28 + 32),                      # keypoint + descriptor out
         "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call

@@ -13,6 +13,8 @@ constexpr int kMinBorder = kEdgeThreshold - 3;
 constexpr int kCellCap = 512;          // max FAST survivors of one cell window (checked on host)
 constexpr int kCellWinMax = 72;        // max cell window side (LDS tile pitch)
 constexpr int kNodeCap = 1024;         // max DistributeOctTree list length (checked on host)
+constexpr int kLevelTileW = 64;        // level_kernel output tile
+constexpr int kLevelTileH = 32;
 
 struct LevelGeom {
     int w, h;                 // level image size
@@ -31,7 +33,9 @@ struct LevelGeom {
     int key_base;             // offset of the level's key scratch (in keys) per frame
     int patch_size;           // (int)(PATCH_SIZE * mvScaleFactor[level])
     float scale;              // mvScaleFactor[level]
-    int pad2_;
+    int tiles_x;              // level_kernel tiles per row
+    uint8_t* score;           // FAST score map (pitch w, frame stride blur_frame_stride), frame 0
+    double rscale_x, rscale_y;  // resize from level-1: 1. / ((double)w / w_prev), as OpenCV computes it
 };
 
 struct OrbGeom {
@@ -40,8 +44,8 @@ struct OrbGeom {
     int cells_per_frame;
     int lvl_kp_per_frame;     // sum of kp_cap over levels
     int keys_per_frame;       // sum of ncells*kCellCap over levels
-    int blur_tiles_per_frame;
-    int pad_[3];
+    int level_tiles[kMaxLevels];  // level_kernel tiles per frame, per level
+    int pad_[4];
 };
 
 // Intermediate per-level keypoint (DistributeOctTree output, level coordinates).

@@ -1,12 +1,13 @@
 // gfx950 kernels for SP-SLAM's ORB extractor (reference: src/ORBextractor.cc).
 //
-// One batched pass over B frames is five kernel kinds:
-//   resize_level_kernel   x7  pyramid level l from level l-1 (OpenCV INTER_LINEAR
-//                             8U fixed point, :1107-1132)
-//   fast_cells_kernel     x1  one wave per 30x30 FAST cell of every level: window
-//                             in LDS, FAST-9/16 score, 3x3 NMS at iniThFAST, retry
-//                             at minThFAST if the cell came back empty (:789-829)
-//   blur_kernel           x1  7x7 sigma-2 Gaussian of every level (:1085-1086)
+// One batched pass over B frames is four kernel kinds:
+//   level_kernel          x8  per pyramid level, 64x32 tiles: level image (OpenCV
+//                             INTER_LINEAR 8U fixed point from level l-1,
+//                             :1107-1132), its 7x7 sigma-2 Gaussian (:1085-1086)
+//                             and its FAST-9/16 score map, from one LDS tile
+//   fast_cells_kernel     x1  one wave per 30x30 FAST cell of every level: 3x3
+//                             NMS at iniThFAST on the score map, retry at
+//                             minThFAST if the cell came back empty (:789-829)
 //   octree_kernel         x1  one workgroup per (frame, level): DistributeOctTree
 //                             (:539-763) as data-parallel passes over the keys
 //   desc_kernel           x1  one wave per keypoint: IC_Angle (:77-104) + rotated
@@ -28,48 +29,6 @@ __constant__ int8_t c_pattern[1024] = {
 __constant__ int c_umax[16];
 
 __device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
-
-// ---------------------------------------------------------------------------
-// Pyramid: OpenCV resize INTER_LINEAR on 8U (classic fixed-point path).
-// One thread per destination pixel; the per-column / per-row coefficients are
-// recomputed from the same double/float expressions OpenCV uses.
-__global__ __launch_bounds__(256) void resize_level_kernel(const uint8_t* __restrict__ src, int sw, int sh,
-                                                           int sstride, long long sfs, uint8_t* __restrict__ dst,
-                                                           int dw, int dh, int dstride, long long dfs) {
-    const int f = blockIdx.y;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= dw * dh) return;
-    const int dy = idx / dw, dx = idx - dy * dw;
-    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
-    float fx = (float)((dx + 0.5) * scale_x - 0.5);
-    int sx = (int)floorf(fx);
-    fx -= sx;
-    bool tail = false;
-    if (sx < 0) { fx = 0; sx = 0; }
-    if (sx + 1 >= sw) {
-        tail = true;
-        if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
-    }
-    const int a0 = (short)cv_round((1.f - fx) * 2048.f), a1 = (short)cv_round(fx * 2048.f);
-    float fy = (float)((dy + 0.5) * scale_y - 0.5);
-    int sy = (int)floorf(fy);
-    fy -= sy;
-    const int b0 = (short)cv_round((1.f - fy) * 2048.f), b1 = (short)cv_round(fy * 2048.f);
-    const int y0 = min(max(sy, 0), sh - 1), y1 = min(max(sy + 1, 0), sh - 1);
-    const uint8_t* s = src + f * sfs;
-    const uint8_t* r0p = s + (size_t)y0 * sstride + sx;
-    const uint8_t* r1p = s + (size_t)y1 * sstride + sx;
-    int r0, r1;
-    if (!tail) {
-        r0 = r0p[0] * a0 + r0p[1] * a1;
-        r1 = r1p[0] * a0 + r1p[1] * a1;
-    } else {
-        r0 = r0p[0] * 2048;
-        r1 = r1p[0] * 2048;
-    }
-    dst[f * dfs + (size_t)dy * dstride + dx] =
-        (uint8_t)((((b0 * (r0 >> 4)) >> 16) + ((b1 * (r1 >> 4)) >> 16) + 2) >> 2);
-}
 
 // ---------------------------------------------------------------------------
 // FAST-9/16.  Score = max over the 16 contiguous 9-arcs of min(v - x) and of
@@ -99,6 +58,170 @@ __device__ __forceinline__ int fast_score(const uint8_t* p, int P) {
     return max(best, -worst) - 1;
 }
 
+
+// ---------------------------------------------------------------------------
+// One pyramid level, one 64x32 output tile per 256-thread workgroup:
+//   * the tile plus a 3-pixel halo of level l, resized from level l-1 with
+//     OpenCV's INTER_LINEAR 8U fixed point (:1107-1132; per-pixel
+//     coefficients from the same double/float expressions OpenCV uses), or
+//     read from the input frame at level 0; BORDER_REFLECT_101 outside;
+//   * the level image (tile interior) for the next level, IC_Angle and BRIEF;
+//   * GaussianBlur 7x7 sigma 2 (:1085-1086), OpenCV's bit-exact 8U fixed point:
+//     out = (sum_ij k_i k_j p + 2^15) >> 16 with k = [18,34,48,56,48,34,18];
+//   * the FAST score map (0 where no cell window evaluates a pixel).
+constexpr int kLH = kLevelTileH + 6, kLW = kLevelTileW + 6;
+constexpr int kLevelThreads = 256;
+
+// BORDER_REFLECT_101 for positions at most one image length outside (tiles
+// overhang by < 64 + 3 pixels; levels are >= 64 wide/high).
+__device__ __forceinline__ int reflect1(int p, int len) {
+    p = p < 0 ? -p : p;
+    return p >= len ? 2 * len - 2 - p : p;
+}
+
+// OpenCV INTER_LINEAR 8U coefficients for one destination column / row: the
+// same double/float expressions as cv::resize.
+struct RzCol { int16_t x0, x1, a0, a1; };
+__device__ __forceinline__ RzCol resize_coef(double s, int d, int slen, bool horizontal) {
+    float fx = (float)((d + 0.5) * s - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= sx;
+    RzCol r;
+    if (horizontal) {
+        bool tail = false;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= slen) {
+            tail = true;
+            if (sx >= slen - 1) { fx = 0; sx = slen - 1; }
+        }
+        const int a0 = (short)cv_round((1.f - fx) * 2048.f), a1 = (short)cv_round(fx * 2048.f);
+        r.x0 = (int16_t)sx;
+        r.x1 = (int16_t)(tail ? sx : sx + 1);
+        r.a0 = (int16_t)(tail ? 2048 : a0);
+        r.a1 = (int16_t)(tail ? 0 : a1);
+    } else {
+        const int b0 = (short)cv_round((1.f - fx) * 2048.f), b1 = (short)cv_round(fx * 2048.f);
+        r.x0 = (int16_t)min(max(sx, 0), slen - 1);
+        r.x1 = (int16_t)min(max(sx + 1, 0), slen - 1);
+        r.a0 = (int16_t)b0;
+        r.a1 = (int16_t)b1;
+    }
+    return r;
+}
+
+// Necessary condition for a FAST-9 corner at threshold t: some 9-arc contains
+// two consecutive compass pixels (0, 4, 8, 12), both brighter or both darker.
+__device__ __forceinline__ bool fast_maybe(const uint8_t* p, int P, int t) {
+    const int v = p[0];
+    const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
+    const int hi = v + t, lo = v - t;
+    const int b = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
+    const int k = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
+    const int br = b & ((b >> 1) | (b << 3));
+    const int dk = k & ((k >> 1) | (k << 3));
+    return (br | dk) & 15;
+}
+
+__global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
+    __shared__ uint8_t tin[kLH][kLW + 2];
+    __shared__ uint16_t th[kLH][kLevelTileW];
+    __shared__ RzCol rx[kLW], ry[kLH];
+    __shared__ uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
+    const LevelGeom& L = g.lv[l];
+    const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int x0 = (blockIdx.x % L.tiles_x) * kLevelTileW, y0 = (blockIdx.x / L.tiles_x) * kLevelTileH;
+    const int w = L.w, h = L.h;
+    uint8_t* img = const_cast<uint8_t*>(L.img) + f * L.frame_stride;
+    constexpr int kN = kLH * kLW, kIter = (kN + kLevelThreads - 1) / kLevelThreads;
+    if (l == 0) {
+        uint8_t v[kIter];
+#pragma unroll
+        for (int k = 0; k < kIter; k++) {
+            const int q = t + k * kLevelThreads;
+            v[k] = 0;
+            if (q < kN) {
+                const int r = q / kLW, c = q - r * kLW;
+                const int y = reflect1(y0 + r - 3, h), x = reflect1(min(x0 + c - 3, w + 2), w);
+                v[k] = img[(size_t)y * L.stride + x];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kIter; k++) {
+            const int q = t + k * kLevelThreads;
+            if (q < kN) tin[q / kLW][q % kLW] = v[k];
+        }
+    } else {
+        const LevelGeom& S = g.lv[l - 1];
+        const uint8_t* src = S.img + f * S.frame_stride;
+        if (t < kLW) rx[t] = resize_coef(L.rscale_x, reflect1(min(x0 + t - 3, w + 2), w), S.w, true);
+        else if (t < kLW + kLH) ry[t - kLW] = resize_coef(L.rscale_y, reflect1(y0 + (t - kLW) - 3, h), S.h, false);
+        __syncthreads();
+        int v[kIter];
+#pragma unroll
+        for (int k = 0; k < kIter; k++) {
+            const int q = t + k * kLevelThreads;
+            v[k] = 0;
+            if (q < kN) {
+                const int r = q / kLW, c = q - r * kLW;
+                const RzCol cx = rx[c], cy = ry[r];
+                const uint8_t* r0p = src + (size_t)cy.x0 * S.stride;
+                const uint8_t* r1p = src + (size_t)cy.x1 * S.stride;
+                const int r0 = r0p[cx.x0] * cx.a0 + r0p[cx.x1] * cx.a1;
+                const int r1 = r1p[cx.x0] * cx.a0 + r1p[cx.x1] * cx.a1;
+                v[k] = (((cy.a0 * (r0 >> 4)) >> 16) + ((cy.a1 * (r1 >> 4)) >> 16) + 2) >> 2;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kIter; k++) {
+            const int q = t + k * kLevelThreads;
+            if (q < kN) {
+                const int r = q / kLW, c = q - r * kLW;
+                tin[r][c] = (uint8_t)v[k];
+                if (r >= 3 && r < 3 + kLevelTileH && c >= 3 && c < 3 + kLevelTileW && y0 + r - 3 < h &&
+                    x0 + c - 3 < w)
+                    img[(size_t)(y0 + r - 3) * L.stride + (x0 + c - 3)] = (uint8_t)v[k];
+            }
+        }
+    }
+    __syncthreads();
+    // horizontal blur pass over all tile rows
+    for (int q = t; q < kLH * kLevelTileW; q += kLevelThreads) {
+        const int r = q / kLevelTileW, c = q - r * kLevelTileW;
+        const uint8_t* p = &tin[r][c];
+        th[r][c] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3]);
+    }
+    __syncthreads();
+    uint8_t* blur = L.blur + f * L.blur_frame_stride;
+    uint8_t* score = L.score + f * L.blur_frame_stride;
+    // vertical blur pass; FAST pre-test at the lowest threshold, candidates compacted per wave
+    int ncand = 0;
+    for (int q0 = wave * 64; q0 < kLevelTileH * kLevelTileW; q0 += kLevelThreads) {
+        const int q = q0 + lane;
+        const int r = q / kLevelTileW, c = q - r * kLevelTileW;
+        const int y = y0 + r, x = x0 + c;
+        bool maybe = false;
+        if (y < h && x < w) {
+            const int sb = 18 * (th[r][c] + th[r + 6][c]) + 34 * (th[r + 1][c] + th[r + 5][c]) +
+                           48 * (th[r + 2][c] + th[r + 4][c]) + 56 * th[r + 3][c];
+            blur[(size_t)y * w + x] = (uint8_t)min(255, (sb + (1 << 15)) >> 16);
+            maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 && fast_maybe(&tin[r + 3][c + 3], kLW + 2, minTh);
+            if (!maybe) score[(size_t)y * w + x] = 0;
+        }
+        const unsigned long long m = __ballot(maybe);
+        if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)q;
+        ncand += __popcll(m);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int k = lane; k < ncand; k += 64) {
+        const int q = cand[wave][k];
+        const int r = q / kLevelTileW, c = q - r * kLevelTileW;
+        const int sc = max(fast_score(&tin[r + 3][c + 3], kLW + 2), 0);
+        score[(size_t)(y0 + r) * w + (x0 + c)] = (uint8_t)(sc >= minTh ? sc : 0);
+    }
+}
+
 __device__ __forceinline__ int level_of_cell(const OrbGeom& g, int cid) {
     int l = 0;
     for (int k = 1; k < g.nlevels; k++)
@@ -106,14 +229,20 @@ __device__ __forceinline__ int level_of_cell(const OrbGeom& g, int cid) {
     return l;
 }
 
-// One 64-lane wave per FAST cell.  Candidates are written in the reference's
-// order (row-major inside the cell), packed x | y << 12 | score << 24 with
-// (x, y) relative to (minBorderX, minBorderY) as at src/ORBextractor.cc:822-823.
-__global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
-                                                        uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
-    __shared__ uint8_t win[kCellWinMax * kCellWinMax];
-    __shared__ uint8_t sc[kCellWinMax * kCellWinMax];
-    const int cid = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+// FAST cells (:789-829): one wave per 30x30 cell, four cells per workgroup.
+// The cell window's evaluated pixels come from the score map; 3x3 non-max
+// suppression among corners at iniThFAST, retry at minThFAST if the cell came
+// back empty.  Candidates are written in the reference's order (row-major
+// inside the cell), packed x | y << 12 | score << 24 with (x, y) relative to
+// (minBorderX, minBorderY) as at src/ORBextractor.cc:822-823.
+constexpr int kCellScoreMax = kCellWinMax - 6;
+__global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
+                                                         uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
+    __shared__ uint8_t scs[4][kCellScoreMax * kCellScoreMax];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int cid = blockIdx.x * 4 + wave, f = blockIdx.y;
+    if (cid >= g.cells_per_frame) return;
+    uint8_t* sc = scs[wave];
     const int l = level_of_cell(g, cid);
     const LevelGeom& L = g.lv[l];
     const int local = cid - L.cell_base;
@@ -126,21 +255,30 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __r
         return;
     }
     const int maxY = min(iniY + L.hCell + 6, L.maxBorderY), maxX = min(iniX + L.wCell + 6, L.maxBorderX);
-    const int ww = maxX - iniX, wh = maxY - iniY;
-    const uint8_t* img = L.img + f * L.frame_stride + (size_t)iniY * L.stride + iniX;
-    for (int t = lane; t < ww * wh; t += 64) {
-        const int r = t / ww, c = t - r * ww;
-        win[r * kCellWinMax + c] = img[(size_t)r * L.stride + c];
-    }
-    __syncthreads();
-    const int R = wh - 6, C = ww - 6;
+    const int R = maxY - iniY - 6, C = maxX - iniX - 6;
     const int npx = (R > 0 && C > 0) ? R * C : 0;
-    for (int p = lane; p < npx; p += 64) {
-        const int r = 3 + p / C, c = 3 + p % C;
-        const int s = fast_score(&win[r * kCellWinMax + c], kCellWinMax);
-        sc[r * kCellWinMax + c] = (uint8_t)max(s, 0);
+    const uint8_t* smap = L.score + f * L.blur_frame_stride + (size_t)(iniY + 3) * L.w + (iniX + 3);
+    const float invC = 1.f / (float)max(C, 1);   // p / C exactly for p < 2^12
+    for (int p0 = 0; p0 < npx; p0 += 256) {
+        uint8_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = p0 + lane + 64 * k;
+            v[k] = 0;
+            if (p < npx) {
+                const int r = (int)(((float)p + 0.5f) * invC), c = p - r * C;
+                v[k] = smap[(size_t)r * L.w + c];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = p0 + lane + 64 * k;
+            if (p < npx) sc[p] = v[k];
+        }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     int base = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int thr = pass == 0 ? iniTh : minTh;
@@ -150,8 +288,8 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __r
             bool keep = false;
             int r = 0, c = 0, s = 0;
             if (p < npx) {
-                r = 3 + p / C; c = 3 + p % C;
-                s = sc[r * kCellWinMax + c];
+                r = (int)(((float)p + 0.5f) * invC); c = p - r * C;
+                s = sc[p];
                 if (s >= thr) {
                     keep = true;
 #pragma unroll
@@ -161,7 +299,7 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __r
                             if (!dy && !dx) continue;
                             const int rr = r + dy, cc = c + dx;
                             int n = 0;
-                            if (rr >= 3 && rr < wh - 3 && cc >= 3 && cc < ww - 3) n = sc[rr * kCellWinMax + cc];
+                            if (rr >= 0 && rr < R && cc >= 0 && cc < C) n = sc[rr * C + cc];
                             if (n < thr) n = 0;
                             keep = keep && (s > n);
                         }
@@ -170,60 +308,14 @@ __global__ __launch_bounds__(64) void fast_cells_kernel(OrbGeom g, uint32_t* __r
             const unsigned long long mask = __ballot(keep);
             if (keep) {
                 const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-                out[pos] = (uint32_t)(c + cj * L.wCell) | ((uint32_t)(r + ci * L.hCell) << 12) | ((uint32_t)s << 24);
+                out[pos] = (uint32_t)(c + 3 + cj * L.wCell) | ((uint32_t)(r + 3 + ci * L.hCell) << 12) |
+                           ((uint32_t)s << 24);
             }
             base += __popcll(mask);
         }
         if (base > 0) break;
     }
     if (lane == 0) cand_cnt[cell_slot] = (uint16_t)base;
-}
-
-// ---------------------------------------------------------------------------
-// GaussianBlur 7x7 sigma 2, BORDER_REFLECT_101, OpenCV 8U bit-exact fixed
-// point: out = (sum_ij k_i k_j p + 2^15) >> 16 with k = [18,34,48,56,48,34,18].
-constexpr int kBlurTW = 64, kBlurTH = 16;
-__device__ __forceinline__ int reflect101(int p, int len) {
-    if (len == 1) return 0;
-    while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
-    return p;
-}
-__global__ __launch_bounds__(256) void blur_kernel(OrbGeom g) {
-    __shared__ uint8_t tin[kBlurTH + 6][kBlurTW + 8];
-    __shared__ int th[kBlurTH + 6][kBlurTW];
-    const int f = blockIdx.y;
-    int tile = blockIdx.x, l = 0;
-    for (; l < g.nlevels; l++) {
-        const LevelGeom& L = g.lv[l];
-        const int nt = ((L.w + kBlurTW - 1) / kBlurTW) * ((L.h + kBlurTH - 1) / kBlurTH);
-        if (tile < nt) break;
-        tile -= nt;
-    }
-    const LevelGeom& L = g.lv[l];
-    const int tx = (L.w + kBlurTW - 1) / kBlurTW;
-    const int x0 = (tile % tx) * kBlurTW, y0 = (tile / tx) * kBlurTH;
-    const uint8_t* img = L.img + f * L.frame_stride;
-    for (int t = threadIdx.x; t < (kBlurTH + 6) * (kBlurTW + 6); t += 256) {
-        const int r = t / (kBlurTW + 6), c = t - r * (kBlurTW + 6);
-        const int y = reflect101(y0 + r - 3, L.h), x = reflect101(min(x0 + c - 3, L.w + 2), L.w);
-        tin[r][c] = img[(size_t)y * L.stride + x];
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < (kBlurTH + 6) * kBlurTW; t += 256) {
-        const int r = t / kBlurTW, c = t - r * kBlurTW;
-        const uint8_t* p = &tin[r][c];
-        th[r][c] = 18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3];
-    }
-    __syncthreads();
-    uint8_t* out = L.blur + f * L.blur_frame_stride;
-    for (int t = threadIdx.x; t < kBlurTH * kBlurTW; t += 256) {
-        const int r = t / kBlurTW, c = t - r * kBlurTW;
-        const int y = y0 + r, x = x0 + c;
-        if (y >= L.h || x >= L.w) continue;
-        const int s = 18 * (th[r][c] + th[r + 6][c]) + 34 * (th[r + 1][c] + th[r + 5][c]) +
-                      48 * (th[r + 2][c] + th[r + 4][c]) + 56 * th[r + 3][c];
-        out[(size_t)y * L.w + x] = (uint8_t)min(255, (s + (1 << 15)) >> 16);
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -694,9 +786,8 @@ hipError_t orb_upload_tables(const int umax[16]) {
 // Enqueue the whole ORB pass for n frames on `s`.  g.lv[0].img/stride/
 // frame_stride must already point at the caller's gray frames.
 const char* kernel_kind_name(int kind) {
-    static const char* names[kNumKernelKinds] = {"resize_level_kernel", "fast_cells_kernel", "blur_kernel",
-                                                 "octree_kernel", "desc_kernel", "pose_kernel",
-                                                 "plane_cloud_kernel", "plane_distance_kernel",
+    static const char* names[kNumKernelKinds] = {"level_kernel", "fast_cells_kernel", "octree_kernel",
+                                                 "desc_kernel", "pose_kernel", "plane_cloud_kernel", "plane_distance_kernel",
                                                  "plane_integral_kernel", "plane_normal_kernel",
                                                  "plane_segment_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
@@ -706,22 +797,15 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
                       uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer) {
     auto B = [&](int k) { if (timer) timer->begin(k, s); };
     auto E = [&](int k) { if (timer) timer->end(k, s); };
-    B(kKindResize);
-    for (int l = 1; l < g.nlevels; l++) {
-        const LevelGeom& P = g.lv[l - 1];
-        const LevelGeom& D = g.lv[l];
-        dim3 grid((D.w * D.h + 255) / 256, n);
-        hipLaunchKernelGGL(resize_level_kernel, grid, dim3(256), 0, s, P.img, P.w, P.h, P.stride, P.frame_stride,
-                           const_cast<uint8_t*>(D.img), D.w, D.h, D.stride, D.frame_stride);
-    }
-    E(kKindResize);
+    B(kKindLevel);
+    for (int l = 0; l < g.nlevels; l++)
+        hipLaunchKernelGGL(level_kernel, dim3(g.level_tiles[l], n), dim3(kLevelThreads), 0, s, g, l,
+                           min(iniTh, minTh));
+    E(kKindLevel);
     B(kKindFast);
-    hipLaunchKernelGGL(fast_cells_kernel, dim3(g.cells_per_frame, n), dim3(64), 0, s, g, b.cand, b.cand_cnt, iniTh,
-                       minTh);
+    hipLaunchKernelGGL(fast_cells_kernel, dim3((g.cells_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.cand,
+                       b.cand_cnt, iniTh, minTh);
     E(kKindFast);
-    B(kKindBlur);
-    hipLaunchKernelGGL(blur_kernel, dim3(g.blur_tiles_per_frame, n), dim3(256), 0, s, g);
-    E(kKindBlur);
     B(kKindOctree);
     hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
                        b.lvl_kp, b.lvl_cnt);

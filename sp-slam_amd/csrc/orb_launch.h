@@ -18,14 +18,14 @@ struct OrbBuffers {
 
 // Kernel kinds for the per-kind HIP-event timers (spslam_kernel_times).
 enum KernelKind {
-    kKindResize = 0, kKindFast, kKindBlur, kKindOctree, kKindDesc, kKindPose,
+    kKindLevel = 0, kKindFast, kKindOctree, kKindDesc, kKindPose,
     kKindPlaneCloud, kKindPlaneDist, kKindPlaneIntegral, kKindPlaneNormal, kKindPlaneSegment,
     kNumKernelKinds
 };
 const char* kernel_kind_name(int kind);
 
 // Optional timer: begin/end are called on the launch stream around each kernel
-// kind (the resize kind spans its per-level launches).
+// kind (the level kind spans its per-level launches).
 struct KernelTimer {
     virtual void begin(int kind, hipStream_t s) = 0;
     virtual void end(int kind, hipStream_t s) = 0;

@@ -75,6 +75,7 @@ struct spslam_ctx {
     // device buffers
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;
+    uint8_t* d_score = nullptr;
     OrbBuffers b{};
     uint8_t* d_in = nullptr;
     spslam_keypoint* d_kps = nullptr;
@@ -161,7 +162,7 @@ const char* build_geom(spslam_ctx* c) {
     std::memset(&g, 0, sizeof g);
     g.nlevels = c->p.nlevels;
     long long pyr = 0, blur = 0;
-    int cells = 0, kpb = 0, keyb = 0, tiles = 0;
+    int cells = 0, kpb = 0, keyb = 0;
     for (int l = 0; l < g.nlevels; l++) {
         LevelGeom& L = g.lv[l];
         L.w = cv_round((float)c->p.width * c->inv_scale[l]);
@@ -197,21 +198,26 @@ const char* build_geom(spslam_ctx* c) {
             pyr += (long long)L.w * L.h;
         }
         L.blur = reinterpret_cast<uint8_t*>(blur);
+        L.score = reinterpret_cast<uint8_t*>(blur);
         blur += (long long)L.w * L.h;
-        tiles += ((L.w + 63) / 64) * ((L.h + 15) / 16);
+        L.tiles_x = (L.w + kLevelTileW - 1) / kLevelTileW;
+        g.level_tiles[l] = L.tiles_x * ((L.h + kLevelTileH - 1) / kLevelTileH);
+        if (l > 0) {
+            L.rscale_x = 1. / ((double)L.w / g.lv[l - 1].w);
+            L.rscale_y = 1. / ((double)L.h / g.lv[l - 1].h);
+        }
     }
     c->pyr_frame_stride = (pyr + 255) / 256 * 256;
     c->blur_frame_stride = (blur + 255) / 256 * 256;
     g.cells_per_frame = cells;
     g.lvl_kp_per_frame = kpb;
     g.keys_per_frame = keyb;
-    g.blur_tiles_per_frame = tiles;
     c->max_kp = kpb;
     return nullptr;
 }
 
 void free_all(spslam_ctx* c) {
-    void* ptrs[] = {c->d_pyr,    c->d_blur,   c->b.cand,          c->b.cand_cnt,     c->b.keys,
+    void* ptrs[] = {c->d_pyr,    c->d_blur,   c->d_score,         c->b.cand,          c->b.cand_cnt,     c->b.keys,
                     c->b.keynode, c->b.lvl_kp, c->b.lvl_cnt,       c->d_in,           c->d_kps,
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1};
@@ -272,6 +278,7 @@ int spslam_create(int device, const spslam_orb_params* params, spslam_ctx** out)
     const OrbGeom& g = c->geom;
     hip_ok(hipMalloc(&c->d_pyr, B * c->pyr_frame_stride), "alloc pyramid");
     hip_ok(hipMalloc(&c->d_blur, B * c->blur_frame_stride), "alloc blur");
+    hip_ok(hipMalloc(&c->d_score, B * c->blur_frame_stride), "alloc FAST scores");
     hip_ok(hipMalloc(&c->b.cand, B * g.cells_per_frame * kCellCap * sizeof(uint32_t)), "alloc cand");
     hip_ok(hipMalloc(&c->b.cand_cnt, B * g.cells_per_frame * sizeof(uint16_t)), "alloc cand_cnt");
     hip_ok(hipMalloc(&c->b.keys, B * g.keys_per_frame * sizeof(uint32_t)), "alloc keys");
@@ -297,6 +304,7 @@ int spslam_create(int device, const spslam_orb_params* params, spslam_ctx** out)
             L.frame_stride = c->pyr_frame_stride;
         }
         L.blur = c->d_blur + reinterpret_cast<long long>(L.blur);
+        L.score = c->d_score + reinterpret_cast<long long>(L.score);
         L.blur_frame_stride = c->blur_frame_stride;
     }
     *out = c;

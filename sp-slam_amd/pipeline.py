@@ -12,7 +12,8 @@ The correspondences PoseOptimization consumes come from ORBmatcher /
 Map::AssociatePlanesByBoundary in the reference (outside this path,
 SURVEY.md 8(f)); here they are synthesized once per frame from the scene
 ground truth and the frame's own keypoints (synth.pose_problem) and kept in
-HBM.  All launches go to one HIP stream; nothing returns to the host inside
+HBM.  ORB and plane extraction run on two HIP streams (independent inputs),
+joined before PoseOptimization; nothing returns to the host inside
 a step.
 """
 from __future__ import annotations
@@ -58,8 +59,15 @@ class HotPath:
         self.d_pcnt = torch.zeros(B, dtype=torch.int32, device=dev)
         self.d_inl = torch.zeros(B * pe.inlier_cap, dtype=torch.int32, device=dev)
         self.d_con = torch.zeros(B * pe.contour_cap, dtype=torch.int32, device=dev)
+        # --- streams: ORB on the main stream, plane extraction beside it (independent inputs);
+        #     PoseOptimization joins both
+        self.main = torch.cuda.current_stream()
+        self.side = torch.cuda.Stream()
+        self.stream = self.main.cuda_stream
+        self.side_stream = self.side.cuda_stream
+        self.ev_fork = torch.cuda.Event()
+        self.ev_join = torch.cuda.Event()
         # --- pose problems: run one ORB pass to get each unique frame's keypoints
-        self.stream = torch.cuda.current_stream().cuda_stream
         self.orb()
         torch.cuda.synchronize()
         kps = self.d_kps.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(B, cap)
@@ -106,10 +114,10 @@ class HotPath:
         self.ex.extract_batch_device(self.d_gray.data_ptr(), self.B, self.W * self.H, self.W, self.d_kps.data_ptr(),
                                      self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, self.stream)
 
-    def planes(self):
+    def planes(self, stream=None):
         self.pe.extract_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
                                      self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_inl.data_ptr(),
-                                     self.d_con.data_ptr(), self.stream)
+                                     self.d_con.data_ptr(), self.stream if stream is None else stream)
 
     def pose(self):
         A, Bp = self.dA, self.dB
@@ -121,8 +129,13 @@ class HotPath:
                                      init_from_ptr=self.d_res1.data_ptr(), stream=self.stream)
 
     def step(self):
+        # planes of step k may start once step k-1 is done with the plane buffers
+        self.ev_fork.record(self.main)
+        self.side.wait_event(self.ev_fork)
+        self.planes(self.side_stream)
         self.orb()
-        self.planes()
+        self.ev_join.record(self.side)
+        self.main.wait_event(self.ev_join)
         self.pose()
 
     def results(self):

@@ -97,5 +97,5 @@ def test_fails_loudly_without_gpu():
         spslam_gpu.OrbExtractor()
     lib = spslam_gpu.load_library()
     lib.spslam_kernel_name.restype = ctypes.c_char_p
-    assert lib.spslam_kernel_name(0) == b"resize_level_kernel"
+    assert lib.spslam_kernel_name(0) == b"level_kernel"
     assert np.dtype(spslam_gpu.KEYPOINT_DTYPE).itemsize == 28
