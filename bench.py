@@ -3,8 +3,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c5]
 
-A "step" is one pass of the hot path -- ORB extraction, plane extraction and
-two chained PoseOptimizations (motion model, then local map) -- over one
+A "step" is one pass of the hot path -- ORB extraction, plane extraction,
+supposed planes from plane boundaries and two chained PoseOptimizations (motion model, then local map) -- over one
 batch of B synthetic RGB-D frames already resident in HBM (sp-slam_amd/
 pipeline.py).  One process per GPU; for N > 1 launch through
 torch.distributed.run: every rank runs its own independent sequence (the path
@@ -32,10 +32,12 @@ CONFIGS = {
     # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, ORB + planes + PoseOptimization
     "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=3,
                workload="C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud "
-                        "plane extraction + 2x PoseOptimization (point+plane+parallel+perpendicular edges), no LBA"),
+                        "plane extraction + supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), "
+                        "no LBA"),
     # configs[4]: 1280x960, nFeatures=4000, dense-plane scene
     "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8,
-               workload="C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + 2x PoseOptimization"),
+               workload="C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + supposed planes + "
+                        "2x PoseOptimization"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -53,7 +55,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return out
 
 
-def algorithmic_bytes(cfg, n_kp, n_pts, n_pls):
+def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -72,6 +74,8 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls):
         "plane_integral_kernel": 12 * N + 48 * IWH,           # xyz in, 6 fp64 integral images out
         "plane_normal_kernel": 16 * N + 48 * IWH + 16 * N,    # xyz+dist, integral, normal+plane_d out
         "plane_segment_kernel": 28 * N + 4 * N,               # xyz+normal+plane_d in, labels out
+        "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
+        "supp_assemble_kernel": n_sup * (64 + 2601 * 12),     # appended planes + synthetic patches out
     }
 
 
@@ -96,6 +100,7 @@ def cpu_baseline(hp, budget_s=12.0):
     import numpy as np
     import oracle_ctypes
     import oracle_planes
+    import oracle_supposed
     orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     po = oracle_planes.PlaneOracle()
     n = 0
@@ -105,7 +110,8 @@ def cpu_baseline(hp, budget_s=12.0):
     while time.perf_counter() - t0 < budget_s:
         i = n % U
         orb.extract(hp.frames[i][1], cap=20000)
-        po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
+        r = po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
+        oracle_supposed.generate(depth_f[i], po.cloud(), r["coef"], r["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
         pa, pts, pls, _ = hp.probA[i]
         r1, _, _ = oracle_ctypes.pose_optimize(pa, pts, pls)
         pb, pts2, pls2, _ = hp.probB[i]
@@ -116,7 +122,7 @@ def cpu_baseline(hp, budget_s=12.0):
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"2x PoseOptimization), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + 2x PoseOptimization), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -168,7 +174,10 @@ def main():
     dom, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
     n_pts = (hp.dA["n_points"] + hp.dB["n_points"]) / args.batch
     n_pls = (hp.dA["n_planes"] + hp.dB["n_planes"]) / args.batch
-    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls)
+    n_con = float(res["contour_points"].mean())
+    n_sup = float(res["supposed_counts"].mean())
+    n_brd = float(res["line_points"].mean())
+    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step
@@ -197,6 +206,7 @@ def main():
         "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": args.batch,
                    "parallelism": f"shard{world}", "mean_keypoints": hp.mean_keypoints,
                    "mean_planes": float(res["plane_counts"].mean()),
+                   "mean_supposed_planes": n_sup,
                    "pose_edges_per_frame": n_pts + n_pls},
         "kernels_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in sorted(times.items())},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -204,6 +204,11 @@ typedef struct spslam_plane_params {
     float distance_threshold; /* Plane.DistanceThreshold (0.05) */
     float fx, fy, cx, cy;     /* static Frame::fx, fy, cx, cy */
     int width, height;        /* depth image size */
+    /* GeneratePlanesFromBoundries (src/Frame.cc:938-998) */
+    double line_ratio;             /* Line.Ratio (0.2) */
+    float line_distance_threshold; /* Line.DistanceThreshold (0.01) */
+    float image_bounds[4];         /* Frame::mnMinX, mnMaxX, mnMinY, mnMaxY; all 0 -> 0, width, 0, height
+                                      (Frame::ComputeImageBounds without distortion, src/Frame.cc:557-563) */
 } spslam_plane_params;
 
 typedef struct spslam_plane {
@@ -233,6 +238,74 @@ int spslam_planes_extract(spslam_ctx* ctx, const float* depth, int w, int h, int
 int spslam_planes_extract_batch_device(spslam_ctx* ctx, const float* d_depth, int n_frames, size_t frame_stride,
                                        int stride_floats, spslam_plane* d_planes, int* d_counts,
                                        int32_t* d_inliers, int32_t* d_contours, void* hip_stream);
+
+/* ------------------------------------------------------------------------
+ * Supposed planes: Frame::GeneratePlanesFromBoundries (include/Frame.h:121,
+ * src/Frame.cc:938-1144), run by the RGB-D Frame constructor right after
+ * ComputePlanesFromOrganizedPointCloud (src/Frame.cc:186-194).  For each
+ * plane boundary (last to first) up to 4 lines are fitted with PCL's
+ * SACSegmentation (LINE, RANSAC, 1000 iterations, Line.DistanceThreshold,
+ * optimized coefficients); a line that keeps >= Line.Ratio of the boundary,
+ * lies >= 50 px inside the image (LineInRange) and runs along a depth border
+ * (IsBorderLine) yields the plane through the line perpendicular to the source
+ * plane (CaculatePlanes), appended when PlaneNotSeen.  Each appended plane
+ * carries: its coefficients, the line, the source plane index, its line
+ * points (organized-cloud indices; the new plane's mvBoundaryPoints and the
+ * tail of its mvPlanePoints) and its synthetic patch (n_patch xyz points, the
+ * head of its mvPlanePoints).  A source plane whose boundary was empty gets
+ * mvBoundaryPoints = every 20th of its inliers (GenerateBoundaryPoints,
+ * src/Frame.cc:1001-1011) -- an output-formatting step the caller's shim does
+ * from the inlier list; it produces no lines. */
+typedef struct spslam_supposed_plane {
+    float coef[4];            /* appended mvPlaneCoefficients entry (d >= 0) */
+    float line[6];            /* SACMODEL_LINE coefficients: point + unit direction */
+    int32_t source_plane;     /* index i of the plane whose boundary gave the line */
+    int32_t n_line;           /* line points */
+    int32_t line_offset;      /* into the frame's line index buffer */
+    int32_t n_patch;          /* synthetic patch points */
+    int32_t patch_offset;     /* into the frame's patch buffer, in points (3 floats each) */
+    int32_t pad;
+} spslam_supposed_plane;
+
+/* Per-frame capacities: appended planes, line indices, patch points per plane. */
+int spslam_supposed_capacity(const spslam_ctx* ctx, int* supp_cap, int* line_cap, int* patch_points);
+
+/* Drop-in for one frame on host buffers: runs on the planes of the last
+ * spslam_planes_extract call of this context (the reference calls both on the
+ * same Frame).  depth as passed to spslam_planes_extract.  *n receives the
+ * number of appended planes; line_idx (line_cap ints) and patch_xyz
+ * (supp_cap * patch_points * 3 floats) the data referenced by out[]. */
+int spslam_planes_generate_from_boundaries(spslam_ctx* ctx, const float* depth, int w, int h, int stride_floats,
+                                           spslam_supposed_plane* out, int cap, int* n, int32_t* line_idx,
+                                           float* patch_xyz);
+
+/* Batched, device resident: must follow spslam_planes_extract_batch_device
+ * on the same frames (it reads that call's organized clouds) and takes its
+ * outputs.  Per frame f: out_counts[f] appended planes at d_out + f*supp_cap,
+ * line indices at d_line_idx + f*line_cap, patches at
+ * d_patch + f*supp_cap*patch_points*3.  Counts beyond supp_cap are reported
+ * but not stored. */
+int spslam_planes_generate_from_boundaries_batch_device(spslam_ctx* ctx, const float* d_depth, int n_frames,
+                                                        size_t frame_stride, int stride_floats,
+                                                        const spslam_plane* d_planes, const int* d_counts,
+                                                        const int32_t* d_contours, spslam_supposed_plane* d_out,
+                                                        int* d_out_counts, int32_t* d_line_idx, float* d_patch,
+                                                        void* hip_stream);
+
+/* Parity access: the line candidates fitted on boundary `plane` of frame
+ * `frame` in the last call, in fit order (<= 4; the last may be the failing
+ * one).  Per candidate: line[6], inlier count, RANSAC trials, flags (1 kept
+ * >= Line.Ratio, 2 LineInRange, 4 IsBorderLine), offset of its points in idx
+ * (organized-cloud indices, only for flag-1 candidates). */
+typedef struct spslam_line_candidate {
+    float line[6];
+    int32_t n_inliers;
+    int32_t iterations;
+    int32_t flags;
+    int32_t idx_offset;
+} spslam_line_candidate;
+int spslam_supposed_debug(spslam_ctx* ctx, int frame, int plane, spslam_line_candidate* cand, int* n_cand,
+                          int32_t* idx, int idx_cap);
 
 /* Stage access for parity tests, frame `frame` of the last batch:
  * what 0 = organized cloud (3*N floats, x,y,z per point), 1 = normals

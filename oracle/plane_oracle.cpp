@@ -418,11 +418,13 @@ void extract(const float* depth, int w, int h, int stride_floats, const Params& 
     }
     R.labels_ref = lab;
 
-    // --- boundaries (findLabeledRegionBoundary from the first inlier)
+    // --- boundaries: segmentAndRefine traces findLabeledRegionBoundary from
+    // inlier_indices[i].indices[max_inlier_idx], the model's LAST inlier (its
+    // last grow event, else its last component member in raster order)
     std::vector<std::vector<int>> contours(models.size());
     const int ddx[8] = {-1, -1, 0, 1, 1, 1, 0, -1}, ddy[8] = {0, -1, -1, -1, 0, 1, 1, 1};
     for (size_t i = 0; i < models.size(); i++) {
-        const int start = inl[i][0];
+        const int start = inl[i].back();
         int cur = start, cx = start % W, cy = start / W;
         const uint32_t label = lab[start];
         int dir = -1;
@@ -462,8 +464,8 @@ void extract(const float* depth, int w, int h, int stride_floats, const Params& 
         for (const auto& pm : R.coef) {
             const float d = pm[3] - cf[3];
             const float angle = pm[0] * cf[0] + pm[1] * cf[1] + pm[2] * cf[2];
-            if (d > 0.2f || d < -0.2f) continue;
-            if (angle < 0.9397f && angle > -0.9397f) continue;
+            if ((double)d > 0.2 || (double)d < -0.2) continue;
+            if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
             seen = true;
             break;
         }

@@ -789,7 +789,8 @@ const char* kernel_kind_name(int kind) {
     static const char* names[kNumKernelKinds] = {"level_kernel", "fast_cells_kernel", "octree_kernel",
                                                  "desc_kernel", "pose_kernel", "plane_cloud_kernel", "plane_distance_kernel",
                                                  "plane_integral_kernel", "plane_normal_kernel",
-                                                 "plane_segment_kernel"};
+                                                 "plane_segment_kernel", "supp_lines_kernel",
+                                                 "supp_assemble_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

@@ -57,6 +57,7 @@ struct SegShared {
     int nkept;
     int kept[kMaxPlanesPerFrame];
     int con_len[kMaxPlanesPerFrame];
+    int con_start[kMaxPlanesPerFrame];
     alignas(16) float stage[kSegWaves][9][64];   // covariance terms of one 64-pixel chunk, per wave
 };
 
@@ -963,8 +964,8 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 const spslam_plane& pm = planes[q];
                 const float d = pm.coef[3] - cf[3];
                 const float angle = pm.coef[0] * cf[0] + pm.coef[1] * cf[1] + pm.coef[2] * cf[2];
-                if (d > 0.2f || d < -0.2f) continue;
-                if (angle < 0.9397f && angle > -0.9397f) continue;
+                if ((double)d > 0.2 || (double)d < -0.2) continue;
+                if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
                 seen = true;
             }
             if (seen || nk >= planes_cap) continue;
@@ -994,6 +995,18 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         const int m = S.kept[q], j = S.model_big[m], n = S.big_size[j], o = S.big_off[j];
         const int dst = planes[q].inlier_offset, lim = planes[q].n_inliers;
         for (int k = lane; k < min(n, lim); k += 64) inl[dst + k] = members[o + k];
+        // contour start = the model's last inlier (segmentAndRefine's max_inlier_idx):
+        // its last grow event, else its last component member
+        int last = -1;
+        for (int e1 = ng; e1 > 0; e1 -= 64) {
+            const int e = e1 - 64 + lane;
+            const uint64_t mk = __ballot(e >= 0 && (ev[e] >> 24) == m);
+            if (mk) {
+                last = ev[e1 - 64 + (63 - __clzll(mk))] & 0xFFFFFF;
+                break;
+            }
+        }
+        if (lane == 0) S.con_start[q] = last >= 0 ? last : members[o + n - 1];
         int w = n;
         for (int e0 = 0; e0 < ng; e0 += 64) {
             const int e = e0 + lane;
@@ -1007,11 +1020,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     }
     block_sync();
     STAMP(4);
-    // ---- N: contours (findLabeledRegionBoundary from the component's first pixel, on refined labels)
+    // ---- N: contours (findLabeledRegionBoundary from the model's last inlier, on refined labels)
     for (int q = wave; q < nk; q += kSegWaves)
         if (lane == 0) {
             const int m = S.kept[q];
-            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.big_root[S.model_big[m]], m + 1, nullptr, 0);
+            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, nullptr, 0);
         }
     __syncthreads();
     if (t == 0) {
@@ -1026,7 +1039,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     for (int q = wave; q < nk; q += kSegWaves)
         if (lane == 0) {
             const int m = S.kept[q];
-            trace_contour(state, nmask, W, H, N, S.big_root[S.model_big[m]], m + 1, con + planes[q].contour_offset,
+            trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, con + planes[q].contour_offset,
                           planes[q].n_contour);
         }
     STAMP(9);

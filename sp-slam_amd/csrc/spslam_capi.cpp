@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -18,6 +19,7 @@
 #include "orb_launch.h"
 #include "plane_launch.h"
 #include "pose_launch.h"
+#include "supposed_launch.h"
 
 using namespace spslam;
 
@@ -100,6 +102,15 @@ struct spslam_ctx {
     int32_t* d_inl1 = nullptr;
     int32_t* d_con1 = nullptr;
     int plane_last_frames = 0;
+    // supposed-plane stage (GeneratePlanesFromBoundries)
+    SuppParams sp{};
+    SuppBuffers sb{};
+    void* d_supp_scratch = nullptr;
+    spslam_supposed_plane* d_supp1 = nullptr;
+    int* d_supp_cnt1 = nullptr;
+    int32_t* d_line1 = nullptr;
+    float* d_patch1 = nullptr;
+    int supp_last_frames = 0;
 };
 
 namespace {
@@ -220,7 +231,8 @@ void free_all(spslam_ctx* c) {
     void* ptrs[] = {c->d_pyr,    c->d_blur,   c->d_score,         c->b.cand,          c->b.cand_cnt,     c->b.keys,
                     c->b.keynode, c->b.lvl_kp, c->b.lvl_cnt,       c->d_in,           c->d_kps,
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
-                    c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1};
+                    c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
+                    c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -450,6 +462,74 @@ int spslam_pose_optimize(spslam_ctx* c, const spslam_pose_problem* problem, cons
     return SPSLAM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// GeneratePlanesFromBoundries constants and scratch (supposed_kernels.hip).
+hipError_t configure_supposed(spslam_ctx* c, const spslam_plane_params* p) {
+    const PlaneGeom& g = c->pg;
+    SuppParams& sp = c->sp;
+    sp.line_ratio = p->line_ratio;
+    // (double)s < (double)th * th  <=>  s <= sqr_th_f
+    const double T = (double)p->line_distance_threshold * (double)p->line_distance_threshold;
+    float f = (float)T;
+    while ((double)f >= T && f > 0.f) f = std::nextafter(f, 0.f);
+    while ((double)std::nextafter(f, 1.f) < T) f = std::nextafter(f, 1.f);
+    sp.sqr_th_f = f;
+    const bool nob = p->image_bounds[0] == 0.f && p->image_bounds[1] == 0.f && p->image_bounds[2] == 0.f &&
+                     p->image_bounds[3] == 0.f;
+    sp.min_x = nob ? 0.f : p->image_bounds[0];
+    sp.max_x = nob ? (float)p->width : p->image_bounds[1];
+    sp.min_y = nob ? 0.f : p->image_bounds[2];
+    sp.max_y = nob ? (float)p->height : p->image_bounds[3];
+    sp.supp_cap = kMaxSuppPerFrame;
+    sp.line_cap = g.contour_cap;
+    // CaculatePlanes' loop: for (float i = -0.25; i < 0.25;) { ...; i = i + 0.01; } (double step)
+    int ns = 0;
+    for (float v = -0.25f; v < 0.25f; v = (float)((double)v + 0.01)) {
+        if (ns >= kMaxPatchSteps) return hipErrorInvalidValue;
+        sp.steps[ns++] = v;
+    }
+    sp.n_steps = ns;
+    const size_t F = (size_t)c->p.max_batch, CC = (size_t)g.contour_cap;
+    SuppBuffers& b = c->sb;
+    const size_t bytes = (size_t)kSuppRndTable * 4 +
+                         F * kMaxPlanesPerFrame * kMaxLinesPerBoundary * sizeof(LineCand) +
+                         F * kMaxPlanesPerFrame * sizeof(int) + F * CC * (4 + 16 + 4 + 1) + 8 * 256;
+    if (c->d_supp_scratch) (void)hipFree(c->d_supp_scratch);
+    c->d_supp_scratch = nullptr;
+    hipError_t e = hipMalloc(&c->d_supp_scratch, bytes);
+    if (e != hipSuccess) return e;
+    uint8_t* q = (uint8_t*)c->d_supp_scratch;
+    auto carve = [&](size_t n) { uint8_t* r = q; q += (n + 255) / 256 * 256; return r; };
+    b.rnd = (const uint32_t*)carve((size_t)kSuppRndTable * 4);
+    b.cand = (LineCand*)carve(F * kMaxPlanesPerFrame * kMaxLinesPerBoundary * sizeof(LineCand));
+    b.n_cand = (int*)carve(F * kMaxPlanesPerFrame * sizeof(int));
+    b.line_idx = (int32_t*)carve(F * CC * 4);
+    b.big = (float4*)carve(F * CC * 16);
+    b.big_sh = (int*)carve(F * CC * 4);
+    b.big_flag = (uint8_t*)carve(F * CC);
+    // every SACSegmentation::segment() seeds boost::mt19937(12345u); rnd() = uniform_int<>(0, INT_MAX) = mt() >> 1
+    std::vector<uint32_t> tab(kSuppRndTable);
+    std::mt19937 mt(12345u);
+    for (auto& v : tab) v = (uint32_t)mt() >> 1;
+    e = hipMemcpy((void*)b.rnd, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return e;
+    void* olds[] = {c->d_supp1, c->d_supp_cnt1, c->d_line1, c->d_patch1};
+    for (void* o : olds)
+        if (o) (void)hipFree(o);
+    const size_t patch = (size_t)sp.n_steps * sp.n_steps;
+    if ((e = hipMalloc(&c->d_supp1, sp.supp_cap * sizeof(spslam_supposed_plane))) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_supp_cnt1, 16)) != hipSuccess) return e;
+    if ((e = hipMalloc(&c->d_line1, CC * 4)) != hipSuccess) return e;
+    return hipMalloc(&c->d_patch1, sp.supp_cap * patch * 12);
+}
+
+}  // namespace
+
+extern "C" {
+
 int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     if (!c || !p) return SPSLAM_ERR_ARG;
     if (p->cloud_dis < 1 || p->width < 1 || p->height < 1 || p->fx == 0.f || p->fy == 0.f)
@@ -501,6 +581,7 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     HIP_CHECK(c, hipMalloc(&c->d_plane_cnt1, 16));
     HIP_CHECK(c, hipMalloc(&c->d_inl1, (size_t)g.inlier_cap * 4));
     HIP_CHECK(c, hipMalloc(&c->d_con1, (size_t)g.contour_cap * 4));
+    HIP_CHECK(c, configure_supposed(c, p));
     c->planes_ready = true;
     return SPSLAM_OK;
 }
@@ -557,6 +638,104 @@ int spslam_planes_extract(spslam_ctx* c, const float* depth, int w, int h, int s
     if (inliers && ni) HIP_CHECK(c, hipMemcpy(inliers, c->d_inl1, (size_t)ni * 4, hipMemcpyDeviceToHost));
     if (contours && nc) HIP_CHECK(c, hipMemcpy(contours, c->d_con1, (size_t)nc * 4, hipMemcpyDeviceToHost));
     return SPSLAM_OK;
+}
+
+int spslam_supposed_capacity(const spslam_ctx* c, int* supp_cap, int* line_cap, int* patch_points) {
+    if (!c || !c->planes_ready) return SPSLAM_ERR_NOT_READY;
+    if (supp_cap) *supp_cap = c->sp.supp_cap;
+    if (line_cap) *line_cap = c->sp.line_cap;
+    if (patch_points) *patch_points = c->sp.n_steps * c->sp.n_steps;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_generate_from_boundaries_batch_device(spslam_ctx* c, const float* d_depth, int n_frames,
+                                                        size_t frame_stride, int stride_floats,
+                                                        const spslam_plane* d_planes, const int* d_counts,
+                                                        const int32_t* d_contours, spslam_supposed_plane* d_out,
+                                                        int* d_out_counts, int32_t* d_line_idx, float* d_patch,
+                                                        void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
+    if (!d_depth || !d_planes || !d_counts || !d_contours || !d_out || !d_out_counts || !d_line_idx || !d_patch ||
+        n_frames < 1 || stride_floats < c->pg.w)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_generate_from_boundaries_batch_device");
+    if (n_frames > c->plane_last_frames)
+        return fail(c, SPSLAM_ERR_NOT_READY, "%s", "more frames than the last plane extraction holds");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIP_CHECK(c, supp_launch(c->pg, c->pb, c->sp, c->sb, n_frames, d_depth, (long long)frame_stride, stride_floats,
+                             d_planes, d_counts, d_contours, d_out, d_out_counts, d_line_idx, d_patch, s, c->timer));
+    c->supp_last_frames = n_frames;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_generate_from_boundaries(spslam_ctx* c, const float* depth, int w, int h, int stride_floats,
+                                           spslam_supposed_plane* out, int cap, int* n, int32_t* line_idx,
+                                           float* patch_xyz) {
+    if (!c || !n) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
+    if (!depth || w != c->pg.w || h != c->pg.h || stride_floats < w)
+        return fail(c, SPSLAM_ERR_ARG, "depth size does not match the plane configuration%s", "");
+    if (c->plane_last_frames < 1) return fail(c, SPSLAM_ERR_NOT_READY, "%s", "spslam_planes_extract not called");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipMemcpy2DAsync(c->d_depth_in, (size_t)w * 4, depth, (size_t)stride_floats * 4, (size_t)w * 4, h,
+                                  hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_planes_generate_from_boundaries_batch_device(c, c->d_depth_in, 1, (size_t)w * h, w, c->d_planes1,
+                                                                 c->d_plane_cnt1, c->d_con1, c->d_supp1,
+                                                                 c->d_supp_cnt1, c->d_line1, c->d_patch1, c->stream);
+    if (rc) return rc;
+    int m = 0;
+    std::vector<spslam_supposed_plane> tmp(c->sp.supp_cap);
+    HIP_CHECK(c, hipMemcpyAsync(&m, c->d_supp_cnt1, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(tmp.data(), c->d_supp1, tmp.size() * sizeof(spslam_supposed_plane),
+                                hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    *n = m;
+    const int stored = std::min(m, c->sp.supp_cap);
+    if (m > cap || m > c->sp.supp_cap) return fail(c, SPSLAM_ERR_CAPACITY, "supposed-plane buffer too small%s", "");
+    int nl = 0;
+    for (int k = 0; k < stored; k++) {
+        out[k] = tmp[k];
+        nl = std::max(nl, tmp[k].line_offset + tmp[k].n_line);
+    }
+    const size_t patch = (size_t)c->sp.n_steps * c->sp.n_steps;
+    if (line_idx && nl) HIP_CHECK(c, hipMemcpy(line_idx, c->d_line1, (size_t)nl * 4, hipMemcpyDeviceToHost));
+    if (patch_xyz && stored)
+        HIP_CHECK(c, hipMemcpy(patch_xyz, c->d_patch1, stored * patch * 12, hipMemcpyDeviceToHost));
+    return SPSLAM_OK;
+}
+
+int spslam_supposed_debug(spslam_ctx* c, int frame, int plane, spslam_line_candidate* cand, int* n_cand,
+                          int32_t* idx, int idx_cap) {
+    static_assert(sizeof(spslam_line_candidate) == sizeof(LineCand), "candidate layout");
+    if (!c || !cand || !n_cand) return SPSLAM_ERR_ARG;
+    if (frame < 0 || frame >= c->supp_last_frames || plane < 0 || plane >= kMaxPlanesPerFrame)
+        return fail(c, SPSLAM_ERR_NOT_READY, "no supposed-plane data for that frame%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipDeviceSynchronize());
+    int nc = 0;
+    HIP_CHECK(c, hipMemcpy(&nc, c->sb.n_cand + frame * kMaxPlanesPerFrame + plane, sizeof(int), hipMemcpyDeviceToHost));
+    nc = std::min(std::max(nc, 0), kMaxLinesPerBoundary);
+    LineCand lc[kMaxLinesPerBoundary];
+    if (nc)
+        HIP_CHECK(c, hipMemcpy(lc, c->sb.cand + ((size_t)frame * kMaxPlanesPerFrame + plane) * kMaxLinesPerBoundary,
+                               nc * sizeof(LineCand), hipMemcpyDeviceToHost));
+    *n_cand = nc;
+    int lo = 0;
+    for (int k = 0; k < nc; k++) {
+        std::memcpy(&cand[k], &lc[k], sizeof(LineCand));
+        if (lc[k].flags & 1) {
+            const int m = lc[k].n_inliers;
+            if (idx && lo + m <= idx_cap && m)
+                HIP_CHECK(c, hipMemcpy(idx + lo, c->sb.line_idx + (size_t)frame * c->pg.contour_cap + lc[k].idx_off,
+                                       (size_t)m * 4, hipMemcpyDeviceToHost));
+            cand[k].idx_offset = lo;
+            lo += m;
+        } else {
+            cand[k].idx_offset = -1;
+        }
+    }
+    return lo > idx_cap ? SPSLAM_ERR_CAPACITY : SPSLAM_OK;
 }
 
 int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_points) {

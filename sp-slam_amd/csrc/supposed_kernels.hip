@@ -1,0 +1,560 @@
+// Supposed planes from plane boundaries on gfx950:
+// Frame::GeneratePlanesFromBoundries (src/Frame.cc:938-998) with its helpers
+// IsBorderLine / IsBorderPoint / LineInRange / CaculatePlanes / PlaneNotSeen
+// (:1013-1144) and the PCL 1.8.0 SACSegmentation LINE + RANSAC + optimize it
+// calls (semantics: oracle/supposed_oracle.cpp).
+//
+// supp_lines_kernel: one 256-thread workgroup per (frame, boundary).  The
+// boundary's points live in LDS (float4, w = organized-cloud index).  Each
+// segment() call restarts boost::mt19937(12345), so its draws are a fixed
+// sequence, precomputed once per context (kSuppRndTable entries cover the
+// worst case).  RANSAC is run speculatively in rounds of kBatch trials:
+//   - wave 0 replays the sampler (drawIndexSample's partial Fisher-Yates on
+//     the persistent shuffled_indices_, isSampleGood retries); the 64 lanes
+//     fetch and reduce 32 draw pairs at a time, the swap chain is uniform;
+//   - all waves count each trial's inliers (wave per trial, lanes over points);
+//   - one lane replays computeModel's best/k bookkeeping in trial order and
+//     stops exactly where the reference loop stops; trials sampled beyond that
+//     point are discarded (the RNG is discarded by the reference too).
+// Then selectWithinDistance, optimizeModelCoefficients (sequential float
+// centroid / covariance sums, one lane per accumulator, glibc-exact eigen
+// solve), the Line.Ratio test, LineInRange, IsBorderLine (thread per line
+// point) and the order-preserving removal of the line's points.
+//
+// supp_assemble_kernel: one wave per frame; boundaries last to first, the
+// fitted lines in order: CaculatePlanes + PlaneNotSeen against the growing
+// plane list (serial, as in the reference), then the synthetic patches and
+// line point lists are written by all lanes.
+#include <cfloat>
+
+#include "libm_restated.h"
+#include "supposed_launch.h"
+
+namespace spslam {
+namespace supp {
+
+constexpr int kThreads = 256, kWaves = 4;
+constexpr int kBatch = 64;       // RANSAC trials per speculative round
+constexpr int kLdsPts = 2048;    // boundaries up to this size are held in LDS
+constexpr int kMaxTrials = 1001; // RandomSampleConsensus: ++iterations_ > max_iterations_ (1000) -> stop
+
+struct Shared {
+    int s0[kBatch], s1[kBatch], cnt[kBatch];
+    int nb, fail, done, have;
+    int iterations, best, best_s0, best_s1;
+    double k;
+    float line[6];
+    float acc[9];
+    int red[kWaves];
+    int n_inl, flags;
+};
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ int block_sum(int v, Shared& S) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_sum(v);
+    __syncthreads();
+    if (lane == 0) S.red[wave] = v;
+    __syncthreads();
+    int s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) s += S.red[w];
+    return s;
+}
+
+// computeModelCoefficients + tail<3>().normalize() (3-element, unvectorised).
+__device__ __forceinline__ void line_from_samples(const float4 a, const float4 b, float* c) {
+    c[0] = a.x; c[1] = a.y; c[2] = a.z;
+    float d0 = b.x - a.x, d1 = b.y - a.y, d2 = b.z - a.z;
+    const float sq = d0 * d0 + d1 * d1 + d2 * d2;
+    if (sq > 0.f) {
+        const float s = sqrtf(sq);
+        d0 /= s; d1 /= s; d2 /= s;
+    }
+    c[3] = d0; c[4] = d1; c[5] = d2;
+}
+// Vector4f line_dir.normalize() (SSE lane order, w = 0).
+__device__ __forceinline__ void normalize4(float* d) {
+    const float sq = (d[0] * d[0] + d[2] * d[2]) + (d[1] * d[1] + 0.f);
+    if (sq > 0.f) {
+        const float s = sqrtf(sq);
+        d[0] /= s; d[1] /= s; d[2] /= s;
+    }
+}
+// ((line_pt - p).cross3(line_dir)).squaredNorm() in Eigen's SSE order.
+__device__ __forceinline__ float line_sqd(const float* lp, const float* ld, const float4 p) {
+    const float ax = lp[0] - p.x, ay = lp[1] - p.y, az = lp[2] - p.z;
+    const float cx = ay * ld[2] - az * ld[1];
+    const float cy = az * ld[0] - ax * ld[2];
+    const float cz = ax * ld[1] - ay * ld[0];
+    return (cx * cx + cz * cz) + (cy * cy + 0.f);
+}
+
+// pcl::computeRoots on a scaled matrix (float), glibc-exact transcendental calls.
+__device__ void roots2(float b, float c, float* r) {
+    r[0] = 0.f;
+    float d = (float)(b * b - 4.0 * c);
+    if (d < 0.0) d = 0.0;
+    const float sd = sqrtf(d);
+    r[2] = 0.5f * (b + sd);
+    r[1] = 0.5f * (b - sd);
+}
+__device__ void roots3(const float (&m)[3][3], float* r) {
+    const float c0 = m[0][0] * m[1][1] * m[2][2] + 2.f * m[0][1] * m[0][2] * m[1][2] - m[0][0] * m[1][2] * m[1][2] -
+                     m[1][1] * m[0][2] * m[0][2] - m[2][2] * m[0][1] * m[0][1];
+    const float c1 = m[0][0] * m[1][1] - m[0][1] * m[0][1] + m[0][0] * m[2][2] - m[0][2] * m[0][2] +
+                     m[1][1] * m[2][2] - m[1][2] * m[1][2];
+    const float c2 = m[0][0] + m[1][1] + m[2][2];
+    if (fabsf(c0) < FLT_EPSILON) { roots2(c2, c1, r); return; }
+    const float s_inv3 = (float)(1.0 / 3.0), s_sqrt3 = sqrtf(3.0f);
+    const float c2_over_3 = c2 * s_inv3;
+    float a_over_3 = (c1 - c2 * c2_over_3) * s_inv3;
+    if (a_over_3 > 0.f) a_over_3 = 0.f;
+    const float half_b = 0.5f * (c0 + c2_over_3 * (2.f * c2_over_3 * c2_over_3 - c1));
+    float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
+    if (q > 0.f) q = 0.f;
+    const float rho = sqrtf(-a_over_3);
+    const float theta = libm::atan2f_(sqrtf(-q), half_b) * s_inv3;
+    float st, ct;
+    libm::sincosf_(theta, &st, &ct);
+    r[0] = c2_over_3 + 2.f * rho * ct;
+    r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
+    r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);
+    float t;
+    if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+    if (r[1] >= r[2]) {
+        t = r[1]; r[1] = r[2]; r[2] = t;
+        if (r[0] >= r[1]) { t = r[0]; r[0] = r[1]; r[1] = t; }
+    }
+    if (r[0] <= 0) roots2(c2, c1, r);
+}
+__device__ float max_abs3(const float (&m)[3][3]) {
+    float s = 0.f;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) s = fmaxf(s, fabsf(m[i][j]));
+    if (s <= FLT_MIN) s = 1.f;
+    return s;
+}
+// pcl::eigen33(cov, evals) + computeCorrespondingEigenVector(cov, evals[2]).
+__device__ void line_direction(const float (&cov)[3][3], float* evec) {
+    const float scale = max_abs3(cov);
+    float s[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) s[i][j] = cov[i][j] / scale;
+    float r[3];
+    roots3(s, r);
+    const float eval2 = r[2] * scale;
+    const float scale2 = max_abs3(cov);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) s[i][j] = cov[i][j] / scale2;
+    const float sub = eval2 / scale2;
+    for (int i = 0; i < 3; i++) s[i][i] -= sub;
+    const int pr[3][2] = {{0, 1}, {0, 2}, {1, 2}};
+    float v[3][3], len[3];
+    for (int k = 0; k < 3; k++) {
+        const float* a = s[pr[k][0]];
+        const float* b = s[pr[k][1]];
+        v[k][0] = a[1] * b[2] - a[2] * b[1];
+        v[k][1] = a[2] * b[0] - a[0] * b[2];
+        v[k][2] = a[0] * b[1] - a[1] * b[0];
+        len[k] = v[k][0] * v[k][0] + v[k][1] * v[k][1] + v[k][2] * v[k][2];
+    }
+    int k = 2;
+    if (len[0] >= len[1] && len[0] >= len[2]) k = 0;
+    else if (len[1] >= len[0] && len[1] >= len[2]) k = 1;
+    const float sl = sqrtf(len[k]);
+    for (int j = 0; j < 3; j++) evec[j] = v[k][j] / sl;
+}
+
+struct Cam { float fx, fy, cx, cy, min_x, max_x, min_y, max_y; int w, h, stride; };
+
+// Frame::IsBorderPoint (Frame.cc:1027-1057); window read through the flat
+// row-major index of the (continuous) depth image, reads outside the image
+// buffer count as invalid (<= 0.05) pixels -- see oracle/supposed_oracle.cpp.
+__device__ bool is_border_point(const float4 p, const float* __restrict__ depth, const Cam& K) {
+    if (p.z < 0.0f) return false;
+    const float invz = 1.0f / p.z;
+    const float u = fmaf(K.fx * p.x, invz, K.cx);
+    const float v = fmaf(K.fy * p.y, invz, K.cy);
+    if (isnan(u) || isnan(v)) return true;
+    if (!(fabsf(u) < 1e6f) || !(fabsf(v) < 1e6f)) return false;
+    const long long total = (long long)K.w * K.h;
+    int num = 0, nan = 0;
+    float res = 0.f;
+    for (int j = (int)(v - 10.f); (float)j < v + 10.f; ++j)
+        for (int i = (int)(u - 10.f); (float)i < u + 10.f; ++i) {
+            float d = 0.f;
+            if (i >= 0 && i < K.w && j >= 0 && j < K.h) {
+                d = depth[(long long)j * K.stride + i];
+            } else {
+                const long long fi = (long long)j * K.w + i;
+                if (fi >= 0 && fi < total) d = depth[(fi / K.w) * K.stride + fi % K.w];
+            }
+            if ((double)d > 0.05) {
+                res += d;
+                num++;
+            } else if (++nan > 100) {
+                return false;
+            }
+        }
+    if ((double)(p.z - res / (float)num) > 0.1) return false;
+    return true;
+}
+
+// Frame::LineInRange (Frame.cc:1059-1076).
+__device__ bool line_in_range(const float* pc, const Cam& K) {
+    if (pc[2] < 0.0f) return false;
+    const float invz = 1.0f / pc[2];
+    const float u = fmaf(K.fx * pc[0], invz, K.cx);
+    const float v = fmaf(K.fy * pc[1], invz, K.cy);
+    if (u < K.min_x + 50 || u > K.max_x - 50) return false;
+    if (v < K.min_y + 50 || v > K.max_y - 50) return false;
+    return true;
+}
+
+// selectWithinDistance(coef): flag[i] for the n current points; returns the count.
+__device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, int n, float thr, Shared& S) {
+    float lp[3] = {coef[0], coef[1], coef[2]}, ld[3] = {coef[3], coef[4], coef[5]};
+    normalize4(ld);
+    int c = 0;
+    for (int i = threadIdx.x; i < n; i += kThreads) {
+        const bool in = line_sqd(lp, ld, Q[i]) <= thr;
+        flag[i] = in;
+        c += in;
+    }
+    return block_sum(c, S);
+}
+
+__global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
+                                                              SuppBuffers sb, const float* __restrict__ depth,
+                                                              long long depth_fs, int depth_stride,
+                                                              const spslam_plane* __restrict__ planes,
+                                                              const int* __restrict__ plane_counts,
+                                                              const int32_t* __restrict__ contours) {
+    __shared__ float4 Qs[kLdsPts];
+    __shared__ int shs[kLdsPts];
+    __shared__ uint8_t flags_s[kLdsPts];
+    __shared__ Shared S;
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int np = min(plane_counts[f], kMaxPlanesPerFrame);
+    const spslam_plane* P = planes + (size_t)f * kMaxPlanesPerFrame;
+    const int32_t* con = contours + (size_t)f * g.contour_cap;
+    const float* X = pb.cloud + f * pb.cloud_fs;
+    const float* Y = X + g.N;
+    const float* Z = X + 2 * g.N;
+    const Cam K{g.fx, g.fy, g.cx, g.cy, sp.min_x, sp.max_x, sp.min_y, sp.max_y, g.w, g.h, depth_stride};
+    const float* D = depth + f * depth_fs;
+    const float thr = sp.sqr_th_f;
+    for (int q = blockIdx.y; q < np; q += gridDim.y) {
+        LineCand* C = sb.cand + ((size_t)f * kMaxPlanesPerFrame + q) * kMaxLinesPerBoundary;
+        const int bsize = P[q].n_contour, coff = P[q].contour_offset;
+        if (bsize < 50) {  // Frame.cc:951-955 (the 0-point case only fills mvBoundaryPoints)
+            if (t == 0) sb.n_cand[f * kMaxPlanesPerFrame + q] = 0;
+            continue;
+        }
+        const bool in_lds = bsize <= kLdsPts;
+        float4* Q = in_lds ? Qs : sb.big + (size_t)f * g.contour_cap + coff;
+        int* sh = in_lds ? shs : sb.big_sh + (size_t)f * g.contour_cap + coff;
+        uint8_t* flag = in_lds ? flags_s : sb.big_flag + (size_t)f * g.contour_cap + coff;
+        int32_t* lidx = sb.line_idx + (size_t)f * g.contour_cap + coff;
+        for (int i = t; i < bsize; i += kThreads) {
+            const int ci = con[coff + i];
+            Q[i] = make_float4(X[ci], Y[ci], Z[ci], __int_as_float(ci));
+        }
+        __syncthreads();
+        int n = bsize, used = 0, ncand = 0;
+        for (int j = 0; j < kMaxLinesPerBoundary; j++) {
+            // ---------------- RandomSampleConsensus::computeModel
+            if (t == 0) {
+                S.iterations = 0; S.best = -2147483647; S.k = 1.0; S.have = 0; S.done = n < 2;
+            }
+            for (int i = t; i < n; i += kThreads) sh[i] = i;
+            __syncthreads();
+            const double one_over_n = 1.0 / (double)n, log_prob = log(1.0 - 0.99);
+            int r0 = 0, r1 = 1;   // shuffled_indices_[0], [1] (kept in registers by wave 0)
+            uint32_t pos = 0;     // draws consumed
+            while (!S.done) {
+                if (wave == 0) {
+                    const int it0 = S.iterations;
+                    int nb = 0;
+                    bool fail = false;
+                    while (nb < kBatch && it0 + nb < kMaxTrials) {
+                        bool got = false;
+                        for (int chk = 0; chk < 1000 && !got;) {
+                            const uint32_t r = sb.rnd[pos + lane];
+                            const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
+                            int c = 0;
+                            while (c < 32 && chk + c < 1000) {
+                                const int j0 = __shfl((int)jv, 2 * c), j1 = __shfl((int)jv, 2 * c + 1);
+                                if (j0 == 1) { const int x = r0; r0 = r1; r1 = x; }
+                                else if (j0 > 1) { const int x = sh[j0]; sh[j0] = r0; r0 = x; }
+                                if (j1 > 1) { const int x = sh[j1]; sh[j1] = r1; r1 = x; }
+                                c++;
+                                const float4 a = Q[r0], b = Q[r1];
+                                if (a.x != b.x && a.y != b.y && a.z != b.z) { got = true; break; }
+                            }
+                            pos += 2 * c;
+                            chk += c;
+                        }
+                        if (!got) { fail = true; break; }
+                        if (lane == 0) { S.s0[nb] = r0; S.s1[nb] = r1; }
+                        nb++;
+                    }
+                    if (lane == 0) { S.nb = nb; S.fail = fail; }
+                }
+                __syncthreads();
+                const int nb = S.nb;
+                for (int c = wave; c < nb; c += kWaves) {
+                    float L[6];
+                    line_from_samples(Q[S.s0[c]], Q[S.s1[c]], L);
+                    float ld[3] = {L[3], L[4], L[5]};
+                    normalize4(ld);
+                    int cnt = 0;
+                    for (int i = lane; i < n; i += 64) cnt += line_sqd(L, ld, Q[i]) <= thr;
+                    cnt = wave_sum(cnt);
+                    if (lane == 0) S.cnt[c] = cnt;
+                }
+                __syncthreads();
+                if (t == 0) {
+                    int it = S.iterations;
+                    bool done = false;
+                    for (int c = 0; c < nb; c++) {
+                        if (!((double)it < S.k)) { done = true; break; }
+                        if (S.cnt[c] > S.best) {
+                            S.best = S.cnt[c]; S.best_s0 = S.s0[c]; S.best_s1 = S.s1[c]; S.have = 1;
+                            const double w = (double)S.best * one_over_n;
+                            double pno = 1.0 - w * w;
+                            pno = fmax(DBL_EPSILON, pno);
+                            pno = fmin(1.0 - DBL_EPSILON, pno);
+                            S.k = log_prob / log(pno);
+                        }
+                        if (++it > kMaxTrials - 1) { done = true; break; }
+                    }
+                    if (!done && (S.fail || !((double)it < S.k))) done = true;
+                    S.iterations = it;
+                    S.done = done;
+                }
+                __syncthreads();
+            }
+            // ---------------- inliers, optimizeModelCoefficients, refined inliers
+            int n_inl = 0;
+            if (S.have) {
+                float c0[6];
+                line_from_samples(Q[S.best_s0], Q[S.best_s1], c0);
+                n_inl = select_within(c0, Q, flag, n, thr, S);
+                if (n_inl > 2) {
+                    if (wave == 0 && lane < 3) {  // compute3DCentroid (dense): sequential float sums
+                        float s = 0.f;
+                        for (int i = 0; i < n; i++)
+                            if (flag[i]) { const float4 p = Q[i]; s += lane == 0 ? p.x : lane == 1 ? p.y : p.z; }
+                        S.acc[lane] = s / (float)n_inl;
+                    }
+                    __syncthreads();
+                    if (wave == 0 && lane < 6) {  // computeCovarianceMatrix (dense), one accumulator per lane
+                        const float cx = S.acc[0], cy = S.acc[1], cz = S.acc[2];
+                        float s = 0.f;
+                        for (int i = 0; i < n; i++)
+                            if (flag[i]) {
+                                const float4 p = Q[i];
+                                const float x = p.x - cx, y = p.y - cy, z = p.z - cz;
+                                const float a = lane == 0 ? y : lane == 1 ? y : lane == 2 ? z : lane == 3 ? x : lane == 4 ? y : z;
+                                const float b = lane == 0 ? y : lane == 1 ? z : lane == 2 ? z : x;
+                                s += a * b;
+                            }
+                        S.acc[3 + lane] = s;
+                    }
+                    __syncthreads();
+                    if (t == 0) {
+                        // acc[3..8] = (1,1) (1,2) (2,2) (0,0) (0,1) (0,2)
+                        const float cov[3][3] = {{S.acc[6], S.acc[7], S.acc[8]},
+                                                 {S.acc[7], S.acc[3], S.acc[4]},
+                                                 {S.acc[8], S.acc[4], S.acc[5]}};
+                        float ev[3];
+                        line_direction(cov, ev);
+                        S.line[0] = S.acc[0]; S.line[1] = S.acc[1]; S.line[2] = S.acc[2];
+                        S.line[3] = ev[0]; S.line[4] = ev[1]; S.line[5] = ev[2];
+                    }
+                } else if (t == 0) {
+                    for (int k = 0; k < 6; k++) S.line[k] = c0[k];
+                }
+                __syncthreads();
+                float ref[6];
+                for (int k = 0; k < 6; k++) ref[k] = S.line[k];
+                n_inl = select_within(ref, Q, flag, n, thr, S);
+            } else if (t == 0) {
+                for (int k = 0; k < 6; k++) S.line[k] = 0.f;
+            }
+            __syncthreads();
+            // ---------------- Frame.cc:961-988
+            LineCand& out = C[j];
+            if (t == 0) {
+                for (int k = 0; k < 6; k++) out.line[k] = S.line[k];
+                out.n_inliers = n_inl;
+                out.iterations = S.iterations;
+                out.idx_off = coff + used;
+                int fl = 0;
+                if (!((double)n_inl < sp.line_ratio * (double)bsize)) {
+                    fl = 1;
+                    if (line_in_range(S.line, K)) fl |= 2;
+                }
+                S.flags = fl;
+            }
+            ncand = j + 1;
+            __syncthreads();
+            const int fl = S.flags;
+            if (!(fl & 1)) {
+                if (t == 0) out.flags = fl;
+                break;
+            }
+            // line points (ExtractIndices, order kept) + removal of them from the set, in place
+            int nonborder = 0;
+            int wbase = 0, kbase = 0;
+            for (int base = 0; base < n; base += kThreads) {
+                const int i = base + t;
+                const bool valid = i < n;
+                const bool in = valid && flag[i];
+                const float4 p = valid ? Q[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                if (in && (fl & 2) && !is_border_point(p, D, K)) nonborder++;
+                // exclusive ranks of inliers / kept points within this chunk
+                const uint64_t mi = __ballot(in), mk = __ballot(valid && !in);
+                const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                if (lane == 0) { S.s0[wave] = __popcll(mi); S.s1[wave] = __popcll(mk); }
+                __syncthreads();
+                int oi = wbase, ok = kbase;
+                for (int w = 0; w < wave; w++) { oi += S.s0[w]; ok += S.s1[w]; }
+                int ti = 0, tk = 0;
+                for (int w = 0; w < kWaves; w++) { ti += S.s0[w]; tk += S.s1[w]; }
+                __syncthreads();
+                if (in) lidx[used + oi + __popcll(mi & lt)] = __float_as_int(p.w);
+                if (valid && !in) Q[ok + __popcll(mk & lt)] = p;
+                wbase += ti;
+                kbase += tk;
+            }
+            nonborder = block_sum(nonborder, S);
+            if (t == 0) out.flags = fl | ((fl & 2) && nonborder <= n_inl / 4 ? 4 : 0);
+            used += n_inl;
+            n = kbase;
+            __syncthreads();
+        }
+        if (t == 0) sb.n_cand[f * kMaxPlanesPerFrame + q] = ncand;
+        __syncthreads();
+    }
+}
+
+// Frame::CaculatePlanes' plane (Frame.cc:1082-1093) with GCC -O3 -march=native's contractions.
+__device__ void supposed_coef(const float* ip, const float* il, float* coef) {
+    const float a = fmaf(ip[1], il[5], -(ip[2] * il[4]));
+    const float b = fmaf(ip[2], il[3], -(ip[0] * il[5]));
+    const float c = fmaf(ip[0], il[4], -(ip[1] * il[3]));
+    const float d = fmaf(c, il[2], fmaf(a, il[0], b * il[1]));
+    const float v = sqrtf(fmaf(c, c, fmaf(a, a, b * b)));
+    coef[0] = a / v; coef[1] = b / v; coef[2] = c / v; coef[3] = -d / v;
+    if (coef[3] < 0)
+        for (int k = 0; k < 4; k++) coef[k] = -coef[k];
+}
+
+__global__ __launch_bounds__(64) void supp_assemble_kernel(SuppParams sp, SuppBuffers sb, int contour_cap,
+                                                           const spslam_plane* __restrict__ planes,
+                                                           const int* __restrict__ plane_counts,
+                                                           spslam_supposed_plane* __restrict__ out,
+                                                           int* __restrict__ out_counts,
+                                                           int32_t* __restrict__ out_line_idx,
+                                                           float* __restrict__ out_patch) {
+    __shared__ float pl[kMaxPlanesPerFrame + kMaxSuppPerFrame][4];
+    __shared__ int src_cand[kMaxSuppPerFrame];
+    __shared__ int n_out;
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const int np = min(plane_counts[f], kMaxPlanesPerFrame);
+    const spslam_plane* P = planes + (size_t)f * kMaxPlanesPerFrame;
+    const LineCand* C = sb.cand + (size_t)f * kMaxPlanesPerFrame * kMaxLinesPerBoundary;
+    spslam_supposed_plane* O = out + (size_t)f * sp.supp_cap;
+    const int cap = min(sp.supp_cap, kMaxSuppPerFrame);
+    const int n_patch = sp.n_steps * sp.n_steps;
+    if (lane == 0) {
+        for (int q = 0; q < np; q++)
+            for (int k = 0; k < 4; k++) pl[q][k] = P[q].coef[k];
+        int nl = np, ns = 0, loff = 0;
+        for (int q = np - 1; q >= 0; --q) {
+            const int nc = sb.n_cand[f * kMaxPlanesPerFrame + q];
+            for (int j = 0; j < nc; j++) {
+                const LineCand& c = C[q * kMaxLinesPerBoundary + j];
+                if ((c.flags & 7) != 7) continue;
+                float cf[4];
+                supposed_coef(pl[q], c.line, cf);
+                bool seen = false;
+                for (int m = 0; m < nl && !seen; m++) {  // PlaneNotSeen (Frame.cc:1121-1144)
+                    const float d = pl[m][3] - cf[3];
+                    const float angle = pl[m][0] * cf[0] + pl[m][1] * cf[1] + pl[m][2] * cf[2];
+                    if ((double)d > 0.2 || (double)d < -0.2) continue;
+                    if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
+                    seen = true;
+                }
+                if (seen) continue;
+                if (ns < cap && nl < kMaxPlanesPerFrame + kMaxSuppPerFrame) {
+                    for (int k = 0; k < 4; k++) pl[nl][k] = cf[k];
+                    nl++;
+                    spslam_supposed_plane& o = O[ns];
+                    for (int k = 0; k < 4; k++) o.coef[k] = cf[k];
+                    for (int k = 0; k < 6; k++) o.line[k] = c.line[k];
+                    o.source_plane = q;
+                    o.n_line = min(c.n_inliers, sp.line_cap - loff);
+                    o.line_offset = loff;
+                    o.n_patch = n_patch;
+                    o.patch_offset = ns * n_patch;
+                    o.pad = 0;
+                    loff += o.n_line;
+                    src_cand[ns] = q * kMaxLinesPerBoundary + j;
+                }
+                ns++;
+            }
+        }
+        out_counts[f] = ns;
+        n_out = min(ns, cap);
+    }
+    __syncthreads();
+    for (int s = 0; s < n_out; s++) {
+        const spslam_supposed_plane& o = O[s];
+        const LineCand& c = C[src_cand[s]];
+        const int32_t* src = sb.line_idx + (size_t)f * contour_cap + c.idx_off;
+        int32_t* dst = out_line_idx + (size_t)f * sp.line_cap + o.line_offset;
+        for (int i = lane; i < o.n_line; i += 64) dst[i] = src[i];
+        // CaculatePlanes' synthetic patch (Frame.cc:1097-1112), i outer, j inner
+        const float* ip = pl[o.source_plane];
+        float* pp = out_patch + ((size_t)f * sp.supp_cap + s) * (size_t)n_patch * 3;
+        for (int k = lane; k < n_patch; k += 64) {
+            const float a = sp.steps[k / sp.n_steps], b = sp.steps[k % sp.n_steps];
+            const float x = fmaf(b, ip[0], fmaf(a, o.line[3], o.line[0]));
+            const float y = fmaf(b, ip[1], fmaf(a, o.line[4], o.line[1]));
+            const float z = (fmaf(o.coef[0], x, o.coef[1] * y) + o.coef[3]) / (-o.coef[2]);
+            pp[3 * k] = x;
+            pp[3 * k + 1] = y;
+            pp[3 * k + 2] = z;
+        }
+    }
+}
+
+}  // namespace supp
+
+hipError_t supp_launch(const PlaneGeom& g, const PlaneBuffers& pb, const SuppParams& sp, const SuppBuffers& sb,
+                       int n, const float* depth, long long depth_fs, int depth_stride, const spslam_plane* planes,
+                       const int* plane_counts, const int32_t* contours, spslam_supposed_plane* out, int* out_counts,
+                       int32_t* out_line_idx, float* out_patch, hipStream_t s, KernelTimer* timer) {
+    if (sp.n_steps < 1 || sp.n_steps > kMaxPatchSteps || sp.supp_cap < 1) return hipErrorInvalidValue;
+    auto B = [&](int k) { if (timer) timer->begin(k, s); };
+    auto E = [&](int k) { if (timer) timer->end(k, s); };
+    B(kKindSuppLines);
+    hipLaunchKernelGGL(supp::supp_lines_kernel, dim3(n, 16), dim3(supp::kThreads), 0, s, g, pb, sp, sb, depth,
+                       depth_fs, depth_stride, planes, plane_counts, contours);
+    E(kKindSuppLines);
+    B(kKindSuppAssemble);
+    hipLaunchKernelGGL(supp::supp_assemble_kernel, dim3(n), dim3(64), 0, s, sp, sb, g.contour_cap, planes,
+                       plane_counts, out, out_counts, out_line_idx, out_patch);
+    E(kKindSuppAssemble);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

@@ -3,6 +3,7 @@
 One step = for each of B frames resident in HBM (gray u8 + depth f32):
   ORBextractor::operator()                      (spslam_orb_extract_batch_device)
   Frame::ComputePlanesFromOrganizedPointCloud   (spslam_planes_extract_batch_device)
+  Frame::GeneratePlanesFromBoundries            (spslam_planes_generate_from_boundaries_batch_device)
   Optimizer::PoseOptimization, motion model     (spslam_pose_optimize_batch_device)
   Optimizer::PoseOptimization, local map,       (same, chained on the device from
       starting from the motion-model pose        the first call's results)
@@ -59,6 +60,10 @@ class HotPath:
         self.d_pcnt = torch.zeros(B, dtype=torch.int32, device=dev)
         self.d_inl = torch.zeros(B * pe.inlier_cap, dtype=torch.int32, device=dev)
         self.d_con = torch.zeros(B * pe.contour_cap, dtype=torch.int32, device=dev)
+        self.d_supp = torch.zeros(B * pe.supp_cap * 16, dtype=torch.int32, device=dev)
+        self.d_scnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_lines = torch.zeros(B * pe.line_cap, dtype=torch.int32, device=dev)
+        self.d_patch = torch.zeros(B * pe.supp_cap * pe.patch_points * 3, dtype=torch.float32, device=dev)
         # --- streams: ORB on the main stream, plane extraction beside it (independent inputs);
         #     PoseOptimization joins both
         self.main = torch.cuda.current_stream()
@@ -115,9 +120,14 @@ class HotPath:
                                      self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, self.stream)
 
     def planes(self, stream=None):
+        s = self.stream if stream is None else stream
         self.pe.extract_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
                                      self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_inl.data_ptr(),
-                                     self.d_con.data_ptr(), self.stream if stream is None else stream)
+                                     self.d_con.data_ptr(), s)
+        self.pe.generate_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
+                                      self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_con.data_ptr(),
+                                      self.d_supp.data_ptr(), self.d_scnt.data_ptr(), self.d_lines.data_ptr(),
+                                      self.d_patch.data_ptr(), s)
 
     def pose(self):
         A, Bp = self.dA, self.dB
@@ -145,8 +155,21 @@ class HotPath:
             kps=self.d_kps.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(self.B, self.kp_cap),
             kp_counts=self.d_cnt.cpu().numpy(),
             plane_counts=self.d_pcnt.cpu().numpy(),
+            supposed_counts=self.d_scnt.cpu().numpy(),
+            contour_points=self._plane_field("n_contour"),
+            line_points=self._supposed_line_points(),
             pose1=self.d_res1.cpu().numpy().view(G.POSE_RESULT_DTYPE),
             pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE))
+
+    def _plane_field(self, name):
+        pl = self.d_planes.cpu().numpy().view(spslam_planes.PLANE_DTYPE).reshape(self.B, self.pe.planes_cap)
+        cnt = self.d_pcnt.cpu().numpy()
+        return np.array([pl[f, :cnt[f]][name].sum() for f in range(self.B)], np.float64)
+
+    def _supposed_line_points(self):
+        sp = self.d_supp.cpu().numpy().view(spslam_planes.SUPPOSED_DTYPE).reshape(self.B, self.pe.supp_cap)
+        cnt = np.minimum(self.d_scnt.cpu().numpy(), self.pe.supp_cap)
+        return np.array([sp[f, :cnt[f]]["n_line"].sum() for f in range(self.B)], np.float64)
 
     def close(self):
         self.ex.close()

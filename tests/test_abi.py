@@ -56,6 +56,9 @@ int main(void) {
   S(spslam_pose_problem) O(spslam_pose_problem, point_offset) O(spslam_pose_problem, plane_offset)
   S(spslam_pose_result) S(spslam_plane) O(spslam_plane, n_inliers) O(spslam_plane, contour_offset)
   S(spslam_orb_params) S(spslam_plane_params) S(spslam_plane_config)
+  S(spslam_supposed_plane) O(spslam_supposed_plane, line) O(spslam_supposed_plane, source_plane)
+  O(spslam_supposed_plane, patch_offset)
+  S(spslam_line_candidate) O(spslam_line_candidate, n_inliers) O(spslam_line_candidate, idx_offset)
   return 0;
 }
 """
@@ -75,6 +78,7 @@ def test_struct_layouts_match_bindings(tmp_path):
         "spslam_keypoint": spslam_gpu.KEYPOINT_DTYPE, "spslam_point_obs": spslam_gpu.POINT_OBS_DTYPE,
         "spslam_plane_obs": spslam_gpu.PLANE_OBS_DTYPE, "spslam_pose_problem": spslam_gpu.POSE_PROBLEM_DTYPE,
         "spslam_pose_result": spslam_gpu.POSE_RESULT_DTYPE, "spslam_plane": spslam_planes.PLANE_DTYPE,
+        "spslam_supposed_plane": spslam_planes.SUPPOSED_DTYPE, "spslam_line_candidate": spslam_planes.LINE_CAND_DTYPE,
     }
     for name, dt in checks.items():
         assert got[name] == dt.itemsize, (name, got[name], dt.itemsize)

@@ -1,0 +1,155 @@
+"""GPU parity: supposed planes (Frame::GeneratePlanesFromBoundries,
+src/Frame.cc:938-1144, with PCL 1.8 SACSegmentation LINE/RANSAC) vs the CPU
+oracle (oracle/supposed_oracle.cpp).
+
+Bar: on the same planes + contours + organized cloud (the GPU's own plane
+stage output, so this stage is tested in isolation) every line candidate
+(RANSAC trial count, inlier count, line coefficients, flags, line point
+indices) and every appended plane (coefficients, source, line points,
+synthetic patch) is bit-exact.  End to end (oracle planes -> oracle supposed
+planes vs the GPU path) the appended planes agree within 1e-4.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+COEF_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import spslam_gpu
+    import spslam_planes
+    import synth
+    K = synth.TUM3
+    ex = spslam_gpu.OrbExtractor(max_batch=4)
+    pe = spslam_planes.PlaneExtractor(ex, K["fx"], K["fy"], K["cx"], K["cy"])
+    yield ex, pe
+    ex.close()
+
+
+def _frames():
+    import oracle_planes
+    import synth
+    for seq, boxes, fis in ((0, 3, (0, 20, 45)), (2, 6, (0, 20, 45)), (3, 8, (0, 20, 45)), (5, 8, (7, 33))):
+        sc = synth.Scene(seq, n_boxes=boxes)
+        for fi in fis:
+            _, d, _ = sc.render(sc.pose(fi), noise_seed=fi)
+            yield (seq, fi), oracle_planes.depth_to_float(d)
+
+
+def _check_isolated(pe, depth, tag):
+    """GPU supposed stage vs oracle on the GPU's plane output."""
+    import oracle_supposed
+    import synth
+    K = synth.TUM3
+    rg = pe(depth)
+    cloud = pe.debug(0, 0)
+    so = oracle_supposed.generate(depth, cloud, rg["coef"], rg["contour"], K["fx"], K["fy"], K["cx"], K["cy"])
+    sg = pe.generate_from_boundaries(depth)
+    # per-boundary candidates
+    by_plane = {}
+    for c in so["candidates"]:
+        by_plane.setdefault(c["plane"], []).append(c)
+    for q in range(len(rg["coef"])):
+        gc = pe.line_candidates(0, q)
+        oc = by_plane.get(q, [])
+        assert len(gc) == len(oc), f"{tag} boundary {q}: {len(gc)} vs {len(oc)} line candidates"
+        for j, (a, b) in enumerate(zip(gc, oc)):
+            where = f"{tag} boundary {q} line {j}"
+            assert a["iterations"] == b["iterations"], f"{where}: RANSAC trials {a['iterations']} vs {b['iterations']}"
+            assert a["n_inliers"] == b["n_inliers"], f"{where}: inliers {a['n_inliers']} vs {b['n_inliers']}"
+            assert np.array_equal(a["line"], b["line"]), f"{where}: line {a['line']} vs {b['line']}"
+            assert a["flags"] == (b["flags"] & 7), f"{where}: flags {a['flags']} vs {b['flags']}"
+            if b["flags"] & 1:
+                assert np.array_equal(a["cloud_idx"], b["cloud_idx"]), f"{where}: line points"
+    assert len(sg["coef"]) == len(so["coef"]), f"{tag}: {len(sg['coef'])} vs {len(so['coef'])} appended planes"
+    for k in range(len(so["coef"])):
+        assert np.array_equal(sg["coef"][k], so["coef"][k]), f"{tag} appended {k}: coef"
+        assert np.array_equal(sg["line"][k], so["line"][k]), f"{tag} appended {k}: line"
+        assert sg["source"][k] == so["source"][k]
+        assert np.array_equal(sg["line_idx"][k], so["line_idx"][k]), f"{tag} appended {k}: line points"
+        po = oracle_supposed.patch(rg["coef"][so["source"][k]], so["line"][k], so["coef"][k])
+        assert np.array_equal(sg["patch"][k], po), f"{tag} appended {k}: patch"
+    return len(so["coef"]), sum(1 for c in so["candidates"] if c["flags"] & 1)
+
+
+def test_supposed_bit_exact(ctx):
+    _, pe = ctx
+    n_app = n_fit = 0
+    for tag, depth in _frames():
+        a, f = _check_isolated(pe, depth, tag)
+        n_app += a
+        n_fit += f
+    # the synthetic box scenes must exercise the accept path, not only rejections
+    assert n_app >= 5 and n_fit >= 20, (n_app, n_fit)
+
+
+def test_supposed_end_to_end(ctx):
+    """Oracle planes -> oracle supposed planes vs the GPU planes -> GPU supposed planes."""
+    import oracle_planes
+    import oracle_supposed
+    import synth
+    K = synth.TUM3
+    _, pe = ctx
+    for tag, depth in _frames():
+        po = oracle_planes.PlaneOracle()
+        ro = po.extract(depth, K["fx"], K["fy"], K["cx"], K["cy"])
+        so = oracle_supposed.generate(depth, po.cloud(), ro["coef"], ro["contour"], K["fx"], K["fy"], K["cx"],
+                                      K["cy"])
+        pe(depth)
+        sg = pe.generate_from_boundaries(depth)
+        assert len(sg["coef"]) == len(so["coef"]), tag
+        for k in range(len(so["coef"])):
+            assert np.abs(sg["coef"][k] - so["coef"][k]).max() <= COEF_TOL * max(1.0, abs(so["coef"][k][3])), tag
+            assert sg["source"][k] == so["source"][k], tag
+
+
+def test_supposed_small_and_empty_boundaries(ctx):
+    """A frame with no planes (zero depth) and boundaries below 50 points give no lines."""
+    _, pe = ctx
+    depth = np.zeros((480, 640), np.float32)
+    r = pe(depth)
+    s = pe.generate_from_boundaries(depth)
+    assert len(s["coef"]) == 0
+    for q in range(len(r["coef"])):
+        if len(r["contour"][q]) < 50:
+            assert pe.line_candidates(0, q) == []
+
+
+def test_supposed_batch_device_matches_single(ctx):
+    import torch
+    import spslam_planes
+    ex, pe = ctx
+    frames = [d for _, d in _frames()][:4]
+    singles = []
+    for d in frames:
+        pe(d)
+        singles.append(pe.generate_from_boundaries(d))
+    B = len(frames)
+    dd = torch.from_numpy(np.stack(frames)).cuda()
+    planes = torch.zeros(B * pe.planes_cap * 8, dtype=torch.int32, device="cuda")
+    pcnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    inl = torch.zeros(B * pe.inlier_cap, dtype=torch.int32, device="cuda")
+    con = torch.zeros(B * pe.contour_cap, dtype=torch.int32, device="cuda")
+    sup = torch.zeros(B * pe.supp_cap * 16, dtype=torch.int32, device="cuda")
+    scnt = torch.zeros(B, dtype=torch.int32, device="cuda")
+    lines = torch.zeros(B * pe.line_cap, dtype=torch.int32, device="cuda")
+    patch = torch.zeros(B * pe.supp_cap * pe.patch_points * 3, dtype=torch.float32, device="cuda")
+    pe.extract_batch_device(dd.data_ptr(), B, 640 * 480, 640, planes.data_ptr(), pcnt.data_ptr(), inl.data_ptr(),
+                            con.data_ptr())
+    pe.generate_batch_device(dd.data_ptr(), B, 640 * 480, 640, planes.data_ptr(), pcnt.data_ptr(), con.data_ptr(),
+                             sup.data_ptr(), scnt.data_ptr(), lines.data_ptr(), patch.data_ptr())
+    torch.cuda.synchronize()
+    sup = sup.cpu().numpy().view(spslam_planes.SUPPOSED_DTYPE).reshape(B, pe.supp_cap)
+    scnt = scnt.cpu().numpy()
+    lines = lines.cpu().numpy().reshape(B, pe.line_cap)
+    patch = patch.cpu().numpy().reshape(B, pe.supp_cap * pe.patch_points, 3)
+    for f in range(B):
+        s = singles[f]
+        assert scnt[f] == len(s["coef"])
+        for k in range(scnt[f]):
+            o = sup[f, k]
+            assert np.array_equal(o["coef"], s["coef"][k])
+            assert np.array_equal(lines[f, o["line_offset"]:o["line_offset"] + o["n_line"]], s["line_idx"][k])
+            assert np.array_equal(patch[f, o["patch_offset"]:o["patch_offset"] + o["n_patch"]], s["patch"][k])

@@ -14,6 +14,7 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT / "sp-slam_amd"), str(ROOT / "oracle")]
 import oracle_ctypes as O  # noqa: E402
 import oracle_planes as OP  # noqa: E402
+import oracle_supposed as OS  # noqa: E402
 import synth  # noqa: E402
 
 out = ROOT / "tests" / "golden"
@@ -30,7 +31,24 @@ K = synth.TUM3
 res = po.extract(df, K["fx"], K["fy"], K["cx"], K["cy"])
 np.savez_compressed(out / "planes_seq0_f5.npz", coef=np.array(res["coef"]), n_inliers=np.array([len(i) for i in res["inliers"]]),
                     inliers=np.concatenate(res["inliers"]) if res["inliers"] else np.zeros(0, np.int32),
+                    n_contour=np.array([len(c) for c in res["contour"]]),
+                    contours=np.concatenate(res["contour"]) if res["contour"] else np.zeros(0, np.int32),
                     depth_sum=np.int64(d.astype(np.int64).sum()))
+# supposed planes (GeneratePlanesFromBoundries) on a box scene that produces some
+sc2 = synth.Scene(2, n_boxes=6)
+_, d2, _ = sc2.render(sc2.pose(20), noise_seed=20)
+df2 = OP.depth_to_float(d2)
+po2 = OP.PlaneOracle()
+r2 = po2.extract(df2, K["fx"], K["fy"], K["cx"], K["cy"])
+s2 = OS.generate(df2, po2.cloud(), r2["coef"], r2["contour"], K["fx"], K["fy"], K["cx"], K["cy"])
+cands = s2["candidates"]
+np.savez_compressed(out / "supposed_seq2_f20.npz", coef=np.array(s2["coef"]).reshape(-1, 4),
+                    line=np.array(s2["line"]).reshape(-1, 6), source=np.array(s2["source"], np.int32),
+                    n_line=np.array([len(x) for x in s2["line_idx"]], np.int32),
+                    line_idx=np.concatenate(s2["line_idx"]) if s2["line_idx"] else np.zeros(0, np.int32),
+                    cand_info=np.array([[c["plane"], c["j"], c["n_inliers"], c["iterations"], c["flags"]]
+                                        for c in cands], np.int32).reshape(-1, 5),
+                    depth_sum=np.int64(d2.astype(np.int64).sum()))
 # pose
 invs2 = orb.scale_tables()[3]
 rng = np.random.default_rng(11)
