@@ -25,6 +25,7 @@
 //   N  findLabeledRegionBoundary: Moore tracing from per-pixel 8-neighbour
 //      masks, one wave per plane (count pass, offsets, write pass)
 // Reference semantics are restated in oracle/plane_oracle.cpp:268-470.
+#include "libm_restated.h"
 #include <hip/hip_runtime.h>
 
 #include "plane_launch.h"
@@ -149,8 +150,9 @@ __device__ void eigen33_min(const float (&m0)[3][3], float* eval, float* evec) {
         float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
         if (q > 0.f) q = 0.f;
         const float rho = sqrtf(-a_over_3);
-        const float theta = atan2f(sqrtf(-q), half_b) * s_inv3;
-        const float ct = cosf(theta), st = sinf(theta);
+        const float theta = libm::atan2f_(sqrtf(-q), half_b) * s_inv3;  // glibc-exact (libm_restated.h)
+        float st, ct;
+        libm::sincosf_(theta, &st, &ct);
         r[0] = c2_over_3 + 2.f * rho * ct;
         r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);
         r[2] = c2_over_3 - rho * (ct - s_sqrt3 * st);

@@ -61,6 +61,7 @@ def _compare(pe, depth, k, scale=1.0, min_size=500):
     for j in range(len(ro["coef"])):
         assert np.abs(rg["coef"][j] - ro["coef"][j]).max() <= COEF_TOL * max(1.0, abs(ro["coef"][j][3])), \
             f"frame {k} plane {j}: {rg['coef'][j]} vs {ro['coef'][j]}"
+        assert np.array_equal(rg["coef"][j], ro["coef"][j]), f"frame {k} plane {j}: coef not bit-exact"
         assert np.array_equal(rg["inliers"][j], ro["inliers"][j]), f"frame {k} plane {j}: inliers"
         assert np.array_equal(rg["contour"][j], ro["contour"][j]), f"frame {k} plane {j}: contour"
     return len(ro["coef"]), po.n_models
@@ -121,6 +122,7 @@ def test_planes_match_oracle(ctx, depth_frames):
         for j in range(len(ro["coef"])):
             assert np.abs(rg["coef"][j] - ro["coef"][j]).max() <= COEF_TOL * max(1.0, abs(ro["coef"][j][3])), \
                 f"frame {k} plane {j}: {rg['coef'][j]} vs {ro['coef'][j]}"
+            assert np.array_equal(rg["coef"][j], ro["coef"][j]), f"frame {k} plane {j}: coef not bit-exact"
             assert np.array_equal(rg["inliers"][j], ro["inliers"][j]), f"frame {k} plane {j}: inliers"
             assert np.array_equal(rg["contour"][j], ro["contour"][j]), f"frame {k} plane {j}: contour"
         total += len(ro["coef"])

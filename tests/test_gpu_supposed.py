@@ -102,6 +102,7 @@ def test_supposed_end_to_end(ctx):
         assert len(sg["coef"]) == len(so["coef"]), tag
         for k in range(len(so["coef"])):
             assert np.abs(sg["coef"][k] - so["coef"][k]).max() <= COEF_TOL * max(1.0, abs(so["coef"][k][3])), tag
+            assert np.array_equal(sg["coef"][k], so["coef"][k]), f"{tag}: appended plane {k} not bit-exact"
             assert sg["source"][k] == so["source"][k], tag
 
 
