@@ -4,7 +4,9 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--config c2|c5]
 
 A "step" is one pass of the hot path -- ORB extraction, plane extraction,
-supposed planes from plane boundaries and two chained PoseOptimizations (motion model, then local map) -- over one
+supposed planes from plane boundaries, the RGB-D Frame keypoint steps
+(undistortion, depth / right coordinate, 64x48 grid) and two chained
+PoseOptimizations (motion model, then local map) -- over one
 batch of B synthetic RGB-D frames already resident in HBM (sp-slam_amd/
 pipeline.py).  One process per GPU; for N > 1 launch through
 torch.distributed.run: every rank runs its own independent sequence (the path
@@ -76,6 +78,7 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0):
         "plane_segment_kernel": 28 * N + 4 * N,               # xyz+normal+plane_d in, labels out
         "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
         "supp_assemble_kernel": n_sup * (64 + 2601 * 12),     # appended planes + synthetic patches out
+        "frame_rgbd_kernel": n_kp * (28 + 4 + 28 + 4 + 4 + 4) + 4 * 3073,  # kp in, depth gather, kp/depth/uR/idx out
     }
 
 

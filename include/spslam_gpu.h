@@ -314,6 +314,48 @@ int spslam_supposed_debug(spslam_ctx* ctx, int frame, int plane, spslam_line_can
  * timestamps (16 int64 ticks of the 100 MHz GPU real-time clock). */
 int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_points);
 
+/* ------------------------------------------------------------------------
+ * RGB-D Frame per-keypoint steps (src/Frame.cc:146-181): UndistortKeyPoints
+ * (:504-534, cv::undistortPoints with K and mDistCoef), ComputeStereoFromRGBD
+ * (:743-764: mvDepth / mvuRight from the depth at the distorted keypoint) and
+ * AssignFeaturesToGrid (:326-341: 64 x 48 cells over ComputeImageBounds).
+ * Outputs per frame: mvKeysUn (keypoints with undistorted x, y), mvDepth,
+ * mvuRight (-1 where no depth) and mGrid as CSR: cell (x, y) = x * 48 + y owns
+ * grid_idx[grid_off[cell] .. grid_off[cell + 1]) in increasing keypoint index. */
+#define SPSLAM_GRID_COLS 64
+#define SPSLAM_GRID_ROWS 48
+
+typedef struct spslam_frame_params {
+    float fx, fy, cx, cy;   /* Camera.fx .. cy (mK) */
+    float dist[5];          /* Camera.k1 k2 p1 p2 k3 (mDistCoef) */
+    float bf;               /* Camera.bf (mbf) */
+    int width, height;      /* image size (ComputeImageBounds) */
+} spslam_frame_params;
+
+/* Configure the frame stage; computes mnMinX/mnMaxX/mnMinY/mnMaxY and the grid
+ * scale like the reference's first Frame (mbInitialComputations, Frame.cc:162-177).
+ * bounds (4 floats) and grid_inv (2 floats) may be NULL. */
+int spslam_frame_configure(spslam_ctx* ctx, const spslam_frame_params* params, float* bounds, float* grid_inv);
+
+/* Drop-in for one frame on host buffers: kps = mvKeys (n keypoints), depth =
+ * imDepth (float meters).  keys_un, mv_depth, mv_uright receive n entries,
+ * grid_off 64*48+1 ints, grid_idx up to n ints. */
+int spslam_frame_rgbd(spslam_ctx* ctx, const spslam_keypoint* kps, int n, const float* depth, int w, int h,
+                      int stride_floats, spslam_keypoint* keys_un, float* mv_depth, float* mv_uright,
+                      int32_t* grid_off, int32_t* grid_idx);
+
+/* Batched, device resident, on the ORB batch outputs (frame f: counts[f]
+ * keypoints at d_kps + f*cap_per_frame) and the depth frames.  Per frame f:
+ * keys_un / depth / uright / grid_idx at f*cap_per_frame, grid_off at
+ * f*(64*48+1).  d_plane_counts / d_supp_counts (may be NULL) are zeroed for
+ * frames without keypoints: the reference's constructor returns before plane
+ * extraction then (Frame.cc:148-149). */
+int spslam_frame_rgbd_batch_device(spslam_ctx* ctx, const spslam_keypoint* d_kps, const int* d_counts,
+                                   int cap_per_frame, const float* d_depth, int n_frames, size_t frame_stride,
+                                   int stride_floats, spslam_keypoint* d_keys_un, float* d_mv_depth,
+                                   float* d_mv_uright, int32_t* d_grid_off, int32_t* d_grid_idx,
+                                   int* d_plane_counts, int* d_supp_counts, void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

@@ -20,6 +20,7 @@
 #include "plane_launch.h"
 #include "pose_launch.h"
 #include "supposed_launch.h"
+#include "frame_launch.h"
 
 using namespace spslam;
 
@@ -111,6 +112,10 @@ struct spslam_ctx {
     int32_t* d_line1 = nullptr;
     float* d_patch1 = nullptr;
     int supp_last_frames = 0;
+    // RGB-D frame stage (UndistortKeyPoints / ComputeStereoFromRGBD / AssignFeaturesToGrid)
+    bool frame_ready = false;
+    FrameGeom fg{};
+    uint8_t* d_frame1 = nullptr;  // single-frame staging: kps, keys_un, depth, uR, grid_off, grid_idx, count
 };
 
 namespace {
@@ -232,7 +237,7 @@ void free_all(spslam_ctx* c) {
                     c->b.keynode, c->b.lvl_kp, c->b.lvl_cnt,       c->d_in,           c->d_kps,
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
-                    c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1};
+                    c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -768,6 +773,126 @@ int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_po
         return SPSLAM_OK;
     }
     return fail(c, SPSLAM_ERR_ARG, "unknown debug stage%s", "");
+}
+
+}  // extern "C"
+
+namespace {
+
+// cv::undistortPoints(point, K, D, noArray(), K), OpenCV 3.4 (frame_kernels.hip restates it for the device).
+void undistort_host(const FrameGeom& g, float u, float v, float* ou, float* ov) {
+    const double fx = g.fx, fy = g.fy, cx = g.cx, cy = g.cy, ifx = 1. / fx, ify = 1. / fy;
+    const double k0 = g.dist[0], k1 = g.dist[1], k2 = g.dist[2], k3 = g.dist[3], k4 = g.dist[4];
+    const double k5 = 0, k6 = 0, k7 = 0, k8 = 0, k9 = 0, k10 = 0, k11 = 0;
+    double x = ((double)u - cx) * ifx, y = ((double)v - cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k7 * r2 + k6) * r2 + k5) * r2) / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        const double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x) + k8 * r2 + k9 * r2 * r2;
+        const double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y + k10 * r2 + k11 * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    *ou = (float)((fx * x + 0. * y + cx) * (1. / (0. * x + 0. * y + 1.)));
+    *ov = (float)((0. * x + fy * y + cy) * (1. / (0. * x + 0. * y + 1.)));
+}
+
+}  // namespace
+
+extern "C" {
+
+int spslam_frame_configure(spslam_ctx* c, const spslam_frame_params* p, float* bounds, float* grid_inv) {
+    if (!c || !p || p->fx == 0.f || p->fy == 0.f || p->width < 1 || p->height < 1) return SPSLAM_ERR_ARG;
+    FrameGeom& g = c->fg;
+    g.fx = p->fx; g.fy = p->fy; g.cx = p->cx; g.cy = p->cy;
+    for (int k = 0; k < 5; k++) g.dist[k] = p->dist[k];
+    g.bf = p->bf;
+    g.undistort = p->dist[0] != 0.0f;
+    // Frame::ComputeImageBounds (Frame.cc:536-564)
+    if (g.undistort) {
+        float cu[4], cv[4];
+        const float px[4] = {0.f, (float)p->width, 0.f, (float)p->width};
+        const float py[4] = {0.f, 0.f, (float)p->height, (float)p->height};
+        for (int i = 0; i < 4; i++) undistort_host(g, px[i], py[i], &cu[i], &cv[i]);
+        g.min_x = std::min(cu[0], cu[2]); g.max_x = std::max(cu[1], cu[3]);
+        g.min_y = std::min(cv[0], cv[1]); g.max_y = std::max(cv[2], cv[3]);
+    } else {
+        g.min_x = 0.f; g.max_x = (float)p->width; g.min_y = 0.f; g.max_y = (float)p->height;
+    }
+    g.ginv_x = (float)SPSLAM_GRID_COLS / (g.max_x - g.min_x);
+    g.ginv_y = (float)SPSLAM_GRID_ROWS / (g.max_y - g.min_y);
+    if (bounds) { bounds[0] = g.min_x; bounds[1] = g.max_x; bounds[2] = g.min_y; bounds[3] = g.max_y; }
+    if (grid_inv) { grid_inv[0] = g.ginv_x; grid_inv[1] = g.ginv_y; }
+    HIP_CHECK(c, hipSetDevice(c->device));
+    if (!c->d_frame1) {
+        const size_t cap = (size_t)c->max_kp;
+        const size_t bytes = cap * (2 * sizeof(spslam_keypoint) + 3 * 4) + (SPSLAM_GRID_COLS * SPSLAM_GRID_ROWS + 1) * 4 +
+                             4096;
+        HIP_CHECK(c, hipMalloc(&c->d_frame1, bytes));
+    }
+    c->frame_ready = true;
+    return SPSLAM_OK;
+}
+
+int spslam_frame_rgbd_batch_device(spslam_ctx* c, const spslam_keypoint* d_kps, const int* d_counts,
+                                   int cap_per_frame, const float* d_depth, int n_frames, size_t frame_stride,
+                                   int stride_floats, spslam_keypoint* d_keys_un, float* d_mv_depth,
+                                   float* d_mv_uright, int32_t* d_grid_off, int32_t* d_grid_idx,
+                                   int* d_plane_counts, int* d_supp_counts, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->frame_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_frame_configure not called%s", "");
+    if (!d_kps || !d_counts || !d_depth || !d_keys_un || !d_mv_depth || !d_mv_uright || !d_grid_off || !d_grid_idx ||
+        n_frames < 1 || cap_per_frame < 1 || cap_per_frame > 32767 || stride_floats < 1)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_frame_rgbd_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    HIP_CHECK(c, frame_launch(c->fg, n_frames, d_kps, d_counts, cap_per_frame, d_depth, (long long)frame_stride,
+                              stride_floats, d_keys_un, d_mv_depth, d_mv_uright, d_grid_off, d_grid_idx,
+                              d_plane_counts, d_supp_counts, s, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_frame_rgbd(spslam_ctx* c, const spslam_keypoint* kps, int n, const float* depth, int w, int h,
+                      int stride_floats, spslam_keypoint* keys_un, float* mv_depth, float* mv_uright,
+                      int32_t* grid_off, int32_t* grid_idx) {
+    if (!c || n < 0 || (n && (!kps || !keys_un || !mv_depth || !mv_uright || !grid_idx)) || !grid_off || !depth ||
+        w < 1 || h < 1 || stride_floats < w)
+        return SPSLAM_ERR_ARG;
+    if (!c->frame_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_frame_configure not called%s", "");
+    if (n > c->max_kp) return fail(c, SPSLAM_ERR_CAPACITY, "more keypoints than the context holds%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t cap = (size_t)std::max(n, 1);
+    uint8_t* q = c->d_frame1;
+    auto* d_k = (spslam_keypoint*)q; q += (size_t)c->max_kp * sizeof(spslam_keypoint);
+    auto* d_u = (spslam_keypoint*)q; q += (size_t)c->max_kp * sizeof(spslam_keypoint);
+    auto* d_d = (float*)q; q += (size_t)c->max_kp * 4;
+    auto* d_r = (float*)q; q += (size_t)c->max_kp * 4;
+    auto* d_gi = (int32_t*)q; q += (size_t)c->max_kp * 4;
+    auto* d_go = (int32_t*)q; q += (SPSLAM_GRID_COLS * SPSLAM_GRID_ROWS + 1) * 4;
+    auto* d_n = (int*)(((uintptr_t)q + 255) & ~(uintptr_t)255);
+    // the depth image is staged in a stream-ordered temporary
+    float* d_depth = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&d_depth, (size_t)w * h * 4, c->stream));
+    HIP_CHECK(c, hipMemcpy2DAsync(d_depth, (size_t)w * 4, depth, (size_t)stride_floats * 4, (size_t)w * 4, h,
+                                  hipMemcpyHostToDevice, c->stream));
+    if (n) HIP_CHECK(c, hipMemcpyAsync(d_k, kps, n * sizeof(spslam_keypoint), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(d_n, &n, sizeof(int), hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_frame_rgbd_batch_device(c, d_k, d_n, (int)cap, d_depth, 1, (size_t)w * h, w, d_u, d_d, d_r,
+                                            d_go, d_gi, nullptr, nullptr, c->stream);
+    if (rc) { (void)hipFreeAsync(d_depth, c->stream); return rc; }
+    if (n) {
+        HIP_CHECK(c, hipMemcpyAsync(keys_un, d_u, n * sizeof(spslam_keypoint), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(mv_depth, d_d, n * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(mv_uright, d_r, n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_CHECK(c, hipMemcpyAsync(grid_off, d_go, (SPSLAM_GRID_COLS * SPSLAM_GRID_ROWS + 1) * 4, hipMemcpyDeviceToHost,
+                                c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    const int ng = grid_off[SPSLAM_GRID_COLS * SPSLAM_GRID_ROWS];
+    if (ng) HIP_CHECK(c, hipMemcpy(grid_idx, d_gi, (size_t)ng * 4, hipMemcpyDeviceToHost));
+    HIP_CHECK(c, hipFreeAsync(d_depth, c->stream));
+    return SPSLAM_OK;
 }
 
 int spslam_set_timing(spslam_ctx* c, int enable) {

@@ -4,6 +4,8 @@ One step = for each of B frames resident in HBM (gray u8 + depth f32):
   ORBextractor::operator()                      (spslam_orb_extract_batch_device)
   Frame::ComputePlanesFromOrganizedPointCloud   (spslam_planes_extract_batch_device)
   Frame::GeneratePlanesFromBoundries            (spslam_planes_generate_from_boundaries_batch_device)
+  Frame::UndistortKeyPoints / ComputeStereoFromRGBD / AssignFeaturesToGrid
+                                                (spslam_frame_rgbd_batch_device)
   Optimizer::PoseOptimization, motion model     (spslam_pose_optimize_batch_device)
   Optimizer::PoseOptimization, local map,       (same, chained on the device from
       starting from the motion-model pose        the first call's results)
@@ -21,6 +23,7 @@ from __future__ import annotations
 
 import numpy as np
 
+import spslam_frame
 import spslam_gpu as G
 import spslam_planes
 import synth
@@ -37,6 +40,8 @@ class HotPath:
         self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
         self.ex = G.OrbExtractor(nfeatures=nfeatures, width=width, height=height, max_batch=B, device=device)
         self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height)
+        self.fs = spslam_frame.FrameStage(self.ex, self.fx, self.fy, self.cx, self.cy, K.get("dist", (0,) * 5),
+                                          K["bf"], width, height)
         # --- unique synthetic frames
         U = min(unique_frames, B)
         self.frames = []
@@ -55,6 +60,11 @@ class HotPath:
         self.d_kps = torch.zeros((B, cap, 7), dtype=torch.float32, device=dev)
         self.d_desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
         self.d_cnt = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.d_kun = torch.zeros_like(self.d_kps)
+        self.d_kdepth = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+        self.d_kur = torch.zeros((B, cap), dtype=torch.float32, device=dev)
+        self.d_grid_off = torch.zeros((B, spslam_frame.N_CELLS + 1), dtype=torch.int32, device=dev)
+        self.d_grid_idx = torch.zeros((B, cap), dtype=torch.int32, device=dev)
         pe = self.pe
         self.d_planes = torch.zeros(B * pe.planes_cap * 8, dtype=torch.int32, device=dev)
         self.d_pcnt = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -129,6 +139,12 @@ class HotPath:
                                       self.d_supp.data_ptr(), self.d_scnt.data_ptr(), self.d_lines.data_ptr(),
                                       self.d_patch.data_ptr(), s)
 
+    def frame(self):
+        self.fs.batch_device(self.d_kps.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, self.d_depth.data_ptr(),
+                             self.B, self.W * self.H, self.W, self.d_kun.data_ptr(), self.d_kdepth.data_ptr(),
+                             self.d_kur.data_ptr(), self.d_grid_off.data_ptr(), self.d_grid_idx.data_ptr(),
+                             self.d_pcnt.data_ptr(), self.d_scnt.data_ptr(), self.stream)
+
     def pose(self):
         A, Bp = self.dA, self.dB
         G.pose_optimize_batch_device(self.ex, self.B, A["P"].data_ptr(), A["pts"].data_ptr(), A["pls"].data_ptr(),
@@ -146,6 +162,7 @@ class HotPath:
         self.orb()
         self.ev_join.record(self.side)
         self.main.wait_event(self.ev_join)
+        self.frame()
         self.pose()
 
     def results(self):
