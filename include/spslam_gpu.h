@@ -186,6 +186,105 @@ int spslam_pose_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_pose_
                                       uint8_t* d_plane_outlier, void* hip_stream);
 
 /* ------------------------------------------------------------------------
+ * LocalBundleAdjustment (include/Optimizer.h:46, src/Optimizer.cc:1154-1977)
+ * from the point where the local graph is known.  The caller (LocalMapping's
+ * shim) flattens what the reference collects from the Map:
+ *   keyframes  lLocalKeyFrames in list order (fixed = 0; mnId 0 is held fixed
+ *              like the reference), then lFixedCameras (fixed = 1);
+ *   points     lLocalMapPoints in list order, each with its observations in
+ *              MapPoint::GetObservations() order (std::map<KeyFrame*>:
+ *              pointer order in the reference, keyframe-id order here --
+ *              SURVEY.md Appendix A.9), observations of bad keyframes dropped;
+ *   planes     lLocalMapPlanes in list order, each with its GetObservations()
+ *              edges (kind SPSLAM_PLANE_EDGE), then GetVerObservations()
+ *              (SPSLAM_VERTICAL_EDGE), then GetParObservations()
+ *              (SPSLAM_PARALLEL_EDGE), the reference's edge insertion order.
+ * Results: poses of the local keyframes (KeyFrame::SetPose), point positions
+ * (MapPoint::SetWorldPos), plane coefficients (MapPlane::SetWorldPos), and per
+ * observation the outlier flag the reference acts on (point observations:
+ * vToErase -> EraseMapPointMatch / EraseObservation; plane observations:
+ * chi2 above Plane.Chi / VPChi, informational -- the reference's erase is
+ * commented out, Optimizer.cc:1862-1870).  The not-seen plane branches are
+ * dead in the reference (SURVEY.md 8 notes) and are not represented. */
+typedef struct spslam_lba_keyframe {
+    float Tcw[16];            /* KeyFrame::GetPose(), row-major */
+    float fx, fy, cx, cy, bf; /* KeyFrame::fx..cy, mbf (edge intrinsics) */
+    int32_t id;               /* KeyFrame::mnId (g2o vertex id) */
+    int32_t fixed;            /* 1 = fixed camera */
+    int32_t pad;
+} spslam_lba_keyframe;
+
+typedef struct spslam_lba_point {
+    float xw[3];              /* MapPoint::GetWorldPos() */
+    int32_t id;               /* MapPoint::mnId */
+    int32_t obs_offset;       /* observations [obs_offset, obs_offset + n_obs) */
+    int32_t n_obs;
+} spslam_lba_point;
+
+typedef struct spslam_lba_point_obs {
+    int32_t kf;               /* index into the problem's keyframes */
+    float u, v;               /* KeyFrame::mvKeysUn[idx].pt */
+    float ur;                 /* KeyFrame::mvuRight[idx]; < 0 -> monocular edge */
+    float inv_sigma2;         /* KeyFrame::mvInvLevelSigma2[octave] */
+} spslam_lba_point_obs;
+
+typedef struct spslam_lba_plane {
+    float world[4];           /* MapPlane::GetWorldPos() */
+    int32_t id;               /* MapPlane::mnId */
+    int32_t obs_offset;
+    int32_t n_obs;
+    int32_t pad;
+} spslam_lba_plane;
+
+typedef struct spslam_lba_plane_obs {
+    int32_t kf;
+    int32_t kind;             /* SPSLAM_PLANE_EDGE / SPSLAM_VERTICAL_EDGE / SPSLAM_PARALLEL_EDGE */
+    float meas[4];            /* KeyFrame::mvPlaneCoefficients[idx] */
+} spslam_lba_plane_obs;
+
+/* One problem of a batch: its keyframes / points / planes start at the given
+ * offsets of the batch arrays; observation offsets inside points / planes are
+ * absolute indices into the batch observation arrays. */
+typedef struct spslam_lba_problem {
+    int32_t n_kf, n_points, n_planes;
+    int32_t kf_offset, point_offset, plane_offset;
+    int32_t n_point_obs, n_plane_obs;   /* total observations of its points / planes */
+} spslam_lba_problem;
+
+typedef struct spslam_lba_result {
+    int32_t iterations[2];    /* LM iterations of optimize(5) / optimize(10) */
+    int32_t n_point_outliers; /* flagged point observations */
+    int32_t n_plane_outliers;
+    int32_t status;           /* 0 ok, < 0 capacity / numerical failure */
+    int32_t pad[3];
+} spslam_lba_result;
+
+/* Drop-in for Optimizer::LocalBundleAdjustment on host buffers, one problem
+ * (offsets inside *problem are ignored; observation offsets index obs arrays).
+ * kf_out: 16 floats per keyframe (local keyframes optimised, fixed ones
+ * copied), pt_out 3 per point, pl_out 4 per plane, outlier flags per
+ * observation.  cfg = the Plane.* config keys (as for PoseOptimization). */
+int spslam_lba_optimize(spslam_ctx* ctx, const spslam_lba_problem* problem, const spslam_lba_keyframe* kfs,
+                        const spslam_lba_point* points, const spslam_lba_point_obs* point_obs,
+                        const spslam_lba_plane* planes, const spslam_lba_plane_obs* plane_obs,
+                        const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
+                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result);
+
+/* Batched, device resident: n problems (host copy `problems` for sizing, the
+ * same records on the device at d_problems), one workgroup each, the whole
+ * optimize(5) / relabel / optimize(10) schedule on the device.  Outputs are
+ * indexed like the inputs (keyframe / point / plane offsets of each problem,
+ * absolute observation indices).  At most 64 keyframes per problem
+ * (status -2 otherwise).  Asynchronous on hip_stream. */
+int spslam_lba_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_lba_problem* problems,
+                                     const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
+                                     const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
+                                     const spslam_lba_plane* d_planes, const spslam_lba_plane_obs* d_plane_obs,
+                                     const spslam_plane_config* cfg, float* d_kf_out, float* d_pt_out,
+                                     float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
+                                     spslam_lba_result* d_results, void* hip_stream);
+
+/* ------------------------------------------------------------------------
  * Plane extraction: Frame::ComputePlanesFromOrganizedPointCloud
  * (include/Frame.h:120, src/Frame.cc:854-936) with the PCL 1.8
  * IntegralImageNormalEstimation + OrganizedMultiPlaneSegmentation it calls.

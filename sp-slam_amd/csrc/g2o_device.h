@@ -1,0 +1,184 @@
+// g2o / Eigen / g2oAddition math on the device (fp64), shared by the
+// PoseOptimization (pose_kernels.hip) and LocalBundleAdjustment
+// (lba_kernels.hip) kernels: SE3Quat (Thirdparty/g2o/g2o/types/se3quat.h),
+// Eigen quaternion / rotation conversions, g2oAddition/Plane3D.h.
+// See oracle/g2o_restated.h for the CPU restatement of the same routines.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace spslam {
+namespace g2od {
+
+struct V3 { double x, y, z; };
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {
+    return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+
+struct Q { double w, x, y, z; };
+struct SE3 { Q r; V3 t; };
+struct M3 { double a[9]; };  // row-major
+
+__device__ __forceinline__ V3 mv(const M3& R, V3 v) {
+    return {R.a[0] * v.x + R.a[1] * v.y + R.a[2] * v.z, R.a[3] * v.x + R.a[4] * v.y + R.a[5] * v.z,
+            R.a[6] * v.x + R.a[7] * v.y + R.a[8] * v.z};
+}
+__device__ __forceinline__ V3 mtv(const M3& R, V3 v) {  // R^T v
+    return {R.a[0] * v.x + R.a[3] * v.y + R.a[6] * v.z, R.a[1] * v.x + R.a[4] * v.y + R.a[7] * v.z,
+            R.a[2] * v.x + R.a[5] * v.y + R.a[8] * v.z};
+}
+
+// Eigen Quaternion(Matrix3)
+__device__ Q q_from_rot(const M3& R) {
+    Q q;
+    double t = R.a[0] + R.a[4] + R.a[8];
+    if (t > 0) {
+        t = sqrt(t + 1.0);
+        q.w = 0.5 * t;
+        t = 0.5 / t;
+        q.x = (R.a[7] - R.a[5]) * t;
+        q.y = (R.a[2] - R.a[6]) * t;
+        q.z = (R.a[3] - R.a[1]) * t;
+    } else {
+        int i = 0;
+        if (R.a[4] > R.a[0]) i = 1;
+        if (R.a[8] > R.a[4 * i]) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = sqrt(R.a[4 * i] - R.a[4 * j] - R.a[4 * k] + 1.0);
+        const double ci = 0.5 * t;
+        t = 0.5 / t;
+        q.w = (R.a[3 * k + j] - R.a[3 * j + k]) * t;
+        const double cj = (R.a[3 * j + i] + R.a[3 * i + j]) * t;
+        const double ck = (R.a[3 * k + i] + R.a[3 * i + k]) * t;
+        q.x = i == 0 ? ci : (j == 0 ? cj : ck);
+        q.y = i == 1 ? ci : (j == 1 ? cj : ck);
+        q.z = i == 2 ? ci : (j == 2 ? cj : ck);
+    }
+    return q;
+}
+__device__ M3 q_to_rot(const Q& q) {
+    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
+    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
+    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
+    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
+    return M3{{1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx, txz - twy, tyz + twx,
+               1 - (txx + tyy)}};
+}
+__device__ __forceinline__ Q q_mul(const Q& a, const Q& b) {
+    return {a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z, a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y,
+            a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z, a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ V3 q_rot(const Q& q, V3 v) {  // Eigen _transformVector
+    const V3 qv{q.x, q.y, q.z};
+    V3 uv = cross(qv, v);
+    uv = uv + uv;
+    return v + q.w * uv + cross(qv, uv);
+}
+__device__ __forceinline__ void q_normalize(Q& q) {  // SE3Quat::normalizeRotation
+    if (q.w < 0) { q.w = -q.w; q.x = -q.x; q.y = -q.y; q.z = -q.z; }
+    const double n = sqrt(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z);
+    q.w /= n; q.x /= n; q.y /= n; q.z /= n;
+}
+__device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
+    SE3 r = a;
+    r.t = r.t + q_rot(a.r, b.t);
+    r.r = q_mul(r.r, b.r);
+    q_normalize(r.r);
+    return r;
+}
+// SE3Quat::exp (types/se3quat.h:223-257)
+__device__ SE3 se3_exp(const double* u) {
+    const V3 w{u[0], u[1], u[2]}, ups{u[3], u[4], u[5]};
+    const double theta = sqrt(dot(w, w));
+    const double O[9] = {0, -w.z, w.y, w.z, 0, -w.x, -w.y, w.x, 0};
+    double O2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) O2[3 * i + j] = O[3 * i] * O[j] + O[3 * i + 1] * O[3 + j] + O[3 * i + 2] * O[6 + j];
+    M3 R, V;
+    if (theta < 0.00001) {
+        for (int k = 0; k < 9; k++) R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
+        V = R;
+    } else {
+        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta),
+                     c = (theta - sin(theta)) / pow(theta, 3);
+        for (int k = 0; k < 9; k++) {
+            R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
+            V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
+        }
+    }
+    SE3 s;
+    s.r = q_from_rot(R);
+    s.t = mv(V, ups);
+    q_normalize(s.r);
+    return s;
+}
+
+// ---- g2oAddition/Plane3D.h ------------------------------------------------
+struct P4 { double c[4]; };
+__device__ __forceinline__ void p_normalize(double* v) {
+    const double n = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    for (int i = 0; i < 4; i++) v[i] = v[i] * (1. / n);
+    if (v[3] < 0.0)
+        for (int i = 0; i < 4; i++) v[i] = -v[i];
+}
+__device__ __forceinline__ double azimuth(V3 v) { return atan2(v.y, v.x); }
+__device__ __forceinline__ double elevation(V3 v) { return atan2(v.z, sqrt(v.x * v.x + v.y * v.y)); }
+// Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
+__device__ M3 p_rotation(V3 v) {
+    const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
+    const Q a{cos(ha), 0.0 * sin(ha), 0.0 * sin(ha), 1.0 * sin(ha)};
+    const Q e{cos(he), 0.0 * sin(he), 1.0 * sin(he), 0.0 * sin(he)};
+    return q_to_rot(q_mul(a, e));
+}
+// Eigen AngleAxis::toRotationMatrix() * v
+__device__ V3 aa_apply(double ang, V3 ax, V3 v) {
+    const V3 sa = sin(ang) * ax;
+    const double c = cos(ang);
+    const V3 c1 = (1 - c) * ax;
+    M3 r;
+    double tmp;
+    tmp = c1.x * ax.y; r.a[1] = tmp - sa.z; r.a[3] = tmp + sa.z;
+    tmp = c1.x * ax.z; r.a[2] = tmp + sa.y; r.a[6] = tmp - sa.y;
+    tmp = c1.y * ax.z; r.a[5] = tmp - sa.x; r.a[7] = tmp + sa.x;
+    r.a[0] = c1.x * ax.x + c; r.a[4] = c1.y * ax.y + c; r.a[8] = c1.z * ax.z + c;
+    return mv(r, v);
+}
+
+// plane-edge error: (T * world).ominus{,_par,_ver}(meas)
+__device__ void plane_error(int kind, const SE3& T, const P4& world, const P4& meas, double* e) {
+    const M3 R = q_to_rot(T.r);
+    const V3 n2 = mv(R, V3{world.c[0], world.c[1], world.c[2]});
+    double v[4] = {n2.x, n2.y, n2.z, world.c[3] - dot(T.t, n2)};
+    if (v[3] < 0.0)
+        for (int i = 0; i < 4; i++) v[i] = -v[i];
+    p_normalize(v);
+    const V3 ln{v[0], v[1], v[2]}, mn{meas.c[0], meas.c[1], meas.c[2]};
+    V3 ref = ln;
+    if (kind == 1) {
+        if (dot(mn, ln) < 0) ref = -1.0 * ln;
+    } else if (kind == 2) {
+        const V3 a = cross(ln, mn);
+        ref = aa_apply(M_PI / 2, (1.0 / sqrt(dot(a, a))) * a, ln);
+    }
+    const V3 n = mtv(p_rotation(ref), mn);
+    e[0] = azimuth(n);
+    e[1] = elevation(n);
+    if (kind == 0) e[2] = (-v[3]) - (-meas.c[3]);
+}
+
+// Plane3D::oplus (g2oAddition/Plane3D.h:72-85)
+__device__ void p_oplus(P4& p, const double* v) {
+    const double s = sin(v[1]), c = cos(v[1]);
+    const V3 n{c * cos(v[0]), c * sin(v[0]), s};
+    const M3 R = p_rotation(V3{p.c[0], p.c[1], p.c[2]});
+    const double d = -p.c[3] + v[2];
+    const V3 rn = mv(R, n);
+    p.c[0] = rn.x; p.c[1] = rn.y; p.c[2] = rn.z;
+    p.c[3] = -d;
+    p_normalize(p.c);
+}
+
+}  // namespace g2od
+}  // namespace spslam

@@ -1,0 +1,57 @@
+// Host-side entry points of lba_kernels.hip (Optimizer::LocalBundleAdjustment).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/spslam_gpu.h"
+#include "orb_launch.h"
+
+namespace spslam {
+
+constexpr int kLbaMaxKeyframes = 64;   // local + fixed keyframes per problem (pose masks are 64-bit)
+
+// Per-problem scratch layout (bytes), computed identically on host and device.
+struct LbaLayout {
+    size_t pose, pose_b, pt, pt_b, pl, pl_b, e_err, e_con, lm_H, lm_b, lm_Dinv, lm_db, lm_x, blk_H, blk_BD, S, bs,
+        dd, y, Hpp, bp;                                                      // double arrays
+    size_t pose_hidx, hidx_pose, e_lm, e_kf, e_type, e_level, e_blk, e_src, lm_boff, lm_nb, blk_pose, lm_act;  // int
+    size_t lm_mask;                                                          // uint64
+    size_t bytes;
+};
+
+constexpr int kLbaCon = 57;  // per-edge contribution: Hll 9, bl 3, Hpl 18 (3x6), Hpp upper 21, bp 6
+
+__host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
+    LbaLayout L{};
+    const size_t Lm = (size_t)Np + Nq, n6 = 6 * (size_t)K;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
+    L.pose = take(K * 7 * 8); L.pose_b = take(K * 7 * 8);
+    L.pt = take(Np * 3 * 8); L.pt_b = take(Np * 3 * 8);
+    L.pl = take(Nq * 4 * 8); L.pl_b = take(Nq * 4 * 8);
+    L.e_err = take((size_t)E * 3 * 8); L.e_con = take((size_t)E * kLbaCon * 8);
+    L.lm_H = take(Lm * 9 * 8); L.lm_b = take(Lm * 3 * 8); L.lm_Dinv = take(Lm * 9 * 8);
+    L.lm_db = take(Lm * 3 * 8); L.lm_x = take(Lm * 3 * 8);
+    L.blk_H = take((size_t)E * 18 * 8); L.blk_BD = take((size_t)E * 18 * 8);
+    L.S = take(n6 * n6 * 8); L.bs = take(n6 * 8); L.dd = take(n6 * 8); L.y = take(n6 * 8);
+    L.Hpp = take(K * 36 * 8); L.bp = take(K * 6 * 8);
+    L.pose_hidx = take(K * 4); L.hidx_pose = take(K * 4);
+    L.e_lm = take((size_t)E * 4); L.e_kf = take((size_t)E * 4); L.e_type = take((size_t)E * 4);
+    L.e_level = take((size_t)E * 4); L.e_blk = take((size_t)E * 4); L.e_src = take((size_t)E * 4);
+    L.lm_boff = take(Lm * 4); L.lm_nb = take(Lm * 4); L.blk_pose = take((size_t)E * 4); L.lm_act = take(Lm * 4);
+    L.lm_mask = take(Lm * 8);
+    L.bytes = o;
+    return L;
+}
+
+struct LbaConsts {
+    double angle_info, dis_info, par_info, ver_info, plane_chi, vp_chi;  // Optimizer.cc:1489-1500
+    double delta_mono, delta_stereo, delta_plane, delta_vp;             // Huber deltas (float sqrt, as g2o gets them)
+};
+
+hipError_t lba_launch(int n, const spslam_lba_problem* d_probs, const long long* d_scratch_off,
+                      const spslam_lba_keyframe* kfs, const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                      const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs, const LbaConsts& C,
+                      uint8_t* scratch, float* kf_out, float* pt_out, float* pl_out, uint8_t* pobs_out,
+                      uint8_t* plobs_out, spslam_lba_result* res, hipStream_t s, KernelTimer* timer);
+
+}  // namespace spslam

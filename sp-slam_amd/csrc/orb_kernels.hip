@@ -790,7 +790,8 @@ const char* kernel_kind_name(int kind) {
                                                  "desc_kernel", "pose_kernel", "plane_cloud_kernel", "plane_distance_kernel",
                                                  "plane_integral_kernel", "plane_normal_kernel",
                                                  "plane_segment_kernel", "supp_lines_kernel",
-                                                 "supp_assemble_kernel", "frame_rgbd_kernel"};
+                                                 "supp_assemble_kernel", "frame_rgbd_kernel",
+                                                 "lba_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

@@ -21,6 +21,7 @@
 #include "pose_launch.h"
 #include "supposed_launch.h"
 #include "frame_launch.h"
+#include "lba_launch.h"
 
 using namespace spslam;
 
@@ -116,6 +117,13 @@ struct spslam_ctx {
     bool frame_ready = false;
     FrameGeom fg{};
     uint8_t* d_frame1 = nullptr;  // single-frame staging: kps, keys_un, depth, uR, grid_off, grid_idx, count
+    // LocalBundleAdjustment scratch (grown on demand)
+    uint8_t* d_lba_scratch = nullptr;
+    size_t lba_scratch_bytes = 0;
+    long long* d_lba_off = nullptr;
+    int lba_off_cap = 0;
+    uint8_t* d_lba_stage = nullptr;   // drop-in staging
+    size_t lba_stage_bytes = 0;
 };
 
 namespace {
@@ -237,7 +245,8 @@ void free_all(spslam_ctx* c) {
                     c->b.keynode, c->b.lvl_kp, c->b.lvl_cnt,       c->d_in,           c->d_kps,
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
-                    c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1};
+                    c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1,
+                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -893,6 +902,106 @@ int spslam_frame_rgbd(spslam_ctx* c, const spslam_keypoint* kps, int n, const fl
     if (ng) HIP_CHECK(c, hipMemcpy(grid_idx, d_gi, (size_t)ng * 4, hipMemcpyDeviceToHost));
     HIP_CHECK(c, hipFreeAsync(d_depth, c->stream));
     return SPSLAM_OK;
+}
+
+int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_problem* problems,
+                                     const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
+                                     const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
+                                     const spslam_lba_plane* d_planes, const spslam_lba_plane_obs* d_plane_obs,
+                                     const spslam_plane_config* cfg, float* d_kf_out, float* d_pt_out,
+                                     float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
+                                     spslam_lba_result* d_results, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n < 1 || !problems || !d_problems || !d_kfs || !cfg || !d_kf_out || !d_results)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
+    std::vector<long long> off(n);
+    size_t total = 0;
+    for (int i = 0; i < n; i++) {
+        const spslam_lba_problem& p = problems[i];
+        if (p.n_kf < 0 || p.n_points < 0 || p.n_planes < 0 || p.n_point_obs < 0 || p.n_plane_obs < 0)
+            return fail(c, SPSLAM_ERR_ARG, "negative count in LBA problem%s", "");
+        if ((p.n_points && (!d_points || !d_point_obs || !d_pt_out || !d_point_obs_outlier)) ||
+            (p.n_planes && (!d_planes || !d_plane_obs || !d_pl_out || !d_plane_obs_outlier)))
+            return fail(c, SPSLAM_ERR_ARG, "missing LBA buffers%s", "");
+        off[i] = (long long)total;
+        total += lba_layout(p.n_kf, p.n_points, p.n_planes, p.n_point_obs + p.n_plane_obs).bytes;
+    }
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    if (total > c->lba_scratch_bytes) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_lba_scratch) (void)hipFree(c->d_lba_scratch);
+        c->d_lba_scratch = nullptr;
+        c->lba_scratch_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_lba_scratch, total));
+        c->lba_scratch_bytes = total;
+    }
+    if (n > c->lba_off_cap) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_lba_off) (void)hipFree(c->d_lba_off);
+        c->d_lba_off = nullptr;
+        HIP_CHECK(c, hipMalloc(&c->d_lba_off, (size_t)n * sizeof(long long)));
+        c->lba_off_cap = n;
+    }
+    HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
+    LbaConsts C{};
+    C.angle_info = 3282.8 / (cfg->angle_info * cfg->angle_info);
+    C.dis_info = cfg->distance_info * cfg->distance_info;
+    C.par_info = 3282.8 / (cfg->parallel_info * cfg->parallel_info);
+    C.ver_info = 3282.8 / (cfg->vertical_info * cfg->vertical_info);
+    C.plane_chi = cfg->chi;
+    C.vp_chi = cfg->vp_chi;
+    C.delta_mono = (float)std::sqrt(5.991);     // const float thHuberMono = sqrt(5.991)
+    C.delta_stereo = (float)std::sqrt(7.815);
+    C.delta_plane = (float)std::sqrt(cfg->chi);  // const float deltaPlane = sqrt(planeChi)
+    C.delta_vp = (float)std::sqrt(cfg->vp_chi);
+    HIP_CHECK(c, lba_launch(n, d_problems, c->d_lba_off, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs, C,
+                            c->d_lba_scratch, d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier,
+                            d_results, s, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_lba_optimize(spslam_ctx* c, const spslam_lba_problem* problem, const spslam_lba_keyframe* kfs,
+                        const spslam_lba_point* points, const spslam_lba_point_obs* point_obs,
+                        const spslam_lba_plane* planes, const spslam_lba_plane_obs* plane_obs,
+                        const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
+                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result) {
+    if (!c || !problem || !cfg || !result) return SPSLAM_ERR_ARG;
+    spslam_lba_problem P = *problem;
+    P.kf_offset = P.point_offset = P.plane_offset = 0;
+    const size_t nk = P.n_kf, np = P.n_points, nq = P.n_planes, npo = P.n_point_obs, nqo = P.n_plane_obs;
+    if ((nk && (!kfs || !kf_out)) || (np && (!points || !pt_out)) || (nq && (!planes || !pl_out)) ||
+        (npo && (!point_obs || !point_obs_outlier)) || (nqo && (!plane_obs || !plane_obs_outlier)))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    size_t sz[] = {sizeof P,
+                   nk * sizeof(spslam_lba_keyframe), np * sizeof(spslam_lba_point), npo * sizeof(spslam_lba_point_obs),
+                   nq * sizeof(spslam_lba_plane), nqo * sizeof(spslam_lba_plane_obs), nk * 64, np * 12, nq * 16,
+                   npo, nqo, sizeof(spslam_lba_result)};
+    size_t bytes = 0, o[12];
+    for (int i = 0; i < 12; i++) { o[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    if (bytes > c->lba_stage_bytes) {
+        if (c->d_lba_stage) (void)hipFree(c->d_lba_stage);
+        c->d_lba_stage = nullptr;
+        c->lba_stage_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_lba_stage, bytes));
+        c->lba_stage_bytes = bytes;
+    }
+    uint8_t* q = c->d_lba_stage;
+    const void* src[] = {&P, kfs, points, point_obs, planes, plane_obs};
+    for (int i = 0; i < 6; i++)
+        if (sz[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], sz[i], hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_lba_optimize_batch_device(
+        c, 1, &P, (const spslam_lba_problem*)(q + o[0]), (const spslam_lba_keyframe*)(q + o[1]),
+        (const spslam_lba_point*)(q + o[2]), (const spslam_lba_point_obs*)(q + o[3]),
+        (const spslam_lba_plane*)(q + o[4]), (const spslam_lba_plane_obs*)(q + o[5]), cfg, (float*)(q + o[6]),
+        (float*)(q + o[7]), (float*)(q + o[8]), q + o[9], q + o[10], (spslam_lba_result*)(q + o[11]), c->stream);
+    if (rc) return rc;
+    void* dst[] = {kf_out, pt_out, pl_out, point_obs_outlier, plane_obs_outlier, result};
+    for (int i = 0; i < 6; i++)
+        if (sz[6 + i]) HIP_CHECK(c, hipMemcpyAsync(dst[i], q + o[6 + i], sz[6 + i], hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return result->status == 0 ? SPSLAM_OK : fail(c, SPSLAM_ERR_ARG, "LBA problem rejected (status %s)", "< 0");
 }
 
 int spslam_set_timing(spslam_ctx* c, int enable) {

@@ -1,0 +1,68 @@
+"""ctypes binding of the LocalBundleAdjustment part of include/spslam_gpu.h
+(Optimizer::LocalBundleAdjustment on gfx950) and the numpy record types of
+its flattened graph."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+import spslam_gpu
+
+LBA_KEYFRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"), ("cx", "<f4"), ("cy", "<f4"),
+                               ("bf", "<f4"), ("id", "<i4"), ("fixed", "<i4"), ("pad", "<i4")])
+LBA_POINT_DTYPE = np.dtype([("xw", "<f4", 3), ("id", "<i4"), ("obs_offset", "<i4"), ("n_obs", "<i4")])
+LBA_POINT_OBS_DTYPE = np.dtype([("kf", "<i4"), ("u", "<f4"), ("v", "<f4"), ("ur", "<f4"), ("inv_sigma2", "<f4")])
+LBA_PLANE_DTYPE = np.dtype([("world", "<f4", 4), ("id", "<i4"), ("obs_offset", "<i4"), ("n_obs", "<i4"),
+                            ("pad", "<i4")])
+LBA_PLANE_OBS_DTYPE = np.dtype([("kf", "<i4"), ("kind", "<i4"), ("meas", "<f4", 4)])
+LBA_PROBLEM_DTYPE = np.dtype([("n_kf", "<i4"), ("n_points", "<i4"), ("n_planes", "<i4"), ("kf_offset", "<i4"),
+                              ("point_offset", "<i4"), ("plane_offset", "<i4"), ("n_point_obs", "<i4"),
+                              ("n_plane_obs", "<i4")])
+LBA_RESULT_DTYPE = np.dtype([("iterations", "<i4", 2), ("n_point_outliers", "<i4"), ("n_plane_outliers", "<i4"),
+                             ("status", "<i4"), ("pad", "<i4", 3)])
+assert LBA_KEYFRAME_DTYPE.itemsize == 96 and LBA_POINT_DTYPE.itemsize == 24
+assert LBA_POINT_OBS_DTYPE.itemsize == 20 and LBA_PLANE_DTYPE.itemsize == 32
+assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 32
+
+
+spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device"]
+
+PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # TUM yaml Plane.* keys
+
+
+def _bind(lib):
+    vp = ctypes.c_void_p
+    lib.spslam_lba_optimize.argtypes = [vp] * 14
+    lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 15
+
+
+class LocalBA:
+    """GPU Optimizer::LocalBundleAdjustment on a context (shares its stream/device)."""
+
+    def __init__(self, ex: spslam_gpu.OrbExtractor, cfg=PLANE_CONFIG):
+        self.ex = ex
+        _bind(ex.lib)
+        self.cfg = np.ascontiguousarray(cfg, np.float64)
+
+    def __call__(self, prob, kfs, points, point_obs, planes, plane_obs):
+        arrs = [np.ascontiguousarray(a) for a in (prob, kfs, points, point_obs, planes, plane_obs)]
+        kf_out = np.zeros((max(len(kfs), 1), 16), np.float32)
+        pt_out = np.zeros((max(len(points), 1), 3), np.float32)
+        pl_out = np.zeros((max(len(planes), 1), 4), np.float32)
+        po = np.zeros(max(len(point_obs), 1), np.uint8)
+        plo = np.zeros(max(len(plane_obs), 1), np.uint8)
+        res = np.zeros((), LBA_RESULT_DTYPE)
+        ptr = lambda a: a.ctypes.data if a.size else None  # noqa: E731
+        self.ex._check(self.ex.lib.spslam_lba_optimize(
+            self.ex.ctx, *[ptr(a) for a in arrs], self.cfg.ctypes.data, kf_out.ctypes.data, pt_out.ctypes.data,
+            pl_out.ctypes.data, po.ctypes.data, plo.ctypes.data, res.ctypes.data))
+        return dict(Tcw=kf_out[:len(kfs)], points=pt_out[:len(points)], planes=pl_out[:len(planes)],
+                    point_outlier=po[:len(point_obs)], plane_outlier=plo[:len(plane_obs)], result=res)
+
+    def batch_device(self, n, problems_host, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
+                     d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream=0):
+        ph = np.ascontiguousarray(problems_host)
+        self.ex._check(self.ex.lib.spslam_lba_optimize_batch_device(
+            self.ex.ctx, n, ph.ctypes.data, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
+            self.cfg.ctypes.data, d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream or None))

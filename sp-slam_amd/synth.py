@@ -270,3 +270,102 @@ def pose_problem(scene: Scene, frame: int, kps, depth_u16, fid, inv_level_sigma2
     prob["fx"], prob["fy"], prob["cx"], prob["cy"], prob["bf"] = fx, fy, cx, cy, bf
     prob["n_points"], prob["n_planes"] = len(points), len(planes)
     return prob, points, planes, Tcw
+
+
+def lba_problem(scene: Scene, kf_frames, rng, n_fixed=2, n_points=1500, K=TUM3, stereo_frac=0.9,
+                outlier_frac=0.04, pix_noise=1.0, pose_rot_deg=0.4, pose_trans=0.02, point_noise=0.02,
+                plane_noise_deg=0.5, plane_noise_d=0.01, first_kf_id=1, with_planes=True):
+    """A LocalBundleAdjustment graph over keyframes at `kf_frames` (the first
+    len - n_fixed are local, the rest fixed cameras): map points sampled on the
+    scene faces, observed by every keyframe that sees them in the image,
+    room / box planes with observation, parallel and vertical edges.  Returns
+    (problem, keyframes, points, point_obs, planes, plane_obs, ground truth)
+    in the record types of spslam_lba."""
+    import spslam_lba as L
+    fx, fy, cx, cy, bf = K["fx"], K["fy"], K["cx"], K["cy"], K["bf"]
+    n_kf = len(kf_frames)
+    Tcw_gt = [np.linalg.inv(scene.pose(f)) for f in kf_frames]
+    kfs = np.zeros(n_kf, L.LBA_KEYFRAME_DTYPE)
+    for k, f in enumerate(kf_frames):
+        T = Tcw_gt[k].copy()
+        fixed = k >= n_kf - n_fixed
+        if not fixed:
+            T[:3, :3] = _rot(rng.normal(0, np.deg2rad(pose_rot_deg), 3)) @ T[:3, :3]
+            T[:3, 3] = T[:3, 3] + rng.normal(0, pose_trans, 3)
+        kfs[k]["Tcw"] = T.astype(np.float32).ravel()
+        kfs[k]["fx"], kfs[k]["fy"], kfs[k]["cx"], kfs[k]["cy"], kfs[k]["bf"] = fx, fy, cx, cy, bf
+        kfs[k]["id"] = first_kf_id + k
+        kfs[k]["fixed"] = int(fixed)
+    inv_s2 = [1.0 / (1.2 ** (2 * o)) for o in range(8)]
+    # map points on faces in front of the cameras
+    pts, obs = [], []
+    faces = scene.faces
+    tries = 0
+    while len(pts) < n_points and tries < 50 * n_points:
+        tries += 1
+        face = faces[rng.integers(len(faces))]
+        o = [a for a in range(3) if a != face.axis]
+        X = np.zeros(3)
+        X[face.axis] = face.offset
+        X[o] = rng.uniform(face.lo, face.hi)
+        seen = []
+        for k in range(n_kf):
+            Xc = Tcw_gt[k][:3, :3] @ X + Tcw_gt[k][:3, 3]
+            if Xc[2] < 0.3:
+                continue
+            u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+            if 10 <= u < 630 and 10 <= v < 470 and rng.random() < 0.85:
+                seen.append((k, u, v, Xc[2]))
+        if len(seen) < 2:
+            continue
+        pid = len(pts)
+        off = len(obs)
+        for k, u, v, z in seen:
+            oc = int(rng.integers(8))
+            if rng.random() < outlier_frac:
+                u, v = rng.uniform(10, 630), rng.uniform(10, 470)
+            else:
+                u, v = u + rng.normal(0, pix_noise), v + rng.normal(0, pix_noise)
+            ur = u - bf / (z + rng.normal(0, 0.002 * z * z)) if rng.random() < stereo_frac else -1.0
+            obs.append((k, u, v, ur, inv_s2[oc]))
+        Xn = X + rng.normal(0, point_noise, 3)
+        pts.append((Xn.astype(np.float32), 1000 + 3 * pid, off, len(seen)))
+    points = np.array(pts, L.LBA_POINT_DTYPE)
+    point_obs = np.array(obs, L.LBA_POINT_OBS_DTYPE)
+    # planes: faces seen (plane passing in front) by at least two keyframes
+    planes, pobs = [], []
+    if with_planes:
+        room = list(range(min(6, len(faces)))) + list(range(6, len(faces)))[:4]
+        vis = {}
+        for j in room:
+            wp = face_plane(faces[j])
+            ks = [k for k in range(n_kf) if transform_plane(Tcw_gt[k], wp)[3] > 0.3]
+            if len(ks) >= 2:
+                vis[j] = ks
+        for j, ks in vis.items():
+            wp = face_plane(faces[j])
+            off = len(pobs)
+            cnt = 0
+            for kind in (0, 2, 1):  # observations, vertical, parallel (Optimizer.cc:1501-1613)
+                for k in ks:
+                    if kind == 0:
+                        m = j
+                    else:
+                        cand = [q for q in vis if q != j and ((faces[q].axis == faces[j].axis) == (kind == 1))]
+                        if not cand or rng.random() < 0.6:
+                            continue
+                        m = cand[rng.integers(len(cand))]
+                    cp = transform_plane(Tcw_gt[k], face_plane(faces[m]))
+                    Rn = _rot(rng.normal(0, np.deg2rad(plane_noise_deg), 3))
+                    meas = np.array([*(Rn @ cp[:3]), cp[3] + rng.normal(0, plane_noise_d)])
+                    pobs.append((k, kind, meas.astype(np.float32)))
+                    cnt += 1
+            Rn = _rot(rng.normal(0, np.deg2rad(plane_noise_deg), 3))
+            wn = np.array([*(Rn @ wp[:3]), wp[3] + rng.normal(0, plane_noise_d)])
+            planes.append((wn.astype(np.float32), 7 + j, off, cnt, 0))
+    planes = np.array(planes, L.LBA_PLANE_DTYPE) if planes else np.zeros(0, L.LBA_PLANE_DTYPE)
+    plane_obs = np.array(pobs, L.LBA_PLANE_OBS_DTYPE) if pobs else np.zeros(0, L.LBA_PLANE_OBS_DTYPE)
+    prob = np.zeros((), L.LBA_PROBLEM_DTYPE)
+    prob["n_kf"], prob["n_points"], prob["n_planes"] = n_kf, len(points), len(planes)
+    prob["n_point_obs"], prob["n_plane_obs"] = len(point_obs), len(plane_obs)
+    return prob, kfs, points, point_obs, planes, plane_obs, dict(Tcw=np.array(Tcw_gt))
