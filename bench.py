@@ -36,6 +36,10 @@ CONFIGS = {
                workload="C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud "
                         "plane extraction + supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), "
                         "no LBA"),
+    # configs[2]: full pipeline incl. LocalBundleAdjustment (a keyframe every 5 frames, 12-keyframe local maps)
+    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=3, lba_every=5,
+               workload="C3 (synthetic proxy): C2 + LocalBundleAdjustment with plane/parallel/perpendicular edges "
+                        "for every 5th frame (12 keyframes, 1500 points per local map)"),
     # configs[4]: 1280x960, nFeatures=4000, dense-plane scene
     "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8,
                workload="C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + supposed planes + "
@@ -57,7 +61,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return out
 
 
-def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0):
+def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -79,6 +83,7 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0):
         "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
         "supp_assemble_kernel": n_sup * (64 + 2601 * 12),     # appended planes + synthetic patches out
         "frame_rgbd_kernel": n_kp * (28 + 4 + 28 + 4 + 4 + 4) + 4 * 3073,  # kp in, depth gather, kp/depth/uR/idx out
+        "lba_kernel": lba_bytes,                              # graph in + poses/points/planes/flags out, per problem
     }
 
 
@@ -103,6 +108,7 @@ def cpu_baseline(hp, budget_s=12.0):
     import numpy as np
     import oracle_ctypes
     import oracle_planes
+    import oracle_lba
     import oracle_supposed
     orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     po = oracle_planes.PlaneOracle()
@@ -121,11 +127,13 @@ def cpu_baseline(hp, budget_s=12.0):
         pb = pb.copy()
         pb["Tcw"] = r1["Tcw"]
         oracle_ctypes.pose_optimize(pb, pts2, pls2)
+        if hp.n_lba and n % hp.lba_every == 0:  # LocalMapping: one local BA per keyframe
+            oracle_lba.lba_optimize(*hp.lba_problems[(n // hp.lba_every) % len(hp.lba_problems)][:6])
         n += 1
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + 2x PoseOptimization), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + 2x PoseOptimization{' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -152,7 +160,8 @@ def main():
 
     import pipeline
     hp = pipeline.HotPath(args.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"],
-                          unique_frames=args.unique_frames, device=local, **shard_of(rank))
+                          unique_frames=args.unique_frames, device=local, lba_every=cfg.get("lba_every", 0),
+                          **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
     torch.cuda.synchronize()
@@ -180,7 +189,10 @@ def main():
     n_con = float(res["contour_points"].mean())
     n_sup = float(res["supposed_counts"].mean())
     n_brd = float(res["line_points"].mean())
-    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup)
+    lba_bytes = 0
+    if hp.n_lba:  # per frame: the keyframe's local map in (records) and its results out
+        lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
+    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step

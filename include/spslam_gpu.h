@@ -256,7 +256,10 @@ typedef struct spslam_lba_result {
     int32_t n_point_outliers; /* flagged point observations */
     int32_t n_plane_outliers;
     int32_t status;           /* 0 ok, < 0 capacity / numerical failure */
-    int32_t pad[3];
+    int32_t trials;           /* LM trials (lambda steps) in total */
+    int32_t pad[2];
+    float phase_us[8];        /* diagnostics: device time per phase (setup, errors, edge terms, block sums,
+                                 Schur, factorisation, substitution, update), microseconds */
 } spslam_lba_result;
 
 /* Drop-in for Optimizer::LocalBundleAdjustment on host buffers, one problem

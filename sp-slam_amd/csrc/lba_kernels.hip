@@ -38,7 +38,7 @@ namespace lba {
 
 using namespace g2od;
 
-constexpr int kThreads = 512, kWaves = kThreads / 64;
+constexpr int kThreads = 256, kWaves = kThreads / 64;
 
 struct Shared {
     double red[kWaves][8];
@@ -49,7 +49,19 @@ struct Shared {
     int hidx_pose[kLbaMaxKeyframes];
     int pose_act[kLbaMaxKeyframes];
     int wsum[kWaves];
+    long long t_phase[8];   // wall_clock64 ticks per phase (100 MHz), thread 0
+    long long t_mark;
+    int trials;
 };
+
+// Phase timer (diagnostics): thread 0 charges the time since the last mark to phase p.
+__device__ __forceinline__ void mark(Shared& S, int p) {
+    if (threadIdx.x == 0) {
+        const long long now = wall_clock64();
+        S.t_phase[p] += now - S.t_mark;
+        S.t_mark = now;
+    }
+}
 
 struct Ctx {
     int K, Np, Nq, E, Ep, L;
@@ -288,7 +300,8 @@ __device__ void edge_jacobians(const Ctx& c, int e, bool pose_free, double (&A)[
         P = P0;
         p_oplus(P, add);
         plane_edge_error(t, T, P, meas, em);
-        for (int i = 0; i < dim; i++) A[i][d] = scalar * (ep[i] - em[i]);
+#pragma unroll
+        for (int i = 0; i < 3; i++) A[i][d] = i < dim ? scalar * (ep[i] - em[i]) : 0.0;
     }
     if (!pose_free) return;
     for (int d = 0; d < 6; d++) {
@@ -297,7 +310,8 @@ __device__ void edge_jacobians(const Ctx& c, int e, bool pose_free, double (&A)[
         plane_edge_error(t, se3_mul(se3_exp(add), T), P0, meas, ep);
         add[d] = -delta;
         plane_edge_error(t, se3_mul(se3_exp(add), T), P0, meas, em);
-        for (int i = 0; i < dim; i++) B[i][d] = scalar * (ep[i] - em[i]);
+#pragma unroll
+        for (int i = 0; i < 3; i++) B[i][d] = i < dim ? scalar * (ep[i] - em[i]) : 0.0;
     }
 }
 
@@ -398,44 +412,41 @@ __device__ double build_system(Ctx& c, const LbaConsts& C, bool robust, Shared& 
         const double* err = c.err + 3 * e;
         double r0, w;
         huber(chi2_of(err, info, dim), delta_of(C, ty), robust, &r0, &w);
-        double W[3], om[3];
-        for (int r = 0; r < dim; r++) {
-            W[r] = robust ? w * info[r] : info[r];
-            om[r] = -(info[r] * err[r]);
-            if (robust) om[r] *= w;
-        }
+        double W[3] = {0, 0, 0}, om[3] = {0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            if (r < dim) {
+                W[r] = robust ? w * info[r] : info[r];
+                om[r] = -(info[r] * err[r]);
+                if (robust) om[r] *= w;
+            }
+        // rows >= dim of A, B, W, om are zero: the padded terms add exact zeros
         double* o = c.con + (size_t)kLbaCon * e;
+#pragma unroll
         for (int i = 0; i < 3; i++) {
-            double s = A[0][i] * om[0];
-            for (int r = 1; r < dim; r++) s += A[r][i] * om[r];
-            o[9 + i] = s;
-            for (int j = 0; j < 3; j++) {
-                double h = (A[0][i] * W[0]) * A[0][j];
-                for (int r = 1; r < dim; r++) h += (A[r][i] * W[r]) * A[r][j];
-                o[3 * i + j] = h;
-            }
-            for (int j = 0; j < 6; j++) {
-                double h = (A[0][i] * W[0]) * B[0][j];
-                for (int r = 1; r < dim; r++) h += (A[r][i] * W[r]) * B[r][j];
-                o[12 + 6 * i + j] = pfree ? h : 0.0;
-            }
+            o[9 + i] = (A[0][i] * om[0] + A[1][i] * om[1]) + A[2][i] * om[2];
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                o[3 * i + j] = ((A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j]) + (A[2][i] * W[2]) * A[2][j];
+#pragma unroll
+            for (int j = 0; j < 6; j++)
+                o[12 + 6 * i + j] = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
+                                                (A[2][i] * W[2]) * B[2][j]
+                                          : 0.0;
         }
         if (pfree) {
             int q = 30;
+#pragma unroll
             for (int i = 0; i < 6; i++)
-                for (int j = i; j < 6; j++) {
-                    double h = (B[0][i] * W[0]) * B[0][j];
-                    for (int r = 1; r < dim; r++) h += (B[r][i] * W[r]) * B[r][j];
-                    o[q++] = h;
-                }
-            for (int i = 0; i < 6; i++) {
-                double s = B[0][i] * om[0];
-                for (int r = 1; r < dim; r++) s += B[r][i] * om[r];
-                o[51 + i] = s;
-            }
+#pragma unroll
+                for (int j = i; j < 6; j++)
+                    o[q++] = ((B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j]) + (B[2][i] * W[2]) * B[2][j];
+#pragma unroll
+            for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
         }
     }
     __syncthreads();
+    mark(S, 2);
     double mx = 0.0;
     // landmarks: Hll, bl, blocks (edges of a landmark are contiguous, summed in order)
     for (int l = t; l < c.L; l += kThreads) {
@@ -462,12 +473,15 @@ __device__ double build_system(Ctx& c, const LbaConsts& C, bool robust, Shared& 
     for (int h = wave; h < S.np; h += kWaves) {
         const int k = S.hidx_pose[h];
         double acc[27];
+#pragma unroll
         for (int j = 0; j < 27; j++) acc[j] = 0.0;
         for (int e = lane; e < c.E; e += 64) {
             if (c.e_level[e] != 0 || c.e_kf[e] != k) continue;
             const double* o = c.con + (size_t)kLbaCon * e + 30;
+#pragma unroll
             for (int j = 0; j < 27; j++) acc[j] += o[j];
         }
+#pragma unroll
         for (int j = 0; j < 27; j++) {
             double x = acc[j];
 #pragma unroll
@@ -477,12 +491,15 @@ __device__ double build_system(Ctx& c, const LbaConsts& C, bool robust, Shared& 
         if (lane == 0) {
             double* H = c.Hpp + 36 * h;
             int q = 0;
+#pragma unroll
             for (int i = 0; i < 6; i++)
+#pragma unroll
                 for (int j = i; j < 6; j++) { H[6 * i + j] = acc[q]; H[6 * j + i] = acc[q]; q++; }
+#pragma unroll
             for (int i = 0; i < 6; i++) c.bp[6 * h + i] = acc[21 + i];
+            mx = fmax(mx, fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fmax(fabs(acc[11]), fabs(acc[15])),
+                                                                      fmax(fabs(acc[18]), fabs(acc[20])))));
         }
-        if (lane == 0)
-            for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(acc[(i * (13 - i)) / 2]));
     }
     __syncthreads();
     return block_max(mx, S);
@@ -522,6 +539,7 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
             const int p2 = p1 + rem;
             const uint64_t need = (1ull << p1) | (1ull << p2);
             double acc[36];
+#pragma unroll
             for (int j = 0; j < 36; j++) acc[j] = 0.0;
             for (int l = lane; l < c.L; l += 64) {
                 const uint64_t m = c.lm_mask[l];
@@ -530,10 +548,16 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
                 const int a = b0 + __popcll(m & ((1ull << p1) - 1)), b = b0 + __popcll(m & ((1ull << p2) - 1));
                 const double* BD = c.blkBD + (size_t)a * 18;
                 const double* H = c.blkH + (size_t)b * 18;
+                double bd[18], hh[18];
+#pragma unroll
+                for (int j = 0; j < 18; j++) { bd[j] = BD[j]; hh[j] = H[j]; }
+#pragma unroll
                 for (int r = 0; r < 6; r++)
+#pragma unroll
                     for (int q = 0; q < 6; q++)
-                        acc[6 * r + q] += (BD[3 * r] * H[q] + BD[3 * r + 1] * H[6 + q]) + BD[3 * r + 2] * H[12 + q];
+                        acc[6 * r + q] += (bd[3 * r] * hh[q] + bd[3 * r + 1] * hh[6 + q]) + bd[3 * r + 2] * hh[12 + q];
             }
+#pragma unroll
             for (int j = 0; j < 36; j++) {
                 double x = acc[j];
 #pragma unroll
@@ -543,6 +567,7 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
             if (lane < 36) {
                 const int r = lane / 6, q = lane % 6;
                 double v = 0.0;
+#pragma unroll
                 for (int j = 0; j < 36; j++) if (j == lane) v = acc[j];
                 double base = 0.0;
                 if (p1 == p2) base = c.Hpp[36 * p1 + lane] + (r == q ? lam : 0.0);
@@ -557,8 +582,10 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
                 const int a = lm_block_base(c, l) + __popcll(m & ((1ull << p) - 1));
                 const double* H = c.blkH + (size_t)a * 18;
                 const double* db = c.db + 3 * l;
+#pragma unroll
                 for (int r = 0; r < 6; r++) acc[r] += (H[r] * db[0] + H[6 + r] * db[1]) + H[12 + r] * db[2];
             }
+#pragma unroll
             for (int j = 0; j < 6; j++) {
                 double x = acc[j];
 #pragma unroll
@@ -567,12 +594,14 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
             }
             if (lane < 6) {
                 double v = 0.0;
+#pragma unroll
                 for (int j = 0; j < 6; j++) if (j == lane) v = acc[j];
                 c.bs[6 * p + lane] = c.bp[6 * p + lane] - v;
             }
         }
     }
     __syncthreads();
+    mark(S, 4);
     // LDL^T of the upper triangle, right-looking: entry (r, q), r <= q, loses (L[q][k] d_k) L[r][k]
     // at step k; L[i][j] is kept in the lower triangle of S.
     for (int j = 0; j < n; j++) {
@@ -589,6 +618,7 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
         }
         __syncthreads();
     }
+    mark(S, 5);
     for (int i = t; i < n; i += kThreads) c.y[i] = c.bs[i];
     __syncthreads();
     for (int k = 0; k < n; k++) {  // forward: y[i] -= L[i][k] y[k], k increasing
@@ -625,6 +655,7 @@ __device__ bool solve(Ctx& c, double lam, Shared& S) {
         for (int i = 0; i < 3; i++) c.xl[3 * l + i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
     }
     __syncthreads();
+    mark(S, 6);
     return true;
 }
 
@@ -680,18 +711,24 @@ __device__ int optimize(Ctx& c, const LbaConsts& C, bool robust, int iterations,
     if (S.np == 0 && c.L == 0) return 0;
     int its = 0;
     for (int it = 0; it < iterations; it++) {
+        mark(S, 7);
         const double chi = active_chi2(c, C, robust, S);
+        mark(S, 1);
         if (threadIdx.x == 0) { S.currentChi = chi; S.iniChi = chi; }
         const double mx = build_system(c, C, robust, S);
+        mark(S, 3);
         if (threadIdx.x == 0 && it == 0) { S.lambda = 1e-5 * mx; S.ni = 2; S.nBad = 0; }
         if (threadIdx.x == 0) S.qmax = 0;
         __syncthreads();
         double rho = 0;
         do {
             push_state(c, S);
+            mark(S, 7);
             const bool ok = solve(c, S.lambda, S);
             if (ok) apply_update(c, S);
+            mark(S, 7);
             const double tempChi0 = active_chi2(c, C, robust, S);
+            mark(S, 1);
             const double scale = ok ? step_scale(c, S.lambda, S) : 0.0;
             if (threadIdx.x == 0) {
                 const double tempChi = ok ? tempChi0 : DBL_MAX;
@@ -709,6 +746,7 @@ __device__ int optimize(Ctx& c, const LbaConsts& C, bool robust, int iterations,
                     S.ok = 0;
                 }
                 S.qmax++;
+                S.trials++;
                 S.rho = rho;
             }
             __syncthreads();
@@ -743,6 +781,9 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
     c.kf = kfs + pb.kf_offset; c.pt = pts + pb.point_offset; c.pl = pls + pb.plane_offset;
     c.pobs = pobs; c.plobs = plobs;
     spslam_lba_result* R = res + blockIdx.x;
+    if (t < 8) S.t_phase[t] = 0;
+    if (t == 0) { S.t_mark = wall_clock64(); S.trials = 0; }
+    __syncthreads();
     if (c.K > kLbaMaxKeyframes) {
         if (t == 0) { R->status = -2; R->iterations[0] = R->iterations[1] = 0; }
         return;
@@ -815,9 +856,11 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
     }
     __syncthreads();
     int its[2] = {0, 0};
+    mark(S, 0);
     if (c.E > 0) {
         for (int phase = 0; phase < 2; phase++) {
             initialize(c, S);
+            mark(S, 0);
             its[phase] = optimize(c, C, phase == 0, phase == 0 ? 5 : 10, S);
             if (phase == 0) {  // relabel with the errors cached by the last computeActiveErrors
                 for (int e = t; e < c.E; e += kThreads) {
@@ -878,6 +921,8 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
         R->n_point_outliers = (int)cnt[0];
         R->n_plane_outliers = (int)cnt[1];
         R->status = 0;
+        R->trials = S.trials;
+        for (int k = 0; k < 8; k++) R->phase_us[k] = (float)(S.t_phase[k] * 0.01);  // 100 MHz ticks
     }
 }
 

@@ -31,7 +31,7 @@ import synth
 
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
-                 device=0, K=synth.TUM3, oracle_kps=None):
+                 device=0, K=synth.TUM3, oracle_kps=None, lba_every=0, lba_unique=4, lba_points=1500):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -103,6 +103,12 @@ class HotPath:
         self.d_res1 = torch.zeros(B * G.POSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.d_res2 = torch.zeros_like(self.d_res1)
         self.mean_keypoints = float(cnts.mean())
+        # --- LocalBundleAdjustment (C3): one local map per `lba_every` frames (a keyframe), run on the
+        #     LocalMapping stream beside tracking like the reference's LocalMapping thread
+        self.n_lba = B // lba_every if lba_every else 0
+        self.lba_every = lba_every
+        if self.n_lba:
+            self._setup_lba(seq_id, lba_unique, lba_points)
 
     def _upload(self, probs):
         torch = self.torch
@@ -154,16 +160,65 @@ class HotPath:
                                      self.d_res2.data_ptr(), Bp["pout"].data_ptr(), Bp["plout"].data_ptr(),
                                      init_from_ptr=self.d_res1.data_ptr(), stream=self.stream)
 
+    def _setup_lba(self, seq_id, unique, n_points):
+        import spslam_lba as L
+        torch = self.torch
+        probs = []
+        for u in range(min(unique, self.n_lba)):
+            rng = np.random.default_rng(seq_id * 131 + u)
+            f0 = 6 * u
+            probs.append(synth.lba_problem(self.scene, list(range(f0, f0 + 72, 6)), rng, n_fixed=2, n_points=n_points))
+        hdr = np.zeros(self.n_lba, L.LBA_PROBLEM_DTYPE)
+        kf, pt, po, pl, plo = [], [], [], [], []
+        nk = npt = npo = npl = nplo = 0
+        for i in range(self.n_lba):
+            prob, kfs, pts, pobs, pls, plobs, _ = probs[i % len(probs)]
+            hdr[i] = prob
+            hdr[i]["kf_offset"], hdr[i]["point_offset"], hdr[i]["plane_offset"] = nk, npt, npl
+            pts = pts.copy()
+            pts["obs_offset"] += npo
+            pls = pls.copy()
+            pls["obs_offset"] += nplo
+            kf.append(kfs); pt.append(pts); po.append(pobs); pl.append(pls); plo.append(plobs)
+            nk += len(kfs); npt += len(pts); npo += len(pobs); npl += len(pls); nplo += len(plobs)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()  # noqa: E731
+        self.lba_problems = probs
+        self.lba_hdr = hdr
+        self.lba_in = [dev(hdr), dev(np.concatenate(kf)), dev(np.concatenate(pt)), dev(np.concatenate(po)),
+                       dev(np.concatenate(pl)), dev(np.concatenate(plo))]
+        self.lba_out = [torch.zeros((nk, 16), dtype=torch.float32, device="cuda"),
+                        torch.zeros((npt, 3), dtype=torch.float32, device="cuda"),
+                        torch.zeros((max(npl, 1), 4), dtype=torch.float32, device="cuda"),
+                        torch.zeros(npo, dtype=torch.uint8, device="cuda"),
+                        torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
+                        torch.zeros(self.n_lba * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
+        self.lba = L.LocalBA(self.ex)
+        self.lba_stream = torch.cuda.Stream()
+        self.ev_lba = torch.cuda.Event()
+        self.lba_edges = (npo + nplo) / self.n_lba
+        self.lba_points = npt / self.n_lba
+
+    def local_ba(self):
+        self.lba.batch_device(self.n_lba, self.lba_hdr, *[x.data_ptr() for x in self.lba_in],
+                              *[x.data_ptr() for x in self.lba_out], stream=self.lba_stream.cuda_stream)
+
     def step(self):
         # planes of step k may start once step k-1 is done with the plane buffers
         self.ev_fork.record(self.main)
         self.side.wait_event(self.ev_fork)
+        if self.n_lba:
+            # LocalMapping: the keyframes of this step, beside tracking (joined at the end of the step)
+            self.lba_stream.wait_event(self.ev_fork)
+            self.local_ba()
+            self.ev_lba.record(self.lba_stream)
         self.planes(self.side_stream)
         self.orb()
         self.ev_join.record(self.side)
         self.main.wait_event(self.ev_join)
         self.frame()
         self.pose()
+        if self.n_lba:
+            self.main.wait_event(self.ev_lba)
 
     def results(self):
         torch = self.torch

@@ -20,10 +20,10 @@ LBA_PROBLEM_DTYPE = np.dtype([("n_kf", "<i4"), ("n_points", "<i4"), ("n_planes",
                               ("point_offset", "<i4"), ("plane_offset", "<i4"), ("n_point_obs", "<i4"),
                               ("n_plane_obs", "<i4")])
 LBA_RESULT_DTYPE = np.dtype([("iterations", "<i4", 2), ("n_point_outliers", "<i4"), ("n_plane_outliers", "<i4"),
-                             ("status", "<i4"), ("pad", "<i4", 3)])
+                             ("status", "<i4"), ("trials", "<i4"), ("pad", "<i4", 2), ("phase_us", "<f4", 8)])
 assert LBA_KEYFRAME_DTYPE.itemsize == 96 and LBA_POINT_DTYPE.itemsize == 24
 assert LBA_POINT_OBS_DTYPE.itemsize == 20 and LBA_PLANE_DTYPE.itemsize == 32
-assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 32
+assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 64
 
 
 spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device"]

@@ -8,6 +8,7 @@ import pathlib
 import numpy as np
 
 import oracle_ctypes as O
+import oracle_lba as OL
 import oracle_planes as OP
 import oracle_supposed as OS
 import synth
@@ -56,3 +57,13 @@ def test_golden_pose_fixture():
     assert np.array_equal(r["Tcw"], ref["Tcw"])
     assert int(r["n_inliers"]) == int(ref["n_inliers"])
     assert np.array_equal(pout, ref["pout"]) and np.array_equal(plout, ref["plout"])
+
+
+def test_golden_lba_fixture():
+    ref = np.load(GOLDEN / "lba_seq1.npz")
+    r = OL.lba_optimize(ref["prob"], ref["kfs"], ref["points"], ref["point_obs"], ref["planes"], ref["plane_obs"])
+    assert np.array_equal(r["Tcw"], ref["Tcw"]) and np.array_equal(r["points"], ref["pts_out"])
+    assert np.array_equal(r["planes"], ref["pls_out"])
+    assert np.array_equal(r["point_outlier"], ref["point_outlier"])
+    assert np.array_equal(r["plane_outlier"], ref["plane_outlier"])
+    assert list(r["result"]["iterations"]) == list(ref["iterations"])

@@ -1,0 +1,57 @@
+"""CPU pins of the LocalBundleAdjustment oracle (oracle/lba_oracle.cpp):
+known answers on synthetic local maps -- noise-free observations converge to
+the ground truth, injected gross outliers are the observations flagged for
+erasure, fixed keyframes are returned unchanged, and a problem without
+edges is a no-op."""
+import numpy as np
+
+import oracle_lba
+import synth
+
+
+def _prob(seed, **kw):
+    rng = np.random.default_rng(seed)
+    return synth.lba_problem(synth.Scene(seed % 4, n_boxes=3), list(range(0, 60, 6)), rng, **kw)
+
+
+def test_noise_free_converges_to_ground_truth():
+    P = _prob(11, pix_noise=0.0, outlier_frac=0.0, plane_noise_deg=0.0, plane_noise_d=0.0, stereo_frac=0.0,
+              n_points=1200)
+    r = oracle_lba.lba_optimize(*P[:6])
+    gt = P[6]["Tcw"]
+    loc = P[1]["fixed"] == 0
+    err0 = np.abs(P[1]["Tcw"].reshape(-1, 4, 4)[loc, :3, 3] - gt[loc, :3, 3]).max()
+    err1 = np.abs(r["Tcw"].reshape(-1, 4, 4)[loc, :3, 3] - gt[loc, :3, 3]).max()
+    assert err0 > 5e-3 and err1 < 2e-4, (err0, err1)
+    assert r["point_outlier"].sum() == 0
+
+
+def test_gross_outliers_are_flagged():
+    rng = np.random.default_rng(5)
+    P = list(synth.lba_problem(synth.Scene(1, n_boxes=3), list(range(0, 60, 6)), rng, outlier_frac=0.0,
+                               n_points=1000, with_planes=False))
+    pobs = P[3].copy()
+    bad = rng.choice(len(pobs), len(pobs) // 25, replace=False)
+    pobs["u"][bad] = (pobs["u"][bad] + 80.0) % 620.0 + 10.0  # 80 px off
+    P[3] = pobs
+    r = oracle_lba.lba_optimize(*P[:6])
+    flagged = set(np.nonzero(r["point_outlier"])[0])
+    assert len(set(bad) - flagged) <= len(bad) // 50
+    assert len(flagged - set(bad)) <= len(pobs) // 100
+
+
+def test_fixed_keyframes_unchanged_and_empty_problem():
+    P = _prob(3, n_fixed=3, n_points=600)
+    r = oracle_lba.lba_optimize(*P[:6])
+    fixed = P[1]["fixed"] == 1
+    assert np.array_equal(r["Tcw"][fixed], P[1]["Tcw"][fixed])
+    prob, kfs = P[0].copy(), P[1]
+    prob["n_points"] = prob["n_planes"] = prob["n_point_obs"] = prob["n_plane_obs"] = 0
+    import spslam_lba as L
+    e = np.zeros(0, L.LBA_POINT_DTYPE)
+    r = oracle_lba.lba_optimize(prob, kfs, e, np.zeros(0, L.LBA_POINT_OBS_DTYPE), np.zeros(0, L.LBA_PLANE_DTYPE),
+                                np.zeros(0, L.LBA_PLANE_OBS_DTYPE))
+    assert list(r["result"]["iterations"]) == [0, 0]
+    loc = kfs["fixed"] == 0
+    # local keyframes go through Converter::toSE3Quat / toCvMat unchanged up to float rounding
+    assert np.abs(r["Tcw"][loc] - kfs["Tcw"][loc]).max() < 1e-6

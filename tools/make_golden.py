@@ -15,6 +15,7 @@ sys.path[:0] = [str(ROOT / "sp-slam_amd"), str(ROOT / "oracle")]
 import oracle_ctypes as O  # noqa: E402
 import oracle_planes as OP  # noqa: E402
 import oracle_supposed as OS  # noqa: E402
+import oracle_lba as OL  # noqa: E402
 import synth  # noqa: E402
 
 out = ROOT / "tests" / "golden"
@@ -56,4 +57,12 @@ prob, pts, pls, Tgt = synth.pose_problem(sc, 5, kps, d, fid, invs2, rng)
 r, pout, plout = O.pose_optimize(prob, pts, pls)
 np.savez_compressed(out / "pose_seq0_f5.npz", prob=prob, pts=pts, pls=pls, Tcw=r["Tcw"], n_inliers=r["n_inliers"],
                     pout=pout, plout=plout, Tgt=Tgt)
+# local bundle adjustment (inputs are synthetic and stored with the outputs)
+lrng = np.random.default_rng(21)
+LP = synth.lba_problem(synth.Scene(1, n_boxes=3), list(range(0, 48, 6)), lrng, n_fixed=2, n_points=400)
+lr = OL.lba_optimize(*LP[:6])
+np.savez_compressed(out / "lba_seq1.npz", prob=LP[0], kfs=LP[1], points=LP[2], point_obs=LP[3], planes=LP[4],
+                    plane_obs=LP[5], Tcw=lr["Tcw"], pts_out=lr["points"], pls_out=lr["planes"],
+                    point_outlier=lr["point_outlier"], plane_outlier=lr["plane_outlier"],
+                    iterations=lr["result"]["iterations"])
 print("wrote", sorted(p.name for p in out.iterdir()))
