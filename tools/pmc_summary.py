@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""HBM traffic per launch from two rocprofv3 PMC passes (tools/pmc_round.sh).
+
+    python tools/pmc_summary.py gpurun_out/pmc_fetch_c2 gpurun_out/pmc_write_c2 profiles/pmc_c2_b256.json
+
+FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch.  MI355X_MICROARCH.md
+("HBM"): on gfx950 FETCH_SIZE reports half the bytes of wide coalesced
+streaming reads, so fetch bytes = 2 x FETCH_SIZE x 1024 (the correction is
+calibrated for 16 B/lane streaming loads; narrower gathers are uncalibrated);
+WRITE_SIZE is taken as is.  Output: {kernel: traffic bytes per timed launch of that kernel kind (bench.py)} plus
+a "detail" map with the two components and the dispatch count.
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+
+def short(name):
+    m = re.search(r"(\w+_kernel)\b", name)
+    return m.group(1) if m else name.split("(")[0][-60:]
+
+
+def load(d, counter):
+    path = f"{d}/run_counter_collection.csv"
+    acc = collections.defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter:
+                acc[short(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+    return acc
+
+
+# dispatches per timed kernel-kind launch in bench.py (the level kind times its 8 per-level launches together)
+PER_KIND = {"level_kernel": 8}
+
+
+def main(fetch_dir, write_dir, out):
+    fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
+    res, detail = {}, {}
+    for k in sorted(set(fe) | set(wr)):
+        if not k.endswith("_kernel"):
+            continue
+        per = PER_KIND.get(k, 1)
+        f = sum(fe.get(k, [0])) / max(len(fe.get(k, [])) / per, 1) * 1024 * 2
+        w = sum(wr.get(k, [0])) / max(len(wr.get(k, [])) / per, 1) * 1024
+        res[k] = f + w
+        detail[k] = dict(fetch_bytes=f, write_bytes=w, dispatches=len(fe.get(k, [])))
+        print(f"{k:28s} fetch {f / 1e6:10.3f} MB  write {w / 1e6:10.3f} MB  per launch  ({len(fe.get(k, []))} launches)")
+    res["detail"] = detail
+    res["note"] = ("HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 separate --pmc passes, "
+                   "gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md")
+    with open(out, "w") as fo:
+        json.dump(res, fo, indent=1)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
