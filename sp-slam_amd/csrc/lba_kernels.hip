@@ -2,30 +2,32 @@
 // vendored g2o BlockSolver_6_3 + Levenberg-Marquardt, g2oAddition plane
 // edges).  Semantics: oracle/lba_oracle.cpp.
 //
-// One 512-thread workgroup per problem runs the whole schedule --
-// optimize(5), relabel, optimize(10), outlier flags -- with no host round
-// trip; problems of a batch (keyframes of many sequences) run side by side.
-// Per LM iteration:
-//   edges      thread per edge: error, Huber weight, analytic (points) or
-//              central-difference (planes, both vertices) Jacobians, and the
-//              edge's quadratic-form terms (Hll, bl, Hpl, Hpp, bp) -> HBM;
-//   landmarks  thread per landmark: Hll, bl and its (landmark, pose) blocks
-//              summed over its edges in insertion order;
-//   poses      wave per pose: Hpp, bp summed over the pose's edges.
-// Per LM trial (lambda):
-//   landmarks  thread per landmark: (Hll + lambda)^-1 (Eigen 3x3 cofactor
-//              inverse), Dinv bl, B Dinv per block;
-//   Schur      wave per pose pair (p1 <= p2): Hpp + lambda - sum_l B Dinv B^T
-//              over the landmarks both poses see (64-bit pose masks, lanes
-//              stride over landmarks, 36 accumulators per lane), and
-//              bp - sum_l B Dinv bl per pose;
-//   solve      LDL^T of the reduced 6P x 6P system, right-looking (the same
-//              per-entry operation order as the oracle's factorisation);
-//   update     landmark back-substitution, exp(x) * T, X + x, Plane3D::oplus;
-//   errors     thread per edge, robust chi2 (tree reduction), accept/reject.
-// All arithmetic is fp64; reductions are tree-ordered and the landmark order
-// is the caller's list order, so results match the oracle to rounding
-// (north-star bar 1e-4), not bitwise.
+// A batch of local maps (the keyframes of many sequences) is optimised
+// together.  Every phase of an LM step is a grid-wide kernel whose
+// workgroups cover all problems at once (a (problem, chunk) work table built
+// on the host), so one map spreads over many CUs and latency-bound loops run
+// with hundreds of waves in flight:
+//   structure   per keyframe: active-edge counts and edge lists (stable);
+//               per problem: pose Hessian order (by id), landmark pose masks
+//               and (landmark, pose) blocks;
+//   errors      edge chunks: error + robust chi2, chunk partial sums;
+//   edge terms  edge chunks: analytic (points) / central-difference (planes,
+//               both vertices) Jacobians and the quadratic-form terms;
+//   sums        landmark chunks: Hll, bl, blocks; keyframes: Hpp, bp;
+//   Schur       landmark chunks: (Hll + lambda)^-1 (Eigen 3x3 cofactor inverse),
+//               Dinv bl, B Dinv; pose-pair tasks: Hpp + lambda - sum B Dinv B^T,
+//               bp - sum B Dinv bl (64-bit pose masks, threads over landmarks);
+//   factor      per problem: LDL^T of the reduced 6P x 6P system in LDS
+//               (right-looking, the oracle's per-entry operation order);
+//   update      landmark chunks / keyframes: backup, back-substitution,
+//               exp(x) * T, X + x, Plane3D::oplus, step-scale partials;
+//   decide      per problem: OptimizationAlgorithmLevenberg's accept / reject,
+//               lambda, iteration and schedule bookkeeping (optimize(5),
+//               relabel with the cached errors, optimize(10));
+//   restore     rejected trials roll back.
+// The host enqueues steps and polls a device counter every few steps.
+// All arithmetic is fp64; reductions are tree-ordered, so results match the
+// oracle to rounding (north-star bar 1e-4), not bitwise.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -38,44 +40,55 @@ namespace lba {
 
 using namespace g2od;
 
-constexpr int kThreads = 256, kWaves = kThreads / 64;
-
-struct Shared {
-    double red[kWaves][8];
-    double lambda, ni, currentChi, iniChi, rho;
-    int nBad, stop, ok, qmax, its;
-    int np, nl_active;
-    int pose_hidx[kLbaMaxKeyframes];
-    int hidx_pose[kLbaMaxKeyframes];
-    int pose_act[kLbaMaxKeyframes];
-    int wsum[kWaves];
-    long long t_phase[8];   // wall_clock64 ticks per phase (100 MHz), thread 0
-    long long t_mark;
-    int trials;
-};
-
-// Phase timer (diagnostics): thread 0 charges the time since the last mark to phase p.
-__device__ __forceinline__ void mark(Shared& S, int p) {
-    if (threadIdx.x == 0) {
-        const long long now = wall_clock64();
-        S.t_phase[p] += now - S.t_mark;
-        S.t_mark = now;
-    }
-}
+constexpr int kThreads = kLbaChunk, kWaves = kThreads / 64;
+constexpr int kStruct = 0, kIter = 1, kTrial = 2, kRelabel = 3, kDone = 4;
+constexpr int kFactorLds = 150 * 1024;   // reduced system held in LDS up to n = 140
 
 struct Ctx {
-    int K, Np, Nq, E, Ep, L;
+    int K, Np, Nq, E, Ep, L, nEc, nLc;
     const spslam_lba_keyframe* kf;
     const spslam_lba_point* pt;
     const spslam_lba_point_obs* pobs;
     const spslam_lba_plane* pl;
     const spslam_lba_plane_obs* plobs;
+    LbaCtl* ctl;
     double *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *con, *lmH, *lmb, *Dinv, *db, *xl, *blkH, *blkBD, *S, *bs, *dd, *y,
-        *Hpp, *bp;
-    int *pose_hidx_g, *hidx_pose_g, *e_lm, *e_kf, *e_type, *e_level, *e_blk, *e_src, *lm_boff, *lm_nb, *blk_pose,
-        *lm_act;
+        *Hpp, *bp, *part_chi, *part_scale, *part_max;
+    int *pose_hidx, *hidx_pose, *e_lm, *e_kf, *e_type, *e_level, *e_blk, *e_src, *lm_boff, *lm_nb, *lm_act, *kf_cnt,
+        *pe_off, *pe_idx;
     uint64_t* lm_mask;
 };
+
+__device__ Ctx make_ctx(const LbaBatch& b, int p) {
+    const spslam_lba_problem pb = b.probs[p];
+    Ctx c;
+    c.K = pb.n_kf; c.Np = pb.n_points; c.Nq = pb.n_planes;
+    c.Ep = pb.n_point_obs; c.E = pb.n_point_obs + pb.n_plane_obs; c.L = c.Np + c.Nq;
+    c.nEc = lba_chunks(c.E); c.nLc = lba_chunks(c.L);
+    c.kf = b.kfs + pb.kf_offset; c.pt = b.pts + pb.point_offset; c.pl = b.pls + pb.plane_offset;
+    c.pobs = b.pobs; c.plobs = b.plobs;
+    const LbaLayout Ly = lba_layout(c.K, c.Np, c.Nq, c.E);
+    uint8_t* base = b.scratch + b.scratch_off[p];
+    c.ctl = (LbaCtl*)(base + Ly.ctl);
+    c.pose = (double*)(base + Ly.pose); c.pose_b = (double*)(base + Ly.pose_b);
+    c.X = (double*)(base + Ly.pt); c.X_b = (double*)(base + Ly.pt_b);
+    c.P = (double*)(base + Ly.pl); c.P_b = (double*)(base + Ly.pl_b);
+    c.err = (double*)(base + Ly.e_err); c.con = (double*)(base + Ly.e_con);
+    c.lmH = (double*)(base + Ly.lm_H); c.lmb = (double*)(base + Ly.lm_b); c.Dinv = (double*)(base + Ly.lm_Dinv);
+    c.db = (double*)(base + Ly.lm_db); c.xl = (double*)(base + Ly.lm_x);
+    c.blkH = (double*)(base + Ly.blk_H); c.blkBD = (double*)(base + Ly.blk_BD);
+    c.S = (double*)(base + Ly.S); c.bs = (double*)(base + Ly.bs); c.dd = (double*)(base + Ly.dd);
+    c.y = (double*)(base + Ly.y); c.Hpp = (double*)(base + Ly.Hpp); c.bp = (double*)(base + Ly.bp);
+    c.part_chi = (double*)(base + Ly.part_chi); c.part_scale = (double*)(base + Ly.part_scale);
+    c.part_max = (double*)(base + Ly.part_max);
+    c.pose_hidx = (int*)(base + Ly.pose_hidx); c.hidx_pose = (int*)(base + Ly.hidx_pose);
+    c.e_lm = (int*)(base + Ly.e_lm); c.e_kf = (int*)(base + Ly.e_kf); c.e_type = (int*)(base + Ly.e_type);
+    c.e_level = (int*)(base + Ly.e_level); c.e_blk = (int*)(base + Ly.e_blk); c.e_src = (int*)(base + Ly.e_src);
+    c.lm_boff = (int*)(base + Ly.lm_boff); c.lm_nb = (int*)(base + Ly.lm_nb); c.lm_act = (int*)(base + Ly.lm_act);
+    c.kf_cnt = (int*)(base + Ly.kf_cnt); c.pe_off = (int*)(base + Ly.pe_off); c.pe_idx = (int*)(base + Ly.pe_idx);
+    c.lm_mask = (uint64_t*)(base + Ly.lm_mask);
+    return c;
+}
 
 __device__ __forceinline__ SE3 load_pose(const double* p) { return SE3{Q{p[0], p[1], p[2], p[3]}, V3{p[4], p[5], p[6]}}; }
 __device__ __forceinline__ void store_pose(double* p, const SE3& T) {
@@ -173,38 +186,46 @@ __device__ bool depth_positive(const Ctx& c, int e) {
 }
 
 // Block-wide sum of NV doubles per thread; result valid in every thread.
+
+struct Red {
+    double v[kWaves][40];
+    int wsum[kWaves];
+};
+
+// Block-wide sum of NV doubles per thread (tree order); result valid in every thread.
 template <int NV>
-__device__ void block_sum(double (&v)[NV], Shared& S) {
+__device__ void block_sum(double (&v)[NV], Red& R) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int k = 0; k < NV; k++) {
         double x = v[k];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-        if (lane == 0) S.red[w][k] = x;
+        if (lane == 0) R.v[w][k] = x;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < NV; k++) {
         double s = 0;
-        for (int j = 0; j < kWaves; j++) s += S.red[j][k];
+#pragma unroll
+        for (int j = 0; j < kWaves; j++) s += R.v[j][k];
         v[k] = s;
     }
     __syncthreads();
 }
-__device__ double block_max(double v, Shared& S) {
+__device__ double block_max(double v, Red& R) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-    if (lane == 0) S.red[w][0] = v;
+    if (lane == 0) R.v[w][0] = v;
     __syncthreads();
     double m = 0;
-    for (int j = 0; j < kWaves; j++) m = fmax(m, S.red[j][0]);
+    for (int j = 0; j < kWaves; j++) m = fmax(m, R.v[j][0]);
     __syncthreads();
     return m;
 }
-// exclusive block scan of one int per thread; *total = sum
-__device__ int block_scan(int v, int* total, Shared& S) {
+// Exclusive block scan of one int per thread; *total = block sum.
+__device__ int block_scan(int v, int* total, Red& R) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -212,42 +233,19 @@ __device__ int block_scan(int v, int* total, Shared& S) {
         const int y = __shfl_up(x, o);
         if (lane >= o) x += y;
     }
-    if (lane == 63) S.wsum[w] = x;
+    if (lane == 63) R.wsum[w] = x;
     __syncthreads();
     int base = 0, tot = 0;
     for (int j = 0; j < kWaves; j++) {
-        if (j < w) base += S.wsum[j];
-        tot += S.wsum[j];
+        if (j < w) base += R.wsum[j];
+        tot += R.wsum[j];
     }
     __syncthreads();
     *total = tot;
     return base + x - v;
 }
 
-// Robust chi2 of all active edges at the current estimates (errors cached per edge).
-__device__ double active_chi2(const Ctx& c, const LbaConsts& C, bool robust, Shared& S) {
-    double acc[1] = {0.0};
-    for (int e = threadIdx.x; e < c.E; e += kThreads) {
-        if (c.e_level[e] != 0) continue;
-        const int lm = c.e_lm[e];
-        const SE3 T = load_pose(c.pose + 7 * c.e_kf[e]);
-        double* err = c.err + 3 * e;
-        P4 P;
-        if (lm >= c.Np) {
-            const double* pp = c.P + 4 * (lm - c.Np);
-            P = P4{{pp[0], pp[1], pp[2], pp[3]}};
-        }
-        edge_error(c, e, T, lm < c.Np ? c.X + 3 * lm : nullptr, &P, err);
-        double info[3];
-        info_of(c, C, e, info);
-        const int t = c.e_type[e];
-        double r0, r1;
-        huber(chi2_of(err, info, edge_dim(t)), delta_of(C, t), robust, &r0, &r1);
-        acc[0] += r0;
-    }
-    block_sum(acc, S);
-    return acc[0];
-}
+__device__ __forceinline__ int lm_block_base(const Ctx& c, int l) { return c.lm_act[l] - 1; }
 
 // Edge Jacobians: A (landmark, dim x 3), B (pose, dim x 6); fixed vertices skipped.
 __device__ void edge_jacobians(const Ctx& c, int e, bool pose_free, double (&A)[3][3], double (&B)[3][6]) {
@@ -329,484 +327,22 @@ __device__ void inverse3(const double (&m)[3][3], double* r) {
     r[6] = cof(0, 2) * invdet; r[7] = cof(1, 2) * invdet; r[8] = cof(2, 2) * invdet;
 }
 
-// initializeOptimization(0): active poses (by id) / landmarks, (landmark, pose) blocks.
-__device__ void initialize(Ctx& c, Shared& S) {
-    const int t = threadIdx.x;
-    if (t < c.K) S.pose_act[t] = 0;
-    for (int l = t; l < c.L; l += kThreads) c.lm_act[l] = 0;
-    __syncthreads();
-    for (int e = t; e < c.E; e += kThreads)
-        if (c.e_level[e] == 0) {
-            atomicOr(&S.pose_act[c.e_kf[e]], 1);
-            c.lm_act[c.e_lm[e]] = 1;  // benign race: every writer stores 1
-        }
-    __syncthreads();
-    if (t == 0) {
-        int np = 0;
-        for (int k = 0; k < c.K; k++) S.pose_hidx[k] = -1;
-        for (int k = 0; k < c.K; k++) {  // non-fixed active poses in id order (insertion sort, K <= 64)
-            const spslam_lba_keyframe& kk = c.kf[k];
-            if (!S.pose_act[k] || kk.fixed || kk.id == 0) continue;
-            int j = np++;
-            while (j > 0 && c.kf[S.hidx_pose[j - 1]].id > kk.id) { S.hidx_pose[j] = S.hidx_pose[j - 1]; j--; }
-            S.hidx_pose[j] = k;
-        }
-        for (int j = 0; j < np; j++) S.pose_hidx[S.hidx_pose[j]] = j;
-        S.np = np;
-    }
-    __syncthreads();
-    // blocks: unique free poses among a landmark's active edges, sorted by hessian index
-    const int nchunk = (c.L + kThreads - 1) / kThreads;
-    int base = 0;
-    for (int ch = 0; ch < nchunk; ch++) {
-        const int l = ch * kThreads + t;
-        uint64_t mask = 0;
-        int e_beg = 0, e_end = 0;
-        if (l < c.L) {
-            // edges of a landmark are contiguous: points first (Ep edges), then planes
-            e_beg = c.lm_boff[l];
-            e_end = e_beg + c.lm_nb[l];
-        }
-        for (int e = e_beg; e < e_end; e++)
-            if (c.e_level[e] == 0) {
-                const int h = S.pose_hidx[c.e_kf[e]];
-                if (h >= 0) mask |= 1ull << h;
-            }
-        const int nb = __popcll(mask);
-        int tot;
-        const int off = block_scan(nb, &tot, S) + base;
-        if (l < c.L) {
-            c.lm_mask[l] = mask;
-            // blocks of l at [off, off + nb): pose hidx in increasing order
-            uint64_t m = mask;
-            for (int j = 0; j < nb; j++) {
-                const int h = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
-                c.blk_pose[off + j] = h;
-            }
-            for (int e = e_beg; e < e_end; e++) {
-                const int h = S.pose_hidx[c.e_kf[e]];
-                c.e_blk[e] = (c.e_level[e] == 0 && h >= 0) ? off + __popcll(mask & ((1ull << h) - 1)) : -1;
-            }
-        }
-        base += tot;
-        // block offsets per landmark are recovered from the mask + the running offset
-        if (l < c.L) c.lm_act[l] = c.lm_act[l] ? (off + 1) : 0;  // store off+1 (0 = inactive)
-    }
-    __syncthreads();
-}
 
-__device__ __forceinline__ int lm_block_base(const Ctx& c, int l) { return c.lm_act[l] - 1; }
-
-// buildSystem: edge terms, landmark / pose sums.  Returns max |diag| (lambda init).
-__device__ double build_system(Ctx& c, const LbaConsts& C, bool robust, Shared& S) {
-    const int t = threadIdx.x;
-    for (int e = t; e < c.E; e += kThreads) {
-        if (c.e_level[e] != 0) continue;
-        const int ty = c.e_type[e], dim = edge_dim(ty);
-        const bool pfree = S.pose_hidx[c.e_kf[e]] >= 0;
-        double A[3][3] = {}, B[3][6] = {};
-        edge_jacobians(c, e, pfree, A, B);
-        double info[3];
-        info_of(c, C, e, info);
-        const double* err = c.err + 3 * e;
-        double r0, w;
-        huber(chi2_of(err, info, dim), delta_of(C, ty), robust, &r0, &w);
-        double W[3] = {0, 0, 0}, om[3] = {0, 0, 0};
-#pragma unroll
-        for (int r = 0; r < 3; r++)
-            if (r < dim) {
-                W[r] = robust ? w * info[r] : info[r];
-                om[r] = -(info[r] * err[r]);
-                if (robust) om[r] *= w;
-            }
-        // rows >= dim of A, B, W, om are zero: the padded terms add exact zeros
-        double* o = c.con + (size_t)kLbaCon * e;
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            o[9 + i] = (A[0][i] * om[0] + A[1][i] * om[1]) + A[2][i] * om[2];
-#pragma unroll
-            for (int j = 0; j < 3; j++)
-                o[3 * i + j] = ((A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j]) + (A[2][i] * W[2]) * A[2][j];
-#pragma unroll
-            for (int j = 0; j < 6; j++)
-                o[12 + 6 * i + j] = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
-                                                (A[2][i] * W[2]) * B[2][j]
-                                          : 0.0;
-        }
-        if (pfree) {
-            int q = 30;
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int j = i; j < 6; j++)
-                    o[q++] = ((B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j]) + (B[2][i] * W[2]) * B[2][j];
-#pragma unroll
-            for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
-        }
-    }
-    __syncthreads();
-    mark(S, 2);
-    double mx = 0.0;
-    // landmarks: Hll, bl, blocks (edges of a landmark are contiguous, summed in order)
-    for (int l = t; l < c.L; l += kThreads) {
-        const int b0 = lm_block_base(c, l);
-        if (b0 < 0) continue;
-        const int nb = __popcll(c.lm_mask[l]);
-        for (int j = 0; j < nb * 18; j++) c.blkH[(size_t)b0 * 18 + j] = 0.0;
-        double H[9] = {}, b[3] = {};
-        for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
-            if (c.e_level[e] != 0) continue;
-            const double* o = c.con + (size_t)kLbaCon * e;
-            for (int j = 0; j < 9; j++) H[j] += o[j];
-            for (int j = 0; j < 3; j++) b[j] += o[9 + j];
-            const int bk = c.e_blk[e];
-            if (bk >= 0)
-                for (int j = 0; j < 18; j++) c.blkH[(size_t)bk * 18 + j] += o[12 + j];
-        }
-        for (int j = 0; j < 9; j++) c.lmH[9 * l + j] = H[j];
-        for (int j = 0; j < 3; j++) c.lmb[3 * l + j] = b[j];
-        mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
-    }
-    // poses: wave per pose, lanes stride over edges
-    const int lane = t & 63, wave = t >> 6;
-    for (int h = wave; h < S.np; h += kWaves) {
-        const int k = S.hidx_pose[h];
-        double acc[27];
-#pragma unroll
-        for (int j = 0; j < 27; j++) acc[j] = 0.0;
-        for (int e = lane; e < c.E; e += 64) {
-            if (c.e_level[e] != 0 || c.e_kf[e] != k) continue;
-            const double* o = c.con + (size_t)kLbaCon * e + 30;
-#pragma unroll
-            for (int j = 0; j < 27; j++) acc[j] += o[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 27; j++) {
-            double x = acc[j];
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-            acc[j] = x;
-        }
-        if (lane == 0) {
-            double* H = c.Hpp + 36 * h;
-            int q = 0;
-#pragma unroll
-            for (int i = 0; i < 6; i++)
-#pragma unroll
-                for (int j = i; j < 6; j++) { H[6 * i + j] = acc[q]; H[6 * j + i] = acc[q]; q++; }
-#pragma unroll
-            for (int i = 0; i < 6; i++) c.bp[6 * h + i] = acc[21 + i];
-            mx = fmax(mx, fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fmax(fabs(acc[11]), fabs(acc[15])),
-                                                                      fmax(fabs(acc[18]), fabs(acc[20])))));
-        }
-    }
-    __syncthreads();
-    return block_max(mx, S);
-}
-
-// Schur complement + reduced solve + landmark back-substitution.  Returns false on a zero pivot.
-__device__ bool solve(Ctx& c, double lam, Shared& S) {
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int np = S.np, n = 6 * np;
-    // landmarks: Dinv, db, B Dinv per block
-    for (int l = t; l < c.L; l += kThreads) {
-        const int b0 = lm_block_base(c, l);
-        if (b0 < 0) continue;
-        double D[3][3];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) D[i][j] = c.lmH[9 * l + 3 * i + j] + (i == j ? lam : 0.0);
-        double Di[9];
-        inverse3(D, Di);
-        for (int j = 0; j < 9; j++) c.Dinv[9 * l + j] = Di[j];
-        const double* bl = c.lmb + 3 * l;
-        for (int i = 0; i < 3; i++) c.db[3 * l + i] = (Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1]) + Di[3 * i + 2] * bl[2];
-        const int nb = __popcll(c.lm_mask[l]);
-        for (int a = 0; a < nb; a++) {
-            const double* H = c.blkH + (size_t)(b0 + a) * 18;  // 3 x 6 (landmark x pose)
-            double* BD = c.blkBD + (size_t)(b0 + a) * 18;     // 6 x 3
-            for (int r = 0; r < 6; r++)
-                for (int q = 0; q < 3; q++) BD[3 * r + q] = (H[r] * Di[q] + H[6 + r] * Di[3 + q]) + H[12 + r] * Di[6 + q];
-        }
-    }
-    __syncthreads();
-    // Schur blocks: wave per pose pair (p1 <= p2); lanes stride over landmarks
-    const int npairs = np * (np + 1) / 2;
-    for (int pr = wave; pr < npairs + np; pr += kWaves) {
-        if (pr < npairs) {
-            int p1 = 0, rem = pr;
-            while (rem >= np - p1) { rem -= np - p1; p1++; }
-            const int p2 = p1 + rem;
-            const uint64_t need = (1ull << p1) | (1ull << p2);
-            double acc[36];
-#pragma unroll
-            for (int j = 0; j < 36; j++) acc[j] = 0.0;
-            for (int l = lane; l < c.L; l += 64) {
-                const uint64_t m = c.lm_mask[l];
-                if ((m & need) != need) continue;
-                const int b0 = lm_block_base(c, l);
-                const int a = b0 + __popcll(m & ((1ull << p1) - 1)), b = b0 + __popcll(m & ((1ull << p2) - 1));
-                const double* BD = c.blkBD + (size_t)a * 18;
-                const double* H = c.blkH + (size_t)b * 18;
-                double bd[18], hh[18];
-#pragma unroll
-                for (int j = 0; j < 18; j++) { bd[j] = BD[j]; hh[j] = H[j]; }
-#pragma unroll
-                for (int r = 0; r < 6; r++)
-#pragma unroll
-                    for (int q = 0; q < 6; q++)
-                        acc[6 * r + q] += (bd[3 * r] * hh[q] + bd[3 * r + 1] * hh[6 + q]) + bd[3 * r + 2] * hh[12 + q];
-            }
-#pragma unroll
-            for (int j = 0; j < 36; j++) {
-                double x = acc[j];
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-                acc[j] = x;
-            }
-            if (lane < 36) {
-                const int r = lane / 6, q = lane % 6;
-                double v = 0.0;
-#pragma unroll
-                for (int j = 0; j < 36; j++) if (j == lane) v = acc[j];
-                double base = 0.0;
-                if (p1 == p2) base = c.Hpp[36 * p1 + lane] + (r == q ? lam : 0.0);
-                c.S[(size_t)(6 * p1 + r) * n + 6 * p2 + q] = base - v;
-            }
-        } else {
-            const int p = pr - npairs;
-            double acc[6] = {0, 0, 0, 0, 0, 0};
-            for (int l = lane; l < c.L; l += 64) {
-                const uint64_t m = c.lm_mask[l];
-                if (!((m >> p) & 1)) continue;
-                const int a = lm_block_base(c, l) + __popcll(m & ((1ull << p) - 1));
-                const double* H = c.blkH + (size_t)a * 18;
-                const double* db = c.db + 3 * l;
-#pragma unroll
-                for (int r = 0; r < 6; r++) acc[r] += (H[r] * db[0] + H[6 + r] * db[1]) + H[12 + r] * db[2];
-            }
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                double x = acc[j];
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-                acc[j] = x;
-            }
-            if (lane < 6) {
-                double v = 0.0;
-#pragma unroll
-                for (int j = 0; j < 6; j++) if (j == lane) v = acc[j];
-                c.bs[6 * p + lane] = c.bp[6 * p + lane] - v;
-            }
-        }
-    }
-    __syncthreads();
-    mark(S, 4);
-    // LDL^T of the upper triangle, right-looking: entry (r, q), r <= q, loses (L[q][k] d_k) L[r][k]
-    // at step k; L[i][j] is kept in the lower triangle of S.
-    for (int j = 0; j < n; j++) {
-        const double dj = c.S[(size_t)j * n + j];
-        if (dj == 0.0) { __syncthreads(); return false; }
-        for (int i = j + 1 + t; i < n; i += kThreads) c.S[(size_t)i * n + j] = c.S[(size_t)j * n + i] / dj;
-        if (t == 0) c.dd[j] = dj;
-        __syncthreads();
-        const int m = n - j - 1;
-        for (int idx = t; idx < m * m; idx += kThreads) {
-            const int r = j + 1 + idx / m, q = j + 1 + idx % m;
-            if (r > q) continue;
-            c.S[(size_t)r * n + q] -= (c.S[(size_t)q * n + j] * dj) * c.S[(size_t)r * n + j];
-        }
-        __syncthreads();
-    }
-    mark(S, 5);
-    for (int i = t; i < n; i += kThreads) c.y[i] = c.bs[i];
-    __syncthreads();
-    for (int k = 0; k < n; k++) {  // forward: y[i] -= L[i][k] y[k], k increasing
-        const double yk = c.y[k];
-        __syncthreads();
-        for (int i = k + 1 + t; i < n; i += kThreads) c.y[i] -= c.S[(size_t)i * n + k] * yk;
-        __syncthreads();
-    }
-    for (int i = t; i < n; i += kThreads) c.y[i] /= c.dd[i];
-    __syncthreads();
-    for (int k = n - 1; k >= 0; k--) {  // backward: y[i] -= L[k][i] y[k], k decreasing
-        const double yk = c.y[k];
-        __syncthreads();
-        for (int i = t; i < k; i += kThreads) c.y[i] -= c.S[(size_t)k * n + i] * yk;
-        __syncthreads();
-    }
-    // landmarks: xl = Dinv (bl - Hpl^T xp)
-    for (int l = t; l < c.L; l += kThreads) {
-        const int b0 = lm_block_base(c, l);
-        if (b0 < 0) continue;
-        double cl[3] = {c.lmb[3 * l], c.lmb[3 * l + 1], c.lmb[3 * l + 2]};
-        uint64_t m = c.lm_mask[l];
-        for (int a = 0; m; a++) {
-            const int h = __ffsll((unsigned long long)m) - 1;
-            m &= m - 1;
-            const double* H = c.blkH + (size_t)(b0 + a) * 18;
-            for (int i = 0; i < 3; i++) {
-                double s = 0;
-                for (int j = 0; j < 6; j++) s += H[6 * i + j] * (-c.y[6 * h + j]);
-                cl[i] += s;
-            }
-        }
-        const double* Di = c.Dinv + 9 * l;
-        for (int i = 0; i < 3; i++) c.xl[3 * l + i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
-    }
-    __syncthreads();
-    mark(S, 6);
-    return true;
-}
-
-__device__ void push_state(Ctx& c, Shared& S) {
-    for (int i = threadIdx.x; i < 7 * c.K; i += kThreads) c.pose_b[i] = c.pose[i];
-    for (int i = threadIdx.x; i < 3 * c.Np; i += kThreads) c.X_b[i] = c.X[i];
-    for (int i = threadIdx.x; i < 4 * c.Nq; i += kThreads) c.P_b[i] = c.P[i];
-    __syncthreads();
-}
-__device__ void pop_state(Ctx& c, Shared& S) {
-    for (int i = threadIdx.x; i < 7 * c.K; i += kThreads) c.pose[i] = c.pose_b[i];
-    for (int i = threadIdx.x; i < 3 * c.Np; i += kThreads) c.X[i] = c.X_b[i];
-    for (int i = threadIdx.x; i < 4 * c.Nq; i += kThreads) c.P[i] = c.P_b[i];
-    __syncthreads();
-}
-__device__ void apply_update(Ctx& c, Shared& S) {
-    const int t = threadIdx.x;
-    if (t < S.np) {
-        const int k = S.hidx_pose[t];
-        double u[6];
-        for (int j = 0; j < 6; j++) u[j] = c.y[6 * t + j];
-        store_pose(c.pose + 7 * k, se3_mul(se3_exp(u), load_pose(c.pose + 7 * k)));
-    }
-    for (int l = t; l < c.L; l += kThreads) {
-        if (lm_block_base(c, l) < 0) continue;
-        const double* u = c.xl + 3 * l;
-        if (l < c.Np) {
-            for (int j = 0; j < 3; j++) c.X[3 * l + j] += u[j];
-        } else {
-            double* pp = c.P + 4 * (l - c.Np);
-            P4 P{{pp[0], pp[1], pp[2], pp[3]}};
-            p_oplus(P, u);
-            for (int j = 0; j < 4; j++) pp[j] = P.c[j];
-        }
-    }
-    __syncthreads();
-}
-// computeScale: sum x (lambda x + b) over poses then landmarks
-__device__ double step_scale(Ctx& c, double lam, Shared& S) {
-    double acc[1] = {0.0};
-    const int n = 6 * S.np;
-    for (int i = threadIdx.x; i < n; i += kThreads) acc[0] += c.y[i] * (lam * c.y[i] + c.bp[i]);
-    for (int l = threadIdx.x; l < c.L; l += kThreads) {
-        if (lm_block_base(c, l) < 0) continue;
-        for (int j = 0; j < 3; j++) acc[0] += c.xl[3 * l + j] * (lam * c.xl[3 * l + j] + c.lmb[3 * l + j]);
-    }
-    block_sum(acc, S);
-    return acc[0];
-}
-
-// SparseOptimizer::optimize(iterations), OptimizationAlgorithmLevenberg.
-__device__ int optimize(Ctx& c, const LbaConsts& C, bool robust, int iterations, Shared& S) {
-    if (S.np == 0 && c.L == 0) return 0;
-    int its = 0;
-    for (int it = 0; it < iterations; it++) {
-        mark(S, 7);
-        const double chi = active_chi2(c, C, robust, S);
-        mark(S, 1);
-        if (threadIdx.x == 0) { S.currentChi = chi; S.iniChi = chi; }
-        const double mx = build_system(c, C, robust, S);
-        mark(S, 3);
-        if (threadIdx.x == 0 && it == 0) { S.lambda = 1e-5 * mx; S.ni = 2; S.nBad = 0; }
-        if (threadIdx.x == 0) S.qmax = 0;
-        __syncthreads();
-        double rho = 0;
-        do {
-            push_state(c, S);
-            mark(S, 7);
-            const bool ok = solve(c, S.lambda, S);
-            if (ok) apply_update(c, S);
-            mark(S, 7);
-            const double tempChi0 = active_chi2(c, C, robust, S);
-            mark(S, 1);
-            const double scale = ok ? step_scale(c, S.lambda, S) : 0.0;
-            if (threadIdx.x == 0) {
-                const double tempChi = ok ? tempChi0 : DBL_MAX;
-                rho = (S.currentChi - tempChi) / (scale + 1e-3);
-                if (rho > 0 && isfinite(tempChi)) {
-                    double alpha = 1. - pow((2 * rho - 1), 3);
-                    alpha = fmin(alpha, 2. / 3.);
-                    S.lambda *= fmax(1. / 3., alpha);
-                    S.ni = 2;
-                    S.currentChi = tempChi;
-                    S.ok = 1;
-                } else {
-                    S.lambda *= S.ni;
-                    S.ni *= 2;
-                    S.ok = 0;
-                }
-                S.qmax++;
-                S.trials++;
-                S.rho = rho;
-            }
-            __syncthreads();
-            rho = S.rho;
-            if (!S.ok) pop_state(c, S);
-        } while (rho < 0 && S.qmax < 10);
-        its++;
-        if (S.qmax == 10 || rho == 0) break;
-        if (threadIdx.x == 0) {
-            if ((S.iniChi - S.currentChi) * 1e3 < S.iniChi) S.nBad++;
-            else S.nBad = 0;
-        }
-        __syncthreads();
-        if (S.nBad >= 3) break;
-    }
-    return its;
-}
-
-__global__ __launch_bounds__(kThreads) void lba_kernel(
-    const spslam_lba_problem* __restrict__ probs, const long long* __restrict__ scratch_off,
-    const spslam_lba_keyframe* __restrict__ kfs, const spslam_lba_point* __restrict__ pts,
-    const spslam_lba_point_obs* __restrict__ pobs, const spslam_lba_plane* __restrict__ pls,
-    const spslam_lba_plane_obs* __restrict__ plobs, LbaConsts C, uint8_t* __restrict__ scratch,
-    float* __restrict__ kf_out, float* __restrict__ pt_out, float* __restrict__ pl_out,
-    uint8_t* __restrict__ pobs_out, uint8_t* __restrict__ plobs_out, spslam_lba_result* __restrict__ res) {
-    __shared__ Shared S;
-    const spslam_lba_problem pb = probs[blockIdx.x];
-    const int t = threadIdx.x;
-    Ctx c;
-    c.K = pb.n_kf; c.Np = pb.n_points; c.Nq = pb.n_planes;
-    c.Ep = pb.n_point_obs; c.E = pb.n_point_obs + pb.n_plane_obs; c.L = c.Np + c.Nq;
-    c.kf = kfs + pb.kf_offset; c.pt = pts + pb.point_offset; c.pl = pls + pb.plane_offset;
-    c.pobs = pobs; c.plobs = plobs;
-    spslam_lba_result* R = res + blockIdx.x;
-    if (t < 8) S.t_phase[t] = 0;
-    if (t == 0) { S.t_mark = wall_clock64(); S.trials = 0; }
-    __syncthreads();
+// ---------------------------------------------------------------- setup
+__global__ __launch_bounds__(kThreads) void k_setup(LbaBatch b, int max_it0) {
+    __shared__ Red R;
+    const int p = blockIdx.x, t = threadIdx.x;
+    Ctx c = make_ctx(b, p);
+    spslam_lba_result* res = b.res + p;
     if (c.K > kLbaMaxKeyframes) {
-        if (t == 0) { R->status = -2; R->iterations[0] = R->iterations[1] = 0; }
+        if (t == 0) {
+            *res = spslam_lba_result{};
+            res->status = -2;
+            c.ctl->state = kDone;
+        }
         return;
     }
-    const LbaLayout Ly = lba_layout(c.K, c.Np, c.Nq, c.E);
-    uint8_t* base = scratch + scratch_off[blockIdx.x];
-    c.pose = (double*)(base + Ly.pose); c.pose_b = (double*)(base + Ly.pose_b);
-    c.X = (double*)(base + Ly.pt); c.X_b = (double*)(base + Ly.pt_b);
-    c.P = (double*)(base + Ly.pl); c.P_b = (double*)(base + Ly.pl_b);
-    c.err = (double*)(base + Ly.e_err); c.con = (double*)(base + Ly.e_con);
-    c.lmH = (double*)(base + Ly.lm_H); c.lmb = (double*)(base + Ly.lm_b); c.Dinv = (double*)(base + Ly.lm_Dinv);
-    c.db = (double*)(base + Ly.lm_db); c.xl = (double*)(base + Ly.lm_x);
-    c.blkH = (double*)(base + Ly.blk_H); c.blkBD = (double*)(base + Ly.blk_BD);
-    c.S = (double*)(base + Ly.S); c.bs = (double*)(base + Ly.bs); c.dd = (double*)(base + Ly.dd);
-    c.y = (double*)(base + Ly.y); c.Hpp = (double*)(base + Ly.Hpp); c.bp = (double*)(base + Ly.bp);
-    c.pose_hidx_g = (int*)(base + Ly.pose_hidx); c.hidx_pose_g = (int*)(base + Ly.hidx_pose);
-    c.e_lm = (int*)(base + Ly.e_lm); c.e_kf = (int*)(base + Ly.e_kf); c.e_type = (int*)(base + Ly.e_type);
-    c.e_level = (int*)(base + Ly.e_level); c.e_blk = (int*)(base + Ly.e_blk); c.e_src = (int*)(base + Ly.e_src);
-    c.lm_boff = (int*)(base + Ly.lm_boff); c.lm_nb = (int*)(base + Ly.lm_nb); c.blk_pose = (int*)(base + Ly.blk_pose);
-    c.lm_act = (int*)(base + Ly.lm_act); c.lm_mask = (uint64_t*)(base + Ly.lm_mask);
-
-    // ---- vertices: Converter::toSE3Quat / toVector3d / toPlane3D
-    for (int k = t; k < c.K; k += kThreads) {
+    for (int k = t; k < c.K; k += kThreads) {  // Converter::toSE3Quat
         const float* T = c.kf[k].Tcw;
         M3 Rm;
         for (int i = 0; i < 3; i++)
@@ -820,66 +356,654 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
     for (int i = t; i < c.Np; i += kThreads)
         for (int j = 0; j < 3; j++) c.X[3 * i + j] = c.pt[i].xw[j];
     for (int i = t; i < c.Nq; i += kThreads) {
-        const P4 p = plane_from_f(c.pl[i].world);
-        for (int j = 0; j < 4; j++) c.P[4 * i + j] = p.c[j];
+        const P4 q = plane_from_f(c.pl[i].world);
+        for (int j = 0; j < 4; j++) c.P[4 * i + j] = q.c[j];
     }
-    // ---- edges in insertion order: point observations (points in list order), then plane observations
-    {
-        int base_e = 0;
-        for (int ch = 0; ch < c.L; ch += kThreads) {
-            const int l = ch + t;
-            const int n_obs = l < c.Np ? c.pt[l].n_obs : (l < c.L ? c.pl[l - c.Np].n_obs : 0);
-            int tot;
-            const int off = block_scan(n_obs, &tot, S) + base_e;
-            if (l < c.L) {
-                c.lm_boff[l] = off;  // first edge of the landmark (edges contiguous)
-                c.lm_nb[l] = n_obs;
-                const int src0 = l < c.Np ? c.pt[l].obs_offset : c.pl[l - c.Np].obs_offset;
-                for (int o = 0; o < n_obs; o++) {
-                    const int e = off + o;
-                    c.e_lm[e] = l;
-                    c.e_src[e] = src0 + o;
-                    c.e_level[e] = 0;
-                    if (l < c.Np) {
-                        const spslam_lba_point_obs& ob = c.pobs[src0 + o];
-                        c.e_kf[e] = ob.kf;
-                        c.e_type[e] = ob.ur < 0 ? 0 : 1;
-                    } else {
-                        const spslam_lba_plane_obs& ob = c.plobs[src0 + o];
-                        c.e_kf[e] = ob.kf;
-                        c.e_type[e] = ob.kind == SPSLAM_PLANE_EDGE ? 2 : (ob.kind == SPSLAM_PARALLEL_EDGE ? 3 : 4);
-                    }
+    // edges in insertion order: point observations (points in list order), then plane observations
+    int base_e = 0;
+    for (int ch = 0; ch < c.L; ch += kThreads) {
+        const int l = ch + t;
+        const int n_obs = l < c.Np ? c.pt[l].n_obs : (l < c.L ? c.pl[l - c.Np].n_obs : 0);
+        int tot;
+        const int off = block_scan(n_obs, &tot, R) + base_e;
+        if (l < c.L) {
+            c.lm_boff[l] = off;
+            c.lm_nb[l] = n_obs;
+            const int src0 = l < c.Np ? c.pt[l].obs_offset : c.pl[l - c.Np].obs_offset;
+            for (int o = 0; o < n_obs; o++) {
+                const int e = off + o;
+                c.e_lm[e] = l;
+                c.e_src[e] = src0 + o;
+                c.e_level[e] = 0;
+                if (l < c.Np) {
+                    const spslam_lba_point_obs& ob = c.pobs[src0 + o];
+                    c.e_kf[e] = ob.kf;
+                    c.e_type[e] = ob.ur < 0 ? 0 : 1;
+                } else {
+                    const spslam_lba_plane_obs& ob = c.plobs[src0 + o];
+                    c.e_kf[e] = ob.kf;
+                    c.e_type[e] = ob.kind == SPSLAM_PLANE_EDGE ? 2 : (ob.kind == SPSLAM_PARALLEL_EDGE ? 3 : 4);
                 }
             }
-            base_e += tot;
         }
+        base_e += tot;
+    }
+    if (t == 0) {
+        LbaCtl& k = *c.ctl;
+        k = LbaCtl{};
+        k.state = c.E > 0 ? kStruct : kDone;
+        k.phase = 0;
+        k.it = 0;
+        k.max_it = max_it0;
+        k.robust = 1;
+        k.restore_step = -1;
+        k.t0 = wall_clock64();
+    }
+}
+
+// ---------------------------------------------------------------- structure
+__global__ __launch_bounds__(kThreads) void k_struct_count(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.kf_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kStruct) return;
+    const int k = task.y;
+    int n = 0;
+    for (int e = threadIdx.x; e < c.E; e += kThreads) n += (c.e_level[e] == 0 && c.e_kf[e] == k);
+    int tot;
+    block_scan(n, &tot, R);
+    if (threadIdx.x == 0) c.kf_cnt[k] = tot;
+}
+
+// pose order (non-fixed keyframes with active edges, by id), edge-list offsets, landmark masks / blocks
+__global__ __launch_bounds__(kThreads) void k_struct_final(LbaBatch b) {
+    __shared__ Red R;
+    __shared__ int hidx[kLbaMaxKeyframes];
+    const int t = threadIdx.x;
+    Ctx c = make_ctx(b, blockIdx.x);
+    if (c.ctl->state != kStruct) return;
+    if (t == 0) {
+        int np = 0, o = 0;
+        for (int k = 0; k < c.K; k++) {
+            hidx[k] = -1;
+            c.pe_off[k] = o;
+            o += c.kf_cnt[k];
+        }
+        c.pe_off[c.K] = o;
+        for (int k = 0; k < c.K; k++) {
+            const spslam_lba_keyframe& kk = c.kf[k];
+            if (!c.kf_cnt[k] || kk.fixed || kk.id == 0) continue;
+            int j = np++;
+            while (j > 0 && c.kf[c.hidx_pose[j - 1]].id > kk.id) { c.hidx_pose[j] = c.hidx_pose[j - 1]; j--; }
+            c.hidx_pose[j] = k;
+        }
+        for (int j = 0; j < np; j++) hidx[c.hidx_pose[j]] = j;
+        for (int k = 0; k < c.K; k++) c.pose_hidx[k] = hidx[k];
+        c.ctl->np = np;
     }
     __syncthreads();
-    int its[2] = {0, 0};
-    mark(S, 0);
-    if (c.E > 0) {
-        for (int phase = 0; phase < 2; phase++) {
-            initialize(c, S);
-            mark(S, 0);
-            its[phase] = optimize(c, C, phase == 0, phase == 0 ? 5 : 10, S);
-            if (phase == 0) {  // relabel with the errors cached by the last computeActiveErrors
-                for (int e = t; e < c.E; e += kThreads) {
-                    double info[3];
-                    info_of(c, C, e, info);
-                    const int ty = c.e_type[e];
-                    const double chi = chi2_of(c.err + 3 * e, info, edge_dim(ty));
-                    bool bad;
-                    if (ty == 0) bad = chi > 5.991 || !depth_positive(c, e);
-                    else if (ty == 1) bad = chi > 7.815 || !depth_positive(c, e);
-                    else if (ty == 2) bad = chi > C.plane_chi;
-                    else bad = chi > C.vp_chi;
-                    if (bad) c.e_level[e] = 1;
+    int base = 0;
+    for (int ch = 0; ch < c.L; ch += kThreads) {
+        const int l = ch + t;
+        uint64_t mask = 0;
+        bool act = false;
+        int e_beg = 0, e_end = 0;
+        if (l < c.L) {
+            e_beg = c.lm_boff[l];
+            e_end = e_beg + c.lm_nb[l];
+        }
+        for (int e = e_beg; e < e_end; e++)
+            if (c.e_level[e] == 0) {
+                act = true;
+                const int h = hidx[c.e_kf[e]];
+                if (h >= 0) mask |= 1ull << h;
+            }
+        const int nb = __popcll(mask);
+        int tot;
+        const int off = block_scan(nb, &tot, R) + base;
+        if (l < c.L) {
+            c.lm_mask[l] = mask;
+            c.lm_act[l] = act ? off + 1 : 0;
+            for (int e = e_beg; e < e_end; e++) {
+                const int h = hidx[c.e_kf[e]];
+                c.e_blk[e] = (c.e_level[e] == 0 && h >= 0) ? off + __popcll(mask & ((1ull << h) - 1)) : -1;
+            }
+        }
+        base += tot;
+    }
+}
+
+// stable per-keyframe lists of active edges (insertion order)
+__global__ __launch_bounds__(kThreads) void k_struct_fill(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.kf_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kStruct) return;
+    const int k = task.y;
+    int o = c.pe_off[k];
+    for (int ch = 0; ch < c.E; ch += kThreads) {
+        const int e = ch + threadIdx.x;
+        const int f = e < c.E && c.e_level[e] == 0 && c.e_kf[e] == k;
+        int tot;
+        const int r = block_scan(f, &tot, R);
+        if (f) c.pe_idx[o + r] = e;
+        o += tot;
+    }
+}
+
+__global__ void k_struct_done(LbaBatch b) {
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kStruct) return;
+    k.state = kIter;
+    k.it = 0;
+}
+
+// ---------------------------------------------------------------- errors, edge terms, sums
+// mode 0: at the start of an LM iteration (ITER problems); mode 1: after a trial update (TRIAL problems)
+__global__ __launch_bounds__(kThreads) void k_errors(LbaBatch b, LbaWork w, LbaConsts C, int mode) {
+    __shared__ Red R;
+    const int2 task = w.edge_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != (mode == 0 ? kIter : kTrial)) return;
+    const int e = task.y + threadIdx.x;
+    double acc[1] = {0.0};
+    if (e < c.E && c.e_level[e] == 0) {
+        const int lm = c.e_lm[e];
+        const SE3 T = load_pose(c.pose + 7 * c.e_kf[e]);
+        double* err = c.err + 3 * e;
+        P4 P;
+        if (lm >= c.Np) {
+            const double* pp = c.P + 4 * (lm - c.Np);
+            P = P4{{pp[0], pp[1], pp[2], pp[3]}};
+        }
+        edge_error(c, e, T, lm < c.Np ? c.X + 3 * lm : nullptr, &P, err);
+        double info[3];
+        info_of(c, C, e, info);
+        const int ty = c.e_type[e];
+        double r0, r1;
+        huber(chi2_of(err, info, edge_dim(ty)), delta_of(C, ty), k.robust, &r0, &r1);
+        acc[0] = r0;
+    }
+    block_sum(acc, R);
+    if (threadIdx.x == 0) c.part_chi[task.y / kThreads] = acc[0];
+}
+
+__global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, LbaConsts C) {
+    const int2 task = w.edge_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kIter) return;
+    const int e = task.y + threadIdx.x;
+    if (e >= c.E || c.e_level[e] != 0) return;
+    const bool robust = k.robust;
+    const int ty = c.e_type[e], dim = edge_dim(ty);
+    const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
+    double A[3][3] = {}, B[3][6] = {};
+    edge_jacobians(c, e, pfree, A, B);
+    double info[3];
+    info_of(c, C, e, info);
+    const double* err = c.err + 3 * e;
+    double r0, wgt;
+    huber(chi2_of(err, info, dim), delta_of(C, ty), robust, &r0, &wgt);
+    double W[3] = {0, 0, 0}, om[3] = {0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+        if (r < dim) {
+            W[r] = robust ? wgt * info[r] : info[r];
+            om[r] = -(info[r] * err[r]);
+            if (robust) om[r] *= wgt;
+        }
+    // rows >= dim of A, B, W, om are zero: the padded terms add exact zeros
+    double* o = c.con + (size_t)kLbaCon * e;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        o[9 + i] = (A[0][i] * om[0] + A[1][i] * om[1]) + A[2][i] * om[2];
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            o[3 * i + j] = ((A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j]) + (A[2][i] * W[2]) * A[2][j];
+#pragma unroll
+        for (int j = 0; j < 6; j++)
+            o[12 + 6 * i + j] = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
+                                            (A[2][i] * W[2]) * B[2][j]
+                                      : 0.0;
+    }
+    if (pfree) {
+        int q = 30;
+#pragma unroll
+        for (int i = 0; i < 6; i++)
+#pragma unroll
+            for (int j = i; j < 6; j++)
+                o[q++] = ((B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j]) + (B[2][i] * W[2]) * B[2][j];
+#pragma unroll
+        for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
+    }
+}
+
+// landmark Hll, bl and (landmark, pose) blocks, summed over the landmark's edges in insertion order
+__global__ __launch_bounds__(kThreads) void k_lm_sums(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.lm_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kIter) return;
+    const int l = task.y + threadIdx.x;
+    double mx = 0.0;
+    if (l < c.L && lm_block_base(c, l) >= 0) {
+        const int b0 = lm_block_base(c, l);
+        const int nb = __popcll(c.lm_mask[l]);
+        for (int j = 0; j < nb * 18; j++) c.blkH[(size_t)b0 * 18 + j] = 0.0;
+        double H[9] = {}, bl[3] = {};
+        for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
+            if (c.e_level[e] != 0) continue;
+            const double* o = c.con + (size_t)kLbaCon * e;
+#pragma unroll
+            for (int j = 0; j < 9; j++) H[j] += o[j];
+#pragma unroll
+            for (int j = 0; j < 3; j++) bl[j] += o[9 + j];
+            const int bk = c.e_blk[e];
+            if (bk >= 0) {
+                double* hb = c.blkH + (size_t)bk * 18;
+#pragma unroll
+                for (int j = 0; j < 18; j++) hb[j] += o[12 + j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 9; j++) c.lmH[9 * l + j] = H[j];
+#pragma unroll
+        for (int j = 0; j < 3; j++) c.lmb[3 * l + j] = bl[j];
+        mx = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
+    }
+    mx = block_max(mx, R);
+    if (threadIdx.x == 0) c.part_max[task.y / kThreads] = mx;
+}
+
+// keyframe Hpp, bp over its active edges (free poses only)
+__global__ __launch_bounds__(kThreads) void k_pose_sums(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.kf_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kIter) return;
+    const int k = task.y, h = c.pose_hidx[k];
+    if (h < 0) {
+        if (threadIdx.x == 0) c.part_max[c.nLc + k] = 0.0;
+        return;
+    }
+    double acc[27];
+#pragma unroll
+    for (int j = 0; j < 27; j++) acc[j] = 0.0;
+    for (int i = c.pe_off[k] + threadIdx.x; i < c.pe_off[k + 1]; i += kThreads) {
+        const double* o = c.con + (size_t)kLbaCon * c.pe_idx[i] + 30;
+#pragma unroll
+        for (int j = 0; j < 27; j++) acc[j] += o[j];
+    }
+    block_sum(acc, R);
+    if (threadIdx.x < 36) {
+        const int r = threadIdx.x / 6, q = threadIdx.x % 6, i = r < q ? r : q, j = r < q ? q : r;
+        const int idx = 6 * i - i * (i - 1) / 2 + (j - i);
+        double v = 0.0;
+#pragma unroll
+        for (int m = 0; m < 21; m++) if (m == idx) v = acc[m];
+        c.Hpp[36 * h + threadIdx.x] = v;
+    } else if (threadIdx.x < 42) {
+        double v = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; m++) if (m == threadIdx.x - 36) v = acc[21 + m];
+        c.bp[6 * h + threadIdx.x - 36] = v;
+    }
+    if (threadIdx.x == 0)
+        c.part_max[c.nLc + k] = fmax(fmax(fmax(fabs(acc[0]), fabs(acc[6])), fmax(fabs(acc[11]), fabs(acc[15]))),
+                                     fmax(fabs(acc[18]), fabs(acc[20])));
+}
+
+__global__ void k_iter_begin(LbaBatch b) {
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kIter) return;
+    double chi = 0.0;
+    for (int i = 0; i < c.nEc; i++) chi += c.part_chi[i];
+    k.currentChi = chi;
+    k.iniChi = chi;
+    if (k.it == 0) {  // computeLambdaInit: tau * max |diag| over the Hessian vertices
+        double mx = 0.0;
+        for (int i = 0; i < c.nLc + c.K; i++) mx = fmax(mx, c.part_max[i]);
+        k.lambda = 1e-5 * mx;
+        k.ni = 2;
+        k.nBad = 0;
+    }
+    k.qmax = 0;
+    k.state = kTrial;
+}
+
+// ---------------------------------------------------------------- Schur complement
+__global__ __launch_bounds__(kThreads) void k_schur_lm(LbaBatch b, LbaWork w) {
+    const int2 task = w.lm_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int l = task.y + threadIdx.x;
+    if (l >= c.L || lm_block_base(c, l) < 0) return;
+    const double lam = k.lambda;
+    const int b0 = lm_block_base(c, l);
+    double D[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) D[i][j] = c.lmH[9 * l + 3 * i + j] + (i == j ? lam : 0.0);
+    double Di[9];
+    inverse3(D, Di);
+#pragma unroll
+    for (int j = 0; j < 9; j++) c.Dinv[9 * l + j] = Di[j];
+    const double* bl = c.lmb + 3 * l;
+#pragma unroll
+    for (int i = 0; i < 3; i++) c.db[3 * l + i] = (Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1]) + Di[3 * i + 2] * bl[2];
+    const int nb = __popcll(c.lm_mask[l]);
+    for (int a = 0; a < nb; a++) {
+        const double* H = c.blkH + (size_t)(b0 + a) * 18;  // 3 x 6 (landmark x pose)
+        double* BD = c.blkBD + (size_t)(b0 + a) * 18;     // 6 x 3
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) BD[3 * r + q] = (H[r] * Di[q] + H[6 + r] * Di[3 + q]) + H[12 + r] * Di[6 + q];
+    }
+}
+
+// pose-pair tasks: S(p1, p2) for p1 <= p2 (task < np(np+1)/2), then bs(p) (next np tasks)
+__global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.pair_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int np = k.np, n = 6 * np, npairs = np * (np + 1) / 2, tid = task.y;
+    if (tid >= npairs + np) return;
+    if (tid < npairs) {
+        int p1 = 0, rem = tid;
+        while (rem >= np - p1) { rem -= np - p1; p1++; }
+        const int p2 = p1 + rem;
+        const uint64_t need = (1ull << p1) | (1ull << p2);
+        double acc[36];
+#pragma unroll
+        for (int j = 0; j < 36; j++) acc[j] = 0.0;
+        for (int l = threadIdx.x; l < c.L; l += kThreads) {
+            const uint64_t m = c.lm_mask[l];
+            if ((m & need) != need) continue;
+            const int b0 = lm_block_base(c, l);
+            const int ia = b0 + __popcll(m & ((1ull << p1) - 1)), ib = b0 + __popcll(m & ((1ull << p2) - 1));
+            const double* BD = c.blkBD + (size_t)ia * 18;
+            const double* H = c.blkH + (size_t)ib * 18;
+            double bd[18], hh[18];
+#pragma unroll
+            for (int j = 0; j < 18; j++) { bd[j] = BD[j]; hh[j] = H[j]; }
+#pragma unroll
+            for (int r = 0; r < 6; r++)
+#pragma unroll
+                for (int q = 0; q < 6; q++)
+                    acc[6 * r + q] += (bd[3 * r] * hh[q] + bd[3 * r + 1] * hh[6 + q]) + bd[3 * r + 2] * hh[12 + q];
+        }
+        block_sum(acc, R);
+        if (threadIdx.x < 36) {
+            const int r = threadIdx.x / 6, q = threadIdx.x % 6;
+            double v = 0.0;
+#pragma unroll
+            for (int j = 0; j < 36; j++) if (j == (int)threadIdx.x) v = acc[j];
+            const double base = p1 == p2 ? c.Hpp[36 * p1 + threadIdx.x] + (r == q ? k.lambda : 0.0) : 0.0;
+            c.S[(size_t)(6 * p1 + r) * n + 6 * p2 + q] = base - v;
+        }
+    } else {
+        const int p = tid - npairs;
+        double acc[6] = {0, 0, 0, 0, 0, 0};
+        for (int l = threadIdx.x; l < c.L; l += kThreads) {
+            const uint64_t m = c.lm_mask[l];
+            if (!((m >> p) & 1)) continue;
+            const int ia = lm_block_base(c, l) + __popcll(m & ((1ull << p) - 1));
+            const double* H = c.blkH + (size_t)ia * 18;
+            const double* db = c.db + 3 * l;
+#pragma unroll
+            for (int r = 0; r < 6; r++) acc[r] += (H[r] * db[0] + H[6 + r] * db[1]) + H[12 + r] * db[2];
+        }
+        block_sum(acc, R);
+        if (threadIdx.x < 6) {
+            double v = 0.0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) if (j == (int)threadIdx.x) v = acc[j];
+            c.bs[6 * p + threadIdx.x] = c.bp[6 * p + threadIdx.x] - v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- reduced system
+__global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
+    extern __shared__ double lds[];
+    const int t = threadIdx.x;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int n = 6 * k.np;
+    const bool in_lds = (size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds;
+    double* A = in_lds ? lds : c.S;
+    double* y = in_lds ? lds + (size_t)n * n : c.y;
+    double* dd = in_lds ? y + n : c.dd;
+    if (in_lds) {
+        for (int i = t; i < n * n; i += kThreads) A[i] = c.S[i];
+        for (int i = t; i < n; i += kThreads) y[i] = c.bs[i];
+    } else {
+        for (int i = t; i < n; i += kThreads) y[i] = c.bs[i];
+    }
+    __syncthreads();
+    // LDL^T of the upper triangle, right-looking: entry (r, q), r <= q, loses (L[q][j] d_j) L[r][j] at step j;
+    // L[i][j] is kept in the lower triangle
+    bool ok = true;
+    for (int j = 0; j < n; j++) {
+        const double dj = A[(size_t)j * n + j];
+        if (dj == 0.0) { ok = false; break; }
+        for (int i = j + 1 + t; i < n; i += kThreads) A[(size_t)i * n + j] = A[(size_t)j * n + i] / dj;
+        if (t == 0) dd[j] = dj;
+        __syncthreads();
+        const int m = n - j - 1;
+        for (int r = j + 1 + t / 16; r < n; r += kThreads / 16) {
+            const double lr = A[(size_t)r * n + j];
+            for (int q = r + (t & 15); q < n; q += 16) A[(size_t)r * n + q] -= (A[(size_t)q * n + j] * dj) * lr;
+        }
+        (void)m;
+        __syncthreads();
+    }
+    if (ok) {
+        for (int kk = 0; kk < n; kk++) {  // forward: y[i] -= L[i][k] y[k], k increasing
+            const double yk = y[kk];
+            __syncthreads();
+            for (int i = kk + 1 + t; i < n; i += kThreads) y[i] -= A[(size_t)i * n + kk] * yk;
+            __syncthreads();
+        }
+        for (int i = t; i < n; i += kThreads) y[i] /= dd[i];
+        __syncthreads();
+        for (int kk = n - 1; kk >= 0; kk--) {  // backward: y[i] -= L[k][i] y[k], k decreasing
+            const double yk = y[kk];
+            __syncthreads();
+            for (int i = t; i < kk; i += kThreads) y[i] -= A[(size_t)kk * n + i] * yk;
+            __syncthreads();
+        }
+        if (in_lds)
+            for (int i = t; i < n; i += kThreads) c.y[i] = y[i];
+    }
+    if (t == 0) k.ok = ok;
+}
+
+// ---------------------------------------------------------------- update / restore
+__global__ __launch_bounds__(kThreads) void k_update_lm(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.lm_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int l = task.y + threadIdx.x;
+    double acc[1] = {0.0};
+    if (l < c.L) {
+        // push()
+        if (l < c.Np) for (int j = 0; j < 3; j++) c.X_b[3 * l + j] = c.X[3 * l + j];
+        else for (int j = 0; j < 4; j++) c.P_b[4 * (l - c.Np) + j] = c.P[4 * (l - c.Np) + j];
+        const int b0 = lm_block_base(c, l);
+        if (k.ok && b0 >= 0) {
+            double cl[3] = {c.lmb[3 * l], c.lmb[3 * l + 1], c.lmb[3 * l + 2]};
+            uint64_t m = c.lm_mask[l];
+            for (int a = 0; m; a++) {
+                const int h = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const double* H = c.blkH + (size_t)(b0 + a) * 18;
+#pragma unroll
+                for (int i = 0; i < 3; i++) {
+                    double s = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) s += H[6 * i + j] * (-c.y[6 * h + j]);
+                    cl[i] += s;
                 }
-                __syncthreads();
+            }
+            const double* Di = c.Dinv + 9 * l;
+            double x[3];
+#pragma unroll
+            for (int i = 0; i < 3; i++) x[i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
+#pragma unroll
+            for (int i = 0; i < 3; i++) acc[0] += x[i] * (k.lambda * x[i] + c.lmb[3 * l + i]);
+            if (l < c.Np) {
+                for (int j = 0; j < 3; j++) c.X[3 * l + j] += x[j];
+            } else {
+                double* pp = c.P + 4 * (l - c.Np);
+                P4 P{{pp[0], pp[1], pp[2], pp[3]}};
+                p_oplus(P, x);
+                for (int j = 0; j < 4; j++) pp[j] = P.c[j];
             }
         }
     }
-    // ---- outlier flags (cached errors), write back
+    block_sum(acc, R);
+    if (threadIdx.x == 0) c.part_scale[task.y / kThreads] = acc[0];
+}
+
+__global__ void k_update_pose(LbaBatch b, LbaWork w) {
+    const int2 task = w.kf_tasks[blockIdx.x];
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int kf = task.y, h = c.pose_hidx[kf];
+    for (int j = 0; j < 7; j++) c.pose_b[7 * kf + j] = c.pose[7 * kf + j];
+    if (!k.ok || h < 0) return;
+    double u[6];
+    for (int j = 0; j < 6; j++) u[j] = c.y[6 * h + j];
+    store_pose(c.pose + 7 * kf, se3_mul(se3_exp(u), load_pose(c.pose + 7 * kf)));
+}
+
+// OptimizationAlgorithmLevenberg accept / reject + iteration / schedule bookkeeping
+__global__ void k_decide(LbaBatch b, int step) {
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    double tempChi = 0.0;
+    for (int i = 0; i < c.nEc; i++) tempChi += c.part_chi[i];
+    double scale = 0.0;
+    if (k.ok) {
+        const int n = 6 * k.np;
+        for (int i = 0; i < n; i++) scale += c.y[i] * (k.lambda * c.y[i] + c.bp[i]);
+        for (int i = 0; i < c.nLc; i++) scale += c.part_scale[i];
+    } else {
+        tempChi = DBL_MAX;
+    }
+    double rho = (k.currentChi - tempChi) / (scale + 1e-3);
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3);
+        alpha = fmin(alpha, 2. / 3.);
+        k.lambda *= fmax(1. / 3., alpha);
+        k.ni = 2;
+        k.currentChi = tempChi;
+    } else {
+        k.lambda *= k.ni;
+        k.ni *= 2;
+        k.restore_step = step;  // k_restore_* roll back in this step
+    }
+    k.qmax++;
+    k.trials++;
+    if (rho < 0 && k.qmax < 10) return;  // next trial
+    k.its[k.phase]++;
+    bool term = k.qmax == 10 || rho == 0;
+    if (!term) {
+        if ((k.iniChi - k.currentChi) * 1e3 < k.iniChi) k.nBad++;
+        else k.nBad = 0;
+        term = k.nBad >= 3;
+    }
+    k.it++;
+    if (k.it >= k.max_it) term = true;
+    if (term) k.state = k.phase == 0 ? kRelabel : kDone;
+    else k.state = kIter;
+}
+
+__global__ __launch_bounds__(kThreads) void k_restore_lm(LbaBatch b, LbaWork w, int step) {
+    const int2 task = w.lm_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->restore_step != step) return;
+    const int l = task.y + threadIdx.x;
+    if (l >= c.L) return;
+    if (l < c.Np) for (int j = 0; j < 3; j++) c.X[3 * l + j] = c.X_b[3 * l + j];
+    else for (int j = 0; j < 4; j++) c.P[4 * (l - c.Np) + j] = c.P_b[4 * (l - c.Np) + j];
+}
+__global__ void k_restore_pose(LbaBatch b, LbaWork w, int step) {
+    const int2 task = w.kf_tasks[blockIdx.x];
+    if (threadIdx.x >= 7) return;
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->restore_step != step) return;
+    c.pose[7 * task.y + threadIdx.x] = c.pose_b[7 * task.y + threadIdx.x];
+}
+
+// ---------------------------------------------------------------- relabel (between optimize(5) and optimize(10))
+__global__ __launch_bounds__(kThreads) void k_relabel(LbaBatch b, LbaWork w, LbaConsts C) {
+    const int2 task = w.edge_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kRelabel) return;
+    const int e = task.y + threadIdx.x;
+    if (e >= c.E) return;
+    double info[3];
+    info_of(c, C, e, info);
+    const int ty = c.e_type[e];
+    const double chi = chi2_of(c.err + 3 * e, info, edge_dim(ty));
+    bool bad;
+    if (ty == 0) bad = chi > 5.991 || !depth_positive(c, e);
+    else if (ty == 1) bad = chi > 7.815 || !depth_positive(c, e);
+    else if (ty == 2) bad = chi > C.plane_chi;
+    else bad = chi > C.vp_chi;
+    if (bad) c.e_level[e] = 1;
+}
+__global__ void k_relabel_done(LbaBatch b, int max_it1) {
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kRelabel) return;
+    k.state = kStruct;
+    k.phase = 1;
+    k.robust = 0;  // setRobustKernel(0) on every edge
+    k.it = 0;
+    k.max_it = max_it1;
+}
+
+__global__ void k_count_active(LbaBatch b) {
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (int p = threadIdx.x; p < b.n; p += blockDim.x) {
+        Ctx c = make_ctx(b, p);
+        if (c.ctl->state != kDone) atomicAdd(&cnt, 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *b.active = cnt;
+}
+
+// ---------------------------------------------------------------- outputs
+__global__ __launch_bounds__(kThreads) void k_outputs(LbaBatch b, LbaConsts C) {
+    __shared__ Red R;
+    const int p = blockIdx.x, t = threadIdx.x;
+    Ctx c = make_ctx(b, p);
+    const spslam_lba_problem pb = b.probs[p];
+    if (c.K > kLbaMaxKeyframes) return;
     int npo = 0, nplo = 0;
     for (int e = t; e < c.E; e += kThreads) {
         double info[3];
@@ -888,18 +1012,18 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
         const double chi = chi2_of(c.err + 3 * e, info, edge_dim(ty));
         if (ty <= 1) {
             const bool bad = chi > (ty == 0 ? 5.991 : 7.815) || !depth_positive(c, e);
-            pobs_out[c.e_src[e]] = bad;
+            b.pobs_out[c.e_src[e]] = bad;
             npo += bad;
         } else {
             const bool bad = ty == 2 ? chi > C.plane_chi : chi > C.vp_chi;
-            plobs_out[c.e_src[e]] = bad;
+            b.plobs_out[c.e_src[e]] = bad;
             nplo += bad;
         }
     }
     double cnt[2] = {(double)npo, (double)nplo};
-    block_sum(cnt, S);
+    block_sum(cnt, R);
     for (int k = t; k < c.K; k += kThreads) {
-        float* o = kf_out + 16 * ((size_t)pb.kf_offset + k);
+        float* o = b.kf_out + 16 * ((size_t)pb.kf_offset + k);
         if (c.kf[k].fixed) {
             for (int j = 0; j < 16; j++) o[j] = c.kf[k].Tcw[j];
             continue;
@@ -912,31 +1036,70 @@ __global__ __launch_bounds__(kThreads) void lba_kernel(
         o[12] = 0.f; o[13] = 0.f; o[14] = 0.f; o[15] = 1.f;
     }
     for (int i = t; i < c.Np; i += kThreads)
-        for (int j = 0; j < 3; j++) pt_out[3 * ((size_t)pb.point_offset + i) + j] = (float)c.X[3 * i + j];
+        for (int j = 0; j < 3; j++) b.pt_out[3 * ((size_t)pb.point_offset + i) + j] = (float)c.X[3 * i + j];
     for (int i = t; i < c.Nq; i += kThreads)
-        for (int j = 0; j < 4; j++) pl_out[4 * ((size_t)pb.plane_offset + i) + j] = (float)c.P[4 * i + j];
+        for (int j = 0; j < 4; j++) b.pl_out[4 * ((size_t)pb.plane_offset + i) + j] = (float)c.P[4 * i + j];
     if (t == 0) {
-        R->iterations[0] = its[0];
-        R->iterations[1] = its[1];
-        R->n_point_outliers = (int)cnt[0];
-        R->n_plane_outliers = (int)cnt[1];
-        R->status = 0;
-        R->trials = S.trials;
-        for (int k = 0; k < 8; k++) R->phase_us[k] = (float)(S.t_phase[k] * 0.01);  // 100 MHz ticks
+        const LbaCtl& k = *c.ctl;
+        spslam_lba_result* r = b.res + p;
+        *r = spslam_lba_result{};
+        r->iterations[0] = k.its[0];
+        r->iterations[1] = k.its[1];
+        r->n_point_outliers = (int)cnt[0];
+        r->n_plane_outliers = (int)cnt[1];
+        r->status = k.state == kDone ? 0 : -3;
+        r->trials = k.trials;
+        r->phase_us[0] = (float)((wall_clock64() - k.t0) * 0.01);  // 100 MHz ticks: setup to outputs
     }
 }
 
 }  // namespace lba
 
-hipError_t lba_launch(int n, const spslam_lba_problem* d_probs, const long long* d_scratch_off,
-                      const spslam_lba_keyframe* kfs, const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
-                      const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs, const LbaConsts& C,
-                      uint8_t* scratch, float* kf_out, float* pt_out, float* pl_out, uint8_t* pobs_out,
-                      uint8_t* plobs_out, spslam_lba_result* res, hipStream_t s, KernelTimer* timer) {
+hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int max_steps, hipStream_t s,
+                   KernelTimer* timer, int* steps_out) {
+    using namespace lba;
+    static const hipError_t lds_attr =
+        hipFuncSetAttribute((const void*)k_factor, hipFuncAttributeMaxDynamicSharedMemorySize, kFactorLds);
+    (void)lds_attr;
     if (timer) timer->begin(kKindLba, s);
-    hipLaunchKernelGGL(lba::lba_kernel, dim3(n), dim3(lba::kThreads), 0, s, d_probs, d_scratch_off, kfs, pts, pobs,
-                       pls, plobs, C, scratch, kf_out, pt_out, pl_out, pobs_out, plobs_out, res);
+    const dim3 T(kThreads);
+    const int P = b.n;
+    hipLaunchKernelGGL(k_setup, dim3(P), T, 0, s, b, 5);
+    int steps = 0, active = 1;
+    while (steps < max_steps) {
+        const int st = steps;
+        hipLaunchKernelGGL(k_struct_count, dim3(w.n_kf_tasks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_struct_final, dim3(P), T, 0, s, b);
+        hipLaunchKernelGGL(k_struct_fill, dim3(w.n_kf_tasks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_struct_done, dim3(P), dim3(64), 0, s, b);
+        hipLaunchKernelGGL(k_errors, dim3(w.n_edge_chunks), T, 0, s, b, w, C, 0);
+        hipLaunchKernelGGL(k_edge_terms, dim3(w.n_edge_chunks), T, 0, s, b, w, C);
+        hipLaunchKernelGGL(k_lm_sums, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_pose_sums, dim3(w.n_kf_tasks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_iter_begin, dim3(P), dim3(64), 0, s, b);
+        hipLaunchKernelGGL(k_schur_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_pairs, dim3(w.n_pair_tasks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_factor, dim3(P), T, kFactorLds, s, b);
+        hipLaunchKernelGGL(k_update_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_update_pose, dim3(w.n_kf_tasks), dim3(64), 0, s, b, w);
+        hipLaunchKernelGGL(k_errors, dim3(w.n_edge_chunks), T, 0, s, b, w, C, 1);
+        hipLaunchKernelGGL(k_decide, dim3(P), dim3(64), 0, s, b, st);
+        hipLaunchKernelGGL(k_restore_lm, dim3(w.n_lm_chunks), T, 0, s, b, w, st);
+        hipLaunchKernelGGL(k_restore_pose, dim3(w.n_kf_tasks), dim3(64), 0, s, b, w, st);
+        hipLaunchKernelGGL(k_relabel, dim3(w.n_edge_chunks), T, 0, s, b, w, C);
+        hipLaunchKernelGGL(k_relabel_done, dim3(P), dim3(64), 0, s, b, 10);
+        steps++;
+        if (steps % 4 == 0) {
+            hipLaunchKernelGGL(k_count_active, dim3(1), T, 0, s, b);
+            hipError_t e = hipMemcpyAsync(&active, b.active, sizeof(int), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            if (active == 0) break;
+        }
+    }
+    hipLaunchKernelGGL(k_outputs, dim3(P), T, 0, s, b, C);
     if (timer) timer->end(kKindLba, s);
+    if (steps_out) *steps_out = steps;
     return hipGetLastError();
 }
 

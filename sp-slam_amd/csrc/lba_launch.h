@@ -8,23 +8,38 @@
 namespace spslam {
 
 constexpr int kLbaMaxKeyframes = 64;   // local + fixed keyframes per problem (pose masks are 64-bit)
+constexpr int kLbaChunk = 256;         // edges / landmarks per workgroup in the grid-wide phases
+constexpr int kLbaCon = 57;            // per-edge terms: Hll 9, bl 3, Hpl 18 (3x6), Hpp upper 21, bp 6
+
+// LM / schedule state of one problem (device, in its scratch); see lba_kernels.hip.
+struct LbaCtl {
+    int state;        // 0 STRUCT, 1 ITER, 2 TRIAL, 3 RELABEL, 4 DONE
+    int phase, it, max_it, robust, qmax, nBad, np, ok, restore_step, trials, its[2];
+    int pad;
+    double lambda, ni, currentChi, iniChi;
+    long long t0;     // wall_clock64 at setup (diagnostics)
+};
 
 // Per-problem scratch layout (bytes), computed identically on host and device.
 struct LbaLayout {
+    size_t ctl;
     size_t pose, pose_b, pt, pt_b, pl, pl_b, e_err, e_con, lm_H, lm_b, lm_Dinv, lm_db, lm_x, blk_H, blk_BD, S, bs,
-        dd, y, Hpp, bp;                                                      // double arrays
-    size_t pose_hidx, hidx_pose, e_lm, e_kf, e_type, e_level, e_blk, e_src, lm_boff, lm_nb, blk_pose, lm_act;  // int
-    size_t lm_mask;                                                          // uint64
+        dd, y, Hpp, bp, part_chi, part_scale, part_max;                                    // double arrays
+    size_t pose_hidx, hidx_pose, e_lm, e_kf, e_type, e_level, e_blk, e_src, lm_boff, lm_nb, lm_act, kf_cnt, pe_off,
+        pe_idx;                                                                            // int arrays
+    size_t lm_mask;                                                                        // uint64
     size_t bytes;
 };
 
-constexpr int kLbaCon = 57;  // per-edge contribution: Hll 9, bl 3, Hpl 18 (3x6), Hpp upper 21, bp 6
+__host__ __device__ inline int lba_chunks(int n) { return (n + kLbaChunk - 1) / kLbaChunk; }
 
 __host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
     LbaLayout L{};
     const size_t Lm = (size_t)Np + Nq, n6 = 6 * (size_t)K;
+    const size_t nEc = lba_chunks(E), nLc = lba_chunks((int)Lm);
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
+    L.ctl = take(sizeof(LbaCtl));
     L.pose = take(K * 7 * 8); L.pose_b = take(K * 7 * 8);
     L.pt = take(Np * 3 * 8); L.pt_b = take(Np * 3 * 8);
     L.pl = take(Nq * 4 * 8); L.pl_b = take(Nq * 4 * 8);
@@ -34,10 +49,12 @@ __host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
     L.blk_H = take((size_t)E * 18 * 8); L.blk_BD = take((size_t)E * 18 * 8);
     L.S = take(n6 * n6 * 8); L.bs = take(n6 * 8); L.dd = take(n6 * 8); L.y = take(n6 * 8);
     L.Hpp = take(K * 36 * 8); L.bp = take(K * 6 * 8);
+    L.part_chi = take(nEc * 8); L.part_scale = take(nLc * 8); L.part_max = take((nLc + K) * 8);
     L.pose_hidx = take(K * 4); L.hidx_pose = take(K * 4);
     L.e_lm = take((size_t)E * 4); L.e_kf = take((size_t)E * 4); L.e_type = take((size_t)E * 4);
     L.e_level = take((size_t)E * 4); L.e_blk = take((size_t)E * 4); L.e_src = take((size_t)E * 4);
-    L.lm_boff = take(Lm * 4); L.lm_nb = take(Lm * 4); L.blk_pose = take((size_t)E * 4); L.lm_act = take(Lm * 4);
+    L.lm_boff = take(Lm * 4); L.lm_nb = take(Lm * 4); L.lm_act = take(Lm * 4);
+    L.kf_cnt = take(K * 4); L.pe_off = take((K + 1) * 4); L.pe_idx = take((size_t)E * 4);
     L.lm_mask = take(Lm * 8);
     L.bytes = o;
     return L;
@@ -48,10 +65,34 @@ struct LbaConsts {
     double delta_mono, delta_stereo, delta_plane, delta_vp;             // Huber deltas (float sqrt, as g2o gets them)
 };
 
-hipError_t lba_launch(int n, const spslam_lba_problem* d_probs, const long long* d_scratch_off,
-                      const spslam_lba_keyframe* kfs, const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
-                      const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs, const LbaConsts& C,
-                      uint8_t* scratch, float* kf_out, float* pt_out, float* pl_out, uint8_t* pobs_out,
-                      uint8_t* plobs_out, spslam_lba_result* res, hipStream_t s, KernelTimer* timer);
+// Work tables of a batch (host-built, device copies): (problem, first index) per workgroup.
+struct LbaWork {
+    const int2* edge_chunks; int n_edge_chunks;
+    const int2* lm_chunks; int n_lm_chunks;
+    const int2* kf_tasks; int n_kf_tasks;
+    const int2* pair_tasks; int n_pair_tasks;
+};
+
+struct LbaBatch {
+    int n;
+    const spslam_lba_problem* probs;
+    const long long* scratch_off;
+    uint8_t* scratch;
+    const spslam_lba_keyframe* kfs;
+    const spslam_lba_point* pts;
+    const spslam_lba_point_obs* pobs;
+    const spslam_lba_plane* pls;
+    const spslam_lba_plane_obs* plobs;
+    float *kf_out, *pt_out, *pl_out;
+    uint8_t *pobs_out, *plobs_out;
+    spslam_lba_result* res;
+    int* active;      // problems not DONE (polled by the host)
+};
+
+// Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase
+// kernels step by step on `s` and polls the device every few steps until
+// every problem is DONE (so it returns after the work completed).
+hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int max_steps, hipStream_t s,
+                   KernelTimer* timer, int* steps_out);
 
 }  // namespace spslam

@@ -124,6 +124,8 @@ struct spslam_ctx {
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
     size_t lba_stage_bytes = 0;
+    int2* d_lba_work = nullptr;       // (problem, first index) work tables + the active counter
+    size_t lba_work_cap = 0;
 };
 
 namespace {
@@ -246,7 +248,7 @@ void free_all(spslam_ctx* c) {
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
                     c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1,
-                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage};
+                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -915,6 +917,8 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
     if (n < 1 || !problems || !d_problems || !d_kfs || !cfg || !d_kf_out || !d_results)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
     std::vector<long long> off(n);
+    // work tables: edge chunks, landmark chunks, keyframe tasks, pose-pair (+ bs) tasks per problem
+    std::vector<int2> ec, lc, kt, pt;
     size_t total = 0;
     for (int i = 0; i < n; i++) {
         const spslam_lba_problem& p = problems[i];
@@ -923,8 +927,15 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
         if ((p.n_points && (!d_points || !d_point_obs || !d_pt_out || !d_point_obs_outlier)) ||
             (p.n_planes && (!d_planes || !d_plane_obs || !d_pl_out || !d_plane_obs_outlier)))
             return fail(c, SPSLAM_ERR_ARG, "missing LBA buffers%s", "");
+        const int E = p.n_point_obs + p.n_plane_obs, L = p.n_points + p.n_planes;
         off[i] = (long long)total;
-        total += lba_layout(p.n_kf, p.n_points, p.n_planes, p.n_point_obs + p.n_plane_obs).bytes;
+        total += lba_layout(p.n_kf, p.n_points, p.n_planes, E).bytes;
+        if (p.n_kf > kLbaMaxKeyframes) continue;  // rejected on the device (status -2)
+        for (int e = 0; e < E; e += kLbaChunk) ec.push_back(int2{i, e});
+        for (int l = 0; l < L; l += kLbaChunk) lc.push_back(int2{i, l});
+        for (int k = 0; k < p.n_kf; k++) kt.push_back(int2{i, k});
+        const int npmax = p.n_kf;  // bound on the free poses; surplus tasks exit on the device
+        for (int q = 0; q < npmax * (npmax + 1) / 2 + npmax; q++) pt.push_back(int2{i, q});
     }
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
@@ -943,7 +954,23 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
         HIP_CHECK(c, hipMalloc(&c->d_lba_off, (size_t)n * sizeof(long long)));
         c->lba_off_cap = n;
     }
+    std::vector<int2> work;
+    work.reserve(ec.size() + lc.size() + kt.size() + pt.size() + 1);
+    work.insert(work.end(), ec.begin(), ec.end());
+    work.insert(work.end(), lc.begin(), lc.end());
+    work.insert(work.end(), kt.begin(), kt.end());
+    work.insert(work.end(), pt.begin(), pt.end());
+    work.push_back(int2{0, 0});  // active counter
+    if (work.size() > c->lba_work_cap) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_lba_work) (void)hipFree(c->d_lba_work);
+        c->d_lba_work = nullptr;
+        c->lba_work_cap = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_lba_work, work.size() * sizeof(int2)));
+        c->lba_work_cap = work.size();
+    }
     HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
+    HIP_CHECK(c, hipMemcpyAsync(c->d_lba_work, work.data(), work.size() * sizeof(int2), hipMemcpyHostToDevice, s));
     LbaConsts C{};
     C.angle_info = 3282.8 / (cfg->angle_info * cfg->angle_info);
     C.dis_info = cfg->distance_info * cfg->distance_info;
@@ -955,9 +982,14 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
     C.delta_stereo = (float)std::sqrt(7.815);
     C.delta_plane = (float)std::sqrt(cfg->chi);  // const float deltaPlane = sqrt(planeChi)
     C.delta_vp = (float)std::sqrt(cfg->vp_chi);
-    HIP_CHECK(c, lba_launch(n, d_problems, c->d_lba_off, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs, C,
-                            c->d_lba_scratch, d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier,
-                            d_results, s, c->timer));
+    const int2* w0 = c->d_lba_work;
+    LbaWork W{w0, (int)ec.size(), w0 + ec.size(), (int)lc.size(), w0 + ec.size() + lc.size(), (int)kt.size(),
+              w0 + ec.size() + lc.size() + kt.size(), (int)pt.size()};
+    LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
+               d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
+               (int*)(c->d_lba_work + work.size() - 1)};
+    // optimize(5) + optimize(10), at most 10 trials per iteration, plus the two structure steps
+    HIP_CHECK(c, lba_run(B, W, C, 15 * 10 + 4, s, c->timer, nullptr));
     return SPSLAM_OK;
 }
 
