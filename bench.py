@@ -83,7 +83,7 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
         "supp_assemble_kernel": n_sup * (64 + 2601 * 12),     # appended planes + synthetic patches out
         "frame_rgbd_kernel": n_kp * (28 + 4 + 28 + 4 + 4 + 4) + 4 * 3073,  # kp in, depth gather, kp/depth/uR/idx out
-        "lba_kernel": lba_bytes,                              # graph in + poses/points/planes/flags out, per problem
+        "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
 
 
@@ -165,7 +165,7 @@ def main():
     for _ in range(args.warmup):
         hp.step()
     torch.cuda.synchronize()
-    hp.ex.set_timing(True)
+    hp.set_timing(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -176,7 +176,7 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    times = {k: v for k, v in hp.ex.kernel_times().items() if v[1] > 0}
+    times = {k: v for k, v in hp.kernel_times().items() if v[1] > 0}
     res = hp.results()
     elapsed = max_over_ranks(elapsed, dist, "cuda")
 

@@ -458,6 +458,63 @@ int spslam_frame_rgbd_batch_device(spslam_ctx* ctx, const spslam_keypoint* d_kps
                                    float* d_mv_uright, int32_t* d_grid_off, int32_t* d_grid_idx,
                                    int* d_plane_counts, int* d_supp_counts, void* hip_stream);
 
+/* ---------------------------------------------------------------- plane association
+ * Map::AssociatePlanesByBoundary (src/Map.cc:196-340) with
+ * Map::PointDistanceFromPlane (:343-359) and Frame::ComputePlaneWorldCoeff
+ * (src/Frame.cc:1146-1150).  For every frame plane (mvPlaneCoefficients, the
+ * extracted planes followed by the supposed planes) against the map planes in
+ * mnId order (the reference iterates a std::set<MapPlane*> by pointer; the build
+ * fixes id order):
+ *   |angle| > angle_th and min boundary distance < running distance threshold
+ *      -> mvpMapPlanes[i] (the last such map plane wins, thresholds tighten);
+ *   else |angle| < running vertical threshold  -> mvpVerticalPlanes[i];
+ *   else |angle| > running parallel threshold  -> mvpParallelPlanes[i].
+ * Outputs are map-plane indices into the map-plane array (-1 = none) and
+ * mbNewPlane (some frame plane without a match).  The not-seen branches
+ * (:259-337) are dead in the reference and are not provided. */
+typedef struct spslam_map_plane {
+    float world[4];           /* MapPlane::GetWorldPos (a, b, c, d) */
+    int32_t id;               /* mnId (informative: the array order is the iteration order) */
+    int32_t boundary_offset;  /* first point of mvBoundaryPoints in the boundary xyz array */
+    int32_t n_boundary;
+    int32_t pad;
+} spslam_map_plane;           /* 32 bytes */
+
+typedef struct spslam_assoc_params {
+    float dis_th;    /* Plane.AssociationDisRef (mfDisTh) */
+    float angle_th;  /* Plane.AssociationAngRef (mfAngleTh) */
+    float ver_th;    /* Plane.VerticalThreshold (mfVerTh) */
+    float par_th;    /* Plane.ParallelThreshold (mfParTh) */
+} spslam_assoc_params;
+
+typedef struct spslam_assoc_frame {
+    float Tcw[16];            /* Frame::mTcw, row-major float */
+    int32_t map_offset;       /* this frame's map: planes [map_offset, map_offset + n_map) */
+    int32_t n_map;
+    int32_t pad[2];
+} spslam_assoc_frame;         /* 80 bytes */
+
+/* Drop-in for one frame on host buffers.  coefs: n_planes x 4 floats; boundary_xyz:
+ * float x, y, z per boundary point.  match / parallel / vertical: n_planes ints;
+ * new_plane (may be NULL) receives mbNewPlane. */
+int spslam_planes_associate(spslam_ctx* ctx, const spslam_assoc_frame* frame, const float* coefs, int n_planes,
+                            const spslam_map_plane* map_planes, int n_map, const float* boundary_xyz,
+                            int n_boundary, const spslam_assoc_params* params, int32_t* match, int32_t* parallel,
+                            int32_t* vertical, int* new_plane);
+
+/* Batched, device resident.  Frame f's planes are the first d_count_a[f] records of
+ * source A (record r of frame f at d_planes_a + (f * cap_a + r) * stride_a bytes,
+ * coefficients = its first 4 floats; spslam_plane / spslam_supposed_plane layouts)
+ * followed by the first d_count_b[f] records of source B (may be NULL).  Outputs at
+ * f * (cap_a + cap_b) + i; d_new_plane: one int per frame (may be NULL).  max_map
+ * bounds every frame's n_map (host-known launch size). */
+int spslam_planes_associate_batch_device(spslam_ctx* ctx, int n_frames, const spslam_assoc_frame* d_frames,
+                                         const void* d_planes_a, int stride_a, const int* d_count_a, int cap_a,
+                                         const void* d_planes_b, int stride_b, const int* d_count_b, int cap_b,
+                                         const spslam_map_plane* d_map, const float* d_boundary_xyz, int max_map,
+                                         const spslam_assoc_params* params, int32_t* d_match, int32_t* d_parallel,
+                                         int32_t* d_vertical, int* d_new_plane, void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

@@ -1,0 +1,182 @@
+// Map::AssociatePlanesByBoundary on gfx950 (src/Map.cc:196-359): frame planes
+// against the map planes of the frame's map, for a batch of frames.
+// Semantics: oracle/assoc_oracle.cpp.
+//
+//   assoc_dist_kernel    grid (frame, map plane): the map plane's boundary cloud
+//                        is streamed once per 8 frame planes; every thread keeps
+//                        8 running minima of |pM . (p, 1)| (float, exact min, so
+//                        the order of the reduction does not matter), then wave
+//                        and workgroup minima -> dist[frame][plane][map plane]
+//                        (-1 where the angle test fails and the reference never
+//                        computes the distance);
+//   assoc_decide_kernel  grid (frame): one thread per frame plane walks the map
+//                        planes in id order with the reference's running
+//                        thresholds; mbNewPlane by a workgroup OR.
+// Float dot products use the reference build's FMA contraction pattern (GCC
+// -O3 -march=native): fma(a2, b2, fma(a0, b0, a1*b1)) (+ a3).
+#include <hip/hip_runtime.h>
+
+#include "assoc_launch.h"
+
+namespace spslam {
+namespace assoc {
+
+constexpr int kThreads = 256, kWaves = kThreads / 64, kGroup = 8;
+
+__device__ __forceinline__ float dot3(const float* a, const float* b) {
+    return __fmaf_rn(a[2], b[2], __fmaf_rn(a[0], b[0], __fmul_rn(a[1], b[1])));
+}
+
+// Frame::ComputePlaneWorldCoeff: transpose(Tcw) * coef, cv::Mat float gemm (double accumulation)
+__device__ __forceinline__ void world_coeff(const float* T, const float* c, float* pM) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) s = __dadd_rn(s, __dmul_rn((double)T[4 * k + j], (double)c[k]));
+        pM[j] = (float)s;
+    }
+}
+
+__device__ __forceinline__ const float* coef_of(const AssocSources& S, int f, int i, int na) {
+    return i < na ? (const float*)(S.a + ((size_t)f * S.cap_a + i) * S.stride_a)
+                  : (const float*)(S.b + ((size_t)f * S.cap_b + (i - na)) * S.stride_b);
+}
+
+__device__ __forceinline__ void plane_counts(const AssocSources& S, int f, int* na, int* nb) {
+    *na = min(S.count_a[f], S.cap_a);
+    *nb = S.count_b ? min(S.count_b[f], S.cap_b) : 0;
+}
+
+__global__ __launch_bounds__(kThreads) void assoc_dist_kernel(const spslam_assoc_frame* __restrict__ frames,
+                                                              AssocSources S, const spslam_map_plane* __restrict__ map,
+                                                              const float* __restrict__ boundary, int max_map,
+                                                              float angle_th, float* __restrict__ dist) {
+    __shared__ float pm_s[kGroup][4];
+    __shared__ int idx_s[kGroup];
+    __shared__ float red[kWaves][kGroup];
+    const int f = blockIdx.x, j = blockIdx.y, t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const spslam_assoc_frame& F = frames[f];
+    if (j >= F.n_map) return;
+    int na, nb;
+    plane_counts(S, f, &na, &nb);
+    const int n = na + nb, P = S.cap_a + S.cap_b;
+    const spslam_map_plane M = map[F.map_offset + j];
+    const float* pts = boundary + 3 * (size_t)M.boundary_offset;
+    float* D = dist + (size_t)f * P * max_map;
+    for (int i0 = 0; i0 < n; i0 += kGroup) {
+        // the frame planes of this group whose normal passes the angle test
+        if (t == 0) {
+            int g = 0;
+            for (int i = i0; i < min(i0 + kGroup, n); i++) {
+                float pM[4];
+                world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
+                const float angle = dot3(pM, M.world);
+                if (angle > angle_th || angle < -angle_th) {
+                    for (int k = 0; k < 4; k++) pm_s[g][k] = pM[k];
+                    idx_s[g++] = i;
+                } else {
+                    D[(size_t)i * max_map + j] = -1.f;
+                }
+            }
+            for (int k = g; k < kGroup; k++) idx_s[k] = -1;
+        }
+        __syncthreads();
+        float pm[kGroup][4], mn[kGroup];
+#pragma unroll
+        for (int g = 0; g < kGroup; g++) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) pm[g][k] = pm_s[g][k];
+            mn[g] = 100.f;  // PointDistanceFromPlane: res = 100
+        }
+        if (idx_s[0] >= 0) {
+            for (int p = t; p < M.n_boundary; p += kThreads) {
+                const float q[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
+#pragma unroll
+                for (int g = 0; g < kGroup; g++) mn[g] = fminf(mn[g], fabsf(__fadd_rn(dot3(pm[g], q), pm[g][3])));
+            }
+#pragma unroll
+            for (int g = 0; g < kGroup; g++) {
+                float v = mn[g];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+                if (lane == 0) red[w][g] = v;
+            }
+        }
+        __syncthreads();
+        if (t < kGroup && idx_s[t] >= 0) {
+            float v = red[0][t];
+            for (int k = 1; k < kWaves; k++) v = fminf(v, red[k][t]);
+            D[(size_t)idx_s[t] * max_map + j] = v;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(64) void assoc_decide_kernel(const spslam_assoc_frame* __restrict__ frames,
+                                                          AssocSources S, const spslam_map_plane* __restrict__ map,
+                                                          int max_map, spslam_assoc_params Pm,
+                                                          const float* __restrict__ dist, int32_t* __restrict__ match,
+                                                          int32_t* __restrict__ parallel,
+                                                          int32_t* __restrict__ vertical, int* __restrict__ new_plane) {
+    const int f = blockIdx.x;
+    const spslam_assoc_frame& F = frames[f];
+    int na, nb;
+    plane_counts(S, f, &na, &nb);
+    const int n = na + nb, P = S.cap_a + S.cap_b;
+    const float* D = dist + (size_t)f * P * max_map;
+    const spslam_map_plane* Mp = map + F.map_offset;
+    int unmatched = 0;
+    for (int i = threadIdx.x; i < n; i += 64) {
+        float pM[4];
+        world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
+        float ldTh = Pm.dis_th, lverTh = Pm.ver_th, lparTh = Pm.par_th;
+        int m = -1, par = -1, ver = -1;
+        for (int j = 0; j < F.n_map; j++) {
+            const float angle = dot3(pM, Mp[j].world);
+            if (angle > Pm.angle_th || angle < -Pm.angle_th) {
+                const float dis = D[(size_t)i * max_map + j];
+                if (dis < ldTh) {
+                    ldTh = dis;
+                    m = j;
+                    continue;
+                }
+            }
+            if (angle < lverTh && angle > -lverTh) {
+                lverTh = fabsf(angle);
+                ver = j;
+                continue;
+            }
+            if (angle > lparTh || angle < -lparTh) {
+                lparTh = fabsf(angle);
+                par = j;
+            }
+        }
+        const size_t o = (size_t)f * P + i;
+        match[o] = m < 0 ? -1 : F.map_offset + m;
+        parallel[o] = par < 0 ? -1 : F.map_offset + par;
+        vertical[o] = ver < 0 ? -1 : F.map_offset + ver;
+        unmatched |= m < 0;
+    }
+    const int any = __syncthreads_or(unmatched);
+    if (new_plane && threadIdx.x == 0) new_plane[f] = any;
+}
+
+}  // namespace assoc
+
+hipError_t assoc_launch(int n_frames, const spslam_assoc_frame* frames, const AssocSources& src,
+                        const spslam_map_plane* map, const float* boundary, int max_map,
+                        const spslam_assoc_params& P, float* dist, int32_t* match, int32_t* parallel,
+                        int32_t* vertical, int* new_plane, hipStream_t s, KernelTimer* timer) {
+    if (n_frames < 1 || max_map < 0 || src.cap_a < 0 || src.cap_b < 0) return hipErrorInvalidValue;
+    if (timer) timer->begin(kKindAssoc, s);
+    if (max_map > 0)
+        hipLaunchKernelGGL(assoc::assoc_dist_kernel, dim3(n_frames, max_map), dim3(assoc::kThreads), 0, s, frames,
+                           src, map, boundary, max_map, P.angle_th, dist);
+    hipLaunchKernelGGL(assoc::assoc_decide_kernel, dim3(n_frames), dim3(64), 0, s, frames, src, map, max_map, P,
+                       dist, match, parallel, vertical, new_plane);
+    if (timer) timer->end(kKindAssoc, s);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

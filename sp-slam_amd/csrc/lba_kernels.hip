@@ -592,21 +592,32 @@ __global__ __launch_bounds__(kThreads) void k_lm_sums(LbaBatch b, LbaWork w) {
     double mx = 0.0;
     if (l < c.L && lm_block_base(c, l) >= 0) {
         const int b0 = lm_block_base(c, l);
-        const int nb = __popcll(c.lm_mask[l]);
-        for (int j = 0; j < nb * 18; j++) c.blkH[(size_t)b0 * 18 + j] = 0.0;
+        // every block of l receives at least one edge: the first edge stores it, later ones (a landmark
+        // seen twice from one keyframe) accumulate, in insertion order
+        uint64_t written = 0;
         double H[9] = {}, bl[3] = {};
         for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
             if (c.e_level[e] != 0) continue;
             const double* o = c.con + (size_t)kLbaCon * e;
+            double r[30];
 #pragma unroll
-            for (int j = 0; j < 9; j++) H[j] += o[j];
-#pragma unroll
-            for (int j = 0; j < 3; j++) bl[j] += o[9 + j];
+            for (int j = 0; j < 30; j++) r[j] = o[j];
             const int bk = c.e_blk[e];
+#pragma unroll
+            for (int j = 0; j < 9; j++) H[j] += r[j];
+#pragma unroll
+            for (int j = 0; j < 3; j++) bl[j] += r[9 + j];
             if (bk >= 0) {
                 double* hb = c.blkH + (size_t)bk * 18;
+                const uint64_t bit = 1ull << (bk - b0);
+                if (written & bit) {
 #pragma unroll
-                for (int j = 0; j < 18; j++) hb[j] += o[12 + j];
+                    for (int j = 0; j < 18; j++) hb[j] += r[12 + j];
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 18; j++) hb[j] = r[12 + j];
+                }
+                written |= bit;
             }
         }
 #pragma unroll
@@ -633,6 +644,7 @@ __global__ __launch_bounds__(kThreads) void k_pose_sums(LbaBatch b, LbaWork w) {
     double acc[27];
 #pragma unroll
     for (int j = 0; j < 27; j++) acc[j] = 0.0;
+#pragma unroll 1
     for (int i = c.pe_off[k] + threadIdx.x; i < c.pe_off[k + 1]; i += kThreads) {
         const double* o = c.con + (size_t)kLbaCon * c.pe_idx[i] + 30;
 #pragma unroll
@@ -727,6 +739,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
         double acc[36];
 #pragma unroll
         for (int j = 0; j < 36; j++) acc[j] = 0.0;
+#pragma unroll 1
         for (int l = threadIdx.x; l < c.L; l += kThreads) {
             const uint64_t m = c.lm_mask[l];
             if ((m & need) != need) continue;

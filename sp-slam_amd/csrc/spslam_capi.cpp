@@ -22,6 +22,7 @@
 #include "supposed_launch.h"
 #include "frame_launch.h"
 #include "lba_launch.h"
+#include "assoc_launch.h"
 
 using namespace spslam;
 
@@ -126,6 +127,9 @@ struct spslam_ctx {
     size_t lba_stage_bytes = 0;
     int2* d_lba_work = nullptr;       // (problem, first index) work tables + the active counter
     size_t lba_work_cap = 0;
+    // plane association: per (frame, frame plane, map plane) boundary distances
+    float* d_assoc_dist = nullptr;
+    size_t assoc_dist_bytes = 0;
 };
 
 namespace {
@@ -248,7 +252,7 @@ void free_all(spslam_ctx* c) {
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
                     c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1,
-                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work};
+                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work, c->d_assoc_dist};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1034,6 +1038,82 @@ int spslam_lba_optimize(spslam_ctx* c, const spslam_lba_problem* problem, const 
         if (sz[6 + i]) HIP_CHECK(c, hipMemcpyAsync(dst[i], q + o[6 + i], sz[6 + i], hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return result->status == 0 ? SPSLAM_OK : fail(c, SPSLAM_ERR_ARG, "LBA problem rejected (status %s)", "< 0");
+}
+
+int spslam_planes_associate_batch_device(spslam_ctx* c, int n_frames, const spslam_assoc_frame* d_frames,
+                                         const void* d_planes_a, int stride_a, const int* d_count_a, int cap_a,
+                                         const void* d_planes_b, int stride_b, const int* d_count_b, int cap_b,
+                                         const spslam_map_plane* d_map, const float* d_boundary_xyz, int max_map,
+                                         const spslam_assoc_params* params, int32_t* d_match, int32_t* d_parallel,
+                                         int32_t* d_vertical, int* d_new_plane, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !d_frames || !params || !d_match || !d_parallel || !d_vertical || max_map < 0 ||
+        (cap_a > 0 && (!d_planes_a || !d_count_a || stride_a < 16)) || cap_a < 0 || cap_b < 0 ||
+        (cap_b > 0 && (!d_planes_b || !d_count_b || stride_b < 16)) || (max_map > 0 && (!d_map || !d_boundary_xyz)))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_associate_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    const size_t need = std::max<size_t>((size_t)n_frames * (cap_a + cap_b) * max_map * sizeof(float), 256);
+    if (need > c->assoc_dist_bytes) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_assoc_dist) (void)hipFree(c->d_assoc_dist);
+        c->d_assoc_dist = nullptr;
+        c->assoc_dist_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_assoc_dist, need));
+        c->assoc_dist_bytes = need;
+    }
+    AssocSources S{(const uint8_t*)d_planes_a, cap_b > 0 ? (const uint8_t*)d_planes_b : nullptr, stride_a,
+                   stride_b, d_count_a, cap_b > 0 ? d_count_b : nullptr, cap_a, cap_b};
+    HIP_CHECK(c, assoc_launch(n_frames, d_frames, S, d_map, d_boundary_xyz, max_map, *params, c->d_assoc_dist,
+                              d_match, d_parallel, d_vertical, d_new_plane, s, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_planes_associate(spslam_ctx* c, const spslam_assoc_frame* frame, const float* coefs, int n_planes,
+                            const spslam_map_plane* map_planes, int n_map, const float* boundary_xyz,
+                            int n_boundary, const spslam_assoc_params* params, int32_t* match, int32_t* parallel,
+                            int32_t* vertical, int* new_plane) {
+    if (!c || !frame || !params || n_planes < 0 || n_map < 0 || n_boundary < 0 ||
+        (n_planes && (!coefs || !match || !parallel || !vertical)) || (n_map && !map_planes) ||
+        (n_boundary && !boundary_xyz))
+        return SPSLAM_ERR_ARG;
+    for (int j = 0; j < n_map; j++)
+        if (map_planes[j].n_boundary < 0 || map_planes[j].boundary_offset < 0 ||
+            (long long)map_planes[j].boundary_offset + map_planes[j].n_boundary > n_boundary)
+            return fail(c, SPSLAM_ERR_ARG, "map plane boundary range outside the boundary array%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    spslam_assoc_frame F = *frame;
+    F.map_offset = 0;
+    F.n_map = n_map;
+    const int cap = std::max(n_planes, 1);
+    size_t sz[] = {sizeof F, (size_t)cap * 16, sizeof(int), (size_t)std::max(n_map, 1) * sizeof(spslam_map_plane),
+                   (size_t)std::max(n_boundary, 1) * 12, (size_t)cap * 4 * 3, sizeof(int)};
+    size_t o[7], bytes = 0;
+    for (int i = 0; i < 7; i++) { o[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    uint8_t* q = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&q, bytes, c->stream));
+    const void* src[] = {&F, coefs, &n_planes, map_planes, boundary_xyz};
+    const size_t len[] = {sizeof F, (size_t)n_planes * 16, sizeof(int), (size_t)n_map * sizeof(spslam_map_plane),
+                          (size_t)n_boundary * 12};
+    for (int i = 0; i < 5; i++)
+        if (len[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], len[i], hipMemcpyHostToDevice, c->stream));
+    auto* d_out = (int32_t*)(q + o[5]);
+    int rc = spslam_planes_associate_batch_device(
+        c, 1, (const spslam_assoc_frame*)(q + o[0]), q + o[1], 16, (const int*)(q + o[2]), cap, nullptr, 0, nullptr,
+        0, (const spslam_map_plane*)(q + o[3]), (const float*)(q + o[4]), n_map, params, d_out, d_out + cap,
+        d_out + 2 * cap, (int*)(q + o[6]), c->stream);
+    if (rc) { (void)hipFreeAsync(q, c->stream); return rc; }
+    int np = 0;
+    if (n_planes) {
+        HIP_CHECK(c, hipMemcpyAsync(match, d_out, (size_t)n_planes * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(parallel, d_out + cap, (size_t)n_planes * 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(vertical, d_out + 2 * cap, (size_t)n_planes * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_CHECK(c, hipMemcpyAsync(&np, q + o[6], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (new_plane) *new_plane = np;
+    return SPSLAM_OK;
 }
 
 int spslam_set_timing(spslam_ctx* c, int enable) {

@@ -35,6 +35,7 @@ class HotPath:
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
+        self.device = device
         s = width / 640.0
         self.fx, self.fy, self.cx, self.cy = K["fx"] * s, K["fy"] * s, K["cx"] * s, K["cy"] * s
         self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
@@ -192,15 +193,36 @@ class HotPath:
                         torch.zeros(npo, dtype=torch.uint8, device="cuda"),
                         torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
                         torch.zeros(self.n_lba * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
-        self.lba = L.LocalBA(self.ex)
+        # LocalMapping runs in its own thread on its own context (as the reference's LocalMapping thread):
+        # the batched LM drives its steps from the host, so tracking launches must not wait behind it
+        self.lba_ex = G.OrbExtractor(max_batch=1, device=self.device)
+        self.lba = L.LocalBA(self.lba_ex)
         self.lba_stream = torch.cuda.Stream()
         self.ev_lba = torch.cuda.Event()
+        import concurrent.futures as cf
+        self.lba_pool = cf.ThreadPoolExecutor(1, initializer=torch.cuda.set_device, initargs=(self.device,))
+        self.lba_job = None
         self.lba_edges = (npo + nplo) / self.n_lba
         self.lba_points = npt / self.n_lba
 
     def local_ba(self):
         self.lba.batch_device(self.n_lba, self.lba_hdr, *[x.data_ptr() for x in self.lba_in],
                               *[x.data_ptr() for x in self.lba_out], stream=self.lba_stream.cuda_stream)
+        self.ev_lba.record(self.lba_stream)
+
+    def set_timing(self, on):
+        self.ex.set_timing(on)
+        if self.n_lba:
+            self.lba_ex.set_timing(on)
+
+    def kernel_times(self):
+        """{kernel name: (total ms, launches)} over both contexts (tracking, LocalMapping)."""
+        t = dict(self.ex.kernel_times())
+        if self.n_lba:
+            for k, (ms, n) in self.lba_ex.kernel_times().items():
+                a = t.get(k, (0.0, 0))
+                t[k] = (a[0] + ms, a[1] + n)
+        return t
 
     def step(self):
         # planes of step k may start once step k-1 is done with the plane buffers
@@ -209,8 +231,7 @@ class HotPath:
         if self.n_lba:
             # LocalMapping: the keyframes of this step, beside tracking (joined at the end of the step)
             self.lba_stream.wait_event(self.ev_fork)
-            self.local_ba()
-            self.ev_lba.record(self.lba_stream)
+            self.lba_job = self.lba_pool.submit(self.local_ba)
         self.planes(self.side_stream)
         self.orb()
         self.ev_join.record(self.side)
@@ -218,6 +239,7 @@ class HotPath:
         self.frame()
         self.pose()
         if self.n_lba:
+            self.lba_job.result()
             self.main.wait_event(self.ev_lba)
 
     def results(self):
@@ -244,4 +266,7 @@ class HotPath:
         return np.array([sp[f, :cnt[f]]["n_line"].sum() for f in range(self.B)], np.float64)
 
     def close(self):
+        if self.n_lba:
+            self.lba_pool.shutdown()
+            self.lba_ex.close()
         self.ex.close()

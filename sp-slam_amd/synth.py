@@ -369,3 +369,64 @@ def lba_problem(scene: Scene, kf_frames, rng, n_fixed=2, n_points=1500, K=TUM3, 
     prob["n_kf"], prob["n_points"], prob["n_planes"] = n_kf, len(points), len(planes)
     prob["n_point_obs"], prob["n_plane_obs"] = len(point_obs), len(plane_obs)
     return prob, kfs, points, point_obs, planes, plane_obs, dict(Tcw=np.array(Tcw_gt))
+
+
+# ---------------------------------------------------------------- plane association
+def map_planes(scene: Scene, rng, boundary_step=0.02, boundary_noise=0.005, coef_noise_deg=0.5,
+               coef_noise_d=0.01, max_faces=None):
+    """Map planes (MapPlane world coefficients + mvBoundaryPoints) for the scene's
+    faces, in id order: the boundary cloud samples the face rectangle's border
+    every `boundary_step` metres with Gaussian noise.  Returns (records in the
+    spslam_map_plane layout as a dict of arrays, boundary xyz float32)."""
+    faces = scene.faces if max_faces is None else scene.faces[:max_faces]
+    world, offs, counts, pts = [], [], [], []
+    n = 0
+    for face in faces:
+        p = face_plane(face)
+        ax = rng.normal(size=3)
+        ax *= np.deg2rad(coef_noise_deg) * rng.uniform() / max(np.linalg.norm(ax), 1e-12)
+        nrm = _rot(ax) @ p[:3]
+        world.append([*nrm, p[3] + rng.normal() * coef_noise_d])
+        o = [a for a in range(3) if a != face.axis]
+        (u0, v0), (u1, v1) = face.lo, face.hi
+        nu, nv = max(int((u1 - u0) / boundary_step), 1), max(int((v1 - v0) / boundary_step), 1)
+        us, vs = np.linspace(u0, u1, nu + 1), np.linspace(v0, v1, nv + 1)
+        border = np.concatenate([np.stack([us, np.full_like(us, v0)], 1), np.stack([us, np.full_like(us, v1)], 1),
+                                 np.stack([np.full_like(vs, u0), vs], 1), np.stack([np.full_like(vs, u1), vs], 1)])
+        xyz = np.zeros((len(border), 3))
+        xyz[:, face.axis] = face.offset
+        xyz[:, o[0]], xyz[:, o[1]] = border[:, 0], border[:, 1]
+        xyz += rng.normal(size=xyz.shape) * boundary_noise
+        offs.append(n)
+        counts.append(len(xyz))
+        pts.append(xyz)
+        n += len(xyz)
+    return (dict(world=np.array(world, np.float32), boundary_offset=np.array(offs, np.int32),
+                 n_boundary=np.array(counts, np.int32), id=np.arange(1, len(faces) + 1, dtype=np.int32)),
+            np.concatenate(pts).astype(np.float32))
+
+
+def assoc_frame_planes(scene: Scene, frame: int, rng, n_faces=6, n_random=2, far_frac=0.25, noise_deg=1.0,
+                       noise_d=0.02):
+    """A frame's mvPlaneCoefficients for AssociatePlanesByBoundary: camera-frame
+    coefficients of `n_faces` scene faces (noisy; a fraction shifted 0.3-1 m so
+    they only qualify as parallel), plus random planes.  Returns (Tcw float32,
+    coefs float32 (n, 4) with d >= 0, source face index or -1)."""
+    Tcw = np.linalg.inv(scene.pose(frame))
+    idx = rng.choice(len(scene.faces), size=min(n_faces, len(scene.faces)), replace=False)
+    coefs, src = [], []
+    for f in idx:
+        p = face_plane(scene.faces[f]).copy()
+        if rng.uniform() < far_frac:
+            p[3] += rng.choice([-1, 1]) * rng.uniform(0.3, 1.0)
+        ax = rng.normal(size=3)
+        ax *= np.deg2rad(noise_deg) * rng.uniform() / max(np.linalg.norm(ax), 1e-12)
+        q = np.array([*(_rot(ax) @ p[:3]), p[3] + rng.normal() * noise_d])
+        coefs.append(transform_plane(Tcw, q))
+        src.append(int(f))
+    for _ in range(n_random):
+        n = rng.normal(size=3)
+        n /= np.linalg.norm(n)
+        coefs.append(np.array([*n, rng.uniform(0.2, 3.0)]))
+        src.append(-1)
+    return Tcw.astype(np.float32), np.array(coefs, np.float32).reshape(-1, 4), np.array(src, np.int32)

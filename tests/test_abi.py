@@ -59,12 +59,15 @@ int main(void) {
   S(spslam_supposed_plane) O(spslam_supposed_plane, line) O(spslam_supposed_plane, source_plane)
   O(spslam_supposed_plane, patch_offset)
   S(spslam_line_candidate) O(spslam_line_candidate, n_inliers) O(spslam_line_candidate, idx_offset)
+  S(spslam_map_plane) O(spslam_map_plane, id) O(spslam_map_plane, boundary_offset) O(spslam_map_plane, n_boundary)
+  S(spslam_assoc_frame) O(spslam_assoc_frame, map_offset) O(spslam_assoc_frame, n_map) S(spslam_assoc_params)
   return 0;
 }
 """
 
 
 def test_struct_layouts_match_bindings(tmp_path):
+    import spslam_assoc
     import spslam_gpu
     import spslam_planes
     src = tmp_path / "layout.c"
@@ -79,6 +82,7 @@ def test_struct_layouts_match_bindings(tmp_path):
         "spslam_plane_obs": spslam_gpu.PLANE_OBS_DTYPE, "spslam_pose_problem": spslam_gpu.POSE_PROBLEM_DTYPE,
         "spslam_pose_result": spslam_gpu.POSE_RESULT_DTYPE, "spslam_plane": spslam_planes.PLANE_DTYPE,
         "spslam_supposed_plane": spslam_planes.SUPPOSED_DTYPE, "spslam_line_candidate": spslam_planes.LINE_CAND_DTYPE,
+        "spslam_map_plane": spslam_assoc.MAP_PLANE_DTYPE, "spslam_assoc_frame": spslam_assoc.ASSOC_FRAME_DTYPE,
     }
     for name, dt in checks.items():
         assert got[name] == dt.itemsize, (name, got[name], dt.itemsize)
@@ -89,6 +93,7 @@ def test_struct_layouts_match_bindings(tmp_path):
     assert got["spslam_orb_params"] == ctypes.sizeof(spslam_gpu.OrbParams)
     assert got["spslam_plane_params"] == ctypes.sizeof(spslam_planes.PlaneParams)
     assert got["spslam_plane_config"] == 6 * 8
+    assert got["spslam_assoc_params"] == ctypes.sizeof(spslam_assoc.AssocParams)
     assert got["spslam_keypoint"] == 28  # cv::KeyPoint
 
 
