@@ -61,7 +61,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return out
 
 
-def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0):
+def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0, n_fpl=0, n_map=0, n_bnd=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -83,6 +83,9 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
         "supp_assemble_kernel": n_sup * (64 + 2601 * 12),     # appended planes + synthetic patches out
         "frame_rgbd_kernel": n_kp * (28 + 4 + 28 + 4 + 4 + 4) + 4 * 3073,  # kp in, depth gather, kp/depth/uR/idx out
+        # two AssociatePlanesByBoundary calls: frame + plane coefficients + map records + boundary cloud in,
+        # match / parallel / vertical out
+        "plane_assoc_kernel": 2 * (80 + n_fpl * (16 + 12) + n_map * 32 + n_bnd * 12),
         "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
 
@@ -110,6 +113,8 @@ def cpu_baseline(hp, budget_s=12.0):
     import oracle_planes
     import oracle_lba
     import oracle_supposed
+    import oracle_assoc
+    import oracle_frame
     orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     po = oracle_planes.PlaneOracle()
     n = 0
@@ -118,11 +123,16 @@ def cpu_baseline(hp, budget_s=12.0):
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         i = n % U
-        orb.extract(hp.frames[i][1], cap=20000)
+        ko, _ = orb.extract(hp.frames[i][1], cap=20000)
         r = po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
-        oracle_supposed.generate(depth_f[i], po.cloud(), r["coef"], r["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
+        so = oracle_supposed.generate(depth_f[i], po.cloud(), r["coef"], r["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
+        oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy, bf=40.0)
+        coefs = np.concatenate([np.asarray(r["coef"], np.float32).reshape(-1, 4),
+                                np.asarray(so["coef"], np.float32).reshape(-1, 4)])
         pa, pts, pls, _ = hp.probA[i]
+        oracle_assoc.associate(pa["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
         r1, _, _ = oracle_ctypes.pose_optimize(pa, pts, pls)
+        oracle_assoc.associate(r1["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
         pb, pts2, pls2, _ = hp.probB[i]
         pb = pb.copy()
         pb["Tcw"] = r1["Tcw"]
@@ -133,7 +143,7 @@ def cpu_baseline(hp, budget_s=12.0):
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + 2x PoseOptimization{' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + frame steps + 2x (plane association + PoseOptimization){' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -192,7 +202,9 @@ def main():
     lba_bytes = 0
     if hp.n_lba:  # per frame: the keyframe's local map in (records) and its results out
         lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
-    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes)
+    n_fpl = float(res["plane_counts"].mean()) + n_sup
+    alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes, n_fpl, hp.n_map,
+                            hp.n_boundary)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step

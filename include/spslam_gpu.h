@@ -17,6 +17,15 @@
  *                       src/ORBextractor.cc:410-470, 1043-1132)
  *   spslam_pose_*       Optimizer::PoseOptimization (include/Optimizer.h:47,
  *                       src/Optimizer.cc:519-1152) with g2oAddition plane edges
+ *   spslam_planes_extract*  Frame::ComputePlanesFromOrganizedPointCloud
+ *                       (include/Frame.h:120, src/Frame.cc:854-936)
+ *   spslam_planes_generate_from_boundaries*  Frame::GeneratePlanesFromBoundries
+ *                       (include/Frame.h:121, src/Frame.cc:938-1144)
+ *   spslam_frame_*      RGB-D Frame constructor keypoint steps (src/Frame.cc:146-181)
+ *   spslam_lba_*        Optimizer::LocalBundleAdjustment (include/Optimizer.h:46,
+ *                       src/Optimizer.cc:1154-1977)
+ *   spslam_planes_associate*  Map::AssociatePlanesByBoundary (include/Map.h:69-74,
+ *                       src/Map.cc:196-359)
  */
 #ifndef SPSLAM_GPU_H
 #define SPSLAM_GPU_H
@@ -91,7 +100,10 @@ int spslam_orb_extract(spslam_ctx* ctx, const uint8_t* gray, int w, int h, int s
  * (frame f at d_gray + f*frame_stride, rows `stride` bytes apart).  Writes,
  * per frame f, counts[f] keypoints to d_kps + f*cap_per_frame and
  * descriptors to d_desc + f*cap_per_frame*32.  Asynchronous on `hip_stream`
- * (a hipStream_t; NULL = the context's own stream). */
+ * (a hipStream_t).  In every *_batch_device call NULL means HIP's default
+ * (NULL) stream -- the one PyTorch calls its default stream -- so device
+ * buffers filled by the caller on that stream are ordered before the work;
+ * the host-buffer drop-ins run on the context's own stream. */
 int spslam_orb_extract_batch_device(spslam_ctx* ctx, const uint8_t* d_gray, int n_frames, size_t frame_stride,
                                     int stride, spslam_keypoint* d_kps, uint8_t* d_desc, int* d_counts,
                                     int cap_per_frame, void* hip_stream);
@@ -178,7 +190,7 @@ int spslam_pose_optimize(spslam_ctx* ctx, const spslam_pose_problem* problem, co
  * flag arrays share those offsets.  If d_init_from is non-NULL, problem p
  * starts from d_init_from[p].Tcw instead of its own Tcw (used to chain the
  * motion-model and local-map optimizations of one frame on the device).
- * Asynchronous on hip_stream (NULL = context stream). */
+ * Asynchronous on hip_stream (NULL = the default stream). */
 int spslam_pose_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_pose_problem* d_problems,
                                       const spslam_point_obs* d_points, const spslam_plane_obs* d_planes,
                                       const spslam_plane_config* cfg, const spslam_pose_result* d_init_from,

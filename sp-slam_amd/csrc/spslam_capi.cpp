@@ -385,7 +385,7 @@ int spslam_orb_extract_batch_device(spslam_ctx* c, const uint8_t* d_gray, int n_
         stride < c->p.width || (n_frames > 1 && frame_stride < (size_t)stride * c->p.height) || cap_per_frame < 1)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_orb_extract_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     bind_frames(c, d_gray, frame_stride, stride);
     HIP_CHECK(c, orb_launch(c->geom, c->b, n_frames, c->p.ini_th_fast, c->p.min_th_fast, d_kps, d_desc, d_counts,
                             cap_per_frame, s, c->timer));
@@ -432,7 +432,7 @@ int spslam_pose_optimize_batch_device(spslam_ctx* c, int n, const spslam_pose_pr
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_pose_optimize_batch_device");
     if (n == 0) return SPSLAM_OK;
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     const PoseConsts K = make_pose_consts(*cfg);
     if (c->timer) c->timer->begin(kKindPose, s);
     HIP_CHECK(c, pose_launch(n, d_problems, d_points, d_planes, K, d_init_from, d_results, d_point_outlier,
@@ -623,7 +623,7 @@ int spslam_planes_extract_batch_device(spslam_ctx* c, const float* d_depth, int 
         n_frames > c->p.max_batch || stride_floats < c->pg.w)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_extract_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     HIP_CHECK(c, plane_launch(c->pg, c->pb, n_frames, d_depth, (long long)frame_stride, stride_floats, d_planes,
                               d_counts, kMaxPlanesPerFrame, d_inliers, d_contours, s, c->timer));
     c->plane_last_frames = n_frames;
@@ -682,7 +682,7 @@ int spslam_planes_generate_from_boundaries_batch_device(spslam_ctx* c, const flo
     if (n_frames > c->plane_last_frames)
         return fail(c, SPSLAM_ERR_NOT_READY, "%s", "more frames than the last plane extraction holds");
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     HIP_CHECK(c, supp_launch(c->pg, c->pb, c->sp, c->sb, n_frames, d_depth, (long long)frame_stride, stride_floats,
                              d_planes, d_counts, d_contours, d_out, d_out_counts, d_line_idx, d_patch, s, c->timer));
     c->supp_last_frames = n_frames;
@@ -861,7 +861,7 @@ int spslam_frame_rgbd_batch_device(spslam_ctx* c, const spslam_keypoint* d_kps, 
         n_frames < 1 || cap_per_frame < 1 || cap_per_frame > 32767 || stride_floats < 1)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_frame_rgbd_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     HIP_CHECK(c, frame_launch(c->fg, n_frames, d_kps, d_counts, cap_per_frame, d_depth, (long long)frame_stride,
                               stride_floats, d_keys_un, d_mv_depth, d_mv_uright, d_grid_off, d_grid_idx,
                               d_plane_counts, d_supp_counts, s, c->timer));
@@ -942,7 +942,7 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
         for (int q = 0; q < npmax * (npmax + 1) / 2 + npmax; q++) pt.push_back(int2{i, q});
     }
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     if (total > c->lba_scratch_bytes) {
         HIP_CHECK(c, hipStreamSynchronize(s));
         if (c->d_lba_scratch) (void)hipFree(c->d_lba_scratch);
@@ -1052,7 +1052,7 @@ int spslam_planes_associate_batch_device(spslam_ctx* c, int n_frames, const spsl
         (cap_b > 0 && (!d_planes_b || !d_count_b || stride_b < 16)) || (max_map > 0 && (!d_map || !d_boundary_xyz)))
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_associate_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : c->stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     const size_t need = std::max<size_t>((size_t)n_frames * (cap_a + cap_b) * max_map * sizeof(float), 256);
     if (need > c->assoc_dist_bytes) {
         HIP_CHECK(c, hipStreamSynchronize(s));

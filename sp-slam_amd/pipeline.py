@@ -77,7 +77,9 @@ class HotPath:
         self.d_patch = torch.zeros(B * pe.supp_cap * pe.patch_points * 3, dtype=torch.float32, device=dev)
         # --- streams: ORB on the main stream, plane extraction beside it (independent inputs);
         #     PoseOptimization joins both
-        self.main = torch.cuda.current_stream()
+        # (an explicit stream: torch's default is the legacy NULL stream, which a HIP call given
+        # stream 0 would replace by the context's own non-blocking stream, outside these events)
+        self.main = torch.cuda.Stream()
         self.side = torch.cuda.Stream()
         self.stream = self.main.cuda_stream
         self.side_stream = self.side.cuda_stream
@@ -104,12 +106,54 @@ class HotPath:
         self.d_res1 = torch.zeros(B * G.POSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
         self.d_res2 = torch.zeros_like(self.d_res1)
         self.mean_keypoints = float(cnts.mean())
+        self._setup_assoc(seq_id)
         # --- LocalBundleAdjustment (C3): one local map per `lba_every` frames (a keyframe), run on the
         #     LocalMapping stream beside tracking like the reference's LocalMapping thread
         self.n_lba = B // lba_every if lba_every else 0
         self.lba_every = lba_every
         if self.n_lba:
             self._setup_lba(seq_id, lba_unique, lba_points)
+        torch.cuda.synchronize()  # buffers were filled on the default stream
+
+    def _setup_assoc(self, seq_id):
+        """Map::AssociatePlanesByBoundary before each PoseOptimization (TrackWithMotionModel,
+        TrackLocalMap): the frame's extracted + supposed planes against the sequence's map planes
+        (the scene faces with boundary clouds).  The first call uses the motion-model pose, the
+        second the pose after the first optimisation (copied on the device)."""
+        import spslam_assoc as SA
+        torch, B = self.torch, self.B
+        rng = np.random.default_rng(seq_id * 31 + 7)
+        mp, bxyz = synth.map_planes(self.scene, rng)
+        m = np.zeros(len(mp["world"]), SA.MAP_PLANE_DTYPE)
+        for k, v in mp.items():
+            m[k] = v
+        fr = np.zeros(B, SA.ASSOC_FRAME_DTYPE)
+        for i in range(B):
+            fr[i]["Tcw"] = self.probA[i][0]["Tcw"]
+        fr["map_offset"], fr["n_map"] = 0, len(m)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
+        self.assoc = SA.PlaneAssociator(self.ex)
+        self.d_map, self.d_bound = dev(m), dev(bxyz)
+        self.d_afr1, self.d_afr2 = dev(fr), dev(fr)
+        self.n_map, self.n_boundary = len(m), len(bxyz)
+        self.assoc_map, self.assoc_boundary = m, bxyz  # host copies (CPU baseline)
+        P = self.pe.planes_cap + self.pe.supp_cap
+        self.d_assoc = torch.zeros((2, 3, B * P), dtype=torch.int32, device="cuda")
+        self.d_newp = torch.zeros((2, B), dtype=torch.int32, device="cuda")
+
+    def associate(self, k):
+        import spslam_planes as SP
+        d_fr = self.d_afr1 if k == 0 else self.d_afr2
+        if k == 1:  # the second association sees the pose after the first PoseOptimization
+            f32 = self.torch.float32
+            with self.torch.cuda.stream(self.main):
+                d_fr.view(f32).view(self.B, 20)[:, :16].copy_(self.d_res1.view(f32).view(self.B, 20)[:, :16])
+        o = self.d_assoc[k]
+        self.assoc.batch_device(self.B, d_fr.data_ptr(), self.d_planes.data_ptr(), SP.PLANE_DTYPE.itemsize,
+                                self.d_pcnt.data_ptr(), self.pe.planes_cap, self.d_supp.data_ptr(),
+                                SP.SUPPOSED_DTYPE.itemsize, self.d_scnt.data_ptr(), self.pe.supp_cap,
+                                self.d_map.data_ptr(), self.d_bound.data_ptr(), self.n_map, o[0].data_ptr(),
+                                o[1].data_ptr(), o[2].data_ptr(), self.d_newp[k].data_ptr(), stream=self.stream)
 
     def _upload(self, probs):
         torch = self.torch
@@ -154,9 +198,11 @@ class HotPath:
 
     def pose(self):
         A, Bp = self.dA, self.dB
+        self.associate(0)
         G.pose_optimize_batch_device(self.ex, self.B, A["P"].data_ptr(), A["pts"].data_ptr(), A["pls"].data_ptr(),
                                      self.d_res1.data_ptr(), A["pout"].data_ptr(), A["plout"].data_ptr(),
                                      stream=self.stream)
+        self.associate(1)
         G.pose_optimize_batch_device(self.ex, self.B, Bp["P"].data_ptr(), Bp["pts"].data_ptr(), Bp["pls"].data_ptr(),
                                      self.d_res2.data_ptr(), Bp["pout"].data_ptr(), Bp["plout"].data_ptr(),
                                      init_from_ptr=self.d_res1.data_ptr(), stream=self.stream)
@@ -253,7 +299,9 @@ class HotPath:
             contour_points=self._plane_field("n_contour"),
             line_points=self._supposed_line_points(),
             pose1=self.d_res1.cpu().numpy().view(G.POSE_RESULT_DTYPE),
-            pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE))
+            pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE),
+            assoc=self.d_assoc.cpu().numpy().reshape(2, 3, self.B, -1),
+            new_plane=self.d_newp.cpu().numpy())
 
     def _plane_field(self, name):
         pl = self.d_planes.cpu().numpy().view(spslam_planes.PLANE_DTYPE).reshape(self.B, self.pe.planes_cap)

@@ -1,0 +1,102 @@
+"""GPU parity of the benchmarked step itself (sp-slam_amd/pipeline.py HotPath,
+the path bench.py times): one step over a small batch, every stage's output
+checked against the CPU oracle on the same inputs --
+ORBextractor::operator() (bit-exact keypoints + descriptors), the RGB-D Frame
+steps (bit-exact), ComputePlanesFromOrganizedPointCloud + GeneratePlanesFromBoundries
+(bit-exact coefficients), AssociatePlanesByBoundary before each PoseOptimization
+(identical indices; the second call with the first optimisation's pose), and
+the two PoseOptimization calls (pose within 1e-4, identical outlier flags)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def run():
+    import pipeline
+    hp = pipeline.HotPath(6, unique_frames=6, n_boxes=3)
+    hp.step()
+    res = hp.results()
+    yield hp, res
+    hp.close()
+
+
+def test_orb_and_frame_stage(run):
+    import oracle_ctypes
+    import oracle_frame
+    hp, res = run
+    orb = oracle_ctypes.OrbOracle()
+    kun = hp.d_kun.cpu().numpy().reshape(hp.B, hp.kp_cap, 7)
+    kdep = hp.d_kdepth.cpu().numpy()
+    for i in range(hp.B):
+        g = hp.d_gray[i].cpu().numpy()
+        ko, do = orb.extract(g)
+        n = int(res["kp_counts"][i])
+        kg = res["kps"][i, :n]
+        assert n == len(ko), (i, n, len(ko))
+        for f in ("x", "y", "size", "angle", "response", "octave"):
+            assert np.array_equal(kg[f], ko[f]), (i, f)
+        assert np.array_equal(hp.d_desc[i, :n].cpu().numpy(), do), i
+        fo = oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), hp.d_depth[i].cpu().numpy(), hp.fx, hp.fy,
+                                     hp.cx, hp.cy, bf=40.0)
+        assert np.array_equal(kun[i, :n, :2], fo["un"]), i
+        assert np.array_equal(kdep[i, :n], fo["depth"]), i
+
+
+def _frame_planes(hp, res, i):
+    import spslam_planes as SP
+    pl = hp.d_planes.cpu().numpy().view(SP.PLANE_DTYPE).reshape(hp.B, hp.pe.planes_cap)
+    sp = hp.d_supp.cpu().numpy().view(SP.SUPPOSED_DTYPE).reshape(hp.B, hp.pe.supp_cap)
+    na, nb = int(res["plane_counts"][i]), min(int(res["supposed_counts"][i]), hp.pe.supp_cap)
+    return pl[i, :na]["coef"], sp[i, :nb]["coef"]
+
+
+def test_planes_stage(run):
+    import oracle_planes
+    import oracle_supposed
+    hp, res = run
+    po = oracle_planes.PlaneOracle()
+    for i in range(hp.B):
+        depth = hp.d_depth[i].cpu().numpy()
+        ro = po.extract(depth, hp.fx, hp.fy, hp.cx, hp.cy)
+        ca, cb = _frame_planes(hp, res, i)
+        assert np.array_equal(ca, ro["coef"]), i
+        so = oracle_supposed.generate(depth, po.cloud(), ro["coef"], ro["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
+        want = np.asarray(so["coef"], np.float32).reshape(-1, 4)[:hp.pe.supp_cap]
+        assert int(res["supposed_counts"][i]) == len(so["coef"]), i
+        assert np.array_equal(cb, want), i
+
+
+def test_association_and_pose(run):
+    import oracle_assoc as OA
+    import oracle_ctypes
+    import spslam_assoc as SA
+    from test_gpu_pose import pose_close
+    hp, res = run
+    m = hp.d_map.cpu().numpy().view(SA.MAP_PLANE_DTYPE)
+    b = hp.d_bound.cpu().numpy().view(np.float32).reshape(-1, 3)
+    P = hp.pe.planes_cap + hp.pe.supp_cap
+    assoc = res["assoc"]
+    n_matched = 0
+    for i in range(hp.B):
+        ca, cb = _frame_planes(hp, res, i)
+        coefs = np.concatenate([ca, cb])
+        probA, ptsA, plsA, _ = hp.probA[i]
+        r1, po1, plo1 = oracle_ctypes.pose_optimize(probA, ptsA, plsA)
+        g1 = res["pose1"][i]
+        ok, err = pose_close(g1["Tcw"], r1["Tcw"])
+        assert ok, (i, err)
+        for k, T in enumerate((probA["Tcw"], g1["Tcw"])):
+            o = OA.associate(T.reshape(4, 4), coefs, m, b)
+            for q, key in enumerate(("match", "parallel", "vertical")):
+                assert np.array_equal(assoc[k, q, i, :len(coefs)], o[key]), (i, k, key)
+            assert bool(res["new_plane"][k, i]) == o["new_plane"], (i, k)
+            n_matched += int((o["match"] >= 0).sum())
+        probB, ptsB, plsB, _ = hp.probB[i]
+        p2 = probB.copy()
+        p2["Tcw"] = g1["Tcw"]
+        r2, _, _ = oracle_ctypes.pose_optimize(p2, ptsB, plsB)
+        ok, err = pose_close(res["pose2"][i]["Tcw"], r2["Tcw"])
+        assert ok, (i, err)
+    assert n_matched > 0
