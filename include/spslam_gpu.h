@@ -527,6 +527,66 @@ int spslam_planes_associate_batch_device(spslam_ctx* ctx, int n_frames, const sp
                                          const spslam_assoc_params* params, int32_t* d_match, int32_t* d_parallel,
                                          int32_t* d_vertical, int* d_new_plane, void* hip_stream);
 
+/* ---------------------------------------------------------------- projection matching
+ * ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame,
+ * th, bMono) (src/ORBmatcher.cc:1328-1470) with Frame::GetFeaturesInArea
+ * (src/Frame.cc:427-480), DescriptorDistance (src/ORBmatcher.cc:1647-1662) and
+ * the rotation-consistency check (ComputeThreeMaxima, :1601-1642), as
+ * Tracking::TrackWithMotionModel calls it (src/Tracking.cc:951-975: matcher
+ * (0.9, checkOri = true), mvpMapPoints cleared, and when fewer than 20 matches
+ * a second search at 2*th).  The last frame is given as its map points: one
+ * spslam_proj_point per keypoint i with mvpMapPoints[i] && !mvbOutlier[i], in
+ * increasing i.  The current frame is the frame stage's output (mvKeysUn,
+ * mvuRight, mGrid) with the ORB descriptors; camera and grid geometry come
+ * from spslam_frame_configure, the scale factors from the ORB tables.
+ * Output per current keypoint: the index (into the frame's point list) of the
+ * map point assigned to it (mvpMapPoints), -1 if none; and nmatches. */
+typedef struct spslam_proj_point {
+    float xw[3];          /* MapPoint::GetWorldPos */
+    float angle;          /* LastFrame.mvKeysUn[i].angle */
+    int32_t octave;       /* LastFrame.mvKeys[i].octave */
+    int32_t n_obs;        /* MapPoint::Observations(): 0 (a visual-odometry point) does not block a keypoint */
+    int32_t last_index;   /* i (informative) */
+    int32_t pad;
+    uint8_t desc[32];     /* MapPoint::GetDescriptor */
+} spslam_proj_point;      /* 64 bytes */
+
+typedef struct spslam_proj_frame {
+    float Tcw[16];        /* CurrentFrame.mTcw (motion-model prediction), row-major */
+    float Tlw[16];        /* LastFrame.mTcw */
+    int32_t point_offset; /* this frame's last-frame map points: [point_offset, point_offset + n_points) */
+    int32_t n_points;
+    int32_t pad[2];
+} spslam_proj_frame;      /* 144 bytes */
+
+typedef struct spslam_match_params {
+    float th;                   /* window radius at level 0 (15 for RGB-D, Tracking.cc:963-967) */
+    int32_t mono;               /* bMono */
+    int32_t check_orientation;  /* ORBmatcher mbCheckOrientation */
+    int32_t retry_below;        /* nmatches < retry_below -> clear and search at 2*th (20; 0 = no retry) */
+} spslam_match_params;
+
+/* Drop-in for one frame pair on host buffers.  keys_un / desc / uright: the
+ * current frame's n_kp keypoints; grid_off (64*48+1) / grid_idx: its mGrid CSR.
+ * match: n_kp ints.  *nmatches receives the return value of the (last) search. */
+int spslam_search_by_projection(spslam_ctx* ctx, const spslam_proj_frame* frame, const spslam_proj_point* points,
+                                const spslam_keypoint* keys_un, const uint8_t* desc, const float* uright, int n_kp,
+                                const int32_t* grid_off, const int32_t* grid_idx, const spslam_match_params* params,
+                                int32_t* match, int* nmatches);
+
+/* Batched, device resident.  Frame f: d_frames[f]; its current frame at
+ * d_keys_un / d_uright / d_match + f*cap, d_desc + f*cap*32, d_grid_off +
+ * f*(64*48+1), d_grid_idx + f*cap, d_counts[f] keypoints (the ORB / frame-stage
+ * batch layouts).  max_points bounds every frame's n_points (host-known launch
+ * size).  d_nmatches: one int per frame. */
+int spslam_search_by_projection_batch_device(spslam_ctx* ctx, int n_frames, const spslam_proj_frame* d_frames,
+                                             const spslam_proj_point* d_points, int max_points,
+                                             const spslam_keypoint* d_keys_un, const uint8_t* d_desc,
+                                             const float* d_uright, const int32_t* d_grid_off,
+                                             const int32_t* d_grid_idx, const int* d_counts, int cap,
+                                             const spslam_match_params* params, int32_t* d_match, int* d_nmatches,
+                                             void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

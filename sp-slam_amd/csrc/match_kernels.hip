@@ -1,0 +1,281 @@
+// ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) on gfx950
+// (src/ORBmatcher.cc:1328-1470, Frame::GetFeaturesInArea src/Frame.cc:427-480,
+// DescriptorDistance :1647-1662, ComputeThreeMaxima :1601-1642) for a batch of
+// frame pairs, with TrackWithMotionModel's second search at 2*th when fewer
+// than retry_below matches (src/Tracking.cc:968-975).  Semantics:
+// oracle/match_oracle.cpp.
+//
+//   match_window_kernel  grid (frame, 256 last-frame points): projection, the
+//                        search window and every candidate's Hamming distance
+//                        (v_bcnt over the XOR of 8 dwords); keeps the best as
+//                        (distance << 20 | CSR position), which orders ties
+//                        like the reference's cell-by-cell scan;
+//   match_assign_kernel  grid (frame), one wave: the reference's loop is
+//                        sequential only through `mvpMapPoints[i2] taken`, so
+//                        the wave walks the points in order, accepts each
+//                        point's precomputed best unless an earlier point took
+//                        that keypoint, and only then re-scans the window
+//                        cooperatively (64 lanes, min over keys) excluding the
+//                        taken keypoints (LDS bitmap); then the rotation
+//                        histogram check.
+// Float expressions follow the reference build's contraction pattern; the
+// cv::Mat products are accumulated in double and rounded once (oracle header).
+#include <hip/hip_runtime.h>
+
+#include "match_launch.h"
+
+namespace spslam {
+namespace match {
+
+constexpr int kThreads = 256, kCols = SPSLAM_GRID_COLS, kRows = SPSLAM_GRID_ROWS, kHisto = 30, kThHigh = 100;
+constexpr uint32_t kNone = 0xffffffffu;
+
+__device__ __forceinline__ void mat3_mul(const float* T, const float* x, const float* c, bool transpose, double sign,
+                                         float* y) {
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+            s = __dadd_rn(s, __dmul_rn((double)(transpose ? T[4 * k + r] : T[4 * r + k]), (double)x[k]));
+        s = __dmul_rn(s, sign);
+        if (c) s = __dadd_rn(s, (double)c[r]);
+        y[r] = (float)s;
+    }
+}
+
+__device__ __forceinline__ int hamming(const uint4& a0, const uint4& a1, const uint8_t* b) {
+    const uint4 b0 = *(const uint4*)b, b1 = *(const uint4*)(b + 16);
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// bForward / bBackward of one frame pair (src/ORBmatcher.cc:1336-1349)
+__device__ __forceinline__ void direction(const spslam_proj_frame& F, const MatchGeom& g, bool mono, bool* fwd,
+                                          bool* bwd) {
+    const float tcw[3] = {F.Tcw[3], F.Tcw[7], F.Tcw[11]};
+    const float tlw[3] = {F.Tlw[3], F.Tlw[7], F.Tlw[11]};
+    float twc[3], tlc[3];
+    mat3_mul(F.Tcw, tcw, nullptr, true, -1.0, twc);
+    mat3_mul(F.Tlw, twc, tlw, false, 1.0, tlc);
+    const float mb = __fdiv_rn(g.bf, g.fx);
+    *fwd = tlc[2] > mb && !mono;
+    *bwd = -tlc[2] > mb && !mono;
+}
+
+// Candidate test of GetFeaturesInArea + the stereo check; returns the key or kNone.
+__device__ __forceinline__ uint32_t candidate_key(const MatchWindow& w, const MatchCurrent& C, const float* uright,
+                                                  const uint8_t* desc, const spslam_keypoint* kun, int j, int k,
+                                                  const uint4& d0, const uint4& d1, const MatchGeom& g) {
+    const spslam_keypoint kp = kun[k];
+    const bool check = (w.min_level > 0) || (w.max_level >= 0);
+    if (check) {
+        if (kp.octave < w.min_level) return kNone;
+        if (w.max_level >= 0 && kp.octave > w.max_level) return kNone;
+    }
+    const float dx = __fsub_rn(kp.x, w.u), dy = __fsub_rn(kp.y, w.v);
+    if (!(fabsf(dx) < w.r && fabsf(dy) < w.r)) return kNone;
+    const float urk = uright[k];
+    if (urk > 0) {
+        const float ur = __fmaf_rn(-g.bf, w.invzc, w.u);
+        const float er = fabsf(__fsub_rn(ur, urk));
+        if (er > w.r) return kNone;
+    }
+    return ((uint32_t)hamming(d0, d1, desc + 32 * (size_t)k) << 20) | (uint32_t)j;
+}
+
+__global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_proj_frame* __restrict__ frames,
+                                                                const spslam_proj_point* __restrict__ points,
+                                                                int max_points, MatchCurrent C, MatchGeom g, float th,
+                                                                int mono, int retry_below, int pass,
+                                                                const int* __restrict__ nmatches,
+                                                                MatchWindow* __restrict__ win) {
+    const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
+    const spslam_proj_frame& F = frames[f];
+    if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
+    if (i >= F.n_points || i >= max_points) return;
+    MatchWindow w{};
+    w.best = kNone;
+    w.valid = 0;
+    w.x0 = 1;
+    w.x1 = 0;
+    const spslam_proj_point p = points[F.point_offset + i];
+    bool fwd, bwd;
+    direction(F, g, mono != 0, &fwd, &bwd);
+    const float tcw[3] = {F.Tcw[3], F.Tcw[7], F.Tcw[11]};
+    float x3Dc[3];
+    mat3_mul(F.Tcw, p.xw, tcw, false, 1.0, x3Dc);
+    const float invzc = (float)__ddiv_rn(1.0, (double)x3Dc[2]);
+    MatchWindow* W = win + (size_t)f * max_points + i;
+    if (invzc < 0) { *W = w; return; }
+    const float u = __fmaf_rn(__fmul_rn(g.fx, x3Dc[0]), invzc, g.cx);
+    const float v = __fmaf_rn(__fmul_rn(g.fy, x3Dc[1]), invzc, g.cy);
+    if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) { *W = w; return; }
+    const int oct = p.octave;
+    const float th_eff = pass == 1 ? __fmul_rn(2.0f, th) : th;
+    const float r = __fmul_rn(th_eff, g.scale[oct]);
+    w.u = u; w.v = v; w.r = r; w.invzc = invzc;
+    if (fwd) { w.min_level = oct; w.max_level = -1; }
+    else if (bwd) { w.min_level = 0; w.max_level = oct; }
+    else { w.min_level = oct - 1; w.max_level = oct + 1; }
+    w.valid = 1;
+    // GetFeaturesInArea cell range
+    const int x0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(u, g.min_x), r), g.ginv_x)));
+    const int x1 = min(kCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(u, g.min_x), r), g.ginv_x)));
+    const int y0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(v, g.min_y), r), g.ginv_y)));
+    const int y1 = min(kRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(v, g.min_y), r), g.ginv_y)));
+    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { *W = w; return; }
+    w.x0 = (int16_t)x0; w.x1 = (int16_t)x1; w.y0 = (int16_t)y0; w.y1 = (int16_t)y1;
+    const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
+    const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
+    const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
+    const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
+    const float* uright = C.uright + (size_t)f * C.cap;
+    const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
+    uint32_t best = kNone;
+    for (int ix = x0; ix <= x1; ix++)
+        for (int iy = y0; iy <= y1; iy++) {
+            const int c = ix * kRows + iy;
+            for (int j = GO[c]; j < GO[c + 1]; j++) best = min(best, candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g));
+        }
+    w.best = best;
+    *W = w;
+}
+
+// ComputeThreeMaxima
+__device__ void three_maxima(const int* h, int* i1, int* i2, int* i3) {
+    int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+    for (int i = 0; i < kHisto; i++) {
+        const int s = h[i];
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < __fmul_rn(0.1f, (float)max1)) { ind2 = -1; ind3 = -1; }
+    else if (max3 < __fmul_rn(0.1f, (float)max1)) ind3 = -1;
+    *i1 = ind1; *i2 = ind2; *i3 = ind3;
+}
+
+__global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_frame* __restrict__ frames,
+                                                          const spslam_proj_point* __restrict__ points, int max_points,
+                                                          MatchCurrent C, MatchGeom g, int check_ori, int retry_below,
+                                                          int pass, const MatchWindow* __restrict__ win,
+                                                          int2* __restrict__ pushes, int32_t* __restrict__ match,
+                                                          int* __restrict__ nmatches) {
+    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
+    __shared__ int hist[kHisto];
+    __shared__ int ind[3];
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const spslam_proj_frame& F = frames[f];
+    if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
+    const int n_kp = min(C.counts[f], C.cap), np = min(F.n_points, max_points);
+    int32_t* M = match + (size_t)f * C.cap;
+    const int words = (C.cap + 31) / 32;
+    for (int k = lane; k < n_kp; k += 64) M[k] = -1;  // fill(mvpMapPoints, NULL)
+    for (int k = lane; k < words; k += 64) taken[k] = 0;
+    if (lane < kHisto) hist[lane] = 0;
+    __syncthreads();
+    const MatchWindow* Wf = win + (size_t)f * max_points;
+    const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
+    const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
+    const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
+    const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
+    const float* uright = C.uright + (size_t)f * C.cap;
+    int2* PU = pushes + (size_t)f * max_points;
+    const float factor = __fdiv_rn(1.0f, (float)kHisto);
+    int n_push = 0;
+    for (int i = 0; i < np; i++) {
+        const MatchWindow w = Wf[i];  // uniform (every lane reads the same entry)
+        if (!w.valid) continue;
+        uint32_t best = w.best;
+        if (best != kNone) {
+            const int b = GI[best & 0xfffff];
+            if ((taken[b >> 5] >> (b & 31)) & 1) {
+                // an earlier point holds this keypoint: search the window again without the taken ones
+                const spslam_proj_point& p = points[F.point_offset + i];
+                const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
+                uint32_t m = kNone;
+                for (int ix = w.x0; ix <= w.x1; ix++)
+                    for (int iy = w.y0; iy <= w.y1; iy++) {
+                        const int c = ix * kRows + iy;
+                        for (int j = GO[c] + lane; j < GO[c + 1]; j += 64) {
+                            const int k = GI[j];
+                            if ((taken[k >> 5] >> (k & 31)) & 1) continue;
+                            m = min(m, candidate_key(w, C, uright, desc, kun, j, k, d0, d1, g));
+                        }
+                    }
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
+                best = m;
+            }
+        }
+        if (best == kNone || (int)(best >> 20) > kThHigh) continue;
+        const int b = GI[best & 0xfffff];
+        const spslam_proj_point& p = points[F.point_offset + i];
+        if (lane == 0) {
+            M[b] = i;
+            if (p.n_obs > 0) taken[b >> 5] |= 1u << (b & 31);
+            int bin = 0;
+            if (check_ori) {
+                float rot = __fsub_rn(p.angle, kun[b].angle);
+                if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                bin = (int)roundf(__fmul_rn(rot, factor));
+                if (bin == kHisto) bin = 0;
+                hist[bin]++;
+            }
+            PU[n_push] = make_int2(b, bin);
+        }
+        n_push++;
+        __syncthreads();
+    }
+    int n = n_push;
+    if (check_ori) {
+        __syncthreads();
+        if (lane == 0) three_maxima(hist, &ind[0], &ind[1], &ind[2]);
+        __syncthreads();
+        const int i1 = ind[0], i2 = ind[1], i3 = ind[2];
+        int removed = 0;
+        for (int q = lane; q < n_push; q += 64) {
+            const int2 e = PU[q];
+            if (e.y != i1 && e.y != i2 && e.y != i3) {
+                M[e.x] = -1;
+                removed++;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) removed += __shfl_xor(removed, o);
+        n -= removed;
+    }
+    if (lane == 0) nmatches[f] = n;
+}
+
+}  // namespace match
+
+hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const spslam_proj_point* points,
+                        int max_points, const MatchCurrent& cur, const MatchGeom& g, const spslam_match_params& P,
+                        MatchWindow* win, int2* pushes, int32_t* match, int* nmatches, hipStream_t s,
+                        KernelTimer* timer) {
+    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
+    if (timer) timer->begin(kKindMatch, s);
+    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4;
+    const int passes = P.retry_below > 0 ? 2 : 1;
+    for (int pass = 0; pass < passes; pass++) {
+        if (max_points > 0)
+            hipLaunchKernelGGL(match::match_window_kernel, dim3(n_frames, (max_points + match::kThreads - 1) / match::kThreads),
+                               dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P.th, P.mono,
+                               P.retry_below, pass, nmatches, win);
+        hipLaunchKernelGGL(match::match_assign_kernel, dim3(n_frames), dim3(64), lds, s, frames, points, max_points, cur,
+                           g, P.check_orientation, P.retry_below, pass, win, pushes, match, nmatches);
+    }
+    if (timer) timer->end(kKindMatch, s);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

@@ -1,0 +1,40 @@
+// Host-side entry points of match_kernels.hip (ORBmatcher::SearchByProjection).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../include/spslam_gpu.h"
+#include "orb_launch.h"
+
+namespace spslam {
+
+struct MatchGeom {
+    float fx, fy, cx, cy, bf;          // mK, mbf
+    float min_x, max_x, min_y, max_y;  // ComputeImageBounds
+    float ginv_x, ginv_y;              // mfGridElementWidthInv / HeightInv
+    float scale[8];                    // mvScaleFactors
+};
+
+struct MatchCurrent {
+    const spslam_keypoint* kun;
+    const uint8_t* desc;
+    const float* uright;
+    const int32_t* grid_off;
+    const int32_t* grid_idx;
+    const int* counts;
+    int cap;
+};
+
+// Per-point search state between the two kernels (scratch, n_frames * max_points entries).
+struct MatchWindow {
+    float u, v, r, invzc;
+    int16_t x0, x1, y0, y1;  // GetFeaturesInArea cell range (x0 > x1: empty)
+    int8_t min_level, max_level, valid, pad;
+    uint32_t best;           // (distance << 20) | CSR position of the best candidate; ~0u: none
+};
+
+hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const spslam_proj_point* points,
+                        int max_points, const MatchCurrent& cur, const MatchGeom& g, const spslam_match_params& P,
+                        MatchWindow* win, int2* pushes, int32_t* match, int* nmatches, hipStream_t s,
+                        KernelTimer* timer);
+
+}  // namespace spslam

@@ -430,3 +430,48 @@ def assoc_frame_planes(scene: Scene, frame: int, rng, n_faces=6, n_random=2, far
         coefs.append(np.array([*n, rng.uniform(0.2, 3.0)]))
         src.append(-1)
     return Tcw.astype(np.float32), np.array(coefs, np.float32).reshape(-1, 4), np.array(src, np.int32)
+
+
+# ---------------------------------------------------------------- projection matching
+def proj_problem(scene: Scene, last_fi: int, cur_fi: int, last_kps, last_desc, last_depth_u16, rng, K=TUM3,
+                 map_frac=0.8, flip_bits=6, zero_obs_frac=0.05, rot_noise_deg=0.3, trans_noise=0.01):
+    """TrackWithMotionModel inputs: the last frame's map points (its keypoints with
+    depth, back-projected with the true pose, descriptors with a few flipped bits,
+    a fraction without observations) and the current pose prediction (true pose
+    with a small error).  Returns (spslam_proj_frame record, spslam_proj_point
+    records)."""
+    import spslam_match as M
+    fx, fy, cx, cy = K["fx"], K["fy"], K["cx"], K["cy"]
+    Twl = scene.pose(last_fi)
+    Tcw = np.linalg.inv(scene.pose(cur_fi))
+    ax = rng.normal(size=3)
+    ax *= np.deg2rad(rot_noise_deg) / max(np.linalg.norm(ax), 1e-12)
+    dT = np.eye(4)
+    dT[:3, :3] = _rot(ax)
+    dT[:3, 3] = rng.normal(size=3) * trans_noise
+    Tcw = dT @ Tcw
+    pts = []
+    for i, kp in enumerate(last_kps):
+        if rng.uniform() > map_frac:
+            continue
+        x, y = int(kp["x"]), int(kp["y"])
+        z = float(last_depth_u16[y, x]) / K["depth_factor"]
+        if z <= 0:
+            continue
+        Xc = np.array([(kp["x"] - cx) * z / fx, (kp["y"] - cy) * z / fy, z, 1.0])
+        Xw = Twl @ Xc
+        d = np.array(last_desc[i], np.uint8).copy()
+        bits = np.unpackbits(d)
+        flip = rng.choice(256, size=flip_bits, replace=False)
+        bits[flip] ^= 1
+        pts.append((Xw[:3], float(kp["angle"]), int(kp["octave"]),
+                    0 if rng.uniform() < zero_obs_frac else int(rng.integers(1, 6)), i, np.packbits(bits)))
+    P = np.zeros(len(pts), M.PROJ_POINT_DTYPE)
+    for j, (xw, ang, octv, nobs, i, d) in enumerate(pts):
+        P[j]["xw"], P[j]["angle"], P[j]["octave"], P[j]["n_obs"], P[j]["last_index"], P[j]["desc"] = \
+            xw, ang, octv, nobs, i, d
+    fr = np.zeros((), M.PROJ_FRAME_DTYPE)
+    fr["Tcw"] = Tcw.astype(np.float32).reshape(16)
+    fr["Tlw"] = np.linalg.inv(Twl).astype(np.float32).reshape(16)
+    fr["n_points"] = len(P)
+    return fr, P

@@ -61,6 +61,8 @@ int main(void) {
   S(spslam_line_candidate) O(spslam_line_candidate, n_inliers) O(spslam_line_candidate, idx_offset)
   S(spslam_map_plane) O(spslam_map_plane, id) O(spslam_map_plane, boundary_offset) O(spslam_map_plane, n_boundary)
   S(spslam_assoc_frame) O(spslam_assoc_frame, map_offset) O(spslam_assoc_frame, n_map) S(spslam_assoc_params)
+  S(spslam_proj_point) O(spslam_proj_point, angle) O(spslam_proj_point, n_obs) O(spslam_proj_point, desc)
+  S(spslam_proj_frame) O(spslam_proj_frame, Tlw) O(spslam_proj_frame, point_offset) S(spslam_match_params)
   return 0;
 }
 """
@@ -69,6 +71,7 @@ int main(void) {
 def test_struct_layouts_match_bindings(tmp_path):
     import spslam_assoc
     import spslam_gpu
+    import spslam_match
     import spslam_planes
     src = tmp_path / "layout.c"
     src.write_text(LAYOUT_C)
@@ -83,6 +86,7 @@ def test_struct_layouts_match_bindings(tmp_path):
         "spslam_pose_result": spslam_gpu.POSE_RESULT_DTYPE, "spslam_plane": spslam_planes.PLANE_DTYPE,
         "spslam_supposed_plane": spslam_planes.SUPPOSED_DTYPE, "spslam_line_candidate": spslam_planes.LINE_CAND_DTYPE,
         "spslam_map_plane": spslam_assoc.MAP_PLANE_DTYPE, "spslam_assoc_frame": spslam_assoc.ASSOC_FRAME_DTYPE,
+        "spslam_proj_point": spslam_match.PROJ_POINT_DTYPE, "spslam_proj_frame": spslam_match.PROJ_FRAME_DTYPE,
     }
     for name, dt in checks.items():
         assert got[name] == dt.itemsize, (name, got[name], dt.itemsize)
@@ -94,6 +98,7 @@ def test_struct_layouts_match_bindings(tmp_path):
     assert got["spslam_plane_params"] == ctypes.sizeof(spslam_planes.PlaneParams)
     assert got["spslam_plane_config"] == 6 * 8
     assert got["spslam_assoc_params"] == ctypes.sizeof(spslam_assoc.AssocParams)
+    assert got["spslam_match_params"] == ctypes.sizeof(spslam_match.MatchParams)
     assert got["spslam_keypoint"] == 28  # cv::KeyPoint
 
 
