@@ -61,7 +61,8 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
     return out
 
 
-def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0, n_fpl=0, n_map=0, n_bnd=0):
+def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0, n_fpl=0, n_map=0, n_bnd=0,
+                      n_proj=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -86,6 +87,9 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         # two AssociatePlanesByBoundary calls: frame + plane coefficients + map records + boundary cloud in,
         # match / parallel / vertical out
         "plane_assoc_kernel": 2 * (80 + n_fpl * (16 + 12) + n_map * 32 + n_bnd * 12),
+        # SearchByProjection: last-frame map points in, current keypoints + descriptors + uR + grid read,
+        # match out
+        "search_projection": n_proj * 64 + n_kp * (28 + 32 + 4 + 4 + 4) + 4 * 3073,
         "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
 
@@ -115,18 +119,26 @@ def cpu_baseline(hp, budget_s=12.0):
     import oracle_supposed
     import oracle_assoc
     import oracle_frame
+    import oracle_match
     orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     po = oracle_planes.PlaneOracle()
     n = 0
     U = len(hp.frames)
     depth_f = [f[2].astype(np.float32) * np.float32(np.float32(1.0) / np.float32(5000.0)) for f in hp.frames]
+    b, gin = hp.fs.bounds, hp.fs.grid_inv
+    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, 40.0, *b, *gin], hp.ex.tables()["scale"]]).astype(np.float32)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
         i = n % U
-        ko, _ = orb.extract(hp.frames[i][1], cap=20000)
+        ko, do = orb.extract(hp.frames[i][1], cap=20000)
         r = po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
         so = oracle_supposed.generate(depth_f[i], po.cloud(), r["coef"], r["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
-        oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy, bf=40.0)
+        fo = oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy,
+                                     bf=40.0)
+        kun = ko.copy()
+        kun["x"], kun["y"] = fo["un"][:, 0], fo["un"][:, 1]
+        fr, P = hp.match_probs[i % len(hp.match_probs)]
+        oracle_match.search_by_projection(fr, P, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"], geo)
         coefs = np.concatenate([np.asarray(r["coef"], np.float32).reshape(-1, 4),
                                 np.asarray(so["coef"], np.float32).reshape(-1, 4)])
         pa, pts, pls, _ = hp.probA[i]
@@ -143,7 +155,7 @@ def cpu_baseline(hp, budget_s=12.0):
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + frame steps + 2x (plane association + PoseOptimization){' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + PoseOptimization){' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -204,7 +216,7 @@ def main():
         lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
     n_fpl = float(res["plane_counts"].mean()) + n_sup
     alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes, n_fpl, hp.n_map,
-                            hp.n_boundary)
+                            hp.n_boundary, hp.mean_proj_points)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step

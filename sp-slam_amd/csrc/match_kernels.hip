@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
     if (i >= F.n_points || i >= max_points) return;
     MatchWindow w{};
-    w.best = kNone;
+    w.best[0] = w.best[1] = w.best[2] = kNone;
     w.valid = 0;
     w.x0 = 1;
     w.x1 = 0;
@@ -132,13 +132,24 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
     const float* uright = C.uright + (size_t)f * C.cap;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-    uint32_t best = kNone;
+    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;  // keys are unique (CSR position in the low bits)
     for (int ix = x0; ix <= x1; ix++)
         for (int iy = y0; iy <= y1; iy++) {
             const int c = ix * kRows + iy;
-            for (int j = GO[c]; j < GO[c + 1]; j++) best = min(best, candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g));
+            for (int j = GO[c]; j < GO[c + 1]; j++) {
+                const uint32_t key = candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g);
+                if (key < b2) {
+                    if (key < b1) {
+                        b2 = b1;
+                        if (key < b0) { b1 = b0; b0 = key; }
+                        else b1 = key;
+                    } else {
+                        b2 = key;
+                    }
+                }
+            }
         }
-    w.best = best;
+    w.best[0] = b0; w.best[1] = b1; w.best[2] = b2;
     *W = w;
 }
 
@@ -188,56 +199,98 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
     const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
     const float* uright = C.uright + (size_t)f * C.cap;
+    const spslam_proj_point* P = points + F.point_offset;
     int2* PU = pushes + (size_t)f * max_points;
     const float factor = __fdiv_rn(1.0f, (float)kHisto);
     int n_push = 0;
-    for (int i = 0; i < np; i++) {
-        const MatchWindow w = Wf[i];  // uniform (every lane reads the same entry)
-        if (!w.valid) continue;
-        uint32_t best = w.best;
-        if (best != kNone) {
-            const int b = GI[best & 0xfffff];
-            if ((taken[b >> 5] >> (b & 31)) & 1) {
+    for (int c0 = 0; c0 < np; c0 += 64) {
+        // every lane fetches its point's precomputed state (one round of loads per 64 points) ...
+        const int i = c0 + lane;
+        int valid = 0, blocking = 0;
+        uint32_t best[3] = {kNone, kNone, kNone};
+        int b[3] = {-1, -1, -1};
+        float kang[3] = {0.f, 0.f, 0.f};
+        float pangle = 0.f;
+        if (i < np) {
+            const MatchWindow w = Wf[i];
+            valid = w.valid;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                best[q] = w.best[q];
+                if (valid && best[q] != kNone) {
+                    b[q] = GI[best[q] & 0xfffff];
+                    kang[q] = kun[b[q]].angle;
+                }
+            }
+            blocking = P[i].n_obs > 0;
+            pangle = P[i].angle;
+        }
+        // ... then the reference's loop walks the 64 points in order
+        const int m = min(64, np - c0);
+        for (int L = 0; L < m; L++) {
+            if (!__shfl(valid, L)) continue;
+            // the best candidate not taken by an earlier point: the first of the 3 smallest keys whose keypoint
+            // is free, else (all 3 taken) a re-scan of the window
+            __builtin_amdgcn_wave_barrier();
+            uint32_t bestL = kNone;
+            int bL = -1;
+            float kangL = 0.f;
+            bool rescan = false;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
+                const int bq = __shfl(b[q], L);
+                const float aq = __shfl(kang[q], L);
+                if (bestL != kNone || rescan || kq == kNone) continue;  // sorted: kNone ends the list
+                if (!((taken[bq >> 5] >> (bq & 31)) & 1)) { bestL = kq; bL = bq; kangL = aq; }
+                else if (q == 2) rescan = true;
+            }
+            if (rescan) {
                 // an earlier point holds this keypoint: search the window again without the taken ones
-                const spslam_proj_point& p = points[F.point_offset + i];
+                const MatchWindow w = Wf[c0 + L];
+                const spslam_proj_point& p = P[c0 + L];
                 const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-                uint32_t m = kNone;
+                uint32_t mn = kNone;
                 for (int ix = w.x0; ix <= w.x1; ix++)
                     for (int iy = w.y0; iy <= w.y1; iy++) {
                         const int c = ix * kRows + iy;
                         for (int j = GO[c] + lane; j < GO[c + 1]; j += 64) {
                             const int k = GI[j];
                             if ((taken[k >> 5] >> (k & 31)) & 1) continue;
-                            m = min(m, candidate_key(w, C, uright, desc, kun, j, k, d0, d1, g));
+                            mn = min(mn, candidate_key(w, C, uright, desc, kun, j, k, d0, d1, g));
                         }
                     }
 #pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o));
-                best = m;
+                for (int o = 32; o >= 1; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+                bestL = mn;
+                if (bestL != kNone) {
+                    bL = GI[bestL & 0xfffff];
+                    kangL = kun[bL].angle;
+                }
             }
-        }
-        if (best == kNone || (int)(best >> 20) > kThHigh) continue;
-        const int b = GI[best & 0xfffff];
-        const spslam_proj_point& p = points[F.point_offset + i];
-        if (lane == 0) {
-            M[b] = i;
-            if (p.n_obs > 0) taken[b >> 5] |= 1u << (b & 31);
-            int bin = 0;
-            if (check_ori) {
-                float rot = __fsub_rn(p.angle, kun[b].angle);
-                if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-                bin = (int)roundf(__fmul_rn(rot, factor));
-                if (bin == kHisto) bin = 0;
-                hist[bin]++;
+            if (bestL == kNone || (int)(bestL >> 20) > kThHigh) continue;
+            const int blockL = __shfl(blocking, L);
+            const float pangL = __shfl(pangle, L);
+            if (lane == 0) {
+                M[bL] = c0 + L;
+                if (blockL) taken[bL >> 5] |= 1u << (bL & 31);
+                int bin = 0;
+                if (check_ori) {
+                    float rot = __fsub_rn(pangL, kangL);
+                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                    bin = (int)roundf(__fmul_rn(rot, factor));
+                    if (bin == kHisto) bin = 0;
+                    hist[bin]++;
+                }
+                PU[n_push] = make_int2(bL, bin);
             }
-            PU[n_push] = make_int2(b, bin);
+            n_push++;
+            __builtin_amdgcn_wave_barrier();
         }
-        n_push++;
-        __syncthreads();
     }
+    __syncthreads();
     int n = n_push;
     if (check_ori) {
-        __syncthreads();
         if (lane == 0) three_maxima(hist, &ind[0], &ind[1], &ind[2]);
         __syncthreads();
         const int i1 = ind[0], i2 = ind[1], i3 = ind[2];

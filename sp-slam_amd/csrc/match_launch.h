@@ -29,7 +29,7 @@ struct MatchWindow {
     float u, v, r, invzc;
     int16_t x0, x1, y0, y1;  // GetFeaturesInArea cell range (x0 > x1: empty)
     int8_t min_level, max_level, valid, pad;
-    uint32_t best;           // (distance << 20) | CSR position of the best candidate; ~0u: none
+    uint32_t best[3];        // the 3 smallest (distance << 20) | CSR position over the window; ~0u: none
 };
 
 hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const spslam_proj_point* points,

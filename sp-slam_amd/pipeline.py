@@ -107,6 +107,7 @@ class HotPath:
         self.d_res2 = torch.zeros_like(self.d_res1)
         self.mean_keypoints = float(cnts.mean())
         self._setup_assoc(seq_id)
+        self._setup_match(seq_id)
         # --- LocalBundleAdjustment (C3): one local map per `lba_every` frames (a keyframe), run on the
         #     LocalMapping stream beside tracking like the reference's LocalMapping thread
         self.n_lba = B // lba_every if lba_every else 0
@@ -140,6 +141,49 @@ class HotPath:
         P = self.pe.planes_cap + self.pe.supp_cap
         self.d_assoc = torch.zeros((2, 3, B * P), dtype=torch.int32, device="cuda")
         self.d_newp = torch.zeros((2, B), dtype=torch.int32, device="cuda")
+
+    def _setup_match(self, seq_id):
+        """ORBmatcher::SearchByProjection(CurrentFrame, LastFrame) of TrackWithMotionModel: every frame
+        of the batch is matched against the map points of the frame rendered just before it (its ORB
+        keypoints back-projected with the true depth, descriptors with a few flipped bits), from a
+        motion-model pose prediction."""
+        import spslam_match as SM
+        torch, B, U = self.torch, self.B, len(self.frames)
+        rng = np.random.default_rng(seq_id * 977 + 3)
+        last = [self.scene.render(self.scene.pose(f[0] - 1), self.W, self.H, noise_seed=seq_id * 1000 + f[0] + 500)
+                for f in self.frames]
+        d_g = torch.from_numpy(np.stack([g for g, _, _ in last])).cuda()
+        cap = self.kp_cap
+        d_k = torch.zeros((U, cap, 7), dtype=torch.float32, device="cuda")
+        d_d = torch.zeros((U, cap, 32), dtype=torch.uint8, device="cuda")
+        d_n = torch.zeros(U, dtype=torch.int32, device="cuda")
+        self.ex.extract_batch_device(d_g.data_ptr(), U, self.W * self.H, self.W, d_k.data_ptr(), d_d.data_ptr(),
+                                     d_n.data_ptr(), cap, self.stream)
+        torch.cuda.synchronize()
+        kps = d_k.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(U, cap)
+        desc, cnt = d_d.cpu().numpy(), d_n.cpu().numpy()
+        Ks = dict(synth.TUM3, fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy)
+        probs = [synth.proj_problem(self.scene, self.frames[i][0] - 1, self.frames[i][0], kps[i, :cnt[i]],
+                                    desc[i, :cnt[i]], last[i][1], rng, K=Ks) for i in range(U)]
+        offs = np.cumsum([0] + [len(p[1]) for p in probs])
+        fr = np.zeros(B, SM.PROJ_FRAME_DTYPE)
+        for i in range(B):
+            fr[i] = probs[i % U][0]
+            fr[i]["point_offset"] = offs[i % U]
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
+        self.match_probs = probs
+        self.matcher = SM.Matcher(self.ex)
+        self.d_pframes, self.d_ppoints = dev(fr), dev(np.concatenate([p[1] for p in probs]))
+        self.max_points = int(max(len(p[1]) for p in probs))
+        self.mean_proj_points = float(np.mean([len(probs[i % U][1]) for i in range(B)]))
+        self.d_match = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+        self.d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
+
+    def match(self):
+        self.matcher.batch_device(self.B, self.d_pframes.data_ptr(), self.d_ppoints.data_ptr(), self.max_points,
+                                  self.d_kun.data_ptr(), self.d_desc.data_ptr(), self.d_kur.data_ptr(),
+                                  self.d_grid_off.data_ptr(), self.d_grid_idx.data_ptr(), self.d_cnt.data_ptr(),
+                                  self.kp_cap, self.d_match.data_ptr(), self.d_nmatch.data_ptr(), stream=self.stream)
 
     def associate(self, k):
         import spslam_planes as SP
@@ -283,6 +327,7 @@ class HotPath:
         self.ev_join.record(self.side)
         self.main.wait_event(self.ev_join)
         self.frame()
+        self.match()
         self.pose()
         if self.n_lba:
             self.lba_job.result()
@@ -301,6 +346,7 @@ class HotPath:
             pose1=self.d_res1.cpu().numpy().view(G.POSE_RESULT_DTYPE),
             pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE),
             assoc=self.d_assoc.cpu().numpy().reshape(2, 3, self.B, -1),
+            match=self.d_match.cpu().numpy(), nmatches=self.d_nmatch.cpu().numpy(),
             new_plane=self.d_newp.cpu().numpy())
 
     def _plane_field(self, name):

@@ -44,6 +44,28 @@ def test_orb_and_frame_stage(run):
         assert np.array_equal(kdep[i, :n], fo["depth"]), i
 
 
+def test_projection_matching(run):
+    import oracle_match as OM
+    import spslam_gpu as G
+    hp, res = run
+    t = hp.ex.tables()
+    kun = hp.d_kun.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(hp.B, hp.kp_cap)
+    desc = hp.d_desc.cpu().numpy()
+    ur = hp.d_kur.cpu().numpy()
+    go, gi = hp.d_grid_off.cpu().numpy(), hp.d_grid_idx.cpu().numpy()
+    b, ginv = hp.fs.bounds, hp.fs.grid_inv
+    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, 40.0, *b, *ginv], t["scale"]]).astype(np.float32)
+    total = 0
+    for i in range(hp.B):
+        n = int(res["kp_counts"][i])
+        fr, P = hp.match_probs[i % len(hp.match_probs)]
+        mo, nmo, _ = OM.search_by_projection(fr, P, kun[i, :n], desc[i, :n], ur[i, :n], go[i], gi[i, :go[i][-1]], geo)
+        assert int(res["nmatches"][i]) == nmo, i
+        assert np.array_equal(res["match"][i, :n], mo), i
+        total += nmo
+    assert total > 0
+
+
 def _frame_planes(hp, res, i):
     import spslam_planes as SP
     pl = hp.d_planes.cpu().numpy().view(SP.PLANE_DTYPE).reshape(hp.B, hp.pe.planes_cap)
