@@ -62,7 +62,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
 
 
 def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0, n_fpl=0, n_map=0, n_bnd=0,
-                      n_proj=0):
+                      n_proj=0, n_local=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -90,6 +90,8 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         # SearchByProjection: last-frame map points in, current keypoints + descriptors + uR + grid read,
         # match out
         "search_projection": n_proj * 64 + n_kp * (28 + 32 + 4 + 4 + 4) + 4 * 3073,
+        # SearchLocalPoints: local map points in, the same current-frame reads, taken flags in, match out
+        "search_local_points": n_local * 80 + n_kp * (28 + 32 + 4 + 4 + 1 + 4) + 4 * 3073,
         "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
 
@@ -138,12 +140,16 @@ def cpu_baseline(hp, budget_s=12.0):
         kun = ko.copy()
         kun["x"], kun["y"] = fo["un"][:, 0], fo["un"][:, 1]
         fr, P = hp.match_probs[i % len(hp.match_probs)]
-        oracle_match.search_by_projection(fr, P, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"], geo)
+        mo, _, _ = oracle_match.search_by_projection(fr, P, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"],
+                                                     geo)
         coefs = np.concatenate([np.asarray(r["coef"], np.float32).reshape(-1, 4),
                                 np.asarray(so["coef"], np.float32).reshape(-1, 4)])
         pa, pts, pls, _ = hp.probA[i]
         oracle_assoc.associate(pa["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
         r1, _, _ = oracle_ctypes.pose_optimize(pa, pts, pls)
+        lfr, LP = hp.local_probs[i % len(hp.local_probs)]
+        oracle_match.search_local_points(lfr, LP, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"], geo,
+                                         taken=(mo >= 0).astype(np.uint8))
         oracle_assoc.associate(r1["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
         pb, pts2, pls2, _ = hp.probB[i]
         pb = pb.copy()
@@ -155,7 +161,7 @@ def cpu_baseline(hp, budget_s=12.0):
     dt = time.perf_counter() - t0
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + PoseOptimization){' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + PoseOptimization) + SearchLocalPoints{' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
 
 
 def main():
@@ -216,7 +222,7 @@ def main():
         lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
     n_fpl = float(res["plane_counts"].mean()) + n_sup
     alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes, n_fpl, hp.n_map,
-                            hp.n_boundary, hp.mean_proj_points)
+                            hp.n_boundary, hp.mean_proj_points, hp.mean_local_points)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step

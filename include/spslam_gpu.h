@@ -587,6 +587,57 @@ int spslam_search_by_projection_batch_device(spslam_ctx* ctx, int n_frames, cons
                                              const spslam_match_params* params, int32_t* d_match, int* d_nmatches,
                                              void* hip_stream);
 
+/* Local-map projection matching: Tracking::SearchLocalPoints (src/Tracking.cc:
+ * 1375-1425) -- Frame::isInFrustum (src/Frame.cc:369-425, viewing-cosine
+ * limit 0.5) with MapPoint::PredictScale (src/MapPoint.cc:402-417), then
+ * ORBmatcher(nn_ratio).SearchByProjection(F, vpMapPoints, th)
+ * (src/ORBmatcher.cc:45-130, RadiusByViewingCos :131-137).  The local map
+ * points are given in mvpLocalMapPoints order without those the caller skips
+ * (already matched in this frame, or bad).  d_taken (may be NULL) marks the
+ * current keypoints whose mvpMapPoints entry is already set with
+ * Observations() > 0.  Output per current keypoint: the index of the local
+ * point newly assigned to it, -1 otherwise; nmatches; optionally
+ * mbTrackInView per point. */
+typedef struct spslam_local_point {
+    float xw[3];          /* MapPoint::GetWorldPos */
+    float normal[3];      /* MapPoint::GetNormal */
+    float min_dist;       /* mfMinDistance (the invariance region is 0.8x .. 1.2x mfMaxDistance) */
+    float max_dist;       /* mfMaxDistance */
+    int32_t id;           /* mnId (informative) */
+    int32_t pad[3];
+    uint8_t desc[32];     /* MapPoint::GetDescriptor */
+} spslam_local_point;     /* 80 bytes */
+
+typedef struct spslam_local_frame {
+    float Tcw[16];        /* CurrentFrame.mTcw after the motion-model PoseOptimization */
+    int32_t point_offset; /* local points [point_offset, point_offset + n_points) */
+    int32_t n_points;
+    int32_t pad[2];
+} spslam_local_frame;     /* 80 bytes */
+
+typedef struct spslam_local_params {
+    float th;             /* 3 for RGB-D, 5 right after relocalisation (Tracking.cc:1416-1422) */
+    float nn_ratio;       /* ORBmatcher mfNNratio (0.8) */
+    float view_cos_limit; /* isInFrustum limit (0.5) */
+    int32_t pad;
+} spslam_local_params;
+
+int spslam_search_local_points(spslam_ctx* ctx, const spslam_local_frame* frame, const spslam_local_point* points,
+                               const spslam_keypoint* keys_un, const uint8_t* desc, const float* uright, int n_kp,
+                               const int32_t* grid_off, const int32_t* grid_idx, const uint8_t* taken,
+                               const spslam_local_params* params, int32_t* match, int* nmatches, uint8_t* in_view);
+
+/* Batched, device resident, same current-frame layout as
+ * spslam_search_by_projection_batch_device; d_taken at f*cap (may be NULL),
+ * d_in_view at the points' global index (may be NULL). */
+int spslam_search_local_points_batch_device(spslam_ctx* ctx, int n_frames, const spslam_local_frame* d_frames,
+                                            const spslam_local_point* d_points, int max_points,
+                                            const spslam_keypoint* d_keys_un, const uint8_t* d_desc,
+                                            const float* d_uright, const int32_t* d_grid_off,
+                                            const int32_t* d_grid_idx, const int* d_counts, int cap,
+                                            const uint8_t* d_taken, const spslam_local_params* params,
+                                            int32_t* d_match, int* d_nmatches, uint8_t* d_in_view, void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

@@ -238,3 +238,139 @@ int oracle_search_by_projection(const void* frame, const void* points, const voi
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Tracking::SearchLocalPoints (src/Tracking.cc:1375-1425): Frame::isInFrustum
+// (src/Frame.cc:369-425, viewing-cosine limit 0.5) with MapPoint::PredictScale
+// (src/MapPoint.cc:402-417), then ORBmatcher(0.8).SearchByProjection(F,
+// vpMapPoints, th) (src/ORBmatcher.cc:45-130) with RadiusByViewingCos
+// (:131-137).  Points the caller already holds (mnLastFrameSeen == current, or
+// bad) are left out of the list; `taken` marks keypoints whose mvpMapPoints
+// entry is set with Observations() > 0 before the call.
+// FP (OpenCV parts parity-unpinned): Rcw*P + tcw and -Rcw^T*tcw as above;
+// cv::norm of a float 3-vector = sqrt((double)(float)(x*x + y*y + z*z)) with
+// float partial sums; Mat::dot in double with exact products; log / ceil as
+// PredictScale writes them (float logf).
+namespace oracle {
+namespace match {
+
+struct LocalPoint {  // spslam_local_point
+    float xw[3], normal[3];
+    float min_dist, max_dist;
+    int32_t id, pad[3];
+    uint8_t desc[32];
+};
+struct LocalFrame {  // spslam_local_frame
+    float Tcw[16];
+    int32_t point_offset, n_points, pad[2];
+};
+struct LocalParams {  // spslam_local_params
+    float th, nn_ratio, view_cos_limit, log_scale_factor;
+    int32_t n_levels, pad[3];
+};
+
+struct InView {
+    bool in;
+    float u, ur, v, view_cos;
+    int level;
+};
+
+InView is_in_frustum(const float* Tcw, const LocalPoint& p, const Geometry& G, const LocalParams& P) {
+    InView r{};
+    const float tcw[3] = {Tcw[3], Tcw[7], Tcw[11]};
+    float Pc[3], Ow[3];
+    mat3_mul(Tcw, p.xw, tcw, false, 1.0f, Pc);
+    if (Pc[2] < 0.0f) return r;
+    const float invz = 1.0f / Pc[2];
+    const float u = std::fmaf(G.fx * Pc[0], invz, G.cx);
+    const float v = std::fmaf(G.fy * Pc[1], invz, G.cy);
+    if (u < G.min_x || u > G.max_x) return r;
+    if (v < G.min_y || v > G.max_y) return r;
+    const float maxDistance = 1.2f * p.max_dist, minDistance = 0.8f * p.min_dist;
+    mat3_mul(Tcw, tcw, nullptr, true, -1.0f, Ow);
+    const float PO[3] = {p.xw[0] - Ow[0], p.xw[1] - Ow[1], p.xw[2] - Ow[2]};
+    float s = PO[0] * PO[0];
+    s = s + PO[1] * PO[1];
+    s = s + PO[2] * PO[2];
+    const float dist = (float)std::sqrt((double)s);
+    if (dist < minDistance || dist > maxDistance) return r;
+    double dot = 0.0;
+    for (int k = 0; k < 3; k++) dot += (double)PO[k] * (double)p.normal[k];
+    const float viewCos = (float)(dot / (double)dist);
+    if (viewCos < P.view_cos_limit) return r;
+    const float ratio = p.max_dist / dist;
+    int nScale = (int)std::ceil(std::log(ratio) / P.log_scale_factor);
+    if (nScale < 0) nScale = 0;
+    else if (nScale >= P.n_levels) nScale = P.n_levels - 1;
+    r.in = true;
+    r.u = u;
+    r.ur = std::fmaf(-G.bf, invz, u);
+    r.v = v;
+    r.view_cos = viewCos;
+    r.level = nScale;
+    return r;
+}
+
+int search_local(const LocalFrame& fr, const LocalPoint* P, const Current& F, const Geometry& G,
+                 const LocalParams& prm, const uint8_t* taken_in, int32_t* match, uint8_t* in_view) {
+    std::vector<uint8_t> taken(F.n, 0);
+    for (int k = 0; k < F.n; k++) {
+        match[k] = -1;
+        taken[k] = taken_in ? taken_in[k] : 0;
+    }
+    const bool bFactor = prm.th != 1.0f;
+    int nmatches = 0;
+    std::vector<int> idx;
+    for (int i = 0; i < fr.n_points; i++) {
+        const InView iv = is_in_frustum(fr.Tcw, P[i], G, prm);
+        if (in_view) in_view[i] = iv.in;
+        if (!iv.in) continue;
+        const int nPredictedLevel = iv.level;
+        float r = iv.view_cos > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos
+        if (bFactor) r *= prm.th;
+        const float rs = r * G.scale[nPredictedLevel];
+        features_in_area(F, G, iv.u, iv.v, rs, nPredictedLevel - 1, nPredictedLevel, idx);
+        if (idx.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int k : idx) {
+            if (taken[k]) continue;
+            if (F.uright[k] > 0) {
+                const float er = std::fabs(iv.ur - F.uright[k]);
+                if (er > rs) continue;
+            }
+            const int dist = descriptor_distance(P[i].desc, F.desc + 32 * (size_t)k);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = F.kun[k].octave;
+                bestIdx = k;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F.kun[k].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= kThHigh) {
+            if (bestLevel == bestLevel2 && bestDist > prm.nn_ratio * bestDist2) continue;
+            match[bestIdx] = i;
+            taken[bestIdx] = 1;  // a local map point has observations
+            nmatches++;
+        }
+    }
+    return nmatches;
+}
+
+}  // namespace match
+}  // namespace oracle
+
+extern "C" int oracle_search_local_points(const void* frame, const void* points, const void* keys_un,
+                                          const uint8_t* desc, const float* uright, int n_kp, const int32_t* grid_off,
+                                          const int32_t* grid_idx, const float* geometry, const void* params,
+                                          const uint8_t* taken, int32_t* match, uint8_t* in_view) {
+    using namespace oracle::match;
+    Geometry G;
+    std::memcpy(&G, geometry, sizeof G);
+    const Current F{(const Keypoint*)keys_un, desc, uright, grid_off, grid_idx, n_kp};
+    return search_local(*(const LocalFrame*)frame, (const LocalPoint*)points, F, G, *(const LocalParams*)params,
+                        taken, match, in_view);
+}

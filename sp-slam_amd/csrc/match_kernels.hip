@@ -309,7 +309,249 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     if (lane == 0) nmatches[f] = n;
 }
 
+// ---------------------------------------------------------------------------
+// Tracking::SearchLocalPoints: isInFrustum + PredictScale per local point,
+// then ORBmatcher::SearchByProjection(F, vpMapPoints, th) (src/ORBmatcher.cc:
+// 45-130).  Same two-kernel shape: the window kernel keeps the 3 smallest keys
+// over the window (initially taken keypoints excluded); the in-order walk
+// needs the best AND the second best among the keypoints still free (the
+// ratio test), which the 3 keys give unless in-loop assignments took two of
+// them -- then the wave re-scans for both.
+__global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_local_frame* __restrict__ frames,
+                                                                const spslam_local_point* __restrict__ points,
+                                                                int max_points, MatchCurrent C, MatchGeom g,
+                                                                LocalConsts P, const uint8_t* __restrict__ taken_in,
+                                                                LocalWindow* __restrict__ win,
+                                                                uint8_t* __restrict__ in_view) {
+    const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
+    const spslam_local_frame& F = frames[f];
+    if (i >= F.n_points || i >= max_points) return;
+    LocalWindow w{};
+    w.best[0] = w.best[1] = w.best[2] = kNone;
+    w.x0 = 1;
+    w.x1 = 0;
+    LocalWindow* W = win + (size_t)f * max_points + i;
+    const spslam_local_point& p = points[F.point_offset + i];
+    bool in = false;
+    // Frame::isInFrustum(pMP, 0.5)
+    const float tcw[3] = {F.Tcw[3], F.Tcw[7], F.Tcw[11]};
+    float Pc[3], Ow[3];
+    mat3_mul(F.Tcw, p.xw, tcw, false, 1.0, Pc);
+    float u = 0.f, v = 0.f, invz = 0.f, viewCos = 0.f;
+    int level = 0;
+    do {
+        if (Pc[2] < 0.0f) break;
+        invz = __fdiv_rn(1.0f, Pc[2]);
+        u = __fmaf_rn(__fmul_rn(g.fx, Pc[0]), invz, g.cx);
+        v = __fmaf_rn(__fmul_rn(g.fy, Pc[1]), invz, g.cy);
+        if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) break;
+        const float maxD = __fmul_rn(1.2f, p.max_dist), minD = __fmul_rn(0.8f, p.min_dist);
+        mat3_mul(F.Tcw, tcw, nullptr, true, -1.0, Ow);
+        const float PO[3] = {__fsub_rn(p.xw[0], Ow[0]), __fsub_rn(p.xw[1], Ow[1]), __fsub_rn(p.xw[2], Ow[2])};
+        float sq = __fmul_rn(PO[0], PO[0]);
+        sq = __fadd_rn(sq, __fmul_rn(PO[1], PO[1]));
+        sq = __fadd_rn(sq, __fmul_rn(PO[2], PO[2]));
+        const float dist = (float)__dsqrt_rn((double)sq);  // cv::norm
+        if (dist < minD || dist > maxD) break;
+        double dot = __dmul_rn((double)PO[0], (double)p.normal[0]);
+        dot = __dadd_rn(dot, __dmul_rn((double)PO[1], (double)p.normal[1]));
+        dot = __dadd_rn(dot, __dmul_rn((double)PO[2], (double)p.normal[2]));
+        viewCos = (float)__ddiv_rn(dot, (double)dist);
+        if (viewCos < P.view_cos_limit) break;
+        // PredictScale: ceil(log(ratio) / mfLogScaleFactor); the correctly rounded logf gives the same
+        // level as glibc's for every float ratio (tests/test_libm_restated.py)
+        const float ratio = __fdiv_rn(p.max_dist, dist);
+        int n = (int)ceilf(__fdiv_rn((float)log((double)ratio), P.log_scale_factor));
+        level = n < 0 ? 0 : (n >= P.n_levels ? P.n_levels - 1 : n);
+        in = true;
+    } while (false);
+    if (in_view) in_view[F.point_offset + i] = in;
+    if (!in) { *W = w; return; }
+    float r = viewCos > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos
+    if (P.th != 1.0f) r = __fmul_rn(r, P.th);
+    const float rs = __fmul_rn(r, g.scale[level]);
+    w.u = u; w.v = v; w.rs = rs; w.ur = __fmaf_rn(-g.bf, invz, u);
+    w.level = (int8_t)level;
+    w.in_view = 1;
+    const int x0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(u, g.min_x), rs), g.ginv_x)));
+    const int x1 = min(kCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(u, g.min_x), rs), g.ginv_x)));
+    const int y0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(v, g.min_y), rs), g.ginv_y)));
+    const int y1 = min(kRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(v, g.min_y), rs), g.ginv_y)));
+    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { *W = w; return; }
+    w.x0 = (int16_t)x0; w.x1 = (int16_t)x1; w.y0 = (int16_t)y0; w.y1 = (int16_t)y1;
+    // the frame-to-frame candidate test with its window: same expressions (ur = fma(-mbf, invz, u))
+    MatchWindow mw{};
+    mw.u = u; mw.v = v; mw.r = rs; mw.invzc = invz;
+    mw.min_level = (int8_t)(level - 1);
+    mw.max_level = (int8_t)level;
+    const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
+    const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
+    const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
+    const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
+    const float* uright = C.uright + (size_t)f * C.cap;
+    const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
+    const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
+    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;
+    for (int ix = x0; ix <= x1; ix++)
+        for (int iy = y0; iy <= y1; iy++) {
+            const int c = ix * kRows + iy;
+            for (int j = GO[c]; j < GO[c + 1]; j++) {
+                const int k = GI[j];
+                if (tk && tk[k]) continue;
+                const uint32_t key = candidate_key(mw, C, uright, desc, kun, j, k, d0, d1, g);
+                if (key < b2) {
+                    if (key < b1) {
+                        b2 = b1;
+                        if (key < b0) { b1 = b0; b0 = key; }
+                        else b1 = key;
+                    } else {
+                        b2 = key;
+                    }
+                }
+            }
+        }
+    w.best[0] = b0; w.best[1] = b1; w.best[2] = b2;
+    *W = w;
+}
+
+__global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_frame* __restrict__ frames,
+                                                          const spslam_local_point* __restrict__ points,
+                                                          int max_points, MatchCurrent C, MatchGeom g, LocalConsts P,
+                                                          const uint8_t* __restrict__ taken_in,
+                                                          const LocalWindow* __restrict__ win,
+                                                          int32_t* __restrict__ match, int* __restrict__ nmatches) {
+    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
+    const int f = blockIdx.x, lane = threadIdx.x;
+    const spslam_local_frame& F = frames[f];
+    const int n_kp = min(C.counts[f], C.cap), np = min(F.n_points, max_points);
+    int32_t* M = match + (size_t)f * C.cap;
+    const int words = (C.cap + 31) / 32;
+    const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
+    for (int k = lane; k < n_kp; k += 64) M[k] = -1;
+    for (int wd = lane; wd < words; wd += 64) {
+        uint32_t bits = 0;
+        if (tk)
+            for (int q = 0; q < 32; q++) {
+                const int k = wd * 32 + q;
+                if (k < n_kp && tk[k]) bits |= 1u << q;
+            }
+        taken[wd] = bits;
+    }
+    __syncthreads();
+    const LocalWindow* Wf = win + (size_t)f * max_points;
+    const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
+    const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
+    const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
+    const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
+    const float* uright = C.uright + (size_t)f * C.cap;
+    const spslam_local_point* Pp = points + F.point_offset;
+    int nm = 0;
+    for (int c0 = 0; c0 < np; c0 += 64) {
+        const int i = c0 + lane;
+        int valid = 0;
+        uint32_t best[3] = {kNone, kNone, kNone};
+        int b[3] = {-1, -1, -1}, oc[3] = {-1, -1, -1};
+        if (i < np) {
+            const LocalWindow w = Wf[i];
+            valid = w.in_view;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                best[q] = w.best[q];
+                if (valid && best[q] != kNone) {
+                    b[q] = GI[best[q] & 0xfffff];
+                    oc[q] = kun[b[q]].octave;
+                }
+            }
+        }
+        const int m = min(64, np - c0);
+        for (int L = 0; L < m; L++) {
+            if (!__shfl(valid, L)) continue;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t k1 = kNone, k2 = kNone;
+            int b1 = -1, o1 = -1, o2 = -1, nk = 0;
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
+                const int bq = __shfl(b[q], L), oq = __shfl(oc[q], L);
+                if (kq == kNone) continue;
+                nk++;
+                if ((taken[bq >> 5] >> (bq & 31)) & 1) continue;
+                if (k1 == kNone) { k1 = kq; b1 = bq; o1 = oq; }
+                else if (k2 == kNone) { k2 = kq; o2 = oq; }
+            }
+            if (nk == 3 && k2 == kNone) {
+                // in-loop assignments took two of the 3 keys: best and second best over the window again
+                const LocalWindow w = Wf[c0 + L];
+                MatchWindow mw{};
+                mw.u = w.u; mw.v = w.v; mw.r = w.rs;
+                mw.invzc = 0.f;
+                mw.min_level = (int8_t)(w.level - 1);
+                mw.max_level = w.level;
+                const spslam_local_point& p = Pp[c0 + L];
+                const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
+                uint32_t m1 = kNone, m2 = kNone;
+                for (int ix = w.x0; ix <= w.x1; ix++)
+                    for (int iy = w.y0; iy <= w.y1; iy++) {
+                        const int c = ix * kRows + iy;
+                        for (int j = GO[c] + lane; j < GO[c + 1]; j += 64) {
+                            const int k = GI[j];
+                            if ((taken[k >> 5] >> (k & 31)) & 1) continue;
+                            // candidate_key's stereo test recomputes ur from invzc; use the stored mTrackProjXR
+                            const spslam_keypoint kp = kun[k];
+                            if (kp.octave < mw.min_level || kp.octave > mw.max_level) continue;
+                            if (!(fabsf(__fsub_rn(kp.x, w.u)) < w.rs && fabsf(__fsub_rn(kp.y, w.v)) < w.rs)) continue;
+                            const float urk = uright[k];
+                            if (urk > 0 && fabsf(__fsub_rn(w.ur, urk)) > w.rs) continue;
+                            const uint32_t key = ((uint32_t)hamming(d0, d1, desc + 32 * (size_t)k) << 20) | (uint32_t)j;
+                            if (key < m1) { m2 = m1; m1 = key; }
+                            else if (key < m2) m2 = key;
+                        }
+                    }
+                // wave top-2: the smallest key, then the smallest key above it
+                uint32_t t1 = m1;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) t1 = min(t1, (uint32_t)__shfl_xor((int)t1, o));
+                uint32_t t2 = m1 == t1 ? m2 : m1;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) t2 = min(t2, (uint32_t)__shfl_xor((int)t2, o));
+                k1 = t1;
+                k2 = t2;
+                b1 = k1 != kNone ? GI[k1 & 0xfffff] : -1;
+                o1 = b1 >= 0 ? kun[b1].octave : -1;
+                o2 = k2 != kNone ? kun[GI[k2 & 0xfffff]].octave : -1;
+            }
+            if (k1 == kNone) continue;
+            const int bestDist = (int)(k1 >> 20), bestDist2 = k2 != kNone ? (int)(k2 >> 20) : 256;
+            const int bestLevel2 = k2 != kNone ? o2 : -1;
+            if (bestDist > kThHigh) continue;
+            if (o1 == bestLevel2 && (float)bestDist > __fmul_rn(P.nn_ratio, (float)bestDist2)) continue;
+            if (lane == 0) {
+                M[b1] = c0 + L;
+                taken[b1 >> 5] |= 1u << (b1 & 31);
+            }
+            nm++;
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    if (lane == 0) nmatches[f] = nm;
+}
+
 }  // namespace match
+
+hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, const spslam_local_point* points,
+                              int max_points, const MatchCurrent& cur, const MatchGeom& g, const LocalConsts& P,
+                              const uint8_t* taken_in, LocalWindow* win, int32_t* match, int* nmatches,
+                              uint8_t* in_view, hipStream_t s, KernelTimer* timer) {
+    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
+    if (timer) timer->begin(kKindLocalMatch, s);
+    if (max_points > 0)
+        hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kThreads - 1) / match::kThreads),
+                           dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, win, in_view);
+    hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), (size_t)((cur.cap + 31) / 32) * 4, s,
+                       frames, points, max_points, cur, g, P, taken_in, win, match, nmatches);
+    if (timer) timer->end(kKindLocalMatch, s);
+    return hipGetLastError();
+}
 
 hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const spslam_proj_point* points,
                         int max_points, const MatchCurrent& cur, const MatchGeom& g, const spslam_match_params& P,

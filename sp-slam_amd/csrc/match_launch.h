@@ -32,6 +32,24 @@ struct MatchWindow {
     uint32_t best[3];        // the 3 smallest (distance << 20) | CSR position over the window; ~0u: none
 };
 
+// Local-map search state per point (SearchLocalPoints).
+struct LocalWindow {
+    float u, v, rs, ur;      // mTrackProjX / Y, r * mvScaleFactors[level], mTrackProjXR
+    int16_t x0, x1, y0, y1;
+    int8_t level, in_view, pad[2];
+    uint32_t best[3];        // 3 smallest keys over the window without the initially taken keypoints
+};
+
+struct LocalConsts {
+    float th, nn_ratio, view_cos_limit, log_scale_factor;
+    int n_levels;
+};
+
+hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, const spslam_local_point* points,
+                              int max_points, const MatchCurrent& cur, const MatchGeom& g, const LocalConsts& P,
+                              const uint8_t* taken_in, LocalWindow* win, int32_t* match, int* nmatches,
+                              uint8_t* in_view, hipStream_t s, KernelTimer* timer);
+
 hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const spslam_proj_point* points,
                         int max_points, const MatchCurrent& cur, const MatchGeom& g, const spslam_match_params& P,
                         MatchWindow* win, int2* pushes, int32_t* match, int* nmatches, hipStream_t s,

@@ -791,7 +791,8 @@ const char* kernel_kind_name(int kind) {
                                                  "plane_integral_kernel", "plane_normal_kernel",
                                                  "plane_segment_kernel", "supp_lines_kernel",
                                                  "supp_assemble_kernel", "frame_rgbd_kernel",
-                                                 "lba_batch", "plane_assoc_kernel", "search_projection"};
+                                                 "lba_batch", "plane_assoc_kernel", "search_projection",
+                                                 "search_local_points"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

@@ -20,7 +20,7 @@ struct OrbBuffers {
 enum KernelKind {
     kKindLevel = 0, kKindFast, kKindOctree, kKindDesc, kKindPose,
     kKindPlaneCloud, kKindPlaneDist, kKindPlaneIntegral, kKindPlaneNormal, kKindPlaneSegment,
-    kKindSuppLines, kKindSuppAssemble, kKindFrame, kKindLba, kKindAssoc, kKindMatch,
+    kKindSuppLines, kKindSuppAssemble, kKindFrame, kKindLba, kKindAssoc, kKindMatch, kKindLocalMatch,
     kNumKernelKinds
 };
 const char* kernel_kind_name(int kind);

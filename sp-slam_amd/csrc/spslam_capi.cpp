@@ -1198,6 +1198,86 @@ int spslam_search_by_projection(spslam_ctx* c, const spslam_proj_frame* frame, c
     return SPSLAM_OK;
 }
 
+int spslam_search_local_points_batch_device(spslam_ctx* c, int n_frames, const spslam_local_frame* d_frames,
+                                            const spslam_local_point* d_points, int max_points,
+                                            const spslam_keypoint* d_keys_un, const uint8_t* d_desc,
+                                            const float* d_uright, const int32_t* d_grid_off,
+                                            const int32_t* d_grid_idx, const int* d_counts, int cap,
+                                            const uint8_t* d_taken, const spslam_local_params* params,
+                                            int32_t* d_match, int* d_nmatches, uint8_t* d_in_view,
+                                            void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->frame_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_frame_configure not called%s", "");
+    if (n_frames < 1 || !d_frames || max_points < 0 || (max_points > 0 && !d_points) || !d_keys_un || !d_desc ||
+        !d_uright || !d_grid_off || !d_grid_idx || !d_counts || cap < 1 || cap > (1 << 20) || !params ||
+        !d_match || !d_nmatches)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_search_local_points_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
+    const size_t need = (size_t)n_frames * std::max(max_points, 1) * sizeof(LocalWindow) + 256;
+    if (need > c->match_scratch_bytes) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_match_scratch) (void)hipFree(c->d_match_scratch);
+        c->d_match_scratch = nullptr;
+        c->match_scratch_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_match_scratch, need));
+        c->match_scratch_bytes = need;
+    }
+    MatchGeom g{};
+    g.fx = c->fg.fx; g.fy = c->fg.fy; g.cx = c->fg.cx; g.cy = c->fg.cy; g.bf = c->fg.bf;
+    g.min_x = c->fg.min_x; g.max_x = c->fg.max_x; g.min_y = c->fg.min_y; g.max_y = c->fg.max_y;
+    g.ginv_x = c->fg.ginv_x; g.ginv_y = c->fg.ginv_y;
+    for (int l = 0; l < 8; l++) g.scale[l] = l < c->p.nlevels ? c->scale[l] : 0.f;
+    LocalConsts P{params->th, params->nn_ratio, params->view_cos_limit,
+                  std::log(c->p.scale_factor),  // Frame::mfLogScaleFactor = log(mfScaleFactor), float
+                  c->p.nlevels};
+    MatchCurrent cur{d_keys_un, d_desc, d_uright, d_grid_off, d_grid_idx, d_counts, cap};
+    HIP_CHECK(c, local_match_launch(n_frames, d_frames, d_points, max_points, cur, g, P, d_taken,
+                                    (LocalWindow*)c->d_match_scratch, d_match, d_nmatches, d_in_view, s, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_search_local_points(spslam_ctx* c, const spslam_local_frame* frame, const spslam_local_point* points,
+                               const spslam_keypoint* keys_un, const uint8_t* desc, const float* uright, int n_kp,
+                               const int32_t* grid_off, const int32_t* grid_idx, const uint8_t* taken,
+                               const spslam_local_params* params, int32_t* match, int* nmatches, uint8_t* in_view) {
+    if (!c || !frame || !params || !grid_off || !nmatches || n_kp < 0 || frame->n_points < 0 ||
+        (frame->n_points && !points) || (n_kp && (!keys_un || !desc || !uright || !grid_idx || !match)))
+        return SPSLAM_ERR_ARG;
+    constexpr int kCells = SPSLAM_GRID_COLS * SPSLAM_GRID_ROWS;
+    if (grid_off[0] != 0 || grid_off[kCells] > n_kp)
+        return fail(c, SPSLAM_ERR_ARG, "grid CSR does not fit the keypoints%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    spslam_local_frame F = *frame;
+    F.point_offset = 0;
+    const int np = F.n_points, cap = std::max(n_kp, 1);
+    size_t sz[] = {sizeof F, (size_t)std::max(np, 1) * sizeof(spslam_local_point), (size_t)cap * sizeof(spslam_keypoint),
+                   (size_t)cap * 32, (size_t)cap * 4, (kCells + 1) * 4, (size_t)cap * 4, sizeof(int), (size_t)cap,
+                   (size_t)cap * 4, sizeof(int), (size_t)std::max(np, 1)};
+    size_t o[12], bytes = 0;
+    for (int i = 0; i < 12; i++) { o[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    uint8_t* q = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&q, bytes, c->stream));
+    const void* src[] = {&F, points, keys_un, desc, uright, grid_off, grid_idx, &n_kp, taken};
+    const size_t len[] = {sizeof F, (size_t)np * sizeof(spslam_local_point), (size_t)n_kp * sizeof(spslam_keypoint),
+                          (size_t)n_kp * 32, (size_t)n_kp * 4, (kCells + 1) * 4, (size_t)grid_off[kCells] * 4,
+                          sizeof(int), taken ? (size_t)n_kp : 0};
+    for (int i = 0; i < 9; i++)
+        if (len[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], len[i], hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_search_local_points_batch_device(
+        c, 1, (const spslam_local_frame*)(q + o[0]), (const spslam_local_point*)(q + o[1]), np,
+        (const spslam_keypoint*)(q + o[2]), q + o[3], (const float*)(q + o[4]), (const int32_t*)(q + o[5]),
+        (const int32_t*)(q + o[6]), (const int*)(q + o[7]), cap, taken ? q + o[8] : nullptr, params,
+        (int32_t*)(q + o[9]), (int*)(q + o[10]), q + o[11], c->stream);
+    if (rc) { (void)hipFreeAsync(q, c->stream); return rc; }
+    if (n_kp) HIP_CHECK(c, hipMemcpyAsync(match, q + o[9], (size_t)n_kp * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[10], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    if (in_view && np) HIP_CHECK(c, hipMemcpyAsync(in_view, q + o[11], (size_t)np, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
 int spslam_set_timing(spslam_ctx* c, int enable) {
     if (!c) return SPSLAM_ERR_ARG;
     (void)hipSetDevice(c->device);

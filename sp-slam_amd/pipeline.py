@@ -178,12 +178,48 @@ class HotPath:
         self.mean_proj_points = float(np.mean([len(probs[i % U][1]) for i in range(B)]))
         self.d_match = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
         self.d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
+        # Tracking::SearchLocalPoints (TrackLocalMap): the local map = map points of the keyframe four
+        # frames back (true depth, MapPoint normal / distance range), matched after the first pose
+        # optimisation; keypoints holding a motion-model match are taken
+        kf = [self.scene.render(self.scene.pose(f[0] - 4), self.W, self.H, noise_seed=seq_id * 1000 + f[0] + 900)
+              for f in self.frames]
+        d_g = torch.from_numpy(np.stack([g for g, _, _ in kf])).cuda()
+        self.ex.extract_batch_device(d_g.data_ptr(), U, self.W * self.H, self.W, d_k.data_ptr(), d_d.data_ptr(),
+                                     d_n.data_ptr(), cap, self.stream)
+        torch.cuda.synchronize()
+        kps = d_k.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(U, cap)
+        desc, cnt = d_d.cpu().numpy(), d_n.cpu().numpy()
+        lprobs = [synth.local_problem(self.scene, self.frames[i][0] - 4, self.frames[i][0], kps[i, :cnt[i]],
+                                      desc[i, :cnt[i]], kf[i][1], rng, K=Ks) for i in range(U)]
+        loffs = np.cumsum([0] + [len(p[1]) for p in lprobs])
+        lfr = np.zeros(B, SM.LOCAL_FRAME_DTYPE)
+        for i in range(B):
+            lfr[i] = lprobs[i % U][0]
+            lfr[i]["point_offset"] = loffs[i % U]
+        self.local_probs = lprobs
+        self.local_matcher = SM.LocalMatcher(self.ex)
+        self.d_lframes, self.d_lpoints = dev(lfr), dev(np.concatenate([p[1] for p in lprobs]))
+        self.max_local_points = int(max(len(p[1]) for p in lprobs))
+        self.mean_local_points = float(np.mean([len(lprobs[i % U][1]) for i in range(B)]))
+        self.d_taken = torch.zeros((B, cap), dtype=torch.uint8, device="cuda")
+        self.d_lmatch = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+        self.d_nlmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
 
     def match(self):
         self.matcher.batch_device(self.B, self.d_pframes.data_ptr(), self.d_ppoints.data_ptr(), self.max_points,
                                   self.d_kun.data_ptr(), self.d_desc.data_ptr(), self.d_kur.data_ptr(),
                                   self.d_grid_off.data_ptr(), self.d_grid_idx.data_ptr(), self.d_cnt.data_ptr(),
                                   self.kp_cap, self.d_match.data_ptr(), self.d_nmatch.data_ptr(), stream=self.stream)
+
+    def search_local_points(self):
+        with self.torch.cuda.stream(self.main):
+            self.d_taken.copy_(self.d_match >= 0)
+        self.local_matcher.batch_device(self.B, self.d_lframes.data_ptr(), self.d_lpoints.data_ptr(),
+                                        self.max_local_points, self.d_kun.data_ptr(), self.d_desc.data_ptr(),
+                                        self.d_kur.data_ptr(), self.d_grid_off.data_ptr(),
+                                        self.d_grid_idx.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap,
+                                        self.d_taken.data_ptr(), self.d_lmatch.data_ptr(), self.d_nlmatch.data_ptr(),
+                                        stream=self.stream)
 
     def associate(self, k):
         import spslam_planes as SP
@@ -246,6 +282,7 @@ class HotPath:
         G.pose_optimize_batch_device(self.ex, self.B, A["P"].data_ptr(), A["pts"].data_ptr(), A["pls"].data_ptr(),
                                      self.d_res1.data_ptr(), A["pout"].data_ptr(), A["plout"].data_ptr(),
                                      stream=self.stream)
+        self.search_local_points()
         self.associate(1)
         G.pose_optimize_batch_device(self.ex, self.B, Bp["P"].data_ptr(), Bp["pts"].data_ptr(), Bp["pls"].data_ptr(),
                                      self.d_res2.data_ptr(), Bp["pout"].data_ptr(), Bp["plout"].data_ptr(),
@@ -347,6 +384,7 @@ class HotPath:
             pose2=self.d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE),
             assoc=self.d_assoc.cpu().numpy().reshape(2, 3, self.B, -1),
             match=self.d_match.cpu().numpy(), nmatches=self.d_nmatch.cpu().numpy(),
+            local_match=self.d_lmatch.cpu().numpy(), local_nmatches=self.d_nlmatch.cpu().numpy(),
             new_plane=self.d_newp.cpu().numpy())
 
     def _plane_field(self, name):

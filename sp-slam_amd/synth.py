@@ -475,3 +475,47 @@ def proj_problem(scene: Scene, last_fi: int, cur_fi: int, last_kps, last_desc, l
     fr["Tlw"] = np.linalg.inv(Twl).astype(np.float32).reshape(16)
     fr["n_points"] = len(P)
     return fr, P
+
+
+def local_problem(scene: Scene, kf_fi: int, cur_fi: int, kf_kps, kf_desc, kf_depth_u16, rng, K=TUM3,
+                  map_frac=0.9, flip_bits=6, rot_noise_deg=0.2, trans_noise=0.005, scale=1.2, n_levels=8):
+    """SearchLocalPoints inputs: local map points built from a nearby keyframe's
+    keypoints (true depth), with MapPoint::UpdateNormalAndDepth's normal and
+    distance range (mfMaxDistance = dist * 1.2^octave, mfMinDistance =
+    mfMaxDistance / 1.2^7), descriptors with flipped bits, and the current pose
+    after the motion-model optimisation (true pose, small error).  Returns
+    (spslam_local_frame record, spslam_local_point records)."""
+    import spslam_match as M
+    fx, fy, cx, cy = K["fx"], K["fy"], K["cx"], K["cy"]
+    Twk = scene.pose(kf_fi)
+    Tcw = np.linalg.inv(scene.pose(cur_fi))
+    ax = rng.normal(size=3)
+    ax *= np.deg2rad(rot_noise_deg) / max(np.linalg.norm(ax), 1e-12)
+    dT = np.eye(4)
+    dT[:3, :3] = _rot(ax)
+    dT[:3, 3] = rng.normal(size=3) * trans_noise
+    Tcw = dT @ Tcw
+    sf = np.float32(scale) ** np.arange(n_levels, dtype=np.float32)
+    rows = []
+    for i, kp in enumerate(kf_kps):
+        if rng.uniform() > map_frac:
+            continue
+        x, y = int(kp["x"]), int(kp["y"])
+        z = float(kf_depth_u16[y, x]) / K["depth_factor"]
+        if z <= 0:
+            continue
+        Xw = (Twk @ np.array([(kp["x"] - cx) * z / fx, (kp["y"] - cy) * z / fy, z, 1.0]))[:3]
+        PC = Xw - Twk[:3, 3]
+        dist = np.linalg.norm(PC)
+        maxd = np.float32(dist) * sf[int(kp["octave"])]
+        bits = np.unpackbits(np.array(kf_desc[i], np.uint8))
+        bits[rng.choice(256, size=flip_bits, replace=False)] ^= 1
+        rows.append((Xw, PC / dist, maxd / sf[-1], maxd, i, np.packbits(bits)))
+    P = np.zeros(len(rows), M.LOCAL_POINT_DTYPE)
+    for j, (xw, nrm, mind, maxd, i, d) in enumerate(rows):
+        P[j]["xw"], P[j]["normal"], P[j]["min_dist"], P[j]["max_dist"], P[j]["id"], P[j]["desc"] = \
+            xw, nrm, mind, maxd, i, d
+    fr = np.zeros((), M.LOCAL_FRAME_DTYPE)
+    fr["Tcw"] = Tcw.astype(np.float32).reshape(16)
+    fr["n_points"] = len(P)
+    return fr, P

@@ -63,6 +63,8 @@ int main(void) {
   S(spslam_assoc_frame) O(spslam_assoc_frame, map_offset) O(spslam_assoc_frame, n_map) S(spslam_assoc_params)
   S(spslam_proj_point) O(spslam_proj_point, angle) O(spslam_proj_point, n_obs) O(spslam_proj_point, desc)
   S(spslam_proj_frame) O(spslam_proj_frame, Tlw) O(spslam_proj_frame, point_offset) S(spslam_match_params)
+  S(spslam_local_point) O(spslam_local_point, normal) O(spslam_local_point, max_dist) O(spslam_local_point, desc)
+  S(spslam_local_frame) O(spslam_local_frame, n_points) S(spslam_local_params)
   return 0;
 }
 """
@@ -87,6 +89,7 @@ def test_struct_layouts_match_bindings(tmp_path):
         "spslam_supposed_plane": spslam_planes.SUPPOSED_DTYPE, "spslam_line_candidate": spslam_planes.LINE_CAND_DTYPE,
         "spslam_map_plane": spslam_assoc.MAP_PLANE_DTYPE, "spslam_assoc_frame": spslam_assoc.ASSOC_FRAME_DTYPE,
         "spslam_proj_point": spslam_match.PROJ_POINT_DTYPE, "spslam_proj_frame": spslam_match.PROJ_FRAME_DTYPE,
+        "spslam_local_point": spslam_match.LOCAL_POINT_DTYPE, "spslam_local_frame": spslam_match.LOCAL_FRAME_DTYPE,
     }
     for name, dt in checks.items():
         assert got[name] == dt.itemsize, (name, got[name], dt.itemsize)
@@ -99,6 +102,7 @@ def test_struct_layouts_match_bindings(tmp_path):
     assert got["spslam_plane_config"] == 6 * 8
     assert got["spslam_assoc_params"] == ctypes.sizeof(spslam_assoc.AssocParams)
     assert got["spslam_match_params"] == ctypes.sizeof(spslam_match.MatchParams)
+    assert got["spslam_local_params"] == ctypes.sizeof(spslam_match.LocalParams)
     assert got["spslam_keypoint"] == 28  # cv::KeyPoint
 
 

@@ -100,3 +100,68 @@ def test_batch_device_matches_single(gpu, pairs):
     for f, q in enumerate(pairs):
         ms, ns = m(q["fr"], q["P"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"])
         assert nb[f] == ns and np.array_equal(mb[f, :len(q["kun"])], ms), f
+
+
+@pytest.fixture(scope="module")
+def local_pairs(pairs):
+    from test_oracle_match import local_problems
+    return local_problems(pairs, seed=23)
+
+
+def test_local_points_match_oracle(gpu, local_pairs):
+    import oracle_match as OM
+    ex, M = gpu
+    for params in ((3.0, 0.8, 0.5, 0), (5.0, 0.8, 0.5, 0), (1.0, 0.6, 0.5, 0), (3.0, 0.95, 0.9, 0)):
+        lm = M.LocalMatcher(ex, params)
+        for k, q in enumerate(local_pairs):
+            for taken in (q["taken"], None):
+                mo, nmo, ivo = OM.search_local_points(q["lfr"], q["LP"], q["kun"], q["desc"], q["ur"], q["go"],
+                                                      q["gi"], q["geo"], taken=taken, params=params[:3])
+                mg, nmg, ivg = lm(q["lfr"], q["LP"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"], taken)
+                assert np.array_equal(ivg, ivo), (params, k)
+                assert nmg == nmo, (params, k, nmg, nmo)
+                assert np.array_equal(mg, mo), (params, k, np.nonzero(mg != mo)[0][:10])
+
+
+def test_local_points_batch_matches_single(gpu, local_pairs):
+    import torch
+    import spslam_gpu as G
+    ex, M = gpu
+    lm = M.LocalMatcher(ex)
+    F, cap = len(local_pairs), max(len(q["kun"]) for q in local_pairs)
+    frames = np.zeros(F, M.LOCAL_FRAME_DTYPE)
+    kun = np.zeros((F, cap), G.KEYPOINT_DTYPE)
+    desc = np.zeros((F, cap, 32), np.uint8)
+    ur = np.zeros((F, cap), np.float32)
+    go = np.zeros((F, 64 * 48 + 1), np.int32)
+    gi = np.zeros((F, cap), np.int32)
+    tk = np.zeros((F, cap), np.uint8)
+    counts = np.zeros(F, np.int32)
+    pts, off = [], 0
+    for f, q in enumerate(local_pairs):
+        n = len(q["kun"])
+        frames[f] = q["lfr"]
+        frames[f]["point_offset"] = off
+        off += len(q["LP"])
+        pts.append(q["LP"])
+        kun[f, :n], desc[f, :n], ur[f, :n], go[f] = q["kun"], q["desc"], q["ur"], q["go"]
+        gi[f, :len(q["gi"])] = q["gi"]
+        tk[f, :n] = q["taken"]
+        counts[f] = n
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
+    d = [dev(frames), dev(np.concatenate(pts)), dev(kun), dev(desc), dev(ur), dev(go), dev(gi), dev(counts), dev(tk)]
+    max_points = max(len(p) for p in pts)
+    d_match = torch.full((F * cap,), -9, dtype=torch.int32, device="cuda")
+    d_nm = torch.zeros(F, dtype=torch.int32, device="cuda")
+    d_iv = torch.zeros(off, dtype=torch.uint8, device="cuda")
+    lm.batch_device(F, d[0].data_ptr(), d[1].data_ptr(), max_points, d[2].data_ptr(), d[3].data_ptr(),
+                    d[4].data_ptr(), d[5].data_ptr(), d[6].data_ptr(), d[7].data_ptr(), cap, d[8].data_ptr(),
+                    d_match.data_ptr(), d_nm.data_ptr(), d_iv.data_ptr())
+    torch.cuda.synchronize()
+    mb, nb, ivb = d_match.cpu().numpy().reshape(F, cap), d_nm.cpu().numpy(), d_iv.cpu().numpy().astype(bool)
+    off = 0
+    for f, q in enumerate(local_pairs):
+        ms, ns, ivs = lm(q["lfr"], q["LP"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"], q["taken"])
+        assert nb[f] == ns and np.array_equal(mb[f, :len(q["kun"])], ms), f
+        assert np.array_equal(ivb[off:off + len(q["LP"])], ivs), f
+        off += len(q["LP"])

@@ -63,6 +63,12 @@ def test_projection_matching(run):
         assert int(res["nmatches"][i]) == nmo, i
         assert np.array_equal(res["match"][i, :n], mo), i
         total += nmo
+        # SearchLocalPoints after it, with the motion-model matches taken
+        lfr, LP = hp.local_probs[i % len(hp.local_probs)]
+        lo, nlo, _ = OM.search_local_points(lfr, LP, kun[i, :n], desc[i, :n], ur[i, :n], go[i], gi[i, :go[i][-1]],
+                                            geo, taken=(mo >= 0).astype(np.uint8))
+        assert int(res["local_nmatches"][i]) == nlo, i
+        assert np.array_equal(res["local_match"][i, :n], lo), i
     assert total > 0
 
 

@@ -68,3 +68,42 @@ def test_sincosf_matches_glibc(libs):
     chk.check_sincosf(t.ctypes.data, s.ctypes.data, c.ctypes.data, len(t))
     assert np.array_equal(s.view(np.uint32), _libm_vec(libm, "sinf", t.tolist()).view(np.uint32))
     assert np.array_equal(c.view(np.uint32), _libm_vec(libm, "cosf", t.tolist()).view(np.uint32))
+
+
+PREDICT_SCALE_C = r"""
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+#include <stdint.h>
+int main(void) {
+    uint32_t lo, hi; float a = 0.05f, b = 64.0f;
+    memcpy(&lo, &a, 4); memcpy(&hi, &b, 4);
+    const float lsf = logf(1.2f);
+    long bad = 0, fragile = 0;
+    for (uint32_t u = lo; u < hi; u++) {
+        float x; memcpy(&x, &u, 4);
+        const double d = log((double)x);
+        const int g = (int)ceilf(logf(x) / lsf);
+        const int c = (int)ceilf((float)d / lsf);
+        if (g != c) bad++;
+        if ((int)ceilf((float)nextafter(d, INFINITY) / lsf) != c || (int)ceilf((float)nextafter(d, -INFINITY) / lsf) != c)
+            fragile++;
+    }
+    printf("%ld %ld\n", bad, fragile);
+    return 0;
+}
+"""
+
+
+def test_predict_scale_with_rounded_log_equals_glibc_logf(tmp_path):
+    """MapPoint::PredictScale (src/MapPoint.cc:402-417) computes ceil(logf(ratio) / logf(1.2f)).
+    The GPU evaluates the log as (float)log((double)ratio): glibc's logf is not correctly rounded
+    (it differs in ~0.7% of inputs), but the resulting level is identical for every float ratio in
+    [0.05, 64) (the isInFrustum range is [1/1.2, 1.2^7/0.8]), also with a 1-ulp error in the double
+    log (the device's log is within 1 ulp)."""
+    src = tmp_path / "ps.c"
+    src.write_text(PREDICT_SCALE_C)
+    exe = tmp_path / "ps"
+    subprocess.run(["gcc", "-O2", str(src), "-o", str(exe), "-lm"], check=True)
+    bad, fragile = map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split())
+    assert bad == 0 and fragile == 0

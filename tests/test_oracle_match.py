@@ -245,3 +245,111 @@ def test_projection_expressions_match_gcc_march_native(tmp_path):
         v = _fma(_f(_f(K["fy"]) * yc), invz, K["cy"])
         assert out[0] == u and out[1] == v
         assert out[2] == _fma(-_f(K["bf"]), invz, u)
+
+
+# ---------------------------------------------------------------- SearchLocalPoints
+_libm = ctypes.CDLL("libm.so.6")
+_libm.logf.restype, _libm.logf.argtypes = ctypes.c_float, [ctypes.c_float]
+
+
+def py_search_local(fr, P, kun, desc, ur, go, gi, geo, taken, th=3.0, nn=0.8, vcl=0.5):
+    """Transcription of Frame::isInFrustum, MapPoint::PredictScale and ORBmatcher.cc:45-130."""
+    fx, fy, cx, cy, bf, minx, maxx, miny, maxy, gix, giy = [_f(v) for v in geo[:11]]
+    scale = [_f(v) for v in geo[11:]]
+    lsf = _f(_libm.logf(_f(1.2)))
+    n = len(kun)
+    match, tk = [-1] * n, [bool(t) for t in taken]
+    Tcw = fr["Tcw"].reshape(4, 4)
+    tcw = Tcw[:3, 3]
+    Ow = _mat3(Tcw, tcw, transpose=True, sign=-1.0)
+    nm = 0
+    inview = []
+    for i, p in enumerate(P):
+        Pc = _mat3(Tcw, p["xw"], c=tcw)
+        ok = False
+        if Pc[2] >= 0:
+            invz = _f(_f(1.0) / Pc[2])
+            u, v = _fma(_f(fx * Pc[0]), invz, cx), _fma(_f(fy * Pc[1]), invz, cy)
+            if minx <= u <= maxx and miny <= v <= maxy:
+                PO = [_f(p["xw"][k] - Ow[k]) for k in range(3)]
+                s = _f(PO[0] * PO[0])
+                s = _f(s + _f(PO[1] * PO[1]))
+                s = _f(s + _f(PO[2] * PO[2]))
+                dist = _f(np.sqrt(np.float64(s)))
+                if not (dist < _f(_f(0.8) * p["min_dist"]) or dist > _f(_f(1.2) * p["max_dist"])):
+                    dot = float(PO[0]) * float(p["normal"][0]) + float(PO[1]) * float(p["normal"][1])
+                    dot += float(PO[2]) * float(p["normal"][2])
+                    vc = _f(dot / float(dist))
+                    if not vc < vcl:
+                        ok = True
+                        lvl = int(np.ceil(_f(_f(_libm.logf(_f(p["max_dist"] / dist))) / lsf)))
+                        lvl = min(max(lvl, 0), 7)
+        inview.append(ok)
+        if not ok:
+            continue
+        r = _f(2.5) if vc > _f(0.998) else _f(4.0)
+        if th != 1.0:
+            r = _f(r * _f(th))
+        rs = _f(r * scale[lvl])
+        urp = _fma(-bf, invz, u)
+        x0 = max(0, int(np.floor(_f(_f(_f(u - minx) - rs) * gix))))
+        x1 = min(63, int(np.ceil(_f(_f(_f(u - minx) + rs) * gix))))
+        y0 = max(0, int(np.floor(_f(_f(_f(v - miny) - rs) * giy))))
+        y1 = min(47, int(np.ceil(_f(_f(_f(v - miny) + rs) * giy))))
+        if x0 >= 64 or x1 < 0 or y0 >= 48 or y1 < 0:
+            continue
+        bd, bl, bd2, bl2, bi = 256, -1, 256, -1, -1
+        for ix in range(x0, x1 + 1):
+            for iy in range(y0, y1 + 1):
+                c = ix * 48 + iy
+                for j in range(go[c], go[c + 1]):
+                    k = gi[j]
+                    o = kun[k]["octave"]
+                    if o < lvl - 1 or o > lvl:
+                        continue
+                    if not (abs(_f(kun[k]["x"] - u)) < rs and abs(_f(kun[k]["y"] - v)) < rs):
+                        continue
+                    if tk[k]:
+                        continue
+                    if ur[k] > 0 and abs(_f(urp - ur[k])) > rs:
+                        continue
+                    d = OM.descriptor_distance(p["desc"], desc[k])
+                    if d < bd:
+                        bd2, bl2, bd, bl, bi = bd, bl, d, o, k
+                    elif d < bd2:
+                        bd2, bl2 = d, o
+        if bd <= 100:
+            if bl == bl2 and _f(bd) > _f(_f(nn) * _f(bd2)):
+                continue
+            match[bi] = i
+            tk[bi] = True
+            nm += 1
+    return np.array(match, np.int32), nm, np.array(inview)
+
+
+def local_problems(pairs_list, seed=6):
+    """Local-map problems on the current frames of `pairs_list` (keyframe 4 frames earlier)."""
+    orb = oracle_ctypes.OrbOracle()
+    rng = np.random.default_rng(seed)
+    out = []
+    for q in pairs_list:
+        sc, c = q["sc"], q["c"]
+        gk, dk, _ = sc.render(sc.pose(c - 4), noise_seed=c + 900)
+        kk, dsk = orb.extract(gk)
+        fr, P = synth.local_problem(sc, c - 4, c, kk, dsk, dk, rng)
+        taken = (rng.uniform(size=len(q["kun"])) < 0.3).astype(np.uint8)
+        out.append(dict(q, lfr=fr, LP=P, taken=taken))
+    return out
+
+
+def test_local_oracle_matches_python_transcription(pairs):
+    for k, q in enumerate(local_problems(pairs)):
+        for taken in (q["taken"], np.zeros_like(q["taken"])):
+            mo, nmo, ivo = OM.search_local_points(q["lfr"], q["LP"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"],
+                                                  q["geo"], taken=taken)
+            mp, nmp, ivp = py_search_local(q["lfr"], q["LP"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"],
+                                           q["geo"], taken)
+            assert np.array_equal(ivo, ivp), k
+            assert nmo == nmp and np.array_equal(mo, mp), (k, nmo, nmp)
+            assert nmo > 0.3 * ivo.sum(), (nmo, ivo.sum())
+            assert not (mo[taken.astype(bool)] >= 0).any()
