@@ -92,6 +92,10 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "search_projection": n_proj * 64 + n_kp * (28 + 32 + 4 + 4 + 4) + 4 * 3073,
         # SearchLocalPoints: local map points in, the same current-frame reads, taken flags in, match out
         "search_local_points": n_local * 80 + n_kp * (28 + 32 + 4 + 4 + 1 + 4) + 4 * 3073,
+        # the three graph stages: MOTION_MODEL (match + keypoint + uR in, edge index out), DISCARD (edge index,
+        # outlier flag, match in, taken out), LOCAL_MAP (local match, edge index, keypoint, uR in); map point
+        # gathers and point / plane edges out for both graphs, problem headers
+        "track_graph_kernel": n_kp * (40 + 10 + 40) + n_pts * (12 + 32) + n_pls * 48 + 3 * 104,
         "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
 
@@ -112,56 +116,53 @@ def shard_of(rank):
 
 
 def cpu_baseline(hp, budget_s=12.0):
-    """CPU restatement (oracle) of the same per-frame work, one core, bounded sample."""
+    """CPU restatement (oracle) of the same per-frame work, one core, bounded sample.  Also returns the
+    oracle's local-map pose of each distinct frame (the CPU reference trajectory of the ATE)."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    import numpy as np
     import oracle_ctypes
     import oracle_planes
     import oracle_lba
-    import oracle_supposed
-    import oracle_assoc
-    import oracle_frame
-    import oracle_match
+    import oracle_step
     orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     po = oracle_planes.PlaneOracle()
-    n = 0
     U = len(hp.frames)
-    depth_f = [f[2].astype(np.float32) * np.float32(np.float32(1.0) / np.float32(5000.0)) for f in hp.frames]
-    b, gin = hp.fs.bounds, hp.fs.grid_inv
-    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, 40.0, *b, *gin], hp.ex.tables()["scale"]]).astype(np.float32)
+    inputs = [oracle_step.from_hotpath(hp, i) for i in range(U)]
+    poses = {}
+    n = 0
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s:
+    while time.perf_counter() - t0 < budget_s or len(poses) < U:
         i = n % U
-        ko, do = orb.extract(hp.frames[i][1], cap=20000)
-        r = po.extract(depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy)
-        so = oracle_supposed.generate(depth_f[i], po.cloud(), r["coef"], r["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
-        fo = oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), depth_f[i], hp.fx, hp.fy, hp.cx, hp.cy,
-                                     bf=40.0)
-        kun = ko.copy()
-        kun["x"], kun["y"] = fo["un"][:, 0], fo["un"][:, 1]
-        fr, P = hp.match_probs[i % len(hp.match_probs)]
-        mo, _, _ = oracle_match.search_by_projection(fr, P, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"],
-                                                     geo)
-        coefs = np.concatenate([np.asarray(r["coef"], np.float32).reshape(-1, 4),
-                                np.asarray(so["coef"], np.float32).reshape(-1, 4)])
-        pa, pts, pls, _ = hp.probA[i]
-        oracle_assoc.associate(pa["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
-        r1, _, _ = oracle_ctypes.pose_optimize(pa, pts, pls)
-        lfr, LP = hp.local_probs[i % len(hp.local_probs)]
-        oracle_match.search_local_points(lfr, LP, kun, do, fo["uright"], fo["grid_off"], fo["grid_idx"], geo,
-                                         taken=(mo >= 0).astype(np.uint8))
-        oracle_assoc.associate(r1["Tcw"].reshape(4, 4), coefs, hp.assoc_map, hp.assoc_boundary)
-        pb, pts2, pls2, _ = hp.probB[i]
-        pb = pb.copy()
-        pb["Tcw"] = r1["Tcw"]
-        oracle_ctypes.pose_optimize(pb, pts2, pls2)
+        o = oracle_step.run(inputs[i], orb, po, supp_cap=hp.pe.supp_cap)
+        poses.setdefault(i, o["pose2"][0]["Tcw"].copy())
         if hp.n_lba and n % hp.lba_every == 0:  # LocalMapping: one local BA per keyframe
             oracle_lba.lba_optimize(*hp.lba_problems[(n // hp.lba_every) % len(hp.lba_problems)][:6])
         n += 1
     dt = time.perf_counter() - t0
+    lba = f" + LocalBundleAdjustment every {hp.lba_every} frames" if hp.n_lba else ""
     return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
                 sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + PoseOptimization) + SearchLocalPoints{' + LocalBundleAdjustment every %d frames' % hp.lba_every if hp.n_lba else ''}), {dt:.1f}s on one core, oracle/liboracle.so -O3 x86-64-v3")
+                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + graph + "
+                       f"PoseOptimization) + SearchLocalPoints{lba}), {dt:.1f}s on one core, "
+                       f"oracle/liboracle.so -O3 x86-64-v3"), poses
+
+
+def ate_report(hp, res, cpu_poses=None):
+    """ATE (TUM evaluate_ate: Horn alignment + RMSE of camera centres, sp-slam_amd/trajectory.py) of the
+    step's local-map poses over the distinct frames: against the CPU reference's poses on the same
+    inputs, and against the synthetic ground truth."""
+    import numpy as np
+    import trajectory
+    U = len(hp.frames)
+    gpu = [trajectory.camera_center(res["pose2"][i]["Tcw"]) for i in range(U)]
+    gt = [hp.scene.pose(hp.frames[i][0])[:3, 3] for i in range(U)]
+    out = {"frames": U, "vs_ground_truth_m": trajectory.ate_rmse(gpu, gt), "vs_cpu_ref_m": None,
+           "max_center_diff_vs_cpu_ref_m": None}
+    if cpu_poses is not None:
+        cpu = [trajectory.camera_center(cpu_poses[i]) for i in range(U)]
+        out["vs_cpu_ref_m"] = trajectory.ate_rmse(gpu, cpu)
+        d = np.linalg.norm(np.array(gpu, np.float64) - np.array(cpu, np.float64), axis=1)
+        out["max_center_diff_vs_cpu_ref_m"] = float(d.max())
+    return out
 
 
 def main():
@@ -212,8 +213,9 @@ def main():
     value = frames / elapsed
     total_kernel_ms = sum(v[0] for v in times.values())
     dom, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
-    n_pts = (hp.dA["n_points"] + hp.dB["n_points"]) / args.batch
-    n_pls = (hp.dA["n_planes"] + hp.dB["n_planes"]) / args.batch
+    P1, P2 = hp.graph(0)[0], hp.graph(1)[0]
+    n_pts = float((P1["n_points"].sum() + P2["n_points"].sum()) / args.batch)
+    n_pls = float((P1["n_planes"].sum() + P2["n_planes"].sum()) / args.batch)
     n_con = float(res["contour_points"].mean())
     n_sup = float(res["supposed_counts"].mean())
     n_brd = float(res["line_points"].mean())
@@ -246,8 +248,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8+f32+f64",
-        "data": "synthetic (in-repo textured-room RGB-D renderer sp-slam_amd/synth.py; pose correspondences "
-                "synthesized from scene ground truth)",
+        "data": "synthetic (in-repo textured-room RGB-D renderer sp-slam_amd/synth.py; map points / map planes "
+                "synthesized from the scene, every correspondence from the step's own matching + association)",
         "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": args.batch,
                    "parallelism": f"shard{world}", "mean_keypoints": hp.mean_keypoints,
                    "mean_planes": float(res["plane_counts"].mean()),
@@ -260,8 +262,11 @@ def main():
                      "share_of_kernel_time": dom_ms / max(total_kernel_ms, 1e-9)},
         "cpu_baseline": None,
     }
+    cpu_poses = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(hp)
+        result["cpu_baseline"], cpu_poses = cpu_baseline(hp)
+    if rank == 0:
+        result["ate"] = ate_report(hp, res, cpu_poses)
     if rank == 0:
         print(json.dumps(result), flush=True)
     hp.close()

@@ -638,6 +638,83 @@ int spslam_search_local_points_batch_device(spslam_ctx* ctx, int n_frames, const
                                             const uint8_t* d_taken, const spslam_local_params* params,
                                             int32_t* d_match, int* d_nmatches, uint8_t* d_in_view, void* hip_stream);
 
+/* ---------------------------------------------------------------- tracking graph glue
+ * The Tracking-side bookkeeping between matching / plane association and
+ * PoseOptimization, on the device, for a batch of frames (one stage per call):
+ *
+ * SPSLAM_TRACK_MOTION_MODEL -- TrackWithMotionModel's graph (src/Tracking.cc:
+ *   951-981): mvpMapPoints[i] = the SearchByProjection match of keypoint i,
+ *   mvpMapPlanes / mvpParallelPlanes / mvpVerticalPlanes = the first
+ *   AssociatePlanesByBoundary; then Optimizer::PoseOptimization's edge loops
+ *   (src/Optimizer.cc:561-640: one point edge per keypoint with a map point, in
+ *   keypoint order, stereo iff mvuRight >= 0, information mvInvLevelSigma2
+ *   [octave]; :681-860: plane edges over the frame planes in index order, then
+ *   parallel, then vertical).  The initial pose is the motion-model prediction
+ *   (proj_frames[f].Tcw).  edge_of_kp[i] receives keypoint i's edge index.
+ * SPSLAM_TRACK_DISCARD -- the outlier discard after that PoseOptimization
+ *   (src/Tracking.cc:986-1000: mvpMapPoints[i] = NULL where mvbOutlier[i]) and
+ *   the SearchLocalPoints preconditions: taken[i] = keypoint i keeps a map point
+ *   with Observations() > 0 (src/ORBmatcher.cc:95-97); the optimized pose is
+ *   written into local_frames[f].Tcw and, if given, assoc_frames_next[f].Tcw
+ *   (the second association runs at that pose, src/Tracking.cc:1066).
+ * SPSLAM_TRACK_LOCAL_MAP -- TrackLocalMap's graph (src/Tracking.cc:1062-1068):
+ *   mvpMapPoints = the surviving motion-model points, replaced by the
+ *   SearchLocalPoints match where it assigned one (it may re-assign a keypoint
+ *   whose point has no observations, src/ORBmatcher.cc:115); planes from the
+ *   second association; initial pose = the motion-model result.
+ *
+ * Layouts: current frame f's keypoints / mvuRight / matches / taken /
+ * edge_of_kp at f * cap (ORB and frame-stage batch layout); match indices are
+ * relative to the frame's proj / local point_offset; plane association outputs
+ * at f * (cap_a + cap_b) + i (spslam_planes_associate_batch_device layout) are
+ * global map-plane indices.  The graphs are written with point_offset = f * cap
+ * and plane_offset = f * 3 * (cap_a + cap_b), so the PoseOptimization outlier
+ * flags of frame f are at the same offsets.  The Tracking state machine
+ * (nmatches < 10 -> TrackReferenceKeyFrame, relocalisation) is the caller's. */
+#define SPSLAM_TRACK_MOTION_MODEL 0
+#define SPSLAM_TRACK_DISCARD 1
+#define SPSLAM_TRACK_LOCAL_MAP 2
+
+typedef struct spslam_track_batch {
+    /* current frames */
+    const spslam_keypoint* keys_un;  /* mvKeysUn */
+    const float* uright;             /* mvuRight */
+    const int* kp_counts;
+    int32_t cap;
+    /* motion model: last-frame map points and the SearchByProjection matches */
+    const spslam_proj_frame* proj_frames;
+    const spslam_proj_point* proj_points;
+    const int32_t* proj_match;
+    /* local map: SearchLocalPoints inputs / matches */
+    spslam_local_frame* local_frames;     /* DISCARD writes Tcw */
+    const spslam_local_point* local_points;
+    const int32_t* local_match;           /* LOCAL_MAP */
+    uint8_t* taken;                       /* DISCARD writes */
+    /* frame planes (extracted, then supposed) and their association */
+    const void* planes_a;
+    const void* planes_b;
+    const int* count_a;
+    const int* count_b;
+    int32_t stride_a, stride_b, cap_a, cap_b;
+    const spslam_map_plane* map;
+    const int32_t* assoc_match;
+    const int32_t* assoc_parallel;
+    const int32_t* assoc_vertical;
+    spslam_assoc_frame* assoc_frames_next;  /* DISCARD writes Tcw (may be NULL) */
+    /* PoseOptimization graphs */
+    spslam_pose_problem* problems;
+    spslam_point_obs* points;             /* f * cap */
+    spslam_plane_obs* planes;             /* f * 3 * (cap_a + cap_b) */
+    int32_t* edge_of_kp;                  /* MOTION_MODEL writes, DISCARD / LOCAL_MAP read */
+    const spslam_pose_result* results;    /* the motion-model PoseOptimization (DISCARD, LOCAL_MAP) */
+    const uint8_t* point_outlier;         /* its point outlier flags (DISCARD, LOCAL_MAP) */
+    float fx, fy, cx, cy, bf;
+    int32_t pad;
+} spslam_track_batch;
+
+int spslam_track_graph_batch_device(spslam_ctx* ctx, int n_frames, int stage, const spslam_track_batch* batch,
+                                    void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

@@ -24,6 +24,7 @@
 #include "lba_launch.h"
 #include "assoc_launch.h"
 #include "match_launch.h"
+#include "track_launch.h"
 
 using namespace spslam;
 
@@ -1195,6 +1196,38 @@ int spslam_search_by_projection(spslam_ctx* c, const spslam_proj_frame* frame, c
     HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[9], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipFreeAsync(q, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
+int spslam_track_graph_batch_device(spslam_ctx* c, int n_frames, int stage, const spslam_track_batch* batch,
+                                    void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !batch || stage < SPSLAM_TRACK_MOTION_MODEL || stage > SPSLAM_TRACK_LOCAL_MAP)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_track_graph_batch_device");
+    const spslam_track_batch& b = *batch;
+    const bool common = b.kp_counts && b.cap >= 1 && b.cap <= (1 << 20) && b.proj_frames && b.proj_match &&
+                        b.proj_points && b.edge_of_kp;
+    bool ok = common;
+    if (stage == SPSLAM_TRACK_DISCARD) {
+        ok = ok && b.taken && b.local_frames && b.results && b.point_outlier;
+    } else {
+        ok = ok && b.keys_un && b.uright && b.problems && b.points && b.cap_a >= 0 && b.cap_b >= 0 &&
+             (b.cap_a == 0 || (b.planes_a && b.count_a && b.stride_a >= 16)) &&
+             (b.cap_b == 0 || (b.planes_b && b.count_b && b.stride_b >= 16)) &&
+             (b.cap_a + b.cap_b == 0 || (b.planes && b.map && b.assoc_match && b.assoc_parallel && b.assoc_vertical));
+        if (stage == SPSLAM_TRACK_LOCAL_MAP)
+            ok = ok && b.local_frames && b.local_points && b.local_match && b.results && b.point_outlier;
+    }
+    static const char* names[3] = {"MOTION_MODEL", "DISCARD", "LOCAL_MAP"};
+    if (!ok) return fail(c, SPSLAM_ERR_ARG, "missing buffer for stage %s of spslam_track_graph_batch_device",
+                         names[stage]);
+    HIP_CHECK(c, hipSetDevice(c->device));
+    TrackArgs a{};
+    a.b = b;
+    if (b.cap_b == 0) a.b.count_b = nullptr;
+    for (int l = 0; l < kMaxLevels; l++)
+        a.inv_sigma2[l] = c->inv_sigma2[std::min<int>(l, (int)c->inv_sigma2.size() - 1)];
+    HIP_CHECK(c, track_launch(n_frames, stage, a, (hipStream_t)hip_stream, c->timer));
     return SPSLAM_OK;
 }
 

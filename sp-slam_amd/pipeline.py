@@ -1,23 +1,32 @@
 """Batched per-frame tracking hot path on one GPU (the throughput step of bench.py).
 
-One step = for each of B frames resident in HBM (gray u8 + depth f32):
-  ORBextractor::operator()                      (spslam_orb_extract_batch_device)
-  Frame::ComputePlanesFromOrganizedPointCloud   (spslam_planes_extract_batch_device)
-  Frame::GeneratePlanesFromBoundries            (spslam_planes_generate_from_boundaries_batch_device)
+One step = for each of B frames resident in HBM (gray u8 + depth f32), the
+sequence Tracking::Track runs per RGB-D frame (src/Tracking.cc:233-1080):
+  ORBextractor::operator()                      spslam_orb_extract_batch_device
+  Frame::ComputePlanesFromOrganizedPointCloud   spslam_planes_extract_batch_device
+  Frame::GeneratePlanesFromBoundries            spslam_planes_generate_from_boundaries_batch_device
   Frame::UndistortKeyPoints / ComputeStereoFromRGBD / AssignFeaturesToGrid
-                                                (spslam_frame_rgbd_batch_device)
-  Optimizer::PoseOptimization, motion model     (spslam_pose_optimize_batch_device)
-  Optimizer::PoseOptimization, local map,       (same, chained on the device from
-      starting from the motion-model pose        the first call's results)
-mirroring Tracking::Track's per-frame sequence (src/Tracking.cc:233, 982, 1061).
+                                                spslam_frame_rgbd_batch_device
+  TrackWithMotionModel:
+    ORBmatcher::SearchByProjection(Cur, Last)   spslam_search_by_projection_batch_device
+    Map::AssociatePlanesByBoundary              spslam_planes_associate_batch_device
+    graph from the matches                      spslam_track_graph_batch_device (MOTION_MODEL)
+    Optimizer::PoseOptimization                 spslam_pose_optimize_batch_device
+    outlier discard                             spslam_track_graph_batch_device (DISCARD)
+  TrackLocalMap:
+    SearchLocalPoints                           spslam_search_local_points_batch_device
+    Map::AssociatePlanesByBoundary              (at the optimized pose)
+    graph                                       spslam_track_graph_batch_device (LOCAL_MAP)
+    Optimizer::PoseOptimization                 spslam_pose_optimize_batch_device
 
-The correspondences PoseOptimization consumes come from ORBmatcher /
-Map::AssociatePlanesByBoundary in the reference (outside this path,
-SURVEY.md 8(f)); here they are synthesized once per frame from the scene
-ground truth and the frame's own keypoints (synth.pose_problem) and kept in
-HBM.  ORB and plane extraction run on two HIP streams (independent inputs),
-joined before PoseOptimization; nothing returns to the host inside
-a step.
+The map the frames track against is synthesized once per sequence from the
+scene (sp-slam_amd/synth.py): the last frame's map points (its keypoints
+back-projected with the true depth and pose), a keyframe's local map points,
+and the map planes with boundary clouds.  Every correspondence PoseOptimization
+consumes is produced inside the step by the path's own matching and plane
+association.  ORB and plane extraction run on two HIP streams (independent
+inputs), joined before the frame steps; nothing returns to the host inside a
+step.
 """
 from __future__ import annotations
 
@@ -38,6 +47,7 @@ class HotPath:
         self.device = device
         s = width / 640.0
         self.fx, self.fy, self.cx, self.cy = K["fx"] * s, K["fy"] * s, K["cx"] * s, K["cy"] * s
+        self.bf = K["bf"]
         self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
         self.ex = G.OrbExtractor(nfeatures=nfeatures, width=width, height=height, max_batch=B, device=device)
         self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height)
@@ -85,29 +95,15 @@ class HotPath:
         self.side_stream = self.side.cuda_stream
         self.ev_fork = torch.cuda.Event()
         self.ev_join = torch.cuda.Event()
-        # --- pose problems: run one ORB pass to get each unique frame's keypoints
+        # --- one ORB pass for the map-point generators (they back-project the frames' own keypoints)
         self.orb()
         torch.cuda.synchronize()
-        kps = self.d_kps.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(B, cap)
         cnts = self.d_cnt.cpu().numpy()
-        invs2 = self.ex.tables()["inv_sigma2"]
-        probA, probB = [], []
-        for i in range(U):
-            fi, g, d, fid = self.frames[i]
-            k = kps[i, :cnts[i]]
-            rng = np.random.default_rng(seq_id * 7919 + i)
-            probA.append(synth.pose_problem(self.scene, fi, k, d, fid, invs2, rng, K=K, match_frac=0.6))
-            probB.append(synth.pose_problem(self.scene, fi, k, d, fid, invs2, rng, K=K, match_frac=0.85,
-                                            rot_noise_deg=0.3, trans_noise=0.01))
-        self.probA = [probA[i % U] for i in range(B)]
-        self.probB = [probB[i % U] for i in range(B)]
-        self.dA = self._upload(self.probA)
-        self.dB = self._upload(self.probB)
-        self.d_res1 = torch.zeros(B * G.POSE_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-        self.d_res2 = torch.zeros_like(self.d_res1)
+        self.inv_sigma2 = self.ex.tables()["inv_sigma2"]
         self.mean_keypoints = float(cnts.mean())
-        self._setup_assoc(seq_id)
         self._setup_match(seq_id)
+        self._setup_assoc(seq_id)
+        self._setup_track()
         # --- LocalBundleAdjustment (C3): one local map per `lba_every` frames (a keyframe), run on the
         #     LocalMapping stream beside tracking like the reference's LocalMapping thread
         self.n_lba = B // lba_every if lba_every else 0
@@ -120,7 +116,7 @@ class HotPath:
         """Map::AssociatePlanesByBoundary before each PoseOptimization (TrackWithMotionModel,
         TrackLocalMap): the frame's extracted + supposed planes against the sequence's map planes
         (the scene faces with boundary clouds).  The first call uses the motion-model pose, the
-        second the pose after the first optimisation (copied on the device)."""
+        second the pose after the first optimisation (written by the DISCARD graph stage)."""
         import spslam_assoc as SA
         torch, B = self.torch, self.B
         rng = np.random.default_rng(seq_id * 31 + 7)
@@ -129,8 +125,8 @@ class HotPath:
         for k, v in mp.items():
             m[k] = v
         fr = np.zeros(B, SA.ASSOC_FRAME_DTYPE)
-        for i in range(B):
-            fr[i]["Tcw"] = self.probA[i][0]["Tcw"]
+        for i in range(B):  # the first association runs at the motion-model prediction (Tracking.cc:958, 979)
+            fr[i]["Tcw"] = self.match_probs[i % len(self.match_probs)][0]["Tcw"]
         fr["map_offset"], fr["n_map"] = 0, len(m)
         dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
         self.assoc = SA.PlaneAssociator(self.ex)
@@ -212,8 +208,7 @@ class HotPath:
                                   self.kp_cap, self.d_match.data_ptr(), self.d_nmatch.data_ptr(), stream=self.stream)
 
     def search_local_points(self):
-        with self.torch.cuda.stream(self.main):
-            self.d_taken.copy_(self.d_match >= 0)
+        # taken flags and the local frames' pose come from the DISCARD graph stage
         self.local_matcher.batch_device(self.B, self.d_lframes.data_ptr(), self.d_lpoints.data_ptr(),
                                         self.max_local_points, self.d_kun.data_ptr(), self.d_desc.data_ptr(),
                                         self.d_kur.data_ptr(), self.d_grid_off.data_ptr(),
@@ -224,10 +219,6 @@ class HotPath:
     def associate(self, k):
         import spslam_planes as SP
         d_fr = self.d_afr1 if k == 0 else self.d_afr2
-        if k == 1:  # the second association sees the pose after the first PoseOptimization
-            f32 = self.torch.float32
-            with self.torch.cuda.stream(self.main):
-                d_fr.view(f32).view(self.B, 20)[:, :16].copy_(self.d_res1.view(f32).view(self.B, 20)[:, :16])
         o = self.d_assoc[k]
         self.assoc.batch_device(self.B, d_fr.data_ptr(), self.d_planes.data_ptr(), SP.PLANE_DTYPE.itemsize,
                                 self.d_pcnt.data_ptr(), self.pe.planes_cap, self.d_supp.data_ptr(),
@@ -235,25 +226,45 @@ class HotPath:
                                 self.d_map.data_ptr(), self.d_bound.data_ptr(), self.n_map, o[0].data_ptr(),
                                 o[1].data_ptr(), o[2].data_ptr(), self.d_newp[k].data_ptr(), stream=self.stream)
 
-    def _upload(self, probs):
-        torch = self.torch
-        n = len(probs)
-        P = np.zeros(n, G.POSE_PROBLEM_DTYPE)
-        pts, pls = [], []
-        po = pl = 0
-        for i, (prob, p, q, _) in enumerate(probs):
-            P[i] = prob
-            P[i]["point_offset"], P[i]["plane_offset"] = po, pl
-            po += len(p)
-            pl += len(q)
-            pts.append(p)
-            pls.append(q)
-        pts = np.concatenate(pts)
-        pls = np.concatenate(pls) if pl else np.zeros(1, G.PLANE_OBS_DTYPE)
-        dev = lambda a: torch.from_numpy(a.view(np.uint8).copy()).cuda()
-        return dict(P=dev(P), pts=dev(pts), pls=dev(pls),
-                    pout=torch.zeros(max(po, 1), dtype=torch.uint8, device="cuda"),
-                    plout=torch.zeros(max(pl, 1), dtype=torch.uint8, device="cuda"), n_points=po, n_planes=pl)
+    def _setup_track(self):
+        """Device buffers of the two PoseOptimization graphs (spslam_track_graph_batch_device): point
+        edges at f * cap, plane edges at f * 3 * (planes_cap + supp_cap), outlier flags alike."""
+        import spslam_track as ST
+        torch, B, cap = self.torch, self.B, self.kp_cap
+        self.plane_edge_cap = 3 * (self.pe.planes_cap + self.pe.supp_cap)
+        self.track = ST.TrackGraph(self.ex)
+        u8 = dict(dtype=torch.uint8, device="cuda")
+        self.graphs = []
+        for _ in range(2):  # motion model, local map
+            self.graphs.append(dict(
+                P=torch.zeros(B * G.POSE_PROBLEM_DTYPE.itemsize, **u8),
+                pts=torch.zeros(B * cap * G.POINT_OBS_DTYPE.itemsize, **u8),
+                pls=torch.zeros(B * self.plane_edge_cap * G.PLANE_OBS_DTYPE.itemsize, **u8),
+                pout=torch.zeros(B * cap, **u8), plout=torch.zeros(B * self.plane_edge_cap, **u8)))
+        self.d_edge = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+        self.d_res1 = torch.zeros(B * G.POSE_RESULT_DTYPE.itemsize, **u8)
+        self.d_res2 = torch.zeros_like(self.d_res1)
+
+    def _track_batch(self, k):
+        """spslam_track_batch for graph k (0 = motion model, 1 = local map) on the current buffers."""
+        import spslam_planes as SP
+        import spslam_track as ST
+        g = self.graphs[k]
+        a = self.d_assoc[k]
+        return ST.TrackBatch(
+            keys_un=self.d_kun.data_ptr(), uright=self.d_kur.data_ptr(), kp_counts=self.d_cnt.data_ptr(),
+            cap=self.kp_cap, proj_frames=self.d_pframes.data_ptr(), proj_points=self.d_ppoints.data_ptr(),
+            proj_match=self.d_match.data_ptr(), local_frames=self.d_lframes.data_ptr(),
+            local_points=self.d_lpoints.data_ptr(), local_match=self.d_lmatch.data_ptr(),
+            taken=self.d_taken.data_ptr(), planes_a=self.d_planes.data_ptr(), planes_b=self.d_supp.data_ptr(),
+            count_a=self.d_pcnt.data_ptr(), count_b=self.d_scnt.data_ptr(), stride_a=SP.PLANE_DTYPE.itemsize,
+            stride_b=SP.SUPPOSED_DTYPE.itemsize, cap_a=self.pe.planes_cap, cap_b=self.pe.supp_cap,
+            map=self.d_map.data_ptr(), assoc_match=a[0].data_ptr(), assoc_parallel=a[1].data_ptr(),
+            assoc_vertical=a[2].data_ptr(), assoc_frames_next=self.d_afr2.data_ptr(),
+            problems=g["P"].data_ptr(), points=g["pts"].data_ptr(), planes=g["pls"].data_ptr(),
+            edge_of_kp=self.d_edge.data_ptr(), results=self.d_res1.data_ptr(),
+            point_outlier=self.graphs[0]["pout"].data_ptr(), fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy,
+            bf=self.bf)
 
     # --- stages
     def orb(self):
@@ -277,16 +288,35 @@ class HotPath:
                              self.d_pcnt.data_ptr(), self.d_scnt.data_ptr(), self.stream)
 
     def pose(self):
-        A, Bp = self.dA, self.dB
+        """TrackWithMotionModel then TrackLocalMap (src/Tracking.cc:951-1068) from the matches on."""
+        import spslam_track as ST
+        g1, g2 = self.graphs
         self.associate(0)
-        G.pose_optimize_batch_device(self.ex, self.B, A["P"].data_ptr(), A["pts"].data_ptr(), A["pls"].data_ptr(),
-                                     self.d_res1.data_ptr(), A["pout"].data_ptr(), A["plout"].data_ptr(),
-                                     stream=self.stream)
+        self.track.batch_device(self.B, ST.MOTION_MODEL, self._track_batch(0), stream=self.stream)
+        G.pose_optimize_batch_device(self.ex, self.B, g1["P"].data_ptr(), g1["pts"].data_ptr(),
+                                     g1["pls"].data_ptr(), self.d_res1.data_ptr(), g1["pout"].data_ptr(),
+                                     g1["plout"].data_ptr(), stream=self.stream)
+        self.track.batch_device(self.B, ST.DISCARD, self._track_batch(0), stream=self.stream)
         self.search_local_points()
         self.associate(1)
-        G.pose_optimize_batch_device(self.ex, self.B, Bp["P"].data_ptr(), Bp["pts"].data_ptr(), Bp["pls"].data_ptr(),
-                                     self.d_res2.data_ptr(), Bp["pout"].data_ptr(), Bp["plout"].data_ptr(),
-                                     init_from_ptr=self.d_res1.data_ptr(), stream=self.stream)
+        self.track.batch_device(self.B, ST.LOCAL_MAP, self._track_batch(1), stream=self.stream)
+        G.pose_optimize_batch_device(self.ex, self.B, g2["P"].data_ptr(), g2["pts"].data_ptr(),
+                                     g2["pls"].data_ptr(), self.d_res2.data_ptr(), g2["pout"].data_ptr(),
+                                     g2["plout"].data_ptr(), stream=self.stream)
+
+    def graph(self, k):
+        """Host copy of PoseOptimization graph k: (problems, [points per frame], [planes per frame],
+        point outlier flags per frame, plane outlier flags per frame)."""
+        g = self.graphs[k]
+        P = g["P"].cpu().numpy().view(G.POSE_PROBLEM_DTYPE)
+        pts = g["pts"].cpu().numpy().view(G.POINT_OBS_DTYPE)
+        pls = g["pls"].cpu().numpy().view(G.PLANE_OBS_DTYPE)
+        po, plo = g["pout"].cpu().numpy(), g["plout"].cpu().numpy()
+        sl = lambda a, o, n: a[o:o + n]  # noqa: E731
+        return (P, [sl(pts, p["point_offset"], p["n_points"]) for p in P],
+                [sl(pls, p["plane_offset"], p["n_planes"]) for p in P],
+                [sl(po, p["point_offset"], p["n_points"]).astype(bool) for p in P],
+                [sl(plo, p["plane_offset"], p["n_planes"]).astype(bool) for p in P])
 
     def _setup_lba(self, seq_id, unique, n_points):
         import spslam_lba as L

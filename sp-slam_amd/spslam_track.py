@@ -1,0 +1,47 @@
+"""ctypes binding of the tracking-graph part of include/spslam_gpu.h
+(spslam_track_graph_batch_device: TrackWithMotionModel / TrackLocalMap's
+bookkeeping between matching and Optimizer::PoseOptimization,
+src/Tracking.cc:951-1000, 1055-1068; src/Optimizer.cc:561-640, 681-860)."""
+from __future__ import annotations
+
+import ctypes
+
+import spslam_gpu
+
+MOTION_MODEL, DISCARD, LOCAL_MAP = 0, 1, 2
+
+spslam_gpu.EXPORTED += ["spslam_track_graph_batch_device"]
+
+_P = ctypes.c_void_p
+
+
+class TrackBatch(ctypes.Structure):
+    """struct spslam_track_batch (device pointers as ints)."""
+    _fields_ = [("keys_un", _P), ("uright", _P), ("kp_counts", _P), ("cap", ctypes.c_int32),
+                ("proj_frames", _P), ("proj_points", _P), ("proj_match", _P),
+                ("local_frames", _P), ("local_points", _P), ("local_match", _P), ("taken", _P),
+                ("planes_a", _P), ("planes_b", _P), ("count_a", _P), ("count_b", _P),
+                ("stride_a", ctypes.c_int32), ("stride_b", ctypes.c_int32), ("cap_a", ctypes.c_int32),
+                ("cap_b", ctypes.c_int32),
+                ("map", _P), ("assoc_match", _P), ("assoc_parallel", _P), ("assoc_vertical", _P),
+                ("assoc_frames_next", _P),
+                ("problems", _P), ("points", _P), ("planes", _P), ("edge_of_kp", _P), ("results", _P),
+                ("point_outlier", _P),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("bf", ctypes.c_float), ("pad", ctypes.c_int32)]
+
+
+def _bind(lib):
+    lib.spslam_track_graph_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P]
+
+
+class TrackGraph:
+    """GPU tracking-graph bookkeeping on a context (its ORB tables give mvInvLevelSigma2)."""
+
+    def __init__(self, ex: spslam_gpu.OrbExtractor):
+        self.ex = ex
+        _bind(ex.lib)
+
+    def batch_device(self, n_frames: int, stage: int, batch: TrackBatch, stream=0):
+        self.ex._check(self.ex.lib.spslam_track_graph_batch_device(self.ex.ctx, n_frames, stage,
+                                                                    ctypes.byref(batch), stream or None))

@@ -22,7 +22,10 @@ def declared_functions():
 
 
 def test_library_exports_every_declared_symbol():
+    import spslam_assoc  # noqa: F401  (each binding module registers its entry points)
     import spslam_gpu
+    import spslam_match  # noqa: F401
+    import spslam_track  # noqa: F401
     lib = spslam_gpu.load_library()
     names = declared_functions()
     assert len(names) >= 19, names
@@ -65,6 +68,9 @@ int main(void) {
   S(spslam_proj_frame) O(spslam_proj_frame, Tlw) O(spslam_proj_frame, point_offset) S(spslam_match_params)
   S(spslam_local_point) O(spslam_local_point, normal) O(spslam_local_point, max_dist) O(spslam_local_point, desc)
   S(spslam_local_frame) O(spslam_local_frame, n_points) S(spslam_local_params)
+  S(spslam_track_batch) O(spslam_track_batch, cap) O(spslam_track_batch, proj_frames)
+  O(spslam_track_batch, stride_a) O(spslam_track_batch, cap_b) O(spslam_track_batch, map)
+  O(spslam_track_batch, point_outlier) O(spslam_track_batch, fx) O(spslam_track_batch, bf)
   return 0;
 }
 """
@@ -104,6 +110,12 @@ def test_struct_layouts_match_bindings(tmp_path):
     assert got["spslam_match_params"] == ctypes.sizeof(spslam_match.MatchParams)
     assert got["spslam_local_params"] == ctypes.sizeof(spslam_match.LocalParams)
     assert got["spslam_keypoint"] == 28  # cv::KeyPoint
+    import spslam_track
+    tb = spslam_track.TrackBatch
+    assert got["spslam_track_batch"] == ctypes.sizeof(tb)
+    for key, off in got.items():
+        if key.startswith("spslam_track_batch."):
+            assert getattr(tb, key.split(".", 1)[1]).offset == off, key
 
 
 def test_fails_loudly_without_gpu():

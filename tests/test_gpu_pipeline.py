@@ -3,9 +3,11 @@ the path bench.py times): one step over a small batch, every stage's output
 checked against the CPU oracle on the same inputs --
 ORBextractor::operator() (bit-exact keypoints + descriptors), the RGB-D Frame
 steps (bit-exact), ComputePlanesFromOrganizedPointCloud + GeneratePlanesFromBoundries
-(bit-exact coefficients), AssociatePlanesByBoundary before each PoseOptimization
-(identical indices; the second call with the first optimisation's pose), and
-the two PoseOptimization calls (pose within 1e-4, identical outlier flags)."""
+(bit-exact coefficients), then the tracking chain: SearchByProjection,
+AssociatePlanesByBoundary, the motion-model PoseOptimization graph built from
+those matches (bit-identical edges), PoseOptimization (pose within 1e-4,
+identical outlier flags), the outlier discard, SearchLocalPoints, the second
+association and local-map graph, and the second PoseOptimization."""
 import numpy as np
 import pytest
 
@@ -44,34 +46,6 @@ def test_orb_and_frame_stage(run):
         assert np.array_equal(kdep[i, :n], fo["depth"]), i
 
 
-def test_projection_matching(run):
-    import oracle_match as OM
-    import spslam_gpu as G
-    hp, res = run
-    t = hp.ex.tables()
-    kun = hp.d_kun.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(hp.B, hp.kp_cap)
-    desc = hp.d_desc.cpu().numpy()
-    ur = hp.d_kur.cpu().numpy()
-    go, gi = hp.d_grid_off.cpu().numpy(), hp.d_grid_idx.cpu().numpy()
-    b, ginv = hp.fs.bounds, hp.fs.grid_inv
-    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, 40.0, *b, *ginv], t["scale"]]).astype(np.float32)
-    total = 0
-    for i in range(hp.B):
-        n = int(res["kp_counts"][i])
-        fr, P = hp.match_probs[i % len(hp.match_probs)]
-        mo, nmo, _ = OM.search_by_projection(fr, P, kun[i, :n], desc[i, :n], ur[i, :n], go[i], gi[i, :go[i][-1]], geo)
-        assert int(res["nmatches"][i]) == nmo, i
-        assert np.array_equal(res["match"][i, :n], mo), i
-        total += nmo
-        # SearchLocalPoints after it, with the motion-model matches taken
-        lfr, LP = hp.local_probs[i % len(hp.local_probs)]
-        lo, nlo, _ = OM.search_local_points(lfr, LP, kun[i, :n], desc[i, :n], ur[i, :n], go[i], gi[i, :go[i][-1]],
-                                            geo, taken=(mo >= 0).astype(np.uint8))
-        assert int(res["local_nmatches"][i]) == nlo, i
-        assert np.array_equal(res["local_match"][i, :n], lo), i
-    assert total > 0
-
-
 def _frame_planes(hp, res, i):
     import spslam_planes as SP
     pl = hp.d_planes.cpu().numpy().view(SP.PLANE_DTYPE).reshape(hp.B, hp.pe.planes_cap)
@@ -96,35 +70,70 @@ def test_planes_stage(run):
         assert np.array_equal(cb, want), i
 
 
-def test_association_and_pose(run):
-    import oracle_assoc as OA
+def test_tracking_chain(run):
+    """TrackWithMotionModel + TrackLocalMap from the matches on, each stage on identical inputs:
+    SearchByProjection, association, motion-model graph, PoseOptimization, outlier discard,
+    SearchLocalPoints, association at the optimized pose, local-map graph, PoseOptimization."""
     import oracle_ctypes
-    import spslam_assoc as SA
+    import oracle_planes
+    import oracle_step
     from test_gpu_pose import pose_close
     hp, res = run
-    m = hp.d_map.cpu().numpy().view(SA.MAP_PLANE_DTYPE)
-    b = hp.d_bound.cpu().numpy().view(np.float32).reshape(-1, 3)
-    P = hp.pe.planes_cap + hp.pe.supp_cap
-    assoc = res["assoc"]
-    n_matched = 0
+    orb, po = oracle_ctypes.OrbOracle(), oracle_planes.PlaneOracle()
+    P1, pts1, pls1, out1, plout1 = hp.graph(0)
+    P2, pts2, pls2, out2, plout2 = hp.graph(1)
+    taken = hp.d_taken.cpu().numpy()
+    n_edges = n_local = n_plane_edges = 0
     for i in range(hp.B):
-        ca, cb = _frame_planes(hp, res, i)
-        coefs = np.concatenate([ca, cb])
-        probA, ptsA, plsA, _ = hp.probA[i]
-        r1, po1, plo1 = oracle_ctypes.pose_optimize(probA, ptsA, plsA)
+        n = int(res["kp_counts"][i])
         g1 = res["pose1"][i]
+        o = oracle_step.run(oracle_step.from_hotpath(hp, i), orb, po, chain={"pose1_Tcw": g1["Tcw"]},
+                            supp_cap=hp.pe.supp_cap)
+        assert int(res["nmatches"][i]) == o["nmatches"], i
+        assert np.array_equal(res["match"][i, :n], o["match"]), i
+        M = len(o["coefs"])
+        for k, key in ((0, "assoc0"), (1, "assoc1")):
+            for q, name in enumerate(("match", "parallel", "vertical")):
+                assert np.array_equal(res["assoc"][k, q, i, :M], o[key][name]), (i, k, name)
+            assert bool(res["new_plane"][k, i]) == o[key]["new_plane"], (i, k)
+        # motion-model graph: bit-identical edges, then the optimisation
+        prob, pts, pls, _ = o["graph1"]
+        assert (P1[i]["n_points"], P1[i]["n_planes"]) == (prob["n_points"], prob["n_planes"]), i
+        assert np.array_equal(P1[i]["Tcw"], prob["Tcw"]), i
+        assert pts1[i].tobytes() == pts.tobytes(), i
+        assert pls1[i].tobytes() == pls.tobytes(), i
+        r1, po1, plo1 = o["pose1"]
         ok, err = pose_close(g1["Tcw"], r1["Tcw"])
         assert ok, (i, err)
-        for k, T in enumerate((probA["Tcw"], g1["Tcw"])):
-            o = OA.associate(T.reshape(4, 4), coefs, m, b)
-            for q, key in enumerate(("match", "parallel", "vertical")):
-                assert np.array_equal(assoc[k, q, i, :len(coefs)], o[key]), (i, k, key)
-            assert bool(res["new_plane"][k, i]) == o["new_plane"], (i, k)
-            n_matched += int((o["match"] >= 0).sum())
-        probB, ptsB, plsB, _ = hp.probB[i]
-        p2 = probB.copy()
-        p2["Tcw"] = g1["Tcw"]
-        r2, _, _ = oracle_ctypes.pose_optimize(p2, ptsB, plsB)
-        ok, err = pose_close(res["pose2"][i]["Tcw"], r2["Tcw"])
+        assert int(g1["n_inliers"]) == int(r1["n_inliers"]), i
+        assert np.array_equal(out1[i], po1) and np.array_equal(plout1[i], plo1), i
+        # discard + SearchLocalPoints at the optimized pose
+        assert np.array_equal(taken[i, :n], o["taken"]), i
+        assert int(res["local_nmatches"][i]) == o["local_nmatches"], i
+        assert np.array_equal(res["local_match"][i, :n], o["local_match"]), i
+        # local-map graph and the second optimisation
+        prob, pts, pls = o["graph2"]
+        assert (P2[i]["n_points"], P2[i]["n_planes"]) == (prob["n_points"], prob["n_planes"]), i
+        assert pts2[i].tobytes() == pts.tobytes(), i
+        assert pls2[i].tobytes() == pls.tobytes(), i
+        r2, po2, plo2 = oracle_ctypes.pose_optimize(prob, pts, pls)
+        g2 = res["pose2"][i]
+        ok, err = pose_close(g2["Tcw"], r2["Tcw"])
         assert ok, (i, err)
-    assert n_matched > 0
+        assert int(g2["n_inliers"]) == int(r2["n_inliers"]), i
+        assert np.array_equal(out2[i], po2) and np.array_equal(plout2[i], plo2), i
+        n_edges += len(pts)
+        n_local += o["local_nmatches"]
+        n_plane_edges += len(pls)
+    assert n_edges > 0 and n_local > 0 and n_plane_edges > 0
+
+
+def test_tracked_pose_near_ground_truth(run):
+    """Sanity (not parity): the local-map pose lands near the synthetic scene's true pose."""
+    hp, res = run
+    for i in range(hp.B):
+        fi = hp.frames[i % len(hp.frames)][0]
+        Twc = hp.scene.pose(fi)
+        T = res["pose2"][i]["Tcw"].reshape(4, 4).astype(np.float64)
+        c = -T[:3, :3].T @ T[:3, 3]
+        assert np.linalg.norm(c - Twc[:3, 3]) < 0.02, (i, c, Twc[:3, 3])
