@@ -40,7 +40,8 @@ import synth
 
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
-                 device=0, K=synth.TUM3, oracle_kps=None, lba_every=0, lba_unique=4, lba_points=1500):
+                 device=0, K=synth.TUM3, oracle_kps=None, lba_every=0, lba_unique=4, lba_points=1500,
+                 pipelined=False, tail_priority=True):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -89,7 +90,9 @@ class HotPath:
         #     PoseOptimization joins both
         # (an explicit stream: torch's default is the legacy NULL stream, which a HIP call given
         # stream 0 would replace by the context's own non-blocking stream, outside these events)
-        self.main = torch.cuda.Stream()
+        # the tracking tail is a chain of latency-bound one-workgroup-per-frame kernels: in pipelined mode its
+        # stream gets the high priority so its workgroups dispatch ahead of the next batch's extraction
+        self.main = torch.cuda.Stream(priority=-1 if pipelined and tail_priority else 0)
         self.side = torch.cuda.Stream()
         self.stream = self.main.cuda_stream
         self.side_stream = self.side.cuda_stream
@@ -110,6 +113,9 @@ class HotPath:
         self.lba_every = lba_every
         if self.n_lba:
             self._setup_lba(seq_id, lba_unique, lba_points)
+        self.pipelined = pipelined
+        if pipelined:
+            self._setup_pipeline()
         torch.cuda.synchronize()  # buffers were filled on the default stream
 
     def _setup_assoc(self, seq_id):
@@ -267,9 +273,10 @@ class HotPath:
             bf=self.bf)
 
     # --- stages
-    def orb(self):
+    def orb(self, stream=None):
+        s = self.stream if stream is None else stream
         self.ex.extract_batch_device(self.d_gray.data_ptr(), self.B, self.W * self.H, self.W, self.d_kps.data_ptr(),
-                                     self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, self.stream)
+                                     self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, s)
 
     def planes(self, stream=None):
         s = self.stream if stream is None else stream
@@ -381,21 +388,82 @@ class HotPath:
                 t[k] = (a[0] + ms, a[1] + n)
         return t
 
+    # Extraction outputs: the only buffers written by ORB / plane extraction and read by the tracking tail.
+    EXTRACTION_BUFFERS = ("d_kps", "d_desc", "d_cnt", "d_planes", "d_pcnt", "d_inl", "d_con", "d_supp", "d_scnt",
+                          "d_lines", "d_patch")
+
+    def _setup_pipeline(self):
+        """Software pipelining across steps: batch k+1's extraction (ORB and planes, two streams) runs beside
+        batch k's tracking tail (frame steps, matching, association, graphs, PoseOptimization), which is
+        latency-bound and leaves most CUs idle.  The extraction outputs are double-buffered; set j may be
+        overwritten once the tail that read it has finished (ev_tail[j])."""
+        torch = self.torch
+        self.sets = [{k: getattr(self, k) for k in self.EXTRACTION_BUFFERS},
+                     {k: torch.zeros_like(getattr(self, k)) for k in self.EXTRACTION_BUFFERS}]
+        self.ext_orb, self.ext_planes = torch.cuda.Stream(), torch.cuda.Stream()
+        self.ev_orb = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
+        self.k = 0
+        self.primed = False
+        torch.cuda.synchronize()
+
+    def _bind(self, j):
+        for k, v in self.sets[j].items():
+            setattr(self, k, v)
+
+    def _extract(self, j):
+        self._bind(j)
+        for st in (self.ext_orb, self.ext_planes):
+            st.wait_event(self.ev_tail[j])
+        self.planes(self.ext_planes.cuda_stream)
+        self.ev_planes[j].record(self.ext_planes)
+        self.orb(self.ext_orb.cuda_stream)
+        self.ev_orb[j].record(self.ext_orb)
+
+    def _tail(self):
+        self.frame()
+        self.match()
+        self.pose()
+
     def step(self):
+        if self.pipelined:
+            return self._step_pipelined()
         # planes of step k may start once step k-1 is done with the plane buffers
         self.ev_fork.record(self.main)
         self.side.wait_event(self.ev_fork)
-        if self.n_lba:
-            # LocalMapping: the keyframes of this step, beside tracking (joined at the end of the step)
-            self.lba_stream.wait_event(self.ev_fork)
-            self.lba_job = self.lba_pool.submit(self.local_ba)
+        self._lba_begin()
         self.planes(self.side_stream)
         self.orb()
         self.ev_join.record(self.side)
         self.main.wait_event(self.ev_join)
-        self.frame()
-        self.match()
-        self.pose()
+        self._tail()
+        self._lba_end()
+
+    def _step_pipelined(self):
+        """One extraction (batch k+1) and one tracking tail (batch k) per step."""
+        if not self.primed:  # the first batch's extraction (warmup absorbs it)
+            self._extract(0)
+            self.primed = True
+        j = self.k % 2
+        self.ev_fork.record(self.main)
+        self._lba_begin()
+        self._extract(1 - j)
+        self._bind(j)
+        self.main.wait_event(self.ev_orb[j])
+        self.main.wait_event(self.ev_planes[j])
+        self._tail()
+        self.ev_tail[j].record(self.main)
+        self._lba_end()
+        self.k += 1
+
+    def _lba_begin(self):
+        if self.n_lba:
+            # LocalMapping: the keyframes of this step, beside tracking (joined at the end of the step)
+            self.lba_stream.wait_event(self.ev_fork)
+            self.lba_job = self.lba_pool.submit(self.local_ba)
+
+    def _lba_end(self):
         if self.n_lba:
             self.lba_job.result()
             self.main.wait_event(self.ev_lba)

@@ -137,3 +137,23 @@ def test_tracked_pose_near_ground_truth(run):
         T = res["pose2"][i]["Tcw"].reshape(4, 4).astype(np.float64)
         c = -T[:3, :3].T @ T[:3, 3]
         assert np.linalg.norm(c - Twc[:3, 3]) < 0.02, (i, c, Twc[:3, 3])
+
+
+def test_pipelined_steps_match_serial(run):
+    """Software-pipelined steps (extraction of batch k+1 beside the tracking of batch k, double-buffered
+    extraction outputs) give the serial step's results bit for bit."""
+    import pipeline
+    hp0, res0 = run
+    hp = pipeline.HotPath(hp0.B, unique_frames=hp0.B, n_boxes=3, pipelined=True)
+    try:
+        for _ in range(3):
+            hp.step()
+        res = hp.results()
+    finally:
+        hp.close()
+    for key in ("kp_counts", "plane_counts", "supposed_counts", "match", "nmatches", "local_match",
+                "local_nmatches", "assoc", "new_plane"):
+        assert np.array_equal(res[key], res0[key]), key
+    assert res["kps"].tobytes() == res0["kps"].tobytes()
+    for key in ("pose1", "pose2"):
+        assert res[key].tobytes() == res0[key].tobytes(), key
