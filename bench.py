@@ -74,7 +74,7 @@ def level_sizes(w, h, nlevels=8, scale=1.2):
 
 
 def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_bytes=0, n_fpl=0, n_map=0, n_bnd=0,
-                      n_proj=0, n_local=0):
+                      n_proj=0, n_local=0, n_cand=0):
     """Compulsory HBM bytes per frame for each kernel kind (DESIGN.md "Roofline" table)."""
     lv = level_sizes(cfg["width"], cfg["height"])
     px = [w * h for w, h in lv]
@@ -82,10 +82,13 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
     N = W * H
     IWH = (W + 1) * (H + 1)
     return {
+        # GrabImageRGBD: RGB u8 x3 + depth u16 in, gray u8 + depth f32 out
+        "grab_rgbd_kernel": cfg["width"] * cfg["height"] * (3 + 2 + 1 + 4),
         # level l-1 (or the input frame) read; level image (l >= 1), blur and FAST score map written
         "level_kernel": px[0] + sum(px[:-1]) + sum(px[1:]) + 2 * sum(px),
         "fast_cells_kernel": sum(px),                         # score maps read once
-        "octree_kernel": 0,                                   # serial list algorithm, no streamed bytes
+        # FAST survivors (4 B each) + per-cell counts in, retained level keypoints (8 B) out
+        "octree_kernel": n_cand * 4 + 2 * sum(_cells(w, h) for w, h in lv) + n_kp * 8,
         "desc_kernel": n_kp * (28 + 32),                      # keypoint + descriptor out
         "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call
         "plane_cloud_kernel": 4 * N + 12 * N,                 # depth samples in, xyz out
@@ -110,6 +113,12 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "track_graph_kernel": n_kp * (40 + 10 + 40) + n_pts * (12 + 32) + n_pls * 48 + 3 * 104,
         "lba_batch": lba_bytes,                               # whole LM schedule of the step's local maps (all phase kernels): records in + results out
     }
+
+
+def _cells(w, h, cell=30):
+    """ComputeKeyPointsOctTree's FAST cell grid of one level: (cols - 32) / 30 x (rows - 32) / 30
+    (src/ORBextractor.cc:772-787)."""
+    return max((w - 32) // cell, 1) * max((h - 32) // cell, 1)
 
 
 def max_over_ranks(elapsed, dist=None, device="cpu"):
@@ -253,11 +262,17 @@ def main():
         lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
     n_fpl = float(res["plane_counts"].mean()) + n_sup
     alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes, n_fpl, hp.n_map,
-                            hp.n_boundary, hp.mean_proj_points, hp.mean_local_points)
+                            hp.n_boundary, hp.mean_proj_points, hp.mean_local_points, hp.mean_fast_candidates)
     launches_per_step = dom_n / args.steps
     avg_launch_s = dom_ms / 1e3 / max(dom_n, 1)
     bytes_per_launch = alg[dom] * args.batch * (2 if dom == "pose_kernel" else 1) / launches_per_step
     achieved = bytes_per_launch / avg_launch_s / 1e9
+    # every kernel kind: algorithmic bytes of a step / its event time in a step, as a fraction of HBM peak
+    by_kernel = {}
+    for k, (ms, _) in sorted(times.items()):
+        if k in alg and ms > 0:
+            gbs = alg[k] * args.batch * (2 if k == "pose_kernel" else 1) / (ms / 1e3 / args.steps) / 1e9
+            by_kernel[k] = {"achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS}
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.config}_b{args.batch}.json"
     if pmc.exists():
@@ -286,6 +301,7 @@ def main():
                    "mean_supposed_planes": n_sup,
                    "pose_edges_per_frame": n_pts + n_pls},
         "kernels_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in sorted(times.items())},
+        "roofline_by_kernel": by_kernel,
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_launch_s * 1e3,

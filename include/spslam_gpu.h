@@ -638,6 +638,36 @@ int spslam_search_local_points_batch_device(spslam_ctx* ctx, int n_frames, const
                                             const uint8_t* d_taken, const spslam_local_params* params,
                                             int32_t* d_match, int* d_nmatches, uint8_t* d_in_view, void* hip_stream);
 
+/* ---------------------------------------------------------------- input images
+ * Tracking::GrabImageRGBD's image preparation (src/Tracking.cc:208-229), the
+ * first kernel of a step:
+ *   gray  = cvtColor(imRGB, RGB2GRAY / BGR2GRAY / RGBA2GRAY / BGRA2GRAY by
+ *           channels and mbRGB), OpenCV's 8U fixed point
+ *           (R*4899 + G*9617 + B*1868 + 8192) >> 14; a 1-channel image is copied;
+ *   depth = imD.convertTo(CV_32F, mDepthMapFactor) when the factor is not 1 or
+ *           the depth is not CV_32F: float(d) * (float)factor; else copied.
+ * mDepthMapFactor is the reciprocal of the YAML DepthMapFactor (Tracking.cc:142-146),
+ * i.e. depth_scale = 1.0f / 5000.0f for TUM. */
+typedef struct spslam_grab_params {
+    int32_t channels;     /* 1, 3 or 4 (interleaved u8) */
+    int32_t rgb;          /* mbRGB: 1 = R,G,B(,A) order, 0 = B,G,R(,A) */
+    int32_t depth_u16;    /* 1 = CV_16U depth, 0 = CV_32F */
+    float depth_scale;    /* mDepthMapFactor */
+} spslam_grab_params;
+
+/* Drop-in for one frame on host buffers: color (row stride color_stride bytes),
+ * depth (row stride depth_stride elements); gray (w*h u8) and depth_out (w*h f32) dense. */
+int spslam_grab_rgbd(spslam_ctx* ctx, const uint8_t* color, int color_stride, const void* depth, int depth_stride,
+                     int w, int h, const spslam_grab_params* params, uint8_t* gray, float* depth_out);
+
+/* Batched, device resident: frame f's color at d_color + f * color_frame_stride bytes,
+ * depth at d_depth + f * depth_frame_stride elements; outputs dense, frame f at
+ * d_gray + f*w*h and d_depth_out + f*w*h (the ORB / plane batch layouts). */
+int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* d_color, size_t color_frame_stride,
+                                  int color_stride, const void* d_depth, size_t depth_frame_stride, int depth_stride,
+                                  int w, int h, const spslam_grab_params* params, uint8_t* d_gray, float* d_depth_out,
+                                  void* hip_stream);
+
 /* ---------------------------------------------------------------- tracking graph glue
  * The Tracking-side bookkeeping between matching / plane association and
  * PoseOptimization, on the device, for a batch of frames (one stage per call):

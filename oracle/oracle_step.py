@@ -16,6 +16,7 @@ import numpy as np
 import oracle_assoc
 import oracle_ctypes
 import oracle_frame
+import oracle_grab
 import oracle_match
 import oracle_supposed
 import oracle_track
@@ -82,8 +83,8 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
 def from_hotpath(hp, i):
     """FrameInputs of batch slot i of a sp-slam_amd/pipeline.py HotPath (host copies of its inputs)."""
     U = len(hp.frames)
-    gray = hp.frames[i % U][1]
-    depth = hp.frames[i % U][2].astype(np.float32) * np.float32(np.float32(1.0) / np.float32(5000.0))
+    gray = oracle_grab.cvt_gray(hp.frames[i % U][1], rgb=True)  # GrabImageRGBD, Tracking.cc:214-229
+    depth = oracle_grab.convert_depth(hp.frames[i % U][2], oracle_grab.depth_scale(hp.depth_factor))
     t = hp.ex.tables()
     b, ginv = hp.fs.bounds, hp.fs.grid_inv
     geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, hp.bf, *b, *ginv], t["scale"]]).astype(np.float32)

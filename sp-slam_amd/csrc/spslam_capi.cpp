@@ -25,6 +25,7 @@
 #include "assoc_launch.h"
 #include "match_launch.h"
 #include "track_launch.h"
+#include "grab_launch.h"
 
 using namespace spslam;
 
@@ -1194,6 +1195,49 @@ int spslam_search_by_projection(spslam_ctx* c, const spslam_proj_frame* frame, c
     if (rc) { (void)hipFreeAsync(q, c->stream); return rc; }
     if (n_kp) HIP_CHECK(c, hipMemcpyAsync(match, q + o[8], (size_t)n_kp * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[9], sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
+int spslam_grab_rgbd_batch_device(spslam_ctx* c, int n_frames, const uint8_t* d_color, size_t color_frame_stride,
+                                  int color_stride, const void* d_depth, size_t depth_frame_stride, int depth_stride,
+                                  int w, int h, const spslam_grab_params* params, uint8_t* d_gray, float* d_depth_out,
+                                  void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !d_color || !d_depth || !params || !d_gray || !d_depth_out || w < 1 || h < 1 ||
+        (params->channels != 1 && params->channels != 3 && params->channels != 4) ||
+        color_stride < w * params->channels || depth_stride < w ||
+        (n_frames > 1 && (color_frame_stride < (size_t)color_stride * h || depth_frame_stride < (size_t)depth_stride * h)))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_grab_rgbd_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    GrabArgs a{d_color, color_frame_stride, color_stride, d_depth, depth_frame_stride, depth_stride, w, h, *params,
+               d_gray, d_depth_out};
+    // a CV_32F depth with |factor - 1| <= 1e-5 is used as is (Tracking.cc:228)
+    if (!params->depth_u16 && std::fabs(params->depth_scale - 1.0f) <= 1e-5f) a.p.depth_scale = 1.0f;
+    HIP_CHECK(c, grab_launch(n_frames, a, (hipStream_t)hip_stream, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_grab_rgbd(spslam_ctx* c, const uint8_t* color, int color_stride, const void* depth, int depth_stride,
+                     int w, int h, const spslam_grab_params* params, uint8_t* gray, float* depth_out) {
+    if (!c || !color || !depth || !params || !gray || !depth_out || w < 1 || h < 1 ||
+        (params->channels != 1 && params->channels != 3 && params->channels != 4) ||
+        color_stride < w * params->channels || depth_stride < w)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_grab_rgbd");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t de = params->depth_u16 ? 2 : 4;
+    const size_t cb = (size_t)color_stride * h, db = (size_t)depth_stride * h * de, gb = (size_t)w * h;
+    const size_t o1 = (cb + 255) / 256 * 256, o2 = o1 + (db + 255) / 256 * 256, o3 = o2 + (gb + 255) / 256 * 256;
+    uint8_t* q = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&q, o3 + gb * 4, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(q, color, cb, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(q + o1, depth, db, hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_grab_rgbd_batch_device(c, 1, q, cb, color_stride, q + o1, (size_t)depth_stride * h, depth_stride,
+                                           w, h, params, q + o2, (float*)(q + o3), c->stream);
+    if (rc) { (void)hipFreeAsync(q, c->stream); return rc; }
+    HIP_CHECK(c, hipMemcpyAsync(gray, q + o2, gb, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(depth_out, q + o3, gb * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipFreeAsync(q, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return SPSLAM_OK;

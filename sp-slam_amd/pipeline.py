@@ -33,6 +33,7 @@ from __future__ import annotations
 import numpy as np
 
 import spslam_frame
+import spslam_grab
 import spslam_gpu as G
 import spslam_planes
 import synth
@@ -54,19 +55,22 @@ class HotPath:
         self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height)
         self.fs = spslam_frame.FrameStage(self.ex, self.fx, self.fy, self.cx, self.cy, K.get("dist", (0,) * 5),
                                           K["bf"], width, height)
-        # --- unique synthetic frames
+        # --- unique synthetic frames: colour (R,G,B u8) + raw depth (u16, DepthMapFactor 5000), as
+        #     GrabImageRGBD receives them; the step converts them on the device (spslam_grab_rgbd)
         U = min(unique_frames, B)
         self.frames = []
         for i in range(U):
             fi = 3 * i
             g, d, fid = self.scene.render(self.scene.pose(fi), width, height, noise_seed=seq_id * 1000 + fi)
-            self.frames.append((fi, g, d, fid))
-        gray = np.stack([self.frames[i % U][1] for i in range(B)])
-        depth = np.stack([self.frames[i % U][2] for i in range(B)]).astype(np.float32) * \
-            np.float32(np.float32(1.0) / np.float32(K["depth_factor"]))
+            self.frames.append((fi, synth.colorize(g, fid), d, fid))
         dev = "cuda"
-        self.d_gray = torch.from_numpy(gray).to(dev)
-        self.d_depth = torch.from_numpy(depth).to(dev)
+        self.d_rgb = torch.from_numpy(np.stack([self.frames[i % U][1] for i in range(B)])).to(dev)
+        self.d_depth_raw = torch.from_numpy(np.stack([self.frames[i % U][2] for i in range(B)]).view(np.int16)).to(dev)
+        self.depth_factor = K["depth_factor"]
+        self.grabber = spslam_grab.Grabber(self.ex, channels=3, rgb=True, depth_u16=True,
+                                           depth_factor=K["depth_factor"])
+        self.d_gray = torch.zeros((B, height, width), dtype=torch.uint8, device=dev)
+        self.d_depth = torch.zeros((B, height, width), dtype=torch.float32, device=dev)
         cap = self.ex.max_kp
         self.kp_cap = cap
         self.d_kps = torch.zeros((B, cap, 7), dtype=torch.float32, device=dev)
@@ -98,10 +102,15 @@ class HotPath:
         self.side_stream = self.side.cuda_stream
         self.ev_fork = torch.cuda.Event()
         self.ev_join = torch.cuda.Event()
-        # --- one ORB pass for the map-point generators (they back-project the frames' own keypoints)
+        # --- one grab + ORB pass for the map-point generators (they back-project the frames' own keypoints)
+        self.grab()
         self.orb()
         torch.cuda.synchronize()
         cnts = self.d_cnt.cpu().numpy()
+        # FAST cell candidates per frame (DistributeOctTree's input; bench roofline bytes of octree_kernel)
+        nf = min(U, 4)
+        self.mean_fast_candidates = sum(len(self.ex.debug_stage(f, l, 2, cap=1 << 16)) for f in range(nf)
+                                        for l in range(self.ex.params.nlevels)) / nf
         self.inv_sigma2 = self.ex.tables()["inv_sigma2"]
         self.mean_keypoints = float(cnts.mean())
         self._setup_match(seq_id)
@@ -273,6 +282,13 @@ class HotPath:
             bf=self.bf)
 
     # --- stages
+    def grab(self, stream=None):
+        """GrabImageRGBD's cvtColor + depth convertTo (src/Tracking.cc:214-229) into d_gray / d_depth."""
+        s = self.stream if stream is None else stream
+        self.grabber.batch_device(self.B, self.d_rgb.data_ptr(), self.H * self.W * 3, self.W * 3,
+                                  self.d_depth_raw.data_ptr(), self.H * self.W, self.W, self.W, self.H,
+                                  self.d_gray.data_ptr(), self.d_depth.data_ptr(), s)
+
     def orb(self, stream=None):
         s = self.stream if stream is None else stream
         self.ex.extract_batch_device(self.d_gray.data_ptr(), self.B, self.W * self.H, self.W, self.d_kps.data_ptr(),
@@ -389,7 +405,7 @@ class HotPath:
         return t
 
     # Extraction outputs: the only buffers written by ORB / plane extraction and read by the tracking tail.
-    EXTRACTION_BUFFERS = ("d_kps", "d_desc", "d_cnt", "d_planes", "d_pcnt", "d_inl", "d_con", "d_supp", "d_scnt",
+    EXTRACTION_BUFFERS = ("d_gray", "d_depth", "d_kps", "d_desc", "d_cnt", "d_planes", "d_pcnt", "d_inl", "d_con", "d_supp", "d_scnt",
                           "d_lines", "d_patch")
 
     def _setup_pipeline(self):
@@ -404,6 +420,7 @@ class HotPath:
         self.ev_orb = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
+        self.ev_grab = [torch.cuda.Event(), torch.cuda.Event()]
         self.k = 0
         self.primed = False
         torch.cuda.synchronize()
@@ -414,8 +431,10 @@ class HotPath:
 
     def _extract(self, j):
         self._bind(j)
-        for st in (self.ext_orb, self.ext_planes):
-            st.wait_event(self.ev_tail[j])
+        self.ext_orb.wait_event(self.ev_tail[j])
+        self.grab(self.ext_orb.cuda_stream)
+        self.ev_grab[j].record(self.ext_orb)
+        self.ext_planes.wait_event(self.ev_grab[j])
         self.planes(self.ext_planes.cuda_stream)
         self.ev_planes[j].record(self.ext_planes)
         self.orb(self.ext_orb.cuda_stream)
@@ -429,7 +448,8 @@ class HotPath:
     def step(self):
         if self.pipelined:
             return self._step_pipelined()
-        # planes of step k may start once step k-1 is done with the plane buffers
+        # planes of step k may start once step k-1 is done with the plane buffers and this step's depth exists
+        self.grab()
         self.ev_fork.record(self.main)
         self.side.wait_event(self.ev_fork)
         self._lba_begin()

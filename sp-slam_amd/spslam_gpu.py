@@ -152,7 +152,7 @@ class OrbExtractor:
         return {self.lib.spslam_kernel_name(k).decode(): (tot[k], cnt[k]) for k in range(n)}
 
     # --- stage access for parity tests
-    def debug_stage(self, frame: int, level: int, stage: int):
+    def debug_stage(self, frame: int, level: int, stage: int, cap: int | None = None):
         w, h = self.level_size(level)
         n = ctypes.c_int()
         if stage in (0, 1):
@@ -160,7 +160,7 @@ class OrbExtractor:
             self._check(self.lib.spslam_orb_debug_stage(self.ctx, frame, level, stage, out.ctypes.data, out.size,
                                                         ctypes.byref(n)))
             return out
-        cap = 1 << 20 if stage == 2 else 4096
+        cap = cap or (1 << 20 if stage == 2 else 4096)
         out = np.zeros(cap, KEYPOINT_DTYPE)
         self._check(self.lib.spslam_orb_debug_stage(self.ctx, frame, level, stage, out.ctypes.data, cap,
                                                     ctypes.byref(n)))

@@ -519,3 +519,16 @@ def local_problem(scene: Scene, kf_fi: int, cur_fi: int, kf_kps, kf_desc, kf_dep
     fr["Tcw"] = Tcw.astype(np.float32).reshape(16)
     fr["n_points"] = len(P)
     return fr, P
+
+
+# Per-face colour tints (R, G, B gains) for colour frames; the background stays gray.
+_TINTS = np.array([[1.00, 0.92, 0.85], [0.85, 0.95, 1.00], [0.95, 1.00, 0.88], [1.00, 0.86, 0.95],
+                   [0.90, 0.90, 1.00], [0.97, 0.97, 0.90], [0.88, 1.00, 1.00], [1.00, 0.95, 0.80]], np.float32)
+
+
+def colorize(gray: np.ndarray, fid: np.ndarray) -> np.ndarray:
+    """An interleaved RGB u8 frame (HxWx3, R,G,B order) from a rendered gray frame: each face's texture
+    tinted by a per-face gain, so cvtColor's weights matter (TUM frames are colour, rgbd_tum reads them
+    with imread and GrabImageRGBD converts them, src/Tracking.cc:214-224)."""
+    tint = np.where((fid >= 0)[..., None], _TINTS[np.maximum(fid, 0) % len(_TINTS)], 1.0).astype(np.float32)
+    return np.clip(np.rint(gray[..., None].astype(np.float32) * tint), 0, 255).astype(np.uint8)

@@ -24,6 +24,18 @@ def run():
     hp.close()
 
 
+def test_grab_stage(run):
+    """GrabImageRGBD's cvtColor(RGB2GRAY) + depth convertTo on the device, bit-exact."""
+    import oracle_grab
+    hp, _ = run
+    scale = oracle_grab.depth_scale(hp.depth_factor)
+    for i in range(hp.B):
+        rgb = hp.d_rgb[i].cpu().numpy()
+        raw = hp.d_depth_raw[i].cpu().numpy().view(np.uint16)
+        assert np.array_equal(hp.d_gray[i].cpu().numpy(), oracle_grab.cvt_gray(rgb, rgb=True)), i
+        assert hp.d_depth[i].cpu().numpy().tobytes() == oracle_grab.convert_depth(raw, scale).tobytes(), i
+
+
 def test_orb_and_frame_stage(run):
     import oracle_ctypes
     import oracle_frame
