@@ -30,8 +30,21 @@ __device__ __forceinline__ V3 mtv(const M3& R, V3 v) {  // R^T v
             R.a[2] * v.x + R.a[5] * v.y + R.a[8] * v.z};
 }
 
+template <int I, int J, int K>
+__device__ __forceinline__ void q_case(const M3& R, Q& q) {
+    double t = sqrt(R.a[4 * I] - R.a[4 * J] - R.a[4 * K] + 1.0);
+    const double ci = 0.5 * t;
+    t = 0.5 / t;
+    q.w = (R.a[3 * K + J] - R.a[3 * J + K]) * t;
+    const double cj = (R.a[3 * J + I] + R.a[3 * I + J]) * t;
+    const double ck = (R.a[3 * K + I] + R.a[3 * I + K]) * t;
+    q.x = I == 0 ? ci : (J == 0 ? cj : ck);
+    q.y = I == 1 ? ci : (J == 1 ? cj : ck);
+    q.z = I == 2 ? ci : (J == 2 ? cj : ck);
+}
+
 // Eigen Quaternion(Matrix3)
-__device__ Q q_from_rot(const M3& R) {
+__device__ __forceinline__ Q q_from_rot(const M3& R) {
     Q q;
     double t = R.a[0] + R.a[4] + R.a[8];
     if (t > 0) {
@@ -42,19 +55,14 @@ __device__ Q q_from_rot(const M3& R) {
         q.y = (R.a[2] - R.a[6]) * t;
         q.z = (R.a[3] - R.a[1]) * t;
     } else {
+        // largest diagonal i, j = (i+1)%3, k = (j+1)%3; one branch per i so every index is a
+        // constant (a dynamically indexed R would live in scratch memory)
         int i = 0;
         if (R.a[4] > R.a[0]) i = 1;
-        if (R.a[8] > R.a[4 * i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(R.a[4 * i] - R.a[4 * j] - R.a[4 * k] + 1.0);
-        const double ci = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (R.a[3 * k + j] - R.a[3 * j + k]) * t;
-        const double cj = (R.a[3 * j + i] + R.a[3 * i + j]) * t;
-        const double ck = (R.a[3 * k + i] + R.a[3 * i + k]) * t;
-        q.x = i == 0 ? ci : (j == 0 ? cj : ck);
-        q.y = i == 1 ? ci : (j == 1 ? cj : ck);
-        q.z = i == 2 ? ci : (j == 2 ? cj : ck);
+        if (R.a[8] > (i == 0 ? R.a[0] : R.a[4])) i = 2;
+        if (i == 0) q_case<0, 1, 2>(R, q);
+        else if (i == 1) q_case<1, 2, 0>(R, q);
+        else q_case<2, 0, 1>(R, q);
     }
     return q;
 }
@@ -89,7 +97,7 @@ __device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
     return r;
 }
 // SE3Quat::exp (types/se3quat.h:223-257)
-__device__ SE3 se3_exp(const double* u) {
+__device__ __forceinline__ SE3 se3_exp(const double* u) {
     const V3 w{u[0], u[1], u[2]}, ups{u[3], u[4], u[5]};
     const double theta = sqrt(dot(w, w));
     const double O[9] = {0, -w.z, w.y, w.z, 0, -w.x, -w.y, w.x, 0};
@@ -101,8 +109,10 @@ __device__ SE3 se3_exp(const double* u) {
         for (int k = 0; k < 9; k++) R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + O[k] + O2[k];
         V = R;
     } else {
-        const double a = sin(theta) / theta, b = (1 - cos(theta)) / (theta * theta),
-                     c = (theta - sin(theta)) / pow(theta, 3);
+        double st, ct;
+        sincos(theta, &st, &ct);
+        // pow(theta, 3) as two products: within an ulp of glibc's pow, far cheaper than ocml's
+        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / (theta * theta * theta);
         for (int k = 0; k < 9; k++) {
             R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
             V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
@@ -126,14 +136,14 @@ __device__ __forceinline__ void p_normalize(double* v) {
 __device__ __forceinline__ double azimuth(V3 v) { return atan2(v.y, v.x); }
 __device__ __forceinline__ double elevation(V3 v) { return atan2(v.z, sqrt(v.x * v.x + v.y * v.y)); }
 // Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
-__device__ M3 p_rotation(V3 v) {
+__device__ __forceinline__ M3 p_rotation(V3 v) {
     const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
     const Q a{cos(ha), 0.0 * sin(ha), 0.0 * sin(ha), 1.0 * sin(ha)};
     const Q e{cos(he), 0.0 * sin(he), 1.0 * sin(he), 0.0 * sin(he)};
     return q_to_rot(q_mul(a, e));
 }
 // Eigen AngleAxis::toRotationMatrix() * v
-__device__ V3 aa_apply(double ang, V3 ax, V3 v) {
+__device__ __forceinline__ V3 aa_apply(double ang, V3 ax, V3 v) {
     const V3 sa = sin(ang) * ax;
     const double c = cos(ang);
     const V3 c1 = (1 - c) * ax;
@@ -147,7 +157,7 @@ __device__ V3 aa_apply(double ang, V3 ax, V3 v) {
 }
 
 // plane-edge error: (T * world).ominus{,_par,_ver}(meas)
-__device__ void plane_error(int kind, const SE3& T, const P4& world, const P4& meas, double* e) {
+__device__ __forceinline__ void plane_error(int kind, const SE3& T, const P4& world, const P4& meas, double* e) {
     const M3 R = q_to_rot(T.r);
     const V3 n2 = mv(R, V3{world.c[0], world.c[1], world.c[2]});
     double v[4] = {n2.x, n2.y, n2.z, world.c[3] - dot(T.t, n2)};
@@ -166,6 +176,14 @@ __device__ void plane_error(int kind, const SE3& T, const P4& world, const P4& m
     e[0] = azimuth(n);
     e[1] = elevation(n);
     if (kind == 0) e[2] = (-v[3]) - (-meas.c[3]);
+}
+
+struct E3 { double e0, e1, e2; };
+// plane_error returning the error by value (no address-taken array: keeps it in registers)
+__device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& world, const P4& meas) {
+    double e[3] = {0, 0, 0};
+    plane_error(kind, T, world, meas, e);
+    return E3{e[0], e[1], e[2]};
 }
 
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)

@@ -27,48 +27,65 @@ using namespace g2od;
 
 struct Cam { double fx, fy, cx, cy, bf; };
 
-__device__ __forceinline__ void point_error(const spslam_point_obs& o, const SE3& T, const Cam& c, double* e,
-                                            V3* pc) {
+__device__ __forceinline__ E3 point_error(const spslam_point_obs& o, const SE3& T, const Cam& c, V3& pc) {
     const V3 p = q_rot(T.r, V3{(double)o.xw[0], (double)o.xw[1], (double)o.xw[2]}) + T.t;
-    if (pc) *pc = p;
+    pc = p;
     if (o.ur < 0) {
-        e[0] = (double)o.u - (p.x / p.z * c.fx + c.cx);
-        e[1] = (double)o.v - (p.y / p.z * c.fy + c.cy);
-    } else {
-        const float invz = (float)(1.0f / p.z);  // float reciprocal, types_six_dof_expmap.cpp:300
-        const double r0 = p.x * invz * c.fx + c.cx, r1 = p.y * invz * c.fy + c.cy;
-        e[0] = (double)o.u - r0;
-        e[1] = (double)o.v - r1;
-        e[2] = (double)o.ur - (r0 - c.bf * invz);
+        return E3{(double)o.u - (p.x / p.z * c.fx + c.cx), (double)o.v - (p.y / p.z * c.fy + c.cy), 0.0};
     }
+    const float invz = (float)(1.0f / p.z);  // float reciprocal, types_six_dof_expmap.cpp:300
+    const double r0 = p.x * invz * c.fx + c.cx, r1 = p.y * invz * c.fy + c.cy;
+    return E3{(double)o.u - r0, (double)o.v - r1, (double)o.ur - (r0 - c.bf * invz)};
 }
 
-// Eigen::LDLT (lower, diagonal pivoting) + solve.  Returns false when the
-// factor is not positive (LinearSolverDense::solve returns false, x unchanged).
-// m, tr, temp and y live in LDS (dynamic pivot indexing would otherwise spill to scratch).
-__device__ __forceinline__ bool ldlt_solve(double (*m)[6], const double* b, double* x, int* tr, double* temp,
-                                           double* y) {
-    const int n = 6;
+// Eigen::LDLT (lower, diagonal pivoting) + solve on H + lambda I.  Returns
+// false when the factor is not positive (LinearSolverDense::solve returns
+// false, x unchanged).  Fully unrolled over the 6x6 matrix so that it lives in
+// registers; the data-dependent pivot swaps are unrolled over the candidate
+// rows, so the arithmetic (and its order) is exactly Eigen's unblocked LDLT.
+__device__ __forceinline__ void swapd(double& a, double& b) { const double t = a; a = b; b = t; }
+
+__device__ __forceinline__ bool ldlt_solve(const double (*H)[6], double lambda, const double* b, double* x) {
+    constexpr int n = 6;
+    double m[n][n];
+#pragma unroll
+    for (int i = 0; i < n; i++)
+#pragma unroll
+        for (int j = 0; j < n; j++) m[i][j] = H[i][j] + (i == j ? lambda : 0.0);
+    int tr[n];
     int sign = 0;
+#pragma unroll
     for (int k = 0; k < n; ++k) {
         int big = k;
         double bv = fabs(m[k][k]);
+#pragma unroll
         for (int i = k + 1; i < n; i++)
             if (fabs(m[i][i]) > bv) { bv = fabs(m[i][i]); big = i; }
         tr[k] = big;
-        if (k != big) {
-            for (int j = 0; j < k; j++) { double t = m[k][j]; m[k][j] = m[big][j]; m[big][j] = t; }
-            for (int i = big + 1; i < n; i++) { double t = m[i][k]; m[i][k] = m[i][big]; m[i][big] = t; }
-            { double t = m[k][k]; m[k][k] = m[big][big]; m[big][big] = t; }
-            for (int i = k + 1; i < big; ++i) { double t = m[i][k]; m[i][k] = m[big][i]; m[big][i] = t; }
+#pragma unroll
+        for (int c = k + 1; c < n; c++) {
+            if (big == c) {
+#pragma unroll
+                for (int j = 0; j < k; j++) swapd(m[k][j], m[c][j]);
+#pragma unroll
+                for (int i = c + 1; i < n; i++) swapd(m[i][k], m[i][c]);
+                swapd(m[k][k], m[c][c]);
+#pragma unroll
+                for (int i = k + 1; i < c; ++i) swapd(m[i][k], m[c][i]);
+            }
         }
         if (k > 0) {
+            double temp[n];
+#pragma unroll
             for (int j = 0; j < k; j++) temp[j] = m[j][j] * m[k][j];
             double s = 0;
+#pragma unroll
             for (int j = 0; j < k; j++) s += m[k][j] * temp[j];
             m[k][k] -= s;
+#pragma unroll
             for (int i = k + 1; i < n; i++) {
                 double t = 0;
+#pragma unroll
                 for (int j = 0; j < k; j++) t += m[i][j] * temp[j];
                 m[i][k] -= t;
             }
@@ -76,25 +93,45 @@ __device__ __forceinline__ bool ldlt_solve(double (*m)[6], const double* b, doub
         const double akk = m[k][k];
         const bool valid = fabs(akk) > 0;
         if (k == 0 && !valid) return false;
-        if (k + 1 < n && valid)
+        if (k + 1 < n && valid) {
+#pragma unroll
             for (int i = k + 1; i < n; i++) m[i][k] /= akk;
+        }
         if (sign == 1) { if (akk < 0) sign = 3; }
         else if (sign == 2) { if (akk > 0) sign = 3; }
         else if (sign == 0) { if (akk > 0) sign = 1; else if (akk < 0) sign = 2; }
     }
     if (!(sign == 1 || sign == 0)) return false;
+    double y[n];
+#pragma unroll
     for (int i = 0; i < n; i++) y[i] = b[i];
-    for (int k = 0; k < n; k++) { double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+    for (int k = 0; k < n; k++)
+#pragma unroll
+        for (int c = k + 1; c < n; c++)
+            if (tr[k] == c) swapd(y[k], y[c]);
+#pragma unroll
     for (int i = 0; i < n; i++)
+#pragma unroll
         for (int j = 0; j < i; j++) y[i] -= m[i][j] * y[j];
+#pragma unroll
     for (int i = 0; i < n; i++) y[i] = fabs(m[i][i]) > 2.2250738585072014e-308 ? y[i] / m[i][i] : 0.0;
+#pragma unroll
     for (int i = n - 1; i >= 0; i--)
+#pragma unroll
         for (int j = i + 1; j < n; j++) y[i] -= m[j][i] * y[j];
-    for (int k = n - 1; k >= 0; k--) { double t = y[k]; y[k] = y[tr[k]]; y[tr[k]] = t; }
+#pragma unroll
+    for (int k = n - 1; k >= 0; k--)
+#pragma unroll
+        for (int c = k + 1; c < n; c++)
+            if (tr[k] == c) swapd(y[k], y[c]);
+#pragma unroll
     for (int i = 0; i < n; i++) x[i] = y[i];
     return true;
 }
 
+// Four waves per problem (measured: one wave per problem frees SIMDs for the
+// pipelined extraction but makes the edge passes 4x longer -- a net loss).
 constexpr int kThreads = 256;
 constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
 constexpr int kPlaneChunk = 64;  // plane edges whose 12 perturbed errors are evaluated together
@@ -105,26 +142,30 @@ struct Shared {
     SE3 Tp[12];                      // exp(+-1e-9 e_d) * T for the current iterate
     double perr[kPlaneChunk][12][3]; // plane errors at the 12 perturbed poses
     double H[6][6], b[6], x[6];
-    double Hl[6][6], ly[6], ltemp[6];
-    int ltr[6];
     double lambda, ni, currentChi, iniChi, tempChi;
     SE3 T, T0, Ttrial, Tlast;
     int nBad, stop, active_any;
     int count[kThreads / 64];
 };
 
-// Block reduction of `n` doubles per thread (v[0..n)) into S.red[0][0..n).
+// Block reduction of NV doubles per thread (v[0..NV)) into S.red[0][0..NV).  The
+// NV butterfly chains are unrolled together so their shuffle latencies overlap.
 template <int NV>
-__device__ void block_reduce(double (&v)[NV], int n, Shared& S) {
+__device__ void block_reduce(double (&v)[NV], Shared& S) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int k = 0; k < n; k++) {
-        double x = v[k];
+    double x[NV];
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off);
-        if (lane == 0) S.red[w][k] = x;
+    for (int k = 0; k < NV; k++) x[k] = v[k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < NV; k++) x[k] += __shfl_xor(x[k], off);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; k++) S.red[w][k] = x[k];
     }
     __syncthreads();
-    if (threadIdx.x < n) {
+    if (threadIdx.x < NV) {
         double s = 0;
         for (int j = 0; j < kThreads / 64; j++) s += S.red[j][threadIdx.x];
         S.red[0][threadIdx.x] = s;
@@ -144,7 +185,7 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
 
 using namespace pose;
 
-__global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+__global__ __launch_bounds__(kThreads) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
                                                    const spslam_point_obs* __restrict__ pts_all,
                                                    const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
                                                    const spslam_pose_result* __restrict__ init_from,
@@ -158,7 +199,7 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
     uint8_t* pout = pout_all + P.point_offset;
     uint8_t* plout = plout_all + P.plane_offset;
     spslam_pose_result* res = results + blockIdx.x;
-    const float* Tin = init_from ? init_from[blockIdx.x].Tcw : P.Tcw;
+    const float* Tin = init_from ? init_from[blockIdx.x].Tcw : probs[blockIdx.x].Tcw;
     const int np = P.n_points, nl = P.n_planes, ne = np + nl;
     const Cam cam{P.fx, P.fy, P.cx, P.cy, P.bf};
 
@@ -185,7 +226,7 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
     __syncthreads();
 
     // edge e < np: point e; else plane e - np.  Per-edge info/delta:
-    auto edge_info = [&](int e, double* info, double* delta, int* dim) {
+    auto edge_info = [&](int e, double* info, double* delta, int* dim) __attribute__((always_inline)) {
         if (e < np) {
             const spslam_point_obs& o = pts[e];
             info[0] = info[1] = info[2] = (double)o.inv_sigma2;
@@ -197,7 +238,7 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
             else { info[0] = info[1] = kind == 1 ? K.par_info : K.ver_info; info[2] = 0; *delta = K.delta_vp; *dim = 2; }
         }
     };
-    auto plane_of = [&](int e, P4& w, P4& m) {
+    auto plane_of = [&](int e, P4& w, P4& m) __attribute__((always_inline)) {
         const spslam_plane_obs& o = pls[e - np];
         for (int k = 0; k < 4; k++) { w.c[k] = o.world[k]; m.c[k] = o.meas[k]; }
         if (o.world[3] < 0.0f) for (int k = 0; k < 4; k++) w.c[k] = -w.c[k];  // Converter::toPlane3D
@@ -205,15 +246,20 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
         p_normalize(w.c);
         p_normalize(m.c);
     };
-    auto error_at = [&](int e, const SE3& T, double* err, V3* pc) {
-        if (e < np) point_error(pts[e], T, cam, err, pc);
-        else {
+    auto error_at = [&](int e, const SE3& T, double* err, V3* pc) __attribute__((always_inline)) {
+        E3 r;
+        if (e < np) {
+            V3 p;
+            r = point_error(pts[e], T, cam, p);
+            if (pc) *pc = p;
+        } else {
             P4 w, m;
             plane_of(e, w, m);
-            plane_error(pls[e - np].kind, T, w, m, err);
+            r = plane_error3(pls[e - np].kind, T, w, m);
         }
+        err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
     };
-    auto is_outlier = [&](int e) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
+    auto is_outlier = [&](int e) __attribute__((always_inline)) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
 
     bool robust = true;
     int nBad = 0, total_its = 0;
@@ -236,8 +282,7 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                     // rows beyond dim carry zero error and Jacobian: their terms add exact zeros
                     (void)dim;
                     double chi = 0;
-#pragma unroll
-                    for (int r = 0; r < 3; r++) chi += err[r] * info[r] * err[r];
+                    chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
                     double rho0, rho1;
                     huber(chi, delta, robust, &rho0, &rho1);
                     v[0] += rho0;
@@ -313,7 +358,7 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                         __syncthreads();
                     }
                 }
-                block_reduce(v, kRed, S);
+                block_reduce(v, S);
                 if (t == 0) {
                     S.Tlast = S.T;
                     S.currentChi = S.red[0][0];
@@ -338,10 +383,8 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                 bool ok2 = true;
                 do {
                     if (t == 0) {
-                        for (int i = 0; i < 6; i++)
-                            for (int j = 0; j < 6; j++) S.Hl[i][j] = S.H[i][j] + (i == j ? S.lambda : 0.0);
                         double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten
-                        S.stop = ldlt_solve(S.Hl, S.b, x, S.ltr, S.ltemp, S.ly) ? 1 : 0;
+                        S.stop = ldlt_solve(S.H, S.lambda, S.b, x) ? 1 : 0;
                         for (int j = 0; j < 6; j++) S.x[j] = x[j];
                         S.Ttrial = se3_mul(se3_exp(x), S.T);
                     }
@@ -356,12 +399,13 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                         edge_info(e, info, &delta, &dim);
                         error_at(e, Tt, err, nullptr);
                         double chi = 0;
-                        for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
+                        // rows beyond dim hold a zero error: their +0 terms leave chi unchanged
+                        chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
                         double rho0, rho1;
                         huber(chi, delta, robust, &rho0, &rho1);
                         c[0] += rho0;
                     }
-                    block_reduce(c, 1, S);
+                    block_reduce(c, S);
                     if (t == 0) {
                         S.Tlast = S.Ttrial;
                         double tempChi = S.red[0][0];
@@ -372,7 +416,8 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
                         scale += 1e-3;
                         r /= scale;
                         if (r > 0 && isfinite(tempChi)) {
-                            double alpha = 1. - pow((2 * r - 1), 3);
+                            const double r21 = 2 * r - 1;  // pow(2r - 1, 3) as two products (an ocml pow is ~200 serial fp64 ops)
+                            double alpha = 1. - r21 * r21 * r21;
                             alpha = fmin(alpha, 2. / 3.);
                             S.lambda *= fmax(1. / 3., alpha);
                             S.ni = 2;
@@ -410,9 +455,14 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
             int dim;
             edge_info(e, info, &delta, &dim);
             const bool was_out = is_outlier(e);
-            error_at(e, was_out ? T : Tl, err, nullptr);
+            SE3 Te;  // field-wise select (a selected reference would put both poses in scratch memory)
+            Te.r.w = was_out ? T.r.w : Tl.r.w; Te.r.x = was_out ? T.r.x : Tl.r.x;
+            Te.r.y = was_out ? T.r.y : Tl.r.y; Te.r.z = was_out ? T.r.z : Tl.r.z;
+            Te.t.x = was_out ? T.t.x : Tl.t.x; Te.t.y = was_out ? T.t.y : Tl.t.y; Te.t.z = was_out ? T.t.z : Tl.t.z;
+            error_at(e, Te, err, nullptr);
             double chi = 0;
-            for (int r = 0; r < dim; r++) chi += err[r] * info[r] * err[r];
+            // rows beyond dim hold a zero error: their +0 terms leave chi unchanged
+                        chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
             const float chi2 = (float)chi;
             bool b;
             if (e < np) b = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
@@ -425,7 +475,9 @@ __global__ __launch_bounds__(256) void pose_kernel(const spslam_pose_problem* __
         for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
         if ((t & 63) == 0) S.count[t >> 6] = bad;
         __syncthreads();
-        nBad = S.count[0] + S.count[1] + S.count[2] + S.count[3];
+        nBad = 0;
+#pragma unroll
+        for (int w = 0; w < kThreads / 64; w++) nBad += S.count[w];
         __syncthreads();
         if (round == 2) robust = false;
         if (ne < 10) break;

@@ -50,7 +50,7 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    lib = ctypes.CDLL(str(path or LIB_PATH))
+    lib = ctypes.CDLL(str(path or os.environ.get("SPSLAM_GPU_LIB") or LIB_PATH))
     vp, ip, fp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_float)
     lib.spslam_create.argtypes = [ctypes.c_int, ctypes.POINTER(OrbParams), ctypes.POINTER(vp)]
     lib.spslam_destroy.argtypes = [vp]
