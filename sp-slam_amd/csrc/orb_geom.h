@@ -18,11 +18,11 @@ constexpr int kLevelTileH = 32;
 
 struct LevelGeom {
     int w, h;                 // level image size
-    int stride;               // row pitch in bytes of the level image
-    int pad_;
+    int stride;               // row pitch in bytes of the level image (levels >= 1: w rounded up to 64)
+    int bpitch;               // row pitch of the blurred level and the FAST score map (w rounded up to 64)
     long long frame_stride;   // bytes between frames of this level
     const uint8_t* img;       // level image, frame 0
-    uint8_t* blur;            // blurred level, frame 0 (pitch = w, frame stride = blur_frame_stride)
+    uint8_t* blur;            // blurred level, frame 0 (pitch bpitch, frame stride blur_frame_stride)
     long long blur_frame_stride;
     int maxBorderX, maxBorderY;
     int nCols, nRows, wCell, hCell;
@@ -34,7 +34,7 @@ struct LevelGeom {
     int patch_size;           // (int)(PATCH_SIZE * mvScaleFactor[level])
     float scale;              // mvScaleFactor[level]
     int tiles_x;              // level_kernel tiles per row
-    uint8_t* score;           // FAST score map (pitch w, frame stride blur_frame_stride), frame 0
+    uint8_t* score;           // FAST score map (pitch bpitch, frame stride blur_frame_stride), frame 0
     double rscale_x, rscale_y;  // resize from level-1: 1. / ((double)w / w_prev), as OpenCV computes it
 };
 

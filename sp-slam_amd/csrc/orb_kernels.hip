@@ -124,9 +124,10 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* p, int P, int t) {
 
 __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
     __shared__ uint8_t tin[kLH][kLW + 2];
-    __shared__ uint16_t th[kLH][kLevelTileW];
+    __shared__ __attribute__((aligned(16))) uint16_t th[kLH][kLevelTileW];
     __shared__ RzCol rx[kLW], ry[kLH];
     __shared__ uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
+    __shared__ __attribute__((aligned(16))) uint8_t stile[kLevelTileH][kLevelTileW];  // FAST scores of the tile
     const LevelGeom& L = g.lv[l];
     const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int x0 = (blockIdx.x % L.tiles_x) * kLevelTileW, y0 = (blockIdx.x / L.tiles_x) * kLevelTileH;
@@ -177,13 +178,24 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             if (q < kN) {
                 const int r = q / kLW, c = q - r * kLW;
                 tin[r][c] = (uint8_t)v[k];
-                if (r >= 3 && r < 3 + kLevelTileH && c >= 3 && c < 3 + kLevelTileW && y0 + r - 3 < h &&
-                    x0 + c - 3 < w)
-                    img[(size_t)(y0 + r - 3) * L.stride + (x0 + c - 3)] = (uint8_t)v[k];
             }
         }
     }
     __syncthreads();
+    const int lr = lane >> 4, lc = (lane & 15) * 4;  // 4 adjacent pixels per lane, 16 lanes per tile row
+    if (l > 0) {
+        // the level image (tile interior) for the next level, IC_Angle and BRIEF: one dword store per
+        // 4 pixels (row pitch L.stride is a multiple of 64; columns past w land in the row padding)
+        for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
+            const int r = rb + lr;
+            if (y0 + r < h) {
+                const uint8_t* p = &tin[r + 3][lc + 3];
+                const uint32_t v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+                                   ((uint32_t)p[3] << 24);
+                *reinterpret_cast<uint32_t*>(img + (size_t)(y0 + r) * L.stride + (x0 + lc)) = v;
+            }
+        }
+    }
     // horizontal blur pass over all tile rows
     for (int q = t; q < kLH * kLevelTileW; q += kLevelThreads) {
         const int r = q / kLevelTileW, c = q - r * kLevelTileW;
@@ -193,23 +205,34 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
     __syncthreads();
     uint8_t* blur = L.blur + f * L.blur_frame_stride;
     uint8_t* score = L.score + f * L.blur_frame_stride;
-    // vertical blur pass; FAST pre-test at the lowest threshold, candidates compacted per wave
+    const int bp = L.bpitch;
+    // vertical blur pass, 4 pixels per lane (8-byte LDS reads of the row sums, one dword store); FAST
+    // pre-test at the lowest threshold, candidates compacted per wave.  A wave owns tile rows
+    // {4w..4w+3, 16+4w..16+4w+3}; their scores are assembled in LDS and stored as dwords by the same wave.
     int ncand = 0;
-    for (int q0 = wave * 64; q0 < kLevelTileH * kLevelTileW; q0 += kLevelThreads) {
-        const int q = q0 + lane;
-        const int r = q / kLevelTileW, c = q - r * kLevelTileW;
-        const int y = y0 + r, x = x0 + c;
-        bool maybe = false;
-        if (y < h && x < w) {
-            const int sb = 18 * (th[r][c] + th[r + 6][c]) + 34 * (th[r + 1][c] + th[r + 5][c]) +
-                           48 * (th[r + 2][c] + th[r + 4][c]) + 56 * th[r + 3][c];
-            blur[(size_t)y * w + x] = (uint8_t)min(255, (sb + (1 << 15)) >> 16);
-            maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 && fast_maybe(&tin[r + 3][c + 3], kLW + 2, minTh);
-            if (!maybe) score[(size_t)y * w + x] = 0;
+    for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
+        const int r = rb + lr, y = y0 + r;
+        uint16_t tv[7][4];
+#pragma unroll
+        for (int i = 0; i < 7; i++) *reinterpret_cast<uint2*>(tv[i]) = *reinterpret_cast<const uint2*>(&th[r + i][lc]);
+        uint32_t bw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int sb = 18 * (tv[0][j] + tv[6][j]) + 34 * (tv[1][j] + tv[5][j]) + 48 * (tv[2][j] + tv[4][j]) +
+                           56 * tv[3][j];
+            bw |= (uint32_t)min(255, (sb + (1 << 15)) >> 16) << (8 * j);
         }
-        const unsigned long long m = __ballot(maybe);
-        if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)q;
-        ncand += __popcll(m);
+        if (y < h) *reinterpret_cast<uint32_t*>(blur + (size_t)y * bp + (x0 + lc)) = bw;
+        *reinterpret_cast<uint32_t*>(&stile[r][lc]) = 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int x = x0 + lc + j;
+            const bool maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 &&
+                               fast_maybe(&tin[r + 3][lc + j + 3], kLW + 2, minTh);
+            const unsigned long long m = __ballot(maybe);
+            if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(r * kLevelTileW + lc + j);
+            ncand += __popcll(m);
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -218,7 +241,16 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         const int q = cand[wave][k];
         const int r = q / kLevelTileW, c = q - r * kLevelTileW;
         const int sc = max(fast_score(&tin[r + 3][c + 3], kLW + 2), 0);
-        score[(size_t)(y0 + r) * w + (x0 + c)] = (uint8_t)(sc >= minTh ? sc : 0);
+        stile[r][c] = (uint8_t)(sc >= minTh ? sc : 0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
+        const int r = rb + lr, y = y0 + r;
+        if (y < h)
+            *reinterpret_cast<uint32_t*>(score + (size_t)y * bp + (x0 + lc)) =
+                *reinterpret_cast<const uint32_t*>(&stile[r][lc]);
     }
 }
 
@@ -257,7 +289,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __
     const int maxY = min(iniY + L.hCell + 6, L.maxBorderY), maxX = min(iniX + L.wCell + 6, L.maxBorderX);
     const int R = maxY - iniY - 6, C = maxX - iniX - 6;
     const int npx = (R > 0 && C > 0) ? R * C : 0;
-    const uint8_t* smap = L.score + f * L.blur_frame_stride + (size_t)(iniY + 3) * L.w + (iniX + 3);
+    const uint8_t* smap = L.score + f * L.blur_frame_stride + (size_t)(iniY + 3) * L.bpitch + (iniX + 3);
     const float invC = 1.f / (float)max(C, 1);   // p / C exactly for p < 2^12
     for (int p0 = 0; p0 < npx; p0 += 256) {
         uint8_t v[4];
@@ -267,7 +299,7 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __
             v[k] = 0;
             if (p < npx) {
                 const int r = (int)(((float)p + 0.5f) * invC), c = p - r * C;
-                v[k] = smap[(size_t)r * L.w + c];
+                v[k] = smap[(size_t)r * L.bpitch + c];
             }
         }
 #pragma unroll
@@ -740,7 +772,7 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
     float sb, ca;
     glibc_sincosf(angle * factorPI, &sb, &ca);
     const uint8_t* bimg = L.blur + f * L.blur_frame_stride;
-    const uint8_t* bc = bimg + (size_t)kp.y * L.w + kp.x;
+    const uint8_t* bc = bimg + (size_t)kp.y * L.bpitch + kp.x;
     const size_t o = (size_t)f * cap_per_frame + off + i;
     uint64_t* dd = reinterpret_cast<uint64_t*>(out_desc + o * 32);
 #pragma unroll
@@ -752,7 +784,7 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
             const float x = (float)c_pattern[4 * tst + 2 * e], y = (float)c_pattern[4 * tst + 2 * e + 1];
             const int r = cv_round(__builtin_fmaf(x, sb, y * ca));
             const int c = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
-            val[e] = bc[r * L.w + c];
+            val[e] = bc[r * L.bpitch + c];
         }
         const unsigned long long m = __ballot(val[0] < val[1]);
         if (lane == 0) dd[k] = m;

@@ -228,14 +228,17 @@ const char* build_geom(spslam_ctx* c) {
         keyb += L.nCols * L.nRows * kCellCap;
         L.scale = c->scale[l];
         L.patch_size = (int)(31 * c->scale[l]);
+        // pitched rows (multiple of 64 bytes): level_kernel writes 4 pixels per dword store, its 64-wide
+        // tiles never cross a row's padded end
+        L.bpitch = (L.w + kLevelTileW - 1) / kLevelTileW * kLevelTileW;
         if (l > 0) {
-            L.stride = L.w;
+            L.stride = L.bpitch;
             L.img = reinterpret_cast<const uint8_t*>(pyr);  // offset, rebased after allocation
-            pyr += (long long)L.w * L.h;
+            pyr += (long long)L.stride * L.h;
         }
         L.blur = reinterpret_cast<uint8_t*>(blur);
         L.score = reinterpret_cast<uint8_t*>(blur);
-        blur += (long long)L.w * L.h;
+        blur += (long long)L.bpitch * L.h;
         L.tiles_x = (L.w + kLevelTileW - 1) / kLevelTileW;
         g.level_tiles[l] = L.tiles_x * ((L.h + kLevelTileH - 1) / kLevelTileH);
         if (l > 0) {
@@ -1394,7 +1397,7 @@ int spslam_orb_debug_stage(spslam_ctx* c, int frame, int level, int stage, void*
             pitch = level == 0 ? c->last_stride : L.stride;
         } else {
             src = L.blur + (size_t)frame * L.blur_frame_stride;
-            pitch = L.w;
+            pitch = L.bpitch;
         }
         HIP_CHECK(c, hipMemcpy2D(out, L.w, src, pitch, L.w, L.h, hipMemcpyDeviceToHost));
         if (n) *n = L.w * L.h;
