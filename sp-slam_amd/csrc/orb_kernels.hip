@@ -366,17 +366,22 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __
 // reaches N with one scan instead of one division at a time.
 constexpr int kFlagNoMore = 1, kFlagToExp = 2;
 
+// NC = node capacity: the list never exceeds the level's kp_cap (N + 16; the main loop only runs a
+// pass when L + 3 * nToExpand <= N, the final phase stops at >= N), so the launcher picks the
+// smallest instance that holds every level -- 256 for nFeatures = 1000 (25 KB of LDS, 6 workgroups
+// per CU) instead of 1024 (77 KB, 2 per CU).
+template <int NC>
 struct OctShared {
-    short x0[2][kNodeCap], y0[2][kNodeCap], x1[2][kNodeCap], y1[2][kNodeCap];
-    int cnt[2][kNodeCap];
-    int seq[2][kNodeCap];
-    uint8_t flags[2][kNodeCap];
-    uint8_t div[kNodeCap];
-    int c4[kNodeCap][4];   // child counts, then child positions (-1 = empty)
-    int sa[kNodeCap];      // scan scratch
-    int sb[kNodeCap];      // scan scratch / remap
-    int sc[kNodeCap];      // scan scratch / sort
-    int cand[kNodeCap];
+    short x0[2][NC], y0[2][NC], x1[2][NC], y1[2][NC];
+    int cnt[2][NC];
+    int seq[2][NC];
+    uint8_t flags[2][NC];
+    uint8_t div[NC];
+    int c4[NC][4];   // child counts, then child positions (-1 = empty)
+    int sa[NC];      // scan scratch
+    int sb[NC];      // scan scratch / remap
+    int sc[NC];      // scan scratch / sort
+    int cand[NC];
     int cellpre[2048];
     int wsum[4];
     int misc[8];
@@ -432,7 +437,8 @@ __device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1
 // Rebuild the list after dividing the nodes flagged in S.div (proc rank of a
 // divided node in S.sb[node] = position in division order, P_c prefix in
 // S.sa[node]).  T = number of children pushed.  Returns the new length.
-__device__ int rebuild_list(OctShared& S, int cur, int L, int T, int seqc, const uint32_t* keys, uint16_t* keynode,
+template <int NC>
+__device__ int rebuild_list(OctShared<NC>& S, int cur, int L, int T, int seqc, const uint32_t* keys, uint16_t* keynode,
                             int C) {
     const int nb = cur ^ 1;
     // rank of non-divided nodes in list order
@@ -486,7 +492,8 @@ __device__ int rebuild_list(OctShared& S, int cur, int L, int T, int seqc, const
 }
 
 // Count the four children of every node with S.div set.
-__device__ void count_children(OctShared& S, int cur, int L, const uint32_t* keys, const uint16_t* keynode, int C) {
+template <int NC>
+__device__ void count_children(OctShared<NC>& S, int cur, int L, const uint32_t* keys, const uint16_t* keynode, int C) {
     for (int i = threadIdx.x; i < L; i += 256) S.c4[i][0] = S.c4[i][1] = S.c4[i][2] = S.c4[i][3] = 0;
     __syncthreads();
     for (int k = threadIdx.x; k < C; k += 256) {
@@ -501,11 +508,12 @@ __device__ void count_children(OctShared& S, int cur, int L, const uint32_t* key
     __syncthreads();
 }
 
+template <int NC>
 __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* __restrict__ cand,
                                                      const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
                                                      uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
                                                      int* __restrict__ lvl_cnt) {
-    __shared__ OctShared S;
+    __shared__ OctShared<NC> S;
     const int l = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
     const LevelGeom& Lg = g.lv[l];
     const int ncells = Lg.nRows * Lg.nCols;
@@ -842,7 +850,10 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
                        b.cand_cnt, iniTh, minTh);
     E(kKindFast);
     B(kKindOctree);
-    hipLaunchKernelGGL(octree_kernel, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
+    int maxcap = 0;
+    for (int l = 0; l < g.nlevels; l++) maxcap = max(maxcap, g.lv[l].kp_cap);
+    auto* octree = maxcap <= 256 ? octree_kernel<256> : octree_kernel<kNodeCap>;
+    hipLaunchKernelGGL(octree, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
                        b.lvl_kp, b.lvl_cnt);
     E(kKindOctree);
     B(kKindDesc);
