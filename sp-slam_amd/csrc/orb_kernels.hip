@@ -111,9 +111,8 @@ __device__ __forceinline__ RzCol resize_coef(double s, int d, int slen, bool hor
 
 // Necessary condition for a FAST-9 corner at threshold t: some 9-arc contains
 // two consecutive compass pixels (0, 4, 8, 12), both brighter or both darker.
-__device__ __forceinline__ bool fast_maybe(const uint8_t* p, int P, int t) {
-    const int v = p[0];
-    const int c0 = p[3 * P], c4 = p[3], c8 = p[-3 * P], c12 = p[-3];
+// v = centre; c0 = p[3P], c4 = p[3], c8 = p[-3P], c12 = p[-3].
+__device__ __forceinline__ bool fast_maybe_v(int v, int c0, int c4, int c8, int c12, int t) {
     const int hi = v + t, lo = v - t;
     const int b = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
     const int k = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
@@ -123,7 +122,7 @@ __device__ __forceinline__ bool fast_maybe(const uint8_t* p, int P, int t) {
 }
 
 __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
-    __shared__ uint8_t tin[kLH][kLW + 2];
+    __shared__ __attribute__((aligned(16))) uint8_t tin[kLH][kLW + 2];  // row pitch 72: dword-aligned rows
     __shared__ __attribute__((aligned(16))) uint16_t th[kLH][kLevelTileW];
     __shared__ RzCol rx[kLW], ry[kLH];
     __shared__ uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
@@ -196,11 +195,25 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             }
         }
     }
-    // horizontal blur pass over all tile rows
-    for (int q = t; q < kLH * kLevelTileW; q += kLevelThreads) {
-        const int r = q / kLevelTileW, c = q - r * kLevelTileW;
-        const uint8_t* p = &tin[r][c];
-        th[r][c] = (uint16_t)(18 * (p[0] + p[6]) + 34 * (p[1] + p[5]) + 48 * (p[2] + p[4]) + 56 * p[3]);
+    // horizontal blur pass over all tile rows, 4 outputs per lane from three dword LDS reads (bytes c..c+11)
+    for (int q = t; q < kLH * (kLevelTileW / 4); q += kLevelThreads) {
+        const int r = q / (kLevelTileW / 4), c = (q - r * (kLevelTileW / 4)) * 4;
+        const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&tin[r][c]);
+        const uint32_t a = w3[0], b = w3[1], d = w3[2];
+        int p[10];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            p[k] = (a >> (8 * k)) & 255;
+            p[4 + k] = (b >> (8 * k)) & 255;
+        }
+        p[8] = d & 255;
+        p[9] = (d >> 8) & 255;
+        uint16_t o[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            o[j] = (uint16_t)(18 * (p[j] + p[j + 6]) + 34 * (p[j + 1] + p[j + 5]) + 48 * (p[j + 2] + p[j + 4]) +
+                              56 * p[j + 3]);
+        *reinterpret_cast<uint2*>(&th[r][c]) = *reinterpret_cast<const uint2*>(o);
     }
     __syncthreads();
     uint8_t* blur = L.blur + f * L.blur_frame_stride;
@@ -224,11 +237,23 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         }
         if (y < h) *reinterpret_cast<uint32_t*>(blur + (size_t)y * bp + (x0 + lc)) = bw;
         *reinterpret_cast<uint32_t*>(&stile[r][lc]) = 0u;
+        // the FAST pre-test's 5 pixels for the 4 centres (tin[r+3][lc+3+j]): centre row bytes lc..lc+11
+        // and rows r, r+6 bytes lc+3..lc+6, from 7 dword LDS reads
+        const uint32_t* rc = reinterpret_cast<const uint32_t*>(&tin[r + 3][lc]);
+        const uint32_t* ru = reinterpret_cast<const uint32_t*>(&tin[r][lc]);
+        const uint32_t* rd = reinterpret_cast<const uint32_t*>(&tin[r + 6][lc]);
+        const uint32_t c0w = rc[0], c1w = rc[1], c2w = rc[2];
+        const uint32_t u0 = ru[0], u1 = ru[1], d0 = rd[0], d1 = rd[1];
+        auto byte_at = [](uint32_t a, uint32_t b, uint32_t c, int k) {  // byte k of the 12-byte a|b|c
+            return (int)(((k < 4 ? a : (k < 8 ? b : c)) >> (8 * (k & 3))) & 255);
+        };
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int x = x0 + lc + j;
-            const bool maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 &&
-                               fast_maybe(&tin[r + 3][lc + j + 3], kLW + 2, minTh);
+            const int v = byte_at(c0w, c1w, c2w, j + 3);
+            const int cu = byte_at(u0, u1, 0, j + 3), cd = byte_at(d0, d1, 0, j + 3);
+            const int cl = byte_at(c0w, c1w, c2w, j), cr = byte_at(c0w, c1w, c2w, j + 6);
+            const bool maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 && fast_maybe_v(v, cd, cr, cu, cl, minTh);
             const unsigned long long m = __ballot(maybe);
             if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(r * kLevelTileW + lc + j);
             ncand += __popcll(m);

@@ -140,7 +140,7 @@ struct Shared {
     double red[kThreads / 64][kRed];
     SE3 Eadd[12];                    // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
     SE3 Tp[12];                      // exp(+-1e-9 e_d) * T for the current iterate
-    double perr[kPlaneChunk][12][3]; // plane errors at the 12 perturbed poses
+    double perr[kPlaneChunk][13][3]; // plane errors at the 12 perturbed poses and at T
     double H[6][6], b[6], x[6];
     double lambda, ni, currentChi, iniChi, tempChi;
     SE3 T, T0, Ttrial, Tlast;
@@ -333,20 +333,30 @@ __global__ __launch_bounds__(kThreads) void pose_kernel(const spslam_pose_proble
                     __syncthreads();
                     for (int base = 0; base < nl; base += kPlaneChunk) {
                         const int cnt = min(kPlaneChunk, nl - base);
-                        for (int w = t; w < cnt * 12; w += kThreads) {
-                            const int j = w / 12, q = w - j * 12, e = np + base + j;
+                        // 13 evaluations per edge in parallel: the 12 perturbed poses and T itself (the
+                        // error the edge's own accumulation needs -- no second serial evaluation after the sync)
+                        for (int w = t; w < cnt * 13; w += kThreads) {
+                            const int j = w / 13, q = w - j * 13, e = np + base + j;
                             double err[3] = {0, 0, 0};
-                            if (!plout[e - np]) error_at(e, S.Tp[q], err, nullptr);
+                            if (!plout[e - np]) {
+                                const SE3& P = S.Tp[q < 12 ? q : 0];
+                                const bool pt = q < 12;
+                                SE3 Tq;  // field-wise select keeps both poses in registers
+                                Tq.r.w = pt ? P.r.w : T.r.w; Tq.r.x = pt ? P.r.x : T.r.x;
+                                Tq.r.y = pt ? P.r.y : T.r.y; Tq.r.z = pt ? P.r.z : T.r.z;
+                                Tq.t.x = pt ? P.t.x : T.t.x; Tq.t.y = pt ? P.t.y : T.t.y; Tq.t.z = pt ? P.t.z : T.t.z;
+                                error_at(e, Tq, err, nullptr);
+                            }
                             S.perr[j][q][0] = err[0]; S.perr[j][q][1] = err[1]; S.perr[j][q][2] = err[2];
                         }
                         __syncthreads();
                         for (int j = t; j < cnt; j += kThreads) {
                             const int e = np + base + j;
                             if (plout[e - np]) continue;
-                            double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
+                            double info[3], delta, J[3][6];
                             int dim;
                             edge_info(e, info, &delta, &dim);
-                            error_at(e, T, err, nullptr);
+                            const double err[3] = {S.perr[j][12][0], S.perr[j][12][1], S.perr[j][12][2]};
                             const double scalar = 1.0 / (2 * 1e-9);
 #pragma unroll
                             for (int d = 0; d < 6; d++)
