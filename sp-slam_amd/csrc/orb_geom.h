@@ -48,6 +48,19 @@ struct OrbGeom {
     int pad_[4];
 };
 
+// XCD-aware workgroup order.  MI355X dispatches consecutive workgroups of a
+// launch round-robin over its 8 XCDs, each with its own L2.  xcd_remap turns
+// the hardware id b of an n-workgroup 1-D launch into a logical id such that
+// every XCD runs one contiguous range of logical ids -- a kernel that derives
+// (frame, item) from the logical id then keeps each frame's reads on one L2.
+constexpr int kXcds = 8;
+#if defined(__HIPCC__)
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+    const int x = b % kXcds, local = b / kXcds, q = n / kXcds, r = n % kXcds;
+    return x * q + min(x, r) + local;  // XCD x owns q (+1 for x < r) consecutive logical ids
+}
+#endif
+
 // Intermediate per-level keypoint (DistributeOctTree output, level coordinates).
 struct LevelKp {
     uint16_t x, y;            // level pixel coordinates (integral in the reference)

@@ -762,8 +762,12 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
                                                    const int* __restrict__ lvl_cnt, spslam_keypoint* __restrict__ out_kp,
                                                    uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt,
                                                    int cap_per_frame) {
-    const int f = blockIdx.y, lane = threadIdx.x & 63;
-    const int slot = blockIdx.x * 4 + (threadIdx.x >> 6);
+    // 1-D launch of gx * frames workgroups in XCD-aware order: one frame's keypoints (and its level
+    // images / blurred levels, ~1.9 MB at 640x480) stay on one XCD's L2
+    const int gx = (g.lvl_kp_per_frame + 3) / 4;
+    const int lid = xcd_remap(blockIdx.x, gridDim.x);
+    const int f = lid / gx, lane = threadIdx.x & 63;
+    const int slot = (lid - f * gx) * 4 + (threadIdx.x >> 6);
     if (slot >= g.lvl_kp_per_frame) return;
     int l = 0;
     for (int k = 1; k < g.nlevels; k++)
@@ -882,7 +886,7 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
                        b.lvl_kp, b.lvl_cnt);
     E(kKindOctree);
     B(kKindDesc);
-    hipLaunchKernelGGL(desc_kernel, dim3((g.lvl_kp_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.lvl_kp, b.lvl_cnt,
+    hipLaunchKernelGGL(desc_kernel, dim3((g.lvl_kp_per_frame + 3) / 4 * n), dim3(256), 0, s, g, b.lvl_kp, b.lvl_cnt,
                        kps, desc, counts, cap_per_frame);
     E(kKindDesc);
     return hipGetLastError();
