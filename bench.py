@@ -92,8 +92,8 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "desc_kernel": n_kp * (28 + 32),                      # keypoint + descriptor out
         "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call
         "plane_cloud_kernel": 4 * N + 12 * N,                 # depth samples in, xyz out
-        "plane_distance_kernel": 4 * N + 4 * N,               # z in, distance map out
-        "plane_integral_kernel": 12 * N + 48 * IWH,           # xyz in, 6 fp64 integral images out
+        # xyz in, distance map + 6 fp64 integral images out (one fused wavefront kernel)
+        "plane_dist_integral_kernel": 12 * N + 4 * N + 48 * IWH,
         "plane_normal_kernel": 16 * N + 48 * IWH + 16 * N,    # xyz+dist, integral, normal+plane_d out
         "plane_segment_kernel": 28 * N + 4 * N,               # xyz+normal+plane_d in, labels out
         "supp_lines_kernel": n_con * (4 + 12 + 4) + n_brd * 1600,  # contour idx + xyz in, line idx out, border windows
@@ -209,6 +209,7 @@ def main():
     ap.add_argument("--unique-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
+    ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
     args = ap.parse_args()
@@ -228,6 +229,7 @@ def main():
     hp = pipeline.HotPath(args.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"],
                           unique_frames=args.unique_frames, device=local, lba_every=cfg.get("lba_every", 0),
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
+                          orb_priority=args.orb_priority,
                           **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()

@@ -856,8 +856,8 @@ hipError_t orb_upload_tables(const int umax[16]) {
 // frame_stride must already point at the caller's gray frames.
 const char* kernel_kind_name(int kind) {
     static const char* names[kNumKernelKinds] = {"level_kernel", "fast_cells_kernel", "octree_kernel",
-                                                 "desc_kernel", "pose_kernel", "plane_cloud_kernel", "plane_distance_kernel",
-                                                 "plane_integral_kernel", "plane_normal_kernel",
+                                                 "desc_kernel", "pose_kernel", "plane_cloud_kernel", "plane_dist_integral_kernel",
+                                                 "plane_integral_kernel (fused)", "plane_normal_kernel",
                                                  "plane_segment_kernel", "supp_lines_kernel",
                                                  "supp_assemble_kernel", "frame_rgbd_kernel",
                                                  "lba_batch", "plane_assoc_kernel", "search_projection",

@@ -2,12 +2,14 @@
 // (src/Frame.cc:854-936) and the PCL 1.8 routines it calls.
 //
 //   plane_cloud_kernel     organized cloud, stride Cloud.Dis (Frame.cc:857-874)
-//   plane_distance_kernel  depth-change map + PCL's two-pass chamfer distance
+//   plane_dist_integral_kernel
+//                          depth-change map + PCL's two-pass chamfer distance
 //                          transform, as two anti-diagonal wavefronts (one
-//                          wave lane per cloud row, slope 2): every cell sees
-//                          exactly the operands of the reference's raster scan
-//   plane_integral_kernel  PCL IntegralImage2D<float,3> of the x/y gradient
-//                          images, fp64, same recurrence order, wavefront t=r+c
+//                          lane per cloud row, slope 2): every cell sees
+//                          exactly the operands of the reference's raster scan;
+//                          PCL IntegralImage2D<float,3> of the x/y gradient
+//                          images (fp64, same recurrence order) rides along
+//                          in the first wavefront
 //   plane_normal_kernel    AVERAGE_3D_GRADIENT normals + flip to viewpoint,
 //                          plane_d = p . n (one thread per cloud point)
 //   plane_segment_kernel   (plane_segment.hip) connected components, models,
@@ -53,97 +55,173 @@ __device__ __forceinline__ float dist_init(const float* Z, int W, int H, int r, 
     return zero ? 0.0f : (float)(W + H);
 }
 
-__global__ __launch_bounds__(kWaveThreads) void plane_distance_kernel(PlaneGeom g, const float* __restrict__ cloud,
-                                                                      long long cloud_fs, float* dist,
-                                                                      long long dist_fs) {
-    __shared__ float ring[kWaveThreads][4];
-    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H;
-    const float* Z = cloud + f * cloud_fs + 2 * g.N;
-    float* D = dist + f * dist_fs;
-    // pass 1 (top-left to bottom-right), step s handles column c = s - 2r of row r
-    float left = 0.f;
-    const float row0 = r < H ? dist_init(Z, W, H, r, 0) : 0.f;
-    for (int s = 0; s < 2 * (H - 1) + W; s++) {
-        const int c = s - 2 * r;
-        if (r < H && c >= 0 && c < W) {
-            const float center = dist_init(Z, W, H, r, c);
-            float v = center;
-            if (r > 0 && c > 0) {
-                const float upLeft = ring[r - 1][(c - 1) & 3] + 1.4f;
-                const float up = ring[r - 1][c & 3] + 1.0f;
-                // c == W-1 reads previous_row[W] == this row's element 0 (PCL quirk)
-                const float upRight = (c + 1 < W ? ring[r - 1][(c + 1) & 3] : row0) + 1.4f;
-                const float lft = left + 1.0f;
-                const float mv = fminf(fminf(upLeft, up), fminf(lft, upRight));
-                if (mv < center) v = mv;
-            }
-            ring[r][c & 3] = v;
-            left = v;
-            D[r * W + c] = v;
-        }
-        __syncthreads();
-    }
-    // pass 2 (bottom-right to top-left): step s handles c = W-1 - (s - 2(H-1-r))
-    float right = 0.f;
-    const float lastcol = r < H ? D[r * W + W - 1] : 0.f;
-    for (int s = 0; s < 2 * (H - 1) + W; s++) {
-        const int c = W - 1 - (s - 2 * (H - 1 - r));
-        if (r < H && c >= 0 && c < W) {
-            const float center = D[r * W + c];
-            float v = center;
-            if (r < H - 1 && c < W - 1) {
-                // c == 0 reads next_row[-1] == this row's element W-1 (PCL quirk)
-                const float lowerLeft = (c > 0 ? ring[r + 1][(c - 1) & 3] : lastcol) + 1.4f;
-                const float lower = ring[r + 1][c & 3] + 1.0f;
-                const float lowerRight = ring[r + 1][(c + 1) & 3] + 1.4f;
-                const float rgt = right + 1.0f;
-                const float mv = fminf(fminf(lowerLeft, lower), fminf(rgt, lowerRight));
-                if (mv < center) v = mv;
-            }
-            ring[r][c & 3] = v;
-            right = v;
-            D[r * W + c] = v;
-        }
-        __syncthreads();
-    }
-}
+// Workgroup barrier that orders LDS only: global prefetches of the next wavefront step stay in flight
+// across it (nothing another lane reads goes through global memory inside these kernels).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__global__ __launch_bounds__(kWaveThreads) void plane_integral_kernel(PlaneGeom g, const float* __restrict__ cloud,
-                                                                      long long cloud_fs, double* integral,
-                                                                      long long integral_fs) {
-    __shared__ double ring[kWaveThreads][3][6];
-    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, N = g.N, IW = W + 1;
+// Pass-1 operands of every cell, written in the skewed layout (plane_launch.h): thread per skewed
+// entry, so the wavefront kernel reads one step's operands with coalesced loads (lane = row; in raster
+// layout the lanes of one step are a row pitch apart and every access is its own cache line).
+__global__ __launch_bounds__(256) void plane_wave_prep_kernel(PlaneGeom g, const float* __restrict__ cloud,
+                                                              long long cloud_fs, float* wave, long long wave_fs) {
+    const int W = g.W, H = g.H, N = g.N, HP = wave_pitch(H);
+    const long long SZ = wave_size(W, H);
+    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int st = (int)(t / HP), r = (int)(t - (long long)st * HP), c = st - 2 * r;
+    if (r >= H || c < 0 || c >= W) return;
+    const int f = blockIdx.y;
     const float* X = cloud + f * cloud_fs;
     const float* Y = X + N;
     const float* Z = X + 2 * N;
-    double* I = integral + f * integral_fs;
-    for (int c = threadIdx.x; c < IW; c += blockDim.x)
-        for (int k = 0; k < 6; k++) I[(size_t)c * 6 + k] = 0.0;  // integral row 0
-    if (r < H)
-        for (int k = 0; k < 6; k++) I[(size_t)(r + 1) * IW * 6 + k] = 0.0;  // column 0
-    double left[6] = {0, 0, 0, 0, 0, 0};
-    for (int s = 0; s < W + H - 1; s++) {
-        const int c = s - r;
-        if (r < H && c >= 0 && c < W) {
-            float e[6] = {0, 0, 0, 0, 0, 0};
-            if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
-                const int i = r * W + c;
-                e[0] = X[i + 1] - X[i - 1]; e[1] = Y[i + 1] - Y[i - 1]; e[2] = Z[i + 1] - Z[i - 1];
-                e[3] = X[i + W] - X[i - W]; e[4] = Y[i + W] - Y[i - W]; e[5] = Z[i + W] - Z[i - W];
-            }
-            double* out = &I[((size_t)(r + 1) * IW + c + 1) * 6];
+    float e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
+        const int i = r * W + c;
+        e[0] = X[i + 1] - X[i - 1]; e[1] = Y[i + 1] - Y[i - 1]; e[2] = Z[i + 1] - Z[i - 1];
+        e[3] = X[i + W] - X[i - W]; e[4] = Y[i + W] - Y[i - W]; e[5] = Z[i + W] - Z[i - W];
+    }
+    float* O = wave + f * wave_fs;
+    const long long o = wave_index(r, c, H);
+    O[o] = dist_init(Z, W, H, r, c);
 #pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const double up = r > 0 ? ring[r - 1][c % 3][k] : 0.0;
-                const double upleft = (r > 0 && c > 0) ? ring[r - 1][(c + 2) % 3][k] : 0.0;
-                double v = up + left[k] - upleft;
-                v += (double)e[k];
-                left[k] = v;
-                ring[r][c % 3][k] = v;
-                out[k] = v;
+    for (int k = 0; k < 6; k++) O[(k + 1) * SZ + o] = e[k];
+}
+
+// Depth-change distance map (PCL's two-pass chamfer transform) and the six fp64 integral images
+// (IntegralImage2D<float,3> of the x / y gradients) in one workgroup per frame.  Both are raster
+// recurrences replayed as anti-diagonal wavefronts, one lane per cloud row: the integral image's
+// recurrence (up, left, up-left) fits inside the distance pass 1 schedule (slope 2: row r-1 is two
+// columns ahead of row r), so both run in the same 2(H-1)+W barrier steps; a 4-column ring per row
+// holds what row r+1 still reads.  Pass 2 visits the cells in exactly the reverse order of pass 1, so
+// in the skewed layout both passes read and write one contiguous span per step.  Each lane loads the
+// operands of the next kWaveChunk steps while it works through the current ones (issued at the top of
+// the unrolled chunk, consumed at its bottom, so the compiler's wait covers only those loads, not the
+// stores in between); lanes outside the image compute on unused entries and keep their row state.
+// Every cell sees exactly the operands of the reference's raster scans: both outputs stay
+// bit-identical.
+template <int MAXR>
+__global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, const float* __restrict__ wave,
+                                                                   long long wave_fs, float* dist, long long dist_fs,
+                                                                   double* integral, long long integral_fs) {
+    constexpr int K = kWaveChunk;
+    // wave holds the 7 operand planes and, as plane 7, the skewed pass-1 distance map; the final
+    // distance map and the integral images are written in raster layout for the normal kernel
+    // slot-major rings: lane r touches consecutive LDS words
+    __shared__ float ring[4][MAXR];
+    __shared__ double iring[4][6][MAXR];
+    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, HP = wave_pitch(H), SK = wave_steps(W, H);
+    const long long SZ = wave_size(W, H);
+    const float* In = wave + f * wave_fs + r;
+    float* D = const_cast<float*>(In) + 7 * SZ;  // skewed pass-1 distance map (this lane's column)
+    float* Dout = dist + f * dist_fs + (long long)r * W;  // raster row r
+    const int IW = W + 1;
+    double* Iraw = integral + f * integral_fs;
+    for (int c = threadIdx.x; c < IW; c += blockDim.x)
+        for (int k = 0; k < 6; k++) Iraw[(size_t)c * 6 + k] = 0.0;  // integral row 0
+    if (r < H)
+        for (int k = 0; k < 6; k++) Iraw[(size_t)(r + 1) * IW * 6 + k] = 0.0;  // column 0
+    // raster integral entry (r+1, c+1) of this row; lanes beyond the cloud write into a dummy row
+    double* I = Iraw + (size_t)((r < H ? r : H) + 1) * IW * 6 + 6;
+    double* Idummy = Iraw + (size_t)(H + 1) * IW * 6;  // sink of the stores of cells outside the cloud
+    const bool row_ok = r < H;
+    const int rm = r > 0 ? r - 1 : 0, rp = r + 1 < MAXR ? r + 1 : r;  // neighbour rows (reads masked below)
+    struct Cell { float center, e[6]; };
+    auto load = [&](int st) {
+        Cell o;
+        const long long t = (long long)(st + K) * HP;
+        o.center = In[t];
+#pragma unroll
+        for (int k = 0; k < 6; k++) o.e[k] = In[(k + 1) * SZ + t];
+        return o;
+    };
+    // pass 1 (top-left to bottom-right), step s handles column c = s - 2r of row r
+    float left = 0.f;
+    double ileft[6] = {0, 0, 0, 0, 0, 0};
+    const float row0 = row_ok ? In[(long long)(2 * r + K) * HP] : 0.f;  // initial value of (r, 0)
+    auto step1 = [&](int s, const Cell& q) {
+        const int c = s - 2 * r;
+        const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
+        const float upLeft = ring[(c - 1) & 3][rm] + 1.4f;
+        const float up = ring[c & 3][rm] + 1.0f;
+        // c == W-1 reads previous_row[W] == this row's element 0 (PCL quirk)
+        const float upRight = (c + 1 < W ? ring[(c + 1) & 3][rm] : row0) + 1.4f;
+        const float lft = left + 1.0f;
+        const float mv = fminf(fminf(upLeft, up), fminf(lft, upRight));
+        const float v = inner && mv < q.center ? mv : q.center;
+        if (ok) {
+            ring[c & 3][r] = v;
+            left = v;
+        }
+        D[(long long)(s + K) * HP] = v;
+        double iv[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+            const double upI = r > 0 ? iring[c & 3][k][rm] : 0.0;
+            const double upleftI = inner ? iring[(c - 1) & 3][k][rm] : 0.0;
+            iv[k] = upI + ileft[k] - upleftI;
+            iv[k] += (double)q.e[k];
+            if (ok) {
+                ileft[k] = iv[k];
+                iring[c & 3][k][r] = iv[k];
             }
         }
-        __syncthreads();
+        {  // unconditional store (a branch around it would make the compiler's prefetch waits conservative)
+            double2* out = reinterpret_cast<double2*>(ok ? I + (long long)c * 6 : Idummy);
+            out[0] = make_double2(iv[0], iv[1]);
+            out[1] = make_double2(iv[2], iv[3]);
+            out[2] = make_double2(iv[4], iv[5]);
+        }
+    };
+    Cell cur[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) cur[j] = load(j);
+    for (int s0 = 0; s0 < SK; s0 += K) {
+        Cell nxt[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) nxt[j] = load(s0 + K + j);
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            step1(s0 + j, cur[j]);
+            lds_barrier();
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) cur[j] = nxt[j];
+    }
+    // pass 2 (bottom-right to top-left): iteration j visits the cells pass 1 visited at step SK-1-j
+    // (column c = W-1 - (s - 2(H-1-r)) of the reference's order, shifted by the padded steps); each lane
+    // reads back only the values it wrote itself
+    float right = 0.f;
+    const float lastcol = row_ok ? D[(long long)(W - 1 + 2 * r + K) * HP] : 0.f;
+    auto step2 = [&](int j, float center) {
+        const int st = SK - 1 - j, c = st - 2 * r;
+        const bool ok = row_ok && c >= 0 && c < W, inner = r < H - 1 && c < W - 1;
+        // c == 0 reads next_row[-1] == this row's element W-1 (PCL quirk)
+        const float lowerLeft = (c > 0 ? ring[(c - 1) & 3][rp] : lastcol) + 1.4f;
+        const float lower = ring[c & 3][rp] + 1.0f;
+        const float lowerRight = ring[(c + 1) & 3][rp] + 1.4f;
+        const float rgt = right + 1.0f;
+        const float mv = fminf(fminf(lowerLeft, lower), fminf(rgt, lowerRight));
+        const float v = inner && mv < center ? mv : center;
+        if (ok) {
+            ring[c & 3][r] = v;
+            right = v;
+        }
+        *(ok ? Dout + c : D + (long long)(st + K) * HP) = v;  // outside the cloud: this lane's consumed entry
+    };
+    auto dval = [&](int j) { return D[(long long)(SK - 1 - j + K) * HP]; };
+    float dcur[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) dcur[j] = dval(j);
+    for (int j0 = 0; j0 < SK; j0 += K) {
+        float dnxt[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) dnxt[j] = dval(j0 + K + j);
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            step2(j0 + j, dcur[j]);
+            lds_barrier();
+        }
+#pragma unroll
+        for (int j = 0; j < K; j++) dcur[j] = dnxt[j];
     }
 }
 
@@ -205,13 +283,17 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
     hipLaunchKernelGGL(plane_cloud_kernel, pts, dim3(256), 0, s, g, depth, depth_fs, depth_stride, b.cloud, b.cloud_fs);
     E(kKindPlaneCloud);
     B(kKindPlaneDist);
-    hipLaunchKernelGGL(plane_distance_kernel, dim3(n), dim3(kWaveThreads), 0, s, g, b.cloud, b.cloud_fs, b.dist,
-                       b.dist_fs);
+    // skewed entries of the real steps (the padding steps hold no cell)
+    const dim3 skew((unsigned)(((long long)(2 * (g.H - 1) + g.W) * wave_pitch(g.H) + 255) / 256), n);
+    {
+        hipLaunchKernelGGL(plane_wave_prep_kernel, skew, dim3(256), 0, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs);
+        const int rows = wave_pitch(g.H);
+        auto* k = g.H <= 192 ? plane_dist_integral_kernel<192>
+                             : g.H <= 320 ? plane_dist_integral_kernel<320> : plane_dist_integral_kernel<kWaveThreads>;
+        hipLaunchKernelGGL(k, dim3(n), dim3(rows), 0, s, g, b.wave, b.wave_fs, b.dist, b.dist_fs, b.integral,
+                           b.integral_fs);
+    }
     E(kKindPlaneDist);
-    B(kKindPlaneIntegral);
-    hipLaunchKernelGGL(plane_integral_kernel, dim3(n), dim3(kWaveThreads), 0, s, g, b.cloud, b.cloud_fs, b.integral,
-                       b.integral_fs);
-    E(kKindPlaneIntegral);
     B(kKindPlaneNormal);
     hipLaunchKernelGGL(plane_normal_kernel, pts, dim3(256), 0, s, g, b.cloud, b.cloud_fs, b.dist, b.dist_fs,
                        b.integral, b.integral_fs, b.normal, b.normal_fs, b.pd, b.pd_fs);

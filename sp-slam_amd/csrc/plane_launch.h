@@ -25,8 +25,11 @@ struct PlaneGeom {
 // Per-frame scratch, frame f at base + f * stride (element counts).
 struct PlaneBuffers {
     float* cloud;        // [F][3][N]  x | y | z planes
-    float* dist;         // [F][N]
-    double* integral;    // [F][(W+1)*(H+1)][6]  (dx xyz, dy xyz)
+    // wave: the wavefront kernel's skewed buffers (wave_index: one step's cells are contiguous),
+    // 7 pass-1 operand planes (initial distance, x / y gradients of xyz) + the pass-1 distance map
+    float* wave;         // [F][8][wave_size]
+    float* dist;         // [F][N]  distance map
+    double* integral;    // [F][(W+1)*(H+2)][6]  (dx xyz, dy xyz); row H+1 absorbs padding lanes
     float* normal;       // [F][3][N]
     float* pd;           // [F][N]  plane_d = p . n
     uint32_t* labels;    // [F][N]
@@ -34,8 +37,25 @@ struct PlaneBuffers {
     int* grown;          // [F][N] refinement grow events (target | model << 24), reference order
     uint8_t* maps;       // [F][2N] component tag / model map + contour masks (when not in LDS)
     long long* ts;       // [F][16] segmentation phase stamps (s_memrealtime, 100 MHz), diagnostics
-    long long cloud_fs, dist_fs, integral_fs, normal_fs, pd_fs, labels_fs, work_fs, grown_fs, maps_fs;
+    long long cloud_fs, wave_fs, dist_fs, integral_fs, normal_fs, pd_fs, labels_fs, work_fs, grown_fs, maps_fs;
 };
+
+// Skewed wavefront layout: entry (st, r) = cloud cell (r, c = st - 2r), the cell wavefront step st
+// visits in row r, at (st + kWaveChunk) * pitch + r.  pitch = H rounded up to a wave (every lane of
+// the wavefront workgroup owns an entry, so its loads and stores need no bounds test); steps are
+// padded to a multiple of kWaveChunk (the kernel's prefetch unit) plus one chunk of prefetch slack
+// on either side.
+constexpr int kWaveChunk = 8;
+__host__ __device__ inline int wave_pitch(int H) { return (H + 63) / 64 * 64; }
+__host__ __device__ inline int wave_steps(int W, int H) {
+    return (2 * (H - 1) + W + kWaveChunk - 1) / kWaveChunk * kWaveChunk;
+}
+__host__ __device__ inline long long wave_size(int W, int H) {
+    return (long long)(wave_steps(W, H) + 2 * kWaveChunk) * wave_pitch(H);
+}
+__host__ __device__ inline long long wave_index(int r, int c, int H) {
+    return (long long)(c + 2 * r + kWaveChunk) * wave_pitch(H) + r;
+}
 
 hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const float* depth, long long depth_fs,
                         int depth_stride, spslam_plane* planes, int* plane_counts, int planes_cap,

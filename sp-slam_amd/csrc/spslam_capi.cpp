@@ -582,9 +582,10 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     g.contour_cap = 4 * g.N;
     const long long N = g.N, F = c->p.max_batch, IWH = (long long)(g.W + 1) * (g.H + 1);
     PlaneBuffers& b = c->pb;
-    b.cloud_fs = 3 * N; b.dist_fs = N; b.integral_fs = 6 * IWH; b.normal_fs = 3 * N; b.pd_fs = N;
+    const long long SH = wave_size(g.W, g.H);
+    b.cloud_fs = 3 * N; b.wave_fs = 8 * SH; b.dist_fs = N; b.integral_fs = 6 * (IWH + g.W + 1); b.normal_fs = 3 * N; b.pd_fs = N;
     b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N; b.maps_fs = 2 * N;
-    const size_t bytes = F * (sizeof(float) * (b.cloud_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
+    const size_t bytes = F * (sizeof(float) * (b.cloud_fs + b.wave_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
                               sizeof(double) * b.integral_fs + sizeof(uint32_t) * b.labels_fs +
                               sizeof(int) * (b.work_fs + b.grown_fs) + b.maps_fs + 16 * sizeof(long long)) + 8192;
     if (c->d_plane_scratch) (void)hipFree(c->d_plane_scratch);
@@ -594,6 +595,7 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     auto carve = [&](size_t n) { uint8_t* r = q; q += (n + 255) / 256 * 256; return r; };
     b.integral = (double*)carve(F * b.integral_fs * sizeof(double));
     b.cloud = (float*)carve(F * b.cloud_fs * 4);
+    b.wave = (float*)carve(F * b.wave_fs * 4);
     b.dist = (float*)carve(F * b.dist_fs * 4);
     b.normal = (float*)carve(F * b.normal_fs * 4);
     b.pd = (float*)carve(F * b.pd_fs * 4);

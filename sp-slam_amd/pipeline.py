@@ -42,7 +42,7 @@ import synth
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, oracle_kps=None, lba_every=0, lba_unique=4, lba_points=1500,
-                 pipelined=False, tail_priority=True):
+                 pipelined=False, tail_priority=True, orb_priority=False):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -123,6 +123,7 @@ class HotPath:
         if self.n_lba:
             self._setup_lba(seq_id, lba_unique, lba_points)
         self.pipelined = pipelined
+        self.orb_priority = orb_priority
         if pipelined:
             self._setup_pipeline()
         torch.cuda.synchronize()  # buffers were filled on the default stream
@@ -416,7 +417,10 @@ class HotPath:
         torch = self.torch
         self.sets = [{k: getattr(self, k) for k in self.EXTRACTION_BUFFERS},
                      {k: torch.zeros_like(getattr(self, k)) for k in self.EXTRACTION_BUFFERS}]
-        self.ext_orb, self.ext_planes = torch.cuda.Stream(), torch.cuda.Stream()
+        # ORB extraction is the longest extraction chain; orb_priority lets its workgroups dispatch ahead of the
+        # plane chain's (the tracking tail keeps its high priority)
+        self.ext_orb = torch.cuda.Stream(priority=-1 if self.orb_priority else 0)
+        self.ext_planes = torch.cuda.Stream()
         self.ev_orb = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
