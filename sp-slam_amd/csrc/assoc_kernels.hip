@@ -16,6 +16,8 @@
 // -O3 -march=native): fma(a2, b2, fma(a0, b0, a1*b1)) (+ a3).
 #include <hip/hip_runtime.h>
 
+#include "wave_priority.h"
+
 #include "assoc_launch.h"
 
 namespace spslam {
@@ -52,6 +54,7 @@ __global__ __launch_bounds__(kThreads) void assoc_dist_kernel(const spslam_assoc
                                                               AssocSources S, const spslam_map_plane* __restrict__ map,
                                                               const float* __restrict__ boundary, int max_map,
                                                               float angle_th, float* __restrict__ dist) {
+    tail_wave_priority();
     __shared__ float pm_s[kGroup][4];
     __shared__ int idx_s[kGroup];
     __shared__ float red[kWaves][kGroup];
@@ -119,6 +122,7 @@ __global__ __launch_bounds__(64) void assoc_decide_kernel(const spslam_assoc_fra
                                                           const float* __restrict__ dist, int32_t* __restrict__ match,
                                                           int32_t* __restrict__ parallel,
                                                           int32_t* __restrict__ vertical, int* __restrict__ new_plane) {
+    tail_wave_priority();
     const int f = blockIdx.x;
     const spslam_assoc_frame& F = frames[f];
     int na, nb;

@@ -11,6 +11,8 @@
 // increasing keypoint index like the reference's push_back order.
 #include <hip/hip_runtime.h>
 
+#include "wave_priority.h"
+
 #include "frame_launch.h"
 
 namespace spslam {
@@ -47,6 +49,7 @@ __global__ __launch_bounds__(kThreads) void frame_rgbd_kernel(
     const float* __restrict__ depth, long long depth_fs, int stride, spslam_keypoint* __restrict__ keys_un,
     float* __restrict__ dout, float* __restrict__ urout, int32_t* __restrict__ grid_off,
     int32_t* __restrict__ grid_idx, int* __restrict__ plane_counts, int* __restrict__ supp_counts) {
+    tail_wave_priority();
     __shared__ int cnt[kCells];
     __shared__ int wsum[kThreads / 64];
     extern __shared__ int16_t cell_of[];  // [cap]

@@ -22,6 +22,8 @@
 // cv::Mat products are accumulated in double and rounded once (oracle header).
 #include <hip/hip_runtime.h>
 
+#include "wave_priority.h"
+
 #include "match_launch.h"
 
 namespace spslam {
@@ -90,6 +92,7 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
                                                                 int mono, int retry_below, int pass,
                                                                 const int* __restrict__ nmatches,
                                                                 MatchWindow* __restrict__ win) {
+    tail_wave_priority();
     const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
     const spslam_proj_frame& F = frames[f];
     if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
@@ -180,6 +183,7 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
                                                           int pass, const MatchWindow* __restrict__ win,
                                                           int2* __restrict__ pushes, int32_t* __restrict__ match,
                                                           int* __restrict__ nmatches) {
+    tail_wave_priority();
     extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
     __shared__ int hist[kHisto];
     __shared__ int ind[3];
@@ -323,6 +327,7 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
                                                                 LocalConsts P, const uint8_t* __restrict__ taken_in,
                                                                 LocalWindow* __restrict__ win,
                                                                 uint8_t* __restrict__ in_view) {
+    tail_wave_priority();
     const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
     const spslam_local_frame& F = frames[f];
     if (i >= F.n_points || i >= max_points) return;
@@ -420,6 +425,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                                                           const uint8_t* __restrict__ taken_in,
                                                           const LocalWindow* __restrict__ win,
                                                           int32_t* __restrict__ match, int* __restrict__ nmatches) {
+    tail_wave_priority();
     extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
     const int f = blockIdx.x, lane = threadIdx.x;
     const spslam_local_frame& F = frames[f];

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     __shared__ float ring[4][MAXR];
     __shared__ double iring[4][6][MAXR];
     const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, HP = wave_pitch(H), SK = wave_steps(W, H);
-    const long long SZ = wave_size(W, H);
+    const int SZ = (int)wave_size(W, H);  // per-frame offsets fit in 32 bits (planes: 8 x SZ)
     const float* In = wave + f * wave_fs + r;
     float* D = const_cast<float*>(In) + 7 * SZ;  // skewed pass-1 distance map (this lane's column)
     float* Dout = dist + f * dist_fs + (long long)r * W;  // raster row r
@@ -125,9 +125,12 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     const bool row_ok = r < H;
     const int rm = r > 0 ? r - 1 : 0, rp = r + 1 < MAXR ? r + 1 : r;  // neighbour rows (reads masked below)
     struct Cell { float center, e[6]; };
+    // steps where this lane has no cell read a fixed entry instead (an address select, not a branch:
+    // no HBM traffic for the skewed layout's empty entries, and the prefetch waits stay exact)
     auto load = [&](int st) {
         Cell o;
-        const long long t = (long long)(st + K) * HP;
+        const int c = st - 2 * r;
+        const int t = ((row_ok && c >= 0 && c < W ? st : 0) + K) * HP;
         o.center = In[t];
 #pragma unroll
         for (int k = 0; k < 6; k++) o.e[k] = In[(k + 1) * SZ + t];
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     // pass 1 (top-left to bottom-right), step s handles column c = s - 2r of row r
     float left = 0.f;
     double ileft[6] = {0, 0, 0, 0, 0, 0};
-    const float row0 = row_ok ? In[(long long)(2 * r + K) * HP] : 0.f;  // initial value of (r, 0)
+    const float row0 = row_ok ? In[(2 * r + K) * HP] : 0.f;  // initial value of (r, 0)
     auto step1 = [&](int s, const Cell& q) {
         const int c = s - 2 * r;
         const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             left = v;
         }
-        D[(long long)(s + K) * HP] = v;
+        D[(s + K) * HP] = v;
         double iv[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             }
         }
         {  // unconditional store (a branch around it would make the compiler's prefetch waits conservative)
-            double2* out = reinterpret_cast<double2*>(ok ? I + (long long)c * 6 : Idummy);
+            double2* out = reinterpret_cast<double2*>(ok ? I + c * 6 : Idummy);
             out[0] = make_double2(iv[0], iv[1]);
             out[1] = make_double2(iv[2], iv[3]);
             out[2] = make_double2(iv[4], iv[5]);
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     // (column c = W-1 - (s - 2(H-1-r)) of the reference's order, shifted by the padded steps); each lane
     // reads back only the values it wrote itself
     float right = 0.f;
-    const float lastcol = row_ok ? D[(long long)(W - 1 + 2 * r + K) * HP] : 0.f;
+    const float lastcol = row_ok ? D[(W - 1 + 2 * r + K) * HP] : 0.f;
     auto step2 = [&](int j, float center) {
         const int st = SK - 1 - j, c = st - 2 * r;
         const bool ok = row_ok && c >= 0 && c < W, inner = r < H - 1 && c < W - 1;
@@ -205,9 +208,12 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             right = v;
         }
-        *(ok ? Dout + c : D + (long long)(st + K) * HP) = v;  // outside the cloud: this lane's consumed entry
+        *(ok ? Dout + c : D + (st + K) * HP) = v;  // outside the cloud: this lane's consumed entry
     };
-    auto dval = [&](int j) { return D[(long long)(SK - 1 - j + K) * HP]; };
+    auto dval = [&](int j) {
+        const int st = SK - 1 - j, c = st - 2 * r;
+        return D[((row_ok && c >= 0 && c < W ? st : 0) + K) * HP];
+    };
     float dcur[K];
 #pragma unroll
     for (int j = 0; j < K; j++) dcur[j] = dval(j);

@@ -16,6 +16,8 @@
 // result matches the reference to rounding, not bitwise.
 #include <hip/hip_runtime.h>
 
+#include "wave_priority.h"
+
 #include "../../include/spslam_gpu.h"
 #include "g2o_device.h"
 #include "pose_launch.h"
@@ -191,6 +193,7 @@ __global__ __launch_bounds__(kThreads) void pose_kernel(const spslam_pose_proble
                                                    const spslam_pose_result* __restrict__ init_from,
                                                    spslam_pose_result* __restrict__ results,
                                                    uint8_t* __restrict__ pout_all, uint8_t* __restrict__ plout_all) {
+    tail_wave_priority();
     __shared__ Shared S;
     const int t = threadIdx.x;
     const spslam_pose_problem P = probs[blockIdx.x];

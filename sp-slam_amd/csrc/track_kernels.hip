@@ -13,6 +13,8 @@
 // a few microseconds per batch); no arithmetic touches the values it moves.
 #include <hip/hip_runtime.h>
 
+#include "wave_priority.h"
+
 #include "track_launch.h"
 
 namespace spslam {
@@ -27,6 +29,7 @@ __device__ __forceinline__ const float* plane_coef(const spslam_track_batch& B, 
 }
 
 __global__ __launch_bounds__(kThreads) void track_graph_kernel(TrackArgs A, int stage) {
+    tail_wave_priority();
     const spslam_track_batch& B = A.b;
     const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     __shared__ int wsum[kThreads / 64];

@@ -1,0 +1,24 @@
+// Issue priority of the tracking tail's waves.
+//
+// In the pipelined step the tracking tail (frame steps, matching, association,
+// graphs, PoseOptimization: one latency-bound workgroup per frame, barrier
+// after barrier) shares every CU with the next batch's ORB and plane
+// extraction (wide, high-occupancy kernels).  The HIP stream priority only
+// orders workgroup dispatch; once resident, a tail wave competes for issue
+// slots with the extraction waves on its SIMD and every dependent step of its
+// chain stretches.  s_setprio raises the wave's issue priority in the SIMD
+// arbiter so the chain advances first and the extraction waves fill the gaps.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#ifndef SPSLAM_TAIL_PRIO
+#define SPSLAM_TAIL_PRIO 1
+#endif
+
+namespace spslam {
+__device__ __forceinline__ void tail_wave_priority() {
+#if SPSLAM_TAIL_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
+}
+}  // namespace spslam
