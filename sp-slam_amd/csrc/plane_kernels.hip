@@ -45,13 +45,14 @@ __device__ __forceinline__ bool dc_bad(float za, float zb) {
     return fabsf(za - zb) > thr || !isfinite(za) || !isfinite(zb);
 }
 
-// Initial distance-map value of cell (r, c): 0 where the depth-change map is 0.
-__device__ __forceinline__ float dist_init(const float* Z, int W, int H, int r, int c) {
-    const int i = r * W + c;
+// Initial distance-map value of cell (r, c): 0 where the depth-change map is 0.  z(r, c) reads the
+// cloud's z.
+template <class ZAt>
+__device__ __forceinline__ float dist_init(ZAt z, int W, int H, int r, int c) {
     bool zero = false;
-    if (r < H - 1 && c < W - 1) zero = dc_bad(Z[i], Z[i + 1]) || dc_bad(Z[i], Z[i + W]);
-    if (r < H - 1 && c >= 1) zero = zero || dc_bad(Z[i - 1], Z[i]);
-    if (r >= 1 && c < W - 1) zero = zero || dc_bad(Z[i - W], Z[i]);
+    if (r < H - 1 && c < W - 1) zero = dc_bad(z(r, c), z(r, c + 1)) || dc_bad(z(r, c), z(r + 1, c));
+    if (r < H - 1 && c >= 1) zero = zero || dc_bad(z(r, c - 1), z(r, c));
+    if (r >= 1 && c < W - 1) zero = zero || dc_bad(z(r - 1, c), z(r, c));
     return zero ? 0.0f : (float)(W + H);
 }
 
@@ -59,31 +60,47 @@ __device__ __forceinline__ float dist_init(const float* Z, int W, int H, int r, 
 // across it (nothing another lane reads goes through global memory inside these kernels).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Pass-1 operands of every cell, written in the skewed layout (plane_launch.h): thread per skewed
-// entry, so the wavefront kernel reads one step's operands with coalesced loads (lane = row; in raster
-// layout the lanes of one step are a row pitch apart and every access is its own cache line).
+// Pass-1 operands of every cell, written in the skewed layout (plane_launch.h) so the wavefront
+// kernel reads one step's operands with coalesced loads.  One workgroup per band of RB cloud rows:
+// the band (+1 row either side) is staged in LDS with coalesced row reads, then the band's skewed
+// entries are written step by step, RB consecutive rows = one contiguous run per step.
+template <int RB>
 __global__ __launch_bounds__(256) void plane_wave_prep_kernel(PlaneGeom g, const float* __restrict__ cloud,
                                                               long long cloud_fs, float* wave, long long wave_fs) {
-    const int W = g.W, H = g.H, N = g.N, HP = wave_pitch(H);
-    const long long SZ = wave_size(W, H);
-    const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
-    const int st = (int)(t / HP), r = (int)(t - (long long)st * HP), c = st - 2 * r;
-    if (r >= H || c < 0 || c >= W) return;
-    const int f = blockIdx.y;
+    extern __shared__ float band[];  // [3][RB + 2][W]: x | y | z of rows rlo .. rhi-1
+    const int W = g.W, H = g.H, N = g.N;
+    const int SZ = (int)wave_size(W, H);
+    const int f = blockIdx.y, r0 = blockIdx.x * RB;
+    const int rlo = max(r0 - 1, 0), rhi = min(r0 + RB + 1, H), BP = (RB + 2) * W;
     const float* X = cloud + f * cloud_fs;
-    const float* Y = X + N;
-    const float* Z = X + 2 * N;
-    float e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
-        const int i = r * W + c;
-        e[0] = X[i + 1] - X[i - 1]; e[1] = Y[i + 1] - Y[i - 1]; e[2] = Z[i + 1] - Z[i - 1];
-        e[3] = X[i + W] - X[i - W]; e[4] = Y[i + W] - Y[i - W]; e[5] = Z[i + W] - Z[i - W];
+    for (int q = threadIdx.x; q < (rhi - rlo) * W; q += 256) {
+        const int i = rlo * W + q;
+        band[q] = X[i];
+        band[BP + q] = X[N + i];
+        band[2 * BP + q] = X[2 * N + i];
     }
+    __syncthreads();
+    auto at = [&](int k, int r, int c) { return band[k * BP + (r - rlo) * W + c]; };
+    auto zat = [&](int r, int c) { return at(2, r, c); };
     float* O = wave + f * wave_fs;
-    const long long o = wave_index(r, c, H);
-    O[o] = dist_init(Z, W, H, r, c);
+    const int nst = 2 * (RB - 1) + W;  // steps that visit a cell of the band
+    for (int q = threadIdx.x; q < nst * RB; q += 256) {
+        const int j = q / RB, rr = q - j * RB;
+        const int r = r0 + rr, c = 2 * r0 + j - 2 * r;
+        if (r >= H || c < 0 || c >= W) continue;
+        float e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
 #pragma unroll
-    for (int k = 0; k < 6; k++) O[(k + 1) * SZ + o] = e[k];
+            for (int k = 0; k < 3; k++) {
+                e[k] = at(k, r, c + 1) - at(k, r, c - 1);
+                e[3 + k] = at(k, r + 1, c) - at(k, r - 1, c);
+            }
+        }
+        const int o = (int)wave_index(r, c, H);
+        O[o] = dist_init(zat, W, H, r, c);
+#pragma unroll
+        for (int k = 0; k < 6; k++) O[(k + 1) * SZ + o] = e[k];
+    }
 }
 
 // Depth-change distance map (PCL's two-pass chamfer transform) and the six fp64 integral images
@@ -289,10 +306,12 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
     hipLaunchKernelGGL(plane_cloud_kernel, pts, dim3(256), 0, s, g, depth, depth_fs, depth_stride, b.cloud, b.cloud_fs);
     E(kKindPlaneCloud);
     B(kKindPlaneDist);
-    // skewed entries of the real steps (the padding steps hold no cell)
-    const dim3 skew((unsigned)(((long long)(2 * (g.H - 1) + g.W) * wave_pitch(g.H) + 255) / 256), n);
     {
-        hipLaunchKernelGGL(plane_wave_prep_kernel, skew, dim3(256), 0, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs);
+        // 16-row bands while the staged band fits 64 KB of LDS, else 8-row bands
+        const int rb = 3 * 18 * g.W * 4 <= 65536 ? 16 : 8;
+        const size_t lds = (size_t)3 * (rb + 2) * g.W * 4;
+        hipLaunchKernelGGL(rb == 16 ? plane_wave_prep_kernel<16> : plane_wave_prep_kernel<8>,
+                           dim3((g.H + rb - 1) / rb, n), dim3(256), lds, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs);
         const int rows = wave_pitch(g.H);
         auto* k = g.H <= 192 ? plane_dist_integral_kernel<192>
                              : g.H <= 320 ? plane_dist_integral_kernel<320> : plane_dist_integral_kernel<kWaveThreads>;

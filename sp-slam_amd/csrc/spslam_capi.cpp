@@ -574,6 +574,7 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     g.N = g.W * g.H;
     if (g.H > 512) return fail(c, SPSLAM_ERR_ARG, "organized cloud taller than 512 rows%s", "");
     if (g.N > 160000) return fail(c, SPSLAM_ERR_ARG, "organized cloud larger than the LDS state map%s", "");
+    if (3 * 10 * g.W * 4 > 65536) return fail(c, SPSLAM_ERR_ARG, "organized cloud wider than the LDS row band%s", "");
     g.fx = p->fx; g.fy = p->fy; g.cx = p->cx; g.cy = p->cy;
     g.min_size = p->min_size;
     g.ang_cos = std::cos((float)(0.017453 * p->angle_threshold));  // cosf(static_cast<float>(0.017453*AngTh))
