@@ -11,7 +11,10 @@
 // worst case).  RANSAC is run speculatively in rounds of kBatch trials:
 //   - wave 0 replays the sampler (drawIndexSample's partial Fisher-Yates on
 //     the persistent shuffled_indices_, isSampleGood retries); the 64 lanes
-//     fetch and reduce 32 draw pairs at a time, the swap chain is uniform;
+//     fetch and reduce 32 draw pairs at a time and the uniform swap chain
+//     applies them (the swaps are the same whichever pairs isSampleGood
+//     rejects), then the 32 pairs' isSampleGood tests run in parallel and
+//     the good ones become trials in order;
 //   - all waves count each trial's inliers (wave per trial, lanes over points);
 //   - one lane replays computeModel's best/k bookkeeping in trial order and
 //     stops exactly where the reference loop stops; trials sampled beyond that
@@ -276,33 +279,60 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
             __syncthreads();
             const double one_over_n = 1.0 / (double)n, log_prob = log(1.0 - 0.99);
             int r0 = 0, r1 = 1;   // shuffled_indices_[0], [1] (kept in registers by wave 0)
-            uint32_t pos = 0;     // draws consumed
+            uint32_t pos = 0;     // draws applied to the shuffle state
+            // Draw pairs already applied, not yet consumed by a trial: pair qh..qn-1 of the last block of 32,
+            // lane c holding pair c's sample (bp0, bp1); gmask = its isSampleGood bits.
+            int bp0 = 0, bp1 = 0, qh = 0, qn = 0;
+            uint64_t gmask = 0;
             while (!S.done) {
                 if (wave == 0) {
                     const int it0 = S.iterations;
-                    int nb = 0;
+                    int nb = 0, chk = 0;  // chk: failed samples of the trial being drawn
                     bool fail = false;
                     while (nb < kBatch && it0 + nb < kMaxTrials) {
-                        bool got = false;
-                        for (int chk = 0; chk < 1000 && !got;) {
+                        if (qh == qn) {
+                            // apply the next 32 draw pairs to the shuffle state: their swaps do not depend on
+                            // whether a pair becomes a trial's sample, so isSampleGood is checked afterwards,
+                            // for all 32 pairs at once (the chain keeps one LDS round trip per pair)
                             const uint32_t r = sb.rnd[pos + lane];
                             const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
-                            int c = 0;
-                            while (c < 32 && chk + c < 1000) {
+                            pos += 64;
+                            for (int c = 0; c < 32; c++) {
                                 const int j0 = __shfl((int)jv, 2 * c), j1 = __shfl((int)jv, 2 * c + 1);
-                                if (j0 == 1) { const int x = r0; r0 = r1; r1 = x; }
-                                else if (j0 > 1) { const int x = sh[j0]; sh[j0] = r0; r0 = x; }
-                                if (j1 > 1) { const int x = sh[j1]; sh[j1] = r1; r1 = x; }
-                                c++;
-                                const float4 a = Q[r0], b = Q[r1];
-                                if (a.x != b.x && a.y != b.y && a.z != b.z) { got = true; break; }
+                                const int x0 = j0 > 1 ? sh[j0] : 0, x1 = j1 > 1 ? sh[j1] : 0;
+                                const int a0 = r0;
+                                if (j0 == 1) { r0 = r1; r1 = a0; }
+                                else if (j0 > 1) { sh[j0] = a0; r0 = x0; }
+                                if (j1 > 1) {
+                                    const int v = j1 == j0 ? a0 : x1;  // j1 == j0: the value the first swap stored
+                                    sh[j1] = r1;
+                                    r1 = v;
+                                }
+                                if (lane == c) { bp0 = r0; bp1 = r1; }
                             }
-                            pos += 2 * c;
-                            chk += c;
+                            bool good = false;
+                            if (lane < 32) {
+                                const float4 a = Q[bp0], b = Q[bp1];
+                                good = a.x != b.x && a.y != b.y && a.z != b.z;
+                            }
+                            gmask = __ballot(good);
+                            qh = 0;
+                            qn = 32;
                         }
-                        if (!got) { fail = true; break; }
-                        if (lane == 0) { S.s0[nb] = r0; S.s1[nb] = r1; }
+                        const uint64_t m = gmask & (~0ull << qh) & 0xFFFFFFFFull;
+                        if (m == 0) {  // the rest of the block failed isSampleGood
+                            chk += qn - qh;
+                            qh = qn;
+                            if (chk >= 1000) { fail = true; break; }
+                            continue;
+                        }
+                        const int gi = __ffsll((unsigned long long)m) - 1;
+                        if (chk + (gi - qh) >= 1000) { fail = true; break; }  // 1000 failed samples first
+                        const int s0v = __shfl(bp0, gi), s1v = __shfl(bp1, gi);
+                        if (lane == 0) { S.s0[nb] = s0v; S.s1[nb] = s1v; }
                         nb++;
+                        chk = 0;
+                        qh = gi + 1;
                     }
                     if (lane == 0) { S.nb = nb; S.fail = fail; }
                 }
