@@ -260,10 +260,12 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
             continue;
         }
         const bool in_lds = bsize <= kLdsPts;
-        float4* Q = in_lds ? Qs : sb.big + (size_t)f * g.contour_cap + coff;
-        int* sh = in_lds ? shs : sb.big_sh + (size_t)f * g.contour_cap + coff;
-        uint8_t* flag = in_lds ? flags_s : sb.big_flag + (size_t)f * g.contour_cap + coff;
         int32_t* lidx = sb.line_idx + (size_t)f * g.contour_cap + coff;
+        // The boundary's points, shuffle state and flags live in LDS (or, for big boundaries, in HBM
+        // scratch): the body is instantiated once per case, so the LDS case compiles to ds_* accesses
+        // (one pointer selected at run time would make every access a flat one, waited on by both the
+        // vector-memory and the LDS counters).
+        auto boundary = [&](float4* Q, int* sh, uint8_t* flag) __attribute__((always_inline)) -> int {
         for (int i = t; i < bsize; i += kThreads) {
             const int ci = con[coff + i];
             Q[i] = make_float4(X[ci], Y[ci], Z[ci], __int_as_float(ci));
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                             const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
                             pos += 64;
                             for (int c = 0; c < 32; c++) {
-                                const int j0 = __shfl((int)jv, 2 * c), j1 = __shfl((int)jv, 2 * c + 1);
+                                const int j0 = __builtin_amdgcn_readlane((int)jv, 2 * c), j1 = __builtin_amdgcn_readlane((int)jv, 2 * c + 1);
                                 const int x0 = j0 > 1 ? sh[j0] : 0, x1 = j1 > 1 ? sh[j1] : 0;
                                 const int a0 = r0;
                                 if (j0 == 1) { r0 = r1; r1 = a0; }
@@ -328,7 +330,7 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                         }
                         const int gi = __ffsll((unsigned long long)m) - 1;
                         if (chk + (gi - qh) >= 1000) { fail = true; break; }  // 1000 failed samples first
-                        const int s0v = __shfl(bp0, gi), s1v = __shfl(bp1, gi);
+                        const int s0v = __builtin_amdgcn_readlane(bp0, gi), s1v = __builtin_amdgcn_readlane(bp1, gi);
                         if (lane == 0) { S.s0[nb] = s0v; S.s1[nb] = s1v; }
                         nb++;
                         chk = 0;
@@ -470,6 +472,12 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
             n = kbase;
             __syncthreads();
         }
+            return ncand;
+        };
+        const int ncand = in_lds ? boundary(Qs, shs, flags_s)
+                                 : boundary(sb.big + (size_t)f * g.contour_cap + coff,
+                                            sb.big_sh + (size_t)f * g.contour_cap + coff,
+                                            sb.big_flag + (size_t)f * g.contour_cap + coff);
         if (t == 0) sb.n_cand[f * kMaxPlanesPerFrame + q] = ncand;
         __syncthreads();
     }
