@@ -286,6 +286,7 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
             // lane c holding pair c's sample (bp0, bp1); gmask = its isSampleGood bits.
             int bp0 = 0, bp1 = 0, qh = 0, qn = 0;
             uint64_t gmask = 0;
+            uint32_t rnext = wave == 0 ? sb.rnd[lane] : 0u;  // next block's draws, loaded one block ahead
             while (!S.done) {
                 if (wave == 0) {
                     const int it0 = S.iterations;
@@ -296,9 +297,10 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                             // apply the next 32 draw pairs to the shuffle state: their swaps do not depend on
                             // whether a pair becomes a trial's sample, so isSampleGood is checked afterwards,
                             // for all 32 pairs at once (the chain keeps one LDS round trip per pair)
-                            const uint32_t r = sb.rnd[pos + lane];
+                            const uint32_t r = rnext;
                             const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
                             pos += 64;
+                            rnext = sb.rnd[pos + lane];  // (the table holds one block beyond the worst case)
                             for (int c = 0; c < 32; c++) {
                                 const int j0 = __builtin_amdgcn_readlane((int)jv, 2 * c), j1 = __builtin_amdgcn_readlane((int)jv, 2 * c + 1);
                                 const int x0 = j0 > 1 ? sh[j0] : 0, x1 = j1 > 1 ? sh[j1] : 0;
