@@ -812,40 +812,59 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         float* st = &S.stage[wave][0][0];
         float acc = 0.f;
         int found = 0;
-        int base = S.big_root[j] & ~63;
-        float cx = 0.f, cy = 0.f, cz = 0.f;
-        if (base + lane < N) { cx = X[base + lane]; cy = Y[base + lane]; cz = Z[base + lane]; }
-        for (; found < n && base < N; base += 64) {
-            const int i = base + lane;
-            float nx = 0.f, ny = 0.f, nz = 0.f;
-            if (i + 64 < N) { nx = X[i + 64]; ny = Y[i + 64]; nz = Z[i + 64]; }
-            const bool m = i < N && state[i] == tag;
-            const uint64_t mk = __ballot(m);
-            if (mk) {
-                const int cnt = __popcll(mk), pos = __popcll(mk & lanemask_lt()), pad = (cnt + 3) & ~3;
-                if (m) {
-                    members[o + found + pos] = i;
-                    st[0 * 64 + pos] = cx * cx; st[1 * 64 + pos] = cx * cy; st[2 * 64 + pos] = cx * cz;
-                    st[3 * 64 + pos] = cy * cy; st[4 * 64 + pos] = cy * cz; st[5 * 64 + pos] = cz * cz;
-                    st[6 * 64 + pos] = cx; st[7 * 64 + pos] = cy; st[8 * 64 + pos] = cz;
-                }
-                if (lane >= cnt && lane < pad)
-                    for (int q = 0; q < 9; q++) st[q * 64 + lane] = 0.f;
-                wave_sync();
-                if (lane < 9) {
-                    const float4* row = (const float4*)(st + lane * 64);
-                    for (int q = 0; q < (pad >> 2); q++) {
-                        const float4 v = row[q];
-                        acc += v.x;
-                        acc += v.y;
-                        acc += v.z;
-                        acc += v.w;
-                    }
-                }
-                wave_sync();
-                found += cnt;
+        // the cloud is scanned in chunks of 64 points from the region's first member; coordinates are
+        // loaded one group of 4 chunks ahead (consumed from registers of the group before, so the wait
+        // for them does not cover the chunks' member-list stores)
+        const int start = S.big_root[j] & ~63;
+        float cx[4], cy[4], cz[4];
+        auto load_group = [&](int b0, float* gx, float* gy, float* gz) __attribute__((always_inline)) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = b0 + 64 * u + lane;
+                gx[u] = i < N ? X[i] : 0.f;
+                gy[u] = i < N ? Y[i] : 0.f;
+                gz[u] = i < N ? Z[i] : 0.f;
             }
-            cx = nx; cy = ny; cz = nz;
+        };
+        load_group(start, cx, cy, cz);
+        for (int b0 = start; found < n && b0 < N; b0 += 256) {
+            float nx[4], ny[4], nz[4];
+            load_group(b0 + 256, nx, ny, nz);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int base = b0 + 64 * u;
+                if (found >= n || base >= N) continue;
+                const int i = base + lane;
+                const bool m = i < N && state[i] == tag;
+                const uint64_t mk = __ballot(m);
+                if (mk) {
+                    const int cnt = __popcll(mk), pos = __popcll(mk & lanemask_lt()), pad = (cnt + 3) & ~3;
+                    if (m) {
+                        const float px = cx[u], py = cy[u], pz = cz[u];
+                        members[o + found + pos] = i;
+                        st[0 * 64 + pos] = px * px; st[1 * 64 + pos] = px * py; st[2 * 64 + pos] = px * pz;
+                        st[3 * 64 + pos] = py * py; st[4 * 64 + pos] = py * pz; st[5 * 64 + pos] = pz * pz;
+                        st[6 * 64 + pos] = px; st[7 * 64 + pos] = py; st[8 * 64 + pos] = pz;
+                    }
+                    if (lane >= cnt && lane < pad)
+                        for (int q = 0; q < 9; q++) st[q * 64 + lane] = 0.f;
+                    wave_sync();
+                    if (lane < 9) {
+                        const float4* row = (const float4*)(st + lane * 64);
+                        for (int q = 0; q < (pad >> 2); q++) {
+                            const float4 v = row[q];
+                            acc += v.x;
+                            acc += v.y;
+                            acc += v.z;
+                            acc += v.w;
+                        }
+                    }
+                    wave_sync();
+                    found += cnt;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) { cx[u] = nx[u]; cy[u] = ny[u]; cz[u] = nz[u]; }
         }
         if (lane < 9) acc /= (float)n;
         float a[9];
