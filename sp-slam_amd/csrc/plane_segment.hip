@@ -1041,16 +1041,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     }
     block_sync();
     STAMP(4);
-    // ---- N: contours (findLabeledRegionBoundary from the model's last inlier, on refined labels).
-    // Each walk is recorded while it is measured, into a provisional slot of contour_cap / 64 points
-    // per plane; once the lengths fix the final offsets (each <= its slot's start while every walk
-    // fits its slot), the walks move down in plane order.  A walk longer than its slot makes every
-    // plane walk again, straight into its final place.
-    const int slot = g.contour_cap / kMaxPlanesPerFrame;
+    // ---- N: contours (findLabeledRegionBoundary from the model's last inlier, on refined labels)
     for (int q = wave; q < nk; q += kSegWaves)
         if (lane == 0) {
             const int m = S.kept[q];
-            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, con + (size_t)q * slot, slot);
+            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, nullptr, 0);
         }
     __syncthreads();
     if (t == 0) {
@@ -1062,30 +1057,12 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         }
     }
     block_sync();
-    bool all_fit = true;
-    for (int q = 0; q < nk; q++) all_fit = all_fit && S.con_len[q] <= slot;
-    if (all_fit) {
-        int coff = 0;
-        for (int q = 0; q < nk; q++) {
-            const int n = min(S.con_len[q], g.contour_cap - coff);
-            const int src = q * slot;  // >= coff
-            for (int k0 = 0; k0 < n; k0 += kSegThreads) {  // read a chunk, then write it (forward move)
-                const int k = k0 + t;
-                const int32_t v = k < n ? con[src + k] : 0;
-                __syncthreads();
-                if (k < n) con[coff + k] = v;
-                __syncthreads();
-            }
-            coff += n;
+    for (int q = wave; q < nk; q += kSegWaves)
+        if (lane == 0) {
+            const int m = S.kept[q];
+            trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, con + planes[q].contour_offset,
+                          planes[q].n_contour);
         }
-    } else {
-        for (int q = wave; q < nk; q += kSegWaves)
-            if (lane == 0) {
-                const int m = S.kept[q];
-                trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, con + planes[q].contour_offset,
-                              planes[q].n_contour);
-            }
-    }
     STAMP(9);
 #undef STAMP
 }
