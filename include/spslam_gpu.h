@@ -428,6 +428,13 @@ int spslam_supposed_debug(spslam_ctx* ctx, int frame, int plane, spslam_line_can
  * timestamps (16 int64 ticks of the 100 MHz GPU real-time clock). */
 int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_points);
 
+/* Test hook: Frame::PlaneNotSeen (src/Frame.cc:1116-1130) of each of n_coefs
+ * candidate coefficient vectors against n_planes planes (4 floats each, host
+ * buffers), evaluated by the device predicate the plane-extraction and
+ * supposed-plane kernels use; not_seen[k] = 1 when candidate k would be kept. */
+int spslam_debug_plane_not_seen(spslam_ctx* ctx, const float* planes, int n_planes, const float* coefs, int n_coefs,
+                                int* not_seen);
+
 /* ------------------------------------------------------------------------
  * RGB-D Frame per-keypoint steps (src/Frame.cc:146-181): UndistortKeyPoints
  * (:504-534, cv::undistortPoints with K and mDistCoef), ComputeStereoFromRGBD
@@ -482,7 +489,14 @@ int spslam_frame_rgbd_batch_device(spslam_ctx* ctx, const spslam_keypoint* d_kps
  *   else |angle| < running vertical threshold  -> mvpVerticalPlanes[i];
  *   else |angle| > running parallel threshold  -> mvpParallelPlanes[i].
  * Outputs are map-plane indices into the map-plane array (-1 = none) and
- * mbNewPlane (some frame plane without a match).  The not-seen branches
+ * mbNewPlane (some frame plane without a match).  The reference never clears
+ * mvpMapPlanes / mvpParallelPlanes / mvpVerticalPlanes (they are only
+ * overwritten when a candidate is found), so the second call of a frame
+ * (TrackLocalMap, src/Tracking.cc:1058) starts from what the first call left
+ * after TrackWithMotionModel's plane-outlier discard (:1004-1028): with
+ * spslam_assoc_frame.carry != 0 the match / parallel / vertical arrays are
+ * read as that starting state and updated in place; with carry == 0 they start
+ * at -1 (a new Frame, src/Frame.cc:199-213).  The not-seen branches
  * (:259-337) are dead in the reference and are not provided. */
 typedef struct spslam_map_plane {
     float world[4];           /* MapPlane::GetWorldPos (a, b, c, d) */
@@ -503,12 +517,13 @@ typedef struct spslam_assoc_frame {
     float Tcw[16];            /* Frame::mTcw, row-major float */
     int32_t map_offset;       /* this frame's map: planes [map_offset, map_offset + n_map) */
     int32_t n_map;
-    int32_t pad[2];
+    int32_t carry;            /* != 0: match / parallel / vertical hold the frame's current associations */
+    int32_t pad;
 } spslam_assoc_frame;         /* 80 bytes */
 
 /* Drop-in for one frame on host buffers.  coefs: n_planes x 4 floats; boundary_xyz:
- * float x, y, z per boundary point.  match / parallel / vertical: n_planes ints;
- * new_plane (may be NULL) receives mbNewPlane. */
+ * float x, y, z per boundary point.  match / parallel / vertical: n_planes ints
+ * (read first when frame->carry != 0); new_plane (may be NULL) receives mbNewPlane. */
 int spslam_planes_associate(spslam_ctx* ctx, const spslam_assoc_frame* frame, const float* coefs, int n_planes,
                             const spslam_map_plane* map_planes, int n_map, const float* boundary_xyz,
                             int n_boundary, const spslam_assoc_params* params, int32_t* match, int32_t* parallel,
@@ -682,7 +697,11 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
  *   parallel, then vertical).  The initial pose is the motion-model prediction
  *   (proj_frames[f].Tcw).  edge_of_kp[i] receives keypoint i's edge index.
  * SPSLAM_TRACK_DISCARD -- the outlier discard after that PoseOptimization
- *   (src/Tracking.cc:986-1000: mvpMapPoints[i] = NULL where mvbOutlier[i]) and
+ *   (src/Tracking.cc:986-1000: mvpMapPoints[i] = NULL where mvbOutlier[i];
+ *   :1004-1028: mvpMapPlanes / mvpParallelPlanes / mvpVerticalPlanes[i] = NULL
+ *   where the plane / parallel / vertical edge is an outlier -- written to
+ *   next_match / next_parallel / next_vertical, the starting state of the
+ *   second association (spslam_assoc_frame.carry), when those are given) and
  *   the SearchLocalPoints preconditions: taken[i] = keypoint i keeps a map point
  *   with Observations() > 0 (src/ORBmatcher.cc:95-97); the optimized pose is
  *   written into local_frames[f].Tcw and, if given, assoc_frames_next[f].Tcw
@@ -731,6 +750,10 @@ typedef struct spslam_track_batch {
     const int32_t* assoc_parallel;
     const int32_t* assoc_vertical;
     spslam_assoc_frame* assoc_frames_next;  /* DISCARD writes Tcw (may be NULL) */
+    const uint8_t* plane_outlier;           /* motion-model plane edge outlier flags (DISCARD, with next_*) */
+    int32_t* next_match;                    /* DISCARD writes the surviving associations (may be NULL) */
+    int32_t* next_parallel;
+    int32_t* next_vertical;
     /* PoseOptimization graphs */
     spslam_pose_problem* problems;
     spslam_point_obs* points;             /* f * cap */

@@ -15,6 +15,11 @@
 //     |angle| < lverTh -> vertical, lverTh = |angle|, next map plane;
 //     |angle| > lparTh -> parallel, lparTh = |angle|.
 //   mbNewPlane = some frame plane has no match.
+// The frame's mvpMapPlanes / mvpParallelPlanes / mvpVerticalPlanes are never
+// cleared by the reference, only overwritten when a candidate is found
+// (:230-252): with carry != 0 the match / parallel / vertical arrays hold the
+// frame's current associations on entry (TrackLocalMap's call after
+// TrackWithMotionModel's outlier discard, src/Tracking.cc:1004-1028, 1058).
 // The not-seen branches (:259-337) are dead (mvNotSeenPlaneCoefficients is
 // never written, SURVEY.md §8 notes) and are not restated.
 //
@@ -65,11 +70,12 @@ double point_distance_from_plane(const float* pM, const float* xyz, int n) {
 extern "C" {
 
 // Map planes must be given in mnId order.  Outputs per frame plane: index of the
-// matched / parallel / vertical map plane (-1 if none), the world coefficients and
-// the min boundary distance to every map plane (-1 where the angle test failed).
+// matched / parallel / vertical map plane (-1 if none; read first when carry != 0),
+// the world coefficients and the min boundary distance to every map plane (-1
+// where the angle test failed).
 int oracle_planes_associate(const float* Tcw, const float* coefs, int n_planes, const void* map_planes, int n_map,
                             const float* boundary_xyz, const float* params, int32_t* match, int32_t* parallel,
-                            int32_t* vertical, float* world, double* dist) {
+                            int32_t* vertical, float* world, double* dist, int carry) {
     using namespace oracle::assoc;
     const MapPlane* M = (const MapPlane*)map_planes;
     const Params P{params[0], params[1], params[2], params[3]};
@@ -80,7 +86,7 @@ int oracle_planes_associate(const float* Tcw, const float* coefs, int n_planes, 
         if (world)
             for (int k = 0; k < 4; k++) world[4 * i + k] = pM[k];
         float ldTh = P.dis_th, lverTh = P.ver_th, lparTh = P.par_th;
-        match[i] = parallel[i] = vertical[i] = -1;
+        if (!carry) match[i] = parallel[i] = vertical[i] = -1;
         for (int j = 0; j < n_map; j++) {
             const float angle = dot3(pM, M[j].world);
             double dis = -1.0;

@@ -72,7 +72,11 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     lfr["Tcw"] = np.asarray(T1, np.float32).reshape(16)
     lo, nlo, _ = oracle_match.search_local_points(lfr, LP, kun, do, ur, go, gi, fi.geometry, taken=taken)
     out["local_match"], out["local_nmatches"] = lo, nlo
-    a1 = oracle_assoc.associate(np.asarray(T1, np.float32).reshape(4, 4), coefs, fi.map_planes, fi.boundary)
+    # the second association starts from the first one's survivors (Tracking.cc:1004-1028, Map.cc:230-252)
+    a0_kept = oracle_track.discard_planes(a0, plo1)
+    out["assoc0_kept"] = a0_kept
+    a1 = oracle_assoc.associate(np.asarray(T1, np.float32).reshape(4, 4), coefs, fi.map_planes, fi.boundary,
+                                init=a0_kept)
     g2 = oracle_track.local_map_graph(T1, P, mo, keep, LP, lo, kun, ur, fi.inv_sigma2, coefs, a1, fi.map_planes,
                                       fi.cam)
     r2, po2, plo2 = oracle_ctypes.pose_optimize(*g2)

@@ -13,6 +13,8 @@ reference's loops:
   discard_outliers     src/Tracking.cc:986-1000, plus SearchLocalPoints' "keypoint
                        already holds a map point with observations" test
                        (src/ORBmatcher.cc:95-97)
+  discard_planes       src/Tracking.cc:1004-1028 (plane / parallel / vertical
+                       associations whose edge is an outlier)
   local_map_graph      TrackLocalMap, src/Tracking.cc:1062-1068 (SearchLocalPoints
                        assigns mvpMapPoints[bestIdx] = pMP, src/ORBmatcher.cc:115)
 
@@ -82,6 +84,24 @@ def discard_outliers(match, edge_of_kp, point_outlier, proj_points):
             keep[i] = True
             taken[i] = proj_points[m]["n_obs"] > 0
     return keep, taken
+
+
+def discard_planes(assoc, plane_outlier):
+    """Tracking.cc:1004-1028: mvpMapPlanes / mvpParallelPlanes / mvpVerticalPlanes[i] = NULL where the
+    motion-model PoseOptimization flagged that edge an outlier (edges laid out as _planes: match, then
+    parallel, then vertical, frame-plane order).  Returns the surviving associations, the starting state
+    of TrackLocalMap's AssociatePlanesByBoundary."""
+    out, e = {}, 0
+    for key in ("match", "parallel", "vertical"):
+        a = np.array(assoc[key], np.int32)
+        for i in range(len(a)):
+            if a[i] >= 0:
+                if plane_outlier[e]:
+                    a[i] = -1
+                e += 1
+        out[key] = a
+    assert e == len(plane_outlier)
+    return out
 
 
 def local_map_graph(Tcw, proj_points, match, keep, local_points, local_match, keys_un, uright, inv_level_sigma2,

@@ -463,7 +463,7 @@ void extract(const float* depth, int w, int h, int stride_floats, const Params& 
         bool seen = false;
         for (const auto& pm : R.coef) {
             const float d = pm[3] - cf[3];
-            const float angle = pm[0] * cf[0] + pm[1] * cf[1] + pm[2] * cf[2];
+            const float angle = std::fmaf(pm[2], cf[2], std::fmaf(pm[1], cf[1], pm[0] * cf[0]));  // GCC -O3 -march=native
             if ((double)d > 0.2 || (double)d < -0.2) continue;
             if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
             seen = true;

@@ -135,31 +135,38 @@ __global__ __launch_bounds__(64) void assoc_decide_kernel(const spslam_assoc_fra
         float pM[4];
         world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
         float ldTh = Pm.dis_th, lverTh = Pm.ver_th, lparTh = Pm.par_th;
-        int m = -1, par = -1, ver = -1;
+        const size_t o = (size_t)f * P + i;
+        // the frame's associations are only overwritten when a candidate is found (Map.cc:230-252): a
+        // carried call (TrackLocalMap's) starts from what the first call left after the outlier discard
+        int32_t m = -1, par = -1, ver = -1;
+        if (F.carry) {
+            m = match[o];
+            par = parallel[o];
+            ver = vertical[o];
+        }
         for (int j = 0; j < F.n_map; j++) {
             const float angle = dot3(pM, Mp[j].world);
             if (angle > Pm.angle_th || angle < -Pm.angle_th) {
                 const float dis = D[(size_t)i * max_map + j];
                 if (dis < ldTh) {
                     ldTh = dis;
-                    m = j;
+                    m = F.map_offset + j;
                     continue;
                 }
             }
             if (angle < lverTh && angle > -lverTh) {
                 lverTh = fabsf(angle);
-                ver = j;
+                ver = F.map_offset + j;
                 continue;
             }
             if (angle > lparTh || angle < -lparTh) {
                 lparTh = fabsf(angle);
-                par = j;
+                par = F.map_offset + j;
             }
         }
-        const size_t o = (size_t)f * P + i;
-        match[o] = m < 0 ? -1 : F.map_offset + m;
-        parallel[o] = par < 0 ? -1 : F.map_offset + par;
-        vertical[o] = ver < 0 ? -1 : F.map_offset + ver;
+        match[o] = m;
+        parallel[o] = par;
+        vertical[o] = ver;
         unmatched |= m < 0;
     }
     const int any = __syncthreads_or(unmatched);

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include "plane_launch.h"
+#include "plane_not_seen.h"
 
 namespace spslam {
 namespace planes {
@@ -982,12 +983,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 for (int k = 0; k < 4; k++) cf[k] = -cf[k];
             bool seen = false;
             for (int q = 0; q < nk && !seen; q++) {
-                const spslam_plane& pm = planes[q];
-                const float d = pm.coef[3] - cf[3];
-                const float angle = pm.coef[0] * cf[0] + pm.coef[1] * cf[1] + pm.coef[2] * cf[2];
-                if ((double)d > 0.2 || (double)d < -0.2) continue;
-                if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
-                seen = true;
+                seen = plane_seen_by(planes[q].coef, cf);
             }
             if (seen || nk >= planes_cap) continue;
             for (int k = 0; k < 4; k++) planes[nk].coef[k] = cf[k];

@@ -737,6 +737,25 @@ int spslam_planes_generate_from_boundaries(spslam_ctx* c, const float* depth, in
     return SPSLAM_OK;
 }
 
+int spslam_debug_plane_not_seen(spslam_ctx* c, const float* planes, int n_planes, const float* coefs, int n_coefs,
+                                int* not_seen) {
+    if (!c || n_planes < 0 || n_coefs < 0 || (n_planes && !planes) || (n_coefs && (!coefs || !not_seen)))
+        return SPSLAM_ERR_ARG;
+    if (!n_coefs) return SPSLAM_OK;
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t pb = (size_t)std::max(n_planes, 1) * 16, cb = (size_t)n_coefs * 16;
+    uint8_t* q = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&q, pb + cb + (size_t)n_coefs * 4, c->stream));
+    if (n_planes) HIP_CHECK(c, hipMemcpyAsync(q, planes, (size_t)n_planes * 16, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(q + pb, coefs, cb, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, plane_not_seen_debug_launch((const float*)q, n_planes, (const float*)(q + pb), n_coefs,
+                                             (int*)(q + pb + cb), c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(not_seen, q + pb + cb, (size_t)n_coefs * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
 int spslam_supposed_debug(spslam_ctx* c, int frame, int plane, spslam_line_candidate* cand, int* n_cand,
                           int32_t* idx, int idx_cap) {
     static_assert(sizeof(spslam_line_candidate) == sizeof(LineCand), "candidate layout");
@@ -1110,6 +1129,11 @@ int spslam_planes_associate(spslam_ctx* c, const spslam_assoc_frame* frame, cons
     for (int i = 0; i < 5; i++)
         if (len[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], len[i], hipMemcpyHostToDevice, c->stream));
     auto* d_out = (int32_t*)(q + o[5]);
+    if (F.carry && n_planes) {  // the frame's current associations are the starting state
+        HIP_CHECK(c, hipMemcpyAsync(d_out, match, (size_t)n_planes * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(d_out + cap, parallel, (size_t)n_planes * 4, hipMemcpyHostToDevice, c->stream));
+        HIP_CHECK(c, hipMemcpyAsync(d_out + 2 * cap, vertical, (size_t)n_planes * 4, hipMemcpyHostToDevice, c->stream));
+    }
     int rc = spslam_planes_associate_batch_device(
         c, 1, (const spslam_assoc_frame*)(q + o[0]), q + o[1], 16, (const int*)(q + o[2]), cap, nullptr, 0, nullptr,
         0, (const spslam_map_plane*)(q + o[3]), (const float*)(q + o[4]), n_map, params, d_out, d_out + cap,
@@ -1260,6 +1284,10 @@ int spslam_track_graph_batch_device(spslam_ctx* c, int n_frames, int stage, cons
     bool ok = common;
     if (stage == SPSLAM_TRACK_DISCARD) {
         ok = ok && b.taken && b.local_frames && b.results && b.point_outlier;
+        if (b.next_match)  // the plane-outlier discard needs the first association and its edge flags
+            ok = ok && b.next_parallel && b.next_vertical && b.plane_outlier && b.assoc_match && b.assoc_parallel &&
+                 b.assoc_vertical && b.cap_a >= 0 && b.cap_b >= 0 && (b.cap_a == 0 || b.count_a) &&
+                 (b.cap_b == 0 || b.count_b);
     } else {
         ok = ok && b.keys_un && b.uright && b.problems && b.points && b.cap_a >= 0 && b.cap_b >= 0 &&
              (b.cap_a == 0 || (b.planes_a && b.count_a && b.stride_a >= 16)) &&

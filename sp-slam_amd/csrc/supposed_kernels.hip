@@ -31,6 +31,7 @@
 #include <cfloat>
 
 #include "libm_restated.h"
+#include "plane_not_seen.h"
 #include "supposed_launch.h"
 
 namespace spslam {
@@ -526,13 +527,8 @@ __global__ __launch_bounds__(64) void supp_assemble_kernel(SuppParams sp, SuppBu
                 float cf[4];
                 supposed_coef(pl[q], c.line, cf);
                 bool seen = false;
-                for (int m = 0; m < nl && !seen; m++) {  // PlaneNotSeen (Frame.cc:1121-1144)
-                    const float d = pl[m][3] - cf[3];
-                    const float angle = pl[m][0] * cf[0] + pl[m][1] * cf[1] + pl[m][2] * cf[2];
-                    if ((double)d > 0.2 || (double)d < -0.2) continue;
-                    if ((double)angle < 0.9397 && (double)angle > -0.9397) continue;
-                    seen = true;
-                }
+                for (int m = 0; m < nl && !seen; m++)  // PlaneNotSeen (Frame.cc:1116-1130)
+                    seen = plane_seen_by(pl[m], cf);
                 if (seen) continue;
                 if (ns < cap && nl < kMaxPlanesPerFrame + kMaxSuppPerFrame) {
                     for (int k = 0; k < 4; k++) pl[nl][k] = cf[k];
@@ -594,6 +590,25 @@ hipError_t supp_launch(const PlaneGeom& g, const PlaneBuffers& pb, const SuppPar
     hipLaunchKernelGGL(supp::supp_assemble_kernel, dim3(n), dim3(64), 0, s, sp, sb, g.contour_cap, planes,
                        plane_counts, out, out_counts, out_line_idx, out_patch);
     E(kKindSuppAssemble);
+    return hipGetLastError();
+}
+
+// Test hook (spslam_debug_plane_not_seen): Frame::PlaneNotSeen of each candidate against a plane list,
+// through the same device predicate the extraction kernels use.
+__global__ __launch_bounds__(64) void plane_not_seen_debug_kernel(const float* __restrict__ planes, int n,
+                                                                  const float* __restrict__ coefs, int m,
+                                                                  int* __restrict__ out) {
+    const int k = blockIdx.x * 64 + threadIdx.x;
+    if (k >= m) return;
+    bool seen = false;
+    for (int j = 0; j < n && !seen; j++) seen = plane_seen_by(planes + 4 * j, coefs + 4 * k);
+    out[k] = !seen;
+}
+
+hipError_t plane_not_seen_debug_launch(const float* planes, int n, const float* coefs, int m, int* out,
+                                       hipStream_t s) {
+    if (m < 1) return hipSuccess;
+    hipLaunchKernelGGL(plane_not_seen_debug_kernel, dim3((m + 63) / 64), dim3(64), 0, s, planes, n, coefs, m, out);
     return hipGetLastError();
 }
 

@@ -47,4 +47,8 @@ hipError_t supp_launch(const PlaneGeom& g, const PlaneBuffers& pb, const SuppPar
                        const int* plane_counts, const int32_t* contours, spslam_supposed_plane* out, int* out_counts,
                        int32_t* out_line_idx, float* out_patch, hipStream_t s, KernelTimer* timer);
 
+// Frame::PlaneNotSeen of m candidates against n planes (4 floats each), device buffers: out[k] = 1 if not seen.
+hipError_t plane_not_seen_debug_launch(const float* planes, int n, const float* coefs, int m, int* out,
+                                       hipStream_t s);
+
 }  // namespace spslam

@@ -51,6 +51,30 @@ __global__ __launch_bounds__(kThreads) void track_graph_kernel(TrackArgs A, int 
             B.local_frames[f].Tcw[t] = v;
             if (B.assoc_frames_next) B.assoc_frames_next[f].Tcw[t] = v;
         }
+        // src/Tracking.cc:1004-1028: associations whose edge is an outlier are dropped; the rest are the
+        // second association's starting state.  Edge e of a kind is found by the same ballot scan that
+        // laid the plane edges out (match, then parallel, then vertical, frame-plane order).
+        if (B.next_match && wave == 0) {
+            const int na = min(B.count_a[f], B.cap_a);
+            const int nb = B.count_b ? min(B.count_b[f], B.cap_b) : 0;
+            const int M = na + nb, PC = B.cap_a + B.cap_b;
+            const size_t ao = (size_t)f * PC, po = (size_t)f * 3 * PC;
+            const int32_t* src[3] = {B.assoc_match, B.assoc_parallel, B.assoc_vertical};
+            int32_t* dst[3] = {B.next_match, B.next_parallel, B.next_vertical};
+            int np = 0;
+            for (int kind = 0; kind < 3; kind++) {
+                for (int j0 = 0; j0 < M; j0 += 64) {
+                    const int j = j0 + lane;
+                    const int mp = j < M ? src[kind][ao + j] : -1;
+                    const unsigned long long m = __ballot(mp >= 0);
+                    if (j < M) {
+                        const int e = np + __popcll(m & ((1ull << lane) - 1ull));
+                        dst[kind][ao + j] = (mp >= 0 && !B.plane_outlier[po + e]) ? mp : -1;
+                    }
+                    np += __popcll(m);
+                }
+            }
+        }
         return;
     }
 

@@ -41,7 +41,7 @@ import synth
 
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
-                 device=0, K=synth.TUM3, oracle_kps=None, lba_every=0, lba_unique=4, lba_points=1500,
+                 device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False):
         import torch
         self.torch = torch
@@ -147,7 +147,9 @@ class HotPath:
         dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
         self.assoc = SA.PlaneAssociator(self.ex)
         self.d_map, self.d_bound = dev(m), dev(bxyz)
-        self.d_afr1, self.d_afr2 = dev(fr), dev(fr)
+        fr2 = fr.copy()
+        fr2["carry"] = 1  # TrackLocalMap's association keeps what survived TrackWithMotionModel's discard
+        self.d_afr1, self.d_afr2 = dev(fr), dev(fr2)
         self.n_map, self.n_boundary = len(m), len(bxyz)
         self.assoc_map, self.assoc_boundary = m, bxyz  # host copies (CPU baseline)
         P = self.pe.planes_cap + self.pe.supp_cap
@@ -277,6 +279,8 @@ class HotPath:
             stride_b=SP.SUPPOSED_DTYPE.itemsize, cap_a=self.pe.planes_cap, cap_b=self.pe.supp_cap,
             map=self.d_map.data_ptr(), assoc_match=a[0].data_ptr(), assoc_parallel=a[1].data_ptr(),
             assoc_vertical=a[2].data_ptr(), assoc_frames_next=self.d_afr2.data_ptr(),
+            plane_outlier=self.graphs[0]["plout"].data_ptr(), next_match=self.d_assoc[1][0].data_ptr(),
+            next_parallel=self.d_assoc[1][1].data_ptr(), next_vertical=self.d_assoc[1][2].data_ptr(),
             problems=g["P"].data_ptr(), points=g["pts"].data_ptr(), planes=g["pls"].data_ptr(),
             edge_of_kp=self.d_edge.data_ptr(), results=self.d_res1.data_ptr(),
             point_outlier=self.graphs[0]["pout"].data_ptr(), fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy,

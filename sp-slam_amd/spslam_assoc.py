@@ -11,7 +11,8 @@ import spslam_gpu
 MAP_PLANE_DTYPE = np.dtype([("world", "<f4", 4), ("id", "<i4"), ("boundary_offset", "<i4"),
                             ("n_boundary", "<i4"), ("pad", "<i4")])
 assert MAP_PLANE_DTYPE.itemsize == 32
-ASSOC_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("map_offset", "<i4"), ("n_map", "<i4"), ("pad", "<i4", 2)])
+ASSOC_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("map_offset", "<i4"), ("n_map", "<i4"), ("carry", "<i4"),
+                              ("pad", "<i4")])
 assert ASSOC_FRAME_DTYPE.itemsize == 80
 
 
@@ -41,9 +42,11 @@ class PlaneAssociator:
         _bind(ex.lib)
         self.params = AssocParams(*params)
 
-    def __call__(self, Tcw, coefs, map_planes, boundary_xyz):
+    def __call__(self, Tcw, coefs, map_planes, boundary_xyz, init=None):
         """One frame against one map (map planes in id order).  Returns match /
-        parallel / vertical map-plane indices (-1 = none) and mbNewPlane."""
+        parallel / vertical map-plane indices (-1 = none) and mbNewPlane.  init: the
+        frame's current associations (dict match / parallel / vertical) that the
+        reference keeps where no candidate is found; None = a new Frame."""
         fr = np.zeros((), ASSOC_FRAME_DTYPE)
         fr["Tcw"] = np.asarray(Tcw, np.float32).reshape(16)
         c = np.ascontiguousarray(coefs, np.float32).reshape(-1, 4)
@@ -51,6 +54,10 @@ class PlaneAssociator:
         b = np.ascontiguousarray(boundary_xyz, np.float32).reshape(-1, 3)
         n = len(c)
         out = np.zeros((3, max(n, 1)), np.int32)
+        if init is not None:
+            fr["carry"] = 1
+            for k, key in enumerate(("match", "parallel", "vertical")):
+                out[k, :n] = init[key]
         new = ctypes.c_int(0)
         ptr = lambda a: a.ctypes.data if a.size else None  # noqa: E731
         self.ex._check(self.ex.lib.spslam_planes_associate(

@@ -31,7 +31,8 @@ LINE_CAND_DTYPE = np.dtype([("line", "<f4", 6), ("n_inliers", "<i4"), ("iteratio
 spslam_gpu.EXPORTED += ["spslam_planes_configure", "spslam_planes_capacity", "spslam_planes_extract",
                         "spslam_planes_extract_batch_device", "spslam_planes_debug", "spslam_supposed_capacity",
                         "spslam_planes_generate_from_boundaries",
-                        "spslam_planes_generate_from_boundaries_batch_device", "spslam_supposed_debug"]
+                        "spslam_planes_generate_from_boundaries_batch_device", "spslam_supposed_debug",
+                        "spslam_debug_plane_not_seen"]
 
 
 def _bind(lib):
@@ -49,6 +50,19 @@ def _bind(lib):
     lib.spslam_planes_generate_from_boundaries_batch_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_size_t,
                                                                         ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.spslam_supposed_debug.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ip, vp, ctypes.c_int]
+    lib.spslam_debug_plane_not_seen.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]
+
+
+def plane_not_seen(ex: spslam_gpu.OrbExtractor, planes, coefs):
+    """Frame::PlaneNotSeen (src/Frame.cc:1116-1130) of each candidate against the planes, through the
+    device predicate the extraction kernels use (test hook).  Returns a bool per candidate."""
+    _bind(ex.lib)
+    p = np.ascontiguousarray(planes, np.float32).reshape(-1, 4)
+    c = np.ascontiguousarray(coefs, np.float32).reshape(-1, 4)
+    out = np.zeros(max(len(c), 1), np.int32)
+    ex._check(ex.lib.spslam_debug_plane_not_seen(ex.ctx, p.ctypes.data if len(p) else None, len(p),
+                                                 c.ctypes.data if len(c) else None, len(c), out.ctypes.data))
+    return out[:len(c)].astype(bool)
 
 
 class PlaneExtractor:

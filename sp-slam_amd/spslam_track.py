@@ -24,7 +24,8 @@ class TrackBatch(ctypes.Structure):
                 ("stride_a", ctypes.c_int32), ("stride_b", ctypes.c_int32), ("cap_a", ctypes.c_int32),
                 ("cap_b", ctypes.c_int32),
                 ("map", _P), ("assoc_match", _P), ("assoc_parallel", _P), ("assoc_vertical", _P),
-                ("assoc_frames_next", _P),
+                ("assoc_frames_next", _P), ("plane_outlier", _P), ("next_match", _P), ("next_parallel", _P),
+                ("next_vertical", _P),
                 ("problems", _P), ("points", _P), ("planes", _P), ("edge_of_kp", _P), ("results", _P),
                 ("point_outlier", _P),
                 ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),

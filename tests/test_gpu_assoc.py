@@ -125,3 +125,35 @@ def test_batch_two_sources_per_frame_maps(assoc):
             want = np.where(o[key] >= 0, o[key] + moff, -1)
             assert np.array_equal(out[k, f, :n], want), (f, key)
         assert bool(newp[f]) == o["new_plane"], f
+
+
+def test_carried_associations(assoc):
+    """TrackLocalMap's AssociatePlanesByBoundary starts from what TrackWithMotionModel's association left
+    after the plane-outlier discard (src/Map.cc:230-252 never clears mvpMapPlanes; Tracking.cc:1004-1028):
+    at a pose shifted so that some first-call matches miss the distance threshold, those matches are kept.
+    GPU and oracle must agree entry for entry, and the carried state must change the result somewhere."""
+    import oracle_assoc as OA
+    import oracle_track as OT
+    import synth
+    rng = np.random.default_rng(33)
+    n = n_kept = 0
+    for seq in range(3):
+        sc = synth.Scene(seq, n_boxes=2 + seq)
+        m, b = _map(rng, sc)
+        for fr in range(0, 150, 10):
+            T, c, _ = synth.assoc_frame_planes(sc, fr, rng, n_faces=5, n_random=1)
+            a0 = OA.associate(T, c, m, b)
+            # a few first-call edges flagged as PoseOptimization outliers (edge order: match, parallel, vertical)
+            n_edges = sum(int((a0[k] >= 0).sum()) for k in ("match", "parallel", "vertical"))
+            kept = OT.discard_planes(a0, rng.random(n_edges) < 0.25)
+            T2 = T.copy()
+            T2[:3, 3] += rng.normal(0, 0.15, 3).astype(np.float32)  # the optimized pose, far enough to miss
+            o = OA.associate(T2, c, m, b, init=kept)
+            g = assoc(T2, c, m, b, init=kept)
+            for k in ("match", "parallel", "vertical"):
+                assert np.array_equal(g[k], o[k]), (seq, fr, k, g[k], o[k])
+            assert g["new_plane"] == o["new_plane"]
+            fresh = OA.associate(T2, c, m, b)
+            n_kept += int(((fresh["match"] < 0) & (o["match"] >= 0)).sum())
+            n += 1
+    assert n >= 40 and n_kept > 0, (n, n_kept)

@@ -84,10 +84,13 @@ def test_float_expressions_match_gcc_march_native(tmp_path):
                     assert r["dist"][i, j] == d, (trial, i, j)
 
 
-def _decide(world, m, dist, P):
-    """Independent transcription of the Map.cc:207-257 loop over precomputed distances."""
+def _decide(world, m, dist, P, init=None):
+    """Independent transcription of the Map.cc:207-257 loop over precomputed distances; init = the
+    frame's current associations (the reference only overwrites them)."""
     n = len(world)
     out = np.full((3, n), -1, np.int32)
+    if init is not None:
+        out[:] = np.stack([init["match"], init["parallel"], init["vertical"]])
     for i in range(n):
         ld, lv, lp = np.float32(P[0]), np.float32(P[2]), np.float32(P[3])
         for j in range(len(m)):
@@ -128,6 +131,14 @@ def test_decision_loop_matches_transcription():
             got = np.stack([r["match"], r["parallel"], r["vertical"]])
             assert np.array_equal(got, _decide(r["world"], m, r["dist"], OA.ASSOC_PARAMS)), (seq, fr)
             assert r["new_plane"] == bool((r["match"] < 0).any())
+            # a carried call (TrackLocalMap's) at a shifted pose keeps what it does not overwrite
+            init = {k: rng.integers(-1, len(m), len(c)).astype(np.int32) for k in ("match", "parallel", "vertical")}
+            T2 = T.copy()
+            T2[:3, 3] += np.float32(0.1)
+            r2 = OA.associate(T2, c, m, b, init=init)
+            got = np.stack([r2["match"], r2["parallel"], r2["vertical"]])
+            assert np.array_equal(got, _decide(r2["world"], m, r2["dist"], OA.ASSOC_PARAMS, init)), (seq, fr)
+            assert r2["new_plane"] == bool((r2["match"] < 0).any())
 
 
 def test_ground_truth_association():

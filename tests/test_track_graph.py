@@ -119,3 +119,17 @@ def test_ate_is_invariant_to_a_rigid_transform():
     noisy = ref + rng.normal(0, 0.01, ref.shape)
     assert 0.005 < trajectory.ate_rmse(noisy, ref) < 0.02
     assert trajectory.ate_rmse(est, ref, align=False) > 0.5
+
+
+def test_discard_planes_known_answer():
+    """Tracking.cc:1004-1028: associations whose edge is an outlier are dropped; the rest carry into
+    TrackLocalMap's association.  Edges: match (plane 0 -> 2), parallel (plane 1 -> 0), vertical (0 -> 1,
+    1 -> 1)."""
+    _, _, _, _, _, _, _, assoc = _case()
+    kept = OT.discard_planes(assoc, np.array([0, 1, 0, 1], bool))
+    assert list(kept["match"]) == [2, -1]
+    assert list(kept["parallel"]) == [-1, -1]
+    assert list(kept["vertical"]) == [1, -1]
+    kept = OT.discard_planes(assoc, np.zeros(4, bool))
+    for k in ("match", "parallel", "vertical"):
+        assert list(kept[k]) == list(assoc[k])
