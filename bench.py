@@ -42,20 +42,20 @@ ROOT = pathlib.Path(__file__).resolve().parent
 HW_QUEUES = 8
 sys.path.insert(0, str(ROOT / "sp-slam_amd"))
 
-CONFIGS = {
+# HotPath parameters of each config: sp-slam_amd/pipeline.py CONFIGS (the YAML keys of the path)
+WORKLOADS = {
     # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, ORB + planes + PoseOptimization
-    "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=3,
-               workload="C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud "
-                        "plane extraction + supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), "
-                        "no LBA"),
+    "c2": "C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud plane extraction + "
+          "supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), no LBA",
     # configs[2]: full pipeline incl. LocalBundleAdjustment (a keyframe every 5 frames, 12-keyframe local maps)
-    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=3, lba_every=5,
-               workload="C3 (synthetic proxy): C2 + LocalBundleAdjustment with plane/parallel/perpendicular edges "
-                        "for every 5th frame (12 keyframes, 1500 points per local map)"),
+    "c3": "C3 (synthetic proxy): C2 + LocalBundleAdjustment with plane/parallel/perpendicular edges for every 5th "
+          "frame (12 keyframes, 1500 points per local map)",
+    # configs[3]: independent ICL-NUIM living-room sequences, one per GPU
+    "c4": "C4 (synthetic proxy): ICL-NUIM parameter set (Examples/RGB-D/ICL.yaml: fx 481.2, fy -480.0, cx 319.5, "
+          "cy 239.5, Plane.MinSize 1000, Plane.Chi 1000, Plane.VPChi 200), one independent sequence per GPU rank; "
+          "ORB + planes + supposed planes + 2x PoseOptimization",
     # configs[4]: 1280x960, nFeatures=4000, dense-plane scene
-    "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8,
-               workload="C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + supposed planes + "
-                        "2x PoseOptimization"),
+    "c5": "C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + supposed planes + 2x PoseOptimization",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -131,6 +131,73 @@ def max_over_ranks(elapsed, dist=None, device="cpu"):
     return float(t.item())
 
 
+def per_rank(frames, elapsed, dist=None, device="cpu"):
+    """[(frames, elapsed s)] of every rank (one all-gather of two numbers; RCCL over xGMI on the GPU node)."""
+    if dist is None:
+        return [(frames, elapsed)]
+    import torch
+    t = torch.tensor([float(frames), elapsed], dtype=torch.float64, device=device)
+    got = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, t)
+    return [(int(g[0].item()), float(g[1].item())) for g in got]
+
+
+def _free_port():
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` started without a launcher: start N rank processes of this script (one per GPU,
+    LOCAL_RANK = GPU index) with the torch.distributed environment torch.distributed.run would give them, before
+    anything here touches the GPU, and return the first non-zero exit status (0 if all succeed)."""
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("GPU_MAX_HW_QUEUES", str(HW_QUEUES))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    return next((rc for rc in rcs if rc), 0)
+
+
+def dist_check(args, rank, world):
+    """CPU rehearsal of the multi-rank path (gloo): the same spawn, rendezvous, shard assignment and max / gather
+    aggregation as a GPU run, each rank timing the CPU oracle's ORB on its own shard's first frame."""
+    import numpy as np
+    import torch.distributed as dist
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_ctypes
+    import synth
+    dist.init_process_group("gloo")
+    try:
+        shard = shard_of(rank)
+        sc = synth.Scene(shard["seq_id"])
+        g, _, _ = sc.render(sc.pose(0), noise_seed=shard["seq_id"] * 1000)
+        t0 = time.perf_counter()
+        kps, _ = oracle_ctypes.OrbOracle().extract(g)
+        elapsed = time.perf_counter() - t0
+        ranks = per_rank(1, elapsed, dist)
+        elapsed = max_over_ranks(elapsed, dist)
+        import torch
+        chk = torch.tensor([float(len(kps)), float(g.astype(np.int64).sum())], dtype=torch.float64)
+        got = [torch.zeros_like(chk) for _ in range(world)]
+        dist.all_gather(got, chk)
+        if rank == 0:
+            print(json.dumps({"dist_check": True, "n_gpus": world, "value": sum(f for f, _ in ranks) / elapsed,
+                              "max_elapsed_s": elapsed, "per_rank": [{"rank": r, "frames": f, "elapsed_s": e}
+                                                                     for r, (f, e) in enumerate(ranks)],
+                              "shards": [shard_of(r)["seq_id"] for r in range(world)],
+                              "keypoints": [int(x[0].item()) for x in got],
+                              "image_sums": [int(x[1].item()) for x in got]}), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 def shard_of(rank):
     """Rank r tracks its own synthetic sequence: frames are independent units, no data-path collective."""
     return dict(seq_id=rank)
@@ -156,7 +223,10 @@ def cpu_baseline(hp, budget_s=12.0):
         o = oracle_step.run(inputs[i], orb, po, supp_cap=hp.pe.supp_cap)
         poses.setdefault(i, o["pose2"][0]["Tcw"].copy())
         if hp.n_lba and n % hp.lba_every == 0:  # LocalMapping: one local BA per keyframe
-            oracle_lba.lba_optimize(*hp.lba_problems[(n // hp.lba_every) % len(hp.lba_problems)][:6])
+            pc = hp.plane_cfg
+            oracle_lba.lba_optimize(*hp.lba_problems[(n // hp.lba_every) % len(hp.lba_problems)][:6],
+                                    cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info, pc.chi,
+                                         pc.vp_chi))
         n += 1
     dt = time.perf_counter() - t0
     lba = f" + LocalBundleAdjustment every {hp.lba_every} frames" if hp.n_lba else ""
@@ -199,25 +269,33 @@ def _ensure_hw_queues():
 
 
 def main():
-    _ensure_hw_queues()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
-    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--unique-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
     ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
+    ap.add_argument("--dist-check", action="store_true",
+                    help="CPU rehearsal of the multi-rank launch (gloo, no GPU): spawn, rendezvous, aggregation")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))  # one process per GPU (no launcher was used)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dist_check:
+        return dist_check(args, rank, world)
+    _ensure_hw_queues()
+    import pipeline
+    cfg = pipeline.CONFIGS[args.config]
     import torch
     torch.cuda.set_device(local)
     dist = None
@@ -225,12 +303,9 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    import pipeline
-    hp = pipeline.HotPath(args.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"],
-                          unique_frames=args.unique_frames, device=local, lba_every=cfg.get("lba_every", 0),
+    hp = pipeline.HotPath(args.batch, unique_frames=args.unique_frames, device=local,
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
-                          orb_priority=args.orb_priority,
-                          **shard_of(rank))
+                          orb_priority=args.orb_priority, **cfg, **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
     torch.cuda.synchronize()
@@ -247,9 +322,10 @@ def main():
     elapsed = time.perf_counter() - t0
     times = {k: v for k, v in hp.kernel_times().items() if v[1] > 0}
     res = hp.results()
+    ranks = per_rank(args.batch * args.steps, elapsed, dist, "cuda")
     elapsed = max_over_ranks(elapsed, dist, "cuda")
 
-    frames = world * args.batch * args.steps
+    frames = sum(f for f, _ in ranks)
     value = frames / elapsed
     total_kernel_ms = sum(v[0] for v in times.values())
     dom, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
@@ -296,7 +372,8 @@ def main():
         "dtype": "u8+f32+f64",
         "data": "synthetic (in-repo textured-room RGB-D renderer sp-slam_amd/synth.py; map points / map planes "
                 "synthesized from the scene, every correspondence from the step's own matching + association)",
-        "config": {"workload": cfg["workload"], "frames_per_step_per_gpu": args.batch,
+        "per_rank": [{"rank": r, "frames": f, "elapsed_s": e} for r, (f, e) in enumerate(ranks)],
+        "config": {"workload": WORKLOADS[args.config], "name": args.config, "frames_per_step_per_gpu": args.batch,
                    "parallelism": f"shard{world}", "mean_keypoints": hp.mean_keypoints,
                    "pipelined": hp.pipelined,
                    "mean_planes": float(res["plane_counts"].mean()),

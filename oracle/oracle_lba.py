@@ -11,7 +11,7 @@ import numpy as np
 import oracle_ctypes
 import spslam_lba as L
 
-PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # TUM yaml Plane.* keys
+PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # ICL.yaml Plane.* keys (Chi 1000, VPChi 200)
 
 
 def lba_optimize(prob, kfs, points, point_obs, planes, plane_obs, cfg=PLANE_CONFIG):

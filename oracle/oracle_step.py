@@ -25,9 +25,12 @@ import oracle_track
 class FrameInputs:
     """Everything one frame of the step reads: images, camera, the map it tracks against."""
 
-    def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary):
+    def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary, min_size=500,
+                 pose_cfg=None):
         self.gray, self.depth = gray, depth
         self.cam = cam                  # fx, fy, cx, cy, bf
+        self.min_size = min_size        # Plane.MinSize
+        self.pose_cfg = pose_cfg        # Plane.*Info / Chi / VPChi (spslam_gpu.PlaneConfig; None = TUM1.yaml)
         self.geometry = geometry        # oracle_match geometry vector (19 floats)
         self.inv_sigma2 = inv_sigma2
         self.proj = proj                # (spslam_proj_frame, spslam_proj_point[])
@@ -42,7 +45,7 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     out = {}
     ko, do = orb.extract(fi.gray, cap=20000)
     out["kps"], out["desc"] = ko, do
-    r = planes.extract(fi.depth, fx, fy, cx, cy)
+    r = planes.extract(fi.depth, fx, fy, cx, cy, min_size=fi.min_size)
     so = oracle_supposed.generate(fi.depth, planes.cloud(), r["coef"], r["contour"], fx, fy, cx, cy)
     ca = np.asarray(r["coef"], np.float32).reshape(-1, 4)
     cb = np.asarray(so["coef"], np.float32).reshape(-1, 4)
@@ -61,7 +64,7 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     out["match"], out["nmatches"] = mo, nmo
     a0 = oracle_assoc.associate(pfr["Tcw"].reshape(4, 4), coefs, fi.map_planes, fi.boundary)
     g1 = oracle_track.motion_model_graph(pfr, P, mo, kun, ur, fi.inv_sigma2, coefs, a0, fi.map_planes, fi.cam)
-    r1, po1, plo1 = oracle_ctypes.pose_optimize(*g1[:3])
+    r1, po1, plo1 = oracle_ctypes.pose_optimize(*g1[:3], cfg=fi.pose_cfg)
     out["assoc0"], out["graph1"], out["pose1"] = a0, g1, (r1, po1, plo1)
     T1 = r1["Tcw"] if not chain else np.asarray(chain["pose1_Tcw"], np.float32)
     keep, taken = oracle_track.discard_outliers(mo, g1[3], po1, P)
@@ -79,7 +82,7 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
                                 init=a0_kept)
     g2 = oracle_track.local_map_graph(T1, P, mo, keep, LP, lo, kun, ur, fi.inv_sigma2, coefs, a1, fi.map_planes,
                                       fi.cam)
-    r2, po2, plo2 = oracle_ctypes.pose_optimize(*g2)
+    r2, po2, plo2 = oracle_ctypes.pose_optimize(*g2, cfg=fi.pose_cfg)
     out["assoc1"], out["graph2"], out["pose2"] = a1, g2, (r2, po2, plo2)
     return out
 
@@ -94,4 +97,4 @@ def from_hotpath(hp, i):
     geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, hp.bf, *b, *ginv], t["scale"]]).astype(np.float32)
     return FrameInputs(gray, depth, (hp.fx, hp.fy, hp.cx, hp.cy, hp.bf), geo, t["inv_sigma2"],
                        hp.match_probs[i % len(hp.match_probs)], hp.local_probs[i % len(hp.local_probs)],
-                       hp.assoc_map, hp.assoc_boundary)
+                       hp.assoc_map, hp.assoc_boundary, min_size=hp.min_size, pose_cfg=hp.plane_cfg)

@@ -39,20 +39,40 @@ import spslam_planes
 import synth
 
 
+# Parameter sets of the BASELINE.json configs (the YAML keys the path reads):
+#   c2/c3  TUM-style 640x480 (Examples/RGB-D/TUM3.yaml intrinsics, TUM1.yaml plane keys)
+#   c4     ICL-NUIM (Examples/RGB-D/ICL.yaml: fx 481.2, fy -480.0, Plane.MinSize 1000, Chi 1000, VPChi 200)
+#   c5     1280x960, nFeatures 4000, dense-plane scene
+CONFIGS = {
+    "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=3),
+    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=3, lba_every=5),
+    "c4": dict(width=640, height=480, nfeatures=1000, n_boxes=3, K=synth.ICL, min_size=1000, chi=1000.0,
+               vp_chi=200.0),
+    "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8),
+}
+
+
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
-                 pipelined=False, tail_priority=True, orb_priority=False):
+                 pipelined=False, tail_priority=True, orb_priority=False, min_size=500, chi=300.0, vp_chi=300.0,
+                 rotate_inputs=False):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
         self.device = device
         s = width / 640.0
+        self.K = K
         self.fx, self.fy, self.cx, self.cy = K["fx"] * s, K["fy"] * s, K["cx"] * s, K["cy"] * s
+        self.Ks = dict(K, fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy)  # intrinsics at this resolution
         self.bf = K["bf"]
+        self.min_size = min_size
+        # Plane.AngleInfo / DistanceInfo / ParallelInfo / VerticalInfo / Chi / VPChi (Optimizer.cc:681-693)
+        self.plane_cfg = G.PlaneConfig(1.0, 100.0, 0.5, 0.5, chi, vp_chi)
         self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
         self.ex = G.OrbExtractor(nfeatures=nfeatures, width=width, height=height, max_batch=B, device=device)
-        self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height)
+        self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height,
+                                               min_size=min_size)
         self.fs = spslam_frame.FrameStage(self.ex, self.fx, self.fy, self.cx, self.cy, K.get("dist", (0,) * 5),
                                           K["bf"], width, height)
         # --- unique synthetic frames: colour (R,G,B u8) + raw depth (u16, DepthMapFactor 5000), as
@@ -61,7 +81,7 @@ class HotPath:
         self.frames = []
         for i in range(U):
             fi = 3 * i
-            g, d, fid = self.scene.render(self.scene.pose(fi), width, height, noise_seed=seq_id * 1000 + fi)
+            g, d, fid = self.scene.render(self.scene.pose(fi), width, height, K=K, noise_seed=seq_id * 1000 + fi)
             self.frames.append((fi, synth.colorize(g, fid), d, fid))
         dev = "cuda"
         self.d_rgb = torch.from_numpy(np.stack([self.frames[i % U][1] for i in range(B)])).to(dev)
@@ -122,6 +142,12 @@ class HotPath:
         self.lba_every = lba_every
         if self.n_lba:
             self._setup_lba(seq_id, lba_unique, lba_points)
+        # rotate_inputs (tests): batch k's slot i takes the inputs of slot (i + k) % B -- images and the per-frame
+        # tracking records together -- so consecutive batches differ and a stage reading the wrong buffer set shows
+        self.rotate_inputs = rotate_inputs
+        self.n_loaded = 0
+        if rotate_inputs:
+            self.base_inputs = {k: getattr(self, k).clone() for k in self.INPUT_BUFFERS}
         self.pipelined = pipelined
         self.orb_priority = orb_priority
         if pipelined:
@@ -164,8 +190,8 @@ class HotPath:
         import spslam_match as SM
         torch, B, U = self.torch, self.B, len(self.frames)
         rng = np.random.default_rng(seq_id * 977 + 3)
-        last = [self.scene.render(self.scene.pose(f[0] - 1), self.W, self.H, noise_seed=seq_id * 1000 + f[0] + 500)
-                for f in self.frames]
+        last = [self.scene.render(self.scene.pose(f[0] - 1), self.W, self.H, K=self.K,
+                                  noise_seed=seq_id * 1000 + f[0] + 500) for f in self.frames]
         d_g = torch.from_numpy(np.stack([g for g, _, _ in last])).cuda()
         cap = self.kp_cap
         d_k = torch.zeros((U, cap, 7), dtype=torch.float32, device="cuda")
@@ -176,7 +202,7 @@ class HotPath:
         torch.cuda.synchronize()
         kps = d_k.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(U, cap)
         desc, cnt = d_d.cpu().numpy(), d_n.cpu().numpy()
-        Ks = dict(synth.TUM3, fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy)
+        Ks = self.Ks
         probs = [synth.proj_problem(self.scene, self.frames[i][0] - 1, self.frames[i][0], kps[i, :cnt[i]],
                                     desc[i, :cnt[i]], last[i][1], rng, K=Ks) for i in range(U)]
         offs = np.cumsum([0] + [len(p[1]) for p in probs])
@@ -195,8 +221,8 @@ class HotPath:
         # Tracking::SearchLocalPoints (TrackLocalMap): the local map = map points of the keyframe four
         # frames back (true depth, MapPoint normal / distance range), matched after the first pose
         # optimisation; keypoints holding a motion-model match are taken
-        kf = [self.scene.render(self.scene.pose(f[0] - 4), self.W, self.H, noise_seed=seq_id * 1000 + f[0] + 900)
-              for f in self.frames]
+        kf = [self.scene.render(self.scene.pose(f[0] - 4), self.W, self.H, K=self.K,
+                                noise_seed=seq_id * 1000 + f[0] + 900) for f in self.frames]
         d_g = torch.from_numpy(np.stack([g for g, _, _ in kf])).cuda()
         self.ex.extract_batch_device(d_g.data_ptr(), U, self.W * self.H, self.W, d_k.data_ptr(), d_d.data_ptr(),
                                      d_n.data_ptr(), cap, self.stream)
@@ -323,14 +349,14 @@ class HotPath:
         self.track.batch_device(self.B, ST.MOTION_MODEL, self._track_batch(0), stream=self.stream)
         G.pose_optimize_batch_device(self.ex, self.B, g1["P"].data_ptr(), g1["pts"].data_ptr(),
                                      g1["pls"].data_ptr(), self.d_res1.data_ptr(), g1["pout"].data_ptr(),
-                                     g1["plout"].data_ptr(), stream=self.stream)
+                                     g1["plout"].data_ptr(), cfg=self.plane_cfg, stream=self.stream)
         self.track.batch_device(self.B, ST.DISCARD, self._track_batch(0), stream=self.stream)
         self.search_local_points()
         self.associate(1)
         self.track.batch_device(self.B, ST.LOCAL_MAP, self._track_batch(1), stream=self.stream)
         G.pose_optimize_batch_device(self.ex, self.B, g2["P"].data_ptr(), g2["pts"].data_ptr(),
                                      g2["pls"].data_ptr(), self.d_res2.data_ptr(), g2["pout"].data_ptr(),
-                                     g2["plout"].data_ptr(), stream=self.stream)
+                                     g2["plout"].data_ptr(), cfg=self.plane_cfg, stream=self.stream)
 
     def graph(self, k):
         """Host copy of PoseOptimization graph k: (problems, [points per frame], [planes per frame],
@@ -353,7 +379,8 @@ class HotPath:
         for u in range(min(unique, self.n_lba)):
             rng = np.random.default_rng(seq_id * 131 + u)
             f0 = 6 * u
-            probs.append(synth.lba_problem(self.scene, list(range(f0, f0 + 72, 6)), rng, n_fixed=2, n_points=n_points))
+            probs.append(synth.lba_problem(self.scene, list(range(f0, f0 + 72, 6)), rng, n_fixed=2, n_points=n_points,
+                                           K=self.Ks))
         hdr = np.zeros(self.n_lba, L.LBA_PROBLEM_DTYPE)
         kf, pt, po, pl, plo = [], [], [], [], []
         nk = npt = npo = npl = nplo = 0
@@ -381,7 +408,9 @@ class HotPath:
         # LocalMapping runs in its own thread on its own context (as the reference's LocalMapping thread):
         # the batched LM drives its steps from the host, so tracking launches must not wait behind it
         self.lba_ex = G.OrbExtractor(max_batch=1, device=self.device)
-        self.lba = L.LocalBA(self.lba_ex)
+        pc = self.plane_cfg
+        self.lba = L.LocalBA(self.lba_ex, cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info,
+                                               pc.chi, pc.vp_chi))
         self.lba_stream = torch.cuda.Stream()
         self.ev_lba = torch.cuda.Event()
         import concurrent.futures as cf
@@ -412,6 +441,27 @@ class HotPath:
     # Extraction outputs: the only buffers written by ORB / plane extraction and read by the tracking tail.
     EXTRACTION_BUFFERS = ("d_gray", "d_depth", "d_kps", "d_desc", "d_cnt", "d_planes", "d_pcnt", "d_inl", "d_con", "d_supp", "d_scnt",
                           "d_lines", "d_patch")
+    # Per-batch inputs: the colour / depth frames and the per-frame tracking records (the map point and plane
+    # arrays they index are shared).  Static in the bench; rotated per batch with rotate_inputs.
+    INPUT_BUFFERS = ("d_rgb", "d_depth_raw", "d_pframes", "d_lframes", "d_afr1", "d_afr2")
+
+    def batch_slots(self, k):
+        """Source slot of each slot of batch k (identity unless rotate_inputs)."""
+        return [(i + k) % self.B if self.rotate_inputs else i for i in range(self.B)]
+
+    def _load(self, stream):
+        """Per-batch inputs of the next batch into the bound buffers, on `stream` (rotate_inputs only)."""
+        k = self.n_loaded
+        self.n_loaded += 1
+        if not self.rotate_inputs:
+            return
+        torch = self.torch
+        perm = torch.tensor(self.batch_slots(k), dtype=torch.long, device="cuda")
+        with torch.cuda.stream(stream):
+            perm.record_stream(stream)
+            for name in self.INPUT_BUFFERS:
+                dst, src = getattr(self, name), self.base_inputs[name]
+                dst.view(self.B, -1).copy_(src.view(self.B, -1).index_select(0, perm))
 
     def _setup_pipeline(self):
         """Software pipelining across steps: batch k+1's extraction (ORB and planes, two streams) runs beside
@@ -419,8 +469,8 @@ class HotPath:
         latency-bound and leaves most CUs idle.  The extraction outputs are double-buffered; set j may be
         overwritten once the tail that read it has finished (ev_tail[j])."""
         torch = self.torch
-        self.sets = [{k: getattr(self, k) for k in self.EXTRACTION_BUFFERS},
-                     {k: torch.zeros_like(getattr(self, k)) for k in self.EXTRACTION_BUFFERS}]
+        names = self.EXTRACTION_BUFFERS + (self.INPUT_BUFFERS if self.rotate_inputs else ())
+        self.sets = [{k: getattr(self, k) for k in names}, {k: getattr(self, k).clone() for k in names}]
         # ORB extraction is the longest extraction chain; orb_priority lets its workgroups dispatch ahead of the
         # plane chain's (the tracking tail keeps its high priority)
         self.ext_orb = torch.cuda.Stream(priority=-1 if self.orb_priority else 0)
@@ -440,6 +490,7 @@ class HotPath:
     def _extract(self, j):
         self._bind(j)
         self.ext_orb.wait_event(self.ev_tail[j])
+        self._load(self.ext_orb)
         self.grab(self.ext_orb.cuda_stream)
         self.ev_grab[j].record(self.ext_orb)
         self.ext_planes.wait_event(self.ev_grab[j])
@@ -457,6 +508,7 @@ class HotPath:
         if self.pipelined:
             return self._step_pipelined()
         # planes of step k may start once step k-1 is done with the plane buffers and this step's depth exists
+        self._load(self.main)
         self.grab()
         self.ev_fork.record(self.main)
         self.side.wait_event(self.ev_fork)

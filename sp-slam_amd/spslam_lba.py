@@ -28,7 +28,7 @@ assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 a
 
 spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device"]
 
-PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # TUM yaml Plane.* keys
+PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # ICL.yaml Plane.* keys (Chi 1000, VPChi 200)
 
 
 def _bind(lib):

@@ -22,6 +22,9 @@ import dataclasses
 import numpy as np
 
 TUM3 = dict(fx=535.4, fy=539.2, cx=320.1, cy=247.6, bf=40.0, depth_factor=5000.0, th_depth=40.0)
+# Examples/RGB-D/ICL.yaml (ICL-NUIM): note the negative fy -- the organized cloud's y, the image bounds test and
+# every projection flip sign (Frame.cc:864-865, ORBmatcher.cc:1370-1371)
+ICL = dict(fx=481.2, fy=-480.0, cx=319.5, cy=239.5, bf=40.0, depth_factor=5000.0, th_depth=40.0)
 
 
 @dataclasses.dataclass

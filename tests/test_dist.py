@@ -61,3 +61,44 @@ def test_single_rank_helpers():
     assert bench.max_over_ranks(3.5) == 3.5
     assert bench.shard_of(0) != bench.shard_of(1)
     pytest.importorskip("torch")
+
+
+def _bench_json(out):
+    import json
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def test_bench_spawns_ranks_itself():
+    """`python bench.py --gpus 2` with no launcher starts its own two rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* set before any GPU work) and rank 0 reports both ranks' frames and the max elapsed.
+    --dist-check runs that exact spawn + rendezvous + aggregation path over gloo on the CPU."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--dist-check"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = _bench_json(p.stdout)
+    assert r["n_gpus"] == 2 and [x["rank"] for x in r["per_rank"]] == [0, 1]
+    assert r["max_elapsed_s"] == max(x["elapsed_s"] for x in r["per_rank"])
+    assert r["shards"] == [0, 1] and r["image_sums"][0] != r["image_sums"][1]
+    assert all(1000 <= k <= 1016 for k in r["keypoints"])
+
+
+def test_bench_rejects_launcher_mismatch():
+    """Launched as 2 ranks by torch.distributed.run but asked for --gpus 4: refuse instead of reporting a
+    wrong n_gpus."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    p = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "4", "--dist-check"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "--gpus 4" in p.stderr

@@ -14,12 +14,19 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def run():
+# BASELINE.json configs: C2 (TUM-style 640x480), C4 (ICL.yaml: fy = -480, Plane.MinSize 1000, Chi 1000,
+# VPChi 200), C5 (1280x960, nFeatures 4000, dense planes) -- small batches
+SIZES = {"c2": 6, "c4": 6, "c5": 2}
+
+
+@pytest.fixture(scope="module", params=sorted(SIZES))
+def run(request):
     import pipeline
-    hp = pipeline.HotPath(6, unique_frames=6, n_boxes=3)
+    B = SIZES[request.param]
+    hp = pipeline.HotPath(B, unique_frames=B, **pipeline.CONFIGS[request.param])
     hp.step()
     res = hp.results()
+    hp.config_name = request.param
     yield hp, res
     hp.close()
 
@@ -40,7 +47,7 @@ def test_orb_and_frame_stage(run):
     import oracle_ctypes
     import oracle_frame
     hp, res = run
-    orb = oracle_ctypes.OrbOracle()
+    orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
     kun = hp.d_kun.cpu().numpy().reshape(hp.B, hp.kp_cap, 7)
     kdep = hp.d_kdepth.cpu().numpy()
     for i in range(hp.B):
@@ -53,7 +60,7 @@ def test_orb_and_frame_stage(run):
             assert np.array_equal(kg[f], ko[f]), (i, f)
         assert np.array_equal(hp.d_desc[i, :n].cpu().numpy(), do), i
         fo = oracle_frame.frame_rgbd(np.stack([ko["x"], ko["y"]], 1), hp.d_depth[i].cpu().numpy(), hp.fx, hp.fy,
-                                     hp.cx, hp.cy, bf=40.0)
+                                     hp.cx, hp.cy, bf=hp.bf)
         assert np.array_equal(kun[i, :n, :2], fo["un"]), i
         assert np.array_equal(kdep[i, :n], fo["depth"]), i
 
@@ -73,7 +80,7 @@ def test_planes_stage(run):
     po = oracle_planes.PlaneOracle()
     for i in range(hp.B):
         depth = hp.d_depth[i].cpu().numpy()
-        ro = po.extract(depth, hp.fx, hp.fy, hp.cx, hp.cy)
+        ro = po.extract(depth, hp.fx, hp.fy, hp.cx, hp.cy, min_size=hp.min_size)
         ca, cb = _frame_planes(hp, res, i)
         assert np.array_equal(ca, ro["coef"]), i
         so = oracle_supposed.generate(depth, po.cloud(), ro["coef"], ro["contour"], hp.fx, hp.fy, hp.cx, hp.cy)
@@ -91,7 +98,7 @@ def test_tracking_chain(run):
     import oracle_step
     from test_gpu_pose import pose_close
     hp, res = run
-    orb, po = oracle_ctypes.OrbOracle(), oracle_planes.PlaneOracle()
+    orb, po = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures), oracle_planes.PlaneOracle()
     P1, pts1, pls1, out1, plout1 = hp.graph(0)
     P2, pts2, pls2, out2, plout2 = hp.graph(1)
     taken = hp.d_taken.cpu().numpy()
@@ -128,7 +135,7 @@ def test_tracking_chain(run):
         assert (P2[i]["n_points"], P2[i]["n_planes"]) == (prob["n_points"], prob["n_planes"]), i
         assert pts2[i].tobytes() == pts.tobytes(), i
         assert pls2[i].tobytes() == pls.tobytes(), i
-        r2, po2, plo2 = oracle_ctypes.pose_optimize(prob, pts, pls)
+        r2, po2, plo2 = oracle_ctypes.pose_optimize(prob, pts, pls, cfg=hp.plane_cfg)
         g2 = res["pose2"][i]
         ok, err = pose_close(g2["Tcw"], r2["Tcw"])
         assert ok, (i, err)
@@ -138,6 +145,43 @@ def test_tracking_chain(run):
         n_local += o["local_nmatches"]
         n_plane_edges += len(pls)
     assert n_edges > 0 and n_local > 0 and n_plane_edges > 0
+
+
+def test_tracking_chain_independent(run):
+    """The oracle runs the whole step on its own (no GPU value fed into its chain): every decision of the
+    chain -- matches, both associations (the second carried from the first's survivors), outlier flags,
+    SearchLocalPoints -- identical, and both poses within 1e-4 (the north-star bar)."""
+    import oracle_ctypes
+    import oracle_planes
+    import oracle_step
+    from test_gpu_pose import pose_close
+    hp, res = run
+    orb, po = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures), oracle_planes.PlaneOracle()
+    _, _, _, out1, plout1 = hp.graph(0)
+    _, pts2, pls2, out2, plout2 = hp.graph(1)
+    n_planes = 0
+    for i in range(hp.B):
+        n = int(res["kp_counts"][i])
+        o = oracle_step.run(oracle_step.from_hotpath(hp, i), orb, po, supp_cap=hp.pe.supp_cap)
+        assert np.array_equal(res["match"][i, :n], o["match"]), i
+        M = len(o["coefs"])
+        for k, key in ((0, "assoc0"), (1, "assoc1")):
+            for q, name in enumerate(("match", "parallel", "vertical")):
+                assert np.array_equal(res["assoc"][k, q, i, :M], o[key][name]), (i, k, name)
+        r1, po1, plo1 = o["pose1"]
+        ok, err = pose_close(res["pose1"][i]["Tcw"], r1["Tcw"])
+        assert ok, (i, err)
+        assert np.array_equal(out1[i], po1) and np.array_equal(plout1[i], plo1), i
+        assert np.array_equal(res["local_match"][i, :n], o["local_match"]), i
+        prob, pts, pls = o["graph2"]
+        assert len(pts2[i]) == len(pts) and pls2[i].tobytes() == pls.tobytes(), i
+        r2, po2, plo2 = o["pose2"]
+        ok, err = pose_close(res["pose2"][i]["Tcw"], r2["Tcw"])
+        assert ok, (i, err)
+        assert int(res["pose2"][i]["n_inliers"]) == int(r2["n_inliers"]), i
+        assert np.array_equal(out2[i], po2) and np.array_equal(plout2[i], plo2), i
+        n_planes += M
+    assert n_planes > 0
 
 
 def test_tracked_pose_near_ground_truth(run):
@@ -153,19 +197,31 @@ def test_tracked_pose_near_ground_truth(run):
 
 def test_pipelined_steps_match_serial(run):
     """Software-pipelined steps (extraction of batch k+1 beside the tracking of batch k, double-buffered
-    extraction outputs) give the serial step's results bit for bit."""
+    extraction outputs and per-batch inputs) give the serial step's results bit for bit, step by step.  The
+    inputs rotate between batches (slot i of batch k = slot (i + k) % B), so a stage that read the other
+    buffer set, or an extraction that overwrote a set still being tracked, changes some step's results."""
     import pipeline
-    hp0, res0 = run
-    hp = pipeline.HotPath(hp0.B, unique_frames=hp0.B, n_boxes=3, pipelined=True)
-    try:
-        for _ in range(3):
-            hp.step()
-        res = hp.results()
-    finally:
-        hp.close()
-    for key in ("kp_counts", "plane_counts", "supposed_counts", "match", "nmatches", "local_match",
-                "local_nmatches", "assoc", "new_plane"):
-        assert np.array_equal(res[key], res0[key]), key
-    assert res["kps"].tobytes() == res0["kps"].tobytes()
-    for key in ("pose1", "pose2"):
-        assert res[key].tobytes() == res0[key].tobytes(), key
+    hp0, _ = run
+    if hp0.config_name != "c2":
+        pytest.skip("one config suffices for the scheduling check")
+    steps = 4
+    out = {}
+    for mode in (False, True):
+        hp = pipeline.HotPath(hp0.B, unique_frames=hp0.B, n_boxes=3, pipelined=mode, rotate_inputs=True)
+        try:
+            out[mode] = []
+            for _ in range(steps):
+                hp.step()
+                out[mode].append(hp.results())
+        finally:
+            hp.close()
+    for k in range(steps):
+        ser, pip = out[False][k], out[True][k]
+        for key in ("kp_counts", "plane_counts", "supposed_counts", "match", "nmatches", "local_match",
+                    "local_nmatches", "assoc", "new_plane"):
+            assert np.array_equal(pip[key], ser[key]), (k, key)
+        assert pip["kps"].tobytes() == ser["kps"].tobytes(), k
+        for key in ("pose1", "pose2"):
+            assert pip[key].tobytes() == ser[key].tobytes(), (k, key)
+    # the batches really differ: slot 0 of consecutive steps tracks different frames
+    assert not np.array_equal(out[True][0]["pose2"][0]["Tcw"], out[True][1]["pose2"][0]["Tcw"])
