@@ -1,6 +1,7 @@
 # Build of the MI355X (gfx950) hot-path library and the CPU oracle.
 #   make            -> sp-slam_amd/libspslam_gpu.so  and  oracle/liboracle.so
 # hipcc cross-compiles for gfx950 in the build container (no GPU needed).
+# One object per source (parallel with make -j), linked into one shared library.
 HIPCC ?= /opt/rocm/bin/hipcc
 OFFLOAD_ARCH ?= gfx950
 HIPFLAGS ?= --offload-arch=$(OFFLOAD_ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
@@ -8,20 +9,30 @@ HIPFLAGS ?= --offload-arch=$(OFFLOAD_ARCH) -O3 -std=c++17 -fPIC -ffp-contract=of
 
 PKG := sp-slam_amd
 CSRC := $(PKG)/csrc
-GPU_SRCS := $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/plane_kernels.hip $(CSRC)/plane_segment.hip $(CSRC)/supposed_kernels.hip $(CSRC)/frame_kernels.hip $(CSRC)/lba_kernels.hip $(CSRC)/assoc_kernels.hip $(CSRC)/match_kernels.hip $(CSRC)/track_kernels.hip $(CSRC)/grab_kernels.hip $(CSRC)/spslam_capi.cpp
-GPU_HDRS := $(CSRC)/wave_priority.h $(CSRC)/orb_geom.h $(CSRC)/orb_launch.h $(CSRC)/pose_launch.h $(CSRC)/plane_launch.h $(CSRC)/supposed_launch.h $(CSRC)/frame_launch.h $(CSRC)/libm_restated.h $(CSRC)/g2o_device.h $(CSRC)/lba_launch.h $(CSRC)/assoc_launch.h $(CSRC)/match_launch.h $(CSRC)/track_launch.h $(CSRC)/grab_launch.h $(CSRC)/plane_not_seen.h include/spslam_gpu.h include/spslam_brief_pattern.inc
+OBJDIR := build/obj
+KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels \
+           assoc_kernels match_kernels track_kernels grab_kernels bow_kernels
+OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+GPU_HDRS := $(wildcard $(CSRC)/*.h) include/spslam_gpu.h include/spslam_brief_pattern.inc
 
 all: $(PKG)/libspslam_gpu.so oracle/liboracle.so
 
-$(PKG)/libspslam_gpu.so: $(GPU_SRCS) $(GPU_HDRS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(CSRC)/orb_kernels.hip $(CSRC)/pose_kernels.hip $(CSRC)/plane_kernels.hip $(CSRC)/plane_segment.hip $(CSRC)/supposed_kernels.hip $(CSRC)/frame_kernels.hip $(CSRC)/lba_kernels.hip $(CSRC)/assoc_kernels.hip $(CSRC)/match_kernels.hip $(CSRC)/track_kernels.hip $(CSRC)/grab_kernels.hip \
-	    -x hip $(CSRC)/spslam_capi.cpp
+$(OBJDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OBJDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -x hip -o $@ $<
+
+$(PKG)/libspslam_gpu.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(OBJS)
 
 oracle/liboracle.so:
 	$(MAKE) -C oracle liboracle.so
 
 clean:
-	rm -f $(PKG)/libspslam_gpu.so
+	rm -rf $(PKG)/libspslam_gpu.so $(OBJDIR)
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean oracle/liboracle.so

@@ -768,6 +768,92 @@ typedef struct spslam_track_batch {
 int spslam_track_graph_batch_device(spslam_ctx* ctx, int n_frames, int stage, const spslam_track_batch* batch,
                                     void* hip_stream);
 
+/* ---------------------------------------------------------------- bag of words
+ * DBoW2 (vendored Thirdparty/DBoW2) as the tracking path uses it:
+ *   spslam_bow_load_vocabulary  TemplatedVocabulary::loadFromTextFile
+ *                               (DBoW2/TemplatedVocabulary.h:1338-1424; System.cc:64 loads
+ *                               ORBvoc.txt this way).  The text is "k L scoring weighting"
+ *                               then one "parent isLeaf d0..d31 weight" line per node; an
+ *                               empty line after a final newline becomes one more leaf under
+ *                               the root with weight 0 (the reference's eof loop), whose
+ *                               descriptor the reference leaves uninitialised (zero here).
+ *                               One vocabulary per context, resident in HBM.
+ *   spslam_bow_transform        Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:495-502,
+ *                               src/KeyFrame.cc:64-72): TemplatedVocabulary::transform(
+ *                               descriptors, mBowVec, mFeatVec, levelsup = 4) (:1127-1194,
+ *                               :1217-1259): BowVector = sorted (word id, value) pairs
+ *                               (TF-IDF: summed idf weights, then L1-normalised for ORBvoc's
+ *                               L1_NORM scoring), FeatureVector = sorted node ids (the node at
+ *                               level L - levelsup on each feature's path) with the feature
+ *                               indices of each node in increasing order (CSR: fv_start has
+ *                               n_fv + 1 entries).  Stop words (weight 0) are in neither.
+ *   spslam_search_by_bow        ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+ *                               (src/ORBmatcher.cc:159-288), as TrackReferenceKeyFrame
+ *                               (matcher(0.7, true), Tracking.cc:797-802) and Relocalization
+ *                               (0.75, Tracking.cc:1593-1609) call it: per shared FeatureVector
+ *                               node, each keyframe feature with a good map point takes the
+ *                               closest free frame feature if its distance <= TH_LOW (50) and
+ *                               < nn_ratio x the second best; rotation-consistency filter
+ *                               (HISTO_LENGTH 30, ComputeThreeMaxima).  Output per frame
+ *                               feature: the keyframe feature whose map point it receives
+ *                               (vpMapPointMatches), -1 if none; return value nmatches. */
+typedef struct spslam_bow_params {
+    float nn_ratio;           /* ORBmatcher mfNNratio (0.7 TrackReferenceKeyFrame, 0.75 Relocalization) */
+    int32_t check_orientation;/* mbCheckOrientation */
+} spslam_bow_params;
+
+/* text: the vocabulary file's bytes (len of them).  Outputs (may be NULL): k, L, node and word counts. */
+int spslam_bow_load_vocabulary(spslam_ctx* ctx, const char* text, size_t len, int* k, int* L, int* n_nodes,
+                               int* n_words);
+
+/* Drop-in for one frame on host buffers: desc n x 32 bytes.  bow_words / bow_values:
+ * >= n entries, *n_bow receives the BowVector size; fv_nodes: >= n, fv_start: >= n + 1,
+ * fv_features: >= n entries, *n_fv the FeatureVector size. */
+int spslam_bow_transform(spslam_ctx* ctx, const uint8_t* desc, int n, int levelsup, uint32_t* bow_words,
+                         double* bow_values, int* n_bow, uint32_t* fv_nodes, int32_t* fv_start,
+                         int32_t* fv_features, int* n_fv);
+
+/* Batched, device resident: frame f's d_counts[f] descriptors at d_desc + f*cap*32 (the ORB
+ * batch layout).  Outputs of frame f at f*cap (d_fv_start at f*(cap+1), relative to the
+ * frame's f*cap); d_n_bow / d_n_fv one int per frame.  cap <= 8192. */
+int spslam_bow_transform_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* d_desc, const int* d_counts,
+                                      int cap, int levelsup, uint32_t* d_bow_words, double* d_bow_values,
+                                      int* d_n_bow, uint32_t* d_fv_nodes, int32_t* d_fv_start,
+                                      int32_t* d_fv_features, int* d_n_fv, void* hip_stream);
+
+/* One side of SearchByBoW in the batch layout of spslam_bow_transform_batch_device:
+ * slot f's features at f*cap (descriptors, keypoints -- only .angle is read -- and, on the
+ * keyframe side, has_point[i] = GetMapPointMatches()[i] && !isBad()), its FeatureVector at
+ * f*cap / f*(cap+1). */
+typedef struct spslam_bow_side {
+    const uint8_t* desc;
+    const spslam_keypoint* keys;     /* keyframe: mvKeysUn; frame: mvKeys */
+    const uint8_t* has_point;        /* keyframe side; ignored on the frame side */
+    const int* counts;
+    const uint32_t* fv_nodes;
+    const int32_t* fv_start;
+    const int32_t* fv_features;
+    const int* n_fv;
+    int32_t cap;
+    int32_t pad;
+} spslam_bow_side;
+
+/* Drop-in for one (keyframe, frame) pair on host buffers (FeatureVectors as spslam_bow_transform
+ * returns them).  match: f_n ints. */
+int spslam_search_by_bow(spslam_ctx* ctx, const uint8_t* kf_desc, const spslam_keypoint* kf_keys,
+                         const uint8_t* kf_has_point, int kf_n, const uint32_t* kf_fv_nodes,
+                         const int32_t* kf_fv_start, const int32_t* kf_fv_features, int kf_n_fv,
+                         const uint8_t* f_desc, const spslam_keypoint* f_keys, int f_n, const uint32_t* f_fv_nodes,
+                         const int32_t* f_fv_start, const int32_t* f_fv_features, int f_n_fv,
+                         const spslam_bow_params* params, int32_t* match, int* nmatches);
+
+/* Batched, device resident: pair p = (keyframe slot, frame slot) = d_pairs[2p], d_pairs[2p+1];
+ * d_match at p * frame.cap, d_nmatches one int per pair. */
+int spslam_search_by_bow_batch_device(spslam_ctx* ctx, int n_pairs, const int32_t* d_pairs,
+                                      const spslam_bow_side* keyframe, const spslam_bow_side* frame,
+                                      const spslam_bow_params* params, int32_t* d_match, int* d_nmatches,
+                                      void* hip_stream);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

@@ -861,7 +861,8 @@ const char* kernel_kind_name(int kind) {
                                                  "plane_segment_kernel", "supp_lines_kernel",
                                                  "supp_assemble_kernel", "frame_rgbd_kernel",
                                                  "lba_batch", "plane_assoc_kernel", "search_projection",
-                                                 "search_local_points", "track_graph_kernel", "grab_rgbd_kernel"};
+                                                 "search_local_points", "track_graph_kernel", "grab_rgbd_kernel",
+                                                 "bow_words_kernel", "bow_vectors_kernel", "bow_search_kernel"};
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 

@@ -21,7 +21,7 @@ enum KernelKind {
     kKindLevel = 0, kKindFast, kKindOctree, kKindDesc, kKindPose,
     kKindPlaneCloud, kKindPlaneDist, kKindPlaneIntegral, kKindPlaneNormal, kKindPlaneSegment,
     kKindSuppLines, kKindSuppAssemble, kKindFrame, kKindLba, kKindAssoc, kKindMatch, kKindLocalMatch,
-    kKindTrack, kKindGrab, kNumKernelKinds
+    kKindTrack, kKindGrab, kKindBowWords, kKindBowVectors, kKindBowMatch, kNumKernelKinds
 };
 const char* kernel_kind_name(int kind);
 

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <sstream>
 #include <random>
 #include <string>
 #include <vector>
@@ -23,6 +24,7 @@
 #include "frame_launch.h"
 #include "lba_launch.h"
 #include "assoc_launch.h"
+#include "bow_launch.h"
 #include "match_launch.h"
 #include "track_launch.h"
 #include "grab_launch.h"
@@ -136,6 +138,13 @@ struct spslam_ctx {
     // projection matching: per (frame, last-frame point) windows + accepted-match lists
     uint8_t* d_match_scratch = nullptr;
     size_t match_scratch_bytes = 0;
+    // bag of words: the vocabulary (one HBM blob), per-feature transform scratch, drop-in staging
+    uint8_t* d_vocab = nullptr;
+    VocabDev vocab{};
+    uint8_t* d_bow_scratch = nullptr;
+    size_t bow_scratch_bytes = 0;
+    uint8_t* d_bow_stage = nullptr;
+    size_t bow_stage_bytes = 0;
 };
 
 namespace {
@@ -261,7 +270,8 @@ void free_all(spslam_ctx* c) {
                     c->d_desc,   c->d_cnt,    c->d_pose_scratch,  c->d_plane_scratch, c->d_depth_in,
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
                     c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1,
-                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work, c->d_assoc_dist, c->d_match_scratch};
+                    c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work, c->d_assoc_dist, c->d_match_scratch,
+                    c->d_vocab, c->d_bow_scratch, c->d_bow_stage};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1385,6 +1395,250 @@ int spslam_search_local_points(spslam_ctx* c, const spslam_local_frame* frame, c
     HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[10], sizeof(int), hipMemcpyDeviceToHost, c->stream));
     if (in_view && np) HIP_CHECK(c, hipMemcpyAsync(in_view, q + o[11], (size_t)np, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
+// ---------------------------------------------------------------- bag of words
+// TemplatedVocabulary::loadFromTextFile (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1338-1424), host side,
+// then one HBM blob: descriptors, children CSR, weights, word ids.
+int spslam_bow_load_vocabulary(spslam_ctx* c, const char* text, size_t len, int* k_out, int* L_out, int* n_nodes_out,
+                               int* n_words_out) {
+    if (!c || (!text && len)) return SPSLAM_ERR_ARG;
+    std::istringstream f(std::string(text ? text : "", len));
+    std::string line;
+    std::getline(f, line);
+    std::stringstream ss;
+    ss << line;
+    int k = 0, L = 0, n1 = 0, n2 = 0;
+    ss >> k >> L >> n1 >> n2;
+    if (k < 0 || k > 20 || L < 1 || L > 10 || n1 < 0 || n1 > 5 || n2 < 0 || n2 > 3)
+        return fail(c, SPSLAM_ERR_ARG, "vocabulary header is not DBoW2 text%s", "");
+    std::vector<int> parent(1, 0);
+    std::vector<std::vector<int>> children(1);
+    std::vector<uint8_t> desc(32, 0);
+    std::vector<double> weight(1, 0.0);
+    std::vector<uint32_t> word(1, 0);
+    uint32_t n_words = 0;
+    while (!f.eof()) {  // the reference's loop: an empty last line still makes a node
+        std::string sn;
+        std::getline(f, sn);
+        std::stringstream sl;
+        sl << sn;
+        const int nid = (int)parent.size();
+        int pid = 0, leaf = 0;
+        sl >> pid;
+        if (pid < 0 || pid >= nid) return fail(c, SPSLAM_ERR_ARG, "vocabulary node with a bad parent%s", "");
+        sl >> leaf;
+        std::stringstream sd;
+        for (int i = 0; i < 32; i++) {
+            std::string e;
+            sl >> e;
+            sd << e << " ";
+        }
+        uint8_t d[32] = {0};  // FORB::fromString leaves unparsed bytes unset (uninitialised there, zero here)
+        for (int i = 0; i < 32; i++) {
+            int v;
+            sd >> v;
+            if (!sd.fail()) d[i] = (uint8_t)v;
+        }
+        double w = 0.0;
+        sl >> w;
+        parent.push_back(pid);
+        children.emplace_back();
+        children[pid].push_back(nid);
+        desc.insert(desc.end(), d, d + 32);
+        weight.push_back(w);
+        word.push_back(leaf > 0 ? n_words++ : 0u);
+    }
+    const int n = (int)parent.size();
+    std::vector<int> cbeg(n), ccnt(n), cids;
+    cids.reserve(n);
+    for (int i = 0; i < n; i++) {
+        cbeg[i] = (int)cids.size();
+        ccnt[i] = (int)children[i].size();
+        cids.insert(cids.end(), children[i].begin(), children[i].end());
+    }
+    if (cids.empty()) cids.push_back(0);
+    const size_t sz[] = {(size_t)n * 32, (size_t)n * 4, (size_t)n * 4, cids.size() * 4, (size_t)n * 8, (size_t)n * 4};
+    size_t off[6], bytes = 0;
+    for (int i = 0; i < 6; i++) { off[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (c->d_vocab) (void)hipFree(c->d_vocab);
+    c->d_vocab = nullptr;
+    c->vocab = VocabDev{};
+    HIP_CHECK(c, hipMalloc(&c->d_vocab, bytes));
+    const void* src[] = {desc.data(), cbeg.data(), ccnt.data(), cids.data(), weight.data(), word.data()};
+    for (int i = 0; i < 6; i++) HIP_CHECK(c, hipMemcpy(c->d_vocab + off[i], src[i], sz[i], hipMemcpyHostToDevice));
+    VocabDev& V = c->vocab;
+    V.n_nodes = n; V.k = k; V.L = L; V.scoring = n1; V.weighting = n2;
+    V.desc = (const uint4*)(c->d_vocab + off[0]);
+    V.child_begin = (const int*)(c->d_vocab + off[1]);
+    V.child_count = (const int*)(c->d_vocab + off[2]);
+    V.child_ids = (const int*)(c->d_vocab + off[3]);
+    V.weight = (const double*)(c->d_vocab + off[4]);
+    V.word_id = (const uint32_t*)(c->d_vocab + off[5]);
+    if (k_out) *k_out = k;
+    if (L_out) *L_out = L;
+    if (n_nodes_out) *n_nodes_out = n;
+    if (n_words_out) *n_words_out = (int)n_words;
+    return SPSLAM_OK;
+}
+
+int spslam_bow_transform_batch_device(spslam_ctx* c, int n_frames, const uint8_t* d_desc, const int* d_counts,
+                                      int cap, int levelsup, uint32_t* d_bow_words, double* d_bow_values,
+                                      int* d_n_bow, uint32_t* d_fv_nodes, int32_t* d_fv_start,
+                                      int32_t* d_fv_features, int* d_n_fv, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->d_vocab) return fail(c, SPSLAM_ERR_NOT_READY, "no vocabulary loaded (spslam_bow_load_vocabulary)%s", "");
+    if (n_frames < 1 || !d_desc || !d_counts || cap < 1 || cap > 8192 || !d_bow_words || !d_bow_values || !d_n_bow ||
+        !d_fv_nodes || !d_fv_start || !d_fv_features || !d_n_fv)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_bow_transform_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (c->vocab.n_nodes < 2) {  // empty vocabulary: transform clears both vectors
+        HIP_CHECK(c, hipMemsetAsync(d_n_bow, 0, (size_t)n_frames * sizeof(int), s));
+        HIP_CHECK(c, hipMemsetAsync(d_n_fv, 0, (size_t)n_frames * sizeof(int), s));
+        return SPSLAM_OK;
+    }
+    const size_t n = (size_t)n_frames * cap;
+    const size_t need = n * 16 + 512;
+    if (need > c->bow_scratch_bytes) {
+        HIP_CHECK(c, hipStreamSynchronize(s));
+        if (c->d_bow_scratch) (void)hipFree(c->d_bow_scratch);
+        c->d_bow_scratch = nullptr;
+        c->bow_scratch_bytes = 0;
+        HIP_CHECK(c, hipMalloc(&c->d_bow_scratch, need));
+        c->bow_scratch_bytes = need;
+    }
+    auto* s_weight = (double*)c->d_bow_scratch;
+    auto* s_word = (uint32_t*)(c->d_bow_scratch + ((n * 8 + 255) & ~(size_t)255));
+    auto* s_node = s_word + ((n + 63) & ~(size_t)63);
+    BowOut out{d_bow_words, d_bow_values, d_n_bow, d_fv_nodes, d_fv_start, d_fv_features, d_n_fv};
+    HIP_CHECK(c, bow_transform_launch(c->vocab, n_frames, d_desc, d_counts, cap, levelsup, s_word, s_weight, s_node,
+                                      out, s, c->timer));
+    return SPSLAM_OK;
+}
+
+// grow the BoW drop-in staging buffer
+static int bow_stage(spslam_ctx* c, size_t bytes) {
+    if (bytes <= c->bow_stage_bytes) return SPSLAM_OK;
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (c->d_bow_stage) (void)hipFree(c->d_bow_stage);
+    c->d_bow_stage = nullptr;
+    c->bow_stage_bytes = 0;
+    HIP_CHECK(c, hipMalloc(&c->d_bow_stage, bytes));
+    c->bow_stage_bytes = bytes;
+    return SPSLAM_OK;
+}
+
+int spslam_bow_transform(spslam_ctx* c, const uint8_t* desc, int n, int levelsup, uint32_t* bow_words,
+                         double* bow_values, int* n_bow, uint32_t* fv_nodes, int32_t* fv_start,
+                         int32_t* fv_features, int* n_fv) {
+    if (!c || n < 0 || (n && !desc) || !n_bow || !n_fv || n > 8192 || !fv_start ||
+        (n && (!bow_words || !bow_values || !fv_nodes || !fv_features)))
+        return SPSLAM_ERR_ARG;
+    if (!c->d_vocab) return fail(c, SPSLAM_ERR_NOT_READY, "no vocabulary loaded (spslam_bow_load_vocabulary)%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const int cap = std::max(n, 1);
+    const size_t sz[] = {(size_t)cap * 32, 4, (size_t)cap * 4, (size_t)cap * 8, 4, (size_t)cap * 4,
+                         (size_t)(cap + 1) * 4, (size_t)cap * 4, 4};
+    size_t o[9], bytes = 0;
+    for (int i = 0; i < 9; i++) { o[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    if (int rc = bow_stage(c, bytes)) return rc;
+    uint8_t* q = c->d_bow_stage;
+    if (n) HIP_CHECK(c, hipMemcpyAsync(q + o[0], desc, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(q + o[1], &n, 4, hipMemcpyHostToDevice, c->stream));
+    int rc = spslam_bow_transform_batch_device(c, 1, q + o[0], (const int*)(q + o[1]), cap, levelsup,
+                                               (uint32_t*)(q + o[2]), (double*)(q + o[3]), (int*)(q + o[4]),
+                                               (uint32_t*)(q + o[5]), (int32_t*)(q + o[6]), (int32_t*)(q + o[7]),
+                                               (int*)(q + o[8]), c->stream);
+    if (rc) return rc;
+    HIP_CHECK(c, hipMemcpyAsync(n_bow, q + o[4], 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(n_fv, q + o[8], 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (*n_bow) {
+        HIP_CHECK(c, hipMemcpy(bow_words, q + o[2], (size_t)*n_bow * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(c, hipMemcpy(bow_values, q + o[3], (size_t)*n_bow * 8, hipMemcpyDeviceToHost));
+    }
+    if (*n_fv) {
+        HIP_CHECK(c, hipMemcpy(fv_nodes, q + o[5], (size_t)*n_fv * 4, hipMemcpyDeviceToHost));
+        HIP_CHECK(c, hipMemcpy(fv_start, q + o[6], (size_t)(*n_fv + 1) * 4, hipMemcpyDeviceToHost));
+        int m = 0;
+        std::memcpy(&m, fv_start + *n_fv, 4);
+        if (m) HIP_CHECK(c, hipMemcpy(fv_features, q + o[7], (size_t)m * 4, hipMemcpyDeviceToHost));
+    } else {
+        fv_start[0] = 0;
+    }
+    return SPSLAM_OK;
+}
+
+int spslam_search_by_bow_batch_device(spslam_ctx* c, int n_pairs, const int32_t* d_pairs,
+                                      const spslam_bow_side* kf, const spslam_bow_side* fr,
+                                      const spslam_bow_params* params, int32_t* d_match, int* d_nmatches,
+                                      void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    auto side_ok = [](const spslam_bow_side* b, bool keyframe) {
+        return b && b->desc && b->keys && b->counts && b->fv_nodes && b->fv_start && b->fv_features && b->n_fv &&
+               b->cap >= 1 && b->cap <= 8192 && (!keyframe || b->has_point);
+    };
+    if (n_pairs < 1 || !d_pairs || !side_ok(kf, true) || !side_ok(fr, false) || !params || !d_match || !d_nmatches)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_search_by_bow_batch_device");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    BowSide K{kf->desc, kf->keys, kf->has_point, kf->counts, kf->fv_nodes, kf->fv_start, kf->fv_features, kf->n_fv,
+              kf->cap};
+    BowSide F{fr->desc, fr->keys, nullptr, fr->counts, fr->fv_nodes, fr->fv_start, fr->fv_features, fr->n_fv, fr->cap};
+    HIP_CHECK(c, bow_search_launch(n_pairs, (const int2*)d_pairs, K, F, params->nn_ratio, params->check_orientation,
+                                   d_match, d_nmatches, (hipStream_t)hip_stream, c->timer));
+    return SPSLAM_OK;
+}
+
+int spslam_search_by_bow(spslam_ctx* c, const uint8_t* kf_desc, const spslam_keypoint* kf_keys,
+                         const uint8_t* kf_has_point, int kf_n, const uint32_t* kf_fv_nodes,
+                         const int32_t* kf_fv_start, const int32_t* kf_fv_features, int kf_n_fv,
+                         const uint8_t* f_desc, const spslam_keypoint* f_keys, int f_n, const uint32_t* f_fv_nodes,
+                         const int32_t* f_fv_start, const int32_t* f_fv_features, int f_n_fv,
+                         const spslam_bow_params* params, int32_t* match, int* nmatches) {
+    if (!c || !params || !nmatches || kf_n < 0 || f_n < 0 || kf_n > 8192 || f_n > 8192 || kf_n_fv < 0 ||
+        f_n_fv < 0 || kf_n_fv > std::max(kf_n, 1) || f_n_fv > std::max(f_n, 1) || !kf_fv_start || !f_fv_start ||
+        (kf_n && (!kf_desc || !kf_keys || !kf_has_point)) || (f_n && (!f_desc || !f_keys || !match)) ||
+        (kf_n_fv && (!kf_fv_nodes || !kf_fv_features)) || (f_n_fv && (!f_fv_nodes || !f_fv_features)))
+        return SPSLAM_ERR_ARG;
+    const int kc = std::max(kf_n, 1), fc = std::max(f_n, 1);
+    const int km = kf_fv_start[kf_n_fv], fm = f_fv_start[f_n_fv];
+    if (km < 0 || km > kf_n || fm < 0 || fm > f_n)
+        return fail(c, SPSLAM_ERR_ARG, "FeatureVector does not fit the features%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    // keyframe slot 0 and frame slot 0 of a one-pair batch
+    const size_t sz[] = {(size_t)kc * 32, (size_t)kc * sizeof(spslam_keypoint), (size_t)kc, 4, (size_t)kc * 4,
+                         (size_t)(kc + 1) * 4, (size_t)kc * 4, 4,
+                         (size_t)fc * 32, (size_t)fc * sizeof(spslam_keypoint), 4, (size_t)fc * 4,
+                         (size_t)(fc + 1) * 4, (size_t)fc * 4, 4, 8, (size_t)fc * 4, 4};
+    size_t o[18], bytes = 0;
+    for (int i = 0; i < 18; i++) { o[i] = bytes; bytes += (sz[i] + 255) / 256 * 256; }
+    if (int rc = bow_stage(c, bytes)) return rc;
+    uint8_t* q = c->d_bow_stage;
+    const int32_t pair[2] = {0, 0};
+    const void* src[] = {kf_desc, kf_keys, kf_has_point, &kf_n, kf_fv_nodes, kf_fv_start, kf_fv_features, &kf_n_fv,
+                         f_desc, f_keys, &f_n, f_fv_nodes, f_fv_start, f_fv_features, &f_n_fv, pair};
+    const size_t len[] = {(size_t)kf_n * 32, (size_t)kf_n * sizeof(spslam_keypoint), (size_t)kf_n, 4,
+                          (size_t)kf_n_fv * 4, (size_t)(kf_n_fv + 1) * 4, (size_t)km * 4, 4,
+                          (size_t)f_n * 32, (size_t)f_n * sizeof(spslam_keypoint), 4, (size_t)f_n_fv * 4,
+                          (size_t)(f_n_fv + 1) * 4, (size_t)fm * 4, 4, 8};
+    for (int i = 0; i < 16; i++)
+        if (len[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], len[i], hipMemcpyHostToDevice, c->stream));
+    spslam_bow_side K{q + o[0], (const spslam_keypoint*)(q + o[1]), q + o[2], (const int*)(q + o[3]),
+                      (const uint32_t*)(q + o[4]), (const int32_t*)(q + o[5]), (const int32_t*)(q + o[6]),
+                      (const int*)(q + o[7]), kc, 0};
+    spslam_bow_side F{q + o[8], (const spslam_keypoint*)(q + o[9]), nullptr, (const int*)(q + o[10]),
+                      (const uint32_t*)(q + o[11]), (const int32_t*)(q + o[12]), (const int32_t*)(q + o[13]),
+                      (const int*)(q + o[14]), fc, 0};
+    int rc = spslam_search_by_bow_batch_device(c, 1, (const int32_t*)(q + o[15]), &K, &F, params,
+                                               (int32_t*)(q + o[16]), (int*)(q + o[17]), c->stream);
+    if (rc) return rc;
+    if (f_n) HIP_CHECK(c, hipMemcpyAsync(match, q + o[16], (size_t)f_n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[17], 4, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
     return SPSLAM_OK;
 }

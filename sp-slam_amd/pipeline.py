@@ -43,10 +43,12 @@ import synth
 #   c2/c3  TUM-style 640x480 (Examples/RGB-D/TUM3.yaml intrinsics, TUM1.yaml plane keys)
 #   c4     ICL-NUIM (Examples/RGB-D/ICL.yaml: fx 481.2, fy -480.0, Plane.MinSize 1000, Chi 1000, VPChi 200)
 #   c5     1280x960, nFeatures 4000, dense-plane scene
+# 640x480 scenes hold 5 boxes: about 6 extracted planes and 0.4 supposed planes per frame (GeneratePlanesFromBoundries
+# accepts a boundary line only where a box edge is not an occlusion border; 3 boxes gave none on sequence 0)
 CONFIGS = {
-    "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=3),
-    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=3, lba_every=5),
-    "c4": dict(width=640, height=480, nfeatures=1000, n_boxes=3, K=synth.ICL, min_size=1000, chi=1000.0,
+    "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=5),
+    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=5, lba_every=5),
+    "c4": dict(width=640, height=480, nfeatures=1000, n_boxes=5, K=synth.ICL, min_size=1000, chi=1000.0,
                vp_chi=200.0),
     "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8),
 }

@@ -207,7 +207,7 @@ def test_pipelined_steps_match_serial(run):
     steps = 4
     out = {}
     for mode in (False, True):
-        hp = pipeline.HotPath(hp0.B, unique_frames=hp0.B, n_boxes=3, pipelined=mode, rotate_inputs=True)
+        hp = pipeline.HotPath(hp0.B, unique_frames=hp0.B, pipelined=mode, rotate_inputs=True, **pipeline.CONFIGS["c2"])
         try:
             out[mode] = []
             for _ in range(steps):
