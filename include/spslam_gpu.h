@@ -562,7 +562,7 @@ typedef struct spslam_proj_point {
     int32_t octave;       /* LastFrame.mvKeys[i].octave */
     int32_t n_obs;        /* MapPoint::Observations(): 0 (a visual-odometry point) does not block a keypoint */
     int32_t last_index;   /* i (informative) */
-    int32_t pad;
+    int32_t id;           /* MapPoint::mnId (the caller's bookkeeping: seen stamps, next last frame) */
     uint8_t desc[32];     /* MapPoint::GetDescriptor */
 } spslam_proj_point;      /* 64 bytes */
 
@@ -618,8 +618,9 @@ typedef struct spslam_local_point {
     float normal[3];      /* MapPoint::GetNormal */
     float min_dist;       /* mfMinDistance (the invariance region is 0.8x .. 1.2x mfMaxDistance) */
     float max_dist;       /* mfMaxDistance */
-    int32_t id;           /* mnId (informative) */
-    int32_t pad[3];
+    int32_t id;           /* mnId: index into the frame's seen-stamp array (batched form) */
+    int32_t n_obs;        /* MapPoint::Observations() (carried into the next last frame) */
+    int32_t pad[2];
     uint8_t desc[32];     /* MapPoint::GetDescriptor */
 } spslam_local_point;     /* 80 bytes */
 
@@ -627,7 +628,8 @@ typedef struct spslam_local_frame {
     float Tcw[16];        /* CurrentFrame.mTcw after the motion-model PoseOptimization */
     int32_t point_offset; /* local points [point_offset, point_offset + n_points) */
     int32_t n_points;
-    int32_t pad[2];
+    int32_t seen_offset;  /* batched form with d_seen: point p is skipped when d_seen[seen_offset + p.id] == stamp */
+    int32_t stamp;        /*   (mnLastFrameSeen == mCurrentFrame.mnId, Tracking.cc:1380-1395) */
 } spslam_local_frame;     /* 80 bytes */
 
 typedef struct spslam_local_params {
@@ -644,14 +646,18 @@ int spslam_search_local_points(spslam_ctx* ctx, const spslam_local_frame* frame,
 
 /* Batched, device resident, same current-frame layout as
  * spslam_search_by_projection_batch_device; d_taken at f*cap (may be NULL),
- * d_in_view at the points' global index (may be NULL). */
+ * d_in_view at the points' global index (may be NULL).  d_seen (may be NULL):
+ * the frames' seen stamps (spslam_local_frame.seen_offset / stamp; the
+ * SPSLAM_TRACK_DISCARD stage writes them), so the local map can be passed
+ * whole and the points the frame already tracks are skipped on the device. */
 int spslam_search_local_points_batch_device(spslam_ctx* ctx, int n_frames, const spslam_local_frame* d_frames,
                                             const spslam_local_point* d_points, int max_points,
                                             const spslam_keypoint* d_keys_un, const uint8_t* d_desc,
                                             const float* d_uright, const int32_t* d_grid_off,
                                             const int32_t* d_grid_idx, const int* d_counts, int cap,
                                             const uint8_t* d_taken, const spslam_local_params* params,
-                                            int32_t* d_match, int* d_nmatches, uint8_t* d_in_view, void* hip_stream);
+                                            int32_t* d_match, int* d_nmatches, uint8_t* d_in_view,
+                                            const int32_t* d_seen, void* hip_stream);
 
 /* ---------------------------------------------------------------- input images
  * Tracking::GrabImageRGBD's image preparation (src/Tracking.cc:208-229), the
@@ -706,6 +712,10 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
  *   with Observations() > 0 (src/ORBmatcher.cc:95-97); the optimized pose is
  *   written into local_frames[f].Tcw and, if given, assoc_frames_next[f].Tcw
  *   (the second association runs at that pose, src/Tracking.cc:1066).
+ *   With `seen` given it also stamps every map point the motion model matched
+ *   (inliers and discarded outliers both get mnLastFrameSeen = the frame,
+ *   Tracking.cc:997 and :1380-1390): seen[local_frames[f].seen_offset + id] =
+ *   local_frames[f].stamp, which spslam_search_local_points_batch_device skips.
  * SPSLAM_TRACK_LOCAL_MAP -- TrackLocalMap's graph (src/Tracking.cc:1062-1068):
  *   mvpMapPoints = the surviving motion-model points, replaced by the
  *   SearchLocalPoints match where it assigned one (it may re-assign a keypoint
@@ -719,10 +729,30 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
  * global map-plane indices.  The graphs are written with point_offset = f * cap
  * and plane_offset = f * 3 * (cap_a + cap_b), so the PoseOptimization outlier
  * flags of frame f are at the same offsets.  The Tracking state machine
- * (nmatches < 10 -> TrackReferenceKeyFrame, relocalisation) is the caller's. */
+ * (nmatches < 10 -> TrackReferenceKeyFrame, relocalisation) is the caller's.
+ *
+ * Frame-to-frame state of a tracked sequence (Tracking::Track, src/Tracking.cc:
+ * 443-505, TrackWithMotionModel :956-958), for batches that are consecutive
+ * frames of their sequences:
+ * SPSLAM_TRACK_MOTION_PRIOR -- mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw):
+ *   proj_frames[f].Tcw = velocity[f] (4x4 row-major float) * proj_frames[f].Tlw
+ *   (cv::Mat float product), also into assoc_frames_first[f].Tcw when given.
+ *   The reference re-derives mLastFrame.mTcw through its reference keyframe
+ *   (UpdateLastFrame, Tlr * Tref) first; with fixed keyframe poses that is the
+ *   last pose up to float rounding, and is not restated.
+ * SPSLAM_TRACK_LAST_FRAME -- after the local-map PoseOptimization (results /
+ *   point_outlier = that optimisation's): mVelocity = mTcw * LastTwc (LastTwc =
+ *   [Rlw^T | -Rlw^T tlw] of proj_frames[f].Tlw), the VO-match clean-up (points
+ *   with Observations() < 1 dropped, :456-466) and the outlier drop (:484-488);
+ *   the surviving map points (local-map match, else the kept motion-model
+ *   match), in keypoint order, become the next frame's last-frame points:
+ *   next_points at f * cap (xw, mvKeysUn angle, octave, n_obs, id, descriptor),
+ *   next_frames[f] = {Tlw = mTcw, point_offset = f * cap, n_points}, velocity[f]. */
 #define SPSLAM_TRACK_MOTION_MODEL 0
 #define SPSLAM_TRACK_DISCARD 1
 #define SPSLAM_TRACK_LOCAL_MAP 2
+#define SPSLAM_TRACK_MOTION_PRIOR 3
+#define SPSLAM_TRACK_LAST_FRAME 4
 
 typedef struct spslam_track_batch {
     /* current frames */
@@ -754,6 +784,13 @@ typedef struct spslam_track_batch {
     int32_t* next_match;                    /* DISCARD writes the surviving associations (may be NULL) */
     int32_t* next_parallel;
     int32_t* next_vertical;
+    /* sequence state (MOTION_PRIOR, DISCARD stamps, LAST_FRAME) */
+    spslam_assoc_frame* assoc_frames_first;  /* MOTION_PRIOR writes Tcw (may be NULL) */
+    int32_t* seen;                        /* DISCARD stamps (may be NULL) */
+    spslam_proj_frame* next_frames;       /* LAST_FRAME writes */
+    spslam_proj_point* next_points;       /* LAST_FRAME writes, f * cap */
+    float* velocity;                      /* 16 floats per frame: MOTION_PRIOR reads, LAST_FRAME writes */
+    const uint8_t* point_outlier_local;   /* LAST_FRAME: the local-map PoseOptimization's point outlier flags */
     /* PoseOptimization graphs */
     spslam_pose_problem* problems;
     spslam_point_obs* points;             /* f * cap */

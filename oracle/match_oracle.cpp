@@ -29,13 +29,13 @@ constexpr int kCols = 64, kRows = 48, kHisto = 30, kThHigh = 100;
 struct ProjPoint {  // spslam_proj_point
     float xw[3];
     float angle;
-    int32_t octave, n_obs, last_index, pad;
+    int32_t octave, n_obs, last_index, id;
     uint8_t desc[32];
 };
 struct ProjFrame {  // spslam_proj_frame
     float Tcw[16];
     float Tlw[16];
-    int32_t point_offset, n_points, pad[2];
+    int32_t point_offset, n_points, seen_offset, stamp;
 };
 struct Keypoint {  // spslam_keypoint
     float x, y, size, angle, response;
@@ -257,12 +257,12 @@ namespace match {
 struct LocalPoint {  // spslam_local_point
     float xw[3], normal[3];
     float min_dist, max_dist;
-    int32_t id, pad[3];
+    int32_t id, n_obs, pad[2];
     uint8_t desc[32];
 };
 struct LocalFrame {  // spslam_local_frame
     float Tcw[16];
-    int32_t point_offset, n_points, pad[2];
+    int32_t point_offset, n_points, seen_offset, stamp;
 };
 struct LocalParams {  // spslam_local_params
     float th, nn_ratio, view_cos_limit, log_scale_factor;

@@ -13,7 +13,7 @@ import numpy as np
 import oracle_ctypes
 
 PROJ_POINT_DTYPE = np.dtype([("xw", "<f4", 3), ("angle", "<f4"), ("octave", "<i4"), ("n_obs", "<i4"),
-                             ("last_index", "<i4"), ("pad", "<i4"), ("desc", "u1", 32)])
+                             ("last_index", "<i4"), ("id", "<i4"), ("desc", "u1", 32)])
 PROJ_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("Tlw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"),
                              ("pad", "<i4", 2)])
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"), ("response", "<f4"),
@@ -56,8 +56,9 @@ def descriptor_distance(a, b):
 
 
 LOCAL_POINT_DTYPE = np.dtype([("xw", "<f4", 3), ("normal", "<f4", 3), ("min_dist", "<f4"), ("max_dist", "<f4"),
-                              ("id", "<i4"), ("pad", "<i4", 3), ("desc", "u1", 32)])
-LOCAL_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"), ("pad", "<i4", 2)])
+                              ("id", "<i4"), ("n_obs", "<i4"), ("pad", "<i4", 2), ("desc", "u1", 32)])
+LOCAL_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"), ("seen_offset", "<i4"),
+                              ("stamp", "<i4")])
 
 
 def search_local_points(frame, points, keys_un, desc, uright, grid_off, grid_idx, geometry, taken=None,

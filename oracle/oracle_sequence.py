@@ -1,0 +1,52 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of a tracked RGB-D sequence (the checker of
+sp-slam_amd/sequence.py and bench.py's ATE): Tracking::Track frame after
+frame (src/Tracking.cc:276-526) with the motion model --
+  mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw)       :958
+  TrackWithMotionModel + TrackLocalMap                     :950-1136 (oracle_step.run)
+  mVelocity = mCurrentFrame.mTcw * LastTwc                 :443-450
+  VO-match clean-up, outlier drop, mLastFrame = current    :456-505
+against a map of keyframe points on a fixed keyframe schedule (the harness's
+stand-in for LocalMapping; sp-slam_amd/sequence.py describes it)."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle_grab
+import oracle_match as OM
+import oracle_step
+import oracle_track as OT
+
+
+def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb, planes,
+          supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None):
+    """frames: [(rgb, depth_u16)] of frames first .. ; T0 / P0: the pose and last-frame points of frame
+    first - 1; local_of(t): the local map points of frame t (whole; the seen ones are skipped).  Returns the
+    local-map pose (float 4x4) of every frame."""
+    Tlw = np.asarray(T0, np.float32).reshape(4, 4)
+    V = np.eye(4, dtype=np.float32)  # the first tracked frame: constant-position prior (see sequence.py)
+    P = P0
+    poses = []
+    for k, (rgb, d) in enumerate(frames):
+        t = first + k
+        gray = oracle_grab.cvt_gray(rgb, rgb=True)
+        depth = oracle_grab.convert_depth(d, depth_scale)
+        pfr = np.zeros((), OM.PROJ_FRAME_DTYPE)
+        pfr["Tcw"] = OT.mat4(V, Tlw).reshape(16)
+        pfr["Tlw"] = Tlw.reshape(16)
+        pfr["n_points"] = len(P)
+        LP = local_of(t)
+        lfr = np.zeros((), OM.LOCAL_FRAME_DTYPE)
+        lfr["n_points"] = len(LP)
+        fi = oracle_step.FrameInputs(gray, depth, cam, geometry, inv_sigma2, (pfr, P), (lfr, LP), map_planes,
+                                     boundary, min_size=min_size, pose_cfg=pose_cfg, local_seen=True)
+        o = oracle_step.run(fi, orb, planes, supp_cap=supp_cap)
+        T2 = np.asarray(o["pose2"][0]["Tcw"], np.float32).reshape(4, 4)
+        P = OT.last_frame(P, o["match"], o["keep"], LP, o["local_match"], o["keys_un"], o["pose2"][1])
+        V = OT.mat4(T2, OT.inverse_pose(Tlw))
+        Tlw = T2
+        poses.append(T2.copy())
+        if on_frame:
+            on_frame(t, o, P)
+    return poses

@@ -26,11 +26,14 @@ class FrameInputs:
     """Everything one frame of the step reads: images, camera, the map it tracks against."""
 
     def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary, min_size=500,
-                 pose_cfg=None):
+                 pose_cfg=None, local_seen=False):
         self.gray, self.depth = gray, depth
         self.cam = cam                  # fx, fy, cx, cy, bf
         self.min_size = min_size        # Plane.MinSize
         self.pose_cfg = pose_cfg        # Plane.*Info / Chi / VPChi (spslam_gpu.PlaneConfig; None = TUM1.yaml)
+        # local_seen: the local map is given whole; SearchLocalPoints skips the points the motion model matched
+        # (mnLastFrameSeen, Tracking.cc:997, 1380-1401) -- by MapPoint id
+        self.local_seen = local_seen
         self.geometry = geometry        # oracle_match geometry vector (19 floats)
         self.inv_sigma2 = inv_sigma2
         self.proj = proj                # (spslam_proj_frame, spslam_proj_point[])
@@ -73,7 +76,17 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     lfr, LP = fi.local
     lfr = lfr.copy()
     lfr["Tcw"] = np.asarray(T1, np.float32).reshape(16)
-    lo, nlo, _ = oracle_match.search_local_points(lfr, LP, kun, do, ur, go, gi, fi.geometry, taken=taken)
+    if fi.local_seen:  # the caller's loop in SearchLocalPoints: points already seen by this frame are skipped
+        seen = {int(P[m]["id"]) for m in mo if m >= 0}
+        idx = np.array([j for j in range(len(LP)) if int(LP[j]["id"]) not in seen], np.int64)
+        lfs = lfr.copy()
+        lfs["n_points"] = len(idx)
+        lo_s, nlo, _ = oracle_match.search_local_points(lfs, LP[idx], kun, do, ur, go, gi, fi.geometry, taken=taken)
+        lo = np.full(len(lo_s), -1, np.int32)
+        sel = lo_s >= 0
+        lo[sel] = idx[lo_s[sel]]
+    else:
+        lo, nlo, _ = oracle_match.search_local_points(lfr, LP, kun, do, ur, go, gi, fi.geometry, taken=taken)
     out["local_match"], out["local_nmatches"] = lo, nlo
     # the second association starts from the first one's survivors (Tracking.cc:1004-1028, Map.cc:230-252)
     a0_kept = oracle_track.discard_planes(a0, plo1)
@@ -87,14 +100,20 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     return out
 
 
+def camera_inputs(hp):
+    """(cam, matcher geometry, mvInvLevelSigma2) of a sp-slam_amd/pipeline.py HotPath."""
+    t = hp.ex.tables()
+    b, ginv = hp.fs.bounds, hp.fs.grid_inv
+    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, hp.bf, *b, *ginv], t["scale"]]).astype(np.float32)
+    return (hp.fx, hp.fy, hp.cx, hp.cy, hp.bf), geo, t["inv_sigma2"]
+
+
 def from_hotpath(hp, i):
     """FrameInputs of batch slot i of a sp-slam_amd/pipeline.py HotPath (host copies of its inputs)."""
     U = len(hp.frames)
     gray = oracle_grab.cvt_gray(hp.frames[i % U][1], rgb=True)  # GrabImageRGBD, Tracking.cc:214-229
     depth = oracle_grab.convert_depth(hp.frames[i % U][2], oracle_grab.depth_scale(hp.depth_factor))
-    t = hp.ex.tables()
-    b, ginv = hp.fs.bounds, hp.fs.grid_inv
-    geo = np.concatenate([[hp.fx, hp.fy, hp.cx, hp.cy, hp.bf, *b, *ginv], t["scale"]]).astype(np.float32)
-    return FrameInputs(gray, depth, (hp.fx, hp.fy, hp.cx, hp.cy, hp.bf), geo, t["inv_sigma2"],
+    cam, geo, inv_s2 = camera_inputs(hp)
+    return FrameInputs(gray, depth, cam, geo, inv_s2,
                        hp.match_probs[i % len(hp.match_probs)], hp.local_probs[i % len(hp.local_probs)],
                        hp.assoc_map, hp.assoc_boundary, min_size=hp.min_size, pose_cfg=hp.plane_cfg)

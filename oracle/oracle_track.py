@@ -17,6 +17,10 @@ reference's loops:
                        associations whose edge is an outlier)
   local_map_graph      TrackLocalMap, src/Tracking.cc:1062-1068 (SearchLocalPoints
                        assigns mvpMapPoints[bestIdx] = pMP, src/ORBmatcher.cc:115)
+  last_frame           Track()'s end of frame: VO-match clean-up and outlier drop
+                       (src/Tracking.cc:456-466, 484-488), mLastFrame = mCurrentFrame
+  mat4 / inverse_pose  the cv::Mat float products of the motion model
+                       (Tracking.cc:446-449, 958; Frame::UpdatePoseMatrices)
 
 Returned arrays use the dtypes of include/spslam_gpu.h (spslam_pose_problem,
 spslam_point_obs, spslam_plane_obs)."""
@@ -119,3 +123,56 @@ def local_map_graph(Tcw, proj_points, match, keep, local_points, local_match, ke
     pts = _points(xw, keys_un, uright, inv_level_sigma2)
     pls = _planes(np.asarray(coefs, np.float32).reshape(-1, 4), assoc, map_planes)
     return _problem(Tcw, cam, len(pts), len(pls)), pts, pls
+
+
+def mat4(A, B):
+    """cv::Mat float 4x4 product: each entry a double sum over k in order, rounded once to float."""
+    A = np.asarray(A, np.float32).reshape(4, 4)
+    B = np.asarray(B, np.float32).reshape(4, 4)
+    C = np.zeros((4, 4), np.float32)
+    for i in range(4):
+        for j in range(4):
+            s = 0.0
+            for k in range(4):
+                s += float(A[i, k]) * float(B[k, j])
+            C[i, j] = np.float32(s)
+    return C
+
+
+def inverse_pose(T):
+    """[Rcw^T | mOw] with mOw = -Rcw^T * tcw (float product, double sum): LastTwc of Tracking.cc:446-448."""
+    T = np.asarray(T, np.float32).reshape(4, 4)
+    W = np.eye(4, dtype=np.float32)
+    W[:3, :3] = T[:3, :3].T
+    for i in range(3):
+        s = 0.0
+        for k in range(3):
+            s += -float(T[k, i]) * float(T[k, 3])
+        W[i, 3] = np.float32(s)
+    return W
+
+
+def last_frame(proj_points, match, keep, local_points, local_match, keys_un, point_outlier_local):
+    """The next frame's last-frame points (spslam_proj_point records, keypoint order): each keypoint's map
+    point after TrackLocalMap (the local-map match, else the kept motion-model match) unless the local-map
+    PoseOptimization flagged it (Tracking.cc:484-488) or it has no observations (:456-466)."""
+    import oracle_match as OM
+    out, e = [], 0
+    for i in range(len(match)):
+        if local_match[i] >= 0:
+            src = local_points[local_match[i]]
+        elif keep[i]:
+            src = proj_points[match[i]]
+        else:
+            continue
+        out_flag = point_outlier_local[e]
+        e += 1
+        if out_flag or int(src["n_obs"]) < 1:
+            continue
+        out.append((src["xw"], keys_un[i]["angle"], keys_un[i]["octave"], src["n_obs"], i, src["id"], src["desc"]))
+    P = np.zeros(len(out), OM.PROJ_POINT_DTYPE)
+    for j, (xw, ang, octv, nobs, i, pid, d) in enumerate(out):
+        P[j]["xw"], P[j]["angle"], P[j]["octave"], P[j]["n_obs"] = xw, ang, octv, nobs
+        P[j]["last_index"], P[j]["id"], P[j]["desc"] = i, pid, d
+    assert e == len(point_outlier_local)
+    return P

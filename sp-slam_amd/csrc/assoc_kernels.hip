@@ -16,6 +16,8 @@
 // -O3 -march=native): fma(a2, b2, fma(a0, b0, a1*b1)) (+ a3).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "wave_priority.h"
 
 #include "assoc_launch.h"
@@ -173,6 +175,118 @@ __global__ __launch_bounds__(64) void assoc_decide_kernel(const spslam_assoc_fra
     if (new_plane && threadIdx.x == 0) new_plane[f] = any;
 }
 
+// Fused form (the default when the per-frame distance table fits in LDS): one workgroup per frame computes
+// every frame plane's world coefficients, streams each map plane's boundary cloud once for all the frame
+// planes that pass its angle test (float minima, exact in any order), and runs the decision walk from LDS.
+// One launch of n_frames workgroups instead of n_frames x max_map + n_frames: inside the pipelined step the
+// tracking chain's launches wait for CU slots behind the extraction kernels, so the grid size is the cost.
+__global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_assoc_frame* __restrict__ frames,
+                                                               AssocSources S, const spslam_map_plane* __restrict__ map,
+                                                               const float* __restrict__ boundary, int max_map,
+                                                               spslam_assoc_params Pm, int32_t* __restrict__ match,
+                                                               int32_t* __restrict__ parallel,
+                                                               int32_t* __restrict__ vertical,
+                                                               int* __restrict__ new_plane) {
+    tail_wave_priority();
+    extern __shared__ float dmin[];  // [cap_a + cap_b][max_map] as ordered ints (non-negative floats)
+    __shared__ float pm_s[kGroup][4];
+    __shared__ int idx_s[kGroup];
+    __shared__ int ng_s;
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63;
+    const spslam_assoc_frame& F = frames[f];
+    int na, nb;
+    plane_counts(S, f, &na, &nb);
+    const int n = na + nb, P = S.cap_a + S.cap_b, nm = F.n_map;
+    int* D = reinterpret_cast<int*>(dmin);
+    for (int q = t; q < n * max_map; q += kThreads) D[q] = __float_as_int(100.f);  // PointDistanceFromPlane: 100
+    __syncthreads();
+    for (int j = 0; j < nm; j++) {
+        const spslam_map_plane M = map[F.map_offset + j];
+        const float* pts = boundary + 3 * (size_t)M.boundary_offset;
+        for (int i0 = 0; i0 < n; i0 += kGroup) {
+            if (t == 0) {  // the planes of this group whose normal passes the angle test against map plane j
+                int g = 0;
+                for (int i = i0; i < min(i0 + kGroup, n); i++) {
+                    float pM[4];
+                    world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
+                    const float angle = dot3(pM, M.world);
+                    if (angle > Pm.angle_th || angle < -Pm.angle_th) {
+                        for (int k = 0; k < 4; k++) pm_s[g][k] = pM[k];
+                        idx_s[g++] = i;
+                    }
+                }
+                ng_s = g;
+            }
+            __syncthreads();
+            const int g = ng_s;
+            if (g > 0) {
+                float pmr[kGroup][4], mn[kGroup];
+#pragma unroll
+                for (int q = 0; q < kGroup; q++) {
+#pragma unroll
+                    for (int k = 0; k < 4; k++) pmr[q][k] = pm_s[q < g ? q : 0][k];
+                    mn[q] = 100.f;
+                }
+                for (int p = t; p < M.n_boundary; p += kThreads) {
+                    const float qv[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
+#pragma unroll
+                    for (int q = 0; q < kGroup; q++)
+                        mn[q] = fminf(mn[q], fabsf(__fadd_rn(dot3(pmr[q], qv), pmr[q][3])));
+                }
+#pragma unroll
+                for (int q = 0; q < kGroup; q++) {
+                    float v = mn[q];
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+                    if (lane == 0 && q < g) atomicMin(&D[idx_s[q] * max_map + j], __float_as_int(v));
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the reference's walk over the map planes (Map.cc:207-257), one thread per frame plane
+    int unmatched = 0;
+    const spslam_map_plane* Mp = map + F.map_offset;
+    for (int i = t; i < n; i += kThreads) {
+        float pM[4];
+        world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
+        float ldTh = Pm.dis_th, lverTh = Pm.ver_th, lparTh = Pm.par_th;
+        const size_t o = (size_t)f * P + i;
+        int32_t m = -1, par = -1, ver = -1;
+        if (F.carry) {
+            m = match[o];
+            par = parallel[o];
+            ver = vertical[o];
+        }
+        for (int j = 0; j < nm; j++) {
+            const float angle = dot3(pM, Mp[j].world);
+            if (angle > Pm.angle_th || angle < -Pm.angle_th) {
+                const float dis = __int_as_float(D[i * max_map + j]);
+                if (dis < ldTh) {
+                    ldTh = dis;
+                    m = F.map_offset + j;
+                    continue;
+                }
+            }
+            if (angle < lverTh && angle > -lverTh) {
+                lverTh = fabsf(angle);
+                ver = F.map_offset + j;
+                continue;
+            }
+            if (angle > lparTh || angle < -lparTh) {
+                lparTh = fabsf(angle);
+                par = F.map_offset + j;
+            }
+        }
+        match[o] = m;
+        parallel[o] = par;
+        vertical[o] = ver;
+        unmatched |= m < 0;
+    }
+    const int any = __syncthreads_or(unmatched);
+    if (new_plane && t == 0) new_plane[f] = any;
+}
+
 }  // namespace assoc
 
 hipError_t assoc_launch(int n_frames, const spslam_assoc_frame* frames, const AssocSources& src,
@@ -181,6 +295,13 @@ hipError_t assoc_launch(int n_frames, const spslam_assoc_frame* frames, const As
                         int32_t* vertical, int* new_plane, hipStream_t s, KernelTimer* timer) {
     if (n_frames < 1 || max_map < 0 || src.cap_a < 0 || src.cap_b < 0) return hipErrorInvalidValue;
     if (timer) timer->begin(kKindAssoc, s);
+    const size_t lds = (size_t)(src.cap_a + src.cap_b) * max_map * sizeof(float);
+    if (lds <= 48 * 1024) {
+        hipLaunchKernelGGL(assoc::assoc_fused_kernel, dim3(n_frames), dim3(assoc::kThreads), std::max<size_t>(lds, 4),
+                           s, frames, src, map, boundary, max_map, P, match, parallel, vertical, new_plane);
+        if (timer) timer->end(kKindAssoc, s);
+        return hipGetLastError();
+    }
     if (max_map > 0)
         hipLaunchKernelGGL(assoc::assoc_dist_kernel, dim3(n_frames, max_map), dim3(assoc::kThreads), 0, s, frames,
                            src, map, boundary, max_map, P.angle_th, dist);

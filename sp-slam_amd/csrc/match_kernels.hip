@@ -337,6 +337,13 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     w.x1 = 0;
     LocalWindow* W = win + (size_t)f * max_points + i;
     const spslam_local_point& p = points[F.point_offset + i];
+    // points the frame already tracks (mnLastFrameSeen == the frame) are skipped before isInFrustum
+    // (Tracking.cc:1396-1401); their mbTrackInView stays false
+    if (P.seen && P.seen[F.seen_offset + p.id] == F.stamp) {
+        if (in_view) in_view[F.point_offset + i] = 0;
+        *W = w;
+        return;
+    }
     bool in = false;
     // Frame::isInFrustum(pMP, 0.5)
     const float tcw[3] = {F.Tcw[3], F.Tcw[7], F.Tcw[11]};

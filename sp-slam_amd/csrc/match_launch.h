@@ -43,6 +43,7 @@ struct LocalWindow {
 struct LocalConsts {
     float th, nn_ratio, view_cos_limit, log_scale_factor;
     int n_levels;
+    const int32_t* seen;  // per-frame seen stamps (spslam_local_frame.seen_offset / stamp), may be NULL
 };
 
 hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, const spslam_local_point* points,

@@ -16,6 +16,8 @@
 // result matches the reference to rounding, not bitwise.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "wave_priority.h"
 
 #include "../../include/spslam_gpu.h"
@@ -187,7 +189,11 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
 
 using namespace pose;
 
-__global__ __launch_bounds__(kThreads) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+// kMinWaves: waves per SIMD the register allocation must leave room for (launch-bounds occupancy).  At 1 the
+// kernel takes 256 VGPRs + AGPRs, so a workgroup only starts on a CU whose four SIMDs are nearly empty --
+// inside the pipelined step that waits for the extraction kernels' waves to drain.
+template <int kMinWaves>
+__global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
                                                    const spslam_point_obs* __restrict__ pts_all,
                                                    const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
                                                    const spslam_pose_result* __restrict__ init_from,
@@ -524,7 +530,16 @@ PoseConsts make_pose_consts(const spslam_plane_config& c) {
 hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_point_obs* pts,
                        const spslam_plane_obs* pls, const PoseConsts& K, const spslam_pose_result* init_from,
                        spslam_pose_result* res, uint8_t* pout, uint8_t* plout, hipStream_t s) {
-    hipLaunchKernelGGL(pose_kernel, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+    static const int occ = [] {
+        const char* e = std::getenv("SPSLAM_POSE_OCCUPANCY");  // measurement knob: 1, 2 or 4
+        return e ? std::atoi(e) : 1;
+    }();
+    if (occ >= 4)
+        hipLaunchKernelGGL(pose_kernel<4>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+    else if (occ >= 2)
+        hipLaunchKernelGGL(pose_kernel<2>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+    else
+        hipLaunchKernelGGL(pose_kernel<1>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
     return hipGetLastError();
 }
 

@@ -1286,13 +1286,18 @@ int spslam_grab_rgbd(spslam_ctx* c, const uint8_t* color, int color_stride, cons
 int spslam_track_graph_batch_device(spslam_ctx* c, int n_frames, int stage, const spslam_track_batch* batch,
                                     void* hip_stream) {
     if (!c) return SPSLAM_ERR_ARG;
-    if (n_frames < 1 || !batch || stage < SPSLAM_TRACK_MOTION_MODEL || stage > SPSLAM_TRACK_LOCAL_MAP)
+    if (n_frames < 1 || !batch || stage < SPSLAM_TRACK_MOTION_MODEL || stage > SPSLAM_TRACK_LAST_FRAME)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_track_graph_batch_device");
     const spslam_track_batch& b = *batch;
     const bool common = b.kp_counts && b.cap >= 1 && b.cap <= (1 << 20) && b.proj_frames && b.proj_match &&
                         b.proj_points && b.edge_of_kp;
     bool ok = common;
-    if (stage == SPSLAM_TRACK_DISCARD) {
+    if (stage == SPSLAM_TRACK_MOTION_PRIOR) {
+        ok = b.proj_frames && b.velocity;
+    } else if (stage == SPSLAM_TRACK_LAST_FRAME) {
+        ok = common && b.keys_un && b.local_frames && b.local_points && b.local_match && b.results &&
+             b.point_outlier && b.point_outlier_local && b.next_frames && b.next_points && b.velocity;
+    } else if (stage == SPSLAM_TRACK_DISCARD) {
         ok = ok && b.taken && b.local_frames && b.results && b.point_outlier;
         if (b.next_match)  // the plane-outlier discard needs the first association and its edge flags
             ok = ok && b.next_parallel && b.next_vertical && b.plane_outlier && b.assoc_match && b.assoc_parallel &&
@@ -1306,7 +1311,7 @@ int spslam_track_graph_batch_device(spslam_ctx* c, int n_frames, int stage, cons
         if (stage == SPSLAM_TRACK_LOCAL_MAP)
             ok = ok && b.local_frames && b.local_points && b.local_match && b.results && b.point_outlier;
     }
-    static const char* names[3] = {"MOTION_MODEL", "DISCARD", "LOCAL_MAP"};
+    static const char* names[5] = {"MOTION_MODEL", "DISCARD", "LOCAL_MAP", "MOTION_PRIOR", "LAST_FRAME"};
     if (!ok) return fail(c, SPSLAM_ERR_ARG, "missing buffer for stage %s of spslam_track_graph_batch_device",
                          names[stage]);
     HIP_CHECK(c, hipSetDevice(c->device));
@@ -1326,7 +1331,7 @@ int spslam_search_local_points_batch_device(spslam_ctx* c, int n_frames, const s
                                             const int32_t* d_grid_idx, const int* d_counts, int cap,
                                             const uint8_t* d_taken, const spslam_local_params* params,
                                             int32_t* d_match, int* d_nmatches, uint8_t* d_in_view,
-                                            void* hip_stream) {
+                                            const int32_t* d_seen, void* hip_stream) {
     if (!c) return SPSLAM_ERR_ARG;
     if (!c->frame_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_frame_configure not called%s", "");
     if (n_frames < 1 || !d_frames || max_points < 0 || (max_points > 0 && !d_points) || !d_keys_un || !d_desc ||
@@ -1351,7 +1356,7 @@ int spslam_search_local_points_batch_device(spslam_ctx* c, int n_frames, const s
     for (int l = 0; l < 8; l++) g.scale[l] = l < c->p.nlevels ? c->scale[l] : 0.f;
     LocalConsts P{params->th, params->nn_ratio, params->view_cos_limit,
                   std::log(c->p.scale_factor),  // Frame::mfLogScaleFactor = log(mfScaleFactor), float
-                  c->p.nlevels};
+                  c->p.nlevels, d_seen};
     MatchCurrent cur{d_keys_un, d_desc, d_uright, d_grid_off, d_grid_idx, d_counts, cap};
     HIP_CHECK(c, local_match_launch(n_frames, d_frames, d_points, max_points, cur, g, P, d_taken,
                                     (LocalWindow*)c->d_match_scratch, d_match, d_nmatches, d_in_view, s, c->timer));
@@ -1389,7 +1394,7 @@ int spslam_search_local_points(spslam_ctx* c, const spslam_local_frame* frame, c
         c, 1, (const spslam_local_frame*)(q + o[0]), (const spslam_local_point*)(q + o[1]), np,
         (const spslam_keypoint*)(q + o[2]), q + o[3], (const float*)(q + o[4]), (const int32_t*)(q + o[5]),
         (const int32_t*)(q + o[6]), (const int*)(q + o[7]), cap, taken ? q + o[8] : nullptr, params,
-        (int32_t*)(q + o[9]), (int*)(q + o[10]), q + o[11], c->stream);
+        (int32_t*)(q + o[9]), (int*)(q + o[10]), q + o[11], nullptr, c->stream);
     if (rc) { (void)hipFreeAsync(q, c->stream); return rc; }
     if (n_kp) HIP_CHECK(c, hipMemcpyAsync(match, q + o[9], (size_t)n_kp * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(c, hipMemcpyAsync(nmatches, q + o[10], sizeof(int), hipMemcpyDeviceToHost, c->stream));

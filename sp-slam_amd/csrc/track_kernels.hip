@@ -28,6 +28,52 @@ __device__ __forceinline__ const float* plane_coef(const spslam_track_batch& B, 
     return (const float*)((const uint8_t*)B.planes_b + ((size_t)f * B.cap_b + (j - na)) * B.stride_b);
 }
 
+// cv::Mat float product C = A * B of 4x4 row-major matrices (double accumulation, rounded once)
+__device__ __forceinline__ void mat4_mul(const float* A, const float* Bm, float* C) {
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) s = __dadd_rn(s, __dmul_rn((double)A[4 * i + k], (double)Bm[4 * k + j]));
+            C[4 * i + j] = (float)s;
+        }
+}
+
+// Frame::GetRotationInverse / GetCameraCenter as a 4x4 (Tracking.cc:446-448): [Rcw^T | -Rcw^T tcw]
+__device__ __forceinline__ void inverse_pose(const float* T, float* W) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) W[4 * i + j] = T[4 * j + i];
+        double s = 0.0;  // mOw = -mRcw.t() * mtcw (Frame::UpdatePoseMatrices)
+#pragma unroll
+        for (int k = 0; k < 3; k++) s = __dadd_rn(s, __dmul_rn(-(double)T[4 * k + i], (double)T[4 * k + 3]));
+        W[4 * i + 3] = (float)s;
+    }
+    W[12] = W[13] = W[14] = 0.f;
+    W[15] = 1.f;
+}
+
+// a keypoint's map point after TrackLocalMap: the local-map match, else the motion-model match that survived
+// the discard.  Returns the index into the local (l >= 0) or last-frame (l < 0, m) point arrays, or false.
+__device__ __forceinline__ bool map_point_of(const spslam_track_batch& B, size_t ko, int i, int lpo, int* l,
+                                             int* m) {
+    const int lm = B.local_match[ko + i];
+    if (lm >= 0) {
+        *l = lpo + lm;
+        return true;
+    }
+    const int e = B.edge_of_kp[ko + i];
+    if (e >= 0 && !B.point_outlier[ko + e]) {
+        *l = -1;
+        *m = B.proj_match[ko + i];
+        return true;
+    }
+    return false;
+}
+
 __global__ __launch_bounds__(kThreads) void track_graph_kernel(TrackArgs A, int stage) {
     tail_wave_priority();
     const spslam_track_batch& B = A.b;
@@ -37,14 +83,106 @@ __global__ __launch_bounds__(kThreads) void track_graph_kernel(TrackArgs A, int 
     const size_t ko = (size_t)f * B.cap;
     const spslam_proj_frame& PF = B.proj_frames[f];
 
+    if (stage == SPSLAM_TRACK_MOTION_PRIOR) {
+        // TrackWithMotionModel: mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw) (Tracking.cc:958)
+        if (t == 0) {
+            float Tl[16], V[16], P[16];
+            for (int q = 0; q < 16; q++) { Tl[q] = PF.Tlw[q]; V[q] = B.velocity[16 * f + q]; }
+            mat4_mul(V, Tl, P);
+            for (int q = 0; q < 16; q++) {
+                const_cast<spslam_proj_frame*>(B.proj_frames)[f].Tcw[q] = P[q];  // the stage writes the prediction
+                if (B.assoc_frames_first) B.assoc_frames_first[f].Tcw[q] = P[q];
+            }
+        }
+        return;
+    }
+
+    if (stage == SPSLAM_TRACK_LAST_FRAME) {
+        // Track(): mVelocity = mCurrentFrame.mTcw * LastTwc (:443-450), VO-match clean-up (:456-466) and
+        // outlier drop (:484-488); mLastFrame = Frame(mCurrentFrame) (:505)
+        const int lpo = B.local_frames[f].point_offset;
+        int base = 0, nb = 0;  // local-map graph edge index / surviving points so far
+        for (int i0 = 0; i0 < n; i0 += kThreads) {
+            const int i = i0 + t;
+            int l = -1, m = -1;
+            const bool has = i < n && map_point_of(B, ko, i, lpo, &l, &m);
+            const unsigned long long mh = __ballot(has);
+            if (lane == 0) wsum[wave] = __popcll(mh);
+            __syncthreads();
+            int before = 0, total = 0;
+#pragma unroll
+            for (int w = 0; w < kThreads / 64; w++) {
+                before += w < wave ? wsum[w] : 0;
+                total += wsum[w];
+            }
+            __syncthreads();
+            const int e2 = base + before + __popcll(mh & ((1ull << lane) - 1ull));
+            int n_obs = 0;
+            if (has) n_obs = l >= 0 ? B.local_points[l].n_obs : B.proj_points[PF.point_offset + m].n_obs;
+            const bool keep = has && !B.point_outlier_local[ko + e2] && n_obs >= 1;
+            const unsigned long long mk = __ballot(keep);
+            if (lane == 0) wsum[wave] = __popcll(mk);
+            __syncthreads();
+            int kb = 0, kt = 0;
+#pragma unroll
+            for (int w = 0; w < kThreads / 64; w++) {
+                kb += w < wave ? wsum[w] : 0;
+                kt += wsum[w];
+            }
+            if (keep) {
+                const int j = nb + kb + __popcll(mk & ((1ull << lane) - 1ull));
+                spslam_proj_point o;
+                const spslam_keypoint& k = B.keys_un[ko + i];
+                const float* xw;
+                const uint8_t* d;
+                if (l >= 0) {
+                    const spslam_local_point& L = B.local_points[l];
+                    xw = L.xw; d = L.desc; o.id = L.id;
+                } else {
+                    const spslam_proj_point& Pp = B.proj_points[PF.point_offset + m];
+                    xw = Pp.xw; d = Pp.desc; o.id = Pp.id;
+                }
+                o.xw[0] = xw[0]; o.xw[1] = xw[1]; o.xw[2] = xw[2];
+                o.angle = k.angle;
+                o.octave = k.octave;
+                o.n_obs = n_obs;
+                o.last_index = i;
+                for (int q = 0; q < 32; q++) o.desc[q] = d[q];
+                B.next_points[ko + j] = o;
+            }
+            base += total;
+            nb += kt;
+            __syncthreads();  // wsum reuse
+        }
+        if (t == 0) {
+            const float* Tc = B.results[f].Tcw;
+            float W[16], V[16];
+            inverse_pose(PF.Tlw, W);
+            mat4_mul(Tc, W, V);
+            spslam_proj_frame& N = B.next_frames[f];
+            for (int q = 0; q < 16; q++) {
+                B.velocity[16 * f + q] = V[q];
+                N.Tlw[q] = Tc[q];
+                N.Tcw[q] = Tc[q];  // replaced by MOTION_PRIOR
+            }
+            N.point_offset = (int32_t)ko;
+            N.n_points = nb;
+            N.pad[0] = N.pad[1] = 0;
+        }
+        return;
+    }
+
     if (stage == SPSLAM_TRACK_DISCARD) {
         // src/Tracking.cc:986-1000, then ORBmatcher.cc:95-97's "already has a map point with observations"
+        const spslam_local_frame& LF = B.local_frames[f];
         for (int i = t; i < n; i += kThreads) {
             const int e = B.edge_of_kp[ko + i];
             bool tk = false;
             if (e >= 0 && !B.point_outlier[ko + e])
                 tk = B.proj_points[PF.point_offset + B.proj_match[ko + i]].n_obs > 0;
             B.taken[ko + i] = (uint8_t)tk;
+            // every motion-model match, inlier or discarded, is mnLastFrameSeen = this frame (:997, :1380-1390)
+            if (B.seen && e >= 0) B.seen[LF.seen_offset + B.proj_points[PF.point_offset + B.proj_match[ko + i]].id] = LF.stamp;
         }
         if (t < 16) {
             const float v = B.results[f].Tcw[t];

@@ -54,6 +54,10 @@ CONFIGS = {
 }
 
 
+def _ptr(t):
+    return t.data_ptr() if t is not None else 0
+
+
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
@@ -77,17 +81,11 @@ class HotPath:
                                                min_size=min_size)
         self.fs = spslam_frame.FrameStage(self.ex, self.fx, self.fy, self.cx, self.cy, K.get("dist", (0,) * 5),
                                           K["bf"], width, height)
-        # --- unique synthetic frames: colour (R,G,B u8) + raw depth (u16, DepthMapFactor 5000), as
-        #     GrabImageRGBD receives them; the step converts them on the device (spslam_grab_rgbd)
-        U = min(unique_frames, B)
-        self.frames = []
-        for i in range(U):
-            fi = 3 * i
-            g, d, fid = self.scene.render(self.scene.pose(fi), width, height, K=K, noise_seed=seq_id * 1000 + fi)
-            self.frames.append((fi, synth.colorize(g, fid), d, fid))
+        # sequence state written by the tracking tail (sp-slam_amd/sequence.py); unused here
+        self.d_seen = self.d_afr_first = self.d_velocity = None
+        self._setup_inputs(seq_id, unique_frames)
+        U = len(self.frames)
         dev = "cuda"
-        self.d_rgb = torch.from_numpy(np.stack([self.frames[i % U][1] for i in range(B)])).to(dev)
-        self.d_depth_raw = torch.from_numpy(np.stack([self.frames[i % U][2] for i in range(B)]).view(np.int16)).to(dev)
         self.depth_factor = K["depth_factor"]
         self.grabber = spslam_grab.Grabber(self.ex, channels=3, rgb=True, depth_u16=True,
                                            depth_factor=K["depth_factor"])
@@ -155,6 +153,19 @@ class HotPath:
         if pipelined:
             self._setup_pipeline()
         torch.cuda.synchronize()  # buffers were filled on the default stream
+
+    def _setup_inputs(self, seq_id, unique_frames):
+        """Unique synthetic frames: colour (R,G,B u8) + raw depth (u16, DepthMapFactor 5000), as GrabImageRGBD
+        receives them; the step converts them on the device (spslam_grab_rgbd).  Slot i holds frame i % U."""
+        torch, B, U = self.torch, self.B, min(unique_frames, self.B)
+        self.frames = []
+        for i in range(U):
+            fi = 3 * i
+            g, d, fid = self.scene.render(self.scene.pose(fi), self.W, self.H, K=self.K,
+                                          noise_seed=seq_id * 1000 + fi)
+            self.frames.append((fi, synth.colorize(g, fid), d, fid))
+        self.d_rgb = torch.from_numpy(np.stack([self.frames[i % U][1] for i in range(B)])).cuda()
+        self.d_depth_raw = torch.from_numpy(np.stack([self.frames[i % U][2] for i in range(B)]).view(np.int16)).cuda()
 
     def _setup_assoc(self, seq_id):
         """Map::AssociatePlanesByBoundary before each PoseOptimization (TrackWithMotionModel,
@@ -260,7 +271,7 @@ class HotPath:
                                         self.d_kur.data_ptr(), self.d_grid_off.data_ptr(),
                                         self.d_grid_idx.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap,
                                         self.d_taken.data_ptr(), self.d_lmatch.data_ptr(), self.d_nlmatch.data_ptr(),
-                                        stream=self.stream)
+                                        stream=self.stream, d_seen=_ptr(self.d_seen))
 
     def associate(self, k):
         import spslam_planes as SP
@@ -309,6 +320,7 @@ class HotPath:
             assoc_vertical=a[2].data_ptr(), assoc_frames_next=self.d_afr2.data_ptr(),
             plane_outlier=self.graphs[0]["plout"].data_ptr(), next_match=self.d_assoc[1][0].data_ptr(),
             next_parallel=self.d_assoc[1][1].data_ptr(), next_vertical=self.d_assoc[1][2].data_ptr(),
+            assoc_frames_first=_ptr(self.d_afr_first), seen=_ptr(self.d_seen), velocity=_ptr(self.d_velocity),
             problems=g["P"].data_ptr(), points=g["pts"].data_ptr(), planes=g["pls"].data_ptr(),
             edge_of_kp=self.d_edge.data_ptr(), results=self.d_res1.data_ptr(),
             point_outlier=self.graphs[0]["pout"].data_ptr(), fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy,

@@ -1,0 +1,251 @@
+"""Tracked RGB-D sequences on the GPU: the batched hot path run frame after frame,
+each batch slot carrying its own tracking state (Tracking::Track, src/Tracking.cc:
+276-526).
+
+Batch k holds frame t = k + 1 of every slot's sequence.  Per batch the tracking tail
+(one HIP stream, nothing returns to the host) is
+
+  SPSLAM_TRACK_MOTION_PRIOR  mCurrentFrame.SetPose(mVelocity * mLastFrame.mTcw)  (:958)
+  frame steps, SearchByProjection against the last frame's map points, association,
+  PoseOptimization, outlier discard (+ mnLastFrameSeen stamps), SearchLocalPoints over
+  the local map (seen points skipped on the device), association, PoseOptimization
+                                                       (pipeline.HotPath, :950-1136)
+  SPSLAM_TRACK_LAST_FRAME    mVelocity, VO-match clean-up, outlier drop,
+                             mLastFrame = mCurrentFrame  (:443-505)
+
+so frame t's prior, last-frame map points and matches all come from frame t-1's
+tracked result.  The map is the harness's stand-in for LocalMapping: keyframes on a
+fixed schedule (every synth.KEYFRAME_STEP frames) whose map points are their own
+keypoints back-projected at the true pose (synth.keyframe_points); frame t's local map
+is the points of the two latest keyframes before it; map planes are the scene faces.
+Deviations from the reference, all shared with the CPU oracle
+(oracle/oracle_sequence.py): keyframes are not chosen by NeedNewKeyFrame and do not
+add the current frame's VO points; LocalBundleAdjustment does not move them;
+mLastFrame's pose is not re-derived through its reference keyframe (UpdateLastFrame,
+an identity up to float rounding with fixed keyframes); frame 0 is initialised at its
+true pose with keyframe 0's points (StereoInitialization) and frame 1 uses a
+constant-position prior instead of TrackReferenceKeyFrame (BoW).
+
+Sequence u of a rank is the scene's trajectory from frame `SEQ_STRIDE * u`; slot i
+tracks sequence i % U (slots sharing a sequence carry identical, independent state).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+import pipeline
+import spslam_gpu as G
+import spslam_match as SM
+import synth
+
+SEQ_STRIDE = 53
+
+
+def _render_job(args):
+    scene_seq, n_boxes, first, n, w, h, K, noise_base = args
+    sc = synth.Scene(scene_seq, n_boxes=n_boxes)
+    out = []
+    for t in range(first, first + n):
+        g, d, fid = sc.render(sc.pose(t), w, h, K=K, noise_seed=noise_base + t)
+        out.append((synth.colorize(g, fid), d))
+    return out
+
+
+def render_sequences(seq_id, n_boxes, U, T, w, h, K, workers=0):
+    """frames[u][t] = (rgb, depth u16) of sequence u (scene seq_id, trajectory from SEQ_STRIDE * u)."""
+    jobs = [(seq_id, n_boxes, SEQ_STRIDE * u, T, w, h, K, seq_id * 100003) for u in range(U)]
+    if workers and workers > 1:
+        import concurrent.futures as cf
+        import multiprocessing as mp
+        chunks = []
+        for seq, nb, first, n, ww, hh, KK, nz in jobs:  # split sequences into chunks of frames
+            step = max(1, -(-n // max(1, workers // len(jobs))))
+            chunks += [(seq, nb, f0, min(step, first + n - f0), ww, hh, KK, nz) for f0 in range(first, first + n, step)]
+        with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as pool:
+            parts = list(pool.map(_render_job, chunks))
+        out, k = [], 0
+        for seq, nb, first, n, *_ in jobs:
+            frames = []
+            while len(frames) < n:
+                frames += parts[k]
+                k += 1
+            out.append(frames)
+        return out
+    return [_render_job(j) for j in jobs]
+
+
+class SequencePath(pipeline.HotPath):
+    """HotPath over T frames of U sequences (B slots, slot i -> sequence i % U)."""
+
+    def __init__(self, B, n_frames, n_sequences=None, render_workers=0, **kw):
+        self.T = n_frames
+        self.U = min(n_sequences or B, B)
+        self.render_workers = render_workers
+        self.n_boxes = kw.get("n_boxes", 3)
+        kw.pop("unique_frames", None)
+        kw.pop("rotate_inputs", None)
+        super().__init__(B, unique_frames=self.U, **kw)
+
+    # ---- inputs: every frame of every sequence resident in HBM, loaded per batch
+    def _setup_inputs(self, seq_id, unique_frames):
+        torch, B, U, T = self.torch, self.B, self.U, self.T
+        self.seq_id = seq_id
+        self.seq_frames = render_sequences(seq_id, self.n_boxes, U, T, self.W, self.H, self.K, self.render_workers)
+        rgb = np.stack([self.seq_frames[u][t][0] for t in range(T) for u in range(U)])
+        dep = np.stack([self.seq_frames[u][t][1] for t in range(T) for u in range(U)]).view(np.int16)
+        self.d_rgb_all = torch.from_numpy(rgb).cuda()         # [T * U] frames, frame t of sequence u at t*U + u
+        self.d_depth_all = torch.from_numpy(dep).cuda()
+        self.frames = [(SEQ_STRIDE * u, self.seq_frames[u][0][0], self.seq_frames[u][0][1], None) for u in range(U)]
+        self.d_rgb = self.d_rgb_all[[U + i % U for i in range(B)]].clone()   # frame 1 (batch 0)
+        self.d_depth_raw = self.d_depth_all[[U + i % U for i in range(B)]].clone()
+
+    def _true_pose(self, u, t):
+        return np.linalg.inv(self.scene.pose(SEQ_STRIDE * u + t))
+
+    # ---- the map: keyframe points, the initial last frame, the per-batch local maps
+    def _setup_match(self, seq_id):
+        torch, B, U, T, cap = self.torch, self.B, self.U, self.T, self.kp_cap
+        kf_t = list(range(0, T, synth.KEYFRAME_STEP))
+        self.kf_t = kf_t
+        # ORB of every keyframe frame, on the device (bit-exact with the oracle)
+        idx = [t * U + u for u in range(U) for t in kf_t]
+        n = len(idx)
+        d_g = torch.zeros((n, self.H, self.W), dtype=torch.uint8, device="cuda")
+        d_d = torch.zeros((n, self.H, self.W), dtype=torch.float32, device="cuda")
+        rgb, dep = self.d_rgb_all[idx].contiguous(), self.d_depth_all[idx].contiguous()
+        self.grabber.batch_device(n, rgb.data_ptr(), self.H * self.W * 3, self.W * 3, dep.data_ptr(), self.H * self.W,
+                                  self.W, self.W, self.H, d_g.data_ptr(), d_d.data_ptr(), self.stream)
+        d_k = torch.zeros((n, cap, 7), dtype=torch.float32, device="cuda")
+        d_ds = torch.zeros((n, cap, 32), dtype=torch.uint8, device="cuda")
+        d_n = torch.zeros(n, dtype=torch.int32, device="cuda")
+        for c0 in range(0, n, B):  # the context's batch capacity
+            m = min(B, n - c0)
+            self.ex.extract_batch_device(d_g[c0].data_ptr(), m, self.W * self.H, self.W, d_k[c0].data_ptr(),
+                                         d_ds[c0].data_ptr(), d_n[c0].data_ptr(), cap, self.stream)
+        torch.cuda.synchronize()
+        kps = d_k.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n, cap)
+        desc, cnt = d_ds.cpu().numpy(), d_n.cpu().numpy()
+        self.n_ids = len(kf_t) * cap                   # map point ids per sequence: keyframe index * cap + keypoint
+        self.kf_points, self.kf_kps = {}, {}
+        offs, pts = {}, []
+        o = 0
+        for u in range(U):
+            for j, t in enumerate(kf_t):
+                q = u * len(kf_t) + j
+                sc_t = SEQ_STRIDE * u + t
+                P = synth.keyframe_points(self.scene, sc_t, kps[q, :cnt[q]], desc[q, :cnt[q]],
+                                          self.seq_frames[u][t][1], j * cap, K=self.Ks)
+                self.kf_points[u, j], self.kf_kps[u, j] = P, kps[q, :cnt[q]].copy()
+                offs[u, j] = o
+                pts.append(P)
+                o += len(P)
+        self.d_lpoints = torch.from_numpy(np.concatenate(pts).view(np.uint8).copy()).cuda()
+        # frame t's local map: the two latest keyframes before it (contiguous in the point array)
+        lfr = np.zeros((T, B), SM.LOCAL_FRAME_DTYPE)
+        for t in range(1, T):
+            j = (t - 1) // synth.KEYFRAME_STEP
+            for i in range(B):
+                u = i % U
+                a = max(j - 1, 0)
+                lfr[t, i]["point_offset"] = offs[u, a]
+                lfr[t, i]["n_points"] = sum(len(self.kf_points[u, q]) for q in range(a, j + 1))
+                lfr[t, i]["seen_offset"] = i * self.n_ids
+                lfr[t, i]["stamp"] = t
+        self.local_table = lfr
+        self.max_local_points = int(lfr["n_points"].max())
+        self.local_offsets = offs
+        self.d_local_table = torch.from_numpy(lfr.view(np.uint8).reshape(T, -1).copy()).cuda()
+        self.d_lframes = self.d_local_table[1].clone()
+        self.d_seen = torch.full((B * self.n_ids,), -1, dtype=torch.int32, device="cuda")
+        # frame 0 (StereoInitialization): true pose, keyframe 0's points are its map points
+        pf = np.zeros(B, SM.PROJ_FRAME_DTYPE)
+        pp = np.zeros(B * cap, SM.PROJ_POINT_DTYPE)
+        for i in range(B):
+            u = i % U
+            P0 = synth.as_last_frame_points(self.kf_points[u, 0], self.kf_kps[u, 0], 0)
+            pp[i * cap:i * cap + len(P0)] = P0
+            T0 = self._true_pose(u, 0).astype(np.float32).reshape(16)
+            pf[i]["Tcw"], pf[i]["Tlw"], pf[i]["point_offset"], pf[i]["n_points"] = T0, T0, i * cap, len(P0)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
+        self.proj_sets = [(dev(pf), dev(pp)), (dev(pf), dev(pp))]
+        self.d_pframes, self.d_ppoints = self.proj_sets[0]
+        self.max_points = cap
+        self.d_velocity = torch.from_numpy(np.tile(np.eye(4, dtype=np.float32).reshape(16), B)).cuda()
+        self.match_probs = [(pf[i], None) for i in range(U)]   # _setup_assoc reads the initial pose
+        self.mean_proj_points = float(np.mean([int(pf[i]["n_points"]) for i in range(B)]))
+        self.mean_local_points = float(lfr["n_points"][1:].mean())
+        self.d_match = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+        self.d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
+        self.local_matcher = SM.LocalMatcher(self.ex)
+        self.matcher = SM.Matcher(self.ex)
+        self.d_taken = torch.zeros((B, cap), dtype=torch.uint8, device="cuda")
+        self.d_lmatch = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
+        self.d_nlmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
+        self.local_probs = []
+        self.traj = torch.zeros((T, B, 16), dtype=torch.float32, device="cuda")
+        self.n_tracked = 0
+
+    def _setup_assoc(self, seq_id):
+        super()._setup_assoc(seq_id)
+        self.d_afr_first = self.d_afr1  # MOTION_PRIOR writes the first association's pose
+
+    # ---- per batch: frame t of every slot's sequence and its local map
+    INPUT_BUFFERS = ("d_rgb", "d_depth_raw", "d_lframes")
+
+    def _load(self, stream):
+        k = self.n_loaded
+        self.n_loaded += 1
+        t = k + 1
+        if t >= self.T:
+            raise RuntimeError(f"sequence exhausted: {self.T} frames rendered")
+        torch = self.torch
+        with torch.cuda.stream(stream):
+            idx = torch.tensor([t * self.U + i % self.U for i in range(self.B)], dtype=torch.long, device="cuda")
+            idx.record_stream(stream)
+            self.d_rgb.copy_(self.d_rgb_all.index_select(0, idx))
+            self.d_depth_raw.copy_(self.d_depth_all.index_select(0, idx))
+            self.d_lframes.copy_(self.d_local_table[t])
+
+    def _setup_pipeline(self):
+        self.rotate_inputs = True  # per-batch inputs are double-buffered with the extraction outputs
+        super()._setup_pipeline()
+
+    # ---- the tail with the sequence state
+    def _tail(self):
+        import spslam_track as ST
+        self.track.batch_device(self.B, ST.MOTION_PRIOR, self._track_batch(0), stream=self.stream)
+        super()._tail()
+        nxt = self.proj_sets[1] if self.d_pframes.data_ptr() == self.proj_sets[0][0].data_ptr() else self.proj_sets[0]
+        b = self._track_batch(1)
+        b.results = self.d_res2.data_ptr()
+        b.point_outlier_local = self.graphs[1]["pout"].data_ptr()
+        b.next_frames, b.next_points = nxt[0].data_ptr(), nxt[1].data_ptr()
+        self.track.batch_device(self.B, ST.LAST_FRAME, b, stream=self.stream)
+        with self.torch.cuda.stream(self.main):
+            res = self.d_res2.view(self.B, G.POSE_RESULT_DTYPE.itemsize)[:, :64].contiguous()
+            self.traj[self.n_tracked + 1].copy_(res.view(self.torch.float32).view(self.B, 16))
+        self.n_tracked += 1
+        self.d_pframes, self.d_ppoints = nxt
+
+    def trajectory(self):
+        """Local-map pose (float 4x4) of frames 1 .. n_tracked of every slot: [t][slot] 4x4 (frame 0 = truth)."""
+        self.torch.cuda.synchronize()
+        tr = self.traj[:self.n_tracked + 1].cpu().numpy().reshape(-1, self.B, 4, 4)
+        for i in range(self.B):
+            tr[0, i] = self._true_pose(i % self.U, 0).astype(np.float32)
+        return tr
+
+    def oracle_inputs(self, slot):
+        """Host copies of what slot `slot` tracks, for the CPU oracle (oracle/oracle_sequence.track): frames
+        1 .. T-1, the frame-0 pose and last-frame points, and frame t's whole local map."""
+        u = slot % self.U
+        P0 = synth.as_last_frame_points(self.kf_points[u, 0], self.kf_kps[u, 0], 0)
+        T0 = self._true_pose(u, 0).astype(np.float32)
+        allp = np.concatenate([self.kf_points[u, j] for j in range(len(self.kf_t))])
+        base = self.local_offsets[u, 0]
+
+        def local_of(t):
+            r = self.local_table[t, slot]
+            o = int(r["point_offset"]) - base
+            return allp[o:o + int(r["n_points"])]
+        return self.seq_frames[u][1:], T0, P0, local_of

@@ -10,7 +10,7 @@ import numpy as np
 import spslam_gpu
 
 PROJ_POINT_DTYPE = np.dtype([("xw", "<f4", 3), ("angle", "<f4"), ("octave", "<i4"), ("n_obs", "<i4"),
-                             ("last_index", "<i4"), ("pad", "<i4"), ("desc", "u1", 32)])
+                             ("last_index", "<i4"), ("id", "<i4"), ("desc", "u1", 32)])
 assert PROJ_POINT_DTYPE.itemsize == 64
 PROJ_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("Tlw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"),
                              ("pad", "<i4", 2)])
@@ -68,9 +68,10 @@ class Matcher:
 
 
 LOCAL_POINT_DTYPE = np.dtype([("xw", "<f4", 3), ("normal", "<f4", 3), ("min_dist", "<f4"), ("max_dist", "<f4"),
-                              ("id", "<i4"), ("pad", "<i4", 3), ("desc", "u1", 32)])
+                              ("id", "<i4"), ("n_obs", "<i4"), ("pad", "<i4", 2), ("desc", "u1", 32)])
 assert LOCAL_POINT_DTYPE.itemsize == 80
-LOCAL_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"), ("pad", "<i4", 2)])
+LOCAL_FRAME_DTYPE = np.dtype([("Tcw", "<f4", 16), ("point_offset", "<i4"), ("n_points", "<i4"), ("seen_offset", "<i4"),
+                              ("stamp", "<i4")])
 assert LOCAL_FRAME_DTYPE.itemsize == 80
 
 
@@ -93,7 +94,7 @@ class LocalMatcher:
         vp, ci = ctypes.c_void_p, ctypes.c_int
         ex.lib.spslam_search_local_points.argtypes = [vp, vp, vp, vp, vp, vp, ci, vp, vp, vp, vp, vp, vp, vp]
         ex.lib.spslam_search_local_points_batch_device.argtypes = [vp, ci, vp, vp, ci, vp, vp, vp, vp, vp, vp, ci,
-                                                                   vp, vp, vp, vp, vp, vp]
+                                                                   vp, vp, vp, vp, vp, vp, vp]
         self.params = LocalParams(*params)
 
     def __call__(self, frame, points, keys_un, desc, uright, grid_off, grid_idx, taken=None):
@@ -116,8 +117,8 @@ class LocalMatcher:
         return match[:n], nm.value, inv[:len(pts)].astype(bool)
 
     def batch_device(self, n_frames, d_frames, d_points, max_points, d_keys_un, d_desc, d_uright, d_grid_off,
-                     d_grid_idx, d_counts, cap, d_taken, d_match, d_nmatches, d_in_view=0, stream=0):
+                     d_grid_idx, d_counts, cap, d_taken, d_match, d_nmatches, d_in_view=0, stream=0, d_seen=0):
         self.ex._check(self.ex.lib.spslam_search_local_points_batch_device(
             self.ex.ctx, n_frames, d_frames, d_points, max_points, d_keys_un, d_desc, d_uright, d_grid_off,
             d_grid_idx, d_counts, cap, d_taken or None, ctypes.byref(self.params), d_match, d_nmatches,
-            d_in_view or None, stream or None))
+            d_in_view or None, d_seen or None, stream or None))

@@ -8,7 +8,7 @@ import ctypes
 
 import spslam_gpu
 
-MOTION_MODEL, DISCARD, LOCAL_MAP = 0, 1, 2
+MOTION_MODEL, DISCARD, LOCAL_MAP, MOTION_PRIOR, LAST_FRAME = 0, 1, 2, 3, 4
 
 spslam_gpu.EXPORTED += ["spslam_track_graph_batch_device"]
 
@@ -25,7 +25,8 @@ class TrackBatch(ctypes.Structure):
                 ("cap_b", ctypes.c_int32),
                 ("map", _P), ("assoc_match", _P), ("assoc_parallel", _P), ("assoc_vertical", _P),
                 ("assoc_frames_next", _P), ("plane_outlier", _P), ("next_match", _P), ("next_parallel", _P),
-                ("next_vertical", _P),
+                ("next_vertical", _P), ("assoc_frames_first", _P), ("seen", _P), ("next_frames", _P),
+                ("next_points", _P), ("velocity", _P), ("point_outlier_local", _P),
                 ("problems", _P), ("points", _P), ("planes", _P), ("edge_of_kp", _P), ("results", _P),
                 ("point_outlier", _P),
                 ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),

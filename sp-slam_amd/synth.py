@@ -535,3 +535,59 @@ def colorize(gray: np.ndarray, fid: np.ndarray) -> np.ndarray:
     with imread and GrabImageRGBD converts them, src/Tracking.cc:214-224)."""
     tint = np.where((fid >= 0)[..., None], _TINTS[np.maximum(fid, 0) % len(_TINTS)], 1.0).astype(np.float32)
     return np.clip(np.rint(gray[..., None].astype(np.float32) * tint), 0, 255).astype(np.uint8)
+
+
+# ---------------------------------------------------------------- tracked sequences
+KEYFRAME_STEP = 10  # fixed keyframe schedule of the sequence harness (sp-slam_amd/sequence.py)
+
+
+def keyframe_points(scene: Scene, kf_fi: int, kf_kps, kf_desc, kf_depth_u16, id_base: int, K=TUM3, scale=1.2,
+                    n_levels=8, th_depth=None):
+    """The map points a keyframe contributes (StereoInitialization / CreateNewKeyFrame, src/Tracking.cc:544-560,
+    1315-1345: one MapPoint per keypoint with depth, at the keyframe's pose -- here the true pose), with
+    MapPoint::UpdateNormalAndDepth's normal and distance range (src/MapPoint.cc:357-400), the keyframe's
+    descriptor (one observation: ComputeDistinctiveDescriptors keeps it), Observations() = 1 + id % 3 and ids
+    id_base + keypoint index.  Returns spslam_local_point records."""
+    import spslam_match as M
+    fx, fy, cx, cy = K["fx"], K["fy"], K["cx"], K["cy"]
+    Twk = scene.pose(kf_fi)
+    sf = np.float32(scale) ** np.arange(n_levels, dtype=np.float32)
+    rows = []
+    for i, kp in enumerate(kf_kps):
+        x, y = int(kp["x"]), int(kp["y"])
+        z = float(kf_depth_u16[y, x]) / K["depth_factor"]
+        if z <= 0 or (th_depth is not None and z > th_depth):
+            continue
+        Xw = (Twk @ np.array([(kp["x"] - cx) * z / fx, (kp["y"] - cy) * z / fy, z, 1.0]))[:3]
+        PC = Xw - Twk[:3, 3]
+        dist = np.linalg.norm(PC)
+        maxd = np.float32(dist) * sf[int(kp["octave"])]
+        rows.append((Xw, PC / dist, maxd / sf[-1], maxd, id_base + i, np.asarray(kf_desc[i], np.uint8)))
+    P = np.zeros(len(rows), M.LOCAL_POINT_DTYPE)
+    for j, (xw, nrm, mind, maxd, pid, d) in enumerate(rows):
+        P[j]["xw"], P[j]["normal"], P[j]["min_dist"], P[j]["max_dist"], P[j]["id"], P[j]["desc"] = \
+            xw, nrm, mind, maxd, pid, d
+        P[j]["n_obs"] = 1 + pid % 3
+    return P
+
+
+def as_last_frame_points(points, kps, id_base):
+    """A keyframe's own map points as the last frame's (its mvpMapPoints, keypoint i = id - id_base):
+    spslam_proj_point records in keypoint order with the keypoint's angle and octave."""
+    import spslam_match as M
+    P = np.zeros(len(points), M.PROJ_POINT_DTYPE)
+    for j, p in enumerate(points):
+        i = int(p["id"]) - id_base
+        P[j]["xw"], P[j]["angle"], P[j]["octave"] = p["xw"], kps[i]["angle"], kps[i]["octave"]
+        P[j]["n_obs"], P[j]["last_index"], P[j]["id"], P[j]["desc"] = p["n_obs"], i, p["id"], p["desc"]
+    return P
+
+
+def render_sequence_frames(seq_id, n_frames, w, h, K, n_boxes, first=0):
+    """(colour RGB u8, depth u16) of frames first .. first + n_frames - 1 of a sequence (worker-pool friendly)."""
+    sc = Scene(seq_id, n_boxes=n_boxes)
+    out = []
+    for t in range(first, first + n_frames):
+        g, d, fid = sc.render(sc.pose(t), w, h, K=K, noise_seed=seq_id * 100003 + t)
+        out.append((colorize(g, fid), d))
+    return out

@@ -65,14 +65,17 @@ int main(void) {
   S(spslam_map_plane) O(spslam_map_plane, id) O(spslam_map_plane, boundary_offset) O(spslam_map_plane, n_boundary)
   S(spslam_assoc_frame) O(spslam_assoc_frame, map_offset) O(spslam_assoc_frame, n_map) O(spslam_assoc_frame, carry)
   S(spslam_assoc_params)
-  S(spslam_proj_point) O(spslam_proj_point, angle) O(spslam_proj_point, n_obs) O(spslam_proj_point, desc)
+  S(spslam_proj_point) O(spslam_proj_point, angle) O(spslam_proj_point, n_obs) O(spslam_proj_point, id)
+  O(spslam_proj_point, desc)
   S(spslam_proj_frame) O(spslam_proj_frame, Tlw) O(spslam_proj_frame, point_offset) S(spslam_match_params)
   S(spslam_local_point) O(spslam_local_point, normal) O(spslam_local_point, max_dist) O(spslam_local_point, desc)
-  S(spslam_local_frame) O(spslam_local_frame, n_points) S(spslam_local_params)
+  S(spslam_local_frame) O(spslam_local_frame, n_points) O(spslam_local_frame, stamp) S(spslam_local_params)
+  O(spslam_local_point, n_obs)
   S(spslam_track_batch) O(spslam_track_batch, cap) O(spslam_track_batch, proj_frames)
   O(spslam_track_batch, stride_a) O(spslam_track_batch, cap_b) O(spslam_track_batch, map)
   O(spslam_track_batch, point_outlier) O(spslam_track_batch, fx) O(spslam_track_batch, bf)
   O(spslam_track_batch, plane_outlier) O(spslam_track_batch, next_vertical) O(spslam_track_batch, problems)
+  O(spslam_track_batch, seen) O(spslam_track_batch, velocity)
   return 0;
 }
 """

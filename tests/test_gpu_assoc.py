@@ -157,3 +157,50 @@ def test_carried_associations(assoc):
             n_kept += int(((fresh["match"] < 0) & (o["match"] >= 0)).sum())
             n += 1
     assert n >= 40 and n_kept > 0, (n, n_kept)
+
+
+def test_large_map_two_kernel_path(assoc):
+    """Maps with more planes than the fused kernel's LDS table holds ((cap_a + cap_b) x max_map floats > 48 KB)
+    take the two-kernel path (per (frame, map plane) distance workgroups + the decision walk): same answers."""
+    import torch
+    import oracle_assoc as OA
+    import spslam_assoc as SA
+    import spslam_planes as SP
+    import synth
+    rng = np.random.default_rng(77)
+    sc = synth.Scene(1, n_boxes=6)
+    m0, b0 = _map(rng, sc)
+    reps = -(-200 // len(m0))
+    m = np.concatenate([m0] * reps)
+    b = np.concatenate([b0] * reps)
+    m["boundary_offset"] = np.concatenate([m0["boundary_offset"] + k * len(b0) for k in range(reps)])
+    m["world"][len(m0):, 3] += rng.uniform(-0.3, 0.3, len(m) - len(m0)).astype(np.float32)
+    F, cap_a, cap_b = 4, 64, 32  # 96 x 200+ x 4 B > 48 KB
+    frames = np.zeros(F, SA.ASSOC_FRAME_DTYPE)
+    A = np.zeros((F, cap_a), SP.PLANE_DTYPE)
+    ca = np.zeros(F, np.int32)
+    expect = []
+    for f in range(F):
+        T, c, _ = synth.assoc_frame_planes(sc, 25 * f, rng, n_faces=6, n_random=2)
+        A[f, :len(c)]["coef"] = c
+        ca[f] = len(c)
+        frames[f]["Tcw"] = T.reshape(16)
+        frames[f]["n_map"] = len(m)
+        expect.append(OA.associate(T, c, m, b))
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy()).cuda()  # noqa
+    d_fr, d_A, d_ca, d_m, d_b = dev(frames), dev(A), torch.from_numpy(ca).cuda(), dev(m), dev(b)
+    d_cb = torch.zeros(F, dtype=torch.int32, device="cuda")
+    d_B = torch.zeros(F * cap_b * SP.SUPPOSED_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    out = torch.full((3, F * (cap_a + cap_b)), -7, dtype=torch.int32, device="cuda")
+    newp = torch.zeros(F, dtype=torch.int32, device="cuda")
+    assoc.batch_device(F, d_fr.data_ptr(), d_A.data_ptr(), SP.PLANE_DTYPE.itemsize, d_ca.data_ptr(), cap_a,
+                       d_B.data_ptr(), SP.SUPPOSED_DTYPE.itemsize, d_cb.data_ptr(), cap_b, d_m.data_ptr(),
+                       d_b.data_ptr(), len(m), out[0].data_ptr(), out[1].data_ptr(), out[2].data_ptr(),
+                       newp.data_ptr())
+    torch.cuda.synchronize()
+    out = out.cpu().numpy().reshape(3, F, cap_a + cap_b)
+    for f, o in enumerate(expect):
+        n = int(ca[f])
+        for k, key in enumerate(("match", "parallel", "vertical")):
+            assert np.array_equal(out[k, f, :n], o[key]), (f, key)
+        assert bool(newp[f]) == o["new_plane"], f

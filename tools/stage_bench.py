@@ -19,11 +19,9 @@ def main():
     ap.add_argument("--config", default="c2")
     a = ap.parse_args()
     import torch
-    import bench
     import pipeline
-    cfg = bench.CONFIGS[a.config]
-    hp = pipeline.HotPath(a.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"])
-    stages = {"orb": hp.orb, "planes": hp.planes, "pose": hp.pose}
+    hp = pipeline.HotPath(a.batch, **pipeline.CONFIGS[a.config])
+    stages = {"grab": hp.grab, "orb": hp.orb, "planes": hp.planes, "tail": hp._tail}
     for name, fn in stages.items():
         for _ in range(2):
             fn()
