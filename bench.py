@@ -256,6 +256,66 @@ def ate_report(hp, res, cpu_poses=None):
     return out
 
 
+def ate_sequences(cfg, device, n_frames=300, n_seq=2):
+    """ATE of tracked sequences (sp-slam_amd/sequence.py): n_seq sequences of n_frames tracked frames each on
+    the GPU, every frame's prior and last-frame points from its predecessor's result, against the CPU oracle
+    running the same loop (oracle/oracle_sequence.py) and against the synthetic ground truth.  TUM
+    evaluate_ate (Horn alignment, RMSE of camera centres, sp-slam_amd/trajectory.py) per sequence."""
+    import numpy as np
+    import sequence
+    import trajectory
+    t0 = time.perf_counter()
+    workers = min(16, os.cpu_count() or 1)
+    sp = sequence.SequencePath(n_seq, n_frames + 1, n_sequences=n_seq, device=device, render_workers=workers, **cfg)
+    try:
+        for _ in range(n_frames):
+            sp.step()
+        tr = sp.trajectory()
+        hist = sp.history()
+        t_gpu = time.perf_counter() - t0
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle_ctypes
+        import oracle_grab
+        import oracle_planes
+        import oracle_sequence
+        import oracle_step
+        cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
+        orb, po = oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures), oracle_planes.PlaneOracle()
+        out = {"kind": "tracked sequences (motion model from the previous frame; sp-slam_amd/sequence.py)",
+               "sequences": n_seq, "frames": n_frames, "vs_cpu_ref_m": [], "max_center_diff_vs_cpu_ref_m": [],
+               "max_rotation_diff_vs_cpu_ref": [], "vs_ground_truth_m": [], "cpu_ref_vs_ground_truth_m": [],
+               "ate_difference_vs_cpu_ref_m": [], "identical_decisions_until_frame": []}
+        t1 = time.perf_counter()
+        for slot in range(n_seq):
+            frames, T0, P0, local_of = sp.oracle_inputs(slot)
+            ch = {}
+
+            def rec(t, o, P):
+                ch[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
+                         int(o["pose2"][0]["n_inliers"]))
+            cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
+                                        sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
+                                        pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
+                                        on_frame=rec)
+            same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
+            out["identical_decisions_until_frame"].append(next((t for t, ok in enumerate(same, 1) if not ok), None))
+            g = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n_frames)]
+            c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n_frames)]
+            gt = [np.linalg.inv(sp._true_pose(slot, k + 1))[:3, 3] for k in range(n_frames)]
+            out["vs_cpu_ref_m"].append(trajectory.ate_rmse(g, c))
+            out["max_center_diff_vs_cpu_ref_m"].append(float(np.linalg.norm(np.array(g) - np.array(c), axis=1).max()))
+            out["max_rotation_diff_vs_cpu_ref"].append(float(max(
+                np.abs(tr[k + 1, slot][:3, :3] - cpu[k][:3, :3]).max() for k in range(n_frames))))
+            out["vs_ground_truth_m"].append(trajectory.ate_rmse(g, gt))
+            out["cpu_ref_vs_ground_truth_m"].append(trajectory.ate_rmse(c, gt))
+            out["ate_difference_vs_cpu_ref_m"].append(abs(out["vs_ground_truth_m"][-1] - out["cpu_ref_vs_ground_truth_m"][-1]))
+        out["cpu_frames_per_s"] = n_seq * n_frames / (time.perf_counter() - t1)
+        out["wall_s"] = {"gpu_incl_render": t_gpu, "cpu": time.perf_counter() - t1}
+        return out
+    finally:
+        sp.close()
+
+
 def _ensure_hw_queues():
     try:
         cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
@@ -281,6 +341,8 @@ def main():
     ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
+    ap.add_argument("--ate-frames", type=int, default=300,
+                    help="frames per tracked sequence of the ATE check (0 = skip)")
     ap.add_argument("--dist-check", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU): spawn, rendezvous, aggregation")
     args = ap.parse_args()
@@ -391,10 +453,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], cpu_poses = cpu_baseline(hp)
     if rank == 0:
-        result["ate"] = ate_report(hp, res, cpu_poses)
+        result["open_loop_pose_agreement"] = ate_report(hp, res, cpu_poses)
+    hp.close()
+    if rank == 0 and args.ate_frames > 0:
+        result["ate"] = ate_sequences(cfg, local, n_frames=args.ate_frames)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    hp.close()
     if dist:
         dist.destroy_process_group()
 

@@ -183,6 +183,8 @@ class SequencePath(pipeline.HotPath):
         self.d_nlmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
         self.local_probs = []
         self.traj = torch.zeros((T, B, 16), dtype=torch.float32, device="cuda")
+        # per frame: SearchByProjection matches, SearchLocalPoints matches, inliers of both PoseOptimizations
+        self.hist = torch.zeros((T, 4, B), dtype=torch.int32, device="cuda")
         self.n_tracked = 0
 
     def _setup_assoc(self, seq_id):
@@ -224,8 +226,19 @@ class SequencePath(pipeline.HotPath):
         with self.torch.cuda.stream(self.main):
             res = self.d_res2.view(self.B, G.POSE_RESULT_DTYPE.itemsize)[:, :64].contiguous()
             self.traj[self.n_tracked + 1].copy_(res.view(self.torch.float32).view(self.B, 16))
+            h = self.hist[self.n_tracked + 1]
+            h[0].copy_(self.d_nmatch)
+            h[1].copy_(self.d_nlmatch)
+            for r, d in ((2, self.d_res1), (3, self.d_res2)):  # n_inliers follows the 16 pose floats
+                h[r].copy_(d.view(self.B, G.POSE_RESULT_DTYPE.itemsize)[:, 64:68].contiguous().view(self.torch.int32)
+                           .view(self.B))
         self.n_tracked += 1
         self.d_pframes, self.d_ppoints = nxt
+
+    def history(self):
+        """[t][slot] (nmatches, local nmatches, inliers of the motion-model and local-map PoseOptimization)."""
+        self.torch.cuda.synchronize()
+        return self.hist[:self.n_tracked + 1].cpu().numpy().transpose(0, 2, 1)
 
     def trajectory(self):
         """Local-map pose (float 4x4) of frames 1 .. n_tracked of every slot: [t][slot] 4x4 (frame 0 = truth)."""
