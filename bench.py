@@ -89,7 +89,9 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "fast_cells_kernel": sum(px),                         # score maps read once
         # FAST survivors (4 B each) + per-cell counts in, retained level keypoints (8 B) out
         "octree_kernel": n_cand * 4 + 2 * sum(_cells(w, h) for w, h in lv) + n_kp * 8,
-        "desc_kernel": n_kp * (28 + 32),                      # keypoint + descriptor out
+        # per keypoint: the 31x31 patch around it read from the level (IC_Angle) and from the blurred level
+        # (rotated BRIEF), keypoint + descriptor out
+        "desc_kernel": n_kp * (2 * 31 * 31 + 28 + 32),
         "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call
         "plane_cloud_kernel": 4 * N + 12 * N,                 # depth samples in, xyz out
         # xyz in, distance map + 6 fp64 integral images out (one fused wavefront kernel)
@@ -413,11 +415,15 @@ def main():
         if k in alg and ms > 0:
             gbs = alg[k] * args.batch * (2 if k == "pose_kernel" else 1) / (ms / 1e3 / args.steps) / 1e9
             by_kernel[k] = {"achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS}
-    traffic = None
+    # HBM traffic cannot be counted inside this process (the PMC passes need rocprofv3 around it): it is read
+    # from the committed summary of such a run and reported with where and when it was measured
+    traffic, traffic_src = None, None
     pmc = ROOT / "profiles" / f"pmc_{args.config}_b{args.batch}.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get(dom)
+            pj = json.loads(pmc.read_text())
+            traffic = pj.get(dom)
+            traffic_src = {"file": str(pmc.relative_to(ROOT)), **pj.get("provenance", {})}
         except Exception:
             traffic = None
     result = {
@@ -444,7 +450,7 @@ def main():
         "kernels_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in sorted(times.items())},
         "roofline_by_kernel": by_kernel,
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_launch_s * 1e3,
                      "share_of_kernel_time": dom_ms / max(total_kernel_ms, 1e-9)},
         "cpu_baseline": None,

@@ -1,0 +1,36 @@
+"""Diagnostic: the C3 LocalMapping workload alone -- one batched LocalBundleAdjustment call over the step's
+local maps (51 maps of 12 keyframes / 1500 points at B = 256), wall time and LM step count.
+    python tools/lba_bench.py [--reps 5]"""
+import argparse
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "sp-slam_amd"), str(ROOT)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import pipeline
+    import spslam_lba as L
+    hp = pipeline.HotPath(a.batch, **pipeline.CONFIGS["c3"])
+    for r in range(a.reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hp.local_ba()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        res = hp.lba_out[5].cpu().numpy().view(L.LBA_RESULT_DTYPE)
+        print(f"rep {r}: {dt * 1e3:.2f} ms for {hp.n_lba} maps; iterations max {res['iterations'].max(0)} "
+              f"trials max {res['trials'].max()} device us max {res['phase_us'][:, 0].max():.0f}", flush=True)
+    hp.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -54,6 +54,11 @@ def main(fetch_dir, write_dir, out):
         detail[k] = dict(fetch_bytes=f, write_bytes=w, dispatches=len(fe.get(k, [])))
         print(f"{k:28s} fetch {f / 1e6:10.3f} MB  write {w / 1e6:10.3f} MB  per launch  ({len(fe.get(k, []))} launches)")
     res["detail"] = detail
+    import datetime
+    import os
+    res["provenance"] = {"measured_utc": datetime.datetime.utcnow().isoformat(timespec="seconds"),
+                         "git_head": os.environ.get("SPSLAM_GIT_HEAD", "unknown"),
+                         "command": os.environ.get("SPSLAM_PMC_CMD", "tools/pmc_round.sh")}
     res["note"] = ("HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KB x 1024), rocprofv3 separate --pmc passes, "
                    "gfx950 FETCH_SIZE correction per MI355X_MICROARCH.md")
     with open(out, "w") as fo:

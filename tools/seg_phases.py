@@ -27,10 +27,8 @@ def main():
     ap.add_argument("--config", default="c2")
     a = ap.parse_args()
     import torch
-    import bench
     import pipeline
-    cfg = bench.CONFIGS[a.config]
-    hp = pipeline.HotPath(a.batch, cfg["width"], cfg["height"], cfg["nfeatures"], cfg["n_boxes"])
+    hp = pipeline.HotPath(a.batch, **pipeline.CONFIGS[a.config])
     for _ in range(3):
         hp.planes()
     torch.cuda.synchronize()
