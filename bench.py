@@ -205,38 +205,47 @@ def shard_of(rank):
     return dict(seq_id=rank)
 
 
-def cpu_baseline(hp, budget_s=12.0):
-    """CPU restatement (oracle) of the same per-frame work, one core, bounded sample.  Also returns the
-    oracle's local-map pose of each distinct frame (the CPU reference trajectory of the ATE)."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(hp, timed=300, warmup=10, all_core_frames=40):
+    """CPU restatement (oracle) of the same per-frame work, timed in C++ (oracle/step_oracle.cpp: the whole chain
+    of oracle_step.run with no Python between stages): one core, `warmup` untimed then `timed` frames; then every
+    core of this process's CPU set, one independent frame stream per thread.  Also returns the oracle's local-map
+    pose of each distinct frame (the CPU reference of the ATE)."""
     sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle_ctypes
-    import oracle_planes
-    import oracle_lba
     import oracle_step
-    orb = oracle_ctypes.OrbOracle(nfeatures=hp.ex.params.nfeatures)
-    po = oracle_planes.PlaneOracle()
+    import oracle_step_cpp
     U = len(hp.frames)
     inputs = [oracle_step.from_hotpath(hp, i) for i in range(U)]
-    poses = {}
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < budget_s or len(poses) < U:
-        i = n % U
-        o = oracle_step.run(inputs[i], orb, po, supp_cap=hp.pe.supp_cap)
-        poses.setdefault(i, o["pose2"][0]["Tcw"].copy())
-        if hp.n_lba and n % hp.lba_every == 0:  # LocalMapping: one local BA per keyframe
-            pc = hp.plane_cfg
-            oracle_lba.lba_optimize(*hp.lba_problems[(n // hp.lba_every) % len(hp.lba_problems)][:6],
-                                    cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info, pc.chi,
-                                         pc.vp_chi))
-        n += 1
-    dt = time.perf_counter() - t0
-    lba = f" + LocalBundleAdjustment every {hp.lba_every} frames" if hp.n_lba else ""
-    return dict(value=n / dt, unit="frames/s", cores=1, kind="port",
-                sample=f"{n} frames ({U} distinct) of the same synthetic {hp.W}x{hp.H} workload (ORB + planes + "
-                       f"supposed planes + frame steps + SearchByProjection + 2x (plane association + graph + "
-                       f"PoseOptimization) + SearchLocalPoints{lba}), {dt:.1f}s on one core, "
-                       f"oracle/liboracle.so -O3 x86-64-v3"), poses
+    lba = None
+    if hp.n_lba:  # LocalMapping: one local BA per keyframe
+        lba = ([p[:6] for p in hp.lba_problems], hp.lba_every, hp.plane_cfg)
+    nf = hp.ex.params.nfeatures
+    el, outs = oracle_step_cpp.bench(inputs, nf, max(warmup, U), timed, 1, supp_cap=hp.pe.supp_cap, lba=lba)
+    poses = {i: outs[i]["Tcw2"].reshape(16).copy() for i in range(U)}
+    one = timed / el[0]
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))  # the GPU box's CPU share is 16 (nproc shows the whole machine)
+    el_all, _ = oracle_step_cpp.bench(inputs, nf, warmup, all_core_frames, threads, supp_cap=hp.pe.supp_cap, lba=lba)
+    allc = threads * all_core_frames / el_all.max()
+    lba_s = f" + LocalBundleAdjustment every {hp.lba_every} frames" if hp.n_lba else ""
+    return dict(value=one, unit="frames/s", cores=1, kind="port",
+                sample=f"{timed} frames after {max(warmup, U)} warm-up ({U} distinct) of the same synthetic "
+                       f"{hp.W}x{hp.H} workload (grab + ORB + planes + supposed planes + frame steps + "
+                       f"SearchByProjection + 2x (plane association + graph + PoseOptimization) + SearchLocalPoints"
+                       f"{lba_s}), {el[0]:.1f}s on one core, oracle/liboracle.so C++ -O3 x86-64-v3 "
+                       f"(oracle/step_oracle.cpp, no Python between stages)",
+                all_cores=dict(value=allc, unit="frames/s", threads=threads, frames_per_thread=all_core_frames,
+                               warmup_per_thread=warmup, nproc=os.cpu_count(), cpu_model=_cpu_model(),
+                               seconds=float(el_all.max()))), poses
 
 
 def ate_report(hp, res, cpu_poses=None):
@@ -339,6 +348,8 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--unique-frames", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=0,
+                    help="timed one-core CPU baseline frames (default 300; 100 above 640x480)")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
     ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -457,7 +468,7 @@ def main():
     }
     cpu_poses = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"], cpu_poses = cpu_baseline(hp)
+        result["cpu_baseline"], cpu_poses = cpu_baseline(hp, timed=args.cpu_frames or (300 if hp.W * hp.H <= 640 * 480 else 100))
     if rank == 0:
         result["open_loop_pose_agreement"] = ate_report(hp, res, cpu_poses)
     hp.close()

@@ -269,13 +269,20 @@ typedef struct spslam_lba_result {
     int32_t n_plane_outliers;
     int32_t status;           /* 0 ok, < 0 capacity / numerical failure */
     int32_t trials;           /* LM trials (lambda steps) in total */
-    int32_t pad[2];
+    int32_t stopped;          /* pbStopFlag: 0 not seen (or seen after the schedule ended), 1 seen before
+                                 optimize(5) -- returned, outputs = inputs, no outliers -- 2 seen at a later
+                                 check point: the schedule ended there (trials = trials run) */
+    int32_t pad;
     float phase_us[8];        /* diagnostics: device time per phase (setup, errors, edge terms, block sums,
                                  Schur, factorisation, substitution, update), microseconds */
 } spslam_lba_result;
 
 /* Drop-in for Optimizer::LocalBundleAdjustment on host buffers, one problem
  * (offsets inside *problem are ignored; observation offsets index obs arrays).
+ * stop_flag = pbStopFlag (NULL allowed): a bool another thread may raise while
+ * the call runs (LocalMapping::InterruptBA); it is copied to the device at the
+ * call and at every host poll of the schedule and honoured at g2o's check
+ * points (result.stopped).
  * kf_out: 16 floats per keyframe (local keyframes optimised, fixed ones
  * copied), pt_out 3 per point, pl_out 4 per plane, outlier flags per
  * observation.  cfg = the Plane.* config keys (as for PoseOptimization). */
@@ -283,21 +290,25 @@ int spslam_lba_optimize(spslam_ctx* ctx, const spslam_lba_problem* problem, cons
                         const spslam_lba_point* points, const spslam_lba_point_obs* point_obs,
                         const spslam_lba_plane* planes, const spslam_lba_plane_obs* plane_obs,
                         const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
-                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result);
+                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result,
+                        const volatile uint8_t* stop_flag);
 
 /* Batched, device resident: n problems (host copy `problems` for sizing, the
  * same records on the device at d_problems), one workgroup each, the whole
  * optimize(5) / relabel / optimize(10) schedule on the device.  Outputs are
  * indexed like the inputs (keyframe / point / plane offsets of each problem,
  * absolute observation indices).  At most 64 keyframes per problem
- * (status -2 otherwise).  Asynchronous on hip_stream. */
+ * (status -2 otherwise).  d_stop_flags: one pbStopFlag per problem in
+ * device-visible memory (device, or host-mapped coherent memory another thread
+ * raises), nonzero = stop; NULL = no flags.  The call returns once every
+ * problem is done (it polls the device); results are complete on hip_stream. */
 int spslam_lba_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_lba_problem* problems,
                                      const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
                                      const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
                                      const spslam_lba_plane* d_planes, const spslam_lba_plane_obs* d_plane_obs,
                                      const spslam_plane_config* cfg, float* d_kf_out, float* d_pt_out,
                                      float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
-                                     spslam_lba_result* d_results, void* hip_stream);
+                                     spslam_lba_result* d_results, const int32_t* d_stop_flags, void* hip_stream);
 
 /* ------------------------------------------------------------------------
  * Plane extraction: Frame::ComputePlanesFromOrganizedPointCloud

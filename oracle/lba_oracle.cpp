@@ -412,10 +412,19 @@ struct Opt {
         }
     }
     // SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg
+    // pbStopFlag emulation: the flag is raised right after trial number stop_after (SparseOptimizer::terminate();
+    // stop_after < 0: never).  cut = a check point saw it where the schedule would have continued.
+    int trials = 0, stop_after = -1;
+    bool cut = false;
+    bool terminate() const { return stop_after >= 0 && trials >= stop_after; }
     int optimize(int iterations) {
         if (active.empty() || (np == 0 && nl == 0)) return 0;
         int its = 0;
         for (int it = 0; it < iterations; it++) {
+            if (terminate()) {  // for (...; i < iterations && !terminate() && ok; ...)
+                cut = true;
+                break;
+            }
             compute_errors();
             double currentChi = robust_chi2();
             const double iniChi = currentChi;
@@ -423,6 +432,7 @@ struct Opt {
             if (it == 0) { lambda = lambda_init(); ni = 2; nBad = 0; }
             double rho = 0;
             int qmax = 0;
+            bool more;
             std::vector<double> x;
             do {
                 push();
@@ -448,7 +458,13 @@ struct Opt {
                     pop();
                 }
                 qmax++;
-            } while (rho < 0 && qmax < 10);
+                trials++;
+                more = rho < 0 && qmax < 10;
+                if (more && terminate()) {  // while (rho < 0 && qmax < max && !terminate())
+                    cut = true;
+                    more = false;
+                }
+            } while (more);
             its++;
             if (qmax == 10 || rho == 0) break;
             if ((iniChi - currentChi) * 1e3 < iniChi) nBad++;
@@ -487,11 +503,24 @@ Plane plane_from_cv(const float* c) {  // Converter::toPlane3D: flip d < 0, then
 }
 }  // namespace
 
-extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
-                                   const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
-                                   const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
-                                   const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
-                                   uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res) {
+// stop_after: pbStopFlag raised after that many LM trials (0 = already set at the call: the reference returns
+// before initializeOptimization, Optimizer.cc:1757-1759; < 0 = never raised)
+extern "C" int oracle_lba_optimize_stop(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
+                                        const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                                        const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
+                                        const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
+                                        uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res,
+                                        int stop_after) {
+    std::memset(res, 0, sizeof *res);
+    if (stop_after == 0) {  // if(*pbStopFlag) return;  -- nothing optimised, nothing erased
+        for (int k = 0; k < P->n_kf; k++) std::memcpy(kf_out + 16 * k, kfs[k].Tcw, 64);
+        for (int i = 0; i < P->n_points; i++) std::memcpy(pt_out + 3 * i, pts[i].xw, 12);
+        for (int i = 0; i < P->n_planes; i++) std::memcpy(pl_out + 4 * i, pls[i].world, 16);
+        std::memset(pobs_outlier, 0, P->n_point_obs);
+        std::memset(plobs_outlier, 0, P->n_plane_obs);
+        res->stopped = 1;
+        return 0;
+    }
     Graph G;
     long long maxKFid = 0, maxPointid = 0;
     for (int k = 0; k < P->n_kf; k++) {
@@ -567,10 +596,15 @@ extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba
             G.e.push_back(e);
         }
     Opt opt(G);
+    opt.stop_after = stop_after;
     res->iterations[0] = res->iterations[1] = 0;
     if (!G.e.empty()) {
         opt.initialize(0);
         res->iterations[0] = opt.optimize(5);
+    }
+    if (!G.e.empty() && opt.terminate()) {
+        opt.cut = true;  // bool bDoMore = !*pbStopFlag (Optimizer.cc:1763-1767): no relabel, no optimize(10)
+    } else if (!G.e.empty()) {
         // relabel with the cached errors, drop the robust kernels
         for (Edge& e : G.e) {
             bool bad;
@@ -600,6 +634,8 @@ extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba
     res->n_point_outliers = npo;
     res->n_plane_outliers = nplo;
     res->status = 0;
+    res->trials = opt.trials;
+    res->stopped = opt.cut ? 2 : 0;
     for (int k = 0; k < P->n_kf; k++) {
         if (!kfs[k].fixed) se3_to_cv(G.v[k].T, kf_out + 16 * k);
         else std::memcpy(kf_out + 16 * k, kfs[k].Tcw, 64);
@@ -611,4 +647,13 @@ extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba
     for (int i = 0; i < P->n_planes; i++)
         for (int j = 0; j < 4; j++) pl_out[4 * i + j] = (float)G.v[v_pl0 + i].P.c[j];
     return 0;
+}
+
+extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
+                                   const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                                   const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
+                                   const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
+                                   uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res) {
+    return oracle_lba_optimize_stop(P, kfs, pts, pobs, pls, plobs, cfg, kf_out, pt_out, pl_out, pobs_outlier,
+                                    plobs_outlier, res, -1);
 }

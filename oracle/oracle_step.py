@@ -26,8 +26,10 @@ class FrameInputs:
     """Everything one frame of the step reads: images, camera, the map it tracks against."""
 
     def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary, min_size=500,
-                 pose_cfg=None, local_seen=False):
+                 pose_cfg=None, local_seen=False, rgb=None, depth_raw=None, depth_scale=None):
         self.gray, self.depth = gray, depth
+        # the raw frame GrabImageRGBD receives (the C++ chain, oracle_step_cpp, grabs it itself)
+        self.rgb, self.depth_raw, self.depth_scale = rgb, depth_raw, depth_scale
         self.cam = cam                  # fx, fy, cx, cy, bf
         self.min_size = min_size        # Plane.MinSize
         self.pose_cfg = pose_cfg        # Plane.*Info / Chi / VPChi (spslam_gpu.PlaneConfig; None = TUM1.yaml)
@@ -111,9 +113,47 @@ def camera_inputs(hp):
 def from_hotpath(hp, i):
     """FrameInputs of batch slot i of a sp-slam_amd/pipeline.py HotPath (host copies of its inputs)."""
     U = len(hp.frames)
+    scale = oracle_grab.depth_scale(hp.depth_factor)
     gray = oracle_grab.cvt_gray(hp.frames[i % U][1], rgb=True)  # GrabImageRGBD, Tracking.cc:214-229
-    depth = oracle_grab.convert_depth(hp.frames[i % U][2], oracle_grab.depth_scale(hp.depth_factor))
+    depth = oracle_grab.convert_depth(hp.frames[i % U][2], scale)
     cam, geo, inv_s2 = camera_inputs(hp)
     return FrameInputs(gray, depth, cam, geo, inv_s2,
                        hp.match_probs[i % len(hp.match_probs)], hp.local_probs[i % len(hp.local_probs)],
-                       hp.assoc_map, hp.assoc_boundary, min_size=hp.min_size, pose_cfg=hp.plane_cfg)
+                       hp.assoc_map, hp.assoc_boundary, min_size=hp.min_size, pose_cfg=hp.plane_cfg,
+                       rgb=hp.frames[i % U][1], depth_raw=hp.frames[i % U][2], depth_scale=scale)
+
+
+def synthetic(seq_id=0, frame=6, W=640, H=480, K=None, nfeatures=1000, n_boxes=5, min_size=500, pose_cfg=None):
+    """FrameInputs built on the CPU the way sp-slam_amd/pipeline.py HotPath builds its slots (last-frame map
+    points from frame-1's ORB keypoints, local map from frame-4's, the scene's map planes), with the oracle
+    ORB in place of the device one (bit-identical).  For CPU tests of the C++ chain."""
+    import synth
+    import spslam_match as SM  # noqa: F401  (record dtypes only)
+    K = K or synth.TUM3
+    s = W / 640.0
+    Ks = dict(K, fx=K["fx"] * s, fy=K["fy"] * s, cx=K["cx"] * s, cy=K["cy"] * s)
+    scene = synth.Scene(seq_id, n_boxes=n_boxes)
+    orb = oracle_ctypes.OrbOracle(nfeatures=nfeatures)
+    rng = np.random.default_rng(seq_id * 977 + 3)
+    g, d, fid = scene.render(scene.pose(frame), W, H, K=K, noise_seed=seq_id * 1000 + frame)
+    rgb = synth.colorize(g, fid)
+    scale = oracle_grab.depth_scale(K["depth_factor"])
+    gray = oracle_grab.cvt_gray(rgb, rgb=True)
+    depth = oracle_grab.convert_depth(d, scale)
+    lg, ld, _ = scene.render(scene.pose(frame - 1), W, H, K=K, noise_seed=seq_id * 1000 + frame + 500)
+    kl, dl = orb.extract(lg)
+    proj = synth.proj_problem(scene, frame - 1, frame, kl, dl, ld, rng, K=Ks)
+    kg, kd, _ = scene.render(scene.pose(frame - 4), W, H, K=K, noise_seed=seq_id * 1000 + frame + 900)
+    kk, dk = orb.extract(kg)
+    local = synth.local_problem(scene, frame - 4, frame, kk, dk, kd, rng, K=Ks)
+    mp, bxyz = synth.map_planes(scene, np.random.default_rng(seq_id * 31 + 7))
+    m = np.zeros(len(mp["world"]), oracle_assoc.MAP_PLANE_DTYPE)
+    for k, v in mp.items():
+        m[k] = v
+    fx, fy, cx, cy, bf = Ks["fx"], Ks["fy"], Ks["cx"], Ks["cy"], K["bf"]
+    b = oracle_frame.frame_rgbd(np.zeros((0, 2), np.float32), depth, fx, fy, cx, cy, bf=bf)["bounds"]
+    ginv = [np.float32(64) / np.float32(b[1] - b[0]), np.float32(48) / np.float32(b[3] - b[2])]
+    sc, _, _, inv_s2 = orb.scale_tables()  # mvScaleFactor, mvInvLevelSigma2
+    geo = np.concatenate([[fx, fy, cx, cy, bf, *b, *ginv], sc]).astype(np.float32)
+    return FrameInputs(gray, depth, (fx, fy, cx, cy, bf), geo, np.asarray(inv_s2, np.float32), proj, local, m, bxyz,
+                       min_size=min_size, pose_cfg=pose_cfg, rgb=rgb, depth_raw=d, depth_scale=scale)

@@ -26,6 +26,11 @@
 //               relabel with the cached errors, optimize(10));
 //   restore     rejected trials roll back.
 // The host enqueues steps and polls a device counter every few steps.
+// pbStopFlag (Optimizer.cc:1351-1352, 1757-1767; g2o SparseOptimizer::terminate):
+// read by one thread per problem at g2o's check points -- before optimize(5)
+// (return, nothing changed), after every trial (the LM do-while), at every
+// iteration start (the optimize() loop), between the passes (bDoMore) -- and
+// latched; a raised flag ends the schedule where it would have continued.
 // All arithmetic is fp64; reductions are tree-ordered, so results match the
 // oracle to rounding (north-star bar 1e-4), not bitwise.
 #include <hip/hip_runtime.h>
@@ -94,6 +99,13 @@ __device__ __forceinline__ SE3 load_pose(const double* p) { return SE3{Q{p[0], p
 __device__ __forceinline__ void store_pose(double* p, const SE3& T) {
     p[0] = T.r.w; p[1] = T.r.x; p[2] = T.r.y; p[3] = T.r.z; p[4] = T.t.x; p[5] = T.t.y; p[6] = T.t.z;
 }
+// SparseOptimizer::terminate(): the caller's flag, read through to memory (it may be host-coherent and
+// raised by another thread while the schedule runs), latched once seen
+__device__ __forceinline__ bool stop_requested(const LbaBatch& b, int p, LbaCtl& k) {
+    if (!k.stop && b.stop) k.stop = __hip_atomic_load(b.stop + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    return k.stop != 0;
+}
+
 // Converter::toPlane3D (flip d < 0) + Plane3D(v) normalisation
 __device__ __forceinline__ P4 plane_from_f(const float* c) {
     P4 p{{c[0], c[1], c[2], c[3]}};
@@ -398,7 +410,21 @@ __global__ __launch_bounds__(kThreads) void k_setup(LbaBatch b, int max_it0) {
         k.robust = 1;
         k.restore_step = -1;
         k.t0 = wall_clock64();
+        if (stop_requested(b, p, k)) {  // if(*pbStopFlag) return; before initializeOptimization
+            k.state = kDone;
+            k.stopped = 1;
+        }
     }
+}
+
+// start of a step: the optimize() loop's terminate() check at an iteration start (and at a pass start)
+__global__ void k_step_begin(LbaBatch b) {
+    if (threadIdx.x != 0) return;
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if ((k.state != kStruct && k.state != kIter) || !stop_requested(b, blockIdx.x, k)) return;
+    k.stopped = k.phase == 0 && k.trials == 0 ? 1 : 2;  // nothing done yet: same as the early return
+    k.state = kDone;
 }
 
 // ---------------------------------------------------------------- structure
@@ -937,7 +963,8 @@ __global__ void k_decide(LbaBatch b, int step) {
     }
     k.qmax++;
     k.trials++;
-    if (rho < 0 && k.qmax < 10) return;  // next trial
+    const bool stop = stop_requested(b, blockIdx.x, k);
+    if (rho < 0 && k.qmax < 10 && !stop) return;  // next trial (do-while ... && !terminate())
     k.its[k.phase]++;
     bool term = k.qmax == 10 || rho == 0;
     if (!term) {
@@ -949,6 +976,10 @@ __global__ void k_decide(LbaBatch b, int step) {
     if (k.it >= k.max_it) term = true;
     if (term) k.state = k.phase == 0 ? kRelabel : kDone;
     else k.state = kIter;
+    if (stop && k.state != kDone) {  // the next iteration or (bDoMore) the second pass does not run
+        k.state = kDone;
+        k.stopped = 2;
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_restore_lm(LbaBatch b, LbaWork w, int step) {
@@ -991,6 +1022,11 @@ __global__ void k_relabel_done(LbaBatch b, int max_it1) {
     Ctx c = make_ctx(b, blockIdx.x);
     LbaCtl& k = *c.ctl;
     if (k.state != kRelabel) return;
+    if (stop_requested(b, blockIdx.x, k)) {  // raised after optimize(5) returned: bDoMore = false
+        k.state = kDone;
+        k.stopped = 2;
+        return;
+    }
     k.state = kStruct;
     k.phase = 1;
     k.robust = 0;  // setRobustKernel(0) on every edge
@@ -1017,6 +1053,21 @@ __global__ __launch_bounds__(kThreads) void k_outputs(LbaBatch b, LbaConsts C) {
     Ctx c = make_ctx(b, p);
     const spslam_lba_problem pb = b.probs[p];
     if (c.K > kLbaMaxKeyframes) return;
+    if (c.ctl->stopped == 1) {  // returned before optimizing: the map is untouched, nothing is erased
+        for (int e = t; e < c.E; e += kThreads) {
+            if (e < c.Ep) b.pobs_out[c.e_src[e]] = 0;
+            else b.plobs_out[c.e_src[e]] = 0;
+        }
+        for (int i = t; i < 16 * c.K; i += kThreads) b.kf_out[16 * (size_t)pb.kf_offset + i] = c.kf[i / 16].Tcw[i % 16];
+        for (int i = t; i < 3 * c.Np; i += kThreads) b.pt_out[3 * (size_t)pb.point_offset + i] = c.pt[i / 3].xw[i % 3];
+        for (int i = t; i < 4 * c.Nq; i += kThreads) b.pl_out[4 * (size_t)pb.plane_offset + i] = c.pl[i / 4].world[i % 4];
+        if (t == 0) {
+            spslam_lba_result* r = b.res + p;
+            *r = spslam_lba_result{};
+            r->stopped = 1;
+        }
+        return;
+    }
     int npo = 0, nplo = 0;
     for (int e = t; e < c.E; e += kThreads) {
         double info[3];
@@ -1062,6 +1113,7 @@ __global__ __launch_bounds__(kThreads) void k_outputs(LbaBatch b, LbaConsts C) {
         r->n_plane_outliers = (int)cnt[1];
         r->status = k.state == kDone ? 0 : -3;
         r->trials = k.trials;
+        r->stopped = k.stopped;
         r->phase_us[0] = (float)((wall_clock64() - k.t0) * 0.01);  // 100 MHz ticks: setup to outputs
     }
 }
@@ -1069,7 +1121,7 @@ __global__ __launch_bounds__(kThreads) void k_outputs(LbaBatch b, LbaConsts C) {
 }  // namespace lba
 
 hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int max_steps, hipStream_t s,
-                   KernelTimer* timer, int* steps_out) {
+                   KernelTimer* timer, int* steps_out, const volatile uint8_t* stop_src, volatile int32_t* stop_mirror) {
     using namespace lba;
     static const hipError_t lds_attr =
         hipFuncSetAttribute((const void*)k_factor, hipFuncAttributeMaxDynamicSharedMemorySize, kFactorLds);
@@ -1081,6 +1133,7 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
     int steps = 0, active = 1;
     while (steps < max_steps) {
         const int st = steps;
+        if (b.stop) hipLaunchKernelGGL(k_step_begin, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_struct_count, dim3(w.n_kf_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_struct_final, dim3(P), T, 0, s, b);
         hipLaunchKernelGGL(k_struct_fill, dim3(w.n_kf_tasks), T, 0, s, b, w);
@@ -1103,6 +1156,7 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
         hipLaunchKernelGGL(k_relabel_done, dim3(P), dim3(64), 0, s, b, 10);
         steps++;
         if (steps % 4 == 0) {
+            if (stop_src && *stop_src) *stop_mirror = 1;
             hipLaunchKernelGGL(k_count_active, dim3(1), T, 0, s, b);
             hipError_t e = hipMemcpyAsync(&active, b.active, sizeof(int), hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);

@@ -15,7 +15,8 @@ constexpr int kLbaCon = 57;            // per-edge terms: Hll 9, bl 3, Hpl 18 (3
 struct LbaCtl {
     int state;        // 0 STRUCT, 1 ITER, 2 TRIAL, 3 RELABEL, 4 DONE
     int phase, it, max_it, robust, qmax, nBad, np, ok, restore_step, trials, its[2];
-    int pad;
+    int stop;         // pbStopFlag seen (latched)
+    int stopped;      // 1 = before optimize(5) (nothing changed), 2 = schedule cut short
     double lambda, ni, currentChi, iniChi;
     long long t0;     // wall_clock64 at setup (diagnostics)
 };
@@ -87,12 +88,16 @@ struct LbaBatch {
     uint8_t *pobs_out, *plobs_out;
     spslam_lba_result* res;
     int* active;      // problems not DONE (polled by the host)
+    const int32_t* stop;  // per problem pbStopFlag (device-visible; NULL = no flag)
 };
 
 // Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase
 // kernels step by step on `s` and polls the device every few steps until
 // every problem is DONE (so it returns after the work completed).
+// stop_src / stop_mirror: a host bool (pbStopFlag of the host-buffer entry point) copied into the
+// device-visible flag at every poll (NULL = none).
 hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int max_steps, hipStream_t s,
-                   KernelTimer* timer, int* steps_out);
+                   KernelTimer* timer, int* steps_out, const volatile uint8_t* stop_src = nullptr,
+                   volatile int32_t* stop_mirror = nullptr);
 
 }  // namespace spslam

@@ -127,6 +127,7 @@ struct spslam_ctx {
     uint8_t* d_lba_scratch = nullptr;
     size_t lba_scratch_bytes = 0;
     long long* d_lba_off = nullptr;
+    int32_t* h_lba_stop = nullptr;    // host-mapped coherent pbStopFlag mirror of spslam_lba_optimize
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
     size_t lba_stage_bytes = 0;
@@ -274,6 +275,7 @@ void free_all(spslam_ctx* c) {
                     c->d_vocab, c->d_bow_scratch, c->d_bow_stage};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    if (c->h_lba_stop) (void)hipHostFree(c->h_lba_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c->timer;
     c->timer = nullptr;
@@ -951,13 +953,14 @@ int spslam_frame_rgbd(spslam_ctx* c, const spslam_keypoint* kps, int n, const fl
     return SPSLAM_OK;
 }
 
-int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_problem* problems,
-                                     const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
-                                     const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
-                                     const spslam_lba_plane* d_planes, const spslam_lba_plane_obs* d_plane_obs,
-                                     const spslam_plane_config* cfg, float* d_kf_out, float* d_pt_out,
-                                     float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
-                                     spslam_lba_result* d_results, void* hip_stream) {
+namespace {
+int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const spslam_lba_problem* d_problems,
+              const spslam_lba_keyframe* d_kfs, const spslam_lba_point* d_points,
+              const spslam_lba_point_obs* d_point_obs, const spslam_lba_plane* d_planes,
+              const spslam_lba_plane_obs* d_plane_obs, const spslam_plane_config* cfg, float* d_kf_out,
+              float* d_pt_out, float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
+              spslam_lba_result* d_results, const int32_t* d_stop_flags, void* hip_stream,
+              const volatile uint8_t* stop_src, volatile int32_t* stop_mirror) {
     if (!c) return SPSLAM_ERR_ARG;
     if (n < 1 || !problems || !d_problems || !d_kfs || !cfg || !d_kf_out || !d_results)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
@@ -1032,17 +1035,31 @@ int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_prob
               w0 + ec.size() + lc.size() + kt.size(), (int)pt.size()};
     LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
-               (int*)(c->d_lba_work + work.size() - 1)};
+               (int*)(c->d_lba_work + work.size() - 1), d_stop_flags};
     // optimize(5) + optimize(10), at most 10 trials per iteration, plus the two structure steps
-    HIP_CHECK(c, lba_run(B, W, C, 15 * 10 + 4, s, c->timer, nullptr));
+    HIP_CHECK(c, lba_run(B, W, C, 15 * 10 + 4, s, c->timer, nullptr, stop_src, stop_mirror));
     return SPSLAM_OK;
+}
+}  // namespace
+
+int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_problem* problems,
+                                     const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
+                                     const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
+                                     const spslam_lba_plane* d_planes, const spslam_lba_plane_obs* d_plane_obs,
+                                     const spslam_plane_config* cfg, float* d_kf_out, float* d_pt_out,
+                                     float* d_pl_out, uint8_t* d_point_obs_outlier, uint8_t* d_plane_obs_outlier,
+                                     spslam_lba_result* d_results, const int32_t* d_stop_flags, void* hip_stream) {
+    return lba_batch(c, n, problems, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs, cfg, d_kf_out,
+                     d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
+                     hip_stream, nullptr, nullptr);
 }
 
 int spslam_lba_optimize(spslam_ctx* c, const spslam_lba_problem* problem, const spslam_lba_keyframe* kfs,
                         const spslam_lba_point* points, const spslam_lba_point_obs* point_obs,
                         const spslam_lba_plane* planes, const spslam_lba_plane_obs* plane_obs,
                         const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
-                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result) {
+                        uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result,
+                        const volatile uint8_t* stop_flag) {
     if (!c || !problem || !cfg || !result) return SPSLAM_ERR_ARG;
     spslam_lba_problem P = *problem;
     P.kf_offset = P.point_offset = P.plane_offset = 0;
@@ -1068,11 +1085,15 @@ int spslam_lba_optimize(spslam_ctx* c, const spslam_lba_problem* problem, const 
     const void* src[] = {&P, kfs, points, point_obs, planes, plane_obs};
     for (int i = 0; i < 6; i++)
         if (sz[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], sz[i], hipMemcpyHostToDevice, c->stream));
-    int rc = spslam_lba_optimize_batch_device(
+    if (stop_flag && !c->h_lba_stop)
+        HIP_CHECK(c, hipHostMalloc((void**)&c->h_lba_stop, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+    if (stop_flag) *(volatile int32_t*)c->h_lba_stop = *stop_flag ? 1 : 0;
+    int rc = lba_batch(
         c, 1, &P, (const spslam_lba_problem*)(q + o[0]), (const spslam_lba_keyframe*)(q + o[1]),
         (const spslam_lba_point*)(q + o[2]), (const spslam_lba_point_obs*)(q + o[3]),
         (const spslam_lba_plane*)(q + o[4]), (const spslam_lba_plane_obs*)(q + o[5]), cfg, (float*)(q + o[6]),
-        (float*)(q + o[7]), (float*)(q + o[8]), q + o[9], q + o[10], (spslam_lba_result*)(q + o[11]), c->stream);
+        (float*)(q + o[7]), (float*)(q + o[8]), q + o[9], q + o[10], (spslam_lba_result*)(q + o[11]),
+        stop_flag ? c->h_lba_stop : nullptr, c->stream, stop_flag, stop_flag ? c->h_lba_stop : nullptr);
     if (rc) return rc;
     void* dst[] = {kf_out, pt_out, pl_out, point_obs_outlier, plane_obs_outlier, result};
     for (int i = 0; i < 6; i++)

@@ -20,7 +20,8 @@ LBA_PROBLEM_DTYPE = np.dtype([("n_kf", "<i4"), ("n_points", "<i4"), ("n_planes",
                               ("point_offset", "<i4"), ("plane_offset", "<i4"), ("n_point_obs", "<i4"),
                               ("n_plane_obs", "<i4")])
 LBA_RESULT_DTYPE = np.dtype([("iterations", "<i4", 2), ("n_point_outliers", "<i4"), ("n_plane_outliers", "<i4"),
-                             ("status", "<i4"), ("trials", "<i4"), ("pad", "<i4", 2), ("phase_us", "<f4", 8)])
+                             ("status", "<i4"), ("trials", "<i4"), ("stopped", "<i4"), ("pad", "<i4"),
+                             ("phase_us", "<f4", 8)])
 assert LBA_KEYFRAME_DTYPE.itemsize == 96 and LBA_POINT_DTYPE.itemsize == 24
 assert LBA_POINT_OBS_DTYPE.itemsize == 20 and LBA_PLANE_DTYPE.itemsize == 32
 assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 64
@@ -33,8 +34,17 @@ PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # IC
 
 def _bind(lib):
     vp = ctypes.c_void_p
-    lib.spslam_lba_optimize.argtypes = [vp] * 14
-    lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 15
+    lib.spslam_lba_optimize.argtypes = [vp] * 15
+    lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 16
+
+
+def _addr(flag):
+    if flag is None:
+        return None
+    if isinstance(flag, np.ndarray):
+        assert flag.dtype == np.uint8 and flag.size >= 1
+        return flag.ctypes.data
+    return ctypes.addressof(flag)
 
 
 class LocalBA:
@@ -45,7 +55,9 @@ class LocalBA:
         _bind(ex.lib)
         self.cfg = np.ascontiguousarray(cfg, np.float64)
 
-    def __call__(self, prob, kfs, points, point_obs, planes, plane_obs):
+    def __call__(self, prob, kfs, points, point_obs, planes, plane_obs, stop_flag=None):
+        """stop_flag: pbStopFlag -- a one-byte buffer (ctypes.c_uint8 or numpy u8) another thread may set while
+        the call runs (ctypes releases the GIL for the call)."""
         arrs = [np.ascontiguousarray(a) for a in (prob, kfs, points, point_obs, planes, plane_obs)]
         kf_out = np.zeros((max(len(kfs), 1), 16), np.float32)
         pt_out = np.zeros((max(len(points), 1), 3), np.float32)
@@ -56,13 +68,13 @@ class LocalBA:
         ptr = lambda a: a.ctypes.data if a.size else None  # noqa: E731
         self.ex._check(self.ex.lib.spslam_lba_optimize(
             self.ex.ctx, *[ptr(a) for a in arrs], self.cfg.ctypes.data, kf_out.ctypes.data, pt_out.ctypes.data,
-            pl_out.ctypes.data, po.ctypes.data, plo.ctypes.data, res.ctypes.data))
+            pl_out.ctypes.data, po.ctypes.data, plo.ctypes.data, res.ctypes.data, _addr(stop_flag)))
         return dict(Tcw=kf_out[:len(kfs)], points=pt_out[:len(points)], planes=pl_out[:len(planes)],
                     point_outlier=po[:len(point_obs)], plane_outlier=plo[:len(plane_obs)], result=res)
 
     def batch_device(self, n, problems_host, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
-                     d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream=0):
+                     d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream=0, d_stop=None):
         ph = np.ascontiguousarray(problems_host)
         self.ex._check(self.ex.lib.spslam_lba_optimize_batch_device(
             self.ex.ctx, n, ph.ctypes.data, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
-            self.cfg.ctypes.data, d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream or None))
+            self.cfg.ctypes.data, d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, d_stop or None, stream or None))

@@ -48,6 +48,7 @@ def test_lba_matches_oracle(lba):
         g = lba(*P[:6])
         assert g["result"]["status"] == 0
         assert list(g["result"]["iterations"]) == list(o["result"]["iterations"]), k
+        assert g["result"]["trials"] == o["result"]["trials"] and g["result"]["stopped"] == 0, k
         assert np.array_equal(g["point_outlier"], o["point_outlier"]), \
             f"problem {k}: {np.nonzero(g['point_outlier'] != o['point_outlier'])[0][:10]}"
         assert np.array_equal(g["plane_outlier"], o["plane_outlier"]), k
@@ -64,12 +65,10 @@ def test_lba_matches_oracle(lba):
         assert e1 < 0.6 * e0, (k, e0, e1)
 
 
-def test_lba_batch_device_matches_single(lba):
+def _batch(lba, probs, flags=None):
+    """One batch_device call over `probs` (optionally with per-problem stop flags preset in device memory)."""
     import torch
     import spslam_lba as L
-    probs = _problems()[:3]
-    singles = [lba(*P[:6]) for P in probs]
-    # concatenate into one batch
     hdr = np.zeros(len(probs), L.LBA_PROBLEM_DTYPE)
     kf, pt, po, pl, plo = [], [], [], [], []
     nk = npt = npo = npl = nplo = 0
@@ -91,13 +90,85 @@ def test_lba_batch_device_matches_single(lba):
     po_out = torch.zeros(max(npo, 1), dtype=torch.uint8, device="cuda")
     plo_out = torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda")
     res = torch.zeros(len(probs) * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    stop = None if flags is None else torch.tensor(flags, dtype=torch.int32, device="cuda")
     lba.batch_device(len(probs), hdr, *[x.data_ptr() for x in d], kf_out.data_ptr(), pt_out.data_ptr(),
-                     pl_out.data_ptr(), po_out.data_ptr(), plo_out.data_ptr(), res.data_ptr())
+                     pl_out.data_ptr(), po_out.data_ptr(), plo_out.data_ptr(), res.data_ptr(),
+                     d_stop=None if stop is None else stop.data_ptr())
     torch.cuda.synchronize()
-    kf_out, pt_out, pl_out = kf_out.cpu().numpy(), pt_out.cpu().numpy(), pl_out.cpu().numpy()
-    po_out, plo_out = po_out.cpu().numpy(), plo_out.cpu().numpy()
+    return (hdr, kf_out.cpu().numpy(), pt_out.cpu().numpy(), pl_out.cpu().numpy(), po_out.cpu().numpy(),
+            plo_out.cpu().numpy(), res.cpu().numpy().view(L.LBA_RESULT_DTYPE))
+
+
+def test_lba_batch_device_matches_single(lba):
+    probs = _problems()[:3]
+    singles = [lba(*P[:6]) for P in probs]
+    hdr, kf_out, pt_out, pl_out, po_out, plo_out, _ = _batch(lba, probs)
     for i, s in enumerate(singles):
         h = hdr[i]
         assert np.array_equal(kf_out[h["kf_offset"]:h["kf_offset"] + h["n_kf"]], s["Tcw"])
         assert np.array_equal(pt_out[h["point_offset"]:h["point_offset"] + h["n_points"]], s["points"])
         assert np.array_equal(pl_out[h["plane_offset"]:h["plane_offset"] + h["n_planes"]], s["planes"])
+
+
+def test_lba_stop_flags_preset(lba):
+    """pbStopFlag already raised at the call (Optimizer.cc:1757-1759): those problems return the map untouched and
+    flag nothing; the other problems of the batch are unaffected (bit-identical to an unflagged run)."""
+    probs = _problems()[:3]
+    hdr, kf0, pt0, pl0, po0, plo0, res0 = _batch(lba, probs)
+    hdr, kf1, pt1, pl1, po1, plo1, res1 = _batch(lba, probs, flags=[1, 0, 1])
+    for i, P in enumerate(probs):
+        h = hdr[i]
+        ks, ps, qs = (slice(h["kf_offset"], h["kf_offset"] + h["n_kf"]),
+                      slice(h["point_offset"], h["point_offset"] + h["n_points"]),
+                      slice(h["plane_offset"], h["plane_offset"] + h["n_planes"]))
+        if i == 1:
+            assert res1[i]["stopped"] == 0 and res1[i]["trials"] == res0[i]["trials"]
+            assert np.array_equal(kf1[ks], kf0[ks]) and np.array_equal(pt1[ps], pt0[ps])
+            assert np.array_equal(pl1[qs], pl0[qs])
+            continue
+        assert res1[i]["stopped"] == 1 and res1[i]["trials"] == 0 and list(res1[i]["iterations"]) == [0, 0]
+        assert np.array_equal(kf1[ks], P[1]["Tcw"]) and np.array_equal(pt1[ps], P[2]["xw"])
+        assert np.array_equal(pl1[qs], P[4]["world"])
+    assert not po1[:probs[0][0]["n_point_obs"]].any()
+
+
+def test_lba_stop_flag_raised_while_running(lba):
+    """LocalMapping::InterruptBA: another thread raises pbStopFlag while spslam_lba_optimize runs.  Wherever the
+    device saw it (result.trials), the oracle with the flag raised after that trial gives the same map, flags and
+    iteration counts.  Delays are spread over the unflagged run time, so most runs stop part-way."""
+    import threading
+    import time
+    import oracle_lba
+    P = _problems()[3]
+    t0 = time.perf_counter()
+    full = lba(*P[:6])
+    t_full = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    full = lba(*P[:6])
+    t_full = min(t_full, time.perf_counter() - t0)
+    n_trials = int(full["result"]["trials"])
+    seen = {0: 0, 1: 0, 2: 0}
+    for frac in (0.0, 0.1, 0.25, 0.4, 0.55, 0.7, 0.85, 1.5):
+        flag = np.zeros(1, np.uint8)
+
+        def raise_flag(delay=frac * t_full, f=flag):
+            time.sleep(delay)
+            f[0] = 1
+        th = threading.Thread(target=raise_flag)
+        th.start()
+        g = lba(*P[:6], stop_flag=flag)
+        th.join()
+        r = g["result"]
+        stopped = int(r["stopped"])
+        seen[stopped] += 1
+        T = {0: -1, 1: 0, 2: int(r["trials"])}[stopped]
+        o = oracle_lba.lba_optimize(*P[:6], stop_after=T)
+        assert o["result"]["stopped"] == stopped and o["result"]["trials"] == r["trials"], (frac, r, o["result"])
+        assert list(r["iterations"]) == list(o["result"]["iterations"]), frac
+        assert np.array_equal(g["point_outlier"], o["point_outlier"]), frac
+        assert np.array_equal(g["plane_outlier"], o["plane_outlier"]), frac
+        assert _close(g["Tcw"], o["Tcw"]) and _close(g["points"], o["points"]), frac
+        if stopped == 2:
+            assert 0 < r["trials"] < n_trials
+    print("stop outcomes", seen, "trials", n_trials, "t_full", t_full)
+    assert seen[2] >= 1, seen

@@ -55,3 +55,34 @@ def test_fixed_keyframes_unchanged_and_empty_problem():
     loc = kfs["fixed"] == 0
     # local keyframes go through Converter::toSE3Quat / toCvMat unchanged up to float rounding
     assert np.abs(r["Tcw"][loc] - kfs["Tcw"][loc]).max() < 1e-6
+
+
+def test_stop_flag_schedule():
+    """pbStopFlag (Optimizer.cc:1351-1352, 1757-1767; g2o SparseOptimizer::terminate): raised before the call the
+    reference returns without touching the map; raised after trial T the schedule ends at the next check point
+    (after that trial), so exactly T trials run, and a flag raised after the last trial changes nothing."""
+    P = _prob(7, n_points=900)
+    full = oracle_lba.lba_optimize(*P[:6])
+    n = int(full["result"]["trials"])
+    assert n >= 6 and full["result"]["stopped"] == 0
+    r0 = oracle_lba.lba_optimize(*P[:6], stop_after=0)
+    assert r0["result"]["stopped"] == 1 and r0["result"]["trials"] == 0
+    assert np.array_equal(r0["Tcw"], P[1]["Tcw"]) and np.array_equal(r0["points"], P[2]["xw"])
+    assert np.array_equal(r0["planes"], P[4]["world"]) and not r0["point_outlier"].any()
+    late = oracle_lba.lba_optimize(*P[:6], stop_after=n)
+    assert late["result"]["stopped"] == 0
+    for k in ("Tcw", "points", "planes", "point_outlier", "plane_outlier"):
+        assert np.array_equal(late[k], full[k]), k
+    its_prev = 0
+    pass2_seen = False
+    for T in range(1, n):
+        r = oracle_lba.lba_optimize(*P[:6], stop_after=T)
+        res = r["result"]
+        assert res["stopped"] == 2 and res["trials"] == T, (T, res)
+        its = int(res["iterations"].sum())
+        assert its_prev <= its <= int(full["result"]["iterations"].sum())
+        its_prev = its
+        pass2_seen |= res["iterations"][1] > 0
+        again = oracle_lba.lba_optimize(*P[:6], stop_after=T)
+        assert np.array_equal(again["points"], r["points"])
+    assert pass2_seen
