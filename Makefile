@@ -28,11 +28,27 @@ $(OBJDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 $(PKG)/libspslam_gpu.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(OBJS)
 
+# Diagnostic build: PoseOptimization phase timers (tools/pose_phases.py loads it via SPSLAM_GPU_LIB).
+PROFDIR := build/prof
+PROF_OBJS := $(addprefix $(PROFDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+prof: $(PKG)/libspslam_gpu_prof.so
+
+$(PROFDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
+	@mkdir -p $(PROFDIR)
+	$(HIPCC) $(HIPFLAGS) -DSPSLAM_POSE_PROF -c -o $@ $<
+
+$(PROFDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
+	@mkdir -p $(PROFDIR)
+	$(HIPCC) $(HIPFLAGS) -DSPSLAM_POSE_PROF -c -x hip -o $@ $<
+
+$(PKG)/libspslam_gpu_prof.so: $(PROF_OBJS)
+	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(PROF_OBJS)
+
 oracle/liboracle.so:
 	$(MAKE) -C oracle liboracle.so
 
 clean:
-	rm -rf $(PKG)/libspslam_gpu.so $(OBJDIR)
+	rm -rf $(PKG)/libspslam_gpu.so $(PKG)/libspslam_gpu_prof.so $(OBJDIR) $(PROFDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle/liboracle.so
+.PHONY: all clean prof oracle/liboracle.so

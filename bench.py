@@ -291,27 +291,44 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         import oracle_sequence
         import oracle_step
         cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
-        orb, po = oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures), oracle_planes.PlaneOracle()
         out = {"kind": "tracked sequences (motion model from the previous frame; sp-slam_amd/sequence.py)",
-               "sequences": n_seq, "frames": n_frames, "vs_cpu_ref_m": [], "max_center_diff_vs_cpu_ref_m": [],
+               "sequences": n_seq, "frames": n_frames,
+               "cpu_ref": "CPU oracle with PoseOptimization summed in the kernel's order (oracle/pose_oracle.cpp "
+                          "device-order mode); g2o_order_cpu_ref: the same loop with g2o's edge-order sums",
+               "vs_cpu_ref_m": [], "max_center_diff_vs_cpu_ref_m": [],
                "max_rotation_diff_vs_cpu_ref": [], "vs_ground_truth_m": [], "cpu_ref_vs_ground_truth_m": [],
-               "ate_difference_vs_cpu_ref_m": [], "identical_decisions_until_frame": []}
+               "ate_difference_vs_cpu_ref_m": [], "identical_decisions_until_frame": [],
+               "g2o_order_cpu_ref": {"vs_gpu_m": [], "vs_device_order_cpu_ref_m": [], "vs_ground_truth_m": [],
+                                     "identical_decisions_until_frame": []}}
         t1 = time.perf_counter()
-        for slot in range(n_seq):
+
+        def run_oracle(slot, order):
             frames, T0, P0, local_of = sp.oracle_inputs(slot)
             ch = {}
 
             def rec(t, o, P):
                 ch[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
                          int(o["pose2"][0]["n_inliers"]))
+            orb, po = oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures), oracle_planes.PlaneOracle()
             cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                        on_frame=rec)
+                                        on_frame=rec, pose_order=order)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
-            out["identical_decisions_until_frame"].append(next((t for t, ok in enumerate(same, 1) if not ok), None))
+            return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
+
+        from concurrent.futures import ThreadPoolExecutor
+        jobs = [(slot, order) for slot in range(n_seq)
+                for order in (oracle_ctypes.POSE_ORDER_DEVICE, oracle_ctypes.POSE_ORDER_G2O)]
+        with ThreadPoolExecutor(len(jobs)) as pool:
+            done = dict(zip(jobs, pool.map(lambda j: run_oracle(*j), jobs)))
+        for slot in range(n_seq):
+            cpu, div = done[(slot, oracle_ctypes.POSE_ORDER_DEVICE)]
+            cpu_g, div_g = done[(slot, oracle_ctypes.POSE_ORDER_G2O)]
+            out["identical_decisions_until_frame"].append(div)
             g = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n_frames)]
             c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n_frames)]
+            cg = [trajectory.camera_center(cpu_g[k].reshape(16)) for k in range(n_frames)]
             gt = [np.linalg.inv(sp._true_pose(slot, k + 1))[:3, 3] for k in range(n_frames)]
             out["vs_cpu_ref_m"].append(trajectory.ate_rmse(g, c))
             out["max_center_diff_vs_cpu_ref_m"].append(float(np.linalg.norm(np.array(g) - np.array(c), axis=1).max()))
@@ -320,7 +337,12 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             out["vs_ground_truth_m"].append(trajectory.ate_rmse(g, gt))
             out["cpu_ref_vs_ground_truth_m"].append(trajectory.ate_rmse(c, gt))
             out["ate_difference_vs_cpu_ref_m"].append(abs(out["vs_ground_truth_m"][-1] - out["cpu_ref_vs_ground_truth_m"][-1]))
-        out["cpu_frames_per_s"] = n_seq * n_frames / (time.perf_counter() - t1)
+            go = out["g2o_order_cpu_ref"]
+            go["vs_gpu_m"].append(trajectory.ate_rmse(g, cg))
+            go["vs_device_order_cpu_ref_m"].append(trajectory.ate_rmse(c, cg))
+            go["vs_ground_truth_m"].append(trajectory.ate_rmse(cg, gt))
+            go["identical_decisions_until_frame"].append(div_g)
+        out["cpu_frames_per_s"] = len(jobs) * n_frames / (time.perf_counter() - t1)  # len(jobs) threads
         out["wall_s"] = {"gpu_incl_render": t_gpu, "cpu": time.perf_counter() - t1}
         return out
     finally:

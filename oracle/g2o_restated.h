@@ -13,8 +13,22 @@
 #include <cmath>
 #include <cstring>
 
+#include "../sp-slam_amd/csrc/libm64_restated.h"
+
 namespace oracle {
 namespace g2o_math {
+
+// Elementary functions: glibc (what the reference calls) by default; the device-order mode of
+// pose_oracle.cpp switches this thread to the restatement the GPU kernels run (libm64_restated.h:
+// fdlibm sin / cos / atan2 within 1 ulp of glibc, a correctly rounded cube).
+inline bool& device_math() {
+    static thread_local bool on = false;
+    return on;
+}
+inline double o_sin(double x) { return device_math() ? spslam::libm64::sin_(x) : std::sin(x); }
+inline double o_cos(double x) { return device_math() ? spslam::libm64::cos_(x) : std::cos(x); }
+inline double o_atan2(double y, double x) { return device_math() ? spslam::libm64::atan2_(y, x) : std::atan2(y, x); }
+inline double o_cube(double x) { return device_math() ? spslam::libm64::cube_(x) : std::pow(x, 3); }
 
 struct V3 { double x, y, z; };
 inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
@@ -123,8 +137,8 @@ struct SE3 {
             V = R;
         } else {
             M3 O2 = mul(O, O);
-            double a = std::sin(theta) / theta, b = (1 - std::cos(theta)) / (theta * theta),
-                   c = (theta - std::sin(theta)) / std::pow(theta, 3);
+            double a = o_sin(theta) / theta, b = (1 - o_cos(theta)) / (theta * theta),
+                   c = (theta - o_sin(theta)) / o_cube(theta);
             for (int i = 0; i < 3; i++)
                 for (int j = 0; j < 3; j++) {
                     R.m[i][j] = (i == j ? 1.0 : 0.0) + a * O.m[i][j] + b * O2.m[i][j];
@@ -152,15 +166,15 @@ struct Plane {
     }
     static Plane from(const double* v) { Plane p; std::memcpy(p.c, v, sizeof p.c); normalize(p.c); return p; }
 };
-inline double azimuth(V3 v) { return std::atan2(v.y, v.x); }
-inline double elevation(V3 v) { return std::atan2(v.z, std::sqrt(v.x * v.x + v.y * v.y)); }
+inline double azimuth(V3 v) { return o_atan2(v.y, v.x); }
+inline double elevation(V3 v) { return o_atan2(v.z, std::sqrt(v.x * v.x + v.y * v.y)); }
 inline Quat aa_quat(double angle, V3 axis) {  // Eigen Quaternion(AngleAxis)
-    double ha = 0.5 * angle, s = std::sin(ha);
-    return {std::cos(ha), s * axis.x, s * axis.y, s * axis.z};
+    double ha = 0.5 * angle, s = o_sin(ha);
+    return {o_cos(ha), s * axis.x, s * axis.y, s * axis.z};
 }
 inline M3 aa_rot(double angle, V3 a) {  // Eigen AngleAxis::toRotationMatrix
-    V3 sa = std::sin(angle) * a;
-    double c = std::cos(angle);
+    V3 sa = o_sin(angle) * a;
+    double c = o_cos(angle);
     V3 c1 = (1 - c) * a;
     M3 r;
     double tmp;
@@ -219,8 +233,8 @@ struct Huber {
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85): azimuth/elevation/distance update.
 inline void plane_oplus(Plane& p, const double* v) {
     const double az = v[0], el = v[1];
-    const double s = std::sin(el), c = std::cos(el);
-    const V3 n{c * std::cos(az), c * std::sin(az), s};
+    const double s = o_sin(el), c = o_cos(el);
+    const V3 n{c * o_cos(az), c * o_sin(az), s};
     const M3 R = plane_rotation(p.normal());
     const double d = p.distance() + v[2];
     const V3 rn = mul(R, n);

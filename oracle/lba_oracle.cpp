@@ -447,7 +447,7 @@ struct Opt {
                 scale += 1e-3;
                 rho /= scale;
                 if (rho > 0 && std::isfinite(tempChi)) {
-                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    double alpha = 1. - o_cube(2 * rho - 1);
                     alpha = std::min(alpha, 2. / 3.);
                     lambda *= std::max(1. / 3., alpha);
                     ni = 2;

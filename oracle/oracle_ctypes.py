@@ -7,6 +7,7 @@ Parity status: unpinned against the reference binary -- see orb_oracle.h.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import pathlib
 
@@ -167,6 +168,25 @@ def descriptor(img: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
     out = np.zeros(32, np.uint8)
     lib().oracle_descriptor(img.ctypes.data, img.shape[1], img.shape[0], x, y, angle, out.ctypes.data)
     return out
+
+
+POSE_ORDER_G2O, POSE_ORDER_DEVICE = 0, 1
+
+
+@contextlib.contextmanager
+def pose_order(mode: int):
+    """Summation order of the pose oracle inside the block, for the calling thread (oracle/pose_oracle.cpp):
+    POSE_ORDER_G2O (default, g2o's edge order + glibc) or POSE_ORDER_DEVICE (the GPU kernel's tree order +
+    libm64_restated.h)."""
+    L = lib()
+    L.oracle_get_pose_order.restype = ctypes.c_int
+    L.oracle_set_pose_order.argtypes = [ctypes.c_int]
+    prev = L.oracle_get_pose_order()
+    L.oracle_set_pose_order(int(mode))
+    try:
+        yield
+    finally:
+        L.oracle_set_pose_order(prev)
 
 
 def pose_optimize(problem, points, planes, cfg=None):

@@ -3,8 +3,12 @@
 // (lba_kernels.hip) kernels: SE3Quat (Thirdparty/g2o/g2o/types/se3quat.h),
 // Eigen quaternion / rotation conversions, g2oAddition/Plane3D.h.
 // See oracle/g2o_restated.h for the CPU restatement of the same routines.
+// sin / cos / atan2 / pow(x, 3) come from libm64_restated.h (the same code the
+// oracle's device-order mode runs on the host), not ocml.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include "libm64_restated.h"
 
 namespace spslam {
 namespace g2od {
@@ -110,9 +114,8 @@ __device__ __forceinline__ SE3 se3_exp(const double* u) {
         V = R;
     } else {
         double st, ct;
-        sincos(theta, &st, &ct);
-        // pow(theta, 3) as two products: within an ulp of glibc's pow, far cheaper than ocml's
-        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / (theta * theta * theta);
+        libm64::sincos_(theta, &st, &ct);
+        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / libm64::cube_(theta);
         for (int k = 0; k < 9; k++) {
             R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
             V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
@@ -133,19 +136,23 @@ __device__ __forceinline__ void p_normalize(double* v) {
     if (v[3] < 0.0)
         for (int i = 0; i < 4; i++) v[i] = -v[i];
 }
-__device__ __forceinline__ double azimuth(V3 v) { return atan2(v.y, v.x); }
-__device__ __forceinline__ double elevation(V3 v) { return atan2(v.z, sqrt(v.x * v.x + v.y * v.y)); }
+__device__ __forceinline__ double azimuth(V3 v) { return libm64::atan2_(v.y, v.x); }
+__device__ __forceinline__ double elevation(V3 v) { return libm64::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
 // Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
 __device__ __forceinline__ M3 p_rotation(V3 v) {
     const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
-    const Q a{cos(ha), 0.0 * sin(ha), 0.0 * sin(ha), 1.0 * sin(ha)};
-    const Q e{cos(he), 0.0 * sin(he), 1.0 * sin(he), 0.0 * sin(he)};
+    double sa, ca, se, ce;
+    libm64::sincos_(ha, &sa, &ca);
+    libm64::sincos_(he, &se, &ce);
+    const Q a{ca, 0.0 * sa, 0.0 * sa, 1.0 * sa};
+    const Q e{ce, 0.0 * se, 1.0 * se, 0.0 * se};
     return q_to_rot(q_mul(a, e));
 }
 // Eigen AngleAxis::toRotationMatrix() * v
 __device__ __forceinline__ V3 aa_apply(double ang, V3 ax, V3 v) {
-    const V3 sa = sin(ang) * ax;
-    const double c = cos(ang);
+    double s, c;
+    libm64::sincos_(ang, &s, &c);
+    const V3 sa = s * ax;
     const V3 c1 = (1 - c) * ax;
     M3 r;
     double tmp;
@@ -188,8 +195,10 @@ __device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& wor
 
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)
 __device__ void p_oplus(P4& p, const double* v) {
-    const double s = sin(v[1]), c = cos(v[1]);
-    const V3 n{c * cos(v[0]), c * sin(v[0]), s};
+    double s, c, s0, c0;
+    libm64::sincos_(v[1], &s, &c);
+    libm64::sincos_(v[0], &s0, &c0);
+    const V3 n{c * c0, c * s0, s};
     const M3 R = p_rotation(V3{p.c[0], p.c[1], p.c[2]});
     const double d = -p.c[3] + v[2];
     const V3 rn = mv(R, n);

@@ -951,7 +951,7 @@ __global__ void k_decide(LbaBatch b, int step) {
     }
     double rho = (k.currentChi - tempChi) / (scale + 1e-3);
     if (rho > 0 && isfinite(tempChi)) {
-        double alpha = 1. - pow((2 * rho - 1), 3);
+        double alpha = 1. - libm64::cube_(2 * rho - 1);
         alpha = fmin(alpha, 2. / 3.);
         k.lambda *= fmax(1. / 3., alpha);
         k.ni = 2;

@@ -5,15 +5,19 @@
 // iterations (x <= 10 trials) with no host round trip.  Per LM iteration:
 //   pass A  (all threads)  per-edge error, Huber weight and Jacobian, local
 //                          sums of robust chi2, J^T W J (21 terms), J^T W e (6)
-//   reduce                 wave shuffles + LDS, fp64
-//   solve   (thread 0)     (H + lambda I) x = b by LDLT with diagonal pivoting
+//   wg_sum                 wave butterflies + LDS, fp64; every thread gets the totals
+//   solve   (lane q % K)   (H + lambda_q I) x = b by LDLT with diagonal pivoting
 //                          (Eigen::LDLT, solvers/linear_solver_dense.h:103-110)
-//   pass B  (all threads)  robust chi2 at exp(x) * T, accept/reject, lambda
+//                          for K damping trials at once, poses by readlane
+//   pass B  (all threads)  robust chi2 at exp(x_q) * T for the K trials, then
+//                          the reference's accept/reject walk, redundantly
 // Outlier relabeling after each round reproduces the reference's use of the
 // errors cached by the LAST computeActiveErrors (which may belong to a
 // rejected trial): those errors are recomputed at that trial pose.
-// All arithmetic is fp64 like g2o/Eigen; reductions are tree-ordered, so the
-// result matches the reference to rounding, not bitwise.
+// All arithmetic is fp64 like g2o/Eigen.  Sums run in one fixed tree order
+// (wg_sum) and sin / cos / atan2 / pow(x, 3) come from libm64_restated.h: the
+// oracle's device-order mode restates both and matches this kernel bit for
+// bit; against g2o's sequential edge order the result agrees to rounding.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -23,6 +27,24 @@
 #include "../../include/spslam_gpu.h"
 #include "g2o_device.h"
 #include "pose_launch.h"
+
+// Phase profile (diagnostic build only: make prof -> libspslam_gpu_prof.so).  Thread 0 of every problem
+// accumulates wall_clock64 ticks (100 MHz) per phase; spslam_pose_prof_read returns the grid totals.
+#ifdef SPSLAM_POSE_PROF
+__device__ unsigned long long g_pose_prof[16];
+#define PROF_MARK(k)                                   \
+    do {                                               \
+        if (t == 0) {                                  \
+            const unsigned long long now_ = wall_clock64(); \
+            prof_acc[k] += now_ - prof_t;              \
+            prof_t = now_;                             \
+        }                                              \
+    } while (0)
+#define PROF_COUNT(k) do { if (t == 0) prof_acc[k]++; } while (0)
+#else
+#define PROF_MARK(k) do {} while (0)
+#define PROF_COUNT(k) do {} while (0)
+#endif
 
 namespace spslam {
 namespace pose {
@@ -55,7 +77,7 @@ __device__ __forceinline__ bool ldlt_solve(const double (*H)[6], double lambda, 
 #pragma unroll
     for (int i = 0; i < n; i++)
 #pragma unroll
-        for (int j = 0; j < n; j++) m[i][j] = H[i][j] + (i == j ? lambda : 0.0);
+        for (int j = 0; j < n; j++) m[i][j] = i == j ? H[i][j] + lambda : H[i][j];
     int tr[n];
     int sign = 0;
 #pragma unroll
@@ -137,44 +159,45 @@ __device__ __forceinline__ bool ldlt_solve(const double (*H)[6], double lambda, 
 // Four waves per problem (measured: one wave per problem frees SIMDs for the
 // pipelined extraction but makes the edge passes 4x longer -- a net loss).
 constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
 constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
-constexpr int kPlaneChunk = 64;  // plane edges whose 12 perturbed errors are evaluated together
+constexpr int kPlaneChunk = 64;  // plane edges whose 13 errors (12 perturbed poses + T) are evaluated together
+constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
 
+template <int kSpec>
 struct Shared {
-    double red[kThreads / 64][kRed];
-    SE3 Eadd[12];                    // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
-    SE3 Tp[12];                      // exp(+-1e-9 e_d) * T for the current iterate
-    double perr[kPlaneChunk][13][3]; // plane errors at the 12 perturbed poses and at T
-    double H[6][6], b[6], x[6];
-    double lambda, ni, currentChi, iniChi, tempChi;
-    SE3 T, T0, Ttrial, Tlast;
-    int nBad, stop, active_any;
-    int count[kThreads / 64];
+    double red[2][kWaves][kRed];      // wave totals of the workgroup sums, double-buffered
+    double perr[kPlaneChunk][13][3];  // plane errors at the 12 perturbed poses and at T
+    double perrB[kPlaneChunk][kSpec][3];  // plane errors at the trial poses of the last pass B
+    double perrT[kPlaneChunk][3];     // plane errors at the accepted trial pose = the next iteration's T
+    SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
 };
 
-// Block reduction of NV doubles per thread (v[0..NV)) into S.red[0][0..NV).  The
-// NV butterfly chains are unrolled together so their shuffle latencies overlap.
-template <int NV>
-__device__ void block_reduce(double (&v)[NV], Shared& S) {
+// Workgroup sum of NV doubles per thread; every thread returns the same totals.  Fixed order (the oracle's
+// device-order mode restates it, oracle/pose_oracle.cpp): xor butterfly over the 64 lanes of each wave (all
+// lanes end with the wave total), then ((0 + w0) + w1) + w2) + w3 from LDS in every thread.  One barrier;
+// consecutive calls alternate the two LDS buffers, so a buffer is only rewritten after the next call's
+// barrier has seen every thread finish reading it.
+template <int NV, class Sh>
+__device__ __forceinline__ void wg_sum(double (&v)[NV], Sh& S, int& buf) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double x[NV];
-#pragma unroll
-    for (int k = 0; k < NV; k++) x[k] = v[k];
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1)
 #pragma unroll
-        for (int k = 0; k < NV; k++) x[k] += __shfl_xor(x[k], off);
+        for (int k = 0; k < NV; k++) v[k] += __shfl_xor(v[k], off);
     if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < NV; k++) S.red[w][k] = x[k];
+        for (int k = 0; k < NV; k++) S.red[buf][w][k] = v[k];
     }
     __syncthreads();
-    if (threadIdx.x < NV) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) {
         double s = 0;
-        for (int j = 0; j < kThreads / 64; j++) s += S.red[j][threadIdx.x];
-        S.red[0][threadIdx.x] = s;
+#pragma unroll
+        for (int j = 0; j < kWaves; j++) s += S.red[buf][j][k];
+        v[k] = s;
     }
-    __syncthreads();
+    buf ^= 1;
 }
 
 __device__ __forceinline__ void huber(double chi, double delta, bool on, double* rho0, double* rho1) {
@@ -185,23 +208,44 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
     *rho1 = delta / s;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ SE3 readlane_se3(const SE3& a, int l) {
+    SE3 r;
+    r.r.w = readlane_d(a.r.w, l); r.r.x = readlane_d(a.r.x, l);
+    r.r.y = readlane_d(a.r.y, l); r.r.z = readlane_d(a.r.z, l);
+    r.t.x = readlane_d(a.t.x, l); r.t.y = readlane_d(a.t.y, l); r.t.z = readlane_d(a.t.z, l);
+    return r;
+}
+
 }  // namespace pose
 
 using namespace pose;
 
-// kMinWaves: waves per SIMD the register allocation must leave room for (launch-bounds occupancy).  At 1 the
-// kernel takes 256 VGPRs + AGPRs, so a workgroup only starts on a CU whose four SIMDs are nearly empty --
-// inside the pipelined step that waits for the extraction kernels' waves to drain.
-template <int kMinWaves>
-__global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
-                                                   const spslam_point_obs* __restrict__ pts_all,
-                                                   const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
-                                                   const spslam_pose_result* __restrict__ init_from,
-                                                   spslam_pose_result* __restrict__ results,
-                                                   uint8_t* __restrict__ pout_all, uint8_t* __restrict__ plout_all) {
+// Every thread holds the whole LM state (pose, lambda, chi2 values, H, b): the workgroup sums hand every
+// thread the same totals and every decision is computed redundantly from them, so no thread waits on another
+// except inside wg_sum.  The damping trials of one LM iteration are evaluated kSpec at a time: after a
+// rejected trial the reference only multiplies lambda by ni and doubles ni (optimization_algorithm_levenberg
+// .cpp:145-160), so trial q's lambda is known in advance; lane q % kSpec of every wave solves trial q, the
+// trial poses are broadcast with readlane, one pass over the edges evaluates all kSpec robust chi2 sums, and
+// the accept / reject walk then replays the reference's sequence over them.  Results do not depend on kSpec.
+template <int kSpec>
+__global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+                                                         const spslam_point_obs* __restrict__ pts_all,
+                                                         const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
+                                                         const spslam_pose_result* __restrict__ init_from,
+                                                         spslam_pose_result* __restrict__ results,
+                                                         uint8_t* __restrict__ pout_all, uint8_t* __restrict__ plout_all) {
     tail_wave_priority();
-    __shared__ Shared S;
-    const int t = threadIdx.x;
+    __shared__ Shared<kSpec> S;
+    const int t = threadIdx.x, lane = t & 63;
+#ifdef SPSLAM_POSE_PROF
+    unsigned long long prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof_t = wall_clock64();
+#endif
     const spslam_pose_problem P = probs[blockIdx.x];
     const spslam_point_obs* pts = pts_all + P.point_offset;
     const spslam_plane_obs* pls = pls_all + P.plane_offset;
@@ -224,27 +268,27 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_
         add[t >> 1] = (t & 1) ? -1e-9 : 1e-9;
         S.Eadd[t] = se3_exp(add);
     }
-    if (t == 0) {
+    SE3 T0;  // Converter::toSE3Quat: Quaterniond(R) of the float pose, normalized (every thread)
+    {
         M3 R;
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) R.a[3 * i + j] = Tin[4 * i + j];
-        S.T0.r = q_from_rot(R);
-        S.T0.t = V3{Tin[3], Tin[7], Tin[11]};
-        q_normalize(S.T0.r);
+        T0.r = q_from_rot(R);
+        T0.t = V3{Tin[3], Tin[7], Tin[11]};
+        q_normalize(T0.r);
     }
     __syncthreads();
 
     // edge e < np: point e; else plane e - np.  Per-edge info/delta:
-    auto edge_info = [&](int e, double* info, double* delta, int* dim) __attribute__((always_inline)) {
+    auto edge_info = [&](int e, double* info, double* delta) __attribute__((always_inline)) {
         if (e < np) {
             const spslam_point_obs& o = pts[e];
             info[0] = info[1] = info[2] = (double)o.inv_sigma2;
-            *dim = o.ur < 0 ? 2 : 3;
             *delta = o.ur < 0 ? K.delta_mono : K.delta_stereo;
         } else {
             const int kind = pls[e - np].kind;
-            if (kind == 0) { info[0] = info[1] = K.angle_info; info[2] = K.dis_info; *delta = K.delta_plane; *dim = 3; }
-            else { info[0] = info[1] = kind == 1 ? K.par_info : K.ver_info; info[2] = 0; *delta = K.delta_vp; *dim = 2; }
+            if (kind == 0) { info[0] = info[1] = K.angle_info; info[2] = K.dis_info; *delta = K.delta_plane; }
+            else { info[0] = info[1] = kind == 1 ? K.par_info : K.ver_info; info[2] = 0; *delta = K.delta_vp; }
         }
     };
     auto plane_of = [&](int e, P4& w, P4& m) __attribute__((always_inline)) {
@@ -268,32 +312,36 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_
         }
         err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
     };
+    auto chi2_of = [](const double* err, const double* info) __attribute__((always_inline)) {
+        // rows beyond the edge's dimension hold a zero error: their +0 terms leave chi unchanged
+        return (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
+    };
     auto is_outlier = [&](int e) __attribute__((always_inline)) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
 
+    int buf = 0;
     bool robust = true;
     int nBad = 0, total_its = 0;
+    SE3 T = T0, Tlast = T0;
     for (int round = 0; round < 4; round++) {
-        if (t == 0) S.T = S.T0;
+        PROF_MARK(0);  // setup / previous relabel
+        T = T0;
         // any active edge?
         int act = 0;
         for (int e = t; e < ne; e += kThreads) act |= !is_outlier(e);
         act = __syncthreads_or(act);
         if (act) {
+            double lambda = 0, ni = 2;
+            int lmBad = 0;
+            bool tValid = false;  // perrT holds the plane errors at T (set when a trial is accepted)
             for (int it = 0; it < 10; it++) {
                 // ---- pass A: errors, robust chi2, quadratic form at T
                 double v[kRed];
 #pragma unroll
                 for (int k = 0; k < kRed; k++) v[k] = 0;
-                const SE3 T = S.T;
                 // accumulate one edge's robust chi2, J^T W J and -J^T W e
-                auto accumulate = [&](const double (&J)[3][6], const double* err, const double* info, int dim,
-                                      double delta) {
-                    // rows beyond dim carry zero error and Jacobian: their terms add exact zeros
-                    (void)dim;
-                    double chi = 0;
-                    chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
+                auto accumulate = [&](const double (&J)[3][6], const double* err, const double* info, double delta) {
                     double rho0, rho1;
-                    huber(chi, delta, robust, &rho0, &rho1);
+                    huber(chi2_of(err, info), delta, robust, &rho0, &rho1);
                     v[0] += rho0;
 #pragma unroll
                     for (int i = 0; i < 6; i++)
@@ -315,8 +363,7 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_
                 for (int e = t; e < np; e += kThreads) {
                     if (pout[e]) continue;
                     double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
-                    int dim;
-                    edge_info(e, info, &delta, &dim);
+                    edge_info(e, info, &delta);
                     V3 pc;
                     error_at(e, T, err, &pc);
                     const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
@@ -326,191 +373,253 @@ __global__ __launch_bounds__(kThreads, kMinWaves) void pose_kernel(const spslam_
                     J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
                     J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
                     J[1][5] = y * invz_2 * cam.fy;
-                    if (dim == 3) {
+                    if (pts[e].ur >= 0) {
                         J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
                         J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
                     } else {
 #pragma unroll
                         for (int d = 0; d < 6; d++) J[2][d] = 0;
                     }
-                    accumulate(J, err, info, dim, delta);
+                    accumulate(J, err, info, delta);
                 }
-                // plane edges: numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205);
-                // the 12 perturbed evaluations of each edge run on 12 threads
-                if (nl > 0) {
-                    if (t < 12) S.Tp[t] = se3_mul(S.Eadd[t], T);
-                    __syncthreads();
-                    for (int base = 0; base < nl; base += kPlaneChunk) {
-                        const int cnt = min(kPlaneChunk, nl - base);
-                        // 13 evaluations per edge in parallel: the 12 perturbed poses and T itself (the
-                        // error the edge's own accumulation needs -- no second serial evaluation after the sync)
-                        for (int w = t; w < cnt * 13; w += kThreads) {
-                            const int j = w / 13, q = w - j * 13, e = np + base + j;
-                            double err[3] = {0, 0, 0};
-                            if (!plout[e - np]) {
-                                const SE3& P = S.Tp[q < 12 ? q : 0];
-                                const bool pt = q < 12;
-                                SE3 Tq;  // field-wise select keeps both poses in registers
-                                Tq.r.w = pt ? P.r.w : T.r.w; Tq.r.x = pt ? P.r.x : T.r.x;
-                                Tq.r.y = pt ? P.r.y : T.r.y; Tq.r.z = pt ? P.r.z : T.r.z;
-                                Tq.t.x = pt ? P.t.x : T.t.x; Tq.t.y = pt ? P.t.y : T.t.y; Tq.t.z = pt ? P.t.z : T.t.z;
-                                error_at(e, Tq, err, nullptr);
-                            }
-                            S.perr[j][q][0] = err[0]; S.perr[j][q][1] = err[1]; S.perr[j][q][2] = err[2];
+                PROF_MARK(1);  // pass A point edges
+                // plane edges: numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205); the 13
+                // evaluations of a chunk's edges (12 perturbed poses exp(+-1e-9 e_d) * T, and T) run on
+                // 13 x chunk threads, then thread j accumulates the chunk's edge j
+                // after an accepted trial the errors at T are the ones pass B evaluated at that trial pose
+                // (kept in perrT when the plane edges fit one chunk): 12 evaluations per edge instead of 13
+                const bool haveT = tValid && nl <= kPlaneChunk;
+                const int nev = haveT ? 12 : 13;
+                for (int base = 0; base < nl; base += kPlaneChunk) {
+                    const int cnt = min(kPlaneChunk, nl - base);
+                    for (int w = t; w < cnt * nev; w += kThreads) {
+                        const int j = w / nev, q = w - j * nev, e = np + base + j;
+                        double err[3] = {0, 0, 0};
+                        if (!plout[e - np]) {
+                            const SE3 Tp = se3_mul(S.Eadd[q < 12 ? q : 0], T);
+                            const bool pt = q < 12;
+                            SE3 Tq;  // field-wise select: one inlined error evaluation for both cases
+                            Tq.r.w = pt ? Tp.r.w : T.r.w; Tq.r.x = pt ? Tp.r.x : T.r.x;
+                            Tq.r.y = pt ? Tp.r.y : T.r.y; Tq.r.z = pt ? Tp.r.z : T.r.z;
+                            Tq.t.x = pt ? Tp.t.x : T.t.x; Tq.t.y = pt ? Tp.t.y : T.t.y; Tq.t.z = pt ? Tp.t.z : T.t.z;
+                            error_at(e, Tq, err, nullptr);
                         }
-                        __syncthreads();
-                        for (int j = t; j < cnt; j += kThreads) {
-                            const int e = np + base + j;
-                            if (plout[e - np]) continue;
+                        S.perr[j][q][0] = err[0]; S.perr[j][q][1] = err[1]; S.perr[j][q][2] = err[2];
+                    }
+                    __syncthreads();
+                    if (t < cnt) {
+                        const int e = np + base + t;
+                        if (!plout[e - np]) {
                             double info[3], delta, J[3][6];
-                            int dim;
-                            edge_info(e, info, &delta, &dim);
-                            const double err[3] = {S.perr[j][12][0], S.perr[j][12][1], S.perr[j][12][2]};
+                            edge_info(e, info, &delta);
+                            const double err[3] = {haveT ? S.perrT[t][0] : S.perr[t][12][0],
+                                                   haveT ? S.perrT[t][1] : S.perr[t][12][1],
+                                                   haveT ? S.perrT[t][2] : S.perr[t][12][2]};
                             const double scalar = 1.0 / (2 * 1e-9);
 #pragma unroll
                             for (int d = 0; d < 6; d++)
 #pragma unroll
                                 for (int r = 0; r < 3; r++)
-                                    J[r][d] = scalar * (S.perr[j][2 * d][r] - S.perr[j][2 * d + 1][r]);
-                            accumulate(J, err, info, dim, delta);
+                                    J[r][d] = scalar * (S.perr[t][2 * d][r] - S.perr[t][2 * d + 1][r]);
+                            accumulate(J, err, info, delta);
                         }
-                        __syncthreads();
                     }
+                    if (base + kPlaneChunk < nl) __syncthreads();  // perr reuse (the last chunk: wg_sum's barrier)
                 }
-                block_reduce(v, S);
-                if (t == 0) {
-                    S.Tlast = S.T;
-                    S.currentChi = S.red[0][0];
-                    S.iniChi = S.currentChi;
+                PROF_MARK(2);  // pass A plane edges
+                wg_sum(v, S, buf);
+                Tlast = T;
+                double currentChi = v[0];
+                const double iniChi = currentChi;
+                double H[6][6], b[6];
+                {
                     int k = 1;
+#pragma unroll
                     for (int i = 0; i < 6; i++)
-                        for (int j = i; j < 6; j++, k++) S.H[i][j] = S.H[j][i] = S.red[0][k];
-                    for (int i = 0; i < 6; i++) S.b[i] = S.red[0][22 + i];
-                    if (it == 0) {
-                        double md = 0;
-                        for (int j = 0; j < 6; j++) md = fmax(fabs(S.H[j][j]), md);
-                        S.lambda = 1e-5 * md;
-                        S.ni = 2;
-                        S.nBad = 0;
-                    }
-                    for (int j = 0; j < 6; j++) S.x[j] = 0;
+#pragma unroll
+                        for (int j = i; j < 6; j++, k++) H[i][j] = H[j][i] = v[k];
+#pragma unroll
+                    for (int i = 0; i < 6; i++) b[i] = v[22 + i];
                 }
-                __syncthreads();
-                // ---- trials
+                if (it == 0) {
+                    double md = 0;
+#pragma unroll
+                    for (int j = 0; j < 6; j++) md = fmax(fabs(H[j][j]), md);
+                    lambda = 1e-5 * md;
+                    ni = 2;
+                    lmBad = 0;
+                }
+                PROF_MARK(3);  // reduce A + iteration setup
+                // ---- damping trials, kSpec per pass over the edges
                 double rho = 0;
                 int qmax = 0;
-                bool ok2 = true;
-                do {
-                    if (t == 0) {
-                        double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten
-                        S.stop = ldlt_solve(S.H, S.lambda, S.b, x) ? 1 : 0;
-                        for (int j = 0; j < 6; j++) S.x[j] = x[j];
-                        S.Ttrial = se3_mul(se3_exp(x), S.T);
+                bool more = true;
+                while (more) {
+                    // trial q's damping if trials 0..q-1 are rejected: lambda_{q+1} = lambda_q * ni_q, ni *= 2
+                    double lam = lambda, nq = ni;
+                    const int myq = lane % kSpec;
+                    for (int q = 0; q < myq; q++) { lam *= nq; nq *= 2; }
+                    double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten (rejected step)
+                    const bool ok = ldlt_solve(H, lam, b, x);
+                    const SE3 Tt = se3_mul(se3_exp(x), T);
+                    double scale = 0;  // OptimizationAlgorithmLevenberg::computeScale + 1e-3
+#pragma unroll
+                    for (int j = 0; j < 6; j++) scale += x[j] * (lam * x[j] + b[j]);
+                    scale += 1e-3;
+                    SE3 Tq[kSpec];
+                    double sc[kSpec];
+                    bool okq[kSpec];
+#pragma unroll
+                    for (int q = 0; q < kSpec; q++) {
+                        Tq[q] = readlane_se3(Tt, q);
+                        sc[q] = readlane_d(scale, q);
+                        okq[q] = __builtin_amdgcn_readlane((int)ok, q) != 0;
                     }
-                    __syncthreads();
-                    ok2 = S.stop != 0;
-                    const SE3 Tt = S.Ttrial;
-                    double c[1] = {0};
-                    for (int e = t; e < ne; e += kThreads) {
-                        if (is_outlier(e)) continue;
-                        double info[3], delta, err[3] = {0, 0, 0};
-                        int dim;
-                        edge_info(e, info, &delta, &dim);
-                        error_at(e, Tt, err, nullptr);
-                        double chi = 0;
-                        // rows beyond dim hold a zero error: their +0 terms leave chi unchanged
-                        chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
-                        double rho0, rho1;
-                        huber(chi, delta, robust, &rho0, &rho1);
-                        c[0] += rho0;
-                    }
-                    block_reduce(c, S);
-                    if (t == 0) {
-                        S.Tlast = S.Ttrial;
-                        double tempChi = S.red[0][0];
-                        if (!ok2) tempChi = 1.7976931348623157e308;
-                        double r = S.currentChi - tempChi;
-                        double scale = 0;
-                        for (int j = 0; j < 6; j++) scale += S.x[j] * (S.lambda * S.x[j] + S.b[j]);
-                        scale += 1e-3;
-                        r /= scale;
-                        if (r > 0 && isfinite(tempChi)) {
-                            const double r21 = 2 * r - 1;  // pow(2r - 1, 3) as two products (an ocml pow is ~200 serial fp64 ops)
-                            double alpha = 1. - r21 * r21 * r21;
-                            alpha = fmin(alpha, 2. / 3.);
-                            S.lambda *= fmax(1. / 3., alpha);
-                            S.ni = 2;
-                            S.currentChi = tempChi;
-                            S.T = S.Ttrial;
-                        } else {
-                            S.lambda *= S.ni;
-                            S.ni *= 2;
+                    PROF_MARK(4);  // solves + exp + broadcast
+                    PROF_COUNT(10);
+                    // robust chi2 of every active edge at each trial pose.  Thread t sums the edges e = t
+                    // (mod 256) of the combined index (points, then planes) in order.  A plane error costs far
+                    // more than a point error, so the (plane edge, trial) pairs are evaluated one per thread
+                    // first and handed to their owners through LDS (reusing perr).
+                    double c[kSpec];
+#pragma unroll
+                    for (int q = 0; q < kSpec; q++) c[q] = 0;
+                    for (int e = t; e < np; e += kThreads) {
+                        if (pout[e]) continue;
+                        double info[3], delta;
+                        edge_info(e, info, &delta);
+#pragma unroll
+                        for (int q = 0; q < kSpec; q++) {
+                            double err[3] = {0, 0, 0}, rho0, rho1;
+                            error_at(e, Tq[q], err, nullptr);
+                            huber(chi2_of(err, info), delta, robust, &rho0, &rho1);
+                            c[q] += rho0;
                         }
-                        S.tempChi = r;  // broadcast rho
                     }
-                    __syncthreads();
-                    rho = S.tempChi;
-                    qmax++;
-                } while (rho < 0 && qmax < 10);
-                total_its++;
-                if (qmax == 10 || rho == 0) break;
-                int stop = 0;
-                if (t == 0) {
-                    if ((S.iniChi - S.currentChi) * 1e3 < S.iniChi) S.nBad++;
-                    else S.nBad = 0;
-                    S.stop = S.nBad >= 3;
+                    double* prho = &S.perr[0][0][0];
+                    static_assert(kPlaneChunk * kSpec <= kPlaneChunk * 13 * 3, "one LDS round when perrB is kept");
+                    constexpr int kPairs = kPlaneChunk * 13 * 3;  // pairs per LDS round
+                    for (int base = 0; base < nl * kSpec; base += kPairs) {
+                        const int cnt = min(kPairs, nl * kSpec - base);
+                        for (int w = t; w < cnt; w += kThreads) {
+                            const int pr = base + w, j = pr / kSpec, q = pr - j * kSpec;
+                            double r0 = 0;
+                            if (!plout[j]) {
+                                double info[3], delta, err[3] = {0, 0, 0}, rho1;
+                                edge_info(np + j, info, &delta);
+                                SE3 Tv = Tq[0];  // uniform poses: select by q without dynamic indexing
+#pragma unroll
+                                for (int k = 1; k < kSpec; k++)
+                                    if (q == k) Tv = Tq[k];
+                                error_at(np + j, Tv, err, nullptr);
+                                huber(chi2_of(err, info), delta, robust, &r0, &rho1);
+                                if (nl <= kPlaneChunk) {
+                                    S.perrB[j][q][0] = err[0]; S.perrB[j][q][1] = err[1]; S.perrB[j][q][2] = err[2];
+                                }
+                            }
+                            prho[w] = r0;
+                        }
+                        __syncthreads();
+                        // owner of plane edge j: thread (np + j) % 256, in increasing j
+                        for (int j = ((t - np) % kThreads + kThreads) % kThreads; j < nl; j += kThreads) {
+                            if (j * kSpec < base || j * kSpec >= base + cnt || plout[j]) continue;
+#pragma unroll
+                            for (int q = 0; q < kSpec; q++) c[q] += prho[j * kSpec + q - base];
+                        }
+                        if (base + kPairs < nl * kSpec) __syncthreads();  // prho reuse (last round: wg_sum's)
+                    }
+                    PROF_MARK(5);  // pass B (trial chi2)
+                    wg_sum(c, S, buf);
+                    // the reference's accept / reject sequence over the evaluated trials
+                    int acc = -1;
+#pragma unroll
+                    for (int q = 0; q < kSpec; q++) {
+                        if (more) {
+                            Tlast = Tq[q];  // the last computeActiveErrors
+                            const double tempChi = okq[q] ? c[q] : 1.7976931348623157e308;
+                            double r = currentChi - tempChi;
+                            r /= sc[q];
+                            if (r > 0 && isfinite(tempChi)) {
+                                double alpha = 1. - libm64::cube_(2 * r - 1);
+                                alpha = fmin(alpha, 2. / 3.);
+                                lambda *= fmax(1. / 3., alpha);
+                                ni = 2;
+                                currentChi = tempChi;
+                                T = Tq[q];
+                                acc = q;
+                            } else {
+                                lambda *= ni;
+                                ni *= 2;
+                            }
+                            rho = r;
+                            qmax++;
+                            more = rho < 0 && qmax < kMaxTrials;
+                        }
+                    }
+                    tValid = tValid || acc >= 0;
+                    if (acc >= 0 && t < nl && nl <= kPlaneChunk) {  // thread t reads perrT[t] in the next pass A
+#pragma unroll
+                        for (int q = 0; q < kSpec; q++)
+                            if (q == acc) {
+                                S.perrT[t][0] = S.perrB[t][q][0];
+                                S.perrT[t][1] = S.perrB[t][q][1];
+                                S.perrT[t][2] = S.perrB[t][q][2];
+                            }
+                    }
+                    PROF_MARK(6);  // reduce B + decide
                 }
-                __syncthreads();
-                stop = S.stop;
-                __syncthreads();
-                if (stop) break;
+                total_its++;
+                if (qmax == kMaxTrials || rho == 0) break;
+                if ((iniChi - currentChi) * 1e3 < iniChi) lmBad++;
+                else lmBad = 0;
+                PROF_MARK(7);  // stop test
+                PROF_COUNT(11);
+                if (lmBad >= 3) break;
             }
         }
-        // ---- relabel (:925-1140)
-        const SE3 T = S.T, Tl = S.Tlast;
-        int bad = 0;
+        // ---- relabel (:925-1140): active edges keep the errors of the last trial pose, outliers are
+        // recomputed at the optimized pose
+        double bad = 0;
         for (int e = t; e < ne; e += kThreads) {
             double info[3], delta, err[3] = {0, 0, 0};
-            int dim;
-            edge_info(e, info, &delta, &dim);
+            edge_info(e, info, &delta);
             const bool was_out = is_outlier(e);
             SE3 Te;  // field-wise select (a selected reference would put both poses in scratch memory)
-            Te.r.w = was_out ? T.r.w : Tl.r.w; Te.r.x = was_out ? T.r.x : Tl.r.x;
-            Te.r.y = was_out ? T.r.y : Tl.r.y; Te.r.z = was_out ? T.r.z : Tl.r.z;
-            Te.t.x = was_out ? T.t.x : Tl.t.x; Te.t.y = was_out ? T.t.y : Tl.t.y; Te.t.z = was_out ? T.t.z : Tl.t.z;
+            Te.r.w = was_out ? T.r.w : Tlast.r.w; Te.r.x = was_out ? T.r.x : Tlast.r.x;
+            Te.r.y = was_out ? T.r.y : Tlast.r.y; Te.r.z = was_out ? T.r.z : Tlast.r.z;
+            Te.t.x = was_out ? T.t.x : Tlast.t.x; Te.t.y = was_out ? T.t.y : Tlast.t.y; Te.t.z = was_out ? T.t.z : Tlast.t.z;
             error_at(e, Te, err, nullptr);
-            double chi = 0;
-            // rows beyond dim hold a zero error: their +0 terms leave chi unchanged
-                        chi = (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
-            const float chi2 = (float)chi;
-            bool b;
-            if (e < np) b = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
-            else b = pls[e - np].kind == 0 ? (double)chi2 > K.plane_chi : (double)chi2 > K.vp_chi;
-            bad += b;
-            if (e < np) pout[e] = b;
-            else plout[e - np] = b;
+            const float chi2 = (float)chi2_of(err, info);
+            bool bd;
+            if (e < np) bd = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
+            else bd = pls[e - np].kind == 0 ? (double)chi2 > K.plane_chi : (double)chi2 > K.vp_chi;
+            bad += bd ? 1.0 : 0.0;
+            if (e < np) pout[e] = bd;
+            else plout[e - np] = bd;
         }
-        // wave-sum then LDS
-        for (int off = 32; off >= 1; off >>= 1) bad += __shfl_xor(bad, off);
-        if ((t & 63) == 0) S.count[t >> 6] = bad;
-        __syncthreads();
-        nBad = 0;
-#pragma unroll
-        for (int w = 0; w < kThreads / 64; w++) nBad += S.count[w];
-        __syncthreads();
+        double cb[1] = {bad};
+        wg_sum(cb, S, buf);  // small integers: exact
+        nBad = (int)cb[0];
+        PROF_MARK(8);  // relabel
         if (round == 2) robust = false;
         if (ne < 10) break;
     }
     if (t == 0) {
-        const M3 R = q_to_rot(S.T.r);
+        const M3 R = q_to_rot(T.r);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) res->Tcw[4 * i + j] = (float)R.a[3 * i + j];
-        res->Tcw[3] = (float)S.T.t.x; res->Tcw[7] = (float)S.T.t.y; res->Tcw[11] = (float)S.T.t.z;
+        res->Tcw[3] = (float)T.t.x; res->Tcw[7] = (float)T.t.y; res->Tcw[11] = (float)T.t.z;
         res->Tcw[12] = 0.f; res->Tcw[13] = 0.f; res->Tcw[14] = 0.f; res->Tcw[15] = 1.f;
         res->n_inliers = ne - nBad;
         res->lm_iterations = total_its;
     }
+#ifdef SPSLAM_POSE_PROF
+    PROF_MARK(9);  // outputs
+    if (t == 0)
+        for (int k = 0; k < 12; k++) atomicAdd(&g_pose_prof[k], prof_acc[k]);
+#endif
 }
+
 
 PoseConsts make_pose_consts(const spslam_plane_config& c) {
     PoseConsts K;
@@ -530,17 +639,29 @@ PoseConsts make_pose_consts(const spslam_plane_config& c) {
 hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_point_obs* pts,
                        const spslam_plane_obs* pls, const PoseConsts& K, const spslam_pose_result* init_from,
                        spslam_pose_result* res, uint8_t* pout, uint8_t* plout, hipStream_t s) {
-    static const int occ = [] {
-        const char* e = std::getenv("SPSLAM_POSE_OCCUPANCY");  // measurement knob: 1, 2 or 4
-        return e ? std::atoi(e) : 1;
+    static const int spec = [] {
+        const char* e = std::getenv("SPSLAM_POSE_SPEC");  // measurement knob: damping trials per edge pass
+        return e ? std::atoi(e) : 4;
     }();
-    if (occ >= 4)
-        hipLaunchKernelGGL(pose_kernel<4>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
-    else if (occ >= 2)
+    if (spec <= 1)
+        hipLaunchKernelGGL(pose_kernel<1>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+    else if (spec == 2)
         hipLaunchKernelGGL(pose_kernel<2>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
     else
-        hipLaunchKernelGGL(pose_kernel<1>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+        hipLaunchKernelGGL(pose_kernel<4>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
     return hipGetLastError();
 }
 
 }  // namespace spslam
+
+#ifdef SPSLAM_POSE_PROF
+// Diagnostic build only: the accumulated phase ticks / counters (12 u64), optionally reset.
+extern "C" int spslam_pose_prof_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pose_prof), 12 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_prof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

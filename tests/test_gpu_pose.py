@@ -4,10 +4,13 @@ Bar (BASELINE.json north_star): pose within 1e-4 relative; inlier count and
 every outlier flag identical.  Problems are synthesized from the scene ground
 truth (synth.pose_problem) on top of real ORB keypoints of the frame.
 """
+import pathlib
+
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 POSE_TOL = 1e-4
 
@@ -60,6 +63,59 @@ def test_pose_matches_oracle(gpu, problems):
         # and the optimizer actually converged to the ground truth
         ok_gt, err_gt = pose_close(rg["Tcw"], Tgt.astype(np.float32), tol=2e-2)
         assert ok_gt, f"problem {k}: far from ground truth {err_gt}"
+
+
+def test_pose_bit_exact_to_device_order_oracle(gpu, problems):
+    """With the oracle summing in the kernel's tree order (and the same sin / cos / atan2 / cube), the GPU
+    PoseOptimization is bit-exact: pose, inlier count, iteration count, every outlier flag."""
+    import oracle_ctypes
+    import spslam_gpu
+    for k, (prob, pts, pls, _) in enumerate(problems):
+        rg, pog, plog = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
+        with oracle_ctypes.pose_order(oracle_ctypes.POSE_ORDER_DEVICE):
+            ro, poo, ploo = oracle_ctypes.pose_optimize(prob, pts, pls)
+        assert np.array_equal(rg["Tcw"].view(np.uint32), ro["Tcw"].view(np.uint32)), f"problem {k}"
+        assert int(rg["n_inliers"]) == int(ro["n_inliers"]), f"problem {k}"
+        assert int(rg["lm_iterations"]) == int(ro["lm_iterations"]), f"problem {k}"
+        assert np.array_equal(pog, poo) and np.array_equal(plog, ploo), f"problem {k}"
+
+
+@pytest.mark.parametrize("spec", ["1", "2"])
+def test_pose_result_independent_of_trial_batching(problems, spec, tmp_path):
+    """The kernel evaluates kSpec damping trials per pass over the edges; the accept / reject walk replays the
+    reference's sequence, so the bits must not depend on kSpec (SPSLAM_POSE_SPEC, read once per process)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    probe = tmp_path / "probe.py"
+    probe.write_text(
+        "import sys, json, numpy as np\n"
+        f"sys.path[:0] = [{str(ROOT / 'sp-slam_amd')!r}]\n"
+        "import spslam_gpu\n"
+        "data = np.load(sys.argv[1], allow_pickle=False)\n"
+        "ex = spslam_gpu.OrbExtractor(max_batch=1)\n"
+        "out = []\n"
+        "n = int(data['n'])\n"
+        "for k in range(n):\n"
+        "    r, po, plo = spslam_gpu.pose_optimize(ex, data[f'prob{k}'], data[f'pts{k}'], data[f'pls{k}'])\n"
+        "    out.append([r['Tcw'].view(np.uint32).tolist(), int(r['n_inliers']), po.tolist(), plo.tolist()])\n"
+        "ex.close()\n"
+        "print(json.dumps(out))\n")
+    arrays = {"n": np.array(len(problems))}
+    for k, (prob, pts, pls, _) in enumerate(problems):
+        arrays[f"prob{k}"], arrays[f"pts{k}"], arrays[f"pls{k}"] = prob, pts, pls
+    npz = tmp_path / "problems.npz"
+    np.savez(npz, **arrays)
+    env = dict(os.environ)
+    outs = {}
+    for s in (spec, "4"):
+        env["SPSLAM_POSE_SPEC"] = s
+        r = subprocess.run([sys.executable, str(probe), str(npz)], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[s] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert outs[spec] == outs["4"]
 
 
 def test_fewer_than_three_points_returns_zero(gpu, problems):
@@ -128,3 +184,8 @@ def test_batch_device_chained(gpu, problems):
         r2, _, _ = oracle_ctypes.pose_optimize(p2, pts, pls)
         ok, err = pose_close(res2[i]["Tcw"], r2["Tcw"])
         assert ok, (i, err)
+        with oracle_ctypes.pose_order(oracle_ctypes.POSE_ORDER_DEVICE):  # and bit-exact in the kernel's order
+            d1, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
+            d2, _, _ = oracle_ctypes.pose_optimize(p2, pts, pls)
+        assert np.array_equal(res1[i]["Tcw"].view(np.uint32), d1["Tcw"].view(np.uint32)), i
+        assert np.array_equal(res2[i]["Tcw"].view(np.uint32), d2["Tcw"].view(np.uint32)), i
