@@ -175,11 +175,14 @@ __global__ __launch_bounds__(64) void assoc_decide_kernel(const spslam_assoc_fra
     if (new_plane && threadIdx.x == 0) new_plane[f] = any;
 }
 
-// Fused form (the default when the per-frame distance table fits in LDS): one workgroup per frame computes
-// every frame plane's world coefficients, streams each map plane's boundary cloud once for all the frame
-// planes that pass its angle test (float minima, exact in any order), and runs the decision walk from LDS.
-// One launch of n_frames workgroups instead of n_frames x max_map + n_frames: inside the pipelined step the
-// tracking chain's launches wait for CU slots behind the extraction kernels, so the grid size is the cost.
+// Fused form (the default when the per-frame distance table fits in LDS): one workgroup per frame.  Every
+// frame plane's world coefficients are computed once (thread i: plane i), then each wave takes every 4th map
+// plane: its lanes stride over that plane's boundary cloud keeping the running minima of |pM . (p, 1)| for
+// up to 8 frame planes at a time (those passing the angle test; float minima, exact in any order), and a
+// wave reduction writes the distance column.  Two workgroup barriers in all; the decision walk (the
+// reference's order over the map planes) then runs from LDS, one thread per frame plane.  One launch of
+// n_frames workgroups: inside the pipelined step the tracking chain's launches wait for CU slots behind the
+// extraction kernels, so the grid size and the barrier count are the cost.
 __global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_assoc_frame* __restrict__ frames,
                                                                AssocSources S, const spslam_map_plane* __restrict__ map,
                                                                const float* __restrict__ boundary, int max_map,
@@ -188,68 +191,54 @@ __global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_asso
                                                                int32_t* __restrict__ vertical,
                                                                int* __restrict__ new_plane) {
     tail_wave_priority();
-    extern __shared__ float dmin[];  // [cap_a + cap_b][max_map] as ordered ints (non-negative floats)
-    __shared__ float pm_s[kGroup][4];
-    __shared__ int idx_s[kGroup];
-    __shared__ int ng_s;
-    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63;
+    extern __shared__ float lds[];  // [cap_a + cap_b][max_map] distances, then [cap_a + cap_b][4] world coefs
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
     const spslam_assoc_frame& F = frames[f];
     int na, nb;
     plane_counts(S, f, &na, &nb);
     const int n = na + nb, P = S.cap_a + S.cap_b, nm = F.n_map;
-    int* D = reinterpret_cast<int*>(dmin);
-    for (int q = t; q < n * max_map; q += kThreads) D[q] = __float_as_int(100.f);  // PointDistanceFromPlane: 100
+    float* D = lds;
+    float* pm_s = lds + (size_t)P * max_map;
+    for (int i = t; i < n; i += kThreads) world_coeff(F.Tcw, coef_of(S, f, i, na), pm_s + 4 * i);
     __syncthreads();
-    for (int j = 0; j < nm; j++) {
+    for (int j = w; j < nm; j += kWaves) {
         const spslam_map_plane M = map[F.map_offset + j];
         const float* pts = boundary + 3 * (size_t)M.boundary_offset;
         for (int i0 = 0; i0 < n; i0 += kGroup) {
-            if (t == 0) {  // the planes of this group whose normal passes the angle test against map plane j
-                int g = 0;
-                for (int i = i0; i < min(i0 + kGroup, n); i++) {
-                    float pM[4];
-                    world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
-                    const float angle = dot3(pM, M.world);
-                    if (angle > Pm.angle_th || angle < -Pm.angle_th) {
-                        for (int k = 0; k < 4; k++) pm_s[g][k] = pM[k];
-                        idx_s[g++] = i;
-                    }
-                }
-                ng_s = g;
+            // the frame planes of this group whose normal passes the angle test against map plane j (every
+            // lane evaluates the same tests; planes failing it keep the reference's untouched 100)
+            float pmr[kGroup][4], mn[kGroup];
+            bool pass[kGroup];
+#pragma unroll
+            for (int q = 0; q < kGroup; q++) {
+                const int i = min(i0 + q, n - 1);
+#pragma unroll
+                for (int k = 0; k < 4; k++) pmr[q][k] = pm_s[4 * i + k];
+                const float angle = dot3(pmr[q], M.world);
+                pass[q] = i0 + q < n && (angle > Pm.angle_th || angle < -Pm.angle_th);
+                mn[q] = 100.f;  // PointDistanceFromPlane: res = 100
             }
-            __syncthreads();
-            const int g = ng_s;
-            if (g > 0) {
-                float pmr[kGroup][4], mn[kGroup];
+            for (int p = lane; p < M.n_boundary; p += 64) {
+                const float qv[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
 #pragma unroll
-                for (int q = 0; q < kGroup; q++) {
-#pragma unroll
-                    for (int k = 0; k < 4; k++) pmr[q][k] = pm_s[q < g ? q : 0][k];
-                    mn[q] = 100.f;
-                }
-                for (int p = t; p < M.n_boundary; p += kThreads) {
-                    const float qv[3] = {pts[3 * p], pts[3 * p + 1], pts[3 * p + 2]};
-#pragma unroll
-                    for (int q = 0; q < kGroup; q++)
-                        mn[q] = fminf(mn[q], fabsf(__fadd_rn(dot3(pmr[q], qv), pmr[q][3])));
-                }
-#pragma unroll
-                for (int q = 0; q < kGroup; q++) {
-                    float v = mn[q];
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
-                    if (lane == 0 && q < g) atomicMin(&D[idx_s[q] * max_map + j], __float_as_int(v));
-                }
+                for (int q = 0; q < kGroup; q++)
+                    mn[q] = fminf(mn[q], fabsf(__fadd_rn(dot3(pmr[q], qv), pmr[q][3])));
             }
-            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < kGroup; q++) {
+                float v = mn[q];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+                if (lane == 0 && i0 + q < n) D[(i0 + q) * max_map + j] = pass[q] ? v : 100.f;
+            }
         }
     }
+    __syncthreads();
     // the reference's walk over the map planes (Map.cc:207-257), one thread per frame plane
     int unmatched = 0;
     const spslam_map_plane* Mp = map + F.map_offset;
     for (int i = t; i < n; i += kThreads) {
-        float pM[4];
-        world_coeff(F.Tcw, coef_of(S, f, i, na), pM);
+        const float* pM = pm_s + 4 * i;
         float ldTh = Pm.dis_th, lverTh = Pm.ver_th, lparTh = Pm.par_th;
         const size_t o = (size_t)f * P + i;
         int32_t m = -1, par = -1, ver = -1;
@@ -261,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_asso
         for (int j = 0; j < nm; j++) {
             const float angle = dot3(pM, Mp[j].world);
             if (angle > Pm.angle_th || angle < -Pm.angle_th) {
-                const float dis = __int_as_float(D[i * max_map + j]);
+                const float dis = D[i * max_map + j];
                 if (dis < ldTh) {
                     ldTh = dis;
                     m = F.map_offset + j;
@@ -295,7 +284,7 @@ hipError_t assoc_launch(int n_frames, const spslam_assoc_frame* frames, const As
                         int32_t* vertical, int* new_plane, hipStream_t s, KernelTimer* timer) {
     if (n_frames < 1 || max_map < 0 || src.cap_a < 0 || src.cap_b < 0) return hipErrorInvalidValue;
     if (timer) timer->begin(kKindAssoc, s);
-    const size_t lds = (size_t)(src.cap_a + src.cap_b) * max_map * sizeof(float);
+    const size_t lds = (size_t)(src.cap_a + src.cap_b) * (max_map + 4) * sizeof(float);
     if (lds <= 48 * 1024) {
         hipLaunchKernelGGL(assoc::assoc_fused_kernel, dim3(n_frames), dim3(assoc::kThreads), std::max<size_t>(lds, 4),
                            s, frames, src, map, boundary, max_map, P, match, parallel, vertical, new_plane);

@@ -34,7 +34,10 @@
 namespace spslam {
 namespace planes {
 
-constexpr int kSegThreads = 1024;
+#ifndef SPSLAM_SEG_THREADS
+#define SPSLAM_SEG_THREADS 1024
+#endif
+constexpr int kSegThreads = SPSLAM_SEG_THREADS;
 constexpr int kSegWaves = kSegThreads / 64;
 constexpr int kMaxBig = 255;          // components > MinSize per frame (u8 tags)
 constexpr int kMaxRowWords = 8;       // W <= 512
@@ -400,27 +403,30 @@ __device__ __forceinline__ int refine_pass(SegShared& S, uint8_t* state, const u
 #undef SPSLAM_REFINE_FETCH
 }
 
-// Fast path (nmodel <= 6).  Before each pass every point gets a descriptor
-// byte, computed in parallel: bits 0-5 = models whose plane is within 0.02 m
-// of the point (only for valid, still unlabelled points), bit 6 = its
-// vertical source may grow it, bit 7 = its chain source may grow it (source
-// and source-neighbour validity, row limits of the reference loops).  The
-// pass itself then only composes per-pixel transfer functions, packed in 9
-// bits (bit 8 = constant; low byte = constant state, or the complement of the
-// pass-through set, so 0 is the identity) and scanned with DPP.  Which grow
-// event produced each new label is re-derived afterwards from the final
-// states, in parallel, in the reference's event order.
+// Fast path (nmodel <= kFastModels = 14).  Before each pass every point gets
+// a 16-bit descriptor, computed in parallel: bits 0-13 = models whose plane is
+// within 0.02 m of the point (only for valid, still unlabelled points), bit 14
+// = its vertical source may grow it, bit 15 = its chain source may grow it
+// (source and source-neighbour validity, row limits of the reference loops);
+// stored as two byte planes.  The pass itself then only composes per-pixel
+// transfer functions, packed in 17 bits (bit 16 = constant; low 16 bits =
+// constant state, or the complement of the pass-through set, so 0 is the
+// identity) and scanned with DPP.  Which grow event produced each new label is
+// re-derived afterwards from the final states, in parallel, in the
+// reference's event order.
+constexpr int kFastModels = 14;
+constexpr int kFnConst = 0x10000;
 __device__ __forceinline__ int f8_pass(int f, int L) {  // f: complemented pass-through set
-    return (L > 0 && !((f >> ((L - 1) & 7)) & 1)) ? L : 0;
+    return (L > 0 && !((f >> ((L - 1) & 15)) & 1)) ? L : 0;
 }
 __device__ __forceinline__ int f8_then(int first, int second) {
-    const int through = 0x100 | f8_pass(second, first & 0xFF);
+    const int through = kFnConst | f8_pass(second, first & 0xFFFF);
     const int both = first | second;
-    const int r = (first & 0x100) ? through : both;
-    return (second & 0x100) ? second : r;
+    const int r = (first & kFnConst) ? through : both;
+    return (second & kFnConst) ? second : r;
 }
 __device__ __forceinline__ int f8_apply(int f, int L) {
-    return (f & 0x100) ? (f & 0xFF) : f8_pass(f, L);
+    return (f & kFnConst) ? (f & 0xFFFF) : f8_pass(f, L);
 }
 // Inclusive wave scan of f8_then (lane order), DPP row shifts + row broadcasts.
 __device__ __forceinline__ int f8_scan(int x) {
@@ -452,12 +458,12 @@ __device__ __forceinline__ int refine_desc(const uint8_t* state, const float* X,
         act = r <= H - 2 && isfinite(X[i + W]) && isfinite(X[i + W - 1]);
         link = (c <= W - 2 ? r >= 1 : r <= H - 2) && isfinite(X[i + 1]);
     }
-    return acc | (act ? 0x40 : 0) | (link ? 0x80 : 0);
+    return acc | (act ? 0x4000 : 0) | (link ? 0x8000 : 0);
 }
 
 template <int K>
-__device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc, const uint64_t* cbits, int W, int H,
-                                            bool bw) {
+__device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc, const uint8_t* desc_hi,
+                                            const uint64_t* cbits, int W, int H, bool bw) {
     const int lane = threadIdx.x & 63;
     const int RW = (W + 63) >> 6;
     const int lastLane = (W - 1) / K, lastK = (W - 1) - lastLane * K;
@@ -475,7 +481,7 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc,
             if (p < W && (STEP) < H) {                                             \
                 const int i = r_ * W + (bw ? W - 1 - p : p);                       \
                 qs[k] = state[i];                                                  \
-                qd[k] = desc[i];                                                   \
+                qd[k] = desc[i] | (desc_hi[i] << 8);                               \
             }                                                                      \
         }                                                                          \
     }
@@ -495,12 +501,12 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc,
             int g[K];
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const int acc = d[k] & 0x3F, U = prevS[k];
-                const bool grant = (d[k] & 0x40) && U && ((acc >> ((U - 1) & 7)) & 1);
-                int e = (d[k] & 0x80) ? (~acc & 0xFF) : 0x100;
-                e = grant ? (0x100 | U) : e;
-                e = acc ? e : 0x100;
-                g[k] = s0[k] ? (0x100 | s0[k]) : e;
+                const int acc = d[k] & 0x3FFF, U = prevS[k];
+                const bool grant = (d[k] & 0x4000) && U && ((acc >> ((U - 1) & 15)) & 1);
+                int e = (d[k] & 0x8000) ? (~acc & 0xFFFF) : kFnConst;
+                e = grant ? (kFnConst | U) : e;
+                e = acc ? e : kFnConst;
+                g[k] = s0[k] ? (kFnConst | s0[k]) : e;
             }
             int F = g[0];
 #pragma unroll
@@ -527,15 +533,15 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc,
 // Grow events of one finished fast pass, appended at ev[] in the reference's
 // order (sources in pass order; per source: along the row, then across rows).
 // Returns the number of events (uniform).
-__device__ int refine_events(SegShared& S, const uint8_t* state, const uint8_t* desc, int W, int H, int N, bool bw,
-                             int* ev) {
+__device__ int refine_events(SegShared& S, const uint8_t* state, const uint8_t* desc, const uint8_t* desc_hi, int W,
+                             int H, int N, bool bw, int* ev) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int M = (H - 1) * W;
     // how target j grew in this pass: 0 not, 1 along its row (chain), 2 from the other row
     auto how = [&](int j, int vsrc) -> int {
-        const int dj = desc[j];
-        if (!(dj & 0x3F) || !state[j]) return 0;
-        if (dj & 0x40) {
+        const int dj = desc[j] | (desc_hi[j] << 8);
+        if (!(dj & 0x3FFF) || !state[j]) return 0;
+        if (dj & 0x4000) {
             const int U = state[vsrc];
             if (U && ((dj >> (U - 1)) & 1)) return 2;
         }
@@ -923,8 +929,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     STAMP(7);
     // ---- K: refinement (two passes), one wave per pass
     uint64_t* cbits = hbits;  // rows with growable points (hbits no longer needed)
-    if (nmodel > 0 && nmodel <= 6) {
+    if (nmodel > 0 && nmodel <= kFastModels) {
         uint8_t* desc = nmask;  // the contour masks come later
+        // descriptor high bytes: the covariance staging area (phase G is over) when the frame fits, else the
+        // rank scratch (dead since phase D)
+        uint8_t* desc_hi = (size_t)N <= sizeof(S.stage) ? (uint8_t*)&S.stage[0][0][0] : (uint8_t*)rankA;
         int ng = 0;
         for (int pass = 0; pass < 2; pass++) {
             const bool bw = pass == 1;
@@ -935,16 +944,17 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                     if (c < W) {
                         dsc = refine_desc(state, X, Y, Z, S.model_coef, nmodel, W, H, i, bw);
                         desc[i] = (uint8_t)dsc;
+                        desc_hi[i] = (uint8_t)(dsc >> 8);
                     }
                     const uint64_t m = __ballot(dsc != 0);
                     if (lane == 0) cbits[r * RW + k] = m;
                 }
             __syncthreads();
             if (pass == 0) STAMP(10);
-            if (wave == 0) refine_rows<K>(state, desc, cbits, W, H, bw);
+            if (wave == 0) refine_rows<K>(state, desc, desc_hi, cbits, W, H, bw);
             __syncthreads();
             if (pass == 0) STAMP(11);
-            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng);
+            ng += refine_events(S, state, desc, desc_hi, W, H, N, bw, ev + ng);
         }
         if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
     } else if (nmodel > 0) {

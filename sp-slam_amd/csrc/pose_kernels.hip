@@ -232,8 +232,11 @@ using namespace pose;
 // .cpp:145-160), so trial q's lambda is known in advance; lane q % kSpec of every wave solves trial q, the
 // trial poses are broadcast with readlane, one pass over the edges evaluates all kSpec robust chi2 sums, and
 // the accept / reject walk then replays the reference's sequence over them.  Results do not depend on kSpec.
+#ifndef SPSLAM_POSE_MINW
+#define SPSLAM_POSE_MINW 1  // waves per SIMD the register allocation leaves room for
+#endif
 template <int kSpec>
-__global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+__global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
                                                          const spslam_point_obs* __restrict__ pts_all,
                                                          const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
                                                          const spslam_pose_result* __restrict__ init_from,

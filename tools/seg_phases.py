@@ -43,6 +43,11 @@ def main():
         print(f"{name:18s} mean {d[:, k].mean():9.1f} us   max {d[:, k].max():9.1f} us")
     print(f"{'total':18s} mean {tot.mean():9.1f} us   max {tot.max():9.1f} us")
     k = ts[:, 10] > 0
+    ref = (ts[:, 8] - ts[:, 7]) / 100.0
+    print(f"fast-path frames {k.sum()} / {len(k)}: refine mean {ref[k].mean() if k.any() else 0:.1f} us, "
+          f"max {ref[k].max() if k.any() else 0:.1f};  general-path refine mean "
+          f"{ref[~k].mean() if (~k).any() else 0:.1f} us, max {ref[~k].max() if (~k).any() else 0:.1f}")
+    print("total per frame (us) percentiles 50/90/99/100:", np.percentile(tot, [50, 90, 99, 100]).round(1).tolist())
     if k.any():
         print(f"refine: cand-bitmap {((ts[k, 10] - ts[k, 7]) / 100).mean():.1f} us, forward "
               f"{((ts[k, 11] - ts[k, 10]) / 100).mean():.1f} us, events {ts[k, 12].mean():.1f}")
