@@ -57,7 +57,7 @@ struct Ctx {
     const spslam_lba_plane* pl;
     const spslam_lba_plane_obs* plobs;
     LbaCtl* ctl;
-    double *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *con, *lmH, *lmb, *Dinv, *db, *xl, *blkH, *blkBD, *S, *bs, *dd, *y,
+    double *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *con, *lmH, *lmb, *Dinv, *db, *xl, *blkH, *blkBD, *S, *bs, *dd, *y, *S_part,
         *Hpp, *bp, *part_chi, *part_scale, *part_max;
     int *pose_hidx, *hidx_pose, *e_lm, *e_kf, *e_type, *e_level, *e_blk, *e_src, *lm_boff, *lm_nb, *lm_act, *kf_cnt,
         *pe_off, *pe_idx;
@@ -82,6 +82,7 @@ __device__ Ctx make_ctx(const LbaBatch& b, int p) {
     c.lmH = (double*)(base + Ly.lm_H); c.lmb = (double*)(base + Ly.lm_b); c.Dinv = (double*)(base + Ly.lm_Dinv);
     c.db = (double*)(base + Ly.lm_db); c.xl = (double*)(base + Ly.lm_x);
     c.blkH = (double*)(base + Ly.blk_H); c.blkBD = (double*)(base + Ly.blk_BD);
+    c.S_part = (double*)(base + Ly.S_part);
     c.S = (double*)(base + Ly.S); c.bs = (double*)(base + Ly.bs); c.dd = (double*)(base + Ly.dd);
     c.y = (double*)(base + Ly.y); c.Hpp = (double*)(base + Ly.Hpp); c.bp = (double*)(base + Ly.bp);
     c.part_chi = (double*)(base + Ly.part_chi); c.part_scale = (double*)(base + Ly.part_scale);
@@ -260,10 +261,13 @@ __device__ int block_scan(int v, int* total, Red& R) {
 __device__ __forceinline__ int lm_block_base(const Ctx& c, int l) { return c.lm_act[l] - 1; }
 
 // Edge Jacobians: A (landmark, dim x 3), B (pose, dim x 6); fixed vertices skipped.
+// kOnly: 0 = any edge, 1 = point edges only, 2 = plane edges only (the caller filtered the type; instances
+// without the numeric plane Jacobians need far fewer registers)
+template <int kOnly = 0>
 __device__ void edge_jacobians(const Ctx& c, int e, bool pose_free, double (&A)[3][3], double (&B)[3][6]) {
     const int t = c.e_type[e], lm = c.e_lm[e];
     const SE3 T = load_pose(c.pose + 7 * c.e_kf[e]);
-    if (t <= 1) {
+    if (kOnly != 2 && (kOnly == 1 || t <= 1)) {
         const spslam_lba_keyframe& k = c.kf[c.e_kf[e]];
         const double fx = k.fx, fy = k.fy, bf = k.bf;
         const double* X = c.X + 3 * lm;
@@ -557,18 +561,10 @@ __global__ __launch_bounds__(kThreads) void k_errors(LbaBatch b, LbaWork w, LbaC
     if (threadIdx.x == 0) c.part_chi[task.y / kThreads] = acc[0];
 }
 
-__global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, LbaConsts C) {
-    const int2 task = w.edge_chunks[blockIdx.x];
-    Ctx c = make_ctx(b, task.x);
-    const LbaCtl& k = *c.ctl;
-    if (k.state != kIter) return;
-    const int e = task.y + threadIdx.x;
-    if (e >= c.E || c.e_level[e] != 0) return;
-    const bool robust = k.robust;
-    const int ty = c.e_type[e], dim = edge_dim(ty);
-    const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
-    double A[3][3] = {}, B[3][6] = {};
-    edge_jacobians(c, e, pfree, A, B);
+// quadratic-form terms of active edge e from its Jacobians (A: landmark, B: pose) and cached error
+__device__ __forceinline__ void store_terms(const Ctx& c, const LbaConsts& C, bool robust, int e, int ty, bool pfree,
+                                            const double (&A)[3][3], const double (&B)[3][6]) {
+    const int dim = edge_dim(ty);
     double info[3];
     info_of(c, C, e, info);
     const double* err = c.err + 3 * e;
@@ -606,6 +602,75 @@ __global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, 
 #pragma unroll
         for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
     }
+}
+
+// point edges (analytic Jacobians), one edge per thread
+__global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, LbaConsts C) {
+    const int2 task = w.edge_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kIter) return;
+    if (task.y >= c.Ep) return;  // chunks of plane edges only
+    const int e = task.y + threadIdx.x;
+    if (e >= c.Ep || c.e_level[e] != 0) return;
+    const int ty = c.e_type[e];
+    const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
+    double A[3][3] = {}, B[3][6] = {};
+    edge_jacobians<1>(c, e, pfree, A, B);
+    store_terms(c, C, k.robust, e, ty, pfree, A, B);
+}
+
+// plane / parallel / vertical edges: central differences (base_binary_edge.hpp:130-205), one wave per edge.
+// Lane q < 6 evaluates the error at the plane perturbed by +-1e-9 along coordinate q >> 1 (Plane3D::oplus),
+// lane 6 <= q < 18 at the pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; the differences are gathered with
+// shuffles (the reference's per-coordinate expression) and lane 0 stores the terms.
+__global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w, LbaConsts C) {
+    const int2 task = w.plane_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kIter) return;
+    const int lane = threadIdx.x & 63;
+    const int e = task.y + (threadIdx.x >> 6);
+    if (e >= c.E || c.e_level[e] != 0) return;  // uniform over the wave
+    const int ty = c.e_type[e], dim = edge_dim(ty), lm = c.e_lm[e];
+    const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
+    const SE3 T0 = load_pose(c.pose + 7 * c.e_kf[e]);
+    const double* pp = c.P + 4 * (lm - c.Np);
+    const P4 P0{{pp[0], pp[1], pp[2], pp[3]}};
+    const P4 meas = plane_from_f(c.plobs[c.e_src[e]].meas);
+    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    double ev[3] = {0, 0, 0};
+    if (lane < 18 && (lane < 6 || pfree)) {
+        const double sgn = (lane & 1) ? -delta : delta;
+        SE3 T = T0;
+        P4 P = P0;
+        if (lane < 6) {
+            double add[3] = {0, 0, 0};
+            add[lane >> 1] = sgn;
+            p_oplus(P, add);
+        } else {
+            double add[6] = {0, 0, 0, 0, 0, 0};
+            add[(lane - 6) >> 1] = sgn;
+            T = se3_mul(se3_exp(add), T0);
+        }
+        plane_edge_error(ty, T, P, meas, ev);
+    }
+    double A[3][3] = {}, B[3][6] = {};
+#pragma unroll
+    for (int d = 0; d < 3; d++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const double ep = __shfl(ev[i], 2 * d), em = __shfl(ev[i], 2 * d + 1);
+            A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
+        }
+#pragma unroll
+    for (int d = 0; d < 6; d++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const double ep = __shfl(ev[i], 6 + 2 * d), em = __shfl(ev[i], 7 + 2 * d);
+            B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
+        }
+    if (lane == 0) store_terms(c, C, k.robust, e, ty, pfree, A, B);
 }
 
 // landmark Hll, bl and (landmark, pose) blocks, summed over the landmark's edges in insertion order
@@ -716,6 +781,10 @@ __global__ void k_iter_begin(LbaBatch b) {
 }
 
 // ---------------------------------------------------------------- Schur complement
+// reduced systems of 6 * np <= 80 rows: Schur sums on the matrix cores (k_schur_mfma + k_schur_reduce)
+__device__ __forceinline__ bool mfma_schur(const LbaCtl& k) { return 6 * k.np <= 16 * kLbaMfmaTiles; }
+__device__ __forceinline__ int mfma_tiles(const LbaCtl& k) { return (6 * k.np + 15) / 16; }
+
 __global__ __launch_bounds__(kThreads) void k_schur_lm(LbaBatch b, LbaWork w) {
     const int2 task = w.lm_chunks[blockIdx.x];
     Ctx c = make_ctx(b, task.x);
@@ -737,6 +806,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_lm(LbaBatch b, LbaWork w) {
     const double* bl = c.lmb + 3 * l;
 #pragma unroll
     for (int i = 0; i < 3; i++) c.db[3 * l + i] = (Di[3 * i] * bl[0] + Di[3 * i + 1] * bl[1]) + Di[3 * i + 2] * bl[2];
+    if (mfma_schur(k)) return;  // k_schur_mfma forms B Dinv on the fly
     const int nb = __popcll(c.lm_mask[l]);
     for (int a = 0; a < nb; a++) {
         const double* H = c.blkH + (size_t)(b0 + a) * 18;  // 3 x 6 (landmark x pose)
@@ -748,7 +818,123 @@ __global__ __launch_bounds__(kThreads) void k_schur_lm(LbaBatch b, LbaWork w) {
     }
 }
 
-// pose-pair tasks: S(p1, p2) for p1 <= p2 (task < np(np+1)/2), then bs(p) (next np tasks)
+// sum_l (B Dinv)_l B_l^T over the landmarks on v_mfma_f64_16x16x4: the reduced system (n = 6 np rows, padded
+// to NT x 16) is NT x NT output tiles held by each wave; one MFMA per (tile, landmark) takes k = the landmark's
+// 3 coordinates (+ one zero slot).  Lane l feeds A[row l & 15][k l >> 4] = (B Dinv)(pose row, k) formed on the
+// fly from the landmark's (landmark, pose) block and Dinv (the pose-pair kernel's formula; zero where the pose
+// does not observe the landmark) and B[k l >> 4][col l & 15] = the block's H entry.  Each wave takes
+// kLbaMfmaLm landmarks of its workgroup's landmark chunk and writes its tiles to S_part; k_schur_reduce sums
+// the partial sets in a fixed order.
+template <int NT>
+__global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) {
+    typedef double d4 __attribute__((ext_vector_type(4)));
+    const int2 task = w.lm_chunks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial || !mfma_schur(k) || (mfma_tiles(k) > NT) || (NT > 3 && mfma_tiles(k) < NT)) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n = 6 * k.np, kk = lane >> 4, r16 = lane & 15;
+    const int l0 = task.y + wave * kLbaMfmaLm, nl = min(c.L - l0, kLbaMfmaLm);
+    if (nl <= 0) return;  // partial sets exist for the first ceil(L / kLbaMfmaLm) landmark groups only
+    // the group's pose masks and block bases, one landmark per lane (read back with readlane)
+    const uint64_t m_l = lane < nl ? c.lm_mask[l0 + lane] : 0ull;
+    const int b_l = lane < nl ? lm_block_base(c, l0 + lane) : -1;
+    d4 acc[NT][NT];
+#pragma unroll
+    for (int i = 0; i < NT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    // this lane's pose and component in every tile row / column
+    int pose_t[NT], comp_t[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+        const int r = 16 * t + r16;
+        pose_t[t] = r < n ? r / 6 : 63;
+        comp_t[t] = r - 6 * (r / 6);
+    }
+    // one landmark's operands: Dinv column kk and, per tile, the three H entries of (B Dinv)(row, kk) and
+    // B^T(kk, col).  Loads are unconditional (a lane that does not observe reads the landmark's first block)
+    // so the next landmark's loads can be issued before this one's MFMAs.
+    struct Ops { double d[3]; double h[NT][3]; double hb[NT]; bool obs[NT]; };
+    auto load = [&](int i, Ops& o) __attribute__((always_inline)) {
+        const int bl = __builtin_amdgcn_readlane(b_l, i);
+        const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(m_l >> 32), i) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m_l, i);
+        const int kc = kk < 3 ? kk : 0;
+        const double* Di = c.Dinv + 9 * (size_t)(l0 + i);
+        o.d[0] = Di[kc]; o.d[1] = Di[3 + kc]; o.d[2] = Di[6 + kc];
+#pragma unroll
+        for (int t = 0; t < NT; t++) {
+            const int p = pose_t[t], q = comp_t[t];
+            o.obs[t] = bl >= 0 && kk < 3 && p < 64 && ((m >> p) & 1ull);
+            const int blk = o.obs[t] ? bl + __popcll(m & ((1ull << p) - 1ull)) : (bl >= 0 ? bl : 0);
+            const double* H = c.blkH + (size_t)blk * 18;
+            o.h[t][0] = H[q]; o.h[t][1] = H[6 + q]; o.h[t][2] = H[12 + q];
+            o.hb[t] = H[6 * kc + q];
+        }
+    };
+    Ops cur, nxt;
+    load(0, cur);
+    for (int i = 0; i < nl; i++) {
+        if (i + 1 < nl) load(i + 1, nxt);
+        if (__builtin_amdgcn_readlane(b_l, i) >= 0) {  // landmarks without an active edge add nothing
+            double a[NT], bb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                // (B Dinv)(row, kk): the pose-pair kernel's formula
+                a[t] = cur.obs[t] ? (cur.h[t][0] * cur.d[0] + cur.h[t][1] * cur.d[1]) + cur.h[t][2] * cur.d[2] : 0.0;
+                bb[t] = cur.obs[t] ? cur.hb[t] : 0.0;
+            }
+#pragma unroll
+            for (int ti = 0; ti < NT; ti++)
+#pragma unroll
+                for (int tj = 0; tj < NT; tj++)
+                    acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bb[tj], acc[ti][tj], 0, 0, 0);
+        }
+        cur = nxt;
+    }
+    // C/D layout of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
+    double* out = c.S_part + (size_t)((task.y / kLbaChunk) * (kLbaChunk / kLbaMfmaLm) + wave) * NT * NT * 256;
+#pragma unroll
+    for (int i = 0; i < NT; i++)
+#pragma unroll
+        for (int j = 0; j < NT; j++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) out[(i * NT + j) * 256 + (kk + 4 * g) * 16 + r16] = acc[i][j][g];
+}
+
+// S(p1, p2) = Hpp + lambda - sum of the partial tile sets (in landmark-group order) for p1 <= p2.  Grid:
+// (problem, 256-entry slice of the n x n system).
+__global__ __launch_bounds__(kThreads) void k_schur_reduce(LbaBatch b) {
+    Ctx c = make_ctx(b, blockIdx.x);
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kTrial || !mfma_schur(k)) return;
+    const int np = k.np, n = 6 * np, ntr = mfma_tiles(k);
+    const int NT = ntr < 3 ? 3 : ntr;  // the tile count of the k_schur_mfma instance that served this problem
+    const int nparts = (c.L + kLbaMfmaLm - 1) / kLbaMfmaLm;
+    const int e = blockIdx.y * kThreads + threadIdx.x;
+    if (e >= n * n) return;
+    const int r = e / n, q = e - r * n;
+    const int p1 = r / 6, p2 = q / 6;
+    if (p1 > p2) return;
+    const size_t o = (size_t)((r >> 4) * NT + (q >> 4)) * 256 + (r & 15) * 16 + (q & 15);
+    const double* src = c.S_part + o;
+    const size_t stride = (size_t)NT * NT * 256;
+    double v = 0.0;
+    int s = 0;
+    for (; s + 4 <= nparts; s += 4) {  // four loads in flight, summed in order
+        const double x0 = src[s * stride], x1 = src[(s + 1) * stride], x2 = src[(s + 2) * stride],
+                     x3 = src[(s + 3) * stride];
+        v += x0; v += x1; v += x2; v += x3;
+    }
+    for (; s < nparts; s++) v += src[s * stride];
+    const int rr = r - 6 * p1, qq = q - 6 * p2;
+    const double base = p1 == p2 ? c.Hpp[36 * p1 + 6 * rr + qq] + (rr == qq ? k.lambda : 0.0) : 0.0;
+    c.S[(size_t)r * n + q] = base - v;
+}
+
+// pose-pair tasks: S(p1, p2) for p1 <= p2 (task < np(np+1)/2), then bs(p) (next np tasks); problems of the
+// MFMA path only run the bs tasks here
 __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w) {
     __shared__ Red R;
     const int2 task = w.pair_tasks[blockIdx.x];
@@ -757,6 +943,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
     if (k.state != kTrial) return;
     const int np = k.np, n = 6 * np, npairs = np * (np + 1) / 2, tid = task.y;
     if (tid >= npairs + np) return;
+    if (tid < npairs && mfma_schur(k)) return;
     if (tid < npairs) {
         int p1 = 0, rem = tid;
         while (rem >= np - p1) { rem -= np - p1; p1++; }
@@ -1140,10 +1327,15 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
         hipLaunchKernelGGL(k_struct_done, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_errors, dim3(w.n_edge_chunks), T, 0, s, b, w, C, 0);
         hipLaunchKernelGGL(k_edge_terms, dim3(w.n_edge_chunks), T, 0, s, b, w, C);
+        if (w.n_plane_tasks) hipLaunchKernelGGL(k_plane_terms, dim3(w.n_plane_tasks), T, 0, s, b, w, C);
         hipLaunchKernelGGL(k_lm_sums, dim3(w.n_lm_chunks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_pose_sums, dim3(w.n_kf_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_iter_begin, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_schur_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_mfma<3>, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_mfma<4>, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_mfma<5>, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_reduce, dim3(P, (80 * 80 + kThreads - 1) / kThreads), T, 0, s, b);
         hipLaunchKernelGGL(k_schur_pairs, dim3(w.n_pair_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_factor, dim3(P), T, kFactorLds, s, b);
         hipLaunchKernelGGL(k_update_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);

@@ -10,6 +10,10 @@ namespace spslam {
 constexpr int kLbaMaxKeyframes = 64;   // local + fixed keyframes per problem (pose masks are 64-bit)
 constexpr int kLbaChunk = 256;         // edges / landmarks per workgroup in the grid-wide phases
 constexpr int kLbaCon = 57;            // per-edge terms: Hll 9, bl 3, Hpl 18 (3x6), Hpp upper 21, bp 6
+// Schur complement on the matrix cores (v_mfma_f64_16x16x4): reduced systems of up to kLbaMfmaTiles x 16 rows
+// (6 * free poses <= 80); larger ones use the pose-pair kernel.  One partial 16x16-tile set per 64 landmarks.
+constexpr int kLbaMfmaTiles = 5;
+constexpr int kLbaMfmaLm = 64;
 
 // LM / schedule state of one problem (device, in its scratch); see lba_kernels.hip.
 struct LbaCtl {
@@ -25,7 +29,7 @@ struct LbaCtl {
 struct LbaLayout {
     size_t ctl;
     size_t pose, pose_b, pt, pt_b, pl, pl_b, e_err, e_con, lm_H, lm_b, lm_Dinv, lm_db, lm_x, blk_H, blk_BD, S, bs,
-        dd, y, Hpp, bp, part_chi, part_scale, part_max;                                    // double arrays
+        dd, y, Hpp, bp, part_chi, part_scale, part_max, S_part;                            // double arrays
     size_t pose_hidx, hidx_pose, e_lm, e_kf, e_type, e_level, e_blk, e_src, lm_boff, lm_nb, lm_act, kf_cnt, pe_off,
         pe_idx;                                                                            // int arrays
     size_t lm_mask;                                                                        // uint64
@@ -51,6 +55,11 @@ __host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
     L.S = take(n6 * n6 * 8); L.bs = take(n6 * 8); L.dd = take(n6 * 8); L.y = take(n6 * 8);
     L.Hpp = take(K * 36 * 8); L.bp = take(K * 6 * 8);
     L.part_chi = take(nEc * 8); L.part_scale = take(nLc * 8); L.part_max = take((nLc + K) * 8);
+    // partial tile sets of k_schur_mfma: NT = max(3, ceil(6 np / 16)) <= kLbaMfmaTiles tiles per dimension,
+    // np <= K free poses
+    size_t nt = (n6 + 15) / 16;
+    nt = nt < 3 ? 3 : (nt > (size_t)kLbaMfmaTiles ? (size_t)kLbaMfmaTiles : nt);
+    L.S_part = take(((Lm + kLbaMfmaLm - 1) / kLbaMfmaLm) * nt * nt * 256 * 8);
     L.pose_hidx = take(K * 4); L.hidx_pose = take(K * 4);
     L.e_lm = take((size_t)E * 4); L.e_kf = take((size_t)E * 4); L.e_type = take((size_t)E * 4);
     L.e_level = take((size_t)E * 4); L.e_blk = take((size_t)E * 4); L.e_src = take((size_t)E * 4);
@@ -72,7 +81,9 @@ struct LbaWork {
     const int2* lm_chunks; int n_lm_chunks;
     const int2* kf_tasks; int n_kf_tasks;
     const int2* pair_tasks; int n_pair_tasks;
+    const int2* plane_tasks; int n_plane_tasks;  // (problem, first plane edge) per kLbaPlaneEdgesPerTask edges
 };
+constexpr int kLbaPlaneEdgesPerTask = kLbaChunk / 64;  // one wave per plane edge
 
 struct LbaBatch {
     int n;

@@ -966,7 +966,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
     std::vector<long long> off(n);
     // work tables: edge chunks, landmark chunks, keyframe tasks, pose-pair (+ bs) tasks per problem
-    std::vector<int2> ec, lc, kt, pt;
+    std::vector<int2> ec, lc, kt, pt, qt;
     size_t total = 0;
     for (int i = 0; i < n; i++) {
         const spslam_lba_problem& p = problems[i];
@@ -984,6 +984,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         for (int k = 0; k < p.n_kf; k++) kt.push_back(int2{i, k});
         const int npmax = p.n_kf;  // bound on the free poses; surplus tasks exit on the device
         for (int q = 0; q < npmax * (npmax + 1) / 2 + npmax; q++) pt.push_back(int2{i, q});
+        for (int q = 0; q < p.n_plane_obs; q += kLbaPlaneEdgesPerTask) qt.push_back(int2{i, p.n_point_obs + q});
     }
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
@@ -1003,11 +1004,12 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         c->lba_off_cap = n;
     }
     std::vector<int2> work;
-    work.reserve(ec.size() + lc.size() + kt.size() + pt.size() + 1);
+    work.reserve(ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + 1);
     work.insert(work.end(), ec.begin(), ec.end());
     work.insert(work.end(), lc.begin(), lc.end());
     work.insert(work.end(), kt.begin(), kt.end());
     work.insert(work.end(), pt.begin(), pt.end());
+    work.insert(work.end(), qt.begin(), qt.end());
     work.push_back(int2{0, 0});  // active counter
     if (work.size() > c->lba_work_cap) {
         HIP_CHECK(c, hipStreamSynchronize(s));
@@ -1032,7 +1034,8 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     C.delta_vp = (float)std::sqrt(cfg->vp_chi);
     const int2* w0 = c->d_lba_work;
     LbaWork W{w0, (int)ec.size(), w0 + ec.size(), (int)lc.size(), w0 + ec.size() + lc.size(), (int)kt.size(),
-              w0 + ec.size() + lc.size() + kt.size(), (int)pt.size()};
+              w0 + ec.size() + lc.size() + kt.size(), (int)pt.size(),
+              w0 + ec.size() + lc.size() + kt.size() + pt.size(), (int)qt.size()};
     LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
                (int*)(c->d_lba_work + work.size() - 1), d_stop_flags};
