@@ -15,7 +15,7 @@ KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels
 OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
 GPU_HDRS := $(wildcard $(CSRC)/*.h) include/spslam_gpu.h include/spslam_brief_pattern.inc
 
-all: $(PKG)/libspslam_gpu.so oracle/liboracle.so
+all: $(PKG)/libspslam_gpu.so oracle/liboracle.so tests/shim/libreference_shim.so
 
 $(OBJDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
 	@mkdir -p $(OBJDIR)
@@ -44,11 +44,16 @@ $(PROFDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 $(PKG)/libspslam_gpu_prof.so: $(PROF_OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(PROF_OBJS)
 
+# Reference-side shim (test infrastructure, INTEGRATION.md 1-7 compiled): plain g++ against the C ABI.
+tests/shim/libreference_shim.so: tests/shim/reference_shim.cpp tests/shim/cv_lite.h include/spslam_gpu.h $(PKG)/libspslam_gpu.so
+	g++ -O2 -std=c++17 -fPIC -shared -Wall -Wextra -o $@ tests/shim/reference_shim.cpp \
+	    -L$(PKG) -l:libspslam_gpu.so -Wl,-rpath,'$$ORIGIN/../../$(PKG)'
+
 oracle/liboracle.so:
 	$(MAKE) -C oracle liboracle.so
 
 clean:
-	rm -rf $(PKG)/libspslam_gpu.so $(PKG)/libspslam_gpu_prof.so $(OBJDIR) $(PROFDIR)
+	rm -rf $(PKG)/libspslam_gpu.so $(PKG)/libspslam_gpu_prof.so tests/shim/libreference_shim.so $(OBJDIR) $(PROFDIR)
 	$(MAKE) -C oracle clean
 
 .PHONY: all clean prof oracle/liboracle.so
