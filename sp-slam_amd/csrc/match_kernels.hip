@@ -229,13 +229,63 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             blocking = P[i].n_obs > 0;
             pangle = P[i].angle;
         }
-        // ... then the reference's loop walks the 64 points in order
+        // ... then the reference's loop over the 64 points, in passes: every point still to do takes the first of
+        // its 3 smallest keys whose keypoint is free; the points before the first one that cannot be decided
+        // that way -- all 3 keys taken (a window re-scan), or its keypoint taken by an earlier point of the pass
+        // that blocks it (a map point with observations) -- are committed together, in order; that point is
+        // then walked alone (the reference's step with the updated taken set) and the next pass starts after it.
         const int m = min(64, np - c0);
-        for (int L = 0; L < m; L++) {
-            if (!__shfl(valid, L)) continue;
-            // the best candidate not taken by an earlier point: the first of the 3 smallest keys whose keypoint
-            // is free, else (all 3 taken) a re-scan of the window
+        int start = 0;
+        while (start < m) {
+            uint32_t keyl = kNone;
+            int bl = -1;
+            float kangl = 0.f;
+            bool rescanl = false;
+            const bool act = lane >= start && lane < m && valid;
+            if (act) {
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    if (keyl != kNone || rescanl || best[q] == kNone) continue;
+                    if (!((taken[b[q] >> 5] >> (b[q] & 31)) & 1)) { keyl = best[q]; bl = b[q]; kangl = kang[q]; }
+                    else if (q == 2) rescanl = true;
+                }
+            }
+            const bool acc = act && !rescanl && keyl != kNone && (int)(keyl >> 20) <= kThHigh;
+            const bool accb = acc && blocking;
+            // conflicts with earlier blocking acceptances; the next later acceptance of the same keypoint
+            bool conflict = false;
+            int next_same = 64;
+            for (int j = start; j < m; j++) {
+                const int bj = __shfl(bl, j);
+                const int fj = __shfl((int)acc | ((int)accb << 1), j);
+                if (j < lane && (fj & 2) && bj == bl) conflict = true;
+                if (j > lane && (fj & 1) && bj == bl && next_same == 64) next_same = j;
+            }
+            const bool stop = act && (rescanl || (acc && conflict));
+            const unsigned long long sm = __ballot(stop);
+            const int first = sm ? __ffsll((long long)sm) - 1 : m;
+            const bool commit = acc && lane < first;
+            const unsigned long long cm = __ballot(commit);
+            int bin = 0;
+            if (commit) {
+                if (next_same >= first) M[bl] = c0 + lane;  // the last assignment of a keypoint wins, as in order
+                if (blocking) atomicOr(&taken[bl >> 5], 1u << (bl & 31));
+                if (check_ori) {
+                    float rot = __fsub_rn(pangle, kangl);
+                    if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
+                    bin = (int)roundf(__fmul_rn(rot, factor));
+                    if (bin == kHisto) bin = 0;
+                    atomicAdd(&hist[bin], 1);
+                }
+                PU[n_push + __popcll(cm & ((1ull << lane) - 1ull))] = make_int2(bl, bin);
+            }
+            n_push += __popcll(cm);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (first >= m) break;
+            // the point that stopped the pass, alone (the reference's step for it)
+            const int L = first;
             uint32_t bestL = kNone;
             int bL = -1;
             float kangL = 0.f;
@@ -272,24 +322,27 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
                     kangL = kun[bL].angle;
                 }
             }
+            start = L + 1;
             if (bestL == kNone || (int)(bestL >> 20) > kThHigh) continue;
             const int blockL = __shfl(blocking, L);
             const float pangL = __shfl(pangle, L);
             if (lane == 0) {
                 M[bL] = c0 + L;
                 if (blockL) taken[bL >> 5] |= 1u << (bL & 31);
-                int bin = 0;
+                int binL = 0;
                 if (check_ori) {
                     float rot = __fsub_rn(pangL, kangL);
                     if (rot < 0.0f) rot = __fadd_rn(rot, 360.0f);
-                    bin = (int)roundf(__fmul_rn(rot, factor));
-                    if (bin == kHisto) bin = 0;
-                    hist[bin]++;
+                    binL = (int)roundf(__fmul_rn(rot, factor));
+                    if (binL == kHisto) binL = 0;
+                    hist[binL]++;
                 }
-                PU[n_push] = make_int2(bL, bin);
+                PU[n_push] = make_int2(bL, binL);
             }
             n_push++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
     __syncthreads();
@@ -476,12 +529,55 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                 }
             }
         }
+        // the reference's loop in passes (as in match_assign_kernel): every point still to do evaluates its best
+        // and second best free keys from its 3 smallest; the points before the first one that cannot be decided
+        // that way -- a re-scan, or one of its two keypoints taken by an earlier acceptance of the pass -- are
+        // committed together; that point is walked alone and the next pass starts after it.
         const int m = min(64, np - c0);
-        for (int L = 0; L < m; L++) {
-            if (!__shfl(valid, L)) continue;
-            __builtin_amdgcn_wave_barrier();
+        auto ratio_ok = [&](uint32_t k1, uint32_t k2, int o1, int o2) {
+            const int bestDist = (int)(k1 >> 20), bestDist2 = k2 != kNone ? (int)(k2 >> 20) : 256;
+            const int bestLevel2 = k2 != kNone ? o2 : -1;
+            if (bestDist > kThHigh) return false;
+            return !(o1 == bestLevel2 && (float)bestDist > __fmul_rn(P.nn_ratio, (float)bestDist2));
+        };
+        int start = 0;
+        while (start < m) {
+            const bool act = lane >= start && lane < m && valid;
             uint32_t k1 = kNone, k2 = kNone;
-            int b1 = -1, o1 = -1, o2 = -1, nk = 0;
+            int b1 = -1, b2 = -1, o1 = -1, o2 = -1, nk = 0;
+            if (act) {
+#pragma unroll
+                for (int q = 0; q < 3; q++) {
+                    if (best[q] == kNone) continue;
+                    nk++;
+                    if ((taken[b[q] >> 5] >> (b[q] & 31)) & 1) continue;
+                    if (k1 == kNone) { k1 = best[q]; b1 = b[q]; o1 = oc[q]; }
+                    else if (k2 == kNone) { k2 = best[q]; b2 = b[q]; o2 = oc[q]; }
+                }
+            }
+            const bool rescanl = act && nk == 3 && k2 == kNone;
+            const bool acc = act && !rescanl && k1 != kNone && ratio_ok(k1, k2, o1, o2);
+            bool conflict = false;
+            for (int j = start; j < m; j++) {
+                const int bj = __shfl(b1, j), aj = __shfl((int)acc, j);
+                if (j < lane && aj && (bj == b1 || (b2 >= 0 && bj == b2))) conflict = true;
+            }
+            const bool stop = act && (rescanl || (k1 != kNone && conflict));
+            const unsigned long long sm = __ballot(stop);
+            const int first = sm ? __ffsll((long long)sm) - 1 : m;
+            const bool commit = acc && lane < first;
+            if (commit) {
+                M[b1] = c0 + lane;
+                atomicOr(&taken[b1 >> 5], 1u << (b1 & 31));
+            }
+            nm += __popcll(__ballot(commit));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (first >= m) break;
+            const int L = first;
+            start = L + 1;
+            k1 = kNone; k2 = kNone; b1 = -1; o1 = -1; o2 = -1; nk = 0;
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
@@ -533,17 +629,15 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                 o1 = b1 >= 0 ? kun[b1].octave : -1;
                 o2 = k2 != kNone ? kun[GI[k2 & 0xfffff]].octave : -1;
             }
-            if (k1 == kNone) continue;
-            const int bestDist = (int)(k1 >> 20), bestDist2 = k2 != kNone ? (int)(k2 >> 20) : 256;
-            const int bestLevel2 = k2 != kNone ? o2 : -1;
-            if (bestDist > kThHigh) continue;
-            if (o1 == bestLevel2 && (float)bestDist > __fmul_rn(P.nn_ratio, (float)bestDist2)) continue;
+            if (k1 == kNone || !ratio_ok(k1, k2, o1, o2)) continue;
             if (lane == 0) {
                 M[b1] = c0 + L;
                 taken[b1 >> 5] |= 1u << (b1 & 31);
             }
             nm++;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
     if (lane == 0) nmatches[f] = nm;
