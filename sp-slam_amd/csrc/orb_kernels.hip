@@ -293,9 +293,15 @@ __device__ __forceinline__ int level_of_cell(const OrbGeom& g, int cid) {
 // inside the cell), packed x | y << 12 | score << 24 with (x, y) relative to
 // (minBorderX, minBorderY) as at src/ORBextractor.cc:822-823.
 constexpr int kCellScoreMax = kCellWinMax - 6;
+// The cell's scores live in LDS with a zero frame (one row above and below, one column left, >= 2 right) and a
+// row pitch that is a multiple of 4: lane k evaluates the 4 pixels of group k (row-major groups of 4 columns)
+// from two aligned dword reads per row (the 3x3 neighbourhoods of 4 adjacent pixels span 6 columns), so
+// neither the bounds tests nor a per-pixel division remain; out-of-cell neighbours read the zero frame (the
+// reference's n < thr -> 0).  Candidates keep the reference's row-major order: (group, pixel) order.
+constexpr int kScPitchMax = ((kCellScoreMax + 3) & ~3) + 4, kScRowsMax = kCellScoreMax + 2;
 __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
                                                          uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
-    __shared__ uint8_t scs[4][kCellScoreMax * kCellScoreMax];
+    __shared__ __attribute__((aligned(16))) uint8_t scs[4][kScRowsMax * kScPitchMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cid = blockIdx.x * 4 + wave, f = blockIdx.y;
     if (cid >= g.cells_per_frame) return;
@@ -314,61 +320,88 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __
     const int maxY = min(iniY + L.hCell + 6, L.maxBorderY), maxX = min(iniX + L.wCell + 6, L.maxBorderX);
     const int R = maxY - iniY - 6, C = maxX - iniX - 6;
     const int npx = (R > 0 && C > 0) ? R * C : 0;
+    const int G = (C + 3) >> 2, P = 4 * G + 4;  // groups per row, LDS row pitch (score column c at byte c + 1)
     const uint8_t* smap = L.score + f * L.blur_frame_stride + (size_t)(iniY + 3) * L.bpitch + (iniX + 3);
+    uint32_t* sc32 = reinterpret_cast<uint32_t*>(sc);
+    for (int q = lane; q < ((R + 2) * P) >> 2; q += 64) sc32[q] = 0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const float invC = 1.f / (float)max(C, 1);   // p / C exactly for p < 2^12
     for (int p0 = 0; p0 < npx; p0 += 256) {
         uint8_t v[4];
+        int at[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int p = p0 + lane + 64 * k;
             v[k] = 0;
+            at[k] = -1;
             if (p < npx) {
                 const int r = (int)(((float)p + 0.5f) * invC), c = p - r * C;
                 v[k] = smap[(size_t)r * L.bpitch + c];
+                at[k] = (r + 1) * P + c + 1;
             }
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int p = p0 + lane + 64 * k;
-            if (p < npx) sc[p] = v[k];
-        }
+        for (int k = 0; k < 4; k++)
+            if (at[k] >= 0) sc[at[k]] = v[k];
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int ngroups = R * G;
+    const float invG = 1.f / (float)max(G, 1);
+    const unsigned long long lt = (1ull << lane) - 1ull;
     int base = 0;
     for (int pass = 0; pass < 2; pass++) {
         const int thr = pass == 0 ? iniTh : minTh;
         base = 0;
-        for (int p0 = 0; p0 < npx; p0 += 64) {
-            const int p = p0 + lane;
-            bool keep = false;
-            int r = 0, c = 0, s = 0;
-            if (p < npx) {
-                r = (int)(((float)p + 0.5f) * invC); c = p - r * C;
-                s = sc[p];
-                if (s >= thr) {
-                    keep = true;
+        for (int g0 = 0; g0 < ngroups; g0 += 64) {
+            const int gi = g0 + lane;
+            int keep[4] = {0, 0, 0, 0}, sv[4] = {0, 0, 0, 0}, r = 0, c0 = 0;
+            if (gi < ngroups) {
+                r = (int)(((float)gi + 0.5f) * invG);
+                c0 = (gi - r * G) * 4;
+                int b[3][6];  // rows r-1, r, r+1; score columns c0-1 .. c0+4
 #pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
+                for (int y = 0; y < 3; y++) {
+                    const uint32_t* rowp = reinterpret_cast<const uint32_t*>(sc + (r + y) * P + c0);
+                    const uint32_t lo = rowp[0], hi = rowp[1];
 #pragma unroll
-                        for (int dx = -1; dx <= 1; dx++) {
-                            if (!dy && !dx) continue;
-                            const int rr = r + dy, cc = c + dx;
-                            int n = 0;
-                            if (rr >= 0 && rr < R && cc >= 0 && cc < C) n = sc[rr * C + cc];
-                            if (n < thr) n = 0;
-                            keep = keep && (s > n);
+                    for (int k = 0; k < 6; k++) b[y][k] = (int)(((k < 4 ? lo : hi) >> (8 * (k & 3))) & 255u);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int s = b[1][j + 1];
+                    sv[j] = s;
+                    bool k = s >= thr && c0 + j < C;
+#pragma unroll
+                    for (int y = 0; y < 3; y++)
+#pragma unroll
+                        for (int x = 0; x < 3; x++) {
+                            if (y == 1 && x == 1) continue;
+                            const int n = b[y][j + x];
+                            k = k && (n < thr || s > n);
                         }
+                    keep[j] = k;
                 }
             }
-            const unsigned long long mask = __ballot(keep);
-            if (keep) {
-                const int pos = base + __popcll(mask & ((1ull << lane) - 1ull));
-                out[pos] = (uint32_t)(c + 3 + cj * L.wCell) | ((uint32_t)(r + 3 + ci * L.hCell) << 12) |
-                           ((uint32_t)s << 24);
+            unsigned long long m[4];
+            int before = 0, total = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                m[j] = __ballot(keep[j]);
+                before += __popcll(m[j] & lt);
+                total += __popcll(m[j]);
             }
-            base += __popcll(mask);
+            int pos = base + before;
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (keep[j]) {
+                    out[pos++] = (uint32_t)(c0 + j + 3 + cj * L.wCell) | ((uint32_t)(r + 3 + ci * L.hCell) << 12) |
+                                 ((uint32_t)sv[j] << 24);
+                }
+            base += total;
         }
         if (base > 0) break;
     }
