@@ -44,6 +44,25 @@ $(PROFDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 $(PKG)/libspslam_gpu_prof.so: $(PROF_OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(PROF_OBJS)
 
+# Measurement variants: make variant VARIANT=<name> VAR_FLAGS="-D..." -> sp-slam_amd/libspslam_gpu_<name>.so
+# (loaded via SPSLAM_GPU_LIB by tools/gpu_r02_variants.sh).
+VARIANT ?= var
+VAR_FLAGS ?=
+VARDIR := build/var_$(VARIANT)
+VAR_OBJS := $(addprefix $(VARDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+variant: $(PKG)/libspslam_gpu_$(VARIANT).so
+
+$(VARDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
+	@mkdir -p $(VARDIR)
+	$(HIPCC) $(HIPFLAGS) $(VAR_FLAGS) -c -o $@ $<
+
+$(VARDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
+	@mkdir -p $(VARDIR)
+	$(HIPCC) $(HIPFLAGS) $(VAR_FLAGS) -c -x hip -o $@ $<
+
+$(PKG)/libspslam_gpu_$(VARIANT).so: $(VAR_OBJS)
+	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(VAR_OBJS)
+
 # Reference-side shim (test infrastructure, INTEGRATION.md 1-7 compiled): plain g++ against the C ABI.
 tests/shim/libreference_shim.so: tests/shim/reference_shim.cpp tests/shim/cv_lite.h include/spslam_gpu.h $(PKG)/libspslam_gpu.so
 	g++ -O2 -std=c++17 -fPIC -shared -Wall -Wextra -o $@ tests/shim/reference_shim.cpp \
@@ -53,7 +72,7 @@ oracle/liboracle.so:
 	$(MAKE) -C oracle liboracle.so
 
 clean:
-	rm -rf $(PKG)/libspslam_gpu.so $(PKG)/libspslam_gpu_prof.so tests/shim/libreference_shim.so $(OBJDIR) $(PROFDIR)
+	rm -rf $(PKG)/libspslam_gpu*.so build/var_* tests/shim/libreference_shim.so $(OBJDIR) $(PROFDIR)
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean prof oracle/liboracle.so
+.PHONY: all clean prof variant oracle/liboracle.so

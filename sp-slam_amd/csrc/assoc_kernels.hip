@@ -199,6 +199,7 @@ __global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_asso
     const int n = na + nb, P = S.cap_a + S.cap_b, nm = F.n_map;
     float* D = lds;
     float* pm_s = lds + (size_t)P * max_map;
+#pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
     for (int i = t; i < n; i += kThreads) world_coeff(F.Tcw, coef_of(S, f, i, na), pm_s + 4 * i);
     __syncthreads();
     for (int j = w; j < nm; j += kWaves) {
@@ -213,7 +214,8 @@ __global__ __launch_bounds__(kThreads) void assoc_fused_kernel(const spslam_asso
             for (int q = 0; q < kGroup; q++) {
                 const int i = min(i0 + q, n - 1);
 #pragma unroll
-                for (int k = 0; k < 4; k++) pmr[q][k] = pm_s[4 * i + k];
+                for (int k = 0; k < 4; k++)  // wave-uniform: held in scalar registers
+                    pmr[q][k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(pm_s[4 * i + k])));
                 const float angle = dot3(pmr[q], M.world);
                 pass[q] = i0 + q < n && (angle > Pm.angle_th || angle < -Pm.angle_th);
                 mn[q] = 100.f;  // PointDistanceFromPlane: res = 100

@@ -170,6 +170,8 @@ struct Shared {
     double perr[kPlaneChunk][13][3];  // plane errors at the 12 perturbed poses and at T
     double perrB[kPlaneChunk][kSpec][3];  // plane errors at the trial poses of the last pass B
     double perrT[kPlaneChunk][3];     // plane errors at the accepted trial pose = the next iteration's T
+    double hb[kWaves][kRed];
+    SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)          // each wave's copy of the iteration's H (upper, 21) and b (6), slot 0 unused
     SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
 };
 
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
     int buf = 0;
     bool robust = true;
     int nBad = 0, total_its = 0;
-    SE3 T = T0, Tlast = T0;
+    SE3 T;
     for (int round = 0; round < 4; round++) {
         PROF_MARK(0);  // setup / previous relabel
         T = T0;
@@ -431,27 +433,26 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                 }
                 PROF_MARK(2);  // pass A plane edges
                 wg_sum(v, S, buf);
-                Tlast = T;
                 double currentChi = v[0];
                 const double iniChi = currentChi;
-                double H[6][6], b[6];
-                {
-                    int k = 1;
+                // H and b wait in LDS (one copy per wave, written by its lane 0) for the trial passes: kept in
+                // registers they would stay live across pass B
+                double* hbw = S.hb[t >> 6];
+                if (lane == 0) {
 #pragma unroll
-                    for (int i = 0; i < 6; i++)
-#pragma unroll
-                        for (int j = i; j < 6; j++, k++) H[i][j] = H[j][i] = v[k];
-#pragma unroll
-                    for (int i = 0; i < 6; i++) b[i] = v[22 + i];
+                    for (int k = 1; k < kRed; k++) hbw[k] = v[k];
                 }
                 if (it == 0) {
                     double md = 0;
 #pragma unroll
-                    for (int j = 0; j < 6; j++) md = fmax(fabs(H[j][j]), md);
+                    for (int j = 0; j < 6; j++) md = fmax(fabs(v[1 + j * 6 - j * (j - 1) / 2]), md);
                     lambda = 1e-5 * md;
                     ni = 2;
                     lmBad = 0;
                 }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 PROF_MARK(3);  // reduce A + iteration setup
                 // ---- damping trials, kSpec per pass over the edges
                 double rho = 0;
@@ -462,6 +463,16 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                     double lam = lambda, nq = ni;
                     const int myq = lane % kSpec;
                     for (int q = 0; q < myq; q++) { lam *= nq; nq *= 2; }
+                    double H[6][6], b[6];
+                    {
+                        int k = 1;
+#pragma unroll
+                        for (int i = 0; i < 6; i++)
+#pragma unroll
+                            for (int j = i; j < 6; j++, k++) H[i][j] = H[j][i] = hbw[k];
+#pragma unroll
+                        for (int i = 0; i < 6; i++) b[i] = hbw[22 + i];
+                    }
                     double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten (rejected step)
                     const bool ok = ldlt_solve(H, lam, b, x);
                     const SE3 Tt = se3_mul(se3_exp(x), T);
@@ -534,11 +545,11 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                     PROF_MARK(5);  // pass B (trial chi2)
                     wg_sum(c, S, buf);
                     // the reference's accept / reject sequence over the evaluated trials
-                    int acc = -1;
+                    int acc = -1, lastq = 0;
 #pragma unroll
                     for (int q = 0; q < kSpec; q++) {
                         if (more) {
-                            Tlast = Tq[q];  // the last computeActiveErrors
+                            lastq = q;  // the last computeActiveErrors
                             const double tempChi = okq[q] ? c[q] : 1.7976931348623157e308;
                             double r = currentChi - tempChi;
                             r /= sc[q];
@@ -558,6 +569,13 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                             qmax++;
                             more = rho < 0 && qmax < kMaxTrials;
                         }
+                    }
+                    if (lane == 0) {
+                        SE3 tl = Tq[0];
+#pragma unroll
+                        for (int q = 1; q < kSpec; q++)
+                            if (q == lastq) tl = Tq[q];
+                        S.tlast[t >> 6] = tl;
                     }
                     tValid = tValid || acc >= 0;
                     if (acc >= 0 && t < nl && nl <= kPlaneChunk) {  // thread t reads perrT[t] in the next pass A
@@ -582,6 +600,11 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         }
         // ---- relabel (:925-1140): active edges keep the errors of the last trial pose, outliers are
         // recomputed at the optimized pose
+        // (with no active edge every edge takes T and tlast is not read)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const SE3 Tlast = S.tlast[t >> 6];
         double bad = 0;
         for (int e = t; e < ne; e += kThreads) {
             double info[3], delta, err[3] = {0, 0, 0};
