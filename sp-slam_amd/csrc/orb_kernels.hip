@@ -33,29 +33,35 @@ __device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v
 // ---------------------------------------------------------------------------
 // FAST-9/16.  Score = max over the 16 contiguous 9-arcs of min(v - x) and of
 // min(x - v), minus 1; equals OpenCV cornerScore<16> for every corner, and
-// "corner at threshold t" <=> score >= t.
+// "corner at threshold t" <=> score >= t.  Since min over an arc of v - x is
+// v - max x and max of v - x is v - min x, the score is
+//   max(v - min_k max_arc(k) x, max_k min_arc(k) x - v) - 1,
+// and both arc extremes come from one packed u16 minimum chain over the
+// pairs (255 - x, x) (min of 255 - x = 255 - max x): 16 mads to pack, 64
+// packed minima, 16 packed maxima.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ u16x2 pmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+__device__ __forceinline__ u16x2 pmax(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+__device__ __forceinline__ u16x2 psubs(u16x2 a, u16x2 b) { return __builtin_elementwise_sub_sat(a, b); }
+
 __device__ __forceinline__ int fast_score(const uint8_t* p, int P) {
     const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * P];       d[1] = v - p[3 * P + 1];   d[2] = v - p[2 * P + 2];  d[3] = v - p[P + 3];
-    d[4] = v - p[3];           d[5] = v - p[-P + 3];      d[6] = v - p[-2 * P + 2]; d[7] = v - p[-3 * P + 1];
-    d[8] = v - p[-3 * P];      d[9] = v - p[-3 * P - 1];  d[10] = v - p[-2 * P - 2]; d[11] = v - p[-P - 3];
-    d[12] = v - p[-3];         d[13] = v - p[P - 3];      d[14] = v - p[2 * P - 2]; d[15] = v - p[3 * P - 1];
-    int mn2[16], mx2[16];
+    const int off[16] = {3 * P,  3 * P + 1,  2 * P + 2,  P + 3,  3,  -P + 3, -2 * P + 2, -3 * P + 1,
+                         -3 * P, -3 * P - 1, -2 * P - 2, -P - 3, -3, P - 3,  2 * P - 2,  3 * P - 1};
+    u16x2 X[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) { mn2[k] = min(d[k], d[(k + 1) & 15]); mx2[k] = max(d[k], d[(k + 1) & 15]); }
-    int mn4[16], mx4[16];
+    for (int k = 0; k < 16; k++) X[k] = as_u16x2((uint32_t)p[off[k]] * 65535u + 255u);  // (255 - x, x)
+    u16x2 m2[16], m4[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) { mn4[k] = min(mn2[k], mn2[(k + 2) & 15]); mx4[k] = max(mx2[k], mx2[(k + 2) & 15]); }
-    int best = -1000, worst = 1000;
+    for (int k = 0; k < 16; k++) m2[k] = pmin(X[k], X[(k + 1) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int mn9 = min(min(mn4[k], mn4[(k + 4) & 15]), d[(k + 8) & 15]);
-        const int mx9 = max(max(mx4[k], mx4[(k + 4) & 15]), d[(k + 8) & 15]);
-        best = max(best, mn9);
-        worst = min(worst, mx9);
-    }
-    return max(best, -worst) - 1;
+    for (int k = 0; k < 16; k++) m4[k] = pmin(m2[k], m2[(k + 2) & 15]);
+    u16x2 M = as_u16x2(0u);
+#pragma unroll
+    for (int k = 0; k < 16; k++) M = pmax(M, pmin(pmin(m4[k], m4[(k + 4) & 15]), X[(k + 8) & 15]));
+    return max(v + (int)M.x - 255, (int)M.y - v) - 1;
 }
 
 
@@ -69,7 +75,12 @@ __device__ __forceinline__ int fast_score(const uint8_t* p, int P) {
 //   * GaussianBlur 7x7 sigma 2 (:1085-1086), OpenCV's bit-exact 8U fixed point:
 //     out = (sum_ij k_i k_j p + 2^15) >> 16 with k = [18,34,48,56,48,34,18];
 //   * the FAST score map (0 where no cell window evaluates a pixel).
+// The tile is built and read 4 pixels (one dword) at a time: dword global loads realigned with
+// v_alignbyte, the resize's byte pairs picked with v_perm and weighted with v_dot2_u32_u16, the
+// horizontal blur as two v_dot4_u32_u8 per output, the FAST pre-test on packed u16 pairs.
 constexpr int kLH = kLevelTileH + 6, kLW = kLevelTileW + 6;
+constexpr int kLG = (kLW + 3) / 4;   // 4-column groups of a tile row (the last holds 2 pad columns)
+constexpr int kTinPitch = 4 * kLG;   // 72: dword-aligned rows
 constexpr int kLevelThreads = 256;
 
 // BORDER_REFLECT_101 for positions at most one image length outside (tiles
@@ -108,23 +119,46 @@ __device__ __forceinline__ RzCol resize_coef(double s, int d, int slen, bool hor
     }
     return r;
 }
+// The vertical step of the resize for one destination pixel from its two horizontally interpolated rows.
+__device__ __forceinline__ uint32_t resize_v(const RzCol& cy, int r0, int r1) {
+    return (uint32_t)((((cy.a0 * (r0 >> 4)) >> 16) + ((cy.a1 * (r1 >> 4)) >> 16) + 2) >> 2) & 255u;
+}
 
-// Necessary condition for a FAST-9 corner at threshold t: some 9-arc contains
-// two consecutive compass pixels (0, 4, 8, 12), both brighter or both darker.
-// v = centre; c0 = p[3P], c4 = p[3], c8 = p[-3P], c12 = p[-3].
-__device__ __forceinline__ bool fast_maybe_v(int v, int c0, int c4, int c8, int c12, int t) {
-    const int hi = v + t, lo = v - t;
-    const int b = (c0 > hi) | ((c4 > hi) << 1) | ((c8 > hi) << 2) | ((c12 > hi) << 3);
-    const int k = (c0 < lo) | ((c4 < lo) << 1) | ((c8 < lo) << 2) | ((c12 < lo) << 3);
-    const int br = b & ((b >> 1) | (b << 3));
-    const int dk = k & ((k >> 1) | (k << 3));
-    return (br | dk) & 15;
+// A 4-column group of the resized tile whose 8 source bytes per row lie in one window sb..sb+7 (sb = the
+// first column's left source): the window is read as 3 aligned dwords from a = sb & ~3, realigned by
+// s = sb & 3; sel[j] picks (x0_j, x1_j) of column j into a u16 pair for v_dot2 with coef[j] = (a0, a1).
+// a < 0: the group is gathered per pixel (reflected / clamped border columns, unaligned source rows).
+struct RzGroup { int a, s; uint32_t sel[4], coef[4]; };
+
+// FAST pre-test for 4 pixels at once (byte j of each word = pixel j; c0 = p[3P], c4 = p[3], c8 = p[-3P],
+// c12 = p[-3]): bit j set when some 9-arc may hold pixel j's corner at threshold t, i.e. two consecutive
+// compass pixels are both brighter than v + t or both darker than v - t.  Saturated u16 differences
+// are non-zero exactly when the comparison holds.
+__device__ __forceinline__ uint32_t fast_maybe4(uint32_t V, uint32_t C0, uint32_t C4, uint32_t C8, uint32_t C12,
+                                                uint32_t t2) {
+    uint32_t res = 0;
+#pragma unroll
+    for (int hh = 0; hh < 2; hh++) {  // pixels hh (low half) and hh + 2 (high half)
+        auto half = [&](uint32_t x) { return as_u16x2((x >> (8 * hh)) & 0x00ff00ffu); };
+        const u16x2 v = half(V), t = as_u16x2(t2);
+        const u16x2 hi = v + t, lo = psubs(v, t);
+        const u16x2 c0 = half(C0), c4 = half(C4), c8 = half(C8), c12 = half(C12);
+        const u16x2 b0 = psubs(c0, hi), b4 = psubs(c4, hi), b8 = psubs(c8, hi), b12 = psubs(c12, hi);
+        const u16x2 k0 = psubs(lo, c0), k4 = psubs(lo, c4), k8 = psubs(lo, c8), k12 = psubs(lo, c12);
+        const u16x2 br = pmax(pmax(pmin(b0, b4), pmin(b4, b8)), pmax(pmin(b8, b12), pmin(b12, b0)));
+        const u16x2 dk = pmax(pmax(pmin(k0, k4), pmin(k4, k8)), pmax(pmin(k8, k12), pmin(k12, k0)));
+        const uint32_t m = as_u32(pmax(br, dk));
+        res |= ((m & 0xffffu) ? 1u : 0u) << hh;
+        res |= ((m >> 16) ? 1u : 0u) << (hh + 2);
+    }
+    return res;
 }
 
 __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
-    __shared__ __attribute__((aligned(16))) uint8_t tin[kLH][kLW + 2];  // row pitch 72: dword-aligned rows
+    __shared__ __attribute__((aligned(16))) uint8_t tin[kLH][kTinPitch];
     __shared__ __attribute__((aligned(16))) uint16_t th[kLH][kLevelTileW];
-    __shared__ RzCol rx[kLW], ry[kLH];
+    __shared__ RzCol rx[kTinPitch], ry[kLH];
+    __shared__ RzGroup rg[kLG];
     __shared__ uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
     __shared__ __attribute__((aligned(16))) uint8_t stile[kLevelTileH][kLevelTileW];  // FAST scores of the tile
     const LevelGeom& L = g.lv[l];
@@ -132,51 +166,135 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
     const int x0 = (blockIdx.x % L.tiles_x) * kLevelTileW, y0 = (blockIdx.x / L.tiles_x) * kLevelTileH;
     const int w = L.w, h = L.h;
     uint8_t* img = const_cast<uint8_t*>(L.img) + f * L.frame_stride;
-    constexpr int kN = kLH * kLW, kIter = (kN + kLevelThreads - 1) / kLevelThreads;
+    constexpr int kNG = kLH * kLG, kIterG = (kNG + kLevelThreads - 1) / kLevelThreads;
     if (l == 0) {
-        uint8_t v[kIter];
+        // interior tiles: the 72 bytes x0-4 .. x0+67 of each row as aligned dwords, shifted by one byte
+        if (x0 >= 4 && x0 + kTinPitch <= w && ((reinterpret_cast<uintptr_t>(img) | (uintptr_t)L.stride) & 3) == 0) {
+            uint32_t lo[kIterG], hi[kIterG];
 #pragma unroll
-        for (int k = 0; k < kIter; k++) {
-            const int q = t + k * kLevelThreads;
-            v[k] = 0;
-            if (q < kN) {
-                const int r = q / kLW, c = q - r * kLW;
-                const int y = reflect1(y0 + r - 3, h), x = reflect1(min(x0 + c - 3, w + 2), w);
-                v[k] = img[(size_t)y * L.stride + x];
+            for (int k = 0; k < kIterG; k++) {
+                const int q = t + k * kLevelThreads;
+                lo[k] = hi[k] = 0;
+                if (q < kNG) {
+                    const int r = q / kLG, m = q - r * kLG;
+                    const uint32_t* row = reinterpret_cast<const uint32_t*>(
+                        img + (size_t)reflect1(y0 + r - 3, h) * L.stride + (x0 - 4));
+                    lo[k] = row[m];
+                    hi[k] = row[m + 1];
+                }
             }
-        }
 #pragma unroll
-        for (int k = 0; k < kIter; k++) {
-            const int q = t + k * kLevelThreads;
-            if (q < kN) tin[q / kLW][q % kLW] = v[k];
+            for (int k = 0; k < kIterG; k++) {
+                const int q = t + k * kLevelThreads;
+                if (q < kNG) {
+                    const int r = q / kLG, m = q - r * kLG;
+                    *reinterpret_cast<uint32_t*>(&tin[r][4 * m]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], 1);
+                }
+            }
+        } else {
+            constexpr int kN = kLH * kLW, kIter = (kN + kLevelThreads - 1) / kLevelThreads;
+            uint8_t v[kIter];
+#pragma unroll
+            for (int k = 0; k < kIter; k++) {
+                const int q = t + k * kLevelThreads;
+                v[k] = 0;
+                if (q < kN) {
+                    const int r = q / kLW, c = q - r * kLW;
+                    const int y = reflect1(y0 + r - 3, h), x = reflect1(min(x0 + c - 3, w + 2), w);
+                    v[k] = img[(size_t)y * L.stride + x];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kIter; k++) {
+                const int q = t + k * kLevelThreads;
+                if (q < kN) tin[q / kLW][q % kLW] = v[k];
+            }
         }
     } else {
         const LevelGeom& S = g.lv[l - 1];
         const uint8_t* src = S.img + f * S.frame_stride;
-        if (t < kLW) rx[t] = resize_coef(L.rscale_x, reflect1(min(x0 + t - 3, w + 2), w), S.w, true);
-        else if (t < kLW + kLH) ry[t - kLW] = resize_coef(L.rscale_y, reflect1(y0 + (t - kLW) - 3, h), S.h, false);
-        __syncthreads();
-        int v[kIter];
+        if (t < kLG) {
+            RzCol cx[4];
 #pragma unroll
-        for (int k = 0; k < kIter; k++) {
+            for (int j = 0; j < 4; j++) {
+                const int c = 4 * t + j;
+                cx[j] = resize_coef(L.rscale_x, reflect1(min(x0 + c - 3, w + 2), w), S.w, true);
+                rx[c] = cx[j];
+            }
+            const int sb = cx[0].x0, a = sb & ~3;
+            bool ok = a + 12 <= S.stride && ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)S.stride) & 3) == 0;
+            RzGroup G;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int o0 = cx[j].x0 - sb, o1 = cx[j].x1 - sb;
+                ok = ok && o0 >= 0 && o0 <= 7 && o1 >= 0 && o1 <= 7;
+                G.sel[j] = (uint32_t)(o0 & 7) | 0x0c00u | ((uint32_t)(o1 & 7) << 16) | 0x0c000000u;
+                G.coef[j] = (uint32_t)(uint16_t)cx[j].a0 | ((uint32_t)(uint16_t)cx[j].a1 << 16);
+            }
+            G.a = ok ? a : -1;
+            G.s = sb & 3;
+            rg[t] = G;
+        } else if (t >= 64 && t < 64 + kLH) {
+            ry[t - 64] = resize_coef(L.rscale_y, reflect1(y0 + (t - 64) - 3, h), S.h, false);
+        }
+        __syncthreads();
+        typedef unsigned short u16v2 __attribute__((ext_vector_type(2)));
+        auto dot2 = [](uint32_t a, uint32_t b) {
+            return (int)__builtin_amdgcn_udot2(__builtin_bit_cast(u16v2, a), __builtin_bit_cast(u16v2, b), 0u, false);
+        };
+        uint32_t wv[kIterG][6];
+#pragma unroll
+        for (int k = 0; k < kIterG; k++) {
             const int q = t + k * kLevelThreads;
-            v[k] = 0;
-            if (q < kN) {
-                const int r = q / kLW, c = q - r * kLW;
-                const RzCol cx = rx[c], cy = ry[r];
-                const uint8_t* r0p = src + (size_t)cy.x0 * S.stride;
-                const uint8_t* r1p = src + (size_t)cy.x1 * S.stride;
-                const int r0 = r0p[cx.x0] * cx.a0 + r0p[cx.x1] * cx.a1;
-                const int r1 = r1p[cx.x0] * cx.a0 + r1p[cx.x1] * cx.a1;
-                v[k] = (((cy.a0 * (r0 >> 4)) >> 16) + ((cy.a1 * (r1 >> 4)) >> 16) + 2) >> 2;
+#pragma unroll
+            for (int i = 0; i < 6; i++) wv[k][i] = 0;
+            if (q < kNG) {
+                const int r = q / kLG, m = q - r * kLG;
+                const int a = rg[m].a;
+                if (a >= 0) {
+                    const RzCol cy = ry[r];
+                    const uint32_t* p0 = reinterpret_cast<const uint32_t*>(src + (size_t)cy.x0 * S.stride + a);
+                    const uint32_t* p1 = reinterpret_cast<const uint32_t*>(src + (size_t)cy.x1 * S.stride + a);
+                    wv[k][0] = p0[0]; wv[k][1] = p0[1]; wv[k][2] = p0[2];
+                    wv[k][3] = p1[0]; wv[k][4] = p1[1]; wv[k][5] = p1[2];
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < kIter; k++) {
+        for (int k = 0; k < kIterG; k++) {
             const int q = t + k * kLevelThreads;
-            if (q < kN) {
-                const int r = q / kLW, c = q - r * kLW;
-                tin[r][c] = (uint8_t)v[k];
+            if (q < kNG) {
+                const int r = q / kLG, m = q - r * kLG;
+                const RzGroup& G = rg[m];
+                const RzCol cy = ry[r];
+                uint32_t packed = 0;
+                if (G.a >= 0) {
+                    const uint32_t s = (uint32_t)G.s;
+                    const uint32_t a0 = __builtin_amdgcn_alignbyte(wv[k][1], wv[k][0], s);
+                    const uint32_t a1 = __builtin_amdgcn_alignbyte(wv[k][2], wv[k][1], s);
+                    const uint32_t b0 = __builtin_amdgcn_alignbyte(wv[k][4], wv[k][3], s);
+                    const uint32_t b1 = __builtin_amdgcn_alignbyte(wv[k][5], wv[k][4], s);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int r0 = dot2(__builtin_amdgcn_perm(a1, a0, G.sel[j]), G.coef[j]);
+                        const int r1 = dot2(__builtin_amdgcn_perm(b1, b0, G.sel[j]), G.coef[j]);
+                        packed |= resize_v(cy, r0, r1) << (8 * j);
+                    }
+                } else {
+                    const uint8_t* r0p = src + (size_t)cy.x0 * S.stride;
+                    const uint8_t* r1p = src + (size_t)cy.x1 * S.stride;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int c = 4 * m + j;
+                        if (c < kLW) {
+                            const RzCol cx = rx[c];
+                            const int r0 = r0p[cx.x0] * cx.a0 + r0p[cx.x1] * cx.a1;
+                            const int r1 = r1p[cx.x0] * cx.a0 + r1p[cx.x1] * cx.a1;
+                            packed |= resize_v(cy, r0, r1) << (8 * j);
+                        }
+                    }
+                }
+                *reinterpret_cast<uint32_t*>(&tin[r][4 * m]) = packed;
             }
         }
     }
@@ -188,37 +306,33 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
             const int r = rb + lr;
             if (y0 + r < h) {
-                const uint8_t* p = &tin[r + 3][lc + 3];
-                const uint32_t v = (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
-                                   ((uint32_t)p[3] << 24);
-                *reinterpret_cast<uint32_t*>(img + (size_t)(y0 + r) * L.stride + (x0 + lc)) = v;
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(&tin[r + 3][lc]);
+                *reinterpret_cast<uint32_t*>(img + (size_t)(y0 + r) * L.stride + (x0 + lc)) =
+                    __builtin_amdgcn_alignbyte(p[1], p[0], 3);
             }
         }
     }
-    // horizontal blur pass over all tile rows, 4 outputs per lane from three dword LDS reads (bytes c..c+11)
+    // horizontal blur pass over all tile rows, 4 outputs per lane: bytes c..c+11 from three dword LDS reads,
+    // output j = dot4(bytes j..j+3, k0..k3) + dot4(bytes j+4..j+7, k4, k5, k6, 0)
     for (int q = t; q < kLH * (kLevelTileW / 4); q += kLevelThreads) {
         const int r = q / (kLevelTileW / 4), c = (q - r * (kLevelTileW / 4)) * 4;
         const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&tin[r][c]);
         const uint32_t a = w3[0], b = w3[1], d = w3[2];
-        int p[10];
+        constexpr uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
+        uint32_t o[4];
+        o[0] = __builtin_amdgcn_udot4(a, K0, __builtin_amdgcn_udot4(b, K1, 0u, false), false);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            p[k] = (a >> (8 * k)) & 255;
-            p[4 + k] = (b >> (8 * k)) & 255;
-        }
-        p[8] = d & 255;
-        p[9] = (d >> 8) & 255;
-        uint16_t o[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            o[j] = (uint16_t)(18 * (p[j] + p[j + 6]) + 34 * (p[j + 1] + p[j + 5]) + 48 * (p[j + 2] + p[j + 4]) +
-                              56 * p[j + 3]);
-        *reinterpret_cast<uint2*>(&th[r][c]) = *reinterpret_cast<const uint2*>(o);
+        for (int j = 1; j < 4; j++)
+            o[j] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, j), K0,
+                                          __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d, b, j), K1, 0u, false),
+                                          false);
+        *reinterpret_cast<uint2*>(&th[r][c]) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
     }
     __syncthreads();
     uint8_t* blur = L.blur + f * L.blur_frame_stride;
     uint8_t* score = L.score + f * L.blur_frame_stride;
     const int bp = L.bpitch;
+    const uint32_t t2 = (uint32_t)minTh | ((uint32_t)minTh << 16);
     // vertical blur pass, 4 pixels per lane (8-byte LDS reads of the row sums, one dword store); FAST
     // pre-test at the lowest threshold, candidates compacted per wave.  A wave owns tile rows
     // {4w..4w+3, 16+4w..16+4w+3}; their scores are assembled in LDS and stored as dwords by the same wave.
@@ -238,22 +352,20 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         if (y < h) *reinterpret_cast<uint32_t*>(blur + (size_t)y * bp + (x0 + lc)) = bw;
         *reinterpret_cast<uint32_t*>(&stile[r][lc]) = 0u;
         // the FAST pre-test's 5 pixels for the 4 centres (tin[r+3][lc+3+j]): centre row bytes lc..lc+11
-        // and rows r, r+6 bytes lc+3..lc+6, from 7 dword LDS reads
+        // and rows r, r+6 bytes lc+3..lc+6, from 7 dword LDS reads, realigned to one word per compass point
         const uint32_t* rc = reinterpret_cast<const uint32_t*>(&tin[r + 3][lc]);
         const uint32_t* ru = reinterpret_cast<const uint32_t*>(&tin[r][lc]);
         const uint32_t* rd = reinterpret_cast<const uint32_t*>(&tin[r + 6][lc]);
         const uint32_t c0w = rc[0], c1w = rc[1], c2w = rc[2];
-        const uint32_t u0 = ru[0], u1 = ru[1], d0 = rd[0], d1 = rd[1];
-        auto byte_at = [](uint32_t a, uint32_t b, uint32_t c, int k) {  // byte k of the 12-byte a|b|c
-            return (int)(((k < 4 ? a : (k < 8 ? b : c)) >> (8 * (k & 3))) & 255);
-        };
+        const uint32_t V = __builtin_amdgcn_alignbyte(c1w, c0w, 3);
+        const uint32_t CR = __builtin_amdgcn_alignbyte(c2w, c1w, 2);
+        const uint32_t CU = __builtin_amdgcn_alignbyte(ru[1], ru[0], 3);
+        const uint32_t CD = __builtin_amdgcn_alignbyte(rd[1], rd[0], 3);
+        const uint32_t mb = (y >= 3 && y < h - 3) ? fast_maybe4(V, CD, CR, CU, c0w, t2) : 0u;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const int x = x0 + lc + j;
-            const int v = byte_at(c0w, c1w, c2w, j + 3);
-            const int cu = byte_at(u0, u1, 0, j + 3), cd = byte_at(d0, d1, 0, j + 3);
-            const int cl = byte_at(c0w, c1w, c2w, j), cr = byte_at(c0w, c1w, c2w, j + 6);
-            const bool maybe = y >= 3 && y < h - 3 && x >= 3 && x < w - 3 && fast_maybe_v(v, cd, cr, cu, cl, minTh);
+            const bool maybe = ((mb >> j) & 1u) && x >= 3 && x < w - 3;
             const unsigned long long m = __ballot(maybe);
             if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(r * kLevelTileW + lc + j);
             ncand += __popcll(m);
@@ -265,7 +377,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
     for (int k = lane; k < ncand; k += 64) {
         const int q = cand[wave][k];
         const int r = q / kLevelTileW, c = q - r * kLevelTileW;
-        const int sc = max(fast_score(&tin[r + 3][c + 3], kLW + 2), 0);
+        const int sc = max(fast_score(&tin[r + 3][c + 3], kTinPitch), 0);
         stile[r][c] = (uint8_t)(sc >= minTh ? sc : 0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
