@@ -1001,14 +1001,11 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
 }
 
 // ---------------------------------------------------------------- reduced system
-__global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
-    extern __shared__ double lds[];
+// One body per storage (LDS or the problem's global scratch), so every access is a ds_* or global_* one
+// (a runtime pointer select would make them all flat).
+template <bool in_lds>
+__device__ __forceinline__ void factor_body(const Ctx& c, LbaCtl& k, double* lds, int n) {
     const int t = threadIdx.x;
-    Ctx c = make_ctx(b, blockIdx.x);
-    LbaCtl& k = *c.ctl;
-    if (k.state != kTrial) return;
-    const int n = 6 * k.np;
-    const bool in_lds = (size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds;
     double* A = in_lds ? lds : c.S;
     double* y = in_lds ? lds + (size_t)n * n : c.y;
     double* dd = in_lds ? y + n : c.dd;
@@ -1055,6 +1052,16 @@ __global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
             for (int i = t; i < n; i += kThreads) c.y[i] = y[i];
     }
     if (t == 0) k.ok = ok;
+}
+
+__global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
+    extern __shared__ double lds[];
+    Ctx c = make_ctx(b, blockIdx.x);
+    LbaCtl& k = *c.ctl;
+    if (k.state != kTrial) return;
+    const int n = 6 * k.np;
+    if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds) factor_body<true>(c, k, lds, n);
+    else factor_body<false>(c, k, lds, n);
 }
 
 // ---------------------------------------------------------------- update / restore

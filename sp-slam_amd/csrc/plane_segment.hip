@@ -221,9 +221,9 @@ __device__ __forceinline__ bool ptp_ok(const float* m, float x, float y, float z
     return fabsf(e) < 0.02f;
 }
 
-template <int K>
-__device__ __forceinline__ int sel(const int (&a)[K], int k) {
-    int v = 0;
+template <int K, class T>
+__device__ __forceinline__ T sel(const T (&a)[K], int k) {
+    T v = 0;
 #pragma unroll
     for (int j = 0; j < K; j++)
         if (j == k) v = a[j];
@@ -253,17 +253,16 @@ __device__ __forceinline__ int refine_pass(SegShared& S, uint8_t* state, const u
     // prefetch of the next row (its state is not touched by the current step)
     float qx[K], qy[K], qz[K];
     int qs[K];
+    // unconditional clamped loads, masked at use (see refine_rows)
 #define SPSLAM_REFINE_FETCH(STEP)                                                  \
     {                                                                              \
-        const int r_ = bw ? H - 1 - (STEP) : (STEP);                               \
+        const int st_ = min((STEP), H - 1);                                        \
+        const int r_ = bw ? H - 1 - st_ : st_;                                     \
         _Pragma("unroll") for (int k = 0; k < K; k++) {                            \
-            const int p = lane * K + k;                                            \
-            qs[k] = 0; qx[k] = qy[k] = qz[k] = 0.f;                                \
-            if (p < W && (STEP) < H) {                                             \
-                const int i = r_ * W + (bw ? W - 1 - p : p);                       \
-                qs[k] = state[i];                                                  \
-                qx[k] = X[i]; qy[k] = Y[i]; qz[k] = Z[i];                          \
-            }                                                                      \
+            const int p = min(lane * K + k, W - 1);                                \
+            const int i = r_ * W + (bw ? W - 1 - p : p);                           \
+            qs[k] = state[i];                                                      \
+            qx[k] = X[i]; qy[k] = Y[i]; qz[k] = Z[i];                              \
         }                                                                          \
     }
     SPSLAM_REFINE_FETCH(0)
@@ -274,8 +273,9 @@ __device__ __forceinline__ int refine_pass(SegShared& S, uint8_t* state, const u
         int vm = 0;
 #pragma unroll
         for (int k = 0; k < K; k++) {
-            s0[k] = qs[k]; px[k] = qx[k]; py[k] = qy[k]; pz[k] = qz[k];
-            if (lane * K + k < W && isfinite(px[k])) vm |= 1 << k;
+            const bool in = lane * K + k < W;
+            s0[k] = in ? qs[k] : 0; px[k] = in ? qx[k] : 0.f; py[k] = in ? qy[k] : 0.f; pz[k] = in ? qz[k] : 0.f;
+            if (in && isfinite(px[k])) vm |= 1 << k;
         }
         SPSLAM_REFINE_FETCH(step + 1)
         // neighbours across lanes: previous row at position p+1, current row at p-1 / position 0
@@ -403,51 +403,82 @@ __device__ __forceinline__ int refine_pass(SegShared& S, uint8_t* state, const u
 #undef SPSLAM_REFINE_FETCH
 }
 
-// Fast path (nmodel <= kFastModels = 14).  Before each pass every point gets
-// a 16-bit descriptor, computed in parallel: bits 0-13 = models whose plane is
-// within 0.02 m of the point (only for valid, still unlabelled points), bit 14
-// = its vertical source may grow it, bit 15 = its chain source may grow it
-// (source and source-neighbour validity, row limits of the reference loops);
-// stored as two byte planes.  The pass itself then only composes per-pixel
-// transfer functions, packed in 17 bits (bit 16 = constant; low 16 bits =
-// constant state, or the complement of the pass-through set, so 0 is the
-// identity) and scanned with DPP.  Which grow event produced each new label is
-// re-derived afterwards from the final states, in parallel, in the
-// reference's event order.
+// Fast paths (nmodel <= kFastModels = 14, or <= kWideModels = 30).  Before
+// each pass every point gets a descriptor, computed in parallel: one bit per
+// model whose plane is within 0.02 m of the point (only for valid, still
+// unlabelled points), an "act" bit (its vertical source may grow it) and a
+// "link" bit (its chain source may grow it) -- source and source-neighbour
+// validity, row limits of the reference loops.  Narrow: 16 bits (models 0-13,
+// act 14, link 15) in two byte planes; wide: one 32-bit word (models 0-29, act
+// 30, link 31).  The pass itself then only composes per-pixel transfer
+// functions (a constant flag; the constant state, or the complement of the
+// pass-through set, so 0 is the identity), scanned with DPP.  Which grow event
+// produced each new label is re-derived afterwards from the final states, in
+// parallel, in the reference's event order.
 constexpr int kFastModels = 14;
-constexpr int kFnConst = 0x10000;
-__device__ __forceinline__ int f8_pass(int f, int L) {  // f: complemented pass-through set
-    return (L > 0 && !((f >> ((L - 1) & 15)) & 1)) ? L : 0;
+constexpr int kWideModels = 30;
+template <bool kWide>
+struct Desc;
+template <>
+struct Desc<false> {
+    static constexpr uint32_t kAcc = 0x3FFFu, kAct = 0x4000u, kLink = 0x8000u;
+    static constexpr uint32_t kConst = 0x10000u, kVal = 0xFFFFu;  // transfer functions
+    uint8_t* lo;
+    uint8_t* hi;
+    __device__ __forceinline__ uint32_t get(int i) const { return lo[i] | ((uint32_t)hi[i] << 8); }
+    __device__ __forceinline__ void put(int i, uint32_t d) const {
+        lo[i] = (uint8_t)d;
+        hi[i] = (uint8_t)(d >> 8);
+    }
+};
+template <>
+struct Desc<true> {
+    static constexpr uint32_t kAcc = 0x3FFFFFFFu, kAct = 0x40000000u, kLink = 0x80000000u;
+    static constexpr uint32_t kConst = 0x80000000u, kVal = 0x3FFFFFFFu;
+    uint32_t* w;
+    __device__ __forceinline__ uint32_t get(int i) const { return w[i]; }
+    __device__ __forceinline__ void put(int i, uint32_t d) const { w[i] = d; }
+};
+
+template <class D>
+__device__ __forceinline__ uint32_t fn_pass(uint32_t f, uint32_t L) {  // f: complemented pass-through set
+    return (L > 0 && !((f >> ((L - 1) & 31)) & 1u)) ? L : 0u;
 }
-__device__ __forceinline__ int f8_then(int first, int second) {
-    const int through = kFnConst | f8_pass(second, first & 0xFFFF);
-    const int both = first | second;
-    const int r = (first & kFnConst) ? through : both;
-    return (second & kFnConst) ? second : r;
+template <class D>
+__device__ __forceinline__ uint32_t fn_then(uint32_t first, uint32_t second) {
+    const uint32_t through = D::kConst | fn_pass<D>(second, first & D::kVal);
+    const uint32_t both = first | second;
+    const uint32_t r = (first & D::kConst) ? through : both;
+    return (second & D::kConst) ? second : r;
 }
-__device__ __forceinline__ int f8_apply(int f, int L) {
-    return (f & kFnConst) ? (f & 0xFFFF) : f8_pass(f, L);
+template <class D>
+__device__ __forceinline__ uint32_t fn_apply(uint32_t f, uint32_t L) {
+    return (f & D::kConst) ? (f & D::kVal) : fn_pass<D>(f, L);
 }
-// Inclusive wave scan of f8_then (lane order), DPP row shifts + row broadcasts.
-__device__ __forceinline__ int f8_scan(int x) {
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true), x);  // row_shr:1
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true), x);  // row_shr:2
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true), x);  // row_shr:4
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true), x);  // row_shr:8
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false), x); // row_bcast:15
-    x = f8_then(__builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false), x); // row_bcast:31
+// Inclusive wave scan of fn_then (lane order), DPP row shifts + row broadcasts (0 = identity fills).
+template <class D>
+__device__ __forceinline__ uint32_t fn_scan(uint32_t x) {
+#define SPSLAM_DPP(V, CTRL, ROWS, BC) ((uint32_t)__builtin_amdgcn_update_dpp(0, (int)(V), CTRL, ROWS, 0xF, BC))
+    x = fn_then<D>(SPSLAM_DPP(x, 0x111, 0xF, true), x);   // row_shr:1
+    x = fn_then<D>(SPSLAM_DPP(x, 0x112, 0xF, true), x);   // row_shr:2
+    x = fn_then<D>(SPSLAM_DPP(x, 0x114, 0xF, true), x);   // row_shr:4
+    x = fn_then<D>(SPSLAM_DPP(x, 0x118, 0xF, true), x);   // row_shr:8
+    x = fn_then<D>(SPSLAM_DPP(x, 0x142, 0xA, false), x);  // row_bcast:15
+    x = fn_then<D>(SPSLAM_DPP(x, 0x143, 0xC, false), x);  // row_bcast:31
+#undef SPSLAM_DPP
     return x;
 }
 
-// Descriptor byte of point i for one pass (see above).
-__device__ __forceinline__ int refine_desc(const uint8_t* state, const float* X, const float* Y, const float* Z,
-                                           const float (*coef)[4], int nmodel, int W, int H, int i, bool bw) {
+// Descriptor of point i for one pass (see above).
+template <class D>
+__device__ __forceinline__ uint32_t refine_desc(const uint8_t* state, const float* X, const float* Y, const float* Z,
+                                                const float (*coef)[4], int nmodel, int W, int H, int i, bool bw) {
     if (state[i]) return 0;
     const float x = X[i], y = Y[i], z = Z[i];
     if (!isfinite(x)) return 0;
-    int acc = 0;
+    uint32_t acc = 0;
     for (int v = 0; v < nmodel; v++)
-        if (ptp_ok(coef[v], x, y, z)) acc |= 1 << v;
+        if (ptp_ok(coef[v], x, y, z)) acc |= 1u << v;
     if (!acc) return 0;
     const int r = i / W, c = i - r * W;
     bool act, link;
@@ -458,72 +489,86 @@ __device__ __forceinline__ int refine_desc(const uint8_t* state, const float* X,
         act = r <= H - 2 && isfinite(X[i + W]) && isfinite(X[i + W - 1]);
         link = (c <= W - 2 ? r >= 1 : r <= H - 2) && isfinite(X[i + 1]);
     }
-    return acc | (act ? 0x4000 : 0) | (link ? 0x8000 : 0);
+    return acc | (act ? D::kAct : 0u) | (link ? D::kLink : 0u);
 }
 
-template <int K>
-__device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc, const uint8_t* desc_hi,
-                                            const uint64_t* cbits, int W, int H, bool bw) {
+template <int K, class D>
+__device__ __forceinline__ void refine_rows(uint8_t* state, const D desc, const uint64_t* cbits, int W, int H,
+                                            bool bw) {
+    constexpr bool kWide = D::kAcc > 0xFFFFu;
     const int lane = threadIdx.x & 63;
     const int RW = (W + 63) >> 6;
     const int lastLane = (W - 1) / K, lastK = (W - 1) - lastLane * K;
-    int prevS[K];
+    uint32_t prevS[K];
 #pragma unroll
     for (int k = 0; k < K; k++) prevS[k] = 0;
-    int carry = 0;
-    int qs[K], qd[K];
+    uint32_t carry = 0;
+    // Next row's values, loaded unconditionally (positions past the row and the row after the last read a
+    // clamped in-range pixel and are masked at use) and kept raw until then, so the only wait for them is
+    // the one before their use one row later.
+    uint32_t qs[K], q0[K], q1[K];
+    uint64_t qc = 0;
 #define SPSLAM_FAST_FETCH(STEP)                                                    \
     {                                                                              \
-        const int r_ = bw ? H - 1 - (STEP) : (STEP);                               \
+        const int st_ = min((STEP), H - 1);                                        \
+        const int r_ = bw ? H - 1 - st_ : st_;                                     \
         _Pragma("unroll") for (int k = 0; k < K; k++) {                            \
-            const int p = lane * K + k;                                            \
-            qs[k] = 0; qd[k] = 0;                                                  \
-            if (p < W && (STEP) < H) {                                             \
-                const int i = r_ * W + (bw ? W - 1 - p : p);                       \
-                qs[k] = state[i];                                                  \
-                qd[k] = desc[i] | (desc_hi[i] << 8);                               \
+            const int p = min(lane * K + k, W - 1);                                \
+            const int i = r_ * W + (bw ? W - 1 - p : p);                           \
+            qs[k] = state[i];                                                      \
+            if constexpr (kWide) {                                                 \
+                q0[k] = desc.w[i];                                                 \
+            } else {                                                               \
+                q0[k] = desc.lo[i];                                                \
+                q1[k] = desc.hi[i];                                                \
             }                                                                      \
         }                                                                          \
+        qc = cbits[r_ * RW + min(lane, RW - 1)];                                   \
     }
     SPSLAM_FAST_FETCH(0)
     for (int step = 0; step < H; step++) {
         const int r = bw ? H - 1 - step : step;
-        int s0[K], d[K], fin[K];
+        uint32_t s0[K], d[K], fin[K];
 #pragma unroll
-        for (int k = 0; k < K; k++) { s0[k] = qs[k]; d[k] = qd[k]; }
+        for (int k = 0; k < K; k++) {
+            const bool in = lane * K + k < W;
+            s0[k] = in ? qs[k] : 0u;
+            if constexpr (kWide) d[k] = in ? q0[k] : 0u;
+            else d[k] = in ? (q0[k] | (q1[k] << 8)) : 0u;
+        }
+        // rows without a growable point keep their states (lanes < RW hold the row's candidate words)
+        const bool any = __ballot(lane < RW && qc != 0ull) != 0ull;
         SPSLAM_FAST_FETCH(step + 1)
-        uint64_t any = 0;
-        for (int w = 0; w < RW; w++) any |= cbits[r * RW + w];
         if (!any) {
 #pragma unroll
             for (int k = 0; k < K; k++) fin[k] = s0[k];
         } else {
-            int g[K];
+            uint32_t g[K];
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                const int acc = d[k] & 0x3FFF, U = prevS[k];
-                const bool grant = (d[k] & 0x4000) && U && ((acc >> ((U - 1) & 15)) & 1);
-                int e = (d[k] & 0x8000) ? (~acc & 0xFFFF) : kFnConst;
-                e = grant ? (kFnConst | U) : e;
-                e = acc ? e : kFnConst;
-                g[k] = s0[k] ? (kFnConst | s0[k]) : e;
+                const uint32_t acc = d[k] & D::kAcc, U = prevS[k];
+                const bool grant = (d[k] & D::kAct) && U && ((acc >> ((U - 1) & 31)) & 1u);
+                uint32_t e = (d[k] & D::kLink) ? (~acc & D::kVal) : D::kConst;
+                e = grant ? (D::kConst | U) : e;
+                e = acc ? e : D::kConst;
+                g[k] = s0[k] ? (D::kConst | s0[k]) : e;
             }
-            int F = g[0];
+            uint32_t F = g[0];
 #pragma unroll
-            for (int k = 1; k < K; k++) F = f8_then(F, g[k]);
-            F = f8_scan(F);
-            int ex = __shfl_up(F, 1);
+            for (int k = 1; k < K; k++) F = fn_then<D>(F, g[k]);
+            F = fn_scan<D>(F);
+            uint32_t ex = (uint32_t)__shfl_up((int)F, 1);
             if (lane == 0) ex = 0;
-            int L = f8_apply(ex, bw ? carry : 0);
+            uint32_t L = fn_apply<D>(ex, bw ? carry : 0u);
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                fin[k] = f8_apply(g[k], L);
+                fin[k] = fn_apply<D>(g[k], L);
                 L = fin[k];
                 const int p = lane * K + k;
                 if (p < W && s0[k] == 0 && fin[k] != 0) state[r * W + (bw ? W - 1 - p : p)] = (uint8_t)fin[k];
             }
         }
-        if (bw) carry = __shfl(sel<K>(fin, lastK), lastLane);
+        if (bw) carry = (uint32_t)__shfl((int)sel<K>(fin, lastK), lastLane);
 #pragma unroll
         for (int k = 0; k < K; k++) prevS[k] = fin[k];
     }
@@ -533,17 +578,18 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const uint8_t* desc,
 // Grow events of one finished fast pass, appended at ev[] in the reference's
 // order (sources in pass order; per source: along the row, then across rows).
 // Returns the number of events (uniform).
-__device__ int refine_events(SegShared& S, const uint8_t* state, const uint8_t* desc, const uint8_t* desc_hi, int W,
-                             int H, int N, bool bw, int* ev) {
+template <class D>
+__device__ __forceinline__ int refine_events(SegShared& S, const uint8_t* state, const D desc, int W, int H, int N,
+                                             bool bw, int* ev) {
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int M = (H - 1) * W;
     // how target j grew in this pass: 0 not, 1 along its row (chain), 2 from the other row
     auto how = [&](int j, int vsrc) -> int {
-        const int dj = desc[j] | (desc_hi[j] << 8);
-        if (!(dj & 0x3FFF) || !state[j]) return 0;
-        if (dj & 0x4000) {
+        const uint32_t dj = desc.get(j);
+        if (!(dj & D::kAcc) || !state[j]) return 0;
+        if (dj & D::kAct) {
             const int U = state[vsrc];
-            if (U && ((dj >> (U - 1)) & 1)) return 2;
+            if (U && ((dj >> (U - 1)) & 1u)) return 2;
         }
         return 1;
     };
@@ -603,7 +649,8 @@ __device__ __forceinline__ int nb_bits(const uint8_t* state, int W, int H, int x
 
 // Moore tracing from `start` (reference: findLabeledRegionBoundary); writes
 // at most cap indices, returns the full length.
-__device__ int trace_contour(const uint8_t* state, const uint8_t* nmask, int W, int H, int N, int start, int lab,
+// Inlined so the LDS instance walks with ds_read (a called function sees generic pointers: flat loads).
+__device__ __forceinline__ int trace_contour(const uint8_t* state, const uint8_t* nmask, int W, int H, int N, int start, int lab,
                              int32_t* out, int cap) {
     int cx = start % W, cy = start / W;
     const int ne = nb_bits(state, W, H, cx, cy, lab, false);
@@ -921,6 +968,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     }
     __syncthreads();
     const int nmodel = S.nmodel;
+    if (t == 0) ts[13] = nmodel;
     for (int i = t; i < N; i += kSegThreads) {
         const int s = state[i];
         if (s) state[i] = S.big_state[s];
@@ -929,34 +977,42 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     STAMP(7);
     // ---- K: refinement (two passes), one wave per pass
     uint64_t* cbits = hbits;  // rows with growable points (hbits no longer needed)
-    if (nmodel > 0 && nmodel <= kFastModels) {
-        uint8_t* desc = nmask;  // the contour masks come later
-        // descriptor high bytes: the covariance staging area (phase G is over) when the frame fits, else the
-        // rank scratch (dead since phase D)
-        uint8_t* desc_hi = (size_t)N <= sizeof(S.stage) ? (uint8_t*)&S.stage[0][0][0] : (uint8_t*)rankA;
+    // two passes over the fast-path descriptors (D: narrow or wide format)
+    auto fast_refine = [&](const auto desc) {
+        using D = decltype(desc);
         int ng = 0;
         for (int pass = 0; pass < 2; pass++) {
             const bool bw = pass == 1;
             for (int r = wave; r < H; r += kSegWaves)
                 for (int k = 0; k < RW; k++) {
                     const int c = (k << 6) + lane, i = r * W + c;
-                    int dsc = 0;
+                    uint32_t dsc = 0;
                     if (c < W) {
-                        dsc = refine_desc(state, X, Y, Z, S.model_coef, nmodel, W, H, i, bw);
-                        desc[i] = (uint8_t)dsc;
-                        desc_hi[i] = (uint8_t)(dsc >> 8);
+                        dsc = refine_desc<D>(state, X, Y, Z, S.model_coef, nmodel, W, H, i, bw);
+                        desc.put(i, dsc);
                     }
                     const uint64_t m = __ballot(dsc != 0);
                     if (lane == 0) cbits[r * RW + k] = m;
                 }
             __syncthreads();
             if (pass == 0) STAMP(10);
-            if (wave == 0) refine_rows<K>(state, desc, desc_hi, cbits, W, H, bw);
+            if (wave == 0) refine_rows<K>(state, desc, cbits, W, H, bw);
             __syncthreads();
             if (pass == 0) STAMP(11);
-            ng += refine_events(S, state, desc, desc_hi, W, H, N, bw, ev + ng);
+            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng);
         }
         if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
+    };
+    if (nmodel > 0 && nmodel <= kFastModels) {
+        // narrow descriptors: low bytes in the contour-mask map (the masks come later), high bytes in the
+        // covariance staging area (phase G is over) in the LDS instance (the host picks it only when
+        // N <= sizeof(S.stage)), else in the rank scratch (dead since phase D); fixed per instance so every
+        // access is a ds_* or global_* one, never flat
+        fast_refine(Desc<false>{nmask, kLdsMaps ? (uint8_t*)&S.stage[0][0][0] : (uint8_t*)rankA});
+    } else if (nmodel > 0 && nmodel <= kWideModels) {
+        // wide descriptors: one word per point in the rank scratch
+        fast_refine(Desc<true>{(uint32_t*)rankA});
+#ifndef SPSLAM_SEG_NO_GENERAL  // measurement variant only: frames with more than kFastModels models are not refined
     } else if (nmodel > 0) {
         // general path: accept masks over up to 64 models evaluated in the pass
         for (int r = wave; r < H; r += kSegWaves)
@@ -977,6 +1033,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             ng += refine_pass<K>(S, state, cbits, X, Y, Z, W, H, true, ev, ng);
             if (lane == 0) S.misc[0] = ng;
         }
+#endif
     } else if (t == 0) {
         S.misc[0] = 0;
     }
@@ -1079,7 +1136,9 @@ size_t plane_segment_lds_bytes(const PlaneGeom& g, bool* in_lds) {
     const size_t RW = (g.W + 63) / 64;
     const size_t bits = 2 * g.H * RW * sizeof(uint64_t);
     const size_t maps = ((size_t)2 * g.N + 15) / 16 * 16;
-    const bool fits = sizeof(planes::SegShared) + bits + maps <= (size_t)planes::kLdsBytes;
+    // the LDS instance also keeps the refinement descriptors' high bytes in SegShared::stage
+    const bool fits = sizeof(planes::SegShared) + bits + maps <= (size_t)planes::kLdsBytes &&
+                      (size_t)g.N <= sizeof(planes::SegShared::stage);
     if (in_lds) *in_lds = fits;
     return bits + (fits ? maps : 0);
 }

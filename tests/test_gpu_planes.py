@@ -67,24 +67,30 @@ def _compare(pe, depth, k, scale=1.0, min_size=500):
     return len(ro["coef"]), po.n_models
 
 
+def _refine_path(n_models):
+    """Which refinement the kernel takes (plane_segment.hip phase K): fast narrow (<= 14 models, 16-bit
+    descriptors), fast wide (<= 30, 32-bit descriptors) or the general 64-bit path."""
+    return "narrow" if n_models <= 14 else "wide" if n_models <= 30 else "general"
+
+
 def test_planes_many_models(ctx):
-    """More than 6 candidate models per frame (the general refinement path) and fewer (the fast path)."""
+    """All three refinement paths at 640x480: small MinSize values give more candidate models per frame."""
     import oracle_planes
     import synth
     _, pe = ctx
     sc = synth.Scene(3, n_boxes=8)
     models = []
-    for min_size in (500, 150):
+    for min_size in (500, 30, 15):
         pe.configure(min_size=min_size)
         for fi in (0, 15, 30):
             _, d, _ = sc.render(sc.pose(fi), noise_seed=fi)
             models.append(_compare(pe, oracle_planes.depth_to_float(d), fi, min_size=min_size)[1])
     pe.configure(min_size=500)
-    assert min(models) <= 6 < max(models), models
+    assert {_refine_path(m) for m in models} == {"narrow", "wide", "general"}, models
 
 
 def test_planes_c5_size():
-    """1280x960 (BASELINE config C5): maps in global memory, 8 positions per lane."""
+    """1280x960 (BASELINE config C5): maps in global memory, 8 positions per lane; narrow and wide refinement."""
     import oracle_planes
     import spslam_gpu
     import spslam_planes
@@ -92,13 +98,13 @@ def test_planes_c5_size():
     K = synth.TUM3
     ex = spslam_gpu.OrbExtractor(nfeatures=4000, width=1280, height=960, max_batch=1)
     try:
-        for min_size, expect_general in ((500, True), (4000, False)):
+        for min_size, expect in ((500, "narrow"), (4000, "narrow"), (30, "wide")):
             pe = spslam_planes.PlaneExtractor(ex, K["fx"] * 2, K["fy"] * 2, K["cx"] * 2, K["cy"] * 2, 1280, 960,
                                               min_size=min_size)
             sc = synth.Scene(1, n_boxes=8)
             _, d, _ = sc.render(sc.pose(5), 1280, 960, noise_seed=5)
             n, nm = _compare(pe, oracle_planes.depth_to_float(d), 5, scale=2.0, min_size=min_size)
-            assert n >= 2 and (nm > 6) == expect_general, (n, nm)
+            assert n >= 2 and _refine_path(nm) == expect, (n, nm)
     finally:
         ex.close()
 

@@ -47,6 +47,9 @@ def main():
     print(f"fast-path frames {k.sum()} / {len(k)}: refine mean {ref[k].mean() if k.any() else 0:.1f} us, "
           f"max {ref[k].max() if k.any() else 0:.1f};  general-path refine mean "
           f"{ref[~k].mean() if (~k).any() else 0:.1f} us, max {ref[~k].max() if (~k).any() else 0:.1f}")
+    nm = ts[:, 13]
+    print("models per frame: narrow (<=14)", int((nm <= 14).sum()), " wide (15-30)", int(((nm > 14) & (nm <= 30)).sum()),
+          " general (>30)", int((nm > 30).sum()), " max", int(nm.max()))
     print("total per frame (us) percentiles 50/90/99/100:", np.percentile(tot, [50, 90, 99, 100]).round(1).tolist())
     if k.any():
         print(f"refine: cand-bitmap {((ts[k, 10] - ts[k, 7]) / 100).mean():.1f} us, forward "
