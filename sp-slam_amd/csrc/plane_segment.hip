@@ -1003,7 +1003,13 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         }
         if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
     };
+#ifdef SPSLAM_MEASURE_SKIP_REFINE  // measurement variant only (marginal step cost): no refinement
     if (nmodel > 0 && nmodel <= kFastModels) {
+        if (t == 0) S.misc[0] = 0;
+    } else if (false) {
+#else
+    if (nmodel > 0 && nmodel <= kFastModels) {
+#endif
         // narrow descriptors: low bytes in the contour-mask map (the masks come later), high bytes in the
         // covariance staging area (phase G is over) in the LDS instance (the host picks it only when
         // N <= sizeof(S.stage)), else in the rank scratch (dead since phase D); fixed per instance so every

@@ -537,7 +537,8 @@ hipError_t configure_supposed(spslam_ctx* c, const spslam_plane_params* p) {
     SuppBuffers& b = c->sb;
     const size_t bytes = (size_t)kSuppRndTable * 4 +
                          F * kMaxPlanesPerFrame * kMaxLinesPerBoundary * sizeof(LineCand) +
-                         F * kMaxPlanesPerFrame * sizeof(int) + F * CC * (4 + 16 + 4 + 1) + 8 * 256;
+                         F * kMaxPlanesPerFrame * sizeof(int) + F * CC * (4 + 16 + 4 + 1) +
+                         F * kMaxPlanesPerFrame * 8 * sizeof(long long) + 9 * 256;
     if (c->d_supp_scratch) (void)hipFree(c->d_supp_scratch);
     c->d_supp_scratch = nullptr;
     hipError_t e = hipMalloc(&c->d_supp_scratch, bytes);
@@ -551,6 +552,9 @@ hipError_t configure_supposed(spslam_ctx* c, const spslam_plane_params* p) {
     b.big = (float4*)carve(F * CC * 16);
     b.big_sh = (int*)carve(F * CC * 4);
     b.big_flag = (uint8_t*)carve(F * CC);
+    b.prof = (long long*)carve(F * kMaxPlanesPerFrame * 8 * sizeof(long long));
+    e = hipMemset(b.prof, 0, F * kMaxPlanesPerFrame * 8 * sizeof(long long));
+    if (e != hipSuccess) return e;
     // every SACSegmentation::segment() seeds boost::mt19937(12345u); rnd() = uniform_int<>(0, INT_MAX) = mt() >> 1
     std::vector<uint32_t> tab(kSuppRndTable);
     std::mt19937 mt(12345u);
@@ -828,6 +832,11 @@ int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_po
     }
     if (what == 4) {
         HIP_CHECK(c, hipMemcpy(out, b.ts + frame * 16, 16 * sizeof(long long), hipMemcpyDeviceToHost));
+        return SPSLAM_OK;
+    }
+    if (what == 5) {  // supp_lines phase clocks (SPSLAM_SUPP_PROF build), [kMaxPlanesPerFrame][8]
+        HIP_CHECK(c, hipMemcpy(out, c->sb.prof + (size_t)frame * kMaxPlanesPerFrame * 8,
+                               kMaxPlanesPerFrame * 8 * sizeof(long long), hipMemcpyDeviceToHost));
         return SPSLAM_OK;
     }
     return fail(c, SPSLAM_ERR_ARG, "unknown debug stage%s", "");

@@ -42,6 +42,13 @@ constexpr int kBatch = 64;       // RANSAC trials per speculative round
 constexpr int kLdsPts = 2048;    // boundaries up to this size are held in LDS
 constexpr int kMaxTrials = 1001; // RandomSampleConsensus: ++iterations_ > max_iterations_ (1000) -> stop
 
+#ifdef SPSLAM_SUPP_PROF  // diagnostic build: per-boundary phase clocks (100 MHz ticks) in sb.prof
+#define SUPP_CLK() ((long long)__builtin_amdgcn_s_memrealtime())
+#define SUPP_T(k) do { if (t == 0) { const long long c_ = SUPP_CLK(); pr[k] += c_ - pt; pt = c_; } } while (0)
+#else
+#define SUPP_T(k) do { } while (0)
+#endif
+
 struct Shared {
     int s0[kBatch], s1[kBatch], cnt[kBatch];
     int nb, fail, done, have;
@@ -186,18 +193,34 @@ __device__ bool is_border_point(const float4 p, const float* __restrict__ depth,
     const float v = fmaf(K.fy * p.y, invz, K.cy);
     if (isnan(u) || isnan(v)) return true;
     if (!(fabsf(u) < 1e6f) || !(fabsf(v) < 1e6f)) return false;
-    const long long total = (long long)K.w * K.h;
+    // element offset of window pixel (i, j), or -1 when the reference reads nothing there; 32-bit is exact
+    // here (|u|, |v| < 1e6 and w <= 2048 keep j * w + i inside int)
+    const int total = K.w * K.h;
+    auto offset = [&](int i, int j) -> int {
+        if ((unsigned)i < (unsigned)K.w && (unsigned)j < (unsigned)K.h) return j * K.stride + i;
+        const int fi = j * K.w + i;
+        return (fi >= 0 && fi < total) ? (fi / K.w) * K.stride + fi % K.w : -1;
+    };
     int num = 0, nan = 0;
     float res = 0.f;
-    for (int j = (int)(v - 10.f); (float)j < v + 10.f; ++j)
-        for (int i = (int)(u - 10.f); (float)i < u + 10.f; ++i) {
-            float d = 0.f;
-            if (i >= 0 && i < K.w && j >= 0 && j < K.h) {
-                d = depth[(long long)j * K.stride + i];
-            } else {
-                const long long fi = (long long)j * K.w + i;
-                if (fi >= 0 && fi < total) d = depth[(fi / K.w) * K.stride + fi % K.w];
-            }
+    // A window row is at most 21 pixels wide (|u| < 1e6: float spacing <= 1/16): its depths are loaded
+    // together (unconditional loads from a clamped offset, masked afterwards), then consumed in the
+    // reference's order with its early exit; any pixels beyond the batch are read one by one.
+    constexpr int kRow = 22;
+    const int i0 = (int)(u - 10.f);
+    for (int j = (int)(v - 10.f); (float)j < v + 10.f; ++j) {
+        float dv[kRow];
+#pragma unroll
+        for (int k = 0; k < kRow; k++) {
+            const int o = offset(i0 + k, j);
+            const float x = depth[o < 0 ? 0 : o];
+            dv[k] = o < 0 ? 0.f : x;
+        }
+        int i = i0;
+#pragma unroll
+        for (int k = 0; k < kRow; k++, ++i) {
+            if (!((float)i < u + 10.f)) break;
+            const float d = dv[k];
             if ((double)d > 0.05) {
                 res += d;
                 num++;
@@ -205,6 +228,17 @@ __device__ bool is_border_point(const float4 p, const float* __restrict__ depth,
                 return false;
             }
         }
+        for (; (float)i < u + 10.f; ++i) {
+            const int o = offset(i, j);
+            const float d = o < 0 ? 0.f : depth[o];
+            if ((double)d > 0.05) {
+                res += d;
+                num++;
+            } else if (++nan > 100) {
+                return false;
+            }
+        }
+    }
     if ((double)(p.z - res / (float)num) > 0.1) return false;
     return true;
 }
@@ -242,6 +276,9 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
     __shared__ float4 Qs[kLdsPts];
     __shared__ int shs[kLdsPts];
     __shared__ uint8_t flags_s[kLdsPts];
+#ifdef SPSLAM_MEASURE_SKIP_SUPP  // measurement variant only (marginal step cost): no RANSAC work
+    if (g.W > 0) return;
+#endif
     __shared__ Shared S;
     const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int np = min(plane_counts[f], kMaxPlanesPerFrame);
@@ -267,11 +304,15 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
         // (one pointer selected at run time would make every access a flat one, waited on by both the
         // vector-memory and the LDS counters).
         auto boundary = [&](float4* Q, int* sh, uint8_t* flag) __attribute__((always_inline)) -> int {
+#ifdef SPSLAM_SUPP_PROF
+        long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = SUPP_CLK();
+#endif
         for (int i = t; i < bsize; i += kThreads) {
             const int ci = con[coff + i];
             Q[i] = make_float4(X[ci], Y[ci], Z[ci], __int_as_float(ci));
         }
         __syncthreads();
+        SUPP_T(0);
         int n = bsize, used = 0, ncand = 0;
         for (int j = 0; j < kMaxLinesPerBoundary; j++) {
             // ---------------- RandomSampleConsensus::computeModel
@@ -302,18 +343,22 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                             const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
                             pos += 64;
                             rnext = sb.rnd[pos + lane];  // (the table holds one block beyond the worst case)
+                            // Branch-free: entries 0 and 1 live in r0 / r1 (their LDS slots are never read), so
+                            // a swap that does not touch LDS reads and writes slot 0 (first swap) or 1 (second)
+                            // as a sink; per pair two reads, then two writes, and selects.
+#pragma unroll 4
                             for (int c = 0; c < 32; c++) {
                                 const int j0 = __builtin_amdgcn_readlane((int)jv, 2 * c), j1 = __builtin_amdgcn_readlane((int)jv, 2 * c + 1);
-                                const int x0 = j0 > 1 ? sh[j0] : 0, x1 = j1 > 1 ? sh[j1] : 0;
-                                const int a0 = r0;
-                                if (j0 == 1) { r0 = r1; r1 = a0; }
-                                else if (j0 > 1) { sh[j0] = a0; r0 = x0; }
-                                if (j1 > 1) {
-                                    const int v = j1 == j0 ? a0 : x1;  // j1 == j0: the value the first swap stored
-                                    sh[j1] = r1;
-                                    r1 = v;
-                                }
-                                if (lane == c) { bp0 = r0; bp1 = r1; }
+                                const int i0 = j0 > 1 ? j0 : 0, i1 = j1 > 1 ? j1 : 1;
+                                const int x0 = sh[i0], x1 = sh[i1];
+                                const int a0 = r0, b0 = r1;
+                                const int r1m = j0 == 1 ? a0 : b0;  // entry 1 after the first swap
+                                sh[i0] = a0;
+                                sh[i1] = r1m;
+                                r0 = j0 > 1 ? x0 : (j0 == 1 ? b0 : a0);
+                                r1 = j1 > 1 ? (j1 == j0 ? a0 : x1) : r1m;  // j1 == j0: the value the first swap stored
+                                bp0 = lane == c ? r0 : bp0;
+                                bp1 = lane == c ? r1 : bp1;
                             }
                             bool good = false;
                             if (lane < 32) {
@@ -342,38 +387,92 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                     if (lane == 0) { S.nb = nb; S.fail = fail; }
                 }
                 __syncthreads();
+                SUPP_T(1);
                 const int nb = S.nb;
-                for (int c = wave; c < nb; c += kWaves) {
-                    float L[6];
-                    line_from_samples(Q[S.s0[c]], Q[S.s1[c]], L);
-                    float ld[3] = {L[3], L[4], L[5]};
-                    normalize4(ld);
+                {
+                    // 16 trials per wave, 4 lanes per trial each counting every 4th point (the 16 lanes of a
+                    // point quarter read the same point: an LDS broadcast)
+                    const int c = wave * (kBatch / kWaves) + (lane >> 2), qq = lane & 3;
                     int cnt = 0;
-                    for (int i = lane; i < n; i += 64) cnt += line_sqd(L, ld, Q[i]) <= thr;
-                    cnt = wave_sum(cnt);
-                    if (lane == 0) S.cnt[c] = cnt;
-                }
-                __syncthreads();
-                if (t == 0) {
-                    int it = S.iterations;
-                    bool done = false;
-                    for (int c = 0; c < nb; c++) {
-                        if (!((double)it < S.k)) { done = true; break; }
-                        if (S.cnt[c] > S.best) {
-                            S.best = S.cnt[c]; S.best_s0 = S.s0[c]; S.best_s1 = S.s1[c]; S.have = 1;
-                            const double w = (double)S.best * one_over_n;
-                            double pno = 1.0 - w * w;
-                            pno = fmax(DBL_EPSILON, pno);
-                            pno = fmin(1.0 - DBL_EPSILON, pno);
-                            S.k = log_prob / log(pno);
-                        }
-                        if (++it > kMaxTrials - 1) { done = true; break; }
+                    if (c < nb) {
+                        float L[6];
+                        line_from_samples(Q[S.s0[c]], Q[S.s1[c]], L);
+                        float ld[3] = {L[3], L[4], L[5]};
+                        normalize4(ld);
+#pragma unroll 1
+                        for (int i = qq; i < n; i += 4) cnt += line_sqd(L, ld, Q[i]) <= thr;
                     }
-                    if (!done && (S.fail || !((double)it < S.k))) done = true;
-                    S.iterations = it;
-                    S.done = done;
+                    cnt += __shfl_xor(cnt, 1);
+                    cnt += __shfl_xor(cnt, 2);
+                    if (qq == 0 && c < nb) S.cnt[c] = cnt;
                 }
                 __syncthreads();
+                SUPP_T(2);
+                if (wave == 0) {
+                    // computeModel's bookkeeping over the round's trials, in parallel (lane c = trial c): a
+                    // trial improves the model when its count beats the best so far (exclusive prefix max);
+                    // k changes only there, so the k each trial's `iterations < k` test sees is the k of the
+                    // last improvement before it; the loop stops at the first failed test, or after trial
+                    // 1000 - iterations (max_iterations_)
+                    const int it0 = S.iterations, best0 = S.best;
+                    const double k0 = S.k;
+                    const bool act = lane < nb;
+                    const int cn = act ? S.cnt[lane] : INT_MIN;
+                    int pm = cn, lr;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const int y = __shfl_up(pm, off);
+                        if (lane >= off) pm = max(pm, y);
+                    }
+                    int ex = __shfl_up(pm, 1);
+                    if (lane == 0) ex = INT_MIN;
+                    const bool rec = act && cn > max(ex, best0);
+                    double kc = 0.0;
+                    if (rec) {
+                        const double w = (double)cn * one_over_n;
+                        double pno = 1.0 - w * w;
+                        pno = fmax(DBL_EPSILON, pno);
+                        pno = fmin(1.0 - DBL_EPSILON, pno);
+                        kc = log_prob / log(pno);
+                    }
+                    lr = rec ? lane : -1;
+#pragma unroll
+                    for (int off = 1; off < 64; off <<= 1) {
+                        const int y = __shfl_up(lr, off);
+                        if (lane >= off) lr = max(lr, y);
+                    }
+                    int lre = __shfl_up(lr, 1);
+                    if (lane == 0) lre = -1;
+                    const double kb_rec = __shfl(kc, lre < 0 ? 0 : lre);
+                    const double kb = lre < 0 ? k0 : kb_rec;
+                    const uint64_t m1 = __ballot(act && !((double)(it0 + lane) < kb));
+                    const int stop1 = m1 ? __ffsll((unsigned long long)m1) - 1 : 64;
+                    const int stop2 = (kMaxTrials - 1) - it0;
+                    int proc, it;
+                    bool done;
+                    if (stop1 < nb && stop1 <= stop2) { proc = stop1; it = it0 + stop1; done = true; }
+                    else if (stop2 < nb) { proc = stop2 + 1; it = it0 + stop2 + 1; done = true; }
+                    else { proc = nb; it = it0 + nb; done = false; }
+                    const uint64_t rm = __ballot(rec) & (proc >= 64 ? ~0ull : ((1ull << proc) - 1ull));
+                    double kf = k0;
+                    if (rm) {
+                        const int L = 63 - __clzll(rm);
+                        kf = __shfl(kc, L);
+                        if (lane == L) {
+                            S.best = cn; S.best_s0 = S.s0[L]; S.best_s1 = S.s1[L]; S.have = 1; S.k = kc;
+                        }
+                    }
+                    if (!done && (S.fail || !((double)it < kf))) done = true;
+                    if (lane == 0) {
+                        S.iterations = it;
+                        S.done = done;
+                    }
+                }
+                __syncthreads();
+                SUPP_T(3);
+#ifdef SPSLAM_SUPP_PROF
+                if (t == 0) pr[6]++;
+#endif
             }
             // ---------------- inliers, optimizeModelCoefficients, refined inliers
             int n_inl = 0;
@@ -382,24 +481,50 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                 line_from_samples(Q[S.best_s0], Q[S.best_s1], c0);
                 n_inl = select_within(c0, Q, flag, n, thr, S);
                 if (n_inl > 2) {
+                    // The two sums below are sequential float chains in point order (one accumulator per lane).
+                    // Points outside the line add +0.0f, which leaves a sum that starts at +0.0f unchanged
+                    // (it can never be -0.0f), so the loop is branch-free and its LDS loads are issued a
+                    // group of 8 ahead of the adds instead of one dependent round trip per point.
+                    constexpr int kG = 8;
                     if (wave == 0 && lane < 3) {  // compute3DCentroid (dense): sequential float sums
                         float s = 0.f;
-                        for (int i = 0; i < n; i++)
-                            if (flag[i]) { const float4 p = Q[i]; s += lane == 0 ? p.x : lane == 1 ? p.y : p.z; }
+                        int i = 0;
+                        for (; i + kG <= n; i += kG) {
+                            float v[kG];
+#pragma unroll
+                            for (int u = 0; u < kG; u++) {
+                                const float4 p = Q[i + u];
+                                v[u] = flag[i + u] ? (lane == 0 ? p.x : lane == 1 ? p.y : p.z) : 0.f;
+                            }
+#pragma unroll
+                            for (int u = 0; u < kG; u++) s += v[u];
+                        }
+                        for (; i < n; i++) {
+                            const float4 p = Q[i];
+                            s += flag[i] ? (lane == 0 ? p.x : lane == 1 ? p.y : p.z) : 0.f;
+                        }
                         S.acc[lane] = s / (float)n_inl;
                     }
                     __syncthreads();
                     if (wave == 0 && lane < 6) {  // computeCovarianceMatrix (dense), one accumulator per lane
                         const float cx = S.acc[0], cy = S.acc[1], cz = S.acc[2];
+                        auto term = [&](int i) __attribute__((always_inline)) {
+                            const float4 p = Q[i];
+                            const float x = p.x - cx, y = p.y - cy, z = p.z - cz;
+                            const float a = lane == 0 ? y : lane == 1 ? y : lane == 2 ? z : lane == 3 ? x : lane == 4 ? y : z;
+                            const float b = lane == 0 ? y : lane == 1 ? z : lane == 2 ? z : x;
+                            return flag[i] ? a * b : 0.f;
+                        };
                         float s = 0.f;
-                        for (int i = 0; i < n; i++)
-                            if (flag[i]) {
-                                const float4 p = Q[i];
-                                const float x = p.x - cx, y = p.y - cy, z = p.z - cz;
-                                const float a = lane == 0 ? y : lane == 1 ? y : lane == 2 ? z : lane == 3 ? x : lane == 4 ? y : z;
-                                const float b = lane == 0 ? y : lane == 1 ? z : lane == 2 ? z : x;
-                                s += a * b;
-                            }
+                        int i = 0;
+                        for (; i + kG <= n; i += kG) {
+                            float v[kG];
+#pragma unroll
+                            for (int u = 0; u < kG; u++) v[u] = term(i + u);
+#pragma unroll
+                            for (int u = 0; u < kG; u++) s += v[u];
+                        }
+                        for (; i < n; i++) s += term(i);
                         S.acc[3 + lane] = s;
                     }
                     __syncthreads();
@@ -424,6 +549,7 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
                 for (int k = 0; k < 6; k++) S.line[k] = 0.f;
             }
             __syncthreads();
+            SUPP_T(4);
             // ---------------- Frame.cc:961-988
             LineCand& out = C[j];
             if (t == 0) {
@@ -474,7 +600,14 @@ __global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, Plane
             used += n_inl;
             n = kbase;
             __syncthreads();
+            SUPP_T(5);
         }
+#ifdef SPSLAM_SUPP_PROF
+        if (t == 0) {
+            pr[7] = bsize;
+            for (int k = 0; k < 8; k++) sb.prof[((size_t)f * kMaxPlanesPerFrame + q) * 8 + k] = pr[k];
+        }
+#endif
             return ncand;
         };
         const int ncand = in_lds ? boundary(Qs, shs, flags_s)

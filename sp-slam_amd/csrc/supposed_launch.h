@@ -40,6 +40,7 @@ struct SuppBuffers {
     float4* big;           // [F][contour_cap] point scratch for boundaries beyond the LDS tile
     int* big_sh;           // [F][contour_cap]
     uint8_t* big_flag;     // [F][contour_cap]
+    long long* prof;       // [F][kMaxPlanesPerFrame][8] phase clocks of the SPSLAM_SUPP_PROF diagnostic build
 };
 
 hipError_t supp_launch(const PlaneGeom& g, const PlaneBuffers& pb, const SuppParams& sp, const SuppBuffers& sb,
