@@ -1111,6 +1111,12 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     block_sync();
     STAMP(4);
     // ---- N: contours (findLabeledRegionBoundary from the model's last inlier, on refined labels)
+    // Waves without a contour end here: a wave's VGPRs are released when it ends (LDS only with the
+    // workgroup), and s_barrier waits on the surviving waves only, so the remaining barriers stay correct.
+    // The walks take ~0.35 ms per frame; meanwhile other streams' waves can use those registers.
+#ifndef SPSLAM_SEG_NO_EARLY_EXIT
+    if (wave >= max(nk, 1)) return;
+#endif
     for (int q = wave; q < nk; q += kSegWaves)
         if (lane == 0) {
             const int m = S.kept[q];
