@@ -580,7 +580,7 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const D desc, const 
 // Returns the number of events (uniform).
 template <class D>
 __device__ __forceinline__ int refine_events(SegShared& S, const uint8_t* state, const D desc, int W, int H, int N,
-                                             bool bw, int* ev) {
+                                             bool bw, int* ev, int nw) {  // nw: the workgroup's live waves
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int M = (H - 1) * W;
     // how target j grew in this pass: 0 not, 1 along its row (chain), 2 from the other row
@@ -601,7 +601,7 @@ __device__ __forceinline__ int refine_events(SegShared& S, const uint8_t* state,
         const int b = how(*tB, s) == 2;
         return a | (b << 1);
     };
-    const int span = (M + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
+    const int span = (M + nw * 64 - 1) / (nw * 64) * 64;
     const int q0 = wave * span, q1 = min(M, q0 + span);
     int cnt = 0;
     for (int base = q0; base < q1; base += 64) {
@@ -613,7 +613,7 @@ __device__ __forceinline__ int refine_events(SegShared& S, const uint8_t* state,
     if (lane == 0) S.wsum[wave] = cnt;
     __syncthreads();
     int off = 0, total = 0;
-    for (int j = 0; j < kSegWaves; j++) {
+    for (int j = 0; j < nw; j++) {
         if (j < wave) off += S.wsum[j];
         total += S.wsum[j];
     }
@@ -977,8 +977,17 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     STAMP(7);
     // ---- K: refinement (two passes), one wave per pass
     uint64_t* cbits = hbits;  // rows with growable points (hbits no longer needed)
-    // two passes over the fast-path descriptors (D: narrow or wide format)
-    auto fast_refine = [&](const auto desc) {
+    // Live waves from the second pass's serial row walk on: on the fast paths only one wave per model stays
+    // (the rest end once the second pass's descriptors are written -- their VGPRs go back to the other
+    // streams' waves for the rest of the kernel; s_barrier waits on surviving waves only).
+#if !defined(SPSLAM_SEG_NO_EARLY_EXIT) && !defined(SPSLAM_SEG_EXIT_AT_N_ONLY)  // (measurement variants)
+    const int nlive = (nmodel > 0 && nmodel <= kWideModels) ? min(nmodel, kSegWaves) : kSegWaves;
+#else
+    const int nlive = kSegWaves;
+#endif
+    const int tlive = nlive * 64;
+    // two passes over the fast-path descriptors (D: narrow or wide format); false: this wave has ended its part
+    auto fast_refine = [&](const auto desc) -> bool {
         using D = decltype(desc);
         int ng = 0;
         for (int pass = 0; pass < 2; pass++) {
@@ -996,13 +1005,16 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 }
             __syncthreads();
             if (pass == 0) STAMP(10);
+            if (pass == 1 && wave >= nlive) return false;  // no barrier before the caller's return
             if (wave == 0) refine_rows<K>(state, desc, cbits, W, H, bw);
             __syncthreads();
             if (pass == 0) STAMP(11);
-            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng);
+            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng, pass == 1 ? nlive : kSegWaves);
         }
         if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
+        return true;
     };
+    bool live = true;
 #ifdef SPSLAM_MEASURE_SKIP_REFINE  // measurement variant only (marginal step cost): no refinement
     if (nmodel > 0 && nmodel <= kFastModels) {
         if (t == 0) S.misc[0] = 0;
@@ -1014,10 +1026,10 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         // covariance staging area (phase G is over) in the LDS instance (the host picks it only when
         // N <= sizeof(S.stage)), else in the rank scratch (dead since phase D); fixed per instance so every
         // access is a ds_* or global_* one, never flat
-        fast_refine(Desc<false>{nmask, kLdsMaps ? (uint8_t*)&S.stage[0][0][0] : (uint8_t*)rankA});
+        live = fast_refine(Desc<false>{nmask, kLdsMaps ? (uint8_t*)&S.stage[0][0][0] : (uint8_t*)rankA});
     } else if (nmodel > 0 && nmodel <= kWideModels) {
         // wide descriptors: one word per point in the rank scratch
-        fast_refine(Desc<true>{(uint32_t*)rankA});
+        live = fast_refine(Desc<true>{(uint32_t*)rankA});
 #ifndef SPSLAM_SEG_NO_GENERAL  // measurement variant only: frames with more than kFastModels models are not refined
     } else if (nmodel > 0) {
         // general path: accept masks over up to 64 models evaluated in the pass
@@ -1043,8 +1055,9 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     } else if (t == 0) {
         S.misc[0] = 0;
     }
+    if (!live) return;
     block_sync();
-    for (int e = t; e < S.misc[0]; e += kSegThreads) atomicAdd(&S.model_grown[ev[e] >> 24], 1);
+    for (int e = t; e < S.misc[0]; e += tlive) atomicAdd(&S.model_grown[ev[e] >> 24], 1);
     __syncthreads();
     STAMP(8);
     // ---- L: Frame.cc:912-934: d >= 0, PlaneNotSeen; inlier offsets
@@ -1077,11 +1090,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     const int nk = S.nkept, ng = S.misc[0];
     // ---- M: inlier lists (component members in raster order, then grown points in grow order);
     //         8-neighbour same-state masks for the contour walk
-    for (int i = t; i < N; i += kSegThreads) {
+    for (int i = t; i < N; i += tlive) {
         const int s = state[i];
         nmask[i] = s ? (uint8_t)nb_bits(state, W, H, i % W, i / W, s, true) : 0;
     }
-    for (int q = wave; q < nk; q += kSegWaves) {
+    for (int q = wave; q < nk; q += nlive) {
         const int m = S.kept[q], j = S.model_big[m], n = S.big_size[j], o = S.big_off[j];
         const int dst = planes[q].inlier_offset, lim = planes[q].n_inliers;
         for (int k = lane; k < min(n, lim); k += 64) inl[dst + k] = members[o + k];
