@@ -38,6 +38,14 @@ namespace planes {
 #define SPSLAM_SEG_THREADS 1024
 #endif
 constexpr int kSegThreads = SPSLAM_SEG_THREADS;
+// Fast refinement paths: the waves beyond max(models, SPSLAM_SEG_MIN_LIVE) end after refinement pass
+// SPSLAM_SEG_EXIT_PASS's descriptors (measurement knobs; see plane_segment_kernel phase K)
+#ifndef SPSLAM_SEG_EXIT_PASS
+#define SPSLAM_SEG_EXIT_PASS 0
+#endif
+#ifndef SPSLAM_SEG_MIN_LIVE
+#define SPSLAM_SEG_MIN_LIVE 8
+#endif
 constexpr int kSegWaves = kSegThreads / 64;
 constexpr int kMaxBig = 255;          // components > MinSize per frame (u8 tags)
 constexpr int kMaxRowWords = 8;       // W <= 512
@@ -977,11 +985,13 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     STAMP(7);
     // ---- K: refinement (two passes), one wave per pass
     uint64_t* cbits = hbits;  // rows with growable points (hbits no longer needed)
-    // Live waves from the second pass's serial row walk on: on the fast paths only one wave per model stays
-    // (the rest end once the second pass's descriptors are written -- their VGPRs go back to the other
-    // streams' waves for the rest of the kernel; s_barrier waits on surviving waves only).
+    // Live waves from the first pass's serial row walk on: on the fast paths max(models, 8) waves stay (the
+    // rest end once the first pass's descriptors are written -- their VGPRs go back to the other streams'
+    // waves for the rest of the kernel; s_barrier waits on surviving waves only).  Measured on the pipelined
+    // C2 step against ending at pass 1 or before pass 0, and against 1 / 6 / 12 live waves
+    // (profiles/r02/ab_seg_live_waves).
 #if !defined(SPSLAM_SEG_NO_EARLY_EXIT) && !defined(SPSLAM_SEG_EXIT_AT_N_ONLY)  // (measurement variants)
-    const int nlive = (nmodel > 0 && nmodel <= kWideModels) ? min(nmodel, kSegWaves) : kSegWaves;
+    const int nlive = (nmodel > 0 && nmodel <= kWideModels) ? min(max(nmodel, SPSLAM_SEG_MIN_LIVE), kSegWaves) : kSegWaves;
 #else
     const int nlive = kSegWaves;
 #endif
@@ -990,9 +1000,10 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     auto fast_refine = [&](const auto desc) -> bool {
         using D = decltype(desc);
         int ng = 0;
+        if (SPSLAM_SEG_EXIT_PASS < 0 && wave >= nlive) return false;  // phase H ended with a barrier
         for (int pass = 0; pass < 2; pass++) {
             const bool bw = pass == 1;
-            for (int r = wave; r < H; r += kSegWaves)
+            for (int r = wave; r < H; r += pass > SPSLAM_SEG_EXIT_PASS ? nlive : kSegWaves)
                 for (int k = 0; k < RW; k++) {
                     const int c = (k << 6) + lane, i = r * W + c;
                     uint32_t dsc = 0;
@@ -1005,11 +1016,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 }
             __syncthreads();
             if (pass == 0) STAMP(10);
-            if (pass == 1 && wave >= nlive) return false;  // no barrier before the caller's return
+            if (pass == SPSLAM_SEG_EXIT_PASS && wave >= nlive) return false;  // no barrier before the caller's return
             if (wave == 0) refine_rows<K>(state, desc, cbits, W, H, bw);
             __syncthreads();
             if (pass == 0) STAMP(11);
-            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng, pass == 1 ? nlive : kSegWaves);
+            ng += refine_events(S, state, desc, W, H, N, bw, ev + ng, pass >= SPSLAM_SEG_EXIT_PASS ? nlive : kSegWaves);
         }
         if (t == 0) { S.misc[0] = ng; ts[12] = ng; }
         return true;
