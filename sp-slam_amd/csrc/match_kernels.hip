@@ -5,11 +5,14 @@
 // than retry_below matches (src/Tracking.cc:968-975).  Semantics:
 // oracle/match_oracle.cpp.
 //
-//   match_window_kernel  grid (frame, 256 last-frame points): projection, the
-//                        search window and every candidate's Hamming distance
-//                        (v_bcnt over the XOR of 8 dwords); keeps the best as
-//                        (distance << 20 | CSR position), which orders ties
-//                        like the reference's cell-by-cell scan;
+//   match_window_kernel  grid (frame, 16 last-frame points), 16 lanes per point:
+//                        projection and search window (redundantly per lane),
+//                        the window's grid cells spread over the lanes, every
+//                        candidate's Hamming distance (v_bcnt over the XOR of 8
+//                        dwords); keeps the 3 best as (distance << 20 | CSR
+//                        position), which orders ties like the reference's
+//                        cell-by-cell scan, merged over the lanes (keys are
+//                        unique, so the merge is the serial scan's result);
 //   match_assign_kernel  grid (frame), one wave: the reference's loop is
 //                        sequential only through `mvpMapPoints[i2] taken`, so
 //                        the wave walks the points in order, accepts each
@@ -31,6 +34,20 @@ namespace match {
 
 constexpr int kThreads = 256, kCols = SPSLAM_GRID_COLS, kRows = SPSLAM_GRID_ROWS, kHisto = 30, kThHigh = 100;
 constexpr uint32_t kNone = 0xffffffffu;
+// lanes per last-frame point in match_window_kernel: the serial chain of dependent loads (cell bounds,
+// grid index, keypoint, descriptor) per candidate is what the in-step time of the window search is made of
+// when the extraction streams load the memory system, so the window's cells are split over the lanes
+constexpr int kGrp = 16, kPtsPerBlock = kThreads / kGrp;
+// local-map windows are a few cells (radius 2.5-4 px x scale): 4 lanes per local point
+constexpr int kLGrp = 4, kLPtsPerBlock = kThreads / kLGrp;
+
+// insert a key into an ascending triple (keys unique; kNone = +inf), keeping the 3 smallest
+__device__ __forceinline__ void ins3(uint32_t& b0, uint32_t& b1, uint32_t& b2, uint32_t x) {
+    const uint32_t n1 = min(b1, max(b0, x)), n2 = min(b2, max(b1, x));
+    b0 = min(b0, x);
+    b1 = n1;
+    b2 = n2;
+}
 
 __device__ __forceinline__ void mat3_mul(const float* T, const float* x, const float* c, bool transpose, double sign,
                                          float* y) {
@@ -93,12 +110,14 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
                                                                 const int* __restrict__ nmatches,
                                                                 MatchWindow* __restrict__ win) {
     tail_wave_priority();
-    const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
+    const int f = blockIdx.x, sub = threadIdx.x & (kGrp - 1);
+    const int i = blockIdx.y * kPtsPerBlock + (int)(threadIdx.x / kGrp);
     const spslam_proj_frame& F = frames[f];
     if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
-    if (i >= F.n_points || i >= max_points) return;
+    if (i >= F.n_points || i >= max_points) return;  // uniform over the point's lanes, as every return below
     MatchWindow w{};
     w.best[0] = w.best[1] = w.best[2] = kNone;
+    w.kp[0] = w.kp[1] = w.kp[2] = -1;
     w.valid = 0;
     w.x0 = 1;
     w.x1 = 0;
@@ -110,10 +129,10 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     mat3_mul(F.Tcw, p.xw, tcw, false, 1.0, x3Dc);
     const float invzc = (float)__ddiv_rn(1.0, (double)x3Dc[2]);
     MatchWindow* W = win + (size_t)f * max_points + i;
-    if (invzc < 0) { *W = w; return; }
+    if (invzc < 0) { if (sub == 0) *W = w; return; }
     const float u = __fmaf_rn(__fmul_rn(g.fx, x3Dc[0]), invzc, g.cx);
     const float v = __fmaf_rn(__fmul_rn(g.fy, x3Dc[1]), invzc, g.cy);
-    if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) { *W = w; return; }
+    if (u < g.min_x || u > g.max_x || v < g.min_y || v > g.max_y) { if (sub == 0) *W = w; return; }
     const int oct = p.octave;
     const float th_eff = pass == 1 ? __fmul_rn(2.0f, th) : th;
     const float r = __fmul_rn(th_eff, g.scale[oct]);
@@ -127,7 +146,7 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     const int x1 = min(kCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(u, g.min_x), r), g.ginv_x)));
     const int y0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(v, g.min_y), r), g.ginv_y)));
     const int y1 = min(kRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(v, g.min_y), r), g.ginv_y)));
-    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { *W = w; return; }
+    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { if (sub == 0) *W = w; return; }
     w.x0 = (int16_t)x0; w.x1 = (int16_t)x1; w.y0 = (int16_t)y0; w.y1 = (int16_t)y1;
     const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
     const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
@@ -135,25 +154,38 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
     const float* uright = C.uright + (size_t)f * C.cap;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;  // keys are unique (CSR position in the low bits)
-    for (int ix = x0; ix <= x1; ix++)
-        for (int iy = y0; iy <= y1; iy++) {
-            const int c = ix * kRows + iy;
-            for (int j = GO[c]; j < GO[c + 1]; j++) {
-                const uint32_t key = candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g);
-                if (key < b2) {
-                    if (key < b1) {
-                        b2 = b1;
-                        if (key < b0) { b1 = b0; b0 = key; }
-                        else b1 = key;
-                    } else {
-                        b2 = key;
-                    }
-                }
-            }
-        }
-    w.best[0] = b0; w.best[1] = b1; w.best[2] = b2;
-    *W = w;
+    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;
+    // the window's cells (column-major, as the reference scans them) dealt round-robin to the point's lanes;
+    // x1 < x0 or y1 < y0 (an empty range) gives no cells
+    const int nrows = y1 - y0 + 1, ncells = x1 >= x0 && nrows > 0 ? (x1 - x0 + 1) * nrows : 0;
+    for (int cell = sub; cell < ncells; cell += kGrp) {
+        const int cx = cell / nrows, c = (x0 + cx) * kRows + y0 + (cell - cx * nrows);
+        const int j0 = GO[c], j1 = GO[c + 1];
+        for (int j = j0; j < j1; j++) ins3(b0, b1, b2, candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g));
+    }
+#pragma unroll
+    for (int o = kGrp / 2; o >= 1; o >>= 1) {
+        const uint32_t p0 = (uint32_t)__shfl_xor((int)b0, o), p1 = (uint32_t)__shfl_xor((int)b1, o),
+                       p2 = (uint32_t)__shfl_xor((int)b2, o);
+        ins3(b0, b1, b2, p0);
+        ins3(b0, b1, b2, p1);
+        ins3(b0, b1, b2, p2);
+    }
+    // lanes 0..2 resolve best[sub]'s keypoint and angle (read by the in-order walk)
+    const uint32_t mine = sub == 0 ? b0 : (sub == 1 ? b1 : b2);
+    if (sub < 3 && mine != kNone) {
+        const int k = GI[mine & 0xfffff];
+        W->kp[sub] = k;
+        W->kang[sub] = kun[k].angle;
+    }
+    if (sub == 0) {
+        // kp / kang: written by lanes 0..2
+        W->u = w.u; W->v = w.v; W->r = w.r; W->invzc = w.invzc;
+        W->x0 = w.x0; W->x1 = w.x1; W->y0 = w.y0; W->y1 = w.y1;
+        W->min_level = w.min_level; W->max_level = w.max_level; W->valid = w.valid; W->pad = 0;
+        W->best[0] = b0; W->best[1] = b1; W->best[2] = b2;
+    }
+    if (sub < 3 && mine == kNone) W->kp[sub] = -1;
 }
 
 // ComputeThreeMaxima
@@ -222,8 +254,8 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             for (int q = 0; q < 3; q++) {
                 best[q] = w.best[q];
                 if (valid && best[q] != kNone) {
-                    b[q] = GI[best[q] & 0xfffff];
-                    kang[q] = kun[b[q]].angle;
+                    b[q] = w.kp[q];  // resolved by the window kernel
+                    kang[q] = w.kang[q];
                 }
             }
             blocking = P[i].n_obs > 0;
@@ -381,11 +413,14 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
                                                                 LocalWindow* __restrict__ win,
                                                                 uint8_t* __restrict__ in_view) {
     tail_wave_priority();
-    const int f = blockIdx.x, i = blockIdx.y * kThreads + threadIdx.x;
+    const int f = blockIdx.x, sub = threadIdx.x & (kLGrp - 1);
+    const int i = blockIdx.y * kLPtsPerBlock + (int)(threadIdx.x / kLGrp);
     const spslam_local_frame& F = frames[f];
-    if (i >= F.n_points || i >= max_points) return;
+    if (i >= F.n_points || i >= max_points) return;  // uniform over the point's lanes, as every return below
     LocalWindow w{};
     w.best[0] = w.best[1] = w.best[2] = kNone;
+    w.kp[0] = w.kp[1] = w.kp[2] = -1;
+    w.oct[0] = w.oct[1] = w.oct[2] = -1;
     w.x0 = 1;
     w.x1 = 0;
     LocalWindow* W = win + (size_t)f * max_points + i;
@@ -393,8 +428,10 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     // points the frame already tracks (mnLastFrameSeen == the frame) are skipped before isInFrustum
     // (Tracking.cc:1396-1401); their mbTrackInView stays false
     if (P.seen && P.seen[F.seen_offset + p.id] == F.stamp) {
-        if (in_view) in_view[F.point_offset + i] = 0;
-        *W = w;
+        if (sub == 0) {
+            if (in_view) in_view[F.point_offset + i] = 0;
+            *W = w;
+        }
         return;
     }
     bool in = false;
@@ -430,8 +467,8 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
         level = n < 0 ? 0 : (n >= P.n_levels ? P.n_levels - 1 : n);
         in = true;
     } while (false);
-    if (in_view) in_view[F.point_offset + i] = in;
-    if (!in) { *W = w; return; }
+    if (in_view && sub == 0) in_view[F.point_offset + i] = in;
+    if (!in) { if (sub == 0) *W = w; return; }
     float r = viewCos > 0.998f ? 2.5f : 4.0f;  // RadiusByViewingCos
     if (P.th != 1.0f) r = __fmul_rn(r, P.th);
     const float rs = __fmul_rn(r, g.scale[level]);
@@ -442,7 +479,7 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     const int x1 = min(kCols - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(u, g.min_x), rs), g.ginv_x)));
     const int y0 = max(0, (int)floorf(__fmul_rn(__fsub_rn(__fsub_rn(v, g.min_y), rs), g.ginv_y)));
     const int y1 = min(kRows - 1, (int)ceilf(__fmul_rn(__fadd_rn(__fsub_rn(v, g.min_y), rs), g.ginv_y)));
-    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { *W = w; return; }
+    if (x0 >= kCols || x1 < 0 || y0 >= kRows || y1 < 0) { if (sub == 0) *W = w; return; }
     w.x0 = (int16_t)x0; w.x1 = (int16_t)x1; w.y0 = (int16_t)y0; w.y1 = (int16_t)y1;
     // the frame-to-frame candidate test with its window: same expressions (ur = fma(-mbf, invz, u))
     MatchWindow mw{};
@@ -457,26 +494,34 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
     uint32_t b0 = kNone, b1 = kNone, b2 = kNone;
-    for (int ix = x0; ix <= x1; ix++)
-        for (int iy = y0; iy <= y1; iy++) {
-            const int c = ix * kRows + iy;
-            for (int j = GO[c]; j < GO[c + 1]; j++) {
-                const int k = GI[j];
-                if (tk && tk[k]) continue;
-                const uint32_t key = candidate_key(mw, C, uright, desc, kun, j, k, d0, d1, g);
-                if (key < b2) {
-                    if (key < b1) {
-                        b2 = b1;
-                        if (key < b0) { b1 = b0; b0 = key; }
-                        else b1 = key;
-                    } else {
-                        b2 = key;
-                    }
-                }
-            }
+    // the window's cells dealt round-robin to the point's lanes, the lanes' 3 smallest keys merged (unique keys)
+    const int nrows = y1 - y0 + 1, ncells = x1 >= x0 && nrows > 0 ? (x1 - x0 + 1) * nrows : 0;
+    for (int cell = sub; cell < ncells; cell += kLGrp) {
+        const int cx = cell / nrows, c = (x0 + cx) * kRows + y0 + (cell - cx * nrows);
+        const int j0 = GO[c], j1 = GO[c + 1];
+        for (int j = j0; j < j1; j++) {
+            const int k = GI[j];
+            if (tk && tk[k]) continue;
+            ins3(b0, b1, b2, candidate_key(mw, C, uright, desc, kun, j, k, d0, d1, g));
         }
+    }
+#pragma unroll
+    for (int o = kLGrp / 2; o >= 1; o >>= 1) {
+        const uint32_t p0 = (uint32_t)__shfl_xor((int)b0, o), p1 = (uint32_t)__shfl_xor((int)b1, o),
+                       p2 = (uint32_t)__shfl_xor((int)b2, o);
+        ins3(b0, b1, b2, p0);
+        ins3(b0, b1, b2, p1);
+        ins3(b0, b1, b2, p2);
+    }
     w.best[0] = b0; w.best[1] = b1; w.best[2] = b2;
-    *W = w;
+    // the keypoint and octave of each of the 3 keys (read by the in-order walk), resolved here
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+        if (w.best[q] != kNone) {
+            w.kp[q] = GI[w.best[q] & 0xfffff];
+            w.oct[q] = kun[w.kp[q]].octave;
+        }
+    if (sub == 0) *W = w;
 }
 
 __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_frame* __restrict__ frames,
@@ -524,8 +569,8 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
             for (int q = 0; q < 3; q++) {
                 best[q] = w.best[q];
                 if (valid && best[q] != kNone) {
-                    b[q] = GI[best[q] & 0xfffff];
-                    oc[q] = kun[b[q]].octave;
+                    b[q] = w.kp[q];  // resolved by the window kernel
+                    oc[q] = w.oct[q];
                 }
             }
         }
@@ -652,7 +697,7 @@ hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, co
     if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
     if (timer) timer->begin(kKindLocalMatch, s);
     if (max_points > 0)
-        hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kThreads - 1) / match::kThreads),
+        hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kLPtsPerBlock - 1) / match::kLPtsPerBlock),
                            dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, win, in_view);
     hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), (size_t)((cur.cap + 31) / 32) * 4, s,
                        frames, points, max_points, cur, g, P, taken_in, win, match, nmatches);
@@ -670,7 +715,7 @@ hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const sps
     const int passes = P.retry_below > 0 ? 2 : 1;
     for (int pass = 0; pass < passes; pass++) {
         if (max_points > 0)
-            hipLaunchKernelGGL(match::match_window_kernel, dim3(n_frames, (max_points + match::kThreads - 1) / match::kThreads),
+            hipLaunchKernelGGL(match::match_window_kernel, dim3(n_frames, (max_points + match::kPtsPerBlock - 1) / match::kPtsPerBlock),
                                dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P.th, P.mono,
                                P.retry_below, pass, nmatches, win);
         hipLaunchKernelGGL(match::match_assign_kernel, dim3(n_frames), dim3(64), lds, s, frames, points, max_points, cur,

@@ -30,6 +30,8 @@ struct MatchWindow {
     int16_t x0, x1, y0, y1;  // GetFeaturesInArea cell range (x0 > x1: empty)
     int8_t min_level, max_level, valid, pad;
     uint32_t best[3];        // the 3 smallest (distance << 20) | CSR position over the window; ~0u: none
+    int32_t kp[3];           // their keypoints (grid_idx of the CSR position), -1: none
+    float kang[3];           // and those keypoints' angles
 };
 
 // Local-map search state per point (SearchLocalPoints).
@@ -38,6 +40,8 @@ struct LocalWindow {
     int16_t x0, x1, y0, y1;
     int8_t level, in_view, pad[2];
     uint32_t best[3];        // 3 smallest keys over the window without the initially taken keypoints
+    int32_t kp[3];           // their keypoints, -1: none
+    int32_t oct[3];          // and those keypoints' octaves
 };
 
 struct LocalConsts {

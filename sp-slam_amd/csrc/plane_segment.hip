@@ -683,6 +683,9 @@ __device__ __forceinline__ int trace_contour(const uint8_t* state, const uint8_t
 }
 
 template <bool kLdsMaps, int K>
+#ifdef SPSLAM_SEG_NUM_VGPR
+__attribute__((amdgpu_waves_per_eu(SPSLAM_SEG_NUM_VGPR)))
+#endif
 __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     PlaneGeom g, PlaneBuffers b, spslam_plane* __restrict__ planes_out, int* __restrict__ plane_counts, int planes_cap,
     int32_t* __restrict__ inliers_out, int32_t* __restrict__ contours_out) {

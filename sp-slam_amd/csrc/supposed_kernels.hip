@@ -267,7 +267,10 @@ __device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, 
     return block_sum(c, S);
 }
 
-__global__ __launch_bounds__(kThreads) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
+#ifndef SPSLAM_SUPP_MINB
+#define SPSLAM_SUPP_MINB 1
+#endif
+__global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
                                                               SuppBuffers sb, const float* __restrict__ depth,
                                                               long long depth_fs, int depth_stride,
                                                               const spslam_plane* __restrict__ planes,
