@@ -239,16 +239,24 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     int2* PU = pushes + (size_t)f * max_points;
     const float factor = __fdiv_rn(1.0f, (float)kHisto);
     int n_push = 0;
+    // every lane fetches its point's precomputed state, one round of loads per 64 points, issued one chunk
+    // ahead (in flight during the previous chunk's walk) ...
+    MatchWindow wn{};
+    int nobs_n = 0;
+    float pang_n = 0.f;
+    if (lane < np) { wn = Wf[lane]; nobs_n = P[lane].n_obs; pang_n = P[lane].angle; }
     for (int c0 = 0; c0 < np; c0 += 64) {
-        // every lane fetches its point's precomputed state (one round of loads per 64 points) ...
         const int i = c0 + lane;
         int valid = 0, blocking = 0;
         uint32_t best[3] = {kNone, kNone, kNone};
         int b[3] = {-1, -1, -1};
         float kang[3] = {0.f, 0.f, 0.f};
         float pangle = 0.f;
+        const MatchWindow w = wn;
+        const int nobs = nobs_n;
+        const float pang = pang_n;
+        if (i + 64 < np) { wn = Wf[i + 64]; nobs_n = P[i + 64].n_obs; pang_n = P[i + 64].angle; }
         if (i < np) {
-            const MatchWindow w = Wf[i];
             valid = w.valid;
 #pragma unroll
             for (int q = 0; q < 3; q++) {
@@ -258,8 +266,8 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
                     kang[q] = w.kang[q];
                 }
             }
-            blocking = P[i].n_obs > 0;
-            pangle = P[i].angle;
+            blocking = nobs > 0;
+            pangle = pang;
         }
         // ... then the reference's loop over the 64 points, in passes: every point still to do takes the first of
         // its 3 smallest keys whose keypoint is free; the points before the first one that cannot be decided
@@ -557,13 +565,16 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
     const float* uright = C.uright + (size_t)f * C.cap;
     const spslam_local_point* Pp = points + F.point_offset;
     int nm = 0;
+    LocalWindow wn{};  // the next chunk's window states, loaded one chunk ahead
+    if (lane < np) wn = Wf[lane];
     for (int c0 = 0; c0 < np; c0 += 64) {
         const int i = c0 + lane;
         int valid = 0;
         uint32_t best[3] = {kNone, kNone, kNone};
         int b[3] = {-1, -1, -1}, oc[3] = {-1, -1, -1};
+        const LocalWindow w = wn;
+        if (i + 64 < np) wn = Wf[i + 64];
         if (i < np) {
-            const LocalWindow w = Wf[i];
             valid = w.in_view;
 #pragma unroll
             for (int q = 0; q < 3; q++) {

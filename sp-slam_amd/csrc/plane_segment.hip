@@ -1144,10 +1144,16 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
 #ifndef SPSLAM_SEG_NO_EARLY_EXIT
     if (wave >= max(nk, 1)) return;
 #endif
+    // Each boundary is walked once, recorded while it is measured into a provisional slot of 2 x n_inliers
+    // points (the label scratch sizes..rootOf, 2N ints, dead since phase F; the slots sum to <= 2N); once the
+    // lengths fix the final offsets, each live wave moves its plane's walk into place.  A walk longer than its
+    // slot (a pathological boundary revisiting its pixels) is walked again, straight into its final place.
+    int32_t* ctmp = sizes;
     for (int q = wave; q < nk; q += kSegWaves)
         if (lane == 0) {
             const int m = S.kept[q];
-            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, nullptr, 0);
+            S.con_len[q] = trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1,
+                                         ctmp + 2 * planes[q].inlier_offset, 2 * planes[q].n_inliers);
         }
     __syncthreads();
     if (t == 0) {
@@ -1159,12 +1165,15 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         }
     }
     block_sync();
-    for (int q = wave; q < nk; q += kSegWaves)
-        if (lane == 0) {
-            const int m = S.kept[q];
-            trace_contour(state, nmask, W, H, N, S.con_start[q], m + 1, con + planes[q].contour_offset,
-                          planes[q].n_contour);
+    for (int q = wave; q < nk; q += kSegWaves) {
+        const int n = planes[q].n_contour, off = planes[q].contour_offset;
+        if (S.con_len[q] <= 2 * planes[q].n_inliers) {
+            const int32_t* src = ctmp + 2 * planes[q].inlier_offset;
+            for (int k = lane; k < n; k += 64) con[off + k] = src[k];
+        } else if (lane == 0) {
+            trace_contour(state, nmask, W, H, N, S.con_start[q], S.kept[q] + 1, con + off, n);
         }
+    }
     STAMP(9);
 #undef STAMP
 }
