@@ -267,8 +267,10 @@ __device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, 
     return block_sum(c, S);
 }
 
+// 3 waves per SIMD: 168 VGPRs instead of 172, so the LDS (43.9 KB) and not the registers bounds residency at
+// 3 workgroups per CU instead of 2 (1.35 -> 0.95 ms per 256 frames alone; profiles/r02/ab_contour_single_walk)
 #ifndef SPSLAM_SUPP_MINB
-#define SPSLAM_SUPP_MINB 1
+#define SPSLAM_SUPP_MINB 3
 #endif
 __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
                                                               SuppBuffers sb, const float* __restrict__ depth,
