@@ -417,6 +417,16 @@ int spslam_planes_generate_from_boundaries_batch_device(spslam_ctx* ctx, const f
                                                         int* d_out_counts, int32_t* d_line_idx, float* d_patch,
                                                         void* hip_stream);
 
+/* Pipelining (no reference counterpart; the reference runs both calls on one
+ * Frame before the next): the organized cloud that
+ * spslam_planes_extract_batch_device writes and
+ * spslam_planes_generate_from_boundaries_batch_device reads is one of two sets,
+ * chosen by this call for the calls enqueued after it (host order).  With
+ * alternating sets, batch k+1's extraction may run on one stream while batch
+ * k's supposed planes run on another; the caller orders a set's reuse after its
+ * last reader (stream events).  Set 0 after spslam_planes_configure. */
+int spslam_planes_select_cloud_set(spslam_ctx* ctx, int set);
+
 /* Parity access: the line candidates fitted on boundary `plane` of frame
  * `frame` in the last call, in fit order (<= 4; the last may be the failing
  * one).  Per candidate: line[6], inlier count, RANSAC trials, flags (1 kept

@@ -103,6 +103,7 @@ struct spslam_ctx {
     bool planes_ready = false;
     PlaneGeom pg{};
     PlaneBuffers pb{};
+    float* plane_cloud[2] = {nullptr, nullptr};  // organized-cloud sets (spslam_planes_select_cloud_set)
     void* d_plane_scratch = nullptr;
     float* d_depth_in = nullptr;
     spslam_plane* d_planes1 = nullptr;
@@ -602,7 +603,7 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     const long long SH = wave_size(g.W, g.H);
     b.cloud_fs = 3 * N; b.wave_fs = 8 * SH; b.dist_fs = N; b.integral_fs = 6 * (IWH + g.W + 1); b.normal_fs = 3 * N; b.pd_fs = N;
     b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N; b.maps_fs = 2 * N;
-    const size_t bytes = F * (sizeof(float) * (b.cloud_fs + b.wave_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
+    const size_t bytes = F * (sizeof(float) * (2 * b.cloud_fs + b.wave_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
                               sizeof(double) * b.integral_fs + sizeof(uint32_t) * b.labels_fs +
                               sizeof(int) * (b.work_fs + b.grown_fs) + b.maps_fs + 16 * sizeof(long long)) + 8192;
     if (c->d_plane_scratch) (void)hipFree(c->d_plane_scratch);
@@ -611,7 +612,9 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     uint8_t* q = (uint8_t*)c->d_plane_scratch;
     auto carve = [&](size_t n) { uint8_t* r = q; q += (n + 255) / 256 * 256; return r; };
     b.integral = (double*)carve(F * b.integral_fs * sizeof(double));
-    b.cloud = (float*)carve(F * b.cloud_fs * 4);
+    c->plane_cloud[0] = (float*)carve(F * b.cloud_fs * 4);
+    c->plane_cloud[1] = (float*)carve(F * b.cloud_fs * 4);
+    b.cloud = c->plane_cloud[0];
     b.wave = (float*)carve(F * b.wave_fs * 4);
     b.dist = (float*)carve(F * b.dist_fs * 4);
     b.normal = (float*)carve(F * b.normal_fs * 4);
@@ -693,6 +696,14 @@ int spslam_supposed_capacity(const spslam_ctx* c, int* supp_cap, int* line_cap, 
     if (supp_cap) *supp_cap = c->sp.supp_cap;
     if (line_cap) *line_cap = c->sp.line_cap;
     if (patch_points) *patch_points = c->sp.n_steps * c->sp.n_steps;
+    return SPSLAM_OK;
+}
+
+int spslam_planes_select_cloud_set(spslam_ctx* c, int set) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
+    if (set < 0 || set > 1) return fail(c, SPSLAM_ERR_ARG, "cloud set not 0 or 1%s", "");
+    c->pb.cloud = c->plane_cloud[set];
     return SPSLAM_OK;
 }
 

@@ -30,6 +30,8 @@ step.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import spslam_frame
@@ -340,10 +342,19 @@ class HotPath:
                                      self.d_desc.data_ptr(), self.d_cnt.data_ptr(), self.kp_cap, s)
 
     def planes(self, stream=None):
+        self.planes_extract(stream)
+        self.planes_supposed(stream)
+
+    def planes_extract(self, stream=None):
+        """ComputePlanesFromOrganizedPointCloud for the batch."""
         s = self.stream if stream is None else stream
         self.pe.extract_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
                                      self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_inl.data_ptr(),
                                      self.d_con.data_ptr(), s)
+
+    def planes_supposed(self, stream=None):
+        """GeneratePlanesFromBoundries for the batch (reads the extraction's organized clouds)."""
+        s = self.stream if stream is None else stream
         self.pe.generate_batch_device(self.d_depth.data_ptr(), self.B, self.W * self.H, self.W,
                                       self.d_planes.data_ptr(), self.d_pcnt.data_ptr(), self.d_con.data_ptr(),
                                       self.d_supp.data_ptr(), self.d_scnt.data_ptr(), self.d_lines.data_ptr(),
@@ -493,6 +504,11 @@ class HotPath:
         self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_grab = [torch.cuda.Event(), torch.cuda.Event()]
+        # The supposed planes run on the plane stream after the extraction.  SPSLAM_SUPP_ON_TAIL=1 (measurement
+        # knob) opens the tracking tail with them instead, on alternating cloud sets, so the next batch's
+        # extraction starts earlier: measured 1.5 % slower (the tail becomes the longer chain;
+        # profiles/r02/ab_supp_on_tail).
+        self.supp_on_plane_stream = os.environ.get("SPSLAM_SUPP_ON_TAIL") != "1"
         self.k = 0
         self.primed = False
         torch.cuda.synchronize()
@@ -508,7 +524,13 @@ class HotPath:
         self.grab(self.ext_orb.cuda_stream)
         self.ev_grab[j].record(self.ext_orb)
         self.ext_planes.wait_event(self.ev_grab[j])
-        self.planes(self.ext_planes.cuda_stream)
+        # (with SPSLAM_SUPP_ON_TAIL the batch's supposed planes open its tracking tail: they read the extraction's
+        # organized cloud, set j, while the next batch's extraction writes set 1 - j)
+        self.pe.select_cloud_set(j)
+        if self.supp_on_plane_stream:
+            self.planes(self.ext_planes.cuda_stream)
+        else:
+            self.planes_extract(self.ext_planes.cuda_stream)
         self.ev_planes[j].record(self.ext_planes)
         self.orb(self.ext_orb.cuda_stream)
         self.ev_orb[j].record(self.ext_orb)
@@ -546,6 +568,9 @@ class HotPath:
         self._bind(j)
         self.main.wait_event(self.ev_orb[j])
         self.main.wait_event(self.ev_planes[j])
+        if not self.supp_on_plane_stream:
+            self.pe.select_cloud_set(j)
+            self.planes_supposed(self.stream)
         self._tail()
         self.ev_tail[j].record(self.main)
         self._lba_end()

@@ -32,6 +32,7 @@ spslam_gpu.EXPORTED += ["spslam_planes_configure", "spslam_planes_capacity", "sp
                         "spslam_planes_extract_batch_device", "spslam_planes_debug", "spslam_supposed_capacity",
                         "spslam_planes_generate_from_boundaries",
                         "spslam_planes_generate_from_boundaries_batch_device", "spslam_supposed_debug",
+                        "spslam_planes_select_cloud_set",
                         "spslam_debug_plane_not_seen"]
 
 
@@ -50,6 +51,7 @@ def _bind(lib):
     lib.spslam_planes_generate_from_boundaries_batch_device.argtypes = [vp, vp, ctypes.c_int, ctypes.c_size_t,
                                                                         ctypes.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.spslam_supposed_debug.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp, ip, vp, ctypes.c_int]
+    lib.spslam_planes_select_cloud_set.argtypes = [vp, ctypes.c_int]
     lib.spslam_debug_plane_not_seen.argtypes = [vp, vp, ctypes.c_int, vp, ctypes.c_int, vp]
 
 
@@ -148,6 +150,10 @@ class PlaneExtractor:
             res["line_idx"].append(lines[o["line_offset"]:o["line_offset"] + o["n_line"]].copy())
             res["patch"].append(patch[o["patch_offset"]:o["patch_offset"] + o["n_patch"]].copy())
         return res
+
+    def select_cloud_set(self, cloud_set):
+        """The organized-cloud set of the extraction / supposed-plane calls enqueued next (0 or 1)."""
+        self.ex._check(self.ex.lib.spslam_planes_select_cloud_set(self.ex.ctx, cloud_set))
 
     def generate_batch_device(self, depth_ptr, n_frames, frame_stride, stride, planes_ptr, counts_ptr, contours_ptr,
                               out_ptr, out_counts_ptr, line_ptr, patch_ptr, stream=0):
