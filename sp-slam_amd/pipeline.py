@@ -509,6 +509,7 @@ class HotPath:
         # extraction starts earlier: measured 1.5 % slower (the tail becomes the longer chain;
         # profiles/r02/ab_supp_on_tail).
         self.supp_on_plane_stream = os.environ.get("SPSLAM_SUPP_ON_TAIL") != "1"
+        self.orb_after_supp = os.environ.get("SPSLAM_ORB_AFTER_SUPP") == "1"
         self.k = 0
         self.primed = False
         torch.cuda.synchronize()
@@ -532,6 +533,10 @@ class HotPath:
         else:
             self.planes_extract(self.ext_planes.cuda_stream)
         self.ev_planes[j].record(self.ext_planes)
+        if self.orb_after_supp and self.primed:
+            # the previous batch's supposed planes (the plane stream's head, on both critical chains) dispatch
+            # before this batch's pyramid floods the CUs' LDS
+            self.ext_orb.wait_event(self.ev_planes[1 - j])
         self.orb(self.ext_orb.cuda_stream)
         self.ev_orb[j].record(self.ext_orb)
 
