@@ -509,6 +509,8 @@ class HotPath:
         # extraction starts earlier: measured 1.5 % slower (the tail becomes the longer chain;
         # profiles/r02/ab_supp_on_tail).
         self.supp_on_plane_stream = os.environ.get("SPSLAM_SUPP_ON_TAIL") != "1"
+        # SPSLAM_ORB_AFTER_SUPP=1 (measurement knob): the next pyramid waits for the previous batch's supposed
+        # planes; measured 5 % slower (the GPU idles beside them; profiles/r02/ab_orb_after_supp)
         self.orb_after_supp = os.environ.get("SPSLAM_ORB_AFTER_SUPP") == "1"
         self.k = 0
         self.primed = False
