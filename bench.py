@@ -215,6 +215,15 @@ def _cpu_model():
     return "unknown"
 
 
+def _cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), None when unlimited or unreadable."""
+    try:
+        q, p = pathlib.Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        return None if q == "max" else max(1, -(-int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(hp, timed=300, warmup=10, all_core_frames=40):
     """CPU restatement (oracle) of the same per-frame work, timed in C++ (oracle/step_oracle.cpp: the whole chain
     of oracle_step.run with no Python between stages): one core, `warmup` untimed then `timed` frames; then every
@@ -229,12 +238,22 @@ def cpu_baseline(hp, timed=300, warmup=10, all_core_frames=40):
     if hp.n_lba:  # LocalMapping: one local BA per keyframe
         lba = ([p[:6] for p in hp.lba_problems], hp.lba_every, hp.plane_cfg)
     nf = hp.ex.params.nfeatures
-    el, outs = oracle_step_cpp.bench(inputs, nf, max(warmup, U), timed, 1, supp_cap=hp.pe.supp_cap, lba=lba)
+    import oracle_ctypes
+    # timed with the host glibc's double sin / cos / atan2 / pow (what a current build of the reference runs);
+    # the CPU reference poses of the ATE come from an untimed pass with the pinned, correctly rounded libm
+    el, _ = oracle_step_cpp.bench(inputs, nf, max(warmup, U), timed, 1, supp_cap=hp.pe.supp_cap, lba=lba,
+                                  libm=oracle_ctypes.LIBM_GLIBC)
+    _, outs = oracle_step_cpp.bench(inputs, nf, U, 0, 1, supp_cap=hp.pe.supp_cap, libm=oracle_ctypes.LIBM_CR)
     poses = {i: outs[i]["Tcw2"].reshape(16).copy() for i in range(U)}
     one = timed / el[0]
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))  # the GPU box's CPU share is 16 (nproc shows the whole machine)
-    el_all, _ = oracle_step_cpp.bench(inputs, nf, warmup, all_core_frames, threads, supp_cap=hp.pe.supp_cap, lba=lba)
+    # every core this process may use: its CPU set (sched_getaffinity), capped by the cgroup CPU quota when one
+    # is set (a GPU box grants one job a share of the machine; nproc / os.cpu_count() report the whole machine)
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = _cgroup_cpus()
+    share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    threads = max(1, min(x for x in (affinity, quota, share) if x))
+    el_all, _ = oracle_step_cpp.bench(inputs, nf, warmup, all_core_frames, threads, supp_cap=hp.pe.supp_cap, lba=lba,
+                                      libm=oracle_ctypes.LIBM_GLIBC)
     allc = threads * all_core_frames / el_all.max()
     lba_s = f" + LocalBundleAdjustment every {hp.lba_every} frames" if hp.n_lba else ""
     return dict(value=one, unit="frames/s", cores=1, kind="port",
@@ -242,8 +261,12 @@ def cpu_baseline(hp, timed=300, warmup=10, all_core_frames=40):
                        f"{hp.W}x{hp.H} workload (grab + ORB + planes + supposed planes + frame steps + "
                        f"SearchByProjection + 2x (plane association + graph + PoseOptimization) + SearchLocalPoints"
                        f"{lba_s}), {el[0]:.1f}s on one core, oracle/liboracle.so C++ -O3 x86-64-v3 "
-                       f"(oracle/step_oracle.cpp, no Python between stages)",
-                all_cores=dict(value=allc, unit="frames/s", threads=threads, frames_per_thread=all_core_frames,
+                       f"(oracle/step_oracle.cpp, no Python between stages), host glibc libm",
+                all_cores=dict(value=allc, unit="frames/s", threads=threads, affinity_cpus=affinity,
+                               cgroup_cpu_quota=quota, omp_num_threads=share,
+                               threads_rule="min(sched_getaffinity, cgroup cpu.max, OMP_NUM_THREADS): the CPU share "
+                                            "granted to this job (the GPU box sets OMP_NUM_THREADS to it)",
+                               frames_per_thread=all_core_frames,
                                warmup_per_thread=warmup, nproc=os.cpu_count(), cpu_model=_cpu_model(),
                                seconds=float(el_all.max()))), poses
 
@@ -293,13 +316,14 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
         out = {"kind": "tracked sequences (motion model from the previous frame; sp-slam_amd/sequence.py)",
                "sequences": n_seq, "frames": n_frames,
-               "cpu_ref": "CPU oracle with PoseOptimization summed in the kernel's order (oracle/pose_oracle.cpp "
-                          "device-order mode); g2o_order_cpu_ref: the same loop with g2o's edge-order sums",
+               "cpu_ref": "CPU oracle (oracle/oracle_sequence.py): PoseOptimization summed in g2o's edge order with "
+                          "Eigen's per-edge arithmetic and correctly rounded sin/cos/atan2/pow (the pinned libm, "
+                          "DESIGN.md 3.3); glibc_libm_cpu_ref: the same loop with the host glibc's double routines",
                "vs_cpu_ref_m": [], "max_center_diff_vs_cpu_ref_m": [],
                "max_rotation_diff_vs_cpu_ref": [], "vs_ground_truth_m": [], "cpu_ref_vs_ground_truth_m": [],
                "ate_difference_vs_cpu_ref_m": [], "identical_decisions_until_frame": [],
-               "g2o_order_cpu_ref": {"vs_gpu_m": [], "vs_device_order_cpu_ref_m": [], "vs_ground_truth_m": [],
-                                     "identical_decisions_until_frame": []}}
+               "glibc_libm_cpu_ref": {"vs_gpu_m": [], "vs_cpu_ref_m": [], "vs_ground_truth_m": [],
+                                      "identical_decisions_until_frame": []}}
         t1 = time.perf_counter()
 
         def run_oracle(slot, order):
@@ -313,18 +337,18 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                        on_frame=rec, pose_order=order)
+                                        on_frame=rec, libm=order)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
             return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
 
         from concurrent.futures import ThreadPoolExecutor
         jobs = [(slot, order) for slot in range(n_seq)
-                for order in (oracle_ctypes.POSE_ORDER_DEVICE, oracle_ctypes.POSE_ORDER_G2O)]
+                for order in (oracle_ctypes.LIBM_CR, oracle_ctypes.LIBM_GLIBC)]
         with ThreadPoolExecutor(len(jobs)) as pool:
             done = dict(zip(jobs, pool.map(lambda j: run_oracle(*j), jobs)))
         for slot in range(n_seq):
-            cpu, div = done[(slot, oracle_ctypes.POSE_ORDER_DEVICE)]
-            cpu_g, div_g = done[(slot, oracle_ctypes.POSE_ORDER_G2O)]
+            cpu, div = done[(slot, oracle_ctypes.LIBM_CR)]
+            cpu_g, div_g = done[(slot, oracle_ctypes.LIBM_GLIBC)]
             out["identical_decisions_until_frame"].append(div)
             g = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n_frames)]
             c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n_frames)]
@@ -337,9 +361,9 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             out["vs_ground_truth_m"].append(trajectory.ate_rmse(g, gt))
             out["cpu_ref_vs_ground_truth_m"].append(trajectory.ate_rmse(c, gt))
             out["ate_difference_vs_cpu_ref_m"].append(abs(out["vs_ground_truth_m"][-1] - out["cpu_ref_vs_ground_truth_m"][-1]))
-            go = out["g2o_order_cpu_ref"]
+            go = out["glibc_libm_cpu_ref"]
             go["vs_gpu_m"].append(trajectory.ate_rmse(g, cg))
-            go["vs_device_order_cpu_ref_m"].append(trajectory.ate_rmse(c, cg))
+            go["vs_cpu_ref_m"].append(trajectory.ate_rmse(c, cg))
             go["vs_ground_truth_m"].append(trajectory.ate_rmse(cg, gt))
             go["identical_decisions_until_frame"].append(div_g)
         out["cpu_frames_per_s"] = len(jobs) * n_frames / (time.perf_counter() - t1)  # len(jobs) threads

@@ -293,6 +293,12 @@ int spslam_lba_optimize(spslam_ctx* ctx, const spslam_lba_problem* problem, cons
                         uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result,
                         const volatile uint8_t* stop_flag);
 
+/* Test hook (deterministic LocalMapping::InterruptBA): the context's following
+ * LocalBundleAdjustment calls see pbStopFlag raised once a problem has run
+ * `trials` LM trials -- before optimize(5) when 0 -- at the same check points
+ * as a raised flag; -1 turns the hook off (default). */
+int spslam_lba_debug_stop_after(spslam_ctx* ctx, int trials);
+
 /* Batched, device resident: n problems (host copy `problems` for sizing, the
  * same records on the device at d_problems), one workgroup each, the whole
  * optimize(5) / relabel / optimize(10) schedule on the device.  Outputs are
@@ -455,6 +461,12 @@ int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_
  * supposed-plane kernels use; not_seen[k] = 1 when candidate k would be kept. */
 int spslam_debug_plane_not_seen(spslam_ctx* ctx, const float* planes, int n_planes, const float* coefs, int n_coefs,
                                 int* not_seen);
+
+/* Test hook: the device's double elementary functions (PoseOptimization and
+ * LocalBundleAdjustment: SE3Quat::exp, Plane3D, AngleAxis -> std::sin /
+ * std::cos / std::atan2 / std::pow(x, 3)), correctly rounded.
+ * kind 0 sin(a), 1 cos(a), 2 atan2(a, b), 3 a^3; n host doubles each. */
+int spslam_debug_libm64(spslam_ctx* ctx, int kind, const double* a, const double* b, int n, double* out);
 
 /* ------------------------------------------------------------------------
  * RGB-D Frame per-keypoint steps (src/Frame.cc:146-181): UndistortKeyPoints

@@ -13,22 +13,23 @@
 #include <cmath>
 #include <cstring>
 
-#include "../sp-slam_amd/csrc/libm64_restated.h"
+#include "libm_cr_oracle.h"
 
 namespace oracle {
 namespace g2o_math {
 
-// Elementary functions: glibc (what the reference calls) by default; the device-order mode of
-// pose_oracle.cpp switches this thread to the restatement the GPU kernels run (libm64_restated.h:
-// fdlibm sin / cos / atan2 within 1 ulp of glibc, a correctly rounded cube).
-inline bool& device_math() {
-    static thread_local bool on = false;
-    return on;
+// Elementary functions: correctly rounded by default (libm_cr_oracle.h: the
+// semantics the path pins, which the GPU's libm64_cr.h reproduces); libm mode 1 switches the calling thread
+// to the host glibc's double routines (glibc 2.35 here: fast paths that misround ~0.1 % of arguments) -- a
+// diagnostic of the path's sensitivity to the libm, and the CPU baseline's speed-representative libm.
+inline int& libm_mode() {
+    static thread_local int mode = 0;
+    return mode;
 }
-inline double o_sin(double x) { return device_math() ? spslam::libm64::sin_(x) : std::sin(x); }
-inline double o_cos(double x) { return device_math() ? spslam::libm64::cos_(x) : std::cos(x); }
-inline double o_atan2(double y, double x) { return device_math() ? spslam::libm64::atan2_(y, x) : std::atan2(y, x); }
-inline double o_cube(double x) { return device_math() ? spslam::libm64::cube_(x) : std::pow(x, 3); }
+inline double o_sin(double x) { return libm_mode() ? std::sin(x) : libm_cr::sin(x); }
+inline double o_cos(double x) { return libm_mode() ? std::cos(x) : libm_cr::cos(x); }
+inline double o_atan2(double y, double x) { return libm_mode() ? std::atan2(y, x) : libm_cr::atan2(y, x); }
+inline double o_cube(double x) { return libm_mode() ? std::pow(x, 3) : libm_cr::cube(x); }
 
 struct V3 { double x, y, z; };
 inline V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }

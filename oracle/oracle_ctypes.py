@@ -170,23 +170,34 @@ def descriptor(img: np.ndarray, x: float, y: float, angle: float) -> np.ndarray:
     return out
 
 
-POSE_ORDER_G2O, POSE_ORDER_DEVICE = 0, 1
+LIBM_CR, LIBM_GLIBC = 0, 1
+
+
+def libm_cr(kind: int, a, b=None):
+    """The oracle's correctly rounded sin (0) / cos (1) / atan2(a, b) (2) / cube (3) (oracle/libm_cr_oracle.h)."""
+    L = lib()
+    L.oracle_libm_cr.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p]
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(a if b is None else b, np.float64)
+    out = np.zeros_like(a)
+    L.oracle_libm_cr(int(kind), a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+    return out
 
 
 @contextlib.contextmanager
-def pose_order(mode: int):
-    """Summation order of the pose oracle inside the block, for the calling thread (oracle/pose_oracle.cpp):
-    POSE_ORDER_G2O (default, g2o's edge order + glibc) or POSE_ORDER_DEVICE (the GPU kernel's tree order +
-    libm64_restated.h)."""
+def libm(mode: int):
+    """Elementary functions of the pose / LBA oracle inside the block, for the calling thread
+    (oracle/g2o_restated.h libm_mode): LIBM_CR (default: correctly rounded, the path's pinned semantics,
+    DESIGN.md section 3.3) or LIBM_GLIBC (the host glibc's double sin / cos / atan2 / pow)."""
     L = lib()
-    L.oracle_get_pose_order.restype = ctypes.c_int
-    L.oracle_set_pose_order.argtypes = [ctypes.c_int]
-    prev = L.oracle_get_pose_order()
-    L.oracle_set_pose_order(int(mode))
+    L.oracle_get_libm.restype = ctypes.c_int
+    L.oracle_set_libm.argtypes = [ctypes.c_int]
+    prev = L.oracle_get_libm()
+    L.oracle_set_libm(int(mode))
     try:
         yield
     finally:
-        L.oracle_set_pose_order(prev)
+        L.oracle_set_libm(prev)
 
 
 def pose_optimize(problem, points, planes, cfg=None):

@@ -20,14 +20,14 @@ import oracle_track as OT
 
 
 def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb, planes,
-          supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None, pose_order=None):
+          supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None, libm=None):
     """frames: [(rgb, depth_u16)] of frames first .. ; T0 / P0: the pose and last-frame points of frame
     first - 1; local_of(t): the local map points of frame t (whole; the seen ones are skipped).  Returns the
-    local-map pose (float 4x4) of every frame.  pose_order: the PoseOptimization summation order
-    (oracle_ctypes.POSE_ORDER_*) for this call, on the calling thread; None keeps the current one."""
-    if pose_order is not None:
+    local-map pose (float 4x4) of every frame.  libm: the elementary functions of PoseOptimization
+    (oracle_ctypes.LIBM_*) for this call, on the calling thread; None keeps the current one."""
+    if libm is not None:
         import oracle_ctypes
-        with oracle_ctypes.pose_order(pose_order):
+        with oracle_ctypes.libm(libm):
             return track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb,
                          planes, supp_cap, min_size, pose_cfg, depth_scale, on_frame)
     Tlw = np.asarray(T0, np.float32).reshape(4, 4)

@@ -42,7 +42,7 @@ def _lib():
     if not getattr(L, "_step_bound", False):
         L.oracle_step_frame_run.argtypes = [vp, ctypes.c_int, vp]
         L.oracle_step_bench.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp,
-                                        vp, vp]
+                                        vp, vp, ctypes.c_int]
         L._step_bound = True
     return L
 
@@ -99,9 +99,10 @@ def _out(o):
     return d
 
 
-def bench(inputs, nfeatures, warmup, timed, threads, supp_cap=None, lba=None):
+def bench(inputs, nfeatures, warmup, timed, threads, supp_cap=None, lba=None, libm=0):
     """Timed loop (oracle_step_bench).  lba: (problems, lba_every, spslam_plane_config) with problems a list of
-    synth.lba_problem tuples.  Returns (per-thread timed seconds, thread 0's outputs per distinct frame)."""
+    synth.lba_problem tuples; libm: the workers' elementary functions (oracle_ctypes.LIBM_*).  Returns
+    (per-thread timed seconds, thread 0's outputs per distinct frame)."""
     fr = Frames(inputs, supp_cap)
     n = len(inputs)
     outs = (StepOut * n)()
@@ -120,6 +121,6 @@ def bench(inputs, nfeatures, warmup, timed, threads, supp_cap=None, lba=None):
         fr.keep += keep + cols
     rc = _lib().oracle_step_bench(ctypes.addressof(fr.recs), n, nfeatures, warmup, timed, threads,
                                   ctypes.byref(ls) if ls is not None else None, ctypes.addressof(outs),
-                                  el.ctypes.data)
+                                  el.ctypes.data, int(libm))
     assert rc == 0
     return el, [_out(o) for o in outs]

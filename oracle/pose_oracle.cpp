@@ -19,14 +19,19 @@
 // quaternion product and vector rotation, AngleAxis, LDLT with diagonal
 // pivoting).  All arithmetic is double, like the reference.
 //
-// Two summation orders (oracle_set_pose_order):
-//   0  g2o's: edge by edge in insertion order (BlockSolver::buildSystem,
-//      activeRobustChi2), glibc sin / cos / atan2 / pow -- the default;
-//   1  the GPU kernel's: the sums of sp-slam_amd/csrc/pose_kernels.hip wg_sum
-//      (256 lane-strided partials, xor butterflies over 64 lanes, four wave
-//      totals) and its per-edge term order, with libm64_restated.h's sin / cos /
-//      atan2 / cube.  The kernel must then agree bit for bit.
-// Both run the same LM algorithm; they differ only by the rounding of the sums.
+// Summation order and per-edge arithmetic are g2o's on Eigen's expression structure (no FMA: the
+// reference's -march=native build fuses Eigen's packet products only on FMA hosts, which it does not pin):
+//   chi2  = e . (Omega e)                                   (base_edge.h chi2 -> Eigen dot, in row order)
+//   unary (point) edges, BaseUnaryEdge::constructQuadraticForm (base_unary_edge.hpp:43-72):
+//     b -= (rho' A^T) Omega e,  A_vertex += A^T (rho' Omega) A     (per edge, then added)
+//   binary (plane) edges with the pose as vertex 1, BaseBinaryEdge::constructQuadraticForm
+//   (base_binary_edge.hpp:55-120): b += B^T (rho' (-Omega e)),  A_vertex += B^T (rho' Omega) B
+//   edges accumulated one by one in insertion order (BlockSolver::buildSystem, block_solver.hpp:529-545),
+//   the robust chi2 likewise (SparseOptimizer::activeRobustChi2, sparse_optimizer.cpp:100-114); the LDLT
+//   reads the lower triangle of the vertex block (Eigen::LDLT<MatrixXd, Lower>).
+// Elementary functions are correctly rounded by default; oracle_set_libm(1) switches this thread to the
+// host glibc (g2o_restated.h libm_mode).  The GPU kernel (sp-slam_amd/csrc/pose_kernels.hip) runs the same
+// arithmetic in the same order and must agree bit for bit with the default.
 #include <array>
 #include <cmath>
 #include <cstring>
@@ -51,7 +56,7 @@ struct Edge {
     V3 Xw;
     Plane world, mplane;
     double err[3] = {0, 0, 0};
-    double chi2() const { double s = 0; for (int i = 0; i < dim; i++) s += err[i] * info[i] * err[i]; return s; }
+    double chi2() const { double s = 0; for (int i = 0; i < dim; i++) s += err[i] * (info[i] * err[i]); return s; }  // e . (Omega e)
 };
 
 struct Cam { double fx, fy, cx, cy, bf; };
@@ -178,13 +183,53 @@ struct LM {
     int nBad = 0;
 };
 
+double huber_rho(const Edge& e, double chi, double* rho1) {
+    if (!e.rk.on || chi <= e.rk.dsqr) { *rho1 = 1.0; return chi; }
+    const double s = std::sqrt(chi);
+    *rho1 = e.rk.delta / s;
+    return 2 * s * e.rk.delta - e.rk.dsqr;
+}
+
+// base_edge.h chi2(): _error.dot(information() * _error), Omega diagonal
+double chi2_eigen(const Edge& e) {
+    double c = 0;
+    for (int k = 0; k < e.dim; k++) c += e.err[k] * (e.info[k] * e.err[k]);
+    return c;
+}
+
 double robust_chi2(const std::vector<Edge*>& active) {
     double chi = 0;
     for (Edge* e : active) {
-        if (e->rk.on) { double rho[3]; e->rk.robustify(e->chi2(), rho); chi += rho[0]; }
-        else chi += e->chi2();
+        double rho1;
+        chi += huber_rho(*e, chi2_eigen(*e), &rho1);
     }
     return chi;
+}
+
+// One edge's contribution to the pose vertex block: H_e (lower triangle, row-major i >= j) and the vector
+// s_e with b -= s_e.  A = the edge's Jacobian wrt the pose, rows k < dim.
+void quadratic_form(const Edge& e, const double J[3][6], double He[21], double se[6]) {
+    double rho1;
+    huber_rho(e, chi2_eigen(e), &rho1);
+    double wo[3], q[3];
+    for (int k = 0; k < e.dim; k++) {
+        wo[k] = rho1 * e.info[k];                     // robustInformation: rho' Omega
+        q[k] = (e.info[k] * e.err[k]) * rho1;         // binary: omega_r = -Omega e, *= rho'
+    }
+    for (int i = 0, n = 0; i < 6; i++)
+        for (int j = 0; j <= i; j++, n++) {            // (A^T (rho' Omega)) A, the temporary's row i
+            double h = 0;
+            for (int k = 0; k < e.dim; k++) h += (J[k][i] * wo[k]) * J[k][j];
+            He[n] = h;
+        }
+    for (int i = 0; i < 6; i++) {
+        double b = 0;
+        if (e.type <= 1)
+            for (int k = 0; k < e.dim; k++) b += ((rho1 * J[k][i]) * e.info[k]) * e.err[k];  // ((rho' A^T) Omega) e
+        else
+            for (int k = 0; k < e.dim; k++) b += J[k][i] * q[k];                             // B^T (rho' Omega e)
+        se[i] = b;
+    }
 }
 
 // SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg.
@@ -194,21 +239,18 @@ int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
     for (int it = 0; it < iterations; it++) {
         for (Edge* e : active) compute_error(*e, T, c);
         double currentChi = robust_chi2(active), tempChi = currentChi, iniChi = currentChi;
-        // buildSystem
+        // buildSystem: per edge H_e / s_e, accumulated in insertion order
         double H[6][6] = {}, b[6] = {};
         for (Edge* e : active) {
-            double J[3][6];
+            double J[3][6], He[21], se[6];
             jacobian(*e, T, c, J);
-            double w = 1.0;
-            if (e->rk.on) { double rho[3]; e->rk.robustify(e->chi2(), rho); w = rho[1]; }
-            for (int r = 0; r < e->dim; r++) {
-                const double oe = e->info[r] * e->err[r];
-                for (int i = 0; i < 6; i++) {
-                    b[i] -= w * J[r][i] * oe;
-                    for (int j = 0; j < 6; j++) H[i][j] += J[r][i] * (w * e->info[r]) * J[r][j];
-                }
-            }
+            quadratic_form(*e, J, He, se);
+            for (int i = 0, n = 0; i < 6; i++)
+                for (int j = 0; j <= i; j++, n++) H[i][j] += He[n];
+            for (int i = 0; i < 6; i++) b[i] -= se[i];
         }
+        for (int i = 0; i < 6; i++)
+            for (int j = i + 1; j < 6; j++) H[i][j] = H[j][i];  // the LDLT reads the lower triangle
         if (it == 0) {
             double maxDiag = 0;
             for (int j = 0; j < 6; j++) maxDiag = std::max(std::fabs(H[j][j]), maxDiag);
@@ -258,167 +300,28 @@ int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
 }
 
 
-// ---- device-order mode -------------------------------------------------------
-constexpr int kLanes = 256, kWaveLanes = 64;
-
-// wg_sum (pose_kernels.hip): per-thread partials -> xor butterfly per wave -> ((0 + w0) + w1) + w2) + w3
-template <size_t NV>
-void tree_total(const std::vector<std::array<double, NV>>& part, double* out) {
-    for (size_t k = 0; k < NV; k++) {
-        double s = 0;
-        for (int w = 0; w < kLanes / kWaveLanes; w++) {
-            double x[kWaveLanes], y[kWaveLanes];
-            for (int l = 0; l < kWaveLanes; l++) x[l] = part[w * kWaveLanes + l][k];
-            for (int off = kWaveLanes / 2; off >= 1; off >>= 1) {
-                for (int l = 0; l < kWaveLanes; l++) y[l] = x[l] + x[l ^ off];
-                std::memcpy(x, y, sizeof x);
-            }
-            s += x[0];
-        }
-        out[k] = s;
-    }
-}
-
-double huber_rho(const Edge& e, double chi, double* rho1) {
-    if (!e.rk.on || chi <= e.rk.dsqr) { *rho1 = 1.0; return chi; }
-    const double s = std::sqrt(chi);
-    *rho1 = e.rk.delta / s;
-    return 2 * s * e.rk.delta - e.rk.dsqr;
-}
-
-// 3-row error / Jacobian as the kernel holds them (rows beyond the edge's dimension are zero)
-void jacobian3(Edge& e, const SE3& T, const Cam& c, double J[3][6]) {
-    for (int r = 0; r < 3; r++)
-        for (int d = 0; d < 6; d++) J[r][d] = 0;
-    jacobian(e, T, c, J);
-}
-
-// the kernel's per-edge contribution (pose_kernels.hip accumulate)
-void accumulate_dev(const Edge& e, const double J[3][6], std::array<double, 28>& v) {
-    const double chi = (e.err[0] * e.info[0] * e.err[0] + e.err[1] * e.info[1] * e.err[1]) + e.err[2] * e.info[2] * e.err[2];
-    double rho1;
-    v[0] += huber_rho(e, chi, &rho1);
-    for (int i = 0; i < 6; i++)
-        for (int j = i; j < 6; j++) {
-            double s = 0;
-            for (int r = 0; r < 3; r++) s += J[r][i] * (rho1 * e.info[r]) * J[r][j];
-            v[1 + i * 6 - i * (i - 1) / 2 + (j - i)] += s;
-        }
-    for (int i = 0; i < 6; i++) {
-        double s = 0;
-        for (int r = 0; r < 3; r++) s += rho1 * J[r][i] * (e.info[r] * e.err[r]);
-        v[22 + i] -= s;
-    }
-}
-
-double robust_chi2_dev(Edge* edges, int ne, const std::vector<uint8_t>& active) {
-    std::vector<std::array<double, 1>> part(kLanes, {0.0});
-    for (int k = 0; k < ne; k++) {
-        if (!active[k]) continue;
-        const Edge& e = edges[k];
-        const double chi = (e.err[0] * e.info[0] * e.err[0] + e.err[1] * e.info[1] * e.err[1]) + e.err[2] * e.info[2] * e.err[2];
-        double rho1;
-        part[k % kLanes][0] += huber_rho(e, chi, &rho1);
-    }
-    double out;
-    tree_total(part, &out);
-    return out;
-}
-
-// SparseOptimizer::optimize with the kernel's summation order (edges[0..np) points, then planes)
-int optimize_dev(Edge* edges, int np, int ne, const std::vector<uint8_t>& active, SE3& T, const Cam& c,
-                 int iterations) {
-    LM lm;
-    int its = 0;
-    for (int it = 0; it < iterations; it++) {
-        for (int k = 0; k < ne; k++)
-            if (active[k]) compute_error(edges[k], T, c);
-        // pass A: point edge k on lane k % 256, then plane edge j on lane j % 64
-        std::vector<std::array<double, 28>> part(kLanes);
-        for (auto& p : part) p.fill(0.0);
-        for (int k = 0; k < ne; k++) {
-            if (!active[k]) continue;
-            double J[3][6];
-            jacobian3(edges[k], T, c, J);
-            accumulate_dev(edges[k], J, part[k < np ? k % kLanes : (k - np) % kWaveLanes]);
-        }
-        double tot[28];
-        tree_total(part, tot);
-        double currentChi = tot[0];
-        const double iniChi = currentChi;
-        double H[6][6], b[6];
-        for (int i = 0, k = 1; i < 6; i++)
-            for (int j = i; j < 6; j++, k++) H[i][j] = H[j][i] = tot[k];
-        for (int i = 0; i < 6; i++) b[i] = tot[22 + i];
-        if (it == 0) {
-            double maxDiag = 0;
-            for (int j = 0; j < 6; j++) maxDiag = std::max(std::fabs(H[j][j]), maxDiag);
-            lm.lambda = 1e-5 * maxDiag;
-            lm.ni = 2;
-            lm.nBad = 0;
-        }
-        double rho = 0;
-        int qmax = 0;
-        do {
-            SE3 backup = T;
-            double Hl[6][6];
-            std::memcpy(Hl, H, sizeof Hl);
-            for (int j = 0; j < 6; j++) Hl[j][j] += lm.lambda;
-            double x[6] = {0, 0, 0, 0, 0, 0};
-            bool ok2 = ldlt_solve(Hl, b, x);
-            T = SE3::exp(x) * T;
-            for (int k = 0; k < ne; k++)
-                if (active[k]) compute_error(edges[k], T, c);
-            double tempChi = robust_chi2_dev(edges, ne, active);
-            if (!ok2) tempChi = std::numeric_limits<double>::max();
-            rho = currentChi - tempChi;
-            double scale = 0;
-            for (int j = 0; j < 6; j++) scale += x[j] * (lm.lambda * x[j] + b[j]);
-            scale += 1e-3;
-            rho /= scale;
-            if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - o_cube(2 * rho - 1);
-                alpha = std::min(alpha, 2. / 3.);
-                lm.lambda *= std::max(1. / 3., alpha);
-                lm.ni = 2;
-                currentChi = tempChi;
-            } else {
-                lm.lambda *= lm.ni;
-                lm.ni *= 2;
-                T = backup;
-            }
-            qmax++;
-        } while (rho < 0 && qmax < 10);
-        its++;
-        if (qmax == 10 || rho == 0) break;
-        if ((iniChi - currentChi) * 1e3 < iniChi) lm.nBad++;
-        else lm.nBad = 0;
-        if (lm.nBad >= 3) break;
-    }
-    return its;
-}
-
-thread_local int g_pose_order = 0;  // per thread: concurrent oracle sequences may differ
-
-struct DeviceMathScope {  // switches this thread's g2o_math elementary functions for one call
-    bool prev;
-    explicit DeviceMathScope(bool on) : prev(device_math()) { device_math() = on; }
-    ~DeviceMathScope() { device_math() = prev; }
-};
 
 }  // namespace
 }  // namespace oracle
 
 using namespace oracle;
 
-extern "C" void oracle_set_pose_order(int mode) { g_pose_order = mode; }
-extern "C" int oracle_get_pose_order() { return g_pose_order; }
+// libm of the calling thread's PoseOptimization / LocalBundleAdjustment: 0 correctly rounded (default),
+// 1 host glibc (g2o_restated.h libm_mode)
+// the oracle's correctly rounded elementary functions (libm_cr_oracle.h) on n arguments: kind 0 sin, 1 cos,
+// 2 atan2(a, b), 3 cube -- the checker of the device's spslam_debug_libm64
+extern "C" void oracle_libm_cr(int kind, const double* a, const double* b, long n, double* out) {
+    for (long i = 0; i < n; i++)
+        out[i] = kind == 0 ? libm_cr::sin(a[i])
+                           : kind == 1 ? libm_cr::cos(a[i]) : kind == 2 ? libm_cr::atan2(a[i], b[i]) : libm_cr::cube(a[i]);
+}
+
+extern "C" void oracle_set_libm(int mode) { g2o_math::libm_mode() = mode; }
+extern "C" int oracle_get_libm() { return g2o_math::libm_mode(); }
 
 extern "C" int oracle_pose_optimize(const spslam_pose_problem* P, const spslam_point_obs* pts,
                                     const spslam_plane_obs* pls, const spslam_plane_config* cfg,
                                     spslam_pose_result* out, uint8_t* pout, uint8_t* plout) {
-    const bool dev = g_pose_order == 1;
-    DeviceMathScope math_scope(dev);
     M3 R;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) R.m[i][j] = P->Tcw[4 * i + j];
@@ -470,17 +373,10 @@ extern "C" int oracle_pose_optimize(const spslam_pose_problem* P, const spslam_p
     int nBad = 0, total_its = 0;
     for (int it = 0; it < 4; it++) {
         T = T0;
-        if (dev) {
-            std::vector<uint8_t> act(edges.size());
-            bool any = false;
-            for (size_t k = 0; k < edges.size(); k++) any |= (act[k] = edges[k].level == 0) != 0;
-            if (any) total_its += optimize_dev(edges.data(), P->n_points, (int)edges.size(), act, T, cam, 10);
-        } else {
-            std::vector<Edge*> active;
-            for (Edge& e : edges)
-                if (e.level == 0) active.push_back(&e);
-            total_its += optimize(active, T, cam, 10);
-        }
+        std::vector<Edge*> active;
+        for (Edge& e : edges)
+            if (e.level == 0) active.push_back(&e);
+        total_its += optimize(active, T, cam, 10);
         nBad = 0;
         for (size_t k = 0; k < edges.size(); k++) {
             Edge& e = edges[k];

@@ -367,16 +367,20 @@ int oracle_step_frame_run(const oracle_step_frame* F, int nfeatures, oracle_step
     return 0;
 }
 
+extern "C" void oracle_set_libm(int mode);  // pose_oracle.cpp: this thread's PoseOptimization / LBA libm
+
 // Timed loop: n_threads workers, each its own frame stream (thread t starts at distinct frame t) running
 // `warmup` untimed frames, a barrier, then `timed` frames (+ one LocalBundleAdjustment per lba_every frames when
 // lba is given).  elapsed[t] = thread t's timed seconds; outs (may be NULL) = thread 0's outputs of the distinct
-// frames, from its warm-up and timed frames (needs warmup + timed >= n_frames to cover them all).
+// frames, from its warm-up and timed frames (needs warmup + timed >= n_frames to cover them all).  libm: the
+// workers' elementary functions (oracle_set_libm: 0 correctly rounded, 1 the host glibc).
 int oracle_step_bench(const oracle_step_frame* frames, int n_frames, int nfeatures, int warmup, int timed,
-                      int n_threads, const oracle_lba_set* lba, oracle_step_out* outs, double* elapsed) {
+                      int n_threads, const oracle_lba_set* lba, oracle_step_out* outs, double* elapsed, int libm) {
     if (n_frames < 1 || n_threads < 1 || timed < 0 || warmup < 0) return -1;
     std::atomic<int> ready{0};
     std::vector<std::thread> th;
     auto body = [&](int t) {
+        oracle_set_libm(libm);
         Worker W(nfeatures);
         oracle_step_out o;
         int k = 0;
@@ -397,6 +401,7 @@ int oracle_step_bench(const oracle_step_frame* frames, int n_frames, int nfeatur
     for (int t = 1; t < n_threads; t++) th.emplace_back(body, t);
     body(0);
     for (auto& x : th) x.join();
+    oracle_set_libm(0);
     return 0;
 }
 

@@ -3,12 +3,12 @@
 // (lba_kernels.hip) kernels: SE3Quat (Thirdparty/g2o/g2o/types/se3quat.h),
 // Eigen quaternion / rotation conversions, g2oAddition/Plane3D.h.
 // See oracle/g2o_restated.h for the CPU restatement of the same routines.
-// sin / cos / atan2 / pow(x, 3) come from libm64_restated.h (the same code the
-// oracle's device-order mode runs on the host), not ocml.
+// sin / cos / atan2 / pow(x, 3) are correctly rounded (libm64_cr.h, the path's pinned libm semantics,
+// DESIGN.md section 3.3), not ocml's.
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include "libm64_restated.h"
+#include "libm64_cr.h"
 
 namespace spslam {
 namespace g2od {
@@ -114,8 +114,8 @@ __device__ __forceinline__ SE3 se3_exp(const double* u) {
         V = R;
     } else {
         double st, ct;
-        libm64::sincos_(theta, &st, &ct);
-        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / libm64::cube_(theta);
+        libm64cr::sincos_(theta, &st, &ct);
+        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / libm64cr::cube_(theta);
         for (int k = 0; k < 9; k++) {
             R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
             V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
@@ -136,14 +136,14 @@ __device__ __forceinline__ void p_normalize(double* v) {
     if (v[3] < 0.0)
         for (int i = 0; i < 4; i++) v[i] = -v[i];
 }
-__device__ __forceinline__ double azimuth(V3 v) { return libm64::atan2_(v.y, v.x); }
-__device__ __forceinline__ double elevation(V3 v) { return libm64::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
+__device__ __forceinline__ double azimuth(V3 v) { return libm64cr::atan2_(v.y, v.x); }
+__device__ __forceinline__ double elevation(V3 v) { return libm64cr::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
 // Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
 __device__ __forceinline__ M3 p_rotation(V3 v) {
     const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
     double sa, ca, se, ce;
-    libm64::sincos_(ha, &sa, &ca);
-    libm64::sincos_(he, &se, &ce);
+    libm64cr::sincos_(ha, &sa, &ca);
+    libm64cr::sincos_(he, &se, &ce);
     const Q a{ca, 0.0 * sa, 0.0 * sa, 1.0 * sa};
     const Q e{ce, 0.0 * se, 1.0 * se, 0.0 * se};
     return q_to_rot(q_mul(a, e));
@@ -151,7 +151,7 @@ __device__ __forceinline__ M3 p_rotation(V3 v) {
 // Eigen AngleAxis::toRotationMatrix() * v
 __device__ __forceinline__ V3 aa_apply(double ang, V3 ax, V3 v) {
     double s, c;
-    libm64::sincos_(ang, &s, &c);
+    libm64cr::sincos_(ang, &s, &c);
     const V3 sa = s * ax;
     const V3 c1 = (1 - c) * ax;
     M3 r;
@@ -196,8 +196,8 @@ __device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& wor
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)
 __device__ void p_oplus(P4& p, const double* v) {
     double s, c, s0, c0;
-    libm64::sincos_(v[1], &s, &c);
-    libm64::sincos_(v[0], &s0, &c0);
+    libm64cr::sincos_(v[1], &s, &c);
+    libm64cr::sincos_(v[0], &s0, &c0);
     const V3 n{c * c0, c * s0, s};
     const M3 R = p_rotation(V3{p.c[0], p.c[1], p.c[2]});
     const double d = -p.c[3] + v[2];

@@ -104,6 +104,7 @@ __device__ __forceinline__ void store_pose(double* p, const SE3& T) {
 // raised by another thread while the schedule runs), latched once seen
 __device__ __forceinline__ bool stop_requested(const LbaBatch& b, int p, LbaCtl& k) {
     if (!k.stop && b.stop) k.stop = __hip_atomic_load(b.stop + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    if (!k.stop && b.stop_after >= 0 && k.trials >= b.stop_after) k.stop = 1;  // spslam_lba_debug_stop_after
     return k.stop != 0;
 }
 
@@ -1145,7 +1146,7 @@ __global__ void k_decide(LbaBatch b, int step) {
     }
     double rho = (k.currentChi - tempChi) / (scale + 1e-3);
     if (rho > 0 && isfinite(tempChi)) {
-        double alpha = 1. - libm64::cube_(2 * rho - 1);
+        double alpha = 1. - libm64cr::cube_(2 * rho - 1);
         alpha = fmin(alpha, 2. / 3.);
         k.lambda *= fmax(1. / 3., alpha);
         k.ni = 2;

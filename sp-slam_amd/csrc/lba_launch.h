@@ -100,6 +100,7 @@ struct LbaBatch {
     spslam_lba_result* res;
     int* active;      // problems not DONE (polled by the host)
     const int32_t* stop;  // per problem pbStopFlag (device-visible; NULL = no flag)
+    int stop_after;       // test hook: the flag counts as raised once a problem has run this many trials (-1 off)
 };
 
 // Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase

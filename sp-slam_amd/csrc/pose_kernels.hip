@@ -3,21 +3,27 @@
 //
 // One 256-thread workgroup per frame problem runs all 4 rounds x <= 10 LM
 // iterations (x <= 10 trials) with no host round trip.  Per LM iteration:
-//   pass A  (all threads)  per-edge error, Huber weight and Jacobian, local
-//                          sums of robust chi2, J^T W J (21 terms), J^T W e (6)
-//   wg_sum                 wave butterflies + LDS, fp64; every thread gets the totals
+//   pass A  (all threads)  per-edge error, Huber weight and Jacobian, the edge's
+//                          robust chi2, lower J^T W J (21 terms) and J^T W e (6),
+//                          staged in LDS a chunk of edges at a time
+//   chain                  28 lanes add the staged terms edge by edge in g2o's
+//                          insertion order (BlockSolver::buildSystem,
+//                          SparseOptimizer::activeRobustChi2): the reference's
+//                          sums, not a tree
 //   solve   (lane q % K)   (H + lambda_q I) x = b by LDLT with diagonal pivoting
 //                          (Eigen::LDLT, solvers/linear_solver_dense.h:103-110)
 //                          for K damping trials at once, poses by readlane
-//   pass B  (all threads)  robust chi2 at exp(x_q) * T for the K trials, then
-//                          the reference's accept/reject walk, redundantly
+//   pass B  (all threads)  robust chi2 of every edge at exp(x_q) * T for the K
+//                          trials, chained in edge order by K lanes, then the
+//                          reference's accept/reject walk, redundantly
 // Outlier relabeling after each round reproduces the reference's use of the
 // errors cached by the LAST computeActiveErrors (which may belong to a
 // rejected trial): those errors are recomputed at that trial pose.
-// All arithmetic is fp64 like g2o/Eigen.  Sums run in one fixed tree order
-// (wg_sum) and sin / cos / atan2 / pow(x, 3) come from libm64_restated.h: the
-// oracle's device-order mode restates both and matches this kernel bit for
-// bit; against g2o's sequential edge order the result agrees to rounding.
+// All arithmetic is fp64 like g2o/Eigen, per edge in Eigen's expression
+// structure (oracle/pose_oracle.cpp quadratic_form) with contraction off, and
+// sin / cos / atan2 / pow(x, 3) are correctly rounded (libm64_cr.h): the
+// oracle's default mode restates the same arithmetic and this kernel matches
+// it bit for bit.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -164,14 +170,19 @@ constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
 constexpr int kPlaneChunk = 64;  // plane edges whose 13 errors (12 perturbed poses + T) are evaluated together
 constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
 
+constexpr int kStage = 256;      // edges per chained chunk
+constexpr int kStageStride = kRed + 1;  // odd stride in doubles: the 64 lanes' row writes spread over the banks
+
 template <int kSpec>
 struct Shared {
+    double stage[kStage][kStageStride];  // per-edge terms of one chunk (pass A: 28, pass B: kSpec)
+    double tot[kRed];                 // the chained totals, for every thread
     double red[2][kWaves][kRed];      // wave totals of the workgroup sums, double-buffered
     double perr[kPlaneChunk][13][3];  // plane errors at the 12 perturbed poses and at T
     double perrB[kPlaneChunk][kSpec][3];  // plane errors at the trial poses of the last pass B
     double perrT[kPlaneChunk][3];     // plane errors at the accepted trial pose = the next iteration's T
-    double hb[kWaves][kRed];
-    SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)          // each wave's copy of the iteration's H (upper, 21) and b (6), slot 0 unused
+    double hb[kRed];                  // the iteration's H (lower, 21) and b (6), slot 0 unused
+    SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)
     SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
 };
 
@@ -208,6 +219,20 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
     const double s = sqrt(chi);
     *rho0 = 2 * s * delta - dsqr;
     *rho1 = delta / s;
+}
+
+// acc += col[0], col[stride], ... col[(cnt - 1) stride] one after the other (the reference's order); the
+// loads run ahead of the dependent adds in groups of 8
+__device__ __forceinline__ void chain_add(double& acc, const double* col, int cnt) {
+    int i = 0;
+    for (; i + 8 <= cnt; i += 8) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = col[(i + k) * kStageStride];
+#pragma unroll
+        for (int k = 0; k < 8; k++) acc += v[k];
+    }
+    for (; i < cnt; i++) acc += col[i * kStageStride];
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -318,8 +343,9 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
     };
     auto chi2_of = [](const double* err, const double* info) __attribute__((always_inline)) {
-        // rows beyond the edge's dimension hold a zero error: their +0 terms leave chi unchanged
-        return (err[0] * info[0] * err[0] + err[1] * info[1] * err[1]) + err[2] * info[2] * err[2];
+        // e . (Omega e) (base_edge.h chi2); rows beyond the edge's dimension hold a zero error: their +0 terms
+        // leave chi unchanged
+        return (err[0] * (info[0] * err[0]) + err[1] * (info[1] * err[1])) + err[2] * (info[2] * err[2]);
     };
     auto is_outlier = [&](int e) __attribute__((always_inline)) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
 
@@ -339,58 +365,83 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
             int lmBad = 0;
             bool tValid = false;  // perrT holds the plane errors at T (set when a trial is accepted)
             for (int it = 0; it < 10; it++) {
-                // ---- pass A: errors, robust chi2, quadratic form at T
-                double v[kRed];
-#pragma unroll
-                for (int k = 0; k < kRed; k++) v[k] = 0;
-                // accumulate one edge's robust chi2, J^T W J and -J^T W e
-                auto accumulate = [&](const double (&J)[3][6], const double* err, const double* info, double delta) {
+                // ---- pass A: errors, robust chi2, quadratic form at T, chained in edge order
+                // one edge's terms into row t of the stage: its robust chi2, the lower triangle of its
+                // H_e (BaseUnaryEdge / BaseBinaryEdge::constructQuadraticForm in Eigen's order: the
+                // temporary A^T (rho' Omega) times A) and -s_e with b -= s_e (unary: ((rho' A^T) Omega) e;
+                // binary, pose = vertex 1: B^T (rho' Omega e))
+                auto stage_terms = [&](const double (&J)[3][6], const double* err, const double* info, double delta,
+                                       bool binary) __attribute__((always_inline)) {
+                    double* row = S.stage[t];
                     double rho0, rho1;
                     huber(chi2_of(err, info), delta, robust, &rho0, &rho1);
-                    v[0] += rho0;
+                    row[0] = rho0;
+                    double wo[3], q[3];
+#pragma unroll
+                    for (int r = 0; r < 3; r++) { wo[r] = rho1 * info[r]; q[r] = (info[r] * err[r]) * rho1; }
 #pragma unroll
                     for (int i = 0; i < 6; i++)
 #pragma unroll
-                        for (int j = i; j < 6; j++) {
-                            double s = 0;
+                        for (int j = 0; j <= i; j++) {
+                            double h = 0;
 #pragma unroll
-                            for (int r = 0; r < 3; r++) s += J[r][i] * (rho1 * info[r]) * J[r][j];
-                            v[1 + i * 6 - i * (i - 1) / 2 + (j - i)] += s;
+                            for (int r = 0; r < 3; r++) h += (J[r][i] * wo[r]) * J[r][j];
+                            row[1 + i * (i + 1) / 2 + j] = h;
                         }
 #pragma unroll
                     for (int i = 0; i < 6; i++) {
-                        double s = 0;
+                        double sb = 0;
+                        if (binary) {
 #pragma unroll
-                        for (int r = 0; r < 3; r++) s += rho1 * J[r][i] * (info[r] * err[r]);
-                        v[22 + i] -= s;
+                            for (int r = 0; r < 3; r++) sb += J[r][i] * q[r];
+                        } else {
+#pragma unroll
+                            for (int r = 0; r < 3; r++) sb += ((rho1 * J[r][i]) * info[r]) * err[r];
+                        }
+                        row[22 + i] = -sb;
                     }
                 };
-                for (int e = t; e < np; e += kThreads) {
-                    if (pout[e]) continue;
-                    double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
-                    edge_info(e, info, &delta);
-                    V3 pc;
-                    error_at(e, T, err, &pc);
-                    const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
-                    J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-                    J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
-                    J[0][5] = x * invz_2 * cam.fx;
-                    J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
-                    J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
-                    J[1][5] = y * invz_2 * cam.fy;
-                    if (pts[e].ur >= 0) {
-                        J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
-                        J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
-                    } else {
+                auto stage_zero = [&]() __attribute__((always_inline)) {
 #pragma unroll
-                        for (int d = 0; d < 6; d++) J[2][d] = 0;
+                    for (int k = 0; k < kRed; k++) S.stage[t][k] = 0.0;
+                };
+                // value k of the 28 is chained by lane k / 4 of wave k % 4
+                const int ck = lane * kWaves + (t >> 6);
+                const bool chainer = lane * kWaves < kRed;
+                double achain = 0;
+                for (int base = 0; base < np; base += kStage) {
+                    const int e = base + t;
+                    if (e < np && !pout[e]) {
+                        double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
+                        edge_info(e, info, &delta);
+                        V3 pc;
+                        error_at(e, T, err, &pc);
+                        const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
+                        J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+                        J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
+                        J[0][5] = x * invz_2 * cam.fx;
+                        J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
+                        J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
+                        J[1][5] = y * invz_2 * cam.fy;
+                        if (pts[e].ur >= 0) {
+                            J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
+                            J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
+                        } else {
+#pragma unroll
+                            for (int d = 0; d < 6; d++) J[2][d] = 0;
+                        }
+                        stage_terms(J, err, info, delta, false);
+                    } else {
+                        stage_zero();
                     }
-                    accumulate(J, err, info, delta);
+                    __syncthreads();
+                    if (chainer) chain_add(achain, &S.stage[0][ck], min(kStage, np - base));
+                    __syncthreads();
                 }
                 PROF_MARK(1);  // pass A point edges
                 // plane edges: numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205); the 13
                 // evaluations of a chunk's edges (12 perturbed poses exp(+-1e-9 e_d) * T, and T) run on
-                // 13 x chunk threads, then thread j accumulates the chunk's edge j
+                // 13 x chunk threads, then thread j stages the chunk's edge j
                 // after an accepted trial the errors at T are the ones pass B evaluated at that trial pose
                 // (kept in perrT when the plane edges fit one chunk): 12 evaluations per edge instead of 13
                 const bool haveT = tValid && nl <= kPlaneChunk;
@@ -426,33 +477,32 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
 #pragma unroll
                                 for (int r = 0; r < 3; r++)
                                     J[r][d] = scalar * (S.perr[t][2 * d][r] - S.perr[t][2 * d + 1][r]);
-                            accumulate(J, err, info, delta);
+                            stage_terms(J, err, info, delta, true);
+                        } else {
+                            stage_zero();
                         }
                     }
-                    if (base + kPlaneChunk < nl) __syncthreads();  // perr reuse (the last chunk: wg_sum's barrier)
+                    __syncthreads();
+                    if (chainer) chain_add(achain, &S.stage[0][ck], cnt);
+                    __syncthreads();  // stage / perr reuse
                 }
                 PROF_MARK(2);  // pass A plane edges
-                wg_sum(v, S, buf);
-                double currentChi = v[0];
+                if (chainer) S.tot[ck] = achain;
+                __syncthreads();
+                double currentChi = S.tot[0];
                 const double iniChi = currentChi;
-                // H and b wait in LDS (one copy per wave, written by its lane 0) for the trial passes: kept in
-                // registers they would stay live across pass B
-                double* hbw = S.hb[t >> 6];
-                if (lane == 0) {
-#pragma unroll
-                    for (int k = 1; k < kRed; k++) hbw[k] = v[k];
-                }
+                // H and b wait in LDS for the trial passes: kept in registers they would stay live across pass B
+                const double* hbw = S.hb;
+                if (t < kRed) S.hb[t] = S.tot[t];
                 if (it == 0) {
                     double md = 0;
 #pragma unroll
-                    for (int j = 0; j < 6; j++) md = fmax(fabs(v[1 + j * 6 - j * (j - 1) / 2]), md);
+                    for (int j = 0; j < 6; j++) md = fmax(fabs(S.tot[1 + j * (j + 1) / 2 + j]), md);
                     lambda = 1e-5 * md;
                     ni = 2;
                     lmBad = 0;
                 }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                __syncthreads();
                 PROF_MARK(3);  // reduce A + iteration setup
                 // ---- damping trials, kSpec per pass over the edges
                 double rho = 0;
@@ -469,7 +519,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
 #pragma unroll
                         for (int i = 0; i < 6; i++)
 #pragma unroll
-                            for (int j = i; j < 6; j++, k++) H[i][j] = H[j][i] = hbw[k];
+                            for (int j = 0; j <= i; j++, k++) H[i][j] = H[j][i] = hbw[k];
 #pragma unroll
                         for (int i = 0; i < 6; i++) b[i] = hbw[22 + i];
                     }
@@ -491,32 +541,15 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                     }
                     PROF_MARK(4);  // solves + exp + broadcast
                     PROF_COUNT(10);
-                    // robust chi2 of every active edge at each trial pose.  Thread t sums the edges e = t
-                    // (mod 256) of the combined index (points, then planes) in order.  A plane error costs far
-                    // more than a point error, so the (plane edge, trial) pairs are evaluated one per thread
-                    // first and handed to their owners through LDS (reusing perr).
-                    double c[kSpec];
-#pragma unroll
-                    for (int q = 0; q < kSpec; q++) c[q] = 0;
-                    for (int e = t; e < np; e += kThreads) {
-                        if (pout[e]) continue;
-                        double info[3], delta;
-                        edge_info(e, info, &delta);
-#pragma unroll
-                        for (int q = 0; q < kSpec; q++) {
-                            double err[3] = {0, 0, 0}, rho0, rho1;
-                            error_at(e, Tq[q], err, nullptr);
-                            huber(chi2_of(err, info), delta, robust, &rho0, &rho1);
-                            c[q] += rho0;
-                        }
-                    }
+                    // robust chi2 of every active edge at each trial pose, chained in edge order by lane 0 of
+                    // wave q.  A plane error costs far more than a point error, so the (plane edge, trial)
+                    // pairs are evaluated one per thread first (into perr's space).
                     double* prho = &S.perr[0][0][0];
-                    static_assert(kPlaneChunk * kSpec <= kPlaneChunk * 13 * 3, "one LDS round when perrB is kept");
-                    constexpr int kPairs = kPlaneChunk * 13 * 3;  // pairs per LDS round
-                    for (int base = 0; base < nl * kSpec; base += kPairs) {
-                        const int cnt = min(kPairs, nl * kSpec - base);
-                        for (int w = t; w < cnt; w += kThreads) {
-                            const int pr = base + w, j = pr / kSpec, q = pr - j * kSpec;
+                    constexpr int kPairPlanes = kPlaneChunk * 13 * 3 / kSpec;  // plane edges per prho round
+                    auto pairs = [&](int pb) __attribute__((always_inline)) {
+                        const int cnt = min(kPairPlanes, nl - pb);
+                        for (int w = t; w < cnt * kSpec; w += kThreads) {
+                            const int j = pb + w / kSpec, q = w % kSpec;
                             double r0 = 0;
                             if (!plout[j]) {
                                 double info[3], delta, err[3] = {0, 0, 0}, rho1;
@@ -533,18 +566,50 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                             }
                             prho[w] = r0;
                         }
-                        __syncthreads();
-                        // owner of plane edge j: thread (np + j) % 256, in increasing j
-                        for (int j = ((t - np) % kThreads + kThreads) % kThreads; j < nl; j += kThreads) {
-                            if (j * kSpec < base || j * kSpec >= base + cnt || plout[j]) continue;
+                    };
+                    pairs(0);
+                    double cq = 0;
+                    const bool qchainer = lane == 0 && (t >> 6) < kSpec;
+                    for (int base = 0; base < np; base += kStage) {
+                        const int e = base + t;
+                        double r[kSpec];
 #pragma unroll
-                            for (int q = 0; q < kSpec; q++) c[q] += prho[j * kSpec + q - base];
+                        for (int q = 0; q < kSpec; q++) r[q] = 0;
+                        if (e < np && !pout[e]) {
+                            double info[3], delta;
+                            edge_info(e, info, &delta);
+#pragma unroll
+                            for (int q = 0; q < kSpec; q++) {
+                                double err[3] = {0, 0, 0}, rho1;
+                                error_at(e, Tq[q], err, nullptr);
+                                huber(chi2_of(err, info), delta, robust, &r[q], &rho1);
+                            }
                         }
-                        if (base + kPairs < nl * kSpec) __syncthreads();  // prho reuse (last round: wg_sum's)
+#pragma unroll
+                        for (int q = 0; q < kSpec; q++) S.stage[t][q] = r[q];
+                        __syncthreads();
+                        if (qchainer) chain_add(cq, &S.stage[0][t >> 6], min(kStage, np - base));
+                        __syncthreads();
                     }
+                    for (int pb = 0; pb < nl; pb += kPairPlanes) {
+                        if (pb > 0) pairs(pb);  // prho's previous round was chained (the loop's last barrier)
+                        __syncthreads();
+                        const int cntp = min(kPairPlanes, nl - pb);
+                        for (int sb = 0; sb < cntp; sb += kStage) {
+#pragma unroll
+                            for (int q = 0; q < kSpec; q++) S.stage[t][q] = sb + t < cntp ? prho[(sb + t) * kSpec + q] : 0.0;
+                            __syncthreads();
+                            if (qchainer) chain_add(cq, &S.stage[0][t >> 6], min(kStage, cntp - sb));
+                            __syncthreads();
+                        }
+                    }
+                    if (qchainer) S.tot[t >> 6] = cq;
                     PROF_MARK(5);  // pass B (trial chi2)
-                    wg_sum(c, S, buf);
-                    // the reference's accept / reject sequence over the evaluated trials
+                    __syncthreads();
+                    double c[kSpec];
+#pragma unroll
+                    for (int q = 0; q < kSpec; q++) c[q] = S.tot[q];
+                // the reference's accept / reject sequence over the evaluated trials
                     int acc = -1, lastq = 0;
 #pragma unroll
                     for (int q = 0; q < kSpec; q++) {
@@ -554,7 +619,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                             double r = currentChi - tempChi;
                             r /= sc[q];
                             if (r > 0 && isfinite(tempChi)) {
-                                double alpha = 1. - libm64::cube_(2 * r - 1);
+                                double alpha = 1. - libm64cr::cube_(2 * r - 1);
                                 alpha = fmin(alpha, 2. / 3.);
                                 lambda *= fmax(1. / 3., alpha);
                                 ni = 2;
@@ -646,6 +711,26 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
 #endif
 }
 
+
+// test hook (spslam_debug_libm64): the correctly rounded routines as the pose / LBA kernels run them
+__global__ void libm64_debug_kernel(int kind, const double* __restrict__ a, const double* __restrict__ b, int n,
+                                    double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = a[i];
+    double r;
+    if (kind == 0) r = libm64cr::sin_(x);
+    else if (kind == 1) r = libm64cr::cos_(x);
+    else if (kind == 2) r = libm64cr::atan2_(x, b[i]);
+    else r = libm64cr::cube_(x);
+    out[i] = r;
+}
+
+hipError_t libm64_debug_launch(int kind, const double* a, const double* b, int n, double* out, hipStream_t s) {
+    if (n < 1) return hipSuccess;
+    hipLaunchKernelGGL(libm64_debug_kernel, dim3((n + 255) / 256), dim3(256), 0, s, kind, a, b, n, out);
+    return hipGetLastError();
+}
 
 PoseConsts make_pose_consts(const spslam_plane_config& c) {
     PoseConsts K;

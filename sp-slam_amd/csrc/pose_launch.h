@@ -15,6 +15,7 @@ struct PoseConsts {
 };
 
 PoseConsts make_pose_consts(const spslam_plane_config& c);
+hipError_t libm64_debug_launch(int kind, const double* a, const double* b, int n, double* out, hipStream_t s);
 hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_point_obs* pts,
                        const spslam_plane_obs* pls, const PoseConsts& K, const spslam_pose_result* init_from,
                        spslam_pose_result* res, uint8_t* pout, uint8_t* plout, hipStream_t s);

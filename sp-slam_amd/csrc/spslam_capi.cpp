@@ -129,6 +129,7 @@ struct spslam_ctx {
     size_t lba_scratch_bytes = 0;
     long long* d_lba_off = nullptr;
     int32_t* h_lba_stop = nullptr;    // host-mapped coherent pbStopFlag mirror of spslam_lba_optimize
+    int lba_stop_after = -1;          // spslam_lba_debug_stop_after
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
     size_t lba_stage_bytes = 0;
@@ -783,6 +784,23 @@ int spslam_debug_plane_not_seen(spslam_ctx* c, const float* planes, int n_planes
     return SPSLAM_OK;
 }
 
+int spslam_debug_libm64(spslam_ctx* c, int kind, const double* a, const double* b, int n, double* out) {
+    if (!c || n < 0 || kind < 0 || kind > 3 || (n && (!a || !out || (kind == 2 && !b)))) return SPSLAM_ERR_ARG;
+    if (!n) return SPSLAM_OK;
+    HIP_CHECK(c, hipSetDevice(c->device));
+    const size_t nb = (size_t)n * 8;
+    uint8_t* q = nullptr;
+    HIP_CHECK(c, hipMallocAsync((void**)&q, 3 * nb, c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(q, a, nb, hipMemcpyHostToDevice, c->stream));
+    if (kind == 2) HIP_CHECK(c, hipMemcpyAsync(q + nb, b, nb, hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(c, libm64_debug_launch(kind, (const double*)q, (const double*)(q + nb), n, (double*)(q + 2 * nb),
+                                     c->stream));
+    HIP_CHECK(c, hipMemcpyAsync(out, q + 2 * nb, nb, hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipFreeAsync(q, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    return SPSLAM_OK;
+}
+
 int spslam_supposed_debug(spslam_ctx* c, int frame, int plane, spslam_line_candidate* cand, int* n_cand,
                           int32_t* idx, int idx_cap) {
     static_assert(sizeof(spslam_line_candidate) == sizeof(LineCand), "candidate layout");
@@ -1058,12 +1076,18 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
               w0 + ec.size() + lc.size() + kt.size() + pt.size(), (int)qt.size()};
     LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
-               (int*)(c->d_lba_work + work.size() - 1), d_stop_flags};
+               (int*)(c->d_lba_work + work.size() - 1), d_stop_flags, c->lba_stop_after};
     // optimize(5) + optimize(10), at most 10 trials per iteration, plus the two structure steps
     HIP_CHECK(c, lba_run(B, W, C, 15 * 10 + 4, s, c->timer, nullptr, stop_src, stop_mirror));
     return SPSLAM_OK;
 }
 }  // namespace
+
+int spslam_lba_debug_stop_after(spslam_ctx* c, int trials) {
+    if (!c || trials < -1) return SPSLAM_ERR_ARG;
+    c->lba_stop_after = trials;
+    return SPSLAM_OK;
+}
 
 int spslam_lba_optimize_batch_device(spslam_ctx* c, int n, const spslam_lba_problem* problems,
                                      const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,

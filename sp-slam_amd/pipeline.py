@@ -30,7 +30,6 @@ step.
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 
@@ -504,14 +503,10 @@ class HotPath:
         self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_grab = [torch.cuda.Event(), torch.cuda.Event()]
-        # The supposed planes run on the plane stream after the extraction.  SPSLAM_SUPP_ON_TAIL=1 (measurement
-        # knob) opens the tracking tail with them instead, on alternating cloud sets, so the next batch's
-        # extraction starts earlier: measured 1.5 % slower (the tail becomes the longer chain;
-        # profiles/r02/ab_supp_on_tail).
-        self.supp_on_plane_stream = os.environ.get("SPSLAM_SUPP_ON_TAIL") != "1"
-        # SPSLAM_ORB_AFTER_SUPP=1 (measurement knob): the next pyramid waits for the previous batch's supposed
-        # planes; measured 5 % slower (the GPU idles beside them; profiles/r02/ab_orb_after_supp)
-        self.orb_after_supp = os.environ.get("SPSLAM_ORB_AFTER_SUPP") == "1"
+        # The supposed planes run on the plane stream right after the extraction.  Two alternatives were
+        # measured slower in round 2 and removed: opening the tracking tail with them (1.5 %,
+        # profiles/r02/ab_supp_on_tail) and holding the next pyramid until they finish (5 %,
+        # profiles/r02/ab_orb_after_supp).
         self.k = 0
         self.primed = False
         torch.cuda.synchronize()
@@ -527,18 +522,9 @@ class HotPath:
         self.grab(self.ext_orb.cuda_stream)
         self.ev_grab[j].record(self.ext_orb)
         self.ext_planes.wait_event(self.ev_grab[j])
-        # (with SPSLAM_SUPP_ON_TAIL the batch's supposed planes open its tracking tail: they read the extraction's
-        # organized cloud, set j, while the next batch's extraction writes set 1 - j)
-        self.pe.select_cloud_set(j)
-        if self.supp_on_plane_stream:
-            self.planes(self.ext_planes.cuda_stream)
-        else:
-            self.planes_extract(self.ext_planes.cuda_stream)
+        self.pe.select_cloud_set(j)  # batch j's organized cloud (double-buffered like the other outputs)
+        self.planes(self.ext_planes.cuda_stream)
         self.ev_planes[j].record(self.ext_planes)
-        if self.orb_after_supp and self.primed:
-            # the previous batch's supposed planes (the plane stream's head, on both critical chains) dispatch
-            # before this batch's pyramid floods the CUs' LDS
-            self.ext_orb.wait_event(self.ev_planes[1 - j])
         self.orb(self.ext_orb.cuda_stream)
         self.ev_orb[j].record(self.ext_orb)
 
@@ -575,9 +561,6 @@ class HotPath:
         self._bind(j)
         self.main.wait_event(self.ev_orb[j])
         self.main.wait_event(self.ev_planes[j])
-        if not self.supp_on_plane_stream:
-            self.pe.select_cloud_set(j)
-            self.planes_supposed(self.stream)
         self._tail()
         self.ev_tail[j].record(self.main)
         self._lba_end()

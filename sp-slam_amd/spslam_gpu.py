@@ -200,7 +200,19 @@ def _bind_pose(lib):
                                                       vp, vp, vp, vp]
 
 
-EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device"]
+EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device", "spslam_debug_libm64"]
+
+
+def debug_libm64(ex: "OrbExtractor", kind: int, a, b=None):
+    """The device's correctly rounded sin (kind 0) / cos (1) / atan2(a, b) (2) / cube (3) on host arrays."""
+    lib = ex.lib
+    vp = ctypes.c_void_p
+    lib.spslam_debug_libm64.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int, vp]
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(a if b is None else b, np.float64)
+    out = np.zeros_like(a)
+    ex._check(lib.spslam_debug_libm64(ex.ctx, int(kind), a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data))
+    return out
 
 
 def pose_optimize(ex: OrbExtractor, problem, points, planes, cfg: PlaneConfig | None = None):

@@ -27,7 +27,7 @@ assert LBA_POINT_OBS_DTYPE.itemsize == 20 and LBA_PLANE_DTYPE.itemsize == 32
 assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 64
 
 
-spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device"]
+spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device", "spslam_lba_debug_stop_after"]
 
 PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # ICL.yaml Plane.* keys (Chi 1000, VPChi 200)
 
@@ -36,6 +36,7 @@ def _bind(lib):
     vp = ctypes.c_void_p
     lib.spslam_lba_optimize.argtypes = [vp] * 15
     lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 16
+    lib.spslam_lba_debug_stop_after.argtypes = [vp, ctypes.c_int]
 
 
 def _addr(flag):
@@ -71,6 +72,10 @@ class LocalBA:
             pl_out.ctypes.data, po.ctypes.data, plo.ctypes.data, res.ctypes.data, _addr(stop_flag)))
         return dict(Tcw=kf_out[:len(kfs)], points=pt_out[:len(points)], planes=pl_out[:len(planes)],
                     point_outlier=po[:len(point_obs)], plane_outlier=plo[:len(plane_obs)], result=res)
+
+    def debug_stop_after(self, trials: int):
+        """Test hook: the following calls see pbStopFlag raised after `trials` LM trials (-1 = off)."""
+        self.ex._check(self.ex.lib.spslam_lba_debug_stop_after(self.ex.ctx, int(trials)))
 
     def batch_device(self, n, problems_host, d_problems, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                      d_kf_out, d_pt_out, d_pl_out, d_po, d_plo, d_res, stream=0, d_stop=None):

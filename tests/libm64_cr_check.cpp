@@ -1,0 +1,35 @@
+// Host build of sp-slam_amd/csrc/libm64_cr.h (the GPU's correctly rounded sin / cos / atan2) against the
+// oracle's independent correctly rounded routines (oracle/libm_cr_oracle.h) and the host glibc, for
+// tests/test_libm64_cr.py.
+#include <cmath>
+#include <cstdint>
+
+#include "../oracle/libm_cr_oracle.h"
+#include "../sp-slam_amd/csrc/libm64_cr.h"
+
+extern "C" {
+// kind 0 sin, 1 cos, 2 atan2(a, b).  out: device-code results.  stats[0] = arguments where the device code
+// and the oracle differ, stats[1] = arguments where glibc differs from the oracle.
+void check_libm64_cr(int kind, const double* a, const double* b, long n, double* out, long* stats) {
+    long nd = 0, ng = 0;
+    for (long i = 0; i < n; i++) {
+        double r, ref, g;
+        if (kind == 0) { r = spslam::libm64cr::sin_(a[i]); ref = oracle::libm_cr::sin(a[i]); g = std::sin(a[i]); }
+        else if (kind == 1) { r = spslam::libm64cr::cos_(a[i]); ref = oracle::libm_cr::cos(a[i]); g = std::cos(a[i]); }
+        else { r = spslam::libm64cr::atan2_(a[i], b[i]); ref = oracle::libm_cr::atan2(a[i], b[i]); g = std::atan2(a[i], b[i]); }
+        out[i] = r;
+        const bool same = (r == ref && std::signbit(r) == std::signbit(ref)) || (r != r && ref != ref);
+        const bool gsame = (g == ref && std::signbit(g) == std::signbit(ref)) || (g != g && ref != ref);
+        nd += !same;
+        ng += !gsame;
+    }
+    stats[0] = nd;
+    stats[1] = ng;
+}
+// the oracle's routines alone (for exact-arithmetic spot checks)
+void oracle_libm_cr(int kind, const double* a, const double* b, long n, double* out) {
+    for (long i = 0; i < n; i++)
+        out[i] = kind == 0 ? oracle::libm_cr::sin(a[i])
+                           : (kind == 1 ? oracle::libm_cr::cos(a[i]) : oracle::libm_cr::atan2(a[i], b[i]));
+}
+}

@@ -132,43 +132,29 @@ def test_lba_stop_flags_preset(lba):
     assert not po1[:probs[0][0]["n_point_obs"]].any()
 
 
-def test_lba_stop_flag_raised_while_running(lba):
-    """LocalMapping::InterruptBA: another thread raises pbStopFlag while spslam_lba_optimize runs.  Wherever the
-    device saw it (result.trials), the oracle with the flag raised after that trial gives the same map, flags and
-    iteration counts.  Delays are spread over the unflagged run time, so most runs stop part-way."""
-    import threading
-    import time
+def test_lba_stop_flag_raised_after_trial_k(lba):
+    """LocalMapping::InterruptBA at a known point: the device's stop-after hook raises pbStopFlag once the
+    problem has run k LM trials (k = 0: before optimize(5)).  For every k the map, outlier flags, trial and
+    iteration counts equal the oracle's with the flag raised after trial k (no host timing involved)."""
     import oracle_lba
     P = _problems()[3]
-    t0 = time.perf_counter()
     full = lba(*P[:6])
-    t_full = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    full = lba(*P[:6])
-    t_full = min(t_full, time.perf_counter() - t0)
     n_trials = int(full["result"]["trials"])
-    seen = {0: 0, 1: 0, 2: 0}
-    for frac in (0.0, 0.1, 0.25, 0.4, 0.55, 0.7, 0.85, 1.5):
-        flag = np.zeros(1, np.uint8)
-
-        def raise_flag(delay=frac * t_full, f=flag):
-            time.sleep(delay)
-            f[0] = 1
-        th = threading.Thread(target=raise_flag)
-        th.start()
-        g = lba(*P[:6], stop_flag=flag)
-        th.join()
-        r = g["result"]
-        stopped = int(r["stopped"])
-        seen[stopped] += 1
-        T = {0: -1, 1: 0, 2: int(r["trials"])}[stopped]
-        o = oracle_lba.lba_optimize(*P[:6], stop_after=T)
-        assert o["result"]["stopped"] == stopped and o["result"]["trials"] == r["trials"], (frac, r, o["result"])
-        assert list(r["iterations"]) == list(o["result"]["iterations"]), frac
-        assert np.array_equal(g["point_outlier"], o["point_outlier"]), frac
-        assert np.array_equal(g["plane_outlier"], o["plane_outlier"]), frac
-        assert _close(g["Tcw"], o["Tcw"]) and _close(g["points"], o["points"]), frac
-        if stopped == 2:
-            assert 0 < r["trials"] < n_trials
-    print("stop outcomes", seen, "trials", n_trials, "t_full", t_full)
-    assert seen[2] >= 1, seen
+    assert n_trials > 6
+    try:
+        for k in sorted({0, 1, 2, 3, n_trials // 3, n_trials // 2, n_trials - 1, n_trials, n_trials + 5}):
+            lba.debug_stop_after(k)
+            g = lba(*P[:6])
+            r = g["result"]
+            want_stopped = 1 if k == 0 else (2 if k < n_trials else 0)
+            assert int(r["stopped"]) == want_stopped, (k, r)
+            o = oracle_lba.lba_optimize(*P[:6], stop_after={0: -1, 1: 0, 2: k}[want_stopped])
+            assert o["result"]["stopped"] == r["stopped"] and o["result"]["trials"] == r["trials"], (k, r, o["result"])
+            assert list(r["iterations"]) == list(o["result"]["iterations"]), k
+            assert np.array_equal(g["point_outlier"], o["point_outlier"]), k
+            assert np.array_equal(g["plane_outlier"], o["plane_outlier"]), k
+            assert _close(g["Tcw"], o["Tcw"]) and _close(g["points"], o["points"]), k
+            if want_stopped == 2:
+                assert int(r["trials"]) == k
+    finally:
+        lba.debug_stop_after(-1)

@@ -171,6 +171,7 @@ def test_tracking_chain_independent(run):
         r1, po1, plo1 = o["pose1"]
         ok, err = pose_close(res["pose1"][i]["Tcw"], r1["Tcw"])
         assert ok, (i, err)
+        assert res["pose1"][i]["Tcw"].tobytes() == r1["Tcw"].tobytes(), i  # bit-exact (g2o order, CR libm)
         assert np.array_equal(out1[i], po1) and np.array_equal(plout1[i], plo1), i
         assert np.array_equal(res["local_match"][i, :n], o["local_match"]), i
         prob, pts, pls = o["graph2"]
@@ -178,6 +179,7 @@ def test_tracking_chain_independent(run):
         r2, po2, plo2 = o["pose2"]
         ok, err = pose_close(res["pose2"][i]["Tcw"], r2["Tcw"])
         assert ok, (i, err)
+        assert res["pose2"][i]["Tcw"].tobytes() == r2["Tcw"].tobytes(), i
         assert int(res["pose2"][i]["n_inliers"]) == int(r2["n_inliers"]), i
         assert np.array_equal(out2[i], po2) and np.array_equal(plout2[i], plo2), i
         n_planes += M

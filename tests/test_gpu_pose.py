@@ -1,8 +1,11 @@
 """GPU parity: PoseOptimization (src/Optimizer.cc:519-1152) vs the CPU oracle.
 
-Bar (BASELINE.json north_star): pose within 1e-4 relative; inlier count and
-every outlier flag identical.  Problems are synthesized from the scene ground
-truth (synth.pose_problem) on top of real ORB keypoints of the frame.
+The kernel sums in g2o's edge order with Eigen's per-edge arithmetic and correctly rounded sin / cos /
+atan2 / pow, like the oracle's default mode, so the bar is bit equality: pose, inlier count, LM iteration
+count, every outlier flag (BASELINE.json north_star asks for the pose within 1e-4 relative).  Against the
+oracle run with the host glibc's double routines instead (glibc 2.35 misrounds ~0.1 % of arguments) the
+pose stays within 1e-4 with identical flags.  Problems are synthesized from the scene ground truth
+(synth.pose_problem) on top of real ORB keypoints of the frame.
 """
 import pathlib
 
@@ -49,15 +52,16 @@ def pose_close(Ta, Tb, tol=POSE_TOL):
     return dr <= tol and dt <= tol, (dr, dt)
 
 
-def test_pose_matches_oracle(gpu, problems):
+def test_pose_bit_exact_to_oracle(gpu, problems):
     import oracle_ctypes
     import spslam_gpu
     for k, (prob, pts, pls, Tgt) in enumerate(problems):
         rg, pog, plog = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
         ro, poo, ploo = oracle_ctypes.pose_optimize(prob, pts, pls)
-        ok, err = pose_close(rg["Tcw"], ro["Tcw"])
-        assert ok, f"problem {k}: pose differs {err}"
+        assert np.array_equal(rg["Tcw"].view(np.uint32), ro["Tcw"].view(np.uint32)), \
+            f"problem {k}: pose differs {pose_close(rg['Tcw'], ro['Tcw'])[1]}"
         assert int(rg["n_inliers"]) == int(ro["n_inliers"]), f"problem {k}"
+        assert int(rg["lm_iterations"]) == int(ro["lm_iterations"]), f"problem {k}"
         assert np.array_equal(pog, poo), f"problem {k}: point outliers differ at {np.nonzero(pog != poo)[0][:10]}"
         assert np.array_equal(plog, ploo), f"problem {k}: plane outliers differ"
         # and the optimizer actually converged to the ground truth
@@ -65,18 +69,18 @@ def test_pose_matches_oracle(gpu, problems):
         assert ok_gt, f"problem {k}: far from ground truth {err_gt}"
 
 
-def test_pose_bit_exact_to_device_order_oracle(gpu, problems):
-    """With the oracle summing in the kernel's tree order (and the same sin / cos / atan2 / cube), the GPU
-    PoseOptimization is bit-exact: pose, inlier count, iteration count, every outlier flag."""
+def test_pose_close_to_glibc_libm_oracle(gpu, problems):
+    """The reference built against a libm that is not correctly rounded (the host glibc 2.35): same
+    decisions, pose within the north-star 1e-4."""
     import oracle_ctypes
     import spslam_gpu
     for k, (prob, pts, pls, _) in enumerate(problems):
         rg, pog, plog = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
-        with oracle_ctypes.pose_order(oracle_ctypes.POSE_ORDER_DEVICE):
+        with oracle_ctypes.libm(oracle_ctypes.LIBM_GLIBC):
             ro, poo, ploo = oracle_ctypes.pose_optimize(prob, pts, pls)
-        assert np.array_equal(rg["Tcw"].view(np.uint32), ro["Tcw"].view(np.uint32)), f"problem {k}"
+        ok, err = pose_close(rg["Tcw"], ro["Tcw"])
+        assert ok, f"problem {k}: pose differs {err}"
         assert int(rg["n_inliers"]) == int(ro["n_inliers"]), f"problem {k}"
-        assert int(rg["lm_iterations"]) == int(ro["lm_iterations"]), f"problem {k}"
         assert np.array_equal(pog, poo) and np.array_equal(plog, ploo), f"problem {k}"
 
 
@@ -177,15 +181,8 @@ def test_batch_device_chained(gpu, problems):
     res2 = d_res2.cpu().numpy().view(G.POSE_RESULT_DTYPE)
     for i, (prob, pts, pls, _) in enumerate(problems):
         r1, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
-        ok, err = pose_close(res1[i]["Tcw"], r1["Tcw"])
-        assert ok, (i, err)
+        assert np.array_equal(res1[i]["Tcw"].view(np.uint32), r1["Tcw"].view(np.uint32)), i
         p2 = prob.copy()
         p2["Tcw"] = res1[i]["Tcw"]
         r2, _, _ = oracle_ctypes.pose_optimize(p2, pts, pls)
-        ok, err = pose_close(res2[i]["Tcw"], r2["Tcw"])
-        assert ok, (i, err)
-        with oracle_ctypes.pose_order(oracle_ctypes.POSE_ORDER_DEVICE):  # and bit-exact in the kernel's order
-            d1, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
-            d2, _, _ = oracle_ctypes.pose_optimize(p2, pts, pls)
-        assert np.array_equal(res1[i]["Tcw"].view(np.uint32), d1["Tcw"].view(np.uint32)), i
-        assert np.array_equal(res2[i]["Tcw"].view(np.uint32), d2["Tcw"].view(np.uint32)), i
+        assert np.array_equal(res2[i]["Tcw"].view(np.uint32), r2["Tcw"].view(np.uint32)), i

@@ -3,9 +3,14 @@ motion prior comes from the previous frame's optimised pose and velocity
 (Tracking.cc:443-450, 958), its last-frame map points from the previous frame's
 tracked matches (:456-505), and SearchLocalPoints skips the map points the
 motion model already matched (mnLastFrameSeen).  The CPU oracle runs the same
-loop (oracle/oracle_sequence.py); bar: every frame's local-map pose within 1e-4
-(north star), ATE against the CPU trajectory <= 1e-4 m, the final last-frame
-map points identical, and the pipelined step bit-identical to the serial one."""
+loop (oracle/oracle_sequence.py); bar: every frame's local-map pose bit-identical
+to the CPU's (PoseOptimization sums in g2o's order with the pinned, correctly
+rounded libm on both), hence ATE against the CPU trajectory 0 (north star: <= 1e-4
+m), every frame's decisions (matches, local matches, inliers of both
+PoseOptimizations) identical, and the pipelined step bit-identical to the serial
+one.  C2 over 21 frames of two sequences; C4 (ICL.yaml parameters) over 90 frames,
+past frame 70 where the previous kernel's tree-order sums and fdlibm-based libm
+first changed an outlier decision."""
 import numpy as np
 import pytest
 
@@ -32,7 +37,7 @@ def tracked():
             sp.close()
 
 
-def _oracle(sp, slot, n):
+def _oracle(sp, slot, n, on_frame=None):
     import oracle_ctypes
     import oracle_grab
     import oracle_planes
@@ -43,7 +48,8 @@ def _oracle(sp, slot, n):
     return oracle_sequence.track(frames[:n], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map, sp.assoc_boundary,
                                  oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures),
                                  oracle_planes.PlaneOracle(), supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
-                                 pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor))
+                                 pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
+                                 on_frame=on_frame)
 
 
 def test_pipelined_equals_serial(tracked):
@@ -62,6 +68,7 @@ def test_trajectory_matches_oracle(tracked):
         for k in range(n):
             ok, err = pose_close(tr[k + 1, slot].reshape(16), cpu[k].reshape(16))
             assert ok, (slot, k + 1, err)
+            assert tr[k + 1, slot].tobytes() == cpu[k].tobytes(), (slot, k + 1)
         g = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n)]
         c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n)]
         assert trajectory.ate_rmse(g, c) <= 1e-4
@@ -70,3 +77,31 @@ def test_trajectory_matches_oracle(tracked):
         assert trajectory.ate_rmse(g, gt) < 0.02
     # slots sharing a sequence track identically
     assert tr[:, 0].tobytes() == tr[:, U].tobytes()
+
+
+def test_c4_long_sequence_matches_oracle():
+    """ICL.yaml parameters (fy < 0, Plane.MinSize 1000, Chi 1000, VPChi 200), sequence 0, 90 tracked frames:
+    identical decisions and bit-identical poses on every frame, ATE vs the CPU trajectory <= 1e-4 m."""
+    import pipeline
+    import sequence
+    import trajectory
+    n = 90
+    sp = sequence.SequencePath(2, n + 1, n_sequences=1, pipelined=True, **pipeline.CONFIGS["c4"])
+    try:
+        for _ in range(n):
+            sp.step()
+        tr, hist = sp.trajectory(), sp.history()
+        got = {}
+
+        def rec(t, o, P):
+            got[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
+                      int(o["pose2"][0]["n_inliers"]))
+        cpu = _oracle(sp, 0, n, on_frame=rec)
+        for t in range(1, n + 1):
+            assert tuple(int(x) for x in hist[t, 0]) == tuple(int(x) for x in got[t]), t
+            assert tr[t, 0].tobytes() == cpu[t - 1].tobytes(), t
+        g = [trajectory.camera_center(tr[k + 1, 0].reshape(16)) for k in range(n)]
+        c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n)]
+        assert trajectory.ate_rmse(g, c) <= 1e-4
+    finally:
+        sp.close()
