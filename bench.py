@@ -326,6 +326,10 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
                                       "identical_decisions_until_frame": []}}
         t1 = time.perf_counter()
 
+        import synth
+        vocab_text = synth.shape_vocabulary_text()
+        oracle_sequence.vocabulary(vocab_text)  # loaded once, before the threads
+
         def run_oracle(slot, order):
             frames, T0, P0, local_of = sp.oracle_inputs(slot)
             ch = {}
@@ -334,10 +338,11 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
                 ch[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
                          int(o["pose2"][0]["n_inliers"]))
             orb, po = oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures), oracle_planes.PlaneOracle()
+            ref = oracle_sequence.reference_keyframe(sp.oracle_reference_keyframe(slot), vocab_text)
             cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                        on_frame=rec, libm=order)
+                                        on_frame=rec, libm=order, ref_kf=ref)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
             return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
 

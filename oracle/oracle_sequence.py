@@ -8,7 +8,10 @@ frame (src/Tracking.cc:276-526) with the motion model --
   mVelocity = mCurrentFrame.mTcw * LastTwc                 :443-450
   VO-match clean-up, outlier drop, mLastFrame = current    :456-505
 against a map of keyframe points on a fixed keyframe schedule (the harness's
-stand-in for LocalMapping; sp-slam_amd/sequence.py describes it)."""
+stand-in for LocalMapping; sp-slam_amd/sequence.py describes it).  The first
+tracked frame has no velocity yet and runs TrackReferenceKeyFrame (:791-882:
+ComputeBoW, SearchByBoW against keyframe 0, the same graph / PoseOptimization /
+discard) when the keyframe's BoW inputs are given."""
 from __future__ import annotations
 
 import numpy as np
@@ -19,19 +22,41 @@ import oracle_step
 import oracle_track as OT
 
 
+_VOCAB = {}
+
+
+def vocabulary(text):
+    """oracle_bow.Vocabulary of a vocabulary text, loaded once per process."""
+    import hashlib
+    import oracle_bow
+    key = hashlib.sha1(text).hexdigest()
+    if key not in _VOCAB:
+        _VOCAB[key] = oracle_bow.Vocabulary(text)
+    return _VOCAB[key]
+
+
+def reference_keyframe(ref, vocab_text):
+    """ref = (keypoints, descriptors, has_point, row) of the reference keyframe (sequence.py
+    SequencePath.oracle_inputs) -> FrameInputs.ref_kf."""
+    kps, desc, has, row = ref
+    V = vocabulary(vocab_text)
+    return dict(vocab=V, desc=desc, angle=kps["angle"], has_point=has, fv=V.transform(desc), row=row)
+
+
 def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb, planes,
-          supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None, libm=None):
+          supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None, libm=None, ref_kf=None):
     """frames: [(rgb, depth_u16)] of frames first .. ; T0 / P0: the pose and last-frame points of frame
     first - 1; local_of(t): the local map points of frame t (whole; the seen ones are skipped).  Returns the
-    local-map pose (float 4x4) of every frame.  libm: the elementary functions of PoseOptimization
+    local-map pose (float 4x4) of every frame.  ref_kf: FrameInputs.ref_kf of frame `first` (reference_keyframe;
+    None keeps the motion model with a constant-position prior there).  libm: the elementary functions of PoseOptimization
     (oracle_ctypes.LIBM_*) for this call, on the calling thread; None keeps the current one."""
     if libm is not None:
         import oracle_ctypes
         with oracle_ctypes.libm(libm):
             return track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb,
-                         planes, supp_cap, min_size, pose_cfg, depth_scale, on_frame)
+                         planes, supp_cap, min_size, pose_cfg, depth_scale, on_frame, None, ref_kf)
     Tlw = np.asarray(T0, np.float32).reshape(4, 4)
-    V = np.eye(4, dtype=np.float32)  # the first tracked frame: constant-position prior (see sequence.py)
+    V = np.eye(4, dtype=np.float32)  # the first tracked frame starts at the last frame's pose (SetPose(mLastFrame.mTcw))
     P = P0
     poses = []
     for k, (rgb, d) in enumerate(frames):
@@ -46,7 +71,8 @@ def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes
         lfr = np.zeros((), OM.LOCAL_FRAME_DTYPE)
         lfr["n_points"] = len(LP)
         fi = oracle_step.FrameInputs(gray, depth, cam, geometry, inv_sigma2, (pfr, P), (lfr, LP), map_planes,
-                                     boundary, min_size=min_size, pose_cfg=pose_cfg, local_seen=True)
+                                     boundary, min_size=min_size, pose_cfg=pose_cfg, local_seen=True,
+                                     ref_kf=ref_kf if k == 0 else None)
         o = oracle_step.run(fi, orb, planes, supp_cap=supp_cap)
         T2 = np.asarray(o["pose2"][0]["Tcw"], np.float32).reshape(4, 4)
         P = OT.last_frame(P, o["match"], o["keep"], LP, o["local_match"], o["keys_un"], o["pose2"][1])

@@ -26,7 +26,7 @@ class FrameInputs:
     """Everything one frame of the step reads: images, camera, the map it tracks against."""
 
     def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary, min_size=500,
-                 pose_cfg=None, local_seen=False, rgb=None, depth_raw=None, depth_scale=None):
+                 pose_cfg=None, local_seen=False, rgb=None, depth_raw=None, depth_scale=None, ref_kf=None):
         self.gray, self.depth = gray, depth
         # the raw frame GrabImageRGBD receives (the C++ chain, oracle_step_cpp, grabs it itself)
         self.rgb, self.depth_raw, self.depth_scale = rgb, depth_raw, depth_scale
@@ -41,6 +41,10 @@ class FrameInputs:
         self.proj = proj                # (spslam_proj_frame, spslam_proj_point[])
         self.local = local              # (spslam_local_frame, spslam_local_point[])
         self.map_planes, self.boundary = map_planes, boundary
+        # ref_kf: track against the reference keyframe by BoW instead of the motion model (TrackReferenceKeyFrame,
+        # Tracking.cc:791-882): dict(vocab=oracle_bow.Vocabulary, desc, angle, has_point, fv = the keyframe's
+        # FeatureVector, row = the projection-set row of each keyframe feature's map point or -1)
+        self.ref_kf = ref_kf
 
 
 def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
@@ -63,9 +67,18 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     kun["x"], kun["y"] = fo["un"][:, 0], fo["un"][:, 1]
     out["frame"], out["keys_un"] = fo, kun
     ur, go, gi = fo["uright"], fo["grid_off"], fo["grid_idx"]
-    # --- TrackWithMotionModel
+    # --- TrackWithMotionModel (or TrackReferenceKeyFrame: the same graph, pose and discard on BoW matches)
     pfr, P = fi.proj
-    mo, nmo, _ = oracle_match.search_by_projection(pfr, P, kun, do, ur, go, gi, fi.geometry)
+    if fi.ref_kf is None:
+        mo, nmo, _ = oracle_match.search_by_projection(pfr, P, kun, do, ur, go, gi, fi.geometry)
+    else:
+        import oracle_bow
+        R = fi.ref_kf
+        fv = R["vocab"].transform(do)                  # mCurrentFrame.ComputeBoW()
+        bm, nmo = oracle_bow.search_by_bow(R["desc"], R["angle"], R["has_point"], R["fv"], do, ko["angle"], fv,
+                                           0.7, True)  # ORBmatcher matcher(0.7, true)
+        mo = np.where(bm >= 0, np.asarray(R["row"], np.int32)[np.maximum(bm, 0)], -1).astype(np.int32)
+        out["bow_match"] = bm
     out["match"], out["nmatches"] = mo, nmo
     a0 = oracle_assoc.associate(pfr["Tcw"].reshape(4, 4), coefs, fi.map_planes, fi.boundary)
     g1 = oracle_track.motion_model_graph(pfr, P, mo, kun, ur, fi.inv_sigma2, coefs, a0, fi.map_planes, fi.cam)

@@ -359,6 +359,10 @@ hipError_t bow_transform_launch(const VocabDev& V, int n_frames, const uint8_t* 
     int P = 64;
     while (P < cap) P <<= 1;
     if (P > 8192) return hipErrorInvalidValue;  // 128 KB of LDS keys + values
+    // dynamic LDS beyond the default 64 KB needs the per-kernel opt-in (set once)
+    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)bow::bow_vectors_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 8192 * 16);
+    if (lds_attr != hipSuccess) return lds_attr;
     const int tf = V.weighting == 0 || V.weighting == 1;  // TF_IDF, TF
     const int must = V.scoring != 5;                       // all but DOT_PRODUCT normalise
     const int l2 = V.scoring == 1;
@@ -380,6 +384,9 @@ hipError_t bow_search_launch(int n_pairs, const int2* pairs, const BowSide& kf, 
     if (n_pairs < 1 || kf.cap < 1 || fr.cap < 1) return hipErrorInvalidValue;
     const size_t lds = (size_t)fr.cap * 4 + (size_t)kf.cap * 8 + (size_t)fr.cap;
     if (lds > 150 * 1024) return hipErrorInvalidValue;
+    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)bow::bow_search_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (lds_attr != hipSuccess) return lds_attr;
     if (timer) timer->begin(kKindBowMatch, s);
     hipLaunchKernelGGL(bow::bow_search_kernel, dim3(n_pairs), dim3(bow::kThreads), (lds + 15) / 16 * 16, s, pairs, kf,
                        fr, nn_ratio, check_ori, match, nmatches);

@@ -23,8 +23,12 @@ Deviations from the reference, all shared with the CPU oracle
 add the current frame's VO points; LocalBundleAdjustment does not move them;
 mLastFrame's pose is not re-derived through its reference keyframe (UpdateLastFrame,
 an identity up to float rounding with fixed keyframes); frame 0 is initialised at its
-true pose with keyframe 0's points (StereoInitialization) and frame 1 uses a
-constant-position prior instead of TrackReferenceKeyFrame (BoW).
+true pose with keyframe 0's points (StereoInitialization).  Frame 1 has no velocity
+yet and runs TrackReferenceKeyFrame (:791-882) on the device: ComputeBoW of the
+frame, SearchByBoW against keyframe 0 (ORBmatcher(0.7, true)), then the same graph,
+PoseOptimization and outlier discard as the motion model, from SetPose(mLastFrame.mTcw).
+The vocabulary is synth.shape_vocabulary_text() (ORBvoc.txt's k = 10, L = 6 shape;
+the trained file is not vendored).
 
 Sequence u of a rank is the scene's trajectory from frame `SEQ_STRIDE * u`; slot i
 tracks sequence i % U (slots sharing a sequence carry identical, independent state).
@@ -125,6 +129,8 @@ class SequencePath(pipeline.HotPath):
         torch.cuda.synchronize()
         kps = d_k.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n, cap)
         desc, cnt = d_ds.cpu().numpy(), d_n.cpu().numpy()
+        kf0 = [u * len(kf_t) for u in range(U)]  # keyframe 0 of each sequence: TrackReferenceKeyFrame's reference
+        self.d_kf0_kps, self.d_kf0_desc, self.d_kf0_cnt = d_k[kf0].clone(), d_ds[kf0].clone(), d_n[kf0].clone()
         self.n_ids = len(kf_t) * cap                   # map point ids per sequence: keyframe index * cap + keypoint
         self.kf_points, self.kf_kps = {}, {}
         offs, pts = {}, []
@@ -177,6 +183,7 @@ class SequencePath(pipeline.HotPath):
         self.d_match = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
         self.d_nmatch = torch.zeros(B, dtype=torch.int32, device="cuda")
         self.local_matcher = SM.LocalMatcher(self.ex)
+        self._setup_reference_keyframe()
         self.matcher = SM.Matcher(self.ex)
         self.d_taken = torch.zeros((B, cap), dtype=torch.uint8, device="cuda")
         self.d_lmatch = torch.zeros((B, cap), dtype=torch.int32, device="cuda")
@@ -186,6 +193,67 @@ class SequencePath(pipeline.HotPath):
         # per frame: SearchByProjection matches, SearchLocalPoints matches, inliers of both PoseOptimizations
         self.hist = torch.zeros((T, 4, B), dtype=torch.int32, device="cuda")
         self.n_tracked = 0
+
+    def _setup_reference_keyframe(self):
+        """Keyframe 0's BoW side of SearchByBoW (KeyFrame::ComputeBoW at its creation) and the map of its
+        features to the rows of the frame-0 point set (the map point each feature holds, -1 without one)."""
+        import spslam_bow as SB
+        torch, B, U, cap = self.torch, self.B, self.U, self.kp_cap
+        self.vocab = SB.Vocabulary(self.ex, synth.shape_vocabulary_text())
+        i32 = dict(dtype=torch.int32, device="cuda")
+        has = np.zeros((U, cap), np.uint8)
+        row = np.full((U, cap), -1, np.int32)
+        for u in range(U):
+            kpi = (self.kf_points[u, 0]["id"] - 0).astype(np.int64)  # keyframe 0's ids: id_base 0 + keypoint
+            has[u, kpi] = 1
+            row[u, kpi] = np.arange(len(kpi), dtype=np.int32)       # as_last_frame_points keeps keypoint order
+        self.d_kf0_has = torch.from_numpy(has).cuda()
+        self.d_kf0_row = torch.from_numpy(row).cuda()
+        self.kf0_has, self.kf0_row = has, row
+
+        def fv_buffers(n):
+            return dict(words=torch.zeros((n, cap), **i32), values=torch.zeros((n, cap), dtype=torch.float64,
+                                                                              device="cuda"),
+                        n_bow=torch.zeros(n, **i32), nodes=torch.zeros((n, cap), **i32),
+                        start=torch.zeros((n, cap + 1), **i32), features=torch.zeros((n, cap), **i32),
+                        n_fv=torch.zeros(n, **i32))
+        self.kf0_bow, self.fr_bow = fv_buffers(U), fv_buffers(B)
+        self._bow_transform(U, self.d_kf0_desc, self.d_kf0_cnt, self.kf0_bow)
+        self.kf0_side = SB.BowSide(self.d_kf0_desc.data_ptr(), self.d_kf0_kps.data_ptr(), self.d_kf0_has.data_ptr(),
+                                   self.d_kf0_cnt.data_ptr(), self.kf0_bow["nodes"].data_ptr(),
+                                   self.kf0_bow["start"].data_ptr(), self.kf0_bow["features"].data_ptr(),
+                                   self.kf0_bow["n_fv"].data_ptr(), cap, 0)
+        self.d_bow_pairs = torch.tensor([(i % U, i) for i in range(B)], **i32)
+        self.d_bow_match = torch.zeros((B, cap), **i32)
+        self.d_bow_n = torch.zeros(B, **i32)
+        self.slot_u = torch.tensor([i % U for i in range(B)], dtype=torch.long, device="cuda")
+        torch.cuda.synchronize()
+
+    def _bow_transform(self, n, d_desc, d_cnt, out):
+        self.vocab.transform_batch_device(n, d_desc.data_ptr(), d_cnt.data_ptr(), self.kp_cap, 4,
+                                          out["words"].data_ptr(), out["values"].data_ptr(), out["n_bow"].data_ptr(),
+                                          out["nodes"].data_ptr(), out["start"].data_ptr(),
+                                          out["features"].data_ptr(), out["n_fv"].data_ptr(), stream=self.stream)
+
+    def match(self):
+        if self.n_tracked > 0:
+            return super().match()  # TrackWithMotionModel's SearchByProjection
+        # frame 1: TrackReferenceKeyFrame -- mCurrentFrame.ComputeBoW(); SearchByBoW(mpReferenceKF, mCurrentFrame)
+        import spslam_bow as SB
+        self._bow_transform(self.B, self.d_desc, self.d_cnt, self.fr_bow)
+        fr = SB.BowSide(self.d_desc.data_ptr(), self.d_kps.data_ptr(), 0, self.d_cnt.data_ptr(),
+                        self.fr_bow["nodes"].data_ptr(), self.fr_bow["start"].data_ptr(),
+                        self.fr_bow["features"].data_ptr(), self.fr_bow["n_fv"].data_ptr(), self.kp_cap, 0)
+        SB.search_by_bow_batch_device(self.ex, self.B, self.d_bow_pairs.data_ptr(), self.kf0_side, fr,
+                                      self.d_bow_match.data_ptr(), self.d_bow_n.data_ptr(), nn_ratio=0.7,
+                                      check_orientation=True, stream=self.stream)
+        # mvpMapPoints = vpMapPointMatches: keyframe feature -> its map point's row in the frame-0 point set
+        torch = self.torch
+        with torch.cuda.stream(self.main):
+            m = self.d_bow_match
+            rows = torch.gather(self.d_kf0_row[self.slot_u], 1, m.clamp(min=0).long())
+            self.d_match.copy_(torch.where(m >= 0, rows, torch.full_like(rows, -1)))
+            self.d_nmatch.copy_(self.d_bow_n)
 
     def _setup_assoc(self, seq_id):
         super()._setup_assoc(seq_id)
@@ -247,6 +315,14 @@ class SequencePath(pipeline.HotPath):
         for i in range(self.B):
             tr[0, i] = self._true_pose(i % self.U, 0).astype(np.float32)
         return tr
+
+    def oracle_reference_keyframe(self, slot):
+        """(keypoints, descriptors, has_point, row) of slot `slot`'s keyframe 0 -- the reference keyframe of frame
+        1's TrackReferenceKeyFrame -- for oracle_sequence.reference_keyframe (with synth.shape_vocabulary_text)."""
+        u = slot % self.U
+        n = int(self.d_kf0_cnt[u])
+        kps = self.d_kf0_kps[u, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
+        return kps, self.d_kf0_desc[u, :n].cpu().numpy(), self.kf0_has[u, :n], self.kf0_row[u, :n]
 
     def oracle_inputs(self, slot):
         """Host copies of what slot `slot` tracks, for the CPU oracle (oracle/oracle_sequence.track): frames

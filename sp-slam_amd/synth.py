@@ -591,3 +591,48 @@ def render_sequence_frames(seq_id, n_frames, w, h, K, n_boxes, first=0):
         g, d, fid = sc.render(sc.pose(t), w, h, K=K, noise_seed=seq_id * 100003 + t)
         out.append((colorize(g, fid), d))
     return out
+
+
+def shape_vocabulary_text(k=10, L=6, seed=0x0B0C):
+    """A complete DBoW2 text vocabulary of ORBvoc.txt's shape (k = 10, L = 6: 1,111,111 nodes, 10^6 words),
+    built in memory (the trained ORBvoc.txt is not vendored, .MISSING_LARGE_BLOBS:2, and a k-means tree of
+    that size is not trainable here).  Level-1 nodes are random 256-bit descriptors; each child is its parent
+    with a few random bits flipped (fewer at deeper levels), so a feature and its re-observation tend to
+    descend alike, as in a trained tree.  The vocabulary of the tracked sequences' TrackReferenceKeyFrame
+    (sp-slam_amd/sequence.py) and of the ORBvoc-shape BoW tests.  Leaves carry TF-IDF-like weights in
+    [0.5, 5.5); nodes are listed level by level (parents precede children, which loadFromTextFile needs).
+    Whitespace-aligned fields: the same text any istream-based loader reads."""
+    rng = np.random.default_rng(seed)
+    levels = [rng.integers(0, 256, (k, 32), dtype=np.uint8)]
+    flips = {2: 24, 3: 12, 4: 6, 5: 3, 6: 2, 7: 1, 8: 1}
+    for lv in range(2, L + 1):
+        par = np.repeat(levels[-1], k, axis=0)
+        bits = np.zeros((len(par), 256), np.uint8)
+        pos = rng.integers(0, 256, (len(par), flips.get(lv, 1)))
+        np.put_along_axis(bits, pos, 1, axis=1)
+        levels.append(par ^ np.packbits(bits, axis=1))
+    desc = np.concatenate(levels)
+    n = len(desc)
+    first = np.cumsum([1] + [k ** l for l in range(1, L + 1)])  # id of each level's first node
+    ids = np.arange(1, n + 1)
+    lvl = np.searchsorted(first, ids, side="right")              # 1..L
+    parent = np.where(lvl == 1, 0, first[lvl - 2] + (ids - first[lvl - 1]) // k)
+    leaf = (lvl == L).astype(np.int64)
+    weight = np.where(leaf == 1, rng.integers(500000, 5500000, n), 0)  # micro-units
+
+    def digits(v, width):  # right-aligned decimal, space padded, as a (len(v), width) byte matrix
+        out = np.full((len(v), width), ord(" "), np.uint8)
+        v = v.copy()
+        for c in range(width - 1, -1, -1):
+            nz = (v > 0) | (c == width - 1)
+            out[nz, c] = ord("0") + v[nz] % 10
+            v //= 10
+        return out
+    lut = np.array([digits(np.array([b]), 3)[0].tolist() + [ord(" ")] for b in range(256)], np.uint8)
+    sp = np.full((n, 1), ord(" "), np.uint8)
+    w_int, w_frac = weight // 1000000, weight % 1000000
+    frac = digits(w_frac + 1000000, 7)[:, 1:]                    # 6 zero-padded fraction digits
+    body = np.concatenate([digits(parent, 7), sp, digits(leaf, 1), sp, lut[desc].reshape(n, 128),
+                           digits(w_int, 1), np.full((n, 1), ord("."), np.uint8), frac,
+                           np.full((n, 1), ord("\n"), np.uint8)], axis=1)
+    return f"{k} {L}  0 0\n".encode() + body.tobytes()

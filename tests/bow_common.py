@@ -18,6 +18,13 @@ def vocab_text():
     return gzip.open(VOCAB, "rb").read()
 
 
+def shape_vocab_text(k=10, L=6):
+    """ORBvoc.txt's shape (k = 10, L = 6, 10^6 words): the harness's generated vocabulary
+    (sp-slam_amd/synth.py shape_vocabulary_text)."""
+    import synth
+    return synth.shape_vocabulary_text(k, L)
+
+
 def frames(n=4, seq=0, step=5, n_boxes=3, nfeatures=1000):
     """(keypoints, descriptors) of n synthetic frames, CPU oracle ORB."""
     import oracle_ctypes

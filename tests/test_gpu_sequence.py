@@ -8,7 +8,8 @@ to the CPU's (PoseOptimization sums in g2o's order with the pinned, correctly
 rounded libm on both), hence ATE against the CPU trajectory 0 (north star: <= 1e-4
 m), every frame's decisions (matches, local matches, inliers of both
 PoseOptimizations) identical, and the pipelined step bit-identical to the serial
-one.  C2 over 21 frames of two sequences; C4 (ICL.yaml parameters) over 90 frames,
+one.  Frame 1 runs TrackReferenceKeyFrame (BoW against keyframe 0) on both sides.
+C2 over 21 frames of two sequences; C4 (ICL.yaml parameters) over 90 frames,
 past frame 70 where the previous kernel's tree-order sums and fdlibm-based libm
 first changed an outlier decision."""
 import numpy as np
@@ -43,13 +44,15 @@ def _oracle(sp, slot, n, on_frame=None):
     import oracle_planes
     import oracle_sequence
     import oracle_step
+    import synth
     frames, T0, P0, local_of = sp.oracle_inputs(slot)
     cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
+    ref = oracle_sequence.reference_keyframe(sp.oracle_reference_keyframe(slot), synth.shape_vocabulary_text())
     return oracle_sequence.track(frames[:n], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map, sp.assoc_boundary,
                                  oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures),
                                  oracle_planes.PlaneOracle(), supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                  pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                 on_frame=on_frame)
+                                 on_frame=on_frame, ref_kf=ref)
 
 
 def test_pipelined_equals_serial(tracked):
@@ -105,3 +108,25 @@ def test_c4_long_sequence_matches_oracle():
         assert trajectory.ate_rmse(g, c) <= 1e-4
     finally:
         sp.close()
+
+
+def test_frame1_tracks_reference_keyframe(tracked):
+    """Frame 1 (no velocity yet): SearchByBoW against keyframe 0 on the device equals the oracle's (matches per
+    keypoint, count), and the frame's pose equals the oracle's TrackReferenceKeyFrame + TrackLocalMap pose."""
+    import oracle_bow
+    import oracle_sequence
+    import synth
+    tr, sp = tracked[False]
+    V = oracle_sequence.vocabulary(synth.shape_vocabulary_text())
+    hist = sp.history()
+    for slot in range(U):
+        kps, desc, has, row = sp.oracle_reference_keyframe(slot)
+        got = {}
+        cpu = _oracle(sp, slot, 1, on_frame=lambda t, o, P: got.update(o=o))
+        o = got["o"]
+        fd = o["desc"]
+        om, on = oracle_bow.search_by_bow(desc, kps["angle"], has, V.transform(desc), fd, o["kps"]["angle"],
+                                          V.transform(fd), 0.7, True)
+        assert np.array_equal(o["bow_match"], om) and on == o["nmatches"] > 50, slot
+        assert int(hist[1, slot][0]) == on, slot  # the device's SearchByBoW count (d_nmatch)
+        assert tr[1, slot].tobytes() == cpu[0].tobytes(), slot

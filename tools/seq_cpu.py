@@ -36,11 +36,17 @@ def inputs(cfg, u=0, n_frames=300, seq_id=0, n_boxes=5, W=640, H=480, nfeatures=
         frames.append((synth.colorize(g, fid), d))
     orb = oracle_ctypes.OrbOracle(nfeatures=nfeatures)
     kf_t = list(range(0, n_frames + 1, synth.KEYFRAME_STEP))
-    kfp, kfk = [], []
+    kfp, kfk, kfd = [], [], []
     for j, t in enumerate(kf_t):
         k, dsc = orb.extract(oracle_grab.cvt_gray(frames[t][0], rgb=True))
         kfp.append(synth.keyframe_points(scene, SEQ_STRIDE * u + t, k, dsc, frames[t][1], j * cap, K=K))
         kfk.append(k)
+        kfd.append(dsc)
+    has = np.zeros(len(kfk[0]), np.uint8)
+    row = np.full(len(kfk[0]), -1, np.int32)
+    ids = kfp[0]["id"].astype(np.int64)
+    has[ids], row[ids] = 1, np.arange(len(ids), dtype=np.int32)
+    ref = oracle_sequence.reference_keyframe((kfk[0], kfd[0], has, row), synth.shape_vocabulary_text())
     P0 = synth.as_last_frame_points(kfp[0], kfk[0], 0)
     T0 = np.linalg.inv(scene.pose(SEQ_STRIDE * u)).astype(np.float32)
 
@@ -62,7 +68,7 @@ def inputs(cfg, u=0, n_frames=300, seq_id=0, n_boxes=5, W=640, H=480, nfeatures=
     import spslam_gpu as G  # PlaneConfig record only (no device call)
     pcfg = G.PlaneConfig(1.0, 100.0, 0.5, 0.5, c["chi"], c["vp_chi"])
     return dict(frames=frames[1:], T0=T0, P0=P0, local_of=local_of, cam=(fx, fy, cx, cy, bf), geo=geo,
-                inv_s2=np.asarray(inv_s2, np.float32), map=m, boundary=bxyz, min_size=c["min_size"], pcfg=pcfg,
+                inv_s2=np.asarray(inv_s2, np.float32), map=m, boundary=bxyz, min_size=c["min_size"], pcfg=pcfg, ref=ref,
                 scale=scale, scene=scene, u=u, nfeatures=nfeatures)
 
 
@@ -76,7 +82,7 @@ def run(inp, order, n_frames):
                                   inp["geo"], inp["inv_s2"], inp["map"], inp["boundary"],
                                   oracle_ctypes.OrbOracle(nfeatures=inp["nfeatures"]), oracle_planes.PlaneOracle(),
                                   supp_cap=32, min_size=inp["min_size"], pose_cfg=inp["pcfg"],
-                                  depth_scale=inp["scale"], on_frame=rec, libm=order)
+                                  depth_scale=inp["scale"], on_frame=rec, libm=order, ref_kf=inp["ref"])
     return np.array(poses), hist
 
 
