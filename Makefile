@@ -27,6 +27,7 @@ $(OBJDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 
 $(PKG)/libspslam_gpu.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(OBJS)
+	@python3 tools/build_info.py $@ > $(PKG)/build_info.json
 
 # Diagnostic build: PoseOptimization phase timers (tools/pose_phases.py loads it via SPSLAM_GPU_LIB).
 PROFDIR := build/prof

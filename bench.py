@@ -215,6 +215,18 @@ def _cpu_model():
     return "unknown"
 
 
+def _build_provenance():
+    """The timed library: its sha256 and the build_info.json the Makefile wrote beside it (git commit)."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import build_info
+    lib = ROOT / "sp-slam_amd" / "libspslam_gpu.so"
+    bi = ROOT / "sp-slam_amd" / "build_info.json"
+    out = json.loads(bi.read_text()) if bi.exists() else {}
+    out["lib_sha256_loaded"] = build_info.lib_sha256(lib)
+    out["lib_sha256"] = out["lib_sha256_loaded"]
+    return out
+
+
 def _cgroup_cpus():
     """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), None when unlimited or unreadable."""
     try:
@@ -290,6 +302,38 @@ def ate_report(hp, res, cpu_poses=None):
     return out
 
 
+def closed_loop(cfg, device, B, steps, warmup, n_seq=16):
+    """Closed-loop throughput beside the open-loop headline: sp-slam_amd/sequence.py's tracked sequences at B
+    slots (B / n_seq slots per rendered sequence, each slot its own independent tracking state), one tracked
+    frame per slot per step -- every frame's prior, last-frame points and matches from its predecessor's
+    result, frame 1 by TrackReferenceKeyFrame (BoW).  Same pipelined step structure as the headline."""
+    import torch
+    import sequence
+    sp = sequence.SequencePath(B, warmup + steps + 2, n_sequences=n_seq, device=device,
+                               render_workers=min(16, os.cpu_count() or 1), pipelined=True, **cfg)
+    try:
+        for _ in range(warmup):
+            sp.step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sp.step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        h = sp.history()
+        return {"value": B * steps / el, "unit": "frames/s", "slots": B, "sequences": n_seq, "steps": steps,
+                "warmup": warmup, "ms_per_step": el * 1e3 / steps,
+                "mean_matches": float(h[warmup + 1:, :, 0].mean()),
+                "mean_inliers_local_map": float(h[warmup + 1:, :, 3].mean()),
+                "local_bundle_adjustments": len(getattr(sp, "lm_runs", [])),
+                "kind": "tracked sequences (sp-slam_amd/sequence.py): motion model from the previous frame, "
+                        "TrackReferenceKeyFrame at frame 1" +
+                        (", deterministic LocalMapping with LocalBundleAdjustment every 10 frames"
+                         if sp.local_mapping else "")}
+    finally:
+        sp.close()
+
+
 def ate_sequences(cfg, device, n_frames=300, n_seq=2):
     """ATE of tracked sequences (sp-slam_amd/sequence.py): n_seq sequences of n_frames tracked frames each on
     the GPU, every frame's prior and last-frame points from its predecessor's result, against the CPU oracle
@@ -314,7 +358,9 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         import oracle_sequence
         import oracle_step
         cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
-        out = {"kind": "tracked sequences (motion model from the previous frame; sp-slam_amd/sequence.py)",
+        out = {"kind": "tracked sequences (motion model from the previous frame; sp-slam_amd/sequence.py)" +
+                       (" with the deterministic LocalMapping (local_mapping.py: keyframes every 10 frames, "
+                        "LocalBundleAdjustment written back into the map)" if sp.local_mapping else ""),
                "sequences": n_seq, "frames": n_frames,
                "cpu_ref": "CPU oracle (oracle/oracle_sequence.py): PoseOptimization summed in g2o's edge order with "
                           "Eigen's per-edge arithmetic and correctly rounded sin/cos/atan2/pow (the pinned libm, "
@@ -342,7 +388,8 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                        on_frame=rec, libm=order, ref_kf=ref)
+                                        on_frame=rec, libm=order, ref_kf=ref,
+                                        local_map=sp.oracle_local_map(slot) if sp.local_mapping else None)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
             return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
 
@@ -407,6 +454,8 @@ def main():
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
     ap.add_argument("--ate-frames", type=int, default=300,
                     help="frames per tracked sequence of the ATE check (0 = skip)")
+    ap.add_argument("--closed-loop-steps", type=int, default=20,
+                    help="timed steps of the closed-loop line (tracked sequences at --batch slots; 0 = skip)")
     ap.add_argument("--dist-check", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU): spawn, rendezvous, aggregation")
     args = ap.parse_args()
@@ -479,13 +528,18 @@ def main():
             by_kernel[k] = {"achieved_gbs": gbs, "frac": gbs / HBM_PEAK_GBS}
     # HBM traffic cannot be counted inside this process (the PMC passes need rocprofv3 around it): it is read
     # from the committed summary of such a run and reported with where and when it was measured
+    # (provenance: the library hash at PMC time against the library this process loaded; a mismatch marks the
+    # committed traffic stale and it is not reported)
     traffic, traffic_src = None, None
     pmc = ROOT / "profiles" / f"pmc_{args.config}_b{args.batch}.json"
+    build = _build_provenance()
     if pmc.exists():
         try:
             pj = json.loads(pmc.read_text())
-            traffic = pj.get(dom)
-            traffic_src = {"file": str(pmc.relative_to(ROOT)), **pj.get("provenance", {})}
+            prov = pj.get("provenance", {})
+            fresh = prov.get("lib_sha256") == build.get("lib_sha256")
+            traffic = pj.get(dom) if fresh else None
+            traffic_src = {"file": str(pmc.relative_to(ROOT)), **prov, "matches_timed_library": fresh}
         except Exception:
             traffic = None
     result = {
@@ -516,6 +570,7 @@ def main():
                      "bytes_per_launch": bytes_per_launch, "avg_launch_ms": avg_launch_s * 1e3,
                      "share_of_kernel_time": dom_ms / max(total_kernel_ms, 1e-9)},
         "cpu_baseline": None,
+        "build": build,
     }
     cpu_poses = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -523,6 +578,8 @@ def main():
     if rank == 0:
         result["open_loop_pose_agreement"] = ate_report(hp, res, cpu_poses)
     hp.close()
+    if rank == 0 and args.closed_loop_steps > 0:
+        result["closed_loop"] = closed_loop(cfg, local, args.batch, args.closed_loop_steps, args.warmup)
     if rank == 0 and args.ate_frames > 0:
         result["ate"] = ate_sequences(cfg, local, n_frames=args.ate_frames)
     if rank == 0:

@@ -266,6 +266,7 @@ __host__ __device__ inline double cube_(double x) {
     const double l = fma(x, x, -h);
     const double p = h * x;
     const double e = fma(h, x, -p);
+    if (x == 0 || !(fabs(p) <= 1.7976931348623157e308)) return p;  // +-0, +-inf (overflow included), NaN
     return p + (e + l * x);
 }
 

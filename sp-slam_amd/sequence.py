@@ -81,11 +81,16 @@ def render_sequences(seq_id, n_boxes, U, T, w, h, K, workers=0):
 class SequencePath(pipeline.HotPath):
     """HotPath over T frames of U sequences (B slots, slot i -> sequence i % U)."""
 
-    def __init__(self, B, n_frames, n_sequences=None, render_workers=0, **kw):
+    def __init__(self, B, n_frames, n_sequences=None, render_workers=0, local_mapping=None, **kw):
+        """local_mapping: run the deterministic LocalMapping (local_mapping.py: keyframe insertion and
+        LocalBundleAdjustment written back into the map) after every keyframe frame; default: on when the
+        config asks for LocalBundleAdjustment (C3's lba_every), off otherwise."""
         self.T = n_frames
         self.U = min(n_sequences or B, B)
         self.render_workers = render_workers
         self.n_boxes = kw.get("n_boxes", 3)
+        lba_every = kw.pop("lba_every", 0)  # the side-by-side synthetic local maps of the open-loop HotPath
+        self.local_mapping = bool(lba_every) if local_mapping is None else bool(local_mapping)
         kw.pop("unique_frames", None)
         kw.pop("rotate_inputs", None)
         super().__init__(B, unique_frames=self.U, **kw)
@@ -258,6 +263,126 @@ class SequencePath(pipeline.HotPath):
     def _setup_assoc(self, seq_id):
         super()._setup_assoc(seq_id)
         self.d_afr_first = self.d_afr1  # MOTION_PRIOR writes the first association's pose
+        if self.local_mapping:
+            # each sequence its own copy of the map planes (LocalBundleAdjustment moves them): slot i reads copy
+            # i % U (association indices are absolute into the copies)
+            import spslam_assoc as SA
+            U, n = self.U, self.n_map
+            self.d_map = self.torch.from_numpy(np.tile(self.assoc_map, U).view(np.uint8).copy()).cuda()
+            for d in (self.d_afr1, self.d_afr2):
+                fr = d.cpu().numpy().view(SA.ASSOC_FRAME_DTYPE).copy()
+                fr["map_offset"] = [(i % U) * n for i in range(self.B)]
+                d.copy_(self.torch.from_numpy(fr.view(np.uint8)))
+
+    def _setup_track(self):
+        super()._setup_track()
+        if self.local_mapping:
+            self._setup_local_mapping()
+
+    def _setup_local_mapping(self):
+        """local_mapping.SeqMap per sequence, keyframe 0 inserted (StereoInitialization: its own points), and the
+        LocalMapping context (the reference's LocalMapping thread has its own; here it runs synchronously)."""
+        import local_mapping as LM
+        import spslam_lba as L
+        U, cap = self.U, self.kp_cap
+        tab = self.ex.tables()
+        cam = (self.fx, self.fy, self.cx, self.cy, self.bf)
+        pc = self.plane_cfg
+        self.lm_cfg = (pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info, pc.chi, pc.vp_chi)
+        self.maps = []
+        for u in range(U):
+            m = LM.SeqMap([self.kf_points[u, j] for j in range(len(self.kf_t))], cap, cam, tab["scale"],
+                          tab["inv_sigma2"], self.assoc_map)
+            LM.insert_initial_keyframe(m, self._true_pose(u, 0).astype(np.float32), self.kf_kps[u, 0],
+                                       self.seq_frames[u][0][1], self.depth_factor, self.bf)
+            self.maps.append(m)
+        self.lm_ba = L.LocalBA(self.ex, cfg=self.lm_cfg)
+        self.lm_runs = []  # per LocalBundleAdjustment: (frame, results of slot 0..U-1)
+
+    def _local_mapping(self, t):
+        """After keyframe frame t's tail: insert keyframe t / STEP into every sequence's map and, with more than
+        two keyframes, run LocalBundleAdjustment for every slot (one problem each, on the device) and write the
+        result back (local-map points, the last frame's points and pose, map planes)."""
+        import local_mapping as LM
+        import spslam_lba as L
+        torch, B, U, cap = self.torch, self.B, self.U, self.kp_cap
+        j = t // synth.KEYFRAME_STEP
+        self.main.synchronize()
+        pf = self.d_pframes.cpu().numpy().view(SM.PROJ_FRAME_DTYPE)
+        pp = self.d_ppoints.cpu().numpy().view(SM.PROJ_POINT_DTYPE).reshape(B, cap)
+        traj = self.traj[t].cpu().numpy().reshape(B, 4, 4)
+        cnt = self.d_cnt.cpu().numpy()
+        kun = self.d_kun.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(B, cap)
+        kur = self.d_kur.cpu().numpy()
+        g1 = self.graphs[1]
+        P2 = g1["P"].cpu().numpy().view(G.POSE_PROBLEM_DTYPE)
+        pls = g1["pls"].cpu().numpy().view(G.PLANE_OBS_DTYPE)
+        plout = g1["plout"].cpu().numpy()
+        for u in range(U):  # slot u carries sequence u (slots u + k U are identical copies)
+            n = int(pf[u]["n_points"])
+            o, nl = int(P2[u]["plane_offset"]), int(P2[u]["n_planes"])
+            ins = LM.frame_keyframe_inputs(pp[u, :n], kun[u], kur[u], int(cnt[u]), pls[o:o + nl], plout[o:o + nl])
+            matched, keys, ur, octave, edges = ins
+            self.maps[u].insert_keyframe(j, traj[u], keys, ur, octave, matched, edges)
+        if j < 2:  # LocalMapping::Run: LocalBundleAdjustment once the map holds more than two keyframes
+            return
+        probs = [self.maps[u].lba_problem(j) for u in range(U)]
+        hdr = np.zeros(B, L.LBA_PROBLEM_DTYPE)
+        parts = [[] for _ in range(5)]
+        nk = npt = npo = npl = nplo = 0
+        for i in range(B):
+            prob, kfs, pts, pobs, pls_, plobs = probs[i % U][0]
+            hdr[i] = prob
+            hdr[i]["kf_offset"], hdr[i]["point_offset"], hdr[i]["plane_offset"] = nk, npt, npl
+            pts = pts.copy()
+            pts["obs_offset"] += npo
+            pls_ = pls_.copy()
+            pls_["obs_offset"] += nplo
+            for q, a in enumerate((kfs, pts, pobs, pls_, plobs)):
+                parts[q].append(a)
+            nk += len(kfs); npt += len(pts); npo += len(pobs); npl += len(pls_); nplo += len(plobs)
+        dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()  # noqa: E731
+        ins = [dev(hdr)] + [dev(np.concatenate(p)) if sum(len(x) for x in p) else
+                            torch.zeros(64, dtype=torch.uint8, device="cuda") for p in parts]
+        outs = [torch.zeros((max(nk, 1), 16), dtype=torch.float32, device="cuda"),
+                torch.zeros((max(npt, 1), 3), dtype=torch.float32, device="cuda"),
+                torch.zeros((max(npl, 1), 4), dtype=torch.float32, device="cuda"),
+                torch.zeros(max(npo, 1), dtype=torch.uint8, device="cuda"),
+                torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
+                torch.zeros(B * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
+        self.lm_ba.batch_device(B, hdr, *[x.data_ptr() for x in ins], *[x.data_ptr() for x in outs],
+                                stream=self.stream)
+        self.main.synchronize()
+        kf_o, pt_o, pl_o, po_o = (x.cpu().numpy() for x in outs[:4])
+        res = outs[5].cpu().numpy().view(L.LBA_RESULT_DTYPE)
+        run = []
+        lp = self.d_lpoints.view(-1, SM.LOCAL_POINT_DTYPE.itemsize)
+        for u in range(U):
+            (_, kfs, pts, pobs, pls_, _), book = probs[u]
+            h = hdr[u]
+            k0, p0, q0 = int(h["kf_offset"]), int(h["point_offset"]), int(h["plane_offset"])
+            o0 = sum(len(x) for x in parts[2][:u])  # slot u's first point observation
+            m = self.maps[u]
+            m.apply(book, kf_o[k0:k0 + len(kfs)], pt_o[p0:p0 + len(pts)], pl_o[q0:q0 + len(pls_)],
+                    po_o[o0:o0 + len(pobs)], int(res[u]["stopped"]))
+            run.append(dict(result=res[u].copy(), Tcw=kf_o[k0:k0 + len(kfs)].copy(),
+                            points=pt_o[p0:p0 + len(pts)].copy(), kfs=list(book["kfs"])))
+            # write-back: the sequence's local-map point table, the map planes, and for every slot of the
+            # sequence the last frame's map points and pose (UpdateLastFrame: Tlr = I for the keyframe's frame)
+            a = self.local_offsets[u, 0]
+            lp[a:a + len(m.table)].copy_(torch.from_numpy(m.table.view(np.uint8).reshape(len(m.table), -1)))
+            self.d_map.view(-1, 32)[u * self.n_map:(u + 1) * self.n_map].copy_(
+                torch.from_numpy(m.planes.view(np.uint8).reshape(self.n_map, 32)))
+            n = int(pf[u]["n_points"])
+            P = m.refresh_last_frame(pp[u, :n])
+            Tl = m.kfs[j]["Tcw"].reshape(16)
+            for i in range(u, B, U):
+                pp[i, :n] = P
+                pf[i]["Tlw"] = Tl
+        self.d_ppoints.copy_(torch.from_numpy(pp.view(np.uint8).reshape(-1)))
+        self.d_pframes.copy_(torch.from_numpy(pf.view(np.uint8).reshape(-1)))
+        self.lm_runs.append((t, run))
+        torch.cuda.synchronize()
 
     # ---- per batch: frame t of every slot's sequence and its local map
     INPUT_BUFFERS = ("d_rgb", "d_depth_raw", "d_lframes")
@@ -302,6 +427,8 @@ class SequencePath(pipeline.HotPath):
                            .view(self.B))
         self.n_tracked += 1
         self.d_pframes, self.d_ppoints = nxt
+        if self.local_mapping and self.n_tracked % synth.KEYFRAME_STEP == 0:
+            self._local_mapping(self.n_tracked)
 
     def history(self):
         """[t][slot] (nmatches, local nmatches, inliers of the motion-model and local-map PoseOptimization)."""
@@ -323,6 +450,18 @@ class SequencePath(pipeline.HotPath):
         n = int(self.d_kf0_cnt[u])
         kps = self.d_kf0_kps[u, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
         return kps, self.d_kf0_desc[u, :n].cpu().numpy(), self.kf0_has[u, :n], self.kf0_row[u, :n]
+
+    def oracle_local_map(self, slot):
+        """A fresh local_mapping.SeqMap of slot `slot`'s sequence as it stood before frame 1 (keyframe 0
+        inserted), for the CPU oracle's copy of the deterministic LocalMapping."""
+        import local_mapping as LM
+        u = slot % self.U
+        tab = self.ex.tables()
+        m = LM.SeqMap([self.kf_points[u, j] for j in range(len(self.kf_t))], self.kp_cap,
+                      (self.fx, self.fy, self.cx, self.cy, self.bf), tab["scale"], tab["inv_sigma2"], self.assoc_map)
+        LM.insert_initial_keyframe(m, self._true_pose(u, 0).astype(np.float32), self.kf_kps[u, 0],
+                                   self.seq_frames[u][0][1], self.depth_factor, self.bf)
+        return m
 
     def oracle_inputs(self, slot):
         """Host copies of what slot `slot` tracks, for the CPU oracle (oracle/oracle_sequence.track): frames

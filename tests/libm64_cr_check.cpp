@@ -8,7 +8,7 @@
 #include "../sp-slam_amd/csrc/libm64_cr.h"
 
 extern "C" {
-// kind 0 sin, 1 cos, 2 atan2(a, b).  out: device-code results.  stats[0] = arguments where the device code
+// kind 0 sin, 1 cos, 2 atan2(a, b), 3 cube vs pow(a, 3).  out: device-code results.  stats[0] = arguments where the device code
 // and the oracle differ, stats[1] = arguments where glibc differs from the oracle.
 void check_libm64_cr(int kind, const double* a, const double* b, long n, double* out, long* stats) {
     long nd = 0, ng = 0;
@@ -16,7 +16,8 @@ void check_libm64_cr(int kind, const double* a, const double* b, long n, double*
         double r, ref, g;
         if (kind == 0) { r = spslam::libm64cr::sin_(a[i]); ref = oracle::libm_cr::sin(a[i]); g = std::sin(a[i]); }
         else if (kind == 1) { r = spslam::libm64cr::cos_(a[i]); ref = oracle::libm_cr::cos(a[i]); g = std::cos(a[i]); }
-        else { r = spslam::libm64cr::atan2_(a[i], b[i]); ref = oracle::libm_cr::atan2(a[i], b[i]); g = std::atan2(a[i], b[i]); }
+        else if (kind == 2) { r = spslam::libm64cr::atan2_(a[i], b[i]); ref = oracle::libm_cr::atan2(a[i], b[i]); g = std::atan2(a[i], b[i]); }
+        else { r = spslam::libm64cr::cube_(a[i]); ref = oracle::libm_cr::cube(a[i]); g = std::pow(a[i], 3.0); }
         out[i] = r;
         const bool same = (r == ref && std::signbit(r) == std::signbit(ref)) || (r != r && ref != ref);
         const bool gsame = (g == ref && std::signbit(g) == std::signbit(ref)) || (g != g && ref != ref);

@@ -38,7 +38,13 @@ def tracked():
             sp.close()
 
 
-def _oracle(sp, slot, n, on_frame=None):
+def sequence_path(B, T, U, config, pipelined=True):
+    import pipeline
+    import sequence
+    return sequence.SequencePath(B, T, n_sequences=U, pipelined=pipelined, **pipeline.CONFIGS[config])
+
+
+def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None):
     import oracle_ctypes
     import oracle_grab
     import oracle_planes
@@ -52,7 +58,7 @@ def _oracle(sp, slot, n, on_frame=None):
                                  oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures),
                                  oracle_planes.PlaneOracle(), supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                  pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                 on_frame=on_frame, ref_kf=ref)
+                                 on_frame=on_frame, ref_kf=ref, local_map=local_map, on_lba=on_lba)
 
 
 def test_pipelined_equals_serial(tracked):
@@ -130,3 +136,51 @@ def test_frame1_tracks_reference_keyframe(tracked):
         assert np.array_equal(o["bow_match"], om) and on == o["nmatches"] > 50, slot
         assert int(hist[1, slot][0]) == on, slot  # the device's SearchByBoW count (d_nmatch)
         assert tr[1, slot].tobytes() == cpu[0].tobytes(), slot
+
+
+def test_c3_local_mapping_in_the_loop():
+    """C3 as a pipeline: the deterministic LocalMapping (sp-slam_amd/local_mapping.py) after every keyframe frame
+    -- keyframe insertion from the tracked frame, LocalBundleAdjustment of the local window on the device, its
+    result written back into the map the next frames track against (local-map points, last-frame points and
+    pose, map planes).  The CPU oracle runs the same loop with the oracle's LocalBundleAdjustment.  Bar: every
+    LocalBundleAdjustment with identical LM iteration / trial counts and outlier counts and keyframe poses
+    within 1e-4; every frame's decisions identical and pose within 1e-4; ATE vs the CPU trajectory <= 1e-4 m."""
+    import oracle_sequence
+    import pipeline
+    import synth
+    import trajectory
+    from test_gpu_pose import pose_close
+    n = 45
+    sp = sequence_path(2, n + 1, 1, "c3")
+    try:
+        assert sp.local_mapping
+        for _ in range(n):
+            sp.step()
+        tr, hist = sp.trajectory(), sp.history()
+        got, lbas = {}, {}
+
+        def rec(t, o, P):
+            got[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
+                      int(o["pose2"][0]["n_inliers"]))
+        cpu = _oracle(sp, 0, n, on_frame=rec, local_map=sp.oracle_local_map(0),
+                      on_lba=lambda t, r: lbas.update({t: r}))
+        runs = dict(sp.lm_runs)
+        assert sorted(runs) == sorted(lbas) == [20, 30, 40]
+        for t, r in lbas.items():
+            g = runs[t][0]
+            assert list(g["result"]["iterations"]) == list(r["result"]["iterations"]), t
+            assert int(g["result"]["trials"]) == int(r["result"]["trials"]), t
+            assert int(g["result"]["n_point_outliers"]) == int(r["result"]["n_point_outliers"]), t
+            assert g["kfs"] == r["kfs"], t
+            for k in range(len(g["kfs"])):
+                ok, err = pose_close(g["Tcw"][k], r["Tcw"][k])
+                assert ok, (t, k, err)
+        for t in range(1, n + 1):
+            assert tuple(int(x) for x in hist[t, 0]) == tuple(int(x) for x in got[t]), t
+            ok, err = pose_close(tr[t, 0].reshape(16), cpu[t - 1].reshape(16))
+            assert ok, (t, err)
+        g = [trajectory.camera_center(tr[k + 1, 0].reshape(16)) for k in range(n)]
+        c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n)]
+        assert trajectory.ate_rmse(g, c) <= 1e-4
+    finally:
+        sp.close()

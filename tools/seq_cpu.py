@@ -23,6 +23,7 @@ import synth  # noqa: E402
 
 SEQ_STRIDE = 53
 CFG = {"c2": dict(K=synth.TUM3, min_size=500, chi=300.0, vp_chi=300.0),
+       "c3": dict(K=synth.TUM3, min_size=500, chi=300.0, vp_chi=300.0, local_mapping=True),
        "c4": dict(K=synth.ICL, min_size=1000, chi=1000.0, vp_chi=200.0)}
 
 
@@ -67,12 +68,18 @@ def inputs(cfg, u=0, n_frames=300, seq_id=0, n_boxes=5, W=640, H=480, nfeatures=
         m[k] = v
     import spslam_gpu as G  # PlaneConfig record only (no device call)
     pcfg = G.PlaneConfig(1.0, 100.0, 0.5, 0.5, c["chi"], c["vp_chi"])
-    return dict(frames=frames[1:], T0=T0, P0=P0, local_of=local_of, cam=(fx, fy, cx, cy, bf), geo=geo,
+    lm = None
+    if c.get("local_mapping"):
+        import local_mapping as LM
+        lm = LM.SeqMap(kfp, cap, (fx, fy, cx, cy, bf), sc, inv_s2, m)
+        LM.insert_initial_keyframe(lm, T0, kfk[0], frames[0][1], K["depth_factor"], bf)
+    return dict(lm=lm, frames=frames[1:], T0=T0, P0=P0, local_of=local_of, cam=(fx, fy, cx, cy, bf), geo=geo,
                 inv_s2=np.asarray(inv_s2, np.float32), map=m, boundary=bxyz, min_size=c["min_size"], pcfg=pcfg, ref=ref,
                 scale=scale, scene=scene, u=u, nfeatures=nfeatures)
 
 
 def run(inp, order, n_frames):
+    import copy
     hist = {}
 
     def rec(t, o, P):
@@ -82,7 +89,9 @@ def run(inp, order, n_frames):
                                   inp["geo"], inp["inv_s2"], inp["map"], inp["boundary"],
                                   oracle_ctypes.OrbOracle(nfeatures=inp["nfeatures"]), oracle_planes.PlaneOracle(),
                                   supp_cap=32, min_size=inp["min_size"], pose_cfg=inp["pcfg"],
-                                  depth_scale=inp["scale"], on_frame=rec, libm=order, ref_kf=inp["ref"])
+                                  depth_scale=inp["scale"], on_frame=rec, libm=order, ref_kf=inp["ref"],
+                                  local_map=copy.deepcopy(inp["lm"]),
+                                  on_lba=lambda t, r: print("LBA", t, r["result"], flush=True))
     return np.array(poses), hist
 
 
