@@ -31,6 +31,13 @@
 #include "plane_launch.h"
 #include "plane_not_seen.h"
 
+// The early wave exits below (surplus waves end while the rest of the workgroup still meets __syncthreads)
+// rely on gfx9's s_barrier waiting only for the waves that have not ended.  Other targets keep every wave to
+// the end of the kernel.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__) && !defined(SPSLAM_SEG_NO_EARLY_EXIT)
+#define SPSLAM_SEG_NO_EARLY_EXIT 1
+#endif
+
 namespace spslam {
 namespace planes {
 

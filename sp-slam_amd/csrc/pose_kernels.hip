@@ -222,17 +222,24 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
 }
 
 // acc += col[0], col[stride], ... col[(cnt - 1) stride] one after the other (the reference's order); the
-// loads run ahead of the dependent adds in groups of 8
+// loads of the next group of 8 are in flight while the current group's dependent adds run (the prefetch past
+// the last group reads stage rows that are never used -- unconditional, so the waits stay per group)
 __device__ __forceinline__ void chain_add(double& acc, const double* col, int cnt) {
-    int i = 0;
-    for (; i + 8 <= cnt; i += 8) {
-        double v[8];
+    static_assert((kStage & (kStage - 1)) == 0, "row wrap");
+    const int full = cnt & ~7;
+    double v[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = col[(i + k) * kStageStride];
+    for (int k = 0; k < 8; k++) v[k] = col[k * kStageStride];
+    for (int i = 0; i < full; i += 8) {
+        double w[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) w[k] = col[((i + 8 + k) & (kStage - 1)) * kStageStride];
 #pragma unroll
         for (int k = 0; k < 8; k++) acc += v[k];
+#pragma unroll
+        for (int k = 0; k < 8; k++) v[k] = w[k];
     }
-    for (; i < cnt; i++) acc += col[i * kStageStride];
+    for (int i = full; i < cnt; i++) acc += col[i * kStageStride];
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {

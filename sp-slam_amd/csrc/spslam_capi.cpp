@@ -129,6 +129,7 @@ struct spslam_ctx {
     size_t lba_scratch_bytes = 0;
     long long* d_lba_off = nullptr;
     int32_t* h_lba_stop = nullptr;    // host-mapped coherent pbStopFlag mirror of spslam_lba_optimize
+    int32_t* d_lba_stop = nullptr;    // its device alias (hipHostGetDevicePointer)
     int lba_stop_after = -1;          // spslam_lba_debug_stop_after
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
@@ -1132,15 +1133,17 @@ int spslam_lba_optimize(spslam_ctx* c, const spslam_lba_problem* problem, const 
     const void* src[] = {&P, kfs, points, point_obs, planes, plane_obs};
     for (int i = 0; i < 6; i++)
         if (sz[i]) HIP_CHECK(c, hipMemcpyAsync(q + o[i], src[i], sz[i], hipMemcpyHostToDevice, c->stream));
-    if (stop_flag && !c->h_lba_stop)
+    if (stop_flag && !c->h_lba_stop) {
         HIP_CHECK(c, hipHostMalloc((void**)&c->h_lba_stop, sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_CHECK(c, hipHostGetDevicePointer((void**)&c->d_lba_stop, c->h_lba_stop, 0));
+    }
     if (stop_flag) *(volatile int32_t*)c->h_lba_stop = *stop_flag ? 1 : 0;
     int rc = lba_batch(
         c, 1, &P, (const spslam_lba_problem*)(q + o[0]), (const spslam_lba_keyframe*)(q + o[1]),
         (const spslam_lba_point*)(q + o[2]), (const spslam_lba_point_obs*)(q + o[3]),
         (const spslam_lba_plane*)(q + o[4]), (const spslam_lba_plane_obs*)(q + o[5]), cfg, (float*)(q + o[6]),
         (float*)(q + o[7]), (float*)(q + o[8]), q + o[9], q + o[10], (spslam_lba_result*)(q + o[11]),
-        stop_flag ? c->h_lba_stop : nullptr, c->stream, stop_flag, stop_flag ? c->h_lba_stop : nullptr);
+        stop_flag ? c->d_lba_stop : nullptr, c->stream, stop_flag, stop_flag ? c->h_lba_stop : nullptr);
     if (rc) return rc;
     void* dst[] = {kf_out, pt_out, pl_out, point_obs_outlier, plane_obs_outlier, result};
     for (int i = 0; i < 6; i++)

@@ -95,7 +95,7 @@ def test_c4_long_sequence_matches_oracle():
     import sequence
     import trajectory
     n = 90
-    sp = sequence.SequencePath(2, n + 1, n_sequences=1, pipelined=True, **pipeline.CONFIGS["c4"])
+    sp = sequence.SequencePath(2, n + 2, n_sequences=1, pipelined=True, **pipeline.CONFIGS["c4"])
     try:
         for _ in range(n):
             sp.step()
@@ -151,7 +151,7 @@ def test_c3_local_mapping_in_the_loop():
     import trajectory
     from test_gpu_pose import pose_close
     n = 45
-    sp = sequence_path(2, n + 1, 1, "c3")
+    sp = sequence_path(2, n + 2, 1, "c3")
     try:
         assert sp.local_mapping
         for _ in range(n):
