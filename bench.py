@@ -456,6 +456,10 @@ def main():
                     help="frames per tracked sequence of the ATE check (0 = skip)")
     ap.add_argument("--closed-loop-steps", type=int, default=20,
                     help="timed steps of the closed-loop line (tracked sequences at --batch slots; 0 = skip)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="multi-rank rehearsal on a one-GPU box: every rank on GPU 0, collectives over gloo (the "
+                         "per-rank HotPath and the aggregation run as in an N-GPU job; the value is not a scaling "
+                         "number)")
     ap.add_argument("--dist-check", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU): spawn, rendezvous, aggregation")
     args = ap.parse_args()
@@ -472,11 +476,17 @@ def main():
     import pipeline
     cfg = pipeline.CONFIGS[args.config]
     import torch
+    if args.rehearse_one_gpu:
+        local = 0
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    coll_dev = "cpu" if args.rehearse_one_gpu else "cuda"
 
     hp = pipeline.HotPath(args.batch, unique_frames=args.unique_frames, device=local,
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
@@ -497,8 +507,8 @@ def main():
     elapsed = time.perf_counter() - t0
     times = {k: v for k, v in hp.kernel_times().items() if v[1] > 0}
     res = hp.results()
-    ranks = per_rank(args.batch * args.steps, elapsed, dist, "cuda")
-    elapsed = max_over_ranks(elapsed, dist, "cuda")
+    ranks = per_rank(args.batch * args.steps, elapsed, dist, coll_dev)
+    elapsed = max_over_ranks(elapsed, dist, coll_dev)
 
     frames = sum(f for f, _ in ranks)
     value = frames / elapsed
@@ -558,7 +568,8 @@ def main():
                 "synthesized from the scene, every correspondence from the step's own matching + association)",
         "per_rank": [{"rank": r, "frames": f, "elapsed_s": e} for r, (f, e) in enumerate(ranks)],
         "config": {"workload": WORKLOADS[args.config], "name": args.config, "frames_per_step_per_gpu": args.batch,
-                   "parallelism": f"shard{world}", "mean_keypoints": hp.mean_keypoints,
+                   "parallelism": f"shard{world}" + ("-rehearsal-on-gpu0-gloo" if args.rehearse_one_gpu else ""),
+                   "mean_keypoints": hp.mean_keypoints,
                    "pipelined": hp.pipelined,
                    "mean_planes": float(res["plane_counts"].mean()),
                    "mean_supposed_planes": n_sup,

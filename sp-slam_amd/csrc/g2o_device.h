@@ -13,6 +13,18 @@
 namespace spslam {
 namespace g2od {
 
+// Measurement knob only (never the product build): SPSLAM_LIBM64_OCML swaps the correctly rounded routines for
+// ocml's to price them (tools/pose_phases.py); results then differ from the oracle.
+#ifdef SPSLAM_LIBM64_OCML
+namespace lm {
+__device__ __forceinline__ void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
+__device__ __forceinline__ double atan2_(double y, double x) { return ::atan2(y, x); }
+__device__ __forceinline__ double cube_(double x) { return libm64cr::cube_(x); }
+}  // namespace lm
+#else
+namespace lm = libm64cr;
+#endif
+
 struct V3 { double x, y, z; };
 __device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 __device__ __forceinline__ V3 operator*(double s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
@@ -114,8 +126,8 @@ __device__ __forceinline__ SE3 se3_exp(const double* u) {
         V = R;
     } else {
         double st, ct;
-        libm64cr::sincos_(theta, &st, &ct);
-        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / libm64cr::cube_(theta);
+        lm::sincos_(theta, &st, &ct);
+        const double a = st / theta, b = (1 - ct) / (theta * theta), c = (theta - st) / lm::cube_(theta);
         for (int k = 0; k < 9; k++) {
             R.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + a * O[k] + b * O2[k];
             V.a[k] = (k % 4 == 0 ? 1.0 : 0.0) + b * O[k] + c * O2[k];
@@ -136,22 +148,22 @@ __device__ __forceinline__ void p_normalize(double* v) {
     if (v[3] < 0.0)
         for (int i = 0; i < 4; i++) v[i] = -v[i];
 }
-__device__ __forceinline__ double azimuth(V3 v) { return libm64cr::atan2_(v.y, v.x); }
-__device__ __forceinline__ double elevation(V3 v) { return libm64cr::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
+__device__ __forceinline__ double azimuth(V3 v) { return lm::atan2_(v.y, v.x); }
+__device__ __forceinline__ double elevation(V3 v) { return lm::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
 // Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
 __device__ __forceinline__ M3 p_rotation(V3 v) {
     const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
     double sa, ca, se, ce;
-    libm64cr::sincos_(ha, &sa, &ca);
-    libm64cr::sincos_(he, &se, &ce);
+    lm::sincos_(ha, &sa, &ca);
+    lm::sincos_(he, &se, &ce);
     const Q a{ca, 0.0 * sa, 0.0 * sa, 1.0 * sa};
     const Q e{ce, 0.0 * se, 1.0 * se, 0.0 * se};
     return q_to_rot(q_mul(a, e));
 }
-// Eigen AngleAxis::toRotationMatrix() * v
-__device__ __forceinline__ V3 aa_apply(double ang, V3 ax, V3 v) {
-    double s, c;
-    libm64cr::sincos_(ang, &s, &c);
+// Eigen AngleAxis(M_PI / 2, ax).toRotationMatrix() * v (Plane3D::ominus_ver's only angle): sin and cos of the
+// double nearest pi/2, correctly rounded (tests/test_gpu_libm.py checks both against the oracle)
+__device__ __forceinline__ V3 aa_apply_half_pi(V3 ax, V3 v) {
+    const double s = 1.0, c = 6.123233995736766e-17;
     const V3 sa = s * ax;
     const V3 c1 = (1 - c) * ax;
     M3 r;
@@ -177,7 +189,7 @@ __device__ __forceinline__ void plane_error(int kind, const SE3& T, const P4& wo
         if (dot(mn, ln) < 0) ref = -1.0 * ln;
     } else if (kind == 2) {
         const V3 a = cross(ln, mn);
-        ref = aa_apply(M_PI / 2, (1.0 / sqrt(dot(a, a))) * a, ln);
+        ref = aa_apply_half_pi((1.0 / sqrt(dot(a, a))) * a, ln);
     }
     const V3 n = mtv(p_rotation(ref), mn);
     e[0] = azimuth(n);
@@ -196,8 +208,8 @@ __device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& wor
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)
 __device__ void p_oplus(P4& p, const double* v) {
     double s, c, s0, c0;
-    libm64cr::sincos_(v[1], &s, &c);
-    libm64cr::sincos_(v[0], &s0, &c0);
+    lm::sincos_(v[1], &s, &c);
+    lm::sincos_(v[0], &s0, &c0);
     const V3 n{c * c0, c * s0, s};
     const M3 R = p_rotation(V3{p.c[0], p.c[1], p.c[2]});
     const double d = -p.c[3] + v[2];

@@ -28,6 +28,9 @@ def test_sin_cos_cube_bit_exact(gpu):
                         rng.standard_normal(n) * 10.0 ** rng.uniform(-9, -1, n),
                         ((k * math.pi / 2)[:, None] + rng.standard_normal((41, 500)) * 1e-6).ravel(),
                         [0.0, -0.0, math.pi / 2, math.pi, 1e-300, 5e-324, np.inf, -np.inf, np.nan]])
+    # the constants g2o_device.h aa_apply_half_pi uses for sin / cos (M_PI / 2)
+    assert oracle_ctypes.libm_cr(0, np.array([math.pi / 2]))[0] == 1.0
+    assert oracle_ctypes.libm_cr(1, np.array([math.pi / 2]))[0] == 6.123233995736766e-17
     for kind in (0, 1, 3):
         d = spslam_gpu.debug_libm64(gpu, kind, a)
         o = oracle_ctypes.libm_cr(kind, a)
