@@ -19,6 +19,14 @@ namespace g2od {
 namespace lm {
 __device__ __forceinline__ void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
 __device__ __forceinline__ double atan2_(double y, double x) { return ::atan2(y, x); }
+__device__ __forceinline__ void sincos2_(double a, double b, double* sa, double* ca, double* sb, double* cb) {
+    ::sincos(a, sa, ca);
+    ::sincos(b, sb, cb);
+}
+__device__ __forceinline__ void atan2x2_(double y0, double x0, double y1, double x1, double* r0, double* r1) {
+    *r0 = ::atan2(y0, x0);
+    *r1 = ::atan2(y1, x1);
+}
 __device__ __forceinline__ double cube_(double x) { return libm64cr::cube_(x); }
 }  // namespace lm
 #else
@@ -151,11 +159,16 @@ __device__ __forceinline__ void p_normalize(double* v) {
 __device__ __forceinline__ double azimuth(V3 v) { return lm::atan2_(v.y, v.x); }
 __device__ __forceinline__ double elevation(V3 v) { return lm::atan2_(v.z, sqrt(v.x * v.x + v.y * v.y)); }
 // Plane3D::rotation: (AngleAxis(az, Z) * AngleAxis(-el, Y)).toRotationMatrix()
+// (the two angles, then the two sin / cos pairs, are evaluated side by side: independent dependent chains)
+__device__ __forceinline__ void az_el(V3 v, double* az, double* el) {
+    lm::atan2x2_(v.y, v.x, v.z, sqrt(v.x * v.x + v.y * v.y), az, el);
+}
 __device__ __forceinline__ M3 p_rotation(V3 v) {
-    const double ha = 0.5 * azimuth(v), he = 0.5 * (-elevation(v));
+    double az, el;
+    az_el(v, &az, &el);
+    const double ha = 0.5 * az, he = 0.5 * (-el);
     double sa, ca, se, ce;
-    lm::sincos_(ha, &sa, &ca);
-    lm::sincos_(he, &se, &ce);
+    lm::sincos2_(ha, he, &sa, &ca, &se, &ce);
     const Q a{ca, 0.0 * sa, 0.0 * sa, 1.0 * sa};
     const Q e{ce, 0.0 * se, 1.0 * se, 0.0 * se};
     return q_to_rot(q_mul(a, e));
@@ -192,8 +205,7 @@ __device__ __forceinline__ void plane_error(int kind, const SE3& T, const P4& wo
         ref = aa_apply_half_pi((1.0 / sqrt(dot(a, a))) * a, ln);
     }
     const V3 n = mtv(p_rotation(ref), mn);
-    e[0] = azimuth(n);
-    e[1] = elevation(n);
+    az_el(n, &e[0], &e[1]);
     if (kind == 0) e[2] = (-v[3]) - (-meas.c[3]);
 }
 
@@ -205,11 +217,17 @@ __device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& wor
     return E3{e[0], e[1], e[2]};
 }
 
+// The same, out of line: one copy of the ~1.5K-instruction evaluation (4 atan2, 2 sincos, 3 normalisations)
+// per kernel instead of one per call site and per inlined branch.  Arguments and result travel by value in
+// VGPRs (no stack); the call costs ~100 cycles against ~2K of evaluation.
+__device__ __noinline__ E3 plane_error_call(int kind, SE3 T, P4 world, P4 meas) {
+    return plane_error3(kind, T, world, meas);
+}
+
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)
 __device__ void p_oplus(P4& p, const double* v) {
     double s, c, s0, c0;
-    lm::sincos_(v[1], &s, &c);
-    lm::sincos_(v[0], &s0, &c0);
+    lm::sincos2_(v[1], v[0], &s, &c, &s0, &c0);
     const V3 n{c * c0, c * s0, s};
     const M3 R = p_rotation(V3{p.c[0], p.c[1], p.c[2]});
     const double d = -p.c[3] + v[2];

@@ -159,29 +159,54 @@ __host__ __device__ inline void sincos_eval(double x, dd* s, dd* c) {
     *c = ((n + 1) & 2) ? dneg(b) : b;
 }
 
-__host__ __device__ inline void sincos_(double x, double* sn, double* cs) {
-    const double ax = fabs(x);
-    if (!(ax <= 1.7976931348623157e308)) {  // inf / NaN
-        *sn = *cs = x - x;
-        return;
-    }
-    if (ax < 0x1p-27) {  // sin x = x - x^3/6 and cos x = 1 - x^2/2 both round to their first term
-        *sn = x;
-        *cs = 1.0;
-        return;
-    }
+// The accurate paths run for ~2^-16 of the arguments: kept out of line, so that the callers' inlined code holds
+// the quick paths only (the pose kernel inlines ~20 sin / cos / atan2 sites; inlining both paths at every site
+// made its body ~5x the instruction cache)
+#if defined(__HIP__)
+#define SPSLAM_CR_COLD __attribute__((noinline))
+#else
+#define SPSLAM_CR_COLD
+#endif
+__host__ __device__ SPSLAM_CR_COLD inline dd sincos_accurate(double x) {
     dd s, c;
-    sincos_eval<false>(x, &s, &c);
+    sincos_eval<true>(x, &s, &c);
+    double rs, rc;
+    rounds_to(s, kAccurateEps, &rs);
+    rounds_to(c, kAccurateEps, &rc);
+    return dd{rs, rc};
+}
+
+// The quick path without branches: special arguments select their result at the end (the evaluation then runs
+// on a stand-in argument), so that two evaluations placed side by side form one straight-line block whose
+// dependent chains the scheduler interleaves.  Returns false when the accurate path must decide.
+__host__ __device__ inline bool sincos_quick(double x, double* sn, double* cs) {
+    const double ax = fabs(x);
+    const bool nonfinite = !(ax <= 1.7976931348623157e308);  // inf / NaN: both x - x
+    const bool tiny = ax < 0x1p-27;  // sin x = x - x^3/6 and cos x = 1 - x^2/2 both round to their first term
+    const bool special = nonfinite || tiny;
+    dd s, c;
+    sincos_eval<false>(special ? 1.0 : x, &s, &c);
     double rs, rc;
     const bool ok_s = rounds_to(s, kQuickEps, &rs), ok_c = rounds_to(c, kQuickEps, &rc);
-    const bool ok = ok_s && ok_c;
-    if (!ok) {
-        sincos_eval<true>(x, &s, &c);
-        rounds_to(s, kAccurateEps, &rs);
-        rounds_to(c, kAccurateEps, &rc);
+    *sn = nonfinite ? x - x : (tiny ? x : rs);
+    *cs = nonfinite ? x - x : (tiny ? 1.0 : rc);
+    return special || (ok_s && ok_c);
+}
+
+__host__ __device__ inline void sincos_(double x, double* sn, double* cs) {
+    if (!sincos_quick(x, sn, cs)) {
+        const dd a = sincos_accurate(x);
+        *sn = a.hi;
+        *cs = a.lo;
     }
-    *sn = rs;
-    *cs = rc;
+}
+// sin / cos of two arguments, evaluated side by side
+__host__ __device__ inline void sincos2_(double x0, double x1, double* s0, double* c0, double* s1, double* c1) {
+    const bool ok0 = sincos_quick(x0, s0, c0), ok1 = sincos_quick(x1, s1, c1);
+    if (!(ok0 && ok1)) {
+        if (!ok0) { const dd a = sincos_accurate(x0); *s0 = a.hi; *c0 = a.lo; }
+        if (!ok1) { const dd a = sincos_accurate(x1); *s1 = a.hi; *c1 = a.lo; }
+    }
 }
 __host__ __device__ inline double sin_(double x) {
     double s, c;
@@ -225,36 +250,60 @@ __host__ __device__ inline dd atan2_eval(double y, double x) {
     const double c = fi * 0.015625;
     const dd nm = two_sum(zh - c, z.lo);               // z - i/64 (the high difference is exact)
     const dd dn = dadd_d(dmul_d(z, c), 1.0);           // 1 + z i/64
-    const dd u = i == 0 ? z : ddiv(nm, dn);
+    const dd uq = ddiv(nm, dn);  // computed for i = 0 too: a select, not a branch
+    const dd u{i == 0 ? z.hi : uq.hi, i == 0 ? z.lo : uq.lo};
     dd a = dadd(dd{kAtan64[i][0], kAtan64[i][1]}, atan_small<kAccurate>(u));
-    if (swap) a = dadd(dd{kPio2_hi, kPio2_lo}, dneg(a));
-    if (x < 0) a = dadd(dd{kPi_hi, kPi_lo}, dneg(a));
-    return y < 0 ? dneg(a) : a;
+    // pi/2 - a, pi - a and the sign as selects (no branches inside the quick path)
+    const dd a1 = dadd(dd{kPio2_hi, kPio2_lo}, dneg(a));
+    a = dd{swap ? a1.hi : a.hi, swap ? a1.lo : a.lo};
+    const dd a2 = dadd(dd{kPi_hi, kPi_lo}, dneg(a));
+    a = dd{x < 0 ? a2.hi : a.hi, x < 0 ? a2.lo : a.lo};
+    return dd{y < 0 ? -a.hi : a.hi, y < 0 ? -a.lo : a.lo};
 }
 
-__host__ __device__ inline double atan2_(double y, double x) {
-    if (x != x || y != y) return x + y;
+__host__ __device__ SPSLAM_CR_COLD inline double atan2_accurate(double y, double x) {
+    double out;
+    rounds_to(atan2_eval<true>(y, x), kAccurateEps, &out);
+    return out;
+}
+
+// The quick path without branches (see sincos_quick); false when the accurate path must decide.
+__host__ __device__ inline bool atan2_quick(double y, double x, double* out) {
     const double ax = fabs(x), ay = fabs(y);
     const double inf = 1.7976931348623157e308 * 2.0;
     const double sy = y < 0 || (y == 0 && 1.0 / y < 0) ? -1.0 : 1.0;  // sign of y, zeros included
     const bool xneg = x < 0 || (x == 0 && 1.0 / x < 0);
-    if (ay == 0) return xneg ? sy * kPi_hi : y;                 // atan2(+-0, x): +-pi or +-0
-    if (ax == 0) return sy * kPio2_hi;
-    if (ax == inf || ay == inf) {
-        if (ax == inf && ay == inf) return sy * (xneg ? k3Pio4_hi : kPio4_hi);
-        if (ax == inf) return xneg ? sy * kPi_hi : sy * 0.0;
-        return sy * kPio2_hi;
-    }
+    const bool nan = x != x || y != y;
+    const bool zy = ay == 0, zx = ax == 0, infs = ax == inf || ay == inf;
     // |y / x| below 2^-900 with x > 0: atan2 = y/x (1 - (y/x)^2/3), which rounds like y/x (y / x is never a
     // midpoint) -- and the double-double quotient's low part would be subnormal
-    if (!xneg && ay < ax * 0x1p-900) return y / x;
-    dd r = atan2_eval<false>(y, x);
+    const bool small = !xneg && ay < ax * 0x1p-900;
+    const bool special = nan || zy || zx || infs || small;
+    double sp = y / x;                                            // small
+    if (infs) sp = ax == inf && ay == inf ? sy * (xneg ? k3Pio4_hi : kPio4_hi)
+                                          : (ax == inf ? (xneg ? sy * kPi_hi : sy * 0.0) : sy * kPio2_hi);
+    if (zx) sp = sy * kPio2_hi;
+    if (zy) sp = xneg ? sy * kPi_hi : y;                         // atan2(+-0, x): +-pi or +-0
+    if (nan) sp = x + y;
+    const dd r = atan2_eval<false>(special ? 1.0 : y, special ? 1.0 : x);
+    double q;
+    const bool ok = rounds_to(r, kQuickEps, &q);
+    *out = special ? sp : q;
+    return special || ok;
+}
+
+__host__ __device__ inline double atan2_(double y, double x) {
     double out;
-    if (!rounds_to(r, kQuickEps, &out)) {
-        r = atan2_eval<true>(y, x);
-        rounds_to(r, kAccurateEps, &out);
-    }
+    if (!atan2_quick(y, x, &out)) out = atan2_accurate(y, x);
     return out;
+}
+// atan2 of two argument pairs, evaluated side by side
+__host__ __device__ inline void atan2x2_(double y0, double x0, double y1, double x1, double* r0, double* r1) {
+    const bool ok0 = atan2_quick(y0, x0, r0), ok1 = atan2_quick(y1, x1, r1);
+    if (!(ok0 && ok1)) {
+        if (!ok0) *r0 = atan2_accurate(y0, x0);
+        if (!ok1) *r1 = atan2_accurate(y1, x1);
+    }
 }
 
 // ---- x^3 (pow(x, 3) in SE3Quat::exp and the LM damping update) ---------------------------------------------

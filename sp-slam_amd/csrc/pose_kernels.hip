@@ -162,35 +162,56 @@ __device__ __forceinline__ bool ldlt_solve(const double (*H)[6], double lambda, 
     return true;
 }
 
-// Four waves per problem (measured: one wave per problem frees SIMDs for the
-// pipelined extraction but makes the edge passes 4x longer -- a net loss).
-constexpr int kThreads = 256;
+// Four compute waves and one chain wave per problem.  The compute waves evaluate the edges (errors, Jacobians,
+// quadratic-form terms, trial chi2) and stage one row per edge in an LDS ring; the chain wave adds the rows in
+// edge order as they arrive.  g2o's sums are serial (one dependent fp64 add per edge and value, ~13 ns each on
+// gfx950), so the ordered chains set the floor of every pass; with a wave of their own they run beside the
+// edge evaluation instead of after it.  (Measured before: one wave per problem frees SIMDs for the pipelined
+// extraction but makes the edge passes 4x longer -- a net loss.)
+constexpr int kComputeWaves = 4;
+constexpr int kCompute = 64 * kComputeWaves;
+constexpr int kThreads = kCompute + 64;
 constexpr int kWaves = kThreads / 64;
-constexpr int kRed = 28;  // robust chi2, 21 upper-triangle H terms, 6 b terms
-constexpr int kPlaneChunk = 64;  // plane edges whose 13 errors (12 perturbed poses + T) are evaluated together
+constexpr int kChainWave = kComputeWaves;
+constexpr int kRed = 28;         // robust chi2, 21 lower-triangle H terms, 6 b terms
+constexpr int kPlaneChunk = 64;  // plane edges whose trial-pose errors are kept for the next pass A
 constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
 
-constexpr int kStage = 256;      // edges per chained chunk
-constexpr int kStageStride = kRed + 1;  // odd stride in doubles: the 64 lanes' row writes spread over the banks
+// Pass A ring: rows of the 28 terms (odd stride: the 64 lanes' row writes spread over the banks).  Pass B reuses
+// the same LDS as a ring of kSpec-value rows (trial robust chi2).
+constexpr int kRingA = 256;
+constexpr int kStrideA = kRed + 1;
+constexpr int kSpinCap = 1 << 20;  // bound of every wait (s_sleep 1 each: ~30 ms); never reached in a correct run
+
+template <int kSpec>
+struct RingB {
+    static constexpr int kStride = kSpec + 1;
+    static constexpr int kRows = [] {
+        int r = 1;
+        while (2 * r * kStride <= kRingA * kStrideA) r *= 2;
+        return r;
+    }();
+};
 
 template <int kSpec>
 struct Shared {
-    double stage[kStage][kStageStride];  // per-edge terms of one chunk (pass A: 28, pass B: kSpec)
+    double ring[kRingA * kStrideA];   // pass A: [kRingA][kStrideA]; pass B: [RingB::kRows][kSpec + 1]
     double tot[kRed];                 // the chained totals, for every thread
-    double red[2][kWaves][kRed];      // wave totals of the workgroup sums, double-buffered
-    double perr[kPlaneChunk][13][3];  // plane errors at the 12 perturbed poses and at T
-    double perrB[kPlaneChunk][kSpec][3];  // plane errors at the trial poses of the last pass B
+    double red[2][kWaves][1];         // wave totals of the workgroup sums, double-buffered
+    double perr[kComputeWaves][5][13][3];  // per compute wave: plane errors at the 12 perturbed poses and at T
+    double perrB[kPlaneChunk][kSpec][3];   // plane errors at the trial poses of the last pass B
     double perrT[kPlaneChunk][3];     // plane errors at the accepted trial pose = the next iteration's T
     double hb[kRed];                  // the iteration's H (lower, 21) and b (6), slot 0 unused
     SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)
     SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
+    int done[kComputeWaves];          // rounds each compute wave has staged in the current pass
+    int consumed;                     // rows the chain wave has added in the current pass
+    int stall;                        // a wait hit kSpinCap (reported through lm_iterations)
 };
 
-// Workgroup sum of NV doubles per thread; every thread returns the same totals.  Fixed order (the oracle's
-// device-order mode restates it, oracle/pose_oracle.cpp): xor butterfly over the 64 lanes of each wave (all
-// lanes end with the wave total), then ((0 + w0) + w1) + w2) + w3 from LDS in every thread.  One barrier;
-// consecutive calls alternate the two LDS buffers, so a buffer is only rewritten after the next call's
-// barrier has seen every thread finish reading it.
+// Workgroup sum of NV doubles per thread; every thread returns the same totals.  Fixed order: xor butterfly over
+// the 64 lanes of each wave, then (((0 + w0) + w1) + ...) from LDS in every thread.  Only the relabel's outlier
+// count uses it (small integers: exact in any order).  One barrier; consecutive calls alternate the two buffers.
 template <int NV, class Sh>
 __device__ __forceinline__ void wg_sum(double (&v)[NV], Sh& S, int& buf) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -221,25 +242,135 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
     *rho1 = delta / s;
 }
 
-// acc += col[0], col[stride], ... col[(cnt - 1) stride] one after the other (the reference's order); the
-// loads of the next group of 8 are in flight while the current group's dependent adds run (the prefetch past
-// the last group reads stage rows that are never used -- unconditional, so the waits stay per group)
-__device__ __forceinline__ void chain_add(double& acc, const double* col, int cnt) {
-    static_assert((kStage & (kStage - 1)) == 0, "row wrap");
-    const int full = cnt & ~7;
-    double v[8];
+// acc += rows start .. start + cnt - 1 of a ring column (slot = row & (kRows - 1)), one after the other: the
+// reference's order.  Three register groups of 8 rotate: while one group's dependent adds run, the other two
+// groups' loads are in flight, and a group is refilled right after its adds (no register moves: a FIFO rotated
+// with moves makes the compiler wait for every outstanding load once per group -- a full LDS round trip per 8
+// adds; the scheduling barriers keep each refill ahead of the next group's adds).  Rows past cnt are loaded and
+// never added.
+template <int kStride, int kRows>
+__device__ __forceinline__ void chain_ring(double& acc, const double* col, int start, int cnt) {
+    static_assert((kRows & (kRows - 1)) == 0, "ring wrap");
+    auto ld = [&](double (&v)[8], int i) __attribute__((always_inline)) {
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = col[k * kStageStride];
-    for (int i = 0; i < full; i += 8) {
-        double w[8];
+        for (int k = 0; k < 8; k++) v[k] = col[((start + i + k) & (kRows - 1)) * kStride];
+    };
+    auto add = [&](const double (&v)[8], int n) __attribute__((always_inline)) {
 #pragma unroll
-        for (int k = 0; k < 8; k++) w[k] = col[((i + 8 + k) & (kStage - 1)) * kStageStride];
-#pragma unroll
-        for (int k = 0; k < 8; k++) acc += v[k];
-#pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = w[k];
+        for (int k = 0; k < 8; k++)
+            if (k < n) acc += v[k];
+    };
+    const int full = cnt - cnt % 24;
+    double a[8], b[8], c[8];
+    ld(a, 0);
+    ld(b, 8);
+    ld(c, 16);
+    for (int i = 0; i < full; i += 24) {
+        add(a, 8);
+        ld(a, i + 24);
+        __builtin_amdgcn_sched_barrier(0);
+        add(b, 8);
+        ld(b, i + 32);
+        __builtin_amdgcn_sched_barrier(0);
+        add(c, 8);
+        ld(c, i + 40);
+        __builtin_amdgcn_sched_barrier(0);
     }
-    for (int i = full; i < cnt; i++) acc += col[i * kStageStride];
+    const int r = cnt - full;  // < 24 left: a, b, c hold rows full .. full + 23
+    add(a, r);
+    add(b, r - 8);
+    add(c, r - 16);
+}
+
+// The staging schedule of one pass, known to every wave: point rounds of 256 edges (64 per compute wave), then
+// plane rounds of 4 * ps edges (ps per compute wave).  Compute wave w stages its share of round k and publishes
+// done[w] = k + 1; the rows below available() are staged.
+struct Schedule {
+    int np, ne, ps, npr, nr;
+    __device__ Schedule(int np_, int nl, int ps_) : np(np_), ne(np_ + nl), ps(ps_) {
+        npr = (np + kCompute - 1) / kCompute;
+        nr = npr + (nl + kComputeWaves * ps - 1) / (kComputeWaves * ps);
+    }
+    // edge range [lo, hi) of round k and the edges per wave
+    __device__ void round(int k, int& lo, int& hi, int& s) const {
+        if (k < npr) {
+            lo = kCompute * k; hi = min(lo + kCompute, np); s = 64;
+        } else {
+            lo = np + kComputeWaves * ps * (k - npr); hi = min(lo + kComputeWaves * ps, ne); s = ps;
+        }
+    }
+    // wave w's edges [a, b) of round k (possibly empty)
+    __device__ void share(int k, int w, int& a, int& b) const {
+        int lo, hi, s;
+        round(k, lo, hi, s);
+        a = min(lo + w * s, hi);
+        b = min(lo + (w + 1) * s, hi);
+    }
+};
+
+__device__ __forceinline__ int lds_acquire(const int* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(int* p, int v) {  // after this wave's ring writes (every lane fences)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// rows below this are staged (every compute wave's share of every earlier round, and the leading waves' shares
+// of the current one)
+template <class Sh>
+__device__ __forceinline__ int available(Sh& S, const Schedule& G) {
+    int d[kComputeWaves], m = 1 << 30;
+#pragma unroll
+    for (int w = 0; w < kComputeWaves; w++) {
+        d[w] = lds_acquire(&S.done[w]);
+        m = min(m, d[w]);
+    }
+    if (m >= G.nr) return G.ne;
+    int lo, hi, s;
+    G.round(m, lo, hi, s);
+    int j = 0;
+#pragma unroll
+    for (int w = 0; w < kComputeWaves; w++)
+        if (j == w && d[w] > m) j = w + 1;
+    return min(lo + j * s, hi);
+}
+
+// the chain wave: add every staged row of the pass in edge order, column = this lane's value (lanes past nval
+// read the padding column), and hand out the ring slots as rows are added
+template <int kStride, int kRows, class Sh>
+__device__ __forceinline__ double chain_pass(Sh& S, const Schedule& G, const double* ring, int nval) {
+    const int lane = threadIdx.x & 63;
+    const double* col = ring + (lane < nval ? lane : kStride - 1);
+    double acc = 0;
+    int c = 0;
+    while (c < G.ne) {
+        int a = available(S, G);
+        for (int spin = 0; a <= c; spin++) {
+            if (spin >= kSpinCap) { S.stall = 1; a = G.ne; break; }
+            __builtin_amdgcn_s_sleep(1);
+            a = available(S, G);
+        }
+        chain_ring<kStride, kRows>(acc, col, c, a - c);
+        c = a;
+        lds_publish(&S.consumed, c);
+    }
+    return acc;
+}
+
+// a compute wave about to overwrite ring slots of rows [b - kRows, ...): wait until the chain wave added them
+template <class Sh>
+__device__ __forceinline__ void ring_wait(Sh& S, int need) {
+    if (need <= 0) return;
+    for (int spin = 0; lds_acquire(&S.consumed) < need; spin++) {
+        if (spin >= kSpinCap) { S.stall = 1; return; }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
@@ -255,22 +386,54 @@ __device__ __forceinline__ SE3 readlane_se3(const SE3& a, int l) {
     return r;
 }
 
+// one edge's 28 terms (BaseUnaryEdge / BaseBinaryEdge::constructQuadraticForm in Eigen's order: the temporary
+// A^T (rho' Omega) times A) and -s_e with b -= s_e (unary: ((rho' A^T) Omega) e; binary, pose = vertex 1:
+// B^T (rho' Omega e)), preceded by the edge's robust chi2
+__device__ __forceinline__ void edge_terms(const double (&J)[3][6], const double* err, const double* info, double delta,
+                                           bool robust, bool binary, double (&row)[kRed]) {
+    double rho0, rho1;
+    const double chi = (err[0] * (info[0] * err[0]) + err[1] * (info[1] * err[1])) + err[2] * (info[2] * err[2]);
+    huber(chi, delta, robust, &rho0, &rho1);
+    row[0] = rho0;
+    double wo[3], q[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) { wo[r] = rho1 * info[r]; q[r] = (info[r] * err[r]) * rho1; }
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) {
+            double h = 0;
+#pragma unroll
+            for (int r = 0; r < 3; r++) h += (J[r][i] * wo[r]) * J[r][j];
+            row[1 + i * (i + 1) / 2 + j] = h;
+        }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double sb = 0;
+        if (binary) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) sb += J[r][i] * q[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 3; r++) sb += ((rho1 * J[r][i]) * info[r]) * err[r];
+        }
+        row[22 + i] = -sb;
+    }
+}
+
 }  // namespace pose
 
 using namespace pose;
 
-// Every thread holds the whole LM state (pose, lambda, chi2 values, H, b): the workgroup sums hand every
-// thread the same totals and every decision is computed redundantly from them, so no thread waits on another
-// except inside wg_sum.  The damping trials of one LM iteration are evaluated kSpec at a time: after a
-// rejected trial the reference only multiplies lambda by ni and doubles ni (optimization_algorithm_levenberg
-// .cpp:145-160), so trial q's lambda is known in advance; lane q % kSpec of every wave solves trial q, the
-// trial poses are broadcast with readlane, one pass over the edges evaluates all kSpec robust chi2 sums, and
-// the accept / reject walk then replays the reference's sequence over them.  Results do not depend on kSpec.
-#ifndef SPSLAM_POSE_MINW
-#define SPSLAM_POSE_MINW 1  // waves per SIMD the register allocation leaves room for
-#endif
+// Every thread holds the whole LM state (pose, lambda, chi2 values, H, b): the chained totals reach every thread
+// through LDS and every decision is computed redundantly from them.  The damping trials of one LM iteration are
+// evaluated kSpec at a time: after a rejected trial the reference only multiplies lambda by ni and doubles ni
+// (optimization_algorithm_levenberg.cpp:145-160), so trial q's lambda is known in advance; lane q % kSpec of
+// every wave solves trial q, the trial poses are broadcast with readlane, one pass over the edges evaluates all
+// kSpec robust chi2 sums, and the accept / reject walk then replays the reference's sequence over them.  Results
+// do not depend on kSpec.
 template <int kSpec>
-__global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
+__global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_problem* __restrict__ probs,
                                                          const spslam_point_obs* __restrict__ pts_all,
                                                          const spslam_plane_obs* __restrict__ pls_all, PoseConsts K,
                                                          const spslam_pose_result* __restrict__ init_from,
@@ -278,7 +441,9 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                                                          uint8_t* __restrict__ pout_all, uint8_t* __restrict__ plout_all) {
     tail_wave_priority();
     __shared__ Shared<kSpec> S;
-    const int t = threadIdx.x, lane = t & 63;
+    using RB = RingB<kSpec>;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const bool chain_wave = wv == kChainWave;
 #ifdef SPSLAM_POSE_PROF
     unsigned long long prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long prof_t = wall_clock64();
@@ -305,6 +470,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         add[t >> 1] = (t & 1) ? -1e-9 : 1e-9;
         S.Eadd[t] = se3_exp(add);
     }
+    if (t == 0) S.stall = 0;
     SE3 T0;  // Converter::toSE3Quat: Quaterniond(R) of the float pose, normalized (every thread)
     {
         M3 R;
@@ -336,17 +502,30 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         p_normalize(w.c);
         p_normalize(m.c);
     };
-    auto error_at = [&](int e, const SE3& T, double* err, V3* pc) __attribute__((always_inline)) {
+    auto error_at = [&](int e, const SE3& T, double* err) __attribute__((always_inline)) {
         E3 r;
         if (e < np) {
             V3 p;
             r = point_error(pts[e], T, cam, p);
-            if (pc) *pc = p;
         } else {
             P4 w, m;
             plane_of(e, w, m);
-            r = plane_error3(pls[e - np].kind, T, w, m);
+            r = plane_error_call(pls[e - np].kind, T, w, m);
         }
+        err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
+    };
+    // the same for an edge known to be a point (plane) edge: the loops that only visit one kind call these, so
+    // the other kind's evaluation is not compiled into them as a dead branch
+    auto point_error_at = [&](int e, const SE3& T, double* err, V3* pc) __attribute__((always_inline)) {
+        V3 p;
+        const E3 r = point_error(pts[e], T, cam, p);
+        if (pc) *pc = p;
+        err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
+    };
+    auto plane_error_at = [&](int e, const SE3& T, double* err) __attribute__((always_inline)) {
+        P4 w, m;
+        plane_of(e, w, m);
+        const E3 r = plane_error_call(pls[e - np].kind, T, w, m);
         err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
     };
     auto chi2_of = [](const double* err, const double* info) __attribute__((always_inline)) {
@@ -355,6 +534,14 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         return (err[0] * (info[0] * err[0]) + err[1] * (info[1] * err[1])) + err[2] * (info[2] * err[2]);
     };
     auto is_outlier = [&](int e) __attribute__((always_inline)) -> bool { return e < np ? pout[e] != 0 : plout[e - np] != 0; };
+    // a new pass: nothing staged, nothing consumed (every wave has passed the previous pass's final barrier)
+    auto pass_begin = [&]() __attribute__((always_inline)) {
+        if (t < kComputeWaves) S.done[t] = 0;
+        if (t == 0) S.consumed = 0;
+        __syncthreads();
+    };
+    double* ringA = S.ring;
+    double* ringB = S.ring;
 
     int buf = 0;
     bool robust = true;
@@ -372,130 +559,104 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
             int lmBad = 0;
             bool tValid = false;  // perrT holds the plane errors at T (set when a trial is accepted)
             for (int it = 0; it < 10; it++) {
-                // ---- pass A: errors, robust chi2, quadratic form at T, chained in edge order
-                // one edge's terms into row t of the stage: its robust chi2, the lower triangle of its
-                // H_e (BaseUnaryEdge / BaseBinaryEdge::constructQuadraticForm in Eigen's order: the
-                // temporary A^T (rho' Omega) times A) and -s_e with b -= s_e (unary: ((rho' A^T) Omega) e;
-                // binary, pose = vertex 1: B^T (rho' Omega e))
-                auto stage_terms = [&](const double (&J)[3][6], const double* err, const double* info, double delta,
-                                       bool binary) __attribute__((always_inline)) {
-                    double* row = S.stage[t];
-                    double rho0, rho1;
-                    huber(chi2_of(err, info), delta, robust, &rho0, &rho1);
-                    row[0] = rho0;
-                    double wo[3], q[3];
-#pragma unroll
-                    for (int r = 0; r < 3; r++) { wo[r] = rho1 * info[r]; q[r] = (info[r] * err[r]) * rho1; }
-#pragma unroll
-                    for (int i = 0; i < 6; i++)
-#pragma unroll
-                        for (int j = 0; j <= i; j++) {
-                            double h = 0;
-#pragma unroll
-                            for (int r = 0; r < 3; r++) h += (J[r][i] * wo[r]) * J[r][j];
-                            row[1 + i * (i + 1) / 2 + j] = h;
-                        }
-#pragma unroll
-                    for (int i = 0; i < 6; i++) {
-                        double sb = 0;
-                        if (binary) {
-#pragma unroll
-                            for (int r = 0; r < 3; r++) sb += J[r][i] * q[r];
-                        } else {
-#pragma unroll
-                            for (int r = 0; r < 3; r++) sb += ((rho1 * J[r][i]) * info[r]) * err[r];
-                        }
-                        row[22 + i] = -sb;
-                    }
-                };
-                auto stage_zero = [&]() __attribute__((always_inline)) {
-#pragma unroll
-                    for (int k = 0; k < kRed; k++) S.stage[t][k] = 0.0;
-                };
-                // value k of the 28 is chained by lane k / 4 of wave k % 4
-                const int ck = lane * kWaves + (t >> 6);
-                const bool chainer = lane * kWaves < kRed;
-                double achain = 0;
-                for (int base = 0; base < np; base += kStage) {
-                    const int e = base + t;
-                    if (e < np && !pout[e]) {
-                        double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
-                        edge_info(e, info, &delta);
-                        V3 pc;
-                        error_at(e, T, err, &pc);
-                        const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
-                        J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
-                        J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
-                        J[0][5] = x * invz_2 * cam.fx;
-                        J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
-                        J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
-                        J[1][5] = y * invz_2 * cam.fy;
-                        if (pts[e].ur >= 0) {
-                            J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
-                            J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
-                        } else {
-#pragma unroll
-                            for (int d = 0; d < 6; d++) J[2][d] = 0;
-                        }
-                        stage_terms(J, err, info, delta, false);
-                    } else {
-                        stage_zero();
-                    }
-                    __syncthreads();
-                    if (chainer) chain_add(achain, &S.stage[0][ck], min(kStage, np - base));
-                    __syncthreads();
-                }
-                PROF_MARK(1);  // pass A point edges
-                // plane edges: numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205); the 13
-                // evaluations of a chunk's edges (12 perturbed poses exp(+-1e-9 e_d) * T, and T) run on
-                // 13 x chunk threads, then thread j stages the chunk's edge j
-                // after an accepted trial the errors at T are the ones pass B evaluated at that trial pose
-                // (kept in perrT when the plane edges fit one chunk): 12 evaluations per edge instead of 13
+                // ---- pass A: errors, robust chi2, quadratic form at T, chained in edge order.  Plane edges:
+                // numeric central differences, delta 1e-9 (base_binary_edge.hpp:130-205) -- the errors at the 12
+                // perturbed poses exp(+-1e-9 e_d) * T (and at T unless an accepted trial left them in perrT) are
+                // evaluated on nev lanes per edge, ps edges per compute wave and round, then staged by one lane
                 const bool haveT = tValid && nl <= kPlaneChunk;
-                const int nev = haveT ? 12 : 13;
-                for (int base = 0; base < nl; base += kPlaneChunk) {
-                    const int cnt = min(kPlaneChunk, nl - base);
-                    for (int w = t; w < cnt * nev; w += kThreads) {
-                        const int j = w / nev, q = w - j * nev, e = np + base + j;
-                        double err[3] = {0, 0, 0};
-                        if (!plout[e - np]) {
-                            const SE3 Tp = se3_mul(S.Eadd[q < 12 ? q : 0], T);
-                            const bool pt = q < 12;
-                            SE3 Tq;  // field-wise select: one inlined error evaluation for both cases
-                            Tq.r.w = pt ? Tp.r.w : T.r.w; Tq.r.x = pt ? Tp.r.x : T.r.x;
-                            Tq.r.y = pt ? Tp.r.y : T.r.y; Tq.r.z = pt ? Tp.r.z : T.r.z;
-                            Tq.t.x = pt ? Tp.t.x : T.t.x; Tq.t.y = pt ? Tp.t.y : T.t.y; Tq.t.z = pt ? Tp.t.z : T.t.z;
-                            error_at(e, Tq, err, nullptr);
-                        }
-                        S.perr[j][q][0] = err[0]; S.perr[j][q][1] = err[1]; S.perr[j][q][2] = err[2];
-                    }
-                    __syncthreads();
-                    if (t < cnt) {
-                        const int e = np + base + t;
-                        if (!plout[e - np]) {
-                            double info[3], delta, J[3][6];
+                const int nev = haveT ? 12 : 13, psA = 64 / nev;
+                const Schedule GA(np, nl, psA);
+                pass_begin();
+                if (chain_wave) {
+                    const double a = chain_pass<kStrideA, kRingA>(S, GA, ringA, kRed);
+                    if (lane < kRed) S.tot[lane] = a;
+                } else {
+                    for (int k = 0; k < GA.npr; k++) {
+                        const int e = kCompute * k + t;
+                        double row[kRed];
+#pragma unroll
+                        for (int v = 0; v < kRed; v++) row[v] = 0.0;
+                        if (e < np && !pout[e]) {
+                            double info[3], delta, err[3] = {0, 0, 0}, J[3][6];
                             edge_info(e, info, &delta);
-                            const double err[3] = {haveT ? S.perrT[t][0] : S.perr[t][12][0],
-                                                   haveT ? S.perrT[t][1] : S.perr[t][12][1],
-                                                   haveT ? S.perrT[t][2] : S.perr[t][12][2]};
+                            V3 pc;
+                            point_error_at(e, T, err, &pc);
+                            const double x = pc.x, y = pc.y, invz = 1.0 / pc.z, invz_2 = invz * invz;
+                            J[0][0] = x * y * invz_2 * cam.fx; J[0][1] = -(1 + (x * x * invz_2)) * cam.fx;
+                            J[0][2] = y * invz * cam.fx; J[0][3] = -invz * cam.fx; J[0][4] = 0;
+                            J[0][5] = x * invz_2 * cam.fx;
+                            J[1][0] = (1 + y * y * invz_2) * cam.fy; J[1][1] = -x * y * invz_2 * cam.fy;
+                            J[1][2] = -x * invz * cam.fy; J[1][3] = 0; J[1][4] = -invz * cam.fy;
+                            J[1][5] = y * invz_2 * cam.fy;
+                            if (pts[e].ur >= 0) {
+                                J[2][0] = J[0][0] - cam.bf * y * invz_2; J[2][1] = J[0][1] + cam.bf * x * invz_2;
+                                J[2][2] = J[0][2]; J[2][3] = J[0][3]; J[2][4] = 0; J[2][5] = J[0][5] - cam.bf * invz_2;
+                            } else {
+#pragma unroll
+                                for (int d = 0; d < 6; d++) J[2][d] = 0;
+                            }
+                            edge_terms(J, err, info, delta, robust, false, row);
+                        }
+                        int ea, eb;
+                        GA.share(k, wv, ea, eb);
+                        ring_wait(S, ea < eb ? eb - kRingA : 0);
+                        if (e < np) {
+                            double* dst = ringA + (e & (kRingA - 1)) * kStrideA;
+#pragma unroll
+                            for (int v = 0; v < kRed; v++) dst[v] = row[v];
+                        }
+                        lds_publish(&S.done[wv], k + 1);
+                    }
+                    PROF_MARK(1);  // pass A point edges (compute wave 0's view)
+                    for (int k = GA.npr; k < GA.nr; k++) {
+                        int ea, eb;
+                        GA.share(k, wv, ea, eb);
+                        const int i = lane / nev, q = lane - i * nev, j = ea - np + i;  // evaluation lanes
+                        if (i < psA && np + j < eb) {
+                            double err[3] = {0, 0, 0};
+                            if (!plout[j]) {
+                                const SE3 Tp = se3_mul(S.Eadd[q < 12 ? q : 0], T);
+                                const bool pt = q < 12;
+                                SE3 Tq;  // field-wise select: one inlined error evaluation for both cases
+                                Tq.r.w = pt ? Tp.r.w : T.r.w; Tq.r.x = pt ? Tp.r.x : T.r.x;
+                                Tq.r.y = pt ? Tp.r.y : T.r.y; Tq.r.z = pt ? Tp.r.z : T.r.z;
+                                Tq.t.x = pt ? Tp.t.x : T.t.x; Tq.t.y = pt ? Tp.t.y : T.t.y;
+                                Tq.t.z = pt ? Tp.t.z : T.t.z;
+                                plane_error_at(np + j, Tq, err);
+                            }
+                            S.perr[wv][i][q][0] = err[0]; S.perr[wv][i][q][1] = err[1]; S.perr[wv][i][q][2] = err[2];
+                        }
+                        wave_sync();
+                        double row[kRed];
+#pragma unroll
+                        for (int v = 0; v < kRed; v++) row[v] = 0.0;
+                        const int js = ea - np + lane;  // staging lane: plane edge js
+                        if (lane < psA && np + js < eb && !plout[js]) {
+                            double info[3], delta, J[3][6];
+                            edge_info(np + js, info, &delta);
+                            const double err[3] = {haveT ? S.perrT[js][0] : S.perr[wv][lane][12][0],
+                                                   haveT ? S.perrT[js][1] : S.perr[wv][lane][12][1],
+                                                   haveT ? S.perrT[js][2] : S.perr[wv][lane][12][2]};
                             const double scalar = 1.0 / (2 * 1e-9);
 #pragma unroll
                             for (int d = 0; d < 6; d++)
 #pragma unroll
                                 for (int r = 0; r < 3; r++)
-                                    J[r][d] = scalar * (S.perr[t][2 * d][r] - S.perr[t][2 * d + 1][r]);
-                            stage_terms(J, err, info, delta, true);
-                        } else {
-                            stage_zero();
+                                    J[r][d] = scalar * (S.perr[wv][lane][2 * d][r] - S.perr[wv][lane][2 * d + 1][r]);
+                            edge_terms(J, err, info, delta, robust, true, row);
                         }
+                        ring_wait(S, ea < eb ? eb - kRingA : 0);
+                        if (lane < psA && np + js < eb) {
+                            double* dst = ringA + ((np + js) & (kRingA - 1)) * kStrideA;
+#pragma unroll
+                            for (int v = 0; v < kRed; v++) dst[v] = row[v];
+                        }
+                        lds_publish(&S.done[wv], k + 1);
+                        wave_sync();  // perr[wv] is rewritten by the next round
                     }
-                    __syncthreads();
-                    if (chainer) chain_add(achain, &S.stage[0][ck], cnt);
-                    __syncthreads();  // stage / perr reuse
                 }
-                PROF_MARK(2);  // pass A plane edges
-                if (chainer) S.tot[ck] = achain;
                 __syncthreads();
+                PROF_MARK(2);  // pass A plane edges + the chain's tail
                 double currentChi = S.tot[0];
                 const double iniChi = currentChi;
                 // H and b wait in LDS for the trial passes: kept in registers they would stay live across pass B
@@ -548,75 +709,70 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
                     }
                     PROF_MARK(4);  // solves + exp + broadcast
                     PROF_COUNT(10);
-                    // robust chi2 of every active edge at each trial pose, chained in edge order by lane 0 of
-                    // wave q.  A plane error costs far more than a point error, so the (plane edge, trial)
-                    // pairs are evaluated one per thread first (into perr's space).
-                    double* prho = &S.perr[0][0][0];
-                    constexpr int kPairPlanes = kPlaneChunk * 13 * 3 / kSpec;  // plane edges per prho round
-                    auto pairs = [&](int pb) __attribute__((always_inline)) {
-                        const int cnt = min(kPairPlanes, nl - pb);
-                        for (int w = t; w < cnt * kSpec; w += kThreads) {
-                            const int j = pb + w / kSpec, q = w % kSpec;
+                    // ---- pass B: robust chi2 of every active edge at each trial pose, one ring row of kSpec
+                    // values per edge, chained in edge order by lanes 0 .. kSpec-1 of the chain wave.  Plane edges:
+                    // one (edge, trial) pair per lane, 64 / kSpec edges per compute wave and round
+                    constexpr int psB = 64 / kSpec;
+                    const Schedule GB(np, nl, psB);
+                    pass_begin();
+                    if (chain_wave) {
+                        const double a = chain_pass<RB::kStride, RB::kRows>(S, GB, ringB, kSpec);
+                        if (lane < kSpec) S.tot[lane] = a;
+                    } else {
+                        for (int k = 0; k < GB.npr; k++) {
+                            const int e = kCompute * k + t;
+                            double r[kSpec];
+#pragma unroll
+                            for (int q = 0; q < kSpec; q++) r[q] = 0;
+                            if (e < np && !pout[e]) {
+                                double info[3], delta;
+                                edge_info(e, info, &delta);
+#pragma unroll
+                                for (int q = 0; q < kSpec; q++) {
+                                    double err[3] = {0, 0, 0}, rho1;
+                                    point_error_at(e, Tq[q], err, nullptr);
+                                    huber(chi2_of(err, info), delta, robust, &r[q], &rho1);
+                                }
+                            }
+                            int ea, eb;
+                            GB.share(k, wv, ea, eb);
+                            ring_wait(S, ea < eb ? eb - RB::kRows : 0);
+                            if (e < np) {
+                                double* dst = ringB + (e & (RB::kRows - 1)) * RB::kStride;
+#pragma unroll
+                                for (int q = 0; q < kSpec; q++) dst[q] = r[q];
+                            }
+                            lds_publish(&S.done[wv], k + 1);
+                        }
+                        for (int k = GB.npr; k < GB.nr; k++) {
+                            int ea, eb;
+                            GB.share(k, wv, ea, eb);
+                            const int i = lane / kSpec, q = lane % kSpec, j = ea - np + i;
                             double r0 = 0;
-                            if (!plout[j]) {
+                            if (np + j < eb && !plout[j]) {
                                 double info[3], delta, err[3] = {0, 0, 0}, rho1;
                                 edge_info(np + j, info, &delta);
                                 SE3 Tv = Tq[0];  // uniform poses: select by q without dynamic indexing
 #pragma unroll
-                                for (int k = 1; k < kSpec; k++)
-                                    if (q == k) Tv = Tq[k];
-                                error_at(np + j, Tv, err, nullptr);
+                                for (int u = 1; u < kSpec; u++)
+                                    if (q == u) Tv = Tq[u];
+                                plane_error_at(np + j, Tv, err);
                                 huber(chi2_of(err, info), delta, robust, &r0, &rho1);
                                 if (nl <= kPlaneChunk) {
                                     S.perrB[j][q][0] = err[0]; S.perrB[j][q][1] = err[1]; S.perrB[j][q][2] = err[2];
                                 }
                             }
-                            prho[w] = r0;
-                        }
-                    };
-                    pairs(0);
-                    double cq = 0;
-                    const bool qchainer = lane == 0 && (t >> 6) < kSpec;
-                    for (int base = 0; base < np; base += kStage) {
-                        const int e = base + t;
-                        double r[kSpec];
-#pragma unroll
-                        for (int q = 0; q < kSpec; q++) r[q] = 0;
-                        if (e < np && !pout[e]) {
-                            double info[3], delta;
-                            edge_info(e, info, &delta);
-#pragma unroll
-                            for (int q = 0; q < kSpec; q++) {
-                                double err[3] = {0, 0, 0}, rho1;
-                                error_at(e, Tq[q], err, nullptr);
-                                huber(chi2_of(err, info), delta, robust, &r[q], &rho1);
-                            }
-                        }
-#pragma unroll
-                        for (int q = 0; q < kSpec; q++) S.stage[t][q] = r[q];
-                        __syncthreads();
-                        if (qchainer) chain_add(cq, &S.stage[0][t >> 6], min(kStage, np - base));
-                        __syncthreads();
-                    }
-                    for (int pb = 0; pb < nl; pb += kPairPlanes) {
-                        if (pb > 0) pairs(pb);  // prho's previous round was chained (the loop's last barrier)
-                        __syncthreads();
-                        const int cntp = min(kPairPlanes, nl - pb);
-                        for (int sb = 0; sb < cntp; sb += kStage) {
-#pragma unroll
-                            for (int q = 0; q < kSpec; q++) S.stage[t][q] = sb + t < cntp ? prho[(sb + t) * kSpec + q] : 0.0;
-                            __syncthreads();
-                            if (qchainer) chain_add(cq, &S.stage[0][t >> 6], min(kStage, cntp - sb));
-                            __syncthreads();
+                            ring_wait(S, ea < eb ? eb - RB::kRows : 0);
+                            if (np + j < eb) ringB[((np + j) & (RB::kRows - 1)) * RB::kStride + q] = r0;
+                            lds_publish(&S.done[wv], k + 1);
                         }
                     }
-                    if (qchainer) S.tot[t >> 6] = cq;
                     PROF_MARK(5);  // pass B (trial chi2)
                     __syncthreads();
                     double c[kSpec];
 #pragma unroll
                     for (int q = 0; q < kSpec; q++) c[q] = S.tot[q];
-                // the reference's accept / reject sequence over the evaluated trials
+                    // the reference's accept / reject sequence over the evaluated trials
                     int acc = -1, lastq = 0;
 #pragma unroll
                     for (int q = 0; q < kSpec; q++) {
@@ -647,7 +803,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
 #pragma unroll
                         for (int q = 1; q < kSpec; q++)
                             if (q == lastq) tl = Tq[q];
-                        S.tlast[t >> 6] = tl;
+                        S.tlast[wv] = tl;
                     }
                     tValid = tValid || acc >= 0;
                     if (acc >= 0 && t < nl && nl <= kPlaneChunk) {  // thread t reads perrT[t] in the next pass A
@@ -673,10 +829,8 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         // ---- relabel (:925-1140): active edges keep the errors of the last trial pose, outliers are
         // recomputed at the optimized pose
         // (with no active edge every edge takes T and tlast is not read)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const SE3 Tlast = S.tlast[t >> 6];
+        wave_sync();
+        const SE3 Tlast = S.tlast[wv];
         double bad = 0;
         for (int e = t; e < ne; e += kThreads) {
             double info[3], delta, err[3] = {0, 0, 0};
@@ -686,7 +840,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
             Te.r.w = was_out ? T.r.w : Tlast.r.w; Te.r.x = was_out ? T.r.x : Tlast.r.x;
             Te.r.y = was_out ? T.r.y : Tlast.r.y; Te.r.z = was_out ? T.r.z : Tlast.r.z;
             Te.t.x = was_out ? T.t.x : Tlast.t.x; Te.t.y = was_out ? T.t.y : Tlast.t.y; Te.t.z = was_out ? T.t.z : Tlast.t.z;
-            error_at(e, Te, err, nullptr);
+            error_at(e, Te, err);
             const float chi2 = (float)chi2_of(err, info);
             bool bd;
             if (e < np) bd = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
@@ -709,7 +863,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_POSE_MINW) void pose_kernel(const 
         res->Tcw[3] = (float)T.t.x; res->Tcw[7] = (float)T.t.y; res->Tcw[11] = (float)T.t.z;
         res->Tcw[12] = 0.f; res->Tcw[13] = 0.f; res->Tcw[14] = 0.f; res->Tcw[15] = 1.f;
         res->n_inliers = ne - nBad;
-        res->lm_iterations = total_its;
+        res->lm_iterations = S.stall ? -1 : total_its;  // a bounded wait gave up: the result is not valid
     }
 #ifdef SPSLAM_POSE_PROF
     PROF_MARK(9);  // outputs
