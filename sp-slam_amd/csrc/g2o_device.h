@@ -217,11 +217,56 @@ __device__ __forceinline__ E3 plane_error3(int kind, const SE3& T, const P4& wor
     return E3{e[0], e[1], e[2]};
 }
 
-// The same, out of line: one copy of the ~1.5K-instruction evaluation (4 atan2, 2 sincos, 3 normalisations)
-// per kernel instead of one per call site and per inlined branch.  Arguments and result travel by value in
-// VGPRs (no stack); the call costs ~100 cycles against ~2K of evaluation.
-__device__ __noinline__ E3 plane_error_call(int kind, SE3 T, P4 world, P4 meas) {
-    return plane_error3(kind, T, world, meas);
+// ---- the same error on a pair of adjacent lanes (2k, 2k + 1: half = lane & 1) -----------------------------
+// A plane-edge error is ~2,300 fp64 instructions, 80 % of them the three pairs of correctly rounded functions
+// (azimuth / elevation of the reference normal, the two half-angle sincos, azimuth / elevation of the rotated
+// measurement), and one wave issues them one after the other.  Here each lane of the pair computes one member
+// of every pair and the two halves are exchanged (DPP within the quad): about 1,000 instructions per lane, both
+// lanes end with the whole error.  Same operations on the same operands: bit-identical to plane_error.  Both
+// lanes of a pair must evaluate the same (kind, T, world, meas) and be active together.
+__device__ __forceinline__ double pair_xchg(double v) {
+    // quad_perm [1, 0, 3, 2]: every lane reads its pair partner
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0xB1, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// this lane's member of (atan2(v.y, v.x), atan2(v.z, |v.xy|)) -- azimuth on the even lane, elevation on the odd
+// -- and the partner's, as (azimuth, elevation)
+__device__ __forceinline__ void az_el_pair(V3 v, bool half, double* az, double* el) {
+    const double mine = lm::atan2_(half ? v.z : v.y, half ? sqrt(v.x * v.x + v.y * v.y) : v.x);
+    const double other = pair_xchg(mine);
+    *az = half ? other : mine;
+    *el = half ? mine : other;
+}
+__device__ __forceinline__ E3 plane_error_pair(int kind, const SE3& T, const P4& world, const P4& meas, bool half) {
+    const M3 R = q_to_rot(T.r);
+    const V3 n2 = mv(R, V3{world.c[0], world.c[1], world.c[2]});
+    double v[4] = {n2.x, n2.y, n2.z, world.c[3] - dot(T.t, n2)};
+    if (v[3] < 0.0)
+        for (int i = 0; i < 4; i++) v[i] = -v[i];
+    p_normalize(v);
+    const V3 ln{v[0], v[1], v[2]}, mn{meas.c[0], meas.c[1], meas.c[2]};
+    V3 ref = ln;
+    if (kind == 1) {
+        if (dot(mn, ln) < 0) ref = -1.0 * ln;
+    } else if (kind == 2) {
+        const V3 a = cross(ln, mn);
+        ref = aa_apply_half_pi((1.0 / sqrt(dot(a, a))) * a, ln);
+    }
+    // p_rotation(ref): sincos of 0.5 * az on the even lane, of 0.5 * (-el) on the odd one
+    double az, el;
+    az_el_pair(ref, half, &az, &el);
+    double s, c;
+    lm::sincos_(half ? 0.5 * (-el) : 0.5 * az, &s, &c);
+    const double so = pair_xchg(s), co = pair_xchg(c);
+    const double sa = half ? so : s, ca = half ? co : c, se = half ? s : so, ce = half ? c : co;
+    const Q qa{ca, 0.0 * sa, 0.0 * sa, 1.0 * sa};
+    const Q qe{ce, 0.0 * se, 1.0 * se, 0.0 * se};
+    const V3 n = mtv(q_to_rot(q_mul(qa, qe)), mn);
+    E3 e;
+    az_el_pair(n, half, &e.e0, &e.e1);
+    e.e2 = kind == 0 ? (-v[3]) - (-meas.c[3]) : 0.0;
+    return e;
 }
 
 // Plane3D::oplus (g2oAddition/Plane3D.h:72-85)

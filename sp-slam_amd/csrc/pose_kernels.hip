@@ -37,7 +37,7 @@
 // Phase profile (diagnostic build only: make prof -> libspslam_gpu_prof.so).  Thread 0 of every problem
 // accumulates wall_clock64 ticks (100 MHz) per phase; spslam_pose_prof_read returns the grid totals.
 #ifdef SPSLAM_POSE_PROF
-__device__ unsigned long long g_pose_prof[16];
+__device__ unsigned long long g_pose_prof[24];  // 0-9 phases (thread 0), 10-11 counts, 12-15 the chain wave, 16-19 sub-phases
 #define PROF_MARK(k)                                   \
     do {                                               \
         if (t == 0) {                                  \
@@ -181,6 +181,7 @@ constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
 // the same LDS as a ring of kSpec-value rows (trial robust chi2).
 constexpr int kRingA = 256;
 constexpr int kStrideA = kRed + 1;
+constexpr int kRingPad = 24;       // spare rows past the ring end: chain_seg loads up to 23 rows past a segment
 constexpr int kSpinCap = 1 << 20;  // bound of every wait (s_sleep 1 each: ~30 ms); never reached in a correct run
 
 template <int kSpec>
@@ -195,7 +196,7 @@ struct RingB {
 
 template <int kSpec>
 struct Shared {
-    double ring[kRingA * kStrideA];   // pass A: [kRingA][kStrideA]; pass B: [RingB::kRows][kSpec + 1]
+    double ring[(kRingA + kRingPad) * kStrideA];  // pass A: [kRingA][kStrideA]; pass B: [RingB::kRows][kSpec + 1]
     double tot[kRed];                 // the chained totals, for every thread
     double red[2][kWaves][1];         // wave totals of the workgroup sums, double-buffered
     double perr[kComputeWaves][5][13][3];  // per compute wave: plane errors at the 12 perturbed poses and at T
@@ -204,6 +205,7 @@ struct Shared {
     double hb[kRed];                  // the iteration's H (lower, 21) and b (6), slot 0 unused
     SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)
     SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
+    P4 pw[kPlaneChunk], pm[kPlaneChunk];  // plane edges' world / measured planes, normalized (nl <= kPlaneChunk)
     int done[kComputeWaves];          // rounds each compute wave has staged in the current pass
     int consumed;                     // rows the chain wave has added in the current pass
     int stall;                        // a wait hit kSpinCap (reported through lm_iterations)
@@ -243,17 +245,18 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
 }
 
 // acc += rows start .. start + cnt - 1 of a ring column (slot = row & (kRows - 1)), one after the other: the
-// reference's order.  Three register groups of 8 rotate: while one group's dependent adds run, the other two
-// groups' loads are in flight, and a group is refilled right after its adds (no register moves: a FIFO rotated
-// with moves makes the compiler wait for every outstanding load once per group -- a full LDS round trip per 8
-// adds; the scheduling barriers keep each refill ahead of the next group's adds).  Rows past cnt are loaded and
-// never added.
-template <int kStride, int kRows>
-__device__ __forceinline__ void chain_ring(double& acc, const double* col, int start, int cnt) {
-    static_assert((kRows & (kRows - 1)) == 0, "ring wrap");
+// reference's order.  The rows are added in contiguous segments (the ring wraps at most once), so every group of 8
+// loads is one base address plus immediate offsets.  Three register groups of 8 rotate: while one group's
+// dependent adds run, the other two groups' loads are in flight, and a group is refilled right after its adds
+// (no register moves: a FIFO rotated with moves makes the compiler wait for every outstanding load once per group
+// -- a full LDS round trip per 8 adds; the scheduling barriers keep each refill ahead of the next group's adds).
+// Rows past a segment's end are loaded and never added (the ring carries kRingPad spare rows for them).
+template <int kStride>
+__device__ __forceinline__ void chain_seg(double& acc, const double* p, int cnt) {
     auto ld = [&](double (&v)[8], int i) __attribute__((always_inline)) {
+        const double* q = p + i * kStride;
 #pragma unroll
-        for (int k = 0; k < 8; k++) v[k] = col[((start + i + k) & (kRows - 1)) * kStride];
+        for (int k = 0; k < 8; k++) v[k] = q[k * kStride];
     };
     auto add = [&](const double (&v)[8], int n) __attribute__((always_inline)) {
 #pragma unroll
@@ -280,6 +283,13 @@ __device__ __forceinline__ void chain_ring(double& acc, const double* col, int s
     add(a, r);
     add(b, r - 8);
     add(c, r - 16);
+}
+template <int kStride, int kRows>
+__device__ __forceinline__ void chain_ring(double& acc, const double* col, int start, int cnt) {
+    static_assert((kRows & (kRows - 1)) == 0, "ring wrap");
+    const int s0 = start & (kRows - 1), n0 = min(cnt, kRows - s0);
+    chain_seg<kStride>(acc, col + s0 * kStride, n0);
+    if (cnt > n0) chain_seg<kStride>(acc, col, cnt - n0);
 }
 
 // The staging schedule of one pass, known to every wave: point rounds of 256 edges (64 per compute wave), then
@@ -343,23 +353,36 @@ __device__ __forceinline__ int available(Sh& S, const Schedule& G) {
 
 // the chain wave: add every staged row of the pass in edge order, column = this lane's value (lanes past nval
 // read the padding column), and hand out the ring slots as rows are added
+// (diagnostic build: prof[0] += ticks spent adding, prof[1] += ticks spent waiting for rows)
 template <int kStride, int kRows, class Sh>
-__device__ __forceinline__ double chain_pass(Sh& S, const Schedule& G, const double* ring, int nval) {
+__device__ __forceinline__ double chain_pass(Sh& S, const Schedule& G, const double* ring, int nval,
+                                             unsigned long long* prof) {
     const int lane = threadIdx.x & 63;
     const double* col = ring + (lane < nval ? lane : kStride - 1);
     double acc = 0;
     int c = 0;
     while (c < G.ne) {
+#ifdef SPSLAM_POSE_PROF
+        const unsigned long long w0 = wall_clock64();
+#endif
         int a = available(S, G);
         for (int spin = 0; a <= c; spin++) {
             if (spin >= kSpinCap) { S.stall = 1; a = G.ne; break; }
             __builtin_amdgcn_s_sleep(1);
             a = available(S, G);
         }
+#ifdef SPSLAM_POSE_PROF
+        const unsigned long long w1 = wall_clock64();
+        prof[1] += w1 - w0;
+#endif
         chain_ring<kStride, kRows>(acc, col, c, a - c);
         c = a;
         lds_publish(&S.consumed, c);
+#ifdef SPSLAM_POSE_PROF
+        prof[0] += wall_clock64() - w1;
+#endif
     }
+    (void)prof;
     return acc;
 }
 
@@ -445,8 +468,14 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const bool chain_wave = wv == kChainWave;
 #ifdef SPSLAM_POSE_PROF
-    unsigned long long prof_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long prof_acc[24] = {};
     unsigned long long prof_t = wall_clock64();
+#endif
+    unsigned long long* chain_prof_a = nullptr;  // the chain wave's ticks (diagnostic build only)
+    unsigned long long* chain_prof_b = nullptr;
+#ifdef SPSLAM_POSE_PROF
+    chain_prof_a = prof_acc + 12;
+    chain_prof_b = prof_acc + 14;
 #endif
     const spslam_pose_problem P = probs[blockIdx.x];
     const spslam_point_obs* pts = pts_all + P.point_offset;
@@ -494,7 +523,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
             else { info[0] = info[1] = kind == 1 ? K.par_info : K.ver_info; info[2] = 0; *delta = K.delta_vp; }
         }
     };
-    auto plane_of = [&](int e, P4& w, P4& m) __attribute__((always_inline)) {
+    auto plane_of_global = [&](int e, P4& w, P4& m) __attribute__((always_inline)) {
         const spslam_plane_obs& o = pls[e - np];
         for (int k = 0; k < 4; k++) { w.c[k] = o.world[k]; m.c[k] = o.meas[k]; }
         if (o.world[3] < 0.0f) for (int k = 0; k < 4; k++) w.c[k] = -w.c[k];  // Converter::toPlane3D
@@ -502,17 +531,10 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         p_normalize(w.c);
         p_normalize(m.c);
     };
-    auto error_at = [&](int e, const SE3& T, double* err) __attribute__((always_inline)) {
-        E3 r;
-        if (e < np) {
-            V3 p;
-            r = point_error(pts[e], T, cam, p);
-        } else {
-            P4 w, m;
-            plane_of(e, w, m);
-            r = plane_error_call(pls[e - np].kind, T, w, m);
-        }
-        err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
+    const bool plane_cache = nl <= kPlaneChunk;  // the normalized planes wait in LDS (every evaluation reads them)
+    auto plane_of = [&](int e, P4& w, P4& m) __attribute__((always_inline)) {
+        if (plane_cache) { w = S.pw[e - np]; m = S.pm[e - np]; }
+        else plane_of_global(e, w, m);
     };
     // the same for an edge known to be a point (plane) edge: the loops that only visit one kind call these, so
     // the other kind's evaluation is not compiled into them as a dead branch
@@ -525,7 +547,14 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     auto plane_error_at = [&](int e, const SE3& T, double* err) __attribute__((always_inline)) {
         P4 w, m;
         plane_of(e, w, m);
-        const E3 r = plane_error_call(pls[e - np].kind, T, w, m);
+        const E3 r = plane_error3(pls[e - np].kind, T, w, m);
+        err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
+    };
+    // the same on the lane pair (lane & ~1, lane | 1): both lanes pass the same edge and pose
+    auto plane_error_pair_at = [&](int e, const SE3& T, double* err) __attribute__((always_inline)) {
+        P4 w, m;
+        plane_of(e, w, m);
+        const E3 r = plane_error_pair(pls[e - np].kind, T, w, m, (lane & 1) != 0);
         err[0] = r.e0; err[1] = r.e1; err[2] = r.e2;
     };
     auto chi2_of = [](const double* err, const double* info) __attribute__((always_inline)) {
@@ -542,6 +571,13 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     };
     double* ringA = S.ring;
     double* ringB = S.ring;
+    if (plane_cache && t < nl) {
+        P4 w, m;
+        plane_of_global(np + t, w, m);
+        S.pw[t] = w;
+        S.pm[t] = m;
+    }
+    __syncthreads();
 
     int buf = 0;
     bool robust = true;
@@ -568,7 +604,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                 const Schedule GA(np, nl, psA);
                 pass_begin();
                 if (chain_wave) {
-                    const double a = chain_pass<kStrideA, kRingA>(S, GA, ringA, kRed);
+                    const double a = chain_pass<kStrideA, kRingA>(S, GA, ringA, kRed, chain_prof_a);
                     if (lane < kRed) S.tot[lane] = a;
                 } else {
                     for (int k = 0; k < GA.npr; k++) {
@@ -627,6 +663,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                             S.perr[wv][i][q][0] = err[0]; S.perr[wv][i][q][1] = err[1]; S.perr[wv][i][q][2] = err[2];
                         }
                         wave_sync();
+                        PROF_MARK(16);  // pass A plane evaluations
                         double row[kRed];
 #pragma unroll
                         for (int v = 0; v < kRed; v++) row[v] = 0.0;
@@ -653,6 +690,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                         }
                         lds_publish(&S.done[wv], k + 1);
                         wave_sync();  // perr[wv] is rewritten by the next round
+                        PROF_MARK(17);  // pass A plane staging
                     }
                 }
                 __syncthreads();
@@ -711,12 +749,13 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                     PROF_COUNT(10);
                     // ---- pass B: robust chi2 of every active edge at each trial pose, one ring row of kSpec
                     // values per edge, chained in edge order by lanes 0 .. kSpec-1 of the chain wave.  Plane edges:
-                    // one (edge, trial) pair per lane, 64 / kSpec edges per compute wave and round
-                    constexpr int psB = 64 / kSpec;
+                    // one (edge, trial) pair per lane pair (plane_error_pair), 32 / kSpec edges per compute wave
+                    // and round
+                    constexpr int psB = 32 / kSpec;
                     const Schedule GB(np, nl, psB);
                     pass_begin();
                     if (chain_wave) {
-                        const double a = chain_pass<RB::kStride, RB::kRows>(S, GB, ringB, kSpec);
+                        const double a = chain_pass<RB::kStride, RB::kRows>(S, GB, ringB, kSpec, chain_prof_b);
                         if (lane < kSpec) S.tot[lane] = a;
                     } else {
                         for (int k = 0; k < GB.npr; k++) {
@@ -744,10 +783,12 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                             }
                             lds_publish(&S.done[wv], k + 1);
                         }
+                        PROF_MARK(18);  // pass B point rounds
                         for (int k = GB.npr; k < GB.nr; k++) {
                             int ea, eb;
                             GB.share(k, wv, ea, eb);
-                            const int i = lane / kSpec, q = lane % kSpec, j = ea - np + i;
+                            const int pr = lane >> 1, i = pr / kSpec, q = pr % kSpec, j = ea - np + i;
+                            const bool lead = (lane & 1) == 0;
                             double r0 = 0;
                             if (np + j < eb && !plout[j]) {
                                 double info[3], delta, err[3] = {0, 0, 0}, rho1;
@@ -756,16 +797,17 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
 #pragma unroll
                                 for (int u = 1; u < kSpec; u++)
                                     if (q == u) Tv = Tq[u];
-                                plane_error_at(np + j, Tv, err);
+                                plane_error_pair_at(np + j, Tv, err);
                                 huber(chi2_of(err, info), delta, robust, &r0, &rho1);
-                                if (nl <= kPlaneChunk) {
+                                if (lead && nl <= kPlaneChunk) {
                                     S.perrB[j][q][0] = err[0]; S.perrB[j][q][1] = err[1]; S.perrB[j][q][2] = err[2];
                                 }
                             }
                             ring_wait(S, ea < eb ? eb - RB::kRows : 0);
-                            if (np + j < eb) ringB[((np + j) & (RB::kRows - 1)) * RB::kStride + q] = r0;
+                            if (lead && np + j < eb) ringB[((np + j) & (RB::kRows - 1)) * RB::kStride + q] = r0;
                             lds_publish(&S.done[wv], k + 1);
                         }
+                        PROF_MARK(19);  // pass B plane rounds
                     }
                     PROF_MARK(5);  // pass B (trial chi2)
                     __syncthreads();
@@ -832,22 +874,32 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         wave_sync();
         const SE3 Tlast = S.tlast[wv];
         double bad = 0;
-        for (int e = t; e < ne; e += kThreads) {
-            double info[3], delta, err[3] = {0, 0, 0};
-            edge_info(e, info, &delta);
-            const bool was_out = is_outlier(e);
+        auto relabel_pose = [&](bool was_out) __attribute__((always_inline)) {
             SE3 Te;  // field-wise select (a selected reference would put both poses in scratch memory)
             Te.r.w = was_out ? T.r.w : Tlast.r.w; Te.r.x = was_out ? T.r.x : Tlast.r.x;
             Te.r.y = was_out ? T.r.y : Tlast.r.y; Te.r.z = was_out ? T.r.z : Tlast.r.z;
             Te.t.x = was_out ? T.t.x : Tlast.t.x; Te.t.y = was_out ? T.t.y : Tlast.t.y; Te.t.z = was_out ? T.t.z : Tlast.t.z;
-            error_at(e, Te, err);
+            return Te;
+        };
+        for (int e = t; e < np; e += kThreads) {
+            double info[3], delta, err[3] = {0, 0, 0};
+            edge_info(e, info, &delta);
+            point_error_at(e, relabel_pose(pout[e] != 0), err, nullptr);
             const float chi2 = (float)chi2_of(err, info);
-            bool bd;
-            if (e < np) bd = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
-            else bd = pls[e - np].kind == 0 ? (double)chi2 > K.plane_chi : (double)chi2 > K.vp_chi;
+            const bool bd = pts[e].ur < 0 ? chi2 > 5.991f : chi2 > 7.815f;
             bad += bd ? 1.0 : 0.0;
-            if (e < np) pout[e] = bd;
-            else plout[e - np] = bd;
+            pout[e] = bd;
+        }
+        for (int j = t >> 1; j < nl; j += kThreads / 2) {  // plane edges on lane pairs
+            double info[3], delta, err[3] = {0, 0, 0};
+            edge_info(np + j, info, &delta);
+            plane_error_pair_at(np + j, relabel_pose(plout[j] != 0), err);
+            const float chi2 = (float)chi2_of(err, info);
+            const bool bd = pls[j].kind == 0 ? (double)chi2 > K.plane_chi : (double)chi2 > K.vp_chi;
+            if ((lane & 1) == 0) {
+                bad += bd ? 1.0 : 0.0;
+                plout[j] = bd;
+            }
         }
         double cb[1] = {bad};
         wg_sum(cb, S, buf);  // small integers: exact
@@ -867,8 +919,12 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     }
 #ifdef SPSLAM_POSE_PROF
     PROF_MARK(9);  // outputs
-    if (t == 0)
+    if (t == 0) {
         for (int k = 0; k < 12; k++) atomicAdd(&g_pose_prof[k], prof_acc[k]);
+        for (int k = 16; k < 20; k++) atomicAdd(&g_pose_prof[k], prof_acc[k]);
+    }
+    if (t == kCompute)
+        for (int k = 12; k < 16; k++) atomicAdd(&g_pose_prof[k], prof_acc[k]);
 #endif
 }
 
@@ -927,11 +983,11 @@ hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_poi
 }  // namespace spslam
 
 #ifdef SPSLAM_POSE_PROF
-// Diagnostic build only: the accumulated phase ticks / counters (12 u64), optionally reset.
+// Diagnostic build only: the accumulated phase ticks / counters (24 u64), optionally reset.
 extern "C" int spslam_pose_prof_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pose_prof), 12 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pose_prof), 24 * sizeof(unsigned long long)) != hipSuccess) return -1;
     if (reset) {
-        static const unsigned long long z[16] = {};
+        static const unsigned long long z[24] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_pose_prof), z, sizeof z) != hipSuccess) return -1;
     }
     return 0;
