@@ -58,6 +58,26 @@ WORKLOADS = {
     "c5": "C5: synthetic 1280x960 RGB-D; ORB nFeatures=4000 + planes + supposed planes + 2x PoseOptimization",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# PoseOptimization's serial floor: g2o sums every value edge by edge (sparse_optimizer.cpp:100-114,
+# block_solver.hpp:529-545), so each edge pass is a chain of one dependent fp64 add per edge.  One chain row (LDS
+# read + dependent v_add_f64, 28 values side by side on one wave) measured 13.3 cycles on gfx950
+# (tools/pose_micro.hip, profiles/r03/pose_micro.txt); clock: the 2.4 GHz nominal.
+CHAIN_CYCLES_PER_ROW = 13.3
+CLOCK_HZ = 2.4e9
+
+
+def pose_chain_floor(P1, P2, r1, r2):
+    """Per launch, the ordered-sum chain floor of the PoseOptimization kernel (ms): each problem chains its
+    n_points + n_planes rows once per LM iteration (the quadratic form) and once per trial pass (the trial
+    chi2); the problems of a launch run side by side (one CU each), so a launch lasts at least as long as its
+    longest chain.  Mean over the two graphs."""
+    import numpy as np
+    out = []
+    for P, r in ((P1, r1), (P2, r2)):
+        rows = (P["n_points"] + P["n_planes"]).astype(np.float64)
+        passes = r["lm_iterations"].astype(np.float64) + r["trial_passes"].astype(np.float64)
+        out.append(float((rows * passes).max()) * CHAIN_CYCLES_PER_ROW / CLOCK_HZ * 1e3)
+    return float(np.mean(out))
 
 
 def level_sizes(w, h, nlevels=8, scale=1.2):
@@ -583,6 +603,17 @@ def main():
         "cpu_baseline": None,
         "build": build,
     }
+    if dom == "pose_kernel":
+        # the bound that limits it: not HBM (a few MB per launch) but its ordered fp64 chains and the fp64 issue
+        # of the plane-edge evaluations
+        floor = pose_chain_floor(P1, P2, res["pose1"], res["pose2"])
+        result["roofline"]["latency_model"] = {
+            "model": "ordered fp64 sums (g2o edge order): per problem (LM iterations + trial passes) x edges chain "
+                     f"rows at {CHAIN_CYCLES_PER_ROW} cycles, longest problem of the launch, {CLOCK_HZ / 1e9} GHz",
+            "chain_floor_ms_per_launch": floor, "avg_launch_ms": avg_launch_s * 1e3,
+            "frac": floor / max(avg_launch_s * 1e3, 1e-9),
+            "mean_lm_iterations": float((res["pose1"]["lm_iterations"].mean() + res["pose2"]["lm_iterations"].mean()) / 2),
+            "mean_trial_passes": float((res["pose1"]["trial_passes"].mean() + res["pose2"]["trial_passes"].mean()) / 2)}
     cpu_poses = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], cpu_poses = cpu_baseline(hp, timed=args.cpu_frames or (300 if hp.W * hp.H <= 640 * 480 else 100))

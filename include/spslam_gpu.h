@@ -175,7 +175,8 @@ typedef struct spslam_pose_result {
     float Tcw[16];      /* optimized pose (unchanged input if n_inliers == 0 by the <3 rule) */
     int32_t n_inliers;  /* PoseOptimization return value */
     int32_t lm_iterations;  /* total LM iterations run (diagnostic) */
-    int32_t pad[2];
+    int32_t trial_passes;   /* edge passes at trial poses (damping trials are evaluated 4 per pass; diagnostic) */
+    int32_t trials;         /* damping trials the reference evaluated (computeActiveErrors calls; diagnostic) */
 } spslam_pose_result;
 
 /* Drop-in for Optimizer::PoseOptimization(Frame*) on host buffers, one frame.

@@ -622,8 +622,9 @@ __global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, 
 }
 
 // plane / parallel / vertical edges: central differences (base_binary_edge.hpp:130-205), one wave per edge.
-// Lane q < 6 evaluates the error at the plane perturbed by +-1e-9 along coordinate q >> 1 (Plane3D::oplus),
-// lane 6 <= q < 18 at the pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; the differences are gathered with
+// Evaluation q < 6 is the error at the plane perturbed by +-1e-9 along coordinate q >> 1 (Plane3D::oplus),
+// 6 <= q < 18 at the pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; evaluation q runs on the lane pair (2q, 2q + 1)
+// (plane_error_pair: each lane one member of every atan2 / sincos pair), the differences are gathered with
 // shuffles (the reference's per-coordinate expression) and lane 0 stores the terms.
 __global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w, LbaConsts C) {
     const int2 task = w.plane_tasks[blockIdx.x];
@@ -641,34 +642,36 @@ __global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w,
     const P4 meas = plane_from_f(c.plobs[c.e_src[e]].meas);
     const double delta = 1e-9, scalar = 1.0 / (2 * delta);
     double ev[3] = {0, 0, 0};
-    if (lane < 18 && (lane < 6 || pfree)) {
-        const double sgn = (lane & 1) ? -delta : delta;
+    const int q = lane >> 1;  // this lane pair's evaluation
+    if (q < 18 && (q < 6 || pfree)) {
+        const double sgn = (q & 1) ? -delta : delta;
         SE3 T = T0;
         P4 P = P0;
-        if (lane < 6) {
+        if (q < 6) {
             double add[3] = {0, 0, 0};
-            add[lane >> 1] = sgn;
+            add[q >> 1] = sgn;
             p_oplus(P, add);
         } else {
             double add[6] = {0, 0, 0, 0, 0, 0};
-            add[(lane - 6) >> 1] = sgn;
+            add[(q - 6) >> 1] = sgn;
             T = se3_mul(se3_exp(add), T0);
         }
-        plane_edge_error(ty, T, P, meas, ev);
+        const E3 r = plane_error_pair(ty - 2, T, P, meas, (lane & 1) != 0);
+        ev[0] = r.e0; ev[1] = r.e1; ev[2] = r.e2;
     }
     double A[3][3] = {}, B[3][6] = {};
 #pragma unroll
     for (int d = 0; d < 3; d++)
 #pragma unroll
         for (int i = 0; i < 3; i++) {
-            const double ep = __shfl(ev[i], 2 * d), em = __shfl(ev[i], 2 * d + 1);
+            const double ep = __shfl(ev[i], 2 * (2 * d)), em = __shfl(ev[i], 2 * (2 * d + 1));
             A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
         }
 #pragma unroll
     for (int d = 0; d < 6; d++)
 #pragma unroll
         for (int i = 0; i < 3; i++) {
-            const double ep = __shfl(ev[i], 6 + 2 * d), em = __shfl(ev[i], 7 + 2 * d);
+            const double ep = __shfl(ev[i], 2 * (6 + 2 * d)), em = __shfl(ev[i], 2 * (7 + 2 * d));
             B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
         }
     if (lane == 0) store_terms(c, C, k.robust, e, ty, pfree, A, B);

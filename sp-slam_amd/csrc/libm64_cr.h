@@ -81,6 +81,14 @@ __host__ __device__ inline dd ddiv(dd a, dd b) {
     const dd r = dadd(a, dneg(dmul_d(b, q1)));
     return fast_two_sum(q1, r.hi / b.hi);
 }
+// a / b through one reciprocal instead of two divisions (the quick paths: q1 within a few ulps of a / b, the
+// double-double remainder exact to ~2^-106, so the quotient's error stays near 2^-103 -- far inside kQuickEps)
+__host__ __device__ inline dd ddiv_r(dd a, dd b) {
+    const double r = 1.0 / b.hi;
+    const double q1 = a.hi * r;
+    const dd rem = dadd(a, dneg(dmul_d(b, q1)));
+    return fast_two_sum(q1, rem.hi * r);
+}
 
 // Round-to-nearest of a value known to lie within eps |r.hi| of r.hi + r.lo: true when both ends of that
 // interval round to the same double (rounding is monotone), which is then the correctly rounded result.
@@ -243,14 +251,24 @@ __host__ __device__ inline dd atan2_eval(double y, double x) {
     const double ax = fabs(x), ay = fabs(y);
     const bool swap = ay > ax;
     const double num = swap ? ax : ay, den = swap ? ay : ax;
-    const double zh = num / den;
-    const dd z{zh, fma(-zh, den, num) / den};  // the division's remainder is exact
+    // z = num / den as a double-double: the accurate path divides twice (the remainder is exact), the quick path
+    // multiplies by one reciprocal (zh within a few ulps, z still exact to ~2^-103)
+    double zh, zl;
+    if (kAccurate) {
+        zh = num / den;
+        zl = fma(-zh, den, num) / den;
+    } else {
+        const double rd = 1.0 / den;
+        zh = num * rd;
+        zl = fma(-zh, den, num) * rd;
+    }
+    const dd z{zh, zl};
     const double fi = rint(zh * 64.0);
     const int i = (int)fi;
     const double c = fi * 0.015625;
     const dd nm = two_sum(zh - c, z.lo);               // z - i/64 (the high difference is exact)
     const dd dn = dadd_d(dmul_d(z, c), 1.0);           // 1 + z i/64
-    const dd uq = ddiv(nm, dn);  // computed for i = 0 too: a select, not a branch
+    const dd uq = kAccurate ? ddiv(nm, dn) : ddiv_r(nm, dn);  // computed for i = 0 too: a select, not a branch
     const dd u{i == 0 ? z.hi : uq.hi, i == 0 ? z.lo : uq.lo};
     dd a = dadd(dd{kAtan64[i][0], kAtan64[i][1]}, atan_small<kAccurate>(u));
     // pi/2 - a, pi - a and the sign as selects (no branches inside the quick path)
@@ -262,6 +280,9 @@ __host__ __device__ inline dd atan2_eval(double y, double x) {
 }
 
 __host__ __device__ SPSLAM_CR_COLD inline double atan2_accurate(double y, double x) {
+    // |y / x| below 2^-900 with x > 0: atan2 = y/x (1 - (y/x)^2/3), which rounds like y/x (y / x is never a
+    // midpoint) -- and the double-double quotient's low part would be subnormal
+    if (!__builtin_signbit(x) && fabs(y) < fabs(x) * 0x1p-900) return y / x;
     double out;
     rounds_to(atan2_eval<true>(y, x), kAccurateEps, &out);
     return out;
@@ -271,23 +292,26 @@ __host__ __device__ SPSLAM_CR_COLD inline double atan2_accurate(double y, double
 __host__ __device__ inline bool atan2_quick(double y, double x, double* out) {
     const double ax = fabs(x), ay = fabs(y);
     const double inf = 1.7976931348623157e308 * 2.0;
-    const double sy = y < 0 || (y == 0 && 1.0 / y < 0) ? -1.0 : 1.0;  // sign of y, zeros included
-    const bool xneg = x < 0 || (x == 0 && 1.0 / x < 0);
+    const double sy = __builtin_signbit(y) ? -1.0 : 1.0;  // sign of y, zeros included (NaN: overridden below)
+    const bool xneg = __builtin_signbit(x);
     const bool nan = x != x || y != y;
     const bool zy = ay == 0, zx = ax == 0, infs = ax == inf || ay == inf;
-    // |y / x| below 2^-900 with x > 0: atan2 = y/x (1 - (y/x)^2/3), which rounds like y/x (y / x is never a
-    // midpoint) -- and the double-double quotient's low part would be subnormal
+    // |y / x| below 2^-900 with x > 0 (y / x, see atan2_accurate): left to the slow path
     const bool small = !xneg && ay < ax * 0x1p-900;
-    const bool special = nan || zy || zx || infs || small;
-    double sp = y / x;                                            // small
+    const bool special = nan || zy || zx || infs;
+    double sp = 0.0;
     if (infs) sp = ax == inf && ay == inf ? sy * (xneg ? k3Pio4_hi : kPio4_hi)
                                           : (ax == inf ? (xneg ? sy * kPi_hi : sy * 0.0) : sy * kPio2_hi);
     if (zx) sp = sy * kPio2_hi;
     if (zy) sp = xneg ? sy * kPi_hi : y;                         // atan2(+-0, x): +-pi or +-0
     if (nan) sp = x + y;
-    const dd r = atan2_eval<false>(special ? 1.0 : y, special ? 1.0 : x);
+    // the reciprocal 1 / max(|x|, |y|) must be a normal double: extreme magnitudes are left to the slow path
+    const double den = ax > ay ? ax : ay;
+    const bool extreme = !(den >= 0x1p-1000 && den <= 0x1p1000);
+    const bool stand_in = special || small || extreme;
+    const dd r = atan2_eval<false>(stand_in ? 1.0 : y, stand_in ? 1.0 : x);
     double q;
-    const bool ok = rounds_to(r, kQuickEps, &q);
+    const bool ok = rounds_to(r, kQuickEps, &q) && !small && !extreme;
     *out = special ? sp : q;
     return special || ok;
 }

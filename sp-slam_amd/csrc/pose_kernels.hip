@@ -491,7 +491,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     for (int i = t; i < nl; i += kThreads) plout[i] = 0;
     if (np < 3) {  // nInitialCorrespondences < 3 (:653): no SetPose
         if (t < 16) res->Tcw[t] = Tin[t];
-        if (t == 0) { res->n_inliers = 0; res->lm_iterations = 0; }
+        if (t == 0) { res->n_inliers = 0; res->lm_iterations = 0; res->trial_passes = 0; res->trials = 0; }
         return;
     }
     if (t < 12 && nl > 0) {
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
 
     int buf = 0;
     bool robust = true;
-    int nBad = 0, total_its = 0;
+    int nBad = 0, total_its = 0, total_passes = 0, total_trials = 0;
     SE3 T;
     for (int round = 0; round < 4; round++) {
         PROF_MARK(0);  // setup / previous relabel
@@ -747,6 +747,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                     }
                     PROF_MARK(4);  // solves + exp + broadcast
                     PROF_COUNT(10);
+                    total_passes++;
                     // ---- pass B: robust chi2 of every active edge at each trial pose, one ring row of kSpec
                     // values per edge, chained in edge order by lanes 0 .. kSpec-1 of the chain wave.  Plane edges:
                     // one (edge, trial) pair per lane pair (plane_error_pair), 32 / kSpec edges per compute wave
@@ -837,6 +838,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                             }
                             rho = r;
                             qmax++;
+                            total_trials++;
                             more = rho < 0 && qmax < kMaxTrials;
                         }
                     }
@@ -916,6 +918,8 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         res->Tcw[12] = 0.f; res->Tcw[13] = 0.f; res->Tcw[14] = 0.f; res->Tcw[15] = 1.f;
         res->n_inliers = ne - nBad;
         res->lm_iterations = S.stall ? -1 : total_its;  // a bounded wait gave up: the result is not valid
+        res->trial_passes = total_passes;
+        res->trials = total_trials;
     }
 #ifdef SPSLAM_POSE_PROF
     PROF_MARK(9);  // outputs

@@ -177,7 +177,7 @@ POSE_PROBLEM_DTYPE = np.dtype([("Tcw", "<f4", 16), ("fx", "<f4"), ("fy", "<f4"),
                                ("bf", "<f4"), ("n_points", "<i4"), ("n_planes", "<i4"), ("point_offset", "<i4"),
                                ("plane_offset", "<i4"), ("pad", "<i4")])
 POSE_RESULT_DTYPE = np.dtype([("Tcw", "<f4", 16), ("n_inliers", "<i4"), ("lm_iterations", "<i4"),
-                              ("pad", "<i4", 2)])
+                              ("trial_passes", "<i4"), ("trials", "<i4")])
 assert POINT_OBS_DTYPE.itemsize == 32 and PLANE_OBS_DTYPE.itemsize == 48
 assert POSE_PROBLEM_DTYPE.itemsize == 104 and POSE_RESULT_DTYPE.itemsize == 80
 

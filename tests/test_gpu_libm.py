@@ -49,6 +49,11 @@ def test_atan2_bit_exact(gpu):
     sp = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, 1e-310, np.nan])
     ys, xs = np.meshgrid(sp, sp)
     y, x = np.concatenate([y, ys.ravel()]), np.concatenate([x, xs.ravel()])
+    # extreme magnitudes (the quick path's reciprocal of max(|x|, |y|) leaves the normal range) and ratios
+    # below 2^-900: the slow path decides
+    ext = np.array([1e300, -3e305, 2.0 ** 1000, 2.0 ** 1001, 2.0 ** -1000, 2.0 ** -1001, -7e-302, 1e-250, 3e-200])
+    ye, xe = np.meshgrid(ext, np.concatenate([ext, [1.0, -2.5, 0.3]]))
+    y, x = np.concatenate([y, ye.ravel(), xe.ravel()]), np.concatenate([x, xe.ravel(), ye.ravel()])
     d = spslam_gpu.debug_libm64(gpu, 2, y, x)
     o = oracle_ctypes.libm_cr(2, y, x)
     bad = np.nonzero(~((d == o) | (np.isnan(d) & np.isnan(o))) | (np.signbit(d) != np.signbit(o)) & ~np.isnan(o))[0]

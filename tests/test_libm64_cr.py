@@ -73,6 +73,12 @@ def test_atan2_matches_oracle(lib):
     x[::19] = y[::19]              # |y| == |x|
     x[::23] = -y[::23]
     y[::29] = y[::29] * 1e-200     # tiny ratios
+    # extreme magnitudes: 1 / max(|x|, |y|) is not a normal double there (the quick path's reciprocal), and
+    # ratios beyond 2^-900
+    ext = np.array([1e300, -3e305, 2.0 ** 1000, 2.0 ** 1001, 2.0 ** -1000, 2.0 ** -1001, -7e-302, 1e-250, 3e-200])
+    ye, xe = np.meshgrid(ext, np.concatenate([ext, [1.0, -2.5, 0.3]]))
+    y = np.concatenate([y, ye.ravel(), xe.ravel()])
+    x = np.concatenate([x, xe.ravel(), ye.ravel()])
     sp = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, 1e-310, 5e-324, np.nan])
     ys, xs = np.meshgrid(sp, sp)
     y = np.concatenate([y, ys.ravel()])
