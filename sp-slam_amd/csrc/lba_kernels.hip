@@ -539,6 +539,9 @@ __global__ __launch_bounds__(kThreads) void k_errors(LbaBatch b, LbaWork w, LbaC
     Ctx c = make_ctx(b, task.x);
     const LbaCtl& k = *c.ctl;
     if (k.state != (mode == 0 ? kIter : kTrial)) return;
+    // the landmark part of computeLambdaInit's max is gathered by atomic max into part_max[0] (slots
+    // 1 .. nLc - 1 stay zero); cleared here, before the iteration's sums
+    if (mode == 0 && task.y == 0 && threadIdx.x < c.nLc) c.part_max[threadIdx.x] = 0.0;
     const int e = task.y + threadIdx.x;
     double acc[1] = {0.0};
     if (e < c.E && c.e_level[e] == 0) {
@@ -605,22 +608,6 @@ __device__ __forceinline__ void store_terms(const Ctx& c, const LbaConsts& C, bo
     }
 }
 
-// point edges (analytic Jacobians), one edge per thread
-__global__ __launch_bounds__(kThreads) void k_edge_terms(LbaBatch b, LbaWork w, LbaConsts C) {
-    const int2 task = w.edge_chunks[blockIdx.x];
-    Ctx c = make_ctx(b, task.x);
-    const LbaCtl& k = *c.ctl;
-    if (k.state != kIter) return;
-    if (task.y >= c.Ep) return;  // chunks of plane edges only
-    const int e = task.y + threadIdx.x;
-    if (e >= c.Ep || c.e_level[e] != 0) return;
-    const int ty = c.e_type[e];
-    const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
-    double A[3][3] = {}, B[3][6] = {};
-    edge_jacobians<1>(c, e, pfree, A, B);
-    store_terms(c, C, k.robust, e, ty, pfree, A, B);
-}
-
 // plane / parallel / vertical edges: central differences (base_binary_edge.hpp:130-205), one wave per edge.
 // Evaluation q < 6 is the error at the plane perturbed by +-1e-9 along coordinate q >> 1 (Plane3D::oplus),
 // 6 <= q < 18 at the pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; evaluation q runs on the lane pair (2q, 2q + 1)
@@ -677,31 +664,87 @@ __global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w,
     if (lane == 0) store_terms(c, C, k.robust, e, ty, pfree, A, B);
 }
 
-// landmark Hll, bl and (landmark, pose) blocks, summed over the landmark's edges in insertion order
-__global__ __launch_bounds__(kThreads) void k_lm_sums(LbaBatch b, LbaWork w) {
+// Point edges and point landmarks in one pass (the point part of k_lm_sums, without a per-edge kernel before
+// it): a workgroup computes the quadratic-form terms of 256 consecutive point edges, one edge per thread
+// (edge_jacobians<1> and store_terms' formulas), and keeps the landmark-side terms (Hll 9, bl 3, Hpl 18) in LDS; a landmark's edges
+// are consecutive and at most kLbaMaxKeyframes, so the workgroup owns the landmarks whose first edge lies in
+// its first kLbaSegOwn edges and finds all their edges in LDS (the last 64 threads are the halo).  Each owned
+// landmark is summed by the thread of its first edge in insertion order, exactly as k_lm_sums sums the stored
+// terms; only the pose-side terms (Hpp 21, bp 6) still go to memory, for k_pose_sums.  Same values as storing
+// every term per edge and summing the stored terms, without the 456-byte per-edge round trip.
+constexpr int kSegStride = 31;  // odd stride in doubles
+__global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWork w, LbaConsts C) {
+    static_assert(kThreads - kLbaSegOwn >= kLbaMaxKeyframes, "halo must hold a landmark's edges");
     __shared__ Red R;
-    const int2 task = w.lm_chunks[blockIdx.x];
+    __shared__ double Tm[kThreads * kSegStride];
+    __shared__ uint8_t act[kThreads];
+    const int2 task = w.seg_chunks[blockIdx.x];
     Ctx c = make_ctx(b, task.x);
-    if (c.ctl->state != kIter) return;
-    const int l = task.y + threadIdx.x;
+    const LbaCtl& k = *c.ctl;
+    if (k.state != kIter) return;
+    const int t = threadIdx.x, e = task.y + t;
+    double* row = Tm + t * kSegStride;
+    bool a = false;
+    if (e < c.Ep && c.e_level[e] == 0) {
+        a = true;
+        const int ty = c.e_type[e];
+        const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
+        double A[3][3] = {}, B[3][6] = {};
+        edge_jacobians<1>(c, e, pfree, A, B);
+        const int dim = edge_dim(ty);
+        double info[3];
+        info_of(c, C, e, info);
+        const double* err = c.err + 3 * e;
+        double r0, wgt;
+        huber(chi2_of(err, info, dim), delta_of(C, ty), k.robust, &r0, &wgt);
+        double W[3] = {0, 0, 0}, om[3] = {0, 0, 0};
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            if (r < dim) {
+                W[r] = k.robust ? wgt * info[r] : info[r];
+                om[r] = -(info[r] * err[r]);
+                if (k.robust) om[r] *= wgt;
+            }
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            row[9 + i] = (A[0][i] * om[0] + A[1][i] * om[1]) + A[2][i] * om[2];
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+                row[3 * i + j] = ((A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j]) + (A[2][i] * W[2]) * A[2][j];
+#pragma unroll
+            for (int j = 0; j < 6; j++)
+                row[12 + 6 * i + j] = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
+                                                  (A[2][i] * W[2]) * B[2][j]
+                                            : 0.0;
+        }
+        if (pfree && t < kLbaSegOwn) {
+            double* o = c.con + (size_t)kLbaCon * e;
+            int q = 30;
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = i; j < 6; j++)
+                    o[q++] = ((B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j]) + (B[2][i] * W[2]) * B[2][j];
+#pragma unroll
+            for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
+        }
+    }
+    act[t] = a;
+    __syncthreads();
     double mx = 0.0;
-    if (l < c.L && lm_block_base(c, l) >= 0) {
-        const int b0 = lm_block_base(c, l);
-        // every block of l receives at least one edge: the first edge stores it, later ones (a landmark
-        // seen twice from one keyframe) accumulate, in insertion order
+    const int l = t < kLbaSegOwn && e < c.Ep ? c.e_lm[e] : -1;
+    if (l >= 0 && c.lm_boff[l] == e && lm_block_base(c, l) >= 0) {
+        const int b0 = lm_block_base(c, l), nb = c.lm_nb[l];
         uint64_t written = 0;
         double H[9] = {}, bl[3] = {};
-        for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
-            if (c.e_level[e] != 0) continue;
-            const double* o = c.con + (size_t)kLbaCon * e;
-            double r[30];
-#pragma unroll
-            for (int j = 0; j < 30; j++) r[j] = o[j];
-            const int bk = c.e_blk[e];
+        for (int q = 0; q < nb; q++) {
+            if (!act[t + q]) continue;
+            const double* r = Tm + (t + q) * kSegStride;
 #pragma unroll
             for (int j = 0; j < 9; j++) H[j] += r[j];
 #pragma unroll
             for (int j = 0; j < 3; j++) bl[j] += r[9 + j];
+            const int bk = c.e_blk[e + q];
             if (bk >= 0) {
                 double* hb = c.blkH + (size_t)bk * 18;
                 const uint64_t bit = 1ull << (bk - b0);
@@ -722,7 +765,45 @@ __global__ __launch_bounds__(kThreads) void k_lm_sums(LbaBatch b, LbaWork w) {
         mx = fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8])));
     }
     mx = block_max(mx, R);
-    if (threadIdx.x == 0) c.part_max[task.y / kThreads] = mx;
+    // max |diag| (computeLambdaInit): non-negative doubles order like their bit patterns; k_errors cleared the slot
+    if (t == 0 && mx > 0.0) atomicMax((unsigned long long*)c.part_max, (unsigned long long)__double_as_longlong(mx));
+}
+
+// Plane landmarks (point landmarks: k_point_terms_sums): Hll, bl and the (landmark, pose) blocks summed over the
+// landmark's edges in insertion order from the terms k_plane_terms stored.  One wave per plane landmark, lane j
+// < 30 owns term j (the same per-term sequence of adds as one thread summing all 30).
+__global__ __launch_bounds__(kThreads) void k_plane_lm_sums(LbaBatch b, LbaWork w) {
+    __shared__ Red R;
+    const int2 task = w.plm_tasks[blockIdx.x];
+    Ctx c = make_ctx(b, task.x);
+    if (c.ctl->state != kIter) return;
+    const int lane = threadIdx.x & 63, l = task.y + (threadIdx.x >> 6);
+    double acc = 0.0;
+    bool have = false;
+    if (l < c.L && lm_block_base(c, l) >= 0) {  // uniform over the wave
+        have = true;
+        const int b0 = lm_block_base(c, l), j = lane < 30 ? lane : 29;
+        uint64_t written = 0;
+        for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
+            if (c.e_level[e] != 0) continue;
+            const double v = c.con[(size_t)kLbaCon * e + j];
+            const int bk = c.e_blk[e];
+            if (lane < 12) acc += v;
+            if (bk >= 0) {
+                const uint64_t bit = 1ull << (bk - b0);
+                double* hb = c.blkH + (size_t)bk * 18;
+                if (lane >= 12 && lane < 30) hb[lane - 12] = (written & bit) ? hb[lane - 12] + v : v;
+                written |= bit;
+            }
+        }
+        if (lane < 9) c.lmH[9 * l + lane] = acc;
+        else if (lane < 12) c.lmb[3 * l + lane - 9] = acc;
+    }
+    const double d0 = __shfl(acc, 0), d4 = __shfl(acc, 4), d8 = __shfl(acc, 8);
+    double mx = have && lane == 0 ? fmax(fabs(d0), fmax(fabs(d4), fabs(d8))) : 0.0;
+    mx = block_max(mx, R);
+    if (threadIdx.x == 0 && mx > 0.0)
+        atomicMax((unsigned long long*)c.part_max, (unsigned long long)__double_as_longlong(mx));
 }
 
 // keyframe Hpp, bp over its active edges (free poses only)
@@ -770,11 +851,13 @@ __global__ void k_iter_begin(LbaBatch b) {
     LbaCtl& k = *c.ctl;
     if (k.state != kIter) return;
     double chi = 0.0;
+#pragma unroll 8
     for (int i = 0; i < c.nEc; i++) chi += c.part_chi[i];
     k.currentChi = chi;
     k.iniChi = chi;
     if (k.it == 0) {  // computeLambdaInit: tau * max |diag| over the Hessian vertices
         double mx = 0.0;
+#pragma unroll 8
         for (int i = 0; i < c.nLc + c.K; i++) mx = fmax(mx, c.part_max[i]);
         k.lambda = 1e-5 * mx;
         k.ni = 2;
@@ -1137,12 +1220,16 @@ __global__ void k_decide(LbaBatch b, int step) {
     Ctx c = make_ctx(b, blockIdx.x);
     LbaCtl& k = *c.ctl;
     if (k.state != kTrial) return;
+    // (serial sums over global partials: unrolled so that 8 loads are in flight per dependent-add group)
     double tempChi = 0.0;
+#pragma unroll 8
     for (int i = 0; i < c.nEc; i++) tempChi += c.part_chi[i];
     double scale = 0.0;
     if (k.ok) {
         const int n = 6 * k.np;
+#pragma unroll 8
         for (int i = 0; i < n; i++) scale += c.y[i] * (k.lambda * c.y[i] + c.bp[i]);
+#pragma unroll 8
         for (int i = 0; i < c.nLc; i++) scale += c.part_scale[i];
     } else {
         tempChi = DBL_MAX;
@@ -1337,9 +1424,9 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
         hipLaunchKernelGGL(k_struct_fill, dim3(w.n_kf_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_struct_done, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_errors, dim3(w.n_edge_chunks), T, 0, s, b, w, C, 0);
-        hipLaunchKernelGGL(k_edge_terms, dim3(w.n_edge_chunks), T, 0, s, b, w, C);
         if (w.n_plane_tasks) hipLaunchKernelGGL(k_plane_terms, dim3(w.n_plane_tasks), T, 0, s, b, w, C);
-        hipLaunchKernelGGL(k_lm_sums, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        if (w.n_seg_chunks) hipLaunchKernelGGL(k_point_terms_sums, dim3(w.n_seg_chunks), T, 0, s, b, w, C);
+        if (w.n_plm_tasks) hipLaunchKernelGGL(k_plane_lm_sums, dim3(w.n_plm_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_pose_sums, dim3(w.n_kf_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_iter_begin, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_schur_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);

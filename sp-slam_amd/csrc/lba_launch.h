@@ -82,7 +82,10 @@ struct LbaWork {
     const int2* kf_tasks; int n_kf_tasks;
     const int2* pair_tasks; int n_pair_tasks;
     const int2* plane_tasks; int n_plane_tasks;  // (problem, first plane edge) per kLbaPlaneEdgesPerTask edges
+    const int2* seg_chunks; int n_seg_chunks;    // (problem, first point edge) per kLbaSegOwn point edges
+    const int2* plm_tasks; int n_plm_tasks;      // (problem, first plane landmark) per kLbaChunk / 64 planes
 };
+constexpr int kLbaSegOwn = kLbaChunk - 64;  // point edges owned per k_point_terms_sums workgroup (64: halo)
 constexpr int kLbaPlaneEdgesPerTask = kLbaChunk / 64;  // one wave per plane edge
 
 struct LbaBatch {

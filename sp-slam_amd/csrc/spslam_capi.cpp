@@ -1005,7 +1005,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
     std::vector<long long> off(n);
     // work tables: edge chunks, landmark chunks, keyframe tasks, pose-pair (+ bs) tasks per problem
-    std::vector<int2> ec, lc, kt, pt, qt;
+    std::vector<int2> ec, lc, kt, pt, qt, sg, pm;
     size_t total = 0;
     for (int i = 0; i < n; i++) {
         const spslam_lba_problem& p = problems[i];
@@ -1024,6 +1024,8 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         const int npmax = p.n_kf;  // bound on the free poses; surplus tasks exit on the device
         for (int q = 0; q < npmax * (npmax + 1) / 2 + npmax; q++) pt.push_back(int2{i, q});
         for (int q = 0; q < p.n_plane_obs; q += kLbaPlaneEdgesPerTask) qt.push_back(int2{i, p.n_point_obs + q});
+        for (int e = 0; e < p.n_point_obs; e += kLbaSegOwn) sg.push_back(int2{i, e});
+        for (int q = 0; q < p.n_planes; q += kLbaChunk / 64) pm.push_back(int2{i, p.n_points + q});
     }
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
@@ -1043,12 +1045,14 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         c->lba_off_cap = n;
     }
     std::vector<int2> work;
-    work.reserve(ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + 1);
+    work.reserve(ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + sg.size() + pm.size() + 1);
     work.insert(work.end(), ec.begin(), ec.end());
     work.insert(work.end(), lc.begin(), lc.end());
     work.insert(work.end(), kt.begin(), kt.end());
     work.insert(work.end(), pt.begin(), pt.end());
     work.insert(work.end(), qt.begin(), qt.end());
+    work.insert(work.end(), sg.begin(), sg.end());
+    work.insert(work.end(), pm.begin(), pm.end());
     work.push_back(int2{0, 0});  // active counter
     if (work.size() > c->lba_work_cap) {
         HIP_CHECK(c, hipStreamSynchronize(s));
@@ -1074,7 +1078,9 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     const int2* w0 = c->d_lba_work;
     LbaWork W{w0, (int)ec.size(), w0 + ec.size(), (int)lc.size(), w0 + ec.size() + lc.size(), (int)kt.size(),
               w0 + ec.size() + lc.size() + kt.size(), (int)pt.size(),
-              w0 + ec.size() + lc.size() + kt.size() + pt.size(), (int)qt.size()};
+              w0 + ec.size() + lc.size() + kt.size() + pt.size(), (int)qt.size(),
+              w0 + ec.size() + lc.size() + kt.size() + pt.size() + qt.size(), (int)sg.size(),
+              w0 + ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + sg.size(), (int)pm.size()};
     LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
                (int*)(c->d_lba_work + work.size() - 1), d_stop_flags, c->lba_stop_after};
