@@ -96,6 +96,12 @@ __device__ Ctx make_ctx(const LbaBatch& b, int p) {
     return c;
 }
 
+__device__ __forceinline__ void wave_sync() {  // LDS written by this wave, visible to this wave
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ SE3 load_pose(const double* p) { return SE3{Q{p[0], p[1], p[2], p[3]}, V3{p[4], p[5], p[6]}}; }
 __device__ __forceinline__ void store_pose(double* p, const SE3& T) {
     p[0] = T.r.w; p[1] = T.r.x; p[2] = T.r.y; p[3] = T.r.z; p[4] = T.t.x; p[5] = T.t.y; p[6] = T.t.z;
@@ -820,7 +826,7 @@ __global__ __launch_bounds__(kThreads) void k_pose_sums(LbaBatch b, LbaWork w) {
     double acc[27];
 #pragma unroll
     for (int j = 0; j < 27; j++) acc[j] = 0.0;
-#pragma unroll 1
+#pragma unroll 2  // the next edge's loads in flight beside this one's adds (same per-thread order)
     for (int i = c.pe_off[k] + threadIdx.x; i < c.pe_off[k + 1]; i += kThreads) {
         const double* o = c.con + (size_t)kLbaCon * c.pe_idx[i] + 30;
 #pragma unroll
@@ -1028,10 +1034,12 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
     Ctx c = make_ctx(b, task.x);
     const LbaCtl& k = *c.ctl;
     if (k.state != kTrial) return;
+    // task.y >= 0: pose pair task.y (only issued for problems that may exceed the matrix-core path);
+    // task.y < 0: the reduced right-hand side of free pose -task.y - 1
     const int np = k.np, n = 6 * np, npairs = np * (np + 1) / 2, tid = task.y;
-    if (tid >= npairs + np) return;
-    if (tid < npairs && mfma_schur(k)) return;
-    if (tid < npairs) {
+    if (tid >= npairs || (tid < 0 && -tid - 1 >= np)) return;
+    if (tid >= 0 && mfma_schur(k)) return;
+    if (tid >= 0) {
         int p1 = 0, rem = tid;
         while (rem >= np - p1) { rem -= np - p1; p1++; }
         const int p2 = p1 + rem;
@@ -1066,7 +1074,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
             c.S[(size_t)(6 * p1 + r) * n + 6 * p2 + q] = base - v;
         }
     } else {
-        const int p = tid - npairs;
+        const int p = -tid - 1;
         double acc[6] = {0, 0, 0, 0, 0, 0};
         for (int l = threadIdx.x; l < c.L; l += kThreads) {
             const uint64_t m = c.lm_mask[l];
@@ -1147,6 +1155,8 @@ __global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
     LbaCtl& k = *c.ctl;
     if (k.state != kTrial) return;
     const int n = 6 * k.np;
+    // (measured: the same factorization on one wave with wave-level synchronisation took twice as long -- the
+    // trailing updates' LDS latency, not the barriers, bounds it)
     if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds) factor_body<true>(c, k, lds, n);
     else factor_body<false>(c, k, lds, n);
 }
