@@ -674,13 +674,12 @@ __global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w,
 // it): a workgroup computes the quadratic-form terms of 256 consecutive point edges, one edge per thread
 // (edge_jacobians<1> and store_terms' formulas), and keeps the landmark-side terms (Hll 9, bl 3, Hpl 18) in LDS; a landmark's edges
 // are consecutive and at most kLbaMaxKeyframes, so the workgroup owns the landmarks whose first edge lies in
-// its first kLbaSegOwn edges and finds all their edges in LDS (the last 64 threads are the halo).  Each owned
+// its first w.seg_own edges and finds all their edges in LDS (the remaining rows are the halo).  Each owned
 // landmark is summed by the thread of its first edge in insertion order, exactly as k_lm_sums sums the stored
 // terms; only the pose-side terms (Hpp 21, bp 6) still go to memory, for k_pose_sums.  Same values as storing
 // every term per edge and summing the stored terms, without the 456-byte per-edge round trip.
 constexpr int kSegStride = 31;  // odd stride in doubles
 __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWork w, LbaConsts C) {
-    static_assert(kThreads - kLbaSegOwn >= kLbaMaxKeyframes, "halo must hold a landmark's edges");
     __shared__ Red R;
     __shared__ double Tm[kThreads * kSegStride];
     __shared__ uint8_t act[kThreads];
@@ -689,18 +688,17 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
     const LbaCtl& k = *c.ctl;
     if (k.state != kIter) return;
     const int t = threadIdx.x, e = task.y + t;
-    double* row = Tm + t * kSegStride;
-    bool a = false;
-    if (e < c.Ep && c.e_level[e] == 0) {
-        a = true;
-        const int ty = c.e_type[e];
-        const bool pfree = c.pose_hidx[c.e_kf[e]] >= 0;
+    // the landmark-side terms (30) of active point edge ee into row[]; its pose-side terms (27) to memory when
+    // write_pose (each edge's by the workgroup that owns it)
+    auto land_terms = [&](int ee, double* row, bool write_pose) __attribute__((always_inline)) {
+        const int ty = c.e_type[ee];
+        const bool pfree = c.pose_hidx[c.e_kf[ee]] >= 0;
         double A[3][3] = {}, B[3][6] = {};
-        edge_jacobians<1>(c, e, pfree, A, B);
+        edge_jacobians<1>(c, ee, pfree, A, B);
         const int dim = edge_dim(ty);
         double info[3];
-        info_of(c, C, e, info);
-        const double* err = c.err + 3 * e;
+        info_of(c, C, ee, info);
+        const double* err = c.err + 3 * ee;
         double r0, wgt;
         huber(chi2_of(err, info, dim), delta_of(C, ty), k.robust, &r0, &wgt);
         double W[3] = {0, 0, 0}, om[3] = {0, 0, 0};
@@ -723,8 +721,8 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
                                                   (A[2][i] * W[2]) * B[2][j]
                                             : 0.0;
         }
-        if (pfree && t < kLbaSegOwn) {
-            double* o = c.con + (size_t)kLbaCon * e;
+        if (pfree && write_pose) {
+            double* o = c.con + (size_t)kLbaCon * ee;
             int q = 30;
 #pragma unroll
             for (int i = 0; i < 6; i++)
@@ -734,18 +732,30 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
 #pragma unroll
             for (int i = 0; i < 6; i++) o[51 + i] = (B[0][i] * om[0] + B[1][i] * om[1]) + B[2][i] * om[2];
         }
-    }
+    };
+    const bool a = e < c.Ep && c.e_level[e] == 0;
+    if (a) land_terms(e, Tm + t * kSegStride, t < w.seg_own);
     act[t] = a;
     __syncthreads();
     double mx = 0.0;
-    const int l = t < kLbaSegOwn && e < c.Ep ? c.e_lm[e] : -1;
+    const int l = t < w.seg_own && e < c.Ep ? c.e_lm[e] : -1;
     if (l >= 0 && c.lm_boff[l] == e && lm_block_base(c, l) >= 0) {
         const int b0 = lm_block_base(c, l), nb = c.lm_nb[l];
         uint64_t written = 0;
         double H[9] = {}, bl[3] = {};
         for (int q = 0; q < nb; q++) {
-            if (!act[t + q]) continue;
-            const double* r = Tm + (t + q) * kSegStride;
+            // rows past the workgroup's 256 (a landmark with more edges than the halo allows: only if a point
+            // has more observations than the batch has keyframes) are computed here
+            double r[30];
+            if (t + q >= kThreads) {
+                if (c.e_level[e + q] != 0) continue;
+                land_terms(e + q, r, false);
+            } else {
+                if (!act[t + q]) continue;
+                const double* src = Tm + (t + q) * kSegStride;
+#pragma unroll
+                for (int j = 0; j < 30; j++) r[j] = src[j];
+            }
 #pragma unroll
             for (int j = 0; j < 9; j++) H[j] += r[j];
 #pragma unroll

@@ -82,10 +82,13 @@ struct LbaWork {
     const int2* kf_tasks; int n_kf_tasks;
     const int2* pair_tasks; int n_pair_tasks;
     const int2* plane_tasks; int n_plane_tasks;  // (problem, first plane edge) per kLbaPlaneEdgesPerTask edges
-    const int2* seg_chunks; int n_seg_chunks;    // (problem, first point edge) per kLbaSegOwn point edges
+    const int2* seg_chunks; int n_seg_chunks;    // (problem, first point edge) per seg_own point edges
     const int2* plm_tasks; int n_plm_tasks;      // (problem, first plane landmark) per kLbaChunk / 64 planes
+    int seg_own;  // point edges owned per k_point_terms_sums workgroup: kLbaChunk - (most keyframes of a problem
+                  // - 1), so the rest of the 256 rows (the halo) holds any landmark's remaining edges
 };
-constexpr int kLbaSegOwn = kLbaChunk - 64;  // point edges owned per k_point_terms_sums workgroup (64: halo)
+// a point has at most one observation per keyframe (MapPoint::mObservations is a map keyed by KeyFrame*)
+inline int lba_seg_own(int max_kf) { return kLbaChunk - (max_kf > 1 ? max_kf - 1 : 0); }
 constexpr int kLbaPlaneEdgesPerTask = kLbaChunk / 64;  // one wave per plane edge
 
 struct LbaBatch {

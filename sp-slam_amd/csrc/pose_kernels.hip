@@ -199,7 +199,7 @@ struct Shared {
     double ring[(kRingA + kRingPad) * kStrideA];  // pass A: [kRingA][kStrideA]; pass B: [RingB::kRows][kSpec + 1]
     double tot[kRed];                 // the chained totals, for every thread
     double red[2][kWaves][1];         // wave totals of the workgroup sums, double-buffered
-    double perr[kComputeWaves][5][13][3];  // per compute wave: plane errors at the 12 perturbed poses and at T
+    double perr[kComputeWaves][9][13][3];  // per compute wave: plane errors at the 12 perturbed poses and at T
     double perrB[kPlaneChunk][kSpec][3];   // plane errors at the trial poses of the last pass B
     double perrT[kPlaneChunk][3];     // plane errors at the accepted trial pose = the next iteration's T
     double hb[kRed];                  // the iteration's H (lower, 21) and b (6), slot 0 unused
@@ -600,7 +600,12 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                 // perturbed poses exp(+-1e-9 e_d) * T (and at T unless an accepted trial left them in perrT) are
                 // evaluated on nev lanes per edge, ps edges per compute wave and round, then staged by one lane
                 const bool haveT = tValid && nl <= kPlaneChunk;
-                const int nev = haveT ? 12 : 13, psA = 64 / nev;
+                // full evaluations per edge: the 6 rotation perturbations, ONE translation perturbation (q = 6)
+                // and T unless perrT holds it; the other 5 translation perturbations share q = 6's rotation and
+                // reference normal bit for bit (exp(+-1e-9 e_d) for d >= 3 is a pure translation: its quaternion
+                // is exactly (1, 0, 0, 0), so every Tq.r equals normalize(T.r)), which leaves only the plane
+                // distance to recompute -- checked per perturbation, with a full evaluation where it fails
+                const int nev = haveT ? 7 : 8, psA = 64 / nev;
                 const Schedule GA(np, nl, psA);
                 pass_begin();
                 if (chain_wave) {
@@ -647,7 +652,8 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                     for (int k = GA.npr; k < GA.nr; k++) {
                         int ea, eb;
                         GA.share(k, wv, ea, eb);
-                        const int i = lane / nev, q = lane - i * nev, j = ea - np + i;  // evaluation lanes
+                        // evaluation lanes: slot qe < 7 -> perturbation qe, slot 7 -> T (stored as q = 12)
+                        const int i = lane / nev, qe = lane - i * nev, q = qe < 7 ? qe : 12, j = ea - np + i;
                         if (i < psA && np + j < eb) {
                             double err[3] = {0, 0, 0};
                             if (!plout[j]) {
@@ -661,6 +667,34 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                                 plane_error_at(np + j, Tq, err);
                             }
                             S.perr[wv][i][q][0] = err[0]; S.perr[wv][i][q][1] = err[1]; S.perr[wv][i][q][2] = err[2];
+                        }
+                        wave_sync();
+                        {   // the other translation perturbations q = 7 .. 11, one lane each
+                            const int i2 = lane / 5, q2 = 7 + (lane - i2 * 5), j2 = ea - np + i2;
+                            if (i2 < psA && np + j2 < eb) {
+                                double err[3] = {0, 0, 0};
+                                if (!plout[j2]) {
+                                    const SE3 T6 = se3_mul(S.Eadd[6], T), Tk = se3_mul(S.Eadd[q2], T);
+                                    P4 w, m;
+                                    plane_of(np + j2, w, m);
+                                    // plane_error's first steps for both poses (same rotation: same n2)
+                                    const V3 n2 = mv(q_to_rot(T6.r), V3{w.c[0], w.c[1], w.c[2]});
+                                    const double va = w.c[3] - dot(T6.t, n2), vb = w.c[3] - dot(Tk.t, n2);
+                                    const double vf = vb < 0.0 ? -vb : vb;
+                                    const double vn = vf * (1. / sqrt(n2.x * n2.x + n2.y * n2.y + n2.z * n2.z));
+                                    auto same = [](double a, double b) { return __double_as_longlong(a) == __double_as_longlong(b); };
+                                    const bool shared = same(T6.r.w, Tk.r.w) && same(T6.r.x, Tk.r.x) && same(T6.r.y, Tk.r.y) &&
+                                                        same(T6.r.z, Tk.r.z) && (va < 0.0) == (vb < 0.0) && !(vn < 0.0);
+                                    if (shared) {
+                                        err[0] = S.perr[wv][i2][6][0];
+                                        err[1] = S.perr[wv][i2][6][1];
+                                        err[2] = pls[j2].kind == 0 ? (-vn) - (-m.c[3]) : 0.0;
+                                    } else {
+                                        plane_error_at(np + j2, Tk, err);
+                                    }
+                                }
+                                S.perr[wv][i2][q2][0] = err[0]; S.perr[wv][i2][q2][1] = err[1]; S.perr[wv][i2][q2][2] = err[2];
+                            }
                         }
                         wave_sync();
                         PROF_MARK(16);  // pass A plane evaluations

@@ -1006,6 +1006,9 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     std::vector<long long> off(n);
     // work tables: edge chunks, landmark chunks, keyframe tasks, pose-pair (+ bs) tasks per problem
     std::vector<int2> ec, lc, kt, pt, qt, sg, pm;
+    int max_kf = 1;
+    for (int i = 0; i < n; i++) max_kf = std::max(max_kf, problems[i].n_kf);
+    const int seg_own = lba_seg_own(std::min(max_kf, kLbaMaxKeyframes));
     size_t total = 0;
     for (int i = 0; i < n; i++) {
         const spslam_lba_problem& p = problems[i];
@@ -1028,7 +1031,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
             for (int q = 0; q < npmax * (npmax + 1) / 2; q++) pt.push_back(int2{i, q});
         for (int q = 0; q < npmax; q++) pt.push_back(int2{i, -(q + 1)});
         for (int q = 0; q < p.n_plane_obs; q += kLbaPlaneEdgesPerTask) qt.push_back(int2{i, p.n_point_obs + q});
-        for (int e = 0; e < p.n_point_obs; e += kLbaSegOwn) sg.push_back(int2{i, e});
+        for (int e = 0; e < p.n_point_obs; e += seg_own) sg.push_back(int2{i, e});
         for (int q = 0; q < p.n_planes; q += kLbaChunk / 64) pm.push_back(int2{i, p.n_points + q});
     }
     HIP_CHECK(c, hipSetDevice(c->device));
@@ -1084,7 +1087,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
               w0 + ec.size() + lc.size() + kt.size(), (int)pt.size(),
               w0 + ec.size() + lc.size() + kt.size() + pt.size(), (int)qt.size(),
               w0 + ec.size() + lc.size() + kt.size() + pt.size() + qt.size(), (int)sg.size(),
-              w0 + ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + sg.size(), (int)pm.size()};
+              w0 + ec.size() + lc.size() + kt.size() + pt.size() + qt.size() + sg.size(), (int)pm.size(), seg_own};
     LbaBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results,
                (int*)(c->d_lba_work + work.size() - 1), d_stop_flags, c->lba_stop_after};
