@@ -470,6 +470,9 @@ def main():
                     help="timed one-core CPU baseline frames (default 300; 100 above 640x480)")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
     ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
+    ap.add_argument("--no-planes-priority", action="store_true",
+                    help="next batch's plane stream at normal priority (default high: 1 %% faster step, "
+                         "profiles/r03/ab_prio_*)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
     ap.add_argument("--ate-frames", type=int, default=300,
@@ -510,7 +513,8 @@ def main():
 
     hp = pipeline.HotPath(args.batch, unique_frames=args.unique_frames, device=local,
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
-                          orb_priority=args.orb_priority, **cfg, **shard_of(rank))
+                          orb_priority=args.orb_priority, planes_priority=not args.no_planes_priority, **cfg,
+                          **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
     torch.cuda.synchronize()

@@ -179,7 +179,11 @@ constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
 
 // Pass A ring: rows of the 28 terms (odd stride: the 64 lanes' row writes spread over the banks).  Pass B reuses
 // the same LDS as a ring of kSpec-value rows (trial robust chi2).
-constexpr int kRingA = 256;
+#ifndef SPSLAM_POSE_RING
+#define SPSLAM_POSE_RING 512  // rows of the pass-A ring; measured in the pipelined C2 step: 128 rows 7.00 ms,
+                              // 256 rows 6.97, 512 rows (146 KB of LDS per problem) 6.80 (profiles/r03/ab_ring*)
+#endif
+constexpr int kRingA = SPSLAM_POSE_RING;
 constexpr int kStrideA = kRed + 1;
 constexpr int kRingPad = 24;       // spare rows past the ring end: chain_seg loads up to 23 rows past a segment
 constexpr int kSpinCap = 1 << 20;  // bound of every wait (s_sleep 1 each: ~30 ms); never reached in a correct run

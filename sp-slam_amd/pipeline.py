@@ -62,7 +62,7 @@ def _ptr(t):
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
-                 pipelined=False, tail_priority=True, orb_priority=False, min_size=500, chi=300.0, vp_chi=300.0,
+                 pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
                  rotate_inputs=False):
         import torch
         self.torch = torch
@@ -151,6 +151,7 @@ class HotPath:
             self.base_inputs = {k: getattr(self, k).clone() for k in self.INPUT_BUFFERS}
         self.pipelined = pipelined
         self.orb_priority = orb_priority
+        self.planes_priority = planes_priority
         if pipelined:
             self._setup_pipeline()
         torch.cuda.synchronize()  # buffers were filled on the default stream
@@ -498,7 +499,7 @@ class HotPath:
         # ORB extraction is the longest extraction chain; orb_priority lets its workgroups dispatch ahead of the
         # plane chain's (the tracking tail keeps its high priority)
         self.ext_orb = torch.cuda.Stream(priority=-1 if self.orb_priority else 0)
-        self.ext_planes = torch.cuda.Stream()
+        self.ext_planes = torch.cuda.Stream(priority=-1 if self.planes_priority else 0)
         self.ev_orb = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
