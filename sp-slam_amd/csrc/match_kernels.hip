@@ -539,12 +539,16 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                                                           const LocalWindow* __restrict__ win,
                                                           int32_t* __restrict__ match, int* __restrict__ nmatches) {
     tail_wave_priority();
-    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
+    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)], then claim[cap]
     const int f = blockIdx.x, lane = threadIdx.x;
     const spslam_local_frame& F = frames[f];
     const int n_kp = min(C.counts[f], C.cap), np = min(F.n_points, max_points);
     int32_t* M = match + (size_t)f * C.cap;
     const int words = (C.cap + 31) / 32;
+    // claim[k]: the first lane of the current pass whose acceptance takes keypoint k (~0u: none); replaces a
+    // 64-step shuffle scan per pass with one LDS atomic and two reads
+    uint32_t* claim = taken + words;
+    for (int k = lane; k < n_kp; k += 64) claim[k] = ~0u;
     const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
     for (int k = lane; k < n_kp; k += 64) M[k] = -1;
     for (int wd = lane; wd < words; wd += 64) {
@@ -613,11 +617,17 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
             }
             const bool rescanl = act && nk == 3 && k2 == kNone;
             const bool acc = act && !rescanl && k1 != kNone && ratio_ok(k1, k2, o1, o2);
-            bool conflict = false;
-            for (int j = start; j < m; j++) {
-                const int bj = __shfl(b1, j), aj = __shfl((int)acc, j);
-                if (j < lane && aj && (bj == b1 || (b2 >= 0 && bj == b2))) conflict = true;
-            }
+            // conflict: an earlier accepting lane of this pass takes my best or second-best keypoint
+            if (acc) atomicMin(&claim[b1], (uint32_t)lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const bool conflict = act && k1 != kNone &&
+                                  (claim[b1] < (uint32_t)lane || (b2 >= 0 && claim[b2] < (uint32_t)lane));
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (acc) claim[b1] = ~0u;
             const bool stop = act && (rescanl || (k1 != kNone && conflict));
             const unsigned long long sm = __ballot(stop);
             const int first = sm ? __ffsll((long long)sm) - 1 : m;
@@ -710,7 +720,13 @@ hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, co
     if (max_points > 0)
         hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kLPtsPerBlock - 1) / match::kLPtsPerBlock),
                            dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, win, in_view);
-    hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), (size_t)((cur.cap + 31) / 32) * 4, s,
+    // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
+    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
+    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::local_assign_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)lds_attr;
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), lds, s,
                        frames, points, max_points, cur, g, P, taken_in, win, match, nmatches);
     if (timer) timer->end(kKindLocalMatch, s);
     return hipGetLastError();
