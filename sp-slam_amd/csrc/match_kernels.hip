@@ -216,7 +216,7 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
                                                           int2* __restrict__ pushes, int32_t* __restrict__ match,
                                                           int* __restrict__ nmatches) {
     tail_wave_priority();
-    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)]
+    extern __shared__ uint32_t taken[];  // [ceil(cap / 32)], then claim[cap]
     __shared__ int hist[kHisto];
     __shared__ int ind[3];
     const int f = blockIdx.x, lane = threadIdx.x;
@@ -225,6 +225,10 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     const int n_kp = min(C.counts[f], C.cap), np = min(F.n_points, max_points);
     int32_t* M = match + (size_t)f * C.cap;
     const int words = (C.cap + 31) / 32;
+    // claim[k]: per pass, first the earliest blocking acceptance of keypoint k, then the last committed one
+    // (~0u / 0: none) -- one LDS atomic per lane instead of a 64-step shuffle scan per pass
+    uint32_t* claim = taken + words;
+    for (int k = lane; k < n_kp; k += 64) claim[k] = ~0u;
     for (int k = lane; k < n_kp; k += 64) M[k] = -1;  // fill(mvpMapPoints, NULL)
     for (int k = lane; k < words; k += 64) taken[k] = 0;
     if (lane < kHisto) hist[lane] = 0;
@@ -292,23 +296,32 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             }
             const bool acc = act && !rescanl && keyl != kNone && (int)(keyl >> 20) <= kThHigh;
             const bool accb = acc && blocking;
-            // conflicts with earlier blocking acceptances; the next later acceptance of the same keypoint
-            bool conflict = false;
-            int next_same = 64;
-            for (int j = start; j < m; j++) {
-                const int bj = __shfl(bl, j);
-                const int fj = __shfl((int)acc | ((int)accb << 1), j);
-                if (j < lane && (fj & 2) && bj == bl) conflict = true;
-                if (j > lane && (fj & 1) && bj == bl && next_same == 64) next_same = j;
-            }
+            // conflicts with earlier blocking acceptances (the earliest blocking lane per keypoint)
+            auto wsync = [] {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            };
+            if (accb) atomicMin(&claim[bl], (uint32_t)lane);
+            wsync();
+            const bool conflict = acc && claim[bl] < (uint32_t)lane;
+            wsync();
+            if (acc) claim[bl] = 0u;  // reused below as "last committed lane + 1" (0: none)
+            wsync();
             const bool stop = act && (rescanl || (acc && conflict));
             const unsigned long long sm = __ballot(stop);
             const int first = sm ? __ffsll((long long)sm) - 1 : m;
             const bool commit = acc && lane < first;
             const unsigned long long cm = __ballot(commit);
+            // the last committed assignment of a keypoint wins, as in the reference's order
+            if (commit) atomicMax(&claim[bl], (uint32_t)lane + 1u);
+            wsync();
+            const bool last = commit && claim[bl] == (uint32_t)lane + 1u;
+            wsync();
+            if (acc) claim[bl] = ~0u;
             int bin = 0;
             if (commit) {
-                if (next_same >= first) M[bl] = c0 + lane;  // the last assignment of a keypoint wins, as in order
+                if (last) M[bl] = c0 + lane;
                 if (blocking) atomicOr(&taken[bl >> 5], 1u << (bl & 31));
                 if (check_ori) {
                     float rot = __fsub_rn(pangle, kangl);
@@ -738,7 +751,12 @@ hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const sps
                         KernelTimer* timer) {
     if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
     if (timer) timer->begin(kKindMatch, s);
-    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4;
+    // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
+    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
+    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::match_assign_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    (void)lds_attr;
+    if (lds > 150 * 1024) return hipErrorInvalidValue;
     const int passes = P.retry_below > 0 ? 2 : 1;
     for (int pass = 0; pass < passes; pass++) {
         if (max_points > 0)
