@@ -184,8 +184,19 @@ constexpr int kMaxTrials = 10;   // OptimizationAlgorithmLevenberg: qmax < 10
                               // 256 rows 6.97, 512 rows (146 KB of LDS per problem) 6.80 (profiles/r03/ab_ring*)
 #endif
 constexpr int kRingA = SPSLAM_POSE_RING;
-constexpr int kStrideA = kRed + 1;
-constexpr int kRingPad = 24;       // spare rows past the ring end: chain_seg loads up to 23 rows past a segment
+#ifndef SPSLAM_POSE_STRIDE
+#define SPSLAM_POSE_STRIDE 29  // doubles per pass-A ring row (28 terms + 1: an odd stride spreads the row writes)
+#endif
+constexpr int kStrideA = SPSLAM_POSE_STRIDE;
+static_assert(kStrideA >= kRed, "a ring row holds the 28 terms (lanes past them read any column: never added)");
+#ifndef SPSLAM_POSE_RING_PAD
+#define SPSLAM_POSE_RING_PAD 24
+#endif
+// spare rows past the ring end (chain_seg loads up to 23 rows past a segment; with 0 those loads read the
+// fields that follow the ring in Shared -- never added, and inside the workgroup's allocation)
+constexpr int kRingPad = SPSLAM_POSE_RING_PAD;
+// A smaller footprint (so ORB's level/fast kernels co-reside beside a pose workgroup) did not pay: pipelined C2
+// step 6.66 ms (29/24, 146 KB) vs 6.68 (29/0, 143.5 KB) vs 6.69 (28/0, 139.5 KB), 3 rounds each (profiles/r03/ab_lds_*)
 constexpr int kSpinCap = 1 << 20;  // bound of every wait (s_sleep 1 each: ~30 ms); never reached in a correct run
 
 template <int kSpec>
