@@ -937,7 +937,8 @@ __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) 
     if (k.state != kTrial || !mfma_schur(k) || (mfma_tiles(k) > NT) || (NT > 3 && mfma_tiles(k) < NT)) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n = 6 * k.np, kk = lane >> 4, r16 = lane & 15;
-    const int l0 = task.y + wave * kLbaMfmaLm, nl = min(c.L - l0, kLbaMfmaLm);
+    const int grp = blockIdx.y * kWaves + wave;  // landmark group of the chunk (kLbaChunk / kLbaMfmaLm per chunk)
+    const int l0 = task.y + grp * kLbaMfmaLm, nl = min(c.L - l0, kLbaMfmaLm);
     if (nl <= 0) return;  // partial sets exist for the first ceil(L / kLbaMfmaLm) landmark groups only
     // the group's pose masks and block bases, one landmark per lane (read back with readlane)
     const uint64_t m_l = lane < nl ? c.lm_mask[l0 + lane] : 0ull;
@@ -976,11 +977,23 @@ __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) 
             o.hb[t] = H[6 * kc + q];
         }
     };
-    Ops cur, nxt;
+    Ops cur, nx1, nx2;  // two landmarks' loads in flight beside this one's MFMAs
     load(0, cur);
+    if (nl > 1) load(1, nx1);
     for (int i = 0; i < nl; i++) {
-        if (i + 1 < nl) load(i + 1, nxt);
+        if (i + 2 < nl) load(i + 2, nx2);
         if (__builtin_amdgcn_readlane(b_l, i) >= 0) {  // landmarks without an active edge add nothing
+            // tiles holding a pose that observes the landmark (wave-uniform): a tile pair without one on either
+            // side only adds exact zeros, and only the upper tile triangle is formed (the factorization reads
+            // the upper triangle of S alone)
+            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(m_l >> 32), i) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m_l, i);
+            unsigned tm = 0;
+#pragma unroll
+            for (int t = 0; t < NT; t++) {
+                const int plo = 16 * t / 6, phi = (16 * t + 15) / 6;
+                if ((m >> plo) & ((2ull << (phi - plo)) - 1ull)) tm |= 1u << t;
+            }
             double a[NT], bb[NT];
 #pragma unroll
             for (int t = 0; t < NT; t++) {
@@ -991,17 +1004,19 @@ __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) 
 #pragma unroll
             for (int ti = 0; ti < NT; ti++)
 #pragma unroll
-                for (int tj = 0; tj < NT; tj++)
-                    acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bb[tj], acc[ti][tj], 0, 0, 0);
+                for (int tj = ti; tj < NT; tj++)
+                    if ((tm >> ti) & (tm >> tj) & 1u)
+                        acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bb[tj], acc[ti][tj], 0, 0, 0);
         }
-        cur = nxt;
+        cur = nx1;
+        nx1 = nx2;
     }
     // C/D layout of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
-    double* out = c.S_part + (size_t)((task.y / kLbaChunk) * (kLbaChunk / kLbaMfmaLm) + wave) * NT * NT * 256;
+    double* out = c.S_part + (size_t)((task.y / kLbaChunk) * (kLbaChunk / kLbaMfmaLm) + grp) * NT * NT * 256;
 #pragma unroll
     for (int i = 0; i < NT; i++)
 #pragma unroll
-        for (int j = 0; j < NT; j++)
+        for (int j = i; j < NT; j++)
 #pragma unroll
             for (int g = 0; g < 4; g++) out[(i * NT + j) * 256 + (kk + 4 * g) * 16 + r16] = acc[i][j][g];
 }
@@ -1019,16 +1034,18 @@ __global__ __launch_bounds__(kThreads) void k_schur_reduce(LbaBatch b) {
     if (e >= n * n) return;
     const int r = e / n, q = e - r * n;
     const int p1 = r / 6, p2 = q / 6;
-    if (p1 > p2) return;
+    if (r > q) return;  // the upper triangle (k_schur_mfma forms the upper tiles; the factorization reads no more)
     const size_t o = (size_t)((r >> 4) * NT + (q >> 4)) * 256 + (r & 15) * 16 + (q & 15);
     const double* src = c.S_part + o;
     const size_t stride = (size_t)NT * NT * 256;
     double v = 0.0;
     int s = 0;
-    for (; s + 4 <= nparts; s += 4) {  // four loads in flight, summed in order
-        const double x0 = src[s * stride], x1 = src[(s + 1) * stride], x2 = src[(s + 2) * stride],
-                     x3 = src[(s + 3) * stride];
-        v += x0; v += x1; v += x2; v += x3;
+    for (; s + 8 <= nparts; s += 8) {  // eight loads in flight, summed in order
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) x[u] = src[(s + u) * stride];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v += x[u];
     }
     for (; s < nparts; s++) v += src[s * stride];
     const int rr = r - 6 * p1, qq = q - 6 * p2;
@@ -1159,15 +1176,137 @@ __device__ __forceinline__ void factor_body(const Ctx& c, LbaCtl& k, double* lds
     if (t == 0) k.ok = ok;
 }
 
+// Reduced systems of n <= 64 kC rows with the upper triangle in registers: row r on wave r % 4 (register slot
+// r / 4), column q on lane q % 64 (column register q / 64).  Column j: the wave holding row j forms
+// L(:, j) = A(j, :) / d_j into LDS (column-major LT, the substitutions' L) and d_j; one barrier; every wave
+// loads the column once and updates all its rows, A(r, q) -= (L(q, j) d_j) L(r, j) -- the same per-entry
+// expression, in the same column order, as factor_body (rows <= j and lanes q < r carry dead values, never
+// read).  One barrier and about one LDS round trip per column instead of a chain of LDS read-modify-writes.
+// The substitutions run on wave 0, y in registers (lane i, i + 64), y_k broadcast by readlane.
+template <int kC>
+__device__ __forceinline__ void factor_reg(const Ctx& c, LbaCtl& k, double* lds, int n) {
+    constexpr int kR = 16 * kC;  // rows per wave (n <= 64 kC)
+    // w through readfirstlane: the compiler then sees every row test as wave-uniform (scalar branches)
+    const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+    double* LT = lds;                    // LT[j n + i] = L(i, j), i > j
+    double* dd = lds + (size_t)n * n;    // d_j
+    double A[kR][kC];
+#pragma unroll
+    for (int s = 0; s < kR; s++)
+#pragma unroll
+        for (int cc = 0; cc < kC; cc++) {
+            const int r = 4 * s + w, q = 64 * cc + lane;
+            A[s][cc] = r < n && q < n ? c.S[(size_t)r * n + q] : 0.0;
+        }
+    auto rl = [&](double v, int l) __attribute__((always_inline)) {
+        const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+        const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+        return __hiloint2double(hi, lo);
+    };
+    // the wave holding row j: L(:, j) and d_j (row j is final once column j - 1's update is done)
+    auto form = [&](int j) __attribute__((always_inline)) {
+        if ((j & 3) != w) return;
+#pragma unroll
+        for (int s = 0; s < kR; s++)
+            if (4 * s + w == j) {
+                double dj = 0.0;
+#pragma unroll
+                for (int cc = 0; cc < kC; cc++)
+                    if ((j >> 6) == cc) dj = rl(A[s][cc], j & 63);
+                if (dj != 0.0)
+#pragma unroll
+                    for (int cc = 0; cc < kC; cc++) {
+                        const int q = 64 * cc + lane;
+                        if (q > j && q < n) LT[(size_t)j * n + q] = A[s][cc] / dj;
+                    }
+                if (lane == 0) dd[j] = dj;
+            }
+    };
+    form(0);
+    __syncthreads();
+    bool ok = true;
+    for (int j = 0; j < n; j++) {
+        const double* col = LT + (size_t)j * n;
+        // every load of the column first (one LDS round trip, d_j with it), then the updates; all rows and lanes
+        // are updated (rows <= j, rows >= n and lanes q < r hold dead values; the loads past the column stay
+        // inside the workgroup's LDS)
+        double P[kC], lr[kR];
+#pragma unroll
+        for (int cc = 0; cc < kC; cc++) P[cc] = col[64 * cc + lane];
+#pragma unroll
+        for (int s = 0; s < kR; s++) lr[s] = col[4 * s + w];
+        const double dj = dd[j];
+        if (dj == 0.0) { ok = false; break; }
+        if (j + 1 == n) break;
+#pragma unroll
+        for (int cc = 0; cc < kC; cc++) P[cc] = P[cc] * dj;
+#pragma unroll
+        for (int s = 0; s < kR; s++)
+#pragma unroll
+            for (int cc = 0; cc < kC; cc++) A[s][cc] = A[s][cc] - P[cc] * lr[s];
+        form(j + 1);
+        __syncthreads();
+    }
+    if (t < 64) {
+        double y[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) y[m] = 64 * m + lane < n ? c.bs[64 * m + lane] : 0.0;
+        if (ok) {
+            // forward: y[i] -= L[i][k] y[k], k increasing (column k + 1 loaded during step k)
+            double a[kC], an[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) a[m] = 64 * m + lane < n ? LT[64 * m + lane] : 0.0;
+#pragma unroll
+            for (int mb = 0; mb < kC; mb++)  // y_k lives in register mb of lane k & 63
+                for (int kk = 64 * mb; kk < n && kk < 64 * mb + 64; kk++) {
+#pragma unroll
+                    for (int m = 0; m < kC; m++)
+                        an[m] = kk + 1 < n && 64 * m + lane < n ? LT[(size_t)(kk + 1) * n + 64 * m + lane] : 0.0;
+                    const double yk = rl(y[mb], kk & 63);
+#pragma unroll
+                    for (int m = 0; m < kC; m++)
+                        if (64 * m + lane > kk && 64 * m + lane < n) y[m] -= a[m] * yk;
+#pragma unroll
+                    for (int m = 0; m < kC; m++) a[m] = an[m];
+                }
+#pragma unroll
+            for (int m = 0; m < kC; m++)
+                if (64 * m + lane < n) y[m] /= dd[64 * m + lane];
+            // backward: y[i] -= L[k][i] y[k], k decreasing (L[k][i] = LT[i n + k])
+#pragma unroll
+            for (int m = 0; m < kC; m++) a[m] = 64 * m + lane < n - 1 ? LT[(size_t)(64 * m + lane) * n + n - 1] : 0.0;
+#pragma unroll
+            for (int mb = kC - 1; mb >= 0; mb--)
+                for (int kk = min(n, 64 * mb + 64) - 1; kk >= 64 * mb; kk--) {
+#pragma unroll
+                    for (int m = 0; m < kC; m++)
+                        an[m] = kk > 0 && 64 * m + lane < kk - 1 ? LT[(size_t)(64 * m + lane) * n + kk - 1] : 0.0;
+                    const double yk = rl(y[mb], kk & 63);
+#pragma unroll
+                    for (int m = 0; m < kC; m++)
+                        if (64 * m + lane < kk) y[m] -= a[m] * yk;
+#pragma unroll
+                    for (int m = 0; m < kC; m++) a[m] = an[m];
+                }
+#pragma unroll
+            for (int m = 0; m < kC; m++)
+                if (64 * m + lane < n) c.y[64 * m + lane] = y[m];
+        }
+        if (t == 0) k.ok = ok;
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_factor(LbaBatch b) {
     extern __shared__ double lds[];
     Ctx c = make_ctx(b, blockIdx.x);
     LbaCtl& k = *c.ctl;
     if (k.state != kTrial) return;
     const int n = 6 * k.np;
-    // (measured: the same factorization on one wave with wave-level synchronisation took twice as long -- the
-    // trailing updates' LDS latency, not the barriers, bounds it)
-    if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds) factor_body<true>(c, k, lds, n);
+    // (measured alone, tools/factor_micro.hip: LDS-resident right-looking updates cost a chain of LDS round
+    // trips per column, ~1 us per column; one wave with wave-level synchronisation was slower still)
+    if (n <= 64) factor_reg<1>(c, k, lds, n);
+    else if (n <= 128) factor_reg<2>(c, k, lds, n);
+    else if ((size_t)n * n * 8 + 3 * (size_t)n * 8 <= (size_t)kFactorLds) factor_body<true>(c, k, lds, n);
     else factor_body<false>(c, k, lds, n);
 }
 
@@ -1450,9 +1589,10 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
         hipLaunchKernelGGL(k_pose_sums, dim3(w.n_kf_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_iter_begin, dim3(P), dim3(64), 0, s, b);
         hipLaunchKernelGGL(k_schur_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);
-        hipLaunchKernelGGL(k_schur_mfma<3>, dim3(w.n_lm_chunks), T, 0, s, b, w);
-        hipLaunchKernelGGL(k_schur_mfma<4>, dim3(w.n_lm_chunks), T, 0, s, b, w);
-        hipLaunchKernelGGL(k_schur_mfma<5>, dim3(w.n_lm_chunks), T, 0, s, b, w);
+        const dim3 G(w.n_lm_chunks, kLbaChunk / (kWaves * kLbaMfmaLm));
+        hipLaunchKernelGGL(k_schur_mfma<3>, G, T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_mfma<4>, G, T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_mfma<5>, G, T, 0, s, b, w);
         hipLaunchKernelGGL(k_schur_reduce, dim3(P, (80 * 80 + kThreads - 1) / kThreads), T, 0, s, b);
         hipLaunchKernelGGL(k_schur_pairs, dim3(w.n_pair_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_factor, dim3(P), T, kFactorLds, s, b);

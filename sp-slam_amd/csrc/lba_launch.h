@@ -13,7 +13,7 @@ constexpr int kLbaCon = 57;            // per-edge terms: Hll 9, bl 3, Hpl 18 (3
 // Schur complement on the matrix cores (v_mfma_f64_16x16x4): reduced systems of up to kLbaMfmaTiles x 16 rows
 // (6 * free poses <= 80); larger ones use the pose-pair kernel.  One partial 16x16-tile set per 64 landmarks.
 constexpr int kLbaMfmaTiles = 5;
-constexpr int kLbaMfmaLm = 64;
+constexpr int kLbaMfmaLm = 32;  // landmarks per k_schur_mfma wave (per partial tile set)
 
 // LM / schedule state of one problem (device, in its scratch); see lba_kernels.hip.
 struct LbaCtl {
