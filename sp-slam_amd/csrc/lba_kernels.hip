@@ -928,6 +928,11 @@ __global__ __launch_bounds__(kThreads) void k_schur_lm(LbaBatch b, LbaWork w) {
 // does not observe the landmark) and B[k l >> 4][col l & 15] = the block's H entry.  Each wave takes
 // kLbaMfmaLm landmarks of its workgroup's landmark chunk and writes its tiles to S_part; k_schur_reduce sums
 // the partial sets in a fixed order.
+// per-wave LDS batch (doubles): Dinv of up to kLbaMfmaLm landmarks (9 each), their bl (3 each), then blocks
+constexpr int kStageB = 9 * kLbaMfmaLm, kStageH = 12 * kLbaMfmaLm, kStageD = 2048;
+constexpr int kStageBlocks = (kStageD - kStageH) / 18;  // 92; the 1 KiB pieces round up within kStageD
+static_assert(kStageH + ((18 * kStageBlocks * 8 + 1023) / 1024) * 128 <= kStageD, "block pieces fit the buffer");
+static_assert(9 * kLbaMfmaLm * 8 <= 256 * 9 && 3 * kLbaMfmaLm * 8 <= 256 * 3, "Dinv / bl pieces");
 template <int NT>
 __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) {
     typedef double d4 __attribute__((ext_vector_type(4)));
@@ -943,11 +948,13 @@ __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) 
     // the group's pose masks and block bases, one landmark per lane (read back with readlane)
     const uint64_t m_l = lane < nl ? c.lm_mask[l0 + lane] : 0ull;
     const int b_l = lane < nl ? lm_block_base(c, l0 + lane) : -1;
-    d4 acc[NT][NT];
+    d4 acc[NT][NT], accb[NT];  // accb: the right-hand side sum_l (B Dinv)_l bl_l (B operand column 0 = bl)
 #pragma unroll
-    for (int i = 0; i < NT; i++)
+    for (int i = 0; i < NT; i++) {
+        accb[i] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < NT; j++) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    }
     // this lane's pose and component in every tile row / column
     int pose_t[NT], comp_t[NT];
 #pragma unroll
@@ -956,73 +963,129 @@ __global__ __launch_bounds__(kThreads) void k_schur_mfma(LbaBatch b, LbaWork w) 
         pose_t[t] = r < n ? r / 6 : 63;
         comp_t[t] = r - 6 * (r / 6);
     }
-    // one landmark's operands: Dinv column kk and, per tile, the three H entries of (B Dinv)(row, kk) and
-    // B^T(kk, col).  Loads are unconditional (a lane that does not observe reads the landmark's first block)
-    // so the next landmark's loads can be issued before this one's MFMAs.
-    struct Ops { double d[3]; double h[NT][3]; double hb[NT]; bool obs[NT]; };
-    auto load = [&](int i, Ops& o) __attribute__((always_inline)) {
+    // The group's operands are staged in LDS by LDS-DMA (global_load_lds: no VGPRs, every piece in flight at
+    // once) in batches of consecutive landmarks whose (landmark, pose) blocks fit the wave's buffer: the blocks of
+    // consecutive landmarks are contiguous (k_struct_final), so a batch is one contiguous range of blocks plus the
+    // landmarks' Dinv and bl.  The landmark loop then reads LDS (a round trip of ~100 cycles instead of a global
+    // load's ~1 us per landmark).
+    __shared__ __attribute__((aligned(16))) double stage[kWaves][kStageD];
+    double* st = stage[wave];
+    const int nb_l = b_l >= 0 ? __popcll(m_l) : 0;  // blocks of this lane's landmark
+    int incl = nb_l;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+    }
+    const int excl = incl - nb_l;
+    const uint64_t actv = __ballot(b_l >= 0);
+    const int f = actv ? __ffsll((unsigned long long)actv) - 1 : 0;
+    const int G = __builtin_amdgcn_readlane(b_l, f) - __builtin_amdgcn_readlane(excl, f);  // the group's first block
+    const int kc = kk < 3 ? kk : 0;
+    // one landmark's operands from the staged batch (rel = its index in the batch, bx = its first block there)
+    struct Ops { double d[3]; double h[NT][3]; double hb[NT]; bool obs[NT]; double bl; };
+    auto load = [&](int i, int rel, int bx, Ops& o) __attribute__((always_inline)) {
         const int bl = __builtin_amdgcn_readlane(b_l, i);
         const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(m_l >> 32), i) << 32) |
                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m_l, i);
-        const int kc = kk < 3 ? kk : 0;
-        const double* Di = c.Dinv + 9 * (size_t)(l0 + i);
+        const double* Di = st + 9 * rel;
         o.d[0] = Di[kc]; o.d[1] = Di[3 + kc]; o.d[2] = Di[6 + kc];
+        o.bl = st[kStageB + 3 * rel + kc];
 #pragma unroll
         for (int t = 0; t < NT; t++) {
             const int p = pose_t[t], q = comp_t[t];
             o.obs[t] = bl >= 0 && kk < 3 && p < 64 && ((m >> p) & 1ull);
-            const int blk = o.obs[t] ? bl + __popcll(m & ((1ull << p) - 1ull)) : (bl >= 0 ? bl : 0);
-            const double* H = c.blkH + (size_t)blk * 18;
+            const int blk = o.obs[t] ? bx + __popcll(m & ((1ull << p) - 1ull)) : 0;
+            const double* H = st + kStageH + 18 * blk;
             o.h[t][0] = H[q]; o.h[t][1] = H[6 + q]; o.h[t][2] = H[12 + q];
             o.hb[t] = H[6 * kc + q];
         }
     };
-    Ops cur, nx1, nx2;  // two landmarks' loads in flight beside this one's MFMAs
-    load(0, cur);
-    if (nl > 1) load(1, nx1);
-    for (int i = 0; i < nl; i++) {
-        if (i + 2 < nl) load(i + 2, nx2);
-        if (__builtin_amdgcn_readlane(b_l, i) >= 0) {  // landmarks without an active edge add nothing
-            // tiles holding a pose that observes the landmark (wave-uniform): a tile pair without one on either
-            // side only adds exact zeros, and only the upper tile triangle is formed (the factorization reads
-            // the upper triangle of S alone)
-            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(m_l >> 32), i) << 32) |
-                               (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m_l, i);
-            unsigned tm = 0;
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    int start = 0;
+    while (start < nl) {  // wave-uniform
+        const int e0 = __builtin_amdgcn_readlane(excl, start);
+        const uint64_t fit = __ballot(lane >= start && lane < nl && incl - e0 <= kStageBlocks);
+        const int cnt = __popcll(fit), end = start + cnt;  // >= 1: a landmark has at most 64 blocks
+        const int nblk = __builtin_amdgcn_readlane(incl, end - 1) - e0;
+        const char* gD = (const char*)(c.Dinv + 9 * (size_t)(l0 + start));
+        const char* gb = (const char*)(c.lmb + 3 * (size_t)(l0 + start));
+        const char* gH = (const char*)(c.blkH + 18 * (size_t)(G + e0));
+        char* sD = (char*)st;
+        char* sb = (char*)(st + kStageB);
+        char* sH = (char*)(st + kStageH);
 #pragma unroll
-            for (int t = 0; t < NT; t++) {
-                const int plo = 16 * t / 6, phi = (16 * t + 15) / 6;
-                if ((m >> plo) & ((2ull << (phi - plo)) - 1ull)) tm |= 1u << t;
+        for (int p = 0; p < 9; p++)  // Dinv: 72 cnt bytes, 256 per piece
+            if (256 * p < 72 * cnt && 256 * p + 4 * lane < 72 * cnt)
+                __builtin_amdgcn_global_load_lds((const void*)(gD + 256 * p + 4 * lane), (lds_ptr)(sD + 256 * p), 4, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 3; p++)  // bl: 24 cnt bytes
+            if (256 * p < 24 * cnt && 256 * p + 4 * lane < 24 * cnt)
+                __builtin_amdgcn_global_load_lds((const void*)(gb + 256 * p + 4 * lane), (lds_ptr)(sb + 256 * p), 4, 0, 0);
+#pragma unroll
+        for (int p = 0; p < 13; p++)  // blocks: 144 nblk bytes, 1 KiB per piece
+            if (1024 * p < 144 * nblk && 1024 * p + 16 * lane < 144 * nblk)
+                __builtin_amdgcn_global_load_lds((const void*)(gH + 1024 * p + 16 * lane), (lds_ptr)(sH + 1024 * p), 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt(0);  // the pieces have landed
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        Ops cur, nxt;  // the next landmark's LDS reads in flight beside this one's MFMAs
+        load(start, 0, 0, cur);
+        for (int i = start; i < end; i++) {
+            if (i + 1 < end) load(i + 1, i + 1 - start, __builtin_amdgcn_readlane(excl, i + 1) - e0, nxt);
+            if (__builtin_amdgcn_readlane(b_l, i) >= 0) {  // landmarks without an active edge add nothing
+                // tiles holding a pose that observes the landmark (wave-uniform): a tile pair without one on either
+                // side only adds exact zeros, and only the upper tile triangle is formed (the factorization reads
+                // the upper triangle of S alone)
+                const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(m_l >> 32), i) << 32) |
+                                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m_l, i);
+                unsigned tm = 0;
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    const int plo = 16 * t / 6, phi = (16 * t + 15) / 6;
+                    if ((m >> plo) & ((2ull << (phi - plo)) - 1ull)) tm |= 1u << t;
+                }
+                double a[NT], bb[NT];
+#pragma unroll
+                for (int t = 0; t < NT; t++) {
+                    // (B Dinv)(row, kk): the pose-pair kernel's formula
+                    a[t] = cur.obs[t] ? (cur.h[t][0] * cur.d[0] + cur.h[t][1] * cur.d[1]) + cur.h[t][2] * cur.d[2] : 0.0;
+                    bb[t] = cur.obs[t] ? cur.hb[t] : 0.0;
+                }
+                const double bv = r16 == 0 && kk < 3 ? cur.bl : 0.0;
+#pragma unroll
+                for (int ti = 0; ti < NT; ti++) {
+#pragma unroll
+                    for (int tj = ti; tj < NT; tj++)
+                        if ((tm >> ti) & (tm >> tj) & 1u)
+                            acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bb[tj], acc[ti][tj], 0, 0, 0);
+                    if ((tm >> ti) & 1u) accb[ti] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bv, accb[ti], 0, 0, 0);
+                }
             }
-            double a[NT], bb[NT];
-#pragma unroll
-            for (int t = 0; t < NT; t++) {
-                // (B Dinv)(row, kk): the pose-pair kernel's formula
-                a[t] = cur.obs[t] ? (cur.h[t][0] * cur.d[0] + cur.h[t][1] * cur.d[1]) + cur.h[t][2] * cur.d[2] : 0.0;
-                bb[t] = cur.obs[t] ? cur.hb[t] : 0.0;
-            }
-#pragma unroll
-            for (int ti = 0; ti < NT; ti++)
-#pragma unroll
-                for (int tj = ti; tj < NT; tj++)
-                    if ((tm >> ti) & (tm >> tj) & 1u)
-                        acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ti], bb[tj], acc[ti][tj], 0, 0, 0);
+            cur = nxt;
         }
-        cur = nx1;
-        nx1 = nx2;
+        // every LDS read of the batch has returned before the next batch's pieces overwrite the buffer
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        start = end;
     }
     // C/D layout of the f64 16x16x4 form: col = lane & 15, row = (lane >> 4) + 4 * reg
-    double* out = c.S_part + (size_t)((task.y / kLbaChunk) * (kLbaChunk / kLbaMfmaLm) + grp) * NT * NT * 256;
+    double* out = c.S_part + (size_t)((task.y / kLbaChunk) * (kLbaChunk / kLbaMfmaLm) + grp) * lba_part_doubles(NT);
 #pragma unroll
-    for (int i = 0; i < NT; i++)
+    for (int i = 0; i < NT; i++) {
 #pragma unroll
         for (int j = i; j < NT; j++)
 #pragma unroll
             for (int g = 0; g < 4; g++) out[(i * NT + j) * 256 + (kk + 4 * g) * 16 + r16] = acc[i][j][g];
+        if (r16 == 0)
+#pragma unroll
+            for (int g = 0; g < 4; g++) out[NT * NT * 256 + i * 16 + kk + 4 * g] = accb[i][g];
+    }
 }
 
-// S(p1, p2) = Hpp + lambda - sum of the partial tile sets (in landmark-group order) for p1 <= p2.  Grid:
-// (problem, 256-entry slice of the n x n system).
+// S(r, q) = Hpp + lambda - sum of the partial tile sets (in landmark-group order) for r <= q, and
+// bs = bp - sum of the partial right-hand sides.  Grid: (problem, 256-entry slice of the n x n + n entries).
 __global__ __launch_bounds__(kThreads) void k_schur_reduce(LbaBatch b) {
     Ctx c = make_ctx(b, blockIdx.x);
     const LbaCtl& k = *c.ctl;
@@ -1031,13 +1094,14 @@ __global__ __launch_bounds__(kThreads) void k_schur_reduce(LbaBatch b) {
     const int NT = ntr < 3 ? 3 : ntr;  // the tile count of the k_schur_mfma instance that served this problem
     const int nparts = (c.L + kLbaMfmaLm - 1) / kLbaMfmaLm;
     const int e = blockIdx.y * kThreads + threadIdx.x;
-    if (e >= n * n) return;
-    const int r = e / n, q = e - r * n;
+    if (e >= n * n + n) return;
+    const bool rhs = e >= n * n;  // entries n^2 .. n^2 + n - 1: the reduced right-hand side bs
+    const int r = rhs ? e - n * n : e / n, q = rhs ? 0 : e - r * n;
     const int p1 = r / 6, p2 = q / 6;
-    if (r > q) return;  // the upper triangle (k_schur_mfma forms the upper tiles; the factorization reads no more)
-    const size_t o = (size_t)((r >> 4) * NT + (q >> 4)) * 256 + (r & 15) * 16 + (q & 15);
+    if (!rhs && r > q) return;  // the upper triangle (k_schur_mfma forms the upper tiles; the factorization reads no more)
+    const size_t o = rhs ? (size_t)NT * NT * 256 + r : (size_t)((r >> 4) * NT + (q >> 4)) * 256 + (r & 15) * 16 + (q & 15);
     const double* src = c.S_part + o;
-    const size_t stride = (size_t)NT * NT * 256;
+    const size_t stride = lba_part_doubles(NT);
     double v = 0.0;
     int s = 0;
     for (; s + 8 <= nparts; s += 8) {  // eight loads in flight, summed in order
@@ -1048,6 +1112,10 @@ __global__ __launch_bounds__(kThreads) void k_schur_reduce(LbaBatch b) {
         for (int u = 0; u < 8; u++) v += x[u];
     }
     for (; s < nparts; s++) v += src[s * stride];
+    if (rhs) {
+        c.bs[r] = c.bp[r] - v;
+        return;
+    }
     const int rr = r - 6 * p1, qq = q - 6 * p2;
     const double base = p1 == p2 ? c.Hpp[36 * p1 + 6 * rr + qq] + (rr == qq ? k.lambda : 0.0) : 0.0;
     c.S[(size_t)r * n + q] = base - v;
@@ -1065,7 +1133,7 @@ __global__ __launch_bounds__(kThreads) void k_schur_pairs(LbaBatch b, LbaWork w)
     // task.y < 0: the reduced right-hand side of free pose -task.y - 1
     const int np = k.np, n = 6 * np, npairs = np * (np + 1) / 2, tid = task.y;
     if (tid >= npairs || (tid < 0 && -tid - 1 >= np)) return;
-    if (tid >= 0 && mfma_schur(k)) return;
+    if (mfma_schur(k)) return;  // k_schur_mfma + k_schur_reduce form S and bs
     if (tid >= 0) {
         int p1 = 0, rem = tid;
         while (rem >= np - p1) { rem -= np - p1; p1++; }
@@ -1593,8 +1661,8 @@ hipError_t lba_run(const LbaBatch& b, const LbaWork& w, const LbaConsts& C, int 
         hipLaunchKernelGGL(k_schur_mfma<3>, G, T, 0, s, b, w);
         hipLaunchKernelGGL(k_schur_mfma<4>, G, T, 0, s, b, w);
         hipLaunchKernelGGL(k_schur_mfma<5>, G, T, 0, s, b, w);
-        hipLaunchKernelGGL(k_schur_reduce, dim3(P, (80 * 80 + kThreads - 1) / kThreads), T, 0, s, b);
-        hipLaunchKernelGGL(k_schur_pairs, dim3(w.n_pair_tasks), T, 0, s, b, w);
+        hipLaunchKernelGGL(k_schur_reduce, dim3(P, (80 * 80 + 80 + kThreads - 1) / kThreads), T, 0, s, b);
+        if (w.n_pair_tasks) hipLaunchKernelGGL(k_schur_pairs, dim3(w.n_pair_tasks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_factor, dim3(P), T, kFactorLds, s, b);
         hipLaunchKernelGGL(k_update_lm, dim3(w.n_lm_chunks), T, 0, s, b, w);
         hipLaunchKernelGGL(k_update_pose, dim3(w.n_kf_tasks), dim3(64), 0, s, b, w);

@@ -37,6 +37,8 @@ struct LbaLayout {
 };
 
 __host__ __device__ inline int lba_chunks(int n) { return (n + kLbaChunk - 1) / kLbaChunk; }
+// one k_schur_mfma partial set: NT x NT tiles of 16 x 16 (the upper ones written) + the right-hand side (16 NT)
+__host__ __device__ inline size_t lba_part_doubles(int nt) { return (size_t)nt * nt * 256 + (size_t)nt * 16; }
 
 __host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
     LbaLayout L{};
@@ -59,7 +61,7 @@ __host__ __device__ inline LbaLayout lba_layout(int K, int Np, int Nq, int E) {
     // np <= K free poses
     size_t nt = (n6 + 15) / 16;
     nt = nt < 3 ? 3 : (nt > (size_t)kLbaMfmaTiles ? (size_t)kLbaMfmaTiles : nt);
-    L.S_part = take(((Lm + kLbaMfmaLm - 1) / kLbaMfmaLm) * nt * nt * 256 * 8);
+    L.S_part = take(((Lm + kLbaMfmaLm - 1) / kLbaMfmaLm) * lba_part_doubles((int)nt) * 8);
     L.pose_hidx = take(K * 4); L.hidx_pose = take(K * 4);
     L.e_lm = take((size_t)E * 4); L.e_kf = take((size_t)E * 4); L.e_type = take((size_t)E * 4);
     L.e_level = take((size_t)E * 4); L.e_blk = take((size_t)E * 4); L.e_src = take((size_t)E * 4);

@@ -1025,11 +1025,12 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         for (int l = 0; l < L; l += kLbaChunk) lc.push_back(int2{i, l});
         for (int k = 0; k < p.n_kf; k++) kt.push_back(int2{i, k});
         const int npmax = p.n_kf;  // bound on the free poses; surplus tasks exit on the device
-        // pose-pair Schur tasks only where the reduced system may exceed the matrix-core path (6 np > 16 x
-        // kLbaMfmaTiles rows); the right-hand-side tasks (encoded -(p + 1)) always
-        if (6 * npmax > 16 * kLbaMfmaTiles)
+        // pose-pair and right-hand-side Schur tasks (the latter encoded -(p + 1)) only where the reduced system
+        // may exceed the matrix-core path (6 np > 16 x kLbaMfmaTiles rows), which forms both
+        if (6 * npmax > 16 * kLbaMfmaTiles) {
             for (int q = 0; q < npmax * (npmax + 1) / 2; q++) pt.push_back(int2{i, q});
-        for (int q = 0; q < npmax; q++) pt.push_back(int2{i, -(q + 1)});
+            for (int q = 0; q < npmax; q++) pt.push_back(int2{i, -(q + 1)});
+        }
         for (int q = 0; q < p.n_plane_obs; q += kLbaPlaneEdgesPerTask) qt.push_back(int2{i, p.n_point_obs + q});
         for (int e = 0; e < p.n_point_obs; e += seg_own) sg.push_back(int2{i, e});
         for (int q = 0; q < p.n_planes; q += kLbaChunk / 64) pm.push_back(int2{i, p.n_points + q});
