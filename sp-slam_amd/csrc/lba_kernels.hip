@@ -266,6 +266,13 @@ __device__ int block_scan(int v, int* total, Red& R) {
 }
 
 __device__ __forceinline__ int lm_block_base(const Ctx& c, int l) { return c.lm_act[l] - 1; }
+// e_blk: the edge's (landmark, pose) block, -1 if none; kBlkShared marks the edges of a landmark with two active
+// edges on one block (summed by the landmark's owner in edge order, not stored per edge)
+constexpr int kBlkShared = 1 << 30;
+__device__ __forceinline__ int edge_block(const Ctx& c, int e) {
+    const int v = c.e_blk[e];
+    return v < 0 ? -1 : (v & (kBlkShared - 1));
+}
 
 // Edge Jacobians: A (landmark, dim x 3), B (pose, dim x 6); fixed vertices skipped.
 // kOnly: 0 = any edge, 1 = point edges only, 2 = plane edges only (the caller filtered the type; instances
@@ -483,7 +490,7 @@ __global__ __launch_bounds__(kThreads) void k_struct_final(LbaBatch b) {
     for (int ch = 0; ch < c.L; ch += kThreads) {
         const int l = ch + t;
         uint64_t mask = 0;
-        bool act = false;
+        bool act = false, dup = false;
         int e_beg = 0, e_end = 0;
         if (l < c.L) {
             e_beg = c.lm_boff[l];
@@ -493,7 +500,10 @@ __global__ __launch_bounds__(kThreads) void k_struct_final(LbaBatch b) {
             if (c.e_level[e] == 0) {
                 act = true;
                 const int h = hidx[c.e_kf[e]];
-                if (h >= 0) mask |= 1ull << h;
+                if (h >= 0) {
+                    dup |= (mask >> h) & 1ull;  // two active edges on one (landmark, pose) block
+                    mask |= 1ull << h;
+                }
             }
         const int nb = __popcll(mask);
         int tot;
@@ -503,7 +513,9 @@ __global__ __launch_bounds__(kThreads) void k_struct_final(LbaBatch b) {
             c.lm_act[l] = act ? off + 1 : 0;
             for (int e = e_beg; e < e_end; e++) {
                 const int h = hidx[c.e_kf[e]];
-                c.e_blk[e] = (c.e_level[e] == 0 && h >= 0) ? off + __popcll(mask & ((1ull << h) - 1)) : -1;
+                c.e_blk[e] = (c.e_level[e] == 0 && h >= 0)
+                                 ? (off + __popcll(mask & ((1ull << h) - 1))) | (dup ? kBlkShared : 0)
+                                 : -1;
             }
         }
         base += tot;
@@ -672,14 +684,18 @@ __global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w,
 
 // Point edges and point landmarks in one pass (the point part of k_lm_sums, without a per-edge kernel before
 // it): a workgroup computes the quadratic-form terms of 256 consecutive point edges, one edge per thread
-// (edge_jacobians<1> and store_terms' formulas), and keeps the landmark-side terms (Hll 9, bl 3, Hpl 18) in LDS; a landmark's edges
-// are consecutive and at most kLbaMaxKeyframes, so the workgroup owns the landmarks whose first edge lies in
-// its first w.seg_own edges and finds all their edges in LDS (the remaining rows are the halo).  Each owned
+// (edge_jacobians<1> and store_terms' formulas).  Each edge's (landmark, pose) block (Hpl, 18) goes straight to
+// memory from its thread -- the block's only term -- and its landmark terms (Hll 9, bl 3) to LDS; a landmark's
+// edges are consecutive and at most kLbaMaxKeyframes, so the workgroup owns the landmarks whose first edge lies
+// in its first w.seg_own edges and finds all their edges in LDS (the remaining rows are the halo).  Each owned
 // landmark is summed by the thread of its first edge in insertion order, exactly as k_lm_sums sums the stored
-// terms; only the pose-side terms (Hpp 21, bp 6) still go to memory, for k_pose_sums.  Same values as storing
-// every term per edge and summing the stored terms, without the 456-byte per-edge round trip.
-constexpr int kSegStride = 31;  // odd stride in doubles
-__global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWork w, LbaConsts C) {
+// terms; a landmark with two active edges on one block (kBlkShared) has its blocks summed by the owner in edge
+// order from recomputed terms.  Only the pose-side terms (Hpp 21, bp 6) still go to memory, for k_pose_sums.
+constexpr int kSegStride = 13;  // odd stride in doubles (12 landmark terms)
+#ifndef SPSLAM_LBA_PT_WAVES
+#define SPSLAM_LBA_PT_WAVES 3  // waves per SIMD asked of k_point_terms_sums (3: no spills; 4 spills 28 VGPRs)
+#endif
+__global__ __launch_bounds__(kThreads, SPSLAM_LBA_PT_WAVES) void k_point_terms_sums(LbaBatch b, LbaWork w, LbaConsts C) {
     __shared__ Red R;
     __shared__ double Tm[kThreads * kSegStride];
     __shared__ uint8_t act[kThreads];
@@ -688,9 +704,9 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
     const LbaCtl& k = *c.ctl;
     if (k.state != kIter) return;
     const int t = threadIdx.x, e = task.y + t;
-    // the landmark-side terms (30) of active point edge ee into row[]; its pose-side terms (27) to memory when
-    // write_pose (each edge's by the workgroup that owns it)
-    auto land_terms = [&](int ee, double* row, bool write_pose) __attribute__((always_inline)) {
+    // the landmark-side terms of active point edge ee into row[] (12, or all 30 with the block's when full); when
+    // own (each edge's by the workgroup that owns it): its pose-side terms (27) and, unless shared, its block
+    auto land_terms = [&](int ee, double* row, bool own, bool full) __attribute__((always_inline)) {
         const int ty = c.e_type[ee];
         const bool pfree = c.pose_hidx[c.e_kf[ee]] >= 0;
         double A[3][3] = {}, B[3][6] = {};
@@ -709,6 +725,9 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
                 om[r] = -(info[r] * err[r]);
                 if (k.robust) om[r] *= wgt;
             }
+        const int bkv = c.e_blk[ee];
+        const bool blk_here = own && bkv >= 0 && !(bkv & kBlkShared);
+        double* hb = c.blkH + (size_t)(bkv & (kBlkShared - 1)) * 18;
 #pragma unroll
         for (int i = 0; i < 3; i++) {
             row[9 + i] = (A[0][i] * om[0] + A[1][i] * om[1]) + A[2][i] * om[2];
@@ -716,12 +735,15 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
             for (int j = 0; j < 3; j++)
                 row[3 * i + j] = ((A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j]) + (A[2][i] * W[2]) * A[2][j];
 #pragma unroll
-            for (int j = 0; j < 6; j++)
-                row[12 + 6 * i + j] = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
-                                                  (A[2][i] * W[2]) * B[2][j]
-                                            : 0.0;
+            for (int j = 0; j < 6; j++) {
+                const double v = pfree ? ((A[0][i] * W[0]) * B[0][j] + (A[1][i] * W[1]) * B[1][j]) +
+                                             (A[2][i] * W[2]) * B[2][j]
+                                       : 0.0;
+                if (full) row[12 + 6 * i + j] = v;
+                if (blk_here) hb[6 * i + j] = v;
+            }
         }
-        if (pfree && write_pose) {
+        if (pfree && own) {
             double* o = c.con + (size_t)kLbaCon * ee;
             int q = 30;
 #pragma unroll
@@ -734,7 +756,12 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
         }
     };
     const bool a = e < c.Ep && c.e_level[e] == 0;
-    if (a) land_terms(e, Tm + t * kSegStride, t < w.seg_own);
+    if (a) {
+        double row[30];
+        land_terms(e, row, t < w.seg_own, false);
+#pragma unroll
+        for (int j = 0; j < 12; j++) Tm[t * kSegStride + j] = row[j];
+    }
     act[t] = a;
     __syncthreads();
     double mx = 0.0;
@@ -744,24 +771,26 @@ __global__ __launch_bounds__(kThreads) void k_point_terms_sums(LbaBatch b, LbaWo
         uint64_t written = 0;
         double H[9] = {}, bl[3] = {};
         for (int q = 0; q < nb; q++) {
+            const int bkv = c.e_blk[e + q];
+            const bool shared = bkv >= 0 && (bkv & kBlkShared);
             // rows past the workgroup's 256 (a landmark with more edges than the halo allows: only if a point
-            // has more observations than the batch has keyframes) are computed here
+            // has more observations than the batch has keyframes) and the edges of shared blocks are computed here
             double r[30];
-            if (t + q >= kThreads) {
+            if (t + q >= kThreads || shared) {
                 if (c.e_level[e + q] != 0) continue;
-                land_terms(e + q, r, false);
+                land_terms(e + q, r, false, true);
             } else {
                 if (!act[t + q]) continue;
                 const double* src = Tm + (t + q) * kSegStride;
 #pragma unroll
-                for (int j = 0; j < 30; j++) r[j] = src[j];
+                for (int j = 0; j < 12; j++) r[j] = src[j];
             }
 #pragma unroll
             for (int j = 0; j < 9; j++) H[j] += r[j];
 #pragma unroll
             for (int j = 0; j < 3; j++) bl[j] += r[9 + j];
-            const int bk = c.e_blk[e + q];
-            if (bk >= 0) {
+            if (shared) {
+                const int bk = bkv & (kBlkShared - 1);
                 double* hb = c.blkH + (size_t)bk * 18;
                 const uint64_t bit = 1ull << (bk - b0);
                 if (written & bit) {
@@ -803,7 +832,7 @@ __global__ __launch_bounds__(kThreads) void k_plane_lm_sums(LbaBatch b, LbaWork 
         for (int e = c.lm_boff[l]; e < c.lm_boff[l] + c.lm_nb[l]; e++) {
             if (c.e_level[e] != 0) continue;
             const double v = c.con[(size_t)kLbaCon * e + j];
-            const int bk = c.e_blk[e];
+            const int bk = edge_block(c, e);
             if (lane < 12) acc += v;
             if (bk >= 0) {
                 const uint64_t bit = 1ull << (bk - b0);
