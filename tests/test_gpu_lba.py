@@ -158,3 +158,34 @@ def test_lba_stop_flag_raised_after_trial_k(lba):
                 assert int(r["trials"]) == k
     finally:
         lba.debug_stop_after(-1)
+
+
+def test_lba_shared_blocks_match_oracle(lba):
+    """Points with two observations from one keyframe (the reference's MapPoint keeps one per keyframe, so this
+    is outside its inputs; g2o itself accepts two edges between the same vertices): the (landmark, pose) block
+    then sums two edges, which the device does on the landmark's owner thread in edge order (kBlkShared)."""
+    import oracle_lba
+    prob, kfs, pts, pobs, pls, plobs, _ = _problems()[0]
+    pts = pts.copy()
+    new_obs = []
+    for i in range(len(pts)):
+        o = pobs[pts[i]["obs_offset"]:pts[i]["obs_offset"] + pts[i]["n_obs"]].copy()
+        if i % 7 == 0 and len(o):
+            d = o[:1].copy()
+            d["u"] += 0.3
+            d["v"] -= 0.2
+            o = np.concatenate([o[:1], d, o[1:]])
+        pts[i]["obs_offset"] = sum(len(x) for x in new_obs)
+        pts[i]["n_obs"] = len(o)
+        new_obs.append(o)
+    pobs = np.concatenate(new_obs)
+    prob = prob.copy()
+    prob["n_point_obs"] = len(pobs)
+    o = oracle_lba.lba_optimize(prob, kfs, pts, pobs, pls, plobs)
+    g = lba(prob, kfs, pts, pobs, pls, plobs)
+    assert g["result"]["status"] == 0
+    assert list(g["result"]["iterations"]) == list(o["result"]["iterations"])
+    assert np.array_equal(g["point_outlier"], o["point_outlier"])
+    for i in range(len(kfs)):
+        assert _close(g["Tcw"][i], o["Tcw"][i]), (i, g["Tcw"][i], o["Tcw"][i])
+    assert _close(g["points"], o["points"])
