@@ -631,7 +631,10 @@ __device__ __forceinline__ void store_terms(const Ctx& c, const LbaConsts& C, bo
 // 6 <= q < 18 at the pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; evaluation q runs on the lane pair (2q, 2q + 1)
 // (plane_error_pair: each lane one member of every atan2 / sincos pair), the differences are gathered with
 // shuffles (the reference's per-coordinate expression) and lane 0 stores the terms.
-__global__ __launch_bounds__(kThreads) void k_plane_terms(LbaBatch b, LbaWork w, LbaConsts C) {
+#ifndef SPSLAM_LBA_PL_WAVES
+#define SPSLAM_LBA_PL_WAVES 3  // waves per SIMD asked of k_plane_terms (3: 130 VGPRs, no spills; 4: 5 spilled)
+#endif
+__global__ __launch_bounds__(kThreads, SPSLAM_LBA_PL_WAVES) void k_plane_terms(LbaBatch b, LbaWork w, LbaConsts C) {
     const int2 task = w.plane_tasks[blockIdx.x];
     Ctx c = make_ctx(b, task.x);
     const LbaCtl& k = *c.ctl;
