@@ -15,18 +15,26 @@
 //   solver    SparseOptimizer::initializeOptimization(level) (active edges,
 //             vertices with active edges, poses then landmarks by id,
 //             sparse_optimizer.cpp), OptimizationAlgorithmLevenberg::solve,
-//             BlockSolver_6_3 buildSystem / setLambda / Schur solve
-//             (block_solver.hpp:354-590; Eigen 3x3 cofactor inverse for each
-//             landmark block) and the reduced pose system solved by an LDL^T
-//             factorisation of its upper triangle;
+//             BlockSolver_6_3 buildStructure / buildSystem / setLambda / Schur
+//             solve in g2o's own order (block_solver.hpp:130-590): every edge's
+//             quadratic form added to its vertex blocks in edge-insertion order
+//             (Eigen's expression for each robust / non-robust branch,
+//             base_binary_edge.hpp:55-120), chi2 summed edge by edge
+//             (sparse_optimizer.cpp:100-114), the Schur complement formed
+//             landmark by landmark in landmark-index order (Hi1i2 -= BDinv Bj^T,
+//             Bb += Bi db, Eigen 3x3 cofactor inverse), the reduced system's
+//             pattern = g2o's Hschur pattern (pose pairs over ALL edges of each
+//             active landmark, outliers included), factorised by Eigen's
+//             SimplicialLDLT after its AMD ordering (eigen_simplicial_restated.h);
 //   schedule  optimize(5); relabel (chi2 > 5.991 / 7.815 or depth <= 0 for
 //             points, > Chi / VPChi for planes) with the errors cached by the
 //             last computeActiveErrors, drop every robust kernel;
 //             initializeOptimization(0); optimize(10); outlier observations
 //             (vToErase); write back poses (local KFs), points and planes.
-// Deviation: LinearSolverEigen factorises with Eigen::SimplicialLDLT after an
-// AMD fill-reducing permutation; the oracle factorises in natural order.
-// Both compute the same LDL^T solution up to rounding.
+// Eigen's reductions inside the fixed-size products (3-term dots, A^T x) are restated left to right, the
+// convention of the pose path.  A failed factorisation leaves g2o's x vector
+// stale (linear_solver_eigen.h:96-101) before the rejected trial is popped; here x is zero (the trial is
+// rejected either way; only computeScale of that rejected trial could differ).
 // Parity: unpinned against the reference binary (g2o needs Eigen, absent).
 #include <algorithm>
 #include <cmath>
@@ -35,6 +43,7 @@
 #include <vector>
 
 #include "../include/spslam_gpu.h"
+#include "eigen_simplicial_restated.h"
 #include "g2o_restated.h"
 
 namespace oracle {
@@ -66,9 +75,9 @@ struct Edge {
     Plane mplane{};
     double fx, fy, cx, cy, bf;
     double err[3] = {0, 0, 0};
-    double chi2() const {
+    double chi2() const {  // _error.dot(information() * _error), Omega diagonal
         double s = 0;
-        for (int i = 0; i < dim; i++) s += err[i] * info[i] * err[i];
+        for (int i = 0; i < dim; i++) s += err[i] * (info[i] * err[i]);
         return s;
     }
 };
@@ -199,12 +208,16 @@ struct Opt {
     std::vector<int> active;   // active edge indices (insertion order)
     std::vector<int> poses;    // active non-fixed poses by id
     std::vector<int> lms;      // active landmarks: points by id, then planes by id
-    // structure: per landmark the (pose hessian index, edges) blocks, sorted by pose index
-    struct Block { int pose; double H[3][6]; };   // Hpl^T block (landmark x pose)
+    // Hpl (pose x landmark, 6 x 3) blocks per landmark, sorted by pose index (the _HplCCS column)
+    struct Block { int pose; double B[6][3]; };
     std::vector<std::vector<Block>> lblocks;
     std::vector<double> Hpp;   // [np][6][6]
     std::vector<double> Hll;   // [nl][3][3]
     std::vector<double> b;     // poses (6 np) then landmarks (3 nl)
+    // the reduced system's pattern (buildStructure's Hschur): upper blocks, scalar CCS of their upper triangle
+    std::vector<int> Ap, Ai;
+    eigen_sparse::SimplicialLDLT ldlt;
+    bool analyzed = false;
     int np = 0, nl = 0;
     double lambda = 0, ni = 2;
     int nBad = 0;
@@ -231,6 +244,30 @@ struct Opt {
             if (!G.v[i].fixed && G.v[i].kind != 0) { G.v[i].hidx = (int)lms.size(); lms.push_back(i); }
         np = (int)poses.size();
         nl = (int)lms.size();
+        // buildStructure's Schur pattern: for every active landmark, every pair of Hessian poses among the
+        // vertices of ALL its edges (HyperGraph::Vertex::edges(), any level), i1 <= i2; Hpp's diagonal blocks
+        std::vector<std::vector<char>> pat((size_t)np, std::vector<char>((size_t)np, 0));
+        for (int p = 0; p < np; p++) pat[p][p] = 1;
+        std::vector<std::vector<int>> lposes((size_t)nl);
+        for (const Edge& e : G.e) {
+            const int l = G.v[e.lm].hidx, h = G.v[e.kf].hidx;
+            if (l >= 0 && G.v[e.lm].kind != 0 && h >= 0 && G.v[e.kf].kind == 0) lposes[l].push_back(h);
+        }
+        for (auto& ps : lposes)
+            for (int a : ps)
+                for (int c : ps) pat[std::min(a, c)][std::max(a, c)] = 1;
+        const int n = 6 * np;
+        Ap.assign(n + 1, 0);
+        Ai.clear();
+        for (int c = 0; c < n; c++) {
+            const int i2 = c / 6;
+            for (int i1 = 0; i1 <= i2; i1++)
+                if (pat[i1][i2])
+                    for (int rr = 0; rr < 6; rr++)
+                        if (6 * i1 + rr <= c) Ai.push_back(6 * i1 + rr);
+            Ap[c + 1] = (int)Ai.size();
+        }
+        analyzed = false;  // LinearSolverEigen::init(): symbolic analysis at the first solve of optimize()
     }
     double robust_chi2() const {
         double chi = 0;
@@ -243,6 +280,12 @@ struct Opt {
     }
     void compute_errors() { for (int k : active) compute_error(G.e[k], G); }
 
+    // BlockSolver::buildSystem: linearizeOplus + constructQuadraticForm of every active edge in insertion order
+    // (base_binary_edge.hpp:55-120; vertex 0 = landmark, Jacobian A; vertex 1 = pose, Jacobian B; the Hpl block is
+    // mapped transposed, _hessianTransposed).  Omega is diagonal, so Eigen's temporaries reduce to:
+    //   robust:     W = rho' Omega;  Hll += (A^T W) A;  Hpl += (B^T W) A;  Hpp += (B^T W) B;
+    //               omega_r = (-(Omega e)) rho';  bl += A^T omega_r;  bp += B^T omega_r
+    //   non-robust: AtO = A^T Omega;  Hll += AtO A;  Hpl += B^T AtO^T;  Hpp += (B^T Omega) B;  omega_r = -Omega e
     void build_system() {
         Hpp.assign((size_t)np * 36, 0.0);
         Hll.assign((size_t)nl * 9, 0.0);
@@ -258,7 +301,7 @@ struct Opt {
             if (e.rk.on) { double rho[3]; e.rk.robustify(e.chi2(), rho); w = rho[1]; }
             double W[3], om_r[3];
             for (int r = 0; r < e.dim; r++) {
-                W[r] = e.rk.on ? w * e.info[r] : e.info[r];       // robustInformation = rho1 * Omega
+                W[r] = e.rk.on ? w * e.info[r] : e.info[r];
                 om_r[r] = -(e.info[r] * e.err[r]);
                 if (e.rk.on) om_r[r] *= w;
             }
@@ -282,11 +325,17 @@ struct Opt {
                     Block* blk = nullptr;
                     for (auto& x : bl_list) if (x.pose == P.hidx) blk = &x;
                     if (!blk) { bl_list.push_back(Block{P.hidx, {}}); blk = &bl_list.back(); }
-                    for (int i = 0; i < 3; i++)
-                        for (int j = 0; j < 6; j++) {
-                            double h = (A[0][i] * W[0]) * B[0][j];
-                            for (int r = 1; r < e.dim; r++) h += (A[r][i] * W[r]) * B[r][j];
-                            blk->H[i][j] += h;
+                    for (int i = 0; i < 6; i++)
+                        for (int j = 0; j < 3; j++) {
+                            double h;
+                            if (e.rk.on) {
+                                h = (B[0][i] * W[0]) * A[0][j];
+                                for (int r = 1; r < e.dim; r++) h += (B[r][i] * W[r]) * A[r][j];
+                            } else {
+                                h = B[0][i] * (A[0][j] * e.info[0]);
+                                for (int r = 1; r < e.dim; r++) h += B[r][i] * (A[r][j] * e.info[r]);
+                            }
+                            blk->B[i][j] += h;
                         }
                 }
             }
@@ -317,10 +366,12 @@ struct Opt {
             for (int j = 0; j < 3; j++) m = std::max(std::fabs(Hll[9 * l + 4 * j]), m);
         return 1e-5 * m;
     }
-    // BlockSolver::solve (Schur complement on the landmarks) with lambda on the diagonals.
+    // BlockSolver::solve with lambda on the diagonals (setLambda): Schur complement landmark by landmark
+    // (block_solver.hpp:381-431), LinearSolverEigen on the reduced system, landmark back-substitution (:444-471).
     bool solve(double lam, std::vector<double>& x) {
         const int n = 6 * np;
         x.assign((size_t)n + 3 * nl, 0.0);
+        // _Hschur->clear(); _Hpp->add(_Hschur)  (whole diagonal blocks, lambda included)
         std::vector<double> S((size_t)n * n, 0.0), coeff((size_t)n, 0.0);
         for (int p = 0; p < np; p++)
             for (int i = 0; i < 6; i++)
@@ -338,52 +389,41 @@ struct Opt {
             const auto& col = lblocks[l];
             for (size_t a = 0; a < col.size(); a++) {
                 const int i1 = col[a].pose;
-                // Bi = Hpl block (pose x landmark) = col[a].H^T
+                const double (&Bi)[6][3] = col[a].B;
                 double BDinv[6][3];
                 for (int r = 0; r < 6; r++)
                     for (int c = 0; c < 3; c++)
-                        BDinv[r][c] = (col[a].H[0][r] * Di[0][c] + col[a].H[1][r] * Di[1][c]) + col[a].H[2][r] * Di[2][c];
-                for (int r = 0; r < 6; r++)
-                    coeff[6 * i1 + r] += (col[a].H[0][r] * db[0] + col[a].H[1][r] * db[1]) + col[a].H[2][r] * db[2];
+                        BDinv[r][c] = (Bi[r][0] * Di[0][c] + Bi[r][1] * Di[1][c]) + Bi[r][2] * Di[2][c];
+                for (int r = 0; r < 6; r++) coeff[6 * i1 + r] += (Bi[r][0] * db[0] + Bi[r][1] * db[1]) + Bi[r][2] * db[2];
                 for (size_t c2 = a; c2 < col.size(); c2++) {
                     const int i2 = col[c2].pose;
+                    const double (&Bj)[6][3] = col[c2].B;
                     for (int r = 0; r < 6; r++)
                         for (int c = 0; c < 6; c++)
                             S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] -=
-                                (BDinv[r][0] * col[c2].H[0][c] + BDinv[r][1] * col[c2].H[1][c]) + BDinv[r][2] * col[c2].H[2][c];
+                                (BDinv[r][0] * Bj[c][0] + BDinv[r][1] * Bj[c][1]) + BDinv[r][2] * Bj[c][2];
                 }
             }
         }
         std::vector<double> bs((size_t)n);
         for (int i = 0; i < n; i++) bs[i] = b[i] - coeff[i];
-        // LDL^T of the upper triangle (U = L^T), natural order; fails on an exact zero pivot
-        std::vector<double> Lm((size_t)n * n, 0.0), d((size_t)n, 0.0);
-        for (int j = 0; j < n; j++) {
-            double dj = S[(size_t)j * n + j];
-            for (int k = 0; k < j; k++) dj -= (Lm[(size_t)j * n + k] * d[k]) * Lm[(size_t)j * n + k];
-            if (dj == 0.0) return false;
-            d[j] = dj;
-            for (int i = j + 1; i < n; i++) {
-                double s = S[(size_t)j * n + i];
-                for (int k = 0; k < j; k++) s -= (Lm[(size_t)i * n + k] * d[k]) * Lm[(size_t)j * n + k];
-                Lm[(size_t)i * n + j] = s / dj;
-            }
+        if (!analyzed) {
+            ldlt.analyze(n, Ap, Ai);
+            analyzed = true;
         }
-        std::vector<double> y(bs);
-        for (int i = 0; i < n; i++)
-            for (int k = 0; k < i; k++) y[i] -= Lm[(size_t)i * n + k] * y[k];
-        for (int i = 0; i < n; i++) y[i] /= d[i];
-        for (int k = n - 1; k >= 0; k--)  // column-oriented back substitution
-            for (int i = 0; i < k; i++) y[i] -= Lm[(size_t)k * n + i] * y[k];
-        for (int i = 0; i < n; i++) x[i] = y[i];
-        // landmarks: xl = Dinv (bl - Hpl^T xp)
+        std::vector<double> Ax(Ai.size());
+        for (int c = 0; c < n; c++)
+            for (int p = Ap[c]; p < Ap[c + 1]; p++) Ax[p] = S[(size_t)Ai[p] * n + c];
+        if (!ldlt.factorize(Ax)) return false;
+        ldlt.solve(bs.data(), x.data());
+        // landmarks: cl = bl - Hpl^T xp (_HplCCS->rightMultiply with cp = -xp), xl = Dinv cl
         for (int l = 0; l < nl; l++) {
             double cl[3];
             for (int i = 0; i < 3; i++) cl[i] = b[n + 3 * l + i];
             for (const auto& blk : lblocks[l])
                 for (int i = 0; i < 3; i++) {
                     double s = 0;
-                    for (int j = 0; j < 6; j++) s += blk.H[i][j] * (-x[6 * blk.pose + j]);
+                    for (int j = 0; j < 6; j++) s += blk.B[j][i] * (-x[6 * blk.pose + j]);
                     cl[i] += s;
                 }
             const double* Di = &Dinv[9 * l];
@@ -656,4 +696,18 @@ extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba
                                    uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res) {
     return oracle_lba_optimize_stop(P, kfs, pts, pobs, pls, plobs, cfg, kf_out, pt_out, pl_out, pobs_outlier,
                                     plobs_outlier, res, -1);
+}
+
+// Test access to the SimplicialLDLT restatement (tests/test_oracle_lba.py): factorise the upper-triangular CCS
+// pattern (Ap, Ai) with values Ax, solve A x = b; perm receives the AMD order (Pinv).  Returns 0, or 1 on a
+// zero pivot.
+extern "C" int oracle_eigen_ldlt(int n, const int* Ap, const int* Ai, const double* Ax, const double* b, double* x,
+                                 int* perm) {
+    oracle::eigen_sparse::SimplicialLDLT s;
+    std::vector<int> ap(Ap, Ap + n + 1), ai(Ai, Ai + Ap[n]);
+    s.analyze(n, ap, ai);
+    for (int k = 0; k < n; k++) perm[k] = s.Pinv[k];
+    if (!s.factorize(std::vector<double>(Ax, Ax + Ap[n]))) return 1;
+    s.solve(b, x);
+    return 0;
 }

@@ -32,3 +32,30 @@ def lba_optimize(prob, kfs, points, point_obs, planes, plane_obs, cfg=PLANE_CONF
                                  res.ctypes.data, int(stop_after))
     return dict(Tcw=kf_out, points=pt_out[:len(points)], planes=pl_out[:len(planes)],
                 point_outlier=po[:len(point_obs)], plane_outlier=plo[:len(plane_obs)], result=res)
+
+
+def eigen_ldlt(A_upper_pattern, A, b):
+    """Eigen SimplicialLDLT<Upper> restatement (oracle/eigen_simplicial_restated.h) on a dense matrix A whose
+    structural upper pattern is the boolean matrix A_upper_pattern.  Returns (x, perm) or (None, perm) on a zero
+    pivot."""
+    lib = oracle_ctypes.lib()
+    vp = ctypes.c_void_p
+    lib.oracle_eigen_ldlt.argtypes = [ctypes.c_int] + [vp] * 6
+    lib.oracle_eigen_ldlt.restype = ctypes.c_int
+    n = A.shape[0]
+    Ap, Ai, Ax = [0], [], []
+    for c in range(n):
+        for r in range(c + 1):
+            if A_upper_pattern[r, c]:
+                Ai.append(r)
+                Ax.append(A[r, c])
+        Ap.append(len(Ai))
+    Ap = np.asarray(Ap, np.int32)
+    Ai = np.asarray(Ai if Ai else [0], np.int32)
+    Ax = np.asarray(Ax if Ax else [0.0], np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.zeros(n, np.float64)
+    perm = np.zeros(n, np.int32)
+    rc = lib.oracle_eigen_ldlt(n, Ap.ctypes.data, Ai.ctypes.data, Ax.ctypes.data, b.ctypes.data, x.ctypes.data,
+                               perm.ctypes.data)
+    return (None if rc else x), perm
