@@ -10,7 +10,7 @@ HIPFLAGS ?= --offload-arch=$(OFFLOAD_ARCH) -O3 -std=c++17 -fPIC -ffp-contract=of
 PKG := sp-slam_amd
 CSRC := $(PKG)/csrc
 OBJDIR := build/obj
-KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels \
+KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels lba_g2o \
            assoc_kernels match_kernels track_kernels grab_kernels bow_kernels
 OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
 GPU_HDRS := $(wildcard $(CSRC)/*.h) include/spslam_gpu.h include/spslam_brief_pattern.inc

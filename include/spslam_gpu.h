@@ -174,7 +174,8 @@ typedef struct spslam_pose_problem {
 typedef struct spslam_pose_result {
     float Tcw[16];      /* optimized pose (unchanged input if n_inliers == 0 by the <3 rule) */
     int32_t n_inliers;  /* PoseOptimization return value */
-    int32_t lm_iterations;  /* total LM iterations run (diagnostic) */
+    int32_t lm_iterations;  /* total LM iterations run (diagnostic); -1 = the device gave up on a bounded
+                               internal wait (never observed): invalid result, Tcw = input, n_inliers = 0 */
     int32_t trial_passes;   /* edge passes at trial poses (damping trials are evaluated 4 per pass; diagnostic) */
     int32_t trials;         /* damping trials the reference evaluated (computeActiveErrors calls; diagnostic) */
 } spslam_pose_result;
@@ -294,6 +295,18 @@ int spslam_lba_optimize(spslam_ctx* ctx, const spslam_lba_problem* problem, cons
                         uint8_t* point_obs_outlier, uint8_t* plane_obs_outlier, spslam_lba_result* result,
                         const volatile uint8_t* stop_flag);
 
+/* Summation order of the LocalBundleAdjustment entries (default SPSLAM_LBA_G2O_ORDER):
+ *   SPSLAM_LBA_G2O_ORDER  g2o's own arithmetic, bit-exact to the reference-order oracle: edge-insertion-order
+ *                         sums, the landmark-ordered Schur complement (block_solver.hpp:381-431), Eigen's
+ *                         SimplicialLDLT with its AMD ordering (linear_solver_eigen.h:58-121); one workgroup per
+ *                         problem, the whole schedule in one launch;
+ *   SPSLAM_LBA_FAST_ORDER the grid-wide phase kernels (tree-ordered reductions, Schur sums on the f64 matrix
+ *                         cores, natural-order LDL^T): the same algorithm to rounding (<= 1e-4 on the tested maps),
+ *                         a throughput mode for maps that do not need the reference's bits. */
+#define SPSLAM_LBA_G2O_ORDER 0
+#define SPSLAM_LBA_FAST_ORDER 1
+int spslam_lba_set_order(spslam_ctx* ctx, int order);
+
 /* Test hook (deterministic LocalMapping::InterruptBA): the context's following
  * LocalBundleAdjustment calls see pbStopFlag raised once a problem has run
  * `trials` LM trials -- before optimize(5) when 0 -- at the same check points
@@ -307,8 +320,9 @@ int spslam_lba_debug_stop_after(spslam_ctx* ctx, int trials);
  * absolute observation indices).  At most 64 keyframes per problem
  * (status -2 otherwise).  d_stop_flags: one pbStopFlag per problem in
  * device-visible memory (device, or host-mapped coherent memory another thread
- * raises), nonzero = stop; NULL = no flags.  The call returns once every
- * problem is done (it polls the device); results are complete on hip_stream. */
+ * raises), nonzero = stop; NULL = no flags.  Results are complete on
+ * hip_stream (SPSLAM_LBA_G2O_ORDER only enqueues one launch; the fast order
+ * polls the device and returns once every problem is done). */
 int spslam_lba_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_lba_problem* problems,
                                      const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
                                      const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,
@@ -468,6 +482,11 @@ int spslam_debug_plane_not_seen(spslam_ctx* ctx, const float* planes, int n_plan
  * std::cos / std::atan2 / std::pow(x, 3)), correctly rounded.
  * kind 0 sin(a), 1 cos(a), 2 atan2(a, b), 3 a^3; n host doubles each. */
 int spslam_debug_libm64(spslam_ctx* ctx, int kind, const double* a, const double* b, int n, double* out);
+
+/* Test hook: bound of PoseOptimization's internal waits (the chain wave and the compute waves hand edge rows over
+ * through LDS; every wait gives up after `cap` polls).  0 restores the default (2^20 polls, never reached).  A
+ * tiny cap forces the give-up path: the problem then reports lm_iterations = -1, n_inliers = 0, Tcw = input. */
+int spslam_debug_pose_spin_cap(spslam_ctx* ctx, int cap);
 
 /* ------------------------------------------------------------------------
  * RGB-D Frame per-keypoint steps (src/Frame.cc:146-181): UndistortKeyPoints

@@ -1,0 +1,1627 @@
+// gfx950 LocalBundleAdjustment in g2o's own arithmetic (reference: src/Optimizer.cc:1154-1977 on the vendored
+// g2o SparseOptimizer + OptimizationAlgorithmLevenberg + BlockSolver_6_3 + LinearSolverEigen, g2oAddition plane
+// edges).  Semantics: oracle/lba_oracle.cpp, which this reproduces bit for bit.
+//
+// One persistent 512-thread workgroup per problem runs the whole schedule -- setup, optimize(5), relabel,
+// optimize(10), outputs -- with no host round trip and no cross-workgroup hand-off; many problems (the local maps
+// of many sequences) run side by side, one per CU.  Every order-sensitive sum follows g2o:
+//   chi2          activeRobustChi2: one lane adds the edges' robust chi2 in edge-insertion order (the others
+//                 evaluate the errors first; inactive edges contribute an exact +0.0);
+//   Hll, bl, Hpl  per landmark, its edges in insertion order (one thread per landmark);
+//   Hpp, bp       per free pose and term, its edges in insertion order (one lane per (pose, term) chain);
+//   Schur         Hschur = Hpp (+ lambda), then landmark by landmark in landmark-index (vertex-id) order
+//                 Hi1i2 -= BDinv Bj^T and Bb += Bi db (block_solver.hpp:381-431): one lane per (block row of a
+//                 pattern block, i.e. (i1, i2, r)) holds the row's six entries and subtracts each landmark's
+//                 contribution in order;
+//   factor/solve  Eigen SimplicialLDLT<Upper> on g2o's Hschur pattern: AMD ordering (the scalar
+//                 minimum_degree_ordering, one lane; every scalar dense -> the natural order at once), elimination
+//                 tree and L's column patterns as bitsets, each row's topological pattern order from the same
+//                 tree walks, then the up-looking factorisation on one wave (y in registers, one lane per row of
+//                 the reduced system, the pattern order's steps as readlane broadcasts), Eigen's triangular solves;
+//   scale         computeScale: x . (lambda x + b) over poses then landmarks, one lane.
+// The quadratic-form terms of every edge (Jacobians: analytic for points, central differences for planes on lane
+// pairs), errors and updates run in parallel.  Floating-point expressions are the oracle's (g2o_restated.h,
+// eigen_simplicial_restated.h); DESIGN.md section 3.9.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+
+#include "g2o_device.h"
+#include "lba_launch.h"
+
+namespace spslam {
+namespace lbag {
+
+using namespace g2od;
+
+constexpr int kT = kLbgThreads, kW = kT / 64;
+constexpr int kMaxK = kLbaMaxKeyframes;
+constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
+constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
+constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised with L in LDS
+
+struct Sh {
+    double red[kW][4];
+    int iscan[kW];
+    uint64_t kfact;
+    uint64_t pat[kMaxK];                // Schur block pattern: row i1, bits i2 >= i1
+    int hidx[kMaxK];                    // keyframe -> free-pose Hessian index (-1: fixed or inactive)
+    int hpose[kMaxK];                   // Hessian index -> keyframe
+    int pdeg[kMaxK];                    // poses coupled with each pose (itself included)
+    int np, nl, nact, flag;
+    // LM / schedule state (thread 0 writes between barriers)
+    int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
+    double lambda, ni, currentChi, iniChi, tempChi, scale;
+};
+
+struct G {
+    int K, Np, Nq, L, E, Ep;
+    const spslam_lba_keyframe* kf;
+    const spslam_lba_point* pt;
+    const spslam_lba_plane* pl;
+    const spslam_lba_point_obs* pobs;
+    const spslam_lba_plane_obs* plobs;
+    double *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *echi, *sc, *terms, *Hll, *bl, *Dinv, *db, *blkB, *blkBD, *Hps,
+        *S, *bs, *x, *Ld;
+    int *e_lm, *e_kf, *e_type, *e_level, *e_src, *e_blk, *lm_boff, *lm_nb, *lm_sorted, *lm_hidx, *hidx_lm, *lmh_blk,
+        *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W;
+    uint64_t *lmh_mask, *lm_amask, *Lbits, *Abits;
+};
+
+__device__ G make_g(const LbgBatch& b, int p) {
+    const spslam_lba_problem pb = b.probs[p];
+    G g;
+    g.K = pb.n_kf; g.Np = pb.n_points; g.Nq = pb.n_planes;
+    g.Ep = pb.n_point_obs; g.E = pb.n_point_obs + pb.n_plane_obs; g.L = g.Np + g.Nq;
+    g.kf = b.kfs + pb.kf_offset; g.pt = b.pts + pb.point_offset; g.pl = b.pls + pb.plane_offset;
+    g.pobs = b.pobs; g.plobs = b.plobs;
+    const LbgLayout Ly = lbg_layout(g.K, g.Np, g.Nq, g.E);
+    uint8_t* base = b.scratch + b.scratch_off[p];
+    auto D = [&](size_t o) { return (double*)(base + o); };
+    auto I = [&](size_t o) { return (int*)(base + o); };
+    g.pose = D(Ly.pose); g.pose_b = D(Ly.pose_b); g.X = D(Ly.X); g.X_b = D(Ly.X_b); g.P = D(Ly.P); g.P_b = D(Ly.P_b);
+    g.err = D(Ly.err); g.echi = D(Ly.echi); g.sc = D(Ly.sc); g.terms = D(Ly.terms); g.Hll = D(Ly.Hll);
+    g.bl = D(Ly.bl); g.Dinv = D(Ly.Dinv); g.db = D(Ly.db); g.blkB = D(Ly.blkB); g.blkBD = D(Ly.blkBD);
+    g.Hps = D(Ly.Hps); g.S = D(Ly.S); g.bs = D(Ly.bs); g.x = D(Ly.x); g.Ld = D(Ly.Ld);
+    g.e_lm = I(Ly.e_lm); g.e_kf = I(Ly.e_kf); g.e_type = I(Ly.e_type); g.e_level = I(Ly.e_level);
+    g.e_src = I(Ly.e_src); g.e_blk = I(Ly.e_blk); g.lm_boff = I(Ly.lm_boff); g.lm_nb = I(Ly.lm_nb);
+    g.lm_sorted = I(Ly.lm_sorted); g.lm_hidx = I(Ly.lm_hidx); g.hidx_lm = I(Ly.hidx_lm); g.lmh_blk = I(Ly.lmh_blk);
+    g.pe_off = I(Ly.pe_off); g.pe_idx = I(Ly.pe_idx); g.Pinv = I(Ly.Pinv); g.Pm = I(Ly.Pm); g.parent = I(Ly.parent);
+    g.rs_off = I(Ly.rs_off); g.rs_idx = I(Ly.rs_idx); g.amd_Ci = I(Ly.amd_Ci); g.amd_W = I(Ly.amd_W);
+    g.lmh_mask = (uint64_t*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t*)(base + Ly.lm_amask);
+    g.Lbits = (uint64_t*)(base + Ly.Lbits); g.Abits = (uint64_t*)(base + Ly.Abits);
+    return g;
+}
+
+// ---------------------------------------------------------------- workgroup primitives
+__device__ __forceinline__ int block_scan(int v, int* total, Sh& s) {  // exclusive; *total = sum
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s.iscan[w] = x;
+    __syncthreads();
+    int base = 0, tot = 0;
+#pragma unroll
+    for (int j = 0; j < kW; j++) {
+        const int q = s.iscan[j];
+        if (j < w) base += q;
+        tot += q;
+    }
+    __syncthreads();
+    *total = tot;
+    return base + x - v;
+}
+__device__ __forceinline__ int block_and(int v, Sh& s) {
+    const int w = threadIdx.x >> 6;
+    const bool all = __all(v != 0);
+    if ((threadIdx.x & 63) == 0) s.iscan[w] = all;
+    __syncthreads();
+    int r = 1;
+#pragma unroll
+    for (int j = 0; j < kW; j++) r &= s.iscan[j];
+    __syncthreads();
+    return r;
+}
+__device__ __forceinline__ double block_max(double v, Sh& s) {  // max of non-negative values
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    if ((threadIdx.x & 63) == 0) s.red[w][0] = v;
+    __syncthreads();
+    double m = 0.0;
+#pragma unroll
+    for (int j = 0; j < kW; j++) m = fmax(m, s.red[j][0]);
+    __syncthreads();
+    return m;
+}
+__device__ __forceinline__ double rl(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+// value of entry i of a vector spread over the wave (entry 64 m + lane in register m)
+template <int kC>
+__device__ __forceinline__ double pick(const double (&v)[kC], int i) {
+    double r = 0.0;
+#pragma unroll
+    for (int m = 0; m < kC; m++)
+        if ((i >> 6) == m) r = rl(v[m], i & 63);
+    return r;
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------- edge math (oracle/lba_oracle.cpp)
+__device__ __forceinline__ SE3 load_pose(const double* p) { return SE3{Q{p[0], p[1], p[2], p[3]}, V3{p[4], p[5], p[6]}}; }
+__device__ __forceinline__ void store_pose(double* p, const SE3& T) {
+    p[0] = T.r.w; p[1] = T.r.x; p[2] = T.r.y; p[3] = T.r.z; p[4] = T.t.x; p[5] = T.t.y; p[6] = T.t.z;
+}
+__device__ __forceinline__ P4 plane_from_f(const float* c) {  // Converter::toPlane3D + Plane3D(v)
+    P4 p{{c[0], c[1], c[2], c[3]}};
+    if (c[3] < 0.0f)
+        for (int i = 0; i < 4; i++) p.c[i] = -p.c[i];
+    p_normalize(p.c);
+    return p;
+}
+__device__ __forceinline__ P4 plane_transform(const SE3& T, const P4& w) {
+    const M3 R = q_to_rot(T.r);
+    const V3 n2 = mv(R, V3{w.c[0], w.c[1], w.c[2]});
+    P4 v{{n2.x, n2.y, n2.z, w.c[3] - dot(T.t, n2)}};
+    if (v.c[3] < 0.0)
+        for (int i = 0; i < 4; i++) v.c[i] = -v.c[i];
+    p_normalize(v.c);
+    return v;
+}
+__device__ __forceinline__ int edge_dim(int type) { return type == 0 ? 2 : (type <= 2 ? 3 : 2); }
+__device__ __forceinline__ void info_of(const G& g, const LbaConsts& C, int e, int t, double* info) {
+    if (t <= 1) {
+        const double s = (double)g.pobs[g.e_src[e]].inv_sigma2;
+        info[0] = info[1] = info[2] = s;
+    } else if (t == 2) {
+        info[0] = info[1] = C.angle_info; info[2] = C.dis_info;
+    } else {
+        info[0] = info[1] = t == 3 ? C.par_info : C.ver_info;
+        info[2] = 0;
+    }
+}
+__device__ __forceinline__ double chi2_of(const double* err, const double* info, int dim) {  // e . (Omega e)
+    double s = 0;
+    for (int i = 0; i < dim; i++) s += err[i] * (info[i] * err[i]);
+    return s;
+}
+__device__ __forceinline__ double delta_of(const LbaConsts& C, int t) {
+    return t == 0 ? C.delta_mono : t == 1 ? C.delta_stereo : t == 2 ? C.delta_plane : C.delta_vp;
+}
+// RobustKernelHuber::robustify; rho0 / rho1 (non-robust: chi2, 1)
+__device__ __forceinline__ void huber(double chi, double delta, bool on, double* rho0, double* rho1) {
+    const double dsqr = delta * delta;
+    if (!on || chi <= dsqr) { *rho0 = chi; *rho1 = 1.0; return; }
+    const double s = sqrt(chi);
+    *rho0 = 2 * s * delta - dsqr;
+    *rho1 = delta / s;
+}
+__device__ __forceinline__ void point_error(const G& g, int e, int t, const SE3& T, const double* X, double* err) {
+    const spslam_lba_point_obs& o = g.pobs[g.e_src[e]];
+    const spslam_lba_keyframe& k = g.kf[g.e_kf[e]];
+    const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
+    if (t == 0) {
+        err[0] = (double)o.u - (p.x / p.z * (double)k.fx + (double)k.cx);
+        err[1] = (double)o.v - (p.y / p.z * (double)k.fy + (double)k.cy);
+        err[2] = 0.0;
+    } else {
+        const float invz = (float)(1.0f / p.z);
+        const double r0 = p.x * invz * (double)k.fx + (double)k.cx, r1 = p.y * invz * (double)k.fy + (double)k.cy;
+        const double r2 = r0 - (double)(k.bf * invz);  // cam_project(..., const float& bf)
+        err[0] = (double)o.u - r0;
+        err[1] = (double)o.v - r1;
+        err[2] = (double)o.ur - r2;
+    }
+}
+__device__ bool depth_positive(const G& g, int e) {
+    const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
+    const int lm = g.e_lm[e];
+    if (g.e_type[e] <= 1) {
+        const double* X = g.X + 3 * lm;
+        return (q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t).z > 0.0;
+    }
+    const double* pp = g.P + 4 * (lm - g.Np);
+    return -plane_transform(T, P4{{pp[0], pp[1], pp[2], pp[3]}}).c[3] > 0;
+}
+// EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:103-234)
+__device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double (&A)[3][3], double (&B)[3][6]) {
+    const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
+    const spslam_lba_keyframe& k = g.kf[g.e_kf[e]];
+    const double fx = k.fx, fy = k.fy, bf = k.bf;
+    const double* X = g.X + 3 * g.e_lm[e];
+    const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
+    const double x = p.x, y = p.y, z = p.z, z_2 = z * z;
+    const M3 R = q_to_rot(T.r);
+    if (t == 0) {
+        const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
+        const double s = -1. / z;
+        for (int r = 0; r < 2; r++) {
+            const double t0 = s * tmp[r][0], t1 = s * tmp[r][1], t2 = s * tmp[r][2];
+            for (int q = 0; q < 3; q++) A[r][q] = t0 * R.a[q] + t1 * R.a[3 + q] + t2 * R.a[6 + q];
+        }
+        A[2][0] = A[2][1] = A[2][2] = 0.0;
+    } else {
+        for (int q = 0; q < 3; q++) {
+            A[0][q] = -fx * R.a[q] / z + fx * x * R.a[6 + q] / z_2;
+            A[1][q] = -fy * R.a[3 + q] / z + fy * y * R.a[6 + q] / z_2;
+            A[2][q] = A[0][q] - bf * R.a[6 + q] / z_2;
+        }
+    }
+    B[0][0] = x * y / z_2 * fx; B[0][1] = -(1 + (x * x / z_2)) * fx; B[0][2] = y / z * fx;
+    B[0][3] = -1. / z * fx; B[0][4] = 0; B[0][5] = x / z_2 * fx;
+    B[1][0] = (1 + y * y / z_2) * fy; B[1][1] = -x * y / z_2 * fy; B[1][2] = -x / z * fy;
+    B[1][3] = 0; B[1][4] = -1. / z * fy; B[1][5] = y / z_2 * fy;
+    if (t == 1) {
+        B[2][0] = B[0][0] - bf * y / z_2; B[2][1] = B[0][1] + bf * x / z_2; B[2][2] = B[0][2];
+        B[2][3] = B[0][3]; B[2][4] = 0; B[2][5] = B[0][5] - bf / z_2;
+    } else {
+        for (int q = 0; q < 6; q++) B[2][q] = 0.0;
+    }
+}
+// Eigen compute_inverse<Matrix3d> (cofactors), r row-major
+__device__ __forceinline__ void inverse3(const double (&m)[3][3], double* r) {
+    auto cof = [&](int i, int j) {
+        const int i1 = (i + 1) % 3, i2 = (i + 2) % 3, j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+        return m[i1][j1] * m[i2][j2] - m[i1][j2] * m[i2][j1];
+    };
+    const double c0 = cof(0, 0), c1 = cof(1, 0), c2 = cof(2, 0);
+    const double det = (c0 * m[0][0] + c1 * m[1][0]) + c2 * m[2][0];
+    const double invdet = 1.0 / det;
+    r[0] = c0 * invdet; r[1] = c1 * invdet; r[2] = c2 * invdet;
+    r[3] = cof(0, 1) * invdet; r[4] = cof(1, 1) * invdet; r[5] = cof(2, 1) * invdet;
+    r[6] = cof(0, 2) * invdet; r[7] = cof(1, 2) * invdet; r[8] = cof(2, 2) * invdet;
+}
+
+__device__ __forceinline__ constexpr int upper_idx(int r, int c) { return 6 * r - r * (r - 1) / 2 + (c - r); }  // r <= c < 6
+
+// One edge's quadratic-form terms (BaseBinaryEdge::constructQuadraticForm as Eigen evaluates it, Omega diagonal):
+//   [0, 9)   Hll += (A^T W) A                 [9, 12)  bl += A^T omega_r
+//   [12, 30) Hpl (6 x 3, pose-major) += (B^T W) A (robust) | B^T (A^T Omega)^T (non-robust)
+//   [30, 51) Hpp upper (r <= c) += (B^T W) B  [51, 57) bp += B^T omega_r
+// W = rho' Omega (robust) or Omega; omega_r = (-(Omega e)) rho' or -(Omega e).  Rows >= dim are zero.
+__device__ __forceinline__ void edge_terms(const LbaConsts& C, bool robust, int ty, const double* err, const double* info,
+                                           const double (&A)[3][3], const double (&B)[3][6], bool pfree, double* o) {
+    const int dim = edge_dim(ty);
+    double r0, wgt;
+    huber(chi2_of(err, info, dim), delta_of(C, ty), robust, &r0, &wgt);
+    double W[3], om[3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        W[r] = robust ? wgt * info[r] : info[r];
+        om[r] = -(info[r] * err[r]);
+        if (robust) om[r] *= wgt;
+    }
+    const bool d3 = dim == 3;  // (rows >= dim are not added: a dim-2 edge's sums have two terms)
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double s = A[0][i] * om[0] + A[1][i] * om[1];
+        if (d3) s += A[2][i] * om[2];
+        o[9 + i] = s;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double h = (A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j];
+            if (d3) h += (A[2][i] * W[2]) * A[2][j];
+            o[3 * i + j] = h;
+        }
+    }
+    if (!pfree) return;
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double h;
+            if (robust) {
+                h = (B[0][i] * W[0]) * A[0][j] + (B[1][i] * W[1]) * A[1][j];
+                if (d3) h += (B[2][i] * W[2]) * A[2][j];
+            } else {
+                h = B[0][i] * (A[0][j] * info[0]) + B[1][i] * (A[1][j] * info[1]);
+                if (d3) h += B[2][i] * (A[2][j] * info[2]);
+            }
+            o[12 + 3 * i + j] = h;
+        }
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int j = i; j < 6; j++) {
+            double h = (B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j];
+            if (d3) h += (B[2][i] * W[2]) * B[2][j];
+            o[30 + upper_idx(i, j)] = h;
+        }
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        double s = B[0][i] * om[0] + B[1][i] * om[1];
+        if (d3) s += B[2][i] * om[2];
+        o[51 + i] = s;
+    }
+}
+
+// SparseOptimizer::terminate(): the caller's flag, read through to memory (another thread may raise it), latched
+__device__ __forceinline__ bool stop_requested(const LbgBatch& b, int p, Sh& s) {
+    if (!s.stop && b.stop) s.stop = __hip_atomic_load(b.stop + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+    if (!s.stop && b.stop_after >= 0 && s.trials >= b.stop_after) s.stop = 1;  // spslam_lba_debug_stop_after
+    return s.stop != 0;
+}
+
+// ---------------------------------------------------------------- setup (once)
+__device__ __noinline__ void setup(const G& g, Sh& s, int* dyn_i) {
+    const int t = threadIdx.x;
+    for (int k = t; k < g.K; k += kT) {  // Converter::toSE3Quat
+        const float* T = g.kf[k].Tcw;
+        M3 Rm;
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) Rm.a[3 * i + j] = T[4 * i + j];
+        SE3 q;
+        q.r = q_from_rot(Rm);
+        q.t = V3{T[3], T[7], T[11]};
+        q_normalize(q.r);
+        store_pose(g.pose + 7 * k, q);
+    }
+    for (int i = t; i < g.Np; i += kT)
+        for (int j = 0; j < 3; j++) g.X[3 * i + j] = g.pt[i].xw[j];
+    for (int i = t; i < g.Nq; i += kT) {
+        const P4 q = plane_from_f(g.pl[i].world);
+        for (int j = 0; j < 4; j++) g.P[4 * i + j] = q.c[j];
+    }
+    // edges in insertion order: point observations (points in list order), then plane observations
+    int base_e = 0;
+    for (int ch = 0; ch < g.L; ch += kT) {
+        const int l = ch + t;
+        const int n_obs = l < g.Np ? g.pt[l].n_obs : (l < g.L ? g.pl[l - g.Np].n_obs : 0);
+        int tot;
+        const int off = block_scan(n_obs, &tot, s) + base_e;
+        if (l < g.L) {
+            g.lm_boff[l] = off;
+            g.lm_nb[l] = n_obs;
+            const int src0 = l < g.Np ? g.pt[l].obs_offset : g.pl[l - g.Np].obs_offset;
+            for (int o = 0; o < n_obs; o++) {
+                const int e = off + o;
+                g.e_lm[e] = l;
+                g.e_src[e] = src0 + o;
+                g.e_level[e] = 0;
+                if (l < g.Np) {
+                    const spslam_lba_point_obs& ob = g.pobs[src0 + o];
+                    g.e_kf[e] = ob.kf;
+                    g.e_type[e] = ob.ur < 0 ? 0 : 1;
+                } else {
+                    const spslam_lba_plane_obs& ob = g.plobs[src0 + o];
+                    g.e_kf[e] = ob.kf;
+                    g.e_type[e] = ob.kind == SPSLAM_PLANE_EDGE ? 2 : (ob.kind == SPSLAM_PARALLEL_EDGE ? 3 : 4);
+                }
+            }
+        }
+        base_e += tot;
+    }
+    for (int e = g.E + t; e < lbg_pad32(g.E); e += kT) g.echi[e] = 0.0;
+    // landmark (vertex-id) order: points by id (ids mnId + maxKFid + 1), then planes by id (mnId + maxPointid + 1,
+    // above every point id); stable ranks (id, list index)
+    for (int grp = 0; grp < 2; grp++) {
+        const int n0 = grp ? g.Np : 0, cnt = grp ? g.Nq : g.Np;
+        auto id_of = [&](int i) { return grp ? g.pl[i].id : g.pt[i].id; };
+        int ok = 1;
+        for (int i = t; i + 1 < cnt; i += kT) ok &= id_of(i) <= id_of(i + 1);
+        if (block_and(ok, s)) {
+            for (int i = t; i < cnt; i += kT) g.lm_sorted[n0 + i] = n0 + i;
+            continue;
+        }
+        // rank counting over LDS tiles of ids; ranks accumulate in lm_hidx (free until the structure phase)
+        for (int i = t; i < cnt; i += kT) g.lm_hidx[n0 + i] = 0;
+        constexpr int kTile = kDyn / 4;
+        for (int b0 = 0; b0 < cnt; b0 += kTile) {
+            const int nt = min(kTile, cnt - b0);
+            __syncthreads();
+            for (int j = t; j < nt; j += kT) dyn_i[j] = id_of(b0 + j);
+            __syncthreads();
+            for (int i = t; i < cnt; i += kT) {
+                const int id = id_of(i);
+                int r = 0;
+                for (int j = 0; j < nt; j++) {
+                    const int v = dyn_i[j];
+                    r += v < id || (v == id && b0 + j < i);
+                }
+                g.lm_hidx[n0 + i] += r;
+            }
+        }
+        __syncthreads();
+        for (int i = t; i < cnt; i += kT) g.lm_sorted[n0 + g.lm_hidx[n0 + i]] = n0 + i;
+        __syncthreads();
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- AMD (one lane)
+// Eigen::internal::minimum_degree_ordering (oracle/eigen_simplicial_restated.h), workspace Ci (t ints, the full
+// symmetric pattern in its first Cp[n] entries), W (8 (n + 1) ints), perm (n + 1 ints; perm[k] = k-th pivot).
+__device__ int amd_flip(int i) { return -i - 2; }
+__device__ int amd_wclear(int mark, int lemax, int* w, int n) {
+    if (mark < 2 || (mark + lemax < 0)) {
+        for (int k = 0; k < n; k++)
+            if (w[k] != 0) w[k] = 1;
+        mark = 2;
+    }
+    return mark;
+}
+__device__ __noinline__ void amd_order(int n, int* Cp, int* Ci, int t, int* W, int* perm) {
+    int d, dk, dext, lemax = 0, e, elenk, eln, i, j, k, k1, k2, k3, jlast, ln, dense, nzmax, mindeg = 0, nvi, nvj,
+                     nvk, mark, wnvi, ok, nel = 0, p, p1, p2, p3, p4, pj, pk, pk1, pk2, pn, q, h;
+    dense = max(16, (int)(10 * sqrt((double)n)));
+    dense = min(n - 2, dense);
+    int cnz = Cp[n];
+    int* len = W;
+    int* nv = W + (n + 1);
+    int* next = W + 2 * (n + 1);
+    int* head = W + 3 * (n + 1);
+    int* elen = W + 4 * (n + 1);
+    int* degree = W + 5 * (n + 1);
+    int* w = W + 6 * (n + 1);
+    int* hhead = W + 7 * (n + 1);
+    int* last = perm;
+    for (k = 0; k < n; k++) len[k] = Cp[k + 1] - Cp[k];
+    len[n] = 0;
+    nzmax = t;
+    for (i = 0; i <= n; i++) {
+        head[i] = -1; last[i] = -1; next[i] = -1; hhead[i] = -1;
+        nv[i] = 1; w[i] = 1; elen[i] = 0; degree[i] = len[i];
+    }
+    mark = amd_wclear(0, 0, w, n);
+    for (i = 0; i < n; i++) {  // every column holds its diagonal (the pose's own block)
+        d = degree[i];
+        if (d == 1) {
+            elen[i] = -2; nel++; Cp[i] = -1; w[i] = 0;
+        } else if (d > dense) {
+            nv[i] = 0; elen[i] = -1; nel++; Cp[i] = amd_flip(n); nv[n]++;
+        } else {
+            if (head[d] != -1) last[head[d]] = i;
+            next[i] = head[d];
+            head[d] = i;
+        }
+    }
+    elen[n] = -2; Cp[n] = -1; w[n] = 0;
+    while (nel < n) {
+        for (k = -1; mindeg < n && (k = head[mindeg]) == -1; mindeg++) {
+        }
+        if (next[k] != -1) last[next[k]] = -1;
+        head[mindeg] = next[k];
+        elenk = elen[k];
+        nvk = nv[k];
+        nel += nvk;
+        if (elenk > 0 && cnz + mindeg >= nzmax) {
+            for (j = 0; j < n; j++)
+                if ((p = Cp[j]) >= 0) { Cp[j] = Ci[p]; Ci[p] = amd_flip(j); }
+            for (q = 0, p = 0; p < cnz;) {
+                if ((j = amd_flip(Ci[p++])) >= 0) {
+                    Ci[q] = Cp[j];
+                    Cp[j] = q++;
+                    for (k3 = 0; k3 < len[j] - 1; k3++) Ci[q++] = Ci[p++];
+                }
+            }
+            cnz = q;
+        }
+        dk = 0;
+        nv[k] = -nvk;
+        p = Cp[k];
+        pk1 = (elenk == 0) ? p : cnz;
+        pk2 = pk1;
+        for (k1 = 1; k1 <= elenk + 1; k1++) {
+            if (k1 > elenk) { e = k; pj = p; ln = len[k] - elenk; }
+            else { e = Ci[p++]; pj = Cp[e]; ln = len[e]; }
+            for (k2 = 1; k2 <= ln; k2++) {
+                i = Ci[pj++];
+                if ((nvi = nv[i]) <= 0) continue;
+                dk += nvi;
+                nv[i] = -nvi;
+                Ci[pk2++] = i;
+                if (next[i] != -1) last[next[i]] = last[i];
+                if (last[i] != -1) next[last[i]] = next[i];
+                else head[degree[i]] = next[i];
+            }
+            if (e != k) { Cp[e] = amd_flip(k); w[e] = 0; }
+        }
+        if (elenk != 0) cnz = pk2;
+        degree[k] = dk;
+        Cp[k] = pk1;
+        len[k] = pk2 - pk1;
+        elen[k] = -2;
+        mark = amd_wclear(mark, lemax, w, n);
+        for (pk = pk1; pk < pk2; pk++) {
+            i = Ci[pk];
+            if ((eln = elen[i]) <= 0) continue;
+            nvi = -nv[i];
+            wnvi = mark - nvi;
+            for (p = Cp[i]; p <= Cp[i] + eln - 1; p++) {
+                e = Ci[p];
+                if (w[e] >= mark) w[e] -= nvi;
+                else if (w[e] != 0) w[e] = degree[e] + wnvi;
+            }
+        }
+        for (pk = pk1; pk < pk2; pk++) {
+            i = Ci[pk];
+            p1 = Cp[i];
+            p2 = p1 + elen[i] - 1;
+            pn = p1;
+            for (h = 0, d = 0, p = p1; p <= p2; p++) {
+                e = Ci[p];
+                if (w[e] != 0) {
+                    dext = w[e] - mark;
+                    if (dext > 0) { d += dext; Ci[pn++] = e; h += e; }
+                    else { Cp[e] = amd_flip(k); w[e] = 0; }
+                }
+            }
+            elen[i] = pn - p1 + 1;
+            p3 = pn;
+            p4 = p1 + len[i];
+            for (p = p2 + 1; p < p4; p++) {
+                j = Ci[p];
+                if ((nvj = nv[j]) <= 0) continue;
+                d += nvj;
+                Ci[pn++] = j;
+                h += j;
+            }
+            if (d == 0) {
+                Cp[i] = amd_flip(k);
+                nvi = -nv[i];
+                dk -= nvi; nvk += nvi; nel += nvi;
+                nv[i] = 0; elen[i] = -1;
+            } else {
+                degree[i] = min(degree[i], d);
+                Ci[pn] = Ci[p3];
+                Ci[p3] = Ci[p1];
+                Ci[p1] = k;
+                len[i] = pn - p1 + 1;
+                h %= n;
+                next[i] = hhead[h];
+                hhead[h] = i;
+                last[i] = h;
+            }
+        }
+        degree[k] = dk;
+        lemax = max(lemax, dk);
+        mark = amd_wclear(mark + lemax, lemax, w, n);
+        for (pk = pk1; pk < pk2; pk++) {
+            i = Ci[pk];
+            if (nv[i] >= 0) continue;
+            h = last[i];
+            i = hhead[h];
+            hhead[h] = -1;
+            for (; i != -1 && next[i] != -1; i = next[i], mark++) {
+                ln = len[i];
+                eln = elen[i];
+                for (p = Cp[i] + 1; p <= Cp[i] + ln - 1; p++) w[Ci[p]] = mark;
+                jlast = i;
+                for (j = next[i]; j != -1;) {
+                    ok = (len[j] == ln) && (elen[j] == eln);
+                    for (p = Cp[j] + 1; ok && p <= Cp[j] + ln - 1; p++)
+                        if (w[Ci[p]] != mark) ok = 0;
+                    if (ok) {
+                        Cp[j] = amd_flip(i);
+                        nv[i] += nv[j];
+                        nv[j] = 0;
+                        elen[j] = -1;
+                        j = next[j];
+                        next[jlast] = j;
+                    } else {
+                        jlast = j;
+                        j = next[j];
+                    }
+                }
+            }
+        }
+        for (p = pk1, pk = pk1; pk < pk2; pk++) {
+            i = Ci[pk];
+            if ((nvi = -nv[i]) <= 0) continue;
+            nv[i] = nvi;
+            d = degree[i] + dk - nvi;
+            d = min(d, n - nel - nvi);
+            if (head[d] != -1) last[head[d]] = i;
+            next[i] = head[d];
+            last[i] = -1;
+            head[d] = i;
+            mindeg = min(mindeg, d);
+            degree[i] = d;
+            Ci[p++] = i;
+        }
+        nv[k] = nvk;
+        if ((len[k] = p - pk1) == 0) { Cp[k] = -1; w[k] = 0; }
+        if (elenk != 0) cnz = p;
+    }
+    for (i = 0; i < n; i++) Cp[i] = amd_flip(Cp[i]);
+    for (j = 0; j <= n; j++) head[j] = -1;
+    for (j = n; j >= 0; j--) {
+        if (nv[j] > 0) continue;
+        next[j] = head[Cp[j]];
+        head[Cp[j]] = j;
+    }
+    for (e = n; e >= 0; e--) {
+        if (nv[e] <= 0) continue;
+        if (Cp[e] != -1) { next[e] = head[Cp[e]]; head[Cp[e]] = e; }
+    }
+    int* stack = w;
+    for (k = 0, i = 0; i <= n; i++) {
+        if (Cp[i] != -1) continue;
+        int top = 0;
+        stack[0] = i;
+        while (top >= 0) {
+            const int pp = stack[top];
+            const int ii = head[pp];
+            if (ii == -1) { top--; perm[k++] = pp; }
+            else { head[pp] = next[ii]; stack[++top] = ii; }
+        }
+    }
+}
+
+__device__ __forceinline__ bool coupled(const Sh& s, int q1, int q2) {  // pose blocks (q1, q2) in the Schur pattern
+    return q1 <= q2 ? (s.pat[q1] >> q2) & 1ull : (s.pat[q2] >> q1) & 1ull;
+}
+__device__ __forceinline__ bool bit_of(const uint64_t* bits, int i) { return (bits[i >> 6] >> (i & 63)) & 1ull; }
+
+// ---------------------------------------------------------------- structure (per optimize() pass)
+// initializeOptimization(0) + buildStructure + LinearSolverEigen's symbolic analysis
+__device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
+    const int t = threadIdx.x, lane = t & 63;
+    if (t == 0) s.kfact = 0;
+    __syncthreads();
+    uint64_t m = 0;
+    int na = 0;
+    for (int e = t; e < g.E; e += kT)
+        if (g.e_level[e] == 0) {
+            m |= 1ull << g.e_kf[e];
+            na++;
+        }
+    int nact;
+    block_scan(na, &nact, s);
+    if (t == 0) s.nact = nact;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m |= (uint64_t)__shfl_xor((long long)m, o);
+    if (lane == 0 && m) atomicOr((unsigned long long*)&s.kfact, (unsigned long long)m);
+    __syncthreads();
+    if (t == 0) {  // free poses with an active edge, by id (buildIndexMapping over the id-sorted active vertices)
+        int np = 0;
+        for (int k = 0; k < g.K; k++) s.hidx[k] = -1;
+        for (int k = 0; k < g.K; k++) {
+            const spslam_lba_keyframe& kk = g.kf[k];
+            if (!((s.kfact >> k) & 1ull) || kk.fixed || kk.id == 0) continue;
+            int j = np++;
+            while (j > 0 && g.kf[s.hpose[j - 1]].id > kk.id) { s.hpose[j] = s.hpose[j - 1]; j--; }
+            s.hpose[j] = k;
+        }
+        for (int j = 0; j < np; j++) s.hidx[s.hpose[j]] = j;
+        s.np = np;
+    }
+    __syncthreads();
+    const int np = s.np;
+    // landmarks with an active edge in id order; pose masks of their active edges (the Hpl blocks) and of all
+    // their edges (buildStructure's Schur pattern walks v->edges(), any level)
+    int base = 0;
+    for (int ch = 0; ch < g.L; ch += kT) {
+        const int j = ch + t;
+        const int l = j < g.L ? g.lm_sorted[j] : -1;
+        int act = 0;
+        uint64_t mask = 0, amask = 0;
+        if (l >= 0)
+            for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
+                const int h = s.hidx[g.e_kf[e]];
+                if (h >= 0) amask |= 1ull << h;
+                if (g.e_level[e] == 0) {
+                    act = 1;
+                    if (h >= 0) mask |= 1ull << h;
+                }
+            }
+        int tot;
+        const int off = block_scan(act, &tot, s) + base;
+        if (l >= 0) {
+            g.lm_hidx[l] = act ? off : -1;
+            g.lm_amask[l] = amask;
+            if (act) {
+                g.hidx_lm[off] = l;
+                g.lmh_mask[off] = mask;
+            }
+        }
+        base += tot;
+    }
+    const int nl = base;
+    if (t == 0) s.nl = nl;
+    // Hpl blocks of landmark h at lmh_blk[h] .. (pose order), contiguous in landmark order
+    base = 0;
+    for (int ch = 0; ch < nl; ch += kT) {
+        const int h = ch + t;
+        const int c = h < nl ? __popcll(g.lmh_mask[h]) : 0;
+        int tot;
+        const int off = block_scan(c, &tot, s) + base;
+        if (h < nl) g.lmh_blk[h] = off;
+        base += tot;
+    }
+    if (t == 0) g.lmh_blk[nl] = base;
+    if (t < np) s.pat[t] = 1ull << t;
+    __syncthreads();
+    for (int l = t; l < g.L; l += kT) {
+        const int h = g.lm_hidx[l];
+        const uint64_t mask = h >= 0 ? g.lmh_mask[h] : 0;
+        for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
+            int eb = -1;
+            const int ph = s.hidx[g.e_kf[e]];
+            if (h >= 0 && g.e_level[e] == 0 && ph >= 0) eb = g.lmh_blk[h] + __popcll(mask & ((1ull << ph) - 1ull));
+            g.e_blk[e] = eb;
+        }
+        if (h >= 0) {
+            uint64_t am = g.lm_amask[l];
+            while (am) {
+                const int i1 = __ffsll((unsigned long long)am) - 1;
+                const uint64_t row = g.lm_amask[l] & ~((1ull << i1) - 1ull);
+                atomicOr((unsigned long long*)&s.pat[i1], (unsigned long long)row);
+                am &= am - 1;
+            }
+        }
+    }
+    // per free pose, its active edges in insertion order
+    int o = 0;
+    for (int hh = 0; hh < np; hh++) {
+        const int kfi = s.hpose[hh];
+        if (t == 0) g.pe_off[hh] = o;
+        for (int ch = 0; ch < g.E; ch += kT) {
+            const int e = ch + t;
+            const int f = e < g.E && g.e_level[e] == 0 && g.e_kf[e] == kfi;
+            int tot;
+            const int r = block_scan(f, &tot, s);
+            if (f) g.pe_idx[o + r] = e;
+            o += tot;
+        }
+    }
+    if (t == 0) g.pe_off[np] = o;
+    __syncthreads();
+    // ---- LinearSolverEigen::computeSymbolicDecomposition (analyzePattern, Eigen's AMD)
+    const int n = 6 * np;
+    if (n == 0) {
+        if (t == 0) g.rs_off[0] = 0;
+        __syncthreads();
+        return;
+    }
+    if (t < np) {
+        int c = 0;
+        for (int q = 0; q < np; q++) c += coupled(s, t, q);
+        s.pdeg[t] = c;
+    }
+    __syncthreads();
+    const int dense = min(n - 2, max(16, (int)(10 * sqrt((double)n))));
+    int alld = 1;
+    for (int q = t; q < np; q += kT) alld &= 6 * s.pdeg[q] > dense;
+    if (block_and(alld, s)) {
+        for (int k = t; k < n; k += kT) g.Pinv[k] = k;  // every scalar dense: absorbed in index order (natural)
+    } else {
+        // full symmetric pattern (diagonal kept), columns sorted; cs_amd's elbow room
+        int cnz = 0;
+        for (int q = 0; q < np; q++) cnz += 36 * s.pdeg[q];
+        const int tcap = cnz + cnz / 5 + 2 * n;
+        const bool in_lds = (size_t)(tcap + 10 * (n + 1)) * 4 <= (size_t)kDyn;
+        int* Ci = in_lds ? (int*)dyn : g.amd_Ci;
+        int* W = in_lds ? Ci + tcap : g.amd_W;
+        int* perm = W + 8 * (n + 1);
+        int* Cp = perm + (n + 1);
+        if (t < n) {
+            const int q2 = t / 6;
+            int c0 = 0;
+            for (int q = 0; q < q2; q++) c0 += 6 * s.pdeg[q];
+            c0 *= 6;
+            c0 += (t - 6 * q2) * 6 * s.pdeg[q2];
+            Cp[t] = c0;
+            int c = c0;
+            for (int q = 0; q < np; q++)
+                if (coupled(s, q, q2))
+                    for (int rr = 0; rr < 6; rr++) Ci[c++] = 6 * q + rr;
+        }
+        if (t == 0) Cp[n] = cnz;
+        __syncthreads();
+        if (t == 0) amd_order(n, Cp, Ci, tcap, W, perm);
+        __syncthreads();
+        for (int k = t; k < n; k += kT) g.Pinv[k] = perm[k];
+        __syncthreads();
+    }
+    for (int k = t; k < n; k += kT) g.Pm[g.Pinv[k]] = k;
+    __syncthreads();
+    // lower structure of each column j of ap = P a P^T: Abits[j] = {i > j : (Pinv j, Pinv i) in the pattern}
+    if (t < n) {
+        const int qj = g.Pinv[t] / 6;
+        uint64_t wv[kNW] = {0, 0, 0, 0, 0, 0};
+        for (int i = t + 1; i < n; i++)
+            if (coupled(s, qj, g.Pinv[i] / 6)) wv[i >> 6] |= 1ull << (i & 63);
+#pragma unroll
+        for (int w = 0; w < kNW; w++) g.Abits[t * kNW + w] = wv[w];
+    }
+    __syncthreads();
+    // elimination tree and L's column structures: struct L(:, j) = Abits[j] U (children's structures \ {j});
+    // one lane per bitset word
+    if (t < 64) {
+        uint64_t* acc = (uint64_t*)dyn;  // n x kNW
+        for (int i = lane; i < n * kNW; i += 64) acc[i] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int j = 0; j < n; j++) {
+            uint64_t S = 0;
+            if (lane < kNW) S = g.Abits[j * kNW + lane] | acc[j * kNW + lane];
+            const uint64_t nz = __ballot(lane < kNW && S != 0);
+            int par = -1;
+            if (nz) {
+                const int fw = __ffsll((unsigned long long)nz) - 1;
+                const uint64_t wv = rl64(S, fw);
+                par = 64 * fw + __ffsll((unsigned long long)wv) - 1;
+            }
+            if (lane < kNW) {
+                g.Lbits[j * kNW + lane] = S;
+                if (par >= 0) {
+                    const uint64_t keep = (par >> 6) == lane ? ~(1ull << (par & 63)) : ~0ull;
+                    acc[par * kNW + lane] |= S & keep;
+                }
+            }
+            if (lane == 0) g.parent[j] = par;  // (each lane reads and writes its own word of acc only)
+        }
+    }
+    __syncthreads();
+    // each row k of L: its pattern {i : k in struct L(:, i)} in factorize_preordered's order -- ap's column k
+    // entries in source order (original index ascending), an elimination-tree walk from each, the walks' paths
+    // stacked so that the last path comes first, each path from its start upwards
+    int cnt = 0;
+    if (t < n)
+        for (int i = 0; i < t; i++) cnt += bit_of(g.Lbits + i * kNW, t);
+    int tot;
+    const int off = block_scan(cnt, &tot, s);
+    if (t < n) g.rs_off[t] = off;
+    if (t == 0) g.rs_off[n] = tot;
+    if (t < n && cnt > 0) {
+        const int k = t, ok = g.Pinv[k];
+        uint64_t vis[kNW] = {0, 0, 0, 0, 0, 0};
+        vis[k >> 6] |= 1ull << (k & 63);
+        int* seg = g.rs_idx + off;
+        int wpos = 0;
+        for (int o2 = 0; o2 < n; o2++) {
+            const int r = g.Pm[o2];
+            if (r >= k || !coupled(s, o2 / 6, ok / 6)) continue;
+            int i = r;
+            while (!((vis[i >> 6] >> (i & 63)) & 1ull)) {
+                vis[i >> 6] |= 1ull << (i & 63);
+                seg[wpos++] = i;
+                i = g.parent[i];
+            }
+        }
+        // paths were written in discovery order: reverse the whole row, then each path back to start-upwards
+        for (int a = 0, b2 = cnt - 1; a < b2; a++, b2--) {
+            const int v = seg[a];
+            seg[a] = seg[b2];
+            seg[b2] = v;
+        }
+        int a = 0;
+        while (a < cnt) {  // a reversed path: consecutive entries (prev, next) with parent[next] == prev
+            int b2 = a;
+            while (b2 + 1 < cnt && g.parent[seg[b2 + 1]] == seg[b2]) b2++;
+            for (int x = a, y = b2; x < y; x++, y--) {
+                const int v = seg[x];
+                seg[x] = seg[y];
+                seg[y] = v;
+            }
+            a = b2 + 1;
+        }
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- errors + robust chi2
+// computeActiveErrors: err of every active edge, its robust chi2 (activeRobustChi2's terms) in echi (+0.0 for
+// inactive edges: an exact no-op in the ordered sum)
+__device__ __noinline__ void errors(const G& g, const Sh& s, const LbaConsts& C) {
+    const int t = threadIdx.x;
+    const bool robust = s.robust;
+    for (int e = t; e < g.Ep; e += kT) {
+        double chi = 0.0;
+        if (g.e_level[e] == 0) {
+            const int ty = g.e_type[e];
+            const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
+            double err[3], info[3];
+            point_error(g, e, ty, T, g.X + 3 * g.e_lm[e], err);
+            for (int i = 0; i < 3; i++) g.err[3 * e + i] = err[i];
+            info_of(g, C, e, ty, info);
+            double r1;
+            huber(chi2_of(err, info, edge_dim(ty)), delta_of(C, ty), robust, &chi, &r1);
+        }
+        g.echi[e] = chi;
+    }
+    // plane edges: one lane pair per edge (plane_error_pair)
+    const int npl = g.E - g.Ep;
+    for (int q = t >> 1; q < ((npl + kT / 2 - 1) / (kT / 2)) * (kT / 2); q += kT / 2) {
+        const int e = g.Ep + q;
+        const bool act = q < npl && g.e_level[e] == 0;
+        E3 r{0, 0, 0};
+        if (__any(act)) {
+            const int ee = act ? e : g.Ep + (q < npl ? q : 0);
+            if (q < npl) {
+                const int ty = g.e_type[ee];
+                const double* pp = g.P + 4 * (g.e_lm[ee] - g.Np);
+                r = plane_error_pair(ty - 2, load_pose(g.pose + 7 * g.e_kf[ee]), P4{{pp[0], pp[1], pp[2], pp[3]}},
+                                     plane_from_f(g.plobs[g.e_src[ee]].meas), (t & 1) != 0);
+            }
+        }
+        if (q < npl && (t & 1) == 0) {
+            double chi = 0.0;
+            if (act) {
+                const int ty = g.e_type[e];
+                const double err[3] = {r.e0, r.e1, r.e2};
+                for (int i = 0; i < 3; i++) g.err[3 * e + i] = err[i];
+                double info[3], r1;
+                info_of(g, C, e, ty, info);
+                huber(chi2_of(err, info, edge_dim(ty)), delta_of(C, ty), robust, &chi, &r1);
+            }
+            g.echi[e] = chi;
+        }
+    }
+}
+
+// one lane: sum of v[0 .. n32) in index order (n32 a multiple of 32; two 16-load batches in flight)
+__device__ __forceinline__ double ordered_sum(const double* v, int n32) {
+    double acc = 0.0;
+    double A[16], B[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) A[u] = n32 > 0 ? v[u] : 0.0;
+    for (int e = 0; e < n32; e += 32) {
+#pragma unroll
+        for (int u = 0; u < 16; u++) B[u] = v[e + 16 + u];
+#pragma unroll
+        for (int u = 0; u < 16; u++) acc += A[u];
+        const bool more = e + 32 < n32;
+#pragma unroll
+        for (int u = 0; u < 16; u++) A[u] = more ? v[e + 32 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) acc += B[u];
+    }
+    return acc;
+}
+
+// ---------------------------------------------------------------- per iteration: quadratic forms and sums
+__device__ __noinline__ void build_terms(const G& g, const Sh& s, const LbaConsts& C) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const bool robust = s.robust;
+    for (int e = t; e < g.Ep; e += kT) {
+        if (g.e_level[e] != 0) continue;
+        const int ty = g.e_type[e];
+        double A[3][3], B[3][6], info[3], err[3], o[kLbaCon];
+        point_jacobians(g, e, ty, A, B);
+        info_of(g, C, e, ty, info);
+        for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
+        const bool pfree = s.hidx[g.e_kf[e]] >= 0;
+        edge_terms(C, robust, ty, err, info, A, B, pfree, o);
+        double* dst = g.terms + (size_t)kLbaCon * e;
+#pragma unroll
+        for (int j = 0; j < kLbaCon; j++)
+            if (j < 12 || pfree) dst[j] = o[j];
+    }
+    // plane / parallel / vertical edges: numeric Jacobians (base_binary_edge.hpp:130-205), one wave per edge;
+    // evaluation q < 6: plane perturbed by +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose
+    // exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; evaluation q on the lane pair (2q, 2q + 1)
+    for (int pe = g.Ep + wv; pe < g.E; pe += kW) {
+        if (g.e_level[pe] != 0) continue;  // wave-uniform
+        const int ty = g.e_type[pe], dim = edge_dim(ty), lm = g.e_lm[pe];
+        const bool pfree = s.hidx[g.e_kf[pe]] >= 0;
+        const SE3 T0 = load_pose(g.pose + 7 * g.e_kf[pe]);
+        const double* pp = g.P + 4 * (lm - g.Np);
+        const P4 P0{{pp[0], pp[1], pp[2], pp[3]}};
+        const P4 meas = plane_from_f(g.plobs[g.e_src[pe]].meas);
+        const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+        double ev[3] = {0, 0, 0};
+        const int q = lane >> 1;
+        if (q < 18 && (q < 6 || pfree)) {
+            const double sgn = (q & 1) ? -delta : delta;
+            SE3 T = T0;
+            P4 P = P0;
+            if (q < 6) {
+                double add[3] = {0, 0, 0};
+                add[q >> 1] = sgn;
+                p_oplus(P, add);
+            } else {
+                double add[6] = {0, 0, 0, 0, 0, 0};
+                add[(q - 6) >> 1] = sgn;
+                T = se3_mul(se3_exp(add), T0);
+            }
+            const E3 r = plane_error_pair(ty - 2, T, P, meas, (lane & 1) != 0);
+            ev[0] = r.e0; ev[1] = r.e1; ev[2] = r.e2;
+        }
+        double A[3][3], B[3][6];
+#pragma unroll
+        for (int d = 0; d < 3; d++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const double ep = __shfl(ev[i], 2 * (2 * d)), em = __shfl(ev[i], 2 * (2 * d + 1));
+                A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
+            }
+#pragma unroll
+        for (int d = 0; d < 6; d++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const double ep = __shfl(ev[i], 2 * (6 + 2 * d)), em = __shfl(ev[i], 2 * (7 + 2 * d));
+                B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
+            }
+        if (lane == 0) {
+            double info[3], err[3], o[kLbaCon];
+            info_of(g, C, pe, ty, info);
+            for (int i = 0; i < 3; i++) err[i] = g.err[3 * pe + i];
+            edge_terms(C, robust, ty, err, info, A, B, pfree, o);
+            double* dst = g.terms + (size_t)kLbaCon * pe;
+#pragma unroll
+            for (int j = 0; j < kLbaCon; j++)
+                if (j < 12 || pfree) dst[j] = o[j];
+        }
+    }
+}
+
+// Hll, bl and the Hpl blocks of every active landmark over its edges in insertion order (one thread per
+// landmark); Hpp, bp of every free pose over its edges in insertion order (one lane per (pose, term)).
+// Returns (in s.red[0][1]) computeLambdaInit's max |diagonal|.
+__device__ __noinline__ void build_sums(const G& g, Sh& s) {
+    const int t = threadIdx.x;
+    const int nl = s.nl, np = s.np;
+    double mx = 0.0;
+    for (int h = t; h < nl; h += kT) {
+        const int l = g.hidx_lm[h];
+        const int b0 = g.lmh_blk[h];
+        double H[9], bv[3];
+        for (int j = 0; j < 9; j++) H[j] = 0.0;
+        for (int j = 0; j < 3; j++) bv[j] = 0.0;
+        uint64_t touched = 0;
+        for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
+            if (g.e_level[e] != 0) continue;
+            const double* tm = g.terms + (size_t)kLbaCon * e;
+            for (int j = 0; j < 9; j++) H[j] += tm[j];
+            for (int j = 0; j < 3; j++) bv[j] += tm[9 + j];
+            const int bk = g.e_blk[e];
+            if (bk >= 0) {
+                double* dst = g.blkB + (size_t)18 * bk;
+                const uint64_t bit = 1ull << (bk - b0);
+                if (touched & bit)
+                    for (int j = 0; j < 18; j++) dst[j] += tm[12 + j];
+                else
+                    for (int j = 0; j < 18; j++) dst[j] = 0.0 + tm[12 + j];
+                touched |= bit;
+            }
+        }
+        for (int j = 0; j < 9; j++) g.Hll[9 * h + j] = H[j];
+        for (int j = 0; j < 3; j++) g.bl[3 * h + j] = bv[j];
+        mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
+    }
+    for (int task = t; task < 27 * np; task += kT) {
+        const int hh = task / 27, j = task - 27 * hh;
+        const int i0 = g.pe_off[hh], i1 = g.pe_off[hh + 1];
+        double acc = 0.0;
+        int i = i0;
+        for (; i + 8 <= i1; i += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = g.terms[(size_t)kLbaCon * g.pe_idx[i + u] + 30 + j];
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc += v[u];
+        }
+        for (; i < i1; i++) acc += g.terms[(size_t)kLbaCon * g.pe_idx[i] + 30 + j];
+        g.Hps[27 * hh + j] = acc;
+        if (j == 0 || j == 6 || j == 11 || j == 15 || j == 18 || j == 20) mx = fmax(mx, fabs(acc));
+    }
+    mx = block_max(mx, s);
+    if (t == 0) s.red[0][1] = mx;
+}
+
+// ---------------------------------------------------------------- per trial
+
+// setLambda + the Schur complement (block_solver.hpp:367-436): landmark inverses, BDinv, then the ordered chains
+__device__ __noinline__ void schur(const G& g, Sh& s) {
+    const int t = threadIdx.x;
+    const int nl = s.nl, np = s.np, n = 6 * np;
+    const double lam = s.lambda;
+    for (int h = t; h < nl; h += kT) {
+        double D[3][3];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) D[i][j] = g.Hll[9 * h + 3 * i + j] + (i == j ? lam : 0.0);
+        double Di[9];
+        inverse3(D, Di);
+        for (int j = 0; j < 9; j++) g.Dinv[9 * h + j] = Di[j];
+        const double* bv = g.bl + 3 * h;
+        for (int i = 0; i < 3; i++) g.db[3 * h + i] = (Di[3 * i] * bv[0] + Di[3 * i + 1] * bv[1]) + Di[3 * i + 2] * bv[2];
+        for (int bk = g.lmh_blk[h]; bk < g.lmh_blk[h + 1]; bk++) {
+            const double* Bi = g.blkB + (size_t)18 * bk;
+            double* BD = g.blkBD + (size_t)18 * bk;
+            for (int r = 0; r < 6; r++)
+                for (int q = 0; q < 3; q++)
+                    BD[3 * r + q] = (Bi[3 * r] * Di[q] + Bi[3 * r + 1] * Di[3 + q]) + Bi[3 * r + 2] * Di[6 + q];
+        }
+    }
+    __syncthreads();
+    // tasks: (i1 <= i2 in the pattern, row r of the block); the diagonal block's tasks also chain Bb (the rhs)
+    int nb = 0;
+    for (int q = 0; q < np; q++) nb += __popcll(s.pat[q]);
+    for (int task = t; task < 6 * nb; task += kT) {
+        const int blk = task / 6, r = task - 6 * blk;
+        int i1 = 0, rem = blk;
+        while (rem >= __popcll(s.pat[i1])) { rem -= __popcll(s.pat[i1]); i1++; }
+        uint64_t row = s.pat[i1];
+        for (int u = 0; u < rem; u++) row &= row - 1;
+        const int i2 = __ffsll((unsigned long long)row) - 1;
+        const bool diag = i1 == i2;
+        double acc[6];
+        for (int c = 0; c < 6; c++) {
+            double base = 0.0;
+            if (diag && c >= r) base = c == r ? g.Hps[27 * i1 + upper_idx(r, c)] + lam : g.Hps[27 * i1 + upper_idx(r, c)];
+            acc[c] = 0.0 + base;
+        }
+        double cf = 0.0;
+        const uint64_t need = (1ull << i1) | (1ull << i2);
+        for (int h = 0; h < nl; h++) {
+            const uint64_t mk = g.lmh_mask[h];
+            if ((mk & need) != need) continue;
+            const int b0 = g.lmh_blk[h];
+            const double* BD = g.blkBD + (size_t)18 * (b0 + __popcll(mk & ((1ull << i1) - 1ull))) + 3 * r;
+            const double* Bj = g.blkB + (size_t)18 * (b0 + __popcll(mk & ((1ull << i2) - 1ull)));
+            const double d0 = BD[0], d1 = BD[1], d2 = BD[2];
+            for (int c = 0; c < 6; c++) acc[c] -= (d0 * Bj[3 * c] + d1 * Bj[3 * c + 1]) + d2 * Bj[3 * c + 2];
+            if (diag) {
+                const double* db = g.db + 3 * h;
+                cf += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
+            }
+        }
+        for (int c = 0; c < 6; c++) g.S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc[c];
+        if (diag) g.bs[6 * i1 + r] = g.Hps[27 * i1 + 21 + r] - cf;
+    }
+}
+
+// LinearSolverEigen::solve: SimplicialLDLT::factorize + solve on wave 0.  Row r of the permuted system lives in
+// lane r & 63, register r >> 6.  LD: L column-major (LD[i n + r] = L(r, i)), LB: L's column structures (bitsets),
+// RS / RO: the rows' pattern orders, PI: Pinv.
+template <int kC>
+__device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const uint64_t* LB, const int* RS, const int* RO,
+                             const int* PI) {
+    const int lane = threadIdx.x & 63;
+    const int n = 6 * s.np;
+    double Dg[kC];
+#pragma unroll
+    for (int m = 0; m < kC; m++) Dg[m] = 0.0;
+    bool ok = true;
+    for (int k = 0; k < n; k++) {
+        const int ok_ = PI[k], qk = ok_ / 6;
+        double y[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) {
+            const int r = 64 * m + lane;
+            y[m] = 0.0;
+            if (r <= k) {
+                const int orr = PI[r];
+                if (coupled(s, orr / 6, qk)) {
+                    const int lo = min(orr, ok_), hi = max(orr, ok_);
+                    y[m] = 0.0 + g.S[(size_t)lo * n + hi];
+                }
+            }
+        }
+        double d = pick(y, k) * 1.0 + 0.0;
+        const int t0 = RO[k], t1 = RO[k + 1];
+        for (int tt = t0; tt < t1; tt++) {
+            const int i = uni(RS[tt]);
+            const double yi = pick(y, i);
+            const uint64_t* cb = LB + (size_t)i * kNW;
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                if (r < k && ((cb[m] >> lane) & 1ull)) y[m] = y[m] - LD[(size_t)i * n + r] * yi;
+            }
+        }
+        double pr[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) {
+            const int r = 64 * m + lane;
+            pr[m] = 0.0;
+            if (r < k && bit_of(LB + (size_t)r * kNW, k)) {
+                const double l = y[m] / Dg[m];
+                LD[(size_t)r * n + k] = l;
+                pr[m] = l * y[m];
+            }
+        }
+        for (int tt = t0; tt < t1; tt++) d -= pick(pr, uni(RS[tt]));
+#pragma unroll
+        for (int m = 0; m < kC; m++)
+            if (64 * m + lane == k) Dg[m] = d;
+        if (d == 0.0) {
+            ok = false;
+            break;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (lane == 0) s.ok = ok;
+    if (!ok) return;
+    // x = P b; L x = x; x = D^-1 x; L^T x = x; x = P^-1 x
+    const bool haveL = RO[n] > 0;
+    double tv[kC];
+#pragma unroll
+    for (int m = 0; m < kC; m++) {
+        const int r = 64 * m + lane;
+        tv[m] = r < n ? g.bs[PI[r]] : 0.0;
+    }
+    if (haveL)
+        for (int i = 0; i < n; i++) {
+            const double tmp = pick(tv, i);
+            if (tmp != 0.0) {
+                const uint64_t* cb = LB + (size_t)i * kNW;
+#pragma unroll
+                for (int m = 0; m < kC; m++) {
+                    const int r = 64 * m + lane;
+                    if ((cb[m] >> lane) & 1ull) tv[m] = tv[m] - tmp * LD[(size_t)i * n + r];
+                }
+            }
+        }
+#pragma unroll
+    for (int m = 0; m < kC; m++)
+        if (64 * m + lane < n) tv[m] = (1.0 / Dg[m]) * tv[m];
+    if (haveL)
+        for (int i = n - 1; i >= 0; i--) {
+            const uint64_t* cb = LB + (size_t)i * kNW;
+            double pr[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                pr[m] = ((cb[m] >> lane) & 1ull) ? LD[(size_t)i * n + r] * tv[m] : 0.0;
+            }
+            double tmp = pick(tv, i);
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                uint64_t bits = (uint64_t)(uint32_t)uni((int)(uint32_t)cb[m]) | ((uint64_t)(uint32_t)uni((int)(cb[m] >> 32)) << 32);
+                while (bits) {
+                    const int r = __ffsll((unsigned long long)bits) - 1;
+                    tmp -= rl(pr[m], r);
+                    bits &= bits - 1;
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < kC; m++)
+                if (64 * m + lane == i) tv[m] = tmp;
+        }
+#pragma unroll
+    for (int m = 0; m < kC; m++) {
+        const int r = 64 * m + lane;
+        if (r < n) g.x[PI[r]] = tv[m];
+    }
+}
+
+// landmark increments (xl = Dinv (bl - Hpl^T xp)), push, update (block_solver.hpp:444-471, oplus)
+__device__ __noinline__ void update(const G& g, const Sh& s) {
+    const int t = threadIdx.x;
+    const int nl = s.nl, np = s.np, n = 6 * np;
+    const bool ok = s.ok;
+    for (int h = t; h < nl; h += kT) {
+        const int l = g.hidx_lm[h];
+        if (l < g.Np) for (int j = 0; j < 3; j++) g.X_b[3 * l + j] = g.X[3 * l + j];
+        else for (int j = 0; j < 4; j++) g.P_b[4 * (l - g.Np) + j] = g.P[4 * (l - g.Np) + j];
+        double xl[3] = {0.0, 0.0, 0.0};
+        if (ok) {
+            double cl[3] = {g.bl[3 * h], g.bl[3 * h + 1], g.bl[3 * h + 2]};
+            uint64_t m = g.lmh_mask[h];
+            int bk = g.lmh_blk[h];
+            while (m) {
+                const int p = __ffsll((unsigned long long)m) - 1;
+                m &= m - 1;
+                const double* B = g.blkB + (size_t)18 * bk++;
+                for (int i = 0; i < 3; i++) {
+                    double sm = 0;
+                    for (int r = 0; r < 6; r++) sm += B[3 * r + i] * (-g.x[6 * p + r]);
+                    cl[i] += sm;
+                }
+            }
+            const double* Di = g.Dinv + 9 * h;
+            for (int i = 0; i < 3; i++) xl[i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
+            if (l < g.Np) {
+                for (int j = 0; j < 3; j++) g.X[3 * l + j] += xl[j];
+            } else {
+                double* pp = g.P + 4 * (l - g.Np);
+                P4 P{{pp[0], pp[1], pp[2], pp[3]}};
+                p_oplus(P, xl);
+                for (int j = 0; j < 4; j++) pp[j] = P.c[j];
+            }
+        }
+        for (int j = 0; j < 3; j++) g.x[n + 3 * h + j] = xl[j];
+    }
+    for (int k = t; k < g.K; k += kT) {
+        for (int j = 0; j < 7; j++) g.pose_b[7 * k + j] = g.pose[7 * k + j];
+        const int h = s.hidx[k];
+        if (!ok || h < 0) continue;
+        double u[6];
+        for (int j = 0; j < 6; j++) u[j] = g.x[6 * h + j];
+        store_pose(g.pose + 7 * k, se3_mul(se3_exp(u), load_pose(g.pose + 7 * k)));
+    }
+}
+
+__device__ __noinline__ void restore(const G& g, const Sh& s) {  // pop()
+    const int t = threadIdx.x;
+    for (int h = t; h < s.nl; h += kT) {
+        const int l = g.hidx_lm[h];
+        if (l < g.Np) for (int j = 0; j < 3; j++) g.X[3 * l + j] = g.X_b[3 * l + j];
+        else for (int j = 0; j < 4; j++) g.P[4 * (l - g.Np) + j] = g.P_b[4 * (l - g.Np) + j];
+    }
+    for (int k = t; k < g.K; k += kT)
+        for (int j = 0; j < 7; j++) g.pose[7 * k + j] = g.pose_b[7 * k + j];
+}
+
+// computeScale terms x_j (lambda x_j + b_j), poses then landmarks (Hessian order), zero-padded to 32
+__device__ __noinline__ void scale_terms(const G& g, const Sh& s) {
+    const int t = threadIdx.x;
+    const int n = 6 * s.np, tot = n + 3 * s.nl, pad = lbg_pad32(tot);
+    const double lam = s.lambda;
+    for (int j = t; j < pad; j += kT) {
+        double v = 0.0;
+        if (j < tot && s.ok) {
+            const double b = j < n ? g.Hps[27 * (j / 6) + 21 + j % 6] : g.bl[j - n];
+            const double x = g.x[j];
+            v = x * (lam * x + b);
+        }
+        g.sc[j] = v;
+    }
+}
+
+// ---------------------------------------------------------------- outputs
+__device__ __noinline__ void outputs(const LbgBatch& b, int p, const G& g, Sh& s, const LbaConsts& C) {
+    const int t = threadIdx.x;
+    const spslam_lba_problem pb = b.probs[p];
+    if (s.stopped == 1) {  // returned before optimizing: the map is untouched, nothing is erased
+        // (setup did not run: the observations are addressed through the input records)
+        for (int i = t; i < g.Np; i += kT)
+            for (int o = g.pt[i].obs_offset; o < g.pt[i].obs_offset + g.pt[i].n_obs; o++) b.pobs_out[o] = 0;
+        for (int i = t; i < g.Nq; i += kT)
+            for (int o = g.pl[i].obs_offset; o < g.pl[i].obs_offset + g.pl[i].n_obs; o++) b.plobs_out[o] = 0;
+        for (int i = t; i < 16 * g.K; i += kT) b.kf_out[16 * (size_t)pb.kf_offset + i] = g.kf[i / 16].Tcw[i % 16];
+        for (int i = t; i < 3 * g.Np; i += kT) b.pt_out[3 * (size_t)pb.point_offset + i] = g.pt[i / 3].xw[i % 3];
+        for (int i = t; i < 4 * g.Nq; i += kT) b.pl_out[4 * (size_t)pb.plane_offset + i] = g.pl[i / 4].world[i % 4];
+        if (t == 0) {
+            spslam_lba_result* r = b.res + p;
+            *r = spslam_lba_result{};
+            r->stopped = 1;
+        }
+        return;
+    }
+    int cnt[2] = {0, 0};
+    for (int e = t; e < g.E; e += kT) {
+        double info[3];
+        const int ty = g.e_type[e];
+        info_of(g, C, e, ty, info);
+        const double chi = chi2_of(g.err + 3 * e, info, edge_dim(ty));
+        if (ty <= 1) {
+            const bool bad = chi > (ty == 0 ? 5.991 : 7.815) || !depth_positive(g, e);
+            b.pobs_out[g.e_src[e]] = bad;
+            cnt[0] += bad;
+        } else {
+            const bool bad = ty == 2 ? chi > C.plane_chi : chi > C.vp_chi;
+            b.plobs_out[g.e_src[e]] = bad;
+            cnt[1] += bad;
+        }
+    }
+    int tot0, tot1;
+    block_scan(cnt[0], &tot0, s);
+    block_scan(cnt[1], &tot1, s);
+    for (int k = t; k < g.K; k += kT) {
+        float* o = b.kf_out + 16 * ((size_t)pb.kf_offset + k);
+        if (g.kf[k].fixed) {
+            for (int j = 0; j < 16; j++) o[j] = g.kf[k].Tcw[j];
+            continue;
+        }
+        const SE3 T = load_pose(g.pose + 7 * k);
+        const M3 Rm = q_to_rot(T.r);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) o[4 * i + j] = (float)Rm.a[3 * i + j];
+        o[3] = (float)T.t.x; o[7] = (float)T.t.y; o[11] = (float)T.t.z;
+        o[12] = 0.f; o[13] = 0.f; o[14] = 0.f; o[15] = 1.f;
+    }
+    for (int i = t; i < g.Np; i += kT)
+        for (int j = 0; j < 3; j++) b.pt_out[3 * ((size_t)pb.point_offset + i) + j] = (float)g.X[3 * i + j];
+    for (int i = t; i < g.Nq; i += kT)
+        for (int j = 0; j < 4; j++) b.pl_out[4 * ((size_t)pb.plane_offset + i) + j] = (float)g.P[4 * i + j];
+    if (t == 0) {
+        spslam_lba_result* r = b.res + p;
+        *r = spslam_lba_result{};
+        r->iterations[0] = s.its[0];
+        r->iterations[1] = s.its[1];
+        r->n_point_outliers = tot0;
+        r->n_plane_outliers = tot1;
+        r->status = s.fail ? -3 : 0;
+        r->trials = s.trials;
+        r->stopped = s.stopped;
+    }
+}
+
+// ---------------------------------------------------------------- the schedule
+__global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+    __shared__ Sh s;
+    __shared__ G gsh;  // the problem's pointers, read from LDS where used (not ~100 registers held throughout)
+    const int p = blockIdx.x, t = threadIdx.x;
+    if (t == 0) gsh = make_g(b, p);
+    __syncthreads();
+    const G& g = gsh;
+    const long long t0 = wall_clock64();
+    if (g.K > kMaxK) {
+        if (t == 0) {
+            b.res[p] = spslam_lba_result{};
+            b.res[p].status = -2;
+        }
+        return;
+    }
+    if (t == 0) {
+        s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1;
+        s.done = stop_requested(b, p, s) ? 1 : 0;  // if(*pbStopFlag) return; before initializeOptimization
+        if (s.done) s.stopped = 1;
+    }
+    __syncthreads();
+    if (!s.done) setup(g, s, (int*)dyn);
+    if (t == 0 && g.E == 0) s.done = 1;  // no edges: nothing to optimise, the map goes back through the converters
+    __syncthreads();
+    for (int pass = 0; pass < 2 && !s.done; pass++) {
+        structure(g, s, dyn);
+        const int n = 6 * s.np;
+        // the factorisation's operands in LDS for n <= kLdsN: L, its column structures, the rows' pattern orders, P
+        const bool lds = n <= kLdsN;
+        double* LD = lds ? (double*)dyn : g.Ld;
+        uint64_t* LB = lds ? (uint64_t*)(dyn + (size_t)n * n * 8) : g.Lbits;
+        int* RO = lds ? (int*)(LB + (size_t)n * kNW) : g.rs_off;
+        int* RS = lds ? RO + (n + 1) : g.rs_idx;
+        int* PI = lds ? RS + (n * (n + 1)) / 2 + 1 : g.Pinv;
+        if (lds) {
+            for (int i = t; i < n * kNW; i += kT) LB[i] = g.Lbits[i];
+            for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
+            const int nz = g.rs_off[n];
+            for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
+            for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
+        }
+        if (t == 0) {
+            s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1;
+        }
+        __syncthreads();
+        // SparseOptimizer::optimize on a graph without active edges (every edge relabelled): nothing to do
+        const bool empty = s.nact == 0 || (s.np == 0 && s.nl == 0);
+        // SparseOptimizer::optimize(max_it) with OptimizationAlgorithmLevenberg
+        for (int it = 0; it < (empty ? 0 : pass ? 10 : 5); it++) {
+            if (t == 0 && stop_requested(b, p, s)) {  // for (...; !terminate(); ...)
+                s.stopped = pass == 0 && s.trials == 0 ? 1 : 2;
+                s.done = 1;
+            }
+            __syncthreads();
+            if (s.done) break;
+            if (s.need_err) {
+                errors(g, s, C);
+                __syncthreads();
+                if (t == 0) s.currentChi = ordered_sum(g.echi, lbg_pad32(g.E));
+                __syncthreads();
+            }
+            if (t == 0) s.iniChi = s.currentChi;
+            build_terms(g, s, C);
+            __syncthreads();
+            build_sums(g, s);
+            __syncthreads();
+            if (t == 0) {
+                if (it == 0) { s.lambda = 1e-5 * s.red[0][1]; s.ni = 2; s.nBad = 0; }
+                s.qmax = 0;
+            }
+            __syncthreads();
+            double rho = 0.0;
+            bool more = true;
+            while (more) {
+                schur(g, s);
+                __syncthreads();
+                if (t < 64) {
+                    if (n <= 64) factor_solve<1>(g, s, LD, LB, RS, RO, PI);
+                    else if (n <= 128) factor_solve<2>(g, s, LD, LB, RS, RO, PI);
+                    else if (n <= 192) factor_solve<3>(g, s, LD, LB, RS, RO, PI);
+                    else if (n <= 256) factor_solve<4>(g, s, LD, LB, RS, RO, PI);
+                    else factor_solve<6>(g, s, LD, LB, RS, RO, PI);
+                }
+                if (n == 0 && t == 0) s.ok = 1;
+                __syncthreads();
+                update(g, s);
+                __syncthreads();
+                errors(g, s, C);
+                scale_terms(g, s);
+                __syncthreads();
+                if (t == 0) s.tempChi = ordered_sum(g.echi, lbg_pad32(g.E));
+                if (t == 64) s.scale = ordered_sum(g.sc, lbg_pad32(n + 3 * s.nl));
+                __syncthreads();
+                if (t == 0) {
+                    double tempChi = s.ok ? s.tempChi : DBL_MAX;
+                    double r = s.currentChi - tempChi;
+                    double scale = s.scale;
+                    scale += 1e-3;
+                    r /= scale;
+                    if (r > 0 && isfinite(tempChi)) {
+                        double alpha = 1. - libm64cr::cube_(2 * r - 1);
+                        alpha = fmin(alpha, 2. / 3.);
+                        s.lambda *= fmax(1. / 3., alpha);
+                        s.ni = 2;
+                        s.currentChi = tempChi;
+                        s.accepted = 1;
+                    } else {
+                        s.lambda *= s.ni;
+                        s.ni *= 2;
+                        s.accepted = 0;
+                    }
+                    s.qmax++;
+                    s.trials++;
+                    s.red[0][2] = r;
+                    const bool stop = stop_requested(b, p, s);
+                    s.flag = r < 0 && s.qmax < 10 && !stop;  // do { ... } while (rho < 0 && qmax < max && !terminate())
+                }
+                __syncthreads();
+                if (!s.accepted) {
+                    restore(g, s);
+                    __syncthreads();
+                }
+                rho = s.red[0][2];
+                more = s.flag;
+            }
+            if (t == 0) {
+                s.need_err = !s.accepted;  // an accepted trial's errors are the new state's (same operands, same bits)
+                s.its[pass]++;
+                bool term = s.qmax == 10 || rho == 0;
+                if (!term) {
+                    if ((s.iniChi - s.currentChi) * 1e3 < s.iniChi) s.nBad++;
+                    else s.nBad = 0;
+                    term = s.nBad >= 3;
+                }
+                s.flag = term;
+                if (s.stop && !term && it + 1 < (pass ? 10 : 5)) {  // the next iteration's terminate() check
+                    s.stopped = 2;
+                    s.done = 1;
+                }
+            }
+            __syncthreads();
+            if (s.flag || s.done) break;
+        }
+        if (s.done) break;
+        if (pass == 0) {
+            if (t == 0 && stop_requested(b, p, s)) {  // bDoMore = !*pbStopFlag
+                s.stopped = 2;
+                s.done = 1;
+            }
+            __syncthreads();
+            if (s.done) break;
+            // relabel with the errors cached by the last computeActiveErrors, drop the robust kernels
+            for (int e = t; e < g.E; e += kT) {
+                double info[3];
+                const int ty = g.e_type[e];
+                info_of(g, C, e, ty, info);
+                const double chi = chi2_of(g.err + 3 * e, info, edge_dim(ty));
+                bool bad;
+                if (ty == 0) bad = chi > 5.991 || !depth_positive(g, e);
+                else if (ty == 1) bad = chi > 7.815 || !depth_positive(g, e);
+                else if (ty == 2) bad = chi > C.plane_chi;
+                else bad = chi > C.vp_chi;
+                if (bad) g.e_level[e] = 1;
+            }
+            if (t == 0) s.robust = 0;
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    outputs(b, p, g, s, C);
+    if (t == 0) b.res[p].phase_us[0] = (float)((wall_clock64() - t0) * 0.01);
+}
+
+}  // namespace lbag
+
+hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer) {
+    using namespace lbag;
+    static const hipError_t attr =
+        hipFuncSetAttribute((const void*)k_lba_g2o, hipFuncAttributeMaxDynamicSharedMemorySize, kDyn);
+    if (attr != hipSuccess) return attr;
+    if (timer) timer->begin(kKindLba, s);
+    hipLaunchKernelGGL(k_lba_g2o, dim3(b.n), dim3(kT), kDyn, s, b, C);
+    if (timer) timer->end(kKindLba, s);
+    return hipGetLastError();
+}
+
+}  // namespace spslam

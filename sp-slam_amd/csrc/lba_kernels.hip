@@ -557,9 +557,9 @@ __global__ __launch_bounds__(kThreads) void k_errors(LbaBatch b, LbaWork w, LbaC
     Ctx c = make_ctx(b, task.x);
     const LbaCtl& k = *c.ctl;
     if (k.state != (mode == 0 ? kIter : kTrial)) return;
-    // the landmark part of computeLambdaInit's max is gathered by atomic max into part_max[0] (slots
-    // 1 .. nLc - 1 stay zero); cleared here, before the iteration's sums
-    if (mode == 0 && task.y == 0 && threadIdx.x < c.nLc) c.part_max[threadIdx.x] = 0.0;
+    // the landmark part of computeLambdaInit's max is gathered by atomic max into part_max[0]; cleared here,
+    // before the iteration's sums (every problem that reaches ITER has an edge chunk at task.y == 0)
+    if (mode == 0 && task.y == 0 && threadIdx.x == 0) c.part_max[0] = 0.0;
     const int e = task.y + threadIdx.x;
     double acc[1] = {0.0};
     if (e < c.E && c.e_level[e] == 0) {
@@ -906,9 +906,10 @@ __global__ void k_iter_begin(LbaBatch b) {
     k.currentChi = chi;
     k.iniChi = chi;
     if (k.it == 0) {  // computeLambdaInit: tau * max |diag| over the Hessian vertices
-        double mx = 0.0;
+        // the landmark maximum is gathered by atomic max into part_max[0]; the pose maxima sit at [nLc, nLc + K)
+        double mx = c.part_max[0];
 #pragma unroll 8
-        for (int i = 0; i < c.nLc + c.K; i++) mx = fmax(mx, c.part_max[i]);
+        for (int i = c.nLc; i < c.nLc + c.K; i++) mx = fmax(mx, c.part_max[i]);
         k.lambda = 1e-5 * mx;
         k.ni = 2;
         k.nBad = 0;

@@ -111,6 +111,64 @@ struct LbaBatch {
     int stop_after;       // test hook: the flag counts as raised once a problem has run this many trials (-1 off)
 };
 
+// ---------------------------------------------------------------------------------------------------------------
+// g2o-order LocalBundleAdjustment (lba_g2o.hip, the default): one persistent workgroup per problem runs the whole
+// schedule with every sum in g2o's order.  Per-problem scratch, computed identically on host and device.
+constexpr int kLbgThreads = 512;
+struct LbgLayout {
+    size_t pose, pose_b, X, X_b, P, P_b, err, echi, sc, terms, Hll, bl, Dinv, db, blkB, blkBD, Hps, S, bs, x, Ld;  // double
+    size_t e_lm, e_kf, e_type, e_level, e_src, e_blk, lm_boff, lm_nb, lm_sorted, lm_hidx, hidx_lm, lmh_blk, pe_off,
+        pe_idx, Pinv, Pm, parent, rs_off, rs_idx, amd_Ci, amd_W;                                           // int
+    size_t lmh_mask, lm_amask, Lbits, Abits;                                                                // uint64
+    size_t bytes;
+};
+__host__ __device__ inline int lbg_pad32(int n) { return (n + 31) & ~31; }
+__host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
+    LbgLayout Ly{};
+    const size_t L = (size_t)Np + Nq, n = 6 * (size_t)K, Ep = lbg_pad32(E), Xn = lbg_pad32((int)(n + 3 * L));
+    const size_t nC = n * n + n * n / 5 + 2 * n;  // cs_amd's elbow room over the full symmetric pattern
+    size_t o = 0;
+    auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
+    Ly.pose = take(K * 7 * 8); Ly.pose_b = take(K * 7 * 8);
+    Ly.X = take(Np * 3 * 8); Ly.X_b = take(Np * 3 * 8);
+    Ly.P = take(Nq * 4 * 8); Ly.P_b = take(Nq * 4 * 8);
+    Ly.err = take((size_t)E * 3 * 8); Ly.echi = take(Ep * 8); Ly.sc = take(Xn * 8);
+    Ly.terms = take((size_t)E * kLbaCon * 8);
+    Ly.Hll = take(L * 9 * 8); Ly.bl = take(L * 3 * 8); Ly.Dinv = take(L * 9 * 8); Ly.db = take(L * 3 * 8);
+    Ly.blkB = take((size_t)E * 18 * 8); Ly.blkBD = take((size_t)E * 18 * 8);
+    Ly.Hps = take(K * 27 * 8); Ly.S = take(n * n * 8); Ly.bs = take(n * 8); Ly.x = take(Xn * 8);
+    Ly.Ld = take(n * n * 8);
+    Ly.e_lm = take((size_t)E * 4); Ly.e_kf = take((size_t)E * 4); Ly.e_type = take((size_t)E * 4);
+    Ly.e_level = take((size_t)E * 4); Ly.e_src = take((size_t)E * 4); Ly.e_blk = take((size_t)E * 4);
+    Ly.lm_boff = take(L * 4); Ly.lm_nb = take(L * 4); Ly.lm_sorted = take(L * 4); Ly.lm_hidx = take(L * 4);
+    Ly.hidx_lm = take(L * 4); Ly.lmh_blk = take((L + 1) * 4); Ly.pe_off = take((K + 1) * 4);
+    Ly.pe_idx = take((size_t)E * 4);
+    Ly.Pinv = take(n * 4); Ly.Pm = take(n * 4); Ly.parent = take(n * 4); Ly.rs_off = take((n + 1) * 4);
+    Ly.rs_idx = take((n * (n + 1) / 2 + 1) * 4);
+    Ly.amd_Ci = take((nC + 1) * 4); Ly.amd_W = take(10 * (n + 1) * 4);
+    Ly.lmh_mask = take(L * 8); Ly.lm_amask = take(L * 8); Ly.Lbits = take(n * 6 * 8); Ly.Abits = take(n * 6 * 8);
+    Ly.bytes = o;
+    return Ly;
+}
+struct LbgBatch {
+    int n;
+    const spslam_lba_problem* probs;
+    const long long* scratch_off;
+    uint8_t* scratch;
+    const spslam_lba_keyframe* kfs;
+    const spslam_lba_point* pts;
+    const spslam_lba_point_obs* pobs;
+    const spslam_lba_plane* pls;
+    const spslam_lba_plane_obs* plobs;
+    float *kf_out, *pt_out, *pl_out;
+    uint8_t *pobs_out, *plobs_out;
+    spslam_lba_result* res;
+    const int32_t* stop;  // per problem pbStopFlag (device-visible; NULL = no flag)
+    int stop_after;       // test hook: the flag counts as raised once a problem has run this many trials (-1 off)
+};
+// One launch: the whole optimize(5) / relabel / optimize(10) schedule of every problem, no host round trip.
+hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer);
+
 // Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase
 // kernels step by step on `s` and polls the device every few steps until
 // every problem is DONE (so it returns after the work completed).

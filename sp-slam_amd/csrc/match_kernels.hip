@@ -728,17 +728,16 @@ hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, co
                               int max_points, const MatchCurrent& cur, const MatchGeom& g, const LocalConsts& P,
                               const uint8_t* taken_in, LocalWindow* win, int32_t* match, int* nmatches,
                               uint8_t* in_view, hipStream_t s, KernelTimer* timer) {
-    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
+    // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
+    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
+    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || lds > 160 * 1024) return hipErrorInvalidValue;
+    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::local_assign_kernel,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (lds_attr != hipSuccess) return lds_attr;
     if (timer) timer->begin(kKindLocalMatch, s);
     if (max_points > 0)
         hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kLPtsPerBlock - 1) / match::kLPtsPerBlock),
                            dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, win, in_view);
-    // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
-    const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
-    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::local_assign_kernel,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    (void)lds_attr;
-    if (lds > 160 * 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), lds, s,
                        frames, points, max_points, cur, g, P, taken_in, win, match, nmatches);
     if (timer) timer->end(kKindLocalMatch, s);
@@ -749,14 +748,13 @@ hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const sps
                         int max_points, const MatchCurrent& cur, const MatchGeom& g, const spslam_match_params& P,
                         MatchWindow* win, int2* pushes, int32_t* match, int* nmatches, hipStream_t s,
                         KernelTimer* timer) {
-    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || cur.cap > (1 << 20)) return hipErrorInvalidValue;
-    if (timer) timer->begin(kKindMatch, s);
-    // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
+    // taken bits + the claim table in dynamic LDS (opted in up to 150 KB: caps up to ~36K keypoints)
     const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
+    if (n_frames < 1 || max_points < 0 || cur.cap < 1 || lds > 150 * 1024) return hipErrorInvalidValue;
     static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::match_assign_kernel,
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    (void)lds_attr;
-    if (lds > 150 * 1024) return hipErrorInvalidValue;
+    if (lds_attr != hipSuccess) return lds_attr;
+    if (timer) timer->begin(kKindMatch, s);
     const int passes = P.retry_below > 0 ? 2 : 1;
     for (int pass = 0; pass < passes; pass++) {
         if (max_points > 0)

@@ -197,7 +197,8 @@ static_assert(kStrideA >= kRed, "a ring row holds the 28 terms (lanes past them 
 constexpr int kRingPad = SPSLAM_POSE_RING_PAD;
 // A smaller footprint (so ORB's level/fast kernels co-reside beside a pose workgroup) did not pay: pipelined C2
 // step 6.66 ms (29/24, 146 KB) vs 6.68 (29/0, 143.5 KB) vs 6.69 (28/0, 139.5 KB), 3 rounds each (profiles/r03/ab_lds_*)
-constexpr int kSpinCap = 1 << 20;  // bound of every wait (s_sleep 1 each: ~30 ms); never reached in a correct run
+// every wait gives up after PoseConsts::spin_cap polls (default 2^20, s_sleep 1 each: ~30 ms; never reached in a
+// correct run)
 
 template <int kSpec>
 struct RingB {
@@ -223,7 +224,8 @@ struct Shared {
     P4 pw[kPlaneChunk], pm[kPlaneChunk];  // plane edges' world / measured planes, normalized (nl <= kPlaneChunk)
     int done[kComputeWaves];          // rounds each compute wave has staged in the current pass
     int consumed;                     // rows the chain wave has added in the current pass
-    int stall;                        // a wait hit kSpinCap (reported through lm_iterations)
+    int stall;                        // a wait hit spin_cap (reported through lm_iterations)
+    int spin_cap;                     // PoseConsts::spin_cap (kSpinCap unless a test lowers it)
 };
 
 // Workgroup sum of NV doubles per thread; every thread returns the same totals.  Fixed order: xor butterfly over
@@ -382,7 +384,7 @@ __device__ __forceinline__ double chain_pass(Sh& S, const Schedule& G, const dou
 #endif
         int a = available(S, G);
         for (int spin = 0; a <= c; spin++) {
-            if (spin >= kSpinCap) { S.stall = 1; a = G.ne; break; }
+            if (spin >= S.spin_cap) { S.stall = 1; a = G.ne; break; }
             __builtin_amdgcn_s_sleep(1);
             a = available(S, G);
         }
@@ -406,7 +408,7 @@ template <class Sh>
 __device__ __forceinline__ void ring_wait(Sh& S, int need) {
     if (need <= 0) return;
     for (int spin = 0; lds_acquire(&S.consumed) < need; spin++) {
-        if (spin >= kSpinCap) { S.stall = 1; return; }
+        if (spin >= S.spin_cap) { S.stall = 1; return; }
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -514,7 +516,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         add[t >> 1] = (t & 1) ? -1e-9 : 1e-9;
         S.Eadd[t] = se3_exp(add);
     }
-    if (t == 0) S.stall = 0;
+    if (t == 0) { S.stall = 0; S.spin_cap = K.spin_cap; }
     SE3 T0;  // Converter::toSE3Quat: Quaterniond(R) of the float pose, normalized (every thread)
     {
         M3 R;
@@ -959,14 +961,22 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         if (round == 2) robust = false;
         if (ne < 10) break;
     }
-    if (t == 0) {
+    if (t == 0 && S.stall) {
+        // a bounded wait gave up (never observed): the sums are not valid, so the problem reports failure -- the
+        // input pose, no inliers, lm_iterations = -1 -- and callers treat it as a lost frame
+        for (int i = 0; i < 16; i++) res->Tcw[i] = Tin[i];
+        res->n_inliers = 0;
+        res->lm_iterations = -1;
+        res->trial_passes = total_passes;
+        res->trials = total_trials;
+    } else if (t == 0) {
         const M3 R = q_to_rot(T.r);
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) res->Tcw[4 * i + j] = (float)R.a[3 * i + j];
         res->Tcw[3] = (float)T.t.x; res->Tcw[7] = (float)T.t.y; res->Tcw[11] = (float)T.t.z;
         res->Tcw[12] = 0.f; res->Tcw[13] = 0.f; res->Tcw[14] = 0.f; res->Tcw[15] = 1.f;
         res->n_inliers = ne - nBad;
-        res->lm_iterations = S.stall ? -1 : total_its;  // a bounded wait gave up: the result is not valid
+        res->lm_iterations = total_its;
         res->trial_passes = total_passes;
         res->trials = total_trials;
     }
@@ -1014,6 +1024,7 @@ PoseConsts make_pose_consts(const spslam_plane_config& c) {
     K.vp_chi = c.vp_chi;
     K.delta_plane = (double)(float)sqrt(c.chi);
     K.delta_vp = (double)(float)sqrt(c.vp_chi);
+    K.spin_cap = 1 << 20;
     return K;
 }
 

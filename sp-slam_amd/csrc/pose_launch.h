@@ -12,6 +12,7 @@ struct PoseConsts {
     double angle_info, dis_info, par_info, ver_info;
     double plane_chi, vp_chi;
     double delta_plane, delta_vp;           // (float)sqrt(Chi), (float)sqrt(VPChi)
+    int spin_cap;                           // bound of the kernel's internal waits (spslam_debug_pose_spin_cap)
 };
 
 PoseConsts make_pose_consts(const spslam_plane_config& c);

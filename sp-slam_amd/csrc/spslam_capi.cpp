@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -14,6 +15,7 @@
 #include <sstream>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/spslam_gpu.h"
@@ -131,6 +133,8 @@ struct spslam_ctx {
     int32_t* h_lba_stop = nullptr;    // host-mapped coherent pbStopFlag mirror of spslam_lba_optimize
     int32_t* d_lba_stop = nullptr;    // its device alias (hipHostGetDevicePointer)
     int lba_stop_after = -1;          // spslam_lba_debug_stop_after
+    int lba_order = SPSLAM_LBA_G2O_ORDER;  // spslam_lba_set_order
+    int pose_spin_cap = 0;            // spslam_debug_pose_spin_cap (0 = the kernel's default)
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
     size_t lba_stage_bytes = 0;
@@ -457,7 +461,8 @@ int spslam_pose_optimize_batch_device(spslam_ctx* c, int n, const spslam_pose_pr
     if (n == 0) return SPSLAM_OK;
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
-    const PoseConsts K = make_pose_consts(*cfg);
+    PoseConsts K = make_pose_consts(*cfg);
+    if (c->pose_spin_cap > 0) K.spin_cap = c->pose_spin_cap;
     if (c->timer) c->timer->begin(kKindPose, s);
     HIP_CHECK(c, pose_launch(n, d_problems, d_points, d_planes, K, d_init_from, d_results, d_point_outlier,
                              d_plane_outlier, s));
@@ -785,6 +790,12 @@ int spslam_debug_plane_not_seen(spslam_ctx* c, const float* planes, int n_planes
     return SPSLAM_OK;
 }
 
+int spslam_debug_pose_spin_cap(spslam_ctx* c, int cap) {
+    if (!c || cap < 0) return SPSLAM_ERR_ARG;
+    c->pose_spin_cap = cap;
+    return SPSLAM_OK;
+}
+
 int spslam_debug_libm64(spslam_ctx* c, int kind, const double* a, const double* b, int n, double* out) {
     if (!c || n < 0 || kind < 0 || kind > 3 || (n && (!a || !out || (kind == 2 && !b)))) return SPSLAM_ERR_ARG;
     if (!n) return SPSLAM_OK;
@@ -1003,7 +1014,71 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     if (!c) return SPSLAM_ERR_ARG;
     if (n < 1 || !problems || !d_problems || !d_kfs || !cfg || !d_kf_out || !d_results)
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_lba_optimize_batch_device");
+    LbaConsts C{};
+    C.angle_info = 3282.8 / (cfg->angle_info * cfg->angle_info);
+    C.dis_info = cfg->distance_info * cfg->distance_info;
+    C.par_info = 3282.8 / (cfg->parallel_info * cfg->parallel_info);
+    C.ver_info = 3282.8 / (cfg->vertical_info * cfg->vertical_info);
+    C.plane_chi = cfg->chi;
+    C.vp_chi = cfg->vp_chi;
+    C.delta_mono = (float)std::sqrt(5.991);     // const float thHuberMono = sqrt(5.991)
+    C.delta_stereo = (float)std::sqrt(7.815);
+    C.delta_plane = (float)std::sqrt(cfg->chi);  // const float deltaPlane = sqrt(planeChi)
+    C.delta_vp = (float)std::sqrt(cfg->vp_chi);
     std::vector<long long> off(n);
+    if (c->lba_order == SPSLAM_LBA_G2O_ORDER) {
+        size_t total = 0;
+        for (int i = 0; i < n; i++) {
+            const spslam_lba_problem& p = problems[i];
+            if (p.n_kf < 0 || p.n_points < 0 || p.n_planes < 0 || p.n_point_obs < 0 || p.n_plane_obs < 0)
+                return fail(c, SPSLAM_ERR_ARG, "negative count in LBA problem%s", "");
+            if ((p.n_points && (!d_points || !d_point_obs || !d_pt_out || !d_point_obs_outlier)) ||
+                (p.n_planes && (!d_planes || !d_plane_obs || !d_pl_out || !d_plane_obs_outlier)))
+                return fail(c, SPSLAM_ERR_ARG, "missing LBA buffers%s", "");
+            off[i] = (long long)total;
+            total += lbg_layout(std::min(p.n_kf, kLbaMaxKeyframes), p.n_points, p.n_planes,
+                                p.n_point_obs + p.n_plane_obs).bytes;
+        }
+        HIP_CHECK(c, hipSetDevice(c->device));
+        hipStream_t s = (hipStream_t)hip_stream;
+        if (total > c->lba_scratch_bytes) {
+            HIP_CHECK(c, hipStreamSynchronize(s));
+            if (c->d_lba_scratch) (void)hipFree(c->d_lba_scratch);
+            c->d_lba_scratch = nullptr;
+            c->lba_scratch_bytes = 0;
+            HIP_CHECK(c, hipMalloc(&c->d_lba_scratch, total));
+            c->lba_scratch_bytes = total;
+        }
+        if (n > c->lba_off_cap) {
+            HIP_CHECK(c, hipStreamSynchronize(s));
+            if (c->d_lba_off) (void)hipFree(c->d_lba_off);
+            c->d_lba_off = nullptr;
+            HIP_CHECK(c, hipMalloc(&c->d_lba_off, (size_t)n * sizeof(long long)));
+            c->lba_off_cap = n;
+        }
+        HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
+        LbgBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
+                   d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
+                   c->lba_stop_after};
+        HIP_CHECK(c, lba_run_g2o(B, C, s, c->timer));
+        if (stop_src) {  // host-buffer entry: mirror the caller's bool into the device-visible flag while it runs
+            hipEvent_t ev;
+            HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIP_CHECK(c, hipEventRecord(ev, s));
+            for (;;) {
+                if (*stop_src) *stop_mirror = 1;
+                const hipError_t q = hipEventQuery(ev);
+                if (q == hipSuccess) break;
+                if (q != hipErrorNotReady) {
+                    (void)hipEventDestroy(ev);
+                    HIP_CHECK(c, q);
+                }
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+            HIP_CHECK(c, hipEventDestroy(ev));
+        }
+        return SPSLAM_OK;
+    }
     // work tables: edge chunks, landmark chunks, keyframe tasks, pose-pair (+ bs) tasks per problem
     std::vector<int2> ec, lc, kt, pt, qt, sg, pm;
     int max_kf = 1;
@@ -1072,17 +1147,6 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     }
     HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
     HIP_CHECK(c, hipMemcpyAsync(c->d_lba_work, work.data(), work.size() * sizeof(int2), hipMemcpyHostToDevice, s));
-    LbaConsts C{};
-    C.angle_info = 3282.8 / (cfg->angle_info * cfg->angle_info);
-    C.dis_info = cfg->distance_info * cfg->distance_info;
-    C.par_info = 3282.8 / (cfg->parallel_info * cfg->parallel_info);
-    C.ver_info = 3282.8 / (cfg->vertical_info * cfg->vertical_info);
-    C.plane_chi = cfg->chi;
-    C.vp_chi = cfg->vp_chi;
-    C.delta_mono = (float)std::sqrt(5.991);     // const float thHuberMono = sqrt(5.991)
-    C.delta_stereo = (float)std::sqrt(7.815);
-    C.delta_plane = (float)std::sqrt(cfg->chi);  // const float deltaPlane = sqrt(planeChi)
-    C.delta_vp = (float)std::sqrt(cfg->vp_chi);
     const int2* w0 = c->d_lba_work;
     LbaWork W{w0, (int)ec.size(), w0 + ec.size(), (int)lc.size(), w0 + ec.size() + lc.size(), (int)kt.size(),
               w0 + ec.size() + lc.size() + kt.size(), (int)pt.size(),
@@ -1097,6 +1161,12 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     return SPSLAM_OK;
 }
 }  // namespace
+
+int spslam_lba_set_order(spslam_ctx* c, int order) {
+    if (!c || (order != SPSLAM_LBA_G2O_ORDER && order != SPSLAM_LBA_FAST_ORDER)) return SPSLAM_ERR_ARG;
+    c->lba_order = order;
+    return SPSLAM_OK;
+}
 
 int spslam_lba_debug_stop_after(spslam_ctx* c, int trials) {
     if (!c || trials < -1) return SPSLAM_ERR_ARG;

@@ -63,11 +63,12 @@ class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
-                 rotate_inputs=False):
+                 rotate_inputs=False, lba_order=0):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
         self.device = device
+        self.lba_order = lba_order  # spslam_lba.G2O_ORDER (default) / FAST_ORDER
         s = width / 640.0
         self.K = K
         self.fx, self.fy, self.cx, self.cy = K["fx"] * s, K["fy"] * s, K["cx"] * s, K["cy"] * s
@@ -436,6 +437,7 @@ class HotPath:
         pc = self.plane_cfg
         self.lba = L.LocalBA(self.lba_ex, cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info,
                                                pc.chi, pc.vp_chi))
+        self.lba.set_order(self.lba_order)
         self.lba_stream = torch.cuda.Stream()
         self.ev_lba = torch.cuda.Event()
         import concurrent.futures as cf

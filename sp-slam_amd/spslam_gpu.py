@@ -200,7 +200,14 @@ def _bind_pose(lib):
                                                       vp, vp, vp, vp]
 
 
-EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device", "spslam_debug_libm64"]
+EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device", "spslam_debug_libm64",
+             "spslam_debug_pose_spin_cap"]
+
+
+def debug_pose_spin_cap(ex: "OrbExtractor", cap: int):
+    """Test hook: bound of PoseOptimization's internal waits (0 = default); a tiny cap forces the give-up path."""
+    ex.lib.spslam_debug_pose_spin_cap.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    ex._check(ex.lib.spslam_debug_pose_spin_cap(ex.ctx, int(cap)))
 
 
 def debug_libm64(ex: "OrbExtractor", kind: int, a, b=None):

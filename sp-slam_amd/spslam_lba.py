@@ -27,7 +27,9 @@ assert LBA_POINT_OBS_DTYPE.itemsize == 20 and LBA_PLANE_DTYPE.itemsize == 32
 assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 and LBA_RESULT_DTYPE.itemsize == 64
 
 
-spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device", "spslam_lba_debug_stop_after"]
+spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device", "spslam_lba_debug_stop_after",
+                        "spslam_lba_set_order"]
+G2O_ORDER, FAST_ORDER = 0, 1  # SPSLAM_LBA_G2O_ORDER (default, bit-exact to the oracle) / SPSLAM_LBA_FAST_ORDER
 
 PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # ICL.yaml Plane.* keys (Chi 1000, VPChi 200)
 
@@ -37,6 +39,7 @@ def _bind(lib):
     lib.spslam_lba_optimize.argtypes = [vp] * 15
     lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 16
     lib.spslam_lba_debug_stop_after.argtypes = [vp, ctypes.c_int]
+    lib.spslam_lba_set_order.argtypes = [vp, ctypes.c_int]
 
 
 def _addr(flag):
@@ -72,6 +75,10 @@ class LocalBA:
             pl_out.ctypes.data, po.ctypes.data, plo.ctypes.data, res.ctypes.data, _addr(stop_flag)))
         return dict(Tcw=kf_out[:len(kfs)], points=pt_out[:len(points)], planes=pl_out[:len(planes)],
                     point_outlier=po[:len(point_obs)], plane_outlier=plo[:len(plane_obs)], result=res)
+
+    def set_order(self, order: int):
+        """G2O_ORDER (default): g2o's summation order, bit-exact to the oracle; FAST_ORDER: the phase kernels."""
+        self.ex._check(self.ex.lib.spslam_lba_set_order(self.ex.ctx, int(order)))
 
     def debug_stop_after(self, trials: int):
         """Test hook: the following calls see pbStopFlag raised after `trials` LM trials (-1 = off)."""

@@ -132,6 +132,27 @@ def test_fewer_than_three_points_returns_zero(gpu, problems):
     assert np.array_equal(r["Tcw"], prob["Tcw"])  # SetPose is not called (:653-654)
 
 
+def test_wait_give_up_reports_failure(gpu, problems):
+    """A bounded internal wait that gives up (forced with a one-poll cap) must not yield a valid-looking pose:
+    the problem reports lm_iterations = -1, no inliers and the input pose (callers treat it as a lost frame)."""
+    import spslam_gpu
+    prob, pts, pls, _ = problems[1]
+    try:
+        spslam_gpu.debug_pose_spin_cap(gpu, 1)
+        r, po, plo = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
+    finally:
+        spslam_gpu.debug_pose_spin_cap(gpu, 0)
+    if int(r["lm_iterations"]) != -1:  # every wait happened to be satisfied on its first poll: a valid result
+        import oracle_ctypes
+        ro, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
+        assert np.array_equal(r["Tcw"], ro["Tcw"])
+        return
+    assert int(r["n_inliers"]) == 0
+    assert np.array_equal(r["Tcw"], prob["Tcw"])
+    r2, _, _ = spslam_gpu.pose_optimize(gpu, prob, pts, pls)  # the default cap again: a normal result
+    assert int(r2["lm_iterations"]) > 0 and int(r2["n_inliers"]) > 0
+
+
 def test_few_edges_single_round(gpu, problems):
     """< 10 edges: the reference breaks after the first round (:1142-1143)."""
     import oracle_ctypes
