@@ -39,6 +39,8 @@ constexpr int kMaxK = kLbaMaxKeyframes;
 constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
 constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised with L in LDS
+constexpr int kSchurLm = 16;            // Schur phase: landmarks per staged chunk
+constexpr int kSchurBlk = 192;          //   and Hpl blocks per chunk (two staging buffers + one BDinv buffer)
 
 struct Sh {
     double red[kW][4];
@@ -48,37 +50,64 @@ struct Sh {
     int hidx[kMaxK];                    // keyframe -> free-pose Hessian index (-1: fixed or inactive)
     int hpose[kMaxK];                   // Hessian index -> keyframe
     int pdeg[kMaxK];                    // poses coupled with each pose (itself included)
-    int np, nl, nact, flag;
+    int np, nl, nact, nch, flag;
     // LM / schedule state (thread 0 writes between barriers)
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
     double lambda, ni, currentChi, iniChi, tempChi, scale;
+    long long ph[8], tlast, tB;  // diagnostics: wall_clock64 ticks per phase (result phase_us[1..7])
+    long long dg[8];             // SPSLAM_LBG_DIAG sub-phase ticks
 };
+// thread 0 charges the time since the previous mark to phase k (called right after a barrier)
+#define LBG_MARK(k)                                  \
+    if (threadIdx.x == 0) {                          \
+        const long long now_ = wall_clock64();       \
+        s.ph[k] += now_ - s.tlast;                   \
+        s.tlast = now_;                              \
+    }
 
+// Global-memory pointers typed with the global address space: G lives in LDS and the phase functions are not
+// inlined, so a generic pointer would make every access a FLAT instruction (which also counts against the LDS
+// wait counter, so LDS reads would wait for every outstanding global load).
+#define GL __attribute__((address_space(1)))
+typedef double GL gdouble;
+typedef int GL gint;
+typedef uint64_t GL guint64;
 struct G {
     int K, Np, Nq, L, E, Ep;
-    const spslam_lba_keyframe* kf;
-    const spslam_lba_point* pt;
-    const spslam_lba_plane* pl;
-    const spslam_lba_point_obs* pobs;
-    const spslam_lba_plane_obs* plobs;
-    double *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *echi, *sc, *terms, *Hll, *bl, *Dinv, *db, *blkB, *blkBD, *Hps,
+    const spslam_lba_keyframe GL* kf;
+    const spslam_lba_point GL* pt;
+    const spslam_lba_plane GL* pl;
+    const spslam_lba_point_obs GL* pobs;
+    const spslam_lba_plane_obs GL* plobs;
+    gdouble *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *echi, *sc, *terms, *Hll, *bl, *Dinv, *db, *blkB, *blkBD, *Hps,
         *S, *bs, *x, *Ld;
-    int *e_lm, *e_kf, *e_type, *e_level, *e_src, *e_blk, *lm_boff, *lm_nb, *lm_sorted, *lm_hidx, *hidx_lm, *lmh_blk,
-        *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W;
-    uint64_t *lmh_mask, *lm_amask, *Lbits, *Abits;
+    gint *e_lm, *e_kf, *e_type, *e_level, *e_src, *e_blk, *lm_boff, *lm_nb, *lm_sorted, *lm_hidx, *hidx_lm, *lmh_blk,
+        *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W, *sch, *sch_kb;
+    guint64 *lmh_mask, *lm_amask, *Lbits, *Abits;
 };
+
+// The workgroup's LDS objects at namespace scope: the phase functions are not inlined, and a pointer or reference
+// argument would reach them as a generic (flat) address -- every LDS access a FLAT instruction, which also waits on
+// the outstanding global loads.  Referenced by name, they compile to ds_* instructions.
+extern __shared__ __attribute__((aligned(16))) unsigned char lbg_dyn[];
+__shared__ Sh lbg_s;
+__shared__ G lbg_g;
+__shared__ LbaConsts lbg_c;
 
 __device__ G make_g(const LbgBatch& b, int p) {
     const spslam_lba_problem pb = b.probs[p];
     G g;
     g.K = pb.n_kf; g.Np = pb.n_points; g.Nq = pb.n_planes;
     g.Ep = pb.n_point_obs; g.E = pb.n_point_obs + pb.n_plane_obs; g.L = g.Np + g.Nq;
-    g.kf = b.kfs + pb.kf_offset; g.pt = b.pts + pb.point_offset; g.pl = b.pls + pb.plane_offset;
-    g.pobs = b.pobs; g.plobs = b.plobs;
+    g.kf = (const spslam_lba_keyframe GL*)(b.kfs + pb.kf_offset);
+    g.pt = (const spslam_lba_point GL*)(b.pts + pb.point_offset);
+    g.pl = (const spslam_lba_plane GL*)(b.pls + pb.plane_offset);
+    g.pobs = (const spslam_lba_point_obs GL*)b.pobs;
+    g.plobs = (const spslam_lba_plane_obs GL*)b.plobs;
     const LbgLayout Ly = lbg_layout(g.K, g.Np, g.Nq, g.E);
     uint8_t* base = b.scratch + b.scratch_off[p];
-    auto D = [&](size_t o) { return (double*)(base + o); };
-    auto I = [&](size_t o) { return (int*)(base + o); };
+    auto D = [&](size_t o) { return (double GL*)(base + o); };
+    auto I = [&](size_t o) { return (int GL*)(base + o); };
     g.pose = D(Ly.pose); g.pose_b = D(Ly.pose_b); g.X = D(Ly.X); g.X_b = D(Ly.X_b); g.P = D(Ly.P); g.P_b = D(Ly.P_b);
     g.err = D(Ly.err); g.echi = D(Ly.echi); g.sc = D(Ly.sc); g.terms = D(Ly.terms); g.Hll = D(Ly.Hll);
     g.bl = D(Ly.bl); g.Dinv = D(Ly.Dinv); g.db = D(Ly.db); g.blkB = D(Ly.blkB); g.blkBD = D(Ly.blkBD);
@@ -88,8 +117,9 @@ __device__ G make_g(const LbgBatch& b, int p) {
     g.lm_sorted = I(Ly.lm_sorted); g.lm_hidx = I(Ly.lm_hidx); g.hidx_lm = I(Ly.hidx_lm); g.lmh_blk = I(Ly.lmh_blk);
     g.pe_off = I(Ly.pe_off); g.pe_idx = I(Ly.pe_idx); g.Pinv = I(Ly.Pinv); g.Pm = I(Ly.Pm); g.parent = I(Ly.parent);
     g.rs_off = I(Ly.rs_off); g.rs_idx = I(Ly.rs_idx); g.amd_Ci = I(Ly.amd_Ci); g.amd_W = I(Ly.amd_W);
-    g.lmh_mask = (uint64_t*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t*)(base + Ly.lm_amask);
-    g.Lbits = (uint64_t*)(base + Ly.Lbits); g.Abits = (uint64_t*)(base + Ly.Abits);
+    g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb);
+    g.lmh_mask = (uint64_t GL*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t GL*)(base + Ly.lm_amask);
+    g.Lbits = (uint64_t GL*)(base + Ly.Lbits); g.Abits = (uint64_t GL*)(base + Ly.Abits);
     return g;
 }
 
@@ -160,11 +190,14 @@ __device__ __forceinline__ double pick(const double (&v)[kC], int i) {
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // ---------------------------------------------------------------- edge math (oracle/lba_oracle.cpp)
-__device__ __forceinline__ SE3 load_pose(const double* p) { return SE3{Q{p[0], p[1], p[2], p[3]}, V3{p[4], p[5], p[6]}}; }
-__device__ __forceinline__ void store_pose(double* p, const SE3& T) {
+template <class PD>
+__device__ __forceinline__ SE3 load_pose(const PD* p) { return SE3{Q{p[0], p[1], p[2], p[3]}, V3{p[4], p[5], p[6]}}; }
+template <class PD>
+__device__ __forceinline__ void store_pose(PD* p, const SE3& T) {
     p[0] = T.r.w; p[1] = T.r.x; p[2] = T.r.y; p[3] = T.r.z; p[4] = T.t.x; p[5] = T.t.y; p[6] = T.t.z;
 }
-__device__ __forceinline__ P4 plane_from_f(const float* c) {  // Converter::toPlane3D + Plane3D(v)
+template <class PF>
+__device__ __forceinline__ P4 plane_from_f(const PF* c) {  // Converter::toPlane3D + Plane3D(v)
     P4 p{{c[0], c[1], c[2], c[3]}};
     if (c[3] < 0.0f)
         for (int i = 0; i < 4; i++) p.c[i] = -p.c[i];
@@ -192,7 +225,8 @@ __device__ __forceinline__ void info_of(const G& g, const LbaConsts& C, int e, i
         info[2] = 0;
     }
 }
-__device__ __forceinline__ double chi2_of(const double* err, const double* info, int dim) {  // e . (Omega e)
+template <class PE>
+__device__ __forceinline__ double chi2_of(const PE* err, const double* info, int dim) {  // e . (Omega e)
     double s = 0;
     for (int i = 0; i < dim; i++) s += err[i] * (info[i] * err[i]);
     return s;
@@ -208,9 +242,9 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
     *rho0 = 2 * s * delta - dsqr;
     *rho1 = delta / s;
 }
-__device__ __forceinline__ void point_error(const G& g, int e, int t, const SE3& T, const double* X, double* err) {
-    const spslam_lba_point_obs& o = g.pobs[g.e_src[e]];
-    const spslam_lba_keyframe& k = g.kf[g.e_kf[e]];
+__device__ __forceinline__ void point_error(const G& g, int e, int t, const SE3& T, const gdouble* X, double* err) {
+    const auto& o = g.pobs[g.e_src[e]];
+    const auto& k = g.kf[g.e_kf[e]];
     const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
     if (t == 0) {
         err[0] = (double)o.u - (p.x / p.z * (double)k.fx + (double)k.cx);
@@ -229,18 +263,18 @@ __device__ bool depth_positive(const G& g, int e) {
     const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
     const int lm = g.e_lm[e];
     if (g.e_type[e] <= 1) {
-        const double* X = g.X + 3 * lm;
+        auto X = g.X + 3 * lm;
         return (q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t).z > 0.0;
     }
-    const double* pp = g.P + 4 * (lm - g.Np);
+    auto pp = g.P + 4 * (lm - g.Np);
     return -plane_transform(T, P4{{pp[0], pp[1], pp[2], pp[3]}}).c[3] > 0;
 }
 // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:103-234)
 __device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double (&A)[3][3], double (&B)[3][6]) {
     const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
-    const spslam_lba_keyframe& k = g.kf[g.e_kf[e]];
+    const auto& k = g.kf[g.e_kf[e]];
     const double fx = k.fx, fy = k.fy, bf = k.bf;
-    const double* X = g.X + 3 * g.e_lm[e];
+    auto X = g.X + 3 * g.e_lm[e];
     const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
     const double x = p.x, y = p.y, z = p.z, z_2 = z * z;
     const M3 R = q_to_rot(T.r);
@@ -287,65 +321,9 @@ __device__ __forceinline__ void inverse3(const double (&m)[3][3], double* r) {
 __device__ __forceinline__ constexpr int upper_idx(int r, int c) { return 6 * r - r * (r - 1) / 2 + (c - r); }  // r <= c < 6
 
 // One edge's quadratic-form terms (BaseBinaryEdge::constructQuadraticForm as Eigen evaluates it, Omega diagonal):
-//   [0, 9)   Hll += (A^T W) A                 [9, 12)  bl += A^T omega_r
-//   [12, 30) Hpl (6 x 3, pose-major) += (B^T W) A (robust) | B^T (A^T Omega)^T (non-robust)
-//   [30, 51) Hpp upper (r <= c) += (B^T W) B  [51, 57) bp += B^T omega_r
-// W = rho' Omega (robust) or Omega; omega_r = (-(Omega e)) rho' or -(Omega e).  Rows >= dim are zero.
-__device__ __forceinline__ void edge_terms(const LbaConsts& C, bool robust, int ty, const double* err, const double* info,
-                                           const double (&A)[3][3], const double (&B)[3][6], bool pfree, double* o) {
-    const int dim = edge_dim(ty);
-    double r0, wgt;
-    huber(chi2_of(err, info, dim), delta_of(C, ty), robust, &r0, &wgt);
-    double W[3], om[3];
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        W[r] = robust ? wgt * info[r] : info[r];
-        om[r] = -(info[r] * err[r]);
-        if (robust) om[r] *= wgt;
-    }
-    const bool d3 = dim == 3;  // (rows >= dim are not added: a dim-2 edge's sums have two terms)
-#pragma unroll
-    for (int i = 0; i < 3; i++) {
-        double s = A[0][i] * om[0] + A[1][i] * om[1];
-        if (d3) s += A[2][i] * om[2];
-        o[9 + i] = s;
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            double h = (A[0][i] * W[0]) * A[0][j] + (A[1][i] * W[1]) * A[1][j];
-            if (d3) h += (A[2][i] * W[2]) * A[2][j];
-            o[3 * i + j] = h;
-        }
-    }
-    if (!pfree) return;
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int j = 0; j < 3; j++) {
-            double h;
-            if (robust) {
-                h = (B[0][i] * W[0]) * A[0][j] + (B[1][i] * W[1]) * A[1][j];
-                if (d3) h += (B[2][i] * W[2]) * A[2][j];
-            } else {
-                h = B[0][i] * (A[0][j] * info[0]) + B[1][i] * (A[1][j] * info[1]);
-                if (d3) h += B[2][i] * (A[2][j] * info[2]);
-            }
-            o[12 + 3 * i + j] = h;
-        }
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int j = i; j < 6; j++) {
-            double h = (B[0][i] * W[0]) * B[0][j] + (B[1][i] * W[1]) * B[1][j];
-            if (d3) h += (B[2][i] * W[2]) * B[2][j];
-            o[30 + upper_idx(i, j)] = h;
-        }
-#pragma unroll
-    for (int i = 0; i < 6; i++) {
-        double s = B[0][i] * om[0] + B[1][i] * om[1];
-        if (d3) s += B[2][i] * om[2];
-        o[51 + i] = s;
-    }
-}
+//   Hll += (A^T W) A;  bl += A^T omega_r;  Hpl (6 x 3, pose-major) += (B^T W) A (robust) | B^T (A^T Omega)^T
+//   (non-robust);  Hpp upper (r <= c) += (B^T W) B;  bp += B^T omega_r
+// W = rho' Omega (robust) or Omega; omega_r = (-(Omega e)) rho' or -(Omega e) (terms_land / terms_pose below).
 
 // SparseOptimizer::terminate(): the caller's flag, read through to memory (another thread may raise it), latched
 __device__ __forceinline__ bool stop_requested(const LbgBatch& b, int p, Sh& s) {
@@ -355,10 +333,13 @@ __device__ __forceinline__ bool stop_requested(const LbgBatch& b, int p, Sh& s) 
 }
 
 // ---------------------------------------------------------------- setup (once)
-__device__ __noinline__ void setup(const G& g, Sh& s, int* dyn_i) {
+__device__ __noinline__ void setup() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    int* dyn_i = (int*)lbg_dyn;
     const int t = threadIdx.x;
     for (int k = t; k < g.K; k += kT) {  // Converter::toSE3Quat
-        const float* T = g.kf[k].Tcw;
+        const auto* T = g.kf[k].Tcw;
         M3 Rm;
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) Rm.a[3 * i + j] = T[4 * i + j];
@@ -391,11 +372,11 @@ __device__ __noinline__ void setup(const G& g, Sh& s, int* dyn_i) {
                 g.e_src[e] = src0 + o;
                 g.e_level[e] = 0;
                 if (l < g.Np) {
-                    const spslam_lba_point_obs& ob = g.pobs[src0 + o];
+                    const auto& ob = g.pobs[src0 + o];
                     g.e_kf[e] = ob.kf;
                     g.e_type[e] = ob.ur < 0 ? 0 : 1;
                 } else {
-                    const spslam_lba_plane_obs& ob = g.plobs[src0 + o];
+                    const auto& ob = g.plobs[src0 + o];
                     g.e_kf[e] = ob.kf;
                     g.e_type[e] = ob.kind == SPSLAM_PLANE_EDGE ? 2 : (ob.kind == SPSLAM_PARALLEL_EDGE ? 3 : 4);
                 }
@@ -663,11 +644,15 @@ __device__ __noinline__ void amd_order(int n, int* Cp, int* Ci, int t, int* W, i
 __device__ __forceinline__ bool coupled(const Sh& s, int q1, int q2) {  // pose blocks (q1, q2) in the Schur pattern
     return q1 <= q2 ? (s.pat[q1] >> q2) & 1ull : (s.pat[q2] >> q1) & 1ull;
 }
-__device__ __forceinline__ bool bit_of(const uint64_t* bits, int i) { return (bits[i >> 6] >> (i & 63)) & 1ull; }
+template <class PU>
+__device__ __forceinline__ bool bit_of(const PU* bits, int i) { return (bits[i >> 6] >> (i & 63)) & 1ull; }
 
 // ---------------------------------------------------------------- structure (per optimize() pass)
 // initializeOptimization(0) + buildStructure + LinearSolverEigen's symbolic analysis
-__device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
+__device__ __noinline__ void structure() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    unsigned char* dyn = lbg_dyn;
     const int t = threadIdx.x, lane = t & 63;
     if (t == 0) s.kfact = 0;
     __syncthreads();
@@ -689,7 +674,7 @@ __device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
         int np = 0;
         for (int k = 0; k < g.K; k++) s.hidx[k] = -1;
         for (int k = 0; k < g.K; k++) {
-            const spslam_lba_keyframe& kk = g.kf[k];
+            const auto& kk = g.kf[k];
             if (!((s.kfact >> k) & 1ull) || kk.fixed || kk.id == 0) continue;
             int j = np++;
             while (j > 0 && g.kf[s.hpose[j - 1]].id > kk.id) { s.hpose[j] = s.hpose[j - 1]; j--; }
@@ -742,6 +727,50 @@ __device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
         base += tot;
     }
     if (t == 0) g.lmh_blk[nl] = base;
+    __syncthreads();
+    // the Schur phase's landmark chunks: groups of kSchurLm landmarks, split greedily where a group's Hpl blocks
+    // exceed kSchurBlk (a landmark has at most 64 blocks); sch[c] = first landmark of chunk c, sch_kb its first block
+    {
+        int nc = 0;
+        const int ng = (nl + kSchurLm - 1) / kSchurLm;
+        for (int pass2 = 0; pass2 < 2; pass2++) {
+            int my = 0, base2 = 0;
+            for (int ch = 0; ch < ng; ch += kT) {
+                const int gi = ch + t;
+                int cntc = 0;
+                if (gi < ng) {
+                    const int h0 = gi * kSchurLm, h1 = min(nl, h0 + kSchurLm);
+                    int start = h0, k0 = g.lmh_blk[h0];
+                    cntc = 1;
+                    for (int h = h0 + 1; h < h1; h++) {
+                        const int kh = g.lmh_blk[h + 1];
+                        if (kh - k0 > kSchurBlk) { start = h; k0 = g.lmh_blk[h]; cntc++; }
+                    }
+                    (void)start;
+                }
+                int tot;
+                const int off = block_scan(cntc, &tot, s) + base2;
+                if (pass2 == 1 && gi < ng) {
+                    const int h0 = gi * kSchurLm, h1 = min(nl, h0 + kSchurLm);
+                    int k0 = g.lmh_blk[h0], o = off;
+                    g.sch[o] = h0;
+                    g.sch_kb[o++] = k0;
+                    for (int h = h0 + 1; h < h1; h++) {
+                        const int kh = g.lmh_blk[h + 1];
+                        if (kh - k0 > kSchurBlk) { k0 = g.lmh_blk[h]; g.sch[o] = h; g.sch_kb[o++] = k0; }
+                    }
+                }
+                base2 += tot;
+                my += 0;
+            }
+            nc = base2;
+        }
+        if (t == 0) {
+            g.sch[nc] = nl;
+            g.sch_kb[nc] = g.lmh_blk[nl];
+            s.nch = nc;
+        }
+    }
     if (t < np) s.pat[t] = 1ull << t;
     __syncthreads();
     for (int l = t; l < g.L; l += kT) {
@@ -803,8 +832,8 @@ __device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
         for (int q = 0; q < np; q++) cnz += 36 * s.pdeg[q];
         const int tcap = cnz + cnz / 5 + 2 * n;
         const bool in_lds = (size_t)(tcap + 10 * (n + 1)) * 4 <= (size_t)kDyn;
-        int* Ci = in_lds ? (int*)dyn : g.amd_Ci;
-        int* W = in_lds ? Ci + tcap : g.amd_W;
+        int* Ci = in_lds ? (int*)dyn : (int*)g.amd_Ci;
+        int* W = in_lds ? Ci + tcap : (int*)g.amd_W;
         int* perm = W + 8 * (n + 1);
         int* Cp = perm + (n + 1);
         if (t < n) {
@@ -881,7 +910,7 @@ __device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
         const int k = t, ok = g.Pinv[k];
         uint64_t vis[kNW] = {0, 0, 0, 0, 0, 0};
         vis[k >> 6] |= 1ull << (k & 63);
-        int* seg = g.rs_idx + off;
+        auto seg = g.rs_idx + off;
         int wpos = 0;
         for (int o2 = 0; o2 < n; o2++) {
             const int r = g.Pm[o2];
@@ -917,7 +946,10 @@ __device__ __noinline__ void structure(const G& g, Sh& s, unsigned char* dyn) {
 // ---------------------------------------------------------------- errors + robust chi2
 // computeActiveErrors: err of every active edge, its robust chi2 (activeRobustChi2's terms) in echi (+0.0 for
 // inactive edges: an exact no-op in the ordered sum)
-__device__ __noinline__ void errors(const G& g, const Sh& s, const LbaConsts& C) {
+__device__ __noinline__ void errors() {
+    const LbaConsts& C = lbg_c;
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const bool robust = s.robust;
     for (int e = t; e < g.Ep; e += kT) {
@@ -944,7 +976,7 @@ __device__ __noinline__ void errors(const G& g, const Sh& s, const LbaConsts& C)
             const int ee = act ? e : g.Ep + (q < npl ? q : 0);
             if (q < npl) {
                 const int ty = g.e_type[ee];
-                const double* pp = g.P + 4 * (g.e_lm[ee] - g.Np);
+                auto pp = g.P + 4 * (g.e_lm[ee] - g.Np);
                 r = plane_error_pair(ty - 2, load_pose(g.pose + 7 * g.e_kf[ee]), P4{{pp[0], pp[1], pp[2], pp[3]}},
                                      plane_from_f(g.plobs[g.e_src[ee]].meas), (t & 1) != 0);
             }
@@ -965,7 +997,8 @@ __device__ __noinline__ void errors(const G& g, const Sh& s, const LbaConsts& C)
 }
 
 // one lane: sum of v[0 .. n32) in index order (n32 a multiple of 32; two 16-load batches in flight)
-__device__ __forceinline__ double ordered_sum(const double* v, int n32) {
+template <class PD>
+__device__ __forceinline__ double ordered_sum(const PD* v, int n32) {
     double acc = 0.0;
     double A[16], B[16];
 #pragma unroll
@@ -985,141 +1018,296 @@ __device__ __forceinline__ double ordered_sum(const double* v, int n32) {
 }
 
 // ---------------------------------------------------------------- per iteration: quadratic forms and sums
-__device__ __noinline__ void build_terms(const G& g, const Sh& s, const LbaConsts& C) {
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const bool robust = s.robust;
-    for (int e = t; e < g.Ep; e += kT) {
-        if (g.e_level[e] != 0) continue;
-        const int ty = g.e_type[e];
-        double A[3][3], B[3][6], info[3], err[3], o[kLbaCon];
-        point_jacobians(g, e, ty, A, B);
-        info_of(g, C, e, ty, info);
-        for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
-        const bool pfree = s.hidx[g.e_kf[e]] >= 0;
-        edge_terms(C, robust, ty, err, info, A, B, pfree, o);
-        double* dst = g.terms + (size_t)kLbaCon * e;
+// BlockSolver::buildSystem in chunks of kCh consecutive edges: (A) every edge's quadratic-form terms into LDS rows
+// (point edges on thread pairs -- both evaluate the Jacobians, the even thread the landmark side, the odd one the
+// pose side; plane edges one wave each, numeric Jacobians on lane pairs); (B) the sums, in edge order: each
+// landmark's segment in the chunk by the thread of its first edge there (continuing the landmark's partial sums
+// when it started in an earlier chunk), each (free pose, term) chain by its own lane over the chunk's edges of that
+// pose (LDS bitmasks), the chains' accumulators carried in registers from chunk to chunk.
+constexpr int kCh = 256;                    // edges per chunk
+constexpr int kSL = 13, kSP = 27, kSB = 19;  // LDS row strides (doubles): Hll + bl (12), Hpp + bp (27), Hpl (18)
+constexpr int kPoseSlots = (27 * kMaxK + kT - 1) / kT;
+
+struct EdgeW {  // Omega, robust weights and omega_r of one edge
+    int dim;
+    double W[3], om[3], info[3];
+};
+__device__ __forceinline__ EdgeW edge_weights(const LbaConsts& C, bool robust, int ty, const double* err, const double* info) {
+    EdgeW w;
+    w.dim = edge_dim(ty);
+    double r0, wgt;
+    huber(chi2_of(err, info, w.dim), delta_of(C, ty), robust, &r0, &wgt);
 #pragma unroll
-        for (int j = 0; j < kLbaCon; j++)
-            if (j < 12 || pfree) dst[j] = o[j];
+    for (int r = 0; r < 3; r++) {
+        w.info[r] = info[r];
+        w.W[r] = robust ? wgt * info[r] : info[r];
+        w.om[r] = -(info[r] * err[r]);
+        if (robust) w.om[r] *= wgt;
     }
-    // plane / parallel / vertical edges: numeric Jacobians (base_binary_edge.hpp:130-205), one wave per edge;
-    // evaluation q < 6: plane perturbed by +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose
-    // exp(+-1e-9 e_d) * T, d = (q - 6) >> 1; evaluation q on the lane pair (2q, 2q + 1)
-    for (int pe = g.Ep + wv; pe < g.E; pe += kW) {
-        if (g.e_level[pe] != 0) continue;  // wave-uniform
-        const int ty = g.e_type[pe], dim = edge_dim(ty), lm = g.e_lm[pe];
-        const bool pfree = s.hidx[g.e_kf[pe]] >= 0;
-        const SE3 T0 = load_pose(g.pose + 7 * g.e_kf[pe]);
-        const double* pp = g.P + 4 * (lm - g.Np);
-        const P4 P0{{pp[0], pp[1], pp[2], pp[3]}};
-        const P4 meas = plane_from_f(g.plobs[g.e_src[pe]].meas);
-        const double delta = 1e-9, scalar = 1.0 / (2 * delta);
-        double ev[3] = {0, 0, 0};
-        const int q = lane >> 1;
-        if (q < 18 && (q < 6 || pfree)) {
-            const double sgn = (q & 1) ? -delta : delta;
-            SE3 T = T0;
-            P4 P = P0;
-            if (q < 6) {
-                double add[3] = {0, 0, 0};
-                add[q >> 1] = sgn;
-                p_oplus(P, add);
-            } else {
-                double add[6] = {0, 0, 0, 0, 0, 0};
-                add[(q - 6) >> 1] = sgn;
-                T = se3_mul(se3_exp(add), T0);
-            }
-            const E3 r = plane_error_pair(ty - 2, T, P, meas, (lane & 1) != 0);
-            ev[0] = r.e0; ev[1] = r.e1; ev[2] = r.e2;
+    return w;
+}
+// landmark side: Hll 9, bl 3 (L), Hpl 18 (Bk); see edge_terms
+__device__ __forceinline__ void terms_land(const EdgeW& w, bool robust, const double (&A)[3][3], const double (&B)[3][6],
+                                           bool pfree, double* L, double* Bk) {
+    const bool d3 = w.dim == 3;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double s = A[0][i] * w.om[0] + A[1][i] * w.om[1];
+        if (d3) s += A[2][i] * w.om[2];
+        L[9 + i] = s;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double h = (A[0][i] * w.W[0]) * A[0][j] + (A[1][i] * w.W[1]) * A[1][j];
+            if (d3) h += (A[2][i] * w.W[2]) * A[2][j];
+            L[3 * i + j] = h;
         }
-        double A[3][3], B[3][6];
+    }
+    if (!pfree) return;
 #pragma unroll
-        for (int d = 0; d < 3; d++)
+    for (int i = 0; i < 6; i++)
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const double ep = __shfl(ev[i], 2 * (2 * d)), em = __shfl(ev[i], 2 * (2 * d + 1));
-                A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
+        for (int j = 0; j < 3; j++) {
+            double h;
+            if (robust) {
+                h = (B[0][i] * w.W[0]) * A[0][j] + (B[1][i] * w.W[1]) * A[1][j];
+                if (d3) h += (B[2][i] * w.W[2]) * A[2][j];
+            } else {
+                h = B[0][i] * (A[0][j] * w.info[0]) + B[1][i] * (A[1][j] * w.info[1]);
+                if (d3) h += B[2][i] * (A[2][j] * w.info[2]);
             }
+            Bk[3 * i + j] = h;
+        }
+}
+// pose side: Hpp upper 21, bp 6
+__device__ __forceinline__ void terms_pose(const EdgeW& w, const double (&B)[3][6], double* P) {
+    const bool d3 = w.dim == 3;
 #pragma unroll
-        for (int d = 0; d < 6; d++)
+    for (int i = 0; i < 6; i++)
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
-                const double ep = __shfl(ev[i], 2 * (6 + 2 * d)), em = __shfl(ev[i], 2 * (7 + 2 * d));
-                B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
-            }
-        if (lane == 0) {
-            double info[3], err[3], o[kLbaCon];
-            info_of(g, C, pe, ty, info);
-            for (int i = 0; i < 3; i++) err[i] = g.err[3 * pe + i];
-            edge_terms(C, robust, ty, err, info, A, B, pfree, o);
-            double* dst = g.terms + (size_t)kLbaCon * pe;
+        for (int j = i; j < 6; j++) {
+            double h = (B[0][i] * w.W[0]) * B[0][j] + (B[1][i] * w.W[1]) * B[1][j];
+            if (d3) h += (B[2][i] * w.W[2]) * B[2][j];
+            P[upper_idx(i, j)] = h;
+        }
 #pragma unroll
-            for (int j = 0; j < kLbaCon; j++)
-                if (j < 12 || pfree) dst[j] = o[j];
+    for (int i = 0; i < 6; i++) {
+        double s = B[0][i] * w.om[0] + B[1][i] * w.om[1];
+        if (d3) s += B[2][i] * w.om[2];
+        P[21 + i] = s;
+    }
+}
+
+// plane / parallel / vertical edge pe: numeric Jacobians (base_binary_edge.hpp:130-205) on one wave -- evaluation
+// q < 6: plane perturbed by +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose exp(+-1e-9 e_d) * T,
+// d = (q - 6) >> 1; evaluation q on the lane pair (2q, 2q + 1) -- the terms into row `row` from lane 0
+__device__ __forceinline__ void plane_edge_rows(const G& g, const Sh& s, const LbaConsts& C, int pe, int row,
+                                                double* TL, double* TP, double* TB, uint64_t* pm) {
+    const int lane = threadIdx.x & 63;
+    const bool robust = s.robust;
+    const int ty = g.e_type[pe], dim = edge_dim(ty), lm = g.e_lm[pe];
+    const int ph = s.hidx[g.e_kf[pe]];
+    const bool pfree = ph >= 0;
+    const SE3 T0 = load_pose(g.pose + 7 * g.e_kf[pe]);
+    auto pp = g.P + 4 * (lm - g.Np);
+    const P4 P0{{pp[0], pp[1], pp[2], pp[3]}};
+    const P4 meas = plane_from_f(g.plobs[g.e_src[pe]].meas);
+    const double delta = 1e-9, scalar = 1.0 / (2 * delta);
+    double ev[3] = {0, 0, 0};
+    const int q = lane >> 1;
+    if (q < 18 && (q < 6 || pfree)) {
+        const double sgn = (q & 1) ? -delta : delta;
+        SE3 T = T0;
+        P4 P = P0;
+        if (q < 6) {
+            double add[3] = {0, 0, 0};
+            add[q >> 1] = sgn;
+            p_oplus(P, add);
+        } else {
+            double add[6] = {0, 0, 0, 0, 0, 0};
+            add[(q - 6) >> 1] = sgn;
+            T = se3_mul(se3_exp(add), T0);
+        }
+        const E3 r = plane_error_pair(ty - 2, T, P, meas, (lane & 1) != 0);
+        ev[0] = r.e0; ev[1] = r.e1; ev[2] = r.e2;
+    }
+    double A[3][3], B[3][6];
+#pragma unroll
+    for (int d = 0; d < 3; d++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const double ep = __shfl(ev[i], 2 * (2 * d)), em = __shfl(ev[i], 2 * (2 * d + 1));
+            A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
+        }
+#pragma unroll
+    for (int d = 0; d < 6; d++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            const double ep = __shfl(ev[i], 2 * (6 + 2 * d)), em = __shfl(ev[i], 2 * (7 + 2 * d));
+            B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
+        }
+    if (lane == 0) {
+        double info[3], err[3];
+        info_of(g, C, pe, ty, info);
+        for (int i = 0; i < 3; i++) err[i] = g.err[3 * pe + i];
+        const EdgeW w = edge_weights(C, robust, ty, err, info);
+        terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
+        if (pfree) {
+            terms_pose(w, B, TP + kSP * row);
+            atomicOr((unsigned long long*)&pm[ph * 4 + (row >> 6)], 1ull << (row & 63));
         }
     }
 }
 
-// Hll, bl and the Hpl blocks of every active landmark over its edges in insertion order (one thread per
-// landmark); Hpp, bp of every free pose over its edges in insertion order (one lane per (pose, term)).
-// Returns (in s.red[0][1]) computeLambdaInit's max |diagonal|.
-__device__ __noinline__ void build_sums(const G& g, Sh& s) {
-    const int t = threadIdx.x;
-    const int nl = s.nl, np = s.np;
+// Returns (in s.red[0][1]) computeLambdaInit's max |diagonal| over Hpp and Hll.
+__device__ __noinline__ void build_system() {
+    const LbaConsts& C = lbg_c;
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    unsigned char* dyn = lbg_dyn;
+    long long tb0 = wall_clock64(), tA = 0, tB = 0, tP = 0;  // diagnostics
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const bool robust = s.robust;
+    const int np = s.np;
+    double* TL = (double*)dyn;
+    double* TP = TL + kCh * kSL;
+    double* TB = TP + kCh * kSP;
+    uint64_t* pm = (uint64_t*)(TB + kCh * kSB);  // [np][4]: the chunk's edges of each free pose
+    int* RI = (int*)(pm + 4 * kMaxK);            // [kCh] per row: its Hpl block, -1 none, -2 inactive edge
+    double acc[kPoseSlots];
+    int task[kPoseSlots];
+#pragma unroll
+    for (int k = 0; k < kPoseSlots; k++) {
+        acc[k] = 0.0;
+        task[k] = t + k * kT < 27 * np ? t + k * kT : -1;
+    }
     double mx = 0.0;
-    for (int h = t; h < nl; h += kT) {
-        const int l = g.hidx_lm[h];
-        const int b0 = g.lmh_blk[h];
+    for (int c0 = 0; c0 < g.E; c0 += kCh) {
+        const int cnt = min(kCh, g.E - c0);
+        for (int i = t; i < 4 * np; i += kT) pm[i] = 0;
+        // this thread's landmark segment (row t starts one when it is the landmark's first edge or the chunk's
+        // first row): its records load here and are consumed after phase (A)
+        int own_l = -1, own_b0 = 0, own_e1 = 0, own_h = -1, own_kb = 0;
         double H[9], bv[3];
-        for (int j = 0; j < 9; j++) H[j] = 0.0;
-        for (int j = 0; j < 3; j++) bv[j] = 0.0;
         uint64_t touched = 0;
-        for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
-            if (g.e_level[e] != 0) continue;
-            const double* tm = g.terms + (size_t)kLbaCon * e;
-            for (int j = 0; j < 9; j++) H[j] += tm[j];
-            for (int j = 0; j < 3; j++) bv[j] += tm[9 + j];
-            const int bk = g.e_blk[e];
-            if (bk >= 0) {
-                double* dst = g.blkB + (size_t)18 * bk;
-                const uint64_t bit = 1ull << (bk - b0);
-                if (touched & bit)
-                    for (int j = 0; j < 18; j++) dst[j] += tm[12 + j];
-                else
-                    for (int j = 0; j < 18; j++) dst[j] = 0.0 + tm[12 + j];
-                touched |= bit;
+        if (t < cnt) {
+            const int e = c0 + t;
+            RI[t] = g.e_level[e] == 0 ? g.e_blk[e] : -2;
+            const int l = g.e_lm[e];
+            own_b0 = g.lm_boff[l];
+            own_e1 = own_b0 + g.lm_nb[l];
+            own_h = g.lm_hidx[l];
+            if ((e == own_b0 || t == 0) && own_h >= 0) {
+                own_l = l;
+                own_kb = g.lmh_blk[own_h];
+                const bool cont = e > own_b0;  // continuing a landmark of the previous chunk
+#pragma unroll
+                for (int j = 0; j < 9; j++) H[j] = cont ? g.Hll[9 * own_h + j] : 0.0;
+#pragma unroll
+                for (int j = 0; j < 3; j++) bv[j] = cont ? g.bl[3 * own_h + j] : 0.0;
+                touched = cont ? g.lm_amask[l] : 0ull;  // (lm_amask is free after the structure phase)
             }
         }
-        for (int j = 0; j < 9; j++) g.Hll[9 * h + j] = H[j];
-        for (int j = 0; j < 3; j++) g.bl[3 * h + j] = bv[j];
-        mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
-    }
-    for (int task = t; task < 27 * np; task += kT) {
-        const int hh = task / 27, j = task - 27 * hh;
-        const int i0 = g.pe_off[hh], i1 = g.pe_off[hh + 1];
-        double acc = 0.0;
-        int i = i0;
-        for (; i + 8 <= i1; i += 8) {
-            double v[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = g.terms[(size_t)kLbaCon * g.pe_idx[i + u] + 30 + j];
-#pragma unroll
-            for (int u = 0; u < 8; u++) acc += v[u];
+        __syncthreads();
+        // (A) point edges on thread pairs
+        {
+            const int row = t >> 1, e = c0 + row;
+            if (row < cnt && e < g.Ep && g.e_level[e] == 0) {
+                const int ty = g.e_type[e];
+                const int ph = s.hidx[g.e_kf[e]];
+                const bool pfree = ph >= 0;
+                double A[3][3], B[3][6], info[3], err[3];
+                point_jacobians(g, e, ty, A, B);
+                info_of(g, C, e, ty, info);
+                for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
+                const EdgeW w = edge_weights(C, robust, ty, err, info);
+                if ((t & 1) == 0) {
+                    terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
+                } else if (pfree) {
+                    terms_pose(w, B, TP + kSP * row);
+                    atomicOr((unsigned long long*)&pm[ph * 4 + (row >> 6)], 1ull << (row & 63));
+                }
+            }
         }
-        for (; i < i1; i++) acc += g.terms[(size_t)kLbaCon * g.pe_idx[i] + 30 + j];
-        g.Hps[27 * hh + j] = acc;
-        if (j == 0 || j == 6 || j == 11 || j == 15 || j == 18 || j == 20) mx = fmax(mx, fabs(acc));
+        // plane edges of the chunk, one wave each
+        for (int e = max(c0, g.Ep) + wv; e < c0 + cnt; e += kW)
+            if (g.e_level[e] == 0) plane_edge_rows(g, s, C, e, e - c0, TL, TP, TB, pm);  // wave-uniform
+        __syncthreads();
+        const long long tb1 = wall_clock64();
+        if (c0 + cnt > g.Ep) tP += tb1 - tb0; else tA += tb1 - tb0;
+        // (B) landmark segments: the thread of the segment's first edge sums it in edge order
+        if (own_l >= 0) {
+            const int e = c0 + t, e_end = min(own_e1, c0 + cnt);
+            for (int e2 = e; e2 < e_end; e2++) {
+                const int bk = RI[e2 - c0];
+                if (bk == -2) continue;
+                const double* r = TL + kSL * (e2 - c0);
+#pragma unroll
+                for (int j = 0; j < 9; j++) H[j] += r[j];
+#pragma unroll
+                for (int j = 0; j < 3; j++) bv[j] += r[9 + j];
+                if (bk >= 0) {
+                    const double* rb = TB + kSB * (e2 - c0);
+                    auto dst = g.blkB + (size_t)18 * bk;
+                    const uint64_t bit = 1ull << (bk - own_kb);
+                    if (touched & bit) {
+#pragma unroll
+                        for (int j = 0; j < 18; j++) dst[j] += rb[j];
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 18; j++) dst[j] = 0.0 + rb[j];
+                    }
+                    touched |= bit;
+                }
+            }
+            for (int j = 0; j < 9; j++) g.Hll[9 * own_h + j] = H[j];
+            for (int j = 0; j < 3; j++) g.bl[3 * own_h + j] = bv[j];
+            if (e_end == own_e1) mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
+            else g.lm_amask[own_l] = touched;
+        }
+        // (free pose, term) chains over the chunk's edges of the pose
+#pragma unroll
+        for (int k = 0; k < kPoseSlots; k++) {
+            if (task[k] < 0) continue;
+            const int hh = task[k] / 27, j = task[k] - 27 * hh;
+            for (int wd = 0; wd < 4; wd++) {
+                uint64_t bits = pm[hh * 4 + wd];
+                while (bits) {
+                    const int i = 64 * wd + __ffsll((unsigned long long)bits) - 1;
+                    bits &= bits - 1;
+                    acc[k] += TP[kSP * i + j];
+                }
+            }
+        }
+        __syncthreads();
+        tb0 = wall_clock64();
+        tB += tb0 - tb1;
     }
+    if (t == 0) { s.ph[0] += tA; s.ph[7] += tP; s.tB += tB; }
+#pragma unroll
+    for (int k = 0; k < kPoseSlots; k++) {
+        if (task[k] < 0) continue;
+        const int hh = task[k] / 27, j = task[k] - 27 * hh;
+        g.Hps[27 * hh + j] = acc[k];
+        if (j == 0 || j == 6 || j == 11 || j == 15 || j == 18 || j == 20) mx = fmax(mx, fabs(acc[k]));
+    }
+    (void)lane;
     mx = block_max(mx, s);
     if (t == 0) s.red[0][1] = mx;
 }
 
 // ---------------------------------------------------------------- per trial
 
-// setLambda + the Schur complement (block_solver.hpp:367-436): landmark inverses, BDinv, then the ordered chains
-__device__ __noinline__ void schur(const G& g, Sh& s) {
+// setLambda + the Schur complement (block_solver.hpp:367-436).  (1) every landmark's (Hll + lambda)^-1 and
+// Dinv bl; (2) the chains: one lane per (pattern block (i1, i2), row r) holds S(6 i1 + r, 6 i2 .. 6 i2 + 5) (the
+// diagonal block's lanes also Bb(6 i1 + r)) and subtracts the landmarks' contributions in landmark order.  The
+// landmarks are staged in LDS in chunks: their Hpl blocks (one contiguous range, coalesced), masks, Dinv and
+// Dinv bl, then every block's BDinv = Bi Dinv formed in LDS (one thread per block row), then the chains.
+__device__ __noinline__ void schur() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    unsigned char* dyn = lbg_dyn;
     const int t = threadIdx.x;
-    const int nl = s.nl, np = s.np, n = 6 * np;
+    const int nl = s.nl, np = s.np, n = 6 * np, nch = s.nch;
     const double lam = s.lambda;
     for (int h = t; h < nl; h += kT) {
         double D[3][3];
@@ -1128,60 +1316,149 @@ __device__ __noinline__ void schur(const G& g, Sh& s) {
         double Di[9];
         inverse3(D, Di);
         for (int j = 0; j < 9; j++) g.Dinv[9 * h + j] = Di[j];
-        const double* bv = g.bl + 3 * h;
+        auto bv = g.bl + 3 * h;
         for (int i = 0; i < 3; i++) g.db[3 * h + i] = (Di[3 * i] * bv[0] + Di[3 * i + 1] * bv[1]) + Di[3 * i + 2] * bv[2];
-        for (int bk = g.lmh_blk[h]; bk < g.lmh_blk[h + 1]; bk++) {
-            const double* Bi = g.blkB + (size_t)18 * bk;
-            double* BD = g.blkBD + (size_t)18 * bk;
-            for (int r = 0; r < 6; r++)
-                for (int q = 0; q < 3; q++)
-                    BD[3 * r + q] = (Bi[3 * r] * Di[q] + Bi[3 * r + 1] * Di[3 + q]) + Bi[3 * r + 2] * Di[6 + q];
-        }
     }
-    __syncthreads();
-    // tasks: (i1 <= i2 in the pattern, row r of the block); the diagonal block's tasks also chain Bb (the rhs)
+    // LDS: two staging buffers (blocks, Dinv, Dinv bl, masks, block offsets) and the BDinv of the current chunk
+    constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
+    double* BUF = (double*)dyn;                               // [2][kBufD]
+    uint64_t* SM = (uint64_t*)(BUF + 2 * kBufD);              // [2][kSchurLm]
+    int* SO = (int*)(SM + 2 * kSchurLm);                      // [2][kSchurLm + 1]
+    double* SD = (double*)(SO + 2 * (kSchurLm + 2));          // [kSchurBlk][18] BDinv
+    constexpr int kPer = (kBufD + kT - 1) / kT;               // staged doubles per thread
+    // this lane's chain: (i1, i2, r) over the rows of the pattern blocks, row-major over (i1, i2)
     int nb = 0;
     for (int q = 0; q < np; q++) nb += __popcll(s.pat[q]);
-    for (int task = t; task < 6 * nb; task += kT) {
-        const int blk = task / 6, r = task - 6 * blk;
-        int i1 = 0, rem = blk;
-        while (rem >= __popcll(s.pat[i1])) { rem -= __popcll(s.pat[i1]); i1++; }
-        uint64_t row = s.pat[i1];
-        for (int u = 0; u < rem; u++) row &= row - 1;
-        const int i2 = __ffsll((unsigned long long)row) - 1;
-        const bool diag = i1 == i2;
+    for (int round = 0; round * kT < 6 * nb; round++) {
+        int i1 = -1, i2 = 0, r = 0;
+        const int task = t + round * kT;
+        if (task < 6 * nb) {
+            int blk = task / 6, rem = blk;
+            r = task - 6 * blk;
+            i1 = 0;
+            while (rem >= __popcll(s.pat[i1])) { rem -= __popcll(s.pat[i1]); i1++; }
+            uint64_t row = s.pat[i1];
+            for (int u = 0; u < rem; u++) row &= row - 1;
+            i2 = __ffsll((unsigned long long)row) - 1;
+        }
+        const bool have = i1 >= 0;
+        const bool diag = have && i1 == i2;
         double acc[6];
+#pragma unroll
         for (int c = 0; c < 6; c++) {
             double base = 0.0;
             if (diag && c >= r) base = c == r ? g.Hps[27 * i1 + upper_idx(r, c)] + lam : g.Hps[27 * i1 + upper_idx(r, c)];
             acc[c] = 0.0 + base;
         }
         double cf = 0.0;
-        const uint64_t need = (1ull << i1) | (1ull << i2);
-        for (int h = 0; h < nl; h++) {
-            const uint64_t mk = g.lmh_mask[h];
-            if ((mk & need) != need) continue;
-            const int b0 = g.lmh_blk[h];
-            const double* BD = g.blkBD + (size_t)18 * (b0 + __popcll(mk & ((1ull << i1) - 1ull))) + 3 * r;
-            const double* Bj = g.blkB + (size_t)18 * (b0 + __popcll(mk & ((1ull << i2) - 1ull)));
-            const double d0 = BD[0], d1 = BD[1], d2 = BD[2];
-            for (int c = 0; c < 6; c++) acc[c] -= (d0 * Bj[3 * c] + d1 * Bj[3 * c + 1]) + d2 * Bj[3 * c + 2];
-            if (diag) {
-                const double* db = g.db + 3 * h;
-                cf += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
+        const uint64_t need = have ? (1ull << i1) | (1ull << i2) : ~0ull;
+        const uint64_t lo1 = have ? (1ull << i1) - 1ull : 0, lo2 = have ? (1ull << i2) - 1ull : 0;
+        // chunk c's records into registers (global loads in flight), later into staging buffer c & 1
+        double pv[kPer];
+        uint64_t pmk = 0;
+        int pof = 0;
+        auto prefetch = [&](int c) __attribute__((always_inline)) {
+            const int h0 = g.sch[c], h1 = g.sch[c + 1], kb0 = g.sch_kb[c], kb1 = g.sch_kb[c + 1];
+            const int nbk = kb1 - kb0, nh = h1 - h0;
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int i = t + q * kT;
+                double v = 0.0;
+                if (i < nbk * 18) v = g.blkB[(size_t)18 * kb0 + i];
+                else if (i >= kSchurBlk * 18 && i < kSchurBlk * 18 + nh * 9) v = g.Dinv[9 * h0 + i - kSchurBlk * 18];
+                else if (i >= kSchurBlk * 18 + kSchurLm * 9 && i < kSchurBlk * 18 + kSchurLm * 9 + nh * 3)
+                    v = g.db[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
+                pv[q] = v;
             }
+            if (t < nh) pmk = g.lmh_mask[h0 + t];
+            if (t <= nh) pof = g.lmh_blk[h0 + t] - kb0;
+        };
+        auto commit = [&](int c) __attribute__((always_inline)) {
+            double* B = BUF + (c & 1) * kBufD;
+            const int nh = g.sch[c + 1] - g.sch[c];
+#pragma unroll
+            for (int q = 0; q < kPer; q++)
+                if (t + q * kT < kBufD) B[t + q * kT] = pv[q];
+            if (t < nh) SM[(c & 1) * kSchurLm + t] = pmk;
+            if (t <= nh) SO[(c & 1) * (kSchurLm + 2) + t] = pof;
+        };
+        __syncthreads();  // the previous phase's LDS use is over
+        if (nch > 0) {
+            prefetch(0);
+            commit(0);
         }
-        for (int c = 0; c < 6; c++) g.S[(size_t)(6 * i1 + r) * n + 6 * i2 + c] = acc[c];
-        if (diag) g.bs[6 * i1 + r] = g.Hps[27 * i1 + 21 + r] - cf;
+        for (int c = 0; c < nch; c++) {
+            if (c + 1 < nch) prefetch(c + 1);  // lands while chunk c is processed
+#ifdef SPSLAM_LBG_DIAG
+            long long d0 = wall_clock64();
+#endif
+            __syncthreads();                   // chunk c is staged
+#ifdef SPSLAM_LBG_DIAG
+            long long d1 = wall_clock64();
+            if (t == 0) s.dg[0] += d1 - d0;
+#endif
+            const double* SB = BUF + (c & 1) * kBufD;
+            const double* SDi = SB + kSchurBlk * 18;
+            const double* Sdb = SDi + kSchurLm * 9;
+            const uint64_t* Sm = SM + (c & 1) * kSchurLm;
+            const int* So = SO + (c & 1) * (kSchurLm + 2);
+            const int nh = g.sch[c + 1] - g.sch[c];
+            const int nbk = So[nh];
+            for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q)
+                const int bk = i / 6, rr = i - 6 * bk;
+                int hl = 0;
+                while (So[hl + 1] <= bk) hl++;
+                const double* Bi = SB + 18 * bk + 3 * rr;
+                const double* Di = SDi + 9 * hl;
+                double* BD = SD + 18 * bk + 3 * rr;
+#pragma unroll
+                for (int q = 0; q < 3; q++) BD[q] = (Bi[0] * Di[q] + Bi[1] * Di[3 + q]) + Bi[2] * Di[6 + q];
+            }
+            __syncthreads();
+#ifdef SPSLAM_LBG_DIAG
+            long long d2 = wall_clock64();
+            if (t == 0) s.dg[1] += d2 - d1;
+#endif
+            if (have)
+                for (int hl = 0; hl < nh; hl++) {
+                    const uint64_t mk = Sm[hl];
+                    if ((mk & need) != need) continue;
+                    const int o = So[hl];
+                    const double* BD = SD + 18 * (o + __popcll(mk & lo1)) + 3 * r;
+                    const double* Bj = SB + 18 * (o + __popcll(mk & lo2));
+                    const double d0 = BD[0], d1 = BD[1], d2 = BD[2];
+#pragma unroll
+                    for (int cc = 0; cc < 6; cc++) acc[cc] -= (d0 * Bj[3 * cc] + d1 * Bj[3 * cc + 1]) + d2 * Bj[3 * cc + 2];
+                    if (diag) {
+                        const double* db = Sdb + 3 * hl;
+                        cf += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
+                    }
+                }
+            __syncthreads();  // SD and buffer c & 1 are free again
+#ifdef SPSLAM_LBG_DIAG
+            long long d3 = wall_clock64();
+            if (t == 0) s.dg[2] += d3 - d2;
+#endif
+            if (c + 1 < nch) commit(c + 1);
+#ifdef SPSLAM_LBG_DIAG
+            if (t == 0) s.dg[3] += wall_clock64() - d3;
+#endif
+        }
+        if (have) {
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1 + r) * n + 6 * i2 + cc] = acc[cc];
+            if (diag) g.bs[6 * i1 + r] = g.Hps[27 * i1 + 21 + r] - cf;
+        }
     }
 }
 
 // LinearSolverEigen::solve: SimplicialLDLT::factorize + solve on wave 0.  Row r of the permuted system lives in
 // lane r & 63, register r >> 6.  LD: L column-major (LD[i n + r] = L(r, i)), LB: L's column structures (bitsets),
 // RS / RO: the rows' pattern orders, PI: Pinv.
-template <int kC>
-__device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const uint64_t* LB, const int* RS, const int* RO,
-                             const int* PI) {
+template <int kC, class PD, class PU, class PI_>
+__device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO, const PI_* RS, const PI_* PI) {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
     const int lane = threadIdx.x & 63;
     const int n = 6 * s.np;
     double Dg[kC];
@@ -1205,14 +1482,35 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
         }
         double d = pick(y, k) * 1.0 + 0.0;
         const int t0 = RO[k], t1 = RO[k + 1];
-        for (int tt = t0; tt < t1; tt++) {
-            const int i = uni(RS[tt]);
-            const double yi = pick(y, i);
-            const uint64_t* cb = LB + (size_t)i * kNW;
+        // the row's pattern order 64 entries at a time in a register (lane q: entry q of the piece); the next
+        // step's column of L and structure words load while this step runs (two operand sets, no moves)
+        auto fetch = [&](int i, double (&v)[kC], uint64_t (&w)[kC]) __attribute__((always_inline)) {
 #pragma unroll
             for (int m = 0; m < kC; m++) {
                 const int r = 64 * m + lane;
-                if (r < k && ((cb[m] >> lane) & 1ull)) y[m] = y[m] - LD[(size_t)i * n + r] * yi;
+                v[m] = r < n ? LD[(size_t)i * n + r] : 0.0;
+                w[m] = LB[(size_t)i * kNW + m];
+            }
+        };
+        auto stepf = [&](int i, const double (&v)[kC], const uint64_t (&w)[kC]) __attribute__((always_inline)) {
+            const double yi = pick(y, i);
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                if (r < k && ((w[m] >> lane) & 1ull)) y[m] = y[m] - v[m] * yi;
+            }
+        };
+        for (int p0 = t0; p0 < t1; p0 += 64) {
+            const int ns = min(64, t1 - p0);
+            const int rsv = lane < ns ? RS[p0 + lane] : 0;
+            double vA[kC], vB[kC];
+            uint64_t wA[kC], wB[kC];
+            fetch(__builtin_amdgcn_readlane(rsv, 0), vA, wA);
+            for (int j = 0; j < ns; j += 2) {
+                if (j + 1 < ns) fetch(__builtin_amdgcn_readlane(rsv, j + 1), vB, wB);
+                stepf(__builtin_amdgcn_readlane(rsv, j), vA, wA);
+                if (j + 2 < ns) fetch(__builtin_amdgcn_readlane(rsv, j + 2), vA, wA);
+                if (j + 1 < ns) stepf(__builtin_amdgcn_readlane(rsv, j + 1), vB, wB);
             }
         }
         double pr[kC];
@@ -1226,7 +1524,11 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
                 pr[m] = l * y[m];
             }
         }
-        for (int tt = t0; tt < t1; tt++) d -= pick(pr, uni(RS[tt]));
+        for (int p0 = t0; p0 < t1; p0 += 64) {
+            const int ns = min(64, t1 - p0);
+            const int rsv = lane < ns ? RS[p0 + lane] : 0;
+            for (int j = 0; j < ns; j++) d -= pick(pr, __builtin_amdgcn_readlane(rsv, j));
+        }
 #pragma unroll
         for (int m = 0; m < kC; m++)
             if (64 * m + lane == k) Dg[m] = d;
@@ -1239,6 +1541,9 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (lane == 0) s.ok = ok;
+#ifdef SPSLAM_LBG_DIAG
+    if (lane == 0) s.dg[4] = wall_clock64();
+#endif
     if (!ok) return;
     // x = P b; L x = x; x = D^-1 x; L^T x = x; x = P^-1 x
     const bool haveL = RO[n] > 0;
@@ -1252,7 +1557,7 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
         for (int i = 0; i < n; i++) {
             const double tmp = pick(tv, i);
             if (tmp != 0.0) {
-                const uint64_t* cb = LB + (size_t)i * kNW;
+                const auto* cb = LB + (size_t)i * kNW;
 #pragma unroll
                 for (int m = 0; m < kC; m++) {
                     const int r = 64 * m + lane;
@@ -1265,7 +1570,7 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
         if (64 * m + lane < n) tv[m] = (1.0 / Dg[m]) * tv[m];
     if (haveL)
         for (int i = n - 1; i >= 0; i--) {
-            const uint64_t* cb = LB + (size_t)i * kNW;
+            const auto* cb = LB + (size_t)i * kNW;
             double pr[kC];
 #pragma unroll
             for (int m = 0; m < kC; m++) {
@@ -1293,8 +1598,25 @@ __device__ __noinline__ void factor_solve(const G& g, Sh& s, double* LD, const u
     }
 }
 
+template <int kC, bool kLds>
+__device__ __noinline__ void factor_solve() {
+    const int n = 6 * lbg_s.np;
+    if (kLds) {  // the layout of k_lba_g2o's copy in LDS
+        double* LD = (double*)lbg_dyn;
+        const uint64_t* LB = (const uint64_t*)(lbg_dyn + (size_t)n * n * 8);
+        const int* RO = (const int*)(LB + (size_t)n * kNW);
+        const int* RS = RO + (n + 1);
+        factor_body<kC>(LD, LB, RO, RS, RS + (n * (n + 1)) / 2 + 1);
+    } else {
+        const G& g = lbg_g;
+        factor_body<kC>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv);
+    }
+}
+
 // landmark increments (xl = Dinv (bl - Hpl^T xp)), push, update (block_solver.hpp:444-471, oplus)
-__device__ __noinline__ void update(const G& g, const Sh& s) {
+__device__ __noinline__ void update() {
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const int nl = s.nl, np = s.np, n = 6 * np;
     const bool ok = s.ok;
@@ -1310,19 +1632,19 @@ __device__ __noinline__ void update(const G& g, const Sh& s) {
             while (m) {
                 const int p = __ffsll((unsigned long long)m) - 1;
                 m &= m - 1;
-                const double* B = g.blkB + (size_t)18 * bk++;
+                auto B = g.blkB + (size_t)18 * bk++;
                 for (int i = 0; i < 3; i++) {
                     double sm = 0;
                     for (int r = 0; r < 6; r++) sm += B[3 * r + i] * (-g.x[6 * p + r]);
                     cl[i] += sm;
                 }
             }
-            const double* Di = g.Dinv + 9 * h;
+            auto Di = g.Dinv + 9 * h;
             for (int i = 0; i < 3; i++) xl[i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
             if (l < g.Np) {
                 for (int j = 0; j < 3; j++) g.X[3 * l + j] += xl[j];
             } else {
-                double* pp = g.P + 4 * (l - g.Np);
+                auto pp = g.P + 4 * (l - g.Np);
                 P4 P{{pp[0], pp[1], pp[2], pp[3]}};
                 p_oplus(P, xl);
                 for (int j = 0; j < 4; j++) pp[j] = P.c[j];
@@ -1340,7 +1662,9 @@ __device__ __noinline__ void update(const G& g, const Sh& s) {
     }
 }
 
-__device__ __noinline__ void restore(const G& g, const Sh& s) {  // pop()
+__device__ __noinline__ void restore() {  // pop()
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
     const int t = threadIdx.x;
     for (int h = t; h < s.nl; h += kT) {
         const int l = g.hidx_lm[h];
@@ -1352,7 +1676,9 @@ __device__ __noinline__ void restore(const G& g, const Sh& s) {  // pop()
 }
 
 // computeScale terms x_j (lambda x_j + b_j), poses then landmarks (Hessian order), zero-padded to 32
-__device__ __noinline__ void scale_terms(const G& g, const Sh& s) {
+__device__ __noinline__ void scale_terms() {
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const int n = 6 * s.np, tot = n + 3 * s.nl, pad = lbg_pad32(tot);
     const double lam = s.lambda;
@@ -1368,7 +1694,10 @@ __device__ __noinline__ void scale_terms(const G& g, const Sh& s) {
 }
 
 // ---------------------------------------------------------------- outputs
-__device__ __noinline__ void outputs(const LbgBatch& b, int p, const G& g, Sh& s, const LbaConsts& C) {
+__device__ __noinline__ void outputs(const LbgBatch& b, int p) {
+    const LbaConsts& C = lbg_c;
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
     const int t = threadIdx.x;
     const spslam_lba_problem pb = b.probs[p];
     if (s.stopped == 1) {  // returned before optimizing: the map is untouched, nothing is erased
@@ -1438,13 +1767,15 @@ __device__ __noinline__ void outputs(const LbgBatch& b, int p, const G& g, Sh& s
 
 // ---------------------------------------------------------------- the schedule
 __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
-    __shared__ Sh s;
-    __shared__ G gsh;  // the problem's pointers, read from LDS where used (not ~100 registers held throughout)
+    unsigned char* dyn = lbg_dyn;
+    Sh& s = lbg_s;
     const int p = blockIdx.x, t = threadIdx.x;
-    if (t == 0) gsh = make_g(b, p);
+    if (t == 0) {
+        lbg_g = make_g(b, p);
+        lbg_c = C;
+    }
     __syncthreads();
-    const G& g = gsh;
+    const G& g = lbg_g;
     const long long t0 = wall_clock64();
     if (g.K > kMaxK) {
         if (t == 0) {
@@ -1455,30 +1786,26 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     }
     if (t == 0) {
         s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1;
+        for (int i = 0; i < 8; i++) s.ph[i] = s.dg[i] = 0;
+        s.tB = 0;
+        s.tlast = t0;
         s.done = stop_requested(b, p, s) ? 1 : 0;  // if(*pbStopFlag) return; before initializeOptimization
         if (s.done) s.stopped = 1;
     }
     __syncthreads();
-    if (!s.done) setup(g, s, (int*)dyn);
+    if (!s.done) setup();
     if (t == 0 && g.E == 0) s.done = 1;  // no edges: nothing to optimise, the map goes back through the converters
     __syncthreads();
     for (int pass = 0; pass < 2 && !s.done; pass++) {
-        structure(g, s, dyn);
+        structure();
+        LBG_MARK(1);
         const int n = 6 * s.np;
         // the factorisation's operands in LDS for n <= kLdsN: L, its column structures, the rows' pattern orders, P
         const bool lds = n <= kLdsN;
-        double* LD = lds ? (double*)dyn : g.Ld;
-        uint64_t* LB = lds ? (uint64_t*)(dyn + (size_t)n * n * 8) : g.Lbits;
-        int* RO = lds ? (int*)(LB + (size_t)n * kNW) : g.rs_off;
-        int* RS = lds ? RO + (n + 1) : g.rs_idx;
-        int* PI = lds ? RS + (n * (n + 1)) / 2 + 1 : g.Pinv;
-        if (lds) {
-            for (int i = t; i < n * kNW; i += kT) LB[i] = g.Lbits[i];
-            for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
-            const int nz = g.rs_off[n];
-            for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
-            for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
-        }
+        uint64_t* LB = (uint64_t*)(dyn + (size_t)n * n * 8);  // (used when lds)
+        int* RO = (int*)(LB + (size_t)n * kNW);
+        int* RS = RO + (n + 1);
+        int* PI = RS + (n * (n + 1)) / 2 + 1;
         if (t == 0) {
             s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1;
         }
@@ -1494,16 +1821,18 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             __syncthreads();
             if (s.done) break;
             if (s.need_err) {
-                errors(g, s, C);
+                LBG_MARK(1);
+                errors();
                 __syncthreads();
+                LBG_MARK(2);
                 if (t == 0) s.currentChi = ordered_sum(g.echi, lbg_pad32(g.E));
                 __syncthreads();
+                LBG_MARK(3);
             }
             if (t == 0) s.iniChi = s.currentChi;
-            build_terms(g, s, C);
+            build_system();
             __syncthreads();
-            build_sums(g, s);
-            __syncthreads();
+            LBG_MARK(4);
             if (t == 0) {
                 if (it == 0) { s.lambda = 1e-5 * s.red[0][1]; s.ni = 2; s.nBad = 0; }
                 s.qmax = 0;
@@ -1512,25 +1841,46 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             double rho = 0.0;
             bool more = true;
             while (more) {
-                schur(g, s);
+                LBG_MARK(1);
+                schur();
                 __syncthreads();
+                LBG_MARK(5);
+                if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
+                    for (int i = t; i < n * kNW; i += kT) LB[i] = g.Lbits[i];
+                    for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
+                    const int nz = g.rs_off[n];
+                    for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
+                    for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
+                    __syncthreads();
+                }
+#ifdef SPSLAM_LBG_DIAG
+                const long long f0 = wall_clock64();
+#endif
                 if (t < 64) {
-                    if (n <= 64) factor_solve<1>(g, s, LD, LB, RS, RO, PI);
-                    else if (n <= 128) factor_solve<2>(g, s, LD, LB, RS, RO, PI);
-                    else if (n <= 192) factor_solve<3>(g, s, LD, LB, RS, RO, PI);
-                    else if (n <= 256) factor_solve<4>(g, s, LD, LB, RS, RO, PI);
-                    else factor_solve<6>(g, s, LD, LB, RS, RO, PI);
+                    if (n <= 64) factor_solve<1, true>();
+                    else if (n <= kLdsN) factor_solve<2, true>();
+                    else if (n <= 128) factor_solve<2, false>();
+                    else if (n <= 192) factor_solve<3, false>();
+                    else if (n <= 256) factor_solve<4, false>();
+                    else factor_solve<6, false>();
                 }
                 if (n == 0 && t == 0) s.ok = 1;
+#ifdef SPSLAM_LBG_DIAG
+                if (t == 0) s.dg[5] += s.dg[4] - f0;
+#endif
                 __syncthreads();
-                update(g, s);
+                LBG_MARK(6);
+                update();
                 __syncthreads();
-                errors(g, s, C);
-                scale_terms(g, s);
+                LBG_MARK(1);
+                errors();
+                scale_terms();
                 __syncthreads();
+                LBG_MARK(2);
                 if (t == 0) s.tempChi = ordered_sum(g.echi, lbg_pad32(g.E));
                 if (t == 64) s.scale = ordered_sum(g.sc, lbg_pad32(n + 3 * s.nl));
                 __syncthreads();
+                LBG_MARK(3);
                 if (t == 0) {
                     double tempChi = s.ok ? s.tempChi : DBL_MAX;
                     double r = s.currentChi - tempChi;
@@ -1557,7 +1907,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                 }
                 __syncthreads();
                 if (!s.accepted) {
-                    restore(g, s);
+                    restore();
                     __syncthreads();
                 }
                 rho = s.red[0][2];
@@ -1607,8 +1957,16 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         }
     }
     __syncthreads();
-    outputs(b, p, g, s, C);
-    if (t == 0) b.res[p].phase_us[0] = (float)((wall_clock64() - t0) * 0.01);
+    outputs(b, p);
+    if (t == 0) {  // setup / structure / update / decide, errors, ordered chains, terms, Schur, factor + solve, sums
+        b.res[p].phase_us[0] = (float)((wall_clock64() - t0) * 0.01);
+        for (int i = 1; i < 8; i++) b.res[p].phase_us[i] = (float)(s.ph[i] * 0.01);
+        b.res[p].pad = (int)(s.tB * 0.01);  // diagnostic: build phase (B) us; phase_us[7]: (A) of plane chunks
+#ifdef SPSLAM_LBG_DIAG  // Schur: staging wait, BDinv, chains, commit; factor-only
+        for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
+        b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
+#endif
+    }
 }
 
 }  // namespace lbag

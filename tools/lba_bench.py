@@ -1,6 +1,6 @@
 """Diagnostic: the C3 LocalMapping workload alone -- one batched LocalBundleAdjustment call over the step's
 local maps (51 maps of 12 keyframes / 1500 points at B = 256), wall time and LM step count.
-    python tools/lba_bench.py [--reps 5]"""
+    python tools/lba_bench.py [--reps 5] [--order g2o|fast]"""
 import argparse
 import pathlib
 import sys
@@ -14,12 +14,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--order", default="g2o", choices=("g2o", "fast"))
     a = ap.parse_args()
     import numpy as np
     import torch
     import pipeline
     import spslam_lba as L
-    hp = pipeline.HotPath(a.batch, **pipeline.CONFIGS["c3"])
+    hp = pipeline.HotPath(a.batch, lba_order=0 if a.order == "g2o" else 1, **pipeline.CONFIGS["c3"])
     for r in range(a.reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -27,8 +28,9 @@ def main():
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         res = hp.lba_out[5].cpu().numpy().view(L.LBA_RESULT_DTYPE)
-        print(f"rep {r}: {dt * 1e3:.2f} ms for {hp.n_lba} maps; iterations max {res['iterations'].max(0)} "
-              f"trials max {res['trials'].max()} device us max {res['phase_us'][:, 0].max():.0f}", flush=True)
+        print(f"rep {r} ({a.order}): {dt * 1e3:.2f} ms for {hp.n_lba} maps; iterations max {res['iterations'].max(0)} "
+              f"trials max {res['trials'].max()} device us max {res['phase_us'][:, 0].max():.0f}; phases (us, slowest "
+              f"map) {np.round(res['phase_us'][int(res['phase_us'][:, 0].argmax())], 0).tolist()} pad {res['pad'].max()}", flush=True)
     hp.close()
 
 
