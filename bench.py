@@ -384,12 +384,16 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
                "sequences": n_seq, "frames": n_frames,
                "cpu_ref": "CPU oracle (oracle/oracle_sequence.py): PoseOptimization summed in g2o's edge order with "
                           "Eigen's per-edge arithmetic and correctly rounded sin/cos/atan2/pow (the pinned libm, "
-                          "DESIGN.md 3.3); glibc_libm_cpu_ref: the same loop with the host glibc's double routines",
+                          "DESIGN.md 3.3); glibc_libm_cpu_ref: the same loop with the host glibc's double routines; "
+                          "fma_contracted_cpu_ref: the same loop with the pose / LBA restatement compiled with GCC's "
+                          "FP contraction (a -march=native g2o build, Thirdparty/g2o/CMakeLists.txt:57)",
                "vs_cpu_ref_m": [], "max_center_diff_vs_cpu_ref_m": [],
                "max_rotation_diff_vs_cpu_ref": [], "vs_ground_truth_m": [], "cpu_ref_vs_ground_truth_m": [],
                "ate_difference_vs_cpu_ref_m": [], "identical_decisions_until_frame": [],
                "glibc_libm_cpu_ref": {"vs_gpu_m": [], "vs_cpu_ref_m": [], "vs_ground_truth_m": [],
-                                      "identical_decisions_until_frame": []}}
+                                      "identical_decisions_until_frame": []},
+               "fma_contracted_cpu_ref": {"vs_gpu_m": [], "vs_cpu_ref_m": [], "vs_ground_truth_m": [],
+                                          "identical_decisions_until_frame": []}}
         t1 = time.perf_counter()
 
         import synth
@@ -397,6 +401,9 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         oracle_sequence.vocabulary(vocab_text)  # loaded once, before the threads
 
         def run_oracle(slot, order):
+            if order == "fma":  # the pinned libm, contracted g2o arithmetic
+                with oracle_ctypes.g2o_fma(True):
+                    return run_oracle(slot, oracle_ctypes.LIBM_CR)
             frames, T0, P0, local_of = sp.oracle_inputs(slot)
             ch = {}
 
@@ -415,16 +422,18 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
 
         from concurrent.futures import ThreadPoolExecutor
         jobs = [(slot, order) for slot in range(n_seq)
-                for order in (oracle_ctypes.LIBM_CR, oracle_ctypes.LIBM_GLIBC)]
+                for order in (oracle_ctypes.LIBM_CR, oracle_ctypes.LIBM_GLIBC, "fma")]
         with ThreadPoolExecutor(len(jobs)) as pool:
             done = dict(zip(jobs, pool.map(lambda j: run_oracle(*j), jobs)))
         for slot in range(n_seq):
             cpu, div = done[(slot, oracle_ctypes.LIBM_CR)]
             cpu_g, div_g = done[(slot, oracle_ctypes.LIBM_GLIBC)]
+            cpu_f, div_f = done[(slot, "fma")]
             out["identical_decisions_until_frame"].append(div)
             g = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n_frames)]
             c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n_frames)]
             cg = [trajectory.camera_center(cpu_g[k].reshape(16)) for k in range(n_frames)]
+            cf = [trajectory.camera_center(cpu_f[k].reshape(16)) for k in range(n_frames)]
             gt = [np.linalg.inv(sp._true_pose(slot, k + 1))[:3, 3] for k in range(n_frames)]
             out["vs_cpu_ref_m"].append(trajectory.ate_rmse(g, c))
             out["max_center_diff_vs_cpu_ref_m"].append(float(np.linalg.norm(np.array(g) - np.array(c), axis=1).max()))
@@ -438,6 +447,11 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             go["vs_cpu_ref_m"].append(trajectory.ate_rmse(c, cg))
             go["vs_ground_truth_m"].append(trajectory.ate_rmse(cg, gt))
             go["identical_decisions_until_frame"].append(div_g)
+            fo = out["fma_contracted_cpu_ref"]
+            fo["vs_gpu_m"].append(trajectory.ate_rmse(g, cf))
+            fo["vs_cpu_ref_m"].append(trajectory.ate_rmse(c, cf))
+            fo["vs_ground_truth_m"].append(trajectory.ate_rmse(cf, gt))
+            fo["identical_decisions_until_frame"].append(div_f)
         out["cpu_frames_per_s"] = len(jobs) * n_frames / (time.perf_counter() - t1)  # len(jobs) threads
         out["wall_s"] = {"gpu_incl_render": t_gpu, "cpu": time.perf_counter() - t1}
         return out

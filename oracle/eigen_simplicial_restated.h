@@ -37,7 +37,13 @@
 #include <cmath>
 #include <vector>
 
-namespace oracle {
+// ORACLE_NS: the namespace of the g2o / Eigen restatement -- "oracle", or "oracle_fma" when the Makefile compiles
+// pose_oracle.cpp / lba_oracle.cpp a second time with GCC's FP contraction (the FMA diagnostic mode)
+#ifndef ORACLE_NS
+#define ORACLE_NS oracle
+#endif
+
+namespace ORACLE_NS {
 namespace eigen_sparse {
 
 inline int amd_flip(int i) { return -i - 2; }

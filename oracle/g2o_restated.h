@@ -15,7 +15,18 @@
 
 #include "libm_cr_oracle.h"
 
-namespace oracle {
+// ORACLE_NS: the namespace of the g2o / Eigen restatement -- "oracle", or "oracle_fma" when the Makefile compiles
+// pose_oracle.cpp / lba_oracle.cpp a second time with GCC's FP contraction (the FMA diagnostic mode)
+#ifndef ORACLE_NS
+#define ORACLE_NS oracle
+#endif
+#ifdef ORACLE_FMA_VARIANT
+#define ORACLE_ENTRY(name) name##_fma
+#else
+#define ORACLE_ENTRY(name) name
+#endif
+
+namespace ORACLE_NS {
 namespace g2o_math {
 
 // Elementary functions: correctly rounded by default (libm_cr_oracle.h: the

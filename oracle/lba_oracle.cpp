@@ -46,7 +46,7 @@
 #include "eigen_simplicial_restated.h"
 #include "g2o_restated.h"
 
-namespace oracle {
+namespace ORACLE_NS {
 namespace lba {
 
 using namespace g2o_math;
@@ -518,8 +518,8 @@ struct Opt {
 }  // namespace lba
 }  // namespace oracle
 
-using namespace oracle;
-using namespace oracle::lba;
+using namespace ORACLE_NS;
+using namespace ORACLE_NS::lba;
 
 namespace {
 SE3 se3_from_cv(const float* Tcw) {
@@ -545,12 +545,26 @@ Plane plane_from_cv(const float* c) {  // Converter::toPlane3D: flip d < 0, then
 
 // stop_after: pbStopFlag raised after that many LM trials (0 = already set at the call: the reference returns
 // before initializeOptimization, Optimizer.cc:1757-1759; < 0 = never raised)
-extern "C" int oracle_lba_optimize_stop(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
-                                        const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
-                                        const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
-                                        const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
-                                        uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res,
-                                        int stop_after) {
+#ifndef ORACLE_FMA_VARIANT
+extern "C" int oracle_get_g2o_fma();  // pose_oracle.cpp: this thread's FMA diagnostic mode
+extern "C" int oracle_lba_optimize_stop_fma(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
+                                            const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                                            const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
+                                            const spslam_plane_config* cfg, float* kf_out, float* pt_out,
+                                            float* pl_out, uint8_t* pobs_outlier, uint8_t* plobs_outlier,
+                                            spslam_lba_result* res, int stop_after);
+#endif
+extern "C" int ORACLE_ENTRY(oracle_lba_optimize_stop)(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
+                                                      const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                                                      const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
+                                                      const spslam_plane_config* cfg, float* kf_out, float* pt_out,
+                                                      float* pl_out, uint8_t* pobs_outlier, uint8_t* plobs_outlier,
+                                                      spslam_lba_result* res, int stop_after) {
+#ifndef ORACLE_FMA_VARIANT
+    if (oracle_get_g2o_fma())
+        return oracle_lba_optimize_stop_fma(P, kfs, pts, pobs, pls, plobs, cfg, kf_out, pt_out, pl_out, pobs_outlier,
+                                            plobs_outlier, res, stop_after);
+#endif
     std::memset(res, 0, sizeof *res);
     if (stop_after == 0) {  // if(*pbStopFlag) return;  -- nothing optimised, nothing erased
         for (int k = 0; k < P->n_kf; k++) std::memcpy(kf_out + 16 * k, kfs[k].Tcw, 64);
@@ -689,21 +703,22 @@ extern "C" int oracle_lba_optimize_stop(const spslam_lba_problem* P, const spsla
     return 0;
 }
 
-extern "C" int oracle_lba_optimize(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
-                                   const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
-                                   const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
-                                   const spslam_plane_config* cfg, float* kf_out, float* pt_out, float* pl_out,
-                                   uint8_t* pobs_outlier, uint8_t* plobs_outlier, spslam_lba_result* res) {
-    return oracle_lba_optimize_stop(P, kfs, pts, pobs, pls, plobs, cfg, kf_out, pt_out, pl_out, pobs_outlier,
+extern "C" int ORACLE_ENTRY(oracle_lba_optimize)(const spslam_lba_problem* P, const spslam_lba_keyframe* kfs,
+                                                 const spslam_lba_point* pts, const spslam_lba_point_obs* pobs,
+                                                 const spslam_lba_plane* pls, const spslam_lba_plane_obs* plobs,
+                                                 const spslam_plane_config* cfg, float* kf_out, float* pt_out,
+                                                 float* pl_out, uint8_t* pobs_outlier, uint8_t* plobs_outlier,
+                                                 spslam_lba_result* res) {
+    return ORACLE_ENTRY(oracle_lba_optimize_stop)(P, kfs, pts, pobs, pls, plobs, cfg, kf_out, pt_out, pl_out, pobs_outlier,
                                     plobs_outlier, res, -1);
 }
 
 // Test access to the SimplicialLDLT restatement (tests/test_oracle_lba.py): factorise the upper-triangular CCS
 // pattern (Ap, Ai) with values Ax, solve A x = b; perm receives the AMD order (Pinv).  Returns 0, or 1 on a
 // zero pivot.
-extern "C" int oracle_eigen_ldlt(int n, const int* Ap, const int* Ai, const double* Ax, const double* b, double* x,
+extern "C" int ORACLE_ENTRY(oracle_eigen_ldlt)(int n, const int* Ap, const int* Ai, const double* Ax, const double* b, double* x,
                                  int* perm) {
-    oracle::eigen_sparse::SimplicialLDLT s;
+    ORACLE_NS::eigen_sparse::SimplicialLDLT s;
     std::vector<int> ap(Ap, Ap + n + 1), ai(Ai, Ai + Ap[n]);
     s.analyze(n, ap, ai);
     for (int k = 0; k < n; k++) perm[k] = s.Pinv[k];

@@ -11,7 +11,13 @@
 
 #include <cmath>
 
-namespace oracle {
+// ORACLE_NS: the namespace of the g2o / Eigen restatement -- "oracle", or "oracle_fma" when the Makefile compiles
+// pose_oracle.cpp / lba_oracle.cpp a second time with GCC's FP contraction (the FMA diagnostic mode)
+#ifndef ORACLE_NS
+#define ORACLE_NS oracle
+#endif
+
+namespace ORACLE_NS {
 namespace libm_cr {
 
 inline bool settle(long double v, double* out) {

@@ -185,6 +185,22 @@ def libm_cr(kind: int, a, b=None):
 
 
 @contextlib.contextmanager
+def g2o_fma(on: bool = True):
+    """FMA diagnostic mode of the pose / LBA oracle inside the block, for the calling thread: the same restatement
+    compiled with GCC's FP contraction (oracle/Makefile FMA_FLAGS), the arithmetic a -march=native build of the
+    reference's g2o gets (Thirdparty/g2o/CMakeLists.txt:57).  Off (default): the pinned uncontracted semantics."""
+    L = lib()
+    L.oracle_get_g2o_fma.restype = ctypes.c_int
+    L.oracle_set_g2o_fma.argtypes = [ctypes.c_int]
+    prev = L.oracle_get_g2o_fma()
+    L.oracle_set_g2o_fma(int(bool(on)))
+    try:
+        yield
+    finally:
+        L.oracle_set_g2o_fma(prev)
+
+
+@contextlib.contextmanager
 def libm(mode: int):
     """Elementary functions of the pose / LBA oracle inside the block, for the calling thread
     (oracle/g2o_restated.h libm_mode): LIBM_CR (default: correctly rounded, the path's pinned semantics,

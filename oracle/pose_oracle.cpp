@@ -41,7 +41,7 @@
 #include "../include/spslam_gpu.h"
 #include "g2o_restated.h"
 
-namespace oracle {
+namespace ORACLE_NS {
 namespace {
 
 using namespace g2o_math;
@@ -304,12 +304,13 @@ int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
 }  // namespace
 }  // namespace oracle
 
-using namespace oracle;
+using namespace ORACLE_NS;
 
 // libm of the calling thread's PoseOptimization / LocalBundleAdjustment: 0 correctly rounded (default),
 // 1 host glibc (g2o_restated.h libm_mode)
 // the oracle's correctly rounded elementary functions (libm_cr_oracle.h) on n arguments: kind 0 sin, 1 cos,
 // 2 atan2(a, b), 3 cube -- the checker of the device's spslam_debug_libm64
+#ifndef ORACLE_FMA_VARIANT
 extern "C" void oracle_libm_cr(int kind, const double* a, const double* b, long n, double* out) {
     for (long i = 0; i < n; i++)
         out[i] = kind == 0 ? libm_cr::sin(a[i])
@@ -319,9 +320,27 @@ extern "C" void oracle_libm_cr(int kind, const double* a, const double* b, long 
 extern "C" void oracle_set_libm(int mode) { g2o_math::libm_mode() = mode; }
 extern "C" int oracle_get_libm() { return g2o_math::libm_mode(); }
 
-extern "C" int oracle_pose_optimize(const spslam_pose_problem* P, const spslam_point_obs* pts,
-                                    const spslam_plane_obs* pls, const spslam_plane_config* cfg,
-                                    spslam_pose_result* out, uint8_t* pout, uint8_t* plout) {
+// FMA diagnostic mode of the calling thread: 0 (default) the pinned uncontracted arithmetic, 1 PoseOptimization and
+// LocalBundleAdjustment run the same restatement compiled with GCC's FP contraction (-ffp-contract=fast on an FMA
+// target), as the reference's -march=native build of g2o would be (Thirdparty/g2o/CMakeLists.txt:57).  The
+// contracted copies keep the correctly rounded libm.
+static int& g2o_fma_mode() {
+    static thread_local int mode = 0;
+    return mode;
+}
+extern "C" void oracle_set_g2o_fma(int on) { g2o_fma_mode() = on; }
+extern "C" int oracle_get_g2o_fma() { return g2o_fma_mode(); }
+extern "C" int oracle_pose_optimize_fma(const spslam_pose_problem* P, const spslam_point_obs* pts,
+                                        const spslam_plane_obs* pls, const spslam_plane_config* cfg,
+                                        spslam_pose_result* out, uint8_t* pout, uint8_t* plout);
+#endif
+
+extern "C" int ORACLE_ENTRY(oracle_pose_optimize)(const spslam_pose_problem* P, const spslam_point_obs* pts,
+                                                  const spslam_plane_obs* pls, const spslam_plane_config* cfg,
+                                                  spslam_pose_result* out, uint8_t* pout, uint8_t* plout) {
+#ifndef ORACLE_FMA_VARIANT
+    if (g2o_fma_mode()) return oracle_pose_optimize_fma(P, pts, pls, cfg, out, pout, plout);
+#endif
     M3 R;
     for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) R.m[i][j] = P->Tcw[4 * i + j];

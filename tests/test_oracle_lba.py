@@ -137,3 +137,20 @@ def test_eigen_ldlt_restatement_solves_and_orders():
     runs = [blocks[i] for i in range(n) if i == 0 or blocks[i] != blocks[i - 1]]
     assert sorted(runs) == list(range(P)), runs  # supervariables: each pose's 6 scalars eliminated together
     assert list(perm) != list(range(n))          # a genuine fill-reducing order, not the natural one
+
+
+def test_fma_diagnostic_mode_is_contracted_and_scoped():
+    """oracle_ctypes.g2o_fma: the LBA / pose restatement compiled with GCC's FP contraction (the reference's
+    -march=native g2o) -- a different rounding of the same algorithm: close to the pinned result, not bit-equal,
+    and only inside the block."""
+    import oracle_ctypes
+    P = _prob(7, n_points=800)
+    a = oracle_lba.lba_optimize(*P[:6])
+    with oracle_ctypes.g2o_fma(True):
+        f = oracle_lba.lba_optimize(*P[:6])
+    b = oracle_lba.lba_optimize(*P[:6])
+    assert np.array_equal(a["Tcw"], b["Tcw"]) and np.array_equal(a["points"], b["points"])
+    assert not np.array_equal(a["points"], f["points"])
+    loc = P[1]["fixed"] == 0
+    assert np.abs(a["Tcw"][loc] - f["Tcw"][loc]).max() < 1e-4
+    assert np.array_equal(a["point_outlier"], f["point_outlier"])
