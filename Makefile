@@ -12,7 +12,7 @@ CSRC := $(PKG)/csrc
 OBJDIR := build/obj
 KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels lba_g2o \
            assoc_kernels match_kernels track_kernels grab_kernels bow_kernels
-OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi spslam_step))
 GPU_HDRS := $(wildcard $(CSRC)/*.h) include/spslam_gpu.h include/spslam_brief_pattern.inc
 
 all: $(PKG)/libspslam_gpu.so oracle/liboracle.so tests/shim/libreference_shim.so
@@ -25,13 +25,17 @@ $(OBJDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -x hip -o $@ $<
 
+$(OBJDIR)/spslam_step.o: $(CSRC)/spslam_step.cpp $(GPU_HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c -x hip -o $@ $<
+
 $(PKG)/libspslam_gpu.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(OBJS)
 	@python3 tools/build_info.py $@ > $(PKG)/build_info.json
 
 # Diagnostic build: PoseOptimization phase timers (tools/pose_phases.py loads it via SPSLAM_GPU_LIB).
 PROFDIR := build/prof
-PROF_OBJS := $(addprefix $(PROFDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+PROF_OBJS := $(addprefix $(PROFDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi spslam_step))
 prof: $(PKG)/libspslam_gpu_prof.so
 
 $(PROFDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
@@ -39,6 +43,10 @@ $(PROFDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
 	$(HIPCC) $(HIPFLAGS) -DSPSLAM_POSE_PROF -c -o $@ $<
 
 $(PROFDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
+	@mkdir -p $(PROFDIR)
+	$(HIPCC) $(HIPFLAGS) -DSPSLAM_POSE_PROF -c -x hip -o $@ $<
+
+$(PROFDIR)/spslam_step.o: $(CSRC)/spslam_step.cpp $(GPU_HDRS)
 	@mkdir -p $(PROFDIR)
 	$(HIPCC) $(HIPFLAGS) -DSPSLAM_POSE_PROF -c -x hip -o $@ $<
 
@@ -50,7 +58,7 @@ $(PKG)/libspslam_gpu_prof.so: $(PROF_OBJS)
 VARIANT ?= var
 VAR_FLAGS ?=
 VARDIR := build/var_$(VARIANT)
-VAR_OBJS := $(addprefix $(VARDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi))
+VAR_OBJS := $(addprefix $(VARDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi spslam_step))
 variant: $(PKG)/libspslam_gpu_$(VARIANT).so
 
 $(VARDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
@@ -58,6 +66,10 @@ $(VARDIR)/%.o: $(CSRC)/%.hip $(GPU_HDRS)
 	$(HIPCC) $(HIPFLAGS) $(VAR_FLAGS) -c -o $@ $<
 
 $(VARDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
+	@mkdir -p $(VARDIR)
+	$(HIPCC) $(HIPFLAGS) $(VAR_FLAGS) -c -x hip -o $@ $<
+
+$(VARDIR)/spslam_step.o: $(CSRC)/spslam_step.cpp $(GPU_HDRS)
 	@mkdir -p $(VARDIR)
 	$(HIPCC) $(HIPFLAGS) $(VAR_FLAGS) -c -x hip -o $@ $<
 

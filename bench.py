@@ -354,6 +354,46 @@ def closed_loop(cfg, device, B, steps, warmup, n_seq=16):
         sp.close()
 
 
+def single_sequence(cfg, device, n_frames=120, warmup=5):
+    """The reference's own call pattern (Examples/RGB-D/SPSLAM.cc:90-136 -> System::TrackRGBD per frame): ONE
+    tracked sequence, one frame at a time (B = 1, sp-slam_amd/sequence.py; every frame's prior and last-frame
+    points from its predecessor).  frames_per_s: frame k+1's grab / ORB / planes overlapped with frame k's tracking
+    tail (the pipelined step), host synchronised only at the end.  latency_ms_*: the serial step (grab ->
+    extraction -> tracking tail) with the host waiting for each frame's pose -- image on the device to pose on the
+    device, the per-frame latency a TrackRGBD caller sees (the 64-byte pose read-back excluded)."""
+    import numpy as np
+    import torch
+    import sequence
+    out = {"kind": "one sequence, B = 1 (sequence.SequencePath), frames device-resident", "frames": n_frames}
+    for pipelined in (True, False):
+        sp = sequence.SequencePath(1, n_frames + warmup + 2, n_sequences=1, device=device, pipelined=pipelined,
+                                   render_workers=min(16, os.cpu_count() or 1), **cfg)
+        try:
+            for _ in range(warmup):
+                sp.step()
+            torch.cuda.synchronize()
+            lat = []
+            t0 = time.perf_counter()
+            for _ in range(n_frames):
+                ts = time.perf_counter()
+                sp.step()
+                if not pipelined:
+                    torch.cuda.synchronize()
+                    lat.append(time.perf_counter() - ts)
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+        finally:
+            sp.close()
+        if pipelined:
+            out["frames_per_s"] = n_frames / el
+        else:
+            out["serial_frames_per_s"] = n_frames / el
+            out["latency_ms_p50"] = float(np.percentile(lat, 50) * 1e3)
+            out["latency_ms_p99"] = float(np.percentile(lat, 99) * 1e3)
+            out["latency_ms_max"] = float(max(lat) * 1e3)
+    return out
+
+
 def ate_sequences(cfg, device, n_frames=300, n_seq=2):
     """ATE of tracked sequences (sp-slam_amd/sequence.py): n_seq sequences of n_frames tracked frames each on
     the GPU, every frame's prior and last-frame points from its predecessor's result, against the CPU oracle
@@ -490,10 +530,15 @@ def main():
     ap.add_argument("--lba-order", default="g2o", choices=("g2o", "fast"),
                     help="LocalBundleAdjustment summation order (C3): g2o = the reference's arithmetic, bit-exact "
                          "to the oracle (default); fast = the phase kernels (tree / matrix-core order)")
+    ap.add_argument("--python-step", action="store_true",
+                    help="drive the step's stages from Python over torch streams (pipeline.py) instead of the "
+                         "library's whole-step entry spslam_step_run (the default without LocalMapping)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each step's extraction and tracking back to back (no cross-step overlap)")
     ap.add_argument("--ate-frames", type=int, default=300,
                     help="frames per tracked sequence of the ATE check (0 = skip)")
+    ap.add_argument("--single-sequence-frames", type=int, default=120,
+                    help="frames of the single-sequence (B = 1) line (0 = skip)")
     ap.add_argument("--closed-loop-steps", type=int, default=20,
                     help="timed steps of the closed-loop line (tracked sequences at --batch slots; 0 = skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -531,7 +576,8 @@ def main():
     hp = pipeline.HotPath(args.batch, unique_frames=args.unique_frames, device=local,
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
                           orb_priority=args.orb_priority, planes_priority=not args.no_planes_priority,
-                          lba_order=0 if args.lba_order == "g2o" else 1, **cfg,
+                          lba_order=0 if args.lba_order == "g2o" else 1,
+                          native=not args.python_step and not cfg.get("lba_every"), **cfg,
                           **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
@@ -613,6 +659,8 @@ def main():
                    "parallelism": f"shard{world}" + ("-rehearsal-on-gpu0-gloo" if args.rehearse_one_gpu else ""),
                    "mean_keypoints": hp.mean_keypoints,
                    "pipelined": hp.pipelined,
+                   "step": "spslam_step_run (library streams and events)" if hp.native is not None
+                           else "pipeline.py over torch streams",
                    "mean_planes": float(res["plane_counts"].mean()),
                    "mean_supposed_planes": n_sup,
                    "pose_edges_per_frame": n_pts + n_pls},
@@ -653,6 +701,10 @@ def main():
     hp.close()
     if rank == 0 and args.closed_loop_steps > 0:
         result["closed_loop"] = closed_loop(cfg, local, args.batch, args.closed_loop_steps, args.warmup)
+    if rank == 0 and args.single_sequence_frames > 0:
+        result["single_sequence"] = single_sequence(cfg, local, n_frames=args.single_sequence_frames)
+        if result["cpu_baseline"]:  # one core, the same per-frame work (the oracle step, open loop)
+            result["single_sequence"]["cpu_1core_frames_per_s"] = result["cpu_baseline"]["value"]
     if rank == 0 and args.ate_frames > 0:
         result["ate"] = ate_sequences(cfg, local, n_frames=args.ate_frames)
     if rank == 0:

@@ -944,6 +944,101 @@ int spslam_search_by_bow_batch_device(spslam_ctx* ctx, int n_pairs, const int32_
                                       const spslam_bow_params* params, int32_t* d_match, int* d_nmatches,
                                       void* hip_stream);
 
+/* ---------------------------------------------------------------- the whole batched step
+ * The throughput path as one call per step, for a C / C++ caller: GrabImageRGBD (Tracking.cc:208-229) ->
+ * ORB extraction || ComputePlanesFromOrganizedPointCloud + GeneratePlanesFromBoundries (the RGB-D Frame
+ * constructor) -> the tracking tail: Frame keypoint steps, SearchByProjection (TrackWithMotionModel,
+ * Tracking.cc:951-975), AssociatePlanesByBoundary, the motion-model PoseOptimization graph and optimisation,
+ * the outlier discard, SearchLocalPoints, the second association, the local-map graph and PoseOptimization
+ * (TrackLocalMap, :1054-1068) -- the batched entry points above, enqueued on streams and events the step
+ * object owns (the tail stream at high priority).  pipelined != 0: spslam_step_run(k) enqueues batch k+1's
+ * extraction (grab + ORB on one stream, planes on another, into extraction set (k+1) % 2) beside batch k's
+ * tail (set k % 2); a set is rewritten only after the tail that read it has finished.  spslam_step_prime
+ * enqueues batch 0's extraction once before the first run.  pipelined == 0: each run is grab -> (planes ||
+ * ORB) -> tail of `next`, set 0 only.  The context must be configured as for the single stages
+ * (spslam_frame_configure, spslam_planes_configure; the vocabulary is not used).
+ * Buffers: device memory; NULL members of the sets / tail are allocated by the step object (owned, freed by
+ * spslam_step_destroy), others are the caller's; spslam_step_buffers returns all of them. */
+typedef struct spslam_step_config {
+    int32_t n_frames, width, height, kp_cap;      /* batch, image size, keypoint slots per frame */
+    int32_t pipelined, tail_priority, orb_priority, planes_priority;
+    spslam_grab_params grab;                      /* GrabImageRGBD: channels, mbRGB, depth type, mDepthMapFactor */
+    spslam_match_params match;                    /* TrackWithMotionModel: th 15, checkOri, retry below 20 */
+    spslam_local_params local;                    /* SearchLocalPoints: th 3, nn 0.8, viewing cos 0.5 */
+    spslam_assoc_params assoc;                    /* Plane.Association* / Vertical / ParallelThreshold */
+    spslam_plane_config pose;                     /* PoseOptimization Plane.* keys */
+    float fx, fy, cx, cy, bf;                     /* camera (the graph's point edges) */
+    int32_t pad;
+} spslam_step_config;
+
+typedef struct spslam_step_frames {               /* one batch of input frames (GrabImageRGBD's inputs) */
+    const uint8_t* color;                         /* frame f at color + f * color_frame_stride bytes */
+    size_t color_frame_stride;
+    const void* depth;                            /* frame f at depth + f * depth_frame_stride elements */
+    size_t depth_frame_stride;
+    int32_t color_stride, depth_stride;           /* row strides: bytes / elements */
+} spslam_step_frames;
+
+typedef struct spslam_step_tracking {             /* one batch's tracking inputs (device) */
+    const spslam_proj_frame* proj_frames;         /* last frames' map points (spslam_search_by_projection_batch_device) */
+    const spslam_proj_point* proj_points;
+    spslam_local_frame* local_frames;             /* local maps (spslam_search_local_points_batch_device; DISCARD writes Tcw) */
+    const spslam_local_point* local_points;
+    const spslam_assoc_frame* assoc_frames1;      /* first association (motion-model pose) */
+    spslam_assoc_frame* assoc_frames2;            /* second (DISCARD writes Tcw), carry = 1 */
+    const spslam_map_plane* map;
+    const float* boundary_xyz;
+    int32_t max_proj_points, max_local_points, max_map, pad;
+} spslam_step_tracking;
+
+typedef struct spslam_step_set {                  /* extraction outputs of one batch (the batch layouts above) */
+    uint8_t* gray;
+    float* depth;
+    spslam_keypoint* kps;
+    uint8_t* desc;
+    int* counts;
+    spslam_plane* planes;
+    int* plane_counts;
+    int32_t* inliers;
+    int32_t* contours;
+    spslam_supposed_plane* supposed;
+    int* supposed_counts;
+    int32_t* lines;
+    float* patch;
+} spslam_step_set;
+
+typedef struct spslam_step_tail {                 /* the tracking tail's buffers and outputs */
+    spslam_keypoint* keys_un;
+    float* mv_depth;
+    float* uright;
+    int32_t* grid_off;
+    int32_t* grid_idx;
+    int32_t* match;
+    int* nmatches;
+    uint8_t* taken;
+    int32_t* local_match;
+    int* local_nmatches;
+    int32_t* edge_of_kp;
+    int32_t* assoc[2][3];                         /* [association][match, parallel, vertical] */
+    int* new_plane[2];
+    spslam_pose_problem* problems[2];             /* [0] motion model, [1] local map */
+    spslam_point_obs* points[2];
+    spslam_plane_obs* planes[2];
+    uint8_t* point_outlier[2];
+    uint8_t* plane_outlier[2];
+    spslam_pose_result* results[2];
+} spslam_step_tail;
+
+typedef struct spslam_step spslam_step;
+int spslam_step_create(spslam_ctx* ctx, const spslam_step_config* cfg, const spslam_step_set* sets /* [2], may be NULL */,
+                       const spslam_step_tail* tail /* may be NULL */, spslam_step** out);
+int spslam_step_buffers(const spslam_step* step, spslam_step_set* sets /* [2] */, spslam_step_tail* tail);
+int spslam_step_prime(spslam_step* step, const spslam_step_frames* first);
+int spslam_step_run(spslam_step* step, const spslam_step_frames* next, const spslam_step_tracking* tracking);
+int spslam_step_sync(spslam_step* step);          /* host waits for every stream of the step */
+void* spslam_step_stream(const spslam_step* step); /* the tail stream (hipStream_t) */
+void spslam_step_destroy(spslam_step* step);
+
 /* Measurement: when enabled, every kernel kind launched by this context is
  * bracketed by HIP events on its launch stream.  spslam_kernel_times returns,
  * per kind, the summed event time (ms) and number of timed launches since the

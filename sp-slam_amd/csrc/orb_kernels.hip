@@ -18,6 +18,8 @@
 // reference build's contraction of the BRIEF sample expression.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "../../include/spslam_gpu.h"
 #include "orb_launch.h"
 
@@ -154,16 +156,24 @@ __device__ __forceinline__ uint32_t fast_maybe4(uint32_t V, uint32_t C0, uint32_
     return res;
 }
 
-__global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
-    __shared__ __attribute__((aligned(16))) uint8_t tin[kLH][kTinPitch];
-    __shared__ __attribute__((aligned(16))) uint16_t th[kLH][kLevelTileW];
-    __shared__ RzCol rx[kTinPitch], ry[kLH];
-    __shared__ RzGroup rg[kLG];
-    __shared__ uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
-    __shared__ __attribute__((aligned(16))) uint8_t stile[kLevelTileH][kLevelTileW];  // FAST scores of the tile
+// The LDS of one tile (a 256-thread group).
+struct LevelLds {
+    __attribute__((aligned(16))) uint8_t tin[kLH][kTinPitch];
+    __attribute__((aligned(16))) uint16_t th[kLH][kLevelTileW];
+    RzCol rx[kTinPitch], ry[kLH];
+    RzGroup rg[kLG];
+    uint16_t cand[kLevelThreads / 64][kLevelTileH * kLevelTileW / (kLevelThreads / 64)];
+    __attribute__((aligned(16))) uint8_t stile[kLevelTileH][kLevelTileW];  // FAST scores of the tile
+};
+
+// One 64x32 tile of level l of frame f on the 256 threads t of a group.  Every __syncthreads of the body is
+// reached by every thread of the workgroup; `active` false (a group without a tile of its own in the fused
+// launch: it repeats a valid tile in its own LDS) suppresses the global stores.
+__device__ __forceinline__ void level_tile(const OrbGeom& g, int l, int minTh, int f, int tile, bool active, int t,
+                                           LevelLds& sm) {
     const LevelGeom& L = g.lv[l];
-    const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int x0 = (blockIdx.x % L.tiles_x) * kLevelTileW, y0 = (blockIdx.x / L.tiles_x) * kLevelTileH;
+    const int lane = t & 63, wave = t >> 6;
+    const int x0 = (tile % L.tiles_x) * kLevelTileW, y0 = (tile / L.tiles_x) * kLevelTileH;
     const int w = L.w, h = L.h;
     uint8_t* img = const_cast<uint8_t*>(L.img) + f * L.frame_stride;
     constexpr int kNG = kLH * kLG, kIterG = (kNG + kLevelThreads - 1) / kLevelThreads;
@@ -188,7 +198,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
                 const int q = t + k * kLevelThreads;
                 if (q < kNG) {
                     const int r = q / kLG, m = q - r * kLG;
-                    *reinterpret_cast<uint32_t*>(&tin[r][4 * m]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], 1);
+                    *reinterpret_cast<uint32_t*>(&sm.tin[r][4 * m]) = __builtin_amdgcn_alignbyte(hi[k], lo[k], 1);
                 }
             }
         } else {
@@ -207,7 +217,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
 #pragma unroll
             for (int k = 0; k < kIter; k++) {
                 const int q = t + k * kLevelThreads;
-                if (q < kN) tin[q / kLW][q % kLW] = v[k];
+                if (q < kN) sm.tin[q / kLW][q % kLW] = v[k];
             }
         }
     } else {
@@ -219,7 +229,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             for (int j = 0; j < 4; j++) {
                 const int c = 4 * t + j;
                 cx[j] = resize_coef(L.rscale_x, reflect1(min(x0 + c - 3, w + 2), w), S.w, true);
-                rx[c] = cx[j];
+                sm.rx[c] = cx[j];
             }
             const int sb = cx[0].x0, a = sb & ~3;
             bool ok = a + 12 <= S.stride && ((reinterpret_cast<uintptr_t>(src) | (uintptr_t)S.stride) & 3) == 0;
@@ -233,9 +243,9 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             }
             G.a = ok ? a : -1;
             G.s = sb & 3;
-            rg[t] = G;
+            sm.rg[t] = G;
         } else if (t >= 64 && t < 64 + kLH) {
-            ry[t - 64] = resize_coef(L.rscale_y, reflect1(y0 + (t - 64) - 3, h), S.h, false);
+            sm.ry[t - 64] = resize_coef(L.rscale_y, reflect1(y0 + (t - 64) - 3, h), S.h, false);
         }
         __syncthreads();
         typedef unsigned short u16v2 __attribute__((ext_vector_type(2)));
@@ -250,9 +260,9 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             for (int i = 0; i < 6; i++) wv[k][i] = 0;
             if (q < kNG) {
                 const int r = q / kLG, m = q - r * kLG;
-                const int a = rg[m].a;
+                const int a = sm.rg[m].a;
                 if (a >= 0) {
-                    const RzCol cy = ry[r];
+                    const RzCol cy = sm.ry[r];
                     const uint32_t* p0 = reinterpret_cast<const uint32_t*>(src + (size_t)cy.x0 * S.stride + a);
                     const uint32_t* p1 = reinterpret_cast<const uint32_t*>(src + (size_t)cy.x1 * S.stride + a);
                     wv[k][0] = p0[0]; wv[k][1] = p0[1]; wv[k][2] = p0[2];
@@ -265,8 +275,8 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             const int q = t + k * kLevelThreads;
             if (q < kNG) {
                 const int r = q / kLG, m = q - r * kLG;
-                const RzGroup& G = rg[m];
-                const RzCol cy = ry[r];
+                const RzGroup& G = sm.rg[m];
+                const RzCol cy = sm.ry[r];
                 uint32_t packed = 0;
                 if (G.a >= 0) {
                     const uint32_t s = (uint32_t)G.s;
@@ -287,14 +297,14 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
                     for (int j = 0; j < 4; j++) {
                         const int c = 4 * m + j;
                         if (c < kLW) {
-                            const RzCol cx = rx[c];
+                            const RzCol cx = sm.rx[c];
                             const int r0 = r0p[cx.x0] * cx.a0 + r0p[cx.x1] * cx.a1;
                             const int r1 = r1p[cx.x0] * cx.a0 + r1p[cx.x1] * cx.a1;
                             packed |= resize_v(cy, r0, r1) << (8 * j);
                         }
                     }
                 }
-                *reinterpret_cast<uint32_t*>(&tin[r][4 * m]) = packed;
+                *reinterpret_cast<uint32_t*>(&sm.tin[r][4 * m]) = packed;
             }
         }
     }
@@ -305,8 +315,8 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         // 4 pixels (row pitch L.stride is a multiple of 64; columns past w land in the row padding)
         for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
             const int r = rb + lr;
-            if (y0 + r < h) {
-                const uint32_t* p = reinterpret_cast<const uint32_t*>(&tin[r + 3][lc]);
+            if (active && y0 + r < h) {
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(&sm.tin[r + 3][lc]);
                 *reinterpret_cast<uint32_t*>(img + (size_t)(y0 + r) * L.stride + (x0 + lc)) =
                     __builtin_amdgcn_alignbyte(p[1], p[0], 3);
             }
@@ -316,7 +326,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
     // output j = dot4(bytes j..j+3, k0..k3) + dot4(bytes j+4..j+7, k4, k5, k6, 0)
     for (int q = t; q < kLH * (kLevelTileW / 4); q += kLevelThreads) {
         const int r = q / (kLevelTileW / 4), c = (q - r * (kLevelTileW / 4)) * 4;
-        const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&tin[r][c]);
+        const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&sm.tin[r][c]);
         const uint32_t a = w3[0], b = w3[1], d = w3[2];
         constexpr uint32_t K0 = 18u | (34u << 8) | (48u << 16) | (56u << 24), K1 = 48u | (34u << 8) | (18u << 16);
         uint32_t o[4];
@@ -326,7 +336,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             o[j] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, j), K0,
                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d, b, j), K1, 0u, false),
                                           false);
-        *reinterpret_cast<uint2*>(&th[r][c]) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
+        *reinterpret_cast<uint2*>(&sm.th[r][c]) = make_uint2(o[0] | (o[1] << 16), o[2] | (o[3] << 16));
     }
     __syncthreads();
     uint8_t* blur = L.blur + f * L.blur_frame_stride;
@@ -341,7 +351,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
         const int r = rb + lr, y = y0 + r;
         uint16_t tv[7][4];
 #pragma unroll
-        for (int i = 0; i < 7; i++) *reinterpret_cast<uint2*>(tv[i]) = *reinterpret_cast<const uint2*>(&th[r + i][lc]);
+        for (int i = 0; i < 7; i++) *reinterpret_cast<uint2*>(tv[i]) = *reinterpret_cast<const uint2*>(&sm.th[r + i][lc]);
         uint32_t bw = 0;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
@@ -349,13 +359,13 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
                            56 * tv[3][j];
             bw |= (uint32_t)min(255, (sb + (1 << 15)) >> 16) << (8 * j);
         }
-        if (y < h) *reinterpret_cast<uint32_t*>(blur + (size_t)y * bp + (x0 + lc)) = bw;
-        *reinterpret_cast<uint32_t*>(&stile[r][lc]) = 0u;
-        // the FAST pre-test's 5 pixels for the 4 centres (tin[r+3][lc+3+j]): centre row bytes lc..lc+11
+        if (active && y < h) *reinterpret_cast<uint32_t*>(blur + (size_t)y * bp + (x0 + lc)) = bw;
+        *reinterpret_cast<uint32_t*>(&sm.stile[r][lc]) = 0u;
+        // the FAST pre-test's 5 pixels for the 4 centres (sm.tin[r+3][lc+3+j]): centre row bytes lc..lc+11
         // and rows r, r+6 bytes lc+3..lc+6, from 7 dword LDS reads, realigned to one word per compass point
-        const uint32_t* rc = reinterpret_cast<const uint32_t*>(&tin[r + 3][lc]);
-        const uint32_t* ru = reinterpret_cast<const uint32_t*>(&tin[r][lc]);
-        const uint32_t* rd = reinterpret_cast<const uint32_t*>(&tin[r + 6][lc]);
+        const uint32_t* rc = reinterpret_cast<const uint32_t*>(&sm.tin[r + 3][lc]);
+        const uint32_t* ru = reinterpret_cast<const uint32_t*>(&sm.tin[r][lc]);
+        const uint32_t* rd = reinterpret_cast<const uint32_t*>(&sm.tin[r + 6][lc]);
         const uint32_t c0w = rc[0], c1w = rc[1], c2w = rc[2];
         const uint32_t V = __builtin_amdgcn_alignbyte(c1w, c0w, 3);
         const uint32_t CR = __builtin_amdgcn_alignbyte(c2w, c1w, 2);
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
             const int x = x0 + lc + j;
             const bool maybe = ((mb >> j) & 1u) && x >= 3 && x < w - 3;
             const unsigned long long m = __ballot(maybe);
-            if (maybe) cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(r * kLevelTileW + lc + j);
+            if (maybe) sm.cand[wave][ncand + __popcll(m & ((1ull << lane) - 1ull))] = (uint16_t)(r * kLevelTileW + lc + j);
             ncand += __popcll(m);
         }
     }
@@ -375,19 +385,50 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int k = lane; k < ncand; k += 64) {
-        const int q = cand[wave][k];
+        const int q = sm.cand[wave][k];
         const int r = q / kLevelTileW, c = q - r * kLevelTileW;
-        const int sc = max(fast_score(&tin[r + 3][c + 3], kTinPitch), 0);
-        stile[r][c] = (uint8_t)(sc >= minTh ? sc : 0);
+        const int sc = max(fast_score(&sm.tin[r + 3][c + 3], kTinPitch), 0);
+        sm.stile[r][c] = (uint8_t)(sc >= minTh ? sc : 0);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     for (int rb = wave * 4; rb < kLevelTileH; rb += kLevelThreads / 16) {
         const int r = rb + lr, y = y0 + r;
-        if (y < h)
+        if (active && y < h)
             *reinterpret_cast<uint32_t*>(score + (size_t)y * bp + (x0 + lc)) =
-                *reinterpret_cast<const uint32_t*>(&stile[r][lc]);
+                *reinterpret_cast<const uint32_t*>(&sm.stile[r][lc]);
+    }
+}
+
+// One launch per large level: one tile per workgroup.  XCD-aware order: the hardware deals consecutive
+// workgroups round-robin over the 8 XCDs (one L2 each); remapped, every XCD runs whole frames, so the 3-pixel
+// halos a tile shares with its neighbours (and the resize's source rows) are fetched into one L2 once instead
+// of by up to 8 L2s (PMC: 3-4x the algorithmic reads without the remap, profiles/r04/pmc_levels_*).
+__global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
+    __shared__ LevelLds sm;
+    const int nt = gridDim.x, total = nt * gridDim.y;
+    const int id = xcd_remap(blockIdx.y * nt + blockIdx.x, total);
+    level_tile(g, l, minTh, id / nt, id - (id / nt) * nt, true, threadIdx.x, sm);
+}
+
+// The small levels l0 .. nlevels-1 of one frame in one workgroup (no cross-workgroup hand-off): kLevelGroups
+// tiles at a time, one per 256-thread group, level after level; a level's image stores are made visible to
+// the workgroup (release / acquire at workgroup scope: the same CU's L1) before the next level reads them.
+template <int kLevelGroups>
+__global__ __launch_bounds__(kLevelThreads * kLevelGroups) void level_small_kernel(OrbGeom g, int l0, int minTh) {
+    __shared__ LevelLds sm[kLevelGroups];
+    const int grp = threadIdx.x / kLevelThreads, t = threadIdx.x % kLevelThreads, f = blockIdx.x;
+    for (int l = l0; l < g.nlevels; l++) {
+        const int nt = g.level_tiles[l];
+        for (int t0 = 0; t0 < nt; t0 += kLevelGroups) {
+            const int tile = t0 + grp;
+            level_tile(g, l, minTh, f, min(tile, nt - 1), tile < nt, t, sm[grp]);
+            __syncthreads();  // this round's LDS reads are over before the next round's writes
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 }
 
@@ -415,7 +456,9 @@ __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __
                                                          uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
     __shared__ __attribute__((aligned(16))) uint8_t scs[4][kScRowsMax * kScPitchMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int cid = blockIdx.x * 4 + wave, f = blockIdx.y;
+    // XCD-aware order (as level_kernel): a frame's cells, whose windows overlap by 6 pixels, on one L2
+    const int nb = gridDim.x, id = xcd_remap(blockIdx.y * nb + blockIdx.x, nb * gridDim.y);
+    const int f = id / nb, cid = (id - f * nb) * 4 + wave;
     if (cid >= g.cells_per_frame) return;
     uint8_t* sc = scs[wave];
     const int l = level_of_cell(g, cid);
@@ -991,6 +1034,25 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
 // Host-side launchers (called from spslam_capi.cpp).
 namespace spslam {
 
+// levels fused into level_small_kernel: the smallest ones whose tiles fit this budget per frame (640x480: L4-L7,
+// 114 tiles, 180K px); SPSLAM_ORB_SMALL_LEVELS=0 keeps one launch per level (A/B)
+constexpr int kSmallLevelTiles = 128;
+static bool small_levels_off() {
+    static const bool off = [] {
+        const char* e = getenv("SPSLAM_ORB_SMALL_LEVELS");
+        return e && e[0] == '0';
+    }();
+    return off;
+}
+// tile groups per level_small_kernel workgroup: 4 (1024 threads, default) or 2 (SPSLAM_ORB_SMALL_GROUPS=2)
+static int small_level_groups() {
+    static const int n = [] {
+        const char* e = getenv("SPSLAM_ORB_SMALL_GROUPS");
+        return e && e[0] == '2' ? 2 : 4;
+    }();
+    return n;
+}
+
 hipError_t orb_upload_tables(const int umax[16]) {
     return hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, 16 * sizeof(int));
 }
@@ -1016,9 +1078,19 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
     auto B = [&](int k) { if (timer) timer->begin(k, s); };
     auto E = [&](int k) { if (timer) timer->end(k, s); };
     B(kKindLevel);
-    for (int l = 0; l < g.nlevels; l++)
+    // the small levels (at most kSmallLevelTiles tiles per frame together) in one launch, one workgroup per frame
+    int l0 = g.nlevels, tiles = 0;
+    while (l0 > 1 && tiles + g.level_tiles[l0 - 1] <= kSmallLevelTiles) tiles += g.level_tiles[--l0];
+    if (g.nlevels - l0 < 2 || small_levels_off()) l0 = g.nlevels;  // one level alone: the per-level launch
+    for (int l = 0; l < l0; l++)
         hipLaunchKernelGGL(level_kernel, dim3(g.level_tiles[l], n), dim3(kLevelThreads), 0, s, g, l,
                            min(iniTh, minTh));
+    if (l0 < g.nlevels) {
+        if (small_level_groups() == 2)
+            hipLaunchKernelGGL(level_small_kernel<2>, dim3(n), dim3(kLevelThreads * 2), 0, s, g, l0, min(iniTh, minTh));
+        else
+            hipLaunchKernelGGL(level_small_kernel<4>, dim3(n), dim3(kLevelThreads * 4), 0, s, g, l0, min(iniTh, minTh));
+    }
     E(kKindLevel);
     B(kKindFast);
     hipLaunchKernelGGL(fast_cells_kernel, dim3((g.cells_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.cand,

@@ -253,7 +253,10 @@ __global__ __launch_bounds__(256) void plane_normal_kernel(PlaneGeom g, const fl
                                                            long long dist_fs, const double* __restrict__ integral,
                                                            long long integral_fs, float* normal, long long normal_fs,
                                                            float* pd, long long pd_fs) {
-    const int f = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    // XCD-aware order: a frame's blocks on one L2 (the smoothing windows of neighbouring blocks share the
+    // integral-image rows)
+    const int nb = gridDim.x, id = xcd_remap(blockIdx.y * nb + blockIdx.x, nb * gridDim.y);
+    const int f = id / nb, i = (id - f * nb) * 256 + threadIdx.x;
     if (i >= g.N) return;
     const int W = g.W, H = g.H, N = g.N, IW = W + 1, r = i / W, c = i - r * W;
     const float* X = cloud + f * cloud_fs;

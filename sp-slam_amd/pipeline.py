@@ -63,7 +63,7 @@ class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
-                 rotate_inputs=False, lba_order=0):
+                 rotate_inputs=False, lba_order=0, native=False):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -155,6 +155,11 @@ class HotPath:
         self.planes_priority = planes_priority
         if pipelined:
             self._setup_pipeline()
+        # native: the library enqueues the whole step (spslam_step_run, csrc/spslam_step.cpp) on its own streams
+        # and events over these same buffers; Python only makes the call
+        self.native = None
+        if native:
+            self._setup_native()
         torch.cuda.synchronize()  # buffers were filled on the default stream
 
     def _setup_inputs(self, seq_id, unique_frames):
@@ -514,6 +519,60 @@ class HotPath:
         self.primed = False
         torch.cuda.synchronize()
 
+    SET_NAMES = dict(d_gray="gray", d_depth="depth", d_kps="kps", d_desc="desc", d_cnt="counts", d_planes="planes",
+                     d_pcnt="plane_counts", d_inl="inliers", d_con="contours", d_supp="supposed",
+                     d_scnt="supposed_counts", d_lines="lines", d_patch="patch")
+
+    def _setup_native(self):
+        import spslam_match as SM
+        import spslam_step as SS
+        if self.n_lba or self.rotate_inputs:
+            raise ValueError("native step: no LocalMapping beside it and static inputs (use the Python step)")
+        cfg = SS.StepConfig(n_frames=self.B, width=self.W, height=self.H, kp_cap=self.kp_cap,
+                            pipelined=int(self.pipelined), tail_priority=int(self.main.priority < 0),
+                            orb_priority=int(getattr(self, "orb_priority", False)),
+                            planes_priority=int(getattr(self, "planes_priority", False)),
+                            grab=self.grabber.params, match=SM.MatchParams(*SM.MOTION_MODEL),
+                            local=SM.LocalParams(*SM.SEARCH_LOCAL), assoc=self.assoc.params, pose=self.plane_cfg,
+                            fx=self.fx, fy=self.fy, cx=self.cx, cy=self.cy, bf=self.bf)
+        sets = [{v: getattr(self, k).data_ptr() for k, v in self.SET_NAMES.items()}]
+        if self.pipelined:
+            sets = [{v: st[k].data_ptr() for k, v in self.SET_NAMES.items()} for st in self.sets]
+        else:
+            sets.append(dict(sets[0]))  # (the serial step uses set 0 only)
+        t = SS.StepTail(keys_un=self.d_kun.data_ptr(), mv_depth=self.d_kdepth.data_ptr(), uright=self.d_kur.data_ptr(),
+                        grid_off=self.d_grid_off.data_ptr(), grid_idx=self.d_grid_idx.data_ptr(),
+                        match=self.d_match.data_ptr(), nmatches=self.d_nmatch.data_ptr(),
+                        taken=self.d_taken.data_ptr(), local_match=self.d_lmatch.data_ptr(),
+                        local_nmatches=self.d_nlmatch.data_ptr(), edge_of_kp=self.d_edge.data_ptr())
+        for g in range(2):
+            for a in range(3):
+                t.assoc[g][a] = self.d_assoc[g][a].data_ptr()
+            t.new_plane[g] = self.d_newp[g].data_ptr()
+            gr = self.graphs[g]
+            t.problems[g], t.points[g], t.planes[g] = gr["P"].data_ptr(), gr["pts"].data_ptr(), gr["pls"].data_ptr()
+            t.point_outlier[g], t.plane_outlier[g] = gr["pout"].data_ptr(), gr["plout"].data_ptr()
+        t.results[0], t.results[1] = self.d_res1.data_ptr(), self.d_res2.data_ptr()
+        self.native = SS.Step(self.ex, cfg, sets, t)
+        self.native_frames = SS.StepFrames(color=self.d_rgb.data_ptr(), color_frame_stride=self.H * self.W * 3,
+                                           depth=self.d_depth_raw.data_ptr(), depth_frame_stride=self.H * self.W,
+                                           color_stride=self.W * 3, depth_stride=self.W)
+        self.native_tracking = SS.StepTracking(
+            proj_frames=self.d_pframes.data_ptr(), proj_points=self.d_ppoints.data_ptr(),
+            local_frames=self.d_lframes.data_ptr(), local_points=self.d_lpoints.data_ptr(),
+            assoc_frames1=self.d_afr1.data_ptr(), assoc_frames2=self.d_afr2.data_ptr(), map=self.d_map.data_ptr(),
+            boundary_xyz=self.d_bound.data_ptr(), max_proj_points=self.max_points,
+            max_local_points=self.max_local_points, max_map=self.n_map)
+        self.native_k = 0
+
+    def _step_native(self):
+        if self.pipelined and self.native_k == 0:
+            self.native.prime(self.native_frames)
+        self.native.run(self.native_frames, self.native_tracking)
+        if self.pipelined:
+            self._bind(self.native_k % 2)  # results() reads the set batch k's tail used
+        self.native_k += 1
+
     def _bind(self, j):
         for k, v in self.sets[j].items():
             setattr(self, k, v)
@@ -537,6 +596,8 @@ class HotPath:
         self.pose()
 
     def step(self):
+        if self.native is not None:
+            return self._step_native()
         if self.pipelined:
             return self._step_pipelined()
         # planes of step k may start once step k-1 is done with the plane buffers and this step's depth exists
@@ -608,6 +669,9 @@ class HotPath:
         return np.array([sp[f, :cnt[f]]["n_line"].sum() for f in range(self.B)], np.float64)
 
     def close(self):
+        if getattr(self, "native", None) is not None:
+            self.native.close()
+            self.native = None
         if self.n_lba:
             self.lba_pool.shutdown()
             self.lba_ex.close()

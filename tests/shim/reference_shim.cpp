@@ -10,6 +10,9 @@
 //   Optimizer::PoseOptimization                    src/Optimizer.cc:519-1152             (3)
 //   Optimizer::LocalBundleAdjustment               src/Optimizer.cc:1154-1977            (6)
 //   Tracking::GrabImageRGBD                        src/Tracking.cc:208-229               (7)
+//   Map::AssociatePlanesByBoundary                 src/Map.cc:196-359                    (8, f1)
+//   ORBmatcher::SearchByProjection (motion model)  src/ORBmatcher.cc:1328-1470, Tracking.cc:951-975 (9, f2)
+//   Frame/KeyFrame::ComputeBoW, ORBmatcher::SearchByBoW  src/Frame.cc:495-502, ORBmatcher.cc:159-288 (11, f4)
 // extern "C" entry points at the end let tests/test_gpu_shim.py drive them from flat arrays and compare with
 // the oracle.  TEST INFRASTRUCTURE: built by `make` into tests/shim/libreference_shim.so, never part of the
 // product library.
@@ -19,6 +22,7 @@
 #include <list>
 #include <map>
 #include <memory>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -78,6 +82,10 @@ class MapPoint {
    public:
     long unsigned int mnId = 0;
     cv::Mat mWorldPos{3, 1, cv::CV_32F};
+    cv::Mat mDescriptor{1, 32, cv::CV_8U};
+    int nObs = 0;  // kept by AddObservation / EraseObservation in the reference
+    cv::Mat GetDescriptor() const { return mDescriptor.clone(); }
+    int Observations() const { return nObs; }
     std::map<KeyFrame*, size_t, ById> mObservations;
     long unsigned int mnBALocalForKF = 0;
     bool mbBad = false;
@@ -88,10 +96,14 @@ class MapPoint {
     void EraseObservation(KeyFrame* pKF) { mObservations.erase(pKF); }
 };
 
+struct PointXYZ { float x, y, z; };
+struct BoundaryCloud { std::vector<PointXYZ> points; };  // pcl::PointCloud<PointT> stand-in
+
 class MapPlane {
    public:
     long unsigned int mnId = 0;
     cv::Mat mWorldPos{4, 1, cv::CV_32F};
+    BoundaryCloud mvBoundaryPoints;
     std::map<KeyFrame*, int, ById> mObservations, mVerObservations, mParObservations;
     long unsigned int mnBALocalForKF = 0;
     cv::Mat GetWorldPos() const { return mWorldPos.clone(); }
@@ -103,7 +115,11 @@ class KeyFrame {
     long unsigned int mnId = 0;
     cv::Mat mTcw{4, 4, cv::CV_32F};
     float fx = 0, fy = 0, cx = 0, cy = 0, mbf = 0;
+    int N = 0;
     std::vector<cv::KeyPoint> mvKeysUn;
+    cv::Mat mDescriptors;
+    std::map<unsigned int, double> mBowVec;                       // DBoW2::BowVector
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;   // DBoW2::FeatureVector
     std::vector<float> mvuRight;
     std::vector<float> mvInvLevelSigma2;
     std::vector<MapPoint*> mvpMapPoints;
@@ -145,8 +161,12 @@ class Frame {
     std::vector<bool> mvbOutlier;
     std::vector<MapPlane*> mvpMapPlanes, mvpParallelPlanes, mvpVerticalPlanes;
     std::vector<bool> mvbPlaneOutlier, mvbParPlaneOutlier, mvbVerPlaneOutlier;
+    bool mbNewPlane = false;
+    std::map<unsigned int, double> mBowVec;                       // DBoW2::BowVector
+    std::map<unsigned int, std::vector<unsigned int>> mFeatVec;   // DBoW2::FeatureVector
     cv::Mat mTcw{4, 4, cv::CV_32F};
     float fx = 0, fy = 0, cx = 0, cy = 0, mbf = 0;
+    ORBextractor* mpORBextractorLeft = nullptr;
 
     Frame() = default;
     // Frame::Frame(imGray, imDepth, timeStamp, extractor, voc, K, distCoef, bf, thDepth) (src/Frame.cc:130-197):
@@ -154,6 +174,7 @@ class Frame {
     // ComputePlanesFromOrganizedPointCloud (2) and GeneratePlanesFromBoundries (5).
     Frame(const cv::Mat& imGray, const cv::Mat& imDepth, ORBextractor* extractor, const CameraConfig& K) {
         spslam_ctx* ctx = extractor->mGpu;
+        mpORBextractorLeft = extractor;
         fx = K.fx; fy = K.fy; cx = K.cx; cy = K.cy; mbf = K.bf;
         (*extractor)(imGray, cv::Mat(), mvKeys, mDescriptors);
         N = (int)mvKeys.size();
@@ -224,6 +245,179 @@ class Frame {
         mvbVerPlaneOutlier.assign(mnPlaneNum, false);
     }
     void SetPose(const float* T) { std::memcpy(mTcw.data, T, 64); }
+    void ComputeBoW();
+};
+
+// ---------------------------------------------------------------------------------------------------- 11 (f4)
+// The vocabulary is loaded into the tracker's context once, where System loads ORBvoc.txt (src/System.cc:59-71).
+inline void LoadVocabulary(spslam_ctx* ctx, const std::string& text) {
+    check(ctx, spslam_bow_load_vocabulary(ctx, text.data(), text.size(), nullptr, nullptr, nullptr, nullptr),
+          "spslam_bow_load_vocabulary");
+}
+// Frame::ComputeBoW / KeyFrame::ComputeBoW (src/Frame.cc:495-502, src/KeyFrame.cc:64-72): transform(desc, mBowVec,
+// mFeatVec, 4)
+inline void ComputeBoW(spslam_ctx* ctx, const cv::Mat& desc, std::map<unsigned int, double>& bowVec,
+                       std::map<unsigned int, std::vector<unsigned int>>& featVec) {
+    if (!bowVec.empty()) return;
+    const int n = desc.rows;
+    std::vector<uint32_t> bw(std::max(n, 1)), fvn(std::max(n, 1));
+    std::vector<double> bv(std::max(n, 1));
+    std::vector<int32_t> fvs(n + 1), fvf(std::max(n, 1));
+    int nb = 0, nfv = 0;
+    check(ctx, spslam_bow_transform(ctx, desc.data, n, 4, bw.data(), bv.data(), &nb, fvn.data(), fvs.data(),
+                                    fvf.data(), &nfv),
+          "spslam_bow_transform");
+    for (int i = 0; i < nb; ++i) bowVec[bw[i]] = bv[i];
+    for (int j = 0; j < nfv; ++j) featVec[fvn[j]].assign(fvf.begin() + fvs[j], fvf.begin() + fvs[j + 1]);
+}
+inline void Frame::ComputeBoW() { ORB_SLAM2::ComputeBoW(mpORBextractorLeft->mGpu, mDescriptors, mBowVec, mFeatVec); }
+
+// ---------------------------------------------------------------------------------------------------- 9, 11
+class ORBmatcher {
+   public:
+    explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+
+    // SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th, bMono) (src/ORBmatcher.cc:1328-1470):
+    // the last frame's map points (mvpMapPoints[i] && !mvbOutlier[i], in i order) against the current frame's
+    // grid; the assignments go into CurrentFrame.mvpMapPoints
+    int SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, float th, bool bMono) const {
+        spslam_ctx* ctx = CurrentFrame.mpORBextractorLeft->mGpu;
+        std::vector<spslam_proj_point> pts;
+        std::vector<MapPoint*> src;
+        for (int i = 0; i < LastFrame.N; ++i) {
+            MapPoint* pMP = LastFrame.mvpMapPoints[i];
+            if (!pMP || LastFrame.mvbOutlier[i]) continue;
+            const cv::Mat x = pMP->GetWorldPos(), d = pMP->GetDescriptor();
+            spslam_proj_point p{};
+            for (int k = 0; k < 3; ++k) p.xw[k] = x.at<float>(k);
+            p.angle = LastFrame.mvKeysUn[i].angle;
+            p.octave = LastFrame.mvKeys[i].octave;
+            p.n_obs = pMP->Observations();
+            p.last_index = i;
+            p.id = (int)pMP->mnId;
+            std::memcpy(p.desc, d.data, 32);
+            pts.push_back(p);
+            src.push_back(pMP);
+        }
+        spslam_proj_frame fr{};
+        std::memcpy(fr.Tcw, CurrentFrame.mTcw.data, 64);
+        std::memcpy(fr.Tlw, LastFrame.mTcw.data, 64);
+        fr.n_points = (int)pts.size();
+        std::vector<int32_t> goff(1, 0), gidx;
+        for (const auto& cell : CurrentFrame.mGrid) {
+            for (size_t k : cell) gidx.push_back((int32_t)k);
+            goff.push_back((int32_t)gidx.size());
+        }
+        gidx.push_back(0);
+        const spslam_match_params prm{th, bMono ? 1 : 0, mbCheckOrientation ? 1 : 0, /*retry_below*/ 0};
+        std::vector<int32_t> match(std::max(CurrentFrame.N, 1));
+        int n = 0;
+        check(ctx, spslam_search_by_projection(ctx, &fr, pts.data(),
+                                               reinterpret_cast<const spslam_keypoint*>(CurrentFrame.mvKeysUn.data()),
+                                               CurrentFrame.mDescriptors.data, CurrentFrame.mvuRight.data(),
+                                               CurrentFrame.N, goff.data(), gidx.data(), &prm, match.data(), &n),
+              "spslam_search_by_projection");
+        for (int i = 0; i < CurrentFrame.N; ++i)
+            if (match[i] >= 0) CurrentFrame.mvpMapPoints[i] = src[match[i]];
+        return n;
+    }
+
+    // SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches) (src/ORBmatcher.cc:159-288)
+    int SearchByBoW(KeyFrame* pKF, Frame& F, std::vector<MapPoint*>& vpMapPointMatches) const {
+        spslam_ctx* ctx = F.mpORBextractorLeft->mGpu;
+        const std::vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
+        std::vector<uint8_t> has(std::max(pKF->N, 1));
+        for (int i = 0; i < pKF->N; ++i) has[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad();
+        std::vector<uint32_t> kn, fn;
+        std::vector<int32_t> ks, kf, fs, ff;
+        const int nk = flat(pKF->mFeatVec, kn, ks, kf), nf = flat(F.mFeatVec, fn, fs, ff);
+        const spslam_bow_params prm{mfNNratio, mbCheckOrientation ? 1 : 0};
+        std::vector<int32_t> match(std::max(F.N, 1));
+        int nmatches = 0;
+        check(ctx, spslam_search_by_bow(ctx, pKF->mDescriptors.data,
+                                        reinterpret_cast<const spslam_keypoint*>(pKF->mvKeysUn.data()), has.data(),
+                                        pKF->N, kn.data(), ks.data(), kf.data(), nk, F.mDescriptors.data,
+                                        reinterpret_cast<const spslam_keypoint*>(F.mvKeys.data()), F.N, fn.data(),
+                                        fs.data(), ff.data(), nf, &prm, match.data(), &nmatches),
+              "spslam_search_by_bow");
+        vpMapPointMatches = std::vector<MapPoint*>(F.N, static_cast<MapPoint*>(nullptr));
+        for (int i = 0; i < F.N; ++i)
+            if (match[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[match[i]];
+        return nmatches;
+    }
+
+    float mfNNratio;
+    bool mbCheckOrientation;
+
+   private:
+    // a FeatureVector (std::map: ascending node id) as the ABI's CSR; returns its node count
+    static int flat(const std::map<unsigned int, std::vector<unsigned int>>& fv, std::vector<uint32_t>& nodes,
+                    std::vector<int32_t>& start, std::vector<int32_t>& feats) {
+        for (const auto& kv : fv) {
+            nodes.push_back(kv.first);
+            start.push_back((int32_t)feats.size());
+            feats.insert(feats.end(), kv.second.begin(), kv.second.end());
+        }
+        start.push_back((int32_t)feats.size());
+        nodes.push_back(0);  // (non-empty buffers)
+        feats.push_back(0);
+        return (int)fv.size();
+    }
+};
+
+// ---------------------------------------------------------------------------------------------------- 8 (f1)
+class Map {
+   public:
+    std::set<MapPlane*, ById> mspMapPlanes;  // id order replaces the pointer order
+    float mfDisTh = 0, mfAngleTh = 0, mfVerTh = 0, mfParTh = 0;
+    spslam_ctx* mGpu = nullptr;
+
+    // Map::AssociatePlanesByBoundary(Frame& pF, bool out) (src/Map.cc:196-359): the map planes flattened in
+    // mnId order; pF's current associations handed in (the reference only overwrites them, :230-252)
+    void AssociatePlanesByBoundary(Frame& pF, bool /*out*/ = false) {
+        std::vector<spslam_map_plane> mp;
+        std::vector<float> bxyz;
+        std::vector<MapPlane*> byIndex;
+        std::map<unsigned long, int> indexById;
+        for (MapPlane* p : mspMapPlanes) {
+            const cv::Mat w = p->GetWorldPos();
+            indexById[p->mnId] = (int)mp.size();
+            byIndex.push_back(p);
+            mp.push_back({{w.at<float>(0), w.at<float>(1), w.at<float>(2), w.at<float>(3)}, (int)p->mnId,
+                          (int)(bxyz.size() / 3), (int)p->mvBoundaryPoints.points.size(), 0});
+            for (const PointXYZ& q : p->mvBoundaryPoints.points) {
+                bxyz.push_back(q.x);
+                bxyz.push_back(q.y);
+                bxyz.push_back(q.z);
+            }
+        }
+        spslam_assoc_frame f{};
+        std::memcpy(f.Tcw, pF.mTcw.data, 64);
+        f.n_map = (int)mp.size();
+        f.carry = 1;
+        const int n = pF.mnPlaneNum;
+        std::vector<int32_t> m(std::max(n, 1)), par(std::max(n, 1)), ver(std::max(n, 1));
+        std::vector<float> coefs(4 * std::max(n, 1));
+        auto idx = [&](MapPlane* p) { return p ? indexById.at(p->mnId) : -1; };
+        for (int i = 0; i < n; ++i) {
+            m[i] = idx(pF.mvpMapPlanes[i]);
+            par[i] = idx(pF.mvpParallelPlanes[i]);
+            ver[i] = idx(pF.mvpVerticalPlanes[i]);
+            for (int q = 0; q < 4; ++q) coefs[4 * i + q] = pF.mvPlaneCoefficients[i][q];
+        }
+        const spslam_assoc_params prm{mfDisTh, mfAngleTh, mfVerTh, mfParTh};
+        int newPlane = 0;
+        bxyz.resize(std::max<size_t>(bxyz.size(), 3));
+        check(mGpu, spslam_planes_associate(mGpu, &f, coefs.data(), n, mp.data(), (int)mp.size(), bxyz.data(),
+                                            (int)(bxyz.size() / 3), &prm, m.data(), par.data(), ver.data(), &newPlane),
+              "spslam_planes_associate");
+        for (int i = 0; i < n; ++i) {
+            pF.mvpMapPlanes[i] = m[i] < 0 ? nullptr : byIndex[m[i]];
+            pF.mvpParallelPlanes[i] = par[i] < 0 ? nullptr : byIndex[par[i]];
+            pF.mvpVerticalPlanes[i] = ver[i] < 0 ? nullptr : byIndex[ver[i]];
+        }
+        pF.mbNewPlane = newPlane != 0;
+    }
 };
 
 // ---------------------------------------------------------------------------------------------------- 7
@@ -652,6 +846,163 @@ int shim_local_ba(int n_kf, const spslam_lba_keyframe* kfs, int n_points, const 
             KeyFrame* f = obs_slot[o].first;
             pobs_erased[o] = f && f->mvpMapPoints[obs_slot[o].second] == nullptr;
         }
+    });
+}
+
+
+// Map::AssociatePlanesByBoundary (8) on a Frame with n_planes coefficients at pose Tcw against a map of n_map
+// planes (spslam_map_plane records: world, id, boundary range in bxyz); params: dis, angle, ver, par thresholds.
+// Outputs: map-plane array indices (-1 none) and mbNewPlane.
+int shim_associate_planes(const float* Tcw, const float* coefs, int n_planes, const spslam_map_plane* map, int n_map,
+                          const float* bxyz, const float* params, int32_t* match, int32_t* parallel,
+                          int32_t* vertical, int* new_plane) {
+    return guarded([&] {
+        spslam_orb_params p{1000, 1.2f, 8, 20, 7, 640, 480, 1};
+        spslam_ctx* ctx = nullptr;
+        check(nullptr, spslam_create(0, &p, &ctx), "spslam_create");
+        std::unique_ptr<spslam_ctx, void (*)(spslam_ctx*)> hold(ctx, spslam_destroy);
+        std::vector<std::unique_ptr<MapPlane>> planes;
+        Map M;
+        M.mGpu = ctx;
+        M.mfDisTh = params[0]; M.mfAngleTh = params[1]; M.mfVerTh = params[2]; M.mfParTh = params[3];
+        std::map<unsigned long, int> index;
+        for (int j = 0; j < n_map; ++j) {
+            planes.emplace_back(new MapPlane);
+            MapPlane* mp = planes.back().get();
+            mp->mnId = (unsigned long)map[j].id;
+            mp->SetWorldPos(map[j].world);
+            for (int k = 0; k < map[j].n_boundary; ++k) {
+                const float* q = bxyz + 3 * (map[j].boundary_offset + k);
+                mp->mvBoundaryPoints.points.push_back({q[0], q[1], q[2]});
+            }
+            M.mspMapPlanes.insert(mp);
+            index[mp->mnId] = j;
+        }
+        Frame F;
+        F.SetPose(Tcw);
+        F.mnPlaneNum = n_planes;
+        for (int i = 0; i < n_planes; ++i) F.mvPlaneCoefficients.push_back({coefs[4 * i], coefs[4 * i + 1],
+                                                                            coefs[4 * i + 2], coefs[4 * i + 3]});
+        F.mvpMapPlanes.assign(n_planes, nullptr);  // a new Frame (src/Frame.cc:199-213)
+        F.mvpParallelPlanes.assign(n_planes, nullptr);
+        F.mvpVerticalPlanes.assign(n_planes, nullptr);
+        M.AssociatePlanesByBoundary(F);
+        auto out = [&](MapPlane* mp) { return mp ? index.at(mp->mnId) : -1; };
+        for (int i = 0; i < n_planes; ++i) {
+            match[i] = out(F.mvpMapPlanes[i]);
+            parallel[i] = out(F.mvpParallelPlanes[i]);
+            vertical[i] = out(F.mvpVerticalPlanes[i]);
+        }
+        *new_plane = F.mbNewPlane ? 1 : 0;
+    });
+}
+
+// TrackWithMotionModel's matching (9; src/Tracking.cc:951-975): ORBmatcher(0.9, true), mvpMapPoints cleared,
+// SearchByProjection at th, again at 2 th below 20 matches.  The last frame: one keypoint per point record
+// (its map point, angle, octave; no outliers); the current frame: n_kp keypoints (mvKeysUn, descriptors,
+// mvuRight, mGrid as CSR); cam: fx fy cx cy bf width height (the context's frame geometry).  Output per current
+// keypoint: the index of its map point in `points`, -1 none; the returned nmatches.
+int shim_track_motion_model_matching(const spslam_proj_frame* fr, const spslam_proj_point* points, int n_points,
+                                     const cv::KeyPoint* keys_un, const uint8_t* desc, const float* uright, int n_kp,
+                                     const int32_t* grid_off, const int32_t* grid_idx, const float* cam, float th,
+                                     int32_t* match, int* nmatches) {
+    return guarded([&] {
+        ORBextractor ex(1000, 1.2f, 8, 20, 7, (int)cam[5], (int)cam[6]);
+        spslam_frame_params fp{cam[0], cam[1], cam[2], cam[3], {0, 0, 0, 0, 0}, cam[4], (int)cam[5], (int)cam[6]};
+        float bounds[4];
+        check(ex.mGpu, spslam_frame_configure(ex.mGpu, &fp, bounds, nullptr), "spslam_frame_configure");
+        std::vector<std::unique_ptr<MapPoint>> mps;
+        Frame Last, Cur;
+        Last.mpORBextractorLeft = Cur.mpORBextractorLeft = &ex;
+        Last.N = n_points;
+        Last.SetPose(fr->Tlw);
+        Last.mvKeys.resize(n_points);
+        Last.mvKeysUn.resize(n_points);
+        Last.mvbOutlier.assign(n_points, false);
+        for (int i = 0; i < n_points; ++i) {
+            mps.emplace_back(new MapPoint);
+            MapPoint* mp = mps.back().get();
+            mp->mnId = (unsigned long)points[i].id;
+            mp->SetWorldPos(points[i].xw);
+            std::memcpy(mp->mDescriptor.data, points[i].desc, 32);
+            mp->nObs = points[i].n_obs;
+            Last.mvpMapPoints.push_back(mp);
+            Last.mvKeysUn[i].angle = points[i].angle;
+            Last.mvKeys[i].octave = points[i].octave;
+        }
+        Cur.N = n_kp;
+        Cur.SetPose(fr->Tcw);  // mVelocity * mLastFrame.mTcw
+        Cur.mvKeysUn.assign(keys_un, keys_un + n_kp);
+        Cur.mDescriptors = cv::Mat(std::max(n_kp, 1), 32, cv::CV_8U);
+        if (n_kp) std::memcpy(Cur.mDescriptors.data, desc, (size_t)n_kp * 32);
+        Cur.mvuRight.assign(uright, uright + n_kp);
+        Cur.mGrid.assign(64 * 48, {});
+        for (int c = 0; c < 64 * 48; ++c) Cur.mGrid[c].assign(grid_idx + grid_off[c], grid_idx + grid_off[c + 1]);
+        ORBmatcher matcher(0.9f, true);
+        Cur.mvpMapPoints.assign(n_kp, nullptr);
+        int n = matcher.SearchByProjection(Cur, Last, th, false);
+        if (n < 20) {
+            Cur.mvpMapPoints.assign(n_kp, nullptr);
+            n = matcher.SearchByProjection(Cur, Last, 2 * th, false);
+        }
+        std::map<const MapPoint*, int> idx;
+        for (int i = 0; i < n_points; ++i) idx[mps[i].get()] = i;
+        for (int i = 0; i < n_kp; ++i) match[i] = Cur.mvpMapPoints[i] ? idx.at(Cur.mvpMapPoints[i]) : -1;
+        *nmatches = n;
+    });
+}
+
+// TrackReferenceKeyFrame's matching (11; src/Tracking.cc:797-802): the vocabulary into the context, ComputeBoW of
+// the keyframe and the frame, ORBmatcher(nn_ratio, check_ori).SearchByBoW(pKF, F, vpMapPointMatches).  Keyframe
+// feature i has a map point when has_mp[i].  Outputs: per frame feature the keyframe feature whose map point it
+// received (-1 none), nmatches, and the frame's BowVector / FeatureVector (ascending ids; fv_start CSR).
+int shim_bow_match(const char* vocab, size_t vocab_len, const uint8_t* kf_desc, const cv::KeyPoint* kf_keys_un,
+                   const uint8_t* has_mp, int kf_n, const uint8_t* f_desc, const cv::KeyPoint* f_keys, int f_n,
+                   float nn_ratio, int check_ori, int32_t* match, int* nmatches, uint32_t* bow_words,
+                   double* bow_values, int* n_bow, uint32_t* fv_nodes, int32_t* fv_start, int32_t* fv_features,
+                   int* n_fv) {
+    return guarded([&] {
+        ORBextractor ex(1000, 1.2f, 8, 20, 7, 640, 480);
+        LoadVocabulary(ex.mGpu, std::string(vocab, vocab_len));
+        std::vector<std::unique_ptr<MapPoint>> mps;
+        KeyFrame KF;
+        KF.N = kf_n;
+        KF.mvKeysUn.assign(kf_keys_un, kf_keys_un + kf_n);
+        KF.mDescriptors = cv::Mat(kf_n, 32, cv::CV_8U);
+        if (kf_n) std::memcpy(KF.mDescriptors.data, kf_desc, (size_t)kf_n * 32);
+        KF.mvpMapPoints.assign(kf_n, nullptr);
+        for (int i = 0; i < kf_n; ++i)
+            if (has_mp[i]) {
+                mps.emplace_back(new MapPoint);
+                mps.back()->mnId = (unsigned long)i;
+                KF.mvpMapPoints[i] = mps.back().get();
+            }
+        ComputeBoW(ex.mGpu, KF.mDescriptors, KF.mBowVec, KF.mFeatVec);  // KeyFrame::ComputeBoW
+        Frame F;
+        F.mpORBextractorLeft = &ex;
+        F.N = f_n;
+        F.mvKeys.assign(f_keys, f_keys + f_n);
+        F.mDescriptors = cv::Mat(f_n, 32, cv::CV_8U);
+        if (f_n) std::memcpy(F.mDescriptors.data, f_desc, (size_t)f_n * 32);
+        F.ComputeBoW();
+        ORBmatcher matcher(nn_ratio, check_ori != 0);
+        std::vector<MapPoint*> vpMapPointMatches;
+        *nmatches = matcher.SearchByBoW(&KF, F, vpMapPointMatches);
+        for (int i = 0; i < f_n; ++i) match[i] = vpMapPointMatches[i] ? (int32_t)vpMapPointMatches[i]->mnId : -1;
+        int b = 0;
+        for (const auto& kv : F.mBowVec) {
+            bow_words[b] = kv.first;
+            bow_values[b++] = kv.second;
+        }
+        *n_bow = b;
+        int j = 0, o = 0;
+        for (const auto& kv : F.mFeatVec) {
+            fv_nodes[j] = kv.first;
+            fv_start[j++] = o;
+            for (unsigned int q : kv.second) fv_features[o++] = (int32_t)q;
+        }
+        fv_start[j] = o;
+        *n_fv = j;
     });
 }
 

@@ -229,6 +229,34 @@ def test_pipelined_steps_match_serial(run):
     assert not np.array_equal(out[True][0]["pose2"][0]["Tcw"], out[True][1]["pose2"][0]["Tcw"])
 
 
+def test_native_step_matches_python():
+    """The whole step as one C-ABI call (spslam_step_run, csrc/spslam_step.cpp: the library's own streams and
+    events, Python only makes the call) gives the Python-orchestrated step's results bit for bit, pipelined and
+    serial, step by step."""
+    import pipeline
+    steps = 3
+    for pipelined in (True, False):
+        out = {}
+        for native in (False, True):
+            hp = pipeline.HotPath(8, unique_frames=8, pipelined=pipelined, native=native, **pipeline.CONFIGS["c2"])
+            try:
+                out[native] = []
+                for _ in range(steps):
+                    hp.step()
+                    out[native].append(hp.results())
+            finally:
+                hp.close()
+        for k in range(steps):
+            py, na = out[False][k], out[True][k]
+            for key in ("kp_counts", "plane_counts", "supposed_counts", "match", "nmatches", "local_match",
+                        "local_nmatches", "assoc", "new_plane"):
+                assert np.array_equal(na[key], py[key]), (pipelined, k, key)
+            assert na["kps"].tobytes() == py["kps"].tobytes(), (pipelined, k)
+            for key in ("pose1", "pose2"):
+                assert na[key].tobytes() == py[key].tobytes(), (pipelined, k, key)
+        assert out[True][-1]["nmatches"].sum() > 0
+
+
 def test_c3_local_mapping_beside_tracking():
     """C3: the step's LocalBundleAdjustments run on the LocalMapping stream and context while the tracking chain
     runs (pipelined): every local map's result matches the oracle (LM iterations and outlier flags identical,

@@ -12,7 +12,13 @@ reference's call sites, over the C ABI) against the CPU oracle.
     against an independent Python restatement of Optimizer.cc:1156-1298, the GPU result against the oracle
     on that problem (1e-4 relative for poses, planes and every point with two or more inlier observations;
     identical iteration counts and outlier flags), and the applied result (SetPose / SetWorldPos /
-    EraseMapPointMatch) against the optimizer's outputs.
+    EraseMapPointMatch) against the optimizer's outputs;
+  * Map::AssociatePlanesByBoundary (f1) on Frame / MapPlane objects: match / parallel / vertical and
+    mbNewPlane identical to the oracle;
+  * TrackWithMotionModel's SearchByProjection (f2, th then 2 th below 20 matches) on Frame / MapPoint objects:
+    mvpMapPoints and nmatches identical;
+  * KeyFrame / Frame::ComputeBoW and SearchByBoW (f4) with the vocabulary loaded into the context: the frame's
+    BowVector / FeatureVector and the matches identical.
 """
 import ctypes
 import pathlib
@@ -292,3 +298,91 @@ def test_shim_local_bundle_adjustment(shim):
     got = {(j, int(pobs[o]["kf"])) for j, p in enumerate(pts)
            for o in range(p["obs_offset"], p["obs_offset"] + p["n_obs"]) if erased[o]}
     assert got == flagged and len(flagged) > 0
+
+
+def test_shim_associate_planes(shim):
+    import oracle_assoc as OA
+    import synth
+    rng = np.random.default_rng(23)
+    n = 0
+    for seq in range(3):
+        sc = synth.Scene(seq, n_boxes=1 + seq)
+        mp, bxyz = synth.map_planes(sc, rng)
+        m = np.zeros(len(mp["world"]), OA.MAP_PLANE_DTYPE)
+        for k, v in mp.items():
+            m[k] = v
+        b = np.ascontiguousarray(bxyz, np.float32).reshape(-1, 3)
+        for fr in range(0, 120, 11):
+            T, c, _ = synth.assoc_frame_planes(sc, fr, rng, n_faces=4 + fr % 6, n_random=fr % 4)
+            o = OA.associate(T, c, m, b)
+            T = np.ascontiguousarray(T, np.float32).reshape(16)
+            c = np.ascontiguousarray(c, np.float32).reshape(-1, 4)
+            k = len(c)
+            out = [np.full(max(k, 1), -9, np.int32) for _ in range(3)]
+            newp = ctypes.c_int(-1)
+            _call(shim, "shim_associate_planes", _p(T), _p(c), k, _p(m), len(m), _p(b), _p(OA.ASSOC_PARAMS),
+                  _p(out[0]), _p(out[1]), _p(out[2]), ctypes.byref(newp))
+            for key, g in zip(("match", "parallel", "vertical"), out):
+                assert np.array_equal(g[:k], o[key]), (seq, fr, key)
+            assert bool(newp.value) == o["new_plane"], (seq, fr)
+            n += 1
+    assert n > 25
+
+
+def test_shim_motion_model_matching(shim):
+    import oracle_match as OM
+    import synth
+    from test_oracle_match import make_pairs
+    K = synth.TUM3
+    cam = np.array([K["fx"], K["fy"], K["cx"], K["cy"], K["bf"], 640, 480], np.float32)
+    total = 0
+    for q in make_pairs(((0, 10, 12), (1, 30, 31), (2, 50, 53), (3, 5, 9)), seed=17):
+        mo, nmo, _ = OM.search_by_projection(q["fr"], q["P"], q["kun"], q["desc"], q["ur"], q["go"], q["gi"],
+                                             q["geo"], params=(15.0, 0, 1, 20))
+        fr = np.ascontiguousarray(q["fr"], OM.PROJ_FRAME_DTYPE).reshape(1)
+        P = np.ascontiguousarray(q["P"], OM.PROJ_POINT_DTYPE)
+        kun = np.ascontiguousarray(q["kun"])
+        n = len(kun)
+        match = np.full(max(n, 1), -9, np.int32)
+        nm = ctypes.c_int(-1)
+        _call(shim, "shim_track_motion_model_matching", _p(fr), _p(P), len(P), _p(kun),
+              _p(np.ascontiguousarray(q["desc"])), _p(np.ascontiguousarray(q["ur"], np.float32)), n,
+              _p(np.ascontiguousarray(q["go"], np.int32)), _p(np.ascontiguousarray(q["gi"], np.int32)), _p(cam),
+              ctypes.c_float(15.0), _p(match), ctypes.byref(nm))
+        assert nm.value == nmo
+        assert np.array_equal(match[:n], mo), np.nonzero(match[:n] != mo)[0][:10]
+        total += nmo
+    assert total > 400
+
+
+def test_shim_bow_match(shim):
+    import bow_common as BC
+    import oracle_bow
+    text = BC.vocab_text()
+    ov = oracle_bow.Vocabulary(text)
+    feats = BC.frames(3)
+    rng = np.random.default_rng(5)
+    total = 0
+    for a, b, nn, ori in ((0, 1, 0.7, 1), (1, 2, 0.7, 1), (0, 2, 0.75, 0)):
+        (kk, kd), (fk, fd) = feats[a], feats[b]
+        has = (rng.random(len(kd)) < 0.85).astype(np.uint8)
+        ft = ov.transform(fd)
+        om, on = oracle_bow.search_by_bow(kd, kk["angle"], has, ov.transform(kd), fd, fk["angle"], ft, nn, bool(ori))
+        nf = len(fd)
+        match = np.full(max(nf, 1), -9, np.int32)
+        words, values = np.zeros(nf, np.uint32), np.zeros(nf, np.float64)
+        nodes, start, feat = np.zeros(nf, np.uint32), np.zeros(nf + 1, np.int32), np.zeros(nf, np.int32)
+        nm, nb, nfv = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        buf = ctypes.create_string_buffer(text, len(text))
+        _call(shim, "shim_bow_match", buf, ctypes.c_size_t(len(text)), _p(np.ascontiguousarray(kd)),
+              _p(np.ascontiguousarray(kk)), _p(has), len(kd), _p(np.ascontiguousarray(fd)),
+              _p(np.ascontiguousarray(fk)), nf, ctypes.c_float(nn), ori, _p(match), ctypes.byref(nm), _p(words),
+              _p(values), ctypes.byref(nb), _p(nodes), _p(start), _p(feat), ctypes.byref(nfv))
+        assert nm.value == on and np.array_equal(match[:nf], om), (a, b)
+        assert words[:nb.value].tobytes() == np.asarray(ft["words"], np.uint32).tobytes()
+        assert values[:nb.value].tobytes() == np.asarray(ft["values"], np.float64).tobytes()
+        assert nodes[:nfv.value].tobytes() == np.asarray(ft["nodes"], np.uint32).tobytes()
+        assert start[:nfv.value + 1].tobytes() == np.asarray(ft["start"], np.int32).tobytes()
+        assert feat[:start[nfv.value]].tobytes() == np.asarray(ft["features"], np.int32).tobytes()
+        total += on
+    assert total > 150
