@@ -38,9 +38,9 @@ constexpr int kT = kLbgThreads, kW = kT / 64;
 constexpr int kMaxK = kLbaMaxKeyframes;
 constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
-constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised with L in LDS
-constexpr int kSchurLm = 16;            // Schur phase: landmarks per staged chunk
-constexpr int kSchurBlk = 192;          //   and Hpl blocks per chunk (two staging buffers + one BDinv buffer)
+constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised in LDS (L, S packed: 133 KB)
+constexpr int kSchurLm = 64;            // Schur phase: landmarks per staged chunk (one bit each in a 64-bit mask)
+constexpr int kSchurBlk = 412;          //   and Hpl blocks per chunk (the staging buffer, 16 doubles a thread, + BDinv)
 
 struct Sh {
     double red[kW][4];
@@ -55,7 +55,7 @@ struct Sh {
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
     double lambda, ni, currentChi, iniChi, tempChi, scale;
     long long ph[8], tlast, tB;  // diagnostics: wall_clock64 ticks per phase (result phase_us[1..7])
-    long long dg[8];             // SPSLAM_LBG_DIAG sub-phase ticks
+    long long dg[10];            // SPSLAM_LBG_DIAG sub-phase ticks
 };
 // thread 0 charges the time since the previous mark to phase k (called right after a barrier)
 #define LBG_MARK(k)                                  \
@@ -79,10 +79,11 @@ struct G {
     const spslam_lba_plane GL* pl;
     const spslam_lba_point_obs GL* pobs;
     const spslam_lba_plane_obs GL* plobs;
-    gdouble *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *echi, *sc, *terms, *Hll, *bl, *Dinv, *db, *blkB, *blkBD, *Hps,
+    gdouble *pose, *pose_b, *X, *X_b, *P, *P_b, *err, *echi, *sc, *terms, *Hll, *bl, *Dinv, *db, *blkB, *Hps,
         *S, *bs, *x, *Ld;
     gint *e_lm, *e_kf, *e_type, *e_level, *e_src, *e_blk, *lm_boff, *lm_nb, *lm_sorted, *lm_hidx, *hidx_lm, *lmh_blk,
-        *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W, *sch, *sch_kb;
+        *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W, *sch, *sch_kb,
+        *eseg;  // per edge: {RI, landmark hidx, segment end, first block | segment start << 30}
     guint64 *lmh_mask, *lm_amask, *Lbits, *Abits;
 };
 
@@ -110,14 +111,14 @@ __device__ G make_g(const LbgBatch& b, int p) {
     auto I = [&](size_t o) { return (int GL*)(base + o); };
     g.pose = D(Ly.pose); g.pose_b = D(Ly.pose_b); g.X = D(Ly.X); g.X_b = D(Ly.X_b); g.P = D(Ly.P); g.P_b = D(Ly.P_b);
     g.err = D(Ly.err); g.echi = D(Ly.echi); g.sc = D(Ly.sc); g.terms = D(Ly.terms); g.Hll = D(Ly.Hll);
-    g.bl = D(Ly.bl); g.Dinv = D(Ly.Dinv); g.db = D(Ly.db); g.blkB = D(Ly.blkB); g.blkBD = D(Ly.blkBD);
+    g.bl = D(Ly.bl); g.Dinv = D(Ly.Dinv); g.db = D(Ly.db); g.blkB = D(Ly.blkB);
     g.Hps = D(Ly.Hps); g.S = D(Ly.S); g.bs = D(Ly.bs); g.x = D(Ly.x); g.Ld = D(Ly.Ld);
     g.e_lm = I(Ly.e_lm); g.e_kf = I(Ly.e_kf); g.e_type = I(Ly.e_type); g.e_level = I(Ly.e_level);
     g.e_src = I(Ly.e_src); g.e_blk = I(Ly.e_blk); g.lm_boff = I(Ly.lm_boff); g.lm_nb = I(Ly.lm_nb);
     g.lm_sorted = I(Ly.lm_sorted); g.lm_hidx = I(Ly.lm_hidx); g.hidx_lm = I(Ly.hidx_lm); g.lmh_blk = I(Ly.lmh_blk);
     g.pe_off = I(Ly.pe_off); g.pe_idx = I(Ly.pe_idx); g.Pinv = I(Ly.Pinv); g.Pm = I(Ly.Pm); g.parent = I(Ly.parent);
     g.rs_off = I(Ly.rs_off); g.rs_idx = I(Ly.rs_idx); g.amd_Ci = I(Ly.amd_Ci); g.amd_W = I(Ly.amd_W);
-    g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb);
+    g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb); g.eseg = I(Ly.eseg);
     g.lmh_mask = (uint64_t GL*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t GL*)(base + Ly.lm_amask);
     g.Lbits = (uint64_t GL*)(base + Ly.Lbits); g.Abits = (uint64_t GL*)(base + Ly.Abits);
     return g;
@@ -181,11 +182,18 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 // value of entry i of a vector spread over the wave (entry 64 m + lane in register m)
 template <int kC>
 __device__ __forceinline__ double pick(const double (&v)[kC], int i) {
-    double r = 0.0;
+    double r = rl(v[0], i & 63);  // (wave-uniform selects, no branches)
 #pragma unroll
-    for (int m = 0; m < kC; m++)
-        if ((i >> 6) == m) r = rl(v[m], i & 63);
+    for (int m = 1; m < kC; m++) {
+        const double q = rl(v[m], i & 63);
+        r = (i >> 6) == m ? q : r;
+    }
     return r;
+}
+__device__ __forceinline__ int4 ld_i4(const gint* p) {  // one 16-byte load (p 16-byte aligned)
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i v = *(const v4i GL*)p;
+    return make_int4(v.x, v.y, v.z, v.w);
 }
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -776,11 +784,18 @@ __device__ __noinline__ void structure() {
     for (int l = t; l < g.L; l += kT) {
         const int h = g.lm_hidx[l];
         const uint64_t mask = h >= 0 ? g.lmh_mask[h] : 0;
-        for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
+        const int b0 = g.lm_boff[l], e1 = b0 + g.lm_nb[l], kb = h >= 0 ? g.lmh_blk[h] : 0;
+        for (int e = b0; e < e1; e++) {
             int eb = -1;
             const int ph = s.hidx[g.e_kf[e]];
-            if (h >= 0 && g.e_level[e] == 0 && ph >= 0) eb = g.lmh_blk[h] + __popcll(mask & ((1ull << ph) - 1ull));
+            const bool on = g.e_level[e] == 0;
+            if (h >= 0 && on && ph >= 0) eb = kb + __popcll(mask & ((1ull << ph) - 1ull));
             g.e_blk[e] = eb;
+            // build_system's row record: RI (the edge's Hpl block, -1 none, -2 inactive), the landmark's segment
+            g.eseg[4 * e] = on ? eb : -2;
+            g.eseg[4 * e + 1] = h;
+            g.eseg[4 * e + 2] = e1;
+            g.eseg[4 * e + 3] = kb | (e == b0 ? 1 << 30 : 0);
         }
         if (h >= 0) {
             uint64_t am = g.lm_amask[l];
@@ -894,6 +909,7 @@ __device__ __noinline__ void structure() {
             }
             if (lane == 0) g.parent[j] = par;  // (each lane reads and writes its own word of acc only)
         }
+        if (lane == 0) g.Lbits[n * kNW] = 0;  // the factorisation's masked-step structure word
     }
     __syncthreads();
     // each row k of L: its pattern {i : k in struct L(:, i)} in factorize_preordered's order -- ap's column k
@@ -1017,6 +1033,33 @@ __device__ __forceinline__ double ordered_sum(const PD* v, int n32) {
     return acc;
 }
 
+// the ordered sums of a computeActiveErrors (activeRobustChi2: the edges' chi2 in edge order) and, for a trial
+// (nS > 0), of its scale (x . (lambda x + b), entry order): the operands staged in LDS by the whole workgroup
+// (coalesced), then one lane per sum -- the dependent add chains read LDS instead of global memory.  nS == 0:
+// currentChi, else tempChi and scale.
+__device__ __noinline__ void sums_staged(int nE, int nS) {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    const int t = threadIdx.x;
+    double* V = (double*)lbg_dyn;
+    if ((size_t)(nE + nS) * 8 <= (size_t)kDyn) {
+        for (int i = t; i < nE; i += kT) V[i] = g.echi[i];
+        for (int i = t; i < nS; i += kT) V[nE + i] = g.sc[i];
+        __syncthreads();
+        if (t == 0) {
+            const double c = ordered_sum(V, nE);
+            if (nS > 0) s.tempChi = c; else s.currentChi = c;
+        }
+        if (t == 64 && nS > 0) s.scale = ordered_sum(V + nE, nS);
+    } else {
+        if (t == 0) {
+            const double c = ordered_sum(g.echi, nE);
+            if (nS > 0) s.tempChi = c; else s.currentChi = c;
+        }
+        if (t == 64 && nS > 0) s.scale = ordered_sum(g.sc, nS);
+    }
+}
+
 // ---------------------------------------------------------------- per iteration: quadratic forms and sums
 // BlockSolver::buildSystem in chunks of kCh consecutive edges: (A) every edge's quadratic-form terms into LDS rows
 // (point edges on thread pairs -- both evaluate the Jacobians, the even thread the landmark side, the odd one the
@@ -1097,64 +1140,65 @@ __device__ __forceinline__ void terms_pose(const EdgeW& w, const double (&B)[3][
     }
 }
 
-// plane / parallel / vertical edge pe: numeric Jacobians (base_binary_edge.hpp:130-205) on one wave -- evaluation
-// q < 6: plane perturbed by +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose exp(+-1e-9 e_d) * T,
-// d = (q - 6) >> 1; evaluation q on the lane pair (2q, 2q + 1) -- the terms into row `row` from lane 0
-__device__ __forceinline__ void plane_edge_rows(const G& g, const Sh& s, const LbaConsts& C, int pe, int row,
-                                                double* TL, double* TP, double* TB, uint64_t* pm) {
-    const int lane = threadIdx.x & 63;
-    const bool robust = s.robust;
-    const int ty = g.e_type[pe], dim = edge_dim(ty), lm = g.e_lm[pe];
-    const int ph = s.hidx[g.e_kf[pe]];
-    const bool pfree = ph >= 0;
-    const SE3 T0 = load_pose(g.pose + 7 * g.e_kf[pe]);
-    auto pp = g.P + 4 * (lm - g.Np);
-    const P4 P0{{pp[0], pp[1], pp[2], pp[3]}};
-    const P4 meas = plane_from_f(g.plobs[g.e_src[pe]].meas);
+// plane / parallel / vertical edges: numeric Jacobians (base_binary_edge.hpp:130-205) into g.terms (A 3x3, then
+// B 3x6, per edge), kPJ edges at a time: one lane pair per (edge, evaluation q) -- q < 6: plane perturbed by
+// +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1 (free poses
+// only) -- the errors into LDS, then one thread per Jacobian entry: (e(+) - e(-)) / 2e-9
+constexpr int kPJ = 128;
+__device__ __noinline__ void plane_jacobians() {
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
+    double* EV = (double*)lbg_dyn;  // [kPJ][18][3]
+    const int t = threadIdx.x, pr = t >> 1;
+    const bool half = (t & 1) != 0;
     const double delta = 1e-9, scalar = 1.0 / (2 * delta);
-    double ev[3] = {0, 0, 0};
-    const int q = lane >> 1;
-    if (q < 18 && (q < 6 || pfree)) {
-        const double sgn = (q & 1) ? -delta : delta;
-        SE3 T = T0;
-        P4 P = P0;
-        if (q < 6) {
-            double add[3] = {0, 0, 0};
-            add[q >> 1] = sgn;
-            p_oplus(P, add);
-        } else {
-            double add[6] = {0, 0, 0, 0, 0, 0};
-            add[(q - 6) >> 1] = sgn;
-            T = se3_mul(se3_exp(add), T0);
+    __syncthreads();  // the previous phase's LDS use is over
+    for (int e0 = g.Ep; e0 < g.E; e0 += kPJ) {
+        const int cnt = min(kPJ, g.E - e0);
+        for (int task = pr; task < cnt * 18; task += kT / 2) {  // (both lanes of a pair: the same task)
+            const int le = task / 18, q = task - 18 * le, pe = e0 + le;
+            if (g.e_level[pe] != 0) continue;
+            const bool pfree = s.hidx[g.e_kf[pe]] >= 0;
+            if (q >= 6 && !pfree) continue;
+            const int ty = g.e_type[pe], lm = g.e_lm[pe];
+            SE3 T = load_pose(g.pose + 7 * g.e_kf[pe]);
+            auto pp = g.P + 4 * (lm - g.Np);
+            P4 P{{pp[0], pp[1], pp[2], pp[3]}};
+            const P4 meas = plane_from_f(g.plobs[g.e_src[pe]].meas);
+            const double sgn = (q & 1) ? -delta : delta;
+            if (q < 6) {
+                double add[3] = {0, 0, 0};
+                add[q >> 1] = sgn;
+                p_oplus(P, add);
+            } else {
+                double add[6] = {0, 0, 0, 0, 0, 0};
+                add[(q - 6) >> 1] = sgn;
+                T = se3_mul(se3_exp(add), T);
+            }
+            const E3 r = plane_error_pair(ty - 2, T, P, meas, half);
+            if (!half) {
+                double* o = EV + 3 * (18 * le + q);
+                o[0] = r.e0; o[1] = r.e1; o[2] = r.e2;
+            }
         }
-        const E3 r = plane_error_pair(ty - 2, T, P, meas, (lane & 1) != 0);
-        ev[0] = r.e0; ev[1] = r.e1; ev[2] = r.e2;
-    }
-    double A[3][3], B[3][6];
-#pragma unroll
-    for (int d = 0; d < 3; d++)
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const double ep = __shfl(ev[i], 2 * (2 * d)), em = __shfl(ev[i], 2 * (2 * d + 1));
-            A[i][d] = i < dim ? scalar * (ep - em) : 0.0;
+        __syncthreads();
+        for (int i = t; i < cnt * 27; i += kT) {
+            const int le = i / 27, j = i - 27 * le, pe = e0 + le;
+            if (g.e_level[pe] != 0) continue;
+            const int dim = edge_dim(g.e_type[pe]);
+            const bool pfree = s.hidx[g.e_kf[pe]] >= 0;
+            const double* ev = EV + 54 * le;
+            double v;
+            if (j < 9) {  // A[ii][d]: the plane's evaluations 2d, 2d + 1
+                const int ii = j / 3, d = j - 3 * ii;
+                v = ii < dim ? scalar * (ev[3 * (2 * d) + ii] - ev[3 * (2 * d + 1) + ii]) : 0.0;
+            } else {      // B[ii][d]: the pose's evaluations 6 + 2d, 7 + 2d
+                const int ii = (j - 9) / 6, d = (j - 9) - 6 * ii;
+                v = pfree && ii < dim ? scalar * (ev[3 * (6 + 2 * d) + ii] - ev[3 * (7 + 2 * d) + ii]) : 0.0;
+            }
+            g.terms[27 * (size_t)pe + j] = v;
         }
-#pragma unroll
-    for (int d = 0; d < 6; d++)
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            const double ep = __shfl(ev[i], 2 * (6 + 2 * d)), em = __shfl(ev[i], 2 * (7 + 2 * d));
-            B[i][d] = pfree && i < dim ? scalar * (ep - em) : 0.0;
-        }
-    if (lane == 0) {
-        double info[3], err[3];
-        info_of(g, C, pe, ty, info);
-        for (int i = 0; i < 3; i++) err[i] = g.err[3 * pe + i];
-        const EdgeW w = edge_weights(C, robust, ty, err, info);
-        terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
-        if (pfree) {
-            terms_pose(w, B, TP + kSP * row);
-            atomicOr((unsigned long long*)&pm[ph * 4 + (row >> 6)], 1ull << (row & 63));
-        }
+        __syncthreads();
     }
 }
 
@@ -1181,42 +1225,55 @@ __device__ __noinline__ void build_system() {
         task[k] = t + k * kT < 27 * np ? t + k * kT : -1;
     }
     double mx = 0.0;
+    if (g.E > g.Ep) plane_jacobians();
+    // row t's record (structure's eseg) of the next chunk: loaded during the previous chunk's phase (B)
+    int4 sgn = make_int4(-2, -1, 0, 0);
+    if (t < g.E) sgn = ld_i4(g.eseg + 4 * t);
     for (int c0 = 0; c0 < g.E; c0 += kCh) {
         const int cnt = min(kCh, g.E - c0);
+        const int4 sg = sgn;
         for (int i = t; i < 4 * np; i += kT) pm[i] = 0;
         // this thread's landmark segment (row t starts one when it is the landmark's first edge or the chunk's
-        // first row): its records load here and are consumed after phase (A)
-        int own_l = -1, own_b0 = 0, own_e1 = 0, own_h = -1, own_kb = 0;
+        // first row): its records are consumed after phase (A)
+        int own_h = -1, own_e1 = 0, own_kb = 0;
         double H[9], bv[3];
         uint64_t touched = 0;
         if (t < cnt) {
-            const int e = c0 + t;
-            RI[t] = g.e_level[e] == 0 ? g.e_blk[e] : -2;
-            const int l = g.e_lm[e];
-            own_b0 = g.lm_boff[l];
-            own_e1 = own_b0 + g.lm_nb[l];
-            own_h = g.lm_hidx[l];
-            if ((e == own_b0 || t == 0) && own_h >= 0) {
-                own_l = l;
-                own_kb = g.lmh_blk[own_h];
-                const bool cont = e > own_b0;  // continuing a landmark of the previous chunk
+            RI[t] = sg.x;
+            const bool first = (sg.w >> 30) & 1;
+            if ((first || t == 0) && sg.y >= 0) {
+                own_h = sg.y;
+                own_e1 = sg.z;
+                own_kb = sg.w & ((1 << 30) - 1);
+                const bool cont = !first;  // continuing a landmark of the previous chunk
 #pragma unroll
                 for (int j = 0; j < 9; j++) H[j] = cont ? g.Hll[9 * own_h + j] : 0.0;
 #pragma unroll
                 for (int j = 0; j < 3; j++) bv[j] = cont ? g.bl[3 * own_h + j] : 0.0;
-                touched = cont ? g.lm_amask[l] : 0ull;  // (lm_amask is free after the structure phase)
+                touched = cont ? g.lm_amask[own_h] : 0ull;  // (lm_amask is free after the structure phase)
             }
         }
         __syncthreads();
-        // (A) point edges on thread pairs
+        // (A) edges on thread pairs (the plane edges' Jacobians from plane_jacobians)
         {
             const int row = t >> 1, e = c0 + row;
-            if (row < cnt && e < g.Ep && g.e_level[e] == 0) {
+            if (row < cnt && g.e_level[e] == 0) {
                 const int ty = g.e_type[e];
                 const int ph = s.hidx[g.e_kf[e]];
                 const bool pfree = ph >= 0;
                 double A[3][3], B[3][6], info[3], err[3];
-                point_jacobians(g, e, ty, A, B);
+                if (e < g.Ep) {
+                    point_jacobians(g, e, ty, A, B);
+                } else {
+                    auto J = g.terms + 27 * (size_t)e;
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+#pragma unroll
+                        for (int d = 0; d < 3; d++) A[i][d] = J[3 * i + d];
+#pragma unroll
+                        for (int d = 0; d < 6; d++) B[i][d] = J[9 + 6 * i + d];
+                    }
+                }
                 info_of(g, C, e, ty, info);
                 for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
                 const EdgeW w = edge_weights(C, robust, ty, err, info);
@@ -1228,15 +1285,17 @@ __device__ __noinline__ void build_system() {
                 }
             }
         }
-        // plane edges of the chunk, one wave each
-        for (int e = max(c0, g.Ep) + wv; e < c0 + cnt; e += kW)
-            if (g.e_level[e] == 0) plane_edge_rows(g, s, C, e, e - c0, TL, TP, TB, pm);  // wave-uniform
         __syncthreads();
         const long long tb1 = wall_clock64();
         if (c0 + cnt > g.Ep) tP += tb1 - tb0; else tA += tb1 - tb0;
-        // (B) landmark segments: the thread of the segment's first edge sums it in edge order
-        if (own_l >= 0) {
+        // (B) landmark segments: the thread of the segment's first edge sums it in edge order.  A block's first
+        // term is stored (0 + term); a later term of the same (landmark, pose) block -- plane landmarks, whose
+        // plane / parallel / vertical edges share a keyframe -- is added by the second loop, in edge order.  (One
+        // loop with both would wait for every earlier store at each edge: one vector-memory counter on gfx950.)
+        if (own_h >= 0) {
             const int e = c0 + t, e_end = min(own_e1, c0 + cnt);
+            const uint64_t touched0 = touched;  // blocks stored in an earlier chunk (a continuing segment)
+            bool again = false;
             for (int e2 = e; e2 < e_end; e2++) {
                 const int bk = RI[e2 - c0];
                 if (bk == -2) continue;
@@ -1246,25 +1305,47 @@ __device__ __noinline__ void build_system() {
 #pragma unroll
                 for (int j = 0; j < 3; j++) bv[j] += r[9 + j];
                 if (bk >= 0) {
-                    const double* rb = TB + kSB * (e2 - c0);
-                    auto dst = g.blkB + (size_t)18 * bk;
                     const uint64_t bit = 1ull << (bk - own_kb);
-                    if (touched & bit) {
-#pragma unroll
-                        for (int j = 0; j < 18; j++) dst[j] += rb[j];
-                    } else {
+                    if (!(touched & bit)) {
+                        const double* rb = TB + kSB * (e2 - c0);
+                        auto dst = g.blkB + (size_t)18 * bk;
 #pragma unroll
                         for (int j = 0; j < 18; j++) dst[j] = 0.0 + rb[j];
+                        touched |= bit;
+                    } else {
+                        again = true;
                     }
-                    touched |= bit;
+                }
+            }
+            if (again) {  // the repeated blocks' terms, in edge order (rare: plane landmarks)
+                uint64_t seen = 0;
+                for (int e2 = e; e2 < e_end; e2++) {
+                    const int bk = RI[e2 - c0];
+                    if (bk < 0) continue;
+                    const uint64_t bit = 1ull << (bk - own_kb);
+                    // a block's first occurrence in this chunk, unless stored in an earlier chunk, was the plain
+                    // store of the loop above; every other occurrence is an addition
+                    const bool stored_here = !(touched0 & bit) && !(seen & bit);
+                    seen |= bit;
+                    if (stored_here) continue;
+                    const double* rb = TB + kSB * (e2 - c0);
+                    auto dst = g.blkB + (size_t)18 * bk;
+#pragma unroll
+                    for (int j = 0; j < 18; j++) dst[j] += rb[j];
                 }
             }
             for (int j = 0; j < 9; j++) g.Hll[9 * own_h + j] = H[j];
             for (int j = 0; j < 3; j++) g.bl[3 * own_h + j] = bv[j];
             if (e_end == own_e1) mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
-            else g.lm_amask[own_l] = touched;
+            else g.lm_amask[own_h] = touched;
         }
-        // (free pose, term) chains over the chunk's edges of the pose
+        if (c0 + kCh + t < g.E) sgn = ld_i4(g.eseg + 4 * (c0 + kCh + t));  // the next chunk's row records
+#ifdef SPSLAM_LBG_DIAG
+        __syncthreads();
+        if (t == 0) s.dg[9] += wall_clock64() - tb1;  // landmark segments
+#endif
+        // (free pose, term) chains over the chunk's edges of the pose: four rows' loads in flight, then their
+        // four adds in edge order (a missing row: a select keeps the sum)
 #pragma unroll
         for (int k = 0; k < kPoseSlots; k++) {
             if (task[k] < 0) continue;
@@ -1272,9 +1353,17 @@ __device__ __noinline__ void build_system() {
             for (int wd = 0; wd < 4; wd++) {
                 uint64_t bits = pm[hh * 4 + wd];
                 while (bits) {
-                    const int i = 64 * wd + __ffsll((unsigned long long)bits) - 1;
-                    bits &= bits - 1;
-                    acc[k] += TP[kSP * i + j];
+                    double v[4];
+                    bool ok[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        ok[q] = bits != 0;
+                        const int i = 64 * wd + (ok[q] ? __ffsll((unsigned long long)bits) - 1 : 0);
+                        bits &= bits - 1;
+                        v[q] = TP[kSP * i + j];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) acc[k] = ok[q] ? acc[k] + v[q] : acc[k];
                 }
             }
         }
@@ -1300,13 +1389,16 @@ __device__ __noinline__ void build_system() {
 // setLambda + the Schur complement (block_solver.hpp:367-436).  (1) every landmark's (Hll + lambda)^-1 and
 // Dinv bl; (2) the chains: one lane per (pattern block (i1, i2), row r) holds S(6 i1 + r, 6 i2 .. 6 i2 + 5) (the
 // diagonal block's lanes also Bb(6 i1 + r)) and subtracts the landmarks' contributions in landmark order.  The
-// landmarks are staged in LDS in chunks: their Hpl blocks (one contiguous range, coalesced), masks, Dinv and
-// Dinv bl, then every block's BDinv = Bi Dinv formed in LDS (one thread per block row), then the chains.
+// landmarks are staged in LDS in chunks of up to 64: their Hpl blocks (one contiguous range, coalesced), masks,
+// Dinv and Dinv bl; then every block's BDinv = Bi Dinv (one thread per block row) and every free pose's chunk
+// landmarks as a bitmask; then the chains, each lane walking only the landmarks that observe both of its poses
+// (in landmark order) while the next chunk's records load into registers.
+constexpr int kSchurTasks = 2;  // chains per lane per round
 __device__ __noinline__ void schur() {
     const G& g = lbg_g;
     Sh& s = lbg_s;
     unsigned char* dyn = lbg_dyn;
-    const int t = threadIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int nl = s.nl, np = s.np, n = 6 * np, nch = s.nch;
     const double lam = s.lambda;
     for (int h = t; h < nl; h += kT) {
@@ -1319,44 +1411,56 @@ __device__ __noinline__ void schur() {
         auto bv = g.bl + 3 * h;
         for (int i = 0; i < 3; i++) g.db[3 * h + i] = (Di[3 * i] * bv[0] + Di[3 * i + 1] * bv[1]) + Di[3 * i + 2] * bv[2];
     }
-    // LDS: two staging buffers (blocks, Dinv, Dinv bl, masks, block offsets) and the BDinv of the current chunk
+    // LDS: the staged chunk (blocks, Dinv, Dinv bl | masks, block offsets, block -> landmark), its BDinv and the
+    // poses' landmark masks
     constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
-    double* BUF = (double*)dyn;                               // [2][kBufD]
-    uint64_t* SM = (uint64_t*)(BUF + 2 * kBufD);              // [2][kSchurLm]
-    int* SO = (int*)(SM + 2 * kSchurLm);                      // [2][kSchurLm + 1]
-    double* SD = (double*)(SO + 2 * (kSchurLm + 2));          // [kSchurBlk][18] BDinv
-    constexpr int kPer = (kBufD + kT - 1) / kT;               // staged doubles per thread
-    // this lane's chain: (i1, i2, r) over the rows of the pattern blocks, row-major over (i1, i2)
+    double* BUF = (double*)dyn;                          // [kBufD]
+    double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
+    uint64_t* SM = (uint64_t*)(SD + kSchurBlk * 18);     // [kSchurLm]
+    uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
+    int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
+    unsigned char* BL = (unsigned char*)(SO + kSchurLm + 1);  // [kSchurBlk]
+    const double* SDi = BUF + kSchurBlk * 18;
+    const double* Sdb = SDi + kSchurLm * 9;
+    constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
+    // the chains: blocks (i, i) first, then the off-diagonal pattern blocks row-major; task = 6 block + r
     int nb = 0;
     for (int q = 0; q < np; q++) nb += __popcll(s.pat[q]);
-    for (int round = 0; round * kT < 6 * nb; round++) {
-        int i1 = -1, i2 = 0, r = 0;
-        const int task = t + round * kT;
-        if (task < 6 * nb) {
-            int blk = task / 6, rem = blk;
-            r = task - 6 * blk;
-            i1 = 0;
-            while (rem >= __popcll(s.pat[i1])) { rem -= __popcll(s.pat[i1]); i1++; }
-            uint64_t row = s.pat[i1];
-            for (int u = 0; u < rem; u++) row &= row - 1;
-            i2 = __ffsll((unsigned long long)row) - 1;
-        }
-        const bool have = i1 >= 0;
-        const bool diag = have && i1 == i2;
-        double acc[6];
+    for (int round = 0; round * kSchurTasks * kT < 6 * nb; round++) {
+        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
+        double acc[kSchurTasks][6], cf[kSchurTasks];
 #pragma unroll
-        for (int c = 0; c < 6; c++) {
-            double base = 0.0;
-            if (diag && c >= r) base = c == r ? g.Hps[27 * i1 + upper_idx(r, c)] + lam : g.Hps[27 * i1 + upper_idx(r, c)];
-            acc[c] = 0.0 + base;
+        for (int k = 0; k < kSchurTasks; k++) {
+            i1[k] = -1; i2[k] = 0; rr[k] = 0;
+            const int task = (round * kSchurTasks + k) * kT + t;
+            if (task < 6 * nb) {
+                const int blk = task / 6;
+                rr[k] = task - 6 * blk;
+                if (blk < np) {
+                    i1[k] = i2[k] = blk;
+                } else {
+                    int rem = blk - np, a = 0;
+                    while (rem >= __popcll(s.pat[a]) - 1) { rem -= __popcll(s.pat[a]) - 1; a++; }
+                    uint64_t row = s.pat[a] & ~(1ull << a);
+                    for (int u = 0; u < rem; u++) row &= row - 1;
+                    i1[k] = a;
+                    i2[k] = __ffsll((unsigned long long)row) - 1;
+                }
+            }
+            const bool diag = i1[k] >= 0 && i1[k] == i2[k];
+            const int r = rr[k];
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                double base = 0.0;
+                if (diag && c >= r) base = c == r ? g.Hps[27 * i1[k] + upper_idx(r, c)] + lam : g.Hps[27 * i1[k] + upper_idx(r, c)];
+                acc[k][c] = 0.0 + base;
+            }
+            cf[k] = 0.0;
         }
-        double cf = 0.0;
-        const uint64_t need = have ? (1ull << i1) | (1ull << i2) : ~0ull;
-        const uint64_t lo1 = have ? (1ull << i1) - 1ull : 0, lo2 = have ? (1ull << i2) - 1ull : 0;
-        // chunk c's records into registers (global loads in flight), later into staging buffer c & 1
+        // chunk c's records into registers (global loads in flight), later into the staging buffer
         double pv[kPer];
         uint64_t pmk = 0;
-        int pof = 0;
+        int pof = 0, pof1 = 0;
         auto prefetch = [&](int c) __attribute__((always_inline)) {
             const int h0 = g.sch[c], h1 = g.sch[c + 1], kb0 = g.sch_kb[c], kb1 = g.sch_kb[c + 1];
             const int nbk = kb1 - kb0, nh = h1 - h0;
@@ -1370,17 +1474,22 @@ __device__ __noinline__ void schur() {
                     v = g.db[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
                 pv[q] = v;
             }
-            if (t < nh) pmk = g.lmh_mask[h0 + t];
+            if (t < nh) {
+                pmk = g.lmh_mask[h0 + t];
+                pof1 = g.lmh_blk[h0 + t + 1] - kb0;
+            }
             if (t <= nh) pof = g.lmh_blk[h0 + t] - kb0;
         };
         auto commit = [&](int c) __attribute__((always_inline)) {
-            double* B = BUF + (c & 1) * kBufD;
             const int nh = g.sch[c + 1] - g.sch[c];
 #pragma unroll
             for (int q = 0; q < kPer; q++)
-                if (t + q * kT < kBufD) B[t + q * kT] = pv[q];
-            if (t < nh) SM[(c & 1) * kSchurLm + t] = pmk;
-            if (t <= nh) SO[(c & 1) * (kSchurLm + 2) + t] = pof;
+                if (t + q * kT < kBufD) BUF[t + q * kT] = pv[q];
+            if (t < nh) {
+                SM[t] = pmk;
+                for (int bk = pof; bk < pof1; bk++) BL[bk] = (unsigned char)t;
+            }
+            if (t <= nh) SO[t] = pof;
         };
         __syncthreads();  // the previous phase's LDS use is over
         if (nch > 0) {
@@ -1388,53 +1497,59 @@ __device__ __noinline__ void schur() {
             commit(0);
         }
         for (int c = 0; c < nch; c++) {
-            if (c + 1 < nch) prefetch(c + 1);  // lands while chunk c is processed
 #ifdef SPSLAM_LBG_DIAG
             long long d0 = wall_clock64();
 #endif
-            __syncthreads();                   // chunk c is staged
+            __syncthreads();  // chunk c is staged
 #ifdef SPSLAM_LBG_DIAG
             long long d1 = wall_clock64();
             if (t == 0) s.dg[0] += d1 - d0;
 #endif
-            const double* SB = BUF + (c & 1) * kBufD;
-            const double* SDi = SB + kSchurBlk * 18;
-            const double* Sdb = SDi + kSchurLm * 9;
-            const uint64_t* Sm = SM + (c & 1) * kSchurLm;
-            const int* So = SO + (c & 1) * (kSchurLm + 2);
             const int nh = g.sch[c + 1] - g.sch[c];
-            const int nbk = So[nh];
+            const int nbk = SO[nh];
             for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q)
-                const int bk = i / 6, rr = i - 6 * bk;
-                int hl = 0;
-                while (So[hl + 1] <= bk) hl++;
-                const double* Bi = SB + 18 * bk + 3 * rr;
-                const double* Di = SDi + 9 * hl;
-                double* BD = SD + 18 * bk + 3 * rr;
+                const int bk = i / 6, r6 = i - 6 * bk;
+                const double* Bi = BUF + 18 * bk + 3 * r6;
+                const double* Di = SDi + 9 * BL[bk];
+                double* BD = SD + 18 * bk + 3 * r6;
 #pragma unroll
                 for (int q = 0; q < 3; q++) BD[q] = (Bi[0] * Di[q] + Bi[1] * Di[3 + q]) + Bi[2] * Di[6 + q];
+            }
+            for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk
+                const uint64_t m = __ballot(lane < nh && ((SM[lane] >> i) & 1ull));
+                if (lane == 0) PM[i] = m;
             }
             __syncthreads();
 #ifdef SPSLAM_LBG_DIAG
             long long d2 = wall_clock64();
             if (t == 0) s.dg[1] += d2 - d1;
 #endif
-            if (have)
-                for (int hl = 0; hl < nh; hl++) {
-                    const uint64_t mk = Sm[hl];
-                    if ((mk & need) != need) continue;
-                    const int o = So[hl];
-                    const double* BD = SD + 18 * (o + __popcll(mk & lo1)) + 3 * r;
-                    const double* Bj = SB + 18 * (o + __popcll(mk & lo2));
-                    const double d0 = BD[0], d1 = BD[1], d2 = BD[2];
+            if (c + 1 < nch) prefetch(c + 1);  // lands while chunk c is processed
 #pragma unroll
-                    for (int cc = 0; cc < 6; cc++) acc[cc] -= (d0 * Bj[3 * cc] + d1 * Bj[3 * cc + 1]) + d2 * Bj[3 * cc + 2];
+            for (int k = 0; k < kSchurTasks; k++) {
+                if (i1[k] < 0) continue;
+                const int r = rr[k];
+                const bool diag = i1[k] == i2[k];
+                const uint64_t lo1 = (1ull << i1[k]) - 1ull, lo2 = (1ull << i2[k]) - 1ull;
+                uint64_t cand = PM[i1[k]] & PM[i2[k]];
+                while (cand) {
+                    const int hl = __ffsll((unsigned long long)cand) - 1;
+                    cand &= cand - 1;
+                    const uint64_t mk = SM[hl];
+                    const int o = SO[hl];
+                    const double* BD = SD + 18 * (o + __popcll(mk & lo1)) + 3 * r;
+                    const double* Bj = BUF + 18 * (o + __popcll(mk & lo2));
+                    const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
+#pragma unroll
+                    for (int cc = 0; cc < 6; cc++)
+                        acc[k][cc] -= (e0 * Bj[3 * cc] + e1 * Bj[3 * cc + 1]) + e2 * Bj[3 * cc + 2];
                     if (diag) {
                         const double* db = Sdb + 3 * hl;
-                        cf += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
+                        cf[k] += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
                     }
                 }
-            __syncthreads();  // SD and buffer c & 1 are free again
+            }
+            __syncthreads();  // the staging buffer, BDinv and the masks are free again
 #ifdef SPSLAM_LBG_DIAG
             long long d3 = wall_clock64();
             if (t == 0) s.dg[2] += d3 - d2;
@@ -1444,10 +1559,13 @@ __device__ __noinline__ void schur() {
             if (t == 0) s.dg[3] += wall_clock64() - d3;
 #endif
         }
-        if (have) {
 #pragma unroll
-            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1 + r) * n + 6 * i2 + cc] = acc[cc];
-            if (diag) g.bs[6 * i1 + r] = g.Hps[27 * i1 + 21 + r] - cf;
+        for (int k = 0; k < kSchurTasks; k++) {
+            if (i1[k] < 0) continue;
+            const int r = rr[k];
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
+            if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
         }
     }
 }
@@ -1455,8 +1573,11 @@ __device__ __noinline__ void schur() {
 // LinearSolverEigen::solve: SimplicialLDLT::factorize + solve on wave 0.  Row r of the permuted system lives in
 // lane r & 63, register r >> 6.  LD: L column-major (LD[i n + r] = L(r, i)), LB: L's column structures (bitsets),
 // RS / RO: the rows' pattern orders, PI: Pinv.
-template <int kC, class PD, class PU, class PI_>
-__device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO, const PI_* RS, const PI_* PI) {
+// SP: the reduced system's upper triangle, packed column by column (SP[c (c + 1) / 2 + r] = S(r, c), r <= c) when
+// kPacked, else g.S (dense, row-major)
+template <int kC, bool kPacked, class PD, class PU, class PI_, class PS>
+__device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO, const PI_* RS, const PI_* PI,
+                                            const PS* SP) {
     const G& g = lbg_g;
     Sh& s = lbg_s;
     const int lane = threadIdx.x & 63;
@@ -1476,43 +1597,80 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
                 const int orr = PI[r];
                 if (coupled(s, orr / 6, qk)) {
                     const int lo = min(orr, ok_), hi = max(orr, ok_);
-                    y[m] = 0.0 + g.S[(size_t)lo * n + hi];
+                    y[m] = 0.0 + (kPacked ? SP[(hi * (hi + 1)) / 2 + lo] : SP[(size_t)lo * n + hi]);
                 }
             }
         }
         double d = pick(y, k) * 1.0 + 0.0;
         const int t0 = RO[k], t1 = RO[k + 1];
-        // the row's pattern order 64 entries at a time in a register (lane q: entry q of the piece); the next
-        // step's column of L and structure words load while this step runs (two operand sets, no moves)
-        auto fetch = [&](int i, double (&v)[kC], uint64_t (&w)[kC]) __attribute__((always_inline)) {
+        // The row's pattern order 64 entries at a time in registers (lane q: entry q of the piece), with each
+        // entry's LDS byte offsets of its L column and structure word and its lane / register in y precomputed
+        // per lane: a step reads them with v_readlane at a loop-counter lane and uses them only in vector
+        // address arithmetic and as readlane lane selects, so no scalar instruction waits on a vector result
+        // inside the chain.  The columns of L and the structure words of the next kRing steps are in flight
+        // while a step runs (a ring of operand sets, each written only by its fetch and read only by its step).
+        // Past the piece's end the entries repeat its last one with the structure word LB[n kNW] (zero): masked
+        // steps.  A column's rows past n read the next one's (in the LDS layout; unused: masked by r < k).
+        constexpr int kRing = kPacked ? 6 : 2;
+        const char* LDc = (const char*)LD;
+        const char* LBc = (const char*)LB;
+        // rows r < k of register m as a lane mask: a step's update condition is one bit test (a select, no
+        // exec-mask branch)
+        uint64_t km[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) {
+            const int c = k - 64 * m;
+            km[m] = c >= 64 ? ~0ull : c <= 0 ? 0ull : (1ull << c) - 1ull;
+        }
+        auto stepf = [&](int lsel, int rsel, const double (&v)[kC], const uint64_t (&w)[kC]) __attribute__((always_inline)) {
+            double yi = rl(y[0], lsel);
+#pragma unroll
+            for (int m = 1; m < kC; m++) {
+                const double q = rl(y[m], lsel);
+                yi = rsel == m ? q : yi;
+            }
 #pragma unroll
             for (int m = 0; m < kC; m++) {
-                const int r = 64 * m + lane;
-                v[m] = r < n ? LD[(size_t)i * n + r] : 0.0;
-                w[m] = LB[(size_t)i * kNW + m];
+                const double nv = y[m] - v[m] * yi;
+                y[m] = (((w[m] & km[m]) >> lane) & 1ull) ? nv : y[m];
             }
         };
-        auto stepf = [&](int i, const double (&v)[kC], const uint64_t (&w)[kC]) __attribute__((always_inline)) {
-            const double yi = pick(y, i);
-#pragma unroll
-            for (int m = 0; m < kC; m++) {
-                const int r = 64 * m + lane;
-                if (r < k && ((w[m] >> lane) & 1ull)) y[m] = y[m] - v[m] * yi;
-            }
-        };
+#ifdef SPSLAM_LBG_DIAG
+        const long long c0 = clock64();
+#endif
         for (int p0 = t0; p0 < t1; p0 += 64) {
             const int ns = min(64, t1 - p0);
-            const int rsv = lane < ns ? RS[p0 + lane] : 0;
-            double vA[kC], vB[kC];
-            uint64_t wA[kC], wB[kC];
-            fetch(__builtin_amdgcn_readlane(rsv, 0), vA, wA);
-            for (int j = 0; j < ns; j += 2) {
-                if (j + 1 < ns) fetch(__builtin_amdgcn_readlane(rsv, j + 1), vB, wB);
-                stepf(__builtin_amdgcn_readlane(rsv, j), vA, wA);
-                if (j + 2 < ns) fetch(__builtin_amdgcn_readlane(rsv, j + 2), vA, wA);
-                if (j + 1 < ns) stepf(__builtin_amdgcn_readlane(rsv, j + 1), vB, wB);
+            const int rsv = RS[p0 + min(lane, ns - 1)];
+            const int cofs = rsv * n * 8;                                   // L column, bytes
+            const int wofs = (lane < ns ? rsv : n) * (kNW * 8);             // structure words (past the end: zero)
+            const int lsel = rsv & 63, rsel = rsv >> 6;                    // y's lane / register of the entry
+            auto fetch = [&](int j, double (&v)[kC], uint64_t (&w)[kC]) __attribute__((always_inline)) {
+                const int co = __builtin_amdgcn_readlane(cofs, j);
+                int wo = __builtin_amdgcn_readlane(wofs, j);
+                asm volatile("v_mov_b32 %0, %1" : "=v"(wo) : "s"(wo));  // the address sum in a vector op
+#pragma unroll
+                for (int m = 0; m < kC; m++) {
+                    const int r = 64 * m + lane;
+                    v[m] = (kPacked || r < n) ? *(const PD*)(LDc + co + 8 * r) : 0.0;
+                    w[m] = *(const PU*)(LBc + wo + 8 * m);
+                }
+            };
+            double v[kRing][kC];
+            uint64_t w[kRing][kC];
+#pragma unroll
+            for (int q = 0; q < kRing; q++) fetch(min(q, 63), v[q], w[q]);
+            for (int j = 0; j < ns; j += kRing) {
+#pragma unroll
+                for (int q = 0; q < kRing; q++) {
+                    stepf(__builtin_amdgcn_readlane(lsel, j + q), __builtin_amdgcn_readlane(rsel, j + q), v[q], w[q]);
+                    fetch(min(j + q + kRing, 63), v[q], w[q]);
+                }
             }
         }
+#ifdef SPSLAM_LBG_DIAG
+        const long long c1 = clock64();
+        if (lane == 0) { s.dg[6] += c1 - c0; s.dg[8] += t1 - t0; }
+#endif
         double pr[kC];
 #pragma unroll
         for (int m = 0; m < kC; m++) {
@@ -1524,11 +1682,32 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
                 pr[m] = l * y[m];
             }
         }
+        // d -= l_ki y_i in pattern order: the piece's terms gathered into pattern order across the lanes
+        // (ds_bpermute), then subtracted lane by lane (loop-counter readlanes, off the dependent chain)
         for (int p0 = t0; p0 < t1; p0 += 64) {
             const int ns = min(64, t1 - p0);
-            const int rsv = lane < ns ? RS[p0 + lane] : 0;
-            for (int j = 0; j < ns; j++) d -= pick(pr, __builtin_amdgcn_readlane(rsv, j));
+            const int rsv = RS[p0 + min(lane, ns - 1)];
+            const int src = (rsv & 63) * 4;
+            double pv = 0.0;
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int lo = __builtin_amdgcn_ds_bpermute(src, __double2loint(pr[m]));
+                const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(pr[m]));
+                pv = (rsv >> 6) == m ? __hiloint2double(hi, lo) : pv;
+            }
+            int j = 0;
+            for (; j + 4 <= ns; j += 4) {
+                const double a0 = rl(pv, j), a1 = rl(pv, j + 1), a2 = rl(pv, j + 2), a3 = rl(pv, j + 3);
+                d -= a0;
+                d -= a1;
+                d -= a2;
+                d -= a3;
+            }
+            for (; j < ns; j++) d -= rl(pv, j);
         }
+#ifdef SPSLAM_LBG_DIAG
+        if (lane == 0) s.dg[7] += clock64() - c1;
+#endif
 #pragma unroll
         for (int m = 0; m < kC; m++)
             if (64 * m + lane == k) Dg[m] = d;
@@ -1598,18 +1777,31 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
     }
 }
 
+// byte offsets of the factorisation's LDS copy (n <= kLdsN): L, its column structures, the rows' pattern orders
+// (offsets, indices), P^-1, S packed
+struct FactorLds { size_t LB, RO, RS, PI, SP, end; };
+__device__ __forceinline__ FactorLds factor_lds(int n) {
+    FactorLds f;
+    f.LB = (size_t)n * n * 8;
+    f.RO = f.LB + (size_t)(n * kNW + 1) * 8;  // LB[n kNW] = 0
+    f.RS = f.RO + (size_t)(n + 1) * 4;
+    f.PI = f.RS + (size_t)((n * (n + 1)) / 2 + 1) * 4;
+    f.SP = (f.PI + (size_t)n * 4 + 7) & ~(size_t)7;
+    f.end = f.SP + (size_t)((n * (n + 1)) / 2) * 8;
+    return f;
+}
+
 template <int kC, bool kLds>
 __device__ __noinline__ void factor_solve() {
     const int n = 6 * lbg_s.np;
     if (kLds) {  // the layout of k_lba_g2o's copy in LDS
-        double* LD = (double*)lbg_dyn;
-        const uint64_t* LB = (const uint64_t*)(lbg_dyn + (size_t)n * n * 8);
-        const int* RO = (const int*)(LB + (size_t)n * kNW);
-        const int* RS = RO + (n + 1);
-        factor_body<kC>(LD, LB, RO, RS, RS + (n * (n + 1)) / 2 + 1);
+        const FactorLds f = factor_lds(n);
+        factor_body<kC, true>((double*)lbg_dyn, (const uint64_t*)(lbg_dyn + f.LB), (const int*)(lbg_dyn + f.RO),
+                              (const int*)(lbg_dyn + f.RS), (const int*)(lbg_dyn + f.PI),
+                              (const double*)(lbg_dyn + f.SP));
     } else {
         const G& g = lbg_g;
-        factor_body<kC>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv);
+        factor_body<kC, false>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv, g.S);
     }
 }
 
@@ -1786,13 +1978,34 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     }
     if (t == 0) {
         s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1;
-        for (int i = 0; i < 8; i++) s.ph[i] = s.dg[i] = 0;
+        for (int i = 0; i < 8; i++) s.ph[i] = 0;
+        for (int i = 0; i < 10; i++) s.dg[i] = 0;
         s.tB = 0;
         s.tlast = t0;
         s.done = stop_requested(b, p, s) ? 1 : 0;  // if(*pbStopFlag) return; before initializeOptimization
         if (s.done) s.stopped = 1;
     }
     __syncthreads();
+#ifdef SPSLAM_LBG_PROBE  // diagnostic: the cost of the building blocks of the ordered chains inside this kernel
+    double probe[4] = {0, 0, 0, 0};
+    if (t < 64) {
+        const double a = (double)g.E * 1e-9;
+        const int lane = t & 63;
+        double x = 1.0, yv = (double)lane * 1e-3, z = 0.0;
+        long long c0 = clock64();
+        for (int i = 0; i < 4096; i++) x = x + a;  // (1) dependent v_add_f64
+        long long c1 = clock64();
+        for (int i = 0; i < 4096; i++) z = z + rl(yv, i & 63);  // (2) + a v_readlane operand
+        long long c2 = clock64();
+        int k = lane;
+        for (int i = 0; i < 4096; i++) k = __builtin_amdgcn_readlane(k, (k + i) & 63) & 63;  // (3) readlane -> lane select
+        long long c3 = clock64();
+        probe[0] = (double)(c1 - c0) / 4096;
+        probe[1] = (double)(c2 - c1) / 4096;
+        probe[2] = (double)(c3 - c2) / 4096;
+        probe[3] = x + z + k;
+    }
+#endif
     if (!s.done) setup();
     if (t == 0 && g.E == 0) s.done = 1;  // no edges: nothing to optimise, the map goes back through the converters
     __syncthreads();
@@ -1802,10 +2015,11 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         const int n = 6 * s.np;
         // the factorisation's operands in LDS for n <= kLdsN: L, its column structures, the rows' pattern orders, P
         const bool lds = n <= kLdsN;
-        uint64_t* LB = (uint64_t*)(dyn + (size_t)n * n * 8);  // (used when lds)
-        int* RO = (int*)(LB + (size_t)n * kNW);
-        int* RS = RO + (n + 1);
-        int* PI = RS + (n * (n + 1)) / 2 + 1;
+        const FactorLds fl = factor_lds(n);  // (used when lds)
+        uint64_t* LB = (uint64_t*)(dyn + fl.LB);
+        int* RO = (int*)(dyn + fl.RO);
+        int* RS = (int*)(dyn + fl.RS);
+        int* PI = (int*)(dyn + fl.PI);
         if (t == 0) {
             s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1;
         }
@@ -1825,7 +2039,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                 errors();
                 __syncthreads();
                 LBG_MARK(2);
-                if (t == 0) s.currentChi = ordered_sum(g.echi, lbg_pad32(g.E));
+                sums_staged(lbg_pad32(g.E), 0);
                 __syncthreads();
                 LBG_MARK(3);
             }
@@ -1846,11 +2060,16 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                 __syncthreads();
                 LBG_MARK(5);
                 if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
-                    for (int i = t; i < n * kNW; i += kT) LB[i] = g.Lbits[i];
+                    for (int i = t; i <= n * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
                     for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
                     const int nz = g.rs_off[n];
                     for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
                     for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
+                    double* SP = (double*)(dyn + fl.SP);  // S, packed upper
+                    for (int i = t; i < n * n; i += kT) {
+                        const int r = i / n, c = i - r * n;
+                        if (r <= c) SP[(c * (c + 1)) / 2 + r] = g.S[i];
+                    }
                     __syncthreads();
                 }
 #ifdef SPSLAM_LBG_DIAG
@@ -1877,8 +2096,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                 scale_terms();
                 __syncthreads();
                 LBG_MARK(2);
-                if (t == 0) s.tempChi = ordered_sum(g.echi, lbg_pad32(g.E));
-                if (t == 64) s.scale = ordered_sum(g.sc, lbg_pad32(n + 3 * s.nl));
+                sums_staged(lbg_pad32(g.E), lbg_pad32(n + 3 * s.nl));
                 __syncthreads();
                 LBG_MARK(3);
                 if (t == 0) {
@@ -1964,7 +2182,15 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         b.res[p].pad = (int)(s.tB * 0.01);  // diagnostic: build phase (B) us; phase_us[7]: (A) of plane chunks
 #ifdef SPSLAM_LBG_DIAG  // Schur: staging wait, BDinv, chains, commit; factor-only
         for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
+        b.res[p].phase_us[5] = (float)(s.dg[6] * 1e-3);  // factor: step-loop shader kcycles,
+        b.res[p].phase_us[6] = (float)(s.dg[7] * 1e-3);  //   pivot-update kcycles,
+        b.res[p].pad = (int)s.dg[8];                     //   steps
+        b.res[p].phase_us[4] = (float)(s.dg[9] * 0.01);  // build: landmark segments (us)
         b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
+#endif
+#ifdef SPSLAM_LBG_PROBE  // shader-clock ticks per (1) add, (2) add of a readlane, (3) readlane chain
+        for (int i = 0; i < 3; i++) b.res[p].phase_us[1 + i] = (float)probe[i];
+        if (probe[3] == 12345.0) b.res[p].pad = 1;
 #endif
     }
 }

@@ -116,9 +116,9 @@ struct LbaBatch {
 // schedule with every sum in g2o's order.  Per-problem scratch, computed identically on host and device.
 constexpr int kLbgThreads = 512;
 struct LbgLayout {
-    size_t pose, pose_b, X, X_b, P, P_b, err, echi, sc, terms, Hll, bl, Dinv, db, blkB, blkBD, Hps, S, bs, x, Ld;  // double
+    size_t pose, pose_b, X, X_b, P, P_b, err, echi, sc, terms, Hll, bl, Dinv, db, blkB, Hps, S, bs, x, Ld;  // double
     size_t e_lm, e_kf, e_type, e_level, e_src, e_blk, lm_boff, lm_nb, lm_sorted, lm_hidx, hidx_lm, lmh_blk, pe_off,
-        pe_idx, Pinv, Pm, parent, rs_off, rs_idx, amd_Ci, amd_W, sch, sch_kb;                              // int
+        pe_idx, Pinv, Pm, parent, rs_off, rs_idx, amd_Ci, amd_W, sch, sch_kb, eseg;                        // int
     size_t lmh_mask, lm_amask, Lbits, Abits;                                                                // uint64
     size_t bytes;
 };
@@ -135,7 +135,7 @@ __host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
     Ly.err = take((size_t)E * 3 * 8); Ly.echi = take(Ep * 8); Ly.sc = take(Xn * 8);
     Ly.terms = take((size_t)E * kLbaCon * 8);
     Ly.Hll = take(L * 9 * 8); Ly.bl = take(L * 3 * 8); Ly.Dinv = take(L * 9 * 8); Ly.db = take(L * 3 * 8);
-    Ly.blkB = take((size_t)E * 18 * 8); Ly.blkBD = take((size_t)E * 18 * 8);
+    Ly.blkB = take((size_t)E * 18 * 8);
     Ly.Hps = take(K * 27 * 8); Ly.S = take(n * n * 8); Ly.bs = take(n * 8); Ly.x = take(Xn * 8);
     Ly.Ld = take(n * n * 8);
     Ly.e_lm = take((size_t)E * 4); Ly.e_kf = take((size_t)E * 4); Ly.e_type = take((size_t)E * 4);
@@ -146,8 +146,8 @@ __host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
     Ly.Pinv = take(n * 4); Ly.Pm = take(n * 4); Ly.parent = take(n * 4); Ly.rs_off = take((n + 1) * 4);
     Ly.rs_idx = take((n * (n + 1) / 2 + 1) * 4);
     Ly.amd_Ci = take((nC + 1) * 4); Ly.amd_W = take(10 * (n + 1) * 4);
-    Ly.sch = take((L + 2) * 4); Ly.sch_kb = take((L + 2) * 4);
-    Ly.lmh_mask = take(L * 8); Ly.lm_amask = take(L * 8); Ly.Lbits = take(n * 6 * 8); Ly.Abits = take(n * 6 * 8);
+    Ly.sch = take((L + 2) * 4); Ly.sch_kb = take((L + 2) * 4); Ly.eseg = take((size_t)E * 16);
+    Ly.lmh_mask = take(L * 8); Ly.lm_amask = take(L * 8); Ly.Lbits = take((n + 1) * 6 * 8); Ly.Abits = take(n * 6 * 8);
     Ly.bytes = o;
     return Ly;
 }

@@ -144,15 +144,16 @@ def test_c3_local_mapping_in_the_loop():
     """C3 as a pipeline: the deterministic LocalMapping (sp-slam_amd/local_mapping.py) after every keyframe frame
     -- keyframe insertion from the tracked frame, LocalBundleAdjustment of the local window on the device, its
     result written back into the map the next frames track against (local-map points, last-frame points and
-    pose, map planes).  The CPU oracle runs the same loop with the oracle's LocalBundleAdjustment.  LBA sums in
-    tree / MFMA order: its results agree to rounding, not bit for bit, and the loop carries that
-    rounding forward.  Bar: every LocalBundleAdjustment with identical LM iteration / trial / outlier counts,
-    keyframe poses and points within 1e-4 relative; every frame's decisions identical; ATE vs the CPU trajectory
-    <= 1e-4 m (north star).  The differences are written to gpurun_out/c3_local_mapping_parity.json."""
+    pose, map planes).  The CPU oracle runs the same loop with the oracle's LocalBundleAdjustment.  Both sum in
+    g2o's order, so the bar is bit equality over 160 frames (15 LocalBundleAdjustments, past frame
+    80 where the round-3 tree-order LBA first changed a decision): every LocalBundleAdjustment's poses, points,
+    LM iteration / trial / outlier counts, every frame's pose and decisions, hence ATE vs the CPU trajectory 0
+    (up to the rounding of the Horn alignment itself, ~1e-16 m).
+    The per-frame differences (all zero) are written to gpurun_out/c3_local_mapping_parity.json."""
     import json
     import trajectory
     from test_gpu_pose import pose_close
-    n = 45
+    n = 160
     sp = sequence_path(2, n + 2, 1, "c3")
     try:
         assert sp.local_mapping
@@ -168,28 +169,29 @@ def test_c3_local_mapping_in_the_loop():
                       on_lba=lambda t, r: lbas.update({t: r}))
         runs = dict(sp.lm_runs)
         diag = {"lba": {}, "frame_pose_diff": []}
-        assert sorted(runs) == sorted(lbas) == [20, 30, 40]
+        assert sorted(runs) == sorted(lbas) == list(range(20, n + 1, 10))
         for t, r in lbas.items():
             g = runs[t][0]
+            diag["lba"][t] = {"iterations": [int(x) for x in r["result"]["iterations"]],
+                              "trials": int(r["result"]["trials"]), "keyframes": len(g["kfs"]),
+                              "max_pose_diff": float(np.abs(g["Tcw"] - r["Tcw"]).max()),
+                              "max_point_diff": float(np.abs(g["points"] - r["points"]).max())}
+            assert g["kfs"] == r["kfs"], t
             assert list(g["result"]["iterations"]) == list(r["result"]["iterations"]), t
             assert int(g["result"]["trials"]) == int(r["result"]["trials"]), t
             assert int(g["result"]["n_point_outliers"]) == int(r["result"]["n_point_outliers"]), t
-            assert g["kfs"] == r["kfs"], t
-            errs = [pose_close(g["Tcw"][k], r["Tcw"][k])[1] for k in range(len(g["kfs"]))]
-            dp = np.abs(g["points"] - r["points"]).max() / max(np.abs(r["points"]).max(), 1.0)
-            diag["lba"][t] = {"kf_pose_err": [[float(a), float(b)] for a, b in errs], "point_rel": float(dp),
-                              "iterations": [int(x) for x in r["result"]["iterations"]]}
-            assert all(a <= 1e-4 and b <= 1e-4 for a, b in errs), (t, errs)
-            assert dp <= 1e-4, (t, dp)
+            assert np.array_equal(g["Tcw"], r["Tcw"]), (t, diag["lba"][t])
+            assert np.array_equal(g["points"], r["points"]), (t, diag["lba"][t])
         for t in range(1, n + 1):
             assert tuple(int(x) for x in hist[t, 0]) == tuple(int(x) for x in got[t]), t
             diag["frame_pose_diff"].append([float(x) for x in pose_close(tr[t, 0].reshape(16), cpu[t - 1].reshape(16))[1]])
+            assert tr[t, 0].tobytes() == cpu[t - 1].tobytes(), (t, diag["frame_pose_diff"][-1])
         g = [trajectory.camera_center(tr[k + 1, 0].reshape(16)) for k in range(n)]
         c = [trajectory.camera_center(cpu[k].reshape(16)) for k in range(n)]
         diag["ate_vs_cpu_m"] = trajectory.ate_rmse(g, c)
         (pathlib.Path(__file__).resolve().parents[1] / "gpurun_out").mkdir(exist_ok=True)
         (pathlib.Path(__file__).resolve().parents[1] / "gpurun_out" / "c3_local_mapping_parity.json").write_text(
             json.dumps(diag, indent=1))
-        assert diag["ate_vs_cpu_m"] <= 1e-4, diag["ate_vs_cpu_m"]
+        assert diag["ate_vs_cpu_m"] <= 1e-12, diag["ate_vs_cpu_m"]  # identical trajectories (Horn's SVD rounding)
     finally:
         sp.close()
