@@ -685,6 +685,12 @@ def main():
             "frac": floor / max(avg_launch_s * 1e3, 1e-9),
             "mean_lm_iterations": float((res["pose1"]["lm_iterations"].mean() + res["pose2"]["lm_iterations"].mean()) / 2),
             "mean_trial_passes": float((res["pose1"]["trial_passes"].mean() + res["pose2"]["trial_passes"].mean()) / 2)}
+    elif dom == "lba_batch":
+        # one workgroup per LocalBundleAdjustment problem walking g2o's ordered fp64 chains (buildSystem in edge
+        # order, the Schur complement in landmark order, the up-looking LDLT): latency-bound, 16 MB per launch
+        result["roofline"]["bound"] = "fp64-issue/latency"
+        result["roofline"]["note"] = ("ordered fp64 chains per problem (DESIGN.md section 3.9); the launch ends with "
+                                      "its slowest problem, phases in tools/lba_bench.py --order g2o")
     # validity of the timed results: no PoseOptimization gave up on a bounded device wait (lm_iterations = -1),
     # every LocalBundleAdjustment of the step finished (status 0)
     checks = {"pose_wait_give_ups": int((res["pose1"]["lm_iterations"] < 0).sum() + (res["pose2"]["lm_iterations"] < 0).sum())}

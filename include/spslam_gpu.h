@@ -470,6 +470,11 @@ int spslam_supposed_debug(spslam_ctx* ctx, int frame, int plane, spslam_line_can
  * timestamps (16 int64 ticks of the 100 MHz GPU real-time clock). */
 int spslam_planes_debug(spslam_ctx* ctx, int frame, int what, void* out, int* n_points);
 
+/* Test hook: keep = 1 makes the following plane extractions also store the connected-component labels that
+ * spslam_planes_debug(what = 3) returns.  Off by default: frames whose union-find runs in LDS (16-bit labels)
+ * then write no label map at all. */
+int spslam_debug_plane_labels(spslam_ctx* ctx, int keep);
+
 /* Test hook: Frame::PlaneNotSeen (src/Frame.cc:1116-1130) of each of n_coefs
  * candidate coefficient vectors against n_planes planes (4 floats each, host
  * buffers), evaluated by the device predicate the plane-extraction and

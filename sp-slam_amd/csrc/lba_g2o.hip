@@ -55,7 +55,7 @@ struct Sh {
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
     double lambda, ni, currentChi, iniChi, tempChi, scale;
     long long ph[8], tlast, tB;  // diagnostics: wall_clock64 ticks per phase (result phase_us[1..7])
-    long long dg[10];            // SPSLAM_LBG_DIAG sub-phase ticks
+    long long dg[14];            // SPSLAM_LBG_DIAG sub-phase ticks
 };
 // thread 0 charges the time since the previous mark to phase k (called right after a barrier)
 #define LBG_MARK(k)                                  \
@@ -742,19 +742,18 @@ __device__ __noinline__ void structure() {
         int nc = 0;
         const int ng = (nl + kSchurLm - 1) / kSchurLm;
         for (int pass2 = 0; pass2 < 2; pass2++) {
-            int my = 0, base2 = 0;
+            int base2 = 0;
             for (int ch = 0; ch < ng; ch += kT) {
                 const int gi = ch + t;
                 int cntc = 0;
                 if (gi < ng) {
                     const int h0 = gi * kSchurLm, h1 = min(nl, h0 + kSchurLm);
-                    int start = h0, k0 = g.lmh_blk[h0];
+                    int k0 = g.lmh_blk[h0];
                     cntc = 1;
                     for (int h = h0 + 1; h < h1; h++) {
                         const int kh = g.lmh_blk[h + 1];
-                        if (kh - k0 > kSchurBlk) { start = h; k0 = g.lmh_blk[h]; cntc++; }
+                        if (kh - k0 > kSchurBlk) { k0 = g.lmh_blk[h]; cntc++; }
                     }
-                    (void)start;
                 }
                 int tot;
                 const int off = block_scan(cntc, &tot, s) + base2;
@@ -769,7 +768,6 @@ __device__ __noinline__ void structure() {
                     }
                 }
                 base2 += tot;
-                my += 0;
             }
             nc = base2;
         }
@@ -1217,6 +1215,15 @@ __device__ __noinline__ void build_system() {
     double* TB = TP + kCh * kSP;
     uint64_t* pm = (uint64_t*)(TB + kCh * kSB);  // [np][4]: the chunk's edges of each free pose
     int* RI = (int*)(pm + 4 * kMaxK);            // [kCh] per row: its Hpl block, -1 none, -2 inactive edge
+#ifndef SPSLAM_LBG_SEG_SERIAL
+    // the chunk's landmark segments, compacted per wave: (first row, end row, landmark, first block | continuing
+    // << 30 | complete << 31); per row the Hpl term's kind (0 none, 1 the block's first term: a plain store, 2 a
+    // later term of the same block: an addition)
+    int4* SG = (int4*)(RI + kCh);                       // [kCh]
+    unsigned char* RF = (unsigned char*)(SG + kCh);     // [kCh]
+    int* NSW = (int*)(RF + kCh);                        // [kW] segments per wave, [kW]: any addition rows
+    static_assert((kCh * (kSL + kSP + kSB) + 4 * kMaxK) * 8 + kCh * (4 + 16 + 1) + 4 * (kW + 1) <= kDyn, "LDS");
+#endif
     double acc[kPoseSlots];
     int task[kPoseSlots];
 #pragma unroll
@@ -1233,6 +1240,54 @@ __device__ __noinline__ void build_system() {
         const int cnt = min(kCh, g.E - c0);
         const int4 sg = sgn;
         for (int i = t; i < 4 * np; i += kT) pm[i] = 0;
+#ifndef SPSLAM_LBG_SEG_SERIAL
+        // (B) runs on every thread: one (segment, component) chain per task, one (row, entry) plain Hpl store per
+        // task, then -- only in chunks that have them -- each segment's later terms of a repeated (landmark,
+        // pose) block (plane landmarks) added by the segment's head thread in edge order.
+        bool head = false, again = false;
+        int end_row = 0, own_h = -1, own_kb = 0;
+        uint64_t touched = 0;
+        if (t < cnt) {
+            RI[t] = sg.x;
+            RF[t] = 0;
+            const bool first = (sg.w >> 30) & 1;
+            if ((first || t == 0) && sg.y >= 0) {
+                head = true;
+                own_h = sg.y;
+                own_kb = sg.w & ((1 << 30) - 1);
+                end_row = min(sg.z, c0 + cnt) - c0;
+                touched = first ? 0ull : g.lm_amask[own_h];  // (lm_amask is free after the structure phase)
+            }
+        }
+        {
+            const uint64_t hb = __ballot(head);
+            if (head) {
+                const int li = __popcll(hb & ((1ull << lane) - 1));
+                const unsigned fl = (unsigned)own_kb | ((t == 0 && !((sg.w >> 30) & 1)) ? 1u << 30 : 0u) |
+                                    (c0 + end_row == sg.z ? 1u << 31 : 0u);
+                SG[64 * wv + li] = make_int4(t, end_row, own_h, (int)fl);
+            }
+            if (lane == 0) NSW[wv] = __popcll(hb);
+            if (t == 0) NSW[kW] = 0;
+        }
+        __syncthreads();
+        if (head) {  // the rows' Hpl kinds, in edge order
+            for (int r = t; r < end_row; r++) {
+                const int bk = RI[r];
+                unsigned char f = 0;
+                if (bk >= 0) {
+                    const uint64_t bit = 1ull << (bk - own_kb);
+                    f = (touched & bit) ? 2 : 1;
+                    touched |= bit;
+                }
+                RF[r] = f;
+                again |= f == 2;
+            }
+            if (c0 + end_row != sg.z) g.lm_amask[own_h] = touched;
+            if (again) NSW[kW] = 1;
+        }
+#else
+
         // this thread's landmark segment (row t starts one when it is the landmark's first edge or the chunk's
         // first row): its records are consumed after phase (A)
         int own_h = -1, own_e1 = 0, own_kb = 0;
@@ -1254,6 +1309,7 @@ __device__ __noinline__ void build_system() {
             }
         }
         __syncthreads();
+#endif
         // (A) edges on thread pairs (the plane edges' Jacobians from plane_jacobians)
         {
             const int row = t >> 1, e = c0 + row;
@@ -1292,10 +1348,14 @@ __device__ __noinline__ void build_system() {
         // term is stored (0 + term); a later term of the same (landmark, pose) block -- plane landmarks, whose
         // plane / parallel / vertical edges share a keyframe -- is added by the second loop, in edge order.  (One
         // loop with both would wait for every earlier store at each edge: one vector-memory counter on gfx950.)
+#ifdef SPSLAM_LBG_SEG_SERIAL
         if (own_h >= 0) {
             const int e = c0 + t, e_end = min(own_e1, c0 + cnt);
             const uint64_t touched0 = touched;  // blocks stored in an earlier chunk (a continuing segment)
             bool again = false;
+#ifdef SPSLAM_LBG_DIAG
+            const long long sc0 = clock64();
+#endif
             for (int e2 = e; e2 < e_end; e2++) {
                 const int bk = RI[e2 - c0];
                 if (bk == -2) continue;
@@ -1338,8 +1398,67 @@ __device__ __noinline__ void build_system() {
             for (int j = 0; j < 3; j++) g.bl[3 * own_h + j] = bv[j];
             if (e_end == own_e1) mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
             else g.lm_amask[own_h] = touched;
+#ifdef SPSLAM_LBG_DIAG  // segment loops: shader cycles and edges, summed; the longest per chunk, summed
+            const unsigned long long sc = (unsigned long long)(clock64() - sc0);
+            atomicAdd((unsigned long long*)&s.dg[10], sc);
+            atomicAdd((unsigned long long*)&s.dg[11], (unsigned long long)(e_end - e));
+            atomicAdd((unsigned long long*)&s.dg[13], 1ull);
+            atomicMax((unsigned long long*)&s.dg[12], sc);
+#endif
         }
+#endif
         if (c0 + kCh + t < g.E) sgn = ld_i4(g.eseg + 4 * (c0 + kCh + t));  // the next chunk's row records
+#ifndef SPSLAM_LBG_SEG_SERIAL
+        {
+            int nseg = 0;
+#pragma unroll
+            for (int w = 0; w < kCh / 64; w++) nseg += NSW[w];
+            // (segment, component) chains: Hll (9) and bl (3) in edge order, four rows' loads in flight
+            for (int task = t; task < 12 * nseg; task += kT) {
+                const int si = task / 12, comp = task - 12 * si;
+                int w = 0, li = si;
+                while (li >= NSW[w]) li -= NSW[w++];
+                const int4 sgm = SG[64 * w + li];
+                const unsigned fl = (unsigned)sgm.w;
+                const int h = sgm.z;
+                auto dst = comp < 9 ? g.Hll + 9 * h + comp : g.bl + 3 * h + (comp - 9);
+                double a = (fl >> 30) & 1 ? *dst : 0.0;
+                int r = sgm.x;
+                for (; r + 4 <= sgm.y; r += 4) {
+                    double v[4];
+                    bool ok[4];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        ok[q] = RI[r + q] != -2;
+                        v[q] = TL[kSL * (r + q) + comp];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) a = ok[q] ? a + v[q] : a;
+                }
+                for (; r < sgm.y; r++)
+                    if (RI[r] != -2) a += TL[kSL * r + comp];
+                *dst = a;
+                if ((fl >> 31) && (comp == 0 || comp == 4 || comp == 8)) mx = fmax(mx, fabs(a));
+            }
+            // each block's first term: 0 + term (one entry per task)
+            for (int i = t; i < 18 * cnt; i += kT) {
+                const int r = i / 18, c = i - 18 * r;
+                if (RF[r] == 1) g.blkB[(size_t)18 * RI[r] + c] = 0.0 + TB[kSB * r + c];
+            }
+            if (NSW[kW]) {  // (block-uniform) the later terms, after every first term is stored
+                __syncthreads();
+                if (again) {
+                    for (int r = t; r < end_row; r++) {
+                        if (RF[r] != 2) continue;
+                        auto dst = g.blkB + (size_t)18 * RI[r];
+                        const double* rb = TB + kSB * r;
+#pragma unroll
+                        for (int j = 0; j < 18; j++) dst[j] += rb[j];
+                    }
+                }
+            }
+        }
+#endif
 #ifdef SPSLAM_LBG_DIAG
         __syncthreads();
         if (t == 0) s.dg[9] += wall_clock64() - tb1;  // landmark segments
@@ -1380,6 +1499,7 @@ __device__ __noinline__ void build_system() {
         if (j == 0 || j == 6 || j == 11 || j == 15 || j == 18 || j == 20) mx = fmax(mx, fabs(acc[k]));
     }
     (void)lane;
+    (void)wv;
     mx = block_max(mx, s);
     if (t == 0) s.red[0][1] = mx;
 }
@@ -1577,7 +1697,7 @@ __device__ __noinline__ void schur() {
 // kPacked, else g.S (dense, row-major)
 template <int kC, bool kPacked, class PD, class PU, class PI_, class PS>
 __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO, const PI_* RS, const PI_* PI,
-                                            const PS* SP) {
+                                            const PS* SP, double* PR /* LDS, 64 doubles */) {
     const G& g = lbg_g;
     Sh& s = lbg_s;
     const int lane = threadIdx.x & 63;
@@ -1695,15 +1815,24 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
                 const int hi = __builtin_amdgcn_ds_bpermute(src, __double2hiint(pr[m]));
                 pv = (rsv >> 6) == m ? __hiloint2double(hi, lo) : pv;
             }
+            // lane q's term into LDS slot q, then every lane subtracts the slots in order (broadcast reads:
+            // no cross-lane register moves on the chain)
+            PR[lane] = pv;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             int j = 0;
-            for (; j + 4 <= ns; j += 4) {
-                const double a0 = rl(pv, j), a1 = rl(pv, j + 1), a2 = rl(pv, j + 2), a3 = rl(pv, j + 3);
-                d -= a0;
-                d -= a1;
-                d -= a2;
-                d -= a3;
+            for (; j + 8 <= ns; j += 8) {
+                double a[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) a[q] = PR[j + q];
+#pragma unroll
+                for (int q = 0; q < 8; q++) d -= a[q];
             }
-            for (; j < ns; j++) d -= rl(pv, j);
+            for (; j < ns; j++) d -= PR[j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
 #ifdef SPSLAM_LBG_DIAG
         if (lane == 0) s.dg[7] += clock64() - c1;
@@ -1779,7 +1908,7 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
 
 // byte offsets of the factorisation's LDS copy (n <= kLdsN): L, its column structures, the rows' pattern orders
 // (offsets, indices), P^-1, S packed
-struct FactorLds { size_t LB, RO, RS, PI, SP, end; };
+struct FactorLds { size_t LB, RO, RS, PI, SP, PR, end; };
 __device__ __forceinline__ FactorLds factor_lds(int n) {
     FactorLds f;
     f.LB = (size_t)n * n * 8;
@@ -1787,7 +1916,8 @@ __device__ __forceinline__ FactorLds factor_lds(int n) {
     f.RS = f.RO + (size_t)(n + 1) * 4;
     f.PI = f.RS + (size_t)((n * (n + 1)) / 2 + 1) * 4;
     f.SP = (f.PI + (size_t)n * 4 + 7) & ~(size_t)7;
-    f.end = f.SP + (size_t)((n * (n + 1)) / 2) * 8;
+    f.PR = f.SP + (size_t)((n * (n + 1)) / 2) * 8;
+    f.end = f.PR + 64 * 8;
     return f;
 }
 
@@ -1798,10 +1928,10 @@ __device__ __noinline__ void factor_solve() {
         const FactorLds f = factor_lds(n);
         factor_body<kC, true>((double*)lbg_dyn, (const uint64_t*)(lbg_dyn + f.LB), (const int*)(lbg_dyn + f.RO),
                               (const int*)(lbg_dyn + f.RS), (const int*)(lbg_dyn + f.PI),
-                              (const double*)(lbg_dyn + f.SP));
+                              (const double*)(lbg_dyn + f.SP), (double*)(lbg_dyn + f.PR));
     } else {
         const G& g = lbg_g;
-        factor_body<kC, false>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv, g.S);
+        factor_body<kC, false>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv, g.S, (double*)lbg_dyn);  // (LDS unused)
     }
 }
 
@@ -1979,7 +2109,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     if (t == 0) {
         s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1;
         for (int i = 0; i < 8; i++) s.ph[i] = 0;
-        for (int i = 0; i < 10; i++) s.dg[i] = 0;
+        for (int i = 0; i < 14; i++) s.dg[i] = 0;
         s.tB = 0;
         s.tlast = t0;
         s.done = stop_requested(b, p, s) ? 1 : 0;  // if(*pbStopFlag) return; before initializeOptimization
@@ -2186,6 +2316,9 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         b.res[p].phase_us[6] = (float)(s.dg[7] * 1e-3);  //   pivot-update kcycles,
         b.res[p].pad = (int)s.dg[8];                     //   steps
         b.res[p].phase_us[4] = (float)(s.dg[9] * 0.01);  // build: landmark segments (us)
+        b.res[p].phase_us[1] = (float)s.dg[10] / (float)max(1ll, s.dg[11]);  // segments: cycles per edge,
+        b.res[p].phase_us[2] = (float)s.dg[11] / (float)max(1ll, s.dg[13]);  //   edges per segment,
+        b.res[p].phase_us[3] = (float)(s.dg[12] * 1e-3);                     //   longest loop (kcycles)
         b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
 #endif
 #ifdef SPSLAM_LBG_PROBE  // shader-clock ticks per (1) add, (2) add of a readlane, (3) readlane chain

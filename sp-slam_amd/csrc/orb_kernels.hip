@@ -1034,13 +1034,15 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
 // Host-side launchers (called from spslam_capi.cpp).
 namespace spslam {
 
-// levels fused into level_small_kernel: the smallest ones whose tiles fit this budget per frame (640x480: L4-L7,
-// 114 tiles, 180K px); SPSLAM_ORB_SMALL_LEVELS=0 keeps one launch per level (A/B)
+// levels fused into level_small_kernel (SPSLAM_ORB_SMALL_LEVELS=1): the smallest ones whose tiles fit this
+// budget per frame (640x480: L4-L7, 114 tiles, 180K px).  Off by default: one launch per level measured 38.8K
+// against 37.0K frames/s on the pipelined C2 step (profiles/r04/ab_small_levels.txt) -- the fused kernel's
+// 256 workgroups serialise four levels that the per-level launches spread over the whole chip.
 constexpr int kSmallLevelTiles = 128;
 static bool small_levels_off() {
     static const bool off = [] {
         const char* e = getenv("SPSLAM_ORB_SMALL_LEVELS");
-        return e && e[0] == '0';
+        return !(e && e[0] == '1');
     }();
     return off;
 }

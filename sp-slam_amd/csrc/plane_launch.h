@@ -32,12 +32,13 @@ struct PlaneBuffers {
     double* integral;    // [F][(W+1)*(H+2)][6]  (dx xyz, dy xyz); row H+1 absorbs padding lanes
     float* normal;       // [F][3][N]
     float* pd;           // [F][N]  plane_d = p . n
-    uint32_t* labels;    // [F][N]
+    uint32_t* labels;    // [F][N] connected-component labels (global instance: also its union-find parents)
     int* work;           // [F][N + 4*N] misc (ranks, sizes, member lists)
     int* grown;          // [F][N] refinement grow events (target | model << 24), reference order
     uint8_t* maps;       // [F][2N] component tag / model map + contour masks (when not in LDS)
     long long* ts;       // [F][16] segmentation phase stamps (s_memrealtime, 100 MHz), diagnostics
     long long cloud_fs, wave_fs, dist_fs, integral_fs, normal_fs, pd_fs, labels_fs, work_fs, grown_fs, maps_fs;
+    int keep_labels;     // the LDS instance also stores the connected-component labels in `labels` (test hook)
 };
 
 // Skewed wavefront layout: entry (st, r) = cloud cell (r, c = st - 2r), the cell wavefront step st
@@ -62,6 +63,8 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
                         int32_t* inliers, int32_t* contours, hipStream_t s, KernelTimer* timer);
 
 // Segmentation stage alone (plane_segment.hip); needs cloud/normal/pd filled.
+// dynamic LDS bytes of the segmentation kernel; *in_lds: the per-frame maps (and 16-bit labels) live in LDS
+size_t plane_segment_lds_bytes(const PlaneGeom& g, bool* in_lds);
 hipError_t plane_segment_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, spslam_plane* planes,
                                 int* plane_counts, int planes_cap, int32_t* inliers, int32_t* contours,
                                 hipStream_t s);

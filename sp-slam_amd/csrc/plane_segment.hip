@@ -63,7 +63,6 @@ struct SegShared {
     int misc[8];
     int nbig;
     int big_label[kMaxBig];
-    int big_root[kMaxBig];
     int big_size[kMaxBig];
     int big_off[kMaxBig];
     float big_par[kMaxBig][4];
@@ -103,6 +102,44 @@ __device__ void uf_union(int* P, int a, int b) {
         if (old == a) return;
         a = uf_find(P, old);
         b = uf_find(P, b);
+    }
+}
+
+// The LDS instance's parents: 16-bit pixel indices (N < 0xFFFF), kNone16 = invalid point; the same 2N bytes later
+// hold the tag / model map and the contour masks.  gfx950's LDS has no 16-bit min, so the link is a 32-bit
+// compare-and-swap on the word holding the entry.
+constexpr uint32_t kNone16 = 0xFFFFu;
+__device__ __forceinline__ int ld16(const uint16_t* P, int x) {
+    return __hip_atomic_load(&P[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int uf_find16(const uint16_t* P, int x) {
+    int p = ld16(P, x);
+    while (p != x) { x = p; p = ld16(P, x); }
+    return x;
+}
+// P[a] = min(P[a], b); returns the previous P[a]
+__device__ __forceinline__ int fetch_min16(uint16_t* P, int a, int b) {
+    uint32_t* w = (uint32_t*)P + (a >> 1);
+    const int sh = (a & 1) << 4;
+    uint32_t old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (true) {
+        const int cur = (int)((old >> sh) & 0xFFFFu);
+        if (cur <= b) return cur;
+        const uint32_t nw = (old & ~(0xFFFFu << sh)) | ((uint32_t)b << sh);
+        if (__hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+            return cur;
+    }
+}
+__device__ void uf_union16(uint16_t* P, int a, int b) {
+    a = uf_find16(P, a);
+    b = uf_find16(P, b);
+    while (a != b) {
+        if (a < b) { const int t = a; a = b; b = t; }
+        const int old = fetch_min16(P, a, b);
+        if (old == a) return;
+        a = uf_find16(P, old);
+        b = uf_find16(P, b);
     }
 }
 
@@ -484,25 +521,33 @@ __device__ __forceinline__ uint32_t fn_scan(uint32_t x) {
     return x;
 }
 
-// Descriptor of point i for one pass (see above).
+// Descriptor of point i for one pass (see above).  Point validity (isfinite(x)) comes from the valid-point
+// bitmap ok[H][RW]; the backward pass reuses the forward pass's accept set `prev` (a point unlabelled now was
+// unlabelled then), so only the forward pass reads coordinates.
 template <class D>
 __device__ __forceinline__ uint32_t refine_desc(const uint8_t* state, const float* X, const float* Y, const float* Z,
-                                                const float (*coef)[4], int nmodel, int W, int H, int i, bool bw) {
+                                                const uint64_t* ok, int RW, const float (*coef)[4], int nmodel,
+                                                int W, int H, int i, bool bw, uint32_t prev) {
     if (state[i]) return 0;
-    const float x = X[i], y = Y[i], z = Z[i];
-    if (!isfinite(x)) return 0;
-    uint32_t acc = 0;
-    for (int v = 0; v < nmodel; v++)
-        if (ptp_ok(coef[v], x, y, z)) acc |= 1u << v;
-    if (!acc) return 0;
     const int r = i / W, c = i - r * W;
+    auto valid = [&](int rr, int cc) { return (bool)((ok[rr * RW + (cc >> 6)] >> (cc & 63)) & 1ull); };
+    uint32_t acc = 0;
+    if (!bw) {
+        if (!valid(r, c)) return 0;
+        const float x = X[i], y = Y[i], z = Z[i];
+        for (int v = 0; v < nmodel; v++)
+            if (ptp_ok(coef[v], x, y, z)) acc |= 1u << v;
+    } else {
+        acc = prev & D::kAcc;
+    }
+    if (!acc) return 0;
     bool act, link;
     if (!bw) {  // sources (r-1, c) [needs (r-1, c+1)] and (r, c-1)
-        act = r >= 1 && c <= W - 2 && isfinite(X[i - W]) && isfinite(X[i - W + 1]);
-        link = c >= 1 && r <= H - 2 && isfinite(X[i - 1]);
+        act = r >= 1 && c <= W - 2 && valid(r - 1, c) && valid(r - 1, c + 1);
+        link = c >= 1 && r <= H - 2 && valid(r, c - 1);
     } else {    // sources (r+1, c) [needs flat index before it] and flat i+1 (row wrap at c = W-1)
-        act = r <= H - 2 && isfinite(X[i + W]) && isfinite(X[i + W - 1]);
-        link = (c <= W - 2 ? r >= 1 : r <= H - 2) && isfinite(X[i + 1]);
+        act = r <= H - 2 && valid(r + 1, c) && (c >= 1 ? valid(r + 1, c - 1) : valid(r, W - 1));
+        link = (c <= W - 2 ? r >= 1 && valid(r, c + 1) : r <= H - 2 && valid(r + 1, 0));
     }
     return acc | (act ? D::kAct : 0u) | (link ? D::kLink : 0u);
 }
@@ -702,8 +747,10 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     const int W = g.W, H = g.H, N = g.N, RW = (W + 63) >> 6;
     uint64_t* hbits = (uint64_t*)dyn;      // comparator edge to the left neighbour, [H][RW]
     uint64_t* vbits = hbits + H * RW;      // comparator edge to the upper neighbour
-    uint8_t* state = kLdsMaps ? (uint8_t*)(vbits + H * RW) : b.maps + f * b.maps_fs;  // [N] tag / model+1
-    uint8_t* nmask = state + N;                                                        // [N] contour masks
+    uint64_t* okbits = vbits + H * RW;     // valid points
+    uint8_t* state = kLdsMaps ? (uint8_t*)(okbits + H * RW) : b.maps + f * b.maps_fs;  // [N] tag / model+1
+    uint8_t* nmask = state + N;                                                         // [N] contour masks
+    uint16_t* P16 = (uint16_t*)state;      // LDS instance: parents, then labels (phases A-F)
     const float* X = b.cloud + f * b.cloud_fs;
     const float* Y = X + N;
     const float* Z = X + 2 * N;
@@ -711,11 +758,10 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     const float* Ny = Nx + N;
     const float* Nz = Nx + 2 * N;
     const float* PD = b.pd + f * b.pd_fs;
-    int* P = (int*)(b.labels + f * b.labels_fs);   // parents, then labels (-1 = invalid point)
-    int* rankA = b.work + f * b.work_fs;           // [N] label of each root pixel
+    int* P = (int*)(b.labels + f * b.labels_fs);   // global instance: parents, then labels (-1 = invalid point)
+    int* rankA = b.work + f * b.work_fs;           // [N] global instance: label of each root pixel
     int* sizes = rankA + N;                        // [N] per label (big ones: -(index+1))
-    int* rootOf = sizes + N;                       // [N] root pixel of each label
-    int* members = rootOf + N;                     // [N] member lists of big components
+    int* members = sizes + 2 * N;                  // [N] member lists of big components
     int* ev = b.grown + f * b.grown_fs;            // [N] grow events: target | model << 24
     spslam_plane* planes = planes_out + (size_t)f * planes_cap;
     int32_t* inl = inliers_out + (size_t)f * g.inlier_cap;
@@ -725,9 +771,11 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     STAMP(15);
     if (t < kMaxPlanesPerFrame) S.model_grown[t] = 0;
 
-    // PlaneCoefficientComparator::compare (i1 = current, i2 = neighbour)
+    // PlaneCoefficientComparator::compare (i1 = current, i2 = neighbour).  Its z = x * 0 + y * 0 + z * 1: a
+    // cloud point's x, y and z are finite or NaN together (plane_cloud_kernel), so z * z is Z * Z bit for bit
+    // (a zero's sign aside, which the square drops) and x, y are not read.
     auto cmp = [&](int i1, int i2) {
-        const float z = X[i1] * 0.f + Y[i1] * 0.f + Z[i1] * 1.f;
+        const float z = Z[i1];
         float threshold = g.dist_th;
         threshold *= z * z;
         const float nd = Nx[i1] * Nx[i2] + Ny[i1] * Ny[i2] + Nz[i1] * Nz[i2];
@@ -744,16 +792,19 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             const int i = r * W + c;
             bool h = false, v = false, valid = false;
             if (in) {
-                valid = isfinite(X[i]);
+                valid = isfinite(Z[i]);  // (isfinite(x), see cmp)
                 h = c >= 1 && cmp(i, i - 1);
                 v = r >= 1 && cmp(i, i - W);
             }
-            const uint64_t hb = __ballot(h), vb = __ballot(v);
-            if (lane == 0) { hbits[r * RW + k] = hb; vbits[r * RW + k] = vb; }
+            const uint64_t hb = __ballot(h), vb = __ballot(v), ob = __ballot(valid);
+            if (lane == 0) { hbits[r * RW + k] = hb; vbits[r * RW + k] = vb; okbits[r * RW + k] = ob; }
             const uint64_t sb = __ballot(in && !h);
             const uint64_t upto = lane == 63 ? sb : (sb & ((2ull << lane) - 1ull));
             const int head = upto ? r * W + (k << 6) + 63 - __clzll(upto) : carry;
-            if (in) P[i] = valid ? head : -1;
+            if (in) {
+                if constexpr (kLdsMaps) P16[i] = (uint16_t)(valid ? head : (int)kNone16);
+                else P[i] = valid ? head : -1;
+            }
             carry = __shfl(head, 63);
         }
     }
@@ -764,25 +815,47 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         const int r = i / W, c = i - r * W;
         if (!bit(vbits, r, c)) continue;
         if (c >= 1 && bit(hbits, r, c) && bit(hbits, r - 1, c) && bit(vbits, r, c - 1)) continue;
-        uf_union(P, ld_wg(&P[i]), ld_wg(&P[i - W]));
+        if constexpr (kLdsMaps) uf_union16(P16, ld16(P16, i), ld16(P16, i - W));
+        else uf_union(P, ld_wg(&P[i]), ld_wg(&P[i - W]));
     }
     block_sync();
     STAMP(1);
     // ---- C: flatten
     for (int i = t; i < N; i += kSegThreads) {
-        const int p = P[i];
-        if (p >= 0) P[i] = uf_find(P, p);
+        if constexpr (kLdsMaps) {
+            const int p = P16[i];
+            if (p != (int)kNone16) P16[i] = (uint16_t)uf_find16(P16, p);
+        } else {
+            const int p = P[i];
+            if (p >= 0) P[i] = uf_find(P, p);
+        }
     }
     block_sync();
     STAMP(2);
-    // ---- D: labels = rank of the root; sizes
+    // ---- D: labels = rank of the root; sizes.  The LDS instance relabels in place: a root's entry becomes its
+    //         label (its lanes remember which pixels were roots), then every other pixel reads its root's entry.
     const int span = (N + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
+    // component sizes: one atomic per run of equal labels among a wave's 64 pixels
+    auto count_run = [&](int L) {
+        const int prevL = __shfl_up(L, 1);
+        const bool chg = lane == 0 || prevL != L;
+        const uint64_t cb = __ballot(chg);
+        if (chg && L >= 0) {
+            const uint64_t rest = lane == 63 ? 0ull : (cb >> (lane + 1));
+            const int len = rest ? __builtin_ctzll(rest) + 1 : 64 - lane;
+            atomicAdd(&sizes[L], len);
+        }
+    };
+    auto is_root = [&](int i) {
+        if constexpr (kLdsMaps) return (int)P16[i] == i;
+        else return P[i] == i;
+    };
     {
         const int w0 = wave * span, w1 = min(N, w0 + span);
         int cnt = 0;
         for (int base = w0; base < w1; base += 64) {
             const int i = base + lane;
-            cnt += __popcll(__ballot(i < w1 && P[i] == i));
+            cnt += __popcll(__ballot(i < w1 && is_root(i)));
         }
         if (lane == 0) S.wsum[wave] = cnt;
         __syncthreads();
@@ -791,36 +864,44 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             if (j < wave) wb += S.wsum[j];
             ncomp += S.wsum[j];
         }
-        for (int base = w0; base < w1; base += 64) {
+        uint64_t rmask = 0;  // (LDS instance) chunk k of this lane's pixels: bit k = root
+        for (int base = w0, k = 0; base < w1; base += 64, k++) {
             const int i = base + lane;
-            const bool root = i < w1 && P[i] == i;
+            const bool root = i < w1 && is_root(i);
             const uint64_t m = __ballot(root);
             if (root) {
                 const int L = wb + __popcll(m & lanemask_lt());
-                rankA[i] = L;
-                rootOf[L] = i;
+                if constexpr (kLdsMaps) {
+                    P16[i] = (uint16_t)L;
+                    rmask |= 1ull << k;
+                } else {
+                    rankA[i] = L;
+                }
             }
             wb += __popcll(m);
         }
         for (int k = t; k < ncomp; k += kSegThreads) sizes[k] = 0;
         if (t == 0) S.misc[1] = ncomp;
-    }
-    block_sync();
-    for (int base = 0; base < N; base += kSegThreads) {
-        const int i = base + t;
-        int L = -1;
-        if (i < N) {
-            const int p = P[i];
-            if (p >= 0) L = rankA[p];
-            P[i] = L;
-        }
-        const int prevL = __shfl_up(L, 1);
-        const bool chg = lane == 0 || prevL != L;
-        const uint64_t cb = __ballot(chg);
-        if (chg && L >= 0) {
-            const uint64_t rest = lane == 63 ? 0ull : (cb >> (lane + 1));
-            const int len = rest ? __builtin_ctzll(rest) + 1 : 64 - lane;
-            atomicAdd(&sizes[L], len);
+        block_sync();
+        for (int base = w0, k = 0; base < w1; base += 64, k++) {
+            const int i = base + lane;
+            int L = -1;
+            if (i < w1) {
+                if constexpr (kLdsMaps) {
+                    const int p = P16[i];
+                    if (p != (int)kNone16) {
+                        const bool root = (rmask >> k) & 1ull;
+                        L = root ? p : (int)P16[p];
+                        if (!root) P16[i] = (uint16_t)L;
+                    }
+                    if (b.keep_labels) P[i] = L;
+                } else {
+                    const int p = P[i];
+                    if (p >= 0) L = rankA[p];
+                    P[i] = L;
+                }
+            }
+            count_run(L);
         }
     }
     block_sync();
@@ -851,7 +932,6 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             if (big && j < kMaxBig) {
                 S.big_label[j] = L;
                 S.big_size[j] = sizes[L];
-                S.big_root[j] = rootOf[L];
             }
             wb += __popcll(m);
         }
@@ -867,76 +947,109 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     block_sync();
     const int nbig = S.nbig;
     // ---- F: per-pixel component tag
-    for (int i = t; i < N; i += kSegThreads) {
-        const int L = P[i];
-        int s = 0;
-        if (L >= 0) {
-            const int z = sizes[L];
-            s = z < 0 ? -z : 0;
+    auto tag_of = [&](int L) {
+        if (L < 0) return 0;
+        const int z = sizes[L];
+        return z < 0 ? -z : 0;
+    };
+    if constexpr (kLdsMaps) {
+        // the byte map overwrites the 16-bit labels: block j's tags (bytes [b0, b0 + 4T) = labels [b0 / 2, ...))
+        // are stored once every label of the block is read; they cover labels of earlier blocks only
+        constexpr int kU = 4;
+        for (int b0 = 0; b0 < N; b0 += kU * kSegThreads) {
+            int tg[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int i = b0 + u * kSegThreads + t;
+                const int L = i < N ? (int)P16[i] : (int)kNone16;
+                tg[u] = tag_of(L == (int)kNone16 ? -1 : L);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int i = b0 + u * kSegThreads + t;
+                if (i < N) state[i] = (uint8_t)tg[u];
+            }
         }
-        state[i] = (uint8_t)s;
+    } else {
+        for (int i = t; i < N; i += kSegThreads) state[i] = (uint8_t)tag_of(P[i]);
     }
     block_sync();
     STAMP(5);
-    // ---- G: member lists + mean/covariance in PCL's float accumulation order
-    for (int j = wave; j < nbig; j += kSegWaves) {
-        const int n = S.big_size[j], o = S.big_off[j], tag = j + 1;
-        float* st = &S.stage[wave][0][0];
-        float acc = 0.f;
-        int found = 0;
-        // the cloud is scanned in chunks of 64 points from the region's first member; coordinates are
-        // loaded one group of 4 chunks ahead (consumed from registers of the group before, so the wait
-        // for them does not cover the chunks' member-list stores)
-        const int start = S.big_root[j] & ~63;
-        float cx[4], cy[4], cz[4];
-        auto load_group = [&](int b0, float* gx, float* gy, float* gz) __attribute__((always_inline)) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = b0 + 64 * u + lane;
-                gx[u] = i < N ? X[i] : 0.f;
-                gy[u] = i < N ? Y[i] : 0.f;
-                gz[u] = i < N ? Z[i] : 0.f;
-            }
-        };
-        load_group(start, cx, cy, cz);
-        for (int b0 = start; found < n && b0 < N; b0 += 256) {
-            float nx[4], ny[4], nz[4];
-            load_group(b0 + 256, nx, ny, nz);
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int base = b0 + 64 * u;
-                if (found >= n || base >= N) continue;
+    // ---- G: member lists of the big components in raster order (each wave counts its stripe's members per
+    //         component, a prefix over the stripes places them), then per component, one wave: PCL's float
+    //         mean/covariance accumulation over its member list (terms staged through LDS, nine lanes each own
+    //         one accumulator, so the sums are the reference's sequence; a chunk's zero padding adds nothing)
+    {
+        uint32_t(*cnt)[256] = (uint32_t(*)[256]) & S.stage[0][0][0];
+        static_assert(sizeof(S.stage) >= sizeof(uint32_t) * kSegWaves * 256, "member counters");
+        for (int k = t; k < kSegWaves * 256; k += kSegThreads) (&cnt[0][0])[k] = 0;
+        __syncthreads();
+        const int w0 = wave * span, w1 = min(N, w0 + span);
+        // one round per distinct tag of a 64-pixel chunk
+        auto stripe = [&](bool place) {
+            for (int base = w0; base < w1; base += 64) {
                 const int i = base + lane;
-                const bool m = i < N && state[i] == tag;
-                const uint64_t mk = __ballot(m);
-                if (mk) {
-                    const int cnt = __popcll(mk), pos = __popcll(mk & lanemask_lt()), pad = (cnt + 3) & ~3;
-                    if (m) {
-                        const float px = cx[u], py = cy[u], pz = cz[u];
-                        members[o + found + pos] = i;
-                        st[0 * 64 + pos] = px * px; st[1 * 64 + pos] = px * py; st[2 * 64 + pos] = px * pz;
-                        st[3 * 64 + pos] = py * py; st[4 * 64 + pos] = py * pz; st[5 * 64 + pos] = pz * pz;
-                        st[6 * 64 + pos] = px; st[7 * 64 + pos] = py; st[8 * 64 + pos] = pz;
-                    }
-                    if (lane >= cnt && lane < pad)
-                        for (int q = 0; q < 9; q++) st[q * 64 + lane] = 0.f;
-                    wave_sync();
-                    if (lane < 9) {
-                        const float4* row = (const float4*)(st + lane * 64);
-                        for (int q = 0; q < (pad >> 2); q++) {
-                            const float4 v = row[q];
-                            acc += v.x;
-                            acc += v.y;
-                            acc += v.z;
-                            acc += v.w;
-                        }
-                    }
-                    wave_sync();
-                    found += cnt;
+                const int tg = i < w1 ? (int)state[i] : 0;
+                uint64_t rem = __ballot(tg != 0);
+                while (rem) {
+                    const int tq = __shfl(tg, __builtin_ctzll(rem));
+                    const uint64_t m = __ballot(tg == tq);
+                    if (place && tg == tq) members[(int)cnt[wave][tq] + __popcll(m & lanemask_lt())] = i;
+                    if (lane == 0) cnt[wave][tq] += __popcll(m);
+                    rem &= ~m;
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) { cx[u] = nx[u]; cy[u] = ny[u]; cz[u] = nz[u]; }
+        };
+        stripe(false);
+        __syncthreads();
+        for (int j = t; j < nbig; j += kSegThreads) {
+            int o = S.big_off[j];
+            for (int w = 0; w < kSegWaves; w++) {
+                const int c = (int)cnt[w][j + 1];
+                cnt[w][j + 1] = o;
+                o += c;
+            }
+        }
+        __syncthreads();
+        stripe(true);
+        __syncthreads();
+    }
+    for (int j = wave; j < nbig; j += kSegWaves) {
+        const int n = S.big_size[j], o = S.big_off[j];
+        float* st = &S.stage[wave][0][0];
+        float acc = 0.f;
+        // member indices two chunks ahead, coordinates one chunk ahead
+        auto idx_at = [&](int c0) { return c0 + lane < n ? members[o + c0 + lane] : -1; };
+        int icur = idx_at(0), inext = idx_at(64);
+        float px = 0.f, py = 0.f, pz = 0.f;
+        if (icur >= 0) { px = X[icur]; py = Y[icur]; pz = Z[icur]; }
+        for (int c0 = 0; c0 < n; c0 += 64) {
+            const int i2 = idx_at(c0 + 128);
+            float nx = 0.f, ny = 0.f, nz = 0.f;
+            if (inext >= 0) { nx = X[inext]; ny = Y[inext]; nz = Z[inext]; }
+            const int cnt = min(64, n - c0), pad = (cnt + 3) & ~3;
+            if (lane < cnt) {
+                st[0 * 64 + lane] = px * px; st[1 * 64 + lane] = px * py; st[2 * 64 + lane] = px * pz;
+                st[3 * 64 + lane] = py * py; st[4 * 64 + lane] = py * pz; st[5 * 64 + lane] = pz * pz;
+                st[6 * 64 + lane] = px; st[7 * 64 + lane] = py; st[8 * 64 + lane] = pz;
+            } else if (lane < pad) {
+                for (int q = 0; q < 9; q++) st[q * 64 + lane] = 0.f;
+            }
+            wave_sync();
+            if (lane < 9) {
+                const float4* row = (const float4*)(st + lane * 64);
+                for (int q = 0; q < (pad >> 2); q++) {
+                    const float4 v = row[q];
+                    acc += v.x;
+                    acc += v.y;
+                    acc += v.z;
+                    acc += v.w;
+                }
+            }
+            wave_sync();
+            px = nx; py = ny; pz = nz;
+            inext = i2;
         }
         if (lane < 9) acc /= (float)n;
         float a[9];
@@ -1018,7 +1131,8 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                     const int c = (k << 6) + lane, i = r * W + c;
                     uint32_t dsc = 0;
                     if (c < W) {
-                        dsc = refine_desc<D>(state, X, Y, Z, S.model_coef, nmodel, W, H, i, bw);
+                        dsc = refine_desc<D>(state, X, Y, Z, okbits, RW, S.model_coef, nmodel, W, H, i, bw,
+                                             bw ? desc.get(i) : 0u);
                         desc.put(i, dsc);
                     }
                     const uint64_t m = __ballot(dsc != 0);
@@ -1189,11 +1303,13 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
 
 size_t plane_segment_lds_bytes(const PlaneGeom& g, bool* in_lds) {
     const size_t RW = (g.W + 63) / 64;
-    const size_t bits = 2 * g.H * RW * sizeof(uint64_t);
+    const size_t bits = 3 * g.H * RW * sizeof(uint64_t);
     const size_t maps = ((size_t)2 * g.N + 15) / 16 * 16;
-    // the LDS instance also keeps the refinement descriptors' high bytes in SegShared::stage
+    // the LDS instance also keeps the refinement descriptors' high bytes in SegShared::stage, its parents are
+    // 16-bit (kNone16 reserved) and its relabelling marks roots in one 64-bit mask per lane
     const bool fits = sizeof(planes::SegShared) + bits + maps <= (size_t)planes::kLdsBytes &&
-                      (size_t)g.N <= sizeof(planes::SegShared::stage);
+                      (size_t)g.N <= sizeof(planes::SegShared::stage) && g.N < (int)planes::kNone16 &&
+                      g.N <= 64 * planes::kSegThreads;
     if (in_lds) *in_lds = fits;
     return bits + (fits ? maps : 0);
 }

@@ -796,6 +796,12 @@ int spslam_debug_pose_spin_cap(spslam_ctx* c, int cap) {
     return SPSLAM_OK;
 }
 
+int spslam_debug_plane_labels(spslam_ctx* c, int keep) {
+    if (!c) return SPSLAM_ERR_ARG;
+    c->pb.keep_labels = keep ? 1 : 0;
+    return SPSLAM_OK;
+}
+
 int spslam_debug_libm64(spslam_ctx* c, int kind, const double* a, const double* b, int n, double* out) {
     if (!c || n < 0 || kind < 0 || kind > 3 || (n && (!a || !out || (kind == 2 && !b)))) return SPSLAM_ERR_ARG;
     if (!n) return SPSLAM_OK;
@@ -868,6 +874,10 @@ int spslam_planes_debug(spslam_ctx* c, int frame, int what, void* out, int* n_po
         return SPSLAM_OK;
     }
     if (what == 3) {
+        bool in_lds = false;
+        plane_segment_lds_bytes(c->pg, &in_lds);
+        if (in_lds && !b.keep_labels)
+            return fail(c, SPSLAM_ERR_NOT_READY, "labels are kept only after spslam_debug_plane_labels(ctx, 1)%s", "");
         HIP_CHECK(c, hipMemcpy(out, b.labels + frame * b.labels_fs, N * 4, hipMemcpyDeviceToHost));
         return SPSLAM_OK;
     }

@@ -29,7 +29,8 @@ LINE_CAND_DTYPE = np.dtype([("line", "<f4", 6), ("n_inliers", "<i4"), ("iteratio
 
 
 spslam_gpu.EXPORTED += ["spslam_planes_configure", "spslam_planes_capacity", "spslam_planes_extract",
-                        "spslam_planes_extract_batch_device", "spslam_planes_debug", "spslam_supposed_capacity",
+                        "spslam_planes_extract_batch_device", "spslam_planes_debug", "spslam_debug_plane_labels",
+                        "spslam_supposed_capacity",
                         "spslam_planes_generate_from_boundaries",
                         "spslam_planes_generate_from_boundaries_batch_device", "spslam_supposed_debug",
                         "spslam_planes_select_cloud_set",
@@ -122,6 +123,11 @@ class PlaneExtractor:
         self.ex._check(self.ex.lib.spslam_planes_extract_batch_device(
             self.ex.ctx, depth_ptr, n_frames, frame_stride, stride, planes_ptr, counts_ptr, inliers_ptr,
             contours_ptr, stream or None))
+
+    def keep_labels(self, on=True):
+        """Test hook: store the connected-component labels (debug(frame, 3)) on later extractions."""
+        self.ex.lib.spslam_debug_plane_labels.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        self.ex._check(self.ex.lib.spslam_debug_plane_labels(self.ex.ctx, int(on)))
 
     def debug(self, frame, what):
         N = self.W * self.H

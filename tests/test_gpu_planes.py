@@ -20,6 +20,7 @@ def ctx():
     K = synth.TUM3
     ex = spslam_gpu.OrbExtractor(max_batch=4)
     pe = spslam_planes.PlaneExtractor(ex, K["fx"], K["fy"], K["cx"], K["cy"])
+    pe.keep_labels()
     yield ex, pe
     ex.close()
 

@@ -9,6 +9,6 @@ export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=8
 CFG=${1:-c2}
 TAG=${2:-pmc}
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_pmc_fetch_${CFG} -o run -- python3 bench.py --config ${CFG} --steps 3 --warmup 1 --no-cpu-baseline --ate-frames 0 > gpurun_out/${TAG}_pmc_fetch_${CFG}.log 2>&1 && \
-timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_pmc_write_${CFG} -o run -- python3 bench.py --config ${CFG} --steps 3 --warmup 1 --no-cpu-baseline --ate-frames 0 > gpurun_out/${TAG}_pmc_write_${CFG}.log 2>&1 && \
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_pmc_fetch_${CFG} -o run -- python3 bench.py --config ${CFG} --steps 3 --warmup 1 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0 > gpurun_out/${TAG}_pmc_fetch_${CFG}.log 2>&1 && \
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d gpurun_out/${TAG}_pmc_write_${CFG} -o run -- python3 bench.py --config ${CFG} --steps 3 --warmup 1 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0 > gpurun_out/${TAG}_pmc_write_${CFG}.log 2>&1 && \
 python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc_fetch_${CFG} gpurun_out/${TAG}_pmc_write_${CFG} gpurun_out/${TAG}_pmc_${CFG}.json
