@@ -1311,6 +1311,9 @@ __device__ __noinline__ void build_system() {
         __syncthreads();
 #endif
         // (A) edges on thread pairs (the plane edges' Jacobians from plane_jacobians)
+#ifdef SPSLAM_LBG_A_TWICE  // measurement variant: phase (A) evaluated twice (its writes are idempotent but pm's)
+        for (int rep_a = 0; rep_a < 2; rep_a++)
+#endif
         {
             const int row = t >> 1, e = c0 + row;
             if (row < cnt && g.e_level[e] == 0) {

@@ -761,7 +761,15 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     int* P = (int*)(b.labels + f * b.labels_fs);   // global instance: parents, then labels (-1 = invalid point)
     int* rankA = b.work + f * b.work_fs;           // [N] global instance: label of each root pixel
     int* sizes = rankA + N;                        // [N] per label (big ones: -(index+1))
-    int* members = sizes + 2 * N;                  // [N] member lists of big components
+    int* members = sizes + 2 * N;                  // [N] member lists of big components (LDS instance: 16-bit)
+    auto mem_at = [&](int k) -> int {
+        if constexpr (kLdsMaps) return ((const uint16_t*)members)[k];
+        else return members[k];
+    };
+    auto mem_put = [&](int k, int i) {
+        if constexpr (kLdsMaps) ((uint16_t*)members)[k] = (uint16_t)i;
+        else members[k] = i;
+    };
     int* ev = b.grown + f * b.grown_fs;            // [N] grow events: target | model << 24
     spslam_plane* planes = planes_out + (size_t)f * planes_cap;
     int32_t* inl = inliers_out + (size_t)f * g.inlier_cap;
@@ -835,7 +843,16 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     // ---- D: labels = rank of the root; sizes.  The LDS instance relabels in place: a root's entry becomes its
     //         label (its lanes remember which pixels were roots), then every other pixel reads its root's entry.
     const int span = (N + kSegWaves * 64 - 1) / (kSegWaves * 64) * 64;
-    // component sizes: one atomic per run of equal labels among a wave's 64 pixels
+    // component sizes: one atomic per run of equal labels among a wave's 64 pixels.  The LDS instance counts in
+    // 16-bit halves of the (still unused) covariance staging area when the labels fit (a count <= N < 2^16 never
+    // carries into the next half); after phase E the same halves hold each label's tag.
+    uint32_t* sz16 = (uint32_t*)&S.stage[0][0][0];
+    constexpr int kSz16 = (int)(sizeof(S.stage) / sizeof(uint16_t));
+    bool lsz = false;
+    auto size_of = [&](int L) -> int {
+        if (lsz) return (int)((sz16[L >> 1] >> ((L & 1) << 4)) & 0xFFFFu);
+        return sizes[L];
+    };
     auto count_run = [&](int L) {
         const int prevL = __shfl_up(L, 1);
         const bool chg = lane == 0 || prevL != L;
@@ -843,7 +860,8 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         if (chg && L >= 0) {
             const uint64_t rest = lane == 63 ? 0ull : (cb >> (lane + 1));
             const int len = rest ? __builtin_ctzll(rest) + 1 : 64 - lane;
-            atomicAdd(&sizes[L], len);
+            if (lsz) atomicAdd(&sz16[L >> 1], (uint32_t)len << ((L & 1) << 4));
+            else atomicAdd(&sizes[L], len);
         }
     };
     auto is_root = [&](int i) {
@@ -880,7 +898,12 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             }
             wb += __popcll(m);
         }
-        for (int k = t; k < ncomp; k += kSegThreads) sizes[k] = 0;
+        lsz = kLdsMaps && ncomp <= kSz16;
+        if (lsz) {
+            for (int k = t; k < (ncomp + 1) >> 1; k += kSegThreads) sz16[k] = 0;
+        } else {
+            for (int k = t; k < ncomp; k += kSegThreads) sizes[k] = 0;
+        }
         if (t == 0) S.misc[1] = ncomp;
         block_sync();
         for (int base = w0, k = 0; base < w1; base += 64, k++) {
@@ -914,7 +937,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         int cnt = 0;
         for (int base = w0; base < w1; base += 64) {
             const int L = base + lane;
-            cnt += __popcll(__ballot(L < w1 && (unsigned)sizes[L] > (unsigned)g.min_size));
+            cnt += __popcll(__ballot(L < w1 && (unsigned)size_of(L) > (unsigned)g.min_size));
         }
         __syncthreads();
         if (lane == 0) S.wsum[wave] = cnt;
@@ -926,12 +949,12 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         }
         for (int base = w0; base < w1; base += 64) {
             const int L = base + lane;
-            const bool big = L < w1 && (unsigned)sizes[L] > (unsigned)g.min_size;
+            const bool big = L < w1 && (unsigned)size_of(L) > (unsigned)g.min_size;
             const uint64_t m = __ballot(big);
             const int j = wb + __popcll(m & lanemask_lt());
             if (big && j < kMaxBig) {
                 S.big_label[j] = L;
-                S.big_size[j] = sizes[L];
+                S.big_size[j] = size_of(L);
             }
             wb += __popcll(m);
         }
@@ -942,13 +965,20 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             for (int j = 0; j < S.nbig; j++) { S.big_off[j] = off; off += S.big_size[j]; }
         }
         __syncthreads();
-        for (int j = t; j < S.nbig; j += kSegThreads) sizes[S.big_label[j]] = -(j + 1);
+        if (lsz) {  // the halves become tags: 0, or j + 1 for big component j
+            for (int k = t; k < (ncomp + 1) >> 1; k += kSegThreads) sz16[k] = 0;
+            __syncthreads();
+            for (int j = t; j < S.nbig; j += kSegThreads) ((uint16_t*)sz16)[S.big_label[j]] = (uint16_t)(j + 1);
+        } else {
+            for (int j = t; j < S.nbig; j += kSegThreads) sizes[S.big_label[j]] = -(j + 1);
+        }
     }
     block_sync();
     const int nbig = S.nbig;
     // ---- F: per-pixel component tag
     auto tag_of = [&](int L) {
         if (L < 0) return 0;
+        if (lsz) return (int)((const uint16_t*)sz16)[L];
         const int z = sizes[L];
         return z < 0 ? -z : 0;
     };
@@ -995,7 +1025,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 while (rem) {
                     const int tq = __shfl(tg, __builtin_ctzll(rem));
                     const uint64_t m = __ballot(tg == tq);
-                    if (place && tg == tq) members[(int)cnt[wave][tq] + __popcll(m & lanemask_lt())] = i;
+                    if (place && tg == tq) mem_put((int)cnt[wave][tq] + __popcll(m & lanemask_lt()), i);
                     if (lane == 0) cnt[wave][tq] += __popcll(m);
                     rem &= ~m;
                 }
@@ -1020,7 +1050,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         float* st = &S.stage[wave][0][0];
         float acc = 0.f;
         // member indices two chunks ahead, coordinates one chunk ahead
-        auto idx_at = [&](int c0) { return c0 + lane < n ? members[o + c0 + lane] : -1; };
+        auto idx_at = [&](int c0) { return c0 + lane < n ? mem_at(o + c0 + lane) : -1; };
         int icur = idx_at(0), inext = idx_at(64);
         float px = 0.f, py = 0.f, pz = 0.f;
         if (icur >= 0) { px = X[icur]; py = Y[icur]; pz = Z[icur]; }
@@ -1232,7 +1262,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
     for (int q = wave; q < nk; q += nlive) {
         const int m = S.kept[q], j = S.model_big[m], n = S.big_size[j], o = S.big_off[j];
         const int dst = planes[q].inlier_offset, lim = planes[q].n_inliers;
-        for (int k = lane; k < min(n, lim); k += 64) inl[dst + k] = members[o + k];
+        for (int k = lane; k < min(n, lim); k += 64) inl[dst + k] = mem_at(o + k);
         // contour start = the model's last inlier (segmentAndRefine's max_inlier_idx):
         // its last grow event, else its last component member
         int last = -1;
@@ -1244,7 +1274,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 break;
             }
         }
-        if (lane == 0) S.con_start[q] = last >= 0 ? last : members[o + n - 1];
+        if (lane == 0) S.con_start[q] = last >= 0 ? last : mem_at(o + n - 1);
         int w = n;
         for (int e0 = 0; e0 < ng; e0 += 64) {
             const int e = e0 + lane;
