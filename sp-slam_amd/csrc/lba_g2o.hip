@@ -1031,6 +1031,36 @@ __device__ __forceinline__ double ordered_sum(const PD* v, int n32) {
     return acc;
 }
 
+// the same over LDS, 16-byte reads: 8 loads per batch of 16 values, so the wait for one batch can leave the next
+// batch in flight (the LDS counter holds at most 15 outstanding loads; 16 single loads would force a full wait)
+__device__ __forceinline__ double ordered_sum_lds(const double* v, int n32) {
+    const double2* w = (const double2*)v;
+    double acc = 0.0;
+    double2 A[8], B[8];
+    const double2 z = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int u = 0; u < 8; u++) A[u] = n32 > 0 ? w[u] : z;
+    for (int e = 0; e < n32; e += 32) {
+        const int q = e >> 1;
+#pragma unroll
+        for (int u = 0; u < 8; u++) B[u] = w[q + 8 + u];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            acc += A[u].x;
+            acc += A[u].y;
+        }
+        const bool more = e + 32 < n32;
+#pragma unroll
+        for (int u = 0; u < 8; u++) A[u] = more ? w[q + 16 + u] : z;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            acc += B[u].x;
+            acc += B[u].y;
+        }
+    }
+    return acc;
+}
+
 // the ordered sums of a computeActiveErrors (activeRobustChi2: the edges' chi2 in edge order) and, for a trial
 // (nS > 0), of its scale (x . (lambda x + b), entry order): the operands staged in LDS by the whole workgroup
 // (coalesced), then one lane per sum -- the dependent add chains read LDS instead of global memory.  nS == 0:
@@ -1045,10 +1075,10 @@ __device__ __noinline__ void sums_staged(int nE, int nS) {
         for (int i = t; i < nS; i += kT) V[nE + i] = g.sc[i];
         __syncthreads();
         if (t == 0) {
-            const double c = ordered_sum(V, nE);
+            const double c = ordered_sum_lds(V, nE);
             if (nS > 0) s.tempChi = c; else s.currentChi = c;
         }
-        if (t == 64 && nS > 0) s.scale = ordered_sum(V + nE, nS);
+        if (t == 64 && nS > 0) s.scale = ordered_sum_lds(V + nE, nS);
     } else {
         if (t == 0) {
             const double c = ordered_sum(g.echi, nE);

@@ -135,7 +135,9 @@ __host__ __device__ inline void sincos_reduced(dd r, dd* s, dd* c) {
     const dd t = two_sum(r.hi - jf * 0.015625, r.lo);  // r.hi - j/64 is exact (Sterbenz)
     dd st, cm1;
     sin_cm1<kAccurate>(t, &st, &cm1);
-    const int aj = j < 0 ? -j : j;
+    // |j| <= 51 for every argument the reduction handles (|x| < 2^20 pi/2); the clamp only keeps a wild argument
+    // (a diverged LM step) from indexing past the table -- its result is then garbage, as the reduction's
+    const int aj = (int)fmin(fabs(jf), 64.0);
     const double sg = j < 0 ? -1.0 : 1.0;
     const dd S{sg * kSinCos64[aj][0], sg * kSinCos64[aj][1]}, C{kSinCos64[aj][2], kSinCos64[aj][3]};
     // sin(a + t) = S + (S (cos t - 1) + C sin t), cos(a + t) = C + (C (cos t - 1) - S sin t)
