@@ -250,21 +250,35 @@ __device__ __forceinline__ void huber(double chi, double delta, bool on, double*
     *rho0 = 2 * s * delta - dsqr;
     *rho1 = delta / s;
 }
-__device__ __forceinline__ void point_error(const G& g, int e, int t, const SE3& T, const gdouble* X, double* err) {
-    const auto& o = g.pobs[g.e_src[e]];
-    const auto& k = g.kf[g.e_kf[e]];
-    const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
+// A point edge's operands, loaded together (errors() gathers several edges' before evaluating any)
+struct PointIn {
+    SE3 T;
+    double X[3];
+    float u, v, ur, isg, fx, fy, cx, cy, bf;
+};
+__device__ __forceinline__ PointIn point_in(const G& g, int kf, int lm, int src) {
+    PointIn a;
+    a.T = load_pose(g.pose + 7 * kf);
+    for (int i = 0; i < 3; i++) a.X[i] = g.X[3 * lm + i];
+    const auto& o = g.pobs[src];
+    a.u = o.u; a.v = o.v; a.ur = o.ur; a.isg = o.inv_sigma2;
+    const auto& k = g.kf[kf];
+    a.fx = k.fx; a.fy = k.fy; a.cx = k.cx; a.cy = k.cy; a.bf = k.bf;
+    return a;
+}
+__device__ __forceinline__ void point_error_v(int t, const PointIn& a, double* err) {
+    const V3 p = q_rot(a.T.r, V3{a.X[0], a.X[1], a.X[2]}) + a.T.t;
     if (t == 0) {
-        err[0] = (double)o.u - (p.x / p.z * (double)k.fx + (double)k.cx);
-        err[1] = (double)o.v - (p.y / p.z * (double)k.fy + (double)k.cy);
+        err[0] = (double)a.u - (p.x / p.z * (double)a.fx + (double)a.cx);
+        err[1] = (double)a.v - (p.y / p.z * (double)a.fy + (double)a.cy);
         err[2] = 0.0;
     } else {
         const float invz = (float)(1.0f / p.z);
-        const double r0 = p.x * invz * (double)k.fx + (double)k.cx, r1 = p.y * invz * (double)k.fy + (double)k.cy;
-        const double r2 = r0 - (double)(k.bf * invz);  // cam_project(..., const float& bf)
-        err[0] = (double)o.u - r0;
-        err[1] = (double)o.v - r1;
-        err[2] = (double)o.ur - r2;
+        const double r0 = p.x * invz * (double)a.fx + (double)a.cx, r1 = p.y * invz * (double)a.fy + (double)a.cy;
+        const double r2 = r0 - (double)(a.bf * invz);  // cam_project(..., const float& bf)
+        err[0] = (double)a.u - r0;
+        err[1] = (double)a.v - r1;
+        err[2] = (double)a.ur - r2;
     }
 }
 __device__ bool depth_positive(const G& g, int e) {
@@ -966,19 +980,38 @@ __device__ __noinline__ void errors() {
     const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const bool robust = s.robust;
-    for (int e = t; e < g.Ep; e += kT) {
-        double chi = 0.0;
-        if (g.e_level[e] == 0) {
-            const int ty = g.e_type[e];
-            const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
-            double err[3], info[3];
-            point_error(g, e, ty, T, g.X + 3 * g.e_lm[e], err);
-            for (int i = 0; i < 3; i++) g.err[3 * e + i] = err[i];
-            info_of(g, C, e, ty, info);
-            double r1;
-            huber(chi2_of(err, info, edge_dim(ty)), delta_of(C, ty), robust, &chi, &r1);
+    // point edges, kEU per thread at a time: every edge's records, then every edge's operands, are loaded before
+    // any is evaluated (a dependent load chain per group instead of per edge)
+    constexpr int kEU = 3;
+    for (int e0 = t; e0 < g.Ep; e0 += kEU * kT) {
+        int lv[kEU], ty[kEU], kf[kEU], lm[kEU], src[kEU];
+#pragma unroll
+        for (int u = 0; u < kEU; u++) {
+            const int e = e0 + u * kT, ec = e < g.Ep ? e : e0;
+            lv[u] = e < g.Ep ? g.e_level[ec] : 1;
+            ty[u] = g.e_type[ec];
+            kf[u] = g.e_kf[ec];
+            lm[u] = g.e_lm[ec];
+            src[u] = g.e_src[ec];
         }
-        g.echi[e] = chi;
+        PointIn in[kEU];
+#pragma unroll
+        for (int u = 0; u < kEU; u++) in[u] = point_in(g, kf[u], lm[u], src[u]);
+#pragma unroll
+        for (int u = 0; u < kEU; u++) {
+            const int e = e0 + u * kT;
+            if (e >= g.Ep) break;
+            double chi = 0.0;
+            if (lv[u] == 0) {
+                double err[3];
+                point_error_v(ty[u], in[u], err);
+                for (int i = 0; i < 3; i++) g.err[3 * e + i] = err[i];
+                const double info[3] = {(double)in[u].isg, (double)in[u].isg, (double)in[u].isg};  // info_of, t <= 1
+                double r1;
+                huber(chi2_of(err, info, edge_dim(ty[u])), delta_of(C, ty[u]), robust, &chi, &r1);
+            }
+            g.echi[e] = chi;
+        }
     }
     // plane edges: one lane pair per edge (plane_error_pair)
     const int npl = g.E - g.Ep;
@@ -1617,11 +1650,14 @@ __device__ __noinline__ void schur() {
         auto prefetch = [&](int c) __attribute__((always_inline)) {
             const int h0 = g.sch[c], h1 = g.sch[c + 1], kb0 = g.sch_kb[c], kb1 = g.sch_kb[c + 1];
             const int nbk = kb1 - kb0, nh = h1 - h0;
+            const gdouble* pb = g.blkB + (size_t)18 * kb0;
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
                 const int i = t + q * kT;
                 double v = 0.0;
-                if (i < nbk * 18) v = g.blkB[(size_t)18 * kb0 + i];
+                if ((q + 1) * kT <= kSchurBlk * 18) {  // (compile time) this load is in the Hpl block range
+                    if (i < nbk * 18) v = pb[i];
+                } else if (i < nbk * 18) v = pb[i];
                 else if (i >= kSchurBlk * 18 && i < kSchurBlk * 18 + nh * 9) v = g.Dinv[9 * h0 + i - kSchurBlk * 18];
                 else if (i >= kSchurBlk * 18 + kSchurLm * 9 && i < kSchurBlk * 18 + kSchurLm * 9 + nh * 3)
                     v = g.db[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
@@ -1685,6 +1721,7 @@ __device__ __noinline__ void schur() {
                 const bool diag = i1[k] == i2[k];
                 const uint64_t lo1 = (1ull << i1[k]) - 1ull, lo2 = (1ull << i2[k]) - 1ull;
                 uint64_t cand = PM[i1[k]] & PM[i2[k]];
+#ifndef SPSLAM_LBG_SCHUR_PAIR
                 while (cand) {
                     const int hl = __ffsll((unsigned long long)cand) - 1;
                     cand &= cand - 1;
@@ -1701,6 +1738,43 @@ __device__ __noinline__ void schur() {
                         cf[k] += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
                     }
                 }
+#else  // measurement variant: two landmarks per step, both landmarks' operands loaded before either is
+       // subtracted (landmark order kept; a missing second one is a select) -- 2.7x slower: at 248 VGPRs the
+       // extra operands spill (profiles/r04/lba_bench_schur_pair.txt)
+                while (cand) {
+                    const int ha = __ffsll((unsigned long long)cand) - 1;
+                    cand &= cand - 1;
+                    const bool two = cand != 0;
+                    const int hb = two ? __ffsll((unsigned long long)cand) - 1 : ha;
+                    cand = two ? cand & (cand - 1) : cand;
+                    const uint64_t mka = SM[ha], mkb = SM[hb];
+                    const int oa = SO[ha], ob = SO[hb];
+                    const double* BDa = SD + 18 * (oa + __popcll(mka & lo1)) + 3 * r;
+                    const double* Bja = BUF + 18 * (oa + __popcll(mka & lo2));
+                    const double* BDb = SD + 18 * (ob + __popcll(mkb & lo1)) + 3 * r;
+                    const double* Bjb = BUF + 18 * (ob + __popcll(mkb & lo2));
+                    double ja[18], jb[18];
+#pragma unroll
+                    for (int q = 0; q < 18; q++) {
+                        ja[q] = Bja[q];
+                        jb[q] = Bjb[q];
+                    }
+                    const double a0 = BDa[0], a1 = BDa[1], a2 = BDa[2], b0 = BDb[0], b1 = BDb[1], b2 = BDb[2];
+#pragma unroll
+                    for (int cc = 0; cc < 6; cc++) {
+                        const double va = acc[k][cc] - ((a0 * ja[3 * cc] + a1 * ja[3 * cc + 1]) + a2 * ja[3 * cc + 2]);
+                        const double vb = va - ((b0 * jb[3 * cc] + b1 * jb[3 * cc + 1]) + b2 * jb[3 * cc + 2]);
+                        acc[k][cc] = two ? vb : va;
+                    }
+                    if (diag) {
+                        const double* da = Sdb + 3 * ha;
+                        const double* dbb = Sdb + 3 * hb;
+                        const double ca = cf[k] + ((ja[3 * r] * da[0] + ja[3 * r + 1] * da[1]) + ja[3 * r + 2] * da[2]);
+                        const double cb = ca + ((jb[3 * r] * dbb[0] + jb[3 * r + 1] * dbb[1]) + jb[3 * r + 2] * dbb[2]);
+                        cf[k] = two ? cb : ca;
+                    }
+                }
+#endif
             }
             __syncthreads();  // the staging buffer, BDinv and the masks are free again
 #ifdef SPSLAM_LBG_DIAG
