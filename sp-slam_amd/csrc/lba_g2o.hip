@@ -1123,11 +1123,11 @@ __device__ __noinline__ void sums_staged(int nE, int nS) {
 
 // ---------------------------------------------------------------- per iteration: quadratic forms and sums
 // BlockSolver::buildSystem in chunks of kCh consecutive edges: (A) every edge's quadratic-form terms into LDS rows
-// (point edges on thread pairs -- both evaluate the Jacobians, the even thread the landmark side, the odd one the
-// pose side; plane edges one wave each, numeric Jacobians on lane pairs); (B) the sums, in edge order: each
-// landmark's segment in the chunk by the thread of its first edge there (continuing the landmark's partial sums
-// when it started in an earlier chunk), each (free pose, term) chain by its own lane over the chunk's edges of that
-// pose (LDS bitmasks), the chains' accumulators carried in registers from chunk to chunk.
+// (every edge on two threads of different waves -- both evaluate the Jacobians, one the landmark side, the other the
+// pose side; the plane edges' numeric Jacobians from plane_jacobians); (B) the sums, in edge order: each
+// landmark's segment in the chunk as (segment, component) chains (continuing the landmark's partial sums when it
+// started in an earlier chunk), each (free pose, term) chain by its own lane over the chunk's edges of that pose
+// (LDS bitmasks), the chains' accumulators carried in registers from chunk to chunk.
 constexpr int kCh = 256;                    // edges per chunk
 constexpr int kSL = 13, kSP = 27, kSB = 19;  // LDS row strides (doubles): Hll + bl (12), Hpp + bp (27), Hpl (18)
 constexpr int kPoseSlots = (27 * kMaxK + kT - 1) / kT;
@@ -1373,12 +1373,16 @@ __device__ __noinline__ void build_system() {
         }
         __syncthreads();
 #endif
-        // (A) edges on thread pairs (the plane edges' Jacobians from plane_jacobians)
+        // (A) every edge twice: the landmark side on threads 0 .. kCh - 1, the pose side on threads kCh .. 2 kCh - 1
+        // (the plane edges' Jacobians from plane_jacobians).  Split by wave, not by lane: a wave runs only one of
+        // the two term evaluations instead of both under complementary lane masks.
+        static_assert(kT == 2 * kCh, "phase (A): two threads per chunk row");
 #ifdef SPSLAM_LBG_A_TWICE  // measurement variant: phase (A) evaluated twice (its writes are idempotent but pm's)
         for (int rep_a = 0; rep_a < 2; rep_a++)
 #endif
         {
-            const int row = t >> 1, e = c0 + row;
+            const bool land = t < kCh;
+            const int row = t & (kCh - 1), e = c0 + row;
             if (row < cnt && g.e_level[e] == 0) {
                 const int ty = g.e_type[e];
                 const int ph = s.hidx[g.e_kf[e]];
@@ -1399,7 +1403,7 @@ __device__ __noinline__ void build_system() {
                 info_of(g, C, e, ty, info);
                 for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
                 const EdgeW w = edge_weights(C, robust, ty, err, info);
-                if ((t & 1) == 0) {
+                if (land) {
                     terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
                 } else if (pfree) {
                     terms_pose(w, B, TP + kSP * row);
