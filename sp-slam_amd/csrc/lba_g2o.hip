@@ -292,15 +292,18 @@ __device__ bool depth_positive(const G& g, int e) {
     return -plane_transform(T, P4{{pp[0], pp[1], pp[2], pp[3]}}).c[3] > 0;
 }
 // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:103-234)
-__device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double (&A)[3][3], double (&B)[3][6]) {
+// needA false (a uniform branch): only B (the pose side's Jacobian) is formed
+__device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double (&A)[3][3], double (&B)[3][6],
+                                                bool needA = true) {
     const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
     const auto& k = g.kf[g.e_kf[e]];
     const double fx = k.fx, fy = k.fy, bf = k.bf;
     auto X = g.X + 3 * g.e_lm[e];
     const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
     const double x = p.x, y = p.y, z = p.z, z_2 = z * z;
-    const M3 R = q_to_rot(T.r);
-    if (t == 0) {
+    if (!needA) {
+    } else if (t == 0) {
+        const M3 R = q_to_rot(T.r);
         const double tmp[2][3] = {{fx, 0, -x / z * fx}, {0, fy, -y / z * fy}};
         const double s = -1. / z;
         for (int r = 0; r < 2; r++) {
@@ -309,6 +312,7 @@ __device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double
         }
         A[2][0] = A[2][1] = A[2][2] = 0.0;
     } else {
+        const M3 R = q_to_rot(T.r);
         for (int q = 0; q < 3; q++) {
             A[0][q] = -fx * R.a[q] / z + fx * x * R.a[6 + q] / z_2;
             A[1][q] = -fy * R.a[3 + q] / z + fy * y * R.a[6 + q] / z_2;
@@ -1389,7 +1393,7 @@ __device__ __noinline__ void build_system() {
                 const bool pfree = ph >= 0;
                 double A[3][3], B[3][6], info[3], err[3];
                 if (e < g.Ep) {
-                    point_jacobians(g, e, ty, A, B);
+                    point_jacobians(g, e, ty, A, B, land);
                 } else {
                     auto J = g.terms + 27 * (size_t)e;
 #pragma unroll
