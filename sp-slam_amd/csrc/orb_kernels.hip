@@ -453,13 +453,14 @@ constexpr int kCellScoreMax = kCellWinMax - 6;
 // reference's n < thr -> 0).  Candidates keep the reference's row-major order: (group, pixel) order.
 constexpr int kScPitchMax = ((kCellScoreMax + 3) & ~3) + 4, kScRowsMax = kCellScoreMax + 2;
 __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
-                                                         uint16_t* __restrict__ cand_cnt, int iniTh, int minTh) {
+                                                         uint16_t* __restrict__ cand_cnt, int iniTh, int minTh,
+                                                         int cid0, int cid1) {  // this launch's cells [cid0, cid1)
     __shared__ __attribute__((aligned(16))) uint8_t scs[4][kScRowsMax * kScPitchMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // XCD-aware order (as level_kernel): a frame's cells, whose windows overlap by 6 pixels, on one L2
     const int nb = gridDim.x, id = xcd_remap(blockIdx.y * nb + blockIdx.x, nb * gridDim.y);
-    const int f = id / nb, cid = (id - f * nb) * 4 + wave;
-    if (cid >= g.cells_per_frame) return;
+    const int f = id / nb, cid = cid0 + (id - f * nb) * 4 + wave;
+    if (cid >= cid1) return;
     uint8_t* sc = scs[wave];
     const int l = level_of_cell(g, cid);
     const LevelGeom& L = g.lv[l];
@@ -725,9 +726,9 @@ template <int NC>
 __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* __restrict__ cand,
                                                      const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
                                                      uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
-                                                     int* __restrict__ lvl_cnt) {
+                                                     int* __restrict__ lvl_cnt, int l0) {  // levels l0 + blockIdx.x
     __shared__ OctShared<NC> S;
-    const int l = blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+    const int l = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;
     const LevelGeom& Lg = g.lv[l];
     const int ncells = Lg.nRows * Lg.nCols;
     uint32_t* keys = keys_all + (size_t)f * g.keys_per_frame + Lg.key_base;
@@ -1075,36 +1076,84 @@ const char* kernel_kind_name(int kind) {
     return kind >= 0 && kind < kNumKernelKinds ? names[kind] : "?";
 }
 
+// the small levels' chain on orb_launch's second stream (SPSLAM_ORB_SPLIT=1): off by default -- 39.5K against
+// 40.0K frames/s on the pipelined C2 step (profiles/r04/ab_orb_split.txt): the small levels' launches wait for
+// CUs inside the step on either stream, and the second chain only adds contention
+static bool orb_split_off() {
+    static const bool off = [] {
+        const char* e = getenv("SPSLAM_ORB_SPLIT");
+        return !(e && e[0] == '1');
+    }();
+    return off;
+}
+
 hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, int minTh, spslam_keypoint* kps,
-                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer) {
+                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer,
+                      hipStream_t aux, hipEvent_t ev_fork, hipEvent_t ev_join) {
     auto B = [&](int k) { if (timer) timer->begin(k, s); };
     auto E = [&](int k) { if (timer) timer->end(k, s); };
-    B(kKindLevel);
-    // the small levels (at most kSmallLevelTiles tiles per frame together) in one launch, one workgroup per frame
-    int l0 = g.nlevels, tiles = 0;
-    while (l0 > 1 && tiles + g.level_tiles[l0 - 1] <= kSmallLevelTiles) tiles += g.level_tiles[--l0];
-    if (g.nlevels - l0 < 2 || small_levels_off()) l0 = g.nlevels;  // one level alone: the per-level launch
-    for (int l = 0; l < l0; l++)
-        hipLaunchKernelGGL(level_kernel, dim3(g.level_tiles[l], n), dim3(kLevelThreads), 0, s, g, l,
-                           min(iniTh, minTh));
-    if (l0 < g.nlevels) {
-        if (small_level_groups() == 2)
-            hipLaunchKernelGGL(level_small_kernel<2>, dim3(n), dim3(kLevelThreads * 2), 0, s, g, l0, min(iniTh, minTh));
-        else
-            hipLaunchKernelGGL(level_small_kernel<4>, dim3(n), dim3(kLevelThreads * 4), 0, s, g, l0, min(iniTh, minTh));
-    }
-    E(kKindLevel);
-    B(kKindFast);
-    hipLaunchKernelGGL(fast_cells_kernel, dim3((g.cells_per_frame + 3) / 4, n), dim3(256), 0, s, g, b.cand,
-                       b.cand_cnt, iniTh, minTh);
-    E(kKindFast);
-    B(kKindOctree);
+    // the small levels (at most kSmallLevelTiles tiles per frame together): levels ls .. nlevels - 1
+    int ls = g.nlevels, tiles = 0;
+    while (ls > 1 && tiles + g.level_tiles[ls - 1] <= kSmallLevelTiles) tiles += g.level_tiles[--ls];
+    if (g.nlevels - ls < 2) ls = g.nlevels;
     int maxcap = 0;
     for (int l = 0; l < g.nlevels; l++) maxcap = max(maxcap, g.lv[l].kp_cap);
     auto* octree = maxcap <= 256 ? octree_kernel<256> : octree_kernel<kNodeCap>;
-    hipLaunchKernelGGL(octree, dim3(g.nlevels, n), dim3(256), 0, s, g, b.cand, b.cand_cnt, b.keys, b.keynode,
-                       b.lvl_kp, b.lvl_cnt);
-    E(kKindOctree);
+    auto fast = [&](int la, int lb, hipStream_t st) {
+        const int c0 = g.lv[la].cell_base, c1 = lb < g.nlevels ? g.lv[lb].cell_base : g.cells_per_frame;
+        hipLaunchKernelGGL(fast_cells_kernel, dim3((c1 - c0 + 3) / 4, n), dim3(256), 0, st, g, b.cand, b.cand_cnt,
+                           iniTh, minTh, c0, c1);
+    };
+    auto tree = [&](int la, int lb, hipStream_t st) {
+        hipLaunchKernelGGL(octree, dim3(lb - la, n), dim3(256), 0, st, g, b.cand, b.cand_cnt, b.keys, b.keynode,
+                           b.lvl_kp, b.lvl_cnt, la);
+    };
+    auto level = [&](int l, hipStream_t st) {
+        hipLaunchKernelGGL(level_kernel, dim3(g.level_tiles[l], n), dim3(kLevelThreads), 0, st, g, l,
+                           min(iniTh, minTh));
+    };
+    if (aux && ev_fork && ev_join && ls < g.nlevels && !orb_split_off() && small_levels_off()) {
+        // Two chains from level ls - 1 on: the small levels, their FAST cells and their octrees on `aux`; the large
+        // levels' cells and octrees on `s` meanwhile; the descriptors (every level's keypoints) after both.  The
+        // small levels' launches are short but wait for CUs inside the pipelined step; off the caller's stream
+        // they no longer lengthen its chain.  (Timed: the caller's stream's part.)
+        B(kKindLevel);
+        for (int l = 0; l < ls; l++) level(l, s);
+        E(kKindLevel);
+        hipError_t e = hipEventRecord(ev_fork, s);
+        if (e == hipSuccess) e = hipStreamWaitEvent(aux, ev_fork, 0);
+        if (e != hipSuccess) return e;
+        for (int l = ls; l < g.nlevels; l++) level(l, aux);
+        fast(ls, g.nlevels, aux);
+        tree(ls, g.nlevels, aux);
+        e = hipEventRecord(ev_join, aux);
+        if (e != hipSuccess) return e;
+        B(kKindFast);
+        fast(0, ls, s);
+        E(kKindFast);
+        B(kKindOctree);
+        tree(0, ls, s);
+        E(kKindOctree);
+        e = hipStreamWaitEvent(s, ev_join, 0);
+        if (e != hipSuccess) return e;
+    } else {
+        B(kKindLevel);
+        const int l0 = small_levels_off() ? g.nlevels : ls;  // SPSLAM_ORB_SMALL_LEVELS=1: one fused launch
+        for (int l = 0; l < l0; l++) level(l, s);
+        if (l0 < g.nlevels) {
+            if (small_level_groups() == 2)
+                hipLaunchKernelGGL(level_small_kernel<2>, dim3(n), dim3(kLevelThreads * 2), 0, s, g, l0, min(iniTh, minTh));
+            else
+                hipLaunchKernelGGL(level_small_kernel<4>, dim3(n), dim3(kLevelThreads * 4), 0, s, g, l0, min(iniTh, minTh));
+        }
+        E(kKindLevel);
+        B(kKindFast);
+        fast(0, g.nlevels, s);
+        E(kKindFast);
+        B(kKindOctree);
+        tree(0, g.nlevels, s);
+        E(kKindOctree);
+    }
     B(kKindDesc);
     hipLaunchKernelGGL(desc_kernel, dim3((g.lvl_kp_per_frame + 3) / 4 * n), dim3(256), 0, s, g, b.lvl_kp, b.lvl_cnt,
                        kps, desc, counts, cap_per_frame);

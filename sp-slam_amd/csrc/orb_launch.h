@@ -34,7 +34,9 @@ struct KernelTimer {
 };
 
 hipError_t orb_upload_tables(const int umax[16]);
+// aux / ev_fork / ev_join (optional): a second stream for the small levels' chain (orb_kernels.hip)
 hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, int minTh, spslam_keypoint* kps,
-                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer);
+                      uint8_t* desc, int* counts, int cap_per_frame, hipStream_t s, KernelTimer* timer,
+                      hipStream_t aux = nullptr, hipEvent_t ev_fork = nullptr, hipEvent_t ev_join = nullptr);
 
 }  // namespace spslam

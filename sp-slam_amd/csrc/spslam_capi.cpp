@@ -130,6 +130,8 @@ struct spslam_ctx {
     uint8_t* d_lba_scratch = nullptr;
     size_t lba_scratch_bytes = 0;
     long long* d_lba_off = nullptr;
+    hipStream_t orb_aux = nullptr;  // orb_launch's second stream (the small pyramid levels' chain)
+    hipEvent_t orb_fork = nullptr, orb_join = nullptr;
     int32_t* h_lba_stop = nullptr;    // host-mapped coherent pbStopFlag mirror of spslam_lba_optimize
     int32_t* d_lba_stop = nullptr;    // its device alias (hipHostGetDevicePointer)
     int lba_stop_after = -1;          // spslam_lba_debug_stop_after
@@ -283,6 +285,9 @@ void free_all(spslam_ctx* c) {
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_lba_stop) (void)hipHostFree(c->h_lba_stop);
+    if (c->orb_fork) (void)hipEventDestroy(c->orb_fork);
+    if (c->orb_join) (void)hipEventDestroy(c->orb_join);
+    if (c->orb_aux) (void)hipStreamDestroy(c->orb_aux);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c->timer;
     c->timer = nullptr;
@@ -415,8 +420,13 @@ int spslam_orb_extract_batch_device(spslam_ctx* c, const uint8_t* d_gray, int n_
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     bind_frames(c, d_gray, frame_stride, stride);
+    if (!c->orb_aux) {  // the small levels' chain (orb_launch)
+        HIP_CHECK(c, hipStreamCreateWithFlags(&c->orb_aux, hipStreamNonBlocking));
+        HIP_CHECK(c, hipEventCreateWithFlags(&c->orb_fork, hipEventDisableTiming));
+        HIP_CHECK(c, hipEventCreateWithFlags(&c->orb_join, hipEventDisableTiming));
+    }
     HIP_CHECK(c, orb_launch(c->geom, c->b, n_frames, c->p.ini_th_fast, c->p.min_th_fast, d_kps, d_desc, d_counts,
-                            cap_per_frame, s, c->timer));
+                            cap_per_frame, s, c->timer, c->orb_aux, c->orb_fork, c->orb_join));
     c->last_gray = d_gray;
     c->last_frame_stride = frame_stride;
     c->last_stride = stride;
