@@ -685,6 +685,12 @@ def main():
             "frac": floor / max(avg_launch_s * 1e3, 1e-9),
             "mean_lm_iterations": float((res["pose1"]["lm_iterations"].mean() + res["pose2"]["lm_iterations"].mean()) / 2),
             "mean_trial_passes": float((res["pose1"]["trial_passes"].mean() + res["pose2"]["trial_passes"].mean()) / 2)}
+    elif dom == "level_kernel":
+        # the pyramid's 8 launches stream 3.8 MB per frame, but inside the pipelined step their spans include the
+        # wait for CUs held by the plane and tracking streams: the small levels' launches last ~345 us each in
+        # the step against ~15 us alone
+        result["roofline"]["note"] = ("event spans inside the pipelined step (three streams share the CUs); the "
+                                      "small levels' launches mostly wait for CUs")
     elif dom == "lba_batch":
         # one workgroup per LocalBundleAdjustment problem walking g2o's ordered fp64 chains (buildSystem in edge
         # order, the Schur complement in landmark order, the up-looking LDLT): latency-bound, 16 MB per launch
