@@ -38,6 +38,8 @@ constexpr int kT = kLbgThreads, kW = kT / 64;
 constexpr int kMaxK = kLbaMaxKeyframes;
 constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
+constexpr int kDynAlloc = 152 * 1024;   // allocated: kDyn plus the Schur phase's staged Bb terms and block table
+                                        //   (every phase but the Schur one sizes itself against kDyn)
 constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised in LDS (L, S packed: 133 KB)
 constexpr int kSchurLm = 64;            // Schur phase: landmarks per staged chunk (one bit each in a 64-bit mask)
 constexpr int kSchurBlk = 412;          //   and Hpl blocks per chunk (the staging buffer, 16 doubles a thread, + BDinv)
@@ -56,6 +58,8 @@ struct Sh {
     double lambda, ni, currentChi, iniChi, tempChi, scale;
     long long ph[8], tlast, tB;  // diagnostics: wall_clock64 ticks per phase (result phase_us[1..7])
     long long dg[14];            // SPSLAM_LBG_DIAG sub-phase ticks
+    int sorder_n;                       // Schur: pattern blocks in chain-length order (valid when == nb) ...
+    unsigned short sorder[128];         //   ... the order (kSortB)
 };
 // thread 0 charges the time since the previous mark to phase k (called right after a barrier)
 #define LBG_MARK(k)                                  \
@@ -222,9 +226,9 @@ __device__ __forceinline__ P4 plane_transform(const SE3& T, const P4& w) {
     return v;
 }
 __device__ __forceinline__ int edge_dim(int type) { return type == 0 ? 2 : (type <= 2 ? 3 : 2); }
-__device__ __forceinline__ void info_of(const G& g, const LbaConsts& C, int e, int t, double* info) {
+__device__ __forceinline__ void info_of_src(const G& g, const LbaConsts& C, int src, int t, double* info) {
     if (t <= 1) {
-        const double s = (double)g.pobs[g.e_src[e]].inv_sigma2;
+        const double s = (double)g.pobs[src].inv_sigma2;
         info[0] = info[1] = info[2] = s;
     } else if (t == 2) {
         info[0] = info[1] = C.angle_info; info[2] = C.dis_info;
@@ -232,6 +236,9 @@ __device__ __forceinline__ void info_of(const G& g, const LbaConsts& C, int e, i
         info[0] = info[1] = t == 3 ? C.par_info : C.ver_info;
         info[2] = 0;
     }
+}
+__device__ __forceinline__ void info_of(const G& g, const LbaConsts& C, int e, int t, double* info) {
+    info_of_src(g, C, t <= 1 ? g.e_src[e] : 0, t, info);
 }
 template <class PE>
 __device__ __forceinline__ double chi2_of(const PE* err, const double* info, int dim) {  // e . (Omega e)
@@ -293,12 +300,13 @@ __device__ bool depth_positive(const G& g, int e) {
 }
 // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::linearizeOplus (types_six_dof_expmap.cpp:103-234)
 // needA false (a uniform branch): only B (the pose side's Jacobian) is formed
-__device__ __forceinline__ void point_jacobians(const G& g, int e, int t, double (&A)[3][3], double (&B)[3][6],
+// (edge of keyframe kf and landmark lm)
+__device__ __forceinline__ void point_jacobians(const G& g, int kf, int lm, int t, double (&A)[3][3], double (&B)[3][6],
                                                 bool needA = true) {
-    const SE3 T = load_pose(g.pose + 7 * g.e_kf[e]);
-    const auto& k = g.kf[g.e_kf[e]];
+    const SE3 T = load_pose(g.pose + 7 * kf);
+    const auto& k = g.kf[kf];
     const double fx = k.fx, fy = k.fy, bf = k.bf;
-    auto X = g.X + 3 * g.e_lm[e];
+    auto X = g.X + 3 * lm;
     const V3 p = q_rot(T.r, V3{X[0], X[1], X[2]}) + T.t;
     const double x = p.x, y = p.y, z = p.z, z_2 = z * z;
     if (!needA) {
@@ -1303,6 +1311,14 @@ __device__ __noinline__ void build_system() {
     // row t's record (structure's eseg) of the next chunk: loaded during the previous chunk's phase (B)
     int4 sgn = make_int4(-2, -1, 0, 0);
     if (t < g.E) sgn = ld_i4(g.eseg + 4 * t);
+    // phase (A)'s edge record (level, type, keyframe, landmark, observation) of row t & (kCh - 1) of the next
+    // chunk: loaded during the previous chunk's phase (B), so that a chunk's (A) starts with the pose / point /
+    // observation loads instead of waiting for the edge arrays first
+    int nlv = 1, nty = 0, nkf = 0, nlm = 0, nsrc = 0;
+    auto edge_rec = [&](int e) __attribute__((always_inline)) {
+        nlv = g.e_level[e]; nty = g.e_type[e]; nkf = g.e_kf[e]; nlm = g.e_lm[e]; nsrc = g.e_src[e];
+    };
+    if ((t & (kCh - 1)) < g.E) edge_rec(t & (kCh - 1));
     for (int c0 = 0; c0 < g.E; c0 += kCh) {
         const int cnt = min(kCh, g.E - c0);
         const int4 sg = sgn;
@@ -1387,13 +1403,13 @@ __device__ __noinline__ void build_system() {
         {
             const bool land = t < kCh;
             const int row = t & (kCh - 1), e = c0 + row;
-            if (row < cnt && g.e_level[e] == 0) {
-                const int ty = g.e_type[e];
-                const int ph = s.hidx[g.e_kf[e]];
+            if (row < cnt && nlv == 0) {
+                const int ty = nty;
+                const int ph = s.hidx[nkf];
                 const bool pfree = ph >= 0;
                 double A[3][3], B[3][6], info[3], err[3];
                 if (e < g.Ep) {
-                    point_jacobians(g, e, ty, A, B, land);
+                    point_jacobians(g, nkf, nlm, ty, A, B, land);
                 } else {
                     auto J = g.terms + 27 * (size_t)e;
 #pragma unroll
@@ -1404,7 +1420,7 @@ __device__ __noinline__ void build_system() {
                         for (int d = 0; d < 6; d++) B[i][d] = J[9 + 6 * i + d];
                     }
                 }
-                info_of(g, C, e, ty, info);
+                info_of_src(g, C, nsrc, ty, info);
                 for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
                 const EdgeW w = edge_weights(C, robust, ty, err, info);
                 if (land) {
@@ -1482,6 +1498,7 @@ __device__ __noinline__ void build_system() {
         }
 #endif
         if (c0 + kCh + t < g.E) sgn = ld_i4(g.eseg + 4 * (c0 + kCh + t));  // the next chunk's row records
+        if (c0 + kCh + (t & (kCh - 1)) < g.E) edge_rec(c0 + kCh + (t & (kCh - 1)));
 #ifndef SPSLAM_LBG_SEG_SERIAL
         {
             int nseg = 0;
@@ -1587,7 +1604,10 @@ __device__ __noinline__ void build_system() {
 // Dinv and Dinv bl; then every block's BDinv = Bi Dinv (one thread per block row) and every free pose's chunk
 // landmarks as a bitmask; then the chains, each lane walking only the landmarks that observe both of its poses
 // (in landmark order) while the next chunk's records load into registers.
-constexpr int kSchurTasks = 2;  // chains per lane per round
+#ifndef SPSLAM_LBG_SCHUR_TASKS
+#define SPSLAM_LBG_SCHUR_TASKS 2
+#endif
+constexpr int kSchurTasks = SPSLAM_LBG_SCHUR_TASKS;  // chains per lane per round
 __device__ __noinline__ void schur() {
     const G& g = lbg_g;
     Sh& s = lbg_s;
@@ -1610,26 +1630,38 @@ __device__ __noinline__ void schur() {
     constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
     double* BUF = (double*)dyn;                          // [kBufD]
     double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
-    uint64_t* SM = (uint64_t*)(SD + kSchurBlk * 18);     // [kSchurLm]
+    double* SU = SD + kSchurBlk * 18;                    // [kSchurBlk][6] B row . Dinv bl (Bb's terms)
+    uint64_t* SM = (uint64_t*)(SU + kSchurBlk * 6);      // [kSchurLm]
     uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
     int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
-    unsigned char* BL = (unsigned char*)(SO + kSchurLm + 1);  // [kSchurBlk]
+    unsigned short* OB = (unsigned short*)(SO + kSchurLm + 1);  // [kMaxK][kSchurLm] (pose, landmark) -> its block
+    unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk]
     const double* SDi = BUF + kSchurBlk * 18;
     const double* Sdb = SDi + kSchurLm * 9;
+    static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
+                      kSchurBlk <= kDynAlloc, "LDS");
     constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
     // the chains: blocks (i, i) first, then the off-diagonal pattern blocks row-major; task = 6 block + r
     int nb = 0;
     for (int q = 0; q < np; q++) nb += __popcll(s.pat[q]);
+    // The chains of a wave run as long as its longest one: after the pass's first Schur call (pattern order) the
+    // blocks are dealt to the lanes longest chain first (each lane counted its chain's landmarks), so a wave holds
+    // chains of similar length.  Any order gives the same sums (every chain keeps its landmark order).
+    constexpr int kSortB = 128;
+    static_assert(6 * kSortB <= kSchurTasks * kT, "an ordered pattern fits one round");
+    const bool sorted = s.sorder_n == nb;
     for (int round = 0; round * kSchurTasks * kT < 6 * nb; round++) {
-        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
+        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks], pb[kSchurTasks], wsum[kSchurTasks];
         double acc[kSchurTasks][6], cf[kSchurTasks];
 #pragma unroll
         for (int k = 0; k < kSchurTasks; k++) {
-            i1[k] = -1; i2[k] = 0; rr[k] = 0;
+            i1[k] = -1; i2[k] = 0; rr[k] = 0; pb[k] = -1; wsum[k] = 0;
             const int task = (round * kSchurTasks + k) * kT + t;
             if (task < 6 * nb) {
-                const int blk = task / 6;
+                int blk = task / 6;
                 rr[k] = task - 6 * blk;
+                if (sorted) blk = s.sorder[blk];
+                pb[k] = blk;
                 if (blk < np) {
                     i1[k] = i2[k] = blk;
                 } else {
@@ -1704,17 +1736,22 @@ __device__ __noinline__ void schur() {
 #endif
             const int nh = g.sch[c + 1] - g.sch[c];
             const int nbk = SO[nh];
-            for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q)
-                const int bk = i / 6, r6 = i - 6 * bk;
+            for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
+                const int bk = i / 6, r6 = i - 6 * bk, hb = BL[bk];
                 const double* Bi = BUF + 18 * bk + 3 * r6;
-                const double* Di = SDi + 9 * BL[bk];
+                const double* Di = SDi + 9 * hb;
+                const double* db = Sdb + 3 * hb;
                 double* BD = SD + 18 * bk + 3 * r6;
 #pragma unroll
                 for (int q = 0; q < 3; q++) BD[q] = (Bi[0] * Di[q] + Bi[1] * Di[3 + q]) + Bi[2] * Di[6 + q];
+                SU[i] = (Bi[0] * db[0] + Bi[1] * db[1]) + Bi[2] * db[2];
             }
-            for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk
-                const uint64_t m = __ballot(lane < nh && ((SM[lane] >> i) & 1ull));
+            for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk, and their blocks
+                const uint64_t mk = lane < nh ? SM[lane] : 0ull;
+                const bool obs = (mk >> i) & 1ull;
+                const uint64_t m = __ballot(obs);
                 if (lane == 0) PM[i] = m;
+                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + __popcll(mk & ((1ull << i) - 1ull)));
             }
             __syncthreads();
 #ifdef SPSLAM_LBG_DIAG
@@ -1726,29 +1763,56 @@ __device__ __noinline__ void schur() {
             for (int k = 0; k < kSchurTasks; k++) {
                 if (i1[k] < 0) continue;
                 const int r = rr[k];
-                const bool diag = i1[k] == i2[k];
-                const uint64_t lo1 = (1ull << i1[k]) - 1ull, lo2 = (1ull << i2[k]) - 1ull;
                 uint64_t cand = PM[i1[k]] & PM[i2[k]];
+                wsum[k] += __popcll(cand);
 #ifndef SPSLAM_LBG_SCHUR_PAIR
-                while (cand) {
-                    const int hl = __ffsll((unsigned long long)cand) - 1;
+                // one LDS round trip per landmark: the next landmark's blocks (the chunk's (pose, landmark) block
+                // table) load while this one's are subtracted, and the diagonal lanes' Bb term comes staged (SU)
+                // with the blocks instead of through a dependent load of Dinv bl
+                if (cand) {
+                    // LDS address-space pointers: 32-bit address arithmetic in the loop (generic pointers cost a
+                    // 64-bit multiply-add per operand address)
+                    using LdsD = const __attribute__((address_space(3))) double;
+                    using LdsU16 = const __attribute__((address_space(3))) unsigned short;
+                    LdsU16* O1 = (LdsU16*)(OB + kSchurLm * i1[k]);
+                    LdsU16* O2 = (LdsU16*)(OB + kSchurLm * i2[k]);
+                    LdsD* SDr = (LdsD*)(SD + 3 * r);
+                    LdsD* SUr = (LdsD*)(SU + r);
+                    LdsD* BUFl = (LdsD*)BUF;
+                    int hl = __ffsll((unsigned long long)cand) - 1;
                     cand &= cand - 1;
-                    const uint64_t mk = SM[hl];
-                    const int o = SO[hl];
-                    const double* BD = SD + 18 * (o + __popcll(mk & lo1)) + 3 * r;
-                    const double* Bj = BUF + 18 * (o + __popcll(mk & lo2));
-                    const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
+                    int b1 = O1[hl], b2 = O2[hl];
+                    // (opaque here: otherwise the first landmark's loads and the loop's next-landmark loads are
+                    // merged into one load at the top of the loop, behind a wait -- the round trip this loop avoids)
+                    asm volatile("" : "+v"(b1), "+v"(b2));
+                    for (;;) {
+                        LdsD* BD = SDr + __umul24(b1, 18);  // (24-bit products: full-rate multiplies)
+                        LdsD* Bj = BUFl + __umul24(b2, 18);
+                        const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
+                        double bj[18];
 #pragma unroll
-                    for (int cc = 0; cc < 6; cc++)
-                        acc[k][cc] -= (e0 * Bj[3 * cc] + e1 * Bj[3 * cc + 1]) + e2 * Bj[3 * cc + 2];
-                    if (diag) {
-                        const double* db = Sdb + 3 * hl;
-                        cf[k] += (Bj[3 * r] * db[0] + Bj[3 * r + 1] * db[1]) + Bj[3 * r + 2] * db[2];
+                        for (int q = 0; q < 18; q++) bj[q] = Bj[q];
+                        const double u = SUr[__umul24(b1, 6)];  // (b1 = b2 on the diagonal lanes)
+                        const bool more = cand != 0;
+                        const int hn = more ? __ffsll((unsigned long long)cand) - 1 : hl;
+                        cand &= cand - 1;
+                        const int b1n = O1[hn], b2n = O2[hn];
+#pragma unroll
+                        for (int cc = 0; cc < 6; cc++)
+                            acc[k][cc] -= (e0 * bj[3 * cc] + e1 * bj[3 * cc + 1]) + e2 * bj[3 * cc + 2];
+                        cf[k] += u;  // (kept for the diagonal lanes only: unconditional, so the load is not sunk
+                                     // into a branch that waits for the next landmark's loads too)
+                        if (!more) break;
+                        hl = hn;
+                        b1 = b1n;
+                        b2 = b2n;
                     }
                 }
 #else  // measurement variant: two landmarks per step, both landmarks' operands loaded before either is
        // subtracted (landmark order kept; a missing second one is a select) -- 2.7x slower: at 248 VGPRs the
        // extra operands spill (profiles/r04/lba_bench_schur_pair.txt)
+                const bool diag = i1[k] == i2[k];
+                const uint64_t lo1 = (1ull << i1[k]) - 1ull, lo2 = (1ull << i2[k]) - 1ull;
                 while (cand) {
                     const int ha = __ffsll((unsigned long long)cand) - 1;
                     cand &= cand - 1;
@@ -1801,6 +1865,21 @@ __device__ __noinline__ void schur() {
 #pragma unroll
             for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
             if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
+        }
+        if (!sorted && nb <= kSortB) {  // (block-uniform; one round) the chain lengths -> the order
+            int* W = (int*)dyn;  // (the staging buffer is free: every chain is done)
+#pragma unroll
+            for (int k = 0; k < kSchurTasks; k++)
+                if (pb[k] >= 0 && rr[k] == 0) W[pb[k]] = wsum[k];
+            __syncthreads();
+            if (t < nb) {
+                const int w = W[t];
+                int rank = 0;
+                for (int j = 0; j < nb; j++) rank += W[j] > w || (W[j] == w && j < t);
+                s.sorder[rank] = (unsigned short)t;
+            }
+            if (t == 0) s.sorder_n = nb;
+            __syncthreads();
         }
     }
 }
@@ -2266,7 +2345,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         int* RS = (int*)(dyn + fl.RS);
         int* PI = (int*)(dyn + fl.PI);
         if (t == 0) {
-            s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1;
+            s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1; s.sorder_n = 0;
         }
         __syncthreads();
         // SparseOptimizer::optimize on a graph without active edges (every edge relabelled): nothing to do
@@ -2435,6 +2514,9 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         b.res[p].phase_us[2] = (float)s.dg[11] / (float)max(1ll, s.dg[13]);  //   edges per segment,
         b.res[p].phase_us[3] = (float)(s.dg[12] * 1e-3);                     //   longest loop (kcycles)
         b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
+#ifdef SPSLAM_LBG_DIAG_SCHUR  // Schur sub-phases (us) in slots 1-4 instead of the segment statistics
+        for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
+#endif
 #endif
 #ifdef SPSLAM_LBG_PROBE  // shader-clock ticks per (1) add, (2) add of a readlane, (3) readlane chain
         for (int i = 0; i < 3; i++) b.res[p].phase_us[1 + i] = (float)probe[i];
@@ -2448,10 +2530,10 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
 hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer) {
     using namespace lbag;
     static const hipError_t attr =
-        hipFuncSetAttribute((const void*)k_lba_g2o, hipFuncAttributeMaxDynamicSharedMemorySize, kDyn);
+        hipFuncSetAttribute((const void*)k_lba_g2o, hipFuncAttributeMaxDynamicSharedMemorySize, kDynAlloc);
     if (attr != hipSuccess) return attr;
     if (timer) timer->begin(kKindLba, s);
-    hipLaunchKernelGGL(k_lba_g2o, dim3(b.n), dim3(kT), kDyn, s, b, C);
+    hipLaunchKernelGGL(k_lba_g2o, dim3(b.n), dim3(kT), kDynAlloc, s, b, C);
     if (timer) timer->end(kKindLba, s);
     return hipGetLastError();
 }
