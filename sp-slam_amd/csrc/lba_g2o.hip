@@ -1647,7 +1647,7 @@ __device__ __noinline__ void schur() {
     // The chains of a wave run as long as its longest one: after the pass's first Schur call (pattern order) the
     // blocks are dealt to the lanes longest chain first (each lane counted its chain's landmarks), so a wave holds
     // chains of similar length.  Any order gives the same sums (every chain keeps its landmark order).
-    constexpr int kSortB = 128;
+    constexpr int kSortB = kSchurTasks * kT / 6 < 128 ? kSchurTasks * kT / 6 : 128;  // (Sh::sorder holds 128)
     static_assert(6 * kSortB <= kSchurTasks * kT, "an ordered pattern fits one round");
     const bool sorted = s.sorder_n == nb;
     for (int round = 0; round * kSchurTasks * kT < 6 * nb; round++) {
