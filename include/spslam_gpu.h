@@ -313,16 +313,27 @@ int spslam_lba_set_order(spslam_ctx* ctx, int order);
  * as a raised flag; -1 turns the hook off (default). */
 int spslam_lba_debug_stop_after(spslam_ctx* ctx, int trials);
 
+/* Workgroups per problem of the SPSLAM_LBA_G2O_ORDER launch (1 .. 16; 0, the
+ * default: as many as fill the device's compute units, at most 8).  Results do
+ * not depend on it: every sum keeps g2o's order whatever the split. */
+int spslam_lba_set_team(spslam_ctx* ctx, int workgroups);
+
 /* Batched, device resident: n problems (host copy `problems` for sizing, the
- * same records on the device at d_problems), one workgroup each, the whole
- * optimize(5) / relabel / optimize(10) schedule on the device.  Outputs are
- * indexed like the inputs (keyframe / point / plane offsets of each problem,
- * absolute observation indices).  At most 64 keyframes per problem
- * (status -2 otherwise).  d_stop_flags: one pbStopFlag per problem in
- * device-visible memory (device, or host-mapped coherent memory another thread
- * raises), nonzero = stop; NULL = no flags.  Results are complete on
- * hip_stream (SPSLAM_LBA_G2O_ORDER only enqueues one launch; the fast order
- * polls the device and returns once every problem is done). */
+ * same records on the device at d_problems), a team of workgroups each
+ * (spslam_lba_set_team), the whole optimize(5) / relabel / optimize(10)
+ * schedule on the device.  Outputs are indexed like the inputs (keyframe /
+ * point / plane offsets of each problem, absolute observation indices).
+ * SPSLAM_LBA_G2O_ORDER: at most 1024 keyframes per problem (local + fixed) of
+ * which at most 64 free poses (local keyframes, id != 0, with an active
+ * edge); SPSLAM_LBA_FAST_ORDER: at most 64 keyframes; status -2 otherwise
+ * (nothing else written for that problem).  d_stop_flags: one pbStopFlag per
+ * problem in device-visible memory (device, or host-mapped coherent memory
+ * another thread raises), nonzero = stop; NULL = no flags.  Results are
+ * complete on hip_stream (SPSLAM_LBA_G2O_ORDER only enqueues one launch; the
+ * fast order polls the device and returns once every problem is done).  One
+ * LocalBundleAdjustment call per context is in flight at a time: a call on
+ * another stream first waits (on the device) for the context's previous call,
+ * whose scratch it reuses. */
 int spslam_lba_optimize_batch_device(spslam_ctx* ctx, int n, const spslam_lba_problem* problems,
                                      const spslam_lba_problem* d_problems, const spslam_lba_keyframe* d_kfs,
                                      const spslam_lba_point* d_points, const spslam_lba_point_obs* d_point_obs,

@@ -35,7 +35,8 @@ namespace lbag {
 using namespace g2od;
 
 constexpr int kT = kLbgThreads, kW = kT / 64;
-constexpr int kMaxK = kLbaMaxKeyframes;
+constexpr int kMaxKF = kLbgMaxKeyframes;  // keyframes (local + fixed)
+constexpr int kMaxK = kLbgMaxFree;        // free poses (Hessian blocks)
 constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
 constexpr int kDynAlloc = 152 * 1024;   // allocated: kDyn plus the Schur phase's staged Bb terms and block table
@@ -47,19 +48,21 @@ constexpr int kSchurBlk = 412;          //   and Hpl blocks per chunk (the stagi
 struct Sh {
     double red[kW][4];
     int iscan[kW];
-    uint64_t kfact;
     uint64_t pat[kMaxK];                // Schur block pattern: row i1, bits i2 >= i1
-    int hidx[kMaxK];                    // keyframe -> free-pose Hessian index (-1: fixed or inactive)
+    short hidx[kMaxKF];                 // keyframe -> free-pose Hessian index (-1: fixed or inactive)
+    unsigned char kact[kMaxKF];         // structure: keyframes with an active edge
     int hpose[kMaxK];                   // Hessian index -> keyframe
     int pdeg[kMaxK];                    // poses coupled with each pose (itself included)
-    int np, nl, nact, nch, flag;
-    // LM / schedule state (thread 0 writes between barriers)
+    int np, nl, nact, nch, nb, flag, unsup;
+    // the team (one workgroup per member, lba_g2o's header): problem, member, size, barrier generation; this
+    // member's buildSystem share (landmark-aligned edge range, its free poses)
+    int p, m, T, gen, eb0, eb1, npown;
+    int pown[kMaxK];
+    // LM / schedule state (every member computes it identically between barriers)
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
     double lambda, ni, currentChi, iniChi, tempChi, scale;
     long long ph[8], tlast, tB;  // diagnostics: wall_clock64 ticks per phase (result phase_us[1..7])
     long long dg[14];            // SPSLAM_LBG_DIAG sub-phase ticks
-    int sorder_n;                       // Schur: pattern blocks in chain-length order (valid when == nb) ...
-    unsigned short sorder[128];         //   ... the order (kSortB)
 };
 // thread 0 charges the time since the previous mark to phase k (called right after a barrier)
 #define LBG_MARK(k)                                  \
@@ -87,8 +90,10 @@ struct G {
         *S, *bs, *x, *Ld;
     gint *e_lm, *e_kf, *e_type, *e_level, *e_src, *e_blk, *lm_boff, *lm_nb, *lm_sorted, *lm_hidx, *hidx_lm, *lmh_blk,
         *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W, *sch, *sch_kb,
-        *eseg;  // per edge: {RI, landmark hidx, segment end, first block | segment start << 30}
+        *eseg,   // per edge: {RI, landmark hidx, segment end, first block | segment start << 30}
+        *bord;   // Schur pattern blocks, longest chain first
     guint64 *lmh_mask, *lm_amask, *Lbits, *Abits;
+    LbgTeam GL* team;
 };
 
 // The workgroup's LDS objects at namespace scope: the phase functions are not inlined, and a pointer or reference
@@ -122,11 +127,60 @@ __device__ G make_g(const LbgBatch& b, int p) {
     g.lm_sorted = I(Ly.lm_sorted); g.lm_hidx = I(Ly.lm_hidx); g.hidx_lm = I(Ly.hidx_lm); g.lmh_blk = I(Ly.lmh_blk);
     g.pe_off = I(Ly.pe_off); g.pe_idx = I(Ly.pe_idx); g.Pinv = I(Ly.Pinv); g.Pm = I(Ly.Pm); g.parent = I(Ly.parent);
     g.rs_off = I(Ly.rs_off); g.rs_idx = I(Ly.rs_idx); g.amd_Ci = I(Ly.amd_Ci); g.amd_W = I(Ly.amd_W);
-    g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb); g.eseg = I(Ly.eseg);
+    g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb); g.eseg = I(Ly.eseg); g.bord = I(Ly.bord);
     g.lmh_mask = (uint64_t GL*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t GL*)(base + Ly.lm_amask);
     g.Lbits = (uint64_t GL*)(base + Ly.Lbits); g.Abits = (uint64_t GL*)(base + Ly.Abits);
+    g.team = (LbgTeam GL*)(base + Ly.team);
     return g;
 }
+
+// ---------------------------------------------------------------- the team
+// A problem is solved by T workgroups (members; T = b.team), one per CU.  Membership follows arrival: each
+// workgroup takes a ticket (ctl[0]) when it starts; tickets p T .. p T + T - 1 form problem p's team, member 0 (the
+// leader) being the first.  A member therefore only ever waits for workgroups that already run, or for the next
+// workgroup to be dispatched -- never for one queued behind a waiting member -- so teams cannot deadlock however many
+// launches share the chip.  Every member runs the same schedule: the serial steps (setup, structure + AMD, the
+// factorisation) on the leader, the parallel ones split over the members, the LM control replicated (each member
+// computes the same ordered sums from the same global arrays and takes the same decisions).  Phases meet at
+// team_sync, the inter-workgroup hand-off of MI355X_MICROARCH.md ("valid forms"): every storing wave drains its
+// stores (s_waitcnt vmcnt(0)), a workgroup barrier, one lane releases at agent scope (buffer_wbl2: the XCD's L2
+// written back), drains again (the explicit wait the ROCm 7.2 compiler may drop after the release), and adds to the
+// team's counter with a relaxed agent atomic; it polls the counter with relaxed agent loads (sc1: L2, not L1), then
+// acquires at agent scope (buffer_inv sc1: this CU's L1 invalidated), drains, and a workgroup barrier lets the other
+// waves read with plain loads.  The leader also samples the caller's pbStopFlag before it releases; every member
+// reads that sample after the barrier, so all members see the flag change at the same barrier.
+__device__ __forceinline__ int* team_ctr(const LbgBatch& b, int p) { return b.ctl + 16 * (p + 1); }
+__device__ __noinline__ void team_sync(const LbgBatch& b) {
+    Sh& s = lbg_s;
+    const G& g = lbg_g;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int gen = ++s.gen;  // this barrier's number
+        bool seen = false;
+        if (s.m == 0 && b.stop && !s.stop)
+            seen = __hip_atomic_load(b.stop + s.p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
+        if (s.T > 1) {
+            // the sample is published as the barrier number it belongs to: a member that reads the record late
+            // (after the leader has entered a later barrier) still takes the flag at the same barrier as the others
+            if (seen) g.team->stop_gen = gen;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            int* ctr = team_ctr(b, s.p);
+            __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int target = s.T * gen;
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target)
+                __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int sg = g.team->stop_gen;
+            seen = sg != 0 && sg <= gen;
+        }
+        if (seen) s.stop = 1;  // latched (SparseOptimizer::terminate())
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ int split_lo(int n, int m, int T) { return (int)(((long long)n * m) / T); }
 
 // ---------------------------------------------------------------- workgroup primitives
 __device__ __forceinline__ int block_scan(int v, int* total, Sh& s) {  // exclusive; *total = sum
@@ -359,10 +413,10 @@ __device__ __forceinline__ constexpr int upper_idx(int r, int c) { return 6 * r 
 //   (non-robust);  Hpp upper (r <= c) += (B^T W) B;  bp += B^T omega_r
 // W = rho' Omega (robust) or Omega; omega_r = (-(Omega e)) rho' or -(Omega e) (terms_land / terms_pose below).
 
-// SparseOptimizer::terminate(): the caller's flag, read through to memory (another thread may raise it), latched
-__device__ __forceinline__ bool stop_requested(const LbgBatch& b, int p, Sh& s) {
-    if (!s.stop && b.stop) s.stop = __hip_atomic_load(b.stop + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0;
-    if (!s.stop && b.stop_after >= 0 && s.trials >= b.stop_after) s.stop = 1;  // spslam_lba_debug_stop_after
+// SparseOptimizer::terminate(): the caller's flag as the leader sampled it at the last team_sync (latched in s.stop),
+// or the deterministic test hook (spslam_lba_debug_stop_after) on the replicated trial count
+__device__ __forceinline__ bool stop_requested(const LbgBatch& b, Sh& s) {
+    if (!s.stop && b.stop_after >= 0 && s.trials >= b.stop_after) s.stop = 1;
     return s.stop != 0;
 }
 
@@ -681,6 +735,142 @@ __device__ __forceinline__ bool coupled(const Sh& s, int q1, int q2) {  // pose 
 template <class PU>
 __device__ __forceinline__ bool bit_of(const PU* bits, int i) { return (bits[i >> 6] >> (i & 63)) & 1ull; }
 
+// ---------------------------------------------------------------- the members' shares (leader, per pass)
+// Published in the team record with the structure state the members copy (load_team):
+//  * the Schur chains: every pattern block's chain length (the landmarks whose active edges see both of its poses),
+//    the blocks longest first in g.bord; member m takes the order's entries j T + m (even j) / j T + T - 1 - m (odd
+//    j), so every member gets chains of every length (schur());
+//  * buildSystem: the landmarks in list order -- their edges are one contiguous range -- cut into T runs of about
+//    equal work (a plane edge weighs kPlaneW point edges: the Jacobians of its landmark side and of its pose side are
+//    read back from the numeric-differentiation pass), and the free poses dealt by edge count, largest first,
+//    snaking the same way (build_system()).
+constexpr int kPlaneW = 4;
+__device__ __forceinline__ int snake_pick(int j, int m, int T) { return j * T + ((j & 1) ? T - 1 - m : m); }
+__device__ __noinline__ void team_plan() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    const int t = threadIdx.x;
+    const int np = s.np, nl = s.nl, T = s.T;
+    LbgTeam GL* R = g.team;
+    int* len = (int*)lbg_dyn;                        // [nb]
+    int* rowoff = len + kMaxK * (kMaxK + 1) / 2;     // [np]
+    int* prank = rowoff + kMaxK;                     // [np] free poses by edge count
+    if (t == 0) {  // block ids: (i, i) -> i; (i1 < i2) -> rowoff[i1] + rank of i2 among row i1's bits above i1
+        int o = np;
+        for (int a = 0; a < np; a++) {
+            rowoff[a] = o;
+            o += __popcll(s.pat[a]) - 1;
+        }
+        s.nb = o;
+    }
+    __syncthreads();
+    const int nb = s.nb;
+    for (int i = t; i < nb; i += kT) len[i] = 0;
+    __syncthreads();
+    for (int h = t; h < nl; h += kT) {
+        uint64_t a = g.lmh_mask[h];
+        while (a) {
+            const int i1 = __ffsll((unsigned long long)a) - 1;
+            a &= a - 1;
+            atomicAdd(&len[i1], 1);
+            const uint64_t row = s.pat[i1] & ~(1ull << i1);
+            uint64_t b2 = a;
+            while (b2) {
+                const int i2 = __ffsll((unsigned long long)b2) - 1;
+                b2 &= b2 - 1;
+                atomicAdd(&len[rowoff[i1] + __popcll(row & ((1ull << i2) - 1ull))], 1);
+            }
+        }
+    }
+    if (t < np) {
+        const int c = g.pe_off[t + 1] - g.pe_off[t];
+        int r = 0;
+        for (int q = 0; q < np; q++) {
+            const int v = g.pe_off[q + 1] - g.pe_off[q];
+            r += v > c || (v == c && q < t);
+        }
+        prank[r] = t;
+    }
+    __syncthreads();
+    for (int i = t; i < nb; i += kT) {  // longest chain first (ties: block id)
+        const int w = len[i];
+        int r = 0;
+        for (int j = 0; j < nb; j++) {
+            const int v = len[j];
+            r += v > w || (v == w && j < i);
+        }
+        g.bord[r] = i;
+    }
+    // landmark runs: exclusive prefix of the edge weights in list order; run m ends after the landmark whose weight
+    // interval holds W m / T
+    int Wt = 0;
+    {
+        int tot = 0;
+        for (int ch = 0; ch < g.L; ch += kT) {
+            int tt;
+            block_scan(ch + t < g.L ? g.lm_nb[ch + t] * (ch + t < g.Np ? 1 : kPlaneW) : 0, &tt, s);
+            tot += tt;
+        }
+        Wt = tot;
+    }
+    if (t <= T) R->eb[t] = t == 0 ? 0 : g.E;
+    __syncthreads();
+    {
+        int base = 0;
+        for (int ch = 0; ch < g.L; ch += kT) {
+            const int l = ch + t;
+            const int w = l < g.L ? g.lm_nb[l] * (l < g.Np ? 1 : kPlaneW) : 0;
+            int tt;
+            const int ex = block_scan(w, &tt, s) + base;
+            for (int mm = 1; mm < T; mm++) {
+                const long long tgt = ((long long)Wt * mm) / T;
+                if (w > 0 && ex < tgt && tgt <= ex + w) R->eb[mm] = g.lm_boff[l] + g.lm_nb[l];
+            }
+            base += tt;
+        }
+    }
+    if (t == 0) {
+        int o = 0;
+        for (int mm = 0; mm < T; mm++) {
+            R->npo[mm] = o;
+            for (int j = 0; j * T < np; j++) {
+                const int r = snake_pick(j, mm, T);
+                if (r < np) R->pown[o++] = prank[r];
+            }
+        }
+        R->npo[T] = o;
+        R->np = np; R->nl = nl; R->nact = s.nact; R->nch = s.nch; R->nb = nb; R->unsup = 0;
+    }
+    if (t < kMaxK) R->pat[t] = t < np ? s.pat[t] : 0ull;
+    for (int k = t; k < g.K; k += kT) R->hidx[k] = s.hidx[k];
+    __syncthreads();
+}
+
+// every member (after the team_sync that follows the leader's structure pass): the shared structure state into LDS,
+// and this member's shares
+__device__ __noinline__ void load_team() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    const int t = threadIdx.x;
+    const LbgTeam GL* R = g.team;
+    if (s.m != 0) {
+        if (t == 0) {
+            s.unsup = R->unsup;
+            s.np = R->np; s.nl = R->nl; s.nact = R->nact; s.nch = R->nch; s.nb = R->nb;
+        }
+        for (int k = t; k < g.K; k += kT) s.hidx[k] = R->hidx[k];
+        if (t < kMaxK) s.pat[t] = R->pat[t];
+    }
+    const int o0 = R->npo[s.m], o1 = R->npo[s.m + 1];
+    if (t == 0) {
+        s.eb0 = R->eb[s.m];
+        s.eb1 = R->eb[s.m + 1];
+        s.npown = o1 - o0;
+    }
+    if (t < o1 - o0) s.pown[t] = R->pown[o0 + t];
+    __syncthreads();
+}
+
 // ---------------------------------------------------------------- structure (per optimize() pass)
 // initializeOptimization(0) + buildStructure + LinearSolverEigen's symbolic analysis
 __device__ __noinline__ void structure() {
@@ -688,36 +878,38 @@ __device__ __noinline__ void structure() {
     Sh& s = lbg_s;
     unsigned char* dyn = lbg_dyn;
     const int t = threadIdx.x, lane = t & 63;
-    if (t == 0) s.kfact = 0;
+    for (int k = t; k < g.K; k += kT) {
+        s.kact[k] = 0;
+        s.hidx[k] = -1;
+    }
     __syncthreads();
-    uint64_t m = 0;
     int na = 0;
     for (int e = t; e < g.E; e += kT)
         if (g.e_level[e] == 0) {
-            m |= 1ull << g.e_kf[e];
+            s.kact[g.e_kf[e]] = 1;  // (every writer stores the same value)
             na++;
         }
     int nact;
     block_scan(na, &nact, s);
     if (t == 0) s.nact = nact;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m |= (uint64_t)__shfl_xor((long long)m, o);
-    if (lane == 0 && m) atomicOr((unsigned long long*)&s.kfact, (unsigned long long)m);
     __syncthreads();
     if (t == 0) {  // free poses with an active edge, by id (buildIndexMapping over the id-sorted active vertices)
         int np = 0;
-        for (int k = 0; k < g.K; k++) s.hidx[k] = -1;
         for (int k = 0; k < g.K; k++) {
             const auto& kk = g.kf[k];
-            if (!((s.kfact >> k) & 1ull) || kk.fixed || kk.id == 0) continue;
+            if (!s.kact[k] || kk.fixed || kk.id == 0) continue;
+            if (np == kMaxK) { np++; break; }  // more free poses than the 64-bit pose masks hold: status -2
             int j = np++;
             while (j > 0 && g.kf[s.hpose[j - 1]].id > kk.id) { s.hpose[j] = s.hpose[j - 1]; j--; }
             s.hpose[j] = k;
         }
-        for (int j = 0; j < np; j++) s.hidx[s.hpose[j]] = j;
-        s.np = np;
+        s.unsup = np > kMaxK;
+        if (!s.unsup)
+            for (int j = 0; j < np; j++) s.hidx[s.hpose[j]] = (short)j;
+        s.np = s.unsup ? 0 : np;
     }
     __syncthreads();
+    if (s.unsup) return;
     const int np = s.np;
     // landmarks with an active edge in id order; pose masks of their active edges (the Hpl blocks) and of all
     // their edges (buildStructure's Schur pattern walks v->edges(), any level)
@@ -847,6 +1039,7 @@ __device__ __noinline__ void structure() {
     }
     if (t == 0) g.pe_off[np] = o;
     __syncthreads();
+    team_plan();
     // ---- LinearSolverEigen::computeSymbolicDecomposition (analyzePattern, Eigen's AMD)
     const int n = 6 * np;
     if (n == 0) {
@@ -992,15 +1185,18 @@ __device__ __noinline__ void errors() {
     const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const bool robust = s.robust;
+    // this member's share: point edges [p0, p1), plane edges [Ep + q0, Ep + q1)
+    const int p0 = split_lo(g.Ep, s.m, s.T), p1 = split_lo(g.Ep, s.m + 1, s.T);
+    const int npl = g.E - g.Ep, q0 = split_lo(npl, s.m, s.T), q1 = split_lo(npl, s.m + 1, s.T);
     // point edges, kEU per thread at a time: every edge's records, then every edge's operands, are loaded before
     // any is evaluated (a dependent load chain per group instead of per edge)
     constexpr int kEU = 3;
-    for (int e0 = t; e0 < g.Ep; e0 += kEU * kT) {
+    for (int e0 = p0 + t; e0 < p1; e0 += kEU * kT) {
         int lv[kEU], ty[kEU], kf[kEU], lm[kEU], src[kEU];
 #pragma unroll
         for (int u = 0; u < kEU; u++) {
-            const int e = e0 + u * kT, ec = e < g.Ep ? e : e0;
-            lv[u] = e < g.Ep ? g.e_level[ec] : 1;
+            const int e = e0 + u * kT, ec = e < p1 ? e : e0;
+            lv[u] = e < p1 ? g.e_level[ec] : 1;
             ty[u] = g.e_type[ec];
             kf[u] = g.e_kf[ec];
             lm[u] = g.e_lm[ec];
@@ -1012,7 +1208,7 @@ __device__ __noinline__ void errors() {
 #pragma unroll
         for (int u = 0; u < kEU; u++) {
             const int e = e0 + u * kT;
-            if (e >= g.Ep) break;
+            if (e >= p1) break;
             double chi = 0.0;
             if (lv[u] == 0) {
                 double err[3];
@@ -1026,21 +1222,20 @@ __device__ __noinline__ void errors() {
         }
     }
     // plane edges: one lane pair per edge (plane_error_pair)
-    const int npl = g.E - g.Ep;
-    for (int q = t >> 1; q < ((npl + kT / 2 - 1) / (kT / 2)) * (kT / 2); q += kT / 2) {
+    for (int q = q0 + (t >> 1); q < q0 + ((q1 - q0 + kT / 2 - 1) / (kT / 2)) * (kT / 2); q += kT / 2) {
         const int e = g.Ep + q;
-        const bool act = q < npl && g.e_level[e] == 0;
+        const bool act = q < q1 && g.e_level[e] == 0;
         E3 r{0, 0, 0};
         if (__any(act)) {
-            const int ee = act ? e : g.Ep + (q < npl ? q : 0);
-            if (q < npl) {
+            const int ee = act ? e : g.Ep + (q < q1 ? q : q0);
+            if (q < q1) {
                 const int ty = g.e_type[ee];
                 auto pp = g.P + 4 * (g.e_lm[ee] - g.Np);
                 r = plane_error_pair(ty - 2, load_pose(g.pose + 7 * g.e_kf[ee]), P4{{pp[0], pp[1], pp[2], pp[3]}},
                                      plane_from_f(g.plobs[g.e_src[ee]].meas), (t & 1) != 0);
             }
         }
-        if (q < npl && (t & 1) == 0) {
+        if (q < q1 && (t & 1) == 0) {
             double chi = 0.0;
             if (act) {
                 const int ty = g.e_type[e];
@@ -1217,8 +1412,11 @@ __device__ __forceinline__ void terms_pose(const EdgeW& w, const double (&B)[3][
 // B 3x6, per edge), kPJ edges at a time: one lane pair per (edge, evaluation q) -- q < 6: plane perturbed by
 // +-1e-9 along q >> 1 (Plane3D::oplus); 6 <= q < 18: pose exp(+-1e-9 e_d) * T, d = (q - 6) >> 1 (free poses
 // only) -- the errors into LDS, then one thread per Jacobian entry: (e(+) - e(-)) / 2e-9
+// Run by the errors phase on the member's plane edges [e_lo, e_hi): the Jacobians at the state whose errors it
+// computes -- the linearisation point of the next buildSystem whenever one follows (a rejected trial's are never
+// read: the state is popped and the errors recomputed before the next build).
 constexpr int kPJ = 128;
-__device__ __noinline__ void plane_jacobians() {
+__device__ __noinline__ void plane_jacobians(int e_lo, int e_hi) {
     const G& g = lbg_g;
     const Sh& s = lbg_s;
     double* EV = (double*)lbg_dyn;  // [kPJ][18][3]
@@ -1226,8 +1424,8 @@ __device__ __noinline__ void plane_jacobians() {
     const bool half = (t & 1) != 0;
     const double delta = 1e-9, scalar = 1.0 / (2 * delta);
     __syncthreads();  // the previous phase's LDS use is over
-    for (int e0 = g.Ep; e0 < g.E; e0 += kPJ) {
-        const int cnt = min(kPJ, g.E - e0);
+    for (int e0 = e_lo; e0 < e_hi; e0 += kPJ) {
+        const int cnt = min(kPJ, e_hi - e0);
         for (int task = pr; task < cnt * 18; task += kT / 2) {  // (both lanes of a pair: the same task)
             const int le = task / 18, q = task - 18 * le, pe = e0 + le;
             if (g.e_level[pe] != 0) continue;
@@ -1275,62 +1473,101 @@ __device__ __noinline__ void plane_jacobians() {
     }
 }
 
-// Returns (in s.red[0][1]) computeLambdaInit's max |diagonal| over Hpp and Hll.
+// This member's buildSystem share, in steps of kCh rows per side:
+//  * the landmark side of the edges [eb0, eb1) (whole landmarks): every edge's Hll / bl / Hpl terms into LDS rows on
+//    threads 0 .. kCh - 1, then (B) each landmark's segment summed in edge order as (segment, component) chains
+//    (continuing the landmark's partial sums across steps), each Hpl block stored as 0 + its first term and its
+//    later terms added in edge order;
+//  * the pose side of this member's free poses: R = kCh / P rows of each pose's active edges (in insertion order,
+//    g.pe_idx) per step, their Hpp / bp terms into LDS rows on threads kCh .. 2 kCh - 1, then each (pose, term)
+//    chain adds its pose's rows of the step in order (one lane per chain, the accumulators in registers across
+//    steps).
+// Both sides read the plane edges' Jacobians of the errors phase (plane_jacobians).  The partial sums never leave
+// their member before they are complete, so every sum keeps g2o's order (sparse_optimizer.cpp:100-114,
+// block_solver.hpp:502-561).  Returns this member's largest |diagonal| of Hll and Hpp (computeLambdaInit) in the team
+// record.
 __device__ __noinline__ void build_system() {
     const LbaConsts& C = lbg_c;
     const G& g = lbg_g;
     Sh& s = lbg_s;
     unsigned char* dyn = lbg_dyn;
-    long long tb0 = wall_clock64(), tA = 0, tB = 0, tP = 0;  // diagnostics
+    long long tb0 = wall_clock64(), tA = 0, tB = 0;  // diagnostics
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const bool robust = s.robust;
-    const int np = s.np;
+    const int e0 = s.eb0, e1 = s.eb1, P = s.npown;
+    const int R = P > 0 ? kCh / P : kCh;  // rows of each owned pose per step
     double* TL = (double*)dyn;
     double* TP = TL + kCh * kSL;
     double* TB = TP + kCh * kSP;
-    uint64_t* pm = (uint64_t*)(TB + kCh * kSB);  // [np][4]: the chunk's edges of each free pose
-    int* RI = (int*)(pm + 4 * kMaxK);            // [kCh] per row: its Hpl block, -1 none, -2 inactive edge
-#ifndef SPSLAM_LBG_SEG_SERIAL
-    // the chunk's landmark segments, compacted per wave: (first row, end row, landmark, first block | continuing
+    int* RI = (int*)(TB + kCh * kSB);  // [kCh] per landmark-side row: its Hpl block, -1 none, -2 inactive edge
+    // the step's landmark segments, compacted per wave: (first row, end row, landmark, first block | continuing
     // << 30 | complete << 31); per row the Hpl term's kind (0 none, 1 the block's first term: a plain store, 2 a
     // later term of the same block: an addition)
-    int4* SG = (int4*)(RI + kCh);                       // [kCh]
-    unsigned char* RF = (unsigned char*)(SG + kCh);     // [kCh]
-    int* NSW = (int*)(RF + kCh);                        // [kW] segments per wave, [kW]: any addition rows
-    static_assert((kCh * (kSL + kSP + kSB) + 4 * kMaxK) * 8 + kCh * (4 + 16 + 1) + 4 * (kW + 1) <= kDyn, "LDS");
-#endif
+    int4* SG = (int4*)(RI + kCh);                    // [kCh]
+    unsigned char* RF = (unsigned char*)(SG + kCh);  // [kCh]
+    int* NSW = (int*)(RF + kCh);                     // [kW] segments per wave, [kW]: any addition rows
+    int* PS = NSW + kW + 1;                          // [kMaxK] owned pose a: first entry of its edge list in pe_idx
+    int* PC = PS + kMaxK;                            //   and its length
+    int* NST = PC + kMaxK;                           // steps
+    static_assert((size_t)kCh * (kSL + kSP + kSB) * 8 + kCh * (4 + 16 + 1) + 4 * (kW + 2 + 2 * kMaxK) <= (size_t)kDyn,
+                  "LDS");
+    if (t < P) {
+        const int hh = s.pown[t];
+        PS[t] = g.pe_off[hh];
+        PC[t] = g.pe_off[hh + 1] - g.pe_off[hh];
+    }
+    __syncthreads();
+    if (t == 0) {
+        int ns = (e1 - e0 + kCh - 1) / kCh;
+        for (int a = 0; a < P; a++) ns = max(ns, (PC[a] + R - 1) / R);
+        *NST = ns;
+    }
     double acc[kPoseSlots];
     int task[kPoseSlots];
 #pragma unroll
     for (int k = 0; k < kPoseSlots; k++) {
         acc[k] = 0.0;
-        task[k] = t + k * kT < 27 * np ? t + k * kT : -1;
+        task[k] = t + k * kT < 27 * P ? t + k * kT : -1;
     }
     double mx = 0.0;
-    if (g.E > g.Ep) plane_jacobians();
-    // row t's record (structure's eseg) of the next chunk: loaded during the previous chunk's phase (B)
-    int4 sgn = make_int4(-2, -1, 0, 0);
-    if (t < g.E) sgn = ld_i4(g.eseg + 4 * t);
-    // phase (A)'s edge record (level, type, keyframe, landmark, observation) of row t & (kCh - 1) of the next
-    // chunk: loaded during the previous chunk's phase (B), so that a chunk's (A) starts with the pose / point /
-    // observation loads instead of waiting for the edge arrays first
-    int nlv = 1, nty = 0, nkf = 0, nlm = 0, nsrc = 0;
-    auto edge_rec = [&](int e) __attribute__((always_inline)) {
-        nlv = g.e_level[e]; nty = g.e_type[e]; nkf = g.e_kf[e]; nlm = g.e_lm[e]; nsrc = g.e_src[e];
+    // this thread's row: landmark side (t < kCh) row t of the step's landmark chunk, pose side (t >= kCh) row i of
+    // owned pose a.  Its records (level, type, keyframe, landmark, observation) and, landmark side, its structure
+    // record (eseg) are loaded for the next step during the current step's (B)
+    const bool land = t < kCh;
+    const int q = t - kCh, pa = land ? 0 : q / R, pi = land ? 0 : q - pa * R;
+    const bool prow = !land && pa < P;
+    auto edge_of = [&](int st) __attribute__((always_inline)) -> int {  // -1: no row
+        if (land) {
+            const int e = e0 + st * kCh + t;
+            return e < e1 ? e : -1;
+        }
+        if (!prow) return -1;
+        const int i = st * R + pi;
+        return i < PC[pa] ? g.pe_idx[PS[pa] + i] : -1;
     };
-    if ((t & (kCh - 1)) < g.E) edge_rec(t & (kCh - 1));
-    for (int c0 = 0; c0 < g.E; c0 += kCh) {
-        const int cnt = min(kCh, g.E - c0);
+    int nlv = 1, nty = 0, nkf = 0, nlm = 0, nsrc = 0, ne = -1;
+    int4 sgn = make_int4(-2, -1, 0, 0);
+    auto edge_rec = [&](int e) __attribute__((always_inline)) {
+        ne = e;
+        if (e >= 0) {
+            nlv = g.e_level[e]; nty = g.e_type[e]; nkf = g.e_kf[e]; nlm = g.e_lm[e]; nsrc = g.e_src[e];
+            if (land) sgn = ld_i4(g.eseg + 4 * e);
+        } else {
+            nlv = 1;
+        }
+    };
+    __syncthreads();
+    const int nst = *NST;
+    edge_rec(edge_of(0));
+    for (int st = 0; st < nst; st++) {
+        const int c0 = e0 + st * kCh;
+        const int cnt = max(0, min(kCh, e1 - c0));
         const int4 sg = sgn;
-        for (int i = t; i < 4 * np; i += kT) pm[i] = 0;
-#ifndef SPSLAM_LBG_SEG_SERIAL
-        // (B) runs on every thread: one (segment, component) chain per task, one (row, entry) plain Hpl store per
-        // task, then -- only in chunks that have them -- each segment's later terms of a repeated (landmark,
-        // pose) block (plane landmarks) added by the segment's head thread in edge order.
+        // (B) landmark segments: the rows' Hpl kinds in edge order (head threads), segments compacted per wave
         bool head = false, again = false;
         int end_row = 0, own_h = -1, own_kb = 0;
         uint64_t touched = 0;
-        if (t < cnt) {
+        if (land && t < cnt) {
             RI[t] = sg.x;
             RF[t] = 0;
             const bool first = (sg.w >> 30) & 1;
@@ -1350,11 +1587,11 @@ __device__ __noinline__ void build_system() {
                                     (c0 + end_row == sg.z ? 1u << 31 : 0u);
                 SG[64 * wv + li] = make_int4(t, end_row, own_h, (int)fl);
             }
-            if (lane == 0) NSW[wv] = __popcll(hb);
+            if (lane == 0 && wv < kCh / 64) NSW[wv] = __popcll(hb);
             if (t == 0) NSW[kW] = 0;
         }
         __syncthreads();
-        if (head) {  // the rows' Hpl kinds, in edge order
+        if (head) {
             for (int r = t; r < end_row; r++) {
                 const int bk = RI[r];
                 unsigned char f = 0;
@@ -1369,41 +1606,11 @@ __device__ __noinline__ void build_system() {
             if (c0 + end_row != sg.z) g.lm_amask[own_h] = touched;
             if (again) NSW[kW] = 1;
         }
-#else
-
-        // this thread's landmark segment (row t starts one when it is the landmark's first edge or the chunk's
-        // first row): its records are consumed after phase (A)
-        int own_h = -1, own_e1 = 0, own_kb = 0;
-        double H[9], bv[3];
-        uint64_t touched = 0;
-        if (t < cnt) {
-            RI[t] = sg.x;
-            const bool first = (sg.w >> 30) & 1;
-            if ((first || t == 0) && sg.y >= 0) {
-                own_h = sg.y;
-                own_e1 = sg.z;
-                own_kb = sg.w & ((1 << 30) - 1);
-                const bool cont = !first;  // continuing a landmark of the previous chunk
-#pragma unroll
-                for (int j = 0; j < 9; j++) H[j] = cont ? g.Hll[9 * own_h + j] : 0.0;
-#pragma unroll
-                for (int j = 0; j < 3; j++) bv[j] = cont ? g.bl[3 * own_h + j] : 0.0;
-                touched = cont ? g.lm_amask[own_h] : 0ull;  // (lm_amask is free after the structure phase)
-            }
-        }
-        __syncthreads();
-#endif
-        // (A) every edge twice: the landmark side on threads 0 .. kCh - 1, the pose side on threads kCh .. 2 kCh - 1
-        // (the plane edges' Jacobians from plane_jacobians).  Split by wave, not by lane: a wave runs only one of
-        // the two term evaluations instead of both under complementary lane masks.
-        static_assert(kT == 2 * kCh, "phase (A): two threads per chunk row");
-#ifdef SPSLAM_LBG_A_TWICE  // measurement variant: phase (A) evaluated twice (its writes are idempotent but pm's)
-        for (int rep_a = 0; rep_a < 2; rep_a++)
-#endif
+        // (A) every row's terms (the plane edges' Jacobians from plane_jacobians)
         {
-            const bool land = t < kCh;
-            const int row = t & (kCh - 1), e = c0 + row;
-            if (row < cnt && nlv == 0) {
+            const int e = ne;
+            const int row = land ? t : q;
+            if (e >= 0 && nlv == 0) {
                 const int ty = nty;
                 const int ph = s.hidx[nkf];
                 const bool pfree = ph >= 0;
@@ -1423,90 +1630,21 @@ __device__ __noinline__ void build_system() {
                 info_of_src(g, C, nsrc, ty, info);
                 for (int i = 0; i < 3; i++) err[i] = g.err[3 * e + i];
                 const EdgeW w = edge_weights(C, robust, ty, err, info);
-                if (land) {
-                    terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
-                } else if (pfree) {
-                    terms_pose(w, B, TP + kSP * row);
-                    atomicOr((unsigned long long*)&pm[ph * 4 + (row >> 6)], 1ull << (row & 63));
-                }
+                if (land) terms_land(w, robust, A, B, pfree, TL + kSL * row, TB + kSB * row);
+                else terms_pose(w, B, TP + kSP * row);
             }
         }
         __syncthreads();
         const long long tb1 = wall_clock64();
-        if (c0 + cnt > g.Ep) tP += tb1 - tb0; else tA += tb1 - tb0;
-        // (B) landmark segments: the thread of the segment's first edge sums it in edge order.  A block's first
-        // term is stored (0 + term); a later term of the same (landmark, pose) block -- plane landmarks, whose
-        // plane / parallel / vertical edges share a keyframe -- is added by the second loop, in edge order.  (One
-        // loop with both would wait for every earlier store at each edge: one vector-memory counter on gfx950.)
-#ifdef SPSLAM_LBG_SEG_SERIAL
-        if (own_h >= 0) {
-            const int e = c0 + t, e_end = min(own_e1, c0 + cnt);
-            const uint64_t touched0 = touched;  // blocks stored in an earlier chunk (a continuing segment)
-            bool again = false;
-#ifdef SPSLAM_LBG_DIAG
-            const long long sc0 = clock64();
-#endif
-            for (int e2 = e; e2 < e_end; e2++) {
-                const int bk = RI[e2 - c0];
-                if (bk == -2) continue;
-                const double* r = TL + kSL * (e2 - c0);
-#pragma unroll
-                for (int j = 0; j < 9; j++) H[j] += r[j];
-#pragma unroll
-                for (int j = 0; j < 3; j++) bv[j] += r[9 + j];
-                if (bk >= 0) {
-                    const uint64_t bit = 1ull << (bk - own_kb);
-                    if (!(touched & bit)) {
-                        const double* rb = TB + kSB * (e2 - c0);
-                        auto dst = g.blkB + (size_t)18 * bk;
-#pragma unroll
-                        for (int j = 0; j < 18; j++) dst[j] = 0.0 + rb[j];
-                        touched |= bit;
-                    } else {
-                        again = true;
-                    }
-                }
-            }
-            if (again) {  // the repeated blocks' terms, in edge order (rare: plane landmarks)
-                uint64_t seen = 0;
-                for (int e2 = e; e2 < e_end; e2++) {
-                    const int bk = RI[e2 - c0];
-                    if (bk < 0) continue;
-                    const uint64_t bit = 1ull << (bk - own_kb);
-                    // a block's first occurrence in this chunk, unless stored in an earlier chunk, was the plain
-                    // store of the loop above; every other occurrence is an addition
-                    const bool stored_here = !(touched0 & bit) && !(seen & bit);
-                    seen |= bit;
-                    if (stored_here) continue;
-                    const double* rb = TB + kSB * (e2 - c0);
-                    auto dst = g.blkB + (size_t)18 * bk;
-#pragma unroll
-                    for (int j = 0; j < 18; j++) dst[j] += rb[j];
-                }
-            }
-            for (int j = 0; j < 9; j++) g.Hll[9 * own_h + j] = H[j];
-            for (int j = 0; j < 3; j++) g.bl[3 * own_h + j] = bv[j];
-            if (e_end == own_e1) mx = fmax(mx, fmax(fabs(H[0]), fmax(fabs(H[4]), fabs(H[8]))));
-            else g.lm_amask[own_h] = touched;
-#ifdef SPSLAM_LBG_DIAG  // segment loops: shader cycles and edges, summed; the longest per chunk, summed
-            const unsigned long long sc = (unsigned long long)(clock64() - sc0);
-            atomicAdd((unsigned long long*)&s.dg[10], sc);
-            atomicAdd((unsigned long long*)&s.dg[11], (unsigned long long)(e_end - e));
-            atomicAdd((unsigned long long*)&s.dg[13], 1ull);
-            atomicMax((unsigned long long*)&s.dg[12], sc);
-#endif
-        }
-#endif
-        if (c0 + kCh + t < g.E) sgn = ld_i4(g.eseg + 4 * (c0 + kCh + t));  // the next chunk's row records
-        if (c0 + kCh + (t & (kCh - 1)) < g.E) edge_rec(c0 + kCh + (t & (kCh - 1)));
-#ifndef SPSLAM_LBG_SEG_SERIAL
+        tA += tb1 - tb0;
+        edge_rec(edge_of(st + 1));  // the next step's records land during (B)
+        // (B) landmark segment chains: Hll (9) and bl (3) in edge order, four rows' loads in flight
         {
             int nseg = 0;
 #pragma unroll
             for (int w = 0; w < kCh / 64; w++) nseg += NSW[w];
-            // (segment, component) chains: Hll (9) and bl (3) in edge order, four rows' loads in flight
-            for (int task = t; task < 12 * nseg; task += kT) {
-                const int si = task / 12, comp = task - 12 * si;
+            for (int tk = t; tk < 12 * nseg; tk += kT) {
+                const int si = tk / 12, comp = tk - 12 * si;
                 int w = 0, li = si;
                 while (li >= NSW[w]) li -= NSW[w++];
                 const int4 sgm = SG[64 * w + li];
@@ -1519,12 +1657,12 @@ __device__ __noinline__ void build_system() {
                     double v[4];
                     bool ok[4];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        ok[q] = RI[r + q] != -2;
-                        v[q] = TL[kSL * (r + q) + comp];
+                    for (int u = 0; u < 4; u++) {
+                        ok[u] = RI[r + u] != -2;
+                        v[u] = TL[kSL * (r + u) + comp];
                     }
 #pragma unroll
-                    for (int q = 0; q < 4; q++) a = ok[q] ? a + v[q] : a;
+                    for (int u = 0; u < 4; u++) a = ok[u] ? a + v[u] : a;
                 }
                 for (; r < sgm.y; r++)
                     if (RI[r] != -2) a += TL[kSL * r + comp];
@@ -1549,82 +1687,71 @@ __device__ __noinline__ void build_system() {
                 }
             }
         }
-#endif
-#ifdef SPSLAM_LBG_DIAG
-        __syncthreads();
-        if (t == 0) s.dg[9] += wall_clock64() - tb1;  // landmark segments
-#endif
-        // (free pose, term) chains over the chunk's edges of the pose: four rows' loads in flight, then their
-        // four adds in edge order (a missing row: a select keeps the sum)
+        // (free pose, term) chains over the step's rows of the pose: four rows' loads in flight, then their four adds
+        // in edge order (a missing row: a select keeps the sum)
 #pragma unroll
         for (int k = 0; k < kPoseSlots; k++) {
             if (task[k] < 0) continue;
-            const int hh = task[k] / 27, j = task[k] - 27 * hh;
-            for (int wd = 0; wd < 4; wd++) {
-                uint64_t bits = pm[hh * 4 + wd];
-                while (bits) {
-                    double v[4];
-                    bool ok[4];
+            const int a = task[k] / 27, j = task[k] - 27 * a;
+            const int n_a = min(R, PC[a] - st * R);
+            const double* rows = TP + kSP * (a * R) + j;
+            for (int i = 0; i < n_a; i += 4) {
+                double v[4];
+                bool ok[4];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        ok[q] = bits != 0;
-                        const int i = 64 * wd + (ok[q] ? __ffsll((unsigned long long)bits) - 1 : 0);
-                        bits &= bits - 1;
-                        v[q] = TP[kSP * i + j];
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; q++) acc[k] = ok[q] ? acc[k] + v[q] : acc[k];
+                for (int u = 0; u < 4; u++) {
+                    ok[u] = i + u < n_a;
+                    v[u] = rows[kSP * (ok[u] ? i + u : i)];
                 }
+#pragma unroll
+                for (int u = 0; u < 4; u++) acc[k] = ok[u] ? acc[k] + v[u] : acc[k];
             }
         }
         __syncthreads();
         tb0 = wall_clock64();
         tB += tb0 - tb1;
     }
-    if (t == 0) { s.ph[0] += tA; s.ph[7] += tP; s.tB += tB; }
+    if (t == 0) { s.ph[0] += tA; s.tB += tB; }
 #pragma unroll
     for (int k = 0; k < kPoseSlots; k++) {
         if (task[k] < 0) continue;
-        const int hh = task[k] / 27, j = task[k] - 27 * hh;
-        g.Hps[27 * hh + j] = acc[k];
+        const int a = task[k] / 27, j = task[k] - 27 * a;
+        g.Hps[27 * s.pown[a] + j] = acc[k];
         if (j == 0 || j == 6 || j == 11 || j == 15 || j == 18 || j == 20) mx = fmax(mx, fabs(acc[k]));
     }
-    (void)lane;
-    (void)wv;
     mx = block_max(mx, s);
-    if (t == 0) s.red[0][1] = mx;
+    if (t == 0) g.team->mx[s.m] = mx;
 }
 
 // ---------------------------------------------------------------- per trial
 
-// setLambda + the Schur complement (block_solver.hpp:367-436).  (1) every landmark's (Hll + lambda)^-1 and
-// Dinv bl; (2) the chains: one lane per (pattern block (i1, i2), row r) holds S(6 i1 + r, 6 i2 .. 6 i2 + 5) (the
-// diagonal block's lanes also Bb(6 i1 + r)) and subtracts the landmarks' contributions in landmark order.  The
-// landmarks are staged in LDS in chunks of up to 64: their Hpl blocks (one contiguous range, coalesced), masks,
-// Dinv and Dinv bl; then every block's BDinv = Bi Dinv (one thread per block row) and every free pose's chunk
-// landmarks as a bitmask; then the chains, each lane walking only the landmarks that observe both of its poses
-// (in landmark order) while the next chunk's records load into registers.
+// setLambda + the Schur complement (block_solver.hpp:367-436), this member's chains: one lane per (pattern block
+// (i1, i2), row r) holds S(6 i1 + r, 6 i2 .. 6 i2 + 5) (the diagonal block's lanes also Bb(6 i1 + r)) and subtracts
+// the landmarks' contributions in landmark order.  The member's blocks are every T-th of the longest-first order
+// (team_plan), so its waves hold chains of similar length.  Every member stages every landmark, in chunks of up to
+// 64: their Hpl blocks (one contiguous range, coalesced), masks, Hll and bl -- the chunk's (Hll + lambda)^-1 and
+// Dinv bl are formed in place (the same expressions as update()'s) -- then every block's BDinv = Bi Dinv (one thread
+// per block row) and every free pose's chunk landmarks as a bitmask; then the chains, each lane walking only the
+// landmarks that observe both of its poses (in landmark order) while the next chunk's records load into registers.
 #ifndef SPSLAM_LBG_SCHUR_TASKS
 #define SPSLAM_LBG_SCHUR_TASKS 2
 #endif
 constexpr int kSchurTasks = SPSLAM_LBG_SCHUR_TASKS;  // chains per lane per round
+// (Hll + lambda)^-1 (Eigen's cofactor inverse) and Dinv bl of one landmark
+__device__ __forceinline__ void landmark_dinv(const double* H, const double* bv, double lam, double* Di, double* db) {
+    double D[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) D[i][j] = H[3 * i + j] + (i == j ? lam : 0.0);
+    inverse3(D, Di);
+    for (int i = 0; i < 3; i++) db[i] = (Di[3 * i] * bv[0] + Di[3 * i + 1] * bv[1]) + Di[3 * i + 2] * bv[2];
+}
 __device__ __noinline__ void schur() {
     const G& g = lbg_g;
     Sh& s = lbg_s;
     unsigned char* dyn = lbg_dyn;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int nl = s.nl, np = s.np, n = 6 * np, nch = s.nch;
+    const int np = s.np, n = 6 * np, nch = s.nch;
     const double lam = s.lambda;
-    for (int h = t; h < nl; h += kT) {
-        double D[3][3];
-        for (int i = 0; i < 3; i++)
-            for (int j = 0; j < 3; j++) D[i][j] = g.Hll[9 * h + 3 * i + j] + (i == j ? lam : 0.0);
-        double Di[9];
-        inverse3(D, Di);
-        for (int j = 0; j < 9; j++) g.Dinv[9 * h + j] = Di[j];
-        auto bv = g.bl + 3 * h;
-        for (int i = 0; i < 3; i++) g.db[3 * h + i] = (Di[3 * i] * bv[0] + Di[3 * i + 1] * bv[1]) + Di[3 * i + 2] * bv[2];
-    }
     // LDS: the staged chunk (blocks, Dinv, Dinv bl | masks, block offsets, block -> landmark), its BDinv and the
     // poses' landmark masks
     constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
@@ -1641,27 +1768,20 @@ __device__ __noinline__ void schur() {
     static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
                       kSchurBlk <= kDynAlloc, "LDS");
     constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
-    // the chains: blocks (i, i) first, then the off-diagonal pattern blocks row-major; task = 6 block + r
-    int nb = 0;
-    for (int q = 0; q < np; q++) nb += __popcll(s.pat[q]);
-    // The chains of a wave run as long as its longest one: after the pass's first Schur call (pattern order) the
-    // blocks are dealt to the lanes longest chain first (each lane counted its chain's landmarks), so a wave holds
-    // chains of similar length.  Any order gives the same sums (every chain keeps its landmark order).
-    constexpr int kSortB = kSchurTasks * kT / 6 < 128 ? kSchurTasks * kT / 6 : 128;  // (Sh::sorder holds 128)
-    static_assert(6 * kSortB <= kSchurTasks * kT, "an ordered pattern fits one round");
-    const bool sorted = s.sorder_n == nb;
-    for (int round = 0; round * kSchurTasks * kT < 6 * nb; round++) {
-        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks], pb[kSchurTasks], wsum[kSchurTasks];
+    // this member's blocks: entries snake_pick(j, m, T) of g.bord; task = 6 j + r
+    const int nb = s.nb, T = s.T, mm = s.m;
+    const int nbm = nb / T + ((nb % T) ? (((nb / T) & 1) ? (mm >= T - nb % T) : (mm < nb % T)) : 0);
+    for (int round = 0; round * kSchurTasks * kT < 6 * nbm; round++) {
+        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
         double acc[kSchurTasks][6], cf[kSchurTasks];
 #pragma unroll
         for (int k = 0; k < kSchurTasks; k++) {
-            i1[k] = -1; i2[k] = 0; rr[k] = 0; pb[k] = -1; wsum[k] = 0;
+            i1[k] = -1; i2[k] = 0; rr[k] = 0;
             const int task = (round * kSchurTasks + k) * kT + t;
-            if (task < 6 * nb) {
-                int blk = task / 6;
-                rr[k] = task - 6 * blk;
-                if (sorted) blk = s.sorder[blk];
-                pb[k] = blk;
+            if (task < 6 * nbm) {
+                const int jb = task / 6;
+                rr[k] = task - 6 * jb;
+                const int blk = g.bord[snake_pick(jb, mm, T)];
                 if (blk < np) {
                     i1[k] = i2[k] = blk;
                 } else {
@@ -1698,9 +1818,9 @@ __device__ __noinline__ void schur() {
                 if ((q + 1) * kT <= kSchurBlk * 18) {  // (compile time) this load is in the Hpl block range
                     if (i < nbk * 18) v = pb[i];
                 } else if (i < nbk * 18) v = pb[i];
-                else if (i >= kSchurBlk * 18 && i < kSchurBlk * 18 + nh * 9) v = g.Dinv[9 * h0 + i - kSchurBlk * 18];
+                else if (i >= kSchurBlk * 18 && i < kSchurBlk * 18 + nh * 9) v = g.Hll[9 * h0 + i - kSchurBlk * 18];
                 else if (i >= kSchurBlk * 18 + kSchurLm * 9 && i < kSchurBlk * 18 + kSchurLm * 9 + nh * 3)
-                    v = g.db[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
+                    v = g.bl[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
                 pv[q] = v;
             }
             if (t < nh) {
@@ -1736,6 +1856,17 @@ __device__ __noinline__ void schur() {
 #endif
             const int nh = g.sch[c + 1] - g.sch[c];
             const int nbk = SO[nh];
+            if (t < nh) {  // the staged Hll, bl -> Dinv, Dinv bl, in place
+                double* Hd = BUF + kSchurBlk * 18 + 9 * t;
+                double* bd = BUF + kSchurBlk * 18 + kSchurLm * 9 + 3 * t;
+                double H[9], bv[3], Di[9], db[3];
+                for (int j = 0; j < 9; j++) H[j] = Hd[j];
+                for (int j = 0; j < 3; j++) bv[j] = bd[j];
+                landmark_dinv(H, bv, lam, Di, db);
+                for (int j = 0; j < 9; j++) Hd[j] = Di[j];
+                for (int j = 0; j < 3; j++) bd[j] = db[j];
+            }
+            __syncthreads();
             for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
                 const int bk = i / 6, r6 = i - 6 * bk, hb = BL[bk];
                 const double* Bi = BUF + 18 * bk + 3 * r6;
@@ -1764,7 +1895,6 @@ __device__ __noinline__ void schur() {
                 if (i1[k] < 0) continue;
                 const int r = rr[k];
                 uint64_t cand = PM[i1[k]] & PM[i2[k]];
-                wsum[k] += __popcll(cand);
 #ifndef SPSLAM_LBG_SCHUR_PAIR
                 // one LDS round trip per landmark: the next landmark's blocks (the chunk's (pose, landmark) block
                 // table) load while this one's are subtracted, and the diagonal lanes' Bb term comes staged (SU)
@@ -1865,21 +1995,6 @@ __device__ __noinline__ void schur() {
 #pragma unroll
             for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
             if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
-        }
-        if (!sorted && nb <= kSortB) {  // (block-uniform; one round) the chain lengths -> the order
-            int* W = (int*)dyn;  // (the staging buffer is free: every chain is done)
-#pragma unroll
-            for (int k = 0; k < kSchurTasks; k++)
-                if (pb[k] >= 0 && rr[k] == 0) W[pb[k]] = wsum[k];
-            __syncthreads();
-            if (t < nb) {
-                const int w = W[t];
-                int rank = 0;
-                for (int j = 0; j < nb; j++) rank += W[j] > w || (W[j] == w && j < t);
-                s.sorder[rank] = (unsigned short)t;
-            }
-            if (t == 0) s.sorder_n = nb;
-            __syncthreads();
         }
     }
 }
@@ -2129,14 +2244,22 @@ __device__ __noinline__ void factor_solve() {
     }
 }
 
-// landmark increments (xl = Dinv (bl - Hpl^T xp)), push, update (block_solver.hpp:444-471, oplus)
+// this member's landmarks [h0, h1) (Hessian order) and keyframes [k0, k1)
+struct Share { int h0, h1, k0, k1; };
+__device__ __forceinline__ Share my_share(const Sh& s, int K) {
+    return Share{split_lo(s.nl, s.m, s.T), split_lo(s.nl, s.m + 1, s.T), split_lo(K, s.m, s.T), split_lo(K, s.m + 1, s.T)};
+}
+// landmark increments (xl = Dinv (bl - Hpl^T xp), Dinv as the Schur phase formed it), push, update
+// (block_solver.hpp:444-471, oplus); this member's landmarks and keyframes
 __device__ __noinline__ void update() {
     const G& g = lbg_g;
     const Sh& s = lbg_s;
     const int t = threadIdx.x;
-    const int nl = s.nl, np = s.np, n = 6 * np;
+    const int np = s.np, n = 6 * np;
     const bool ok = s.ok;
-    for (int h = t; h < nl; h += kT) {
+    const double lam = s.lambda;
+    const Share sh = my_share(s, g.K);
+    for (int h = sh.h0 + t; h < sh.h1; h += kT) {
         const int l = g.hidx_lm[h];
         if (l < g.Np) for (int j = 0; j < 3; j++) g.X_b[3 * l + j] = g.X[3 * l + j];
         else for (int j = 0; j < 4; j++) g.P_b[4 * (l - g.Np) + j] = g.P[4 * (l - g.Np) + j];
@@ -2155,7 +2278,9 @@ __device__ __noinline__ void update() {
                     cl[i] += sm;
                 }
             }
-            auto Di = g.Dinv + 9 * h;
+            double H[9], Di[9], db[3];
+            for (int j = 0; j < 9; j++) H[j] = g.Hll[9 * h + j];
+            landmark_dinv(H, cl, lam, Di, db);  // (db unused)
             for (int i = 0; i < 3; i++) xl[i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
             if (l < g.Np) {
                 for (int j = 0; j < 3; j++) g.X[3 * l + j] += xl[j];
@@ -2168,7 +2293,7 @@ __device__ __noinline__ void update() {
         }
         for (int j = 0; j < 3; j++) g.x[n + 3 * h + j] = xl[j];
     }
-    for (int k = t; k < g.K; k += kT) {
+    for (int k = sh.k0 + t; k < sh.k1; k += kT) {
         for (int j = 0; j < 7; j++) g.pose_b[7 * k + j] = g.pose[7 * k + j];
         const int h = s.hidx[k];
         if (!ok || h < 0) continue;
@@ -2178,27 +2303,29 @@ __device__ __noinline__ void update() {
     }
 }
 
-__device__ __noinline__ void restore() {  // pop()
+__device__ __noinline__ void restore() {  // pop(): this member's landmarks and keyframes
     const G& g = lbg_g;
     const Sh& s = lbg_s;
     const int t = threadIdx.x;
-    for (int h = t; h < s.nl; h += kT) {
+    const Share sh = my_share(s, g.K);
+    for (int h = sh.h0 + t; h < sh.h1; h += kT) {
         const int l = g.hidx_lm[h];
         if (l < g.Np) for (int j = 0; j < 3; j++) g.X[3 * l + j] = g.X_b[3 * l + j];
         else for (int j = 0; j < 4; j++) g.P[4 * (l - g.Np) + j] = g.P_b[4 * (l - g.Np) + j];
     }
-    for (int k = t; k < g.K; k += kT)
+    for (int k = sh.k0 + t; k < sh.k1; k += kT)
         for (int j = 0; j < 7; j++) g.pose[7 * k + j] = g.pose_b[7 * k + j];
 }
 
-// computeScale terms x_j (lambda x_j + b_j), poses then landmarks (Hessian order), zero-padded to 32
+// computeScale terms x_j (lambda x_j + b_j), poses then landmarks (Hessian order), zero-padded to 32; this member's
+// share of the entries
 __device__ __noinline__ void scale_terms() {
     const G& g = lbg_g;
     const Sh& s = lbg_s;
     const int t = threadIdx.x;
     const int n = 6 * s.np, tot = n + 3 * s.nl, pad = lbg_pad32(tot);
     const double lam = s.lambda;
-    for (int j = t; j < pad; j += kT) {
+    for (int j = split_lo(pad, s.m, s.T) + t; j < split_lo(pad, s.m + 1, s.T); j += kT) {
         double v = 0.0;
         if (j < tot && s.ok) {
             const double b = j < n ? g.Hps[27 * (j / 6) + 21 + j % 6] : g.bl[j - n];
@@ -2207,6 +2334,35 @@ __device__ __noinline__ void scale_terms() {
         }
         g.sc[j] = v;
     }
+}
+
+// relabel between the passes with the errors cached by the last computeActiveErrors (Optimizer.cc:1815-1851); this
+// member's edges
+__device__ __noinline__ void relabel() {
+    const LbaConsts& C = lbg_c;
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
+    for (int e = split_lo(g.E, s.m, s.T) + threadIdx.x; e < split_lo(g.E, s.m + 1, s.T); e += kT) {
+        double info[3];
+        const int ty = g.e_type[e];
+        info_of(g, C, e, ty, info);
+        const double chi = chi2_of(g.err + 3 * e, info, edge_dim(ty));
+        bool bad;
+        if (ty == 0) bad = chi > 5.991 || !depth_positive(g, e);
+        else if (ty == 1) bad = chi > 7.815 || !depth_positive(g, e);
+        else if (ty == 2) bad = chi > C.plane_chi;
+        else bad = chi > C.vp_chi;
+        if (bad) g.e_level[e] = 1;
+    }
+}
+
+// computeActiveErrors (+ the plane edges' Jacobians at the same state): this member's edges
+__device__ __noinline__ void errors_phase() {
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
+    errors();
+    const int npl = g.E - g.Ep;
+    plane_jacobians(g.Ep + split_lo(npl, s.m, s.T), g.Ep + split_lo(npl, s.m + 1, s.T));
 }
 
 // ---------------------------------------------------------------- outputs
@@ -2285,29 +2441,42 @@ __device__ __noinline__ void outputs(const LbgBatch& b, int p) {
 __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     unsigned char* dyn = lbg_dyn;
     Sh& s = lbg_s;
-    const int p = blockIdx.x, t = threadIdx.x;
-    if (t == 0) {
-        lbg_g = make_g(b, p);
+    const int t = threadIdx.x;
+    if (t == 0) {  // the team ticket (lba_g2o's header: membership by arrival)
+        const int T = b.team;
+        const int slot = __hip_atomic_fetch_add(b.ctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s.p = slot / T;
+        s.m = slot - s.p * T;
+        s.T = T;
+        s.gen = 0;
+        lbg_g = make_g(b, s.p);
         lbg_c = C;
     }
     __syncthreads();
+    const int p = s.p;
+    const bool lead = s.m == 0;
     const G& g = lbg_g;
     const long long t0 = wall_clock64();
-    if (g.K > kMaxK) {
-        if (t == 0) {
+    if (g.K > kMaxKF) {  // (every member leaves here)
+        if (lead && t == 0) {
             b.res[p] = spslam_lba_result{};
             b.res[p].status = -2;
         }
         return;
     }
     if (t == 0) {
-        s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1;
+        s.stop = 0; s.stopped = 0; s.trials = 0; s.its[0] = s.its[1] = 0; s.fail = 0; s.robust = 1; s.done = 0;
+        s.unsup = 0;
         for (int i = 0; i < 8; i++) s.ph[i] = 0;
         for (int i = 0; i < 14; i++) s.dg[i] = 0;
         s.tB = 0;
         s.tlast = t0;
-        s.done = stop_requested(b, p, s) ? 1 : 0;  // if(*pbStopFlag) return; before initializeOptimization
-        if (s.done) s.stopped = 1;
+        if (lead) g.team->stop_gen = 0;
+    }
+    team_sync(b);  // the leader's first sample of pbStopFlag
+    if (t == 0 && stop_requested(b, s)) {  // if(*pbStopFlag) return; before initializeOptimization
+        s.stopped = 1;
+        s.done = 1;
     }
     __syncthreads();
 #ifdef SPSLAM_LBG_PROBE  // diagnostic: the cost of the building blocks of the ordered chains inside this kernel
@@ -2330,11 +2499,17 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         probe[3] = x + z + k;
     }
 #endif
-    if (!s.done) setup();
+    if (!s.done && lead) setup();  // (the members wait at the structure pass's team_sync)
     if (t == 0 && g.E == 0) s.done = 1;  // no edges: nothing to optimise, the map goes back through the converters
     __syncthreads();
     for (int pass = 0; pass < 2 && !s.done; pass++) {
-        structure();
+        if (lead) {
+            structure();
+            if (t == 0) g.team->unsup = s.unsup;
+        }
+        team_sync(b);
+        load_team();
+        if (s.unsup) break;
         LBG_MARK(1);
         const int n = 6 * s.np;
         // the factorisation's operands in LDS for n <= kLdsN: L, its column structures, the rows' pattern orders, P
@@ -2345,14 +2520,14 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         int* RS = (int*)(dyn + fl.RS);
         int* PI = (int*)(dyn + fl.PI);
         if (t == 0) {
-            s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1; s.sorder_n = 0;
+            s.it = 0; s.max_it = pass ? 10 : 5; s.need_err = 1;
         }
         __syncthreads();
         // SparseOptimizer::optimize on a graph without active edges (every edge relabelled): nothing to do
         const bool empty = s.nact == 0 || (s.np == 0 && s.nl == 0);
         // SparseOptimizer::optimize(max_it) with OptimizationAlgorithmLevenberg
         for (int it = 0; it < (empty ? 0 : pass ? 10 : 5); it++) {
-            if (t == 0 && stop_requested(b, p, s)) {  // for (...; !terminate(); ...)
+            if (t == 0 && stop_requested(b, s)) {  // for (...; !terminate(); ...)
                 s.stopped = pass == 0 && s.trials == 0 ? 1 : 2;
                 s.done = 1;
             }
@@ -2360,8 +2535,8 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             if (s.done) break;
             if (s.need_err) {
                 LBG_MARK(1);
-                errors();
-                __syncthreads();
+                errors_phase();
+                team_sync(b);
                 LBG_MARK(2);
                 sums_staged(lbg_pad32(g.E), 0);
                 __syncthreads();
@@ -2369,10 +2544,12 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             }
             if (t == 0) s.iniChi = s.currentChi;
             build_system();
-            __syncthreads();
+            team_sync(b);
             LBG_MARK(4);
             if (t == 0) {
-                if (it == 0) { s.lambda = 1e-5 * s.red[0][1]; s.ni = 2; s.nBad = 0; }
+                double mx = 0.0;  // computeLambdaInit: the members' maxima
+                for (int q = 0; q < s.T; q++) mx = fmax(mx, g.team->mx[q]);
+                if (it == 0) { s.lambda = 1e-5 * mx; s.ni = 2; s.nBad = 0; }
                 s.qmax = 0;
             }
             __syncthreads();
@@ -2381,44 +2558,50 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             while (more) {
                 LBG_MARK(1);
                 schur();
-                __syncthreads();
+                team_sync(b);
                 LBG_MARK(5);
-                if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
-                    for (int i = t; i <= n * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
-                    for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
-                    const int nz = g.rs_off[n];
-                    for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
-                    for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
-                    double* SP = (double*)(dyn + fl.SP);  // S, packed upper
-                    for (int i = t; i < n * n; i += kT) {
-                        const int r = i / n, c = i - r * n;
-                        if (r <= c) SP[(c * (c + 1)) / 2 + r] = g.S[i];
+                if (lead) {
+                    if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
+                        for (int i = t; i <= n * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
+                        for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
+                        const int nz = g.rs_off[n];
+                        for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
+                        for (int i = t; i < n; i += kT) PI[i] = g.Pinv[i];
+                        double* SP = (double*)(dyn + fl.SP);  // S, packed upper
+                        for (int i = t; i < n * n; i += kT) {
+                            const int r = i / n, c = i - r * n;
+                            if (r <= c) SP[(c * (c + 1)) / 2 + r] = g.S[i];
+                        }
+                        __syncthreads();
                     }
+#ifdef SPSLAM_LBG_DIAG
+                    const long long f0 = wall_clock64();
+#endif
+                    if (t < 64) {
+                        if (n <= 64) factor_solve<1, true>();
+                        else if (n <= kLdsN) factor_solve<2, true>();
+                        else if (n <= 128) factor_solve<2, false>();
+                        else if (n <= 192) factor_solve<3, false>();
+                        else if (n <= 256) factor_solve<4, false>();
+                        else factor_solve<6, false>();
+                    }
+                    if (n == 0 && t == 0) s.ok = 1;
+#ifdef SPSLAM_LBG_DIAG
+                    if (t == 0) s.dg[5] += s.dg[4] - f0;
+#endif
                     __syncthreads();
+                    if (t == 0) g.team->ok = s.ok;
                 }
-#ifdef SPSLAM_LBG_DIAG
-                const long long f0 = wall_clock64();
-#endif
-                if (t < 64) {
-                    if (n <= 64) factor_solve<1, true>();
-                    else if (n <= kLdsN) factor_solve<2, true>();
-                    else if (n <= 128) factor_solve<2, false>();
-                    else if (n <= 192) factor_solve<3, false>();
-                    else if (n <= 256) factor_solve<4, false>();
-                    else factor_solve<6, false>();
-                }
-                if (n == 0 && t == 0) s.ok = 1;
-#ifdef SPSLAM_LBG_DIAG
-                if (t == 0) s.dg[5] += s.dg[4] - f0;
-#endif
+                team_sync(b);
+                if (!lead && t == 0) s.ok = g.team->ok;
                 __syncthreads();
                 LBG_MARK(6);
                 update();
-                __syncthreads();
+                team_sync(b);
                 LBG_MARK(1);
-                errors();
+                errors_phase();
                 scale_terms();
-                __syncthreads();
+                team_sync(b);
                 LBG_MARK(2);
                 sums_staged(lbg_pad32(g.E), lbg_pad32(n + 3 * s.nl));
                 __syncthreads();
@@ -2444,13 +2627,13 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                     s.qmax++;
                     s.trials++;
                     s.red[0][2] = r;
-                    const bool stop = stop_requested(b, p, s);
+                    const bool stop = stop_requested(b, s);
                     s.flag = r < 0 && s.qmax < 10 && !stop;  // do { ... } while (rho < 0 && qmax < max && !terminate())
                 }
                 __syncthreads();
                 if (!s.accepted) {
                     restore();
-                    __syncthreads();
+                    team_sync(b);
                 }
                 rho = s.red[0][2];
                 more = s.flag;
@@ -2475,48 +2658,38 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         }
         if (s.done) break;
         if (pass == 0) {
-            if (t == 0 && stop_requested(b, p, s)) {  // bDoMore = !*pbStopFlag
+            if (t == 0 && stop_requested(b, s)) {  // bDoMore = !*pbStopFlag
                 s.stopped = 2;
                 s.done = 1;
             }
             __syncthreads();
             if (s.done) break;
             // relabel with the errors cached by the last computeActiveErrors, drop the robust kernels
-            for (int e = t; e < g.E; e += kT) {
-                double info[3];
-                const int ty = g.e_type[e];
-                info_of(g, C, e, ty, info);
-                const double chi = chi2_of(g.err + 3 * e, info, edge_dim(ty));
-                bool bad;
-                if (ty == 0) bad = chi > 5.991 || !depth_positive(g, e);
-                else if (ty == 1) bad = chi > 7.815 || !depth_positive(g, e);
-                else if (ty == 2) bad = chi > C.plane_chi;
-                else bad = chi > C.vp_chi;
-                if (bad) g.e_level[e] = 1;
-            }
+            relabel();
             if (t == 0) s.robust = 0;
-            __syncthreads();
+            team_sync(b);
         }
     }
-    __syncthreads();
+    team_sync(b);  // every member's writes are in before the leader's outputs
+    if (!lead) return;
+    if (s.unsup) {  // more free poses than kLbgMaxFree: nothing written but the status
+        if (t == 0) {
+            b.res[p] = spslam_lba_result{};
+            b.res[p].status = -2;
+        }
+        return;
+    }
     outputs(b, p);
     if (t == 0) {  // setup / structure / update / decide, errors, ordered chains, terms, Schur, factor + solve, sums
         b.res[p].phase_us[0] = (float)((wall_clock64() - t0) * 0.01);
         for (int i = 1; i < 8; i++) b.res[p].phase_us[i] = (float)(s.ph[i] * 0.01);
-        b.res[p].pad = (int)(s.tB * 0.01);  // diagnostic: build phase (B) us; phase_us[7]: (A) of plane chunks
+        b.res[p].pad = (int)(s.tB * 0.01);  // diagnostic: build phase (B) us
 #ifdef SPSLAM_LBG_DIAG  // Schur: staging wait, BDinv, chains, commit; factor-only
         for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
         b.res[p].phase_us[5] = (float)(s.dg[6] * 1e-3);  // factor: step-loop shader kcycles,
         b.res[p].phase_us[6] = (float)(s.dg[7] * 1e-3);  //   pivot-update kcycles,
         b.res[p].pad = (int)s.dg[8];                     //   steps
-        b.res[p].phase_us[4] = (float)(s.dg[9] * 0.01);  // build: landmark segments (us)
-        b.res[p].phase_us[1] = (float)s.dg[10] / (float)max(1ll, s.dg[11]);  // segments: cycles per edge,
-        b.res[p].phase_us[2] = (float)s.dg[11] / (float)max(1ll, s.dg[13]);  //   edges per segment,
-        b.res[p].phase_us[3] = (float)(s.dg[12] * 1e-3);                     //   longest loop (kcycles)
         b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
-#ifdef SPSLAM_LBG_DIAG_SCHUR  // Schur sub-phases (us) in slots 1-4 instead of the segment statistics
-        for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
-#endif
 #endif
 #ifdef SPSLAM_LBG_PROBE  // shader-clock ticks per (1) add, (2) add of a readlane, (3) readlane chain
         for (int i = 0; i < 3; i++) b.res[p].phase_us[1 + i] = (float)probe[i];
@@ -2532,8 +2705,11 @@ hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, Ker
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k_lba_g2o, hipFuncAttributeMaxDynamicSharedMemorySize, kDynAlloc);
     if (attr != hipSuccess) return attr;
+    if (b.team < 1 || b.team > kLbgTeamMax) return hipErrorInvalidValue;
+    const hipError_t z = hipMemsetAsync(b.ctl, 0, lbg_ctl_ints(b.n) * sizeof(int), s);
+    if (z != hipSuccess) return z;
     if (timer) timer->begin(kKindLba, s);
-    hipLaunchKernelGGL(k_lba_g2o, dim3(b.n), dim3(kT), kDynAlloc, s, b, C);
+    hipLaunchKernelGGL(k_lba_g2o, dim3(b.n * b.team), dim3(kT), kDynAlloc, s, b, C);
     if (timer) timer->end(kKindLba, s);
     return hipGetLastError();
 }

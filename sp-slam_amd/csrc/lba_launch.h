@@ -112,23 +112,43 @@ struct LbaBatch {
 };
 
 // ---------------------------------------------------------------------------------------------------------------
-// g2o-order LocalBundleAdjustment (lba_g2o.hip, the default): one persistent workgroup per problem runs the whole
-// schedule with every sum in g2o's order.  Per-problem scratch, computed identically on host and device.
+// g2o-order LocalBundleAdjustment (lba_g2o.hip, the default): a team of persistent workgroups per problem (one CU
+// each) runs the whole schedule with every sum in g2o's order.  Per-problem scratch, computed identically on host and
+// device.
 constexpr int kLbgThreads = 512;
+constexpr int kLbgMaxKeyframes = 1024;  // local + fixed keyframes per problem
+constexpr int kLbgMaxFree = 64;         // free (local) poses with an active edge: pose masks are 64-bit, n <= 384
+constexpr int kLbgTeamMax = 16;         // workgroups per problem
+// What the team's leader publishes for its members after each structure pass (lba_g2o.hip load_team).
+struct LbgTeam {
+    int np, nl, nact, nch, nb, ok, unsup;
+    int stop_gen;               // the team barrier at which the leader first saw pbStopFlag raised (0: not yet)
+    int eb[kLbgTeamMax + 1];    // buildSystem: member m sums the landmarks whose edges are [eb[m], eb[m + 1])
+    int npo[kLbgTeamMax + 1];   //   and the (free pose, term) chains of poses pown[npo[m] .. npo[m + 1])
+    int pown[kLbgMaxFree];
+    double mx[2 * kLbgTeamMax];  // computeLambdaInit: each member's largest |diagonal| (landmarks, poses)
+    uint64_t pat[kLbgMaxFree];
+    short hidx[kLbgMaxKeyframes];
+};
+__host__ __device__ inline int lbg_free_cap(int K) { return K < kLbgMaxFree ? K : kLbgMaxFree; }
 struct LbgLayout {
     size_t pose, pose_b, X, X_b, P, P_b, err, echi, sc, terms, Hll, bl, Dinv, db, blkB, Hps, S, bs, x, Ld;  // double
     size_t e_lm, e_kf, e_type, e_level, e_src, e_blk, lm_boff, lm_nb, lm_sorted, lm_hidx, hidx_lm, lmh_blk, pe_off,
-        pe_idx, Pinv, Pm, parent, rs_off, rs_idx, amd_Ci, amd_W, sch, sch_kb, eseg;                        // int
+        pe_idx, Pinv, Pm, parent, rs_off, rs_idx, amd_Ci, amd_W, sch, sch_kb, eseg, bord;                  // int
     size_t lmh_mask, lm_amask, Lbits, Abits;                                                                // uint64
+    size_t team;                                                                                            // LbgTeam
     size_t bytes;
 };
 __host__ __device__ inline int lbg_pad32(int n) { return (n + 31) & ~31; }
+// K keyframes (<= kLbgMaxKeyframes), the Hessian-sized arrays for at most lbg_free_cap(K) free poses
 __host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
     LbgLayout Ly{};
-    const size_t L = (size_t)Np + Nq, n = 6 * (size_t)K, Ep = lbg_pad32(E), Xn = lbg_pad32((int)(n + 3 * L));
+    const int Kf = lbg_free_cap(K);
+    const size_t L = (size_t)Np + Nq, n = 6 * (size_t)Kf, Ep = lbg_pad32(E), Xn = lbg_pad32((int)(n + 3 * L));
     const size_t nC = n * n + n * n / 5 + 2 * n;  // cs_amd's elbow room over the full symmetric pattern
     size_t o = 0;
     auto take = [&](size_t bytes) { const size_t r = o; o += (bytes + 255) & ~(size_t)255; return r; };
+    Ly.team = take(sizeof(LbgTeam));
     Ly.pose = take(K * 7 * 8); Ly.pose_b = take(K * 7 * 8);
     Ly.X = take(Np * 3 * 8); Ly.X_b = take(Np * 3 * 8);
     Ly.P = take(Nq * 4 * 8); Ly.P_b = take(Nq * 4 * 8);
@@ -136,17 +156,18 @@ __host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
     Ly.terms = take((size_t)E * kLbaCon * 8);
     Ly.Hll = take(L * 9 * 8); Ly.bl = take(L * 3 * 8); Ly.Dinv = take(L * 9 * 8); Ly.db = take(L * 3 * 8);
     Ly.blkB = take((size_t)E * 18 * 8);
-    Ly.Hps = take(K * 27 * 8); Ly.S = take(n * n * 8); Ly.bs = take(n * 8); Ly.x = take(Xn * 8);
+    Ly.Hps = take(Kf * 27 * 8); Ly.S = take(n * n * 8); Ly.bs = take(n * 8); Ly.x = take(Xn * 8);
     Ly.Ld = take(n * n * 8);
     Ly.e_lm = take((size_t)E * 4); Ly.e_kf = take((size_t)E * 4); Ly.e_type = take((size_t)E * 4);
     Ly.e_level = take((size_t)E * 4); Ly.e_src = take((size_t)E * 4); Ly.e_blk = take((size_t)E * 4);
     Ly.lm_boff = take(L * 4); Ly.lm_nb = take(L * 4); Ly.lm_sorted = take(L * 4); Ly.lm_hidx = take(L * 4);
-    Ly.hidx_lm = take(L * 4); Ly.lmh_blk = take((L + 1) * 4); Ly.pe_off = take((K + 1) * 4);
+    Ly.hidx_lm = take(L * 4); Ly.lmh_blk = take((L + 1) * 4); Ly.pe_off = take((Kf + 1) * 4);
     Ly.pe_idx = take((size_t)E * 4);
     Ly.Pinv = take(n * 4); Ly.Pm = take(n * 4); Ly.parent = take(n * 4); Ly.rs_off = take((n + 1) * 4);
     Ly.rs_idx = take((n * (n + 1) / 2 + 1) * 4);
     Ly.amd_Ci = take((nC + 1) * 4); Ly.amd_W = take(10 * (n + 1) * 4);
     Ly.sch = take((L + 2) * 4); Ly.sch_kb = take((L + 2) * 4); Ly.eseg = take((size_t)E * 16);
+    Ly.bord = take(((size_t)Kf * (Kf + 1) / 2 + 1) * 4);
     Ly.lmh_mask = take(L * 8); Ly.lm_amask = take(L * 8); Ly.Lbits = take((n + 1) * 6 * 8); Ly.Abits = take(n * 6 * 8);
     Ly.bytes = o;
     return Ly;
@@ -166,8 +187,13 @@ struct LbgBatch {
     spslam_lba_result* res;
     const int32_t* stop;  // per problem pbStopFlag (device-visible; NULL = no flag)
     int stop_after;       // test hook: the flag counts as raised once a problem has run this many trials (-1 off)
+    int team;             // workgroups per problem (1 .. kLbgTeamMax); the grid is n * team
+    int* ctl;             // lbg_ctl_ints(n) ints, zeroed before the launch: [0] the workgroups' arrival ticket,
+                          //   [16 (p + 1)] problem p's team barrier counter (one 64-byte line each)
 };
-// One launch: the whole optimize(5) / relabel / optimize(10) schedule of every problem, no host round trip.
+__host__ __device__ inline size_t lbg_ctl_ints(int n) { return 16 * ((size_t)n + 1); }
+// One launch: the whole optimize(5) / relabel / optimize(10) schedule of every problem, no host round trip.  The
+// ctl block is cleared on `s` first.
 hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer);
 
 // Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase

@@ -74,6 +74,7 @@ struct EventTimer : KernelTimer {
 
 struct spslam_ctx {
     int device = 0;
+    int num_cus = 256;  // compute units of the device (spslam_create)
     hipStream_t stream = nullptr;
     spslam_orb_params p{};
     std::string err;
@@ -136,6 +137,12 @@ struct spslam_ctx {
     int32_t* d_lba_stop = nullptr;    // its device alias (hipHostGetDevicePointer)
     int lba_stop_after = -1;          // spslam_lba_debug_stop_after
     int lba_order = SPSLAM_LBA_G2O_ORDER;  // spslam_lba_set_order
+    int lba_team = 0;                 // spslam_lba_set_team (0: as many workgroups per problem as fill the chip)
+    int* d_lba_ctl = nullptr;         // the g2o-order launch's tickets and team barrier counters
+    size_t lba_ctl_cap = 0;           //   (ints)
+    hipEvent_t lba_done = nullptr;    // recorded after each LBA launch: the next call's stream waits on it before it
+                                      //   rewrites the offsets, the ctl block or the scratch (one LBA call in flight
+                                      //   per context, whatever the streams)
     int pose_spin_cap = 0;            // spslam_debug_pose_spin_cap (0 = the kernel's default)
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
@@ -281,9 +288,11 @@ void free_all(spslam_ctx* c) {
                     c->d_planes1, c->d_plane_cnt1, c->d_inl1,     c->d_con1,   c->d_supp_scratch,
                     c->d_supp1,   c->d_supp_cnt1,  c->d_line1,    c->d_patch1,  c->d_frame1,
                     c->d_lba_scratch, c->d_lba_off, c->d_lba_stage, c->d_lba_work, c->d_assoc_dist, c->d_match_scratch,
-                    c->d_vocab, c->d_bow_scratch, c->d_bow_stage};
+                    c->d_vocab, c->d_bow_scratch, c->d_bow_stage, c->d_lba_ctl};
+    if (c->lba_done) (void)hipEventSynchronize(c->lba_done);
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    if (c->lba_done) (void)hipEventDestroy(c->lba_done);
     if (c->h_lba_stop) (void)hipHostFree(c->h_lba_stop);
     if (c->orb_fork) (void)hipEventDestroy(c->orb_fork);
     if (c->orb_join) (void)hipEventDestroy(c->orb_join);
@@ -311,6 +320,11 @@ int spslam_create(int device, const spslam_orb_params* params, spslam_ctx** out)
     spslam_ctx* c = new (std::nothrow) spslam_ctx();
     if (!c) return SPSLAM_ERR_ARG;
     c->device = device;
+    {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->num_cus = cus;
+    }
     c->p = *params;
     if (c->p.nlevels < 1 || c->p.nlevels > SPSLAM_MAX_LEVELS || c->p.nfeatures < 1 || c->p.scale_factor <= 1.f ||
         c->p.width < 64 || c->p.height < 64 || c->p.max_batch < 1) {
@@ -1046,6 +1060,13 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     C.delta_plane = (float)std::sqrt(cfg->chi);  // const float deltaPlane = sqrt(planeChi)
     C.delta_vp = (float)std::sqrt(cfg->vp_chi);
     std::vector<long long> off(n);
+    HIP_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
+    if (!c->lba_done) HIP_CHECK(c, hipEventCreateWithFlags(&c->lba_done, hipEventDisableTiming));
+    // the previous LBA call of this context (on any stream) has finished reading the offsets, ctl and scratch
+    // before this one's copies on `s` rewrite them (recorded below after every launch; a never-recorded event
+    // is complete)
+    HIP_CHECK(c, hipStreamWaitEvent(s, c->lba_done, 0));
     if (c->lba_order == SPSLAM_LBA_G2O_ORDER) {
         size_t total = 0;
         for (int i = 0; i < n; i++) {
@@ -1056,11 +1077,9 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
                 (p.n_planes && (!d_planes || !d_plane_obs || !d_pl_out || !d_plane_obs_outlier)))
                 return fail(c, SPSLAM_ERR_ARG, "missing LBA buffers%s", "");
             off[i] = (long long)total;
-            total += lbg_layout(std::min(p.n_kf, kLbaMaxKeyframes), p.n_points, p.n_planes,
+            total += lbg_layout(std::min(p.n_kf, kLbgMaxKeyframes), p.n_points, p.n_planes,
                                 p.n_point_obs + p.n_plane_obs).bytes;
         }
-        HIP_CHECK(c, hipSetDevice(c->device));
-        hipStream_t s = (hipStream_t)hip_stream;
         if (total > c->lba_scratch_bytes) {
             HIP_CHECK(c, hipStreamSynchronize(s));
             if (c->d_lba_scratch) (void)hipFree(c->d_lba_scratch);
@@ -1076,11 +1095,22 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
             HIP_CHECK(c, hipMalloc(&c->d_lba_off, (size_t)n * sizeof(long long)));
             c->lba_off_cap = n;
         }
+        if (lbg_ctl_ints(n) > c->lba_ctl_cap) {
+            HIP_CHECK(c, hipStreamSynchronize(s));
+            if (c->d_lba_ctl) (void)hipFree(c->d_lba_ctl);
+            c->d_lba_ctl = nullptr;
+            HIP_CHECK(c, hipMalloc(&c->d_lba_ctl, lbg_ctl_ints(n) * sizeof(int)));
+            c->lba_ctl_cap = lbg_ctl_ints(n);
+        }
+        // workgroups per problem: the context's setting, else as many as fill the chip's CUs (one each), at most 8
+        int team = c->lba_team;
+        if (team <= 0) team = std::max(1, std::min(8, c->num_cus / n));
         HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
         LbgBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                    d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
-                   c->lba_stop_after};
+                   c->lba_stop_after, team, c->d_lba_ctl};
         HIP_CHECK(c, lba_run_g2o(B, C, s, c->timer));
+        HIP_CHECK(c, hipEventRecord(c->lba_done, s));
         if (stop_src) {  // host-buffer entry: mirror the caller's bool into the device-visible flag while it runs
             hipEvent_t ev;
             HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1130,8 +1160,6 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         for (int e = 0; e < p.n_point_obs; e += seg_own) sg.push_back(int2{i, e});
         for (int q = 0; q < p.n_planes; q += kLbaChunk / 64) pm.push_back(int2{i, p.n_points + q});
     }
-    HIP_CHECK(c, hipSetDevice(c->device));
-    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     if (total > c->lba_scratch_bytes) {
         HIP_CHECK(c, hipStreamSynchronize(s));
         if (c->d_lba_scratch) (void)hipFree(c->d_lba_scratch);
@@ -1178,9 +1206,16 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
                (int*)(c->d_lba_work + work.size() - 1), d_stop_flags, c->lba_stop_after};
     // optimize(5) + optimize(10), at most 10 trials per iteration, plus the two structure steps
     HIP_CHECK(c, lba_run(B, W, C, 15 * 10 + 4, s, c->timer, nullptr, stop_src, stop_mirror));
+    HIP_CHECK(c, hipEventRecord(c->lba_done, s));
     return SPSLAM_OK;
 }
 }  // namespace
+
+int spslam_lba_set_team(spslam_ctx* c, int workgroups) {
+    if (!c || workgroups < 0 || workgroups > kLbgTeamMax) return SPSLAM_ERR_ARG;
+    c->lba_team = workgroups;
+    return SPSLAM_OK;
+}
 
 int spslam_lba_set_order(spslam_ctx* c, int order) {
     if (!c || (order != SPSLAM_LBA_G2O_ORDER && order != SPSLAM_LBA_FAST_ORDER)) return SPSLAM_ERR_ARG;

@@ -28,7 +28,7 @@ assert LBA_PLANE_OBS_DTYPE.itemsize == 24 and LBA_PROBLEM_DTYPE.itemsize == 32 a
 
 
 spslam_gpu.EXPORTED += ["spslam_lba_optimize", "spslam_lba_optimize_batch_device", "spslam_lba_debug_stop_after",
-                        "spslam_lba_set_order"]
+                        "spslam_lba_set_order", "spslam_lba_set_team"]
 G2O_ORDER, FAST_ORDER = 0, 1  # SPSLAM_LBA_G2O_ORDER (default, bit-exact to the oracle) / SPSLAM_LBA_FAST_ORDER
 
 PLANE_CONFIG = np.array([1.0, 100.0, 0.5, 0.5, 1000.0, 200.0], np.float64)  # ICL.yaml Plane.* keys (Chi 1000, VPChi 200)
@@ -40,6 +40,7 @@ def _bind(lib):
     lib.spslam_lba_optimize_batch_device.argtypes = [vp, ctypes.c_int] + [vp] * 16
     lib.spslam_lba_debug_stop_after.argtypes = [vp, ctypes.c_int]
     lib.spslam_lba_set_order.argtypes = [vp, ctypes.c_int]
+    lib.spslam_lba_set_team.argtypes = [vp, ctypes.c_int]
 
 
 def _addr(flag):
@@ -79,6 +80,11 @@ class LocalBA:
     def set_order(self, order: int):
         """G2O_ORDER (default): g2o's summation order, bit-exact to the oracle; FAST_ORDER: the phase kernels."""
         self.ex._check(self.ex.lib.spslam_lba_set_order(self.ex.ctx, int(order)))
+
+    def set_team(self, workgroups: int):
+        """Workgroups per problem of the g2o-order launch (0 = fill the chip, at most 8); results do not depend on
+        it."""
+        self.ex._check(self.ex.lib.spslam_lba_set_team(self.ex.ctx, int(workgroups)))
 
     def debug_stop_after(self, trials: int):
         """Test hook: the following calls see pbStopFlag raised after `trials` LM trials (-1 = off)."""

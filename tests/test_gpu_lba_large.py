@@ -1,6 +1,13 @@
-"""GPU parity: LocalBundleAdjustment with large local windows (18 and 25 free poses: reduced systems of 108 and
-150 rows, factorised with L in global memory past the LDS-resident size), bit-exact to the CPU oracle as in
-test_gpu_lba.py."""
+"""GPU parity: LocalBundleAdjustment with large local windows, bit-exact to the CPU oracle as in test_gpu_lba.py.
+
+The reference collects every covisible keyframe and every fixed camera that sees a local point or plane, with no cap
+(src/Optimizer.cc:1157-1250).  The device takes up to 1024 keyframes per problem of which up to 64 free poses (the
+64-bit pose masks; a reduced system of up to 384 rows).  Covered here: 18 / 25 free poses (n = 108 / 150: the
+factorisation's L in global memory past the LDS-resident n <= 96), 40 and 62 free poses (n = 240 / 372: four and six
+registers per lane, the dense pattern's 820 / 1953 Schur blocks past one task round), a window of 80 keyframes (48
+free + 32 fixed: more keyframes than the 64-bit masks, fewer free poses), and a window with more than 64 free poses
+(status -2, nothing else written).  And the team split: the same problem solved by 1 .. 8 workgroups is bit-identical
+(every sum keeps its order whatever the split)."""
 import numpy as np
 import pytest
 
@@ -16,14 +23,45 @@ def lba():
     ex.close()
 
 
-@pytest.mark.parametrize("n_kf,n_fixed", [(20, 2), (27, 2)])
-def test_lba_large_windows_match_oracle(lba, n_kf, n_fixed):
-    """18 free poses (n = 108, two registers of the factorisation wave per lane) and 25 (n = 150, three); both
-    past the LDS-resident L (n <= 96); several Schur task rounds per lane."""
-    import oracle_lba
+def _window(n_kf, n_fixed, step=4, n_points=2000, seed=None, planes=True):
     import synth
-    rng = np.random.default_rng(300 + n_kf)
-    P = synth.lba_problem(synth.Scene(4, n_boxes=4), list(range(0, 4 * n_kf, 4)), rng, n_fixed=n_fixed,
-                          n_points=2000, first_kf_id=1, with_planes=True)
+    rng = np.random.default_rng(300 + n_kf if seed is None else seed)
+    return synth.lba_problem(synth.Scene(4, n_boxes=4), list(range(0, step * n_kf, step)), rng, n_fixed=n_fixed,
+                             n_points=n_points, first_kf_id=1, with_planes=planes)
+
+
+@pytest.mark.parametrize("n_kf,n_fixed,step", [(20, 2, 4), (27, 2, 4), (42, 2, 2), (64, 2, 3), (80, 32, 3)])
+def test_lba_large_windows_match_oracle(lba, n_kf, n_fixed, step):
+    """Free poses 18 .. 62 (n = 108 .. 372: one to six registers of the factorisation wave per lane, L past the
+    LDS-resident size), dense covisibility (step 2 / 3: every pose coupled with most others, hundreds of Schur
+    blocks), and 80 keyframes of which 32 fixed."""
+    import oracle_lba
     import test_gpu_lba
-    test_gpu_lba._assert_identical(lba(*P[:6]), oracle_lba.lba_optimize(*P[:6]), f"{n_kf} keyframes")
+    P = _window(n_kf, n_fixed, step)
+    o = oracle_lba.lba_optimize(*P[:6])
+    test_gpu_lba._assert_identical(lba(*P[:6]), o, f"{n_kf} keyframes")
+
+
+def test_lba_more_free_poses_than_masks(lba):
+    """66 free poses: past the 64-bit pose masks -- status -2 (the drop-in entry reports the rejection), nothing
+    else written."""
+    import spslam_gpu
+    P = _window(68, 2, 3, n_points=600)
+    with pytest.raises(spslam_gpu.SpslamError, match="rejected"):
+        lba(*P[:6])
+    hdr, kf_out, pt_out, pl_out, po_out, plo_out, res = __import__("test_gpu_lba")._batch(lba, [P])
+    assert int(res[0]["status"]) == -2 and not kf_out.any() and not pt_out.any() and not po_out.any()
+
+
+@pytest.mark.parametrize("team", [1, 2, 3, 5, 8])
+def test_lba_team_split_bit_identical(lba, team):
+    """The same problems with 1 .. 8 workgroups per problem (the Schur chains, the build's landmark runs and pose
+    chains, errors and updates split differently) -- bit-identical to the oracle every time."""
+    import oracle_lba
+    import test_gpu_lba
+    lba.set_team(team)
+    try:
+        for k, P in enumerate(test_gpu_lba._problems()[:2] + [_window(27, 2, 4, n_points=1200, seed=9)]):
+            test_gpu_lba._assert_identical(lba(*P[:6]), oracle_lba.lba_optimize(*P[:6]), f"team {team} problem {k}")
+    finally:
+        lba.set_team(0)
