@@ -39,7 +39,7 @@ constexpr int kMaxKF = kLbgMaxKeyframes;  // keyframes (local + fixed)
 constexpr int kMaxK = kLbgMaxFree;        // free poses (Hessian blocks)
 constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
-constexpr int kDynAlloc = 152 * 1024;   // allocated: kDyn plus the Schur phase's staged Bb terms and block table
+constexpr int kDynAlloc = 154 * 1024;   // allocated: kDyn plus the Schur phase's staged Bb terms and block tables
                                         //   (every phase but the Schur one sizes itself against kDyn)
 constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised in LDS (L, S packed: 133 KB)
 constexpr int kSchurLm = 64;            // Schur phase: landmarks per staged chunk (one bit each in a 64-bit mask)
@@ -53,10 +53,11 @@ struct Sh {
     unsigned char kact[kMaxKF];         // structure: keyframes with an active edge
     int hpose[kMaxK];                   // Hessian index -> keyframe
     int pdeg[kMaxK];                    // poses coupled with each pose (itself included)
-    int np, nl, nact, nch, nb, flag, unsup;
+    int np, nl, nact, nch, nb, flag, unsup, dense;
     // the team (one workgroup per member, lba_g2o's header): problem, member, size, barrier generation; this
     // member's buildSystem share (landmark-aligned edge range, its free poses)
-    int p, m, T, gen, eb0, eb1, npown;
+    int p, m, T, gen, eb0, eb1, npown, bo0, bo1;
+    uint64_t rmask;                     // this member's Schur block rows
     int pown[kMaxK];
     // LM / schedule state (every member computes it identically between barriers)
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
@@ -737,13 +738,14 @@ __device__ __forceinline__ bool bit_of(const PU* bits, int i) { return (bits[i >
 
 // ---------------------------------------------------------------- the members' shares (leader, per pass)
 // Published in the team record with the structure state the members copy (load_team):
-//  * the Schur chains: every pattern block's chain length (the landmarks whose active edges see both of its poses),
-//    the blocks longest first in g.bord; member m takes the order's entries j T + m (even j) / j T + T - 1 - m (odd
-//    j), so every member gets chains of every length (schur());
+//  * the Schur complement by block rows: every pattern block's chain length (the landmarks whose active edges see
+//    both of its poses), the rows (pose i1 with its blocks (i1, i2 >= i1)) dealt to the members by work, largest
+//    first to the least loaded (LPT), each member's blocks longest first in g.bord[bo[m] .. bo[m + 1]) -- a member
+//    then forms BDinv only for its own rows (schur());
 //  * buildSystem: the landmarks in list order -- their edges are one contiguous range -- cut into T runs of about
 //    equal work (a plane edge weighs kPlaneW point edges: the Jacobians of its landmark side and of its pose side are
 //    read back from the numeric-differentiation pass), and the free poses dealt by edge count, largest first,
-//    snaking the same way (build_system()).
+//    snaking (build_system()).
 constexpr int kPlaneW = 4;
 __device__ __forceinline__ int snake_pick(int j, int m, int T) { return j * T + ((j & 1) ? T - 1 - m : m); }
 __device__ __noinline__ void team_plan() {
@@ -753,8 +755,11 @@ __device__ __noinline__ void team_plan() {
     const int np = s.np, nl = s.nl, T = s.T;
     LbgTeam GL* R = g.team;
     int* len = (int*)lbg_dyn;                        // [nb]
-    int* rowoff = len + kMaxK * (kMaxK + 1) / 2;     // [np]
+    int* brow = len + kMaxK * (kMaxK + 1) / 2;       // [nb] block -> its row i1
+    int* rowoff = brow + kMaxK * (kMaxK + 1) / 2;    // [np]
     int* prank = rowoff + kMaxK;                     // [np] free poses by edge count
+    int* rw = prank + kMaxK;                         // [np] row work
+    int* rmem = rw + kMaxK;                          // [np] row -> member
     if (t == 0) {  // block ids: (i, i) -> i; (i1 < i2) -> rowoff[i1] + rank of i2 among row i1's bits above i1
         int o = np;
         for (int a = 0; a < np; a++) {
@@ -766,6 +771,10 @@ __device__ __noinline__ void team_plan() {
     __syncthreads();
     const int nb = s.nb;
     for (int i = t; i < nb; i += kT) len[i] = 0;
+    if (t < np) {
+        brow[t] = t;
+        for (int j = rowoff[t]; j < rowoff[t] + __popcll(s.pat[t]) - 1; j++) brow[j] = t;
+    }
     __syncthreads();
     for (int h = t; h < nl; h += kT) {
         uint64_t a = g.lmh_mask[h];
@@ -792,14 +801,47 @@ __device__ __noinline__ void team_plan() {
         prank[r] = t;
     }
     __syncthreads();
-    for (int i = t; i < nb; i += kT) {  // longest chain first (ties: block id)
-        const int w = len[i];
+    if (t < np) {  // a row's work: its blocks' chains (+1 each: the block's own cost)
+        int w = len[t] + 1;
+        for (int j = rowoff[t]; j < rowoff[t] + __popcll(s.pat[t]) - 1; j++) w += len[j] + 1;
+        rw[t] = w;
+    }
+    __syncthreads();
+    if (t == 0) {  // LPT: rows by work, each to the least loaded member
+        long long load[kLbgTeamMax];
+        uint64_t rm[kLbgTeamMax];
+        for (int mm = 0; mm < T; mm++) { load[mm] = 0; rm[mm] = 0; }
+        uint64_t done = 0;
+        for (int q = 0; q < np; q++) {
+            int best = -1;
+            for (int a = 0; a < np; a++)
+                if (!((done >> a) & 1ull) && (best < 0 || rw[a] > rw[best])) best = a;
+            done |= 1ull << best;
+            int mm = 0;
+            for (int u = 1; u < T; u++)
+                if (load[u] < load[mm]) mm = u;
+            load[mm] += rw[best];
+            rm[mm] |= 1ull << best;
+            rmem[best] = mm;
+        }
+        int o = 0;
+        for (int mm = 0; mm < T; mm++) {  // blocks per member -> the members' segments of bord
+            R->bo[mm] = o;
+            R->rmask[mm] = rm[mm];
+            for (int a = 0; a < np; a++)
+                if ((rm[mm] >> a) & 1ull) o += __popcll(s.pat[a]);
+        }
+        R->bo[T] = o;
+    }
+    __syncthreads();
+    for (int i = t; i < nb; i += kT) {  // each member's blocks longest first (ties: block id)
+        const int w = len[i], mi = rmem[brow[i]];
         int r = 0;
         for (int j = 0; j < nb; j++) {
             const int v = len[j];
-            r += v > w || (v == w && j < i);
+            r += rmem[brow[j]] == mi && (v > w || (v == w && j < i));
         }
-        g.bord[r] = i;
+        g.bord[R->bo[mi] + r] = i;
     }
     // landmark runs: exclusive prefix of the edge weights in list order; run m ends after the landmark whose weight
     // interval holds W m / T
@@ -866,6 +908,9 @@ __device__ __noinline__ void load_team() {
         s.eb0 = R->eb[s.m];
         s.eb1 = R->eb[s.m + 1];
         s.npown = o1 - o0;
+        s.bo0 = R->bo[s.m];
+        s.bo1 = R->bo[s.m + 1];
+        s.rmask = R->rmask[s.m];
     }
     if (t < o1 - o0) s.pown[t] = R->pown[o0 + t];
     __syncthreads();
@@ -904,6 +949,7 @@ __device__ __noinline__ void structure() {
             s.hpose[j] = k;
         }
         s.unsup = np > kMaxK;
+        s.dense = 0;
         if (!s.unsup)
             for (int j = 0; j < np; j++) s.hidx[s.hpose[j]] = (short)j;
         s.np = s.unsup ? 0 : np;
@@ -1056,7 +1102,11 @@ __device__ __noinline__ void structure() {
     const int dense = min(n - 2, max(16, (int)(10 * sqrt((double)n))));
     int alld = 1;
     for (int q = t; q < np; q += kT) alld &= 6 * s.pdeg[q] > dense;
+    int full = 1;  // every pose coupled with every other
+    for (int q = t; q < np; q += kT) full &= s.pat[q] == ((np == 64 ? ~0ull : (1ull << np) - 1ull) & ~((1ull << q) - 1ull));
+    full = block_and(full, s);
     if (block_and(alld, s)) {
+        if (t == 0) s.dense = full;
         for (int k = t; k < n; k += kT) g.Pinv[k] = k;  // every scalar dense: absorbed in index order (natural)
     } else {
         // full symmetric pattern (diagonal kept), columns sorted; cs_amd's elbow room
@@ -1725,18 +1775,22 @@ __device__ __noinline__ void build_system() {
 
 // ---------------------------------------------------------------- per trial
 
-// setLambda + the Schur complement (block_solver.hpp:367-436), this member's chains: one lane per (pattern block
-// (i1, i2), row r) holds S(6 i1 + r, 6 i2 .. 6 i2 + 5) (the diagonal block's lanes also Bb(6 i1 + r)) and subtracts
-// the landmarks' contributions in landmark order.  The member's blocks are every T-th of the longest-first order
-// (team_plan), so its waves hold chains of similar length.  Every member stages every landmark, in chunks of up to
-// 64: their Hpl blocks (one contiguous range, coalesced), masks, Hll and bl -- the chunk's (Hll + lambda)^-1 and
-// Dinv bl are formed in place (the same expressions as update()'s) -- then every block's BDinv = Bi Dinv (one thread
-// per block row) and every free pose's chunk landmarks as a bitmask; then the chains, each lane walking only the
-// landmarks that observe both of its poses (in landmark order) while the next chunk's records load into registers.
-#ifndef SPSLAM_LBG_SCHUR_TASKS
-#define SPSLAM_LBG_SCHUR_TASKS 2
+// setLambda + the Schur complement (block_solver.hpp:367-436), this member's block rows.  Every entry of a pattern
+// block (i1, i2) is its own chain in g2o's order: Hschur(6 i1 + r, 6 i2 + c) = 0 + Hpp (+ lambda) then, landmark by
+// landmark in landmark (vertex-id) order, -= (BDinv(r, 0) Bj(c, 0) + BDinv(r, 1) Bj(c, 1)) + BDinv(r, 2) Bj(c, 2); and
+// Bb(6 i1 + r) = 0 + the landmarks' (Bi db)(r) in the same order.  One wave per block: lane 6 r + c holds entry (r,
+// c), lanes 36 + r the diagonal block's Bb(r) (team_plan gives each member whole block rows, each wave up to kBW
+// blocks, longest chains dealt first).  Every member stages every landmark in chunks of up to 64: their Hpl blocks
+// (one contiguous range, coalesced), masks, Hll and bl -- the chunk's (Hll + lambda)^-1 and Dinv bl formed in place
+// (the expressions of update()) -- then BDinv = Bi Dinv and Bi db for the blocks of its own rows (one thread per
+// block row) and every free pose's chunk landmarks as a bitmask; then each wave, per block, compacts the chunk's
+// landmarks that observe both poses into a list of (BDinv block, Bj block) pairs held one per lane, and walks it with
+// the next landmark's operands loading while the current one is subtracted (the list read with v_readlane at the
+// loop counter: no load on the chain's critical path).
+#ifndef SPSLAM_LBG_SCHUR_BLOCKS
+#define SPSLAM_LBG_SCHUR_BLOCKS 8
 #endif
-constexpr int kSchurTasks = SPSLAM_LBG_SCHUR_TASKS;  // chains per lane per round
+constexpr int kBW = SPSLAM_LBG_SCHUR_BLOCKS;  // blocks per wave per round
 // (Hll + lambda)^-1 (Eigen's cofactor inverse) and Dinv bl of one landmark
 __device__ __forceinline__ void landmark_dinv(const double* H, const double* bv, double lam, double* Di, double* db) {
     double D[3][3];
@@ -1752,8 +1806,8 @@ __device__ __noinline__ void schur() {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int np = s.np, n = 6 * np, nch = s.nch;
     const double lam = s.lambda;
-    // LDS: the staged chunk (blocks, Dinv, Dinv bl | masks, block offsets, block -> landmark), its BDinv and the
-    // poses' landmark masks
+    // LDS: the staged chunk (blocks, Dinv, Dinv bl | masks, block offsets, block -> landmark, block -> pose), its
+    // BDinv and Bi db, the poses' landmark masks, the waves' candidate lists
     constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
     double* BUF = (double*)dyn;                          // [kBufD]
     double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
@@ -1762,26 +1816,33 @@ __device__ __noinline__ void schur() {
     uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
     int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
     unsigned short* OB = (unsigned short*)(SO + kSchurLm + 1);  // [kMaxK][kSchurLm] (pose, landmark) -> its block
-    unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk]
+    unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk] block -> landmark
+    unsigned char* BP = BL + kSchurBlk;                  // [kSchurBlk] block -> pose
+    using LdsU = __attribute__((address_space(3))) unsigned;
+    LdsU* LST = (LdsU*)(unsigned*)(((uintptr_t)(BP + kSchurBlk) + 3) & ~(uintptr_t)3);  // [kW][64]
     const double* SDi = BUF + kSchurBlk * 18;
     const double* Sdb = SDi + kSchurLm * 9;
     static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
-                      kSchurBlk <= kDynAlloc, "LDS");
+                      2 * kSchurBlk + 4 + kW * 64 * 4 <= kDynAlloc, "LDS");
     constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
-    // this member's blocks: entries snake_pick(j, m, T) of g.bord; task = 6 j + r
-    const int nb = s.nb, T = s.T, mm = s.m;
-    const int nbm = nb / T + ((nb % T) ? (((nb / T) & 1) ? (mm >= T - nb % T) : (mm < nb % T)) : 0);
-    for (int round = 0; round * kSchurTasks * kT < 6 * nbm; round++) {
-        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
-        double acc[kSchurTasks][6], cf[kSchurTasks];
+    const int bo0 = s.bo0, nbm = s.bo1 - s.bo0;
+    const uint64_t rmask = s.rmask;
+    // this lane's entry: (r, c) on lanes 0 .. 35, Bb(r) on lanes 36 .. 41 (its operand addresses clamped in range)
+    const bool ent = lane < 36;
+    const int er = ent ? lane / 6 : min(lane - 36, 5), ec = ent ? lane - 6 * (lane / 6) : 0;
+    using LdsD = const __attribute__((address_space(3))) double;
+    LdsD* pE = (LdsD*)(SD + 3 * er);   // (LDS address-space pointers: 32-bit address arithmetic, ds_* accesses)
+    LdsD* pJ = (LdsD*)(BUF + 3 * ec);
+    LdsD* pU = (LdsD*)(SU + er);
+    for (int round = 0; round * kW * kBW < nbm; round++) {
+        int i1[kBW], i2[kBW];
+        double acc[kBW];
 #pragma unroll
-        for (int k = 0; k < kSchurTasks; k++) {
-            i1[k] = -1; i2[k] = 0; rr[k] = 0;
-            const int task = (round * kSchurTasks + k) * kT + t;
-            if (task < 6 * nbm) {
-                const int jb = task / 6;
-                rr[k] = task - 6 * jb;
-                const int blk = g.bord[snake_pick(jb, mm, T)];
+        for (int k = 0; k < kBW; k++) {
+            i1[k] = -1; i2[k] = 0; acc[k] = 0.0;
+            const int jb = round * kW * kBW + snake_pick(k, wv, kW);
+            if (jb < nbm) {
+                const int blk = g.bord[bo0 + jb];
                 if (blk < np) {
                     i1[k] = i2[k] = blk;
                 } else {
@@ -1792,58 +1853,68 @@ __device__ __noinline__ void schur() {
                     i1[k] = a;
                     i2[k] = __ffsll((unsigned long long)row) - 1;
                 }
+                i1[k] = uni(i1[k]);
+                i2[k] = uni(i2[k]);
+                if (i1[k] == i2[k] && ent && ec >= er) {
+                    const double h = g.Hps[27 * i1[k] + upper_idx(er, ec)];
+                    acc[k] = 0.0 + (ec == er ? h + lam : h);
+                }
             }
-            const bool diag = i1[k] >= 0 && i1[k] == i2[k];
-            const int r = rr[k];
-#pragma unroll
-            for (int c = 0; c < 6; c++) {
-                double base = 0.0;
-                if (diag && c >= r) base = c == r ? g.Hps[27 * i1[k] + upper_idx(r, c)] + lam : g.Hps[27 * i1[k] + upper_idx(r, c)];
-                acc[k][c] = 0.0 + base;
-            }
-            cf[k] = 0.0;
         }
-        // chunk c's records into registers (global loads in flight), later into the staging buffer
+        // chunk c's records into registers (global loads in flight), later into the staging buffer.  Every load is
+        // unconditional (addresses clamped into the chunk; the surplus entries are never read) and nothing loaded is
+        // used before the commit, so no wait lands in the chunk loop; the chunk bounds (sch, sch_kb) of the chunk
+        // after next load one chunk ahead.
         double pv[kPer];
         uint64_t pmk = 0;
         int pof = 0, pof1 = 0;
-        auto prefetch = [&](int c) __attribute__((always_inline)) {
-            const int h0 = g.sch[c], h1 = g.sch[c + 1], kb0 = g.sch_kb[c], kb1 = g.sch_kb[c + 1];
+        auto prefetch = [&](int h0, int h1, int kb0, int kb1) __attribute__((always_inline)) {
             const int nbk = kb1 - kb0, nh = h1 - h0;
-            const gdouble* pb = g.blkB + (size_t)18 * kb0;
+            const int cb = max(nbk * 18 - 1, 0), ch = max(nh * 9 - 1, 0), cl = max(nh * 3 - 1, 0);
 #pragma unroll
             for (int q = 0; q < kPer; q++) {
                 const int i = t + q * kT;
-                double v = 0.0;
-                if ((q + 1) * kT <= kSchurBlk * 18) {  // (compile time) this load is in the Hpl block range
-                    if (i < nbk * 18) v = pb[i];
-                } else if (i < nbk * 18) v = pb[i];
-                else if (i >= kSchurBlk * 18 && i < kSchurBlk * 18 + nh * 9) v = g.Hll[9 * h0 + i - kSchurBlk * 18];
-                else if (i >= kSchurBlk * 18 + kSchurLm * 9 && i < kSchurBlk * 18 + kSchurLm * 9 + nh * 3)
-                    v = g.bl[3 * h0 + i - kSchurBlk * 18 - kSchurLm * 9];
-                pv[q] = v;
+                const gdouble* src;
+                if ((q + 1) * kT <= kSchurBlk * 18) {  // (compile time) the slice is in the Hpl block range
+                    src = g.blkB + (size_t)18 * kb0 + min(i, cb);
+                } else {
+                    const int j = i - kSchurBlk * 18, j2 = j - kSchurLm * 9;
+                    const gdouble* a = g.blkB + (size_t)18 * kb0 + min(i, cb);
+                    const gdouble* h = g.Hll + (size_t)9 * h0 + min(max(j, 0), ch);
+                    const gdouble* l = g.bl + (size_t)3 * h0 + min(max(j2, 0), cl);
+                    src = j < 0 ? a : (j2 < 0 ? h : l);
+                }
+                pv[q] = *src;
             }
-            if (t < nh) {
-                pmk = g.lmh_mask[h0 + t];
-                pof1 = g.lmh_blk[h0 + t + 1] - kb0;
-            }
-            if (t <= nh) pof = g.lmh_blk[h0 + t] - kb0;
+            const int tc = min(t, max(nh - 1, 0));
+            pmk = g.lmh_mask[h0 + tc];
+            pof = g.lmh_blk[h0 + min(t, nh)];
+            pof1 = g.lmh_blk[h0 + tc + 1];
         };
-        auto commit = [&](int c) __attribute__((always_inline)) {
-            const int nh = g.sch[c + 1] - g.sch[c];
+        auto commit = [&](int nh, int kb0) __attribute__((always_inline)) {
 #pragma unroll
             for (int q = 0; q < kPer; q++)
                 if (t + q * kT < kBufD) BUF[t + q * kT] = pv[q];
             if (t < nh) {
                 SM[t] = pmk;
-                for (int bk = pof; bk < pof1; bk++) BL[bk] = (unsigned char)t;
+                uint64_t m = pmk;
+                for (int bk = pof - kb0; bk < pof1 - kb0; bk++) {  // (the blocks of a landmark are in pose order)
+                    BL[bk] = (unsigned char)t;
+                    BP[bk] = (unsigned char)(__ffsll((unsigned long long)m) - 1);
+                    m &= m - 1;
+                }
             }
-            if (t <= nh) SO[t] = pof;
+            if (t <= nh) SO[t] = pof - kb0;
         };
         __syncthreads();  // the previous phase's LDS use is over
+        // chunk bounds: (h0, h1, kb0, kb1) of the current chunk, the next, and the one after (loading)
+        int cur_h0 = 0, cur_h1 = 0, cur_k0 = 0, cur_k1 = 0, nx_h1 = 0, nx_k1 = 0, nn_h1 = 0, nn_k1 = 0;
         if (nch > 0) {
-            prefetch(0);
-            commit(0);
+            cur_h0 = g.sch[0]; cur_h1 = g.sch[1]; cur_k0 = g.sch_kb[0]; cur_k1 = g.sch_kb[1];
+            nx_h1 = g.sch[min(2, nch)]; nx_k1 = g.sch_kb[min(2, nch)];
+            prefetch(cur_h0, cur_h1, cur_k0, cur_k1);
+            commit(cur_h1 - cur_h0, cur_k0);
+            nn_h1 = g.sch[min(3, nch)]; nn_k1 = g.sch_kb[min(3, nch)];
         }
         for (int c = 0; c < nch; c++) {
 #ifdef SPSLAM_LBG_DIAG
@@ -1854,8 +1925,8 @@ __device__ __noinline__ void schur() {
             long long d1 = wall_clock64();
             if (t == 0) s.dg[0] += d1 - d0;
 #endif
-            const int nh = g.sch[c + 1] - g.sch[c];
-            const int nbk = SO[nh];
+            const int nh = cur_h1 - cur_h0;
+            const int nbk = cur_k1 - cur_k0;
             if (t < nh) {  // the staged Hll, bl -> Dinv, Dinv bl, in place
                 double* Hd = BUF + kSchurBlk * 18 + 9 * t;
                 double* bd = BUF + kSchurBlk * 18 + kSchurLm * 9 + 3 * t;
@@ -1868,7 +1939,9 @@ __device__ __noinline__ void schur() {
             }
             __syncthreads();
             for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
-                const int bk = i / 6, r6 = i - 6 * bk, hb = BL[bk];
+                const int bk = i / 6, r6 = i - 6 * bk;
+                if (!((rmask >> BP[bk]) & 1ull)) continue;  // a block row of another member
+                const int hb = BL[bk];
                 const double* Bi = BUF + 18 * bk + 3 * r6;
                 const double* Di = SDi + 9 * hb;
                 const double* db = Sdb + 3 * hb;
@@ -1889,112 +1962,97 @@ __device__ __noinline__ void schur() {
             long long d2 = wall_clock64();
             if (t == 0) s.dg[1] += d2 - d1;
 #endif
-            if (c + 1 < nch) prefetch(c + 1);  // lands while chunk c is processed
-#pragma unroll
-            for (int k = 0; k < kSchurTasks; k++) {
-                if (i1[k] < 0) continue;
-                const int r = rr[k];
-                uint64_t cand = PM[i1[k]] & PM[i2[k]];
-#ifndef SPSLAM_LBG_SCHUR_PAIR
-                // one LDS round trip per landmark: the next landmark's blocks (the chunk's (pose, landmark) block
-                // table) load while this one's are subtracted, and the diagonal lanes' Bb term comes staged (SU)
-                // with the blocks instead of through a dependent load of Dinv bl
-                if (cand) {
-                    // LDS address-space pointers: 32-bit address arithmetic in the loop (generic pointers cost a
-                    // 64-bit multiply-add per operand address)
-                    using LdsD = const __attribute__((address_space(3))) double;
-                    using LdsU16 = const __attribute__((address_space(3))) unsigned short;
-                    LdsU16* O1 = (LdsU16*)(OB + kSchurLm * i1[k]);
-                    LdsU16* O2 = (LdsU16*)(OB + kSchurLm * i2[k]);
-                    LdsD* SDr = (LdsD*)(SD + 3 * r);
-                    LdsD* SUr = (LdsD*)(SU + r);
-                    LdsD* BUFl = (LdsD*)BUF;
-                    int hl = __ffsll((unsigned long long)cand) - 1;
-                    cand &= cand - 1;
-                    int b1 = O1[hl], b2 = O2[hl];
-                    // (opaque here: otherwise the first landmark's loads and the loop's next-landmark loads are
-                    // merged into one load at the top of the loop, behind a wait -- the round trip this loop avoids)
-                    asm volatile("" : "+v"(b1), "+v"(b2));
-                    for (;;) {
-                        LdsD* BD = SDr + __umul24(b1, 18);  // (24-bit products: full-rate multiplies)
-                        LdsD* Bj = BUFl + __umul24(b2, 18);
-                        const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
-                        double bj[18];
-#pragma unroll
-                        for (int q = 0; q < 18; q++) bj[q] = Bj[q];
-                        const double u = SUr[__umul24(b1, 6)];  // (b1 = b2 on the diagonal lanes)
-                        const bool more = cand != 0;
-                        const int hn = more ? __ffsll((unsigned long long)cand) - 1 : hl;
-                        cand &= cand - 1;
-                        const int b1n = O1[hn], b2n = O2[hn];
-#pragma unroll
-                        for (int cc = 0; cc < 6; cc++)
-                            acc[k][cc] -= (e0 * bj[3 * cc] + e1 * bj[3 * cc + 1]) + e2 * bj[3 * cc + 2];
-                        cf[k] += u;  // (kept for the diagonal lanes only: unconditional, so the load is not sunk
-                                     // into a branch that waits for the next landmark's loads too)
-                        if (!more) break;
-                        hl = hn;
-                        b1 = b1n;
-                        b2 = b2n;
-                    }
-                }
-#else  // measurement variant: two landmarks per step, both landmarks' operands loaded before either is
-       // subtracted (landmark order kept; a missing second one is a select) -- 2.7x slower: at 248 VGPRs the
-       // extra operands spill (profiles/r04/lba_bench_schur_pair.txt)
-                const bool diag = i1[k] == i2[k];
-                const uint64_t lo1 = (1ull << i1[k]) - 1ull, lo2 = (1ull << i2[k]) - 1ull;
-                while (cand) {
-                    const int ha = __ffsll((unsigned long long)cand) - 1;
-                    cand &= cand - 1;
-                    const bool two = cand != 0;
-                    const int hb = two ? __ffsll((unsigned long long)cand) - 1 : ha;
-                    cand = two ? cand & (cand - 1) : cand;
-                    const uint64_t mka = SM[ha], mkb = SM[hb];
-                    const int oa = SO[ha], ob = SO[hb];
-                    const double* BDa = SD + 18 * (oa + __popcll(mka & lo1)) + 3 * r;
-                    const double* Bja = BUF + 18 * (oa + __popcll(mka & lo2));
-                    const double* BDb = SD + 18 * (ob + __popcll(mkb & lo1)) + 3 * r;
-                    const double* Bjb = BUF + 18 * (ob + __popcll(mkb & lo2));
-                    double ja[18], jb[18];
-#pragma unroll
-                    for (int q = 0; q < 18; q++) {
-                        ja[q] = Bja[q];
-                        jb[q] = Bjb[q];
-                    }
-                    const double a0 = BDa[0], a1 = BDa[1], a2 = BDa[2], b0 = BDb[0], b1 = BDb[1], b2 = BDb[2];
-#pragma unroll
-                    for (int cc = 0; cc < 6; cc++) {
-                        const double va = acc[k][cc] - ((a0 * ja[3 * cc] + a1 * ja[3 * cc + 1]) + a2 * ja[3 * cc + 2]);
-                        const double vb = va - ((b0 * jb[3 * cc] + b1 * jb[3 * cc + 1]) + b2 * jb[3 * cc + 2]);
-                        acc[k][cc] = two ? vb : va;
-                    }
-                    if (diag) {
-                        const double* da = Sdb + 3 * ha;
-                        const double* dbb = Sdb + 3 * hb;
-                        const double ca = cf[k] + ((ja[3 * r] * da[0] + ja[3 * r + 1] * da[1]) + ja[3 * r + 2] * da[2]);
-                        const double cb = ca + ((jb[3 * r] * dbb[0] + jb[3 * r + 1] * dbb[1]) + jb[3 * r + 2] * dbb[2]);
-                        cf[k] = two ? cb : ca;
-                    }
-                }
+            if (c + 1 < nch) prefetch(cur_h1, nx_h1, cur_k1, nx_k1);  // lands while chunk c is processed
+#ifdef SPSLAM_LBG_DIAG_SCHUR
+            const long long wc0 = clock64();
+            int wsteps = 0;
 #endif
+#pragma unroll
+            for (int k = 0; k < kBW; k++) {
+                if (i1[k] < 0) continue;  // (wave-uniform)
+                const uint64_t cand = rl64(PM[i1[k]] & PM[i2[k]], 0);
+                if (!cand) continue;
+                // the candidates' (BDinv block, Bj block) pairs, compacted in landmark order, one per lane
+                const bool in = (cand >> lane) & 1ull;
+                const unsigned pos = __builtin_amdgcn_mbcnt_hi((unsigned)(cand >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((unsigned)cand, 0u));
+                if (in) LST[64 * wv + pos] = (unsigned)OB[kSchurLm * i1[k] + lane] |
+                                             ((unsigned)OB[kSchurLm * i2[k] + lane] << 16);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const unsigned my = LST[64 * wv + lane];
+                const int nc = __popcll(cand);
+
+                // operands of list entry q: BDinv row er of its first block, Bj row ec of its second, Bi db (er).  The
+                // entry is opaque to the compiler, so the next entry's loads (issued before the current one is
+                // subtracted) are not merged with the current one's into loads behind a wait at the loop top.
+                auto ld = [&](int q, double (&E)[3], double (&B)[3], double& u) __attribute__((always_inline)) {
+                    unsigned bb = __builtin_amdgcn_readlane(my, q);
+                    asm volatile("" : "+s"(bb));
+                    const unsigned b1 = bb & 0xffffu, b2 = bb >> 16;
+                    LdsD* pe = pE + 18 * b1;
+                    LdsD* pj = pJ + 18 * b2;
+                    LdsD* pu = pU + 6 * b1;
+                    E[0] = pe[0]; E[1] = pe[1]; E[2] = pe[2];
+                    B[0] = pj[0]; B[1] = pj[1]; B[2] = pj[2];
+                    u = pu[0];
+                };
+                auto step = [&](double a, const double (&E)[3], const double (&B)[3], double u)
+                    __attribute__((always_inline)) {
+                    const double sub = a - ((E[0] * B[0] + E[1] * B[1]) + E[2] * B[2]);
+                    const double add = a + u;
+                    return ent ? sub : add;
+                };
+                double EA[3], BA[3], uA, EB[3], BB[3], uB;
+                ld(0, EA, BA, uA);
+                double a = acc[k];
+                int q = 0;
+                for (; q + 2 <= nc; q += 2) {  // two operand sets in turn: one in flight while the other is used
+                    ld(q + 1, EB, BB, uB);
+                    a = step(a, EA, BA, uA);
+                    ld(min(q + 2, nc - 1), EA, BA, uA);
+                    a = step(a, EB, BB, uB);
+                }
+                if (q < nc) a = step(a, EA, BA, uA);
+                acc[k] = a;
+#ifdef SPSLAM_LBG_DIAG_SCHUR
+                wsteps += nc;
+#endif
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the list is free again
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
+#ifdef SPSLAM_LBG_DIAG_SCHUR  // per wave: chain cycles and steps (summed), the chunk's slowest wave (summed)
+            if (lane == 0) {
+                const unsigned long long wc = (unsigned long long)(clock64() - wc0);
+                atomicAdd((unsigned long long*)&s.dg[10], wc);
+                atomicAdd((unsigned long long*)&s.dg[11], (unsigned long long)wsteps);
+                atomicMax((unsigned long long*)&s.dg[12], wc);
+            }
+#endif
             __syncthreads();  // the staging buffer, BDinv and the masks are free again
+#ifdef SPSLAM_LBG_DIAG_SCHUR
+            if (t == 0) { s.dg[13] += s.dg[12]; s.dg[12] = 0; }
+#endif
 #ifdef SPSLAM_LBG_DIAG
             long long d3 = wall_clock64();
             if (t == 0) s.dg[2] += d3 - d2;
 #endif
-            if (c + 1 < nch) commit(c + 1);
+            if (c + 1 < nch) commit(nx_h1 - cur_h1, cur_k1);
+            // advance the bounds; the chunk after next's load lands during the next chunk
+            cur_h0 = cur_h1; cur_h1 = nx_h1; cur_k0 = cur_k1; cur_k1 = nx_k1;
+            nx_h1 = nn_h1; nx_k1 = nn_k1;
+            nn_h1 = g.sch[min(c + 4, nch)]; nn_k1 = g.sch_kb[min(c + 4, nch)];
 #ifdef SPSLAM_LBG_DIAG
             if (t == 0) s.dg[3] += wall_clock64() - d3;
 #endif
         }
 #pragma unroll
-        for (int k = 0; k < kSchurTasks; k++) {
+        for (int k = 0; k < kBW; k++) {
             if (i1[k] < 0) continue;
-            const int r = rr[k];
-#pragma unroll
-            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
-            if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
+            if (ent) g.S[(size_t)(6 * i1[k] + er) * n + 6 * i2[k] + ec] = acc[k];
+            else if (lane < 42 && i1[k] == i2[k]) g.bs[6 * i1[k] + er] = g.Hps[27 * i1[k] + 21 + er] - acc[k];
         }
     }
 }
@@ -2006,7 +2064,8 @@ __device__ __noinline__ void schur() {
 // kPacked, else g.S (dense, row-major)
 template <int kC, bool kPacked, class PD, class PU, class PI_, class PS>
 __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO, const PI_* RS, const PI_* PI,
-                                            const PS* SP, double* PR /* LDS, 64 doubles */) {
+                                            const PS* SP, double* PR /* LDS, 64 doubles */,
+                                            const double* Dpre = nullptr /* factorised already (factor_dense) */) {
     const G& g = lbg_g;
     Sh& s = lbg_s;
     const int lane = threadIdx.x & 63;
@@ -2015,7 +2074,13 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
 #pragma unroll
     for (int m = 0; m < kC; m++) Dg[m] = 0.0;
     bool ok = true;
-    for (int k = 0; k < n; k++) {
+    if (Dpre) {  // L and D from factor_dense; s.ok set there
+#pragma unroll
+        for (int m = 0; m < kC; m++)
+            if (64 * m + lane < n) Dg[m] = Dpre[64 * m + lane];
+        ok = s.ok;
+    }
+    for (int k = 0; k < (Dpre ? 0 : n); k++) {
         const int ok_ = PI[k], qk = ok_ / 6;
         double y[kC];
 #pragma unroll
@@ -2051,7 +2116,15 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
             const int c = k - 64 * m;
             km[m] = c >= 64 ? ~0ull : c <= 0 ? 0ull : (1ull << c) - 1ull;
         }
-        auto stepf = [&](int lsel, int rsel, const double (&v)[kC], const uint64_t (&w)[kC]) __attribute__((always_inline)) {
+        auto stepf = [&](int lsel, int rsel, const double (&v)[kC], const uint64_t (&wr)[kC]) __attribute__((always_inline)) {
+            // (the structure words opaque until here: otherwise the compiler masks each one as soon as its load is
+            // issued -- a wait for the LDS read every step, which defeats the ring)
+            uint64_t w[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                w[m] = wr[m];
+                asm volatile("" : "+v"(w[m]));
+            }
             double yi = rl(y[0], lsel);
 #pragma unroll
             for (int m = 1; m < kC; m++) {
@@ -2157,7 +2230,7 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (lane == 0) s.ok = ok;
+    if (lane == 0 && !Dpre) s.ok = ok;
 #ifdef SPSLAM_LBG_DIAG
     if (lane == 0) s.dg[4] = wall_clock64();
 #endif
@@ -2217,7 +2290,8 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
 
 // byte offsets of the factorisation's LDS copy (n <= kLdsN): L, its column structures, the rows' pattern orders
 // (offsets, indices), P^-1, S packed
-struct FactorLds { size_t LB, RO, RS, PI, SP, PR, end; };
+// (and factor_dense's pivots D and per-row progress PG, + a failure flag)
+struct FactorLds { size_t LB, RO, RS, PI, SP, PR, D, PG, end; };
 __device__ __forceinline__ FactorLds factor_lds(int n) {
     FactorLds f;
     f.LB = (size_t)n * n * 8;
@@ -2226,18 +2300,96 @@ __device__ __forceinline__ FactorLds factor_lds(int n) {
     f.PI = f.RS + (size_t)((n * (n + 1)) / 2 + 1) * 4;
     f.SP = (f.PI + (size_t)n * 4 + 7) & ~(size_t)7;
     f.PR = f.SP + (size_t)((n * (n + 1)) / 2) * 8;
-    f.end = f.PR + 64 * 8;
+    f.D = f.PR + 64 * 8;
+    f.PG = f.D + (size_t)n * 8;
+    f.end = f.PG + (size_t)(n + 1) * 4;
     return f;
 }
+static_assert((size_t)kLdsN * kLdsN * 8 + (kLdsN * kNW + 1) * 8 + (kLdsN + 1) * 4 + (kLdsN * (kLdsN + 1) / 2 + 1) * 4 +
+                  kLdsN * 4 + 8 + (kLdsN * (kLdsN + 1) / 2) * 8 + 64 * 8 + kLdsN * 8 + (kLdsN + 1) * 4 <= (size_t)kDyn,
+              "the factorisation's LDS copy");
 
-template <int kC, bool kLds>
+// SimplicialLDLT::factorize for a fully dense reduced system in the natural order (every pose coupled with every
+// other; AMD then returns the identity and the elimination tree is a chain, so row k's pattern order is 0 .. k - 1
+// and column i's structure every row below i), pipelined over the workgroup's waves: row k on wave k mod kW.  Row k
+// runs Eigen's up-looking steps exactly as factor_body does -- for i = 0 .. k - 1: y_i read, y_r -= L(r, i) y_i for
+// i < r < k, then l_ki = y_i / D_i and d -= l_ki y_i (the same pivot-update order as factor_body's pattern-order
+// chain) -- and publishes L(k, i) at its step i and D_k when it ends.  Its step i needs L(r, i) for every r < k: row
+// k - 1 has passed step i (PG[k - 1] > i) only after row k - 2 had, and so on, so one progress word per row orders
+// them.  Same arithmetic, same order, rows overlapped.
+template <int kC>
+__device__ __noinline__ void factor_dense() {
+    Sh& s = lbg_s;
+    const int n = 6 * s.np;
+    const FactorLds f = factor_lds(n);
+    double* LD = (double*)lbg_dyn;
+    const double* SP = (const double*)(lbg_dyn + f.SP);
+    double* D = (double*)(lbg_dyn + f.D);
+    volatile int* PG = (volatile int*)(lbg_dyn + f.PG);
+    volatile int* FL = PG + n;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int k = t; k <= n; k += kT) PG[k] = 0;  // (PG[n] = FL)
+    __syncthreads();
+    for (int k = w; k < n; k += kW) {
+        double y[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) {
+            const int r = 64 * m + lane;
+            y[m] = r <= k ? 0.0 + SP[(k * (k + 1)) / 2 + r] : 0.0;
+        }
+        double d = pick(y, k) * 1.0 + 0.0;
+        int seen = 0;
+        bool failed = false;
+        for (int i = 0; i < k; i++) {
+            while (seen <= i) {  // row k - 1 has published L(k - 1, i)
+                seen = __builtin_amdgcn_readfirstlane(PG[k - 1]);
+                if (seen <= i) {
+                    if (*FL) { failed = true; break; }
+                    __builtin_amdgcn_s_sleep(0);
+                }
+            }
+            if (failed) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const double yi = pick(y, i);
+            const double Di = D[i];
+            double v[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) v[m] = LD[(size_t)i * n + 64 * m + lane];  // L(r, i), rows r < k published
+            const double l = yi / Di;
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                const double nv = y[m] - v[m] * yi;
+                y[m] = (r > i && r < k) ? nv : y[m];
+            }
+            d -= l * yi;
+            if (lane == 0) LD[(size_t)i * n + k] = l;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) PG[k] = i + 1;
+        }
+        if (failed) break;
+        if (d == 0.0) {  // Eigen stops at a zero pivot (ok = false); the other rows see the flag and stop
+            if (lane == 0) *FL = 1;
+            break;
+        }
+        if (lane == 0) D[k] = d;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) PG[k] = k + 1;
+    }
+    __syncthreads();
+    if (t == 0) s.ok = *FL == 0;
+    __syncthreads();
+}
+
+template <int kC, bool kLds, bool kPre = false>
 __device__ __noinline__ void factor_solve() {
     const int n = 6 * lbg_s.np;
     if (kLds) {  // the layout of k_lba_g2o's copy in LDS
         const FactorLds f = factor_lds(n);
         factor_body<kC, true>((double*)lbg_dyn, (const uint64_t*)(lbg_dyn + f.LB), (const int*)(lbg_dyn + f.RO),
                               (const int*)(lbg_dyn + f.RS), (const int*)(lbg_dyn + f.PI),
-                              (const double*)(lbg_dyn + f.SP), (double*)(lbg_dyn + f.PR));
+                              (const double*)(lbg_dyn + f.SP), (double*)(lbg_dyn + f.PR),
+                              kPre ? (const double*)(lbg_dyn + f.D) : nullptr);
     } else {
         const G& g = lbg_g;
         factor_body<kC, false>(g.Ld, g.Lbits, g.rs_off, g.rs_idx, g.Pinv, g.S, (double*)lbg_dyn);  // (LDS unused)
@@ -2577,7 +2729,14 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
 #ifdef SPSLAM_LBG_DIAG
                     const long long f0 = wall_clock64();
 #endif
-                    if (t < 64) {
+                    if (lds && s.dense) {  // every pose coupled, natural order: the rows pipelined over the waves
+                        if (n <= 64) factor_dense<1>();
+                        else factor_dense<2>();
+                        if (t < 64) {
+                            if (n <= 64) factor_solve<1, true, true>();
+                            else factor_solve<2, true, true>();
+                        }
+                    } else if (t < 64) {
                         if (n <= 64) factor_solve<1, true>();
                         else if (n <= kLdsN) factor_solve<2, true>();
                         else if (n <= 128) factor_solve<2, false>();
@@ -2690,6 +2849,12 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         b.res[p].phase_us[6] = (float)(s.dg[7] * 1e-3);  //   pivot-update kcycles,
         b.res[p].pad = (int)s.dg[8];                     //   steps
         b.res[p].phase_us[7] = (float)(s.dg[5] * 0.01);
+#endif
+#ifdef SPSLAM_LBG_DIAG_SCHUR  // Schur chains: kcycles summed over waves, steps, cycles per step, sum of chunk maxima
+        b.res[p].phase_us[1] = (float)(s.dg[10] * 1e-3);
+        b.res[p].phase_us[2] = (float)s.dg[11];
+        b.res[p].phase_us[3] = (float)s.dg[10] / (float)max(1ll, s.dg[11]);
+        b.res[p].phase_us[4] = (float)(s.dg[13] * 1e-3);
 #endif
 #ifdef SPSLAM_LBG_PROBE  // shader-clock ticks per (1) add, (2) add of a readlane, (3) readlane chain
         for (int i = 0; i < 3; i++) b.res[p].phase_us[1 + i] = (float)probe[i];

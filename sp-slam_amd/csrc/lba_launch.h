@@ -126,6 +126,8 @@ struct LbgTeam {
     int eb[kLbgTeamMax + 1];    // buildSystem: member m sums the landmarks whose edges are [eb[m], eb[m + 1])
     int npo[kLbgTeamMax + 1];   //   and the (free pose, term) chains of poses pown[npo[m] .. npo[m + 1])
     int pown[kLbgMaxFree];
+    int bo[kLbgTeamMax + 1];    // Schur: member m's pattern blocks bord[bo[m] .. bo[m + 1]), the block rows rmask[m]
+    uint64_t rmask[kLbgTeamMax];
     double mx[2 * kLbgTeamMax];  // computeLambdaInit: each member's largest |diagonal| (landmarks, poses)
     uint64_t pat[kLbgMaxFree];
     short hidx[kLbgMaxKeyframes];

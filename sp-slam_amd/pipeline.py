@@ -443,6 +443,9 @@ class HotPath:
         self.lba = L.LocalBA(self.lba_ex, cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info,
                                                pc.chi, pc.vp_chi))
         self.lba.set_order(self.lba_order)
+        # workgroups per local map (0: fill the chip); SPSLAM_LBA_TEAM overrides for measurements
+        import os
+        self.lba.set_team(int(os.environ.get("SPSLAM_LBA_TEAM", "0")))
         self.lba_stream = torch.cuda.Stream()
         self.ev_lba = torch.cuda.Event()
         import concurrent.futures as cf
