@@ -499,16 +499,20 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         sp.close()
 
 
-def _ensure_hw_queues():
+def _ensure_hw_queues(want=None):
+    want = want or HW_QUEUES
     try:
         cur = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
     except ValueError:
         cur = 4
-    if cur >= HW_QUEUES or os.environ.get("SPSLAM_BENCH_CHILD"):
+    if cur >= want or os.environ.get("SPSLAM_BENCH_CHILD"):
         return
     import subprocess
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(HW_QUEUES), SPSLAM_BENCH_CHILD="1")
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(want), SPSLAM_BENCH_CHILD="1")
     sys.exit(subprocess.call([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+
+LBA_DEPTH, LBA_TEAM = 2, 1  # C3 defaults (profiles/r05/ab_c3_*.txt)
 
 
 def main():
@@ -530,6 +534,11 @@ def main():
     ap.add_argument("--lba-order", default="g2o", choices=("g2o", "fast"),
                     help="LocalBundleAdjustment summation order (C3): g2o = the reference's arithmetic, bit-exact "
                          "to the oracle (default); fast = the phase kernels (tree / matrix-core order)")
+    ap.add_argument("--lba-depth", type=int, default=None,
+                    help="C3: step k's LocalBundleAdjustment call is joined at the end of step k + d (LocalMapping "
+                         "does not block Tracking, LocalMapping.cc:48-124); default %d" % 2)
+    ap.add_argument("--lba-team", type=int, default=None,
+                    help="C3: workgroups per local map (0: as many as fill the chip); default 1 (the least CU time per map: with two calls in flight the LBA overlaps tracking instead of crowding it)")
     ap.add_argument("--python-step", action="store_true",
                     help="drive the step's stages from Python over torch streams (pipeline.py) instead of the "
                          "library's whole-step entry spslam_step_run (the default without LocalMapping)")
@@ -557,7 +566,9 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dist_check:
         return dist_check(args, rank, world)
-    _ensure_hw_queues()
+    # C3: every in-flight LocalBundleAdjustment call has its own context stream; with 8 hardware queues they alias
+    # the tracking streams' queues and serialise (profiles/r05/ab_c3_hwq*.txt), so C3 runs with 16
+    _ensure_hw_queues(16 if args.config == "c3" else None)
     import pipeline
     cfg = pipeline.CONFIGS[args.config]
     import torch
@@ -578,6 +589,8 @@ def main():
                           orb_priority=args.orb_priority, planes_priority=not args.no_planes_priority,
                           lba_order=0 if args.lba_order == "g2o" else 1,
                           native=not args.python_step and not cfg.get("lba_every"), **cfg,
+                          lba_depth=LBA_DEPTH if args.lba_depth is None else args.lba_depth,
+                          lba_team=LBA_TEAM if args.lba_team is None else args.lba_team,
                           **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
@@ -702,9 +715,11 @@ def main():
     checks = {"pose_wait_give_ups": int((res["pose1"]["lm_iterations"] < 0).sum() + (res["pose2"]["lm_iterations"] < 0).sum())}
     if hp.n_lba:
         import spslam_lba
-        lr = hp.lba_out[-1].cpu().numpy().view(spslam_lba.LBA_RESULT_DTYPE)
-        checks["lba_failed"] = int((lr["status"] != 0).sum())
+        lr = [sl["out"][-1].cpu().numpy().view(spslam_lba.LBA_RESULT_DTYPE) for sl in hp.lba_slots]
+        checks["lba_failed"] = int(sum((r["status"] != 0).sum() for r in lr))
         checks["lba_order"] = "g2o" if hp.lba_order == spslam_lba.G2O_ORDER else "fast"
+        checks["lba_in_flight"] = hp.lba_depth + 1
+        checks["lba_team"] = hp.lba_slots[0]["lba"].team
     cpu_poses = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], cpu_poses = cpu_baseline(hp, timed=args.cpu_frames or (300 if hp.W * hp.H <= 640 * 480 else 100))

@@ -1791,6 +1791,14 @@ __device__ __noinline__ void build_system() {
 #define SPSLAM_LBG_SCHUR_BLOCKS 8
 #endif
 constexpr int kBW = SPSLAM_LBG_SCHUR_BLOCKS;  // blocks per wave per round
+#ifndef SPSLAM_LBG_SCHUR_TASKS
+#define SPSLAM_LBG_SCHUR_TASKS 2
+#endif
+constexpr int kSchurTasks = SPSLAM_LBG_SCHUR_TASKS;  // schur_rows: chains per lane per round
+#ifndef SPSLAM_LBG_ROWS_MAX_TEAM
+#define SPSLAM_LBG_ROWS_MAX_TEAM 4
+#endif
+constexpr int kRowsMaxTeam = SPSLAM_LBG_ROWS_MAX_TEAM;  // teams up to this size use schur_rows
 // (Hll + lambda)^-1 (Eigen's cofactor inverse) and Dinv bl of one landmark
 __device__ __forceinline__ void landmark_dinv(const double* H, const double* bv, double lam, double* Di, double* db) {
     double D[3][3];
@@ -2053,6 +2061,240 @@ __device__ __noinline__ void schur() {
             if (i1[k] < 0) continue;
             if (ent) g.S[(size_t)(6 * i1[k] + er) * n + 6 * i2[k] + ec] = acc[k];
             else if (lane < 42 && i1[k] == i2[k]) g.bs[6 * i1[k] + er] = g.Hps[27 * i1[k] + 21 + er] - acc[k];
+        }
+    }
+}
+
+// The same Schur complement with one lane per (block, row r) holding the row's six entries (and the diagonal block's
+// Bb(r)), each lane walking its own candidate landmarks: fewer LDS bytes per entry than schur()'s lane per entry, but
+// a dependent LDS round trip per landmark.  The faster of the two when a member holds many blocks (teams of 1 - 2).
+__device__ __noinline__ void schur_rows() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    unsigned char* dyn = lbg_dyn;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int np = s.np, n = 6 * np, nch = s.nch;
+    const double lam = s.lambda;
+    // LDS: the staged chunk (blocks, Dinv, Dinv bl | masks, block offsets, block -> landmark, block -> pose), its
+    // BDinv and Bi db, the poses' landmark masks, the waves' candidate lists
+    constexpr int kBufD = kSchurBlk * 18 + kSchurLm * 12;
+    double* BUF = (double*)dyn;                          // [kBufD]
+    double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
+    double* SU = SD + kSchurBlk * 18;                    // [kSchurBlk][6] B row . Dinv bl (Bb's terms)
+    uint64_t* SM = (uint64_t*)(SU + kSchurBlk * 6);      // [kSchurLm]
+    uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
+    int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
+    unsigned short* OB = (unsigned short*)(SO + kSchurLm + 1);  // [kMaxK][kSchurLm] (pose, landmark) -> its block
+    unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk] block -> landmark
+    unsigned char* BP = BL + kSchurBlk;                  // [kSchurBlk] block -> pose
+    const double* SDi = BUF + kSchurBlk * 18;
+    const double* Sdb = SDi + kSchurLm * 9;
+    static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
+                      2 * kSchurBlk + 4 + kW * 64 * 4 <= kDynAlloc, "LDS");
+    constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
+    const int bo0 = s.bo0, nbm = s.bo1 - s.bo0;
+    const uint64_t rmask = s.rmask;
+    using LdsD = const __attribute__((address_space(3))) double;
+    for (int round = 0; round * kSchurTasks * kT < 6 * nbm; round++) {
+        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
+        double acc[kSchurTasks][6], cf[kSchurTasks];
+#pragma unroll
+        for (int k = 0; k < kSchurTasks; k++) {
+            i1[k] = -1; i2[k] = 0; rr[k] = 0;
+            const int task = (round * kSchurTasks + k) * kT + t;
+            if (task < 6 * nbm) {
+                const int jb = task / 6;
+                rr[k] = task - 6 * jb;
+                const int blk = g.bord[bo0 + jb];
+                if (blk < np) {
+                    i1[k] = i2[k] = blk;
+                } else {
+                    int rem = blk - np, a = 0;
+                    while (rem >= __popcll(s.pat[a]) - 1) { rem -= __popcll(s.pat[a]) - 1; a++; }
+                    uint64_t row = s.pat[a] & ~(1ull << a);
+                    for (int u = 0; u < rem; u++) row &= row - 1;
+                    i1[k] = a;
+                    i2[k] = __ffsll((unsigned long long)row) - 1;
+                }
+            }
+            const bool diag = i1[k] >= 0 && i1[k] == i2[k];
+            const int r = rr[k];
+#pragma unroll
+            for (int c = 0; c < 6; c++) {
+                double base = 0.0;
+                if (diag && c >= r) base = c == r ? g.Hps[27 * i1[k] + upper_idx(r, c)] + lam : g.Hps[27 * i1[k] + upper_idx(r, c)];
+                acc[k][c] = 0.0 + base;
+            }
+            cf[k] = 0.0;
+        }
+        // chunk c's records into registers (global loads in flight), later into the staging buffer.  Every load is
+        // unconditional (addresses clamped into the chunk; the surplus entries are never read) and nothing loaded is
+        // used before the commit, so no wait lands in the chunk loop; the chunk bounds (sch, sch_kb) of the chunk
+        // after next load one chunk ahead.
+        double pv[kPer];
+        uint64_t pmk = 0;
+        int pof = 0, pof1 = 0;
+        auto prefetch = [&](int h0, int h1, int kb0, int kb1) __attribute__((always_inline)) {
+            const int nbk = kb1 - kb0, nh = h1 - h0;
+            const int cb = max(nbk * 18 - 1, 0), ch = max(nh * 9 - 1, 0), cl = max(nh * 3 - 1, 0);
+#pragma unroll
+            for (int q = 0; q < kPer; q++) {
+                const int i = t + q * kT;
+                const gdouble* src;
+                if ((q + 1) * kT <= kSchurBlk * 18) {  // (compile time) the slice is in the Hpl block range
+                    src = g.blkB + (size_t)18 * kb0 + min(i, cb);
+                } else {
+                    const int j = i - kSchurBlk * 18, j2 = j - kSchurLm * 9;
+                    const gdouble* a = g.blkB + (size_t)18 * kb0 + min(i, cb);
+                    const gdouble* h = g.Hll + (size_t)9 * h0 + min(max(j, 0), ch);
+                    const gdouble* l = g.bl + (size_t)3 * h0 + min(max(j2, 0), cl);
+                    src = j < 0 ? a : (j2 < 0 ? h : l);
+                }
+                pv[q] = *src;
+            }
+            const int tc = min(t, max(nh - 1, 0));
+            pmk = g.lmh_mask[h0 + tc];
+            pof = g.lmh_blk[h0 + min(t, nh)];
+            pof1 = g.lmh_blk[h0 + tc + 1];
+        };
+        auto commit = [&](int nh, int kb0) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < kPer; q++)
+                if (t + q * kT < kBufD) BUF[t + q * kT] = pv[q];
+            if (t < nh) {
+                SM[t] = pmk;
+                uint64_t m = pmk;
+                for (int bk = pof - kb0; bk < pof1 - kb0; bk++) {  // (the blocks of a landmark are in pose order)
+                    BL[bk] = (unsigned char)t;
+                    BP[bk] = (unsigned char)(__ffsll((unsigned long long)m) - 1);
+                    m &= m - 1;
+                }
+            }
+            if (t <= nh) SO[t] = pof - kb0;
+        };
+        __syncthreads();  // the previous phase's LDS use is over
+        // chunk bounds: (h0, h1, kb0, kb1) of the current chunk, the next, and the one after (loading)
+        int cur_h0 = 0, cur_h1 = 0, cur_k0 = 0, cur_k1 = 0, nx_h1 = 0, nx_k1 = 0, nn_h1 = 0, nn_k1 = 0;
+        if (nch > 0) {
+            cur_h0 = g.sch[0]; cur_h1 = g.sch[1]; cur_k0 = g.sch_kb[0]; cur_k1 = g.sch_kb[1];
+            nx_h1 = g.sch[min(2, nch)]; nx_k1 = g.sch_kb[min(2, nch)];
+            prefetch(cur_h0, cur_h1, cur_k0, cur_k1);
+            commit(cur_h1 - cur_h0, cur_k0);
+            nn_h1 = g.sch[min(3, nch)]; nn_k1 = g.sch_kb[min(3, nch)];
+        }
+        for (int c = 0; c < nch; c++) {
+#ifdef SPSLAM_LBG_DIAG
+            long long d0 = wall_clock64();
+#endif
+            __syncthreads();  // chunk c is staged
+#ifdef SPSLAM_LBG_DIAG
+            long long d1 = wall_clock64();
+            if (t == 0) s.dg[0] += d1 - d0;
+#endif
+            const int nh = cur_h1 - cur_h0;
+            const int nbk = cur_k1 - cur_k0;
+            if (t < nh) {  // the staged Hll, bl -> Dinv, Dinv bl, in place
+                double* Hd = BUF + kSchurBlk * 18 + 9 * t;
+                double* bd = BUF + kSchurBlk * 18 + kSchurLm * 9 + 3 * t;
+                double H[9], bv[3], Di[9], db[3];
+                for (int j = 0; j < 9; j++) H[j] = Hd[j];
+                for (int j = 0; j < 3; j++) bv[j] = bd[j];
+                landmark_dinv(H, bv, lam, Di, db);
+                for (int j = 0; j < 9; j++) Hd[j] = Di[j];
+                for (int j = 0; j < 3; j++) bd[j] = db[j];
+            }
+            __syncthreads();
+            for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
+                const int bk = i / 6, r6 = i - 6 * bk;
+                if (!((rmask >> BP[bk]) & 1ull)) continue;  // a block row of another member
+                const int hb = BL[bk];
+                const double* Bi = BUF + 18 * bk + 3 * r6;
+                const double* Di = SDi + 9 * hb;
+                const double* db = Sdb + 3 * hb;
+                double* BD = SD + 18 * bk + 3 * r6;
+#pragma unroll
+                for (int q = 0; q < 3; q++) BD[q] = (Bi[0] * Di[q] + Bi[1] * Di[3 + q]) + Bi[2] * Di[6 + q];
+                SU[i] = (Bi[0] * db[0] + Bi[1] * db[1]) + Bi[2] * db[2];
+            }
+            for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk, and their blocks
+                const uint64_t mk = lane < nh ? SM[lane] : 0ull;
+                const bool obs = (mk >> i) & 1ull;
+                const uint64_t m = __ballot(obs);
+                if (lane == 0) PM[i] = m;
+                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + __popcll(mk & ((1ull << i) - 1ull)));
+            }
+            __syncthreads();
+#ifdef SPSLAM_LBG_DIAG
+            long long d2 = wall_clock64();
+            if (t == 0) s.dg[1] += d2 - d1;
+#endif
+            if (c + 1 < nch) prefetch(cur_h1, nx_h1, cur_k1, nx_k1);  // lands while chunk c is processed
+#pragma unroll
+            for (int k = 0; k < kSchurTasks; k++) {
+                if (i1[k] < 0) continue;
+                const int r = rr[k];
+                uint64_t cand = PM[i1[k]] & PM[i2[k]];
+                // one LDS round trip per landmark: the next landmark's blocks (the chunk's (pose, landmark) block
+                // table) load while this one's are subtracted, and the diagonal lanes' Bb term comes staged (SU)
+                // with the blocks instead of through a dependent load of Dinv bl
+                if (cand) {
+                    using LdsU16 = const __attribute__((address_space(3))) unsigned short;
+                    LdsU16* O1 = (LdsU16*)(OB + kSchurLm * i1[k]);
+                    LdsU16* O2 = (LdsU16*)(OB + kSchurLm * i2[k]);
+                    LdsD* SDr = (LdsD*)(SD + 3 * r);
+                    LdsD* SUr = (LdsD*)(SU + r);
+                    LdsD* BUFl = (LdsD*)BUF;
+                    int hl = __ffsll((unsigned long long)cand) - 1;
+                    cand &= cand - 1;
+                    int b1 = O1[hl], b2 = O2[hl];
+                    // (opaque here: otherwise the first landmark's loads and the loop's next-landmark loads are
+                    // merged into one load at the top of the loop, behind a wait -- the round trip this loop avoids)
+                    asm volatile("" : "+v"(b1), "+v"(b2));
+                    for (;;) {
+                        LdsD* BD = SDr + __umul24(b1, 18);  // (24-bit products: full-rate multiplies)
+                        LdsD* Bj = BUFl + __umul24(b2, 18);
+                        const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
+                        double bj[18];
+#pragma unroll
+                        for (int q = 0; q < 18; q++) bj[q] = Bj[q];
+                        const double u = SUr[__umul24(b1, 6)];  // (b1 = b2 on the diagonal lanes)
+                        const bool more = cand != 0;
+                        const int hn = more ? __ffsll((unsigned long long)cand) - 1 : hl;
+                        cand &= cand - 1;
+                        const int b1n = O1[hn], b2n = O2[hn];
+#pragma unroll
+                        for (int cc = 0; cc < 6; cc++)
+                            acc[k][cc] -= (e0 * bj[3 * cc] + e1 * bj[3 * cc + 1]) + e2 * bj[3 * cc + 2];
+                        cf[k] += u;  // (kept for the diagonal lanes only: unconditional, so the load is not sunk
+                                     // into a branch that waits for the next landmark's loads too)
+                        if (!more) break;
+                        hl = hn;
+                        b1 = b1n;
+                        b2 = b2n;
+                    }
+                }
+            }
+            __syncthreads();  // the staging buffer, BDinv and the masks are free again
+#ifdef SPSLAM_LBG_DIAG
+            long long d3 = wall_clock64();
+            if (t == 0) s.dg[2] += d3 - d2;
+#endif
+            if (c + 1 < nch) commit(nx_h1 - cur_h1, cur_k1);
+            // advance the bounds; the chunk after next's load lands during the next chunk
+            cur_h0 = cur_h1; cur_h1 = nx_h1; cur_k0 = cur_k1; cur_k1 = nx_k1;
+            nx_h1 = nn_h1; nx_k1 = nn_k1;
+            nn_h1 = g.sch[min(c + 4, nch)]; nn_k1 = g.sch_kb[min(c + 4, nch)];
+#ifdef SPSLAM_LBG_DIAG
+            if (t == 0) s.dg[3] += wall_clock64() - d3;
+#endif
+        }
+#pragma unroll
+        for (int k = 0; k < kSchurTasks; k++) {
+            if (i1[k] < 0) continue;
+            const int r = rr[k];
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
+            if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
         }
     }
 }
@@ -2709,7 +2951,8 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             bool more = true;
             while (more) {
                 LBG_MARK(1);
-                schur();
+                if (s.T <= kRowsMaxTeam) schur_rows();
+                else schur();
                 team_sync(b);
                 LBG_MARK(5);
                 if (lead) {

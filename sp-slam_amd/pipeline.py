@@ -63,7 +63,7 @@ class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
-                 rotate_inputs=False, lba_order=0, native=False):
+                 rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -143,7 +143,7 @@ class HotPath:
         self.n_lba = B // lba_every if lba_every else 0
         self.lba_every = lba_every
         if self.n_lba:
-            self._setup_lba(seq_id, lba_unique, lba_points)
+            self._setup_lba(seq_id, lba_unique, lba_points, lba_depth, lba_team)
         # rotate_inputs (tests): batch k's slot i takes the inputs of slot (i + k) % B -- images and the per-frame
         # tracking records together -- so consecutive batches differ and a stage reading the wrong buffer set shows
         self.rotate_inputs = rotate_inputs
@@ -403,7 +403,14 @@ class HotPath:
                 [sl(po, p["point_offset"], p["n_points"]).astype(bool) for p in P],
                 [sl(plo, p["plane_offset"], p["n_planes"]).astype(bool) for p in P])
 
-    def _setup_lba(self, seq_id, unique, n_points):
+    def _setup_lba(self, seq_id, unique, n_points, depth=0, team=0):
+        """LocalMapping beside tracking.  The step's local maps (one per `lba_every` frames) go to one batched
+        LocalBundleAdjustment call on its own stream and context, like the reference's LocalMapping thread
+        (LocalMapping.cc:48-124), which never blocks Tracking.  depth d: step k's call is joined at the end of step
+        k + d (d = 0: the same step), so up to d + 1 calls are in flight, each on its own context (scratch) and
+        output buffers; the join point is fixed, so the results do not depend on timing."""
+        import concurrent.futures as cf
+        import os
         import spslam_lba as L
         torch = self.torch
         probs = []
@@ -430,47 +437,53 @@ class HotPath:
         self.lba_hdr = hdr
         self.lba_in = [dev(hdr), dev(np.concatenate(kf)), dev(np.concatenate(pt)), dev(np.concatenate(po)),
                        dev(np.concatenate(pl)), dev(np.concatenate(plo))]
-        self.lba_out = [torch.zeros((nk, 16), dtype=torch.float32, device="cuda"),
-                        torch.zeros((npt, 3), dtype=torch.float32, device="cuda"),
-                        torch.zeros((max(npl, 1), 4), dtype=torch.float32, device="cuda"),
-                        torch.zeros(npo, dtype=torch.uint8, device="cuda"),
-                        torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
-                        torch.zeros(self.n_lba * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
-        # LocalMapping runs in its own thread on its own context (as the reference's LocalMapping thread):
-        # the batched LM drives its steps from the host, so tracking launches must not wait behind it
-        self.lba_ex = G.OrbExtractor(max_batch=1, device=self.device)
         pc = self.plane_cfg
-        self.lba = L.LocalBA(self.lba_ex, cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info,
-                                               pc.chi, pc.vp_chi))
-        self.lba.set_order(self.lba_order)
-        # workgroups per local map (0: fill the chip); SPSLAM_LBA_TEAM overrides for measurements
-        import os
-        self.lba.set_team(int(os.environ.get("SPSLAM_LBA_TEAM", "0")))
-        self.lba_stream = torch.cuda.Stream()
-        self.ev_lba = torch.cuda.Event()
-        import concurrent.futures as cf
-        self.lba_pool = cf.ThreadPoolExecutor(1, initializer=torch.cuda.set_device, initargs=(self.device,))
-        self.lba_job = None
+        team = int(os.environ.get("SPSLAM_LBA_TEAM", team))  # workgroups per local map (0: fill the chip)
+        self.lba_depth = int(os.environ.get("SPSLAM_LBA_DEPTH", depth))
+        self.lba_slots = []
+        for _ in range(self.lba_depth + 1):
+            ex = G.OrbExtractor(max_batch=1, device=self.device)
+            lba = L.LocalBA(ex, cfg=(pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info, pc.chi,
+                                     pc.vp_chi))
+            lba.set_order(self.lba_order)
+            lba.set_team(team)
+            out = [torch.zeros((nk, 16), dtype=torch.float32, device="cuda"),
+                   torch.zeros((npt, 3), dtype=torch.float32, device="cuda"),
+                   torch.zeros((max(npl, 1), 4), dtype=torch.float32, device="cuda"),
+                   torch.zeros(npo, dtype=torch.uint8, device="cuda"),
+                   torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
+                   torch.zeros(self.n_lba * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
+            self.lba_slots.append(dict(ex=ex, lba=lba, out=out, stream=torch.cuda.Stream(), ev=torch.cuda.Event()))
+        s0 = self.lba_slots[0]
+        self.lba_ex, self.lba, self.lba_out, self.lba_stream, self.ev_lba = (s0["ex"], s0["lba"], s0["out"],
+                                                                             s0["stream"], s0["ev"])
+        self.lba_pool = cf.ThreadPoolExecutor(len(self.lba_slots), initializer=torch.cuda.set_device,
+                                              initargs=(self.device,))
+        self.lba_pending = []  # (job, slot) in launch order
+        self.lba_launched = 0
         self.lba_edges = (npo + nplo) / self.n_lba
         self.lba_points = npt / self.n_lba
 
-    def local_ba(self):
-        self.lba.batch_device(self.n_lba, self.lba_hdr, *[x.data_ptr() for x in self.lba_in],
-                              *[x.data_ptr() for x in self.lba_out], stream=self.lba_stream.cuda_stream)
-        self.ev_lba.record(self.lba_stream)
+    def local_ba(self, slot=0):
+        sl = self.lba_slots[slot]
+        sl["lba"].batch_device(self.n_lba, self.lba_hdr, *[x.data_ptr() for x in self.lba_in],
+                               *[x.data_ptr() for x in sl["out"]], stream=sl["stream"].cuda_stream)
+        sl["ev"].record(sl["stream"])
 
     def set_timing(self, on):
         self.ex.set_timing(on)
         if self.n_lba:
-            self.lba_ex.set_timing(on)
+            for sl in self.lba_slots:
+                sl["ex"].set_timing(on)
 
     def kernel_times(self):
         """{kernel name: (total ms, launches)} over both contexts (tracking, LocalMapping)."""
         t = dict(self.ex.kernel_times())
         if self.n_lba:
-            for k, (ms, n) in self.lba_ex.kernel_times().items():
-                a = t.get(k, (0.0, 0))
-                t[k] = (a[0] + ms, a[1] + n)
+            for sl in self.lba_slots:
+                for k, (ms, n) in sl["ex"].kernel_times().items():
+                    a = t.get(k, (0.0, 0))
+                    t[k] = (a[0] + ms, a[1] + n)
         return t
 
     # Extraction outputs: the only buffers written by ORB / plane extraction and read by the tracking tail.
@@ -635,14 +648,27 @@ class HotPath:
 
     def _lba_begin(self):
         if self.n_lba:
-            # LocalMapping: the keyframes of this step, beside tracking (joined at the end of the step)
-            self.lba_stream.wait_event(self.ev_fork)
-            self.lba_job = self.lba_pool.submit(self.local_ba)
+            # LocalMapping: the keyframes of this step, beside tracking, on the next slot (its previous call was
+            # joined lba_depth steps ago)
+            slot = self.lba_launched % len(self.lba_slots)
+            self.lba_launched += 1
+            self.lba_slots[slot]["stream"].wait_event(self.ev_fork)
+            self.lba_pending.append((self.lba_pool.submit(self.local_ba, slot), slot))
 
     def _lba_end(self):
+        if self.n_lba:  # join the call launched lba_depth steps ago
+            while len(self.lba_pending) > self.lba_depth:
+                job, slot = self.lba_pending.pop(0)
+                job.result()
+                self.main.wait_event(self.lba_slots[slot]["ev"])
+
+    def lba_drain(self):
+        """Join every LocalBundleAdjustment call still in flight (the end of a run)."""
         if self.n_lba:
-            self.lba_job.result()
-            self.main.wait_event(self.ev_lba)
+            while self.lba_pending:
+                job, slot = self.lba_pending.pop(0)
+                job.result()
+                self.main.wait_event(self.lba_slots[slot]["ev"])
 
     def results(self):
         torch = self.torch
@@ -676,6 +702,8 @@ class HotPath:
             self.native.close()
             self.native = None
         if self.n_lba:
+            self.lba_drain()
             self.lba_pool.shutdown()
-            self.lba_ex.close()
+            for sl in self.lba_slots:
+                sl["ex"].close()
         self.ex.close()

@@ -59,6 +59,7 @@ class LocalBA:
         self.ex = ex
         _bind(ex.lib)
         self.cfg = np.ascontiguousarray(cfg, np.float64)
+        self.team = 0
 
     def __call__(self, prob, kfs, points, point_obs, planes, plane_obs, stop_flag=None):
         """stop_flag: pbStopFlag -- a one-byte buffer (ctypes.c_uint8 or numpy u8) another thread may set while
@@ -85,6 +86,7 @@ class LocalBA:
         """Workgroups per problem of the g2o-order launch (0 = fill the chip, at most 8); results do not depend on
         it."""
         self.ex._check(self.ex.lib.spslam_lba_set_team(self.ex.ctx, int(workgroups)))
+        self.team = int(workgroups)
 
     def debug_stop_after(self, trials: int):
         """Test hook: the following calls see pbStopFlag raised after `trials` LM trials (-1 = off)."""
