@@ -175,7 +175,8 @@ typedef struct spslam_pose_result {
     float Tcw[16];      /* optimized pose (unchanged input if n_inliers == 0 by the <3 rule) */
     int32_t n_inliers;  /* PoseOptimization return value */
     int32_t lm_iterations;  /* total LM iterations run (diagnostic); -1 = the device gave up on a bounded
-                               internal wait (never observed): invalid result, Tcw = input, n_inliers = 0 */
+                               internal wait (never observed): invalid result, Tcw = input, n_inliers = 0,
+                               every point / plane outlier flag set to 1 */
     int32_t trial_passes;   /* edge passes at trial poses (damping trials are evaluated 4 per pass; diagnostic) */
     int32_t trials;         /* damping trials the reference evaluated (computeActiveErrors calls; diagnostic) */
 } spslam_pose_result;
@@ -500,9 +501,18 @@ int spslam_debug_plane_not_seen(spslam_ctx* ctx, const float* planes, int n_plan
 int spslam_debug_libm64(spslam_ctx* ctx, int kind, const double* a, const double* b, int n, double* out);
 
 /* Test hook: bound of PoseOptimization's internal waits (the chain wave and the compute waves hand edge rows over
- * through LDS; every wait gives up after `cap` polls).  0 restores the default (2^20 polls, never reached).  A
- * tiny cap forces the give-up path: the problem then reports lm_iterations = -1, n_inliers = 0, Tcw = input. */
+ * through LDS; every wait gives up after `cap` polls).  0 restores the default (2^20 polls, never reached); -1
+ * reports every problem as given up, deterministically.  A problem whose wait gave up reports lm_iterations = -1,
+ * n_inliers = 0, Tcw = input, and every point and plane outlier flag set (nothing of it is kept). */
 int spslam_debug_pose_spin_cap(spslam_ctx* ctx, int cap);
+
+/* Test hook: the context's following PoseOptimization (spslam_pose_optimize*) and g2o-order
+ * LocalBundleAdjustment calls treat the linear solve of LM trial q (0-based, counted over each
+ * call) as failed when bit q of trial_mask is set -- what g2o does on a non-positive dense LDLT
+ * (linear_solver_dense.h:107-112) or a zero SimplicialLDLT pivot (linear_solver_eigen.h:104-110):
+ * the solution vector keeps its previous contents, which the update and computeScale then use
+ * (optimization_algorithm_levenberg.cpp:110-127).  0 (default) turns it off. */
+int spslam_debug_force_solve_failures(spslam_ctx* ctx, unsigned trial_mask);
 
 /* ------------------------------------------------------------------------
  * RGB-D Frame per-keypoint steps (src/Frame.cc:146-181): UndistortKeyPoints

@@ -46,6 +46,8 @@
 #include "eigen_simplicial_restated.h"
 #include "g2o_restated.h"
 
+extern "C" unsigned oracle_get_solve_fail_mask();  // pose_oracle.cpp (test hook)
+
 namespace ORACLE_NS {
 namespace lba {
 
@@ -368,9 +370,13 @@ struct Opt {
     }
     // BlockSolver::solve with lambda on the diagonals (setLambda): Schur complement landmark by landmark
     // (block_solver.hpp:381-431), LinearSolverEigen on the reduced system, landmark back-substitution (:444-471).
-    bool solve(double lam, std::vector<double>& x) {
+    // x: g2o's solution buffer (Solver::_x), written only by a successful solve.  It persists for the whole call --
+    // both optimize() passes, whose layouts may differ (resizeVector keeps the allocation) -- and a failed solve
+    // leaves the previous solution in it, which update() and computeScale() then read anyway
+    // (optimization_algorithm_levenberg.cpp:110-127); "never written" is pinned to zeros (a fresh allocation).
+    bool solve(double lam, std::vector<double>& xbuf) {
         const int n = 6 * np;
-        x.assign((size_t)n + 3 * nl, 0.0);
+        std::vector<double> x((size_t)n + 3 * nl, 0.0);
         // _Hschur->clear(); _Hpp->add(_Hschur)  (whole diagonal blocks, lambda included)
         std::vector<double> S((size_t)n * n, 0.0), coeff((size_t)n, 0.0);
         for (int p = 0; p < np; p++)
@@ -414,6 +420,7 @@ struct Opt {
         std::vector<double> Ax(Ai.size());
         for (int c = 0; c < n; c++)
             for (int p = Ap[c]; p < Ap[c + 1]; p++) Ax[p] = S[(size_t)Ai[p] * n + c];
+        if (((solve_fail_mask >> (trials & 31)) & 1u) && trials < 32) return false;  // (test hook)
         if (!ldlt.factorize(Ax)) return false;
         ldlt.solve(bs.data(), x.data());
         // landmarks: cl = bl - Hpl^T xp (_HplCCS->rightMultiply with cp = -xp), xl = Dinv cl
@@ -429,6 +436,8 @@ struct Opt {
             const double* Di = &Dinv[9 * l];
             for (int i = 0; i < 3; i++) x[n + 3 * l + i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
         }
+        if (xbuf.size() < x.size()) xbuf.resize(x.size(), 0.0);
+        std::copy(x.begin(), x.end(), xbuf.begin());
         return true;
     }
     void push() {
@@ -455,6 +464,8 @@ struct Opt {
     // pbStopFlag emulation: the flag is raised right after trial number stop_after (SparseOptimizer::terminate();
     // stop_after < 0: never).  cut = a check point saw it where the schedule would have continued.
     int trials = 0, stop_after = -1;
+    unsigned solve_fail_mask = oracle_get_solve_fail_mask();
+    std::vector<double> xbuf;  // g2o's _x (see solve())
     bool cut = false;
     bool terminate() const { return stop_after >= 0 && trials >= stop_after; }
     int optimize(int iterations) {
@@ -473,17 +484,18 @@ struct Opt {
             double rho = 0;
             int qmax = 0;
             bool more;
-            std::vector<double> x;
+            const size_t sz = (size_t)6 * np + 3 * nl;  // _solver->vectorSize()
             do {
                 push();
-                const bool ok = solve(lambda, x);
-                if (ok) update(x);
+                const bool ok = solve(lambda, xbuf);
+                if (xbuf.size() < sz) xbuf.resize(sz, 0.0);
+                update(xbuf);  // _optimizer->update(_solver->x()), whether or not the solve succeeded
                 compute_errors();
                 double tempChi = robust_chi2();
                 if (!ok) tempChi = std::numeric_limits<double>::max();
                 rho = currentChi - tempChi;
                 double scale = 0;
-                for (size_t j = 0; j < x.size(); j++) scale += x[j] * (lambda * x[j] + b[j]);
+                for (size_t j = 0; j < sz; j++) scale += xbuf[j] * (lambda * xbuf[j] + b[j]);
                 scale += 1e-3;
                 rho /= scale;
                 if (rho > 0 && std::isfinite(tempChi)) {

@@ -216,6 +216,21 @@ def libm(mode: int):
         L.oracle_set_libm(prev)
 
 
+@contextlib.contextmanager
+def solve_failures(trial_mask: int):
+    """Inside the block (calling thread): bit q set = LM trial q's linear solve of every pose / LBA oracle call
+    reports failure (oracle_set_solve_fail_mask; the device hook is spslam_debug_force_solve_failures)."""
+    L = lib()
+    L.oracle_get_solve_fail_mask.restype = ctypes.c_uint
+    L.oracle_set_solve_fail_mask.argtypes = [ctypes.c_uint]
+    prev = L.oracle_get_solve_fail_mask()
+    L.oracle_set_solve_fail_mask(int(trial_mask))
+    try:
+        yield
+    finally:
+        L.oracle_set_solve_fail_mask(prev)
+
+
 def pose_optimize(problem, points, planes, cfg=None):
     """Oracle Optimizer::PoseOptimization.  Same arrays/dtypes as spslam_gpu.pose_optimize."""
     import spslam_gpu as G  # dtypes/config only (no GPU call)

@@ -41,6 +41,8 @@
 #include "../include/spslam_gpu.h"
 #include "g2o_restated.h"
 
+extern "C" unsigned oracle_get_solve_fail_mask();  // (test hook, defined below)
+
 namespace ORACLE_NS {
 namespace {
 
@@ -232,8 +234,12 @@ void quadratic_form(const Edge& e, const double J[3][6], double He[21], double s
     }
 }
 
-// SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg.
-int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
+// SparseOptimizer::optimize(iterations) with OptimizationAlgorithmLevenberg.  xs: g2o's solution buffer (Solver::_x),
+// kept across the trials and the four optimize(10) calls of one PoseOptimization and written only by a successful
+// solve: a failed LDLT leaves the previous solution, which update() and computeScale() then use anyway
+// (optimization_algorithm_levenberg.cpp:110-127, linear_solver_dense.h:107-112); "never written" is pinned to zeros.
+// trials counts the call's LM trials (the test hook oracle_set_solve_fail_mask).
+int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations, double* xs, int& trials) {
     LM lm;
     int its = 0;
     for (int it = 0; it < iterations; it++) {
@@ -265,8 +271,12 @@ int optimize(std::vector<Edge*>& active, SE3& T, const Cam& c, int iterations) {
             double Hl[6][6];
             std::memcpy(Hl, H, sizeof Hl);
             for (int j = 0; j < 6; j++) Hl[j][j] += lm.lambda;
-            double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten (rejected step)
-            bool ok2 = ldlt_solve(Hl, b, x);
+            double xn[6];
+            const bool forced = trials < 32 && ((oracle_get_solve_fail_mask() >> trials) & 1u);  // (test hook)
+            const bool ok2 = !forced && ldlt_solve(Hl, b, xn);
+            trials++;
+            if (ok2) std::memcpy(xs, xn, sizeof xn);
+            const double* x = xs;
             T = SE3::exp(x) * T;
             for (Edge* e : active) compute_error(*e, T, c);
             tempChi = robust_chi2(active);
@@ -330,6 +340,16 @@ static int& g2o_fma_mode() {
 }
 extern "C" void oracle_set_g2o_fma(int on) { g2o_fma_mode() = on; }
 extern "C" int oracle_get_g2o_fma() { return g2o_fma_mode(); }
+// Test hook of the calling thread (spslam_debug_force_solve_failures on the device): bit q set = the linear solve of
+// LM trial q (0-based, counted over the whole PoseOptimization / LocalBundleAdjustment call) reports failure, as a
+// non-positive (dense LDLT) or zero-pivot (SimplicialLDLT) system would -- the path on which g2o keeps its stale
+// solution vector (optimization_algorithm_levenberg.cpp:110-127, block_solver.hpp:447-457).
+static unsigned& solve_fail_mask() {
+    static thread_local unsigned mask = 0;
+    return mask;
+}
+extern "C" void oracle_set_solve_fail_mask(unsigned mask) { solve_fail_mask() = mask; }
+extern "C" unsigned oracle_get_solve_fail_mask() { return solve_fail_mask(); }
 extern "C" int oracle_pose_optimize_fma(const spslam_pose_problem* P, const spslam_point_obs* pts,
                                         const spslam_plane_obs* pls, const spslam_plane_config* cfg,
                                         spslam_pose_result* out, uint8_t* pout, uint8_t* plout);
@@ -389,13 +409,14 @@ extern "C" int ORACLE_ENTRY(oracle_pose_optimize)(const spslam_pose_problem* P, 
         plout[i] = 0;
     }
     SE3 T = T0;
-    int nBad = 0, total_its = 0;
+    int nBad = 0, total_its = 0, trials = 0;
+    double xs[6] = {0, 0, 0, 0, 0, 0};
     for (int it = 0; it < 4; it++) {
         T = T0;
         std::vector<Edge*> active;
         for (Edge& e : edges)
             if (e.level == 0) active.push_back(&e);
-        total_its += optimize(active, T, cam, 10);
+        total_its += optimize(active, T, cam, 10, xs, trials);
         nBad = 0;
         for (size_t k = 0; k < edges.size(); k++) {
             Edge& e = edges[k];

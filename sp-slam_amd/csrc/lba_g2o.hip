@@ -474,6 +474,9 @@ __device__ __noinline__ void setup() {
         base_e += tot;
     }
     for (int e = g.E + t; e < lbg_pad32(g.E); e += kT) g.echi[e] = 0.0;
+    // g2o's solution buffer (Solver::_x): written only by successful solves and read by every update, so a failed
+    // solve re-applies the previous solution; never written = zeros (update())
+    for (int j = t; j < lbg_pad32(6 * lbg_free_cap(g.K) + 3 * g.L); j += kT) g.x[j] = 0.0;
     // landmark (vertex-id) order: points by id (ids mnId + maxKFid + 1), then planes by id (mnId + maxPointid + 1,
     // above every point id); stable ranks (id, list index)
     for (int grp = 0; grp < 2; grp++) {
@@ -2644,7 +2647,9 @@ __device__ __forceinline__ Share my_share(const Sh& s, int K) {
     return Share{split_lo(s.nl, s.m, s.T), split_lo(s.nl, s.m + 1, s.T), split_lo(K, s.m, s.T), split_lo(K, s.m + 1, s.T)};
 }
 // landmark increments (xl = Dinv (bl - Hpl^T xp), Dinv as the Schur phase formed it), push, update
-// (block_solver.hpp:444-471, oplus); this member's landmarks and keyframes
+// (block_solver.hpp:444-471, oplus); this member's landmarks and keyframes.  After a failed solve nothing of x was
+// written (block_solver.hpp:447-457: the landmark part is formed only after a successful pose solve) and g2o still
+// applies it: every vertex moves by the previous solution (optimization_algorithm_levenberg.cpp:110-115).
 __device__ __noinline__ void update() {
     const G& g = lbg_g;
     const Sh& s = lbg_s;
@@ -2657,7 +2662,7 @@ __device__ __noinline__ void update() {
         const int l = g.hidx_lm[h];
         if (l < g.Np) for (int j = 0; j < 3; j++) g.X_b[3 * l + j] = g.X[3 * l + j];
         else for (int j = 0; j < 4; j++) g.P_b[4 * (l - g.Np) + j] = g.P[4 * (l - g.Np) + j];
-        double xl[3] = {0.0, 0.0, 0.0};
+        double xl[3];
         if (ok) {
             double cl[3] = {g.bl[3 * h], g.bl[3 * h + 1], g.bl[3 * h + 2]};
             uint64_t m = g.lmh_mask[h];
@@ -2676,21 +2681,23 @@ __device__ __noinline__ void update() {
             for (int j = 0; j < 9; j++) H[j] = g.Hll[9 * h + j];
             landmark_dinv(H, cl, lam, Di, db);  // (db unused)
             for (int i = 0; i < 3; i++) xl[i] = (Di[3 * i] * cl[0] + Di[3 * i + 1] * cl[1]) + Di[3 * i + 2] * cl[2];
-            if (l < g.Np) {
-                for (int j = 0; j < 3; j++) g.X[3 * l + j] += xl[j];
-            } else {
-                auto pp = g.P + 4 * (l - g.Np);
-                P4 P{{pp[0], pp[1], pp[2], pp[3]}};
-                p_oplus(P, xl);
-                for (int j = 0; j < 4; j++) pp[j] = P.c[j];
-            }
+            for (int j = 0; j < 3; j++) g.x[n + 3 * h + j] = xl[j];
+        } else {
+            for (int j = 0; j < 3; j++) xl[j] = g.x[n + 3 * h + j];
         }
-        for (int j = 0; j < 3; j++) g.x[n + 3 * h + j] = xl[j];
+        if (l < g.Np) {
+            for (int j = 0; j < 3; j++) g.X[3 * l + j] += xl[j];
+        } else {
+            auto pp = g.P + 4 * (l - g.Np);
+            P4 P{{pp[0], pp[1], pp[2], pp[3]}};
+            p_oplus(P, xl);
+            for (int j = 0; j < 4; j++) pp[j] = P.c[j];
+        }
     }
     for (int k = sh.k0 + t; k < sh.k1; k += kT) {
         for (int j = 0; j < 7; j++) g.pose_b[7 * k + j] = g.pose[7 * k + j];
         const int h = s.hidx[k];
-        if (!ok || h < 0) continue;
+        if (h < 0) continue;
         double u[6];
         for (int j = 0; j < 6; j++) u[j] = g.x[6 * h + j];
         store_pose(g.pose + 7 * k, se3_mul(se3_exp(u), load_pose(g.pose + 7 * k)));
@@ -2721,7 +2728,7 @@ __device__ __noinline__ void scale_terms() {
     const double lam = s.lambda;
     for (int j = split_lo(pad, s.m, s.T) + t; j < split_lo(pad, s.m + 1, s.T); j += kT) {
         double v = 0.0;
-        if (j < tot && s.ok) {
+        if (j < tot) {  // (x as update() applied it: after a failed solve, the previous solution)
             const double b = j < n ? g.Hps[27 * (j / 6) + 21 + j % 6] : g.bl[j - n];
             const double x = g.x[j];
             v = x * (lam * x + b);
@@ -2955,7 +2962,10 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                 else schur();
                 team_sync(b);
                 LBG_MARK(5);
-                if (lead) {
+                const bool forced = s.trials < 32 && ((b.fail_mask >> s.trials) & 1u);  // (test hook)
+                if (lead && forced) {
+                    if (t == 0) { s.ok = 0; g.team->ok = 0; }
+                } else if (lead) {
                     if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
                         for (int i = t; i <= n * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
                         for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];

@@ -190,6 +190,7 @@ struct LbgBatch {
     const int32_t* stop;  // per problem pbStopFlag (device-visible; NULL = no flag)
     int stop_after;       // test hook: the flag counts as raised once a problem has run this many trials (-1 off)
     int team;             // workgroups per problem (1 .. kLbgTeamMax); the grid is n * team
+    unsigned fail_mask;   // test hook: bit q = LM trial q's solve reports failure (spslam_debug_force_solve_failures)
     int* ctl;             // lbg_ctl_ints(n) ints, zeroed before the launch: [0] the workgroups' arrival ticket,
                           //   [16 (p + 1)] problem p's team barrier counter (one 64-byte line each)
 };

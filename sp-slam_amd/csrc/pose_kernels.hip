@@ -516,7 +516,10 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         add[t >> 1] = (t & 1) ? -1e-9 : 1e-9;
         S.Eadd[t] = se3_exp(add);
     }
-    if (t == 0) { S.stall = 0; S.spin_cap = K.spin_cap; }
+    if (t == 0) {  // (spin_cap < 0, a test hook: the problem is reported as stalled whatever its waits do)
+        S.stall = K.spin_cap < 0;
+        S.spin_cap = K.spin_cap < 0 ? (1 << 20) : K.spin_cap;
+    }
     SE3 T0;  // Converter::toSE3Quat: Quaterniond(R) of the float pose, normalized (every thread)
     {
         M3 R;
@@ -599,6 +602,10 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     int buf = 0;
     bool robust = true;
     int nBad = 0, total_its = 0, total_passes = 0, total_trials = 0;
+    // g2o's solution buffer (Solver::_x) across the trials and the four optimize(10) calls: written only by a
+    // successful LDLT, applied and used in computeScale whether or not the trial's solve succeeded
+    // (optimization_algorithm_levenberg.cpp:110-127, linear_solver_dense.h:107-112); never written = zeros
+    double xs[6] = {0, 0, 0, 0, 0, 0};
     SE3 T;
     for (int round = 0; round < 4; round++) {
         PROF_MARK(0);  // setup / previous relabel
@@ -780,8 +787,29 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
 #pragma unroll
                         for (int i = 0; i < 6; i++) b[i] = hbw[22 + i];
                     }
-                    double x[6] = {0, 0, 0, 0, 0, 0};  // a failed LDLT leaves x unwritten (rejected step)
-                    const bool ok = ldlt_solve(H, lam, b, x);
+                    double xn[6] = {0, 0, 0, 0, 0, 0};
+                    const int gq = total_trials + myq;  // this trial's index in the call (test hook)
+                    const bool ok = !(gq < 32 && ((K.fail_mask >> gq) & 1u)) && ldlt_solve(H, lam, b, xn);
+                    // the solution trial q applies: its own if its solve succeeded, else that of the last earlier trial
+                    // of the pass whose solve did, else the buffer carried in (trials q' < q were rejected if q runs)
+                    double x[6];
+                    {
+                        double xe[6];
+#pragma unroll
+                        for (int j = 0; j < 6; j++) xe[j] = xs[j];
+#pragma unroll
+                        for (int q = 0; q < kSpec; q++) {
+                            const bool okq = __builtin_amdgcn_readlane((int)ok, q) != 0;
+#pragma unroll
+                            for (int j = 0; j < 6; j++) {
+                                const double v = readlane_d(xn[j], q);
+                                xe[j] = okq ? v : xe[j];
+                            }
+#pragma unroll
+                            for (int j = 0; j < 6; j++)
+                                if (myq == q) x[j] = xe[j];
+                        }
+                    }
                     const SE3 Tt = se3_mul(se3_exp(x), T);
                     double scale = 0;  // OptimizationAlgorithmLevenberg::computeScale + 1e-3
 #pragma unroll
@@ -900,6 +928,8 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                             if (q == lastq) tl = Tq[q];
                         S.tlast[wv] = tl;
                     }
+#pragma unroll
+                    for (int j = 0; j < 6; j++) xs[j] = readlane_d(x[j], lastq);  // the buffer after the last trial run
                     tValid = tValid || acc >= 0;
                     if (acc >= 0 && t < nl && nl <= kPlaneChunk) {  // thread t reads perrT[t] in the next pass A
 #pragma unroll
@@ -961,9 +991,14 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         if (round == 2) robust = false;
         if (ne < 10) break;
     }
+    __syncthreads();
+    if (S.stall) {  // every outlier flag set: nothing of a failed problem is kept (the tail's discard reads them)
+        for (int e = t; e < np; e += kThreads) pout[e] = 1;
+        for (int j = t; j < nl; j += kThreads) plout[j] = 1;
+    }
     if (t == 0 && S.stall) {
         // a bounded wait gave up (never observed): the sums are not valid, so the problem reports failure -- the
-        // input pose, no inliers, lm_iterations = -1 -- and callers treat it as a lost frame
+        // input pose, no inliers, lm_iterations = -1, every edge flagged -- and callers treat it as a lost frame
         for (int i = 0; i < 16; i++) res->Tcw[i] = Tin[i];
         res->n_inliers = 0;
         res->lm_iterations = -1;
@@ -1025,6 +1060,7 @@ PoseConsts make_pose_consts(const spslam_plane_config& c) {
     K.delta_plane = (double)(float)sqrt(c.chi);
     K.delta_vp = (double)(float)sqrt(c.vp_chi);
     K.spin_cap = 1 << 20;
+    K.fail_mask = 0;
     return K;
 }
 

@@ -13,6 +13,8 @@ struct PoseConsts {
     double plane_chi, vp_chi;
     double delta_plane, delta_vp;           // (float)sqrt(Chi), (float)sqrt(VPChi)
     int spin_cap;                           // bound of the kernel's internal waits (spslam_debug_pose_spin_cap)
+    unsigned fail_mask;                     // test hook: bit q = LM trial q's LDLT reports failure
+                                            //   (spslam_debug_force_solve_failures; 0 otherwise)
 };
 
 PoseConsts make_pose_consts(const spslam_plane_config& c);

@@ -144,6 +144,7 @@ struct spslam_ctx {
                                       //   rewrites the offsets, the ctl block or the scratch (one LBA call in flight
                                       //   per context, whatever the streams)
     int pose_spin_cap = 0;            // spslam_debug_pose_spin_cap (0 = the kernel's default)
+    unsigned solve_fail_mask = 0;     // spslam_debug_force_solve_failures
     int lba_off_cap = 0;
     uint8_t* d_lba_stage = nullptr;   // drop-in staging
     size_t lba_stage_bytes = 0;
@@ -486,7 +487,8 @@ int spslam_pose_optimize_batch_device(spslam_ctx* c, int n, const spslam_pose_pr
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
     PoseConsts K = make_pose_consts(*cfg);
-    if (c->pose_spin_cap > 0) K.spin_cap = c->pose_spin_cap;
+    if (c->pose_spin_cap != 0) K.spin_cap = c->pose_spin_cap;
+    K.fail_mask = c->solve_fail_mask;
     if (c->timer) c->timer->begin(kKindPose, s);
     HIP_CHECK(c, pose_launch(n, d_problems, d_points, d_planes, K, d_init_from, d_results, d_point_outlier,
                              d_plane_outlier, s));
@@ -814,8 +816,14 @@ int spslam_debug_plane_not_seen(spslam_ctx* c, const float* planes, int n_planes
     return SPSLAM_OK;
 }
 
+int spslam_debug_force_solve_failures(spslam_ctx* c, unsigned trial_mask) {
+    if (!c) return SPSLAM_ERR_ARG;
+    c->solve_fail_mask = trial_mask;
+    return SPSLAM_OK;
+}
+
 int spslam_debug_pose_spin_cap(spslam_ctx* c, int cap) {
-    if (!c || cap < 0) return SPSLAM_ERR_ARG;
+    if (!c || cap < -1) return SPSLAM_ERR_ARG;
     c->pose_spin_cap = cap;
     return SPSLAM_OK;
 }
@@ -1108,7 +1116,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
         LbgBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                    d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
-                   c->lba_stop_after, team, c->d_lba_ctl};
+                   c->lba_stop_after, team, c->solve_fail_mask, c->d_lba_ctl};
         HIP_CHECK(c, lba_run_g2o(B, C, s, c->timer));
         HIP_CHECK(c, hipEventRecord(c->lba_done, s));
         if (stop_src) {  // host-buffer entry: mirror the caller's bool into the device-visible flag while it runs

@@ -201,7 +201,14 @@ def _bind_pose(lib):
 
 
 EXPORTED += ["spslam_pose_optimize", "spslam_pose_optimize_batch_device", "spslam_debug_libm64",
-             "spslam_debug_pose_spin_cap"]
+             "spslam_debug_pose_spin_cap", "spslam_debug_force_solve_failures"]
+
+
+def debug_force_solve_failures(ex: "OrbExtractor", trial_mask: int):
+    """Test hook: bit q set = LM trial q's linear solve (PoseOptimization, g2o-order LocalBundleAdjustment) reports
+    failure, so g2o's stale-solution path runs (0 = off)."""
+    ex.lib.spslam_debug_force_solve_failures.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+    ex._check(ex.lib.spslam_debug_force_solve_failures(ex.ctx, int(trial_mask)))
 
 
 def debug_pose_spin_cap(ex: "OrbExtractor", cap: int):

@@ -276,6 +276,28 @@ def test_lba_shared_blocks_match_oracle(lba):
     _assert_identical(lba(prob, kfs, pts, pobs, pls, plobs), o, "shared blocks")
 
 
+@pytest.mark.parametrize("mask", [0b1, 0b10, 0b1100, 0b100000, 0x3FF])
+def test_lba_failed_solve_keeps_previous_solution(lba, mask):
+    """g2o's failed-factorisation path (SimplicialLDLT's zero pivot, linear_solver_eigen.h:104-110): nothing of the
+    solution vector is written (block_solver.hpp:447-457), yet update() applies it and computeScale() reads it
+    (optimization_algorithm_levenberg.cpp:110-127) -- the previous solution, zeros before the first success, kept
+    across the two optimize() passes -- and tempChi is DBL_MAX, so the trial is rejected and popped, its errors
+    staying cached for the relabel.  Trials forced to fail (bit q = trial q) give the oracle's map, flags and counts
+    bit for bit; 0x3FF makes a whole iteration's ten trials fail (qmax = 10)."""
+    import oracle_ctypes
+    import oracle_lba
+    import spslam_gpu
+    for k, P in enumerate(_problems()[:2]):
+        try:
+            spslam_gpu.debug_force_solve_failures(lba.ex, mask)
+            g = lba(*P[:6])
+        finally:
+            spslam_gpu.debug_force_solve_failures(lba.ex, 0)
+        with oracle_ctypes.solve_failures(mask):
+            o = oracle_lba.lba_optimize(*P[:6])
+        _assert_identical(g, o, f"mask {mask:#x} problem {k}")
+
+
 def test_lba_fast_order_within_bar(lba):
     """SPSLAM_LBA_FAST_ORDER (the phase kernels): same decisions, values within 1e-4 relative."""
     import oracle_lba

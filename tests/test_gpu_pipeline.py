@@ -257,15 +257,18 @@ def test_native_step_matches_python():
         assert out[True][-1]["nmatches"].sum() > 0
 
 
-def test_c3_local_mapping_beside_tracking():
-    """C3: the step's LocalBundleAdjustments run on the LocalMapping stream and context while the tracking chain
-    runs (pipelined): every local map's result matches the oracle (LM iterations and outlier flags identical,
-    poses / points / planes within 1e-4), and the tracking results equal a step without LocalMapping."""
+@pytest.mark.parametrize("depth,team", [(0, 0), (2, 1), (1, 3)])
+def test_c3_local_mapping_beside_tracking(depth, team):
+    """C3: the step's LocalBundleAdjustments run on the LocalMapping streams and contexts while the tracking chain
+    runs (pipelined), joined `depth` steps later (depth + 1 calls in flight), `team` workgroups per local map:
+    every local map's result is bit-identical to the oracle's (LM iterations, outlier flags, poses, points,
+    planes) in every in-flight slot, and the tracking results equal a step without LocalMapping."""
     import oracle_lba
     import pipeline
     import spslam_lba as L
     cfg = dict(pipeline.CONFIGS["c3"], lba_every=2)
-    hp = pipeline.HotPath(8, unique_frames=8, pipelined=True, lba_unique=2, lba_points=600, **cfg)
+    hp = pipeline.HotPath(8, unique_frames=8, pipelined=True, lba_unique=2, lba_points=600, lba_depth=depth,
+                          lba_team=team, **cfg)
     ref = pipeline.HotPath(8, unique_frames=8, pipelined=True, **dict(cfg, lba_every=0))
     try:
         for _ in range(3):
@@ -275,23 +278,26 @@ def test_c3_local_mapping_beside_tracking():
         for key in ("pose1", "pose2"):
             assert res[key].tobytes() == rr[key].tobytes(), key
         assert np.array_equal(res["local_match"], rr["local_match"])
-        out = [x.cpu().numpy() for x in hp.lba_out]
-        lres = out[5].view(L.LBA_RESULT_DTYPE)
         pc = hp.plane_cfg
         cfgv = (pc.angle_info, pc.distance_info, pc.parallel_info, pc.vertical_info, pc.chi, pc.vp_chi)
-        nk = npt = npo = npl = nplo = 0
-        for i in range(hp.n_lba):
-            P = hp.lba_problems[i % len(hp.lba_problems)]
-            o = oracle_lba.lba_optimize(*P[:6], cfg=cfgv)
-            k, n_pt, n_po, n_pl, n_plo = len(P[1]), len(P[2]), len(P[3]), len(P[4]), len(P[5])
-            assert lres[i]["status"] == 0
-            assert list(lres[i]["iterations"]) == list(o["result"]["iterations"]), i
-            assert np.array_equal(out[3][npo:npo + n_po].astype(bool), o["point_outlier"]), i
-            assert np.array_equal(out[4][nplo:nplo + n_plo].astype(bool), o["plane_outlier"]), i
-            tol = 1e-4 * max(1.0, np.abs(o["Tcw"]).max())
-            assert np.abs(out[0][nk:nk + k] - o["Tcw"].reshape(k, 16)).max() <= tol, i
-            assert np.abs(out[1][npt:npt + n_pt] - o["points"]).max() <= 1e-4 * max(1.0, np.abs(o["points"]).max()), i
-            nk, npt, npo, npl, nplo = nk + k, npt + n_pt, npo + n_po, npl + n_pl, nplo + n_plo
+        assert len(hp.lba_slots) == depth + 1
+        for sl in hp.lba_slots:  # (3 steps: every slot ran a call)
+            out = [x.cpu().numpy() for x in sl["out"]]
+            lres = out[5].view(L.LBA_RESULT_DTYPE)
+            nk = npt = npo = npl = nplo = 0
+            for i in range(hp.n_lba):
+                P = hp.lba_problems[i % len(hp.lba_problems)]
+                o = oracle_lba.lba_optimize(*P[:6], cfg=cfgv)
+                k, n_pt, n_po, n_pl, n_plo = len(P[1]), len(P[2]), len(P[3]), len(P[4]), len(P[5])
+                assert lres[i]["status"] == 0
+                assert list(lres[i]["iterations"]) == list(o["result"]["iterations"]), i
+                assert np.array_equal(out[3][npo:npo + n_po].astype(bool), o["point_outlier"]), i
+                assert np.array_equal(out[4][nplo:nplo + n_plo].astype(bool), o["plane_outlier"]), i
+                # the default g2o-order LBA: bit-identical to the oracle
+                assert np.array_equal(out[0][nk:nk + k], o["Tcw"].reshape(k, 16)), i
+                assert np.array_equal(out[1][npt:npt + n_pt], o["points"]), i
+                assert np.array_equal(out[2][npl:npl + n_pl], o["planes"]), i
+                nk, npt, npo, npl, nplo = nk + k, npt + n_pt, npo + n_po, npl + n_pl, nplo + n_plo
         assert hp.n_lba == 4
     finally:
         hp.close()

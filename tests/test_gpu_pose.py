@@ -133,24 +133,47 @@ def test_fewer_than_three_points_returns_zero(gpu, problems):
 
 
 def test_wait_give_up_reports_failure(gpu, problems):
-    """A bounded internal wait that gives up (forced with a one-poll cap) must not yield a valid-looking pose:
-    the problem reports lm_iterations = -1, no inliers and the input pose (callers treat it as a lost frame)."""
+    """A bounded internal wait that gives up must not yield a valid-looking pose: the problem reports
+    lm_iterations = -1, no inliers, the input pose and every outlier flag set (callers treat it as a lost frame and
+    keep none of its matches).  The hook's -1 forces the report deterministically; the default cap again gives the
+    normal result."""
     import spslam_gpu
     prob, pts, pls, _ = problems[1]
     try:
-        spslam_gpu.debug_pose_spin_cap(gpu, 1)
+        spslam_gpu.debug_pose_spin_cap(gpu, -1)
         r, po, plo = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
     finally:
         spslam_gpu.debug_pose_spin_cap(gpu, 0)
-    if int(r["lm_iterations"]) != -1:  # every wait happened to be satisfied on its first poll: a valid result
-        import oracle_ctypes
-        ro, _, _ = oracle_ctypes.pose_optimize(prob, pts, pls)
-        assert np.array_equal(r["Tcw"], ro["Tcw"])
-        return
+    assert int(r["lm_iterations"]) == -1
     assert int(r["n_inliers"]) == 0
     assert np.array_equal(r["Tcw"], prob["Tcw"])
+    assert po.all() and (len(plo) == 0 or plo.all())
     r2, _, _ = spslam_gpu.pose_optimize(gpu, prob, pts, pls)  # the default cap again: a normal result
     assert int(r2["lm_iterations"]) > 0 and int(r2["n_inliers"]) > 0
+
+
+@pytest.mark.parametrize("mask", [0b1, 0b10, 0b110, 0b1000001, 0xFFFFFFFF])
+def test_pose_failed_solve_keeps_previous_solution(gpu, problems, mask):
+    """g2o's failed-LDLT path (optimization_algorithm_levenberg.cpp:110-127, linear_solver_dense.h:107-112): the
+    solution vector keeps its previous contents (zeros before the first success), the update and computeScale use
+    it anyway, tempChi is DBL_MAX.  Trials whose solve is forced to fail (bit q = trial q of the call) -- with the
+    device evaluating four trials per pass, so a failed trial's stale solution comes from an earlier lane of the same
+    pass or from the buffer carried over -- give the oracle's pose, inliers, iterations and flags bit for bit."""
+    import oracle_ctypes
+    import spslam_gpu
+    for k in (0, 4, 7):
+        prob, pts, pls, _ = problems[k]
+        try:
+            spslam_gpu.debug_force_solve_failures(gpu, mask)
+            rg, pog, plog = spslam_gpu.pose_optimize(gpu, prob, pts, pls)
+        finally:
+            spslam_gpu.debug_force_solve_failures(gpu, 0)
+        with oracle_ctypes.solve_failures(mask):
+            ro, poo, ploo = oracle_ctypes.pose_optimize(prob, pts, pls)
+        tag = f"mask {mask:#x} problem {k}"
+        assert np.array_equal(rg["Tcw"].view(np.uint32), ro["Tcw"].view(np.uint32)), tag
+        assert int(rg["n_inliers"]) == int(ro["n_inliers"]) and int(rg["lm_iterations"]) == int(ro["lm_iterations"]), tag
+        assert np.array_equal(pog, poo) and np.array_equal(plog, ploo), tag
 
 
 def test_few_edges_single_round(gpu, problems):
