@@ -146,8 +146,9 @@ def test_lba_sparse_reduced_system_amd(lba):
         _assert_identical(lba(*Pc[:6]), oracle_lba.lba_optimize(*Pc[:6]), f"corridor {k}")
 
 
-def _batch(lba, probs, flags=None):
-    """One batch_device call over `probs` (optionally with per-problem stop flags preset in device memory)."""
+def _batch(lba, probs, flags=None, stream=None, sync=True):
+    """One batch_device call over `probs` (optionally with per-problem stop flags preset in device memory); with
+    sync=False the device buffers come back unsynchronised (a callable that finishes the call)."""
     import torch
     import spslam_lba as L
     hdr = np.zeros(len(probs), L.LBA_PROBLEM_DTYPE)
@@ -174,10 +175,14 @@ def _batch(lba, probs, flags=None):
     stop = None if flags is None else torch.tensor(flags, dtype=torch.int32, device="cuda")
     lba.batch_device(len(probs), hdr, *[x.data_ptr() for x in d], kf_out.data_ptr(), pt_out.data_ptr(),
                      pl_out.data_ptr(), po_out.data_ptr(), plo_out.data_ptr(), res.data_ptr(),
-                     d_stop=None if stop is None else stop.data_ptr())
-    torch.cuda.synchronize()
-    return (hdr, kf_out.cpu().numpy(), pt_out.cpu().numpy(), pl_out.cpu().numpy(), po_out.cpu().numpy(),
-            plo_out.cpu().numpy(), res.cpu().numpy().view(L.LBA_RESULT_DTYPE))
+                     d_stop=None if stop is None else stop.data_ptr(),
+                     stream=0 if stream is None else stream.cuda_stream)
+
+    def finish():
+        torch.cuda.synchronize()
+        return (hdr, kf_out.cpu().numpy(), pt_out.cpu().numpy(), pl_out.cpu().numpy(), po_out.cpu().numpy(),
+                plo_out.cpu().numpy(), res.cpu().numpy().view(L.LBA_RESULT_DTYPE), d)
+    return finish()[:7] if sync else finish
 
 
 def test_lba_batch_device_matches_single(lba):
@@ -190,6 +195,26 @@ def test_lba_batch_device_matches_single(lba):
         assert np.array_equal(pt_out[h["point_offset"]:h["point_offset"] + h["n_points"]], s["points"])
         assert np.array_equal(pl_out[h["plane_offset"]:h["plane_offset"] + h["n_planes"]], s["planes"])
         assert res[i]["trials"] == s["result"]["trials"]
+
+
+def test_lba_two_streams_one_context(lba):
+    """Two calls on one context, enqueued back to back on two streams without a host sync: the second
+    waits on the device for the first (the context's scratch, offsets and team counters are reused), so both
+    batches come back bit-identical to single calls."""
+    import torch
+    probs = _problems()
+    a, b = probs[:2], probs[2:4]
+    singles = [lba(*P[:6]) for P in probs[:4]]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    fa = _batch(lba, a, stream=s1, sync=False)
+    fb = _batch(lba, b, stream=s2, sync=False)
+    for f, ps, ss in ((fa, a, singles[:2]), (fb, b, singles[2:])):
+        hdr, kf_out, pt_out, pl_out, po_out, plo_out, res = f()[:7]
+        for i, sref in enumerate(ss):
+            h = hdr[i]
+            assert np.array_equal(kf_out[h["kf_offset"]:h["kf_offset"] + h["n_kf"]], sref["Tcw"])
+            assert np.array_equal(pt_out[h["point_offset"]:h["point_offset"] + h["n_points"]], sref["points"])
+            assert res[i]["trials"] == sref["result"]["trials"]
 
 
 def test_lba_stop_flags_preset(lba):
