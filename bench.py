@@ -354,19 +354,23 @@ def closed_loop(cfg, device, B, steps, warmup, n_seq=16):
         sp.close()
 
 
-def single_sequence(cfg, device, n_frames=120, warmup=5):
+def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
     """The reference's own call pattern (Examples/RGB-D/SPSLAM.cc:90-136 -> System::TrackRGBD per frame): ONE
     tracked sequence, one frame at a time (B = 1, sp-slam_amd/sequence.py; every frame's prior and last-frame
-    points from its predecessor).  frames_per_s: frame k+1's grab / ORB / planes overlapped with frame k's tracking
-    tail (the pipelined step), host synchronised only at the end.  latency_ms_*: the serial step (grab ->
+    points from its predecessor).  frames_per_s: frames k+1 .. k+L's grab / ORB / planes overlapped with frame k's
+    tracking tail (the pipelined step, L = SINGLE_LOOKAHEAD frames read ahead as SPSLAM.cc's loop over the image list
+    allows; two extraction units side by side), host synchronised only at the end.  latency_ms_*: the serial step (grab ->
     extraction -> tracking tail) with the host waiting for each frame's pose -- image on the device to pose on the
     device, the per-frame latency a TrackRGBD caller sees (the 64-byte pose read-back excluded)."""
     import numpy as np
     import torch
     import sequence
-    out = {"kind": "one sequence, B = 1 (sequence.SequencePath), frames device-resident", "frames": n_frames}
+    look = SINGLE_LOOKAHEAD if lookahead is None else lookahead
+    out = {"kind": "one sequence, B = 1 (sequence.SequencePath), frames device-resident", "frames": n_frames,
+           "lookahead": look}
     for pipelined in (True, False):
         sp = sequence.SequencePath(1, n_frames + warmup + 2, n_sequences=1, device=device, pipelined=pipelined,
+                                   lookahead=look if pipelined else 1,
                                    render_workers=min(16, os.cpu_count() or 1), **cfg)
         try:
             for _ in range(warmup):
@@ -513,6 +517,7 @@ def _ensure_hw_queues(want=None):
 
 
 LBA_DEPTH, LBA_TEAM = 2, 1  # C3 defaults (profiles/r05/ab_c3_*.txt)
+SINGLE_LOOKAHEAD = 3  # single_sequence: frames extracted ahead of tracking (profiles/r05/b1_lookahead.txt)
 
 
 def main():

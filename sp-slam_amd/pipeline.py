@@ -63,10 +63,13 @@ class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
-                 rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0):
+                 rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
+        self.nfeatures = nfeatures
+        # pipelined: batches extracted ahead of the tracking tail (1: batch k+1 beside batch k's tail)
+        self.lookahead = max(1, int(lookahead))
         self.device = device
         self.lba_order = lba_order  # spslam_lba.G2O_ORDER (default) / FAST_ORDER
         s = width / 640.0
@@ -518,15 +521,37 @@ class HotPath:
         overwritten once the tail that read it has finished (ev_tail[j])."""
         torch = self.torch
         names = self.EXTRACTION_BUFFERS + (self.INPUT_BUFFERS if self.rotate_inputs else ())
-        self.sets = [{k: getattr(self, k) for k in names}, {k: getattr(self, k).clone() for k in names}]
-        # ORB extraction is the longest extraction chain; orb_priority lets its workgroups dispatch ahead of the
-        # plane chain's (the tracking tail keeps its high priority)
-        self.ext_orb = torch.cuda.Stream(priority=-1 if self.orb_priority else 0)
-        self.ext_planes = torch.cuda.Stream(priority=-1 if self.planes_priority else 0)
-        self.ev_orb = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_planes = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_tail = [torch.cuda.Event(), torch.cuda.Event()]
-        self.ev_grab = [torch.cuda.Event(), torch.cuda.Event()]
+        # lookahead L: batches k+1 .. k+L are extracted ahead of batch k's tail (L + 1 buffer sets).  At small B
+        # the extraction's plane chain (one workgroup per frame) is longer than the tail, so with L >= 2 two
+        # extractions run side by side, each on its own ORB / plane context (their scratch) and streams; batch m
+        # is extracted on unit m % L.  Extraction is per-frame and independent of tracking: results are those of
+        # the serial step for every L.
+        L = self.lookahead
+        self.sets = [{k: getattr(self, k) for k in names}] + [{k: getattr(self, k).clone() for k in names}
+                                                              for _ in range(L)]
+        self.ext_units = []
+        for e in range(L):
+            if e == 0:
+                ex, pe, grabber = self.ex, self.pe, self.grabber
+            else:
+                ex = G.OrbExtractor(nfeatures=self.nfeatures, width=self.W, height=self.H, max_batch=self.B,
+                                    device=self.device)
+                pe = spslam_planes.PlaneExtractor(ex, self.fx, self.fy, self.cx, self.cy, self.W, self.H,
+                                                  min_size=self.min_size)
+                grabber = spslam_grab.Grabber(ex, channels=3, rgb=True, depth_u16=True,
+                                              depth_factor=self.depth_factor)
+            # ORB extraction is the longest extraction chain at large B; orb_priority lets its workgroups dispatch
+            # ahead of the plane chain's (the tracking tail keeps its high priority)
+            self.ext_units.append(dict(ex=ex, pe=pe, grabber=grabber,
+                                       orb=torch.cuda.Stream(priority=-1 if self.orb_priority else 0),
+                                       planes=torch.cuda.Stream(priority=-1 if self.planes_priority else 0)))
+        self.ext_orb, self.ext_planes = self.ext_units[0]["orb"], self.ext_units[0]["planes"]
+        n = L + 1
+        self.ev_orb = [torch.cuda.Event() for _ in range(n)]
+        self.ev_planes = [torch.cuda.Event() for _ in range(n)]
+        self.ev_tail = [torch.cuda.Event() for _ in range(n)]
+        self.ev_grab = [torch.cuda.Event() for _ in range(n)]
+        self.n_extracted = 0
         # The supposed planes run on the plane stream right after the extraction.  Two alternatives were
         # measured slower in round 2 and removed: opening the tracking tail with them (1.5 %,
         # profiles/r02/ab_supp_on_tail) and holding the next pyramid until they finish (5 %,
@@ -542,8 +567,9 @@ class HotPath:
     def _setup_native(self):
         import spslam_match as SM
         import spslam_step as SS
-        if self.n_lba or self.rotate_inputs:
-            raise ValueError("native step: no LocalMapping beside it and static inputs (use the Python step)")
+        if self.n_lba or self.rotate_inputs or self.lookahead != 1:
+            raise ValueError("native step: no LocalMapping beside it, static inputs and lookahead 1 (use the Python "
+                             "step)")
         cfg = SS.StepConfig(n_frames=self.B, width=self.W, height=self.H, kp_cap=self.kp_cap,
                             pipelined=int(self.pipelined), tail_priority=int(self.main.priority < 0),
                             orb_priority=int(getattr(self, "orb_priority", False)),
@@ -594,17 +620,28 @@ class HotPath:
             setattr(self, k, v)
 
     def _extract(self, j):
-        self._bind(j)
-        self.ext_orb.wait_event(self.ev_tail[j])
-        self._load(self.ext_orb)
-        self.grab(self.ext_orb.cuda_stream)
-        self.ev_grab[j].record(self.ext_orb)
-        self.ext_planes.wait_event(self.ev_grab[j])
-        self.pe.select_cloud_set(j)  # batch j's organized cloud (double-buffered like the other outputs)
-        self.planes(self.ext_planes.cuda_stream)
-        self.ev_planes[j].record(self.ext_planes)
-        self.orb(self.ext_orb.cuda_stream)
-        self.ev_orb[j].record(self.ext_orb)
+        """The next batch's extraction into buffer set j, on extraction unit (batch index) % lookahead."""
+        m = self.n_extracted
+        self.n_extracted += 1
+        u = self.ext_units[m % self.lookahead]
+        orb_s, planes_s = u["orb"], u["planes"]
+        main_units = self.ex, self.pe, self.grabber
+        self.ex, self.pe, self.grabber = u["ex"], u["pe"], u["grabber"]
+        try:
+            self._bind(j)
+            orb_s.wait_event(self.ev_tail[j])
+            self._load(orb_s)
+            self.grab(orb_s.cuda_stream)
+            self.ev_grab[j].record(orb_s)
+            planes_s.wait_event(self.ev_grab[j])
+            # the unit's organized cloud alternates between its two sets (double-buffered like the other outputs)
+            self.pe.select_cloud_set((m // self.lookahead) % 2)
+            self.planes(planes_s.cuda_stream)
+            self.ev_planes[j].record(planes_s)
+            self.orb(orb_s.cuda_stream)
+            self.ev_orb[j].record(orb_s)
+        finally:
+            self.ex, self.pe, self.grabber = main_units
 
     def _tail(self):
         self.frame()
@@ -630,14 +667,16 @@ class HotPath:
         self._lba_end()
 
     def _step_pipelined(self):
-        """One extraction (batch k+1) and one tracking tail (batch k) per step."""
-        if not self.primed:  # the first batch's extraction (warmup absorbs it)
-            self._extract(0)
+        """One extraction (batch k + lookahead) and one tracking tail (batch k) per step."""
+        n = self.lookahead + 1
+        if not self.primed:  # the first batches' extraction (warmup absorbs it)
+            for i in range(self.lookahead):
+                self._extract(i)
             self.primed = True
-        j = self.k % 2
+        j = self.k % n
         self.ev_fork.record(self.main)
         self._lba_begin()
-        self._extract(1 - j)
+        self._extract((self.k + self.lookahead) % n)
         self._bind(j)
         self.main.wait_event(self.ev_orb[j])
         self.main.wait_event(self.ev_planes[j])
@@ -706,4 +745,6 @@ class HotPath:
             self.lba_pool.shutdown()
             for sl in self.lba_slots:
                 sl["ex"].close()
+        for u in getattr(self, "ext_units", [])[1:]:
+            u["ex"].close()
         self.ex.close()

@@ -390,9 +390,9 @@ class SequencePath(pipeline.HotPath):
     def _load(self, stream):
         k = self.n_loaded
         self.n_loaded += 1
-        t = k + 1
-        if t >= self.T:
-            raise RuntimeError(f"sequence exhausted: {self.T} frames rendered")
+        # a pipelined step extracts up to `lookahead` frames ahead of tracking: past the last rendered frame it
+        # extracts that frame again (never tracked; _tail raises before tracking past the end)
+        t = min(k + 1, self.T - 1)
         torch = self.torch
         with torch.cuda.stream(stream):
             idx = torch.tensor([t * self.U + i % self.U for i in range(self.B)], dtype=torch.long, device="cuda")
@@ -408,6 +408,8 @@ class SequencePath(pipeline.HotPath):
     # ---- the tail with the sequence state
     def _tail(self):
         import spslam_track as ST
+        if self.n_tracked + 1 >= self.T:
+            raise RuntimeError(f"sequence exhausted: {self.T} frames rendered")
         self.track.batch_device(self.B, ST.MOTION_PRIOR, self._track_batch(0), stream=self.stream)
         super()._tail()
         nxt = self.proj_sets[1] if self.d_pframes.data_ptr() == self.proj_sets[0][0].data_ptr() else self.proj_sets[0]

@@ -28,8 +28,9 @@ def tracked():
     import sequence
     out = {}
     try:
-        for mode in (False, True):
-            sp = sequence.SequencePath(B, T, n_sequences=U, pipelined=mode, **pipeline.CONFIGS["c2"])
+        for mode in (False, True, 3):  # serial, pipelined (lookahead 1), pipelined with lookahead 3
+            sp = sequence.SequencePath(B, T, n_sequences=U, pipelined=bool(mode), lookahead=int(mode) or 1,
+                                       **pipeline.CONFIGS["c2"])
             out[mode] = (None, sp)
             for _ in range(T - 2):
                 sp.step()
@@ -64,9 +65,30 @@ def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None):
 
 
 def test_pipelined_equals_serial(tracked):
-    (ts, _), (tp, _) = tracked[False], tracked[True]
-    assert ts.shape == tp.shape == (T - 1, B, 4, 4)
+    (ts, _), (tp, _), (t3, _) = tracked[False], tracked[True], tracked[3]
+    assert ts.shape == tp.shape == t3.shape == (T - 1, B, 4, 4)
     assert ts.tobytes() == tp.tobytes()
+    assert ts.tobytes() == t3.tobytes()  # three batches extracted ahead, on two extraction units side by side
+    assert np.array_equal(tracked[False][1].history(), tracked[3][1].history())
+
+
+def test_single_sequence_lookahead_equals_serial():
+    """The reference's call pattern (B = 1): frames extracted two ahead of tracking on two extraction units
+    (bench.py single_sequence) track bit-identically to the serial step."""
+    import pipeline
+    import sequence
+    n, tr = 12, {}
+    for look in (0, 2):
+        sp = sequence.SequencePath(1, n + 4, n_sequences=1, pipelined=bool(look), lookahead=look or 1,
+                                   **pipeline.CONFIGS["c2"])
+        try:
+            for _ in range(n):
+                sp.step()
+            tr[look] = (sp.trajectory(), sp.history())
+        finally:
+            sp.close()
+    assert tr[0][0].tobytes() == tr[2][0].tobytes()
+    assert np.array_equal(tr[0][1], tr[2][1])
 
 
 def test_trajectory_matches_oracle(tracked):
