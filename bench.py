@@ -359,7 +359,8 @@ def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
     tracked sequence, one frame at a time (B = 1, sp-slam_amd/sequence.py; every frame's prior and last-frame
     points from its predecessor).  frames_per_s: frames k+1 .. k+L's grab / ORB / planes overlapped with frame k's
     tracking tail (the pipelined step, L = SINGLE_LOOKAHEAD frames read ahead as SPSLAM.cc's loop over the image list
-    allows; two extraction units side by side), host synchronised only at the end.  latency_ms_*: the serial step (grab ->
+    allows; two extraction units side by side), the host waiting for frame k-1's tail before it returns from frame
+    k (SINGLE_INFLIGHT).  latency_ms_*: the serial step (grab ->
     extraction -> tracking tail) with the host waiting for each frame's pose -- image on the device to pose on the
     device, the per-frame latency a TrackRGBD caller sees (the 64-byte pose read-back excluded)."""
     import numpy as np
@@ -367,10 +368,10 @@ def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
     import sequence
     look = SINGLE_LOOKAHEAD if lookahead is None else lookahead
     out = {"kind": "one sequence, B = 1 (sequence.SequencePath), frames device-resident", "frames": n_frames,
-           "lookahead": look}
+           "lookahead": look, "max_inflight": SINGLE_INFLIGHT}
     for pipelined in (True, False):
         sp = sequence.SequencePath(1, n_frames + warmup + 2, n_sequences=1, device=device, pipelined=pipelined,
-                                   lookahead=look if pipelined else 1,
+                                   lookahead=look if pipelined else 1, max_inflight=SINGLE_INFLIGHT,
                                    render_workers=min(16, os.cpu_count() or 1), **cfg)
         try:
             for _ in range(warmup):
@@ -517,7 +518,9 @@ def _ensure_hw_queues(want=None):
 
 
 LBA_DEPTH, LBA_TEAM = 2, 1  # C3 defaults (profiles/r05/ab_c3_*.txt)
-SINGLE_LOOKAHEAD = 3  # single_sequence: frames extracted ahead of tracking (profiles/r05/b1_lookahead.txt)
+# single_sequence: frames extracted ahead of tracking, and the host at most one step ahead of the device
+# (profiles/r05/b1_lookahead.txt, b1_inflight.txt)
+SINGLE_LOOKAHEAD, SINGLE_INFLIGHT = 2, 1
 
 
 def main():

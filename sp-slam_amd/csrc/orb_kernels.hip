@@ -591,7 +591,7 @@ struct OctShared {
     int seq[2][NC];
     uint8_t flags[2][NC];
     uint8_t div[NC];
-    int c4[NC][4];   // child counts, then child positions (-1 = empty)
+    alignas(8) int c4[NC][4];  // child counts, then child positions (-1 = empty); at the end the retained keys
     int sa[NC];      // scan scratch
     int sb[NC];      // scan scratch / remap
     int sc[NC];      // scan scratch / sort
@@ -648,12 +648,57 @@ __device__ __forceinline__ void child_rect(int q, int x0, int y0, int x1, int y1
     cy1 = (short)((q & 2) ? y1 : y0 + hy);
 }
 
+// Where the level's keys live between the passes.  A pass touches every key (its node, and for a divided node
+// its quadrant), and there are ~6-10 passes per level, so the keys stay on chip when they fit: RegKeys holds
+// KPT keys per thread in registers (key k = threadIdx.x + 256 j, its node index packed 4 per register);
+// GlobalKeys is the fallback for levels with more than 256 * KPT candidates (and for the 1024-node instance):
+// the keys gathered once into global scratch, their node indices beside them, a node index written only when
+// it changes.  Both visit every key once per call, in any order: the passes only count (LDS atomics) and
+// re-point keys, and the final retain orders by key index k.
+struct GlobalKeys {
+    const uint32_t* keys;
+    uint16_t* node;
+    int C;
+    template <class F>
+    __device__ __forceinline__ void each(F&& f) {
+        for (int k = threadIdx.x; k < C; k += 256) {
+            int n = node[k];
+            const int n0 = n;
+            f(keys[k], k, n);
+            if (n != n0) node[k] = (uint16_t)n;
+        }
+    }
+};
+
+template <int KPT>
+struct RegKeys {
+    uint32_t key[KPT];
+    uint32_t nodew[(KPT + 3) / 4];
+    int C;
+    template <class F>
+    __device__ __forceinline__ void each(F&& f) {
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < KPT; j++) {
+            const int k = t + 256 * j;
+            if (k >= C) break;
+            const int sh = 8 * (j & 3);
+            // opaque per visit: otherwise the compiler hoists each key's x / y fields (and unpacked node bytes)
+            // out of the pass loop, ~3 registers per key instead of 1.25
+            uint32_t kv = key[j];
+            asm volatile("" : "+v"(kv));
+            int n = (int)((nodew[j >> 2] >> sh) & 0xFFu);
+            f(kv, k, n);
+            nodew[j >> 2] = (nodew[j >> 2] & ~(0xFFu << sh)) | ((uint32_t)n << sh);
+        }
+    }
+};
+
 // Rebuild the list after dividing the nodes flagged in S.div (proc rank of a
 // divided node in S.sb[node] = position in division order, P_c prefix in
 // S.sa[node]).  T = number of children pushed.  Returns the new length.
-template <int NC>
-__device__ int rebuild_list(OctShared<NC>& S, int cur, int L, int T, int seqc, const uint32_t* keys, uint16_t* keynode,
-                            int C) {
+template <int NC, class KS>
+__device__ __forceinline__ int rebuild_list(OctShared<NC>& S, int cur, int L, int T, int seqc, KS& ks) {
     const int nb = cur ^ 1;
     // rank of non-divided nodes in list order
     for (int i = threadIdx.x; i < L; i += 256) S.sc[i] = S.div[i] ? 0 : 1;
@@ -690,63 +735,39 @@ __device__ int rebuild_list(OctShared<NC>& S, int cur, int L, int T, int seqc, c
         }
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < C; k += 256) {
-        const int n = keynode[k];
+    ks.each([&](uint32_t key, int, int& n) {
         if (S.div[n]) {
-            const uint32_t key = keys[k];
             const int q = quadrant(key & 0xFFF, (key >> 12) & 0xFFF, S.x0[cur][n], S.y0[cur][n], S.x1[cur][n],
                                    S.y1[cur][n]);
-            keynode[k] = (uint16_t)S.c4[n][q];
+            n = S.c4[n][q];
         } else {
-            keynode[k] = (uint16_t)S.sb[n];
+            n = S.sb[n];
         }
-    }
+    });
     __syncthreads();
     return T + ND;
 }
 
 // Count the four children of every node with S.div set.
-template <int NC>
-__device__ void count_children(OctShared<NC>& S, int cur, int L, const uint32_t* keys, const uint16_t* keynode, int C) {
+template <int NC, class KS>
+__device__ __forceinline__ void count_children(OctShared<NC>& S, int cur, int L, KS& ks) {
     for (int i = threadIdx.x; i < L; i += 256) S.c4[i][0] = S.c4[i][1] = S.c4[i][2] = S.c4[i][3] = 0;
     __syncthreads();
-    for (int k = threadIdx.x; k < C; k += 256) {
-        const int n = keynode[k];
+    ks.each([&](uint32_t key, int, int& n) {
         if (S.div[n]) {
-            const uint32_t key = keys[k];
             const int q = quadrant(key & 0xFFF, (key >> 12) & 0xFFF, S.x0[cur][n], S.y0[cur][n], S.x1[cur][n],
                                    S.y1[cur][n]);
             atomicAdd(&S.c4[n][q], 1);
         }
-    }
+    });
     __syncthreads();
 }
 
-template <int NC>
-__global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* __restrict__ cand,
-                                                     const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
-                                                     uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
-                                                     int* __restrict__ lvl_cnt, int l0) {  // levels l0 + blockIdx.x
-    __shared__ OctShared<NC> S;
-    const int l = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;
-    const LevelGeom& Lg = g.lv[l];
-    const int ncells = Lg.nRows * Lg.nCols;
-    uint32_t* keys = keys_all + (size_t)f * g.keys_per_frame + Lg.key_base;
-    uint16_t* keynode = keynode_all + (size_t)f * g.keys_per_frame + Lg.key_base;
-    const size_t cell0 = (size_t)f * g.cells_per_frame + Lg.cell_base;
-
-    // --- gather candidates in cell order (vToDistributeKeys, :818-826)
-    for (int c = t; c < ncells; c += 256) S.cellpre[c] = cand_cnt[cell0 + c];
-    __syncthreads();
-    const int C = block_scan(S.cellpre, ncells, S.wsum);
-    for (int c = t >> 6; c < ncells; c += 4) {
-        const int n = (int)cand_cnt[cell0 + c], o = S.cellpre[c];
-        const uint32_t* src = cand + (cell0 + c) * kCellCap;
-        for (int j = t & 63; j < n; j += 64) keys[o + j] = src[j];
-    }
-    __threadfence_block();
-    __syncthreads();
-
+// The level's tree from its keys (initial nodes, main-loop passes, final phase, retained keys).
+template <int NC, class KS>
+__device__ __forceinline__ void octree_body(OctShared<NC>& S, KS& ks, const LevelGeom& Lg, LevelKp* __restrict__ out,
+                                            int* __restrict__ out_cnt) {
+    const int t = threadIdx.x;
     // --- initial nodes (:542-585)
     const int minX = kMinBorder, maxX = Lg.maxBorderX, minY = kMinBorder, maxY = Lg.maxBorderY;
     const int nIni = (int)roundf((float)(maxX - minX) / (maxY - minY));
@@ -754,11 +775,10 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
     int cur = 0;
     if (t < 4 * nIni) S.sa[t] = 0;
     __syncthreads();
-    for (int k = t; k < C; k += 256) {
-        const int i = (int)((float)(keys[k] & 0xFFF) / hX);
-        keynode[k] = (uint16_t)i;
-        atomicAdd(&S.sa[i], 1);
-    }
+    ks.each([&](uint32_t key, int, int& n) {
+        n = (int)((float)(key & 0xFFF) / hX);
+        atomicAdd(&S.sa[n], 1);
+    });
     __syncthreads();
     if (t == 0) {
         int L = 0;
@@ -776,7 +796,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
     }
     __syncthreads();
     int L = S.misc[0];
-    for (int k = t; k < C; k += 256) keynode[k] = (uint16_t)S.sb[keynode[k]];
+    ks.each([&](uint32_t, int, int& n) { n = S.sb[n]; });
     __syncthreads();
     int seqc = nIni;
     const int N = Lg.nfeat;
@@ -787,7 +807,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
         const int prevSize = L;
         for (int i = t; i < L; i += 256) S.div[i] = (S.flags[cur][i] & kFlagNoMore) ? 0 : 1;
         __syncthreads();
-        count_children(S, cur, L, keys, keynode, C);
+        count_children(S, cur, L, ks);
         for (int i = t; i < L; i += 256) {
             int nc = 0, nm = 0;
             if (S.div[i])
@@ -798,7 +818,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
         __syncthreads();
         const int nToExpand = block_scan(S.sb, L, S.wsum);
         const int T = block_scan(S.sa, L, S.wsum);
-        L = rebuild_list(S, cur, L, T, seqc, keys, keynode, C);
+        L = rebuild_list(S, cur, L, T, seqc, ks);
         seqc += T;
         cur ^= 1;
         if (L >= N || L == prevSize) {
@@ -826,7 +846,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
                 }
                 for (int i = t; i < L; i += 256) S.div[i] = (S.flags[cur][i] & kFlagToExp) ? 1 : 0;
                 __syncthreads();
-                count_children(S, cur, L, keys, keynode, C);
+                count_children(S, cur, L, ks);
                 // deltas in processing order
                 for (int p = t; p < M; p += 256) {
                     const int i = S.sc[p];
@@ -857,7 +877,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
                 for (int i = t; i < L; i += 256)
                     if (S.div[i]) S.sa[i] = S.sb[i];
                 __syncthreads();
-                L = rebuild_list(S, cur, L, T2, seqc, keys, keynode, C);
+                L = rebuild_list(S, cur, L, T2, seqc, ks);
                 seqc += T2;
                 cur ^= 1;
                 if (L >= N || L == prev2) finish = true;
@@ -865,19 +885,20 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
         }
     }
 
-    // --- retain the best key of each node (:741-760): first max in key order
-    for (int i = t; i < L; i += 256) S.sa[i] = 0;
+    // --- retain the best key of each node (:741-760): the first maximum response in key order, i.e. the maximum
+    // of (response, -k); the key itself rides in the low word (the child-count table is free here)
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(&S.c4[0][0]);
+    for (int i = t; i < L; i += 256) best[i] = 0;
     __syncthreads();
-    for (int k = t; k < C; k += 256) {
-        const uint32_t key = keys[k];
-        atomicMax(&S.sa[keynode[k]], (int)(((key >> 24) << 23) | (0x7FFFFF - k)));
-    }
+    ks.each([&](uint32_t key, int k, int& n) {
+        const unsigned long long v = ((unsigned long long)(key >> 24) << 55) |
+                                     ((unsigned long long)(0x7FFFFF - k) << 32) | key;
+        atomicMax(&best[n], v);
+    });
     __syncthreads();
-    LevelKp* out = lvl_kp + (size_t)f * g.lvl_kp_per_frame + Lg.kp_base;
     const int nout = min(L, Lg.kp_cap);
     for (int i = t; i < nout; i += 256) {
-        const int k = 0x7FFFFF - (S.sa[i] & 0x7FFFFF);
-        const uint32_t key = keys[k];
+        const uint32_t key = (uint32_t)best[i];
         LevelKp kp;
         kp.x = (uint16_t)((key & 0xFFF) + minX);
         kp.y = (uint16_t)(((key >> 12) & 0xFFF) + minY);
@@ -885,7 +906,70 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
         kp.pad = 0;
         out[i] = kp;
     }
-    if (t == 0) lvl_cnt[f * kMaxLevels + l] = nout;
+    if (t == 0) *out_cnt = nout;
+}
+
+// Keys per thread held in registers (the 256-node instance): 40 covers the C2-C4 levels (level 0 of a
+// 640x480 frame has ~9K FAST candidates); a level with more keys takes the global path
+#ifndef SPSLAM_OCT_KPT
+#define SPSLAM_OCT_KPT 40
+#endif
+
+template <int NC, int KPT>
+__global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* __restrict__ cand,
+                                                     const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
+                                                     uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
+                                                     int* __restrict__ lvl_cnt, int l0) {  // levels l0 + blockIdx.x
+    __shared__ OctShared<NC> S;
+    const int l = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;
+    const LevelGeom& Lg = g.lv[l];
+    const int ncells = Lg.nRows * Lg.nCols;
+    const size_t cell0 = (size_t)f * g.cells_per_frame + Lg.cell_base;
+    LevelKp* out = lvl_kp + (size_t)f * g.lvl_kp_per_frame + Lg.kp_base;
+    int* out_cnt = lvl_cnt + f * kMaxLevels + l;
+
+    // --- candidates in cell order (vToDistributeKeys, :818-826): key k of the level = entry k - cellpre[c] of the
+    // cell c holding it
+    for (int c = t; c < ncells; c += 256) S.cellpre[c] = cand_cnt[cell0 + c];
+    __syncthreads();
+    const int C = block_scan(S.cellpre, ncells, S.wsum);
+    if constexpr (KPT > 0) {
+        static_assert(NC <= 256, "node indices are packed as bytes");
+        if (C <= 256 * KPT) {
+            RegKeys<KPT> ks;
+            ks.C = C;
+#pragma unroll
+            for (int j = 0; j < KPT; j++) {
+                const int k = t + 256 * j;
+                ks.key[j] = 0;
+                if (k < C) {  // the cell holding key k: the last c with cellpre[c] <= k (empty cells share prefixes)
+                    int lo = 0, hi = ncells - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (S.cellpre[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    ks.key[j] = cand[(cell0 + lo) * kCellCap + (k - S.cellpre[lo])];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < (KPT + 3) / 4; j++) ks.nodew[j] = 0;
+            octree_body(S, ks, Lg, out, out_cnt);
+            return;
+        }
+    }
+    GlobalKeys ks;
+    ks.keys = keys_all + (size_t)f * g.keys_per_frame + Lg.key_base;
+    ks.node = keynode_all + (size_t)f * g.keys_per_frame + Lg.key_base;
+    ks.C = C;
+    uint32_t* keys = keys_all + (size_t)f * g.keys_per_frame + Lg.key_base;
+    for (int c = t >> 6; c < ncells; c += 4) {
+        const int n = (int)cand_cnt[cell0 + c], o = S.cellpre[c];
+        const uint32_t* src = cand + (cell0 + c) * kCellCap;
+        for (int j = t & 63; j < n; j += 64) keys[o + j] = src[j];
+    }
+    __threadfence_block();
+    __syncthreads();
+    octree_body(S, ks, Lg, out, out_cnt);
 }
 
 // ---------------------------------------------------------------------------
@@ -1098,7 +1182,7 @@ hipError_t orb_launch(const OrbGeom& g, const OrbBuffers& b, int n, int iniTh, i
     if (g.nlevels - ls < 2) ls = g.nlevels;
     int maxcap = 0;
     for (int l = 0; l < g.nlevels; l++) maxcap = max(maxcap, g.lv[l].kp_cap);
-    auto* octree = maxcap <= 256 ? octree_kernel<256> : octree_kernel<kNodeCap>;
+    auto* octree = maxcap <= 256 ? octree_kernel<256, SPSLAM_OCT_KPT> : octree_kernel<kNodeCap, 0>;
     auto fast = [&](int la, int lb, hipStream_t st) {
         const int c0 = g.lv[la].cell_base, c1 = lb < g.nlevels ? g.lv[lb].cell_base : g.cells_per_frame;
         hipLaunchKernelGGL(fast_cells_kernel, dim3((c1 - c0 + 3) / 4, n), dim3(256), 0, st, g, b.cand, b.cand_cnt,

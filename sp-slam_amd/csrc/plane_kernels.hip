@@ -6,10 +6,11 @@
 //                          depth-change map + PCL's two-pass chamfer distance
 //                          transform, as two anti-diagonal wavefronts (one
 //                          lane per cloud row, slope 2): every cell sees
-//                          exactly the operands of the reference's raster scan;
-//                          PCL IntegralImage2D<float,3> of the x/y gradient
-//                          images (fp64, same recurrence order) rides along
-//                          in the first wavefront
+//                          exactly the operands of the reference's raster scan
+//                          (made from the raster cloud through per-row LDS
+//                          windows); PCL IntegralImage2D<float,3> of the x/y
+//                          gradient images (fp64, same recurrence order) rides
+//                          along in the first wavefront
 //   plane_normal_kernel    AVERAGE_3D_GRADIENT normals + flip to viewpoint,
 //                          plane_d = p . n (one thread per cloud point)
 //   plane_segment_kernel   (plane_segment.hip) connected components, models,
@@ -60,75 +61,35 @@ __device__ __forceinline__ float dist_init(ZAt z, int W, int H, int r, int c) {
 // across it (nothing another lane reads goes through global memory inside these kernels).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Pass-1 operands of every cell, written in the skewed layout (plane_launch.h) so the wavefront
-// kernel reads one step's operands with coalesced loads.  One workgroup per band of RB cloud rows:
-// the band (+1 row either side) is staged in LDS with coalesced row reads, then the band's skewed
-// entries are written step by step, RB consecutive rows = one contiguous run per step.
-template <int RB>
-__global__ __launch_bounds__(256) void plane_wave_prep_kernel(PlaneGeom g, const float* __restrict__ cloud,
-                                                              long long cloud_fs, float* wave, long long wave_fs) {
-    extern __shared__ float band[];  // [3][RB + 2][W]: x | y | z of rows rlo .. rhi-1
-    const int W = g.W, H = g.H, N = g.N;
-    const int SZ = (int)wave_size(W, H);
-    const int f = blockIdx.y, r0 = blockIdx.x * RB;
-    const int rlo = max(r0 - 1, 0), rhi = min(r0 + RB + 1, H), BP = (RB + 2) * W;
-    const float* X = cloud + f * cloud_fs;
-    for (int q = threadIdx.x; q < (rhi - rlo) * W; q += 256) {
-        const int i = rlo * W + q;
-        band[q] = X[i];
-        band[BP + q] = X[N + i];
-        band[2 * BP + q] = X[2 * N + i];
-    }
-    __syncthreads();
-    auto at = [&](int k, int r, int c) { return band[k * BP + (r - rlo) * W + c]; };
-    auto zat = [&](int r, int c) { return at(2, r, c); };
-    float* O = wave + f * wave_fs;
-    const int nst = 2 * (RB - 1) + W;  // steps that visit a cell of the band
-    for (int q = threadIdx.x; q < nst * RB; q += 256) {
-        const int j = q / RB, rr = q - j * RB;
-        const int r = r0 + rr, c = 2 * r0 + j - 2 * r;
-        if (r >= H || c < 0 || c >= W) continue;
-        float e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                e[k] = at(k, r, c + 1) - at(k, r, c - 1);
-                e[3 + k] = at(k, r + 1, c) - at(k, r - 1, c);
-            }
-        }
-        const int o = (int)wave_index(r, c, H);
-        O[o] = dist_init(zat, W, H, r, c);
-#pragma unroll
-        for (int k = 0; k < 6; k++) O[(k + 1) * SZ + o] = e[k];
-    }
-}
-
 // Depth-change distance map (PCL's two-pass chamfer transform) and the six fp64 integral images
 // (IntegralImage2D<float,3> of the x / y gradients) in one workgroup per frame.  Both are raster
 // recurrences replayed as anti-diagonal wavefronts, one lane per cloud row: the integral image's
 // recurrence (up, left, up-left) fits inside the distance pass 1 schedule (slope 2: row r-1 is two
 // columns ahead of row r), so both run in the same 2(H-1)+W barrier steps; a 4-column ring per row
-// holds what row r+1 still reads.  Pass 2 visits the cells in exactly the reverse order of pass 1, so
-// in the skewed layout both passes read and write one contiguous span per step.  Each lane loads the
-// operands of the next kWaveChunk steps while it works through the current ones (issued at the top of
-// the unrolled chunk, consumed at its bottom, so the compiler's wait covers only those loads, not the
-// stores in between); lanes outside the image compute on unused entries and keep their row state.
-// Every cell sees exactly the operands of the reference's raster scans: both outputs stay
-// bit-identical.
-template <int MAXR>
-__global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, const float* __restrict__ wave,
-                                                                   long long wave_fs, float* dist, long long dist_fs,
-                                                                   double* integral, long long integral_fs) {
-    constexpr int K = kWaveChunk;
-    // wave holds the 7 operand planes and, as plane 7, the skewed pass-1 distance map; the final
-    // distance map and the integral images are written in raster layout for the normal kernel
-    // slot-major rings: lane r touches consecutive LDS words
+// holds what row r+1 still reads.
+// Pass 1's operands (each cell's initial distance and its six central differences) are made on chip: per
+// chunk of K steps the workgroup stages, for every row, the K + 4 cloud columns that the chunk's cells of
+// rows r-1, r, r+1 read (row r-1 runs two columns ahead, row r+1 two behind) in an LDS window, loaded from
+// the raster cloud while the previous chunk's steps run, so the cloud is read from HBM once and nothing is
+// staged through HBM.  Pass 2 visits the cells in exactly the reverse order of pass 1, so in the skewed
+// layout both passes read and write one contiguous span per step (the only HBM round trip left: the pass-1
+// map, 4 + 4 bytes per cell).  Lanes outside the image compute on unused entries and keep their row state.
+// Every cell sees exactly the operands of the reference's raster scans: both outputs stay bit-identical.
+template <int MAXR, int K>
+__global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, const float* __restrict__ cloud,
+                                                                   long long cloud_fs, float* wave, long long wave_fs,
+                                                                   float* dist, long long dist_fs, double* integral,
+                                                                   long long integral_fs) {
+    static_assert(K <= kWaveChunk, "the skewed layout pads kWaveChunk steps of prefetch slack");
+    constexpr int WC = K + 4;  // window columns per row: c - 2 .. c + K + 1 around the chunk's first column c
+    // slot-major: lane r touches consecutive LDS words
     __shared__ float ring[4][MAXR];
     __shared__ double iring[4][6][MAXR];
-    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, HP = wave_pitch(H), SK = wave_steps(W, H);
-    const int SZ = (int)wave_size(W, H);  // per-frame offsets fit in 32 bits (planes: 8 x SZ)
-    const float* In = wave + f * wave_fs + r;
-    float* D = const_cast<float*>(In) + 7 * SZ;  // skewed pass-1 distance map (this lane's column)
+    constexpr int WP = WC + 1;  // odd row pitch: the rows' reads of one column spread over the banks
+    __shared__ float win[3][MAXR][WP];
+    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, N = g.N, HP = wave_pitch(H), SK = wave_steps(W, H);
+    const float* X = cloud + f * cloud_fs;
+    float* D = wave + f * wave_fs + r;  // skewed pass-1 distance map (this lane's column)
     float* Dout = dist + f * dist_fs + (long long)r * W;  // raster row r
     const int IW = W + 1;
     double* Iraw = integral + f * integral_fs;
@@ -142,21 +103,53 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     const bool row_ok = r < H;
     const int rm = r > 0 ? r - 1 : 0, rp = r + 1 < MAXR ? r + 1 : r;  // neighbour rows (reads masked below)
     struct Cell { float center, e[6]; };
-    // steps where this lane has no cell read a fixed entry instead (an address select, not a branch:
-    // no HBM traffic for the skewed layout's empty entries, and the prefetch waits stay exact)
-    auto load = [&](int st) {
-        Cell o;
-        const int c = st - 2 * r;
-        const int t = ((row_ok && c >= 0 && c < W ? st : 0) + K) * HP;
-        o.center = In[t];
+    // the windows of the chunk starting at step s0: row rr, columns s0 - 2rr - 2 + i (clamped; the clamped
+    // entries feed only cells outside the cloud).  Loaded by the whole workgroup with the window's columns
+    // across consecutive lanes (a 64-lane load touches ~6 rows, not 64), held in registers while the previous
+    // chunk's steps run, then stored to LDS.
+    const int nthr = blockDim.x;
+    float wn[3][WC];
+    auto wload = [&](int s0) {
 #pragma unroll
-        for (int k = 0; k < 6; k++) o.e[k] = In[(k + 1) * SZ + t];
+        for (int m = 0; m < WC; m++) {
+            const int q = r + m * nthr, rr = q / WC, i = q - rr * WC;
+            const int ro = min(rr, H - 1), c = min(max(s0 - 2 * rr - 2 + i, 0), W - 1);
+            const float* p = X + (size_t)ro * W + c;
+#pragma unroll
+            for (int k = 0; k < 3; k++) wn[k][m] = p[(size_t)k * N];
+        }
+    };
+    auto wstore = [&]() {
+#pragma unroll
+        for (int m = 0; m < WC; m++) {
+            const int q = r + m * nthr, rr = q / WC, i = q - rr * WC;
+            if (rr < H)
+#pragma unroll
+                for (int k = 0; k < 3; k++) win[k][rr][i] = wn[k][m];
+        }
+    };
+    // cell (r, c = s0 + j - 2r): the wave_prep operands, from the windows of rows r-1, r, r+1
+    auto cell = [&](int s0, int j) {
+        const int c = s0 + j - 2 * r;
+        auto at = [&](int k, int rr, int cc) { return win[k][rr][cc - s0 + 2 * rr + 2]; };
+        Cell o;
+        o.center = dist_init([&](int rr, int cc) { return at(2, rr, cc); }, W, H, r, c);
+#pragma unroll
+        for (int k = 0; k < 6; k++) o.e[k] = 0.f;
+        if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                o.e[k] = at(k, r, c + 1) - at(k, r, c - 1);
+                o.e[3 + k] = at(k, r + 1, c) - at(k, r - 1, c);
+            }
+        }
         return o;
     };
     // pass 1 (top-left to bottom-right), step s handles column c = s - 2r of row r
     float left = 0.f;
     double ileft[6] = {0, 0, 0, 0, 0, 0};
-    const float row0 = row_ok ? In[(2 * r + K) * HP] : 0.f;  // initial value of (r, 0)
+    // initial value of (r, 0), which the last column's up-right read sees
+    const float row0 = row_ok ? dist_init([&](int rr, int cc) { return X[2 * N + rr * W + cc]; }, W, H, r, 0) : 0.f;
     auto step1 = [&](int s, const Cell& q) {
         const int c = s - 2 * r;
         const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
@@ -171,7 +164,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             left = v;
         }
-        D[(s + K) * HP] = v;
+        D[(s + kWaveChunk) * HP] = v;
         double iv[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
@@ -191,26 +184,27 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             out[2] = make_double2(iv[4], iv[5]);
         }
     };
-    Cell cur[K];
-#pragma unroll
-    for (int j = 0; j < K; j++) cur[j] = load(j);
+    wload(0);
+    wstore();
+    __syncthreads();
     for (int s0 = 0; s0 < SK; s0 += K) {
-        Cell nxt[K];
+        Cell cur[K];
 #pragma unroll
-        for (int j = 0; j < K; j++) nxt[j] = load(s0 + K + j);
+        for (int j = 0; j < K; j++) cur[j] = cell(s0, j);
+        wload(s0 + K);  // in flight during the chunk's steps; the window is dead once every lane has its cells
 #pragma unroll
         for (int j = 0; j < K; j++) {
             step1(s0 + j, cur[j]);
             lds_barrier();
         }
-#pragma unroll
-        for (int j = 0; j < K; j++) cur[j] = nxt[j];
+        wstore();
+        lds_barrier();
     }
     // pass 2 (bottom-right to top-left): iteration j visits the cells pass 1 visited at step SK-1-j
     // (column c = W-1 - (s - 2(H-1-r)) of the reference's order, shifted by the padded steps); each lane
     // reads back only the values it wrote itself
     float right = 0.f;
-    const float lastcol = row_ok ? D[(W - 1 + 2 * r + K) * HP] : 0.f;
+    const float lastcol = row_ok ? D[(W - 1 + 2 * r + kWaveChunk) * HP] : 0.f;
     auto step2 = [&](int j, float center) {
         const int st = SK - 1 - j, c = st - 2 * r;
         const bool ok = row_ok && c >= 0 && c < W, inner = r < H - 1 && c < W - 1;
@@ -225,26 +219,27 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             right = v;
         }
-        *(ok ? Dout + c : D + (st + K) * HP) = v;  // outside the cloud: this lane's consumed entry
+        *(ok ? Dout + c : D + (st + kWaveChunk) * HP) = v;  // outside the cloud: this lane's consumed entry
     };
     auto dval = [&](int j) {
         const int st = SK - 1 - j, c = st - 2 * r;
-        return D[((row_ok && c >= 0 && c < W ? st : 0) + K) * HP];
+        return D[((row_ok && c >= 0 && c < W ? st : 0) + kWaveChunk) * HP];
     };
-    float dcur[K];
+    constexpr int K2 = kWaveChunk;
+    float dcur[K2];
 #pragma unroll
-    for (int j = 0; j < K; j++) dcur[j] = dval(j);
-    for (int j0 = 0; j0 < SK; j0 += K) {
-        float dnxt[K];
+    for (int j = 0; j < K2; j++) dcur[j] = dval(j);
+    for (int j0 = 0; j0 < SK; j0 += K2) {
+        float dnxt[K2];
 #pragma unroll
-        for (int j = 0; j < K; j++) dnxt[j] = dval(j0 + K + j);
+        for (int j = 0; j < K2; j++) dnxt[j] = dval(j0 + K2 + j);
 #pragma unroll
-        for (int j = 0; j < K; j++) {
+        for (int j = 0; j < K2; j++) {
             step2(j0 + j, dcur[j]);
             lds_barrier();
         }
 #pragma unroll
-        for (int j = 0; j < K; j++) dcur[j] = dnxt[j];
+        for (int j = 0; j < K2; j++) dcur[j] = dnxt[j];
     }
 }
 
@@ -310,16 +305,12 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
     E(kKindPlaneCloud);
     B(kKindPlaneDist);
     {
-        // 16-row bands while the staged band fits 64 KB of LDS, else 8-row bands
-        const int rb = 3 * 18 * g.W * 4 <= 65536 ? 16 : 8;
-        const size_t lds = (size_t)3 * (rb + 2) * g.W * 4;
-        hipLaunchKernelGGL(rb == 16 ? plane_wave_prep_kernel<16> : plane_wave_prep_kernel<8>,
-                           dim3((g.H + rb - 1) / rb, n), dim3(256), lds, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs);
         const int rows = wave_pitch(g.H);
-        auto* k = g.H <= 192 ? plane_dist_integral_kernel<192>
-                             : g.H <= 320 ? plane_dist_integral_kernel<320> : plane_dist_integral_kernel<kWaveThreads>;
-        hipLaunchKernelGGL(k, dim3(n), dim3(rows), 0, s, g, b.wave, b.wave_fs, b.dist, b.dist_fs, b.integral,
-                           b.integral_fs);
+        auto* k = g.H <= 192   ? plane_dist_integral_kernel<192, kWaveChunk>
+                  : g.H <= 320 ? plane_dist_integral_kernel<320, kWaveChunk>
+                               : plane_dist_integral_kernel<kWaveThreads, kWaveChunk / 2>;  // (LDS: 155 KB)
+        hipLaunchKernelGGL(k, dim3(n), dim3(rows), 0, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs, b.dist, b.dist_fs,
+                           b.integral, b.integral_fs);
     }
     E(kKindPlaneDist);
     B(kKindPlaneNormal);

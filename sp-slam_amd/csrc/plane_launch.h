@@ -25,9 +25,8 @@ struct PlaneGeom {
 // Per-frame scratch, frame f at base + f * stride (element counts).
 struct PlaneBuffers {
     float* cloud;        // [F][3][N]  x | y | z planes
-    // wave: the wavefront kernel's skewed buffers (wave_index: one step's cells are contiguous),
-    // 7 pass-1 operand planes (initial distance, x / y gradients of xyz) + the pass-1 distance map
-    float* wave;         // [F][8][wave_size]
+    // wave: the wavefront kernel's skewed pass-1 distance map (wave_index: one step's cells are contiguous)
+    float* wave;         // [F][wave_size]
     float* dist;         // [F][N]  distance map
     double* integral;    // [F][(W+1)*(H+2)][6]  (dx xyz, dy xyz); row H+1 absorbs padding lanes
     float* normal;       // [F][3][N]

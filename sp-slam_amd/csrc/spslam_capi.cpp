@@ -634,7 +634,7 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     const long long N = g.N, F = c->p.max_batch, IWH = (long long)(g.W + 1) * (g.H + 1);
     PlaneBuffers& b = c->pb;
     const long long SH = wave_size(g.W, g.H);
-    b.cloud_fs = 3 * N; b.wave_fs = 8 * SH; b.dist_fs = N; b.integral_fs = 6 * (IWH + g.W + 1); b.normal_fs = 3 * N; b.pd_fs = N;
+    b.cloud_fs = 3 * N; b.wave_fs = SH; b.dist_fs = N; b.integral_fs = 6 * (IWH + g.W + 1); b.normal_fs = 3 * N; b.pd_fs = N;
     b.labels_fs = N; b.work_fs = 4 * N; b.grown_fs = N; b.maps_fs = 2 * N;
     const size_t bytes = F * (sizeof(float) * (2 * b.cloud_fs + b.wave_fs + b.dist_fs + b.normal_fs + b.pd_fs) +
                               sizeof(double) * b.integral_fs + sizeof(uint32_t) * b.labels_fs +

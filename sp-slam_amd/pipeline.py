@@ -31,6 +31,8 @@ step.
 from __future__ import annotations
 
 
+import os
+
 import numpy as np
 
 import spslam_frame
@@ -63,13 +65,16 @@ class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
-                 rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1):
+                 rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1,
+                 max_inflight=0):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
         self.nfeatures = nfeatures
-        # pipelined: batches extracted ahead of the tracking tail (1: batch k+1 beside batch k's tail)
+        # pipelined: batches extracted ahead of the tracking tail (1: batch k+1 beside batch k's tail) and the
+        # steps the host may run ahead of the device (0: unbounded)
         self.lookahead = max(1, int(lookahead))
+        self.max_inflight = int(max_inflight)
         self.device = device
         self.lba_order = lba_order  # spslam_lba.G2O_ORDER (default) / FAST_ORDER
         s = width / 640.0
@@ -552,6 +557,8 @@ class HotPath:
         self.ev_tail = [torch.cuda.Event() for _ in range(n)]
         self.ev_grab = [torch.cuda.Event() for _ in range(n)]
         self.n_extracted = 0
+        self.max_inflight = int(os.environ.get("SPSLAM_MAX_INFLIGHT", self.max_inflight))
+        self.ev_inflight = [torch.cuda.Event() for _ in range(max(1, self.max_inflight))]
         # The supposed planes run on the plane stream right after the extraction.  Two alternatives were
         # measured slower in round 2 and removed: opening the tracking tail with them (1.5 %,
         # profiles/r02/ab_supp_on_tail) and holding the next pyramid until they finish (5 %,
@@ -683,7 +690,19 @@ class HotPath:
         self._tail()
         self.ev_tail[j].record(self.main)
         self._lba_end()
+        self._throttle()
         self.k += 1
+
+    def _throttle(self):
+        """Host-side bound on the steps in flight: wait for the tail of step k - max_inflight before returning
+        from step k.  Unbounded, the host runs hundreds of steps ahead and every extraction stream fills with
+        packets waiting on tail events; at B = 1 that costs ~20 % (profiles/r05/b1_inflight.txt)."""
+        if not self.max_inflight:
+            return
+        ev = self.ev_inflight[self.k % self.max_inflight]
+        if self.k >= self.max_inflight:
+            ev.synchronize()
+        ev.record(self.main)
 
     def _lba_begin(self):
         if self.n_lba:

@@ -87,6 +87,7 @@ class SequencePath(pipeline.HotPath):
         config asks for LocalBundleAdjustment (C3's lba_every), off otherwise."""
         self.T = n_frames
         self.U = min(n_sequences or B, B)
+        self.d_load_idx = None
         self.render_workers = render_workers
         self.n_boxes = kw.get("n_boxes", 3)
         lba_every = kw.pop("lba_every", 0)  # the side-by-side synthetic local maps of the open-loop HotPath
@@ -107,6 +108,9 @@ class SequencePath(pipeline.HotPath):
         self.frames = [(SEQ_STRIDE * u, self.seq_frames[u][0][0], self.seq_frames[u][0][1], None) for u in range(U)]
         self.d_rgb = self.d_rgb_all[[U + i % U for i in range(B)]].clone()   # frame 1 (batch 0)
         self.d_depth_raw = self.d_depth_all[[U + i % U for i in range(B)]].clone()
+        if B > U:
+            self.d_load_idx = torch.tensor([[t * U + i % U for i in range(B)] for t in range(T)], dtype=torch.long,
+                                           device="cuda")
 
     def _true_pose(self, u, t):
         return np.linalg.inv(self.scene.pose(SEQ_STRIDE * u + t))
@@ -395,10 +399,14 @@ class SequencePath(pipeline.HotPath):
         t = min(k + 1, self.T - 1)
         torch = self.torch
         with torch.cuda.stream(stream):
-            idx = torch.tensor([t * self.U + i % self.U for i in range(self.B)], dtype=torch.long, device="cuda")
-            idx.record_stream(stream)
-            self.d_rgb.copy_(self.d_rgb_all.index_select(0, idx))
-            self.d_depth_raw.copy_(self.d_depth_all.index_select(0, idx))
+            if self.B <= self.U:  # slot i = sequence i: frame t of the slots is contiguous
+                a, b = t * self.U, t * self.U + self.B
+                self.d_rgb.copy_(self.d_rgb_all[a:b])
+                self.d_depth_raw.copy_(self.d_depth_all[a:b])
+            else:  # (rows built once in _setup_inputs: a host list -> device tensor per call costs ~1 ms)
+                idx = self.d_load_idx[t]
+                self.d_rgb.copy_(self.d_rgb_all.index_select(0, idx))
+                self.d_depth_raw.copy_(self.d_depth_all.index_select(0, idx))
             self.d_lframes.copy_(self.d_local_table[t])
 
     def _setup_pipeline(self):

@@ -14,7 +14,7 @@ import pipeline  # noqa: E402
 
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
-    hp = pipeline.HotPath(B)
+    hp = pipeline.HotPath(B, **pipeline.CONFIGS["c2"])
     for _ in range(2):
         hp.orb()
     torch.cuda.synchronize()
