@@ -114,7 +114,8 @@ def algorithmic_bytes(cfg, n_kp, n_pts, n_pls, n_con=0, n_brd=0, n_sup=0, lba_by
         "desc_kernel": n_kp * (2 * 31 * 31 + 28 + 32),
         "pose_kernel": (n_pts * 32 + n_pls * 48 + 80) / 2,    # observations in + result out, per call
         "plane_cloud_kernel": 4 * N + 12 * N,                 # depth samples in, xyz out
-        # xyz in, distance map + 6 fp64 integral images out (one fused wavefront kernel)
+        # depth samples in (their lines: 12 B per cell at Cloud.Dis 3, as the cloud's x / y / z), distance map
+        # + 6 fp64 integral images out (one wavefront kernel)
         "plane_dist_integral_kernel": 12 * N + 4 * N + 48 * IWH,
         "plane_normal_kernel": 16 * N + 48 * IWH + 16 * N,    # xyz+dist, integral, normal+plane_d out
         "plane_segment_kernel": 28 * N + 4 * N,               # xyz+normal+plane_d in, labels out
@@ -536,9 +537,10 @@ def main():
                     help="timed one-core CPU baseline frames (default 300; 100 above 640x480)")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
     ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
-    ap.add_argument("--no-planes-priority", action="store_true",
-                    help="next batch's plane stream at normal priority (default high: 1 %% faster step, "
-                         "profiles/r03/ab_prio_*)")
+    ap.add_argument("--planes-priority", action="store_true",
+                    help="next batch's plane stream at high priority (round 3's default; with the round-5 plane "
+                         "wavefront 1.5 %% slower, profiles/r05/ab_octree_planes_pose.txt)")
+    ap.add_argument("--no-planes-priority", action="store_true", help=argparse.SUPPRESS)  # (the default now)
     ap.add_argument("--lba-order", default="g2o", choices=("g2o", "fast"),
                     help="LocalBundleAdjustment summation order (C3): g2o = the reference's arithmetic, bit-exact "
                          "to the oracle (default); fast = the phase kernels (tree / matrix-core order)")
@@ -594,7 +596,7 @@ def main():
 
     hp = pipeline.HotPath(args.batch, unique_frames=args.unique_frames, device=local,
                           pipelined=not args.no_pipeline, tail_priority=not args.no_tail_priority,
-                          orb_priority=args.orb_priority, planes_priority=not args.no_planes_priority,
+                          orb_priority=args.orb_priority, planes_priority=args.planes_priority,
                           lba_order=0 if args.lba_order == "g2o" else 1,
                           native=not args.python_step and not cfg.get("lba_every"), **cfg,
                           lba_depth=LBA_DEPTH if args.lba_depth is None else args.lba_depth,

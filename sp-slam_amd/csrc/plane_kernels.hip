@@ -69,17 +69,17 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // holds what row r+1 still reads.
 // Pass 1's operands (each cell's initial distance and its six central differences) are made on chip: per
 // chunk of K steps the workgroup stages, for every row, the K + 4 cloud columns that the chunk's cells of
-// rows r-1, r, r+1 read (row r-1 runs two columns ahead, row r+1 two behind) in an LDS window, loaded from
-// the raster cloud while the previous chunk's steps run, so the cloud is read from HBM once and nothing is
-// staged through HBM.  Pass 2 visits the cells in exactly the reverse order of pass 1, so in the skewed
+// rows r-1, r, r+1 read (row r-1 runs two columns ahead, row r+1 two behind) in an LDS window, made from the
+// depth image's samples (loaded while the previous chunk's steps run) exactly as plane_cloud_kernel makes the
+// cloud: nothing is staged through HBM.  Pass 2 visits the cells in exactly the reverse order of pass 1, so in the skewed
 // layout both passes read and write one contiguous span per step (the only HBM round trip left: the pass-1
 // map, 4 + 4 bytes per cell).  Lanes outside the image compute on unused entries and keep their row state.
 // Every cell sees exactly the operands of the reference's raster scans: both outputs stay bit-identical.
 template <int MAXR, int K>
-__global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, const float* __restrict__ cloud,
-                                                                   long long cloud_fs, float* wave, long long wave_fs,
-                                                                   float* dist, long long dist_fs, double* integral,
-                                                                   long long integral_fs) {
+__global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, const float* __restrict__ depth,
+                                                                   long long depth_fs, int depth_stride, float* wave,
+                                                                   long long wave_fs, float* dist, long long dist_fs,
+                                                                   double* integral, long long integral_fs) {
     static_assert(K <= kWaveChunk, "the skewed layout pads kWaveChunk steps of prefetch slack");
     constexpr int WC = K + 4;  // window columns per row: c - 2 .. c + K + 1 around the chunk's first column c
     // slot-major: lane r touches consecutive LDS words
@@ -87,9 +87,15 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     __shared__ double iring[4][6][MAXR];
     constexpr int WP = WC + 1;  // odd row pitch: the rows' reads of one column spread over the banks
     __shared__ float win[3][MAXR][WP];
-    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, N = g.N, HP = wave_pitch(H), SK = wave_steps(W, H);
-    const float* X = cloud + f * cloud_fs;
+    const int f = blockIdx.x, r = threadIdx.x, W = g.W, H = g.H, HP = wave_pitch(H), SK = wave_steps(W, H);
+    const float* Z = depth + f * depth_fs;
+    // the organized cloud's point (rr, c) from the depth image, as plane_cloud_kernel makes it (same float
+    // operations, so the same values)
+    auto zof = [&](int rr, int c) { return Z[(long long)(rr * g.ds) * depth_stride + c * g.ds]; };
     float* D = wave + f * wave_fs + r;  // skewed pass-1 distance map (this lane's column)
+    // stores of steps where this lane has no cell: one word of the layout's unused leading slack per lane (an
+    // address select, not a branch; the line stays in L2 instead of every skewed entry reaching HBM)
+    float* Dsink = D;
     float* Dout = dist + f * dist_fs + (long long)r * W;  // raster row r
     const int IW = W + 1;
     double* Iraw = integral + f * integral_fs;
@@ -105,27 +111,37 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     struct Cell { float center, e[6]; };
     // the windows of the chunk starting at step s0: row rr, columns s0 - 2rr - 2 + i (clamped; the clamped
     // entries feed only cells outside the cloud).  Loaded by the whole workgroup with the window's columns
-    // across consecutive lanes (a 64-lane load touches ~6 rows, not 64), held in registers while the previous
-    // chunk's steps run, then stored to LDS.
+    // across consecutive lanes (a 64-lane load touches ~6 rows, not 64), straight from the depth image (one
+    // plane instead of the cloud's three), held in registers while the previous chunk's steps run, then
+    // expanded to x / y / z and stored to LDS.
     const int nthr = blockDim.x;
-    float wn[3][WC];
+    float wz[WC];
+    auto wcell = [&](int s0, int m, int& rr, int& i, int& ro, int& c) {
+        const int q = r + m * nthr;
+        rr = q / WC;
+        i = q - rr * WC;
+        ro = min(rr, H - 1);
+        c = min(max(s0 - 2 * rr - 2 + i, 0), W - 1);
+    };
     auto wload = [&](int s0) {
 #pragma unroll
         for (int m = 0; m < WC; m++) {
-            const int q = r + m * nthr, rr = q / WC, i = q - rr * WC;
-            const int ro = min(rr, H - 1), c = min(max(s0 - 2 * rr - 2 + i, 0), W - 1);
-            const float* p = X + (size_t)ro * W + c;
-#pragma unroll
-            for (int k = 0; k < 3; k++) wn[k][m] = p[(size_t)k * N];
+            int rr, i, ro, c;
+            wcell(s0, m, rr, i, ro, c);
+            wz[m] = zof(ro, c);
         }
     };
-    auto wstore = [&]() {
+    auto wstore = [&](int s0) {
 #pragma unroll
         for (int m = 0; m < WC; m++) {
-            const int q = r + m * nthr, rr = q / WC, i = q - rr * WC;
-            if (rr < H)
-#pragma unroll
-                for (int k = 0; k < 3; k++) win[k][rr][i] = wn[k][m];
+            int rr, i, ro, c;
+            wcell(s0, m, rr, i, ro, c);
+            if (rr < H) {
+                const float z = wz[m];
+                win[0][rr][i] = ((float)(c * g.ds) - g.cx) * z / g.fx;
+                win[1][rr][i] = ((float)(ro * g.ds) - g.cy) * z / g.fy;
+                win[2][rr][i] = z;
+            }
         }
     };
     // cell (r, c = s0 + j - 2r): the wave_prep operands, from the windows of rows r-1, r, r+1
@@ -149,7 +165,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     float left = 0.f;
     double ileft[6] = {0, 0, 0, 0, 0, 0};
     // initial value of (r, 0), which the last column's up-right read sees
-    const float row0 = row_ok ? dist_init([&](int rr, int cc) { return X[2 * N + rr * W + cc]; }, W, H, r, 0) : 0.f;
+    const float row0 = row_ok ? dist_init(zof, W, H, r, 0) : 0.f;
     auto step1 = [&](int s, const Cell& q) {
         const int c = s - 2 * r;
         const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
@@ -164,7 +180,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             left = v;
         }
-        D[(s + kWaveChunk) * HP] = v;
+        *(ok ? D + (s + kWaveChunk) * HP : Dsink) = v;  // entries outside the cloud are never read back
         double iv[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) {
@@ -185,7 +201,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
         }
     };
     wload(0);
-    wstore();
+    wstore(0);
     __syncthreads();
     for (int s0 = 0; s0 < SK; s0 += K) {
         Cell cur[K];
@@ -197,7 +213,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             step1(s0 + j, cur[j]);
             lds_barrier();
         }
-        wstore();
+        wstore(s0 + K);
         lds_barrier();
     }
     // pass 2 (bottom-right to top-left): iteration j visits the cells pass 1 visited at step SK-1-j
@@ -219,7 +235,7 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
             ring[c & 3][r] = v;
             right = v;
         }
-        *(ok ? Dout + c : D + (st + kWaveChunk) * HP) = v;  // outside the cloud: this lane's consumed entry
+        *(ok ? Dout + c : Dsink) = v;
     };
     auto dval = [&](int j) {
         const int st = SK - 1 - j, c = st - 2 * r;
@@ -309,8 +325,8 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
         auto* k = g.H <= 192   ? plane_dist_integral_kernel<192, kWaveChunk>
                   : g.H <= 320 ? plane_dist_integral_kernel<320, kWaveChunk>
                                : plane_dist_integral_kernel<kWaveThreads, kWaveChunk / 2>;  // (LDS: 155 KB)
-        hipLaunchKernelGGL(k, dim3(n), dim3(rows), 0, s, g, b.cloud, b.cloud_fs, b.wave, b.wave_fs, b.dist, b.dist_fs,
-                           b.integral, b.integral_fs);
+        hipLaunchKernelGGL(k, dim3(n), dim3(rows), 0, s, g, depth, depth_fs, depth_stride, b.wave, b.wave_fs, b.dist,
+                           b.dist_fs, b.integral, b.integral_fs);
     }
     E(kKindPlaneDist);
     B(kKindPlaneNormal);

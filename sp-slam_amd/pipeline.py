@@ -64,7 +64,7 @@ def _ptr(t):
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
-                 pipelined=False, tail_priority=True, orb_priority=False, planes_priority=True, min_size=500, chi=300.0, vp_chi=300.0,
+                 pipelined=False, tail_priority=True, orb_priority=False, planes_priority=False, min_size=500, chi=300.0, vp_chi=300.0,
                  rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1,
                  max_inflight=0):
         import torch

@@ -1,0 +1,10 @@
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd ${GRAFT_REPO_ROOT:-.}
+bash tools/pmc_round.sh c2 r5 || exit 1
+B="python bench.py --config c2 --steps 60 --warmup 5 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0"
+for r in 1 2 3; do
+  timeout -k 10 300 $B > gpurun_out/p3_new_def_$r.json 2>/dev/null || exit 1
+  timeout -k 10 300 $B --no-planes-priority > gpurun_out/p3_new_none_$r.json 2>/dev/null || exit 1
+  SPSLAM_GPU_LIB=sp-slam_amd/libspslam_gpu_base.so timeout -k 10 300 $B > gpurun_out/p3_base_def_$r.json 2>/dev/null || exit 1
+done

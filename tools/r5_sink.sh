@@ -1,0 +1,10 @@
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+cd ${GRAFT_REPO_ROOT:-.}
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_planes.py > gpurun_out/depth_tests.log 2>&1 || exit 1
+bash tools/pmc_round.sh c2 r5d || exit 1
+B="python bench.py --config c2 --steps 60 --warmup 5 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0"
+for r in 1 2; do
+  timeout -k 10 300 $B --no-planes-priority > gpurun_out/depth_new_none_$r.json 2>/dev/null || exit 1
+  timeout -k 10 300 $B > gpurun_out/depth_new_def_$r.json 2>/dev/null || exit 1
+done
