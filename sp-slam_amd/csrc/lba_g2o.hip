@@ -1612,6 +1612,9 @@ __device__ __noinline__ void build_system() {
     __syncthreads();
     const int nst = *NST;
     edge_rec(edge_of(0));
+#ifdef SPSLAM_LBG_DIAG_BUILD
+    long long db1 = 0, db2 = 0, db3 = 0;
+#endif
     for (int st = 0; st < nst; st++) {
         const int c0 = e0 + st * kCh;
         const int cnt = max(0, min(kCh, e1 - c0));
@@ -1659,6 +1662,11 @@ __device__ __noinline__ void build_system() {
             if (c0 + end_row != sg.z) g.lm_amask[own_h] = touched;
             if (again) NSW[kW] = 1;
         }
+#ifdef SPSLAM_LBG_DIAG_BUILD
+        __syncthreads();
+        db1 = wall_clock64();
+        if (t == 0) s.dg[0] += db1 - tb0;  // segment heads (Hpl kinds, lm_amask)
+#endif
         // (A) every row's terms (the plane edges' Jacobians from plane_jacobians)
         {
             const int e = ne;
@@ -1690,6 +1698,9 @@ __device__ __noinline__ void build_system() {
         __syncthreads();
         const long long tb1 = wall_clock64();
         tA += tb1 - tb0;
+#ifdef SPSLAM_LBG_DIAG_BUILD
+        if (t == 0) s.dg[1] += tb1 - db1;  // (A) terms
+#endif
         edge_rec(edge_of(st + 1));  // the next step's records land during (B)
         // (B) landmark segment chains: Hll (9) and bl (3) in edge order, four rows' loads in flight
         {
@@ -1722,6 +1733,11 @@ __device__ __noinline__ void build_system() {
                 *dst = a;
                 if ((fl >> 31) && (comp == 0 || comp == 4 || comp == 8)) mx = fmax(mx, fabs(a));
             }
+#ifdef SPSLAM_LBG_DIAG_BUILD
+            __syncthreads();
+            db2 = wall_clock64();
+            if (t == 0) s.dg[2] += db2 - tb1;  // landmark chains
+#endif
             // each block's first term: 0 + term (one entry per task)
             for (int i = t; i < 18 * cnt; i += kT) {
                 const int r = i / 18, c = i - 18 * r;
@@ -1740,6 +1756,11 @@ __device__ __noinline__ void build_system() {
                 }
             }
         }
+#ifdef SPSLAM_LBG_DIAG_BUILD
+        __syncthreads();
+        db3 = wall_clock64();
+        if (t == 0) s.dg[3] += db3 - db2;  // Hpl blocks
+#endif
         // (free pose, term) chains over the step's rows of the pose: four rows' loads in flight, then their four adds
         // in edge order (a missing row: a select keeps the sum)
 #pragma unroll
@@ -1763,6 +1784,9 @@ __device__ __noinline__ void build_system() {
         __syncthreads();
         tb0 = wall_clock64();
         tB += tb0 - tb1;
+#ifdef SPSLAM_LBG_DIAG_BUILD
+        if (t == 0) { s.dg[4] += tb0 - db3; s.dg[5] += 1; }  // pose chains, steps
+#endif
     }
     if (t == 0) { s.ph[0] += tA; s.tB += tB; }
 #pragma unroll
@@ -3096,6 +3120,10 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
         b.res[p].phase_us[0] = (float)((wall_clock64() - t0) * 0.01);
         for (int i = 1; i < 8; i++) b.res[p].phase_us[i] = (float)(s.ph[i] * 0.01);
         b.res[p].pad = (int)(s.tB * 0.01);  // diagnostic: build phase (B) us
+#ifdef SPSLAM_LBG_DIAG_BUILD  // buildSystem: heads, (A) terms, landmark chains, Hpl blocks, pose chains (us); steps
+        for (int i = 0; i < 5; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
+        b.res[p].pad = (int)s.dg[5];
+#endif
 #ifdef SPSLAM_LBG_DIAG  // Schur: staging wait, BDinv, chains, commit; factor-only
         for (int i = 0; i < 4; i++) b.res[p].phase_us[1 + i] = (float)(s.dg[i] * 0.01);
         b.res[p].phase_us[5] = (float)(s.dg[6] * 1e-3);  // factor: step-loop shader kcycles,
