@@ -384,6 +384,7 @@ class HotPath:
         """TrackWithMotionModel then TrackLocalMap (src/Tracking.cc:951-1068) from the matches on."""
         import spslam_track as ST
         g1, g2 = self.graphs
+        self._join_planes()
         self.associate(0)
         self.track.batch_device(self.B, ST.MOTION_MODEL, self._track_batch(0), stream=self.stream)
         G.pose_optimize_batch_device(self.ex, self.B, g1["P"].data_ptr(), g1["pts"].data_ptr(),
@@ -396,6 +397,11 @@ class HotPath:
         G.pose_optimize_batch_device(self.ex, self.B, g2["P"].data_ptr(), g2["pts"].data_ptr(),
                                      g2["pls"].data_ptr(), self.d_res2.data_ptr(), g2["pout"].data_ptr(),
                                      g2["plout"].data_ptr(), cfg=self.plane_cfg, stream=self.stream)
+
+    def _join_planes(self):
+        if getattr(self, "_planes_pending", False):
+            self.main.wait_event(self.ev_join)
+            self._planes_pending = False
 
     def graph(self, k):
         """Host copy of PoseOptimization graph k: (problems, [points per frame], [planes per frame],
@@ -669,8 +675,11 @@ class HotPath:
         self.planes(self.side_stream)
         self.orb()
         self.ev_join.record(self.side)
-        self.main.wait_event(self.ev_join)
+        # the tail's frame steps and SearchByProjection read no plane output: the join waits in pose(), before the
+        # first association, so they run beside the plane chain (B = 1 latency)
+        self._planes_pending = True
         self._tail()
+        self._join_planes()
         self._lba_end()
 
     def _step_pipelined(self):
