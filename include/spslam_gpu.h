@@ -807,8 +807,8 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
  * at f * (cap_a + cap_b) + i (spslam_planes_associate_batch_device layout) are
  * global map-plane indices.  The graphs are written with point_offset = f * cap
  * and plane_offset = f * 3 * (cap_a + cap_b), so the PoseOptimization outlier
- * flags of frame f are at the same offsets.  The Tracking state machine
- * (nmatches < 10 -> TrackReferenceKeyFrame, relocalisation) is the caller's.
+ * flags of frame f are at the same offsets.  The motion model's failure test and the switch to
+ * TrackReferenceKeyFrame: spslam_track_refkf_batch_device below; relocalisation is the caller's.
  *
  * Frame-to-frame state of a tracked sequence (Tracking::Track, src/Tracking.cc:
  * 443-505, TrackWithMotionModel :956-958), for batches that are consecutive
@@ -883,6 +883,65 @@ typedef struct spslam_track_batch {
 
 int spslam_track_graph_batch_device(spslam_ctx* ctx, int n_frames, int stage, const spslam_track_batch* batch,
                                     void* hip_stream);
+
+/* TrackWithMotionModel's failure and the switch to TrackReferenceKeyFrame (src/Tracking.cc:318-324: bOK =
+ * TrackWithMotionModel(); if (!bOK) bOK = TrackReferenceKeyFrame()), batched.  The motion model fails when
+ * SearchByProjection (after the 2*th retry) finds fewer than 10 matches (:977, before the association and
+ * PoseOptimization) or when fewer than 5 map points / map planes survive its discard (nmatchesMap, :986-1053).
+ * For the frames that fail a caller runs ComputeBoW + SearchByBoW against the reference keyframe
+ * (spslam_bow_transform_batch_device / spslam_search_by_bow_batch_device, :796-806); where that finds at least 10
+ * matches the frame is re-tracked from the last frame's pose -- association, MOTION_MODEL graph, PoseOptimization
+ * and DISCARD over the reference keyframe's map points (:808-882) -- into separate buffers that
+ * spslam_masked_frame_copy_device then moves over the motion model's.
+ *   SPSLAM_REFKF_PREPARE (after the motion model's DISCARD; mm = its spslam_track_batch): fallback[f], and
+ *     refkf_counts[f] = kp_counts[f] where it failed, else 0 (the BoW transform's counts: it skips the others).
+ *   SPSLAM_REFKF_SELECT (after SearchByBoW): apply[f] = fallback[f] && bow_nmatches[f] >= 10 (:806);
+ *     state[f] = 0 (motion model), 1 (reference keyframe) or 2 (both failed: LOST, the motion model's result is
+ *     kept); refkf_match = the BoW matches as rows of the keyframe's point set (-1 elsewhere and where !apply);
+ *     refkf_frames[f] = {Tcw = Tlw = proj_frames[f].Tlw (SetPose(mLastFrame.mTcw)), point_offset / n_points =
+ *     refkf_sets[2 f], [2 f + 1] (the keyframe's map points inside proj_points), 0 points where !apply};
+ *     refkf_assoc[f] = assoc_frames[f] at Tcw = Tlw, n_map = 0 where !apply, carry = 1 (the association starts
+ *     from the motion model's surviving planes, which the caller copies into its association arrays) unless the
+ *     motion model stopped before associating (< 10 matches: carry = 0); and the seen stamps: the motion model's
+ *     DISCARD stamped every one of its matches (mnLastFrameSeen); where the keyframe takes over only its discarded
+ *     outliers keep the stamp (:990-997; none when it stopped at < 10 matches), the others get stamp - 1. */
+#define SPSLAM_REFKF_PREPARE 0
+#define SPSLAM_REFKF_SELECT 1
+
+typedef struct spslam_refkf_batch {
+    const int32_t* nmatches;                 /* SearchByProjection's count after the retry, per frame */
+    uint8_t* fallback;                       /* PREPARE writes: the motion model failed */
+    int32_t* refkf_counts;                   /* PREPARE writes */
+    const int32_t* bow_nmatches;             /* SELECT: SearchByBoW's count per frame */
+    const int32_t* bow_match;                /* SELECT: SearchByBoW's keyframe feature per keypoint (cap per frame) */
+    const int32_t* refkf_rows;               /* SELECT: per keyframe feature its map point's row in the keyframe's
+                                                point set or -1 (rows_stride per keyframe) */
+    const int32_t* refkf_index;              /* SELECT: each frame's keyframe (row block of refkf_rows) */
+    int32_t rows_stride, pad;
+    const int32_t* refkf_sets;               /* SELECT: (point_offset, n_points) per frame */
+    const spslam_assoc_frame* assoc_frames;  /* SELECT: the motion model's first-association frames */
+    uint8_t* apply;                          /* SELECT writes */
+    int8_t* state;                           /* SELECT writes (may be NULL) */
+    int32_t* refkf_match;                    /* SELECT writes (cap per frame) */
+    spslam_proj_frame* refkf_frames;         /* SELECT writes */
+    spslam_assoc_frame* refkf_assoc;         /* SELECT writes */
+} spslam_refkf_batch;
+
+int spslam_track_refkf_batch_device(spslam_ctx* ctx, int n_frames, int stage, const spslam_track_batch* mm,
+                                    const spslam_refkf_batch* rk, void* hip_stream);
+
+/* dst[f] = src[f] for every frame f with flags[f] != 0, region by region: frame f's bytes at dst + f * dst_stride
+ * and src + f * src_stride (sizes and strides multiples of 4; at most 32 regions per call). */
+typedef struct spslam_frame_region {
+    void* dst;
+    const void* src;
+    int64_t frame_bytes;
+    int64_t dst_stride;
+    int64_t src_stride;
+} spslam_frame_region;
+
+int spslam_masked_frame_copy_device(spslam_ctx* ctx, int n_frames, const uint8_t* flags, int n_regions,
+                                    const spslam_frame_region* regions, void* hip_stream);
 
 /* ---------------------------------------------------------------- bag of words
  * DBoW2 (vendored Thirdparty/DBoW2) as the tracking path uses it:

@@ -26,7 +26,8 @@ class FrameInputs:
     """Everything one frame of the step reads: images, camera, the map it tracks against."""
 
     def __init__(self, gray, depth, cam, geometry, inv_sigma2, proj, local, map_planes, boundary, min_size=500,
-                 pose_cfg=None, local_seen=False, rgb=None, depth_raw=None, depth_scale=None, ref_kf=None):
+                 pose_cfg=None, local_seen=False, rgb=None, depth_raw=None, depth_scale=None, ref_kf=None,
+                 refkf_fallback=None):
         self.gray, self.depth = gray, depth
         # the raw frame GrabImageRGBD receives (the C++ chain, oracle_step_cpp, grabs it itself)
         self.rgb, self.depth_raw, self.depth_scale = rgb, depth_raw, depth_scale
@@ -45,6 +46,10 @@ class FrameInputs:
         # Tracking.cc:791-882): dict(vocab=oracle_bow.Vocabulary, desc, angle, has_point, fv = the keyframe's
         # FeatureVector, row = the projection-set row of each keyframe feature's map point or -1)
         self.ref_kf = ref_kf
+        # refkf_fallback: the reference keyframe TrackReferenceKeyFrame falls back to when TrackWithMotionModel
+        # fails (Tracking.cc:318-324): ref_kf's fields plus points = its map points as spslam_proj_point records
+        # (the rows `row` indexes); None: the motion model's result is kept whatever it is
+        self.refkf_fallback = refkf_fallback
 
 
 def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
@@ -86,13 +91,50 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
     out["assoc0"], out["graph1"], out["pose1"] = a0, g1, (r1, po1, plo1)
     T1 = r1["Tcw"] if not chain else np.asarray(chain["pose1_Tcw"], np.float32)
     keep, taken = oracle_track.discard_outliers(mo, g1[3], po1, P)
+    seen = {int(P[m]["id"]) for m in mo if m >= 0}  # mnLastFrameSeen: every motion-model match (:997, :1380-1390)
+    out["fallback"] = 0
+    if fi.refkf_fallback is not None and fi.ref_kf is None:
+        # TrackWithMotionModel's verdict: < 10 matches (:977), or nmatchesMap < 5 after the discard (:986-1053)
+        edge = g1[3]
+        nmm = sum(1 for i, m in enumerate(mo) if m >= 0 and edge[i] >= 0 and not po1[edge[i]] and P[m]["n_obs"] > 0)
+        nmm += sum(1 for j, pl in enumerate(g1[2]) if pl["kind"] == 0 and not plo1[j])
+        if nmo < 10 or nmm < 5:
+            import oracle_bow
+            R = fi.refkf_fallback
+            fv = R["vocab"].transform(do)                  # mCurrentFrame.ComputeBoW()
+            bm, nbow = oracle_bow.search_by_bow(R["desc"], R["angle"], R["has_point"], R["fv"], do, ko["angle"], fv,
+                                                0.7, True)
+            if nbow < 10:  # TrackReferenceKeyFrame returns false: LOST (relocalisation is out of scope)
+                out["fallback"] = 2
+            else:
+                out["fallback"] = 1
+                # the motion model's discarded outliers keep their stamp (none when it stopped at < 10 matches);
+                # its other matches are no longer the frame's
+                seen = {int(P[mo[i]]["id"]) for i in range(len(mo))
+                        if nmo >= 10 and mo[i] >= 0 and edge[i] >= 0 and po1[edge[i]]}
+                init = oracle_track.discard_planes(a0, plo1) if nmo >= 10 else None
+                P = R["points"]
+                pfr = pfr.copy()
+                pfr["Tcw"] = pfr["Tlw"]                     # mCurrentFrame.SetPose(mLastFrame.mTcw)
+                pfr["n_points"] = len(P)
+                mo = np.where(bm >= 0, np.asarray(R["row"], np.int32)[np.maximum(bm, 0)], -1).astype(np.int32)
+                nmo = nbow
+                out["match"], out["nmatches"], out["bow_match"] = mo, nmo, bm
+                a0 = oracle_assoc.associate(pfr["Tcw"].reshape(4, 4), coefs, fi.map_planes, fi.boundary, init=init)
+                g1 = oracle_track.motion_model_graph(pfr, P, mo, kun, ur, fi.inv_sigma2, coefs, a0, fi.map_planes,
+                                                     fi.cam)
+                r1, po1, plo1 = oracle_ctypes.pose_optimize(*g1[:3], cfg=fi.pose_cfg)
+                out["assoc0"], out["graph1"], out["pose1"] = a0, g1, (r1, po1, plo1)
+                T1 = r1["Tcw"]
+                keep, taken = oracle_track.discard_outliers(mo, g1[3], po1, P)
+                seen |= {int(P[m]["id"]) for m in mo if m >= 0}
     out["keep"], out["taken"] = keep, taken
+    out["proj_points"] = P  # the point set the frame's matches index (the reference keyframe's after a fallback)
     # --- TrackLocalMap
     lfr, LP = fi.local
     lfr = lfr.copy()
     lfr["Tcw"] = np.asarray(T1, np.float32).reshape(16)
     if fi.local_seen:  # the caller's loop in SearchLocalPoints: points already seen by this frame are skipped
-        seen = {int(P[m]["id"]) for m in mo if m >= 0}
         idx = np.array([j for j in range(len(LP)) if int(LP[j]["id"]) not in seen], np.int64)
         lfs = lfr.copy()
         lfs["n_points"] = len(idx)

@@ -1071,12 +1071,22 @@ hipError_t pose_launch(int n, const spslam_pose_problem* probs, const spslam_poi
         const char* e = std::getenv("SPSLAM_POSE_SPEC");  // measurement knob: damping trials per edge pass
         return e ? std::atoi(e) : 4;
     }();
+    // measurement knob: SPSLAM_POSE_WHOLE_CU=1 pads the workgroup's LDS to the CU's 160 KB, so no other workgroup
+    // shares a PoseOptimization CU (the pose runs at its alone speed; the CUs are unavailable to the rest meanwhile)
+    static const size_t pad = [] {
+        const char* e = std::getenv("SPSLAM_POSE_WHOLE_CU");
+        if (!e || e[0] != '1') return (size_t)0;
+        hipFuncAttributes a{};
+        if (hipFuncGetAttributes(&a, (const void*)pose_kernel<4>) != hipSuccess) return (size_t)0;
+        return a.sharedSizeBytes < 160 * 1024 ? 160 * 1024 - a.sharedSizeBytes : (size_t)0;
+    }();
     if (spec <= 1)
         hipLaunchKernelGGL(pose_kernel<1>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
     else if (spec == 2)
         hipLaunchKernelGGL(pose_kernel<2>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
     else
-        hipLaunchKernelGGL(pose_kernel<4>, dim3(n), dim3(kThreads), 0, s, probs, pts, pls, K, init_from, res, pout, plout);
+        hipLaunchKernelGGL(pose_kernel<4>, dim3(n), dim3(kThreads), pad, s, probs, pts, pls, K, init_from, res, pout,
+                           plout);
     return hipGetLastError();
 }
 

@@ -1542,6 +1542,48 @@ int spslam_track_graph_batch_device(spslam_ctx* c, int n_frames, int stage, cons
     return SPSLAM_OK;
 }
 
+int spslam_track_refkf_batch_device(spslam_ctx* c, int n_frames, int stage, const spslam_track_batch* mm,
+                                    const spslam_refkf_batch* rk, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !mm || !rk || (stage != SPSLAM_REFKF_PREPARE && stage != SPSLAM_REFKF_SELECT))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_track_refkf_batch_device");
+    const spslam_track_batch& b = *mm;
+    const spslam_refkf_batch& r = *rk;
+    bool ok = b.kp_counts && b.cap >= 1 && b.cap <= (1 << 20) && b.proj_frames && b.proj_points && b.proj_match &&
+              b.edge_of_kp && b.point_outlier && r.nmatches && r.fallback;
+    if (stage == SPSLAM_REFKF_PREPARE)
+        ok = ok && b.problems && b.planes && b.plane_outlier && r.refkf_counts;
+    else
+        ok = ok && r.bow_nmatches && r.bow_match && r.refkf_rows && r.refkf_index && r.rows_stride >= 1 &&
+             r.refkf_sets && r.assoc_frames && r.apply && r.refkf_match && r.refkf_frames && r.refkf_assoc &&
+             (!b.seen || b.local_frames);
+    if (!ok)
+        return fail(c, SPSLAM_ERR_ARG, "missing buffer for spslam_track_refkf_batch_device stage %s",
+                    stage == SPSLAM_REFKF_PREPARE ? "PREPARE" : "SELECT");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, refkf_launch(n_frames, stage, b, r, (hipStream_t)hip_stream));
+    return SPSLAM_OK;
+}
+
+int spslam_masked_frame_copy_device(spslam_ctx* c, int n_frames, const uint8_t* flags, int n_regions,
+                                    const spslam_frame_region* regions, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !flags || n_regions < 0 || n_regions > kMaxFrameRegions || (n_regions && !regions))
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_masked_frame_copy_device");
+    FrameRegions G{};
+    G.n = n_regions;
+    for (int k = 0; k < n_regions; k++) {
+        const spslam_frame_region& r = regions[k];
+        if (!r.dst || !r.src || r.frame_bytes < 0 || r.frame_bytes % 4 || r.dst_stride % 4 || r.src_stride % 4 ||
+            ((uintptr_t)r.dst | (uintptr_t)r.src) % 4 || r.frame_bytes > r.dst_stride || r.frame_bytes > r.src_stride)
+            return fail(c, SPSLAM_ERR_ARG, "bad region of %s", "spslam_masked_frame_copy_device");
+        G.r[k] = r;
+    }
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, masked_frame_copy_launch(n_frames, flags, G, (hipStream_t)hip_stream));
+    return SPSLAM_OK;
+}
+
 int spslam_search_local_points_batch_device(spslam_ctx* c, int n_frames, const spslam_local_frame* d_frames,
                                             const spslam_local_point* d_points, int max_points,
                                             const spslam_keypoint* d_keys_un, const uint8_t* d_desc,

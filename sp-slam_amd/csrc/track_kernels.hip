@@ -309,7 +309,96 @@ __global__ __launch_bounds__(kThreads) void track_graph_kernel(TrackArgs A, int 
     }
 }
 
+// TrackWithMotionModel's failure test (src/Tracking.cc:977 and the nmatchesMap count of :986-1053) and the
+// switch to TrackReferenceKeyFrame's re-tracking (:796-817); see spslam_gpu.h.  One workgroup per frame.
+__global__ __launch_bounds__(kThreads) void refkf_kernel(spslam_track_batch B, spslam_refkf_batch R, int stage) {
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    __shared__ int wsum[kThreads / 64];
+    const int n = min(B.kp_counts[f], B.cap);
+    const size_t ko = (size_t)f * B.cap;
+    const spslam_proj_frame& PF = B.proj_frames[f];
+    const int nm = R.nmatches[f];
+    if (stage == SPSLAM_REFKF_SELECT) {
+        const bool fb = R.fallback[f] != 0;
+        const bool ap = fb && R.bow_nmatches[f] >= 10;  // TrackReferenceKeyFrame: if(nmatches<10) return false
+        // the keyframe's matches as rows of its point set
+        const int32_t* rows = R.refkf_rows + (size_t)R.refkf_index[f] * R.rows_stride;
+        for (int i = t; i < B.cap; i += kThreads) {
+            const int m = ap && i < n ? R.bow_match[ko + i] : -1;
+            R.refkf_match[ko + i] = m >= 0 ? rows[m] : -1;
+        }
+        // mnLastFrameSeen: the motion model's matches that the keyframe's replace lose their stamp; its discarded
+        // outliers keep theirs -- unless it stopped at < 10 matches (no discard at all)
+        if (ap && B.seen) {
+            const spslam_local_frame& LF = B.local_frames[f];
+            for (int i = t; i < n; i += kThreads) {
+                const int e = B.edge_of_kp[ko + i];
+                if (e >= 0 && (nm < 10 || !B.point_outlier[ko + e]))
+                    B.seen[LF.seen_offset + B.proj_points[PF.point_offset + B.proj_match[ko + i]].id] = LF.stamp - 1;
+            }
+        }
+        if (t == 0) {
+            R.apply[f] = (uint8_t)ap;
+            if (R.state) R.state[f] = (int8_t)(ap ? 1 : fb ? 2 : 0);
+            spslam_proj_frame& Q = R.refkf_frames[f];
+            for (int q = 0; q < 16; q++) Q.Tcw[q] = Q.Tlw[q] = PF.Tlw[q];  // SetPose(mLastFrame.mTcw)
+            Q.point_offset = R.refkf_sets[2 * f];
+            Q.n_points = ap ? R.refkf_sets[2 * f + 1] : 0;
+            Q.pad[0] = Q.pad[1] = 0;
+            spslam_assoc_frame A = R.assoc_frames[f];
+            for (int q = 0; q < 16; q++) A.Tcw[q] = PF.Tlw[q];
+            if (!ap) A.n_map = 0;
+            A.carry = nm >= 10 ? 1 : 0;
+            R.refkf_assoc[f] = A;
+        }
+        return;
+    }
+    // PREPARE -- nmatchesMap: inlier map points with observations, then inlier matched map planes
+    int c = 0;
+    for (int i = t; i < n; i += kThreads) {
+        const int e = B.edge_of_kp[ko + i];
+        if (e >= 0 && !B.point_outlier[ko + e] && B.proj_points[PF.point_offset + B.proj_match[ko + i]].n_obs > 0) c++;
+    }
+    const spslam_pose_problem& P = B.problems[f];
+    for (int j = t; j < P.n_planes; j += kThreads)
+        if (B.planes[P.plane_offset + j].kind == SPSLAM_PLANE_EDGE && !B.plane_outlier[P.plane_offset + j]) c++;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off);
+    if (lane == 0) wsum[wave] = c;
+    __syncthreads();
+    if (t != 0) return;
+    int nmm = 0;
+    for (int w = 0; w < kThreads / 64; w++) nmm += wsum[w];
+    const bool fb = nm < 10 || nmm < 5;
+    R.fallback[f] = (uint8_t)fb;
+    R.refkf_counts[f] = fb ? B.kp_counts[f] : 0;
+}
+
+// dst[f] = src[f] of every region for the flagged frames, 4 bytes per lane
+__global__ __launch_bounds__(256) void masked_frame_copy_kernel(const uint8_t* __restrict__ flags, FrameRegions G) {
+    const int f = blockIdx.x;
+    if (!flags[f]) return;
+    for (int k = 0; k < G.n; k++) {
+        const spslam_frame_region& r = G.r[k];
+        uint32_t* d = (uint32_t*)((uint8_t*)r.dst + f * r.dst_stride);
+        const uint32_t* sp = (const uint32_t*)((const uint8_t*)r.src + f * r.src_stride);
+        const int64_t nw = r.frame_bytes / 4;
+        for (int64_t i = threadIdx.x; i < nw; i += blockDim.x) d[i] = sp[i];
+    }
+}
+
 }  // namespace
+
+hipError_t refkf_launch(int n_frames, int stage, const spslam_track_batch& mm, const spslam_refkf_batch& rk,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(refkf_kernel, dim3(n_frames), dim3(kThreads), 0, s, mm, rk, stage);
+    return hipGetLastError();
+}
+
+hipError_t masked_frame_copy_launch(int n_frames, const uint8_t* flags, const FrameRegions& regions, hipStream_t s) {
+    hipLaunchKernelGGL(masked_frame_copy_kernel, dim3(n_frames), dim3(256), 0, s, flags, regions);
+    return hipGetLastError();
+}
 
 hipError_t track_launch(int n_frames, int stage, const TrackArgs& a, hipStream_t s, KernelTimer* timer) {
     if (timer) timer->begin(kKindTrack, s);

@@ -15,4 +15,15 @@ struct TrackArgs {
 
 hipError_t track_launch(int n_frames, int stage, const TrackArgs& a, hipStream_t s, KernelTimer* timer);
 
+// TrackWithMotionModel's failure test and the TrackReferenceKeyFrame switch (spslam_track_refkf_batch_device)
+hipError_t refkf_launch(int n_frames, int stage, const spslam_track_batch& mm, const spslam_refkf_batch& rk,
+                        hipStream_t s);
+
+constexpr int kMaxFrameRegions = 32;
+struct FrameRegions {
+    spslam_frame_region r[kMaxFrameRegions];
+    int n;
+};
+hipError_t masked_frame_copy_launch(int n_frames, const uint8_t* flags, const FrameRegions& regions, hipStream_t s);
+
 }  // namespace spslam

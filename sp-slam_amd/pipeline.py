@@ -391,12 +391,16 @@ class HotPath:
                                      g1["pls"].data_ptr(), self.d_res1.data_ptr(), g1["pout"].data_ptr(),
                                      g1["plout"].data_ptr(), cfg=self.plane_cfg, stream=self.stream)
         self.track.batch_device(self.B, ST.DISCARD, self._track_batch(0), stream=self.stream)
+        self._after_motion_model()
         self.search_local_points()
         self.associate(1)
         self.track.batch_device(self.B, ST.LOCAL_MAP, self._track_batch(1), stream=self.stream)
         G.pose_optimize_batch_device(self.ex, self.B, g2["P"].data_ptr(), g2["pts"].data_ptr(),
                                      g2["pls"].data_ptr(), self.d_res2.data_ptr(), g2["pout"].data_ptr(),
                                      g2["plout"].data_ptr(), cfg=self.plane_cfg, stream=self.stream)
+
+    def _after_motion_model(self):
+        """Hook after TrackWithMotionModel's discard (sequence.SequencePath: the TrackReferenceKeyFrame switch)."""
 
     def _join_planes(self):
         if getattr(self, "_planes_pending", False):

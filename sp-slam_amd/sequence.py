@@ -81,17 +81,24 @@ def render_sequences(seq_id, n_boxes, U, T, w, h, K, workers=0):
 class SequencePath(pipeline.HotPath):
     """HotPath over T frames of U sequences (B slots, slot i -> sequence i % U)."""
 
-    def __init__(self, B, n_frames, n_sequences=None, render_workers=0, local_mapping=None, **kw):
+    def __init__(self, B, n_frames, n_sequences=None, render_workers=0, local_mapping=None, refkf_fallback=None,
+                 **kw):
         """local_mapping: run the deterministic LocalMapping (local_mapping.py: keyframe insertion and
         LocalBundleAdjustment written back into the map) after every keyframe frame; default: on when the
         config asks for LocalBundleAdjustment (C3's lba_every), off otherwise."""
         self.T = n_frames
         self.U = min(n_sequences or B, B)
         self.d_load_idx = None
+        self.vel_perturb = {}
         self.render_workers = render_workers
         self.n_boxes = kw.get("n_boxes", 3)
         lba_every = kw.pop("lba_every", 0)  # the side-by-side synthetic local maps of the open-loop HotPath
         self.local_mapping = bool(lba_every) if local_mapping is None else bool(local_mapping)
+        # TrackWithMotionModel -> TrackReferenceKeyFrame on the device (default: on without LocalMapping; the
+        # LocalMapping harness moves the keyframes' points, which the reference keyframe sets do not follow)
+        self.refkf_fallback = (not self.local_mapping) if refkf_fallback is None else bool(refkf_fallback)
+        if self.refkf_fallback and self.local_mapping:
+            raise ValueError("refkf_fallback with local_mapping is not supported")
         kw.pop("unique_frames", None)
         kw.pop("rotate_inputs", None)
         super().__init__(B, unique_frames=self.U, **kw)
@@ -140,6 +147,7 @@ class SequencePath(pipeline.HotPath):
         desc, cnt = d_ds.cpu().numpy(), d_n.cpu().numpy()
         kf0 = [u * len(kf_t) for u in range(U)]  # keyframe 0 of each sequence: TrackReferenceKeyFrame's reference
         self.d_kf0_kps, self.d_kf0_desc, self.d_kf0_cnt = d_k[kf0].clone(), d_ds[kf0].clone(), d_n[kf0].clone()
+        self.d_kf_kps, self.d_kf_desc, self.d_kf_cnt = d_k, d_ds, d_n  # every keyframe (q = u * len(kf_t) + j)
         self.n_ids = len(kf_t) * cap                   # map point ids per sequence: keyframe index * cap + keypoint
         self.kf_points, self.kf_kps = {}, {}
         offs, pts = {}, []
@@ -174,7 +182,16 @@ class SequencePath(pipeline.HotPath):
         self.d_seen = torch.full((B * self.n_ids,), -1, dtype=torch.int32, device="cuda")
         # frame 0 (StereoInitialization): true pose, keyframe 0's points are its map points
         pf = np.zeros(B, SM.PROJ_FRAME_DTYPE)
-        pp = np.zeros(B * cap, SM.PROJ_POINT_DTYPE)
+        # the last-frame point sets (f * cap), then every keyframe's map points as TrackReferenceKeyFrame's point
+        # set (keypoint order, the rows its BoW matches index)
+        nkf = len(kf_t)
+        kfsets = [synth.as_last_frame_points(self.kf_points[u, j], self.kf_kps[u, j], j * cap) for u in range(U)
+                  for j in range(nkf)]
+        self.kf_set_off = B * cap + np.concatenate([[0], np.cumsum([len(k) for k in kfsets])[:-1]]).astype(np.int64)
+        self.kf_set_len = np.array([len(k) for k in kfsets], np.int64)
+        pp = np.zeros(B * cap + int(self.kf_set_len.sum()), SM.PROJ_POINT_DTYPE)
+        for q, k in enumerate(kfsets):
+            pp[self.kf_set_off[q]:self.kf_set_off[q] + len(k)] = k
         for i in range(B):
             u = i % U
             P0 = synth.as_last_frame_points(self.kf_points[u, 0], self.kf_kps[u, 0], 0)
@@ -282,6 +299,133 @@ class SequencePath(pipeline.HotPath):
         super()._setup_track()
         if self.local_mapping:
             self._setup_local_mapping()
+        if self.refkf_fallback:
+            self._setup_refkf()
+
+    def _setup_refkf(self):
+        """TrackWithMotionModel -> TrackReferenceKeyFrame (Tracking.cc:318-324): every keyframe's BoW side and the
+        rows of its map points (its point set in the projection buffer), frame t's reference keyframe = the latest
+        keyframe before it (the one the harness's local map ends with), and the re-tracking's own buffers."""
+        import spslam_bow as SB
+        import spslam_track as ST
+        torch, B, U, cap, T = self.torch, self.B, self.U, self.kp_cap, self.T
+        nkf = len(self.kf_t)
+        i32 = dict(dtype=torch.int32, device="cuda")
+        u8 = dict(dtype=torch.uint8, device="cuda")
+        has = np.zeros((U * nkf, cap), np.uint8)
+        row = np.full((U * nkf, cap), -1, np.int32)
+        for u in range(U):
+            for j in range(nkf):
+                kpi = (self.kf_points[u, j]["id"] - j * cap).astype(np.int64)
+                has[u * nkf + j, kpi] = 1
+                row[u * nkf + j, kpi] = np.arange(len(kpi), dtype=np.int32)
+        self.d_kf_has, self.d_kf_row = torch.from_numpy(has).cuda(), torch.from_numpy(row).cuda()
+        self.kf_bow = self._fv_buffers(U * nkf)
+        self._bow_transform(U * nkf, self.d_kf_desc, self.d_kf_cnt, self.kf_bow)
+        self.kf_side = SB.BowSide(self.d_kf_desc.data_ptr(), self.d_kf_kps.data_ptr(), self.d_kf_has.data_ptr(),
+                                  self.d_kf_cnt.data_ptr(), self.kf_bow["nodes"].data_ptr(),
+                                  self.kf_bow["start"].data_ptr(), self.kf_bow["features"].data_ptr(),
+                                  self.kf_bow["n_fv"].data_ptr(), cap, 0)
+        # per frame t and slot: (reference keyframe's set offset, size), the SearchByBoW pair
+        sets = np.zeros((T, B, 2), np.int32)
+        pairs = np.zeros((T, B, 2), np.int32)
+        self.refkf_of = np.zeros((T, B), np.int64)
+        for t in range(1, T):
+            j = (t - 1) // synth.KEYFRAME_STEP
+            for i in range(B):
+                q = (i % self.U) * nkf + j
+                sets[t, i] = (self.kf_set_off[q], self.kf_set_len[q])
+                pairs[t, i] = (q, i)
+                self.refkf_of[t, i] = q
+        self.d_refkf_sets, self.d_refkf_pairs = torch.from_numpy(sets).cuda(), torch.from_numpy(pairs).cuda()
+        self.d_refkf_q = torch.from_numpy(self.refkf_of.astype(np.int32)).cuda()
+        P = self.pe.planes_cap + self.pe.supp_cap
+        self.fb = dict(
+            fallback=torch.zeros(B, **u8), apply=torch.zeros(B, **u8), counts=torch.zeros(B, **i32),
+            frames=torch.zeros_like(self.d_pframes), assoc_frames=torch.zeros_like(self.d_afr1),
+            match=torch.zeros((B, cap), **i32), taken=torch.zeros((B, cap), **u8), edge=torch.zeros((B, cap), **i32),
+            res=torch.zeros_like(self.d_res1), assoc=torch.zeros((3, B * P), **i32), newp=torch.zeros(B, **i32),
+            next=torch.zeros((3, B * P), **i32), lframes=torch.zeros_like(self.d_lframes),
+            afr2=torch.zeros_like(self.d_afr2), bow_match=torch.zeros((B, cap), **i32), bow_n=torch.zeros(B, **i32),
+            graph={k: torch.zeros_like(v) for k, v in self.graphs[0].items()})
+        self.fb_hist = torch.zeros((T, B), dtype=torch.int8, device="cuda")  # 0 motion model, 1 reference kf, 2 lost
+        self._track_mod = ST
+
+    def _fv_buffers(self, n):
+        torch, cap = self.torch, self.kp_cap
+        i32 = dict(dtype=torch.int32, device="cuda")
+        return dict(words=torch.zeros((n, cap), **i32), values=torch.zeros((n, cap), dtype=torch.float64,
+                                                                          device="cuda"),
+                    n_bow=torch.zeros(n, **i32), nodes=torch.zeros((n, cap), **i32),
+                    start=torch.zeros((n, cap + 1), **i32), features=torch.zeros((n, cap), **i32),
+                    n_fv=torch.zeros(n, **i32))
+
+    def _after_motion_model(self):
+        """TrackWithMotionModel's verdict and, for the frames it fails, TrackReferenceKeyFrame (Tracking.cc:318-324,
+        791-882) on the device: ComputeBoW + SearchByBoW against the reference keyframe; where that finds >= 10
+        matches, association, graph, PoseOptimization and discard from the last frame's pose over the keyframe's
+        map points, moved over the motion model's outputs (spslam_track_refkf_batch_device,
+        spslam_masked_frame_copy_device).  Frames where the motion model holds pass through every kernel as empty
+        problems."""
+        if not self.refkf_fallback or self.n_tracked == 0:  # frame 1 already tracks the reference keyframe
+            return
+        import spslam_bow as SB
+        import spslam_planes as SP
+        ST, torch, B, cap, fb = self._track_mod, self.torch, self.B, self.kp_cap, self.fb
+        t = self.n_tracked + 1
+        mm = self._track_batch(0)
+        rk = ST.RefkfBatch(nmatches=self.d_nmatch.data_ptr(), fallback=fb["fallback"].data_ptr(),
+                           refkf_counts=fb["counts"].data_ptr(), bow_nmatches=fb["bow_n"].data_ptr(),
+                           bow_match=fb["bow_match"].data_ptr(), refkf_rows=self.d_kf_row.data_ptr(),
+                           refkf_index=self.d_refkf_q[t].data_ptr(), rows_stride=cap,
+                           refkf_sets=self.d_refkf_sets[t].data_ptr(), assoc_frames=self.d_afr1.data_ptr(),
+                           apply=fb["apply"].data_ptr(), state=self.fb_hist[t].data_ptr(),
+                           refkf_match=fb["match"].data_ptr(), refkf_frames=fb["frames"].data_ptr(),
+                           refkf_assoc=fb["assoc_frames"].data_ptr())
+        self.track.refkf_device(B, ST.REFKF_PREPARE, mm, rk, stream=self.stream)
+        # mCurrentFrame.ComputeBoW(); SearchByBoW(mpReferenceKF, mCurrentFrame) -- on the failing frames only
+        self._bow_transform(B, self.d_desc, fb["counts"], self.fr_bow)
+        fr = SB.BowSide(self.d_desc.data_ptr(), self.d_kps.data_ptr(), 0, fb["counts"].data_ptr(),
+                        self.fr_bow["nodes"].data_ptr(), self.fr_bow["start"].data_ptr(),
+                        self.fr_bow["features"].data_ptr(), self.fr_bow["n_fv"].data_ptr(), cap, 0)
+        SB.search_by_bow_batch_device(self.ex, B, self.d_refkf_pairs[t].data_ptr(), self.kf_side, fr,
+                                      fb["bow_match"].data_ptr(), fb["bow_n"].data_ptr(), nn_ratio=0.7,
+                                      check_orientation=True, stream=self.stream)
+        self.track.refkf_device(B, ST.REFKF_SELECT, mm, rk, stream=self.stream)
+        # the re-tracking starts from the motion model's surviving planes and its local-frame / next-association
+        # records (the frames it is applied to)
+        a, n = fb["assoc"], fb["next"]
+        self.track.masked_copy_device(B, fb["apply"].data_ptr(),
+                                      [(a[k], self.d_assoc[1][k]) for k in range(3)] +
+                                      [(fb["lframes"], self.d_lframes), (fb["afr2"], self.d_afr2)], stream=self.stream)
+        # mCurrentFrame.SetPose(mLastFrame.mTcw); AssociatePlanesByBoundary; PoseOptimization; discard
+        self.assoc.batch_device(B, fb["assoc_frames"].data_ptr(), self.d_planes.data_ptr(), SP.PLANE_DTYPE.itemsize,
+                                self.d_pcnt.data_ptr(), self.pe.planes_cap, self.d_supp.data_ptr(),
+                                SP.SUPPOSED_DTYPE.itemsize, self.d_scnt.data_ptr(), self.pe.supp_cap,
+                                self.d_map.data_ptr(), self.d_bound.data_ptr(), self.n_map, a[0].data_ptr(),
+                                a[1].data_ptr(), a[2].data_ptr(), fb["newp"].data_ptr(), stream=self.stream)
+        g = fb["graph"]
+        b = self._track_batch(0)
+        b.proj_frames, b.proj_match = fb["frames"].data_ptr(), fb["match"].data_ptr()
+        b.local_frames, b.taken = fb["lframes"].data_ptr(), fb["taken"].data_ptr()
+        b.assoc_match, b.assoc_parallel, b.assoc_vertical = a[0].data_ptr(), a[1].data_ptr(), a[2].data_ptr()
+        b.assoc_frames_next, b.plane_outlier = fb["afr2"].data_ptr(), g["plout"].data_ptr()
+        b.next_match, b.next_parallel, b.next_vertical = n[0].data_ptr(), n[1].data_ptr(), n[2].data_ptr()
+        b.problems, b.points, b.planes = g["P"].data_ptr(), g["pts"].data_ptr(), g["pls"].data_ptr()
+        b.edge_of_kp, b.results, b.point_outlier = fb["edge"].data_ptr(), fb["res"].data_ptr(), g["pout"].data_ptr()
+        b.assoc_frames_first = 0
+        self.track.batch_device(B, ST.MOTION_MODEL, b, stream=self.stream)
+        G.pose_optimize_batch_device(self.ex, B, g["P"].data_ptr(), g["pts"].data_ptr(), g["pls"].data_ptr(),
+                                     fb["res"].data_ptr(), g["pout"].data_ptr(), g["plout"].data_ptr(),
+                                     cfg=self.plane_cfg, stream=self.stream)
+        self.track.batch_device(B, ST.DISCARD, b, stream=self.stream)
+        g0 = self.graphs[0]
+        regions = [(self.d_pframes, fb["frames"]), (self.d_match, fb["match"]), (self.d_nmatch, fb["bow_n"]),
+                   (self.d_taken, fb["taken"]), (self.d_edge, fb["edge"]), (self.d_res1, fb["res"]),
+                   (self.d_newp[0], fb["newp"]), (self.d_afr2, fb["afr2"]), (self.d_lframes, fb["lframes"])]
+        regions += [(g0[k], g[k]) for k in ("P", "pts", "pls", "pout", "plout")]
+        regions += [(self.d_assoc[0][k], a[k]) for k in range(3)] + [(self.d_assoc[1][k], n[k]) for k in range(3)]
+        self.track.masked_copy_device(B, fb["apply"].data_ptr(), regions, stream=self.stream)
 
     def _setup_local_mapping(self):
         """local_mapping.SeqMap per sequence, keyframe 0 inserted (StereoInitialization: its own points), and the
@@ -313,7 +457,8 @@ class SequencePath(pipeline.HotPath):
         j = t // synth.KEYFRAME_STEP
         self.main.synchronize()
         pf = self.d_pframes.cpu().numpy().view(SM.PROJ_FRAME_DTYPE)
-        pp = self.d_ppoints.cpu().numpy().view(SM.PROJ_POINT_DTYPE).reshape(B, cap)
+        npp = B * cap * SM.PROJ_POINT_DTYPE.itemsize  # the last-frame sets (the keyframe sets follow)
+        pp = self.d_ppoints[:npp].cpu().numpy().view(SM.PROJ_POINT_DTYPE).reshape(B, cap)
         traj = self.traj[t].cpu().numpy().reshape(B, 4, 4)
         cnt = self.d_cnt.cpu().numpy()
         kun = self.d_kun.cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(B, cap)
@@ -383,7 +528,7 @@ class SequencePath(pipeline.HotPath):
             for i in range(u, B, U):
                 pp[i, :n] = P
                 pf[i]["Tlw"] = Tl
-        self.d_ppoints.copy_(torch.from_numpy(pp.view(np.uint8).reshape(-1)))
+        self.d_ppoints[:npp].copy_(torch.from_numpy(pp.view(np.uint8).reshape(-1)))
         self.d_pframes.copy_(torch.from_numpy(pf.view(np.uint8).reshape(-1)))
         self.lm_runs.append((t, run))
         torch.cuda.synchronize()
@@ -418,6 +563,9 @@ class SequencePath(pipeline.HotPath):
         import spslam_track as ST
         if self.n_tracked + 1 >= self.T:
             raise RuntimeError(f"sequence exhausted: {self.T} frames rendered")
+        for slot, V in self.vel_perturb.get(self.n_tracked + 1, []):
+            with self.torch.cuda.stream(self.main):
+                self.d_velocity[16 * slot:16 * slot + 16].copy_(self.torch.from_numpy(V).cuda(non_blocking=False))
         self.track.batch_device(self.B, ST.MOTION_PRIOR, self._track_batch(0), stream=self.stream)
         super()._tail()
         nxt = self.proj_sets[1] if self.d_pframes.data_ptr() == self.proj_sets[0][0].data_ptr() else self.proj_sets[0]
@@ -460,6 +608,37 @@ class SequencePath(pipeline.HotPath):
         n = int(self.d_kf0_cnt[u])
         kps = self.d_kf0_kps[u, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
         return kps, self.d_kf0_desc[u, :n].cpu().numpy(), self.kf0_has[u, :n], self.kf0_row[u, :n]
+
+    def oracle_refkf(self, slot, vocab_text):
+        """refkf_of(t) for oracle_sequence.track: frame t's reference keyframe (the latest keyframe before it) as
+        oracle_step.FrameInputs.refkf_fallback -- BoW inputs, feature -> row map and its map points."""
+        import oracle_sequence
+        u, nkf, cap = slot % self.U, len(self.kf_t), self.kp_cap
+        cache = {}
+
+        def of(t):
+            q = u * nkf + (t - 1) // synth.KEYFRAME_STEP
+            if q not in cache:
+                n = int(self.d_kf_cnt[q])
+                kps = self.d_kf_kps[q, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
+                has = self.d_kf_has[q, :n].cpu().numpy()
+                row = self.d_kf_row[q, :n].cpu().numpy()
+                R = oracle_sequence.reference_keyframe((kps, self.d_kf_desc[q, :n].cpu().numpy(), has, row), vocab_text)
+                j = (t - 1) // synth.KEYFRAME_STEP
+                R["points"] = synth.as_last_frame_points(self.kf_points[u, j], self.kf_kps[u, j], j * cap)
+                cache[q] = R
+            return cache[q]
+        return of
+
+    def perturb_velocity(self, t, slot, V):
+        """Test hook: frame t of slot `slot` predicts its pose from velocity V (4x4) instead of its predecessor's
+        (a motion-model failure on demand); oracle_sequence.track(perturb={t: V}) is the CPU side."""
+        self.vel_perturb.setdefault(t, []).append((slot, np.asarray(V, np.float32).reshape(16).copy()))
+
+    def fallback_history(self):
+        """[t][slot]: 0 the motion model held, 1 TrackReferenceKeyFrame took over, 2 both failed (lost)."""
+        self.torch.cuda.synchronize()
+        return self.fb_hist[:self.n_tracked + 1].cpu().numpy()
 
     def oracle_local_map(self, slot):
         """A fresh local_mapping.SeqMap of slot `slot`'s sequence as it stood before frame 1 (keyframe 0

@@ -1,7 +1,10 @@
 """ctypes binding of the tracking-graph part of include/spslam_gpu.h
 (spslam_track_graph_batch_device: TrackWithMotionModel / TrackLocalMap's
 bookkeeping between matching and Optimizer::PoseOptimization,
-src/Tracking.cc:951-1000, 1055-1068; src/Optimizer.cc:561-640, 681-860)."""
+src/Tracking.cc:951-1000, 1055-1068; src/Optimizer.cc:561-640, 681-860;
+spslam_track_refkf_batch_device + spslam_masked_frame_copy_device: the
+motion model's failure test and the TrackReferenceKeyFrame switch,
+src/Tracking.cc:318-324, 791-882)."""
 from __future__ import annotations
 
 import ctypes
@@ -9,8 +12,10 @@ import ctypes
 import spslam_gpu
 
 MOTION_MODEL, DISCARD, LOCAL_MAP, MOTION_PRIOR, LAST_FRAME = 0, 1, 2, 3, 4
+REFKF_PREPARE, REFKF_SELECT = 0, 1
 
-spslam_gpu.EXPORTED += ["spslam_track_graph_batch_device"]
+spslam_gpu.EXPORTED += ["spslam_track_graph_batch_device", "spslam_track_refkf_batch_device",
+                        "spslam_masked_frame_copy_device"]
 
 _P = ctypes.c_void_p
 
@@ -33,8 +38,24 @@ class TrackBatch(ctypes.Structure):
                 ("bf", ctypes.c_float), ("pad", ctypes.c_int32)]
 
 
+class RefkfBatch(ctypes.Structure):
+    """struct spslam_refkf_batch (device pointers as ints)."""
+    _fields_ = [("nmatches", _P), ("fallback", _P), ("refkf_counts", _P), ("bow_nmatches", _P), ("bow_match", _P),
+                ("refkf_rows", _P), ("refkf_index", _P), ("rows_stride", ctypes.c_int32), ("pad", ctypes.c_int32),
+                ("refkf_sets", _P), ("assoc_frames", _P), ("apply", _P), ("state", _P), ("refkf_match", _P),
+                ("refkf_frames", _P), ("refkf_assoc", _P)]
+
+
+class FrameRegion(ctypes.Structure):
+    """struct spslam_frame_region."""
+    _fields_ = [("dst", _P), ("src", _P), ("frame_bytes", ctypes.c_int64), ("dst_stride", ctypes.c_int64),
+                ("src_stride", ctypes.c_int64)]
+
+
 def _bind(lib):
     lib.spslam_track_graph_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P]
+    lib.spslam_track_refkf_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P]
+    lib.spslam_masked_frame_copy_device.argtypes = [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P]
 
 
 class TrackGraph:
@@ -47,3 +68,17 @@ class TrackGraph:
     def batch_device(self, n_frames: int, stage: int, batch: TrackBatch, stream=0):
         self.ex._check(self.ex.lib.spslam_track_graph_batch_device(self.ex.ctx, n_frames, stage,
                                                                     ctypes.byref(batch), stream or None))
+
+    def refkf_device(self, n_frames: int, stage: int, mm: TrackBatch, rk: RefkfBatch, stream=0):
+        self.ex._check(self.ex.lib.spslam_track_refkf_batch_device(self.ex.ctx, n_frames, stage, ctypes.byref(mm),
+                                                                    ctypes.byref(rk), stream or None))
+
+    def masked_copy_device(self, n_frames: int, flags: int, regions, stream=0):
+        """regions: [(dst tensor, src tensor)] of n_frames equal rows each (contiguous, byte sizes multiple of 4)."""
+        arr = (FrameRegion * len(regions))()
+        for k, (d, sv) in enumerate(regions):
+            fb = d.numel() * d.element_size() // n_frames
+            assert d.is_contiguous() and sv.is_contiguous() and sv.numel() * sv.element_size() == fb * n_frames
+            arr[k] = FrameRegion(d.data_ptr(), sv.data_ptr(), fb, fb, fb)
+        self.ex._check(self.ex.lib.spslam_masked_frame_copy_device(self.ex.ctx, n_frames, flags, len(regions), arr,
+                                                                    stream or None))

@@ -47,7 +47,7 @@ def sequence_path(B, T, U, config, pipelined=True):
     return sequence.SequencePath(B, T, n_sequences=U, pipelined=pipelined, **pipeline.CONFIGS[config])
 
 
-def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None):
+def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None, refkf=False, perturb=None):
     import oracle_ctypes
     import oracle_grab
     import oracle_planes
@@ -61,7 +61,9 @@ def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None):
                                  oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures),
                                  oracle_planes.PlaneOracle(), supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                  pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
-                                 on_frame=on_frame, ref_kf=ref, local_map=local_map, on_lba=on_lba)
+                                 on_frame=on_frame, ref_kf=ref, local_map=local_map, on_lba=on_lba,
+                                 refkf_of=sp.oracle_refkf(slot, synth.shape_vocabulary_text()) if refkf else None,
+                                 perturb=perturb)
 
 
 def test_pipelined_equals_serial(tracked):
@@ -215,5 +217,42 @@ def test_c3_local_mapping_in_the_loop():
         (pathlib.Path(__file__).resolve().parents[1] / "gpurun_out" / "c3_local_mapping_parity.json").write_text(
             json.dumps(diag, indent=1))
         assert diag["ate_vs_cpu_m"] <= 1e-12, diag["ate_vs_cpu_m"]  # identical trajectories (Horn's SVD rounding)
+    finally:
+        sp.close()
+
+
+def test_motion_model_failure_falls_back_to_reference_keyframe():
+    """Tracking.cc:318-324: where TrackWithMotionModel fails, TrackReferenceKeyFrame (BoW against the reference
+    keyframe, pose from the last frame) takes over inside the batched step.  The failure is forced by a wrong
+    velocity (a 25 degree yaw and 0.3 m) at frame 6 of slot 0 and frame 9 of slot 3, so SearchByProjection finds
+    almost nothing; the other slots and frames keep the motion model.  Bar: the device's per-frame decisions
+    (motion model / reference keyframe), matches, inliers and poses identical to the CPU loop's."""
+    import sequence
+    import pipeline
+    B, U, n = 4, 4, 12
+    c, s_ = np.cos(np.radians(25.0)), np.sin(np.radians(25.0))
+    V = np.array([[c, 0, s_, 0.3], [0, 1, 0, 0], [-s_, 0, c, 0], [0, 0, 0, 1]], np.float32)
+    bad = {0: 6, 3: 9}
+    sp = sequence.SequencePath(B, n + 2, n_sequences=U, pipelined=True, **pipeline.CONFIGS["c2"])
+    try:
+        assert sp.refkf_fallback
+        for slot, t in bad.items():
+            sp.perturb_velocity(t, slot, V)
+        for _ in range(n):
+            sp.step()
+        tr, hist, fbh = sp.trajectory(), sp.history(), sp.fallback_history()
+        for slot in range(B):
+            got = {}
+
+            def rec(t, o, P):
+                got[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
+                          int(o["pose2"][0]["n_inliers"]), o["fallback"])
+            cpu = _oracle(sp, slot, n, on_frame=rec, refkf=True,
+                          perturb={bad[slot]: V} if slot in bad else None)
+            for t in range(1, n + 1):
+                want = 1 if bad.get(slot) == t else 0
+                assert got[t][4] == want and int(fbh[t, slot]) == want, (slot, t, got[t][4], int(fbh[t, slot]))
+                assert tuple(int(x) for x in hist[t, slot]) == tuple(int(x) for x in got[t][:4]), (slot, t)
+                assert tr[t, slot].tobytes() == cpu[t - 1].tobytes(), (slot, t)
     finally:
         sp.close()
