@@ -462,7 +462,8 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
                                         on_frame=rec, libm=order, ref_kf=ref,
-                                        local_map=sp.oracle_local_map(slot) if sp.local_mapping else None)
+                                        local_map=sp.oracle_local_map(slot) if sp.local_mapping else None,
+                                        refkf_of=sp.oracle_refkf(slot, vocab_text) if sp.refkf_fallback else None)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
             return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
 

@@ -110,7 +110,8 @@ def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes
         fi = oracle_step.FrameInputs(gray, depth, cam, geometry, inv_sigma2, (pfr, P), (lfr, LP), map_planes,
                                      boundary, min_size=min_size, pose_cfg=pose_cfg, local_seen=True,
                                      ref_kf=ref_kf if k == 0 else None,
-                                     refkf_fallback=refkf_of(t) if refkf_of and not (k == 0 and ref_kf) else None)
+                                     refkf_fallback=(lambda t=t: refkf_of(t)) if refkf_of and not (k == 0 and ref_kf)
+                                     else None)
         o = oracle_step.run(fi, orb, planes, supp_cap=supp_cap)
         T2 = np.asarray(o["pose2"][0]["Tcw"], np.float32).reshape(4, 4)
         P = OT.last_frame(o["proj_points"], o["match"], o["keep"], LP, o["local_match"], o["keys_un"], o["pose2"][1])

@@ -48,7 +48,8 @@ class FrameInputs:
         self.ref_kf = ref_kf
         # refkf_fallback: the reference keyframe TrackReferenceKeyFrame falls back to when TrackWithMotionModel
         # fails (Tracking.cc:318-324): ref_kf's fields plus points = its map points as spslam_proj_point records
-        # (the rows `row` indexes); None: the motion model's result is kept whatever it is
+        # (the rows `row` indexes), or a callable returning it (made only when the motion model fails); None: the
+        # motion model's result is kept whatever it is
         self.refkf_fallback = refkf_fallback
 
 
@@ -100,7 +101,7 @@ def run(fi: FrameInputs, orb, planes, chain=None, supp_cap=None):
         nmm += sum(1 for j, pl in enumerate(g1[2]) if pl["kind"] == 0 and not plo1[j])
         if nmo < 10 or nmm < 5:
             import oracle_bow
-            R = fi.refkf_fallback
+            R = fi.refkf_fallback() if callable(fi.refkf_fallback) else fi.refkf_fallback
             fv = R["vocab"].transform(do)                  # mCurrentFrame.ComputeBoW()
             bm, nbow = oracle_bow.search_by_bow(R["desc"], R["angle"], R["has_point"], R["fv"], do, ko["angle"], fv,
                                                 0.7, True)
