@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--config", default="c2")
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--max-inflight", type=int, default=0)
+    ap.add_argument("--no-refkf", action="store_true", help="without the TrackReferenceKeyFrame failure branch")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -28,6 +29,7 @@ def main():
     cfg = pipeline.CONFIGS[a.config]
     sp = sequence.SequencePath(1, a.frames + a.warmup + 2, n_sequences=1, device=0, pipelined=not a.serial,
                                lookahead=a.lookahead, max_inflight=a.max_inflight,
+                               refkf_fallback=False if a.no_refkf else None,
                                render_workers=min(16, os.cpu_count() or 1), **cfg)
     try:
         for _ in range(a.warmup):
@@ -45,7 +47,7 @@ def main():
         el = time.perf_counter() - t0
     finally:
         sp.close()
-    msg = f"B=1 {'serial' if a.serial else f'pipelined lookahead {a.lookahead} inflight {a.max_inflight}'}: {a.frames / el:.1f} frames/s"
+    msg = f"B=1{' no-refkf' if a.no_refkf else ''} {'serial' if a.serial else f'pipelined lookahead {a.lookahead} inflight {a.max_inflight}'}: {a.frames / el:.1f} frames/s"
     if lat:
         msg += f", latency p50 {np.percentile(lat, 50) * 1e3:.2f} ms p99 {np.percentile(lat, 99) * 1e3:.2f} ms"
     print(msg, flush=True)
