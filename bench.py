@@ -336,21 +336,35 @@ def closed_loop(cfg, device, B, steps, warmup, n_seq=16):
         for _ in range(warmup):
             sp.step()
         torch.cuda.synchronize()
+        if sp.local_mapping:
+            sp.lm_time = {"total_s": 0.0, "lba_s": 0.0}  # the timed steps' events only
         t0 = time.perf_counter()
         for _ in range(steps):
             sp.step()
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
         h = sp.history()
-        return {"value": B * steps / el, "unit": "frames/s", "slots": B, "sequences": n_seq, "steps": steps,
-                "warmup": warmup, "ms_per_step": el * 1e3 / steps,
-                "mean_matches": float(h[warmup + 1:, :, 0].mean()),
-                "mean_inliers_local_map": float(h[warmup + 1:, :, 3].mean()),
-                "local_bundle_adjustments": len(getattr(sp, "lm_runs", [])),
-                "kind": "tracked sequences (sp-slam_amd/sequence.py): motion model from the previous frame, "
-                        "TrackReferenceKeyFrame at frame 1" +
-                        (", deterministic LocalMapping with LocalBundleAdjustment every 10 frames"
-                         if sp.local_mapping else "")}
+        out = {"value": B * steps / el, "unit": "frames/s", "slots": B, "sequences": n_seq, "steps": steps,
+               "warmup": warmup, "ms_per_step": el * 1e3 / steps,
+               "mean_matches": float(h[warmup + 1:, :, 0].mean()),
+               "mean_inliers_local_map": float(h[warmup + 1:, :, 3].mean()),
+               "local_bundle_adjustments": len(getattr(sp, "lm_runs", [])),
+               "kind": "tracked sequences (sp-slam_amd/sequence.py): motion model from the previous frame, "
+                       "TrackReferenceKeyFrame at frame 1" +
+                       (" and where the motion model fails" if sp.refkf_fallback else "") +
+                       (", deterministic LocalMapping with LocalBundleAdjustment every 10 frames"
+                        if sp.local_mapping else "")}
+        if sp.refkf_fallback:
+            out["reference_keyframe_frames"] = int((sp.fallback_history()[warmup + 1:] == 1).sum())
+        if sp.local_mapping:
+            # the LocalMapping events are synchronous and mostly host bookkeeping (local_mapping.py, caller side):
+            # their wall time, the device LocalBundleAdjustment inside it, and the step without them
+            lt = sp.lm_time
+            out["local_mapping_wall_s"] = lt["total_s"]
+            out["local_mapping_device_lba_s"] = lt["lba_s"]
+            rest = max(el - lt["total_s"], 1e-9)
+            out["ms_per_step_without_local_mapping"] = rest * 1e3 / steps
+        return out
     finally:
         sp.close()
 

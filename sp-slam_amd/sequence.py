@@ -35,6 +35,8 @@ tracks sequence i % U (slots sharing a sequence carry identical, independent sta
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 import pipeline
@@ -446,6 +448,8 @@ class SequencePath(pipeline.HotPath):
             self.maps.append(m)
         self.lm_ba = L.LocalBA(self.ex, cfg=self.lm_cfg)
         self.lm_runs = []  # per LocalBundleAdjustment: (frame, results of slot 0..U-1)
+        # wall time of the LocalMapping events (host bookkeeping + the synchronous device LocalBundleAdjustment)
+        self.lm_time = {"total_s": 0.0, "lba_s": 0.0}
 
     def _local_mapping(self, t):
         """After keyframe frame t's tail: insert keyframe t / STEP into every sequence's map and, with more than
@@ -456,6 +460,7 @@ class SequencePath(pipeline.HotPath):
         torch, B, U, cap = self.torch, self.B, self.U, self.kp_cap
         j = t // synth.KEYFRAME_STEP
         self.main.synchronize()
+        t_lm0 = time.perf_counter()
         pf = self.d_pframes.cpu().numpy().view(SM.PROJ_FRAME_DTYPE)
         npp = B * cap * SM.PROJ_POINT_DTYPE.itemsize  # the last-frame sets (the keyframe sets follow)
         pp = self.d_ppoints[:npp].cpu().numpy().view(SM.PROJ_POINT_DTYPE).reshape(B, cap)
@@ -499,9 +504,11 @@ class SequencePath(pipeline.HotPath):
                 torch.zeros(max(npo, 1), dtype=torch.uint8, device="cuda"),
                 torch.zeros(max(nplo, 1), dtype=torch.uint8, device="cuda"),
                 torch.zeros(B * L.LBA_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")]
+        t_ba0 = time.perf_counter()
         self.lm_ba.batch_device(B, hdr, *[x.data_ptr() for x in ins], *[x.data_ptr() for x in outs],
                                 stream=self.stream)
         self.main.synchronize()
+        self.lm_time["lba_s"] += time.perf_counter() - t_ba0
         kf_o, pt_o, pl_o, po_o = (x.cpu().numpy() for x in outs[:4])
         res = outs[5].cpu().numpy().view(L.LBA_RESULT_DTYPE)
         run = []
@@ -531,6 +538,7 @@ class SequencePath(pipeline.HotPath):
         self.d_ppoints[:npp].copy_(torch.from_numpy(pp.view(np.uint8).reshape(-1)))
         self.d_pframes.copy_(torch.from_numpy(pf.view(np.uint8).reshape(-1)))
         self.lm_runs.append((t, run))
+        self.lm_time["total_s"] += time.perf_counter() - t_lm0
         torch.cuda.synchronize()
 
     # ---- per batch: frame t of every slot's sequence and its local map
