@@ -58,6 +58,8 @@ struct Sh {
     // member's buildSystem share (landmark-aligned edge range, its free poses)
     int p, m, T, gen, eb0, eb1, npown, bo0, bo1;
     uint64_t rmask;                     // this member's Schur block rows
+    uint64_t carry;                     // buildSystem: Hpl blocks touched by the landmark continuing into the next step
+    double csum[2][12];                 //   and its partial Hll / bl sums (by step parity)
     int pown[kMaxK];
     // LM / schedule state (every member computes it identically between barriers)
     int pass, it, max_it, robust, qmax, nBad, trials, its[2], stop, stopped, ok, need_err, done, accepted, fail;
@@ -1632,7 +1634,7 @@ __device__ __noinline__ void build_system() {
                 own_h = sg.y;
                 own_kb = sg.w & ((1 << 30) - 1);
                 end_row = min(sg.z, c0 + cnt) - c0;
-                touched = first ? 0ull : g.lm_amask[own_h];  // (lm_amask is free after the structure phase)
+                touched = first ? 0ull : s.carry;  // (only row 0 continues a landmark of the previous step)
             }
         }
         {
@@ -1659,7 +1661,7 @@ __device__ __noinline__ void build_system() {
                 RF[r] = f;
                 again |= f == 2;
             }
-            if (c0 + end_row != sg.z) g.lm_amask[own_h] = touched;
+            if (c0 + end_row != sg.z) s.carry = touched;  // (the chunk's last segment; read after two barriers)
             if (again) NSW[kW] = 1;
         }
 #ifdef SPSLAM_LBG_DIAG_BUILD
@@ -1715,7 +1717,8 @@ __device__ __noinline__ void build_system() {
                 const unsigned fl = (unsigned)sgm.w;
                 const int h = sgm.z;
                 auto dst = comp < 9 ? g.Hll + 9 * h + comp : g.bl + 3 * h + (comp - 9);
-                double a = (fl >> 30) & 1 ? *dst : 0.0;
+                // a landmark continuing from the previous step resumes from its partial sums in LDS
+                double a = (fl >> 30) & 1 ? s.csum[st & 1][comp] : 0.0;
                 int r = sgm.x;
                 for (; r + 4 <= sgm.y; r += 4) {
                     double v[4];
@@ -1730,8 +1733,12 @@ __device__ __noinline__ void build_system() {
                 }
                 for (; r < sgm.y; r++)
                     if (RI[r] != -2) a += TL[kSL * r + comp];
-                *dst = a;
-                if ((fl >> 31) && (comp == 0 || comp == 4 || comp == 8)) mx = fmax(mx, fabs(a));
+                if (fl >> 31) {
+                    *dst = a;
+                    if (comp == 0 || comp == 4 || comp == 8) mx = fmax(mx, fabs(a));
+                } else {
+                    s.csum[(st + 1) & 1][comp] = a;
+                }
             }
 #ifdef SPSLAM_LBG_DIAG_BUILD
             __syncthreads();
