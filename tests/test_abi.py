@@ -76,6 +76,9 @@ int main(void) {
   O(spslam_track_batch, point_outlier) O(spslam_track_batch, fx) O(spslam_track_batch, bf)
   O(spslam_track_batch, plane_outlier) O(spslam_track_batch, next_vertical) O(spslam_track_batch, problems)
   O(spslam_track_batch, seen) O(spslam_track_batch, velocity)
+  S(spslam_refkf_batch) O(spslam_refkf_batch, refkf_counts) O(spslam_refkf_batch, rows_stride)
+  O(spslam_refkf_batch, refkf_sets) O(spslam_refkf_batch, state) O(spslam_refkf_batch, refkf_assoc)
+  S(spslam_frame_region) O(spslam_frame_region, frame_bytes) O(spslam_frame_region, src_stride)
   return 0;
 }
 """
@@ -121,6 +124,11 @@ def test_struct_layouts_match_bindings(tmp_path):
     for key, off in got.items():
         if key.startswith("spslam_track_batch."):
             assert getattr(tb, key.split(".", 1)[1]).offset == off, key
+    for name, st in (("spslam_refkf_batch", spslam_track.RefkfBatch), ("spslam_frame_region", spslam_track.FrameRegion)):
+        assert got[name] == ctypes.sizeof(st), name
+        for key, off in got.items():
+            if key.startswith(name + "."):
+                assert getattr(st, key.split(".", 1)[1]).offset == off, key
 
 
 def test_fails_loudly_without_gpu():
