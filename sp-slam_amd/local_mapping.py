@@ -193,29 +193,34 @@ class SeqMap:
             k = book["kfs"][n]
             self.kfs[k]["Tcw"] = kf_out[n].reshape(4, 4).copy()
         rows = []
+        pts = np.asarray(pt_out, np.float32).reshape(-1, 3)
+        centers = {k: camera_center(kf["Tcw"]) for k, kf in self.kfs.items()}  # (the updated poses)
         for n, pid in enumerate(book["points"]):
             r = self.row_of[pid]
-            self.table[r]["xw"] = np.asarray(pt_out, np.float32).reshape(-1, 3)[n]
-            self.update_normal_and_depth(pid, r)
+            self.table[r]["xw"] = pts[n]
+            self.update_normal_and_depth(pid, r, centers)
             rows.append(r)
+        pls = np.asarray(pl_out, np.float32).reshape(-1, 4)
         for n, r in enumerate(book["planes"]):
-            self.planes[r]["world"] = np.asarray(pl_out, np.float32).reshape(-1, 4)[n]
+            self.planes[r]["world"] = pls[n]
         return np.array(rows, np.int64)
 
-    def update_normal_and_depth(self, pid, r):
-        """MapPoint::UpdateNormalAndDepth (MapPoint.cc:357-400), float arithmetic."""
+    def update_normal_and_depth(self, pid, r, centers=None):
+        """MapPoint::UpdateNormalAndDepth (MapPoint.cc:357-400), float arithmetic.  centers: the keyframes' camera
+        centres (camera_center of their current poses), when the caller has them."""
         obs = self.obs.get(pid, {})
         if not obs:
             return
+        center = (lambda i: centers[i]) if centers is not None else (lambda i: camera_center(self.kfs[i]["Tcw"]))
         X = self.table[r]["xw"].astype(np.float32)
         normal = np.zeros(3, np.float32)
         for i in sorted(obs):
-            v = X - camera_center(self.kfs[i]["Tcw"])
+            v = X - center(i)
             normal = normal + v / np.float32(np.linalg.norm(v.astype(np.float64)))
         ref = self.ref.get(pid, min(obs))
         if ref not in obs:
             ref = min(obs)
-        PC = X - camera_center(self.kfs[ref]["Tcw"])
+        PC = X - center(ref)
         dist = np.float32(np.linalg.norm(PC.astype(np.float64)))
         level = int(self.kfs[ref]["octave"][obs[ref]])
         maxd = np.float32(dist * self.scale[level])
