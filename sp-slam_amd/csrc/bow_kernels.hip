@@ -131,6 +131,11 @@ __global__ __launch_bounds__(kThreads) void bow_vectors_kernel(int cap, int P, i
     const int n = min(counts[f], cap);
     const int per = P / kThreads > 0 ? P / kThreads : 1;   // contiguous elements per thread
     const int lo = min(t * per, P), hi = min(lo + per, P);
+    // keys at positions >= n are ~0 (the maximum), so sorting the first power of two >= n gives the full sort's
+    // array: a frame with few features (none, when the caller masks it) does not pay for cap
+    int Pn = n > 0 ? 1 : 0;
+    while (Pn < n) Pn <<= 1;
+    Pn = min(Pn, P);
 
     // ---- BowVector: (word, feature) keys of the features that are not stop words
     int valid = 0;
@@ -141,7 +146,7 @@ __global__ __launch_bounds__(kThreads) void bow_vectors_kernel(int cap, int P, i
     }
     int m;
     block_exclusive_scan(valid, scan_tmp, &m);
-    bitonic_sort(key, P);
+    bitonic_sort(key, Pn);
     int heads = 0;
     for (int q = lo; q < hi; q++)
         heads += q < m && (q == 0 || (key[q] >> 32) != (key[q - 1] >> 32));
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(kThreads) void bow_vectors_kernel(int cap, int P, i
         key[q] = ok ? ((unsigned long long)s_node[fo + q] << 32) | (unsigned)q : ~0ull;
     }
     __syncthreads();
-    bitonic_sort(key, P);
+    bitonic_sort(key, Pn);
     heads = 0;
     for (int q = lo; q < hi; q++)
         heads += q < m && (q == 0 || (key[q] >> 32) != (key[q - 1] >> 32));

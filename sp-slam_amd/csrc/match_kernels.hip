@@ -49,6 +49,16 @@ __device__ __forceinline__ void ins3(uint32_t& b0, uint32_t& b1, uint32_t& b2, u
     b2 = n2;
 }
 
+// insert a key into the ascending kLocalKeys smallest (keys unique; kNone = +inf)
+__device__ __forceinline__ void insk(uint32_t (&b)[kLocalKeys], uint32_t x) {
+#pragma unroll
+    for (int q = 0; q < kLocalKeys; q++) {
+        const uint32_t lo = min(b[q], x);
+        x = max(b[q], x);
+        b[q] = lo;
+    }
+}
+
 __device__ __forceinline__ void mat3_mul(const float* T, const float* x, const float* c, bool transpose, double sign,
                                          float* y) {
 #pragma unroll
@@ -422,11 +432,11 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
 // ---------------------------------------------------------------------------
 // Tracking::SearchLocalPoints: isInFrustum + PredictScale per local point,
 // then ORBmatcher::SearchByProjection(F, vpMapPoints, th) (src/ORBmatcher.cc:
-// 45-130).  Same two-kernel shape: the window kernel keeps the 3 smallest keys
-// over the window (initially taken keypoints excluded); the in-order walk
-// needs the best AND the second best among the keypoints still free (the
-// ratio test), which the 3 keys give unless in-loop assignments took two of
-// them -- then the wave re-scans for both.
+// 45-130).  Same two-kernel shape: the window kernel keeps the kLocalKeys (6)
+// smallest keys over the window (initially taken keypoints excluded); the
+// in-order walk needs the best AND the second best among the keypoints still
+// free (the ratio test), which the keys give unless in-loop assignments took
+// all but one of them -- then the wave re-scans for both.
 __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_local_frame* __restrict__ frames,
                                                                 const spslam_local_point* __restrict__ points,
                                                                 int max_points, MatchCurrent C, MatchGeom g,
@@ -439,9 +449,12 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     const spslam_local_frame& F = frames[f];
     if (i >= F.n_points || i >= max_points) return;  // uniform over the point's lanes, as every return below
     LocalWindow w{};
-    w.best[0] = w.best[1] = w.best[2] = kNone;
-    w.kp[0] = w.kp[1] = w.kp[2] = -1;
-    w.oct[0] = w.oct[1] = w.oct[2] = -1;
+#pragma unroll
+    for (int q = 0; q < kLocalKeys; q++) {
+        w.best[q] = kNone;
+        w.kp[q] = -1;
+        w.oct[q] = -1;
+    }
     w.x0 = 1;
     w.x1 = 0;
     LocalWindow* W = win + (size_t)f * max_points + i;
@@ -514,8 +527,10 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     const float* uright = C.uright + (size_t)f * C.cap;
     const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;
-    // the window's cells dealt round-robin to the point's lanes, the lanes' 3 smallest keys merged (unique keys)
+    uint32_t bk[kLocalKeys];
+#pragma unroll
+    for (int q = 0; q < kLocalKeys; q++) bk[q] = kNone;
+    // the window's cells dealt round-robin to the point's lanes, the lanes' smallest keys merged (unique keys)
     const int nrows = y1 - y0 + 1, ncells = x1 >= x0 && nrows > 0 ? (x1 - x0 + 1) * nrows : 0;
     for (int cell = sub; cell < ncells; cell += kLGrp) {
         const int cx = cell / nrows, c = (x0 + cx) * kRows + y0 + (cell - cx * nrows);
@@ -523,25 +538,26 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
         for (int j = j0; j < j1; j++) {
             const int k = GI[j];
             if (tk && tk[k]) continue;
-            ins3(b0, b1, b2, candidate_key(mw, C, uright, desc, kun, j, k, d0, d1, g));
+            insk(bk, candidate_key(mw, C, uright, desc, kun, j, k, d0, d1, g));
         }
     }
 #pragma unroll
     for (int o = kLGrp / 2; o >= 1; o >>= 1) {
-        const uint32_t p0 = (uint32_t)__shfl_xor((int)b0, o), p1 = (uint32_t)__shfl_xor((int)b1, o),
-                       p2 = (uint32_t)__shfl_xor((int)b2, o);
-        ins3(b0, b1, b2, p0);
-        ins3(b0, b1, b2, p1);
-        ins3(b0, b1, b2, p2);
-    }
-    w.best[0] = b0; w.best[1] = b1; w.best[2] = b2;
-    // the keypoint and octave of each of the 3 keys (read by the in-order walk), resolved here
+        uint32_t pk[kLocalKeys];
 #pragma unroll
-    for (int q = 0; q < 3; q++)
-        if (w.best[q] != kNone) {
-            w.kp[q] = GI[w.best[q] & 0xfffff];
-            w.oct[q] = kun[w.kp[q]].octave;
+        for (int q = 0; q < kLocalKeys; q++) pk[q] = (uint32_t)__shfl_xor((int)bk[q], o);
+#pragma unroll
+        for (int q = 0; q < kLocalKeys; q++) insk(bk, pk[q]);
+    }
+    // the keypoint and octave of each key (read by the in-order walk), resolved here
+#pragma unroll
+    for (int q = 0; q < kLocalKeys; q++) {
+        w.best[q] = bk[q];
+        if (bk[q] != kNone) {
+            w.kp[q] = GI[bk[q] & 0xfffff];
+            w.oct[q] = (int8_t)kun[w.kp[q]].octave;
         }
+    }
     if (sub == 0) *W = w;
 }
 
@@ -564,14 +580,23 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
     for (int k = lane; k < n_kp; k += 64) claim[k] = ~0u;
     const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
     for (int k = lane; k < n_kp; k += 64) M[k] = -1;
-    for (int wd = lane; wd < words; wd += 64) {
-        uint32_t bits = 0;
-        if (tk)
-            for (int q = 0; q < 32; q++) {
-                const int k = wd * 32 + q;
-                if (k < n_kp && tk[k]) bits |= 1u << q;
-            }
-        taken[wd] = bits;
+    // the taken bits: 8 coalesced byte loads in flight per lane, two words per ballot (a lane building its own
+    // word byte by byte waited out 32 dependent loads per word)
+    const int wset = tk ? 2 * ((n_kp + 63) / 64) : 0;  // words written from the flags (the rest are zero)
+    for (int wd = wset + lane; wd < words; wd += 64) taken[wd] = 0u;
+    for (int base = 0; base < n_kp && tk; base += 64 * 8) {
+        uint8_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = base + 64 * u + lane;
+            v[u] = tk[min(k, n_kp - 1)] & (uint8_t)(k < n_kp);  // unconditional load: no wait at a branch join
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const unsigned long long m = __ballot(v[u] != 0);
+            const int wd = (base >> 5) + 2 * u;
+            if (lane < 2 && wd + lane < min(words, wset)) taken[wd + lane] = (uint32_t)(m >> (32 * lane));
+        }
     }
     __syncthreads();
     const LocalWindow* Wf = win + (size_t)f * max_points;
@@ -582,19 +607,29 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
     const float* uright = C.uright + (size_t)f * C.cap;
     const spslam_local_point* Pp = points + F.point_offset;
     int nm = 0;
+#ifdef SPSLAM_LA_DIAG  // diagnostic build: passes, serial stops and window re-scans per frame (device printf)
+    int d_pass = 0, d_stop = 0, d_rescan = 0;
+    const long long d_t0 = wall_clock64();
+#endif
     LocalWindow wn{};  // the next chunk's window states, loaded one chunk ahead
     if (lane < np) wn = Wf[lane];
     for (int c0 = 0; c0 < np; c0 += 64) {
         const int i = c0 + lane;
         int valid = 0;
-        uint32_t best[3] = {kNone, kNone, kNone};
-        int b[3] = {-1, -1, -1}, oc[3] = {-1, -1, -1};
+        uint32_t best[kLocalKeys];
+        int b[kLocalKeys], oc[kLocalKeys];
+#pragma unroll
+        for (int q = 0; q < kLocalKeys; q++) {
+            best[q] = kNone;
+            b[q] = -1;
+            oc[q] = -1;
+        }
         const LocalWindow w = wn;
         if (i + 64 < np) wn = Wf[i + 64];
         if (i < np) {
             valid = w.in_view;
 #pragma unroll
-            for (int q = 0; q < 3; q++) {
+            for (int q = 0; q < kLocalKeys; q++) {
                 best[q] = w.best[q];
                 if (valid && best[q] != kNone) {
                     b[q] = w.kp[q];  // resolved by the window kernel
@@ -603,7 +638,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
             }
         }
         // the reference's loop in passes (as in match_assign_kernel): every point still to do evaluates its best
-        // and second best free keys from its 3 smallest; the points before the first one that cannot be decided
+        // and second best free keys from its smallest keys; the points before the first one that cannot be decided
         // that way -- a re-scan, or one of its two keypoints taken by an earlier acceptance of the pass -- are
         // committed together; that point is walked alone and the next pass starts after it.
         const int m = min(64, np - c0);
@@ -615,12 +650,15 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
         };
         int start = 0;
         while (start < m) {
+#ifdef SPSLAM_LA_DIAG
+            d_pass++;
+#endif
             const bool act = lane >= start && lane < m && valid;
             uint32_t k1 = kNone, k2 = kNone;
             int b1 = -1, b2 = -1, o1 = -1, o2 = -1, nk = 0;
             if (act) {
 #pragma unroll
-                for (int q = 0; q < 3; q++) {
+                for (int q = 0; q < kLocalKeys; q++) {
                     if (best[q] == kNone) continue;
                     nk++;
                     if ((taken[b[q] >> 5] >> (b[q] & 31)) & 1) continue;
@@ -628,7 +666,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                     else if (k2 == kNone) { k2 = best[q]; b2 = b[q]; o2 = oc[q]; }
                 }
             }
-            const bool rescanl = act && nk == 3 && k2 == kNone;
+            const bool rescanl = act && nk == kLocalKeys && k2 == kNone;
             const bool acc = act && !rescanl && k1 != kNone && ratio_ok(k1, k2, o1, o2);
             // conflict: an earlier accepting lane of this pass takes my best or second-best keypoint
             if (acc) atomicMin(&claim[b1], (uint32_t)lane);
@@ -656,9 +694,12 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
             if (first >= m) break;
             const int L = first;
             start = L + 1;
+#ifdef SPSLAM_LA_DIAG
+            d_stop++;
+#endif
             k1 = kNone; k2 = kNone; b1 = -1; o1 = -1; o2 = -1; nk = 0;
 #pragma unroll
-            for (int q = 0; q < 3; q++) {
+            for (int q = 0; q < kLocalKeys; q++) {
                 const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
                 const int bq = __shfl(b[q], L), oq = __shfl(oc[q], L);
                 if (kq == kNone) continue;
@@ -667,8 +708,11 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                 if (k1 == kNone) { k1 = kq; b1 = bq; o1 = oq; }
                 else if (k2 == kNone) { k2 = kq; o2 = oq; }
             }
-            if (nk == 3 && k2 == kNone) {
-                // in-loop assignments took two of the 3 keys: best and second best over the window again
+            if (nk == kLocalKeys && k2 == kNone) {
+                // in-loop assignments took all but one of the keys: best and second best over the window again
+#ifdef SPSLAM_LA_DIAG
+                d_rescan++;
+#endif
                 const LocalWindow w = Wf[c0 + L];
                 MatchWindow mw{};
                 mw.u = w.u; mw.v = w.v; mw.r = w.rs;
@@ -720,6 +764,11 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
         }
     }
     if (lane == 0) nmatches[f] = nm;
+#ifdef SPSLAM_LA_DIAG
+    if (lane == 0)
+        printf("LA np %d nkp %d passes %d stops %d rescans %d matches %d us %.1f\n", np, n_kp, d_pass, d_stop,
+               d_rescan, nm, (double)(wall_clock64() - d_t0) * 0.01);
+#endif
 }
 
 }  // namespace match

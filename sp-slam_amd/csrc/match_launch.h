@@ -34,14 +34,18 @@ struct MatchWindow {
     float kang[3];           // and those keypoints' angles
 };
 
-// Local-map search state per point (SearchLocalPoints).
+// Local-map search state per point (SearchLocalPoints).  kLocalKeys smallest keys: the in-order walk re-scans a
+// point's window only when in-loop assignments took all but one of them (with 3 keys, 12 re-scans of ~10 us
+// each per B = 1 frame: most of the walk's time)
+constexpr int kLocalKeys = 6;
 struct LocalWindow {
     float u, v, rs, ur;      // mTrackProjX / Y, r * mvScaleFactors[level], mTrackProjXR
     int16_t x0, x1, y0, y1;
     int8_t level, in_view, pad[2];
-    uint32_t best[3];        // 3 smallest keys over the window without the initially taken keypoints
-    int32_t kp[3];           // their keypoints, -1: none
-    int32_t oct[3];          // and those keypoints' octaves
+    uint32_t best[kLocalKeys];  // smallest keys over the window without the initially taken keypoints
+    int32_t kp[kLocalKeys];     // their keypoints, -1: none
+    int8_t oct[kLocalKeys];     // and those keypoints' octaves
+    int8_t pad2[(8 - kLocalKeys % 8) % 8];
 };
 
 struct LocalConsts {

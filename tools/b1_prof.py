@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--max-inflight", type=int, default=0)
     ap.add_argument("--no-refkf", action="store_true", help="without the TrackReferenceKeyFrame failure branch")
+    ap.add_argument("--cprofile", default="", help="write the timed loop's host profile (pstats text) here")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -36,6 +37,11 @@ def main():
             sp.step()
         torch.cuda.synchronize()
         lat = []
+        prof = None
+        if a.cprofile:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for _ in range(a.frames):
             ts = time.perf_counter()
@@ -45,6 +51,15 @@ def main():
                 lat.append(time.perf_counter() - ts)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        if prof is not None:
+            import io
+            import pstats
+            prof.disable()
+            buf = io.StringIO()
+            st = pstats.Stats(prof, stream=buf)
+            st.sort_stats("tottime").print_stats(40)
+            st.sort_stats("cumulative").print_stats(40)
+            pathlib.Path(a.cprofile).write_text(f"{a.frames} frames, {el:.3f} s\n" + buf.getvalue())
     finally:
         sp.close()
     msg = f"B=1{' no-refkf' if a.no_refkf else ''} {'serial' if a.serial else f'pipelined lookahead {a.lookahead} inflight {a.max_inflight}'}: {a.frames / el:.1f} frames/s"
