@@ -162,13 +162,20 @@ __device__ __forceinline__ bool ldlt_solve(const double (*H)[6], double lambda, 
     return true;
 }
 
-// Four compute waves and one chain wave per problem.  The compute waves evaluate the edges (errors, Jacobians,
+// kComputeWaves compute waves and one chain wave per problem.  The compute waves evaluate the edges (errors, Jacobians,
 // quadratic-form terms, trial chi2) and stage one row per edge in an LDS ring; the chain wave adds the rows in
 // edge order as they arrive.  g2o's sums are serial (one dependent fp64 add per edge and value, ~13 ns each on
 // gfx950), so the ordered chains set the floor of every pass; with a wave of their own they run beside the
 // edge evaluation instead of after it.  (Measured before: one wave per problem frees SIMDs for the pipelined
 // extraction but makes the edge passes 4x longer -- a net loss.)
-constexpr int kComputeWaves = 4;
+// Seven compute waves: with ~250 VGPRs a SIMD holds 2 waves, so 7 + the chain wave is a full CU.  Against 4
+// compute waves (profiles/r05/ab_pose_waves.txt): B = 1 single sequence 654 -> 689 frames/s (the point rounds of
+// both passes spread over more lanes; the plane evaluations are one round either way), C2 step 6.40 -> 6.31 ms
+// (the workgroup's 158 KB of LDS pinned the CU already; now its waves fill it)
+#ifndef SPSLAM_POSE_COMPUTE_WAVES
+#define SPSLAM_POSE_COMPUTE_WAVES 7
+#endif
+constexpr int kComputeWaves = SPSLAM_POSE_COMPUTE_WAVES;
 constexpr int kCompute = 64 * kComputeWaves;
 constexpr int kThreads = kCompute + 64;
 constexpr int kWaves = kThreads / 64;
