@@ -40,6 +40,13 @@ def camera_center(Tcw):
     return (-(T[:3, :3].T.astype(np.float64) @ T[:3, 3].astype(np.float64))).astype(np.float32)
 
 
+def norm64(v):
+    """cv::norm of float 3-vectors (rows of v): squares summed in double in element order, then sqrt (OpenCV's
+    normL2Sqr accumulation: ((x^2 + y^2) + z^2))."""
+    d = np.asarray(v, np.float32).astype(np.float64)
+    return np.sqrt((d[..., 0] * d[..., 0] + d[..., 1] * d[..., 1]) + d[..., 2] * d[..., 2])
+
+
 class SeqMap:
     """One sequence's map.  table: every keyframe's own points (spslam_local_point records, keyframe order) --
     the local-map point table SearchLocalPoints reads; planes: the sequence's map planes (spslam_map_plane)."""
@@ -145,18 +152,28 @@ class SeqMap:
             K[n]["id"] = k
             K[n]["fixed"] = 1 if (k not in lset or k == 0) else 0  # fixed cameras; KF 0 setFixed(mnId == 0)
         P = np.zeros(len(points), L.LBA_POINT_DTYPE)
-        PO, src = [], []
+        # observations in point order, each point's keyframes ascending; gathered from the keyframes' arrays at once
+        src, ob_kf, ob_kp, n_obs = [], [], [], np.zeros(len(points), np.int32)
         for n, pid in enumerate(points):
-            P[n]["xw"] = self.table[self.row_of[pid]]["xw"]
-            P[n]["id"] = pid
-            P[n]["obs_offset"] = len(PO)
-            for i in sorted(self.obs[pid]):
-                kp = self.obs[pid][i]
-                kf = self.kfs[i]
-                PO.append((kidx[i], kf["keys"][kp, 0], kf["keys"][kp, 1], kf["ur"][kp],
-                           self.inv_sigma2[kf["octave"][kp]]))
+            obs = self.obs[pid]
+            ks = sorted(obs)
+            n_obs[n] = len(ks)
+            for i in ks:
                 src.append((pid, i))
-            P[n]["n_obs"] = len(PO) - P[n]["obs_offset"]
+                ob_kf.append(i)
+                ob_kp.append(obs[i])
+        rows = np.fromiter((self.row_of[pid] for pid in points), np.int64, len(points))
+        P["xw"] = self.table["xw"][rows]
+        P["id"] = np.asarray(points, np.int64)
+        P["n_obs"] = n_obs
+        P["obs_offset"] = np.concatenate([[0], np.cumsum(n_obs)[:-1]]) if len(points) else n_obs
+        po = np.zeros(len(src), L.LBA_POINT_OBS_DTYPE)
+        if src:
+            keys, ur, octv, base = self._kf_arrays()
+            g = base[np.asarray(ob_kf, np.int64)] + np.asarray(ob_kp, np.int64)
+            po["kf"] = np.fromiter((kidx[i] for i in ob_kf), np.int32, len(ob_kf))
+            po["u"], po["v"], po["ur"] = keys[g, 0], keys[g, 1], ur[g]
+            po["inv_sigma2"] = self.inv_sigma2[octv[g]]
         Q = np.zeros(len(planes), L.LBA_PLANE_DTYPE)
         QO = []
         for n, r in enumerate(planes):
@@ -167,7 +184,6 @@ class SeqMap:
                 for i, meas in sorted(self.plane_obs.get(r, {}).get(kind, {}).items()):
                     QO.append((kidx[i], code, meas))
             Q[n]["n_obs"] = len(QO) - Q[n]["obs_offset"]
-        po = np.array(PO, L.LBA_POINT_OBS_DTYPE) if PO else np.zeros(0, L.LBA_POINT_OBS_DTYPE)
         qo = np.zeros(len(QO), L.LBA_PLANE_OBS_DTYPE)
         for n, (k, code, meas) in enumerate(QO):
             qo[n]["kf"], qo[n]["kind"], qo[n]["meas"] = k, code, meas
@@ -177,37 +193,86 @@ class SeqMap:
         book = dict(kfs=kfs_order, n_local=len(local), points=points, planes=planes, src=src)
         return (prob, K, P, po, Q, qo), book
 
+    def _kf_arrays(self):
+        """Every keyframe's keypoints, mvuRight and octaves concatenated (keyframe id order) and each keyframe's
+        first row (indexed by keyframe id)."""
+        ids = sorted(self.kfs)
+        base = np.zeros(ids[-1] + 1, np.int64)
+        o = 0
+        for k in ids:
+            base[k] = o
+            o += len(self.kfs[k]["ur"])
+        return (np.concatenate([self.kfs[k]["keys"] for k in ids]), np.concatenate([self.kfs[k]["ur"] for k in ids]),
+                np.concatenate([self.kfs[k]["octave"] for k in ids]), base)
+
     # ---- the result (Optimizer.cc:1909-1977)
     def apply(self, book, kf_out, pt_out, pl_out, point_outlier, stopped):
         """Returns the table rows whose points moved (for the device copy of the table)."""
         if stopped == 1:
             return np.zeros(0, np.int64)
-        for (pid, i), bad in zip(book["src"], np.asarray(point_outlier)[:len(book["src"])]):
-            if bad:  # pKFi->EraseMapPointMatch(pMPi); pMPi->EraseObservation(pKFi)
-                kp = self.obs[pid].pop(i)
-                self.kfs[i]["mp"].pop(kp, None)
-                if self.ref.get(pid) == i and self.obs[pid]:
-                    self.ref[pid] = min(self.obs[pid])  # MapPoint::EraseObservation: mpRefKF = first observation
+        src = book["src"]
+        for b in np.flatnonzero(np.asarray(point_outlier)[:len(src)]):
+            pid, i = src[b]  # pKFi->EraseMapPointMatch(pMPi); pMPi->EraseObservation(pKFi)
+            kp = self.obs[pid].pop(i)
+            self.kfs[i]["mp"].pop(kp, None)
+            if self.ref.get(pid) == i and self.obs[pid]:
+                self.ref[pid] = min(self.obs[pid])  # MapPoint::EraseObservation: mpRefKF = first observation
         kf_out = np.asarray(kf_out, np.float32).reshape(-1, 16)
         for n in range(book["n_local"]):
             k = book["kfs"][n]
             self.kfs[k]["Tcw"] = kf_out[n].reshape(4, 4).copy()
-        rows = []
-        pts = np.asarray(pt_out, np.float32).reshape(-1, 3)
-        centers = {k: camera_center(kf["Tcw"]) for k, kf in self.kfs.items()}  # (the updated poses)
-        for n, pid in enumerate(book["points"]):
-            r = self.row_of[pid]
-            self.table[r]["xw"] = pts[n]
-            self.update_normal_and_depth(pid, r, centers)
-            rows.append(r)
+        points = book["points"]
+        rows = np.fromiter((self.row_of[pid] for pid in points), np.int64, len(points))
+        self.table["xw"][rows] = np.asarray(pt_out, np.float32).reshape(-1, 3)[:len(points)]
+        self.update_normals_and_depths(points, rows)
         pls = np.asarray(pl_out, np.float32).reshape(-1, 4)
         for n, r in enumerate(book["planes"]):
             self.planes[r]["world"] = pls[n]
-        return np.array(rows, np.int64)
+        return rows
+
+    def update_normals_and_depths(self, pids, rows):
+        """update_normal_and_depth for many points at once (same float operations in the same order: the
+        normal's terms are added keyframe by keyframe, one observation slot at a time over all points)."""
+        ids = sorted(self.kfs)
+        C = np.zeros((ids[-1] + 1, 3), np.float32)
+        for k in ids:
+            C[k] = camera_center(self.kfs[k]["Tcw"])  # (the updated poses)
+        keep, start, okf, rkf, rlev = [], [], [], [], []
+        for n, pid in enumerate(pids):
+            obs = self.obs.get(pid)
+            if not obs:
+                continue
+            ks = sorted(obs)
+            keep.append(n)
+            start.append(len(okf))
+            okf.extend(ks)
+            ref = self.ref.get(pid, ks[0])
+            if ref not in obs:
+                ref = ks[0]
+            rkf.append(ref)
+            rlev.append(int(self.kfs[ref]["octave"][obs[ref]]))
+        if not keep:
+            return
+        r = np.asarray(rows, np.int64)[np.asarray(keep)]
+        start = np.asarray(start, np.int64)
+        cnt = np.diff(np.append(start, len(okf)))
+        X = self.table["xw"][r].astype(np.float32)
+        V = np.repeat(X, cnt, axis=0) - C[np.asarray(okf, np.int64)]
+        T = V / norm64(V).astype(np.float32)[:, None]
+        normal = np.zeros_like(X)
+        for m in range(int(cnt.max())):
+            sel = np.flatnonzero(cnt > m)
+            normal[sel] = normal[sel] + T[start[sel] + m]
+        dist = norm64(X - C[np.asarray(rkf, np.int64)]).astype(np.float32)
+        maxd = (dist * self.scale[np.asarray(rlev, np.int64)]).astype(np.float32)
+        self.table["max_dist"][r] = maxd
+        self.table["min_dist"][r] = (maxd / self.scale[-1]).astype(np.float32)
+        self.table["normal"][r] = normal / cnt.astype(np.float32)[:, None]
 
     def update_normal_and_depth(self, pid, r, centers=None):
-        """MapPoint::UpdateNormalAndDepth (MapPoint.cc:357-400), float arithmetic.  centers: the keyframes' camera
-        centres (camera_center of their current poses), when the caller has them."""
+        """MapPoint::UpdateNormalAndDepth (MapPoint.cc:357-400) for one point, float arithmetic (the scalar
+        statement update_normals_and_depths follows).  centers: the keyframes' camera centres, when the caller
+        has them."""
         obs = self.obs.get(pid, {})
         if not obs:
             return
@@ -216,12 +281,12 @@ class SeqMap:
         normal = np.zeros(3, np.float32)
         for i in sorted(obs):
             v = X - center(i)
-            normal = normal + v / np.float32(np.linalg.norm(v.astype(np.float64)))
+            normal = normal + v / np.float32(norm64(v))
         ref = self.ref.get(pid, min(obs))
         if ref not in obs:
             ref = min(obs)
         PC = X - center(ref)
-        dist = np.float32(np.linalg.norm(PC.astype(np.float64)))
+        dist = np.float32(norm64(PC))
         level = int(self.kfs[ref]["octave"][obs[ref]])
         maxd = np.float32(dist * self.scale[level])
         self.table[r]["max_dist"] = maxd
