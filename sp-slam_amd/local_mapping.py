@@ -82,7 +82,7 @@ class SeqMap:
                   ur=np.asarray(uright, np.float32)[:n].copy(), octave=np.asarray(octave, np.int32)[:n].copy(),
                   mp={}, planes=[])
         a, b = self.kf_rows[j]
-        own = {int(pid) - j * self.cap: int(pid) for pid in self.table["id"][a:b]}
+        own = {pid - j * self.cap: pid for pid in self.table["id"][a:b].tolist()}
         for kp in range(n):
             pid = matched.get(kp)
             if pid is None:
@@ -302,10 +302,9 @@ class SeqMap:
     def refresh_last_frame(self, P):
         """The last frame's map points after the write-back: positions from the table (by id)."""
         P = P.copy()
-        for n in range(len(P)):
-            r = self.row_of.get(int(P[n]["id"]))
-            if r is not None:
-                P[n]["xw"] = self.table[r]["xw"]
+        r = np.fromiter((self.row_of.get(i, -1) for i in P["id"].tolist()), np.int64, len(P))
+        k = np.flatnonzero(r >= 0)
+        P["xw"][k] = self.table["xw"][r[k]]
         return P
 
 
@@ -323,7 +322,7 @@ def insert_initial_keyframe(m, Tcw, kps, depth_u16, depth_factor, bf):
 def frame_keyframe_inputs(P_next, keys_un, uright, n_kp, pls, plout):
     """A tracked frame's keyframe data: its final matches (the next frame's last-frame points: keypoint index ->
     map point id), keypoints, mvuRight, octaves, and its final PoseOptimization's inlier plane edges."""
-    matched = {int(p["last_index"]): int(p["id"]) for p in P_next}
+    matched = dict(zip(P_next["last_index"].tolist(), P_next["id"].tolist()))
     k = np.asarray(keys_un)[:n_kp]
     octave = k["octave"] if k.dtype.names else np.asarray(k[:, 5]).view(np.int32)
     keys = np.stack([k["x"], k["y"]], 1) if k.dtype.names else np.asarray(k[:, :2], np.float32)
