@@ -9,7 +9,7 @@
 //                        projection and search window (redundantly per lane),
 //                        the window's grid cells spread over the lanes, every
 //                        candidate's Hamming distance (v_bcnt over the XOR of 8
-//                        dwords); keeps the 3 best as (distance << 20 | CSR
+//                        dwords); keeps the kProjKeys (6) best as (distance << 20 | CSR
 //                        position), which orders ties like the reference's
 //                        cell-by-cell scan, merged over the lanes (keys are
 //                        unique, so the merge is the serial scan's result);
@@ -41,18 +41,11 @@ constexpr int kGrp = 16, kPtsPerBlock = kThreads / kGrp;
 // local-map windows are a few cells (radius 2.5-4 px x scale): 4 lanes per local point
 constexpr int kLGrp = 4, kLPtsPerBlock = kThreads / kLGrp;
 
-// insert a key into an ascending triple (keys unique; kNone = +inf), keeping the 3 smallest
-__device__ __forceinline__ void ins3(uint32_t& b0, uint32_t& b1, uint32_t& b2, uint32_t x) {
-    const uint32_t n1 = min(b1, max(b0, x)), n2 = min(b2, max(b1, x));
-    b0 = min(b0, x);
-    b1 = n1;
-    b2 = n2;
-}
-
-// insert a key into the ascending kLocalKeys smallest (keys unique; kNone = +inf)
-__device__ __forceinline__ void insk(uint32_t (&b)[kLocalKeys], uint32_t x) {
+// insert a key into the ascending K smallest (keys unique; kNone = +inf)
+template <int K>
+__device__ __forceinline__ void insk(uint32_t (&b)[K], uint32_t x) {
 #pragma unroll
-    for (int q = 0; q < kLocalKeys; q++) {
+    for (int q = 0; q < K; q++) {
         const uint32_t lo = min(b[q], x);
         x = max(b[q], x);
         b[q] = lo;
@@ -93,7 +86,8 @@ __device__ __forceinline__ void direction(const spslam_proj_frame& F, const Matc
 }
 
 // Candidate test of GetFeaturesInArea + the stereo check; returns the key or kNone.
-__device__ __forceinline__ uint32_t candidate_key(const MatchWindow& w, const MatchCurrent& C, const float* uright,
+template <class Win>
+__device__ __forceinline__ uint32_t candidate_key(const Win& w, const MatchCurrent& C, const float* uright,
                                                   const uint8_t* desc, const spslam_keypoint* kun, int j, int k,
                                                   const uint4& d0, const uint4& d1, const MatchGeom& g) {
     const spslam_keypoint kp = kun[k];
@@ -113,21 +107,25 @@ __device__ __forceinline__ uint32_t candidate_key(const MatchWindow& w, const Ma
     return ((uint32_t)hamming(d0, d1, desc + 32 * (size_t)k) << 20) | (uint32_t)j;
 }
 
+template <int K>
 __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_proj_frame* __restrict__ frames,
                                                                 const spslam_proj_point* __restrict__ points,
                                                                 int max_points, MatchCurrent C, MatchGeom g, float th,
                                                                 int mono, int retry_below, int pass,
                                                                 const int* __restrict__ nmatches,
-                                                                MatchWindow* __restrict__ win) {
+                                                                MatchWindowK<K>* __restrict__ win) {
     tail_wave_priority();
     const int f = blockIdx.x, sub = threadIdx.x & (kGrp - 1);
     const int i = blockIdx.y * kPtsPerBlock + (int)(threadIdx.x / kGrp);
     const spslam_proj_frame& F = frames[f];
     if (pass == 1 && !(retry_below > 0 && nmatches[f] < retry_below)) return;
     if (i >= F.n_points || i >= max_points) return;  // uniform over the point's lanes, as every return below
-    MatchWindow w{};
-    w.best[0] = w.best[1] = w.best[2] = kNone;
-    w.kp[0] = w.kp[1] = w.kp[2] = -1;
+    MatchWindowK<K> w{};
+#pragma unroll
+    for (int q = 0; q < K; q++) {
+        w.best[q] = kNone;
+        w.kp[q] = -1;
+    }
     w.valid = 0;
     w.x0 = 1;
     w.x1 = 0;
@@ -138,7 +136,7 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     float x3Dc[3];
     mat3_mul(F.Tcw, p.xw, tcw, false, 1.0, x3Dc);
     const float invzc = (float)__ddiv_rn(1.0, (double)x3Dc[2]);
-    MatchWindow* W = win + (size_t)f * max_points + i;
+    MatchWindowK<K>* W = win + (size_t)f * max_points + i;
     if (invzc < 0) { if (sub == 0) *W = w; return; }
     const float u = __fmaf_rn(__fmul_rn(g.fx, x3Dc[0]), invzc, g.cx);
     const float v = __fmaf_rn(__fmul_rn(g.fy, x3Dc[1]), invzc, g.cy);
@@ -164,38 +162,45 @@ __global__ __launch_bounds__(kThreads) void match_window_kernel(const spslam_pro
     const uint8_t* desc = C.desc + (size_t)f * C.cap * 32;
     const float* uright = C.uright + (size_t)f * C.cap;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-    uint32_t b0 = kNone, b1 = kNone, b2 = kNone;
+    uint32_t bk[K];
+#pragma unroll
+    for (int q = 0; q < K; q++) bk[q] = kNone;
     // the window's cells (column-major, as the reference scans them) dealt round-robin to the point's lanes;
     // x1 < x0 or y1 < y0 (an empty range) gives no cells
     const int nrows = y1 - y0 + 1, ncells = x1 >= x0 && nrows > 0 ? (x1 - x0 + 1) * nrows : 0;
     for (int cell = sub; cell < ncells; cell += kGrp) {
         const int cx = cell / nrows, c = (x0 + cx) * kRows + y0 + (cell - cx * nrows);
         const int j0 = GO[c], j1 = GO[c + 1];
-        for (int j = j0; j < j1; j++) ins3(b0, b1, b2, candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g));
+        for (int j = j0; j < j1; j++) insk(bk, candidate_key(w, C, uright, desc, kun, j, GI[j], d0, d1, g));
     }
 #pragma unroll
     for (int o = kGrp / 2; o >= 1; o >>= 1) {
-        const uint32_t p0 = (uint32_t)__shfl_xor((int)b0, o), p1 = (uint32_t)__shfl_xor((int)b1, o),
-                       p2 = (uint32_t)__shfl_xor((int)b2, o);
-        ins3(b0, b1, b2, p0);
-        ins3(b0, b1, b2, p1);
-        ins3(b0, b1, b2, p2);
+        uint32_t pk[K];
+#pragma unroll
+        for (int q = 0; q < K; q++) pk[q] = (uint32_t)__shfl_xor((int)bk[q], o);
+#pragma unroll
+        for (int q = 0; q < K; q++) insk(bk, pk[q]);
     }
-    // lanes 0..2 resolve best[sub]'s keypoint and angle (read by the in-order walk)
-    const uint32_t mine = sub == 0 ? b0 : (sub == 1 ? b1 : b2);
-    if (sub < 3 && mine != kNone) {
+    // lanes 0 .. K-1 resolve best[sub]'s keypoint and angle (read by the in-order walk)
+    static_assert(K <= kGrp, "a lane per key");
+    uint32_t mine = kNone;
+#pragma unroll
+    for (int q = 0; q < K; q++)
+        if (sub == q) mine = bk[q];
+    if (sub < K && mine != kNone) {
         const int k = GI[mine & 0xfffff];
         W->kp[sub] = k;
         W->kang[sub] = kun[k].angle;
     }
     if (sub == 0) {
-        // kp / kang: written by lanes 0..2
+        // kp / kang: written by lanes 0 .. K-1
         W->u = w.u; W->v = w.v; W->r = w.r; W->invzc = w.invzc;
         W->x0 = w.x0; W->x1 = w.x1; W->y0 = w.y0; W->y1 = w.y1;
         W->min_level = w.min_level; W->max_level = w.max_level; W->valid = w.valid; W->pad = 0;
-        W->best[0] = b0; W->best[1] = b1; W->best[2] = b2;
+#pragma unroll
+        for (int q = 0; q < K; q++) W->best[q] = bk[q];
     }
-    if (sub < 3 && mine == kNone) W->kp[sub] = -1;
+    if (sub < K && mine == kNone) W->kp[sub] = -1;
 }
 
 // ComputeThreeMaxima
@@ -219,10 +224,11 @@ __device__ void three_maxima(const int* h, int* i1, int* i2, int* i3) {
     *i1 = ind1; *i2 = ind2; *i3 = ind3;
 }
 
+template <int K>
 __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_frame* __restrict__ frames,
                                                           const spslam_proj_point* __restrict__ points, int max_points,
                                                           MatchCurrent C, MatchGeom g, int check_ori, int retry_below,
-                                                          int pass, const MatchWindow* __restrict__ win,
+                                                          int pass, const MatchWindowK<K>* __restrict__ win,
                                                           int2* __restrict__ pushes, int32_t* __restrict__ match,
                                                           int* __restrict__ nmatches) {
     tail_wave_priority();
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     for (int k = lane; k < words; k += 64) taken[k] = 0;
     if (lane < kHisto) hist[lane] = 0;
     __syncthreads();
-    const MatchWindow* Wf = win + (size_t)f * max_points;
+    const MatchWindowK<K>* Wf = win + (size_t)f * max_points;
     const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
     const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
     const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
@@ -253,27 +259,37 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
     int2* PU = pushes + (size_t)f * max_points;
     const float factor = __fdiv_rn(1.0f, (float)kHisto);
     int n_push = 0;
+#ifdef SPSLAM_LA_DIAG  // diagnostic build: passes, serial stops and window re-scans per frame (device printf)
+    int d_pass = 0, d_stop = 0, d_rescan = 0;
+    const long long d_t0 = wall_clock64();
+#endif
     // every lane fetches its point's precomputed state, one round of loads per 64 points, issued one chunk
     // ahead (in flight during the previous chunk's walk) ...
-    MatchWindow wn{};
+    MatchWindowK<K> wn{};
     int nobs_n = 0;
     float pang_n = 0.f;
     if (lane < np) { wn = Wf[lane]; nobs_n = P[lane].n_obs; pang_n = P[lane].angle; }
     for (int c0 = 0; c0 < np; c0 += 64) {
         const int i = c0 + lane;
         int valid = 0, blocking = 0;
-        uint32_t best[3] = {kNone, kNone, kNone};
-        int b[3] = {-1, -1, -1};
-        float kang[3] = {0.f, 0.f, 0.f};
+        uint32_t best[K];
+        int b[K];
+        float kang[K];
+#pragma unroll
+        for (int q = 0; q < K; q++) {
+            best[q] = kNone;
+            b[q] = -1;
+            kang[q] = 0.f;
+        }
         float pangle = 0.f;
-        const MatchWindow w = wn;
+        const MatchWindowK<K> w = wn;
         const int nobs = nobs_n;
         const float pang = pang_n;
         if (i + 64 < np) { wn = Wf[i + 64]; nobs_n = P[i + 64].n_obs; pang_n = P[i + 64].angle; }
         if (i < np) {
             valid = w.valid;
 #pragma unroll
-            for (int q = 0; q < 3; q++) {
+            for (int q = 0; q < K; q++) {
                 best[q] = w.best[q];
                 if (valid && best[q] != kNone) {
                     b[q] = w.kp[q];  // resolved by the window kernel
@@ -284,13 +300,16 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             pangle = pang;
         }
         // ... then the reference's loop over the 64 points, in passes: every point still to do takes the first of
-        // its 3 smallest keys whose keypoint is free; the points before the first one that cannot be decided
-        // that way -- all 3 keys taken (a window re-scan), or its keypoint taken by an earlier point of the pass
+        // its smallest keys whose keypoint is free; the points before the first one that cannot be decided
+        // that way -- all K keys taken (a window re-scan), or its keypoint taken by an earlier point of the pass
         // that blocks it (a map point with observations) -- are committed together, in order; that point is
         // then walked alone (the reference's step with the updated taken set) and the next pass starts after it.
         const int m = min(64, np - c0);
         int start = 0;
         while (start < m) {
+#ifdef SPSLAM_LA_DIAG
+            d_pass++;
+#endif
             uint32_t keyl = kNone;
             int bl = -1;
             float kangl = 0.f;
@@ -298,10 +317,10 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             const bool act = lane >= start && lane < m && valid;
             if (act) {
 #pragma unroll
-                for (int q = 0; q < 3; q++) {
+                for (int q = 0; q < K; q++) {
                     if (keyl != kNone || rescanl || best[q] == kNone) continue;
                     if (!((taken[b[q] >> 5] >> (b[q] & 31)) & 1)) { keyl = best[q]; bl = b[q]; kangl = kang[q]; }
-                    else if (q == 2) rescanl = true;
+                    else if (q == K - 1) rescanl = true;
                 }
             }
             const bool acc = act && !rescanl && keyl != kNone && (int)(keyl >> 20) <= kThHigh;
@@ -347,6 +366,9 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             if (first >= m) break;
+#ifdef SPSLAM_LA_DIAG
+            d_stop++;
+#endif
             // the point that stopped the pass, alone (the reference's step for it)
             const int L = first;
             uint32_t bestL = kNone;
@@ -354,17 +376,20 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
             float kangL = 0.f;
             bool rescan = false;
 #pragma unroll
-            for (int q = 0; q < 3; q++) {
+            for (int q = 0; q < K; q++) {
                 const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
                 const int bq = __shfl(b[q], L);
                 const float aq = __shfl(kang[q], L);
                 if (bestL != kNone || rescan || kq == kNone) continue;  // sorted: kNone ends the list
                 if (!((taken[bq >> 5] >> (bq & 31)) & 1)) { bestL = kq; bL = bq; kangL = aq; }
-                else if (q == 2) rescan = true;
+                else if (q == K - 1) rescan = true;
             }
             if (rescan) {
+#ifdef SPSLAM_LA_DIAG
+                d_rescan++;
+#endif
                 // an earlier point holds this keypoint: search the window again without the taken ones
-                const MatchWindow w = Wf[c0 + L];
+                const MatchWindowK<K> w = Wf[c0 + L];
                 const spslam_proj_point& p = P[c0 + L];
                 const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
                 uint32_t mn = kNone;
@@ -427,6 +452,11 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
         n -= removed;
     }
     if (lane == 0) nmatches[f] = n;
+#ifdef SPSLAM_LA_DIAG
+    if (lane == 0)
+        printf("MA pass %d np %d nkp %d passes %d stops %d rescans %d matches %d us %.1f\n", pass, np, n_kp, d_pass,
+               d_stop, d_rescan, n, (double)(wall_clock64() - d_t0) * 0.01);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -437,27 +467,28 @@ __global__ __launch_bounds__(64) void match_assign_kernel(const spslam_proj_fram
 // in-order walk needs the best AND the second best among the keypoints still
 // free (the ratio test), which the keys give unless in-loop assignments took
 // all but one of them -- then the wave re-scans for both.
+template <int K>
 __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_local_frame* __restrict__ frames,
                                                                 const spslam_local_point* __restrict__ points,
                                                                 int max_points, MatchCurrent C, MatchGeom g,
                                                                 LocalConsts P, const uint8_t* __restrict__ taken_in,
-                                                                LocalWindow* __restrict__ win,
+                                                                LocalWindowK<K>* __restrict__ win,
                                                                 uint8_t* __restrict__ in_view) {
     tail_wave_priority();
     const int f = blockIdx.x, sub = threadIdx.x & (kLGrp - 1);
     const int i = blockIdx.y * kLPtsPerBlock + (int)(threadIdx.x / kLGrp);
     const spslam_local_frame& F = frames[f];
     if (i >= F.n_points || i >= max_points) return;  // uniform over the point's lanes, as every return below
-    LocalWindow w{};
+    LocalWindowK<K> w{};
 #pragma unroll
-    for (int q = 0; q < kLocalKeys; q++) {
+    for (int q = 0; q < K; q++) {
         w.best[q] = kNone;
         w.kp[q] = -1;
         w.oct[q] = -1;
     }
     w.x0 = 1;
     w.x1 = 0;
-    LocalWindow* W = win + (size_t)f * max_points + i;
+    LocalWindowK<K>* W = win + (size_t)f * max_points + i;
     const spslam_local_point& p = points[F.point_offset + i];
     // points the frame already tracks (mnLastFrameSeen == the frame) are skipped before isInFrustum
     // (Tracking.cc:1396-1401); their mbTrackInView stays false
@@ -527,9 +558,9 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     const float* uright = C.uright + (size_t)f * C.cap;
     const uint8_t* tk = taken_in ? taken_in + (size_t)f * C.cap : nullptr;
     const uint4 d0 = *(const uint4*)p.desc, d1 = *(const uint4*)(p.desc + 16);
-    uint32_t bk[kLocalKeys];
+    uint32_t bk[K];
 #pragma unroll
-    for (int q = 0; q < kLocalKeys; q++) bk[q] = kNone;
+    for (int q = 0; q < K; q++) bk[q] = kNone;
     // the window's cells dealt round-robin to the point's lanes, the lanes' smallest keys merged (unique keys)
     const int nrows = y1 - y0 + 1, ncells = x1 >= x0 && nrows > 0 ? (x1 - x0 + 1) * nrows : 0;
     for (int cell = sub; cell < ncells; cell += kLGrp) {
@@ -543,15 +574,15 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     }
 #pragma unroll
     for (int o = kLGrp / 2; o >= 1; o >>= 1) {
-        uint32_t pk[kLocalKeys];
+        uint32_t pk[K];
 #pragma unroll
-        for (int q = 0; q < kLocalKeys; q++) pk[q] = (uint32_t)__shfl_xor((int)bk[q], o);
+        for (int q = 0; q < K; q++) pk[q] = (uint32_t)__shfl_xor((int)bk[q], o);
 #pragma unroll
-        for (int q = 0; q < kLocalKeys; q++) insk(bk, pk[q]);
+        for (int q = 0; q < K; q++) insk(bk, pk[q]);
     }
     // the keypoint and octave of each key (read by the in-order walk), resolved here
 #pragma unroll
-    for (int q = 0; q < kLocalKeys; q++) {
+    for (int q = 0; q < K; q++) {
         w.best[q] = bk[q];
         if (bk[q] != kNone) {
             w.kp[q] = GI[bk[q] & 0xfffff];
@@ -561,11 +592,12 @@ __global__ __launch_bounds__(kThreads) void local_window_kernel(const spslam_loc
     if (sub == 0) *W = w;
 }
 
+template <int K>
 __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_frame* __restrict__ frames,
                                                           const spslam_local_point* __restrict__ points,
                                                           int max_points, MatchCurrent C, MatchGeom g, LocalConsts P,
                                                           const uint8_t* __restrict__ taken_in,
-                                                          const LocalWindow* __restrict__ win,
+                                                          const LocalWindowK<K>* __restrict__ win,
                                                           int32_t* __restrict__ match, int* __restrict__ nmatches) {
     tail_wave_priority();
     extern __shared__ uint32_t taken[];  // [ceil(cap / 32)], then claim[cap]
@@ -599,7 +631,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
         }
     }
     __syncthreads();
-    const LocalWindow* Wf = win + (size_t)f * max_points;
+    const LocalWindowK<K>* Wf = win + (size_t)f * max_points;
     const int32_t* GO = C.grid_off + (size_t)f * (kCols * kRows + 1);
     const int32_t* GI = C.grid_idx + (size_t)f * C.cap;
     const spslam_keypoint* kun = C.kun + (size_t)f * C.cap;
@@ -611,25 +643,25 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
     int d_pass = 0, d_stop = 0, d_rescan = 0;
     const long long d_t0 = wall_clock64();
 #endif
-    LocalWindow wn{};  // the next chunk's window states, loaded one chunk ahead
+    LocalWindowK<K> wn{};  // the next chunk's window states, loaded one chunk ahead
     if (lane < np) wn = Wf[lane];
     for (int c0 = 0; c0 < np; c0 += 64) {
         const int i = c0 + lane;
         int valid = 0;
-        uint32_t best[kLocalKeys];
-        int b[kLocalKeys], oc[kLocalKeys];
+        uint32_t best[K];
+        int b[K], oc[K];
 #pragma unroll
-        for (int q = 0; q < kLocalKeys; q++) {
+        for (int q = 0; q < K; q++) {
             best[q] = kNone;
             b[q] = -1;
             oc[q] = -1;
         }
-        const LocalWindow w = wn;
+        const LocalWindowK<K> w = wn;
         if (i + 64 < np) wn = Wf[i + 64];
         if (i < np) {
             valid = w.in_view;
 #pragma unroll
-            for (int q = 0; q < kLocalKeys; q++) {
+            for (int q = 0; q < K; q++) {
                 best[q] = w.best[q];
                 if (valid && best[q] != kNone) {
                     b[q] = w.kp[q];  // resolved by the window kernel
@@ -658,7 +690,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
             int b1 = -1, b2 = -1, o1 = -1, o2 = -1, nk = 0;
             if (act) {
 #pragma unroll
-                for (int q = 0; q < kLocalKeys; q++) {
+                for (int q = 0; q < K; q++) {
                     if (best[q] == kNone) continue;
                     nk++;
                     if ((taken[b[q] >> 5] >> (b[q] & 31)) & 1) continue;
@@ -666,7 +698,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                     else if (k2 == kNone) { k2 = best[q]; b2 = b[q]; o2 = oc[q]; }
                 }
             }
-            const bool rescanl = act && nk == kLocalKeys && k2 == kNone;
+            const bool rescanl = act && nk == K && k2 == kNone;
             const bool acc = act && !rescanl && k1 != kNone && ratio_ok(k1, k2, o1, o2);
             // conflict: an earlier accepting lane of this pass takes my best or second-best keypoint
             if (acc) atomicMin(&claim[b1], (uint32_t)lane);
@@ -699,7 +731,7 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
 #endif
             k1 = kNone; k2 = kNone; b1 = -1; o1 = -1; o2 = -1; nk = 0;
 #pragma unroll
-            for (int q = 0; q < kLocalKeys; q++) {
+            for (int q = 0; q < K; q++) {
                 const uint32_t kq = (uint32_t)__shfl((int)best[q], L);
                 const int bq = __shfl(b[q], L), oq = __shfl(oc[q], L);
                 if (kq == kNone) continue;
@@ -708,12 +740,12 @@ __global__ __launch_bounds__(64) void local_assign_kernel(const spslam_local_fra
                 if (k1 == kNone) { k1 = kq; b1 = bq; o1 = oq; }
                 else if (k2 == kNone) { k2 = kq; o2 = oq; }
             }
-            if (nk == kLocalKeys && k2 == kNone) {
+            if (nk == K && k2 == kNone) {
                 // in-loop assignments took all but one of the keys: best and second best over the window again
 #ifdef SPSLAM_LA_DIAG
                 d_rescan++;
 #endif
-                const LocalWindow w = Wf[c0 + L];
+                const LocalWindowK<K> w = Wf[c0 + L];
                 MatchWindow mw{};
                 mw.u = w.u; mw.v = w.v; mw.r = w.rs;
                 mw.invzc = 0.f;
@@ -780,15 +812,25 @@ hipError_t local_match_launch(int n_frames, const spslam_local_frame* frames, co
     // taken bits + the claim table in dynamic LDS (opted in up to 160 KB: caps up to ~39K keypoints)
     const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
     if (n_frames < 1 || max_points < 0 || cur.cap < 1 || lds > 160 * 1024) return hipErrorInvalidValue;
-    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::local_assign_kernel,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    static const hipError_t lds_attr = [] {
+        const hipError_t a = hipFuncSetAttribute((const void*)match::local_assign_kernel<kLocalKeys>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        return a != hipSuccess ? a : hipFuncSetAttribute((const void*)match::local_assign_kernel<kFewKeys>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    }();
     if (lds_attr != hipSuccess) return lds_attr;
     if (timer) timer->begin(kKindLocalMatch, s);
-    if (max_points > 0)
-        hipLaunchKernelGGL(match::local_window_kernel, dim3(n_frames, (max_points + match::kLPtsPerBlock - 1) / match::kLPtsPerBlock),
-                           dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, win, in_view);
-    hipLaunchKernelGGL(match::local_assign_kernel, dim3(n_frames), dim3(64), lds, s,
-                       frames, points, max_points, cur, g, P, taken_in, win, match, nmatches);
+    auto run = [&](auto* w) {
+        constexpr int K = sizeof(w->best) / sizeof(w->best[0]);
+        if (max_points > 0)
+            hipLaunchKernelGGL(match::local_window_kernel<K>,
+                               dim3(n_frames, (max_points + match::kLPtsPerBlock - 1) / match::kLPtsPerBlock),
+                               dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P, taken_in, w, in_view);
+        hipLaunchKernelGGL(match::local_assign_kernel<K>, dim3(n_frames), dim3(64), lds, s,
+                           frames, points, max_points, cur, g, P, taken_in, w, match, nmatches);
+    };
+    if (n_frames <= kSmallBatchKeys) run(win);
+    else run(reinterpret_cast<LocalWindowK<kFewKeys>*>(win));
     if (timer) timer->end(kKindLocalMatch, s);
     return hipGetLastError();
 }
@@ -800,19 +842,29 @@ hipError_t match_launch(int n_frames, const spslam_proj_frame* frames, const sps
     // taken bits + the claim table in dynamic LDS (opted in up to 150 KB: caps up to ~36K keypoints)
     const size_t lds = (size_t)((cur.cap + 31) / 32) * 4 + (size_t)cur.cap * 4;
     if (n_frames < 1 || max_points < 0 || cur.cap < 1 || lds > 150 * 1024) return hipErrorInvalidValue;
-    static const hipError_t lds_attr = hipFuncSetAttribute((const void*)match::match_assign_kernel,
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    static const hipError_t lds_attr = [] {
+        const hipError_t a = hipFuncSetAttribute((const void*)match::match_assign_kernel<kProjKeys>,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+        return a != hipSuccess ? a : hipFuncSetAttribute((const void*)match::match_assign_kernel<kFewKeys>,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    }();
     if (lds_attr != hipSuccess) return lds_attr;
     if (timer) timer->begin(kKindMatch, s);
     const int passes = P.retry_below > 0 ? 2 : 1;
-    for (int pass = 0; pass < passes; pass++) {
-        if (max_points > 0)
-            hipLaunchKernelGGL(match::match_window_kernel, dim3(n_frames, (max_points + match::kPtsPerBlock - 1) / match::kPtsPerBlock),
-                               dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P.th, P.mono,
-                               P.retry_below, pass, nmatches, win);
-        hipLaunchKernelGGL(match::match_assign_kernel, dim3(n_frames), dim3(64), lds, s, frames, points, max_points, cur,
-                           g, P.check_orientation, P.retry_below, pass, win, pushes, match, nmatches);
-    }
+    auto run = [&](auto* w) {
+        constexpr int K = sizeof(w->best) / sizeof(w->best[0]);
+        for (int pass = 0; pass < passes; pass++) {
+            if (max_points > 0)
+                hipLaunchKernelGGL(match::match_window_kernel<K>,
+                                   dim3(n_frames, (max_points + match::kPtsPerBlock - 1) / match::kPtsPerBlock),
+                                   dim3(match::kThreads), 0, s, frames, points, max_points, cur, g, P.th, P.mono,
+                                   P.retry_below, pass, nmatches, w);
+            hipLaunchKernelGGL(match::match_assign_kernel<K>, dim3(n_frames), dim3(64), lds, s, frames, points,
+                               max_points, cur, g, P.check_orientation, P.retry_below, pass, w, pushes, match, nmatches);
+        }
+    };
+    if (n_frames <= kSmallBatchKeys) run(win);
+    else run(reinterpret_cast<MatchWindowK<kFewKeys>*>(win));
     if (timer) timer->end(kKindMatch, s);
     return hipGetLastError();
 }

@@ -24,29 +24,35 @@ struct MatchCurrent {
     int cap;
 };
 
-// Per-point search state between the two kernels (scratch, n_frames * max_points entries).
-struct MatchWindow {
+// Per-point search state between the two kernels (scratch, n_frames * max_points entries), with the K smallest
+// keys per point: the in-order walks re-scan a point's window only when in-loop assignments took (all but one of)
+// them.  Small batches keep kProjKeys / kLocalKeys = 6 (with 3, a B = 1 frame re-scanned 2.6 last-frame and 12.5
+// local windows of ~10 us each); large batches keep 3, whose window kernels cost less (kSmallBatchKeys).  The
+// results do not depend on K.
+constexpr int kProjKeys = 6, kLocalKeys = 6, kFewKeys = 3, kSmallBatchKeys = 16;
+template <int K>
+struct MatchWindowK {
     float u, v, r, invzc;
-    int16_t x0, x1, y0, y1;  // GetFeaturesInArea cell range (x0 > x1: empty)
+    int16_t x0, x1, y0, y1;   // GetFeaturesInArea cell range (x0 > x1: empty)
     int8_t min_level, max_level, valid, pad;
-    uint32_t best[3];        // the 3 smallest (distance << 20) | CSR position over the window; ~0u: none
-    int32_t kp[3];           // their keypoints (grid_idx of the CSR position), -1: none
-    float kang[3];           // and those keypoints' angles
+    uint32_t best[K];          // the smallest (distance << 20) | CSR position over the window; ~0u: none
+    int32_t kp[K];             // their keypoints (grid_idx of the CSR position), -1: none
+    float kang[K];             // and those keypoints' angles
 };
+using MatchWindow = MatchWindowK<kProjKeys>;  // (the scratch is sized for the larger K)
 
-// Local-map search state per point (SearchLocalPoints).  kLocalKeys smallest keys: the in-order walk re-scans a
-// point's window only when in-loop assignments took all but one of them (with 3 keys, 12 re-scans of ~10 us
-// each per B = 1 frame: most of the walk's time)
-constexpr int kLocalKeys = 6;
-struct LocalWindow {
+// Local-map search state per point (SearchLocalPoints).
+template <int K>
+struct LocalWindowK {
     float u, v, rs, ur;      // mTrackProjX / Y, r * mvScaleFactors[level], mTrackProjXR
     int16_t x0, x1, y0, y1;
     int8_t level, in_view, pad[2];
-    uint32_t best[kLocalKeys];  // smallest keys over the window without the initially taken keypoints
-    int32_t kp[kLocalKeys];     // their keypoints, -1: none
-    int8_t oct[kLocalKeys];     // and those keypoints' octaves
-    int8_t pad2[(8 - kLocalKeys % 8) % 8];
+    uint32_t best[K];        // smallest keys over the window without the initially taken keypoints
+    int32_t kp[K];           // their keypoints, -1: none
+    int8_t oct[K];           // and those keypoints' octaves
+    int8_t pad2[(8 - K % 8) % 8];
 };
+using LocalWindow = LocalWindowK<kLocalKeys>;
 
 struct LocalConsts {
     float th, nn_ratio, view_cos_limit, log_scale_factor;
