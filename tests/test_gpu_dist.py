@@ -15,9 +15,12 @@ pytestmark = pytest.mark.gpu
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 
 
-def test_two_ranks_on_one_gpu():
-    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--rehearse-one-gpu", "--steps", "3",
-           "--warmup", "1", "--batch", "16", "--no-cpu-baseline", "--ate-frames", "0", "--closed-loop-steps", "0"]
+@pytest.mark.parametrize("config", ["c2", "c4"])
+def test_two_ranks_on_one_gpu(config):
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--config", config, "--gpus", "2", "--rehearse-one-gpu", "--steps",
+           "3", "--warmup", "1", "--batch", "16", "--no-cpu-baseline", "--ate-frames", "0", "--closed-loop-steps", "0"]
+    if config != "c2":
+        cmd += ["--single-sequence-frames", "0"]
     env = dict(os.environ, GPU_MAX_HW_QUEUES="8")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=str(ROOT))
     assert r.returncode == 0, r.stderr[-3000:]
