@@ -121,10 +121,8 @@ __global__ __launch_bounds__(kThreads) void frame_rgbd_kernel(
             const int i = i0 + lane;
             const int c = i < n ? cell_of[i] : -1;
             int rank = 0, tot = 0;
-            // lane l's cell by v_readlane (l is uniform): a scalar broadcast instead of an LDS permute round trip
-#pragma unroll 16
             for (int l = 0; l < 64; l++) {
-                const int cl = __builtin_amdgcn_readlane(c, l);
+                const int cl = __shfl(c, l);
                 if (cl == c) {
                     tot++;
                     if (l < lane) rank++;
