@@ -44,6 +44,12 @@ sys.path.insert(0, str(ROOT / "sp-slam_amd"))
 
 # HotPath parameters of each config: sp-slam_amd/pipeline.py CONFIGS (the YAML keys of the path)
 WORKLOADS = {
+    # BASELINE.json configs[0]: TUM fr3 structure_notexture_far, single sequence (the dataset is absent: a proxy)
+    "c1": "C1 (synthetic proxy of TUM fr3 structure_notexture_far, Examples/RGB-D/TUM3.yaml): the C2 room and boxes "
+          "with nearly untextured faces (~250 ORB keypoints per frame, most FAST cells decided by the minThFAST "
+          "retry) and a hand-held trajectory with 9-14 degree jolts on which the motion model fails and "
+          "TrackReferenceKeyFrame takes over; ORB + planes + supposed planes + 2x PoseOptimization; the "
+          "single_sequence line is the config's own (one sequence, B = 1)",
     # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, ORB + planes + PoseOptimization
     "c2": "C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud plane extraction + "
           "supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), no LBA",
@@ -435,6 +441,7 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
         import oracle_ctypes
         import oracle_grab
         import oracle_planes
+        import oracle_seq_inputs as OSI
         import oracle_sequence
         import oracle_step
         cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
@@ -464,20 +471,21 @@ def ate_sequences(cfg, device, n_frames=300, n_seq=2):
             if order == "fma":  # the pinned libm, contracted g2o arithmetic
                 with oracle_ctypes.g2o_fma(True):
                     return run_oracle(slot, oracle_ctypes.LIBM_CR)
-            frames, T0, P0, local_of = sp.oracle_inputs(slot)
+            frames, T0, P0, local_of = OSI.inputs(sp, slot)
             ch = {}
 
             def rec(t, o, P):
                 ch[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
                          int(o["pose2"][0]["n_inliers"]))
             orb, po = oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures), oracle_planes.PlaneOracle()
-            ref = oracle_sequence.reference_keyframe(sp.oracle_reference_keyframe(slot), vocab_text)
+            ref = oracle_sequence.reference_keyframe(OSI.reference_keyframe(sp, slot), vocab_text)
             cpu = oracle_sequence.track(frames[:n_frames], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map,
                                         sp.assoc_boundary, orb, po, supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                         pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
                                         on_frame=rec, libm=order, ref_kf=ref,
-                                        local_map=sp.oracle_local_map(slot) if sp.local_mapping else None,
-                                        refkf_of=sp.oracle_refkf(slot, vocab_text) if sp.refkf_fallback else None)
+                                        local_map=OSI.local_map(sp, slot) if sp.local_mapping else None,
+                                        refkf_of=OSI.refkf_of(sp, slot, vocab_text) if sp.refkf_fallback else None,
+                                        kf_id_stride=sp.kp_cap)
             same = [tuple(int(x) for x in hist[t, slot]) == ch[t] for t in range(1, n_frames + 1)]
             return cpu, next((t for t, ok in enumerate(same, 1) if not ok), None)
 
@@ -627,6 +635,9 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         hp.step()
+    # C3: the LocalBundleAdjustment calls of the timed steps still in flight (a pool thread launches each call, so one
+    # not yet enqueued would escape the synchronize) finish inside the timed region
+    hp.lba_drain()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()

@@ -930,6 +930,33 @@ typedef struct spslam_refkf_batch {
 int spslam_track_refkf_batch_device(spslam_ctx* ctx, int n_frames, int stage, const spslam_track_batch* mm,
                                     const spslam_refkf_batch* rk, void* hip_stream);
 
+/* The reference keyframe TrackReferenceKeyFrame uses (mpReferenceKF), per frame, batched.  TrackLocalMap's
+ * UpdateLocalKeyFrames sets it to pKFmax, the keyframe that observes the most of the frame's map points after
+ * TrackWithMotionModel's (or TrackReferenceKeyFrame's) discard, first maximum in keyframe order (src/Tracking.cc:
+ * 1459-1570; the reference iterates a std::map<KeyFrame*, int> in pointer order: keyframe id order here, as
+ * everywhere at this ABI); it is not run on a LOST frame (:406-409); CreateNewKeyFrame then makes the new keyframe
+ * the reference (:1258).  mm = the first graph's spslam_track_batch after the discard (and after the masked copy
+ * of a TrackReferenceKeyFrame re-tracking): the frame's map points are proj_points[point_offset +
+ * proj_match[i]] for every keypoint i with an edge that is not an outlier; a point's keyframe is id / ids_per_kf
+ * (each map point counted for the keyframe that created it).  Writes refkf_index[f] (kept where LOST or where no
+ * map point remains: pKFmax stays NULL), refkf_sets[2 f .. 2 f + 1] = kf_sets of it and, when refkf_pairs is
+ * given, the (keyframe, frame) pair of spslam_search_by_bow_batch_device. */
+typedef struct spslam_refkf_vote {
+    const int32_t* kf_base;     /* per frame: the index of its sequence's keyframe 0 in the keyframe tables */
+    const int32_t* kf_sets;     /* per keyframe: (point_offset, n_points) of its map points inside proj_points */
+    int32_t ids_per_kf;         /* map point id / ids_per_kf = the keyframe (of the sequence) that created it */
+    int32_t n_kf;               /* keyframes per sequence, 1 .. 1024 */
+    int32_t new_kf;             /* >= 0: the frames become keyframe new_kf of their sequence (CreateNewKeyFrame) */
+    int32_t pad;
+    const int8_t* state;        /* per frame: 2 = LOST (spslam_refkf_batch.state); may be NULL */
+    int32_t* refkf_index;       /* in / out: each frame's reference keyframe (kf_base + its keyframe) */
+    int32_t* refkf_sets;        /* out: (point_offset, n_points) of it */
+    int32_t* refkf_pairs;       /* out (may be NULL): (refkf_index, f) */
+} spslam_refkf_vote;
+
+int spslam_track_refkf_vote_batch_device(spslam_ctx* ctx, int n_frames, const spslam_track_batch* mm,
+                                         const spslam_refkf_vote* vote, void* hip_stream);
+
 /* dst[f] = src[f] for every frame f with flags[f] != 0, region by region: frame f's bytes at dst + f * dst_stride
  * and src + f * src_stride (sizes and strides multiples of 4; at most 32 regions per call). */
 typedef struct spslam_frame_region {

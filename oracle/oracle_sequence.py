@@ -9,7 +9,10 @@ frame (src/Tracking.cc:276-526) with the motion model --
   VO-match clean-up, outlier drop, mLastFrame = current    :456-505
 against a map of keyframe points on a fixed keyframe schedule (the harness's
 stand-in for LocalMapping; sp-slam_amd/sequence.py describes it), and, where the
-motion model fails, TrackReferenceKeyFrame against the latest keyframe (:318-324).  The first
+motion model fails, TrackReferenceKeyFrame against the reference keyframe (:318-324): mpReferenceKF,
+UpdateLocalKeyFrames' pKFmax after every tracked frame (:1459-1570, the keyframe that created the most of
+the frame's map points, first maximum in keyframe order; not on a LOST frame) or the keyframe a keyframe
+frame creates (CreateNewKeyFrame, :1258).  The first
 tracked frame has no velocity yet and runs TrackReferenceKeyFrame (:791-882:
 ComputeBoW, SearchByBoW against keyframe 0, the same graph / PoseOptimization /
 discard) when the keyframe's BoW inputs are given."""
@@ -63,7 +66,7 @@ def vocabulary(text):
 
 def reference_keyframe(ref, vocab_text):
     """ref = (keypoints, descriptors, has_point, row) of the reference keyframe (sequence.py
-    SequencePath.oracle_inputs) -> FrameInputs.ref_kf."""
+    oracle_seq_inputs.reference_keyframe) -> FrameInputs.ref_kf."""
     kps, desc, has, row = ref
     V = vocabulary(vocab_text)
     return dict(vocab=V, desc=desc, angle=kps["angle"], has_point=has, fv=V.transform(desc), row=row)
@@ -71,14 +74,15 @@ def reference_keyframe(ref, vocab_text):
 
 def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb, planes,
           supp_cap=None, min_size=500, pose_cfg=None, depth_scale=None, on_frame=None, libm=None, ref_kf=None,
-          local_map=None, on_lba=None, refkf_of=None, perturb=None):
+          local_map=None, on_lba=None, refkf_of=None, perturb=None, kf_id_stride=None):
     """frames: [(rgb, depth_u16)] of frames first .. ; T0 / P0: the pose and last-frame points of frame
     first - 1; local_of(t): the local map points of frame t (whole; the seen ones are skipped).  Returns the
     local-map pose (float 4x4) of every frame.  local_map: a sp-slam_amd/local_mapping.SeqMap (keyframe 0
     inserted) -- the deterministic LocalMapping after every keyframe frame, LocalBundleAdjustment by the CPU
     oracle (oracle/lba_oracle.cpp), the map it reads replaced by the SeqMap's (local points, map planes);
-    on_lba(t, result) sees each LocalBundleAdjustment.  refkf_of(t): FrameInputs.refkf_fallback of frame t (the
-    TrackWithMotionModel -> TrackReferenceKeyFrame switch; None: no fallback).  perturb: {t: 4x4 velocity} replacing
+    on_lba(t, result) sees each LocalBundleAdjustment.  refkf_of(j): FrameInputs.refkf_fallback of keyframe j (the
+    TrackWithMotionModel -> TrackReferenceKeyFrame switch against the reference keyframe; None: no fallback);
+    kf_id_stride: map point id // kf_id_stride = the keyframe that created it (the reference-keyframe vote).  perturb: {t: 4x4 velocity} replacing
     frame t's motion-model velocity (a test hook).  ref_kf: FrameInputs.ref_kf of frame `first` (reference_keyframe;
     None keeps the motion model with a constant-position prior there).  libm: the elementary functions of PoseOptimization
     (oracle_ctypes.LIBM_*) for this call, on the calling thread; None keeps the current one."""
@@ -87,10 +91,11 @@ def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes
         with oracle_ctypes.libm(libm):
             return track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes, boundary, orb,
                          planes, supp_cap, min_size, pose_cfg, depth_scale, on_frame, None, ref_kf, local_map, on_lba,
-                         refkf_of, perturb)
+                         refkf_of, perturb, kf_id_stride)
     Tlw = np.asarray(T0, np.float32).reshape(4, 4)
     V = np.eye(4, dtype=np.float32)  # the first tracked frame starts at the last frame's pose (SetPose(mLastFrame.mTcw))
     P = P0
+    ref_j = 0  # mpReferenceKF: keyframe 0 (StereoInitialization, :584)
     poses = []
     for k, (rgb, d) in enumerate(frames):
         t = first + k
@@ -110,9 +115,16 @@ def track(frames, first, T0, P0, local_of, cam, geometry, inv_sigma2, map_planes
         fi = oracle_step.FrameInputs(gray, depth, cam, geometry, inv_sigma2, (pfr, P), (lfr, LP), map_planes,
                                      boundary, min_size=min_size, pose_cfg=pose_cfg, local_seen=True,
                                      ref_kf=ref_kf if k == 0 else None,
-                                     refkf_fallback=(lambda t=t: refkf_of(t)) if refkf_of and not (k == 0 and ref_kf)
+                                     refkf_fallback=(lambda j=ref_j: refkf_of(j)) if refkf_of and not (k == 0 and ref_kf)
                                      else None)
         o = oracle_step.run(fi, orb, planes, supp_cap=supp_cap)
+        if kf_id_stride and o["fallback"] != 2:  # UpdateLocalKeyFrames (TrackLocalMap runs unless LOST)
+            ids = o["proj_points"]["id"][o["match"][o["keep"]]].astype(np.int64)
+            if len(ids):
+                ref_j = int(np.argmax(np.bincount(ids // kf_id_stride)))  # the first maximum
+        if t % KEYFRAME_STEP == 0:
+            ref_j = t // KEYFRAME_STEP  # CreateNewKeyFrame
+        o["reference_keyframe"] = ref_j
         T2 = np.asarray(o["pose2"][0]["Tcw"], np.float32).reshape(4, 4)
         P = OT.last_frame(o["proj_points"], o["match"], o["keep"], LP, o["local_match"], o["keys_un"], o["pose2"][1])
         V = OT.mat4(T2, OT.inverse_pose(Tlw))

@@ -228,6 +228,8 @@ struct Shared {
     double hb[kRed];                  // the iteration's H (lower, 21) and b (6), slot 0 unused
     SE3 tlast[kWaves];                // each wave's copy of the last trial pose (the relabel's active-edge pose)
     SE3 Eadd[12];                     // exp(+-1e-9 e_d), d = 0..5 (numeric Jacobian steps)
+    SE3 T0;                           // the input pose (every round restarts from it)
+    double xtrial[2][kSpec][6];       // each trial's applied solution, by trial pass parity (read after pass B)
     P4 pw[kPlaneChunk], pm[kPlaneChunk];  // plane edges' world / measured planes, normalized (nl <= kPlaneChunk)
     int done[kComputeWaves];          // rounds each compute wave has staged in the current pass
     int consumed;                     // rows the chain wave has added in the current pass
@@ -535,6 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         T0.r = q_from_rot(R);
         T0.t = V3{Tin[3], Tin[7], Tin[11]};
         q_normalize(T0.r);
+        if (t == 0) S.T0 = T0;  // read back at each round start: not held in registers across the rounds
     }
     __syncthreads();
 
@@ -616,7 +619,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     SE3 T;
     for (int round = 0; round < 4; round++) {
         PROF_MARK(0);  // setup / previous relabel
-        T = T0;
+        T = S.T0;
         // any active edge?
         int act = 0;
         for (int e = t; e < ne; e += kThreads) act |= !is_outlier(e);
@@ -817,6 +820,13 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                                 if (myq == q) x[j] = xe[j];
                         }
                     }
+                    // trial q's applied solution waits in LDS until the walk below knows the last trial run (kept in
+                    // registers it would stay live across pass B); the parity buffer orders it against the previous
+                    // pass's reads without a barrier
+                    if (t < kSpec) {
+#pragma unroll
+                        for (int j = 0; j < 6; j++) S.xtrial[total_passes & 1][t][j] = x[j];
+                    }
                     const SE3 Tt = se3_mul(se3_exp(x), T);
                     double scale = 0;  // OptimizationAlgorithmLevenberg::computeScale + 1e-3
 #pragma unroll
@@ -936,7 +946,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
                         S.tlast[wv] = tl;
                     }
 #pragma unroll
-                    for (int j = 0; j < 6; j++) xs[j] = readlane_d(x[j], lastq);  // the buffer after the last trial run
+                    for (int j = 0; j < 6; j++) xs[j] = S.xtrial[(total_passes - 1) & 1][lastq][j];  // the buffer after the last trial run
                     tValid = tValid || acc >= 0;
                     if (acc >= 0 && t < nl && nl <= kPlaneChunk) {  // thread t reads perrT[t] in the next pass A
 #pragma unroll
@@ -971,7 +981,11 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
             Te.t.x = was_out ? T.t.x : Tlast.t.x; Te.t.y = was_out ? T.t.y : Tlast.t.y; Te.t.z = was_out ? T.t.z : Tlast.t.z;
             return Te;
         };
-        for (int e = t; e < np; e += kThreads) {
+        // the loops' first indices are opaque here: hoisted out of the round loop, their 64-bit edge addresses
+        // were the kernel's only scratch spills (2 x 8 bytes per lane at 254 VGPRs, stored once per launch)
+        int e0 = t, j0 = t >> 1;
+        asm volatile("" : "+v"(e0), "+v"(j0));
+        for (int e = e0; e < np; e += kThreads) {
             double info[3], delta, err[3] = {0, 0, 0};
             edge_info(e, info, &delta);
             point_error_at(e, relabel_pose(pout[e] != 0), err, nullptr);
@@ -980,7 +994,7 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
             bad += bd ? 1.0 : 0.0;
             pout[e] = bd;
         }
-        for (int j = t >> 1; j < nl; j += kThreads / 2) {  // plane edges on lane pairs
+        for (int j = j0; j < nl; j += kThreads / 2) {  // plane edges on lane pairs
             double info[3], delta, err[3] = {0, 0, 0};
             edge_info(np + j, info, &delta);
             plane_error_pair_at(np + j, relabel_pose(plout[j] != 0), err);
@@ -1000,8 +1014,10 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
     }
     __syncthreads();
     if (S.stall) {  // every outlier flag set: nothing of a failed problem is kept (the tail's discard reads them)
-        for (int e = t; e < np; e += kThreads) pout[e] = 1;
-        for (int j = t; j < nl; j += kThreads) plout[j] = 1;
+        int e0 = t;
+        asm volatile("" : "+v"(e0));  // (no loop bound hoisted to the kernel's start, where it was spilled)
+        for (int e = e0; e < np; e += kThreads) pout[e] = 1;
+        for (int j = e0; j < nl; j += kThreads) plout[j] = 1;
     }
     if (t == 0 && S.stall) {
         // a bounded wait gave up (never observed): the sums are not valid, so the problem reports failure -- the

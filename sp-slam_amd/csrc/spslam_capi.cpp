@@ -1565,6 +1565,25 @@ int spslam_track_refkf_batch_device(spslam_ctx* c, int n_frames, int stage, cons
     return SPSLAM_OK;
 }
 
+int spslam_track_refkf_vote_batch_device(spslam_ctx* c, int n_frames, const spslam_track_batch* mm,
+                                         const spslam_refkf_vote* vote, void* hip_stream) {
+    if (!c) return SPSLAM_ERR_ARG;
+    if (n_frames < 1 || !mm || !vote)
+        return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_track_refkf_vote_batch_device");
+    const spslam_track_batch& b = *mm;
+    const spslam_refkf_vote& v = *vote;
+    if (v.n_kf < 1 || v.n_kf > 1024 || v.ids_per_kf < 1 || v.new_kf >= v.n_kf)
+        return fail(c, SPSLAM_ERR_ARG, "spslam_track_refkf_vote_batch_device: n_kf outside 1 .. 1024, ids_per_kf < 1 "
+                    "or new_kf >= n_kf%s", "");
+    const bool ok = b.kp_counts && b.cap >= 1 && b.cap <= (1 << 20) && b.proj_frames && b.proj_points &&
+                    b.proj_match && b.edge_of_kp && b.point_outlier && v.kf_base && v.kf_sets && v.refkf_index &&
+                    v.refkf_sets;
+    if (!ok) return fail(c, SPSLAM_ERR_ARG, "missing buffer for spslam_track_refkf_vote_batch_device%s", "");
+    HIP_CHECK(c, hipSetDevice(c->device));
+    HIP_CHECK(c, refkf_vote_launch(n_frames, b, v, (hipStream_t)hip_stream));
+    return SPSLAM_OK;
+}
+
 int spslam_masked_frame_copy_device(spslam_ctx* c, int n_frames, const uint8_t* flags, int n_regions,
                                     const spslam_frame_region* regions, void* hip_stream) {
     if (!c) return SPSLAM_ERR_ARG;

@@ -374,6 +374,53 @@ __global__ __launch_bounds__(kThreads) void refkf_kernel(spslam_track_batch B, s
     R.refkf_counts[f] = fb ? B.kp_counts[f] : 0;
 }
 
+// UpdateLocalKeyFrames' pKFmax (src/Tracking.cc:1459-1570) / CreateNewKeyFrame's new keyframe (:1258); see
+// spslam_gpu.h spslam_track_refkf_vote_batch_device.  One workgroup per frame: an LDS histogram of the frame's map
+// points over their keyframes, then the first maximum in keyframe order.
+constexpr int kMaxVoteKf = 1024;
+
+__global__ __launch_bounds__(kThreads) void refkf_vote_kernel(spslam_track_batch B, spslam_refkf_vote V) {
+    const int f = blockIdx.x, t = threadIdx.x;
+    if (V.new_kf < 0 && V.state && V.state[f] == 2) return;  // LOST: TrackLocalMap does not run
+    __shared__ int hist[kMaxVoteKf];
+    __shared__ int best_s;
+    const int nk = V.n_kf;
+    int best = -1;
+    if (V.new_kf < 0) {
+        for (int j = t; j < nk; j += kThreads) hist[j] = 0;
+        __syncthreads();
+        const int n = min(B.kp_counts[f], B.cap);
+        const size_t ko = (size_t)f * B.cap;
+        const spslam_proj_frame& PF = B.proj_frames[f];
+        for (int i = t; i < n; i += kThreads) {
+            const int e = B.edge_of_kp[ko + i];
+            if (e < 0 || B.point_outlier[ko + e]) continue;
+            const int j = B.proj_points[PF.point_offset + B.proj_match[ko + i]].id / V.ids_per_kf;
+            if (j >= 0 && j < nk) atomicAdd(&hist[j], 1);
+        }
+        __syncthreads();
+        if (t == 0) {
+            int mx = 0;
+            for (int j = 0; j < nk; j++)
+                if (hist[j] > mx) { mx = hist[j]; best = j; }  // if(it->second>max): the first maximum
+            best_s = best;
+        }
+        __syncthreads();
+        best = best_s;
+    } else {
+        best = V.new_kf;
+    }
+    if (t != 0) return;
+    const int q = best >= 0 ? V.kf_base[f] + best : V.refkf_index[f];  // no map point: pKFmax stays NULL
+    V.refkf_index[f] = q;
+    V.refkf_sets[2 * f] = V.kf_sets[2 * q];
+    V.refkf_sets[2 * f + 1] = V.kf_sets[2 * q + 1];
+    if (V.refkf_pairs) {
+        V.refkf_pairs[2 * f] = q;
+        V.refkf_pairs[2 * f + 1] = f;
+    }
+}
+
 // dst[f] = src[f] of every region for the flagged frames, 4 bytes per lane
 __global__ __launch_bounds__(256) void masked_frame_copy_kernel(const uint8_t* __restrict__ flags, FrameRegions G) {
     const int f = blockIdx.x;
@@ -388,6 +435,11 @@ __global__ __launch_bounds__(256) void masked_frame_copy_kernel(const uint8_t* _
 }
 
 }  // namespace
+
+hipError_t refkf_vote_launch(int n_frames, const spslam_track_batch& mm, const spslam_refkf_vote& v, hipStream_t s) {
+    hipLaunchKernelGGL(refkf_vote_kernel, dim3(n_frames), dim3(kThreads), 0, s, mm, v);
+    return hipGetLastError();
+}
 
 hipError_t refkf_launch(int n_frames, int stage, const spslam_track_batch& mm, const spslam_refkf_batch& rk,
                         hipStream_t s) {

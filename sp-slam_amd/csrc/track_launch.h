@@ -15,6 +15,8 @@ struct TrackArgs {
 
 hipError_t track_launch(int n_frames, int stage, const TrackArgs& a, hipStream_t s, KernelTimer* timer);
 
+// mpReferenceKF per frame (spslam_track_refkf_vote_batch_device)
+hipError_t refkf_vote_launch(int n_frames, const spslam_track_batch& mm, const spslam_refkf_vote& v, hipStream_t s);
 // TrackWithMotionModel's failure test and the TrackReferenceKeyFrame switch (spslam_track_refkf_batch_device)
 hipError_t refkf_launch(int n_frames, int stage, const spslam_track_batch& mm, const spslam_refkf_batch& rk,
                         hipStream_t s);

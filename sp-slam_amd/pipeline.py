@@ -49,6 +49,9 @@ import synth
 # 640x480 scenes hold 5 boxes: about 6 extracted planes and 0.4 supposed planes per frame (GeneratePlanesFromBoundries
 # accepts a boundary line only where a box edge is not an occlusion border; 3 boxes gave none on sequence 0)
 CONFIGS = {
+    # C1 proxy (TUM fr3 structure_notexture_far, Examples/RGB-D/TUM3.yaml): the C2 geometry with nearly untextured
+    # faces (synth._texture_low) and a hand-held trajectory with jolts (the motion model fails on them)
+    "c1": dict(width=640, height=480, nfeatures=1000, n_boxes=5, texture="low", motion="shaky"),
     "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=5),
     "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=5, lba_every=5),
     "c4": dict(width=640, height=480, nfeatures=1000, n_boxes=5, K=synth.ICL, min_size=1000, chi=1000.0,
@@ -66,7 +69,7 @@ class HotPath:
                  device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=False, min_size=500, chi=300.0, vp_chi=300.0,
                  rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1,
-                 max_inflight=0):
+                 max_inflight=0, texture="dots", motion="smooth"):
         import torch
         self.torch = torch
         self.B, self.W, self.H = B, width, height
@@ -85,7 +88,8 @@ class HotPath:
         self.min_size = min_size
         # Plane.AngleInfo / DistanceInfo / ParallelInfo / VerticalInfo / Chi / VPChi (Optimizer.cc:681-693)
         self.plane_cfg = G.PlaneConfig(1.0, 100.0, 0.5, 0.5, chi, vp_chi)
-        self.scene = synth.Scene(seq_id, n_boxes=n_boxes)
+        self.texture, self.motion = texture, motion
+        self.scene = synth.Scene(seq_id, n_boxes=n_boxes, texture=texture, motion=motion)
         self.ex = G.OrbExtractor(nfeatures=nfeatures, width=width, height=height, max_batch=B, device=device)
         self.pe = spslam_planes.PlaneExtractor(self.ex, self.fx, self.fy, self.cx, self.cy, width, height,
                                                min_size=min_size)

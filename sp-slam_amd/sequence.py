@@ -48,8 +48,8 @@ SEQ_STRIDE = 53
 
 
 def _render_job(args):
-    scene_seq, n_boxes, first, n, w, h, K, noise_base = args
-    sc = synth.Scene(scene_seq, n_boxes=n_boxes)
+    scene_seq, n_boxes, first, n, w, h, K, noise_base, style = args
+    sc = synth.Scene(scene_seq, n_boxes=n_boxes, **style)
     out = []
     for t in range(first, first + n):
         g, d, fid = sc.render(sc.pose(t), w, h, K=K, noise_seed=noise_base + t)
@@ -57,16 +57,18 @@ def _render_job(args):
     return out
 
 
-def render_sequences(seq_id, n_boxes, U, T, w, h, K, workers=0):
+def render_sequences(seq_id, n_boxes, U, T, w, h, K, workers=0, texture="dots", motion="smooth"):
     """frames[u][t] = (rgb, depth u16) of sequence u (scene seq_id, trajectory from SEQ_STRIDE * u)."""
-    jobs = [(seq_id, n_boxes, SEQ_STRIDE * u, T, w, h, K, seq_id * 100003) for u in range(U)]
+    style = dict(texture=texture, motion=motion)
+    jobs = [(seq_id, n_boxes, SEQ_STRIDE * u, T, w, h, K, seq_id * 100003, style) for u in range(U)]
     if workers and workers > 1:
         import concurrent.futures as cf
         import multiprocessing as mp
         chunks = []
-        for seq, nb, first, n, ww, hh, KK, nz in jobs:  # split sequences into chunks of frames
+        for seq, nb, first, n, ww, hh, KK, nz, tx in jobs:  # split sequences into chunks of frames
             step = max(1, -(-n // max(1, workers // len(jobs))))
-            chunks += [(seq, nb, f0, min(step, first + n - f0), ww, hh, KK, nz) for f0 in range(first, first + n, step)]
+            chunks += [(seq, nb, f0, min(step, first + n - f0), ww, hh, KK, nz, tx)
+                       for f0 in range(first, first + n, step)]
         with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn")) as pool:
             parts = list(pool.map(_render_job, chunks))
         out, k = [], 0
@@ -109,7 +111,8 @@ class SequencePath(pipeline.HotPath):
     def _setup_inputs(self, seq_id, unique_frames):
         torch, B, U, T = self.torch, self.B, self.U, self.T
         self.seq_id = seq_id
-        self.seq_frames = render_sequences(seq_id, self.n_boxes, U, T, self.W, self.H, self.K, self.render_workers)
+        self.seq_frames = render_sequences(seq_id, self.n_boxes, U, T, self.W, self.H, self.K, self.render_workers,
+                                           texture=self.texture, motion=self.motion)
         rgb = np.stack([self.seq_frames[u][t][0] for t in range(T) for u in range(U)])
         dep = np.stack([self.seq_frames[u][t][1] for t in range(T) for u in range(U)]).view(np.int16)
         self.d_rgb_all = torch.from_numpy(rgb).cuda()         # [T * U] frames, frame t of sequence u at t*U + u
@@ -306,12 +309,15 @@ class SequencePath(pipeline.HotPath):
 
     def _setup_refkf(self):
         """TrackWithMotionModel -> TrackReferenceKeyFrame (Tracking.cc:318-324): every keyframe's BoW side and the
-        rows of its map points (its point set in the projection buffer), frame t's reference keyframe = the latest
-        keyframe before it (the one the harness's local map ends with), and the re-tracking's own buffers."""
+        rows of its map points (its point set in the projection buffer), each slot's reference keyframe
+        (mpReferenceKF: keyframe 0 after StereoInitialization, then UpdateLocalKeyFrames' pKFmax or the keyframe just
+        created, spslam_track_refkf_vote_batch_device after every frame), and the re-tracking's own buffers."""
         import spslam_bow as SB
         import spslam_track as ST
         torch, B, U, cap, T = self.torch, self.B, self.U, self.kp_cap, self.T
         nkf = len(self.kf_t)
+        if nkf > 1024:
+            raise ValueError(f"{nkf} keyframes per sequence: the reference-keyframe vote holds at most 1024")
         i32 = dict(dtype=torch.int32, device="cuda")
         u8 = dict(dtype=torch.uint8, device="cuda")
         has = np.zeros((U * nkf, cap), np.uint8)
@@ -328,19 +334,17 @@ class SequencePath(pipeline.HotPath):
                                   self.d_kf_cnt.data_ptr(), self.kf_bow["nodes"].data_ptr(),
                                   self.kf_bow["start"].data_ptr(), self.kf_bow["features"].data_ptr(),
                                   self.kf_bow["n_fv"].data_ptr(), cap, 0)
-        # per frame t and slot: (reference keyframe's set offset, size), the SearchByBoW pair
-        sets = np.zeros((T, B, 2), np.int32)
-        pairs = np.zeros((T, B, 2), np.int32)
-        self.refkf_of = np.zeros((T, B), np.int64)
-        for t in range(1, T):
-            j = (t - 1) // synth.KEYFRAME_STEP
-            for i in range(B):
-                q = (i % self.U) * nkf + j
-                sets[t, i] = (self.kf_set_off[q], self.kf_set_len[q])
-                pairs[t, i] = (q, i)
-                self.refkf_of[t, i] = q
-        self.d_refkf_sets, self.d_refkf_pairs = torch.from_numpy(sets).cuda(), torch.from_numpy(pairs).cuda()
-        self.d_refkf_q = torch.from_numpy(self.refkf_of.astype(np.int32)).cuda()
+        # keyframe q = u * nkf + j: its map points' (offset, count) in the projection buffer; per slot its sequence's
+        # keyframe 0 (kf_base) and the current reference keyframe with its point set and SearchByBoW pair
+        kf_sets = np.stack([self.kf_set_off, self.kf_set_len], 1).astype(np.int32)
+        base = np.array([(i % U) * nkf for i in range(B)], np.int32)
+        self.d_kf_sets = torch.from_numpy(kf_sets).cuda()
+        self.d_kf_base = torch.from_numpy(base).cuda()
+        self.d_refkf_q = torch.from_numpy(base.copy()).cuda()
+        self.d_refkf_sets = torch.from_numpy(kf_sets[base].copy()).cuda()
+        self.d_refkf_pairs = torch.from_numpy(np.stack([base, np.arange(B, dtype=np.int32)], 1)).cuda()
+        self.refkf_hist = torch.zeros((T, B), **i32)  # [t][slot] the reference keyframe after frame t
+        self.refkf_hist[0].copy_(self.d_refkf_q)
         P = self.pe.planes_cap + self.pe.supp_cap
         self.fb = dict(
             fallback=torch.zeros(B, **u8), apply=torch.zeros(B, **u8), counts=torch.zeros(B, **i32),
@@ -363,14 +367,36 @@ class SequencePath(pipeline.HotPath):
                     n_fv=torch.zeros(n, **i32))
 
     def _after_motion_model(self):
+        """TrackWithMotionModel's verdict and, for the frames it fails, TrackReferenceKeyFrame (_refkf_fallback); then
+        the reference keyframe the next frame falls back to (_refkf_vote)."""
+        if not self.refkf_fallback:
+            return
+        if self.n_tracked > 0:  # frame 1 already tracks the reference keyframe
+            self._refkf_fallback()
+        self._refkf_vote()
+
+    def _refkf_vote(self):
+        """mpReferenceKF after frame t (spslam_track_refkf_vote_batch_device): TrackLocalMap's UpdateLocalKeyFrames
+        makes it pKFmax, the keyframe that created the most of the frame's map points after the discard
+        (Tracking.cc:1459-1570; not on a LOST frame), and a keyframe frame's CreateNewKeyFrame makes it the new
+        keyframe (:1258)."""
+        ST, torch = self._track_mod, self.torch
+        t = self.n_tracked + 1
+        v = ST.RefkfVote(kf_base=self.d_kf_base.data_ptr(), kf_sets=self.d_kf_sets.data_ptr(), ids_per_kf=self.kp_cap,
+                         n_kf=len(self.kf_t), new_kf=t // synth.KEYFRAME_STEP if t % synth.KEYFRAME_STEP == 0 else -1,
+                         state=self.fb_hist[t].data_ptr(), refkf_index=self.d_refkf_q.data_ptr(),
+                         refkf_sets=self.d_refkf_sets.data_ptr(), refkf_pairs=self.d_refkf_pairs.data_ptr())
+        self.track.refkf_vote_device(self.B, self._track_batch(0), v, stream=self.stream)
+        with torch.cuda.stream(self.main):
+            self.refkf_hist[t].copy_(self.d_refkf_q)
+
+    def _refkf_fallback(self):
         """TrackWithMotionModel's verdict and, for the frames it fails, TrackReferenceKeyFrame (Tracking.cc:318-324,
         791-882) on the device: ComputeBoW + SearchByBoW against the reference keyframe; where that finds >= 10
         matches, association, graph, PoseOptimization and discard from the last frame's pose over the keyframe's
         map points, moved over the motion model's outputs (spslam_track_refkf_batch_device,
         spslam_masked_frame_copy_device).  Frames where the motion model holds pass through every kernel as empty
         problems."""
-        if not self.refkf_fallback or self.n_tracked == 0:  # frame 1 already tracks the reference keyframe
-            return
         import spslam_bow as SB
         import spslam_planes as SP
         ST, torch, B, cap, fb = self._track_mod, self.torch, self.B, self.kp_cap, self.fb
@@ -379,8 +405,8 @@ class SequencePath(pipeline.HotPath):
         rk = ST.RefkfBatch(nmatches=self.d_nmatch.data_ptr(), fallback=fb["fallback"].data_ptr(),
                            refkf_counts=fb["counts"].data_ptr(), bow_nmatches=fb["bow_n"].data_ptr(),
                            bow_match=fb["bow_match"].data_ptr(), refkf_rows=self.d_kf_row.data_ptr(),
-                           refkf_index=self.d_refkf_q[t].data_ptr(), rows_stride=cap,
-                           refkf_sets=self.d_refkf_sets[t].data_ptr(), assoc_frames=self.d_afr1.data_ptr(),
+                           refkf_index=self.d_refkf_q.data_ptr(), rows_stride=cap,
+                           refkf_sets=self.d_refkf_sets.data_ptr(), assoc_frames=self.d_afr1.data_ptr(),
                            apply=fb["apply"].data_ptr(), state=self.fb_hist[t].data_ptr(),
                            refkf_match=fb["match"].data_ptr(), refkf_frames=fb["frames"].data_ptr(),
                            refkf_assoc=fb["assoc_frames"].data_ptr())
@@ -390,7 +416,7 @@ class SequencePath(pipeline.HotPath):
         fr = SB.BowSide(self.d_desc.data_ptr(), self.d_kps.data_ptr(), 0, fb["counts"].data_ptr(),
                         self.fr_bow["nodes"].data_ptr(), self.fr_bow["start"].data_ptr(),
                         self.fr_bow["features"].data_ptr(), self.fr_bow["n_fv"].data_ptr(), cap, 0)
-        SB.search_by_bow_batch_device(self.ex, B, self.d_refkf_pairs[t].data_ptr(), self.kf_side, fr,
+        SB.search_by_bow_batch_device(self.ex, B, self.d_refkf_pairs.data_ptr(), self.kf_side, fr,
                                       fb["bow_match"].data_ptr(), fb["bow_n"].data_ptr(), nn_ratio=0.7,
                                       check_orientation=True, stream=self.stream)
         self.track.refkf_device(B, ST.REFKF_SELECT, mm, rk, stream=self.stream)
@@ -609,35 +635,6 @@ class SequencePath(pipeline.HotPath):
             tr[0, i] = self._true_pose(i % self.U, 0).astype(np.float32)
         return tr
 
-    def oracle_reference_keyframe(self, slot):
-        """(keypoints, descriptors, has_point, row) of slot `slot`'s keyframe 0 -- the reference keyframe of frame
-        1's TrackReferenceKeyFrame -- for oracle_sequence.reference_keyframe (with synth.shape_vocabulary_text)."""
-        u = slot % self.U
-        n = int(self.d_kf0_cnt[u])
-        kps = self.d_kf0_kps[u, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
-        return kps, self.d_kf0_desc[u, :n].cpu().numpy(), self.kf0_has[u, :n], self.kf0_row[u, :n]
-
-    def oracle_refkf(self, slot, vocab_text):
-        """refkf_of(t) for oracle_sequence.track: frame t's reference keyframe (the latest keyframe before it) as
-        oracle_step.FrameInputs.refkf_fallback -- BoW inputs, feature -> row map and its map points."""
-        import oracle_sequence
-        u, nkf, cap = slot % self.U, len(self.kf_t), self.kp_cap
-        cache = {}
-
-        def of(t):
-            q = u * nkf + (t - 1) // synth.KEYFRAME_STEP
-            if q not in cache:
-                n = int(self.d_kf_cnt[q])
-                kps = self.d_kf_kps[q, :n].cpu().numpy().view(G.KEYPOINT_DTYPE).reshape(n)
-                has = self.d_kf_has[q, :n].cpu().numpy()
-                row = self.d_kf_row[q, :n].cpu().numpy()
-                R = oracle_sequence.reference_keyframe((kps, self.d_kf_desc[q, :n].cpu().numpy(), has, row), vocab_text)
-                j = (t - 1) // synth.KEYFRAME_STEP
-                R["points"] = synth.as_last_frame_points(self.kf_points[u, j], self.kf_kps[u, j], j * cap)
-                cache[q] = R
-            return cache[q]
-        return of
-
     def perturb_velocity(self, t, slot, V):
         """Test hook: frame t of slot `slot` predicts its pose from velocity V (4x4) instead of its predecessor's
         (a motion-model failure on demand); oracle_sequence.track(perturb={t: V}) is the CPU side."""
@@ -648,29 +645,7 @@ class SequencePath(pipeline.HotPath):
         self.torch.cuda.synchronize()
         return self.fb_hist[:self.n_tracked + 1].cpu().numpy()
 
-    def oracle_local_map(self, slot):
-        """A fresh local_mapping.SeqMap of slot `slot`'s sequence as it stood before frame 1 (keyframe 0
-        inserted), for the CPU oracle's copy of the deterministic LocalMapping."""
-        import local_mapping as LM
-        u = slot % self.U
-        tab = self.ex.tables()
-        m = LM.SeqMap([self.kf_points[u, j] for j in range(len(self.kf_t))], self.kp_cap,
-                      (self.fx, self.fy, self.cx, self.cy, self.bf), tab["scale"], tab["inv_sigma2"], self.assoc_map)
-        LM.insert_initial_keyframe(m, self._true_pose(u, 0).astype(np.float32), self.kf_kps[u, 0],
-                                   self.seq_frames[u][0][1], self.depth_factor, self.bf)
-        return m
-
-    def oracle_inputs(self, slot):
-        """Host copies of what slot `slot` tracks, for the CPU oracle (oracle/oracle_sequence.track): frames
-        1 .. T-1, the frame-0 pose and last-frame points, and frame t's whole local map."""
-        u = slot % self.U
-        P0 = synth.as_last_frame_points(self.kf_points[u, 0], self.kf_kps[u, 0], 0)
-        T0 = self._true_pose(u, 0).astype(np.float32)
-        allp = np.concatenate([self.kf_points[u, j] for j in range(len(self.kf_t))])
-        base = self.local_offsets[u, 0]
-
-        def local_of(t):
-            r = self.local_table[t, slot]
-            o = int(r["point_offset"]) - base
-            return allp[o:o + int(r["n_points"])]
-        return self.seq_frames[u][1:], T0, P0, local_of
+    def reference_keyframe_history(self):
+        """[t][slot]: the reference keyframe (keyframe index in the slot's sequence) after frame t."""
+        self.torch.cuda.synchronize()
+        return self.refkf_hist[:self.n_tracked + 1].cpu().numpy() - self.d_kf_base.cpu().numpy()[None, :]

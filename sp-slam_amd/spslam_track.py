@@ -4,7 +4,8 @@ bookkeeping between matching and Optimizer::PoseOptimization,
 src/Tracking.cc:951-1000, 1055-1068; src/Optimizer.cc:561-640, 681-860;
 spslam_track_refkf_batch_device + spslam_masked_frame_copy_device: the
 motion model's failure test and the TrackReferenceKeyFrame switch,
-src/Tracking.cc:318-324, 791-882)."""
+src/Tracking.cc:318-324, 791-882; spslam_track_refkf_vote_batch_device: the
+reference keyframe, UpdateLocalKeyFrames' pKFmax, :1459-1570)."""
 from __future__ import annotations
 
 import ctypes
@@ -15,7 +16,7 @@ MOTION_MODEL, DISCARD, LOCAL_MAP, MOTION_PRIOR, LAST_FRAME = 0, 1, 2, 3, 4
 REFKF_PREPARE, REFKF_SELECT = 0, 1
 
 spslam_gpu.EXPORTED += ["spslam_track_graph_batch_device", "spslam_track_refkf_batch_device",
-                        "spslam_masked_frame_copy_device"]
+                        "spslam_track_refkf_vote_batch_device", "spslam_masked_frame_copy_device"]
 
 _P = ctypes.c_void_p
 
@@ -46,6 +47,13 @@ class RefkfBatch(ctypes.Structure):
                 ("refkf_frames", _P), ("refkf_assoc", _P)]
 
 
+class RefkfVote(ctypes.Structure):
+    """struct spslam_refkf_vote (device pointers as ints)."""
+    _fields_ = [("kf_base", _P), ("kf_sets", _P), ("ids_per_kf", ctypes.c_int32), ("n_kf", ctypes.c_int32),
+                ("new_kf", ctypes.c_int32), ("pad", ctypes.c_int32), ("state", _P), ("refkf_index", _P),
+                ("refkf_sets", _P), ("refkf_pairs", _P)]
+
+
 class FrameRegion(ctypes.Structure):
     """struct spslam_frame_region."""
     _fields_ = [("dst", _P), ("src", _P), ("frame_bytes", ctypes.c_int64), ("dst_stride", ctypes.c_int64),
@@ -56,6 +64,7 @@ def _bind(lib):
     lib.spslam_track_graph_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P]
     lib.spslam_track_refkf_batch_device.argtypes = [_P, ctypes.c_int, ctypes.c_int, _P, _P, _P]
     lib.spslam_masked_frame_copy_device.argtypes = [_P, ctypes.c_int, _P, ctypes.c_int, _P, _P]
+    lib.spslam_track_refkf_vote_batch_device.argtypes = [_P, ctypes.c_int, _P, _P, _P]
 
 
 class TrackGraph:
@@ -72,6 +81,10 @@ class TrackGraph:
     def refkf_device(self, n_frames: int, stage: int, mm: TrackBatch, rk: RefkfBatch, stream=0):
         self.ex._check(self.ex.lib.spslam_track_refkf_batch_device(self.ex.ctx, n_frames, stage, ctypes.byref(mm),
                                                                     ctypes.byref(rk), stream or None))
+
+    def refkf_vote_device(self, n_frames: int, mm: TrackBatch, vote: RefkfVote, stream=0):
+        self.ex._check(self.ex.lib.spslam_track_refkf_vote_batch_device(self.ex.ctx, n_frames, ctypes.byref(mm),
+                                                                         ctypes.byref(vote), stream or None))
 
     def masked_copy_device(self, n_frames: int, flags: int, regions, stream=0):
         """regions: [(dst tensor, src tensor)] of n_frames equal rows each (contiguous, byte sizes multiple of 4)."""

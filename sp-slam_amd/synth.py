@@ -36,6 +36,20 @@ class Face:
     tex: int           # texture index
 
 
+def _jolts(rng: np.random.Generator, n_frames: int = 4096, gap=(18, 34), hold=(3, 7), deg=(9.0, 14.0)):
+    """Hand-held jolts of the "shaky" motion: (first frame, frame it ends, camera-frame axis-angle) -- a turn of
+    `deg` degrees about a random axis near the image plane's axes (yaw / pitch), held for `hold` frames, one
+    every `gap` frames."""
+    out, k = [], int(rng.integers(*gap))
+    while k < n_frames:
+        h = int(rng.integers(*hold))
+        ax = np.array([rng.normal(0, 1), rng.normal(0, 1), rng.normal(0, 0.2)])
+        ax /= np.linalg.norm(ax)
+        out.append((k, k + h, ax * np.deg2rad(rng.uniform(*deg))))
+        k += h + int(rng.integers(*gap))
+    return out
+
+
 def _texture(rng: np.random.Generator, size: int = 1024) -> np.ndarray:
     cells = rng.integers(0, 256, size=(size // 8, size // 8)).astype(np.float32)
     img = np.kron(cells, np.ones((8, 8), np.float32))
@@ -56,12 +70,55 @@ def _texture(rng: np.random.Generator, size: int = 1024) -> np.ndarray:
     return np.clip(10 + (img - lo) * (235.0 / max(hi - lo, 1e-3)), 10, 245).astype(np.float32)
 
 
-class Scene:
-    """Room 5 x 2.6 x 4 m (x right, y down, z forward) plus boxes on the floor."""
+def _wrap_blur(img: np.ndarray, sigma: float) -> np.ndarray:
+    """Periodic Gaussian blur (FFT; the textures tile the faces)."""
+    n = img.shape[0]
+    f = np.fft.fftfreq(n)
+    g = np.exp(-2.0 * (np.pi * sigma) ** 2 * f * f)
+    return np.real(np.fft.ifft2(np.fft.fft2(img) * np.outer(g, g))).astype(np.float32)
 
-    def __init__(self, seq_id: int = 0, n_boxes: int = 3, texel: float = 0.006):
+
+def _texture_low(rng: np.random.Generator, size: int = 1024, amp: float = 4.0, spots: int = 25) -> np.ndarray:
+    """A nearly untextured face (the C1 proxy, TUM fr3 structure_notexture_far): a flat albedo in [70, 190], a
+    smooth +-`amp` gray-level shading (blocks of 32 texels blurred with sigma 10 texels: no FAST corner at
+    minThFAST = 7 on its own) and `spots` faint stains (Gaussian blobs of 2-4 texels, contrast 10-30), so the
+    ORB features come from the structure's edges and corners plus a few stains and the per-cell FAST retry at
+    minThFAST (ORBextractor.cc:812-816) decides most cells."""
+    base = rng.uniform(70, 190)
+    cells = rng.normal(0, 1, (size // 32, size // 32)).astype(np.float32)
+    img = _wrap_blur(np.kron(cells, np.ones((32, 32), np.float32)), 10.0)
+    img *= amp / max(float(img.std()), 1e-6)
+    for _ in range(spots):
+        cy, cx = rng.uniform(0, size, 2)
+        r = rng.uniform(2.0, 4.0)
+        c = rng.uniform(10, 30) * rng.choice([-1, 1])
+        R = int(np.ceil(4 * r))
+        iy, ix = np.arange(int(cy) - R, int(cy) + R + 2), np.arange(int(cx) - R, int(cx) + R + 2)
+        d2 = (iy - cy)[:, None] ** 2 + (ix - cx)[None, :] ** 2
+        img[np.ix_(iy % size, ix % size)] += (c * np.exp(-d2 / (2 * r * r))).astype(np.float32)
+    return np.clip(base + img, 5, 250).astype(np.float32)
+
+
+class Scene:
+    """Room 5 x 2.6 x 4 m (x right, y down, z forward) plus boxes on the floor.
+
+    texture: "dots" (random-block texture: the C2-C5 scenes) or "low" (nearly untextured faces, _texture_low:
+    the C1 proxy); the geometry is the same for one seq_id either way.
+    motion: "smooth" (the C2-C5 trajectory) or "shaky" (the same trajectory with hand-held jolts, _jolts: the
+    camera turns by a few degrees from one frame to the next and back a few frames later -- the abrupt velocity
+    changes under which TrackWithMotionModel fails and TrackReferenceKeyFrame takes over, Tracking.cc:318-324)."""
+
+    def __init__(self, seq_id: int = 0, n_boxes: int = 3, texel: float = 0.006, texture: str = "dots",
+                 motion: str = "smooth"):
         self.rng = np.random.Generator(np.random.PCG64(0x5EED0000 + seq_id))
         self.texel = texel
+        if texture not in ("dots", "low"):
+            raise ValueError(f"texture {texture!r}")
+        if motion not in ("smooth", "shaky"):
+            raise ValueError(f"motion {motion!r}")
+        self.texture, self.motion = texture, motion
+        # jolts from their own generator: the scene (geometry, textures) does not depend on the motion
+        self.jolts = _jolts(np.random.Generator(np.random.PCG64(0x10175000 + seq_id))) if motion == "shaky" else []
         X0, X1, Y0, Y1, Z0, Z1 = -2.5, 2.5, -1.3, 1.3, -2.0, 3.5
         faces = [
             Face(0, X0, np.array([Y0, Z0]), np.array([Y1, Z1]), 0),
@@ -84,10 +141,18 @@ class Scene:
                     faces.append(Face(axis, float(off), lo[o].copy(), hi[o].copy(), ntex))
                     ntex += 1
         self.faces = faces
-        self.textures = [_texture(self.rng) for _ in range(ntex)]
+        make = _texture if texture == "dots" else _texture_low
+        self.textures = [make(self.rng) for _ in range(ntex)]
 
     def pose(self, i: int) -> np.ndarray:
         """Camera-to-world 4x4 at frame i (30 Hz)."""
+        T = self._smooth_pose(i)
+        for k0, k1, rv in self.jolts:
+            if k0 <= i < k1:  # the camera turned by rv (axis-angle, camera frame) at k0 and back at k1
+                T[:3, :3] = T[:3, :3] @ _rot(rv)
+        return T
+
+    def _smooth_pose(self, i: int) -> np.ndarray:
         t = i / 30.0
         yaw = 0.26 * np.sin(0.5 * t)
         pitch = -0.32 + 0.08 * np.sin(0.7 * t + 0.3)  # looking down at the floor and boxes
@@ -171,9 +236,10 @@ class Scene:
         return gray, depth, fid.astype(np.int16)
 
 
-def sequence(seq_id: int, n_frames: int, w: int = 640, h: int = 480, n_boxes: int = 3):
+def sequence(seq_id: int, n_frames: int, w: int = 640, h: int = 480, n_boxes: int = 3, texture: str = "dots",
+             motion: str = "smooth"):
     """Yields (Twc, gray, depth_u16) for n_frames frames of sequence seq_id."""
-    sc = Scene(seq_id, n_boxes=n_boxes)
+    sc = Scene(seq_id, n_boxes=n_boxes, texture=texture, motion=motion)
     for i in range(n_frames):
         T = sc.pose(i)
         g, d, _ = sc.render(T, w, h, noise_seed=seq_id * 100003 + i)
@@ -583,9 +649,9 @@ def as_last_frame_points(points, kps, id_base):
     return P
 
 
-def render_sequence_frames(seq_id, n_frames, w, h, K, n_boxes, first=0):
+def render_sequence_frames(seq_id, n_frames, w, h, K, n_boxes, first=0, texture="dots", motion="smooth"):
     """(colour RGB u8, depth u16) of frames first .. first + n_frames - 1 of a sequence (worker-pool friendly)."""
-    sc = Scene(seq_id, n_boxes=n_boxes)
+    sc = Scene(seq_id, n_boxes=n_boxes, texture=texture, motion=motion)
     out = []
     for t in range(first, first + n_frames):
         g, d, fid = sc.render(sc.pose(t), w, h, K=K, noise_seed=seq_id * 100003 + t)

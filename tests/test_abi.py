@@ -79,6 +79,8 @@ int main(void) {
   S(spslam_refkf_batch) O(spslam_refkf_batch, refkf_counts) O(spslam_refkf_batch, rows_stride)
   O(spslam_refkf_batch, refkf_sets) O(spslam_refkf_batch, state) O(spslam_refkf_batch, refkf_assoc)
   S(spslam_frame_region) O(spslam_frame_region, frame_bytes) O(spslam_frame_region, src_stride)
+  S(spslam_refkf_vote) O(spslam_refkf_vote, ids_per_kf) O(spslam_refkf_vote, new_kf) O(spslam_refkf_vote, state)
+  O(spslam_refkf_vote, refkf_sets) O(spslam_refkf_vote, refkf_pairs)
   return 0;
 }
 """
@@ -124,7 +126,8 @@ def test_struct_layouts_match_bindings(tmp_path):
     for key, off in got.items():
         if key.startswith("spslam_track_batch."):
             assert getattr(tb, key.split(".", 1)[1]).offset == off, key
-    for name, st in (("spslam_refkf_batch", spslam_track.RefkfBatch), ("spslam_frame_region", spslam_track.FrameRegion)):
+    for name, st in (("spslam_refkf_batch", spslam_track.RefkfBatch), ("spslam_frame_region", spslam_track.FrameRegion),
+                     ("spslam_refkf_vote", spslam_track.RefkfVote)):
         assert got[name] == ctypes.sizeof(st), name
         for key, off in got.items():
             if key.startswith(name + "."):

@@ -51,19 +51,20 @@ def _oracle(sp, slot, n, on_frame=None, local_map=None, on_lba=None, refkf=False
     import oracle_ctypes
     import oracle_grab
     import oracle_planes
+    import oracle_seq_inputs as OSI
     import oracle_sequence
     import oracle_step
     import synth
-    frames, T0, P0, local_of = sp.oracle_inputs(slot)
+    frames, T0, P0, local_of = OSI.inputs(sp, slot)
     cam, geo, inv_s2 = oracle_step.camera_inputs(sp)
-    ref = oracle_sequence.reference_keyframe(sp.oracle_reference_keyframe(slot), synth.shape_vocabulary_text())
+    ref = oracle_sequence.reference_keyframe(OSI.reference_keyframe(sp, slot), synth.shape_vocabulary_text())
     return oracle_sequence.track(frames[:n], 1, T0, P0, local_of, cam, geo, inv_s2, sp.assoc_map, sp.assoc_boundary,
                                  oracle_ctypes.OrbOracle(nfeatures=sp.ex.params.nfeatures),
                                  oracle_planes.PlaneOracle(), supp_cap=sp.pe.supp_cap, min_size=sp.min_size,
                                  pose_cfg=sp.plane_cfg, depth_scale=oracle_grab.depth_scale(sp.depth_factor),
                                  on_frame=on_frame, ref_kf=ref, local_map=local_map, on_lba=on_lba,
-                                 refkf_of=sp.oracle_refkf(slot, synth.shape_vocabulary_text()) if refkf else None,
-                                 perturb=perturb)
+                                 refkf_of=OSI.refkf_of(sp, slot, synth.shape_vocabulary_text()) if refkf else None,
+                                 perturb=perturb, kf_id_stride=sp.kp_cap)
 
 
 def test_pipelined_equals_serial(tracked):
@@ -152,7 +153,8 @@ def test_frame1_tracks_reference_keyframe(tracked):
     V = oracle_sequence.vocabulary(synth.shape_vocabulary_text())
     hist = sp.history()
     for slot in range(U):
-        kps, desc, has, row = sp.oracle_reference_keyframe(slot)
+        import oracle_seq_inputs as OSI
+        kps, desc, has, row = OSI.reference_keyframe(sp, slot)
         got = {}
         cpu = _oracle(sp, slot, 1, on_frame=lambda t, o, P: got.update(o=o))
         o = got["o"]
@@ -189,7 +191,8 @@ def test_c3_local_mapping_in_the_loop():
         def rec(t, o, P):
             got[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
                       int(o["pose2"][0]["n_inliers"]))
-        cpu = _oracle(sp, 0, n, on_frame=rec, local_map=sp.oracle_local_map(0),
+        import oracle_seq_inputs as OSI
+        cpu = _oracle(sp, 0, n, on_frame=rec, local_map=OSI.local_map(sp, 0),
                       on_lba=lambda t, r: lbas.update({t: r}))
         runs = dict(sp.lm_runs)
         diag = {"lba": {}, "frame_pose_diff": []}
@@ -241,18 +244,80 @@ def test_motion_model_failure_falls_back_to_reference_keyframe():
         for _ in range(n):
             sp.step()
         tr, hist, fbh = sp.trajectory(), sp.history(), sp.fallback_history()
+        rkh = sp.reference_keyframe_history()
         for slot in range(B):
             got = {}
 
             def rec(t, o, P):
                 got[t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
-                          int(o["pose2"][0]["n_inliers"]), o["fallback"])
+                          int(o["pose2"][0]["n_inliers"]), o["fallback"], o["reference_keyframe"])
             cpu = _oracle(sp, slot, n, on_frame=rec, refkf=True,
                           perturb={bad[slot]: V} if slot in bad else None)
             for t in range(1, n + 1):
                 want = 1 if bad.get(slot) == t else 0
                 assert got[t][4] == want and int(fbh[t, slot]) == want, (slot, t, got[t][4], int(fbh[t, slot]))
                 assert tuple(int(x) for x in hist[t, slot]) == tuple(int(x) for x in got[t][:4]), (slot, t)
+                assert int(rkh[t, slot]) == got[t][5], (slot, t, int(rkh[t, slot]), got[t][5])
                 assert tr[t, slot].tobytes() == cpu[t - 1].tobytes(), (slot, t)
+    finally:
+        sp.close()
+
+
+def test_c1_low_texture_sequence_matches_oracle():
+    """C1 proxy (BASELINE configs[0], TUM fr3 structure_notexture_far; Examples/RGB-D/TUM3.yaml): nearly untextured
+    faces (synth._texture_low: most FAST cells are decided by the minThFAST retry, ORBextractor.cc:812-816, and
+    ~200-300 keypoints per frame come from the structure's edges and a few stains) and a hand-held trajectory with
+    jolts (synth._jolts).  Nothing is forced: on the jolts SearchByProjection finds few or wrong matches, the motion
+    model fails by itself (nmatches < 10 or nmatchesMap < 5, Tracking.cc:977-1053) and TrackReferenceKeyFrame
+    against the reference keyframe (UpdateLocalKeyFrames' pKFmax, :1459-1570) takes over (:318-324).  Two sequence
+    offsets, 90 tracked frames each.  Bar, every frame: SearchByProjection / SearchLocalPoints matches, inliers of
+    both PoseOptimizations, the motion model / reference keyframe / lost state and the reference keyframe identical
+    to the CPU loop's, poses bit-identical (hence ATE vs the CPU trajectory 0)."""
+    import json
+    from concurrent.futures import ThreadPoolExecutor
+    import pipeline
+    import sequence
+    import trajectory
+    B, U, n = 2, 2, 90
+    sp = sequence.SequencePath(B, n + 2, n_sequences=U, pipelined=True, render_workers=8, **pipeline.CONFIGS["c1"])
+    try:
+        assert sp.refkf_fallback and sp.texture == "low" and sp.motion == "shaky"
+        for _ in range(n):
+            sp.step()
+        tr, hist, fbh, rkh = sp.trajectory(), sp.history(), sp.fallback_history(), sp.reference_keyframe_history()
+        kp = sp.d_kf_cnt.cpu().numpy()
+        got = [{} for _ in range(U)]
+
+        def run(slot):
+            def rec(t, o, P):
+                got[slot][t] = (o["nmatches"], o["local_nmatches"], int(o["pose1"][0]["n_inliers"]),
+                                int(o["pose2"][0]["n_inliers"]), o["fallback"], o["reference_keyframe"], len(o["kps"]))
+            return _oracle(sp, slot, n, on_frame=rec, refkf=True)
+        with ThreadPoolExecutor(U) as pool:
+            cpus = list(pool.map(run, range(U)))
+        diag = {"fallback_frames": [], "lost_frames": [], "mean_keypoints": [], "keyframe_keypoints": kp.tolist(),
+                "ate_vs_cpu_m": [], "ate_vs_ground_truth_m": []}
+        for slot in range(U):
+            g = got[slot]
+            for t in range(1, n + 1):
+                assert int(fbh[t, slot]) == g[t][4], (slot, t, int(fbh[t, slot]), g[t][4])
+                assert tuple(int(x) for x in hist[t, slot]) == tuple(int(x) for x in g[t][:4]), (slot, t)
+                assert int(rkh[t, slot]) == g[t][5], (slot, t, int(rkh[t, slot]), g[t][5])
+                assert tr[t, slot].tobytes() == cpus[slot][t - 1].tobytes(), (slot, t)
+            diag["fallback_frames"].append([t for t in range(1, n + 1) if g[t][4] == 1])
+            diag["lost_frames"].append([t for t in range(1, n + 1) if g[t][4] == 2])
+            diag["mean_keypoints"].append(float(np.mean([g[t][6] for t in range(1, n + 1)])))
+            gc = [trajectory.camera_center(tr[k + 1, slot].reshape(16)) for k in range(n)]
+            cc = [trajectory.camera_center(cpus[slot][k].reshape(16)) for k in range(n)]
+            gt = [np.linalg.inv(sp._true_pose(slot, k + 1))[:3, 3] for k in range(n)]
+            diag["ate_vs_cpu_m"].append(trajectory.ate_rmse(gc, cc))
+            diag["ate_vs_ground_truth_m"].append(trajectory.ate_rmse(gc, gt))
+        out = pathlib.Path(__file__).resolve().parents[1] / "gpurun_out"
+        out.mkdir(exist_ok=True)
+        (out / "c1_sequence_parity.json").write_text(json.dumps(diag, indent=1))
+        # the regime the proxy stands for: a low-texture scene and natural motion-model failures
+        assert all(100 <= m <= 330 for m in diag["mean_keypoints"]), diag
+        assert sum(len(f) for f in diag["fallback_frames"]) >= 3, diag
+        assert max(diag["ate_vs_cpu_m"]) <= 1e-12, diag
     finally:
         sp.close()
