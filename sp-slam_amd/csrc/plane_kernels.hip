@@ -19,6 +19,8 @@
 // restatement; see DESIGN.md for the float/double semantics chosen.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "plane_launch.h"
 
 namespace spslam {
@@ -259,6 +261,271 @@ __global__ __launch_bounds__(MAXR) void plane_dist_integral_kernel(PlaneGeom g, 
     }
 }
 
+// ---- the same two recurrences with no workgroup barrier (round 6): one wave per 64 cloud rows, lane = row.
+// Pass 1 at wave-local step s has lane l at column c = s - 2 l: a lane's up-row operands (the distance at columns
+// c - 1 .. c + 1 and the integral entries at c - 1, c) are what lane l - 1 produced 3, 2 and 1 steps earlier, so
+// they arrive by DPP (wave_shr:1) into a 3-deep shift register, one hop per step and no barrier.  The first row of
+// wave w > 0 takes the last row of wave w - 1 from a small LDS ring instead (the waves overlap: wave w trails wave
+// w - 1 by the 128 steps its 64 rows take; per-chunk progress counters bound the ring).  The cloud operands come
+// from the depth image: each lane makes its own row's x / y / z a few columns ahead (plane_cloud_kernel's float
+// operations), the rows above and below by DPP from the neighbouring lanes, and a wave's two outer neighbour rows
+// are made once into LDS before the passes.  Pass 2 runs the mirrored schedule (lane l + 1's values by wave_shl:1,
+// wave w + 1's first row through a ring).  Every cell sees exactly the operands of the reference's raster scans,
+// as in plane_dist_integral_kernel, so both outputs stay bit-identical.
+constexpr int kXR = 32;  // ring columns of a wave boundary
+struct WaveXchg {
+    float d1[kXR];       // pass 1: the upper wave's last row (distance)
+    double i1[kXR][6];   //         and its integral entries
+    float d2[kXR];       // pass 2: the lower wave's first row (distance)
+    int prod1, cons1, prod2, cons2;
+};
+__device__ __forceinline__ float from_above(float v) {  // lane l gets lane l - 1's value (wave_shr:1)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_below(float v) {  // lane l gets lane l + 1's value (wave_shl:1)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double from_above_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ int wave_counter(const int* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void wave_publish(int* p, int v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// bounded wait for a counter (the producers always advance; the bound only guards against a hang)
+__device__ __forceinline__ void wave_wait(const int* p, int need) {
+    for (int spin = 0; spin < (1 << 18) && wave_counter(p) < need; spin++) __builtin_amdgcn_s_sleep(1);
+}
+
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void plane_wave_kernel(PlaneGeom g, const float* __restrict__ depth,
+                                                              long long depth_fs, int depth_stride, float* sink,
+                                                              long long sink_fs, float* dist, long long dist_fs,
+                                                              double* integral, long long integral_fs) {
+    constexpr int K = 6;  // steps per chunk (a multiple of the 3-deep shift registers: no register rotation)
+    __shared__ WaveXchg X[NWV > 1 ? NWV - 1 : 1];
+    extern __shared__ float outer_rows[];  // per wave: the row above it and the row below it, x | y | z [3][W] each
+    const int f = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int W = g.W, H = g.H, r = 64 * w + lane, IW = W + 1;
+    const bool row_ok = r < H;
+    const int ro = min(r, H - 1);
+    const float* Z = depth + f * depth_fs;
+    auto zof = [&](int rr, int c) { return Z[(long long)(rr * g.ds) * depth_stride + c * g.ds]; };
+    auto xof = [&](int c, float z) { return ((float)(c * g.ds) - g.cx) * z / g.fx; };
+    auto yof = [&](int rr, float z) { return ((float)(rr * g.ds) - g.cy) * z / g.fy; };
+    float* UP = outer_rows + (size_t)w * 6 * W;  // row 64 w - 1
+    float* DN = UP + 3 * W;                      // row 64 w + 64
+    {
+        const int ru = 64 * w - 1, rd = 64 * w + 64;
+        for (int c = lane; c < W; c += 64) {
+            if (ru >= 0) {
+                const float z = zof(ru, c);
+                UP[c] = xof(c, z); UP[W + c] = yof(ru, z); UP[2 * W + c] = z;
+            }
+            if (rd < H) {
+                const float z = zof(rd, c);
+                DN[c] = xof(c, z); DN[W + c] = yof(rd, z); DN[2 * W + c] = z;
+            }
+        }
+    }
+    if (threadIdx.x < NWV - 1) {
+        X[threadIdx.x].prod1 = X[threadIdx.x].cons1 = X[threadIdx.x].prod2 = X[threadIdx.x].cons2 = 0;
+    }
+    double* Iraw = integral + f * integral_fs;
+    for (int c = threadIdx.x; c < IW; c += blockDim.x)
+        for (int k = 0; k < 6; k++) Iraw[(size_t)c * 6 + k] = 0.0;  // integral row 0
+    if (row_ok)
+        for (int k = 0; k < 6; k++) Iraw[(size_t)(r + 1) * IW * 6 + k] = 0.0;  // column 0
+    double* I = Iraw + (size_t)(ro + 1) * IW * 6 + 6;  // raster integral entry (r + 1, c + 1) at I + 6 c
+    double* Idummy = Iraw + (size_t)(H + 1) * IW * 6;  // sink row of the cells outside the cloud
+    float* D = dist + f * dist_fs + (size_t)ro * W;
+    float* Dsink = sink + f * sink_fs + threadIdx.x;
+    __syncthreads();
+    const float row0 = row_ok ? dist_init(zof, W, H, r, 0) : 0.f;
+    const bool has_up = w > 0, has_dn = w < NWV - 1;
+    // ---------------- pass 1
+    // this lane's row in a window of the chunk's columns c0 - 2 .. c0 + K + 1 (c0 = s0 - 2 lane): the own row's
+    // horizontal operands and, by DPP, the neighbour rows' values at the cell's column (the row above is two
+    // columns ahead: its window index j is column c; the row below two behind: its index j + 4)
+    float wx[K + 4], wy[K + 4], wz[K + 4], nz[K];
+    auto colz = [&](int c) { return zof(ro, min(max(c, 0), W - 1)); };
+    auto fill = [&](int i, int c, float z) {
+        const int cc = min(max(c, 0), W - 1);
+        wz[i] = z; wx[i] = xof(cc, z); wy[i] = yof(ro, z);
+    };
+    {
+        const int c0 = -2 * lane;
+#pragma unroll
+        for (int i = 0; i < K + 4; i++) fill(i, c0 - 2 + i, colz(c0 - 2 + i));
+#pragma unroll
+        for (int i = 0; i < K; i++) nz[i] = colz(c0 + K + 2 + i);
+    }
+    float nd0 = 0.f, nd1 = 0.f, nd2 = 0.f;  // row above: distance at c + 1, c, c - 1
+    double na[6], nb[6], nc[6];             // row above: integral at c + 1, c, c - 1
+#pragma unroll
+    for (int k = 0; k < 6; k++) na[k] = nb[k] = nc[k] = 0.0;
+    float left = 0.f, vprev = 0.f;
+    double ileft[6], iprev[6];
+#pragma unroll
+    for (int k = 0; k < 6; k++) ileft[k] = iprev[k] = 0.0;
+    const int S1 = (W + 126 + K - 1) / K * K;
+    if (has_up) {  // step -1: the first row's register of the upper row's column 0 (its column c - 1 at step 1)
+        wave_wait(&X[w - 1].prod1, 1);
+        nd0 = lane == 0 ? X[w - 1].d1[0] : 0.f;
+#pragma unroll
+        for (int k = 0; k < 6; k++) na[k] = lane == 0 ? X[w - 1].i1[0][k] : 0.0;
+    }
+    for (int s0 = 0; s0 < S1; s0 += K) {
+        const int c0 = s0 - 2 * lane;
+        // this chunk: the first row reads the upper wave's last row up to column s0 + K; the last row overwrites
+        // ring slots of columns s0 - 126 .. s0 - 121, freed once the lower wave has read up to them
+        if (has_up) wave_wait(&X[w - 1].prod1, min(s0 + K + 1, W));
+        if (has_dn) wave_wait(&X[w].cons1, min(s0 - 126 + K - kXR, W));
+        float nzn[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) nzn[i] = colz(c0 + 2 * K + 2 + i);  // the next chunk's new columns (in flight)
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int c = c0 + j;
+            // the row above: its output of the previous step (column c + 1)
+            float vin = from_above(vprev);
+            double iin[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) iin[k] = from_above_d(iprev[k]);
+            if (has_up) {
+                const int sl = (c + 1) & (kXR - 1);
+                const float rv = X[w - 1].d1[sl];
+                vin = lane == 0 ? rv : vin;
+#pragma unroll
+                for (int k = 0; k < 6; k++) {
+                    const double ri = X[w - 1].i1[sl][k];
+                    iin[k] = lane == 0 ? ri : iin[k];
+                }
+            }
+            nd2 = nd1; nd1 = nd0; nd0 = vin;
+#pragma unroll
+            for (int k = 0; k < 6; k++) { nc[k] = nb[k]; nb[k] = na[k]; na[k] = iin[k]; }
+            // cloud operands of cell (r, c)
+            const int cc = min(max(c, 0), W - 1);
+            float ux = from_above(wx[j]), uy = from_above(wy[j]), uz = from_above(wz[j]);
+            float dx = from_below(wx[j + 4]), dy = from_below(wy[j + 4]), dz = from_below(wz[j + 4]);
+            if (lane == 0 && has_up) { ux = UP[cc]; uy = UP[W + cc]; uz = UP[2 * W + cc]; }
+            if (lane == 63 && has_dn) { dx = DN[cc]; dy = DN[W + cc]; dz = DN[2 * W + cc]; }
+            bool zero = false;
+            const float zc = wz[j + 2];
+            if (r < H - 1 && c < W - 1) zero = dc_bad(zc, wz[j + 3]) || dc_bad(zc, dz);
+            if (r < H - 1 && c >= 1) zero = zero || dc_bad(wz[j + 1], zc);
+            if (r >= 1 && c < W - 1) zero = zero || dc_bad(uz, zc);
+            const float center = zero ? 0.0f : (float)(W + H);
+            float e[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
+                e[0] = wx[j + 3] - wx[j + 1]; e[1] = wy[j + 3] - wy[j + 1]; e[2] = wz[j + 3] - wz[j + 1];
+                e[3] = dx - ux; e[4] = dy - uy; e[5] = dz - uz;
+            }
+            // PCL's pass 1 and IntegralImage2D's recurrence (plane_dist_integral_kernel step1)
+            const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
+            const float upLeft = nd2 + 1.4f, up = nd1 + 1.0f;
+            const float upRight = (c + 1 < W ? nd0 : row0) + 1.4f;
+            const float lft = left + 1.0f;
+            const float mv = fminf(fminf(upLeft, up), fminf(lft, upRight));
+            const float v = inner && mv < center ? mv : center;
+            double iv[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const double upI = r > 0 ? nb[k] : 0.0;
+                const double upleftI = inner ? nc[k] : 0.0;
+                iv[k] = upI + ileft[k] - upleftI;
+                iv[k] += (double)e[k];
+            }
+            if (ok) {
+                left = v;
+#pragma unroll
+                for (int k = 0; k < 6; k++) ileft[k] = iv[k];
+            }
+            vprev = v;
+#pragma unroll
+            for (int k = 0; k < 6; k++) iprev[k] = iv[k];
+            *(ok ? D + c : Dsink) = v;  // the pass-1 map: pass 2's centre values, read back by this lane
+            {
+                double2* out = reinterpret_cast<double2*>(ok ? I + c * 6 : Idummy);
+                out[0] = make_double2(iv[0], iv[1]);
+                out[1] = make_double2(iv[2], iv[3]);
+                out[2] = make_double2(iv[4], iv[5]);
+            }
+            if (has_dn && lane == 63 && ok) {
+                const int sl = c & (kXR - 1);
+                X[w].d1[sl] = v;
+#pragma unroll
+                for (int k = 0; k < 6; k++) X[w].i1[sl][k] = iv[k];
+            }
+        }
+        if (has_dn) wave_publish(&X[w].prod1, max(0, min(s0 + K - 126, W)));
+        if (has_up) wave_publish(&X[w - 1].cons1, min(s0 + K + 1, W));
+        // the window moves on by K columns
+#pragma unroll
+        for (int i = 0; i < 4; i++) { wx[i] = wx[K + i]; wy[i] = wy[K + i]; wz[i] = wz[K + i]; }
+#pragma unroll
+        for (int i = 0; i < K; i++) fill(4 + i, c0 + K + 2 + i, nz[i]);
+#pragma unroll
+        for (int i = 0; i < K; i++) nz[i] = nzn[i];
+    }
+    const float lastcol = left;  // this row's pass-1 value at column W - 1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pass-1 map is read back below (same lane)
+    // ---------------- pass 2 (bottom-right to top-left): lane l at step s has column c = W - 1 - s + 2 (lb - l)
+    const int lb = min(63, H - 1 - 64 * w);
+    const int S2 = (W + 2 * lb + K - 1) / K * K;
+    auto dval = [&](int c) { return D[min(max(c, 0), W - 1)]; };
+    float dcur[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) dcur[j] = dval(W - 1 - j + 2 * (lb - lane));
+    float right = 0.f, vp2 = 0.f;
+    float ld0 = 0.f, ld1 = 0.f, ld2 = 0.f;  // row below: distance at c - 1, c, c + 1
+    const bool up_ring = w > 0;             // this wave's first row feeds the upper wave's last row
+    if (has_dn) {  // step -1: the last row's register of the lower row's column W - 1 (its column c + 1 at step 1)
+        wave_wait(&X[w].prod2, 1);
+        ld0 = lane == 63 ? X[w].d2[(W - 1) & (kXR - 1)] : 0.f;
+    }
+    for (int s0 = 0; s0 < S2; s0 += K) {
+        const int cA = W - 1 - s0 + 2 * (lb - lane);  // this lane's column at the chunk's first step
+        // the last row reads the lower wave's first row down to column W - 2 - (s0 + K - 1) + ...; the first row
+        // overwrites ring slots freed once the upper wave has read them
+        if (has_dn) wave_wait(&X[w].prod2, min(s0 + K + 1, W));
+        if (up_ring) wave_wait(&X[w - 1].cons2, min(s0 + K - 2 * lb - kXR, W));
+        float dnx[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) dnx[j] = dval(cA - K - j);
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int c = cA - j;
+            float vin = from_below(vp2);
+            if (has_dn) {
+                const float rv = X[w].d2[(c - 1) & (kXR - 1)];
+                vin = lane == 63 ? rv : vin;
+            }
+            ld2 = ld1; ld1 = ld0; ld0 = vin;
+            const bool ok = row_ok && c >= 0 && c < W, inner = r < H - 1 && c < W - 1;
+            const float lowerLeft = (c > 0 ? ld0 : lastcol) + 1.4f;
+            const float lower = ld1 + 1.0f;
+            const float lowerRight = ld2 + 1.4f;
+            const float rgt = right + 1.0f;
+            const float mv = fminf(fminf(lowerLeft, lower), fminf(rgt, lowerRight));
+            const float center = dcur[j];
+            const float v = inner && mv < center ? mv : center;
+            if (ok) right = v;
+            vp2 = v;
+            *(ok ? D + c : Dsink) = v;
+            if (up_ring && lane == 0 && ok) X[w - 1].d2[c & (kXR - 1)] = v;
+        }
+        if (up_ring) wave_publish(&X[w - 1].prod2, max(0, min(s0 + K - 2 * lb, W)));
+        if (has_dn) wave_publish(&X[w].cons2, min(s0 + K + 1, W));
+#pragma unroll
+        for (int j = 0; j < K; j++) dcur[j] = dnx[j];
+    }
+}
+
 __global__ __launch_bounds__(256) void plane_normal_kernel(PlaneGeom g, const float* __restrict__ cloud,
                                                            long long cloud_fs, const float* __restrict__ dist,
                                                            long long dist_fs, const double* __restrict__ integral,
@@ -320,7 +587,19 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
     hipLaunchKernelGGL(plane_cloud_kernel, pts, dim3(256), 0, s, g, depth, depth_fs, depth_stride, b.cloud, b.cloud_fs);
     E(kKindPlaneCloud);
     B(kKindPlaneDist);
-    {
+    static const bool barrier_wave = [] {
+        const char* e = getenv("SPSLAM_PLANE_WAVE_BARRIER");
+        return e && e[0] == '1';
+    }();
+    if (!barrier_wave) {
+        const int nw = (g.H + 63) / 64;
+        const size_t lds = (size_t)nw * 6 * g.W * sizeof(float);
+        auto* k = nw <= 1 ? plane_wave_kernel<1> : nw <= 2 ? plane_wave_kernel<2> : nw <= 3 ? plane_wave_kernel<3>
+                : nw <= 4 ? plane_wave_kernel<4> : nw <= 5 ? plane_wave_kernel<5> : nw <= 6 ? plane_wave_kernel<6>
+                : nw <= 7 ? plane_wave_kernel<7> : plane_wave_kernel<8>;
+        hipLaunchKernelGGL(k, dim3(n), dim3(64 * nw), lds, s, g, depth, depth_fs, depth_stride, b.wave, b.wave_fs,
+                           b.dist, b.dist_fs, b.integral, b.integral_fs);
+    } else {
         const int rows = wave_pitch(g.H);
         auto* k = g.H <= 192   ? plane_dist_integral_kernel<192, kWaveChunk>
                   : g.H <= 320 ? plane_dist_integral_kernel<320, kWaveChunk>

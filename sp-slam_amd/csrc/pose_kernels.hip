@@ -621,8 +621,9 @@ __global__ __launch_bounds__(kThreads, 1) void pose_kernel(const spslam_pose_pro
         PROF_MARK(0);  // setup / previous relabel
         T = S.T0;
         // any active edge?
-        int act = 0;
-        for (int e = t; e < ne; e += kThreads) act |= !is_outlier(e);
+        int act = 0, ea0 = t;
+        asm volatile("" : "+v"(ea0));  // (its unrolled bounds, hoisted to the kernel's start, were spilled)
+        for (int e = ea0; e < ne; e += kThreads) act |= !is_outlier(e);
         act = __syncthreads_or(act);
         if (act) {
             double lambda = 0, ni = 2;
