@@ -10,7 +10,7 @@ HIPFLAGS ?= --offload-arch=$(OFFLOAD_ARCH) -O3 -std=c++17 -fPIC -ffp-contract=of
 PKG := sp-slam_amd
 CSRC := $(PKG)/csrc
 OBJDIR := build/obj
-KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels lba_g2o \
+KERNELS := orb_kernels pose_kernels plane_kernels plane_segment supposed_kernels frame_kernels lba_kernels lba_g2o lba_g2o_wide \
            assoc_kernels match_kernels track_kernels grab_kernels bow_kernels
 OBJS := $(addprefix $(OBJDIR)/,$(addsuffix .o,$(KERNELS) spslam_capi spslam_step))
 GPU_HDRS := $(wildcard $(CSRC)/*.h) include/spslam_gpu.h include/spslam_brief_pattern.inc
@@ -28,6 +28,9 @@ $(OBJDIR)/spslam_capi.o: $(CSRC)/spslam_capi.cpp $(GPU_HDRS)
 $(OBJDIR)/spslam_step.o: $(CSRC)/spslam_step.cpp $(GPU_HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c -x hip -o $@ $<
+
+# the wide LocalBundleAdjustment instance is lba_g2o.hip compiled again
+$(OBJDIR)/lba_g2o_wide.o $(PROFDIR)/lba_g2o_wide.o $(VARDIR)/lba_g2o_wide.o: $(CSRC)/lba_g2o.hip
 
 $(PKG)/libspslam_gpu.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(OFFLOAD_ARCH) -shared -fPIC -o $@ $(OBJS)

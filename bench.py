@@ -53,9 +53,11 @@ WORKLOADS = {
     # BASELINE.json configs[1]: single MI355X, 640x480 synthetic RGB-D stream, ORB + planes + PoseOptimization
     "c2": "C2: synthetic 640x480 RGB-D stream; ORB (nFeatures=1000, 8 levels) + organized-cloud plane extraction + "
           "supposed planes + 2x PoseOptimization (point+plane+parallel+perpendicular edges), no LBA",
-    # configs[2]: full pipeline incl. LocalBundleAdjustment (a keyframe every 5 frames, 12-keyframe local maps)
+    # configs[2]: full pipeline incl. LocalBundleAdjustment (a keyframe every 5 frames, fr1/room-sized local maps)
     "c3": "C3 (synthetic proxy): C2 + LocalBundleAdjustment with plane/parallel/perpendicular edges for every 5th "
-          "frame (12 keyframes, 1500 points per local map)",
+          "frame over an fr1/room-sized window (25 local + 10 fixed keyframes, 4000 points per local map)",
+    "c3s": "C3 with rounds 1-5's smaller LocalBundleAdjustment window (10 local + 2 fixed keyframes, 1500 points per "
+           "local map)",
     # configs[3]: independent ICL-NUIM living-room sequences, one per GPU
     "c4": "C4 (synthetic proxy): ICL-NUIM parameter set (Examples/RGB-D/ICL.yaml: fx 481.2, fy -480.0, cx 319.5, "
           "cy 239.5, Plane.MinSize 1000, Plane.Chi 1000, Plane.VPChi 200), one independent sequence per GPU rank; "
@@ -601,7 +603,7 @@ def main():
         return dist_check(args, rank, world)
     # C3: every in-flight LocalBundleAdjustment call has its own context stream; with 8 hardware queues they alias
     # the tracking streams' queues and serialise (profiles/r05/ab_c3_hwq*.txt), so C3 runs with 16
-    _ensure_hw_queues(16 if args.config == "c3" else None)
+    _ensure_hw_queues(16 if args.config in ("c3", "c3s") else None)
     import pipeline
     cfg = pipeline.CONFIGS[args.config]
     import torch
@@ -659,7 +661,8 @@ def main():
     n_brd = float(res["line_points"].mean())
     lba_bytes = 0
     if hp.n_lba:  # per frame: the keyframe's local map in (records) and its results out
-        lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) + 12 * (96 + 64)) * hp.n_lba / args.batch
+        lba_bytes = (hp.lba_points * (24 + 12) + hp.lba_edges * (20 + 1) +
+                     hp.lba_window["keyframes"] * (96 + 64)) * hp.n_lba / args.batch
     n_fpl = float(res["plane_counts"].mean()) + n_sup
     alg = algorithmic_bytes(cfg, hp.mean_keypoints, n_pts, n_pls, n_con, n_brd, n_sup, lba_bytes, n_fpl, hp.n_map,
                             hp.n_boundary, hp.mean_proj_points, hp.mean_local_points, hp.mean_fast_candidates)
@@ -707,6 +710,7 @@ def main():
         "config": {"workload": WORKLOADS[args.config], "name": args.config, "frames_per_step_per_gpu": args.batch,
                    "parallelism": f"shard{world}" + ("-rehearsal-on-gpu0-gloo" if args.rehearse_one_gpu else ""),
                    "mean_keypoints": hp.mean_keypoints,
+                   **({"lba_window": hp.lba_window} if hp.n_lba else {}),
                    "pipelined": hp.pipelined,
                    "step": "spslam_step_run (library streams and events)" if hp.native is not None
                            else "pipeline.py over torch streams",

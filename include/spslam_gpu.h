@@ -325,8 +325,9 @@ int spslam_lba_set_team(spslam_ctx* ctx, int workgroups);
  * schedule on the device.  Outputs are indexed like the inputs (keyframe /
  * point / plane offsets of each problem, absolute observation indices).
  * SPSLAM_LBA_G2O_ORDER: at most 1024 keyframes per problem (local + fixed) of
- * which at most 64 free poses (local keyframes, id != 0, with an active
- * edge); SPSLAM_LBA_FAST_ORDER: at most 64 keyframes; status -2 otherwise
+ * which at most 128 free poses (local keyframes, id != 0, with an active
+ * edge; batches whose windows all hold <= 64 keyframes run the narrow
+ * instance, others the wide one); SPSLAM_LBA_FAST_ORDER: at most 64 keyframes; status -2 otherwise
  * (nothing else written for that problem).  d_stop_flags: one pbStopFlag per
  * problem in device-visible memory (device, or host-mapped coherent memory
  * another thread raises), nonzero = stop; NULL = no flags.  Results are
@@ -767,6 +768,18 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
                                   int color_stride, const void* d_depth, size_t depth_frame_stride, int depth_stride,
                                   int w, int h, const spslam_grab_params* params, uint8_t* d_gray, float* d_depth_out,
                                   void* hip_stream);
+
+/* Fusion with the plane stage (no reference counterpart: Frame::ComputePlanesFromOrganizedPointCloud,
+ * Frame.cc:857-874, samples the converted depth a second time).  With enable = 1 (the default) and
+ * spslam_planes_configure called on the same context for the same image size, a
+ * spslam_grab_rgbd_batch_device call also writes the organized cloud of its depth output into the
+ * selected cloud set (spslam_planes_select_cloud_set) and tags the set with that depth output; the
+ * set's next spslam_planes_extract_batch_device over exactly that depth (same pointer, dense layout,
+ * no more frames) uses the cloud as it is instead of sampling the depth again (bit-identical cloud),
+ * and clears the tag.  Any other extraction makes its own cloud.  The caller orders the grab before
+ * the extraction (same stream or an event), as it already must for the depth.  The environment
+ * variable SPSLAM_GRAB_CLOUD=0 makes 0 the default. */
+int spslam_grab_fuse_cloud(spslam_ctx* ctx, int enable);
 
 /* ---------------------------------------------------------------- tracking graph glue
  * The Tracking-side bookkeeping between matching / plane association and

@@ -6,6 +6,9 @@
 // the kernel is HBM bound; each thread moves 8 consecutive pixels of a row
 // with 8/16-byte loads and stores (64 px per wave = 1.5 KB of colour, 1 KB of
 // depth in, 512 B gray + 2 KB depth out, fully coalesced).
+// With a cloud output (CLOUD), the threads of every Cloud.Dis-th row also write the organized cloud's points of
+// their 8 pixels (Frame.cc:857-874; the same float expressions as plane_cloud_kernel, so the cloud is bit-identical),
+// which saves the plane chain a second pass over the depth lines it samples.
 #include <hip/hip_runtime.h>
 
 #include "grab_launch.h"
@@ -24,7 +27,14 @@ __device__ __forceinline__ uint32_t gray_of(uint32_t c0, uint32_t c1, uint32_t c
     return (c0 * w0 + c1 * kG2Y + c2 * w2 + (1u << (kShift - 1))) >> kShift;
 }
 
-template <int CN, bool U16>
+// Cloud point (m, n) of depth z: cloud[i], cloud[N + i], cloud[2N + i] (plane_cloud_kernel's expressions)
+__device__ __forceinline__ void cloud_point(const GrabArgs& a, float* C, int i, int m, int n, float z) {
+    C[i] = ((float)n - a.cx) * z / a.fx;
+    C[a.cN + i] = ((float)m - a.cy) * z / a.fy;
+    C[2 * a.cN + i] = z;
+}
+
+template <int CN, bool U16, bool CLOUD>
 __global__ __launch_bounds__(kThreads) void grab_vec_kernel(GrabArgs a) {
     const int f = blockIdx.y;
     const int per_row = a.w / kPx;
@@ -69,6 +79,21 @@ __global__ __launch_bounds__(kThreads) void grab_vec_kernel(GrabArgs a) {
     float* o = a.depth_out + (size_t)f * a.w * a.h + (size_t)y * a.w + x;
     *(float4*)o = *(const float4*)z;
     *(float4*)(o + 4) = *(const float4*)(z + 4);
+    if constexpr (CLOUD) {
+        const int r = y / a.ds;
+        if (r * a.ds != y) return;
+        float* C = a.cloud + f * a.cloud_fs;
+        const int c0 = (x + a.ds - 1) / a.ds;  // the first sampled column at or after x
+        int k0 = c0 * a.ds - x, cc = c0;      // its pixel in this thread's group (the others follow every ds)
+#pragma unroll
+        for (int k = 0; k < kPx; k++) {
+            if (k == k0) {
+                cloud_point(a, C, r * a.cW + cc, y, x + k, z[k]);
+                k0 += a.ds;
+                cc++;
+            }
+        }
+    }
 }
 
 // Any width / alignment: one pixel per thread.
@@ -88,6 +113,8 @@ __global__ __launch_bounds__(kThreads) void grab_scalar_kernel(GrabArgs a) {
         if (a.p.depth_scale != 1.0f) z = __fmul_rn(z, a.p.depth_scale);
     }
     a.depth_out[(size_t)f * a.w * a.h + q] = z;
+    if (a.cloud && y % a.ds == 0 && x % a.ds == 0)
+        cloud_point(a, a.cloud + f * a.cloud_fs, (y / a.ds) * a.cW + x / a.ds, y, x, z);
 }
 
 bool aligned(const void* p, size_t n) { return ((uintptr_t)p % n) == 0; }
@@ -95,8 +122,9 @@ bool aligned(const void* p, size_t n) { return ((uintptr_t)p % n) == 0; }
 template <int CN, bool U16>
 void launch_vec(int n, const GrabArgs& a, hipStream_t s) {
     const int threads = a.w / kPx * a.h;
-    hipLaunchKernelGGL((grab_vec_kernel<CN, U16>), dim3((threads + kThreads - 1) / kThreads, n), dim3(kThreads), 0,
-                       s, a);
+    const dim3 grid((threads + kThreads - 1) / kThreads, n);
+    if (a.cloud) hipLaunchKernelGGL((grab_vec_kernel<CN, U16, true>), grid, dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((grab_vec_kernel<CN, U16, false>), grid, dim3(kThreads), 0, s, a);
 }
 
 }  // namespace

@@ -18,6 +18,12 @@ struct GrabArgs {
     spslam_grab_params p;
     uint8_t* gray;
     float* depth_out;
+    // the organized cloud of Frame::ComputePlanesFromOrganizedPointCloud (Frame.cc:857-874) made in the same pass
+    // (spslam_grab_fuse_cloud): cloud == nullptr = none; frame f's x | y | z planes at cloud + f * cloud_fs
+    float* cloud;
+    long long cloud_fs;
+    int ds, cW, cN;  // Cloud.Dis, the cloud's width and size (plane configuration)
+    float fx, fy, cx, cy;
 };
 
 hipError_t grab_launch(int n_frames, const GrabArgs& a, hipStream_t s, KernelTimer* timer);

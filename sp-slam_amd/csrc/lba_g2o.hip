@@ -29,26 +29,167 @@
 #include "g2o_device.h"
 #include "lba_launch.h"
 
+// Two instances of this file are compiled (itself and lba_g2o_wide.hip): LBG_PW = 1 (pose masks of one 64-bit
+// word: up to 64 free poses, n <= 384) and LBG_PW = 2 (two words: up to 128 free poses, n <= 768).  The narrow one is
+// the round-5 kernel unchanged in its arithmetic; the host runs the wide one for windows of more than 64 keyframes.
+#ifndef LBG_PW
+#define LBG_PW 1
+#endif
+#if LBG_PW == 1
+#define LBG_NS lbag
+#define LBG_RUN lba_run_g2o_pw1
+#else
+#define LBG_NS lbag2
+#define LBG_RUN lba_run_g2o_pw2
+#endif
+
 namespace spslam {
-namespace lbag {
+namespace LBG_NS {
 
 using namespace g2od;
 
 constexpr int kT = kLbgThreads, kW = kT / 64;
 constexpr int kMaxKF = kLbgMaxKeyframes;  // keyframes (local + fixed)
-constexpr int kMaxK = kLbgMaxFree;        // free poses (Hessian blocks)
-constexpr int kNW = 6;                  // bitset words for up to 6 * 64 = 384 scalars
+constexpr int kPW = LBG_PW;               // 64-bit words of a pose mask
+constexpr int kMaxK = 64 * kPW;           // free poses (Hessian blocks)
+constexpr int kNW = 6 * kPW;              // bitset words for up to 6 * kMaxK scalars
 constexpr int kDyn = 136 * 1024;        // dynamic LDS (setup tiles, AMD workspace, the factorisation's L)
-constexpr int kDynAlloc = 154 * 1024;   // allocated: kDyn plus the Schur phase's staged Bb terms and block tables
+constexpr int kDynAlloc = (LBG_PW == 1 ? 154 : 152) * 1024;  // allocated: kDyn plus the Schur phase's staged Bb
+                                                              //   terms and block tables (static LDS + this <= 160 KB)
                                         //   (every phase but the Schur one sizes itself against kDyn)
-constexpr int kLdsN = 96;               // reduced systems of n <= 96 rows factorised in LDS (L, S packed: 133 KB)
+constexpr int kLdsN = LBG_PW == 1 ? 96 : 90;  // reduced systems of n <= kLdsN rows factorised in LDS (L, S packed:
+                                               //   133 KB; the wide instance's structure words take more)
 constexpr int kSchurLm = 64;            // Schur phase: landmarks per staged chunk (one bit each in a 64-bit mask)
-constexpr int kSchurBlk = 412;          //   and Hpl blocks per chunk (the staging buffer, 16 doubles a thread, + BDinv)
+constexpr int kSchurBlk = LBG_PW == 1 ? 412 : 360;  //   and Hpl blocks per chunk (the staging buffer, 16 doubles a
+                                                    //   thread, + BDinv; the wide instance's tables take more)
+
+// A set of free poses (Hessian indices) as kPW 64-bit words; with kPW = 1 every operation is the plain uint64_t one.
+struct PMask {
+    uint64_t w[kPW];
+};
+__device__ __forceinline__ PMask pm_zero() {
+    PMask m;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) m.w[k] = 0ull;
+    return m;
+}
+__device__ __forceinline__ PMask pm_bit(int i) {
+    PMask m;
+    if constexpr (kPW == 1) {
+        m.w[0] = 1ull << i;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kPW; k++) m.w[k] = (i >> 6) == k ? 1ull << (i & 63) : 0ull;
+    }
+    return m;
+}
+__device__ __forceinline__ bool pm_test(const PMask& m, int i) {
+    if constexpr (kPW == 1) {
+        return (m.w[0] >> i) & 1ull;
+    } else {
+        uint64_t v = m.w[0];
+#pragma unroll
+        for (int k = 1; k < kPW; k++) v = (i >> 6) == k ? m.w[k] : v;
+        return (v >> (i & 63)) & 1ull;
+    }
+}
+__device__ __forceinline__ void pm_set(PMask& m, int i) {
+    if constexpr (kPW == 1) {
+        m.w[0] |= 1ull << i;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kPW; k++) m.w[k] |= (i >> 6) == k ? 1ull << (i & 63) : 0ull;
+    }
+}
+__device__ __forceinline__ PMask pm_and(PMask a, const PMask& b) {
+#pragma unroll
+    for (int k = 0; k < kPW; k++) a.w[k] &= b.w[k];
+    return a;
+}
+__device__ __forceinline__ PMask pm_or(PMask a, const PMask& b) {
+#pragma unroll
+    for (int k = 0; k < kPW; k++) a.w[k] |= b.w[k];
+    return a;
+}
+__device__ __forceinline__ PMask pm_andnot(PMask a, const PMask& b) {
+#pragma unroll
+    for (int k = 0; k < kPW; k++) a.w[k] &= ~b.w[k];
+    return a;
+}
+// bits [0, i), 0 <= i < 64 kPW (the narrow instance: (1 << i) - 1, i < 64)
+__device__ __forceinline__ PMask pm_below(int i) {
+    PMask m;
+    if constexpr (kPW == 1) {
+        m.w[0] = (1ull << i) - 1ull;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kPW; k++) {
+            const int c = i - 64 * k;
+            m.w[k] = c >= 64 ? ~0ull : c <= 0 ? 0ull : (1ull << c) - 1ull;
+        }
+    }
+    return m;
+}
+// bits [0, n), 0 <= n <= 64 kPW
+__device__ __forceinline__ PMask pm_first_n(int n) {
+    PMask m;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) {
+        const int c = n - 64 * k;
+        m.w[k] = c >= 64 ? ~0ull : c <= 0 ? 0ull : (1ull << c) - 1ull;
+    }
+    return m;
+}
+__device__ __forceinline__ int pm_popc(const PMask& m) {
+    int c = 0;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) c += __popcll(m.w[k]);
+    return c;
+}
+__device__ __forceinline__ int pm_popc_below(const PMask& m, int i) { return pm_popc(pm_and(m, pm_below(i))); }
+__device__ __forceinline__ bool pm_any(const PMask& m) {
+    uint64_t v = m.w[0];
+#pragma unroll
+    for (int k = 1; k < kPW; k++) v |= m.w[k];
+    return v != 0ull;
+}
+__device__ __forceinline__ bool pm_eq(const PMask& a, const PMask& b) {
+    bool e = true;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) e = e && a.w[k] == b.w[k];
+    return e;
+}
+// lowest set bit (the mask must not be empty)
+__device__ __forceinline__ int pm_ffs(const PMask& m) {
+    if constexpr (kPW == 1) {
+        return __ffsll((unsigned long long)m.w[0]) - 1;
+    } else {
+        int r = -1;
+#pragma unroll
+        for (int k = kPW - 1; k >= 0; k--)
+            if (m.w[k]) r = 64 * k + __ffsll((unsigned long long)m.w[k]) - 1;
+        return r;
+    }
+}
+// the mask without its lowest set bit
+__device__ __forceinline__ void pm_pop(PMask& m) {
+    if constexpr (kPW == 1) {
+        m.w[0] &= m.w[0] - 1;
+    } else {
+        bool done = false;
+#pragma unroll
+        for (int k = 0; k < kPW; k++)
+            if (!done && m.w[k]) {
+                m.w[k] &= m.w[k] - 1;
+                done = true;
+            }
+    }
+}
 
 struct Sh {
     double red[kW][4];
     int iscan[kW];
-    uint64_t pat[kMaxK];                // Schur block pattern: row i1, bits i2 >= i1
+    PMask pat[kMaxK];                   // Schur block pattern: row i1, bits i2 >= i1
     short hidx[kMaxKF];                 // keyframe -> free-pose Hessian index (-1: fixed or inactive)
     unsigned char kact[kMaxKF];         // structure: keyframes with an active edge
     int hpose[kMaxK];                   // Hessian index -> keyframe
@@ -57,8 +198,8 @@ struct Sh {
     // the team (one workgroup per member, lba_g2o's header): problem, member, size, barrier generation; this
     // member's buildSystem share (landmark-aligned edge range, its free poses)
     int p, m, T, gen, eb0, eb1, npown, bo0, bo1;
-    uint64_t rmask;                     // this member's Schur block rows
-    uint64_t carry;                     // buildSystem: Hpl blocks touched by the landmark continuing into the next step
+    PMask rmask;                        // this member's Schur block rows
+    PMask carry;                        // buildSystem: Hpl blocks touched by the landmark continuing into the next step
     double csum[2][12];                 //   and its partial Hll / bl sums (by step parity)
     int pown[kMaxK];
     // LM / schedule state (every member computes it identically between barriers)
@@ -95,9 +236,23 @@ struct G {
         *pe_off, *pe_idx, *Pinv, *Pm, *parent, *rs_off, *rs_idx, *amd_Ci, *amd_W, *sch, *sch_kb,
         *eseg,   // per edge: {RI, landmark hidx, segment end, first block | segment start << 30}
         *bord;   // Schur pattern blocks, longest chain first
-    guint64 *lmh_mask, *lm_amask, *Lbits, *Abits;
+    PMask GL *lmh_mask, *lm_amask;
+    guint64 *Lbits, *Abits;
     LbgTeam GL* team;
 };
+// pose masks in global memory (word by word: an address-space-qualified PMask has no copy constructor)
+__device__ __forceinline__ PMask pm_ld(const PMask GL* p) {
+    const uint64_t GL* q = (const uint64_t GL*)p;
+    PMask m;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) m.w[k] = q[k];
+    return m;
+}
+__device__ __forceinline__ void pm_st(PMask GL* p, const PMask& m) {
+    uint64_t GL* q = (uint64_t GL*)p;
+#pragma unroll
+    for (int k = 0; k < kPW; k++) q[k] = m.w[k];
+}
 
 // The workgroup's LDS objects at namespace scope: the phase functions are not inlined, and a pointer or reference
 // argument would reach them as a generic (flat) address -- every LDS access a FLAT instruction, which also waits on
@@ -117,7 +272,7 @@ __device__ G make_g(const LbgBatch& b, int p) {
     g.pl = (const spslam_lba_plane GL*)(b.pls + pb.plane_offset);
     g.pobs = (const spslam_lba_point_obs GL*)b.pobs;
     g.plobs = (const spslam_lba_plane_obs GL*)b.plobs;
-    const LbgLayout Ly = lbg_layout(g.K, g.Np, g.Nq, g.E);
+    const LbgLayout Ly = lbg_layout(g.K, g.Np, g.Nq, g.E, kPW);
     uint8_t* base = b.scratch + b.scratch_off[p];
     auto D = [&](size_t o) { return (double GL*)(base + o); };
     auto I = [&](size_t o) { return (int GL*)(base + o); };
@@ -131,7 +286,7 @@ __device__ G make_g(const LbgBatch& b, int p) {
     g.pe_off = I(Ly.pe_off); g.pe_idx = I(Ly.pe_idx); g.Pinv = I(Ly.Pinv); g.Pm = I(Ly.Pm); g.parent = I(Ly.parent);
     g.rs_off = I(Ly.rs_off); g.rs_idx = I(Ly.rs_idx); g.amd_Ci = I(Ly.amd_Ci); g.amd_W = I(Ly.amd_W);
     g.sch = I(Ly.sch); g.sch_kb = I(Ly.sch_kb); g.eseg = I(Ly.eseg); g.bord = I(Ly.bord);
-    g.lmh_mask = (uint64_t GL*)(base + Ly.lmh_mask); g.lm_amask = (uint64_t GL*)(base + Ly.lm_amask);
+    g.lmh_mask = (PMask GL*)(base + Ly.lmh_mask); g.lm_amask = (PMask GL*)(base + Ly.lm_amask);
     g.Lbits = (uint64_t GL*)(base + Ly.Lbits); g.Abits = (uint64_t GL*)(base + Ly.Abits);
     g.team = (LbgTeam GL*)(base + Ly.team);
     return g;
@@ -478,7 +633,7 @@ __device__ __noinline__ void setup() {
     for (int e = g.E + t; e < lbg_pad32(g.E); e += kT) g.echi[e] = 0.0;
     // g2o's solution buffer (Solver::_x): written only by successful solves and read by every update, so a failed
     // solve re-applies the previous solution; never written = zeros (update())
-    for (int j = t; j < lbg_pad32(6 * lbg_free_cap(g.K) + 3 * g.L); j += kT) g.x[j] = 0.0;
+    for (int j = t; j < lbg_pad32(6 * lbg_free_cap(g.K, kPW) + 3 * g.L); j += kT) g.x[j] = 0.0;
     // landmark (vertex-id) order: points by id (ids mnId + maxKFid + 1), then planes by id (mnId + maxPointid + 1,
     // above every point id); stable ranks (id, list index)
     for (int grp = 0; grp < 2; grp++) {
@@ -736,7 +891,7 @@ __device__ __noinline__ void amd_order(int n, int* Cp, int* Ci, int t, int* W, i
 }
 
 __device__ __forceinline__ bool coupled(const Sh& s, int q1, int q2) {  // pose blocks (q1, q2) in the Schur pattern
-    return q1 <= q2 ? (s.pat[q1] >> q2) & 1ull : (s.pat[q2] >> q1) & 1ull;
+    return q1 <= q2 ? pm_test(s.pat[q1], q2) : pm_test(s.pat[q2], q1);
 }
 template <class PU>
 __device__ __forceinline__ bool bit_of(const PU* bits, int i) { return (bits[i >> 6] >> (i & 63)) & 1ull; }
@@ -769,7 +924,7 @@ __device__ __noinline__ void team_plan() {
         int o = np;
         for (int a = 0; a < np; a++) {
             rowoff[a] = o;
-            o += __popcll(s.pat[a]) - 1;
+            o += pm_popc(s.pat[a]) - 1;
         }
         s.nb = o;
     }
@@ -778,21 +933,21 @@ __device__ __noinline__ void team_plan() {
     for (int i = t; i < nb; i += kT) len[i] = 0;
     if (t < np) {
         brow[t] = t;
-        for (int j = rowoff[t]; j < rowoff[t] + __popcll(s.pat[t]) - 1; j++) brow[j] = t;
+        for (int j = rowoff[t]; j < rowoff[t] + pm_popc(s.pat[t]) - 1; j++) brow[j] = t;
     }
     __syncthreads();
     for (int h = t; h < nl; h += kT) {
-        uint64_t a = g.lmh_mask[h];
-        while (a) {
-            const int i1 = __ffsll((unsigned long long)a) - 1;
-            a &= a - 1;
+        PMask a = pm_ld(g.lmh_mask + h);
+        while (pm_any(a)) {
+            const int i1 = pm_ffs(a);
+            pm_pop(a);
             atomicAdd(&len[i1], 1);
-            const uint64_t row = s.pat[i1] & ~(1ull << i1);
-            uint64_t b2 = a;
-            while (b2) {
-                const int i2 = __ffsll((unsigned long long)b2) - 1;
-                b2 &= b2 - 1;
-                atomicAdd(&len[rowoff[i1] + __popcll(row & ((1ull << i2) - 1ull))], 1);
+            const PMask row = pm_andnot(s.pat[i1], pm_bit(i1));
+            PMask b2 = a;
+            while (pm_any(b2)) {
+                const int i2 = pm_ffs(b2);
+                pm_pop(b2);
+                atomicAdd(&len[rowoff[i1] + pm_popc_below(row, i2)], 1);
             }
         }
     }
@@ -808,33 +963,33 @@ __device__ __noinline__ void team_plan() {
     __syncthreads();
     if (t < np) {  // a row's work: its blocks' chains (+1 each: the block's own cost)
         int w = len[t] + 1;
-        for (int j = rowoff[t]; j < rowoff[t] + __popcll(s.pat[t]) - 1; j++) w += len[j] + 1;
+        for (int j = rowoff[t]; j < rowoff[t] + pm_popc(s.pat[t]) - 1; j++) w += len[j] + 1;
         rw[t] = w;
     }
     __syncthreads();
     if (t == 0) {  // LPT: rows by work, each to the least loaded member
         long long load[kLbgTeamMax];
-        uint64_t rm[kLbgTeamMax];
-        for (int mm = 0; mm < T; mm++) { load[mm] = 0; rm[mm] = 0; }
-        uint64_t done = 0;
+        PMask rm[kLbgTeamMax];
+        for (int mm = 0; mm < T; mm++) { load[mm] = 0; rm[mm] = pm_zero(); }
+        PMask done = pm_zero();
         for (int q = 0; q < np; q++) {
             int best = -1;
             for (int a = 0; a < np; a++)
-                if (!((done >> a) & 1ull) && (best < 0 || rw[a] > rw[best])) best = a;
-            done |= 1ull << best;
+                if (!pm_test(done, a) && (best < 0 || rw[a] > rw[best])) best = a;
+            pm_set(done, best);
             int mm = 0;
             for (int u = 1; u < T; u++)
                 if (load[u] < load[mm]) mm = u;
             load[mm] += rw[best];
-            rm[mm] |= 1ull << best;
+            pm_set(rm[mm], best);
             rmem[best] = mm;
         }
         int o = 0;
         for (int mm = 0; mm < T; mm++) {  // blocks per member -> the members' segments of bord
             R->bo[mm] = o;
-            R->rmask[mm] = rm[mm];
+            for (int k = 0; k < kPW; k++) R->rmask[mm * kPW + k] = rm[mm].w[k];
             for (int a = 0; a < np; a++)
-                if ((rm[mm] >> a) & 1ull) o += __popcll(s.pat[a]);
+                if (pm_test(rm[mm], a)) o += pm_popc(s.pat[a]);
         }
         R->bo[T] = o;
     }
@@ -888,7 +1043,8 @@ __device__ __noinline__ void team_plan() {
         R->npo[T] = o;
         R->np = np; R->nl = nl; R->nact = s.nact; R->nch = s.nch; R->nb = nb; R->unsup = 0;
     }
-    if (t < kMaxK) R->pat[t] = t < np ? s.pat[t] : 0ull;
+    if (t < kMaxK)
+        for (int k = 0; k < kPW; k++) R->pat[t * kPW + k] = t < np ? s.pat[t].w[k] : 0ull;
     for (int k = t; k < g.K; k += kT) R->hidx[k] = s.hidx[k];
     __syncthreads();
 }
@@ -906,7 +1062,8 @@ __device__ __noinline__ void load_team() {
             s.np = R->np; s.nl = R->nl; s.nact = R->nact; s.nch = R->nch; s.nb = R->nb;
         }
         for (int k = t; k < g.K; k += kT) s.hidx[k] = R->hidx[k];
-        if (t < kMaxK) s.pat[t] = R->pat[t];
+        if (t < kMaxK)
+            for (int k = 0; k < kPW; k++) s.pat[t].w[k] = R->pat[t * kPW + k];
     }
     const int o0 = R->npo[s.m], o1 = R->npo[s.m + 1];
     if (t == 0) {
@@ -915,7 +1072,7 @@ __device__ __noinline__ void load_team() {
         s.npown = o1 - o0;
         s.bo0 = R->bo[s.m];
         s.bo1 = R->bo[s.m + 1];
-        s.rmask = R->rmask[s.m];
+        for (int k = 0; k < kPW; k++) s.rmask.w[k] = R->rmask[s.m * kPW + k];
     }
     if (t < o1 - o0) s.pown[t] = R->pown[o0 + t];
     __syncthreads();
@@ -948,7 +1105,7 @@ __device__ __noinline__ void structure() {
         for (int k = 0; k < g.K; k++) {
             const auto& kk = g.kf[k];
             if (!s.kact[k] || kk.fixed || kk.id == 0) continue;
-            if (np == kMaxK) { np++; break; }  // more free poses than the 64-bit pose masks hold: status -2
+            if (np == kMaxK) { np++; break; }  // more free poses than the pose masks hold: status -2
             int j = np++;
             while (j > 0 && g.kf[s.hpose[j - 1]].id > kk.id) { s.hpose[j] = s.hpose[j - 1]; j--; }
             s.hpose[j] = k;
@@ -969,24 +1126,24 @@ __device__ __noinline__ void structure() {
         const int j = ch + t;
         const int l = j < g.L ? g.lm_sorted[j] : -1;
         int act = 0;
-        uint64_t mask = 0, amask = 0;
+        PMask mask = pm_zero(), amask = pm_zero();
         if (l >= 0)
             for (int e = g.lm_boff[l]; e < g.lm_boff[l] + g.lm_nb[l]; e++) {
                 const int h = s.hidx[g.e_kf[e]];
-                if (h >= 0) amask |= 1ull << h;
+                if (h >= 0) pm_set(amask, h);
                 if (g.e_level[e] == 0) {
                     act = 1;
-                    if (h >= 0) mask |= 1ull << h;
+                    if (h >= 0) pm_set(mask, h);
                 }
             }
         int tot;
         const int off = block_scan(act, &tot, s) + base;
         if (l >= 0) {
             g.lm_hidx[l] = act ? off : -1;
-            g.lm_amask[l] = amask;
+            pm_st(g.lm_amask + l, amask);
             if (act) {
                 g.hidx_lm[off] = l;
-                g.lmh_mask[off] = mask;
+                pm_st(g.lmh_mask + off, mask);
             }
         }
         base += tot;
@@ -997,7 +1154,7 @@ __device__ __noinline__ void structure() {
     base = 0;
     for (int ch = 0; ch < nl; ch += kT) {
         const int h = ch + t;
-        const int c = h < nl ? __popcll(g.lmh_mask[h]) : 0;
+        const int c = h < nl ? pm_popc(pm_ld(g.lmh_mask + h)) : 0;
         int tot;
         const int off = block_scan(c, &tot, s) + base;
         if (h < nl) g.lmh_blk[h] = off;
@@ -1046,17 +1203,17 @@ __device__ __noinline__ void structure() {
             s.nch = nc;
         }
     }
-    if (t < np) s.pat[t] = 1ull << t;
+    if (t < np) s.pat[t] = pm_bit(t);
     __syncthreads();
     for (int l = t; l < g.L; l += kT) {
         const int h = g.lm_hidx[l];
-        const uint64_t mask = h >= 0 ? g.lmh_mask[h] : 0;
+        const PMask mask = h >= 0 ? pm_ld(g.lmh_mask + h) : pm_zero();
         const int b0 = g.lm_boff[l], e1 = b0 + g.lm_nb[l], kb = h >= 0 ? g.lmh_blk[h] : 0;
         for (int e = b0; e < e1; e++) {
             int eb = -1;
             const int ph = s.hidx[g.e_kf[e]];
             const bool on = g.e_level[e] == 0;
-            if (h >= 0 && on && ph >= 0) eb = kb + __popcll(mask & ((1ull << ph) - 1ull));
+            if (h >= 0 && on && ph >= 0) eb = kb + pm_popc_below(mask, ph);
             g.e_blk[e] = eb;
             // build_system's row record: RI (the edge's Hpl block, -1 none, -2 inactive), the landmark's segment
             g.eseg[4 * e] = on ? eb : -2;
@@ -1065,12 +1222,14 @@ __device__ __noinline__ void structure() {
             g.eseg[4 * e + 3] = kb | (e == b0 ? 1 << 30 : 0);
         }
         if (h >= 0) {
-            uint64_t am = g.lm_amask[l];
-            while (am) {
-                const int i1 = __ffsll((unsigned long long)am) - 1;
-                const uint64_t row = g.lm_amask[l] & ~((1ull << i1) - 1ull);
-                atomicOr((unsigned long long*)&s.pat[i1], (unsigned long long)row);
-                am &= am - 1;
+            const PMask am0 = pm_ld(g.lm_amask + l);
+            PMask am = am0;
+            while (pm_any(am)) {
+                const int i1 = pm_ffs(am);
+                const PMask row = pm_andnot(am0, pm_below(i1));
+                for (int k = 0; k < kPW; k++)
+                    if (row.w[k]) atomicOr((unsigned long long*)&s.pat[i1].w[k], (unsigned long long)row.w[k]);
+                pm_pop(am);
             }
         }
     }
@@ -1108,7 +1267,7 @@ __device__ __noinline__ void structure() {
     int alld = 1;
     for (int q = t; q < np; q += kT) alld &= 6 * s.pdeg[q] > dense;
     int full = 1;  // every pose coupled with every other
-    for (int q = t; q < np; q += kT) full &= s.pat[q] == ((np == 64 ? ~0ull : (1ull << np) - 1ull) & ~((1ull << q) - 1ull));
+    for (int q = t; q < np; q += kT) full &= pm_eq(s.pat[q], pm_andnot(pm_first_n(np), pm_below(q)));
     full = block_and(full, s);
     if (block_and(alld, s)) {
         if (t == 0) s.dense = full;
@@ -1123,13 +1282,13 @@ __device__ __noinline__ void structure() {
         int* W = in_lds ? Ci + tcap : (int*)g.amd_W;
         int* perm = W + 8 * (n + 1);
         int* Cp = perm + (n + 1);
-        if (t < n) {
-            const int q2 = t / 6;
+        for (int tt = t; tt < n; tt += kT) {
+            const int q2 = tt / 6;
             int c0 = 0;
             for (int q = 0; q < q2; q++) c0 += 6 * s.pdeg[q];
             c0 *= 6;
-            c0 += (t - 6 * q2) * 6 * s.pdeg[q2];
-            Cp[t] = c0;
+            c0 += (tt - 6 * q2) * 6 * s.pdeg[q2];
+            Cp[tt] = c0;
             int c = c0;
             for (int q = 0; q < np; q++)
                 if (coupled(s, q, q2))
@@ -1145,13 +1304,13 @@ __device__ __noinline__ void structure() {
     for (int k = t; k < n; k += kT) g.Pm[g.Pinv[k]] = k;
     __syncthreads();
     // lower structure of each column j of ap = P a P^T: Abits[j] = {i > j : (Pinv j, Pinv i) in the pattern}
-    if (t < n) {
-        const int qj = g.Pinv[t] / 6;
-        uint64_t wv[kNW] = {0, 0, 0, 0, 0, 0};
-        for (int i = t + 1; i < n; i++)
+    for (int tt = t; tt < n; tt += kT) {
+        const int qj = g.Pinv[tt] / 6;
+        uint64_t wv[kNW] = {};
+        for (int i = tt + 1; i < n; i++)
             if (coupled(s, qj, g.Pinv[i] / 6)) wv[i >> 6] |= 1ull << (i & 63);
 #pragma unroll
-        for (int w = 0; w < kNW; w++) g.Abits[t * kNW + w] = wv[w];
+        for (int w = 0; w < kNW; w++) g.Abits[tt * kNW + w] = wv[w];
     }
     __syncthreads();
     // elimination tree and L's column structures: struct L(:, j) = Abits[j] U (children's structures \ {j});
@@ -1187,45 +1346,50 @@ __device__ __noinline__ void structure() {
     // each row k of L: its pattern {i : k in struct L(:, i)} in factorize_preordered's order -- ap's column k
     // entries in source order (original index ascending), an elimination-tree walk from each, the walks' paths
     // stacked so that the last path comes first, each path from its start upwards
-    int cnt = 0;
-    if (t < n)
-        for (int i = 0; i < t; i++) cnt += bit_of(g.Lbits + i * kNW, t);
-    int tot;
-    const int off = block_scan(cnt, &tot, s);
-    if (t < n) g.rs_off[t] = off;
-    if (t == 0) g.rs_off[n] = tot;
-    if (t < n && cnt > 0) {
-        const int k = t, ok = g.Pinv[k];
-        uint64_t vis[kNW] = {0, 0, 0, 0, 0, 0};
-        vis[k >> 6] |= 1ull << (k & 63);
-        auto seg = g.rs_idx + off;
-        int wpos = 0;
-        for (int o2 = 0; o2 < n; o2++) {
-            const int r = g.Pm[o2];
-            if (r >= k || !coupled(s, o2 / 6, ok / 6)) continue;
-            int i = r;
-            while (!((vis[i >> 6] >> (i & 63)) & 1ull)) {
-                vis[i >> 6] |= 1ull << (i & 63);
-                seg[wpos++] = i;
-                i = g.parent[i];
+    int rs_base = 0;
+    for (int k0 = 0; k0 < n; k0 += kT) {  // rows k0 .. k0 + kT - 1 (one pass for n <= kT)
+        const int k = k0 + t;
+        int cnt = 0;
+        if (k < n)
+            for (int i = 0; i < k; i++) cnt += bit_of(g.Lbits + i * kNW, k);
+        int tot;
+        const int off = block_scan(cnt, &tot, s) + rs_base;
+        rs_base += tot;
+        if (k < n) g.rs_off[k] = off;
+        if (k0 + kT >= n && t == 0) g.rs_off[n] = rs_base;
+        if (k < n && cnt > 0) {
+            const int ok = g.Pinv[k];
+            uint64_t vis[kNW] = {};
+            vis[k >> 6] |= 1ull << (k & 63);
+            auto seg = g.rs_idx + off;
+            int wpos = 0;
+            for (int o2 = 0; o2 < n; o2++) {
+                const int r = g.Pm[o2];
+                if (r >= k || !coupled(s, o2 / 6, ok / 6)) continue;
+                int i = r;
+                while (!((vis[i >> 6] >> (i & 63)) & 1ull)) {
+                    vis[i >> 6] |= 1ull << (i & 63);
+                    seg[wpos++] = i;
+                    i = g.parent[i];
+                }
             }
-        }
-        // paths were written in discovery order: reverse the whole row, then each path back to start-upwards
-        for (int a = 0, b2 = cnt - 1; a < b2; a++, b2--) {
-            const int v = seg[a];
-            seg[a] = seg[b2];
-            seg[b2] = v;
-        }
-        int a = 0;
-        while (a < cnt) {  // a reversed path: consecutive entries (prev, next) with parent[next] == prev
-            int b2 = a;
-            while (b2 + 1 < cnt && g.parent[seg[b2 + 1]] == seg[b2]) b2++;
-            for (int x = a, y = b2; x < y; x++, y--) {
-                const int v = seg[x];
-                seg[x] = seg[y];
-                seg[y] = v;
+            // paths were written in discovery order: reverse the whole row, then each path back to start-upwards
+            for (int a = 0, b2 = cnt - 1; a < b2; a++, b2--) {
+                const int v = seg[a];
+                seg[a] = seg[b2];
+                seg[b2] = v;
             }
-            a = b2 + 1;
+            int a = 0;
+            while (a < cnt) {  // a reversed path: consecutive entries (prev, next) with parent[next] == prev
+                int b2 = a;
+                while (b2 + 1 < cnt && g.parent[seg[b2 + 1]] == seg[b2]) b2++;
+                for (int x = a, y = b2; x < y; x++, y--) {
+                    const int v = seg[x];
+                    seg[x] = seg[y];
+                    seg[y] = v;
+                }
+                a = b2 + 1;
+            }
         }
     }
     __syncthreads();
@@ -1624,7 +1788,7 @@ __device__ __noinline__ void build_system() {
         // (B) landmark segments: the rows' Hpl kinds in edge order (head threads), segments compacted per wave
         bool head = false, again = false;
         int end_row = 0, own_h = -1, own_kb = 0;
-        uint64_t touched = 0;
+        PMask touched = pm_zero();
         if (land && t < cnt) {
             RI[t] = sg.x;
             RF[t] = 0;
@@ -1634,7 +1798,7 @@ __device__ __noinline__ void build_system() {
                 own_h = sg.y;
                 own_kb = sg.w & ((1 << 30) - 1);
                 end_row = min(sg.z, c0 + cnt) - c0;
-                touched = first ? 0ull : s.carry;  // (only row 0 continues a landmark of the previous step)
+                touched = first ? pm_zero() : s.carry;  // (only row 0 continues a landmark of the previous step)
             }
         }
         {
@@ -1654,9 +1818,8 @@ __device__ __noinline__ void build_system() {
                 const int bk = RI[r];
                 unsigned char f = 0;
                 if (bk >= 0) {
-                    const uint64_t bit = 1ull << (bk - own_kb);
-                    f = (touched & bit) ? 2 : 1;
-                    touched |= bit;
+                    f = pm_test(touched, bk - own_kb) ? 2 : 1;
+                    pm_set(touched, bk - own_kb);
                 }
                 RF[r] = f;
                 again |= f == 2;
@@ -1854,8 +2017,8 @@ __device__ __noinline__ void schur() {
     double* BUF = (double*)dyn;                          // [kBufD]
     double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
     double* SU = SD + kSchurBlk * 18;                    // [kSchurBlk][6] B row . Dinv bl (Bb's terms)
-    uint64_t* SM = (uint64_t*)(SU + kSchurBlk * 6);      // [kSchurLm]
-    uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
+    PMask* SM = (PMask*)(SU + kSchurBlk * 6);            // [kSchurLm]
+    uint64_t* PM = (uint64_t*)(SM + kSchurLm);           // [kMaxK]
     int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
     unsigned short* OB = (unsigned short*)(SO + kSchurLm + 1);  // [kMaxK][kSchurLm] (pose, landmark) -> its block
     unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk] block -> landmark
@@ -1864,11 +2027,11 @@ __device__ __noinline__ void schur() {
     LdsU* LST = (LdsU*)(unsigned*)(((uintptr_t)(BP + kSchurBlk) + 3) & ~(uintptr_t)3);  // [kW][64]
     const double* SDi = BUF + kSchurBlk * 18;
     const double* Sdb = SDi + kSchurLm * 9;
-    static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
+    static_assert((kBufD + kSchurBlk * 24 + kSchurLm * kPW + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
                       2 * kSchurBlk + 4 + kW * 64 * 4 <= kDynAlloc, "LDS");
     constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
     const int bo0 = s.bo0, nbm = s.bo1 - s.bo0;
-    const uint64_t rmask = s.rmask;
+    const PMask rmask = s.rmask;
     // this lane's entry: (r, c) on lanes 0 .. 35, Bb(r) on lanes 36 .. 41 (its operand addresses clamped in range)
     const bool ent = lane < 36;
     const int er = ent ? lane / 6 : min(lane - 36, 5), ec = ent ? lane - 6 * (lane / 6) : 0;
@@ -1889,11 +2052,11 @@ __device__ __noinline__ void schur() {
                     i1[k] = i2[k] = blk;
                 } else {
                     int rem = blk - np, a = 0;
-                    while (rem >= __popcll(s.pat[a]) - 1) { rem -= __popcll(s.pat[a]) - 1; a++; }
-                    uint64_t row = s.pat[a] & ~(1ull << a);
-                    for (int u = 0; u < rem; u++) row &= row - 1;
+                    while (rem >= pm_popc(s.pat[a]) - 1) { rem -= pm_popc(s.pat[a]) - 1; a++; }
+                    PMask row = pm_andnot(s.pat[a], pm_bit(a));
+                    for (int u = 0; u < rem; u++) pm_pop(row);
                     i1[k] = a;
-                    i2[k] = __ffsll((unsigned long long)row) - 1;
+                    i2[k] = pm_ffs(row);
                 }
                 i1[k] = uni(i1[k]);
                 i2[k] = uni(i2[k]);
@@ -1908,7 +2071,7 @@ __device__ __noinline__ void schur() {
         // used before the commit, so no wait lands in the chunk loop; the chunk bounds (sch, sch_kb) of the chunk
         // after next load one chunk ahead.
         double pv[kPer];
-        uint64_t pmk = 0;
+        PMask pmk = pm_zero();
         int pof = 0, pof1 = 0;
         auto prefetch = [&](int h0, int h1, int kb0, int kb1) __attribute__((always_inline)) {
             const int nbk = kb1 - kb0, nh = h1 - h0;
@@ -1929,7 +2092,7 @@ __device__ __noinline__ void schur() {
                 pv[q] = *src;
             }
             const int tc = min(t, max(nh - 1, 0));
-            pmk = g.lmh_mask[h0 + tc];
+            pmk = pm_ld(g.lmh_mask + h0 + tc);
             pof = g.lmh_blk[h0 + min(t, nh)];
             pof1 = g.lmh_blk[h0 + tc + 1];
         };
@@ -1939,11 +2102,11 @@ __device__ __noinline__ void schur() {
                 if (t + q * kT < kBufD) BUF[t + q * kT] = pv[q];
             if (t < nh) {
                 SM[t] = pmk;
-                uint64_t m = pmk;
+                PMask m = pmk;
                 for (int bk = pof - kb0; bk < pof1 - kb0; bk++) {  // (the blocks of a landmark are in pose order)
                     BL[bk] = (unsigned char)t;
-                    BP[bk] = (unsigned char)(__ffsll((unsigned long long)m) - 1);
-                    m &= m - 1;
+                    BP[bk] = (unsigned char)pm_ffs(m);
+                    pm_pop(m);
                 }
             }
             if (t <= nh) SO[t] = pof - kb0;
@@ -1982,7 +2145,7 @@ __device__ __noinline__ void schur() {
             __syncthreads();
             for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
                 const int bk = i / 6, r6 = i - 6 * bk;
-                if (!((rmask >> BP[bk]) & 1ull)) continue;  // a block row of another member
+                if (!pm_test(rmask, BP[bk])) continue;  // a block row of another member
                 const int hb = BL[bk];
                 const double* Bi = BUF + 18 * bk + 3 * r6;
                 const double* Di = SDi + 9 * hb;
@@ -1993,11 +2156,11 @@ __device__ __noinline__ void schur() {
                 SU[i] = (Bi[0] * db[0] + Bi[1] * db[1]) + Bi[2] * db[2];
             }
             for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk, and their blocks
-                const uint64_t mk = lane < nh ? SM[lane] : 0ull;
-                const bool obs = (mk >> i) & 1ull;
+                const PMask mk = lane < nh ? SM[lane] : pm_zero();
+                const bool obs = pm_test(mk, i);
                 const uint64_t m = __ballot(obs);
                 if (lane == 0) PM[i] = m;
-                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + __popcll(mk & ((1ull << i) - 1ull)));
+                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + pm_popc_below(mk, i));
             }
             __syncthreads();
 #ifdef SPSLAM_LBG_DIAG
@@ -2115,19 +2278,19 @@ __device__ __noinline__ void schur_rows() {
     double* BUF = (double*)dyn;                          // [kBufD]
     double* SD = BUF + kBufD;                            // [kSchurBlk][18] BDinv
     double* SU = SD + kSchurBlk * 18;                    // [kSchurBlk][6] B row . Dinv bl (Bb's terms)
-    uint64_t* SM = (uint64_t*)(SU + kSchurBlk * 6);      // [kSchurLm]
-    uint64_t* PM = SM + kSchurLm;                        // [kMaxK]
+    PMask* SM = (PMask*)(SU + kSchurBlk * 6);            // [kSchurLm]
+    uint64_t* PM = (uint64_t*)(SM + kSchurLm);           // [kMaxK]
     int* SO = (int*)(PM + kMaxK);                        // [kSchurLm + 1]
     unsigned short* OB = (unsigned short*)(SO + kSchurLm + 1);  // [kMaxK][kSchurLm] (pose, landmark) -> its block
     unsigned char* BL = (unsigned char*)(OB + kMaxK * kSchurLm);  // [kSchurBlk] block -> landmark
     unsigned char* BP = BL + kSchurBlk;                  // [kSchurBlk] block -> pose
     const double* SDi = BUF + kSchurBlk * 18;
     const double* Sdb = SDi + kSchurLm * 9;
-    static_assert((kBufD + kSchurBlk * 24 + kSchurLm + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
+    static_assert((kBufD + kSchurBlk * 24 + kSchurLm * kPW + kMaxK) * 8 + (kSchurLm + 1) * 4 + kMaxK * kSchurLm * 2 +
                       2 * kSchurBlk + 4 + kW * 64 * 4 <= kDynAlloc, "LDS");
     constexpr int kPer = (kBufD + kT - 1) / kT;          // staged doubles per thread
     const int bo0 = s.bo0, nbm = s.bo1 - s.bo0;
-    const uint64_t rmask = s.rmask;
+    const PMask rmask = s.rmask;
     using LdsD = const __attribute__((address_space(3))) double;
     for (int round = 0; round * kSchurTasks * kT < 6 * nbm; round++) {
         int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
@@ -2144,11 +2307,11 @@ __device__ __noinline__ void schur_rows() {
                     i1[k] = i2[k] = blk;
                 } else {
                     int rem = blk - np, a = 0;
-                    while (rem >= __popcll(s.pat[a]) - 1) { rem -= __popcll(s.pat[a]) - 1; a++; }
-                    uint64_t row = s.pat[a] & ~(1ull << a);
-                    for (int u = 0; u < rem; u++) row &= row - 1;
+                    while (rem >= pm_popc(s.pat[a]) - 1) { rem -= pm_popc(s.pat[a]) - 1; a++; }
+                    PMask row = pm_andnot(s.pat[a], pm_bit(a));
+                    for (int u = 0; u < rem; u++) pm_pop(row);
                     i1[k] = a;
-                    i2[k] = __ffsll((unsigned long long)row) - 1;
+                    i2[k] = pm_ffs(row);
                 }
             }
             const bool diag = i1[k] >= 0 && i1[k] == i2[k];
@@ -2166,7 +2329,7 @@ __device__ __noinline__ void schur_rows() {
         // used before the commit, so no wait lands in the chunk loop; the chunk bounds (sch, sch_kb) of the chunk
         // after next load one chunk ahead.
         double pv[kPer];
-        uint64_t pmk = 0;
+        PMask pmk = pm_zero();
         int pof = 0, pof1 = 0;
         auto prefetch = [&](int h0, int h1, int kb0, int kb1) __attribute__((always_inline)) {
             const int nbk = kb1 - kb0, nh = h1 - h0;
@@ -2187,7 +2350,7 @@ __device__ __noinline__ void schur_rows() {
                 pv[q] = *src;
             }
             const int tc = min(t, max(nh - 1, 0));
-            pmk = g.lmh_mask[h0 + tc];
+            pmk = pm_ld(g.lmh_mask + h0 + tc);
             pof = g.lmh_blk[h0 + min(t, nh)];
             pof1 = g.lmh_blk[h0 + tc + 1];
         };
@@ -2197,11 +2360,11 @@ __device__ __noinline__ void schur_rows() {
                 if (t + q * kT < kBufD) BUF[t + q * kT] = pv[q];
             if (t < nh) {
                 SM[t] = pmk;
-                uint64_t m = pmk;
+                PMask m = pmk;
                 for (int bk = pof - kb0; bk < pof1 - kb0; bk++) {  // (the blocks of a landmark are in pose order)
                     BL[bk] = (unsigned char)t;
-                    BP[bk] = (unsigned char)(__ffsll((unsigned long long)m) - 1);
-                    m &= m - 1;
+                    BP[bk] = (unsigned char)pm_ffs(m);
+                    pm_pop(m);
                 }
             }
             if (t <= nh) SO[t] = pof - kb0;
@@ -2240,7 +2403,7 @@ __device__ __noinline__ void schur_rows() {
             __syncthreads();
             for (int i = t; i < nbk * 6; i += kT) {  // BDinv row by row: (Bi Dinv)(r, q), and Bi(r) . Dinv bl
                 const int bk = i / 6, r6 = i - 6 * bk;
-                if (!((rmask >> BP[bk]) & 1ull)) continue;  // a block row of another member
+                if (!pm_test(rmask, BP[bk])) continue;  // a block row of another member
                 const int hb = BL[bk];
                 const double* Bi = BUF + 18 * bk + 3 * r6;
                 const double* Di = SDi + 9 * hb;
@@ -2251,11 +2414,11 @@ __device__ __noinline__ void schur_rows() {
                 SU[i] = (Bi[0] * db[0] + Bi[1] * db[1]) + Bi[2] * db[2];
             }
             for (int i = wv; i < np; i += kW) {  // free pose i's landmarks in the chunk, and their blocks
-                const uint64_t mk = lane < nh ? SM[lane] : 0ull;
-                const bool obs = (mk >> i) & 1ull;
+                const PMask mk = lane < nh ? SM[lane] : pm_zero();
+                const bool obs = pm_test(mk, i);
                 const uint64_t m = __ballot(obs);
                 if (lane == 0) PM[i] = m;
-                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + __popcll(mk & ((1ull << i) - 1ull)));
+                if (obs) OB[kSchurLm * i + lane] = (unsigned short)(SO[lane] + pm_popc_below(mk, i));
             }
             __syncthreads();
 #ifdef SPSLAM_LBG_DIAG
@@ -2696,11 +2859,11 @@ __device__ __noinline__ void update() {
         double xl[3];
         if (ok) {
             double cl[3] = {g.bl[3 * h], g.bl[3 * h + 1], g.bl[3 * h + 2]};
-            uint64_t m = g.lmh_mask[h];
+            PMask m = pm_ld(g.lmh_mask + h);
             int bk = g.lmh_blk[h];
-            while (m) {
-                const int p = __ffsll((unsigned long long)m) - 1;
-                m &= m - 1;
+            while (pm_any(m)) {
+                const int p = pm_ffs(m);
+                pm_pop(m);
                 auto B = g.blkB + (size_t)18 * bk++;
                 for (int i = 0; i < 3; i++) {
                     double sm = 0;
@@ -3026,7 +3189,11 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                         else if (n <= 128) factor_solve<2, false>();
                         else if (n <= 192) factor_solve<3, false>();
                         else if (n <= 256) factor_solve<4, false>();
-                        else factor_solve<6, false>();
+                        else if (kPW == 1 || n <= 384) factor_solve<6, false>();
+#if LBG_PW > 1
+                        else if (n <= 512) factor_solve<8, false>();
+                        else factor_solve<12, false>();
+#endif
                     }
                     if (n == 0 && t == 0) s.ok = 1;
 #ifdef SPSLAM_LBG_DIAG
@@ -3115,7 +3282,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     }
     team_sync(b);  // every member's writes are in before the leader's outputs
     if (!lead) return;
-    if (s.unsup) {  // more free poses than kLbgMaxFree: nothing written but the status
+    if (s.unsup) {  // more free poses than kMaxK: nothing written but the status
         if (t == 0) {
             b.res[p] = spslam_lba_result{};
             b.res[p].status = -2;
@@ -3151,10 +3318,10 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
     }
 }
 
-}  // namespace lbag
+}  // namespace LBG_NS
 
-hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer) {
-    using namespace lbag;
+hipError_t LBG_RUN(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer) {
+    using namespace LBG_NS;
     static const hipError_t attr =
         hipFuncSetAttribute((const void*)k_lba_g2o, hipFuncAttributeMaxDynamicSharedMemorySize, kDynAlloc);
     if (attr != hipSuccess) return attr;
@@ -3168,3 +3335,12 @@ hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, Ker
 }
 
 }  // namespace spslam
+
+#if LBG_PW == 1
+namespace spslam {
+// the instance of a batch: LbgBatch::pw (lbg_pw_for of its largest window)
+hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer) {
+    return b.pw == 1 ? lba_run_g2o_pw1(b, C, s, timer) : lba_run_g2o_pw2(b, C, s, timer);
+}
+}  // namespace spslam
+#endif

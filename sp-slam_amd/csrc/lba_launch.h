@@ -117,7 +117,9 @@ struct LbaBatch {
 // device.
 constexpr int kLbgThreads = 512;
 constexpr int kLbgMaxKeyframes = 1024;  // local + fixed keyframes per problem
-constexpr int kLbgMaxFree = 64;         // free (local) poses with an active edge: pose masks are 64-bit, n <= 384
+constexpr int kLbgMaxFree = 64;         // free (local) poses with an active edge, narrow instance: 64-bit pose masks,
+                                        //   n <= 384
+constexpr int kLbgMaxFreeWide = 128;    // the wide instance (lba_g2o_wide.hip): two-word pose masks, n <= 768
 constexpr int kLbgTeamMax = 16;         // workgroups per problem
 // What the team's leader publishes for its members after each structure pass (lba_g2o.hip load_team).
 struct LbgTeam {
@@ -125,14 +127,17 @@ struct LbgTeam {
     int stop_gen;               // the team barrier at which the leader first saw pbStopFlag raised (0: not yet)
     int eb[kLbgTeamMax + 1];    // buildSystem: member m sums the landmarks whose edges are [eb[m], eb[m + 1])
     int npo[kLbgTeamMax + 1];   //   and the (free pose, term) chains of poses pown[npo[m] .. npo[m + 1])
-    int pown[kLbgMaxFree];
+    int pown[kLbgMaxFreeWide];
     int bo[kLbgTeamMax + 1];    // Schur: member m's pattern blocks bord[bo[m] .. bo[m + 1]), the block rows rmask[m]
-    uint64_t rmask[kLbgTeamMax];
+    uint64_t rmask[2 * kLbgTeamMax];  //   (pw words per member)
     double mx[2 * kLbgTeamMax];  // computeLambdaInit: each member's largest |diagonal| (landmarks, poses)
-    uint64_t pat[kLbgMaxFree];
+    uint64_t pat[2 * kLbgMaxFreeWide];  // the Schur pattern's rows (pw words per row)
     short hidx[kLbgMaxKeyframes];
 };
-__host__ __device__ inline int lbg_free_cap(int K) { return K < kLbgMaxFree ? K : kLbgMaxFree; }
+// pw: 64-bit words of the instance's pose masks (1: narrow, 2: wide)
+__host__ __device__ inline int lbg_free_cap(int K, int pw) { return K < 64 * pw ? K : 64 * pw; }
+// the instance a batch runs: wide when a window holds more keyframes than the narrow one's free poses
+__host__ __device__ inline int lbg_pw_for(int max_kf) { return max_kf <= kLbgMaxFree ? 1 : 2; }
 struct LbgLayout {
     size_t pose, pose_b, X, X_b, P, P_b, err, echi, sc, terms, Hll, bl, Dinv, db, blkB, Hps, S, bs, x, Ld;  // double
     size_t e_lm, e_kf, e_type, e_level, e_src, e_blk, lm_boff, lm_nb, lm_sorted, lm_hidx, hidx_lm, lmh_blk, pe_off,
@@ -142,10 +147,10 @@ struct LbgLayout {
     size_t bytes;
 };
 __host__ __device__ inline int lbg_pad32(int n) { return (n + 31) & ~31; }
-// K keyframes (<= kLbgMaxKeyframes), the Hessian-sized arrays for at most lbg_free_cap(K) free poses
-__host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
+// K keyframes (<= kLbgMaxKeyframes), the Hessian-sized arrays for at most lbg_free_cap(K, pw) free poses
+__host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E, int pw) {
     LbgLayout Ly{};
-    const int Kf = lbg_free_cap(K);
+    const int Kf = lbg_free_cap(K, pw);
     const size_t L = (size_t)Np + Nq, n = 6 * (size_t)Kf, Ep = lbg_pad32(E), Xn = lbg_pad32((int)(n + 3 * L));
     const size_t nC = n * n + n * n / 5 + 2 * n;  // cs_amd's elbow room over the full symmetric pattern
     size_t o = 0;
@@ -170,7 +175,8 @@ __host__ __device__ inline LbgLayout lbg_layout(int K, int Np, int Nq, int E) {
     Ly.amd_Ci = take((nC + 1) * 4); Ly.amd_W = take(10 * (n + 1) * 4);
     Ly.sch = take((L + 2) * 4); Ly.sch_kb = take((L + 2) * 4); Ly.eseg = take((size_t)E * 16);
     Ly.bord = take(((size_t)Kf * (Kf + 1) / 2 + 1) * 4);
-    Ly.lmh_mask = take(L * 8); Ly.lm_amask = take(L * 8); Ly.Lbits = take((n + 1) * 6 * 8); Ly.Abits = take(n * 6 * 8);
+    Ly.lmh_mask = take(L * 8 * pw); Ly.lm_amask = take(L * 8 * pw);
+    Ly.Lbits = take((n + 1) * 6 * pw * 8); Ly.Abits = take(n * 6 * pw * 8);
     Ly.bytes = o;
     return Ly;
 }
@@ -193,11 +199,14 @@ struct LbgBatch {
     unsigned fail_mask;   // test hook: bit q = LM trial q's solve reports failure (spslam_debug_force_solve_failures)
     int* ctl;             // lbg_ctl_ints(n) ints, zeroed before the launch: [0] the workgroups' arrival ticket,
                           //   [16 (p + 1)] problem p's team barrier counter (one 64-byte line each)
+    int pw;               // the instance: pose-mask words (lbg_pw_for; the scratch laid out with lbg_layout(..., pw))
 };
 __host__ __device__ inline size_t lbg_ctl_ints(int n) { return 16 * ((size_t)n + 1); }
 // One launch: the whole optimize(5) / relabel / optimize(10) schedule of every problem, no host round trip.  The
 // ctl block is cleared on `s` first.
 hipError_t lba_run_g2o(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer);
+hipError_t lba_run_g2o_pw1(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer);
+hipError_t lba_run_g2o_pw2(const LbgBatch& b, const LbaConsts& C, hipStream_t s, KernelTimer* timer);
 
 // Runs the whole LocalBundleAdjustment schedule of a batch: enqueues the phase
 // kernels step by step on `s` and polls the device every few steps until

@@ -578,14 +578,17 @@ using namespace planes;
 
 hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const float* depth, long long depth_fs,
                         int depth_stride, spslam_plane* planes, int* plane_counts, int planes_cap, int32_t* inliers,
-                        int32_t* contours, hipStream_t s, KernelTimer* timer) {
+                        int32_t* contours, hipStream_t s, KernelTimer* timer, bool have_cloud) {
     if (g.H > kWaveThreads) return hipErrorInvalidValue;
     auto B = [&](int k) { if (timer) timer->begin(k, s); };
     auto E = [&](int k) { if (timer) timer->end(k, s); };
     const dim3 pts((g.N + 255) / 256, n);
-    B(kKindPlaneCloud);
-    hipLaunchKernelGGL(plane_cloud_kernel, pts, dim3(256), 0, s, g, depth, depth_fs, depth_stride, b.cloud, b.cloud_fs);
-    E(kKindPlaneCloud);
+    if (!have_cloud) {  // (else a fused grab made it: grab_kernels.hip)
+        B(kKindPlaneCloud);
+        hipLaunchKernelGGL(plane_cloud_kernel, pts, dim3(256), 0, s, g, depth, depth_fs, depth_stride, b.cloud,
+                           b.cloud_fs);
+        E(kKindPlaneCloud);
+    }
     B(kKindPlaneDist);
     static const bool barrier_wave = [] {
         const char* e = getenv("SPSLAM_PLANE_WAVE_BARRIER");

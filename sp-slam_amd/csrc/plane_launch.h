@@ -59,7 +59,8 @@ __host__ __device__ inline long long wave_index(int r, int c, int H) {
 
 hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const float* depth, long long depth_fs,
                         int depth_stride, spslam_plane* planes, int* plane_counts, int planes_cap,
-                        int32_t* inliers, int32_t* contours, hipStream_t s, KernelTimer* timer);
+                        int32_t* inliers, int32_t* contours, hipStream_t s, KernelTimer* timer,
+                        bool have_cloud = false);  // have_cloud: b.cloud already holds the depth's cloud
 
 // Segmentation stage alone (plane_segment.hip); needs cloud/normal/pd filled.
 // dynamic LDS bytes of the segmentation kernel; *in_lds: the per-frame maps (and 16-bit labels) live in LDS

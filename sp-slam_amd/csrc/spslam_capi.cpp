@@ -4,6 +4,7 @@
 // 410-470), the pyramid geometry, device scratch for `max_batch` frames and a
 // HIP stream.  Nothing here falls back to a CPU path: if the HIP runtime or
 // the gfx950 code object is unusable every entry point returns SPSLAM_ERR_HIP.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -107,6 +108,10 @@ struct spslam_ctx {
     PlaneGeom pg{};
     PlaneBuffers pb{};
     float* plane_cloud[2] = {nullptr, nullptr};  // organized-cloud sets (spslam_planes_select_cloud_set)
+    int cloud_set = 0;
+    // the depth output whose cloud a fused grab wrote into each set (spslam_grab_fuse_cloud); null = none
+    struct CloudTag { const float* depth = nullptr; int n = 0; } cloud_tag[2];
+    bool grab_cloud = [] { const char* e = getenv("SPSLAM_GRAB_CLOUD"); return !(e && e[0] == '0'); }();
     void* d_plane_scratch = nullptr;
     float* d_depth_in = nullptr;
     spslam_plane* d_planes1 = nullptr;
@@ -648,6 +653,8 @@ int spslam_planes_configure(spslam_ctx* c, const spslam_plane_params* p) {
     c->plane_cloud[0] = (float*)carve(F * b.cloud_fs * 4);
     c->plane_cloud[1] = (float*)carve(F * b.cloud_fs * 4);
     b.cloud = c->plane_cloud[0];
+    c->cloud_set = 0;
+    c->cloud_tag[0] = c->cloud_tag[1] = {};
     b.wave = (float*)carve(F * b.wave_fs * 4);
     b.dist = (float*)carve(F * b.dist_fs * 4);
     b.normal = (float*)carve(F * b.normal_fs * 4);
@@ -688,8 +695,13 @@ int spslam_planes_extract_batch_device(spslam_ctx* c, const float* d_depth, int 
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_planes_extract_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the default stream (header)
+    // a fused grab already wrote this depth's cloud into the selected set (spslam_grab_fuse_cloud)
+    auto& tag = c->cloud_tag[c->cloud_set];
+    const bool have_cloud = tag.depth == d_depth && n_frames <= tag.n &&
+                            frame_stride == (size_t)c->pg.w * c->pg.h && stride_floats == c->pg.w;
+    tag = {};
     HIP_CHECK(c, plane_launch(c->pg, c->pb, n_frames, d_depth, (long long)frame_stride, stride_floats, d_planes,
-                              d_counts, kMaxPlanesPerFrame, d_inliers, d_contours, s, c->timer));
+                              d_counts, kMaxPlanesPerFrame, d_inliers, d_contours, s, c->timer, have_cloud));
     c->plane_last_frames = n_frames;
     return SPSLAM_OK;
 }
@@ -737,6 +749,7 @@ int spslam_planes_select_cloud_set(spslam_ctx* c, int set) {
     if (!c->planes_ready) return fail(c, SPSLAM_ERR_NOT_READY, "spslam_planes_configure not called%s", "");
     if (set < 0 || set > 1) return fail(c, SPSLAM_ERR_ARG, "cloud set not 0 or 1%s", "");
     c->pb.cloud = c->plane_cloud[set];
+    c->cloud_set = set;
     return SPSLAM_OK;
 }
 
@@ -1076,6 +1089,10 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
     // is complete)
     HIP_CHECK(c, hipStreamWaitEvent(s, c->lba_done, 0));
     if (c->lba_order == SPSLAM_LBA_G2O_ORDER) {
+        // the instance: pose masks of one word (up to 64 free poses) unless a window has more keyframes than that
+        int max_kf = 0;
+        for (int i = 0; i < n; i++) max_kf = std::max(max_kf, problems[i].n_kf);
+        const int pw = lbg_pw_for(max_kf);
         size_t total = 0;
         for (int i = 0; i < n; i++) {
             const spslam_lba_problem& p = problems[i];
@@ -1086,7 +1103,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
                 return fail(c, SPSLAM_ERR_ARG, "missing LBA buffers%s", "");
             off[i] = (long long)total;
             total += lbg_layout(std::min(p.n_kf, kLbgMaxKeyframes), p.n_points, p.n_planes,
-                                p.n_point_obs + p.n_plane_obs).bytes;
+                                p.n_point_obs + p.n_plane_obs, pw).bytes;
         }
         if (total > c->lba_scratch_bytes) {
             HIP_CHECK(c, hipStreamSynchronize(s));
@@ -1116,7 +1133,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
         LbgBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                    d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
-                   c->lba_stop_after, team, c->solve_fail_mask, c->d_lba_ctl};
+                   c->lba_stop_after, team, c->solve_fail_mask, c->d_lba_ctl, pw};
         HIP_CHECK(c, lba_run_g2o(B, C, s, c->timer));
         HIP_CHECK(c, hipEventRecord(c->lba_done, s));
         if (stop_src) {  // host-buffer entry: mirror the caller's bool into the device-visible flag while it runs
@@ -1470,10 +1487,26 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* c, int n_frames, const uint8_t* d_
         return fail(c, SPSLAM_ERR_ARG, "bad argument%s", " to spslam_grab_rgbd_batch_device");
     HIP_CHECK(c, hipSetDevice(c->device));
     GrabArgs a{d_color, color_frame_stride, color_stride, d_depth, depth_frame_stride, depth_stride, w, h, *params,
-               d_gray, d_depth_out};
+               d_gray, d_depth_out, nullptr, 0, 1, 0, 0, 0.f, 0.f, 0.f, 0.f};
     // a CV_32F depth with |factor - 1| <= 1e-5 is used as is (Tracking.cc:228)
     if (!params->depth_u16 && std::fabs(params->depth_scale - 1.0f) <= 1e-5f) a.p.depth_scale = 1.0f;
+    // the organized cloud of the plane stage in the same pass (spslam_grab_fuse_cloud)
+    const bool cloud = c->grab_cloud && c->planes_ready && w == c->pg.w && h == c->pg.h && n_frames <= c->p.max_batch;
+    if (cloud) {
+        const PlaneGeom& g = c->pg;
+        a.cloud = c->pb.cloud; a.cloud_fs = c->pb.cloud_fs;
+        a.ds = g.ds; a.cW = g.W; a.cN = g.N;
+        a.fx = g.fx; a.fy = g.fy; a.cx = g.cx; a.cy = g.cy;
+    }
     HIP_CHECK(c, grab_launch(n_frames, a, (hipStream_t)hip_stream, c->timer));
+    if (cloud) c->cloud_tag[c->cloud_set] = {d_depth_out, n_frames};
+    return SPSLAM_OK;
+}
+
+int spslam_grab_fuse_cloud(spslam_ctx* c, int enable) {
+    if (!c) return SPSLAM_ERR_ARG;
+    c->grab_cloud = enable != 0;
+    if (!enable) c->cloud_tag[0] = c->cloud_tag[1] = {};
     return SPSLAM_OK;
 }
 

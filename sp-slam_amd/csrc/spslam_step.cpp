@@ -204,10 +204,10 @@ int tail(spslam_step* st, int j, const spslam_step_tracking& in, hipStream_t s) 
 // batch into extraction set j on the extraction streams (pipeline.py HotPath._extract)
 int extract(spslam_step* st, int j, const spslam_step_frames& fr) {
     if (hipStreamWaitEvent(st->s_orb, st->ev_tail[j], 0) != hipSuccess) return SPSLAM_ERR_HIP;
+    TRY(spslam_planes_select_cloud_set(st->ctx, j));  // (before the grab: a fused grab writes the set's cloud)
     TRY(grab(st, j, fr, st->s_orb));
     if (hipEventRecord(st->ev_grab[j], st->s_orb) != hipSuccess) return SPSLAM_ERR_HIP;
     if (hipStreamWaitEvent(st->s_planes, st->ev_grab[j], 0) != hipSuccess) return SPSLAM_ERR_HIP;
-    TRY(spslam_planes_select_cloud_set(st->ctx, j));
     TRY(planes(st, j, st->s_planes));
     if (hipEventRecord(st->ev_planes[j], st->s_planes) != hipSuccess) return SPSLAM_ERR_HIP;
     TRY(orb(st, j, st->s_orb));

@@ -53,7 +53,11 @@ CONFIGS = {
     # faces (synth._texture_low) and a hand-held trajectory with jolts (the motion model fails on them)
     "c1": dict(width=640, height=480, nfeatures=1000, n_boxes=5, texture="low", motion="shaky"),
     "c2": dict(width=640, height=480, nfeatures=1000, n_boxes=5),
-    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=5, lba_every=5),
+    # C3: LocalBundleAdjustment for every 5th frame over an fr1/room-sized window (25 local + 10 fixed keyframes,
+    # 4000 points); c3s keeps rounds 1-5's smaller window (10 local + 2 fixed keyframes, 1500 points)
+    "c3": dict(width=640, height=480, nfeatures=1000, n_boxes=5, lba_every=5, lba_kf=35, lba_fixed=10,
+               lba_points=4000, lba_kf_step=4),
+    "c3s": dict(width=640, height=480, nfeatures=1000, n_boxes=5, lba_every=5),
     "c4": dict(width=640, height=480, nfeatures=1000, n_boxes=5, K=synth.ICL, min_size=1000, chi=1000.0,
                vp_chi=200.0),
     "c5": dict(width=1280, height=960, nfeatures=4000, n_boxes=8),
@@ -66,7 +70,8 @@ def _ptr(t):
 
 class HotPath:
     def __init__(self, B, width=640, height=480, nfeatures=1000, n_boxes=3, seq_id=0, unique_frames=16,
-                 device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500,
+                 device=0, K=synth.TUM3, lba_every=0, lba_unique=4, lba_points=1500, lba_kf=12, lba_fixed=2,
+                 lba_kf_step=6,
                  pipelined=False, tail_priority=True, orb_priority=False, planes_priority=False, min_size=500, chi=300.0, vp_chi=300.0,
                  rotate_inputs=False, lba_order=0, native=False, lba_depth=0, lba_team=0, lookahead=1,
                  max_inflight=0, texture="dots", motion="smooth"):
@@ -155,7 +160,7 @@ class HotPath:
         self.n_lba = B // lba_every if lba_every else 0
         self.lba_every = lba_every
         if self.n_lba:
-            self._setup_lba(seq_id, lba_unique, lba_points, lba_depth, lba_team)
+            self._setup_lba(seq_id, lba_unique, lba_points, lba_depth, lba_team, lba_kf, lba_fixed, lba_kf_step)
         # rotate_inputs (tests): batch k's slot i takes the inputs of slot (i + k) % B -- images and the per-frame
         # tracking records together -- so consecutive batches differ and a stage reading the wrong buffer set shows
         self.rotate_inputs = rotate_inputs
@@ -425,7 +430,7 @@ class HotPath:
                 [sl(po, p["point_offset"], p["n_points"]).astype(bool) for p in P],
                 [sl(plo, p["plane_offset"], p["n_planes"]).astype(bool) for p in P])
 
-    def _setup_lba(self, seq_id, unique, n_points, depth=0, team=0):
+    def _setup_lba(self, seq_id, unique, n_points, depth=0, team=0, n_kf=12, n_fixed=2, kf_step=6):
         """LocalMapping beside tracking.  The step's local maps (one per `lba_every` frames) go to one batched
         LocalBundleAdjustment call on its own stream and context, like the reference's LocalMapping thread
         (LocalMapping.cc:48-124), which never blocks Tracking.  depth d: step k's call is joined at the end of step
@@ -436,11 +441,12 @@ class HotPath:
         import spslam_lba as L
         torch = self.torch
         probs = []
-        for u in range(min(unique, self.n_lba)):
+        for u in range(min(unique, self.n_lba)):  # keyframes every kf_step frames, the last n_fixed fixed cameras
             rng = np.random.default_rng(seq_id * 131 + u)
             f0 = 6 * u
-            probs.append(synth.lba_problem(self.scene, list(range(f0, f0 + 72, 6)), rng, n_fixed=2, n_points=n_points,
-                                           K=self.Ks))
+            probs.append(synth.lba_problem(self.scene, list(range(f0, f0 + n_kf * kf_step, kf_step)), rng,
+                                           n_fixed=n_fixed, n_points=n_points, K=self.Ks))
+        self.lba_window = dict(keyframes=n_kf, fixed=n_fixed, points=n_points, keyframe_step=kf_step)
         hdr = np.zeros(self.n_lba, L.LBA_PROBLEM_DTYPE)
         kf, pt, po, pl, plo = [], [], [], [], []
         nk = npt = npo = npl = nplo = 0
@@ -652,11 +658,12 @@ class HotPath:
             self._bind(j)
             orb_s.wait_event(self.ev_tail[j])
             self._load(orb_s)
+            # the unit's organized cloud alternates between its two sets (double-buffered like the other outputs);
+            # selected before the grab, which makes the cloud in the same pass (spslam_grab_fuse_cloud)
+            self.pe.select_cloud_set((m // self.lookahead) % 2)
             self.grab(orb_s.cuda_stream)
             self.ev_grab[j].record(orb_s)
             planes_s.wait_event(self.ev_grab[j])
-            # the unit's organized cloud alternates between its two sets (double-buffered like the other outputs)
-            self.pe.select_cloud_set((m // self.lookahead) % 2)
             self.planes(planes_s.cuda_stream)
             self.ev_planes[j].record(planes_s)
             self.orb(orb_s.cuda_stream)

@@ -8,7 +8,7 @@ import numpy as np
 
 import spslam_gpu
 
-spslam_gpu.EXPORTED += ["spslam_grab_rgbd", "spslam_grab_rgbd_batch_device"]
+spslam_gpu.EXPORTED += ["spslam_grab_rgbd", "spslam_grab_rgbd_batch_device", "spslam_grab_fuse_cloud"]
 
 
 class GrabParams(ctypes.Structure):
@@ -20,6 +20,7 @@ def _bind(lib):
     vp, ci, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
     lib.spslam_grab_rgbd.argtypes = [vp, vp, ci, vp, ci, ci, ci, vp, vp, vp]
     lib.spslam_grab_rgbd_batch_device.argtypes = [vp, ci, vp, sz, ci, vp, sz, ci, ci, ci, vp, vp, vp, vp]
+    lib.spslam_grab_fuse_cloud.argtypes = [vp, ci]
 
 
 class Grabber:
@@ -49,3 +50,7 @@ class Grabber:
         self.ex._check(self.ex.lib.spslam_grab_rgbd_batch_device(
             self.ex.ctx, n, d_color, color_frame_stride, color_stride, d_depth, depth_frame_stride, depth_stride,
             w, h, ctypes.byref(self.params), d_gray, d_depth_out, stream or None))
+
+    def fuse_cloud(self, enable):
+        """spslam_grab_fuse_cloud: batches on this context also make the plane stage's organized cloud."""
+        self.ex._check(self.ex.lib.spslam_grab_fuse_cloud(self.ex.ctx, int(bool(enable))))

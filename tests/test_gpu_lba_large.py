@@ -1,13 +1,15 @@
 """GPU parity: LocalBundleAdjustment with large local windows, bit-exact to the CPU oracle as in test_gpu_lba.py.
 
 The reference collects every covisible keyframe and every fixed camera that sees a local point or plane, with no cap
-(src/Optimizer.cc:1157-1250).  The device takes up to 1024 keyframes per problem of which up to 64 free poses (the
-64-bit pose masks; a reduced system of up to 384 rows).  Covered here: 18 / 25 free poses (n = 108 / 150: the
-factorisation's L in global memory past the LDS-resident n <= 96), 40 and 62 free poses (n = 240 / 372: four and six
-registers per lane, the dense pattern's 820 / 1953 Schur blocks past one task round), a window of 80 keyframes (48
-free + 32 fixed: more keyframes than the 64-bit masks, fewer free poses), and a window with more than 64 free poses
-(status -2, nothing else written).  And the team split: the same problem solved by 1 .. 8 workgroups is bit-identical
-(every sum keeps its order whatever the split)."""
+(src/Optimizer.cc:1157-1250).  The device takes up to 1024 keyframes per problem; windows of up to 64 keyframes run the
+narrow instance of k_lba_g2o (64-bit pose masks, up to 64 free poses, a reduced system of up to 384 rows), larger ones
+the wide instance (two-word pose masks: up to 128 free poses, n <= 768; lba_g2o_wide.hip).  Covered here: 18 / 25 free
+poses (n = 108 / 150: the factorisation's L in global memory past the LDS-resident n <= 96), 40 and 62 free poses
+(n = 240 / 372: four and six registers per lane, the dense pattern's 820 / 1953 Schur blocks past one task round), a
+window of 80 keyframes (48 free + 32 fixed: the wide instance with fewer free poses than the narrow one holds), 66, 98
+and 128 free poses (the wide instance past one mask word: n = 396 / 588 / 768, eight and twelve registers per lane),
+and a window with more than 128 free poses (status -2, nothing else written).  And the team split: the same problem
+solved by 1 .. 8 workgroups is bit-identical (every sum keeps its order whatever the split), narrow and wide."""
 import numpy as np
 import pytest
 
@@ -30,23 +32,26 @@ def _window(n_kf, n_fixed, step=4, n_points=2000, seed=None, planes=True):
                              n_points=n_points, first_kf_id=1, with_planes=planes)
 
 
-@pytest.mark.parametrize("n_kf,n_fixed,step", [(20, 2, 4), (27, 2, 4), (42, 2, 2), (64, 2, 3), (80, 32, 3)])
-def test_lba_large_windows_match_oracle(lba, n_kf, n_fixed, step):
-    """Free poses 18 .. 62 (n = 108 .. 372: one to six registers of the factorisation wave per lane, L past the
-    LDS-resident size), dense covisibility (step 2 / 3: every pose coupled with most others, hundreds of Schur
-    blocks), and 80 keyframes of which 32 fixed."""
+@pytest.mark.parametrize("n_kf,n_fixed,step,n_points", [(20, 2, 4, 2000), (27, 2, 4, 2000), (42, 2, 2, 2000),
+                                                         (64, 2, 3, 2000), (80, 32, 3, 2000), (68, 2, 3, 1200),
+                                                         (100, 2, 3, 1200), (130, 2, 3, 900)])
+def test_lba_large_windows_match_oracle(lba, n_kf, n_fixed, step, n_points):
+    """Free poses 18 .. 62 on the narrow instance (n = 108 .. 372: one to six registers of the factorisation wave per
+    lane, L past the LDS-resident size), dense covisibility (step 2 / 3: every pose coupled with most others, hundreds
+    of Schur blocks); 80 keyframes of which 32 fixed, and 66 / 98 / 128 free poses on the wide instance (a landmark's
+    blocks and the Schur pattern's rows past one mask word, reduced systems of 396 / 588 / 768 rows)."""
     import oracle_lba
     import test_gpu_lba
-    P = _window(n_kf, n_fixed, step)
+    P = _window(n_kf, n_fixed, step, n_points=n_points)
     o = oracle_lba.lba_optimize(*P[:6])
     test_gpu_lba._assert_identical(lba(*P[:6]), o, f"{n_kf} keyframes")
 
 
 def test_lba_more_free_poses_than_masks(lba):
-    """66 free poses: past the 64-bit pose masks -- status -2 (the drop-in entry reports the rejection), nothing
-    else written."""
+    """132 free poses: past the wide instance's two-word pose masks -- status -2 (the drop-in entry reports the
+    rejection), nothing else written."""
     import spslam_gpu
-    P = _window(68, 2, 3, n_points=600)
+    P = _window(134, 2, 3, n_points=400)
     with pytest.raises(spslam_gpu.SpslamError, match="rejected"):
         lba(*P[:6])
     hdr, kf_out, pt_out, pl_out, po_out, plo_out, res = __import__("test_gpu_lba")._batch(lba, [P])
@@ -61,7 +66,8 @@ def test_lba_team_split_bit_identical(lba, team):
     import test_gpu_lba
     lba.set_team(team)
     try:
-        for k, P in enumerate(test_gpu_lba._problems()[:2] + [_window(27, 2, 4, n_points=1200, seed=9)]):
+        for k, P in enumerate(test_gpu_lba._problems()[:2] + [_window(27, 2, 4, n_points=1200, seed=9),
+                                                                 _window(72, 2, 3, n_points=600, seed=11)]):
             test_gpu_lba._assert_identical(lba(*P[:6]), oracle_lba.lba_optimize(*P[:6]), f"team {team} problem {k}")
     finally:
         lba.set_team(0)

@@ -4,6 +4,7 @@
 # Steps run in order, each under its own time limit; the first failing step ends the call.
 #   tests                 pytest -m gpu over tests/ (verbose, thread timeout per test)
 #   tests:F1,F2           pytest over the given test files only
+#   testsk:F1,F2:EXPR     pytest over the files with -k EXPR (_ for spaces); failing tests do not end the call
 #   smoke                 __graft_entry__.smoke()
 #   bench:CFG[:EXTRA]     python bench.py --config CFG --steps 20 --warmup 3 EXTRA (EXTRA: '_' for spaces)
 #   prof:CFG              rocprofv3 --kernel-trace --stats over a short bench of CFG (no CPU baseline / ATE)
@@ -28,6 +29,14 @@ for step in "$@"; do
             timeout -k 10 900 python -u -m pytest $files -m gpu -x -v --timeout 300 --timeout-method thread \
                 > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
             tail -3 gpurun_out/${TAG}_tests.log ;;
+        testsk)  # testsk:F1,F2:EXPR -- the given files, -k EXPR ('_' for spaces), no -x
+            files=$(echo "${arg%%:*}" | tr ',' ' ')
+            expr=$(echo "${arg#*:}" | tr '_' ' ')
+            timeout -k 10 900 python -u -m pytest $files -m gpu -v --timeout 300 --timeout-method thread -k "$expr" \
+                > gpurun_out/${TAG}_tests.log 2>&1
+            rc=$?
+            tail -3 gpurun_out/${TAG}_tests.log
+            [ $rc -le 1 ] || exit 1 ;;  # test failures go on; a time limit, crash or usage error ends the call
         smoke)
             timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
                 || { tail -30 gpurun_out/${TAG}_smoke.log; exit 1; }

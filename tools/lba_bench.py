@@ -1,6 +1,7 @@
 """Diagnostic: the C3 LocalMapping workload alone -- one batched LocalBundleAdjustment call over the step's
-local maps (51 maps of 12 keyframes / 1500 points at B = 256), wall time and LM step count.
-    python tools/lba_bench.py [--reps 5] [--order g2o|fast]"""
+local maps (51 maps at B = 256; --config c3s: 12 keyframes / 1500 points, c3: the fr1/room-sized window of 35
+keyframes / 4000 points), wall time and LM step count.
+    python tools/lba_bench.py [--reps 5] [--order g2o|fast] [--config c3s|c3]"""
 import argparse
 import pathlib
 import sys
@@ -15,6 +16,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--order", default="g2o", choices=("g2o", "fast"))
+    ap.add_argument("--config", default="c3s", choices=("c3s", "c3"))
     ap.add_argument("--team", type=int, nargs="*", default=[0], help="workgroups per problem (0 = auto); several: "
                     "interleaved")
     a = ap.parse_args()
@@ -22,7 +24,7 @@ def main():
     import torch
     import pipeline
     import spslam_lba as L
-    hp = pipeline.HotPath(a.batch, lba_order=0 if a.order == "g2o" else 1, **pipeline.CONFIGS["c3"])
+    hp = pipeline.HotPath(a.batch, lba_order=0 if a.order == "g2o" else 1, **pipeline.CONFIGS[a.config])
     for r in range(a.reps * len(a.team)):
         team = a.team[r % len(a.team)]
         hp.lba.set_team(team)
