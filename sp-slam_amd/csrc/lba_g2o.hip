@@ -1340,7 +1340,9 @@ __device__ __noinline__ void structure() {
             }
             if (lane == 0) g.parent[j] = par;  // (each lane reads and writes its own word of acc only)
         }
-        if (lane == 0) g.Lbits[n * kNW] = 0;  // the factorisation's masked-step structure word
+        // the factorisation's masked-step structure words (a ring step past a piece's end reads row n's kC words:
+        // all of them zero, not only the first -- the rest would be whatever an earlier call left in the scratch)
+        if (lane < kNW) g.Lbits[n * kNW + lane] = 0;
     }
     __syncthreads();
     // each row k of L: its pattern {i : k in struct L(:, i)} in factorize_preordered's order -- ap's column k
@@ -1492,9 +1494,8 @@ __device__ __forceinline__ double ordered_sum(const PD* v, int n32) {
 
 // the same over LDS, 16-byte reads: 8 loads per batch of 16 values, so the wait for one batch can leave the next
 // batch in flight (the LDS counter holds at most 15 outstanding loads; 16 single loads would force a full wait)
-__device__ __forceinline__ double ordered_sum_lds(const double* v, int n32) {
+__device__ __forceinline__ double ordered_sum_lds(const double* v, int n32, double acc = 0.0) {
     const double2* w = (const double2*)v;
-    double acc = 0.0;
     double2 A[8], B[8];
     const double2 z = make_double2(0.0, 0.0);
 #pragma unroll
@@ -1539,11 +1540,31 @@ __device__ __noinline__ void sums_staged(int nE, int nS) {
         }
         if (t == 64 && nS > 0) s.scale = ordered_sum_lds(V + nE, nS);
     } else {
+        // larger graphs: chunks of kHalf values through two LDS buffers, wave 0's lane 0 adding one chunk (the chain
+        // carried across chunks: the same sequence of additions) while the other waves stage the next
+        constexpr int kHalf = kDyn / 16;
+        auto chain = [&](auto src, int n) __attribute__((always_inline)) {
+            double acc = 0.0;
+            for (int i = t; i < min(kHalf, n); i += kT) V[i] = src[i];
+            __syncthreads();
+            for (int c = 0; c * kHalf < n; c++) {
+                const int b0 = c * kHalf, nb = min(kHalf, n - b0), n0 = b0 + kHalf, nn = max(0, min(kHalf, n - n0));
+                double* nxt = V + ((c + 1) & 1) * kHalf;
+                if (t == 0) acc = ordered_sum_lds(V + (c & 1) * kHalf, nb, acc);
+                else if (t >= 64)
+                    for (int i = t - 64; i < nn; i += kT - 64) nxt[i] = src[n0 + i];
+                __syncthreads();
+            }
+            return acc;
+        };
+        const double c = chain(g.echi, nE);
         if (t == 0) {
-            const double c = ordered_sum(g.echi, nE);
             if (nS > 0) s.tempChi = c; else s.currentChi = c;
         }
-        if (t == 64 && nS > 0) s.scale = ordered_sum(g.sc, nS);
+        if (nS > 0) {
+            const double sc = chain(g.sc, nS);
+            if (t == 0) s.scale = sc;
+        }
     }
 }
 
@@ -2544,7 +2565,10 @@ __device__ __forceinline__ void factor_body(PD* LD, const PU* LB, const PI_* RO,
         // while a step runs (a ring of operand sets, each written only by its fetch and read only by its step).
         // Past the piece's end the entries repeat its last one with the structure word LB[n kNW] (zero): masked
         // steps.  A column's rows past n read the next one's (in the LDS layout; unused: masked by r < k).
-        constexpr int kRing = kPacked ? 6 : 2;
+        // (a divisor of 64: a piece's last ring round ends at step 63 -- with 6, a full piece of 64 entries ran two
+        // steps past it, on entry 63's operands refetched and entry 0's lane select).  Global-memory pieces are L2
+        // latency bound: a deeper ring where the registers allow it (kC <= 3: 8 operand sets, kC <= 6: 4)
+        constexpr int kRing = kPacked ? 8 : kC <= 3 ? 8 : kC <= 6 ? 4 : 2;
         const char* LDc = (const char*)LD;
         const char* LBc = (const char*)LB;
         // rows r < k of register m as a lane mask: a step's update condition is one bit test (a select, no
@@ -2734,7 +2758,7 @@ struct FactorLds { size_t LB, RO, RS, PI, SP, PR, D, PG, end; };
 __device__ __forceinline__ FactorLds factor_lds(int n) {
     FactorLds f;
     f.LB = (size_t)n * n * 8;
-    f.RO = f.LB + (size_t)(n * kNW + 1) * 8;  // LB[n kNW] = 0
+    f.RO = f.LB + (size_t)(n + 1) * kNW * 8;  // row n: LB[n kNW ..] = 0
     f.RS = f.RO + (size_t)(n + 1) * 4;
     f.PI = f.RS + (size_t)((n * (n + 1)) / 2 + 1) * 4;
     f.SP = (f.PI + (size_t)n * 4 + 7) & ~(size_t)7;
@@ -2744,7 +2768,7 @@ __device__ __forceinline__ FactorLds factor_lds(int n) {
     f.end = f.PG + (size_t)(n + 1) * 4;
     return f;
 }
-static_assert((size_t)kLdsN * kLdsN * 8 + (kLdsN * kNW + 1) * 8 + (kLdsN + 1) * 4 + (kLdsN * (kLdsN + 1) / 2 + 1) * 4 +
+static_assert((size_t)kLdsN * kLdsN * 8 + ((kLdsN + 1) * kNW) * 8 + (kLdsN + 1) * 4 + (kLdsN * (kLdsN + 1) / 2 + 1) * 4 +
                   kLdsN * 4 + 8 + (kLdsN * (kLdsN + 1) / 2) * 8 + 64 * 8 + kLdsN * 8 + (kLdsN + 1) * 4 <= (size_t)kDyn,
               "the factorisation's LDS copy");
 
@@ -2818,6 +2842,135 @@ __device__ __noinline__ void factor_dense() {
     __syncthreads();
     if (t == 0) s.ok = *FL == 0;
     __syncthreads();
+}
+
+// The same pipelined factorisation for dense systems too large for factor_dense's LDS copy (kLdsN < n <= kPackN,
+// e.g. a window of 25 free poses, n = 150): L packed column by column in LDS (column i's rows i + 1 .. n - 1, a guard
+// in front so that the masked reads of rows <= i stay in range), S read from global memory once per row, D and the
+// progress words in LDS.  Then the solve (factor_body's order with every column's structure "all rows below").
+constexpr int kPackN = 180;
+__host__ __device__ constexpr int pk_col(int i, int n) { return (i * (2 * n - i - 1)) / 2 - i - 1 + n; }  // L(r, i) at + r
+__host__ __device__ constexpr size_t pk_words(int n, int kC) { return (size_t)n + (size_t)n * (n - 1) / 2 + 64 * kC; }
+static_assert((pk_words(kPackN, 3) + kPackN) * 8 + (kPackN + 1) * 4 <= (size_t)kDyn, "packed dense factorisation");
+template <int kC>
+__device__ __noinline__ void factor_dense_packed() {
+    const G& g = lbg_g;
+    Sh& s = lbg_s;
+    const int n = 6 * s.np;
+    double* LP = (double*)lbg_dyn;
+    double* D = LP + pk_words(n, kC);
+    volatile int* PG = (volatile int*)(D + n);
+    volatile int* FL = PG + n;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int k = t; k <= n; k += kT) PG[k] = 0;  // (PG[n] = FL)
+    __syncthreads();
+    for (int k = w; k < n; k += kW) {
+        double y[kC];
+#pragma unroll
+        for (int m = 0; m < kC; m++) {
+            const int r = 64 * m + lane;
+            y[m] = r <= k ? 0.0 + g.S[(size_t)r * n + k] : 0.0;
+        }
+        double d = pick(y, k) * 1.0 + 0.0;
+        int seen = 0;
+        bool failed = false;
+        for (int i = 0; i < k; i++) {
+            while (seen <= i) {  // row k - 1 has published L(k - 1, i)
+                seen = __builtin_amdgcn_readfirstlane(PG[k - 1]);
+                if (seen <= i) {
+                    if (*FL) { failed = true; break; }
+                    __builtin_amdgcn_s_sleep(0);
+                }
+            }
+            if (failed) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const double yi = pick(y, i);
+            const double Di = D[i];
+            const double* col = LP + pk_col(i, n);
+            double v[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) v[m] = col[64 * m + lane];  // L(r, i): rows i < r < k published
+            const double l = yi / Di;
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                const double nv = y[m] - v[m] * yi;
+                y[m] = (r > i && r < k) ? nv : y[m];
+            }
+            d -= l * yi;
+            if (lane == 0) LP[pk_col(i, n) + k] = l;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) PG[k] = i + 1;
+        }
+        if (failed) break;
+        if (d == 0.0) {  // Eigen stops at a zero pivot (ok = false); the other rows see the flag and stop
+            if (lane == 0) *FL = 1;
+            break;
+        }
+        if (lane == 0) D[k] = d;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) PG[k] = k + 1;
+    }
+    __syncthreads();
+    if (t == 0) s.ok = *FL == 0;
+    __syncthreads();
+}
+// x = P b; L x = x; x = D^-1 x; L^T x = x; x = P^-1 x (factor_body's solve, every column's structure the rows below it);
+// one wave
+template <int kC>
+__device__ __noinline__ void solve_dense_packed() {
+    const G& g = lbg_g;
+    const Sh& s = lbg_s;
+    if (!s.ok) return;
+    const int n = 6 * s.np, lane = threadIdx.x & 63;
+    const double* LP = (const double*)lbg_dyn;
+    const double* D = LP + pk_words(n, kC);
+    double tv[kC], Dg[kC];
+#pragma unroll
+    for (int m = 0; m < kC; m++) {
+        const int r = 64 * m + lane;
+        tv[m] = r < n ? g.bs[g.Pinv[r]] : 0.0;
+        Dg[m] = r < n ? D[r] : 0.0;
+    }
+    if (n > 1)
+        for (int i = 0; i < n; i++) {
+            const double tmp = pick(tv, i);
+            if (tmp != 0.0) {
+                const double* col = LP + pk_col(i, n);
+#pragma unroll
+                for (int m = 0; m < kC; m++) {
+                    const int r = 64 * m + lane;
+                    if (r > i && r < n) tv[m] = tv[m] - tmp * col[r];
+                }
+            }
+        }
+#pragma unroll
+    for (int m = 0; m < kC; m++)
+        if (64 * m + lane < n) tv[m] = (1.0 / Dg[m]) * tv[m];
+    if (n > 1)
+        for (int i = n - 1; i >= 0; i--) {
+            const double* col = LP + pk_col(i, n);
+            double pr[kC];
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int r = 64 * m + lane;
+                pr[m] = (r > i && r < n) ? col[r] * tv[m] : 0.0;
+            }
+            double tmp = pick(tv, i);
+#pragma unroll
+            for (int m = 0; m < kC; m++) {
+                const int lo = max(i + 1 - 64 * m, 0), hi = min(n - 64 * m, 64);  // lanes of rows i < r < n
+                for (int q = lo; q < hi; q++) tmp -= rl(pr[m], q);
+            }
+#pragma unroll
+            for (int m = 0; m < kC; m++)
+                if (64 * m + lane == i) tv[m] = tmp;
+        }
+#pragma unroll
+    for (int m = 0; m < kC; m++) {
+        const int r = 64 * m + lane;
+        if (r < n) g.x[g.Pinv[r]] = tv[m];
+    }
 }
 
 template <int kC, bool kLds, bool kPre = false>
@@ -3161,7 +3314,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                     if (t == 0) { s.ok = 0; g.team->ok = 0; }
                 } else if (lead) {
                     if (lds) {  // the factorisation's symbolic data into LDS (the other phases use the same LDS)
-                        for (int i = t; i <= n * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
+                        for (int i = t; i < (n + 1) * kNW; i += kT) LB[i] = i < n * kNW ? g.Lbits[i] : 0ull;
                         for (int i = t; i <= n; i += kT) RO[i] = g.rs_off[i];
                         const int nz = g.rs_off[n];
                         for (int i = t; i < nz; i += kT) RS[i] = g.rs_idx[i];
@@ -3182,6 +3335,13 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
                         if (t < 64) {
                             if (n <= 64) factor_solve<1, true, true>();
                             else factor_solve<2, true, true>();
+                        }
+                    } else if (s.dense && n <= kPackN) {  // dense, past the LDS copy: L packed in LDS
+                        if (n <= 128) factor_dense_packed<2>();
+                        else factor_dense_packed<3>();
+                        if (t < 64) {
+                            if (n <= 128) solve_dense_packed<2>();
+                            else solve_dense_packed<3>();
                         }
                     } else if (t < 64) {
                         if (n <= 64) factor_solve<1, true>();

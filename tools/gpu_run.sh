@@ -33,9 +33,9 @@ for step in "$@"; do
             files=$(echo "${arg%%:*}" | tr ',' ' ')
             expr=$(echo "${arg#*:}" | tr '_' ' ')
             timeout -k 10 900 python -u -m pytest $files -m gpu -v --timeout 300 --timeout-method thread -k "$expr" \
-                > gpurun_out/${TAG}_tests.log 2>&1
+                > gpurun_out/${TAG}_testsk.log 2>&1
             rc=$?
-            tail -3 gpurun_out/${TAG}_tests.log
+            tail -3 gpurun_out/${TAG}_testsk.log
             [ $rc -le 1 ] || exit 1 ;;  # test failures go on; a time limit, crash or usage error ends the call
         smoke)
             timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \

@@ -1,6 +1,7 @@
 """Diagnostic: where a LocalBundleAdjustment window first differs from the oracle -- per team size, the state after
 LM trial k (pbStopFlag raised by the device's stop-after hook) against the oracle's after the same trial.
-    python tools/lba_wide_diag.py [--windows 130:2:3:900 66:2:3:900] [--teams 1 8] [--trials 1 2 3 4 6]"""
+    python tools/lba_wide_diag.py [--windows 130:2:3:900 66:2:3:900 27:2:4:1200:9] [--teams 1 8] [--trials 1 2 3 4 6]
+(a trial count of 0: the full run, no stop flag)"""
 import argparse
 import pathlib
 import sys
@@ -23,16 +24,16 @@ def main():
     ex = spslam_gpu.OrbExtractor(max_batch=1)
     lba = L.LocalBA(ex)
     for w in a.windows:
-        n_kf, n_fixed, step, n_pts = (int(x) for x in w.split(":"))
-        P = T._window(n_kf, n_fixed, step, n_points=n_pts)
+        f = [int(x) for x in w.split(":")]  # keyframes:fixed:step:points[:seed]
+        P = T._window(f[0], f[1], f[2], n_points=f[3], **({"seed": f[4]} if len(f) > 4 else {}))
         full = oracle_lba.lba_optimize(*P[:6])
         print(f"window {w}: free {int((P[1]['fixed'] == 0).sum())}, oracle iterations "
               f"{list(full['result']['iterations'])} trials {int(full['result']['trials'])}", flush=True)
         for k in a.trials:
-            o = oracle_lba.lba_optimize(*P[:6], stop_after=k)
+            o = oracle_lba.lba_optimize(*P[:6], stop_after=k if k > 0 else -1)
             for team in a.teams:
                 lba.set_team(team)
-                lba.debug_stop_after(k)
+                lba.debug_stop_after(k if k > 0 else -1)
                 g = lba(*P[:6])
                 lba.debug_stop_after(-1)
                 dT = float(np.abs(g["Tcw"] - o["Tcw"]).max())
