@@ -770,15 +770,17 @@ int spslam_grab_rgbd_batch_device(spslam_ctx* ctx, int n_frames, const uint8_t* 
                                   void* hip_stream);
 
 /* Fusion with the plane stage (no reference counterpart: Frame::ComputePlanesFromOrganizedPointCloud,
- * Frame.cc:857-874, samples the converted depth a second time).  With enable = 1 (the default) and
+ * Frame.cc:857-874, samples the converted depth a second time).  With enable = 1 and
  * spslam_planes_configure called on the same context for the same image size, a
  * spslam_grab_rgbd_batch_device call also writes the organized cloud of its depth output into the
  * selected cloud set (spslam_planes_select_cloud_set) and tags the set with that depth output; the
  * set's next spslam_planes_extract_batch_device over exactly that depth (same pointer, dense layout,
  * no more frames) uses the cloud as it is instead of sampling the depth again (bit-identical cloud),
  * and clears the tag.  Any other extraction makes its own cloud.  The caller orders the grab before
- * the extraction (same stream or an event), as it already must for the depth.  The environment
- * variable SPSLAM_GRAB_CLOUD=0 makes 0 the default. */
+ * the extraction (same stream or an event), as it already must for the depth.  Default 0: in the
+ * pipelined batch step the grab is on the ORB stream's critical path and the fused pass measured 2 %
+ * slower than a separate cloud kernel on the plane stream (profiles/r06/ab_grab_cloud_c2.txt); the
+ * environment variable SPSLAM_GRAB_CLOUD=1 makes 1 the default. */
 int spslam_grab_fuse_cloud(spslam_ctx* ctx, int enable);
 
 /* ---------------------------------------------------------------- tracking graph glue

@@ -2013,10 +2013,6 @@ constexpr int kBW = SPSLAM_LBG_SCHUR_BLOCKS;  // blocks per wave per round
 #define SPSLAM_LBG_SCHUR_TASKS 2
 #endif
 constexpr int kSchurTasks = SPSLAM_LBG_SCHUR_TASKS;  // schur_rows: chains per lane per round
-#ifndef SPSLAM_LBG_ROWS_MAX_TEAM
-#define SPSLAM_LBG_ROWS_MAX_TEAM 4
-#endif
-constexpr int kRowsMaxTeam = SPSLAM_LBG_ROWS_MAX_TEAM;  // teams up to this size use schur_rows
 // (Hll + lambda)^-1 (Eigen's cofactor inverse) and Dinv bl of one landmark
 __device__ __forceinline__ void landmark_dinv(const double* H, const double* bv, double lam, double* Di, double* db) {
     double D[3][3];
@@ -2283,10 +2279,14 @@ __device__ __noinline__ void schur() {
     }
 }
 
-// The same Schur complement with one lane per (block, row r) holding the row's six entries (and the diagonal block's
-// Bb(r)), each lane walking its own candidate landmarks: fewer LDS bytes per entry than schur()'s lane per entry, but
-// a dependent LDS round trip per landmark.  The faster of the two when a member holds many blocks (teams of 1 - 2).
+// The same Schur complement with one lane per (block, R rows r0 .. r0 + R - 1) holding those rows' entries (and the
+// diagonal block's Bb(r)), each lane walking its own candidate landmarks, TT such tasks per lane: fewer LDS bytes per
+// entry than schur()'s lane per entry (a landmark's Bj block is read once for R rows), but a dependent LDS round trip
+// per landmark.  The faster of the two when a member holds many blocks (teams of 1 - 4); R and TT are chosen per call
+// from the member's block count (schur_rows_pick): every chain keeps g2o's landmark order whatever the split.
+template <int R, int TT>
 __device__ __noinline__ void schur_rows() {
+    constexpr int kG = 6 / R;  // row groups per block
     const G& g = lbg_g;
     Sh& s = lbg_s;
     unsigned char* dyn = lbg_dyn;
@@ -2313,16 +2313,16 @@ __device__ __noinline__ void schur_rows() {
     const int bo0 = s.bo0, nbm = s.bo1 - s.bo0;
     const PMask rmask = s.rmask;
     using LdsD = const __attribute__((address_space(3))) double;
-    for (int round = 0; round * kSchurTasks * kT < 6 * nbm; round++) {
-        int i1[kSchurTasks], i2[kSchurTasks], rr[kSchurTasks];
-        double acc[kSchurTasks][6], cf[kSchurTasks];
+    for (int round = 0; round * TT * kT < kG * nbm; round++) {
+        int i1[TT], i2[TT], rr[TT];
+        double acc[TT][R][6], cf[TT][R];
 #pragma unroll
-        for (int k = 0; k < kSchurTasks; k++) {
+        for (int k = 0; k < TT; k++) {
             i1[k] = -1; i2[k] = 0; rr[k] = 0;
-            const int task = (round * kSchurTasks + k) * kT + t;
-            if (task < 6 * nbm) {
-                const int jb = task / 6;
-                rr[k] = task - 6 * jb;
+            const int task = (round * TT + k) * kT + t;
+            if (task < kG * nbm) {
+                const int jb = task / kG;
+                rr[k] = R * (task - kG * jb);
                 const int blk = g.bord[bo0 + jb];
                 if (blk < np) {
                     i1[k] = i2[k] = blk;
@@ -2336,14 +2336,18 @@ __device__ __noinline__ void schur_rows() {
                 }
             }
             const bool diag = i1[k] >= 0 && i1[k] == i2[k];
-            const int r = rr[k];
 #pragma unroll
-            for (int c = 0; c < 6; c++) {
-                double base = 0.0;
-                if (diag && c >= r) base = c == r ? g.Hps[27 * i1[k] + upper_idx(r, c)] + lam : g.Hps[27 * i1[k] + upper_idx(r, c)];
-                acc[k][c] = 0.0 + base;
+            for (int q = 0; q < R; q++) {
+                const int r = rr[k] + q;
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    double base = 0.0;
+                    if (diag && c >= r)
+                        base = c == r ? g.Hps[27 * i1[k] + upper_idx(r, c)] + lam : g.Hps[27 * i1[k] + upper_idx(r, c)];
+                    acc[k][q][c] = 0.0 + base;
+                }
+                cf[k][q] = 0.0;
             }
-            cf[k] = 0.0;
         }
         // chunk c's records into registers (global loads in flight), later into the staging buffer.  Every load is
         // unconditional (addresses clamped into the chunk; the surplus entries are never read) and nothing loaded is
@@ -2448,7 +2452,7 @@ __device__ __noinline__ void schur_rows() {
 #endif
             if (c + 1 < nch) prefetch(cur_h1, nx_h1, cur_k1, nx_k1);  // lands while chunk c is processed
 #pragma unroll
-            for (int k = 0; k < kSchurTasks; k++) {
+            for (int k = 0; k < TT; k++) {
                 if (i1[k] < 0) continue;
                 const int r = rr[k];
                 uint64_t cand = PM[i1[k]] & PM[i2[k]];
@@ -2471,20 +2475,29 @@ __device__ __noinline__ void schur_rows() {
                     for (;;) {
                         LdsD* BD = SDr + __umul24(b1, 18);  // (24-bit products: full-rate multiplies)
                         LdsD* Bj = BUFl + __umul24(b2, 18);
-                        const double e0 = BD[0], e1 = BD[1], e2 = BD[2];
+                        double e[3 * R];
+#pragma unroll
+                        for (int q = 0; q < 3 * R; q++) e[q] = BD[q];  // BDinv rows r .. r + R - 1
                         double bj[18];
 #pragma unroll
                         for (int q = 0; q < 18; q++) bj[q] = Bj[q];
-                        const double u = SUr[__umul24(b1, 6)];  // (b1 = b2 on the diagonal lanes)
+                        double u[R];
+#pragma unroll
+                        for (int q = 0; q < R; q++) u[q] = SUr[__umul24(b1, 6) + q];  // (b1 = b2 on the diagonal)
                         const bool more = cand != 0;
                         const int hn = more ? __ffsll((unsigned long long)cand) - 1 : hl;
                         cand &= cand - 1;
                         const int b1n = O1[hn], b2n = O2[hn];
 #pragma unroll
-                        for (int cc = 0; cc < 6; cc++)
-                            acc[k][cc] -= (e0 * bj[3 * cc] + e1 * bj[3 * cc + 1]) + e2 * bj[3 * cc + 2];
-                        cf[k] += u;  // (kept for the diagonal lanes only: unconditional, so the load is not sunk
-                                     // into a branch that waits for the next landmark's loads too)
+                        for (int q = 0; q < R; q++)
+#pragma unroll
+                            for (int cc = 0; cc < 6; cc++)
+                                acc[k][q][cc] -= (e[3 * q] * bj[3 * cc] + e[3 * q + 1] * bj[3 * cc + 1]) +
+                                                 e[3 * q + 2] * bj[3 * cc + 2];
+#pragma unroll
+                        for (int q = 0; q < R; q++)
+                            cf[k][q] += u[q];  // (kept for the diagonal lanes only: unconditional, so the load is not
+                                               // sunk into a branch that waits for the next landmark's loads too)
                         if (!more) break;
                         hl = hn;
                         b1 = b1n;
@@ -2507,13 +2520,46 @@ __device__ __noinline__ void schur_rows() {
 #endif
         }
 #pragma unroll
-        for (int k = 0; k < kSchurTasks; k++) {
+        for (int k = 0; k < TT; k++) {
             if (i1[k] < 0) continue;
-            const int r = rr[k];
 #pragma unroll
-            for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][cc];
-            if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k];
+            for (int q = 0; q < R; q++) {
+                const int r = rr[k] + q;
+#pragma unroll
+                for (int cc = 0; cc < 6; cc++) g.S[(size_t)(6 * i1[k] + r) * n + 6 * i2[k] + cc] = acc[k][q][cc];
+                if (i1[k] == i2[k]) g.bs[6 * i1[k] + r] = g.Hps[27 * i1[k] + 21 + r] - cf[k][q];
+            }
         }
+    }
+}
+// the row-group layout for this member's nbm blocks: fewest passes over the landmark chunks first (each pass stages
+// every chunk again), then the least time per landmark step -- the largest of one lane's dependent step (an LDS
+// round trip, ~120 clocks, then its fp64 work: 4 clocks per wave instruction, 6 per entry + 1 per Bb term), the
+// busiest SIMD's fp64 issue and the waves' LDS reads (bytes / 128 per clock).  Measured: 55 blocks per member
+// (12-keyframe maps) run fastest with one row per task, 325 (25 free poses) with two rows and two tasks per lane.
+__device__ __forceinline__ int schur_rows_pick(int nbm) {
+    const int R[4] = {6, 3, 2, 1}, TT[4] = {1, 1, 2, 2};
+    int best = 3;
+    long long best_cost = -1;
+    for (int v = 0; v < 4; v++) {
+        const long long tasks = (long long)(6 / R[v]) * nbm, slots = (long long)kT * TT[v];
+        const long long rounds = (tasks + slots - 1) / slots;
+        const long long per_round = (tasks + rounds - 1) / max(rounds, 1ll);
+        const long long waves = (per_round + 64 * TT[v] - 1) / (64 * TT[v]);
+        const long long lds = waves * 64 * TT[v] * (4 * R[v] + 18) * 8 / 128;
+        const long long step = (long long)TT[v] * (37 * R[v]) * 4;
+        const long long issue = (waves + 3) / 4 * step;
+        const long long cost = rounds * 1000000 + rounds * max(max(lds, issue), 120 + step);
+        if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = v; }
+    }
+    return best;
+}
+__device__ __forceinline__ void schur_rows_any() {
+    switch (schur_rows_pick(lbg_s.bo1 - lbg_s.bo0)) {
+        case 0: schur_rows<6, 1>(); break;
+        case 1: schur_rows<3, 1>(); break;
+        case 2: schur_rows<2, 2>(); break;
+        default: schur_rows<1, kSchurTasks>(); break;
     }
 }
 
@@ -3305,7 +3351,7 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             bool more = true;
             while (more) {
                 LBG_MARK(1);
-                if (s.T <= kRowsMaxTeam) schur_rows();
+                if (s.T <= b.rows_max_team) schur_rows_any();
                 else schur();
                 team_sync(b);
                 LBG_MARK(5);

@@ -200,6 +200,7 @@ struct LbgBatch {
     int* ctl;             // lbg_ctl_ints(n) ints, zeroed before the launch: [0] the workgroups' arrival ticket,
                           //   [16 (p + 1)] problem p's team barrier counter (one 64-byte line each)
     int pw;               // the instance: pose-mask words (lbg_pw_for; the scratch laid out with lbg_layout(..., pw))
+    int rows_max_team;    // teams up to this size use the row-group Schur layout (SPSLAM_LBG_ROWS_MAX_TEAM, default 4)
 };
 __host__ __device__ inline size_t lbg_ctl_ints(int n) { return 16 * ((size_t)n + 1); }
 // One launch: the whole optimize(5) / relabel / optimize(10) schedule of every problem, no host round trip.  The

@@ -111,7 +111,7 @@ struct spslam_ctx {
     int cloud_set = 0;
     // the depth output whose cloud a fused grab wrote into each set (spslam_grab_fuse_cloud); null = none
     struct CloudTag { const float* depth = nullptr; int n = 0; } cloud_tag[2];
-    bool grab_cloud = [] { const char* e = getenv("SPSLAM_GRAB_CLOUD"); return !(e && e[0] == '0'); }();
+    bool grab_cloud = [] { const char* e = getenv("SPSLAM_GRAB_CLOUD"); return e && e[0] == '1'; }();
     void* d_plane_scratch = nullptr;
     float* d_depth_in = nullptr;
     spslam_plane* d_planes1 = nullptr;
@@ -1059,6 +1059,15 @@ int spslam_frame_rgbd(spslam_ctx* c, const spslam_keypoint* kps, int n, const fl
 }
 
 namespace {
+// the Schur layout's team threshold (measurement knob; the results do not depend on it)
+int lba_rows_max_team() {
+    static const int v = [] {
+        const char* e = getenv("SPSLAM_LBG_ROWS_MAX_TEAM");
+        return e ? atoi(e) : 4;
+    }();
+    return v;
+}
+
 int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const spslam_lba_problem* d_problems,
               const spslam_lba_keyframe* d_kfs, const spslam_lba_point* d_points,
               const spslam_lba_point_obs* d_point_obs, const spslam_lba_plane* d_planes,
@@ -1133,7 +1142,7 @@ int lba_batch(spslam_ctx* c, int n, const spslam_lba_problem* problems, const sp
         HIP_CHECK(c, hipMemcpyAsync(c->d_lba_off, off.data(), (size_t)n * sizeof(long long), hipMemcpyHostToDevice, s));
         LbgBatch B{n, d_problems, c->d_lba_off, c->d_lba_scratch, d_kfs, d_points, d_point_obs, d_planes, d_plane_obs,
                    d_kf_out, d_pt_out, d_pl_out, d_point_obs_outlier, d_plane_obs_outlier, d_results, d_stop_flags,
-                   c->lba_stop_after, team, c->solve_fail_mask, c->d_lba_ctl, pw};
+                   c->lba_stop_after, team, c->solve_fail_mask, c->d_lba_ctl, pw, lba_rows_max_team()};
         HIP_CHECK(c, lba_run_g2o(B, C, s, c->timer));
         HIP_CHECK(c, hipEventRecord(c->lba_done, s));
         if (stop_src) {  // host-buffer entry: mirror the caller's bool into the device-visible flag while it runs
