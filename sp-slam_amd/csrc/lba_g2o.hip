@@ -3351,7 +3351,11 @@ __global__ __launch_bounds__(kT) void k_lba_g2o(LbgBatch b, LbaConsts C) {
             bool more = true;
             while (more) {
                 LBG_MARK(1);
-                if (s.T <= b.rows_max_team) schur_rows_any();
+                // the row-group layout for teams of up to 4, and for any member with 16 or more blocks: it reads ~3x
+                // fewer LDS bytes per block step than schur()'s lane per entry, which wins when the LDS is busy;
+                // schur() splits a block's chain over 36 lanes, which wins for a few short chains (measured:
+                // profiles/r06/schur_layouts.txt)
+                if (s.T <= b.rows_max_team || s.bo1 - s.bo0 >= 16) schur_rows_any();
                 else schur();
                 team_sync(b);
                 LBG_MARK(5);

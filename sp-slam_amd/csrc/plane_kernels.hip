@@ -526,6 +526,277 @@ __global__ __launch_bounds__(64 * NWV) void plane_wave_kernel(PlaneGeom g, const
     }
 }
 
+// ---- the same wavefronts split by output (round 6): three workgroups per frame, each on its own CU, each running
+// plane_wave_kernel's schedule for one third of its work -- ROLE 0 the distance map (both passes; it needs only the
+// depth: no x / y, no divisions), ROLE 1 the integral images of the horizontal differences (channels 0..2, the own
+// row's x / y / z at c - 1, c + 1), ROLE 2 those of the vertical differences (channels 3..5, the rows above and below
+// by DPP).  A single wave per 64 rows is bound by its instruction issue (~170 instructions per cell step in
+// plane_wave_kernel); split three ways the longest role issues ~70, and the roles run side by side.  Same operands,
+// same operations per output: bit-identical to plane_wave_kernel.
+template <int NWV, int ROLE>
+__device__ __forceinline__ void plane_wave_role(const PlaneGeom& g, const float* __restrict__ depth, long long depth_fs,
+                                                int depth_stride, float* sink, long long sink_fs, float* dist,
+                                                long long dist_fs, double* integral, long long integral_fs,
+                                                WaveXchg* X, float* outer_rows) {
+    constexpr int K = 6;
+    constexpr bool kDist = ROLE == 0, kXY = ROLE != 0;
+    constexpr int k0 = ROLE == 2 ? 3 : 0;  // the role's first integral channel
+    const int f = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int W = g.W, H = g.H, r = 64 * w + lane, IW = W + 1;
+    const bool row_ok = r < H;
+    const int ro = min(r, H - 1);
+    const float* Z = depth + f * depth_fs;
+    auto zof = [&](int rr, int c) { return Z[(long long)(rr * g.ds) * depth_stride + c * g.ds]; };
+    auto xof = [&](int c, float z) { return ((float)(c * g.ds) - g.cx) * z / g.fx; };
+    auto yof = [&](int rr, float z) { return ((float)(rr * g.ds) - g.cy) * z / g.fy; };
+    float* UP = outer_rows + (size_t)w * 6 * W;  // row 64 w - 1: x | y | z (ROLE 0: z only)
+    float* DN = UP + 3 * W;                      // row 64 w + 64
+    {
+        const int ru = 64 * w - 1, rd = 64 * w + 64;
+        for (int c = lane; c < W; c += 64) {
+            if (ru >= 0) {
+                const float z = zof(ru, c);
+                if constexpr (kXY) { UP[c] = xof(c, z); UP[W + c] = yof(ru, z); }
+                UP[2 * W + c] = z;
+            }
+            if (rd < H) {
+                const float z = zof(rd, c);
+                if constexpr (kXY) { DN[c] = xof(c, z); DN[W + c] = yof(rd, z); }
+                DN[2 * W + c] = z;
+            }
+        }
+    }
+    if (threadIdx.x < NWV - 1) {
+        X[threadIdx.x].prod1 = X[threadIdx.x].cons1 = X[threadIdx.x].prod2 = X[threadIdx.x].cons2 = 0;
+    }
+    double* Iraw = integral + f * integral_fs;
+    if constexpr (!kDist) {
+        for (int c = threadIdx.x; c < IW; c += blockDim.x)
+            for (int k = 0; k < 3; k++) Iraw[(size_t)c * 6 + k0 + k] = 0.0;  // integral row 0
+        if (row_ok)
+            for (int k = 0; k < 3; k++) Iraw[(size_t)(r + 1) * IW * 6 + k0 + k] = 0.0;  // column 0
+    }
+    double* I = Iraw + (size_t)(ro + 1) * IW * 6 + 6 + k0;  // raster integral entry (r + 1, c + 1), the role's channels
+    double* Idummy = Iraw + (size_t)(H + 1) * IW * 6 + k0;   // sink row of the cells outside the cloud
+    float* D = dist + f * dist_fs + (size_t)ro * W;
+    float* Dsink = sink + f * sink_fs + threadIdx.x;
+    __syncthreads();
+    const bool has_up = w > 0, has_dn = w < NWV - 1;
+    // ---------------- pass 1 (plane_wave_kernel's schedule; each role keeps the state of its own outputs)
+    float wx[K + 4], wy[K + 4], wz[K + 4], nz[K];
+    auto colz = [&](int c) { return zof(ro, min(max(c, 0), W - 1)); };
+    auto fill = [&](int i, int c, float z) {
+        wz[i] = z;
+        if constexpr (kXY) {
+            const int cc = min(max(c, 0), W - 1);
+            wx[i] = xof(cc, z); wy[i] = yof(ro, z);
+        }
+    };
+    {
+        const int c0 = -2 * lane;
+#pragma unroll
+        for (int i = 0; i < K + 4; i++) fill(i, c0 - 2 + i, colz(c0 - 2 + i));
+#pragma unroll
+        for (int i = 0; i < K; i++) nz[i] = colz(c0 + K + 2 + i);
+    }
+    const float row0 = kDist && row_ok ? dist_init(zof, W, H, r, 0) : 0.f;
+    float nd0 = 0.f, nd1 = 0.f, nd2 = 0.f;  // ROLE 0, the row above: distance at c + 1, c, c - 1
+    double na[3], nb[3], nc[3];             // ROLES 1, 2, the row above: integral at c + 1, c, c - 1
+#pragma unroll
+    for (int k = 0; k < 3; k++) na[k] = nb[k] = nc[k] = 0.0;
+    float left = 0.f, vprev = 0.f;
+    double ileft[3], iprev[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) ileft[k] = iprev[k] = 0.0;
+    const int S1 = (W + 126 + K - 1) / K * K;
+    if (has_up) {  // step -1: the first row's register of the upper row's column 0
+        wave_wait(&X[w - 1].prod1, 1);
+        if constexpr (kDist) {
+            nd0 = lane == 0 ? X[w - 1].d1[0] : 0.f;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3; k++) na[k] = lane == 0 ? X[w - 1].i1[0][k] : 0.0;
+        }
+    }
+    for (int s0 = 0; s0 < S1; s0 += K) {
+        const int c0 = s0 - 2 * lane;
+        if (has_up) wave_wait(&X[w - 1].prod1, min(s0 + K + 1, W));
+        if (has_dn) wave_wait(&X[w].cons1, min(s0 - 126 + K - kXR, W));
+        float nzn[K];
+#pragma unroll
+        for (int i = 0; i < K; i++) nzn[i] = colz(c0 + 2 * K + 2 + i);
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int c = c0 + j;
+            const int sl = (c + 1) & (kXR - 1);
+            const bool ok = row_ok && c >= 0 && c < W, inner = r > 0 && c > 0;
+            const int cc = min(max(c, 0), W - 1);
+            if constexpr (kDist) {
+                float vin = from_above(vprev);
+                if (has_up) {
+                    const float rv = X[w - 1].d1[sl];
+                    vin = lane == 0 ? rv : vin;
+                }
+                nd2 = nd1; nd1 = nd0; nd0 = vin;
+                float uz = from_above(wz[j]), dz = from_below(wz[j + 4]);
+                if (lane == 0 && has_up) uz = UP[2 * W + cc];
+                if (lane == 63 && has_dn) dz = DN[2 * W + cc];
+                bool zero = false;
+                const float zc = wz[j + 2];
+                if (r < H - 1 && c < W - 1) zero = dc_bad(zc, wz[j + 3]) || dc_bad(zc, dz);
+                if (r < H - 1 && c >= 1) zero = zero || dc_bad(wz[j + 1], zc);
+                if (r >= 1 && c < W - 1) zero = zero || dc_bad(uz, zc);
+                const float center = zero ? 0.0f : (float)(W + H);
+                const float upLeft = nd2 + 1.4f, up = nd1 + 1.0f;
+                const float upRight = (c + 1 < W ? nd0 : row0) + 1.4f;
+                const float lft = left + 1.0f;
+                const float mv = fminf(fminf(upLeft, up), fminf(lft, upRight));
+                const float v = inner && mv < center ? mv : center;
+                if (ok) left = v;
+                vprev = v;
+                *(ok ? D + c : Dsink) = v;
+                if (has_dn && lane == 63 && ok) X[w].d1[c & (kXR - 1)] = v;
+            } else {
+                double iin[3];
+#pragma unroll
+                for (int k = 0; k < 3; k++) iin[k] = from_above_d(iprev[k]);
+                if (has_up) {
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const double ri = X[w - 1].i1[sl][k];
+                        iin[k] = lane == 0 ? ri : iin[k];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) { nc[k] = nb[k]; nb[k] = na[k]; na[k] = iin[k]; }
+                float e[3] = {0.f, 0.f, 0.f};
+                if constexpr (ROLE == 1) {
+                    if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
+                        e[0] = wx[j + 3] - wx[j + 1]; e[1] = wy[j + 3] - wy[j + 1]; e[2] = wz[j + 3] - wz[j + 1];
+                    }
+                } else {
+                    float ux = from_above(wx[j]), uy = from_above(wy[j]), uz = from_above(wz[j]);
+                    float dx = from_below(wx[j + 4]), dy = from_below(wy[j + 4]), dz = from_below(wz[j + 4]);
+                    if (lane == 0 && has_up) { ux = UP[cc]; uy = UP[W + cc]; uz = UP[2 * W + cc]; }
+                    if (lane == 63 && has_dn) { dx = DN[cc]; dy = DN[W + cc]; dz = DN[2 * W + cc]; }
+                    if (r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2) {
+                        e[0] = dx - ux; e[1] = dy - uy; e[2] = dz - uz;
+                    }
+                }
+                double iv[3];
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const double upI = r > 0 ? nb[k] : 0.0;
+                    const double upleftI = inner ? nc[k] : 0.0;
+                    iv[k] = upI + ileft[k] - upleftI;
+                    iv[k] += (double)e[k];
+                }
+                if (ok) {
+#pragma unroll
+                    for (int k = 0; k < 3; k++) ileft[k] = iv[k];
+                }
+#pragma unroll
+                for (int k = 0; k < 3; k++) iprev[k] = iv[k];
+                {
+                    double* out = ok ? I + c * 6 : Idummy;
+                    if constexpr (ROLE == 1) {
+                        *reinterpret_cast<double2*>(out) = make_double2(iv[0], iv[1]);
+                        out[2] = iv[2];
+                    } else {  // (channel 3 at byte 24 of the 48-byte entry: a double, then a 16-byte pair)
+                        out[0] = iv[0];
+                        *reinterpret_cast<double2*>(out + 1) = make_double2(iv[1], iv[2]);
+                    }
+                }
+                if (has_dn && lane == 63 && ok) {
+                    const int so = c & (kXR - 1);
+#pragma unroll
+                    for (int k = 0; k < 3; k++) X[w].i1[so][k] = iv[k];
+                }
+            }
+        }
+        if (has_dn) wave_publish(&X[w].prod1, max(0, min(s0 + K - 126, W)));
+        if (has_up) wave_publish(&X[w - 1].cons1, min(s0 + K + 1, W));
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            wz[i] = wz[K + i];
+            if constexpr (kXY) { wx[i] = wx[K + i]; wy[i] = wy[K + i]; }
+        }
+#pragma unroll
+        for (int i = 0; i < K; i++) fill(4 + i, c0 + K + 2 + i, nz[i]);
+#pragma unroll
+        for (int i = 0; i < K; i++) nz[i] = nzn[i];
+    }
+    if constexpr (!kDist) return;
+    // ---------------- pass 2 (ROLE 0): plane_wave_kernel's
+    const float lastcol = left;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int lb = min(63, H - 1 - 64 * w);
+    const int S2 = (W + 2 * lb + K - 1) / K * K;
+    auto dval = [&](int c) { return D[min(max(c, 0), W - 1)]; };
+    float dcur[K];
+#pragma unroll
+    for (int j = 0; j < K; j++) dcur[j] = dval(W - 1 - j + 2 * (lb - lane));
+    float right = 0.f, vp2 = 0.f;
+    float ld0 = 0.f, ld1 = 0.f, ld2 = 0.f;
+    const bool up_ring = w > 0;
+    if (has_dn) {
+        wave_wait(&X[w].prod2, 1);
+        ld0 = lane == 63 ? X[w].d2[(W - 1) & (kXR - 1)] : 0.f;
+    }
+    for (int s0 = 0; s0 < S2; s0 += K) {
+        const int cA = W - 1 - s0 + 2 * (lb - lane);
+        if (has_dn) wave_wait(&X[w].prod2, min(s0 + K + 1, W));
+        if (up_ring) wave_wait(&X[w - 1].cons2, min(s0 + K - 2 * lb - kXR, W));
+        float dnx[K];
+#pragma unroll
+        for (int j = 0; j < K; j++) dnx[j] = dval(cA - K - j);
+#pragma unroll
+        for (int j = 0; j < K; j++) {
+            const int c = cA - j;
+            float vin = from_below(vp2);
+            if (has_dn) {
+                const float rv = X[w].d2[(c - 1) & (kXR - 1)];
+                vin = lane == 63 ? rv : vin;
+            }
+            ld2 = ld1; ld1 = ld0; ld0 = vin;
+            const bool ok = row_ok && c >= 0 && c < W, inner = r < H - 1 && c < W - 1;
+            const float lowerLeft = (c > 0 ? ld0 : lastcol) + 1.4f;
+            const float lower = ld1 + 1.0f;
+            const float lowerRight = ld2 + 1.4f;
+            const float rgt = right + 1.0f;
+            const float mv = fminf(fminf(lowerLeft, lower), fminf(rgt, lowerRight));
+            const float center = dcur[j];
+            const float v = inner && mv < center ? mv : center;
+            if (ok) right = v;
+            vp2 = v;
+            *(ok ? D + c : Dsink) = v;
+            if (up_ring && lane == 0 && ok) X[w - 1].d2[c & (kXR - 1)] = v;
+        }
+        if (up_ring) wave_publish(&X[w - 1].prod2, max(0, min(s0 + K - 2 * lb, W)));
+        if (has_dn) wave_publish(&X[w].cons2, min(s0 + K + 1, W));
+#pragma unroll
+        for (int j = 0; j < K; j++) dcur[j] = dnx[j];
+    }
+}
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void plane_wave_roles_kernel(PlaneGeom g, const float* __restrict__ depth,
+                                                                    long long depth_fs, int depth_stride, float* sink,
+                                                                    long long sink_fs, float* dist, long long dist_fs,
+                                                                    double* integral, long long integral_fs) {
+    __shared__ WaveXchg X[NWV > 1 ? NWV - 1 : 1];
+    extern __shared__ float outer_rows[];
+    // (the sink: one slot per (role, thread), so the roles' stores of cells outside the cloud do not meet)
+    float* snk = sink + (size_t)blockIdx.y * 64 * NWV;
+    switch (blockIdx.y) {
+        case 0: plane_wave_role<NWV, 0>(g, depth, depth_fs, depth_stride, snk, sink_fs, dist, dist_fs, integral,
+                                        integral_fs, X, outer_rows); break;
+        case 1: plane_wave_role<NWV, 1>(g, depth, depth_fs, depth_stride, snk, sink_fs, dist, dist_fs, integral,
+                                        integral_fs, X, outer_rows); break;
+        default: plane_wave_role<NWV, 2>(g, depth, depth_fs, depth_stride, snk, sink_fs, dist, dist_fs, integral,
+                                         integral_fs, X, outer_rows); break;
+    }
+}
+
 __global__ __launch_bounds__(256) void plane_normal_kernel(PlaneGeom g, const float* __restrict__ cloud,
                                                            long long cloud_fs, const float* __restrict__ dist,
                                                            long long dist_fs, const double* __restrict__ integral,
@@ -594,7 +865,25 @@ hipError_t plane_launch(const PlaneGeom& g, const PlaneBuffers& b, int n, const 
         const char* e = getenv("SPSLAM_PLANE_WAVE_BARRIER");
         return e && e[0] == '1';
     }();
-    if (!barrier_wave) {
+    // three workgroups per frame, one per output group (plane_wave_roles_kernel), for small batches: B = 1 serial
+    // latency 3.72 -> 3.44 ms p50; one per frame (plane_wave_kernel) for large ones, where the roles' extra
+    // workgroups and operand fetches cost the C2 step 3 % (profiles/r06/ab_plane_wave_roles.txt).
+    // SPSLAM_PLANE_WAVE=1 / 3 forces one / three.
+    static const int wave_groups = [] {
+        const char* e = getenv("SPSLAM_PLANE_WAVE");
+        return e ? atoi(e) : 0;
+    }();
+    const bool one_wave_group = wave_groups == 1 || (wave_groups != 3 && n > 16);
+    if (!barrier_wave && !one_wave_group) {
+        const int nw = (g.H + 63) / 64;
+        const size_t lds = (size_t)nw * 6 * g.W * sizeof(float);
+        auto* k = nw <= 1 ? plane_wave_roles_kernel<1> : nw <= 2 ? plane_wave_roles_kernel<2>
+                : nw <= 3 ? plane_wave_roles_kernel<3> : nw <= 4 ? plane_wave_roles_kernel<4>
+                : nw <= 5 ? plane_wave_roles_kernel<5> : nw <= 6 ? plane_wave_roles_kernel<6>
+                : nw <= 7 ? plane_wave_roles_kernel<7> : plane_wave_roles_kernel<8>;
+        hipLaunchKernelGGL(k, dim3(n, 3), dim3(64 * nw), lds, s, g, depth, depth_fs, depth_stride, b.wave, b.wave_fs,
+                           b.dist, b.dist_fs, b.integral, b.integral_fs);
+    } else if (!barrier_wave) {
         const int nw = (g.H + 63) / 64;
         const size_t lds = (size_t)nw * 6 * g.W * sizeof(float);
         auto* k = nw <= 1 ? plane_wave_kernel<1> : nw <= 2 ? plane_wave_kernel<2> : nw <= 3 ? plane_wave_kernel<3>

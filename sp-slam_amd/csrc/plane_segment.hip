@@ -1068,13 +1068,24 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
             }
             wave_sync();
             if (lane < 9) {
+                // the chunk's terms in two batches of 8 loads issued together (one LDS round trip per batch, not
+                // per 4 values), added in order; entries past the padding are loaded but not added
                 const float4* row = (const float4*)(st + lane * 64);
-                for (int q = 0; q < (pad >> 2); q++) {
-                    const float4 v = row[q];
-                    acc += v.x;
-                    acc += v.y;
-                    acc += v.z;
-                    acc += v.w;
+                const int nq = pad >> 2;
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    float4 v[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) v[q] = row[8 * h + q];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        if (8 * h + q < nq) {
+                            acc += v[q].x;
+                            acc += v[q].y;
+                            acc += v[q].z;
+                            acc += v[q].w;
+                        }
+                    }
                 }
             }
             wave_sync();

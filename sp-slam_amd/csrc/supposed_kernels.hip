@@ -37,7 +37,8 @@
 namespace spslam {
 namespace supp {
 
-constexpr int kThreads = 256, kWaves = 4;
+constexpr int kThreads = 256, kWaves = 4;  // the batched launch (one workgroup per boundary)
+constexpr int kMaxWaves = 8;                // small batches: 512 threads (supp_launch)
 constexpr int kBatch = 64;       // RANSAC trials per speculative round
 constexpr int kLdsPts = 2048;    // boundaries up to this size are held in LDS
 constexpr int kMaxTrials = 1001; // RandomSampleConsensus: ++iterations_ > max_iterations_ (1000) -> stop
@@ -56,7 +57,7 @@ struct Shared {
     double k;
     float line[6];
     float acc[9];
-    int red[kWaves];
+    int red[kMaxWaves];
     int n_inl, flags;
 };
 
@@ -65,6 +66,7 @@ __device__ __forceinline__ int wave_sum(int v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
+template <int NT>
 __device__ int block_sum(int v, Shared& S) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     v = wave_sum(v);
@@ -73,7 +75,7 @@ __device__ int block_sum(int v, Shared& S) {
     __syncthreads();
     int s = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) s += S.red[w];
+    for (int w = 0; w < NT / 64; w++) s += S.red[w];
     return s;
 }
 
@@ -255,16 +257,17 @@ __device__ bool line_in_range(const float* pc, const Cam& K) {
 }
 
 // selectWithinDistance(coef): flag[i] for the n current points; returns the count.
+template <int NT>
 __device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, int n, float thr, Shared& S) {
     float lp[3] = {coef[0], coef[1], coef[2]}, ld[3] = {coef[3], coef[4], coef[5]};
     normalize4(ld);
     int c = 0;
-    for (int i = threadIdx.x; i < n; i += kThreads) {
+    for (int i = threadIdx.x; i < n; i += NT) {
         const bool in = line_sqd(lp, ld, Q[i]) <= thr;
         flag[i] = in;
         c += in;
     }
-    return block_sum(c, S);
+    return block_sum<NT>(c, S);
 }
 
 // 3 waves per SIMD: 168 VGPRs instead of 172, so the LDS (43.9 KB) and not the registers bounds residency at
@@ -272,7 +275,10 @@ __device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, 
 #ifndef SPSLAM_SUPP_MINB
 #define SPSLAM_SUPP_MINB 3
 #endif
-__global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
+// NT threads: 256 for batches (SPSLAM_SUPP_MINB workgroups per CU), 512 for a few frames (the inlier counts and the
+// point loops over twice the lanes; the sampler chain is wave 0's either way)
+template <int NT>
+__global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lines_kernel(PlaneGeom g, PlaneBuffers pb, SuppParams sp,
                                                               SuppBuffers sb, const float* __restrict__ depth,
                                                               long long depth_fs, int depth_stride,
                                                               const spslam_plane* __restrict__ planes,
@@ -312,7 +318,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
 #ifdef SPSLAM_SUPP_PROF
         long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = SUPP_CLK();
 #endif
-        for (int i = t; i < bsize; i += kThreads) {
+        for (int i = t; i < bsize; i += NT) {
             const int ci = con[coff + i];
             Q[i] = make_float4(X[ci], Y[ci], Z[ci], __int_as_float(ci));
         }
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
             if (t == 0) {
                 S.iterations = 0; S.best = -2147483647; S.k = 1.0; S.have = 0; S.done = n < 2;
             }
-            for (int i = t; i < n; i += kThreads) sh[i] = i;
+            for (int i = t; i < n; i += NT) sh[i] = i;
             __syncthreads();
             const double one_over_n = 1.0 / (double)n, log_prob = log(1.0 - 0.99);
             int r0 = 0, r1 = 1;   // shuffled_indices_[0], [1] (kept in registers by wave 0)
@@ -395,9 +401,10 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
                 SUPP_T(1);
                 const int nb = S.nb;
                 {
-                    // 16 trials per wave, 4 lanes per trial each counting every 4th point (the 16 lanes of a
-                    // point quarter read the same point: an LDS broadcast)
-                    const int c = wave * (kBatch / kWaves) + (lane >> 2), qq = lane & 3;
+                    // kBatch / NW trials per wave, NW lanes per trial each counting every NW-th point (the lanes of
+                    // a point phase read the same point: an LDS broadcast)
+                    constexpr int NW = NT / 64;
+                    const int c = wave * (kBatch / NW) + lane / NW, qq = lane % NW;
                     int cnt = 0;
                     if (c < nb) {
                         float L[6];
@@ -405,10 +412,10 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
                         float ld[3] = {L[3], L[4], L[5]};
                         normalize4(ld);
 #pragma unroll 1
-                        for (int i = qq; i < n; i += 4) cnt += line_sqd(L, ld, Q[i]) <= thr;
+                        for (int i = qq; i < n; i += NW) cnt += line_sqd(L, ld, Q[i]) <= thr;
                     }
-                    cnt += __shfl_xor(cnt, 1);
-                    cnt += __shfl_xor(cnt, 2);
+#pragma unroll
+                    for (int o = 1; o < NW; o <<= 1) cnt += __shfl_xor(cnt, o);
                     if (qq == 0 && c < nb) S.cnt[c] = cnt;
                 }
                 __syncthreads();
@@ -484,7 +491,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
             if (S.have) {
                 float c0[6];
                 line_from_samples(Q[S.best_s0], Q[S.best_s1], c0);
-                n_inl = select_within(c0, Q, flag, n, thr, S);
+                n_inl = select_within<NT>(c0, Q, flag, n, thr, S);
                 if (n_inl > 2) {
                     // The two sums below are sequential float chains in point order (one accumulator per lane).
                     // Points outside the line add +0.0f, which leaves a sum that starts at +0.0f unchanged
@@ -549,7 +556,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
                 __syncthreads();
                 float ref[6];
                 for (int k = 0; k < 6; k++) ref[k] = S.line[k];
-                n_inl = select_within(ref, Q, flag, n, thr, S);
+                n_inl = select_within<NT>(ref, Q, flag, n, thr, S);
             } else if (t == 0) {
                 for (int k = 0; k < 6; k++) S.line[k] = 0.f;
             }
@@ -579,7 +586,7 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
             // line points (ExtractIndices, order kept) + removal of them from the set, in place
             int nonborder = 0;
             int wbase = 0, kbase = 0;
-            for (int base = 0; base < n; base += kThreads) {
+            for (int base = 0; base < n; base += NT) {
                 const int i = base + t;
                 const bool valid = i < n;
                 const bool in = valid && flag[i];
@@ -593,14 +600,14 @@ __global__ __launch_bounds__(kThreads, SPSLAM_SUPP_MINB) void supp_lines_kernel(
                 int oi = wbase, ok = kbase;
                 for (int w = 0; w < wave; w++) { oi += S.s0[w]; ok += S.s1[w]; }
                 int ti = 0, tk = 0;
-                for (int w = 0; w < kWaves; w++) { ti += S.s0[w]; tk += S.s1[w]; }
+                for (int w = 0; w < NT / 64; w++) { ti += S.s0[w]; tk += S.s1[w]; }
                 __syncthreads();
                 if (in) lidx[used + oi + __popcll(mi & lt)] = __float_as_int(p.w);
                 if (valid && !in) Q[ok + __popcll(mk & lt)] = p;
                 wbase += ti;
                 kbase += tk;
             }
-            nonborder = block_sum(nonborder, S);
+            nonborder = block_sum<NT>(nonborder, S);
             if (t == 0) out.flags = fl | ((fl & 2) && nonborder <= n_inl / 4 ? 4 : 0);
             used += n_inl;
             n = kbase;
@@ -721,8 +728,12 @@ hipError_t supp_launch(const PlaneGeom& g, const PlaneBuffers& pb, const SuppPar
     auto B = [&](int k) { if (timer) timer->begin(k, s); };
     auto E = [&](int k) { if (timer) timer->end(k, s); };
     B(kKindSuppLines);
-    hipLaunchKernelGGL(supp::supp_lines_kernel, dim3(n, 16), dim3(supp::kThreads), 0, s, g, pb, sp, sb, depth,
-                       depth_fs, depth_stride, planes, plane_counts, contours);
+    if (n <= 16)  // a few frames: each boundary's workgroup on twice the lanes (B = 1 latency)
+        hipLaunchKernelGGL(supp::supp_lines_kernel<512>, dim3(n, 16), dim3(512), 0, s, g, pb, sp, sb, depth,
+                           depth_fs, depth_stride, planes, plane_counts, contours);
+    else
+        hipLaunchKernelGGL(supp::supp_lines_kernel<supp::kThreads>, dim3(n, 16), dim3(supp::kThreads), 0, s, g, pb,
+                           sp, sb, depth, depth_fs, depth_stride, planes, plane_counts, contours);
     E(kKindSuppLines);
     B(kKindSuppAssemble);
     hipLaunchKernelGGL(supp::supp_assemble_kernel, dim3(n), dim3(64), 0, s, sp, sb, g.contour_cap, planes,
