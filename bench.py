@@ -543,7 +543,7 @@ def _ensure_hw_queues(want=None):
     sys.exit(subprocess.call([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
 
 
-LBA_DEPTH, LBA_TEAM = 2, 1  # C3 defaults (profiles/r05/ab_c3_*.txt)
+LBA_DEPTH, LBA_TEAM = 3, 1  # C3 defaults: 4 calls in flight, one CU per map (profiles/r06/ab_c3_depth.txt; r05/ab_c3_*)
 # single_sequence: frames extracted ahead of tracking, and the host at most one step ahead of the device
 # (profiles/r05/b1_lookahead.txt, b1_inflight.txt)
 SINGLE_LOOKAHEAD, SINGLE_INFLIGHT = 2, 1
@@ -561,7 +561,10 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=0,
                     help="timed one-core CPU baseline frames (default 300; 100 above 640x480)")
     ap.add_argument("--no-tail-priority", action="store_true", help="tracking stream at normal priority")
-    ap.add_argument("--orb-priority", action="store_true", help="next batch's ORB stream at high priority")
+    ap.add_argument("--orb-priority", action="store_true", default=True,
+                    help="next batch's ORB stream at high priority (default: the ORB chain is the C2 step's critical path, "
+                         "profiles/r06/ab_stream_priority.txt)")
+    ap.add_argument("--no-orb-priority", dest="orb_priority", action="store_false")
     ap.add_argument("--planes-priority", action="store_true",
                     help="next batch's plane stream at high priority (round 3's default; with the round-5 plane "
                          "wavefront 1.5 %% slower, profiles/r05/ab_octree_planes_pose.txt)")
@@ -574,6 +577,8 @@ def main():
                          "does not block Tracking, LocalMapping.cc:48-124); default %d" % 2)
     ap.add_argument("--lba-team", type=int, default=None,
                     help="C3: workgroups per local map (0: as many as fill the chip); default 1 (the least CU time per map: with two calls in flight the LBA overlaps tracking instead of crowding it)")
+    ap.add_argument("--lookahead", type=int, default=1,
+                    help="batches extracted ahead of the tracking tail (the Python step; the native step runs 1)")
     ap.add_argument("--python-step", action="store_true",
                     help="drive the step's stages from Python over torch streams (pipeline.py) instead of the "
                          "library's whole-step entry spslam_step_run (the default without LocalMapping)")
@@ -626,7 +631,7 @@ def main():
                           native=not args.python_step and not cfg.get("lba_every"), **cfg,
                           lba_depth=LBA_DEPTH if args.lba_depth is None else args.lba_depth,
                           lba_team=LBA_TEAM if args.lba_team is None else args.lba_team,
-                          **shard_of(rank))
+                          lookahead=args.lookahead, **shard_of(rank))
     for _ in range(args.warmup):
         hp.step()
     torch.cuda.synchronize()

@@ -1233,22 +1233,61 @@ __device__ __noinline__ void structure() {
             }
         }
     }
-    // per free pose, its active edges in insertion order
-    int o = 0;
-    for (int hh = 0; hh < np; hh++) {
-        const int kfi = s.hpose[hh];
-        if (t == 0) g.pe_off[hh] = o;
+    // per free pose, its active edges in insertion order: a stable bucketing in one pass over the edges (round 5 ran
+    // a block scan over all edges per pose: np x E / 512 scans).  Counts per pose, their prefix = pe_off; then per
+    // chunk of kT edges each edge's rank among the chunk's earlier edges of its pose -- within its wave from the
+    // lanes that share the pose (one ballot per distinct pose of the wave), across waves from the per-wave counts
+    // taken in wave order -- after the edges of earlier chunks (run).
+    {
+        int* cnt = (int*)dyn;          // [kW][kMaxK] this chunk's per-wave counts
+        int* run = cnt + kW * kMaxK;   // [kMaxK] edges placed so far, then (first) the totals
+        const int wv = t >> 6;
+        auto pose_of = [&](int e) { return e < g.E && g.e_level[e] == 0 ? (int)s.hidx[g.e_kf[e]] : -1; };
+        for (int k = t; k < kMaxK; k += kT) run[k] = 0;
+        __syncthreads();
+        for (int e = t; e < g.E; e += kT) {
+            const int h = pose_of(e);
+            if (h >= 0) atomicAdd(&run[h], 1);
+        }
+        __syncthreads();
+        if (t == 0) {
+            int o = 0;
+            for (int hh = 0; hh < np; hh++) {
+                g.pe_off[hh] = o;
+                o += run[hh];
+            }
+            g.pe_off[np] = o;
+        }
+        __syncthreads();
+        for (int k = t; k < kMaxK; k += kT) run[k] = 0;
         for (int ch = 0; ch < g.E; ch += kT) {
-            const int e = ch + t;
-            const int f = e < g.E && g.e_level[e] == 0 && g.e_kf[e] == kfi;
-            int tot;
-            const int r = block_scan(f, &tot, s);
-            if (f) g.pe_idx[o + r] = e;
-            o += tot;
+            for (int k = t; k < kW * kMaxK; k += kT) cnt[k] = 0;
+            __syncthreads();
+            const int e = ch + t, h = pose_of(e);
+            int rank = 0;
+            uint64_t rem = __ballot(h >= 0);
+            while (rem) {
+                const int hq = __builtin_amdgcn_readlane(h, __builtin_ctzll(rem));
+                const uint64_t m = __ballot(h == hq);
+                if (h == hq) rank = __popcll(m & (lane == 0 ? 0ull : ~0ull >> (64 - lane)));
+                if (lane == 0) cnt[wv * kMaxK + hq] = __popcll(m);
+                rem &= ~m;
+            }
+            __syncthreads();
+            if (h >= 0) {
+                int base = g.pe_off[h] + run[h] + rank;
+                for (int w = 0; w < wv; w++) base += cnt[w * kMaxK + h];
+                g.pe_idx[base] = e;
+            }
+            __syncthreads();
+            for (int k = t; k < np; k += kT) {
+                int a = 0;
+                for (int w = 0; w < kW; w++) a += cnt[w * kMaxK + k];
+                run[k] += a;
+            }
+            __syncthreads();  // (the next chunk clears cnt)
         }
     }
-    if (t == 0) g.pe_off[np] = o;
-    __syncthreads();
     team_plan();
     // ---- LinearSolverEigen::computeSymbolicDecomposition (analyzePattern, Eigen's AMD)
     const int n = 6 * np;
@@ -1835,15 +1874,23 @@ __device__ __noinline__ void build_system() {
         }
         __syncthreads();
         if (head) {
-            for (int r = t; r < end_row; r++) {
-                const int bk = RI[r];
-                unsigned char f = 0;
-                if (bk >= 0) {
-                    f = pm_test(touched, bk - own_kb) ? 2 : 1;
-                    pm_set(touched, bk - own_kb);
+            // (the segment's block indices four at a time: one LDS round trip per four rows, not per row)
+            for (int r0 = t; r0 < end_row; r0 += 4) {
+                int bkv[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) bkv[u] = RI[min(r0 + u, end_row - 1)];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (r0 + u >= end_row) break;
+                    const int bk = bkv[u];
+                    unsigned char f = 0;
+                    if (bk >= 0) {
+                        f = pm_test(touched, bk - own_kb) ? 2 : 1;
+                        pm_set(touched, bk - own_kb);
+                    }
+                    RF[r0 + u] = f;
+                    again |= f == 2;
                 }
-                RF[r] = f;
-                again |= f == 2;
             }
             if (c0 + end_row != sg.z) s.carry = touched;  // (the chunk's last segment; read after two barriers)
             if (again) NSW[kW] = 1;

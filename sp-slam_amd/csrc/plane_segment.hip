@@ -617,8 +617,9 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const D desc, const 
 #pragma unroll
             for (int k = 1; k < K; k++) F = fn_then<D>(F, g[k]);
             F = fn_scan<D>(F);
-            uint32_t ex = (uint32_t)__shfl_up((int)F, 1);
-            if (lane == 0) ex = 0;
+            // the lane below's inclusive scan by DPP (wave_shr:1; lane 0 gets 0, the identity): a ds_bpermute here
+            // would make its wait also wait for the next row's LDS prefetch issued above
+            const uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)F, 0x138, 0xF, 0xF, false);
             uint32_t L = fn_apply<D>(ex, bw ? carry : 0u);
 #pragma unroll
             for (int k = 0; k < K; k++) {
@@ -628,7 +629,7 @@ __device__ __forceinline__ void refine_rows(uint8_t* state, const D desc, const 
                 if (p < W && s0[k] == 0 && fin[k] != 0) state[r * W + (bw ? W - 1 - p : p)] = (uint8_t)fin[k];
             }
         }
-        if (bw) carry = (uint32_t)__shfl((int)sel<K>(fin, lastK), lastLane);
+        if (bw) carry = (uint32_t)__builtin_amdgcn_readlane((int)sel<K>(fin, lastK), lastLane);
 #pragma unroll
         for (int k = 0; k < K; k++) prevS[k] = fin[k];
     }

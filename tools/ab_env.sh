@@ -1,9 +1,10 @@
-# Interleaved A/B of step variants selected by bench flags / environment on the pipelined C2 step:
+# Interleaved A/B of step variants selected by bench flags / environment on the pipelined C2 step (AB_CONFIG,
+# AB_STEPS: another config / step count):
 #   bash tools/ab_env.sh TAG ROUNDS "VARIANT_A" "VARIANT_B" ["VARIANT_C" ...]
 # each VARIANT is "ENV=VAL ... -- bench flags" (either part may be empty); gpurun_out/ab_TAG_<i>_<r>.json
 cd ${GRAFT_REPO_ROOT:-.}
 TAG=$1; R=$2; shift 2
-B="python bench.py --config c2 --steps 40 --warmup 5 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0"
+B="python bench.py --config ${AB_CONFIG:-c2} --steps ${AB_STEPS:-40} --warmup 5 --no-cpu-baseline --ate-frames 0 --closed-loop-steps 0 --single-sequence-frames 0"
 for r in $(seq 1 $R); do
   i=0
   for v in "$@"; do

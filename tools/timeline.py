@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """One pipelined step's kernel timeline per queue from a rocprofv3 run of bench.py (rocpd database), plus each
 queue's chain length per step (first start to last end between two grab launches):
-    python tools/timeline.py gpurun_out/<tag>_prof_c2/run_results.db [step_from_end=2]"""
+    python tools/timeline.py gpurun_out/<tag>_prof_c2/run_results.db [step_from_end=2] [min_grab_us=0]
+(min_grab_us: count only grab launches at least that long -- e.g. 50 to skip bench.py's trailing B = 1 steps)"""
 import collections
 import sqlite3
 import sys
@@ -15,11 +16,11 @@ def short(n):
     return parts[-1] if parts else b
 
 
-def main(db, back=2):
+def main(db, back=2, min_grab_us=0.0):
     c = sqlite3.connect(db)
     rows = [(short(n), q, s, e) for n, q, s, e in c.execute("select name, queue_id, start, end from kernels order by start")
             if "copyBuffer" not in n and "at::" not in n]
-    starts = [r[2] for r in rows if r[0] == "grab"]
+    starts = [r[2] for r in rows if r[0] == "grab" and (r[3] - r[2]) / 1e3 >= min_grab_us]
     s0, s1 = starts[-back - 1], starts[-back]
     span = collections.defaultdict(lambda: [None, None])
     print(f"step {(s1 - s0) / 1e3:.0f} us (grab to grab)")
@@ -34,4 +35,4 @@ def main(db, back=2):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2, float(sys.argv[3]) if len(sys.argv) > 3 else 0.0)
