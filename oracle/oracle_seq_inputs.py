@@ -59,11 +59,12 @@ def refkf_of(sp, slot, vocab_text):
 
 
 def local_map(sp, slot):
-    """A fresh local_mapping.SeqMap of the slot's sequence as it stood before frame 1 (keyframe 0 inserted)."""
-    import local_mapping as LM
+    """A fresh oracle_local_map.KeyframeMap of the slot's sequence as it stood before frame 1 (keyframe 0
+    inserted) -- the checker's own LocalMapping bookkeeping (the GPU loop runs sp-slam_amd/local_mapping.py)."""
+    import oracle_local_map as LM
     u = slot % sp.U
     tab = sp.ex.tables()
-    m = LM.SeqMap([sp.kf_points[u, j] for j in range(len(sp.kf_t))], sp.kp_cap,
+    m = LM.KeyframeMap([sp.kf_points[u, j] for j in range(len(sp.kf_t))], sp.kp_cap,
                   (sp.fx, sp.fy, sp.cx, sp.cy, sp.bf), tab["scale"], tab["inv_sigma2"], sp.assoc_map)
     LM.insert_initial_keyframe(m, sp._true_pose(u, 0).astype(np.float32), sp.kf_kps[u, 0], sp.seq_frames[u][0][1],
                                sp.depth_factor, sp.bf)

@@ -21,6 +21,7 @@
 #include <cstdlib>
 
 #include "../../include/spslam_gpu.h"
+#include "wave_priority.h"
 #include "orb_launch.h"
 
 namespace spslam {
@@ -406,6 +407,7 @@ __device__ __forceinline__ void level_tile(const OrbGeom& g, int l, int minTh, i
 // halos a tile shares with its neighbours (and the resize's source rows) are fetched into one L2 once instead
 // of by up to 8 L2s (PMC: 3-4x the algorithmic reads without the remap, profiles/r04/pmc_levels_*).
 __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, int minTh) {
+    orb_wave_priority();
     __shared__ LevelLds sm;
     const int nt = gridDim.x, total = nt * gridDim.y;
     const int id = xcd_remap(blockIdx.y * nt + blockIdx.x, total);
@@ -417,6 +419,7 @@ __global__ __launch_bounds__(kLevelThreads) void level_kernel(OrbGeom g, int l, 
 // the workgroup (release / acquire at workgroup scope: the same CU's L1) before the next level reads them.
 template <int kLevelGroups>
 __global__ __launch_bounds__(kLevelThreads * kLevelGroups) void level_small_kernel(OrbGeom g, int l0, int minTh) {
+    orb_wave_priority();
     __shared__ LevelLds sm[kLevelGroups];
     const int grp = threadIdx.x / kLevelThreads, t = threadIdx.x % kLevelThreads, f = blockIdx.x;
     for (int l = l0; l < g.nlevels; l++) {
@@ -455,6 +458,7 @@ constexpr int kScPitchMax = ((kCellScoreMax + 3) & ~3) + 4, kScRowsMax = kCellSc
 __global__ __launch_bounds__(256) void fast_cells_kernel(OrbGeom g, uint32_t* __restrict__ cand,
                                                          uint16_t* __restrict__ cand_cnt, int iniTh, int minTh,
                                                          int cid0, int cid1) {  // this launch's cells [cid0, cid1)
+    orb_wave_priority();
     __shared__ __attribute__((aligned(16))) uint8_t scs[4][kScRowsMax * kScPitchMax];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     // XCD-aware order (as level_kernel): a frame's cells, whose windows overlap by 6 pixels, on one L2
@@ -920,6 +924,7 @@ __global__ __launch_bounds__(256) void octree_kernel(OrbGeom g, const uint32_t* 
                                                      const uint16_t* __restrict__ cand_cnt, uint32_t* __restrict__ keys_all,
                                                      uint16_t* __restrict__ keynode_all, LevelKp* __restrict__ lvl_kp,
                                                      int* __restrict__ lvl_cnt, int l0) {  // levels l0 + blockIdx.x
+    orb_wave_priority();
     __shared__ OctShared<NC> S;
     const int l = l0 + blockIdx.x, f = blockIdx.y, t = threadIdx.x;
     const LevelGeom& Lg = g.lv[l];
@@ -1035,6 +1040,7 @@ __global__ __launch_bounds__(256) void desc_kernel(OrbGeom g, const LevelKp* __r
                                                    const int* __restrict__ lvl_cnt, spslam_keypoint* __restrict__ out_kp,
                                                    uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt,
                                                    int cap_per_frame) {
+    orb_wave_priority();
     // 1-D launch of gx * frames workgroups in XCD-aware order: one frame's keypoints (and its level
     // images / blurred levels, ~1.9 MB at 640x480) stay on one XCD's L2
     const int gx = (g.lvl_kp_per_frame + 3) / 4;

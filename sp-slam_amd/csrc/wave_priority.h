@@ -21,4 +21,10 @@ __device__ __forceinline__ void tail_wave_priority() {
     __builtin_amdgcn_s_setprio(3);
 #endif
 }
+// Measurement knob: the ORB chain's waves (the C2 step's critical path) at issue priority SPSLAM_ORB_PRIO.
+__device__ __forceinline__ void orb_wave_priority() {
+#ifdef SPSLAM_ORB_PRIO
+    __builtin_amdgcn_s_setprio(SPSLAM_ORB_PRIO);
+#endif
+}
 }  // namespace spslam

@@ -23,8 +23,11 @@ tail produces, and after every keyframe frame (synth.KEYFRAME_STEP) it
     keyframe's own frame), the last frame's pose the motion model starts from.
 
 Deviations (both loops share them): keyframes on a fixed schedule; no MapPointCulling / CreateNewMapPoints /
-SearchInNeighbors / KeyFrameCulling; the keyframe's final PoseOptimization outliers are dropped before it becomes
+SearchInNeighbors / KeyFrameCulling; no bad flags (MapPoint::EraseObservation's nObs <= 2 discard, MapPoint.cc:129-136); the keyframe's final PoseOptimization outliers are dropped before it becomes
 a keyframe (the reference passes them on for the local BA to judge); keyframe 0 is fixed (mnId == 0).
+
+The CPU oracle's loop does not run this module: oracle/oracle_local_map.py states the same bookkeeping
+independently (scalar, from the reference), and tests/test_local_mapping_host.py holds the two bit-exact.
 """
 from __future__ import annotations
 
@@ -100,7 +103,8 @@ class SeqMap:
 
     def covisible(self, j):
         """KeyFrame::UpdateConnections + GetVectorCovisibleKeyFrames: keyframes sharing >= 15 map points with j
-        (else the best one), by weight descending (ties: the higher id first -- pointer order in the reference)."""
+        (else the best one: the first maximum in keyframe order, KeyFrame.cc:353), by weight descending (ties: the
+        higher id first -- sort + push_front in pointer order, KeyFrame.cc:371-378)."""
         cnt = {}
         for kp, pid in self.kfs[j]["mp"].items():
             for i in self.obs.get(pid, {}):
@@ -110,7 +114,7 @@ class SeqMap:
             return []
         pairs = [(w, i) for i, w in cnt.items() if w >= self.COVIS_TH]
         if not pairs:
-            i, w = max(cnt.items(), key=lambda kv: (kv[1], kv[0]))
+            i, w = max(cnt.items(), key=lambda kv: (kv[1], -kv[0]))
             pairs = [(w, i)]
         return [i for w, i in sorted(pairs, reverse=True)]
 

@@ -70,8 +70,8 @@ def inputs(cfg, u=0, n_frames=300, seq_id=0, n_boxes=5, W=640, H=480, nfeatures=
     pcfg = G.PlaneConfig(1.0, 100.0, 0.5, 0.5, c["chi"], c["vp_chi"])
     lm = None
     if c.get("local_mapping"):
-        import local_mapping as LM
-        lm = LM.SeqMap(kfp, cap, (fx, fy, cx, cy, bf), sc, inv_s2, m)
+        import oracle_local_map as LM
+        lm = LM.KeyframeMap(kfp, cap, (fx, fy, cx, cy, bf), sc, inv_s2, m)
         LM.insert_initial_keyframe(lm, T0, kfk[0], frames[0][1], K["depth_factor"], bf)
     return dict(lm=lm, frames=frames[1:], T0=T0, P0=P0, local_of=local_of, cam=(fx, fy, cx, cy, bf), geo=geo,
                 inv_s2=np.asarray(inv_s2, np.float32), map=m, boundary=bxyz, min_size=c["min_size"], pcfg=pcfg, ref=ref,
