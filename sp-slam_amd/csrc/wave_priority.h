@@ -11,8 +11,11 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+// Off by default since round 6: with the ORB stream at high dispatch priority (the C2 step's critical path,
+// bench.py --orb-priority) the raised tail waves cost the ORB chain more than they gain: C2 step 42.7K -> 43.3K
+// frames/s without them, B = 1 unchanged (profiles/r06/ab_wave_priority.txt).  -DSPSLAM_TAIL_PRIO=1 restores it.
 #ifndef SPSLAM_TAIL_PRIO
-#define SPSLAM_TAIL_PRIO 1
+#define SPSLAM_TAIL_PRIO 0
 #endif
 
 namespace spslam {
