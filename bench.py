@@ -422,6 +422,24 @@ def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
     return out
 
 
+def single_sequence_line(config, device, n_frames):
+    """single_sequence() in a process of its own on the same GPU, with HIP's default of 4 hardware queues: the
+    reference's call pattern is one tracking process per sequence, and a B = 1 step's few streams run best on 4
+    queues (pipelined 710 frames/s against 594 with the 8 this process opened for the C2 step, and ~430-475 run
+    after the C2 step inside this process: profiles/r06/ab_single_sequence_queues.txt)."""
+    import subprocess
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(SINGLE_HW_QUEUES), SPSLAM_BENCH_CHILD="1",
+               HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(device)))
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", config, "--single-sequence-child",
+                        "--single-sequence-frames", str(n_frames)], env=env, capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"single_sequence child failed ({r.returncode}): {r.stderr[-2000:]}")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["process"] = f"own process, GPU_MAX_HW_QUEUES={SINGLE_HW_QUEUES}"
+    return out
+
+
 def ate_sequences(cfg, device, n_frames=300, n_seq=2):
     """ATE of tracked sequences (sp-slam_amd/sequence.py): n_seq sequences of n_frames tracked frames each on
     the GPU, every frame's prior and last-frame points from its predecessor's result, against the CPU oracle
@@ -546,7 +564,7 @@ def _ensure_hw_queues(want=None):
 LBA_DEPTH, LBA_TEAM = 3, 1  # C3 defaults: 4 calls in flight, one CU per map (profiles/r06/ab_c3_depth.txt; r05/ab_c3_*)
 # single_sequence: frames extracted ahead of tracking, and the host at most one step ahead of the device
 # (profiles/r05/b1_lookahead.txt, b1_inflight.txt)
-SINGLE_LOOKAHEAD, SINGLE_INFLIGHT = 2, 1
+SINGLE_LOOKAHEAD, SINGLE_INFLIGHT, SINGLE_HW_QUEUES = 2, 1, 4
 
 
 def main():
@@ -588,6 +606,7 @@ def main():
                     help="frames per tracked sequence of the ATE check (0 = skip)")
     ap.add_argument("--single-sequence-frames", type=int, default=120,
                     help="frames of the single-sequence (B = 1) line (0 = skip)")
+    ap.add_argument("--single-sequence-child", action="store_true", help=argparse.SUPPRESS)  # (single_sequence_line)
     ap.add_argument("--closed-loop-steps", type=int, default=20,
                     help="timed steps of the closed-loop line (tracked sequences at --batch slots; 0 = skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -606,6 +625,10 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dist_check:
         return dist_check(args, rank, world)
+    if args.single_sequence_child:
+        import pipeline
+        print(json.dumps(single_sequence(pipeline.CONFIGS[args.config], 0, n_frames=args.single_sequence_frames)))
+        return
     # C3: every in-flight LocalBundleAdjustment call has its own context stream; with 8 hardware queues they alias
     # the tracking streams' queues and serialise (profiles/r05/ab_c3_hwq*.txt), so C3 runs with 16
     _ensure_hw_queues(16 if args.config in ("c3", "c3s") else None)
@@ -774,7 +797,7 @@ def main():
     if rank == 0 and args.closed_loop_steps > 0:
         result["closed_loop"] = closed_loop(cfg, local, args.batch, args.closed_loop_steps, args.warmup)
     if rank == 0 and args.single_sequence_frames > 0:
-        result["single_sequence"] = single_sequence(cfg, local, n_frames=args.single_sequence_frames)
+        result["single_sequence"] = single_sequence_line(args.config, local, args.single_sequence_frames)
         if result["cpu_baseline"]:  # one core, the same per-frame work (the oracle step, open loop)
             result["single_sequence"]["cpu_1core_frames_per_s"] = result["cpu_baseline"]["value"]
     if rank == 0 and args.ate_frames > 0:
