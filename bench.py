@@ -428,8 +428,12 @@ def single_sequence_line(config, device, n_frames):
     queues (pipelined 710 frames/s against 594 with the 8 this process opened for the C2 step, and ~430-475 run
     after the C2 step inside this process: profiles/r06/ab_single_sequence_queues.txt)."""
     import subprocess
-    env = dict(os.environ, GPU_MAX_HW_QUEUES=str(SINGLE_HW_QUEUES), SPSLAM_BENCH_CHILD="1",
-               HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(device)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env.update(GPU_MAX_HW_QUEUES=str(SINGLE_HW_QUEUES), SPSLAM_BENCH_CHILD="1")
+    if "HIP_VISIBLE_DEVICES" not in env and "CUDA_VISIBLE_DEVICES" not in env:
+        env["HIP_VISIBLE_DEVICES"] = str(device)
     r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", config, "--single-sequence-child",
                         "--single-sequence-frames", str(n_frames)], env=env, capture_output=True, text=True,
                        timeout=600)
@@ -616,6 +620,10 @@ def main():
     ap.add_argument("--dist-check", action="store_true",
                     help="CPU rehearsal of the multi-rank launch (gloo, no GPU): spawn, rendezvous, aggregation")
     args = ap.parse_args()
+    if args.single_sequence_child:  # (single_sequence_line: one process, one GPU, no ranks)
+        import pipeline
+        print(json.dumps(single_sequence(pipeline.CONFIGS[args.config], 0, n_frames=args.single_sequence_frames)))
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))  # one process per GPU (no launcher was used)
     rank = int(os.environ.get("RANK", "0"))
@@ -625,10 +633,6 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dist_check:
         return dist_check(args, rank, world)
-    if args.single_sequence_child:
-        import pipeline
-        print(json.dumps(single_sequence(pipeline.CONFIGS[args.config], 0, n_frames=args.single_sequence_frames)))
-        return
     # C3: every in-flight LocalBundleAdjustment call has its own context stream; with 8 hardware queues they alias
     # the tracking streams' queues and serialise (profiles/r05/ab_c3_hwq*.txt), so C3 runs with 16
     _ensure_hw_queues(16 if args.config in ("c3", "c3s") else None)
