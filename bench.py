@@ -377,7 +377,7 @@ def closed_loop(cfg, device, B, steps, warmup, n_seq=16):
         sp.close()
 
 
-def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
+def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None, modes=(True, False)):
     """The reference's own call pattern (Examples/RGB-D/SPSLAM.cc:90-136 -> System::TrackRGBD per frame): ONE
     tracked sequence, one frame at a time (B = 1, sp-slam_amd/sequence.py; every frame's prior and last-frame
     points from its predecessor).  frames_per_s: frames k+1 .. k+L's grab / ORB / planes overlapped with frame k's
@@ -392,7 +392,7 @@ def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
     look = SINGLE_LOOKAHEAD if lookahead is None else lookahead
     out = {"kind": "one sequence, B = 1 (sequence.SequencePath), frames device-resident", "frames": n_frames,
            "lookahead": look, "max_inflight": SINGLE_INFLIGHT}
-    for pipelined in (True, False):
+    for pipelined in modes:
         sp = sequence.SequencePath(1, n_frames + warmup + 2, n_sequences=1, device=device, pipelined=pipelined,
                                    lookahead=look if pipelined else 1, max_inflight=SINGLE_INFLIGHT,
                                    render_workers=min(16, os.cpu_count() or 1), **cfg)
@@ -423,10 +423,11 @@ def single_sequence(cfg, device, n_frames=120, warmup=5, lookahead=None):
 
 
 def single_sequence_line(config, device, n_frames):
-    """single_sequence() in a process of its own on the same GPU, with HIP's default of 4 hardware queues: the
-    reference's call pattern is one tracking process per sequence, and a B = 1 step's few streams run best on 4
-    queues (pipelined 710 frames/s against 594 with the 8 this process opened for the C2 step, and ~430-475 run
-    after the C2 step inside this process: profiles/r06/ab_single_sequence_queues.txt)."""
+    """single_sequence() in processes of their own on the same GPU (one for the pipelined rate, one for the serial
+    latency), with HIP's default of 4 hardware queues: the reference's call pattern is one tracking process per
+    sequence, and a B = 1 step's few streams run best on 4 queues (pipelined 710 frames/s against 594 with the 8
+    this process opened for the C2 step, and ~430-475 run after the C2 step inside this process; serial p50 3.40
+    ms alone against 3.58 after a pipelined run in the same process: profiles/r06/ab_single_sequence_queues.txt)."""
     import subprocess
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
@@ -434,13 +435,15 @@ def single_sequence_line(config, device, n_frames):
     env.update(GPU_MAX_HW_QUEUES=str(SINGLE_HW_QUEUES), SPSLAM_BENCH_CHILD="1")
     if "HIP_VISIBLE_DEVICES" not in env and "CUDA_VISIBLE_DEVICES" not in env:
         env["HIP_VISIBLE_DEVICES"] = str(device)
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", config, "--single-sequence-child",
-                        "--single-sequence-frames", str(n_frames)], env=env, capture_output=True, text=True,
-                       timeout=600)
-    if r.returncode != 0:
-        raise RuntimeError(f"single_sequence child failed ({r.returncode}): {r.stderr[-2000:]}")
-    out = json.loads(r.stdout.strip().splitlines()[-1])
-    out["process"] = f"own process, GPU_MAX_HW_QUEUES={SINGLE_HW_QUEUES}"
+    out = {}
+    for mode in ("pipelined", "serial"):
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", config, "--single-sequence-child",
+                            mode, "--single-sequence-frames", str(n_frames)], env=env, capture_output=True, text=True,
+                           timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"single_sequence {mode} child failed ({r.returncode}): {r.stderr[-2000:]}")
+        out.update(json.loads(r.stdout.strip().splitlines()[-1]))
+    out["process"] = f"one process per mode, GPU_MAX_HW_QUEUES={SINGLE_HW_QUEUES}"
     return out
 
 
@@ -610,7 +613,7 @@ def main():
                     help="frames per tracked sequence of the ATE check (0 = skip)")
     ap.add_argument("--single-sequence-frames", type=int, default=120,
                     help="frames of the single-sequence (B = 1) line (0 = skip)")
-    ap.add_argument("--single-sequence-child", action="store_true", help=argparse.SUPPRESS)  # (single_sequence_line)
+    ap.add_argument("--single-sequence-child", choices=("pipelined", "serial"), help=argparse.SUPPRESS)  # (single_sequence_line)
     ap.add_argument("--closed-loop-steps", type=int, default=20,
                     help="timed steps of the closed-loop line (tracked sequences at --batch slots; 0 = skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -622,7 +625,8 @@ def main():
     args = ap.parse_args()
     if args.single_sequence_child:  # (single_sequence_line: one process, one GPU, no ranks)
         import pipeline
-        print(json.dumps(single_sequence(pipeline.CONFIGS[args.config], 0, n_frames=args.single_sequence_frames)))
+        print(json.dumps(single_sequence(pipeline.CONFIGS[args.config], 0, n_frames=args.single_sequence_frames,
+                                         modes=(args.single_sequence_child == "pipelined",))))
         return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))  # one process per GPU (no launcher was used)
