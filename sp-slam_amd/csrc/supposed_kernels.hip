@@ -59,6 +59,7 @@ struct Shared {
     float acc[9];
     int red[kMaxWaves];
     int n_inl, flags;
+    int s0x[kBatch], s1x[kBatch], nbb[2], failb[2];  // kOverlap: the second sample buffer, both buffers' counts
 };
 
 __device__ __forceinline__ int wave_sum(int v) {
@@ -272,6 +273,12 @@ __device__ int select_within(const float* coef, const float4* Q, uint8_t* flag, 
 
 // 3 waves per SIMD: 168 VGPRs instead of 172, so the LDS (43.9 KB) and not the registers bounds residency at
 // 3 workgroups per CU instead of 2 (1.35 -> 0.95 ms per 256 frames alone; profiles/r02/ab_contour_single_walk)
+#ifndef SPSLAM_SUPP_OVERLAP
+#define SPSLAM_SUPP_OVERLAP 1
+#endif
+#ifndef SPSLAM_SUPP_OVERLAP_ALL  // measurement knob: the overlap in the 256-thread (batched) instance too
+#define SPSLAM_SUPP_OVERLAP_ALL 0
+#endif
 #ifndef SPSLAM_SUPP_MINB
 #define SPSLAM_SUPP_MINB 3
 #endif
@@ -291,6 +298,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
     if (g.W > 0) return;
 #endif
     __shared__ Shared S;
+    // 512-thread instance (a few frames): the next RANSAC round is sampled while the other waves count this one's
+    // inliers (SPSLAM_SUPP_OVERLAP=0 turns it off)
+    constexpr bool kOverlap = SPSLAM_SUPP_OVERLAP && (NT == 512 || SPSLAM_SUPP_OVERLAP_ALL);
     const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int np = min(plane_counts[f], kMaxPlanesPerFrame);
     const spslam_plane* P = planes + (size_t)f * kMaxPlanesPerFrame;
@@ -330,6 +340,9 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
             if (t == 0) {
                 S.iterations = 0; S.best = -2147483647; S.k = 1.0; S.have = 0; S.done = n < 2;
             }
+            if constexpr (kOverlap) {
+                if (t < kBatch) S.cnt[t] = 0;
+            }
             for (int i = t; i < n; i += NT) sh[i] = i;
             __syncthreads();
             const double one_over_n = 1.0 / (double)n, log_prob = log(1.0 - 0.99);
@@ -340,9 +353,157 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
             int bp0 = 0, bp1 = 0, qh = 0, qn = 0;
             uint64_t gmask = 0;
             uint32_t rnext = wave == 0 ? sb.rnd[lane] : 0u;  // next block's draws, loaded one block ahead
-            while (!S.done) {
-                if (wave == 0) {
-                    const int it0 = S.iterations;
+            if constexpr (!kOverlap) {
+                while (!S.done) {
+                    if (wave == 0) {
+                        const int it0 = S.iterations;
+                        int nb = 0, chk = 0;  // chk: failed samples of the trial being drawn
+                        bool fail = false;
+                        while (nb < kBatch && it0 + nb < kMaxTrials) {
+                            if (qh == qn) {
+                                // apply the next 32 draw pairs to the shuffle state: their swaps do not depend on
+                                // whether a pair becomes a trial's sample, so isSampleGood is checked afterwards,
+                                // for all 32 pairs at once (the chain keeps one LDS round trip per pair)
+                                const uint32_t r = rnext;
+                                const uint32_t jv = (lane & 1) ? 1u + r % (uint32_t)(n - 1) : r % (uint32_t)n;
+                                pos += 64;
+                                rnext = sb.rnd[pos + lane];  // (the table holds one block beyond the worst case)
+                                // Branch-free: entries 0 and 1 live in r0 / r1 (their LDS slots are never read), so
+                                // a swap that does not touch LDS reads and writes slot 0 (first swap) or 1 (second)
+                                // as a sink; per pair two reads, then two writes, and selects.
+    #pragma unroll 4
+                                for (int c = 0; c < 32; c++) {
+                                    const int j0 = __builtin_amdgcn_readlane((int)jv, 2 * c), j1 = __builtin_amdgcn_readlane((int)jv, 2 * c + 1);
+                                    const int i0 = j0 > 1 ? j0 : 0, i1 = j1 > 1 ? j1 : 1;
+                                    const int x0 = sh[i0], x1 = sh[i1];
+                                    const int a0 = r0, b0 = r1;
+                                    const int r1m = j0 == 1 ? a0 : b0;  // entry 1 after the first swap
+                                    sh[i0] = a0;
+                                    sh[i1] = r1m;
+                                    r0 = j0 > 1 ? x0 : (j0 == 1 ? b0 : a0);
+                                    r1 = j1 > 1 ? (j1 == j0 ? a0 : x1) : r1m;  // j1 == j0: the value the first swap stored
+                                    bp0 = lane == c ? r0 : bp0;
+                                    bp1 = lane == c ? r1 : bp1;
+                                }
+                                bool good = false;
+                                if (lane < 32) {
+                                    const float4 a = Q[bp0], b = Q[bp1];
+                                    good = a.x != b.x && a.y != b.y && a.z != b.z;
+                                }
+                                gmask = __ballot(good);
+                                qh = 0;
+                                qn = 32;
+                            }
+                            const uint64_t m = gmask & (~0ull << qh) & 0xFFFFFFFFull;
+                            if (m == 0) {  // the rest of the block failed isSampleGood
+                                chk += qn - qh;
+                                qh = qn;
+                                if (chk >= 1000) { fail = true; break; }
+                                continue;
+                            }
+                            const int gi = __ffsll((unsigned long long)m) - 1;
+                            if (chk + (gi - qh) >= 1000) { fail = true; break; }  // 1000 failed samples first
+                            const int s0v = __builtin_amdgcn_readlane(bp0, gi), s1v = __builtin_amdgcn_readlane(bp1, gi);
+                            if (lane == 0) { S.s0[nb] = s0v; S.s1[nb] = s1v; }
+                            nb++;
+                            chk = 0;
+                            qh = gi + 1;
+                        }
+                        if (lane == 0) { S.nb = nb; S.fail = fail; }
+                    }
+                    __syncthreads();
+                    SUPP_T(1);
+                    const int nb = S.nb;
+                    {
+                        // kBatch / NW trials per wave, NW lanes per trial each counting every NW-th point (the lanes of
+                        // a point phase read the same point: an LDS broadcast)
+                        constexpr int NW = NT / 64;
+                        const int c = wave * (kBatch / NW) + lane / NW, qq = lane % NW;
+                        int cnt = 0;
+                        if (c < nb) {
+                            float L[6];
+                            line_from_samples(Q[S.s0[c]], Q[S.s1[c]], L);
+                            float ld[3] = {L[3], L[4], L[5]};
+                            normalize4(ld);
+    #pragma unroll 1
+                            for (int i = qq; i < n; i += NW) cnt += line_sqd(L, ld, Q[i]) <= thr;
+                        }
+    #pragma unroll
+                        for (int o = 1; o < NW; o <<= 1) cnt += __shfl_xor(cnt, o);
+                        if (qq == 0 && c < nb) S.cnt[c] = cnt;
+                    }
+                    __syncthreads();
+                    SUPP_T(2);
+                    if (wave == 0) {
+                        // computeModel's bookkeeping over the round's trials, in parallel (lane c = trial c): a
+                        // trial improves the model when its count beats the best so far (exclusive prefix max);
+                        // k changes only there, so the k each trial's `iterations < k` test sees is the k of the
+                        // last improvement before it; the loop stops at the first failed test, or after trial
+                        // 1000 - iterations (max_iterations_)
+                        const int it0 = S.iterations, best0 = S.best;
+                        const double k0 = S.k;
+                        const bool act = lane < nb;
+                        const int cn = act ? S.cnt[lane] : INT_MIN;
+                        int pm = cn, lr;
+    #pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const int y = __shfl_up(pm, off);
+                            if (lane >= off) pm = max(pm, y);
+                        }
+                        int ex = __shfl_up(pm, 1);
+                        if (lane == 0) ex = INT_MIN;
+                        const bool rec = act && cn > max(ex, best0);
+                        double kc = 0.0;
+                        if (rec) {
+                            const double w = (double)cn * one_over_n;
+                            double pno = 1.0 - w * w;
+                            pno = fmax(DBL_EPSILON, pno);
+                            pno = fmin(1.0 - DBL_EPSILON, pno);
+                            kc = log_prob / log(pno);
+                        }
+                        lr = rec ? lane : -1;
+    #pragma unroll
+                        for (int off = 1; off < 64; off <<= 1) {
+                            const int y = __shfl_up(lr, off);
+                            if (lane >= off) lr = max(lr, y);
+                        }
+                        int lre = __shfl_up(lr, 1);
+                        if (lane == 0) lre = -1;
+                        const double kb_rec = __shfl(kc, lre < 0 ? 0 : lre);
+                        const double kb = lre < 0 ? k0 : kb_rec;
+                        const uint64_t m1 = __ballot(act && !((double)(it0 + lane) < kb));
+                        const int stop1 = m1 ? __ffsll((unsigned long long)m1) - 1 : 64;
+                        const int stop2 = (kMaxTrials - 1) - it0;
+                        int proc, it;
+                        bool done;
+                        if (stop1 < nb && stop1 <= stop2) { proc = stop1; it = it0 + stop1; done = true; }
+                        else if (stop2 < nb) { proc = stop2 + 1; it = it0 + stop2 + 1; done = true; }
+                        else { proc = nb; it = it0 + nb; done = false; }
+                        const uint64_t rm = __ballot(rec) & (proc >= 64 ? ~0ull : ((1ull << proc) - 1ull));
+                        double kf = k0;
+                        if (rm) {
+                            const int L = 63 - __clzll(rm);
+                            kf = __shfl(kc, L);
+                            if (lane == L) {
+                                S.best = cn; S.best_s0 = S.s0[L]; S.best_s1 = S.s1[L]; S.have = 1; S.k = kc;
+                            }
+                        }
+                        if (!done && (S.fail || !((double)it < kf))) done = true;
+                        if (lane == 0) {
+                            S.iterations = it;
+                            S.done = done;
+                        }
+                    }
+                    __syncthreads();
+                    SUPP_T(3);
+    #ifdef SPSLAM_SUPP_PROF
+                    if (t == 0) pr[6]++;
+    #endif
+                }
+            } else {
+                // wave 0: one speculative round's samples from trial it0 on, into buffer sb_ (S.s0 / S.s1 or S.s0x /
+                // S.s1x; S.nbb[sb_] trials, S.failb[sb_]: 1000 failed samples came first)
+                auto sample = [&](int sb_, int it0) __attribute__((always_inline)) {
                     int nb = 0, chk = 0;  // chk: failed samples of the trial being drawn
                     bool fail = false;
                     while (nb < kBatch && it0 + nb < kMaxTrials) {
@@ -357,7 +518,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
                             // Branch-free: entries 0 and 1 live in r0 / r1 (their LDS slots are never read), so
                             // a swap that does not touch LDS reads and writes slot 0 (first swap) or 1 (second)
                             // as a sink; per pair two reads, then two writes, and selects.
-#pragma unroll 4
+    #pragma unroll 4
                             for (int c = 0; c < 32; c++) {
                                 const int j0 = __builtin_amdgcn_readlane((int)jv, 2 * c), j1 = __builtin_amdgcn_readlane((int)jv, 2 * c + 1);
                                 const int i0 = j0 > 1 ? j0 : 0, i1 = j1 > 1 ? j1 : 1;
@@ -390,48 +551,24 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
                         const int gi = __ffsll((unsigned long long)m) - 1;
                         if (chk + (gi - qh) >= 1000) { fail = true; break; }  // 1000 failed samples first
                         const int s0v = __builtin_amdgcn_readlane(bp0, gi), s1v = __builtin_amdgcn_readlane(bp1, gi);
-                        if (lane == 0) { S.s0[nb] = s0v; S.s1[nb] = s1v; }
+                        if (lane == 0) { (sb_ ? S.s0x : S.s0)[nb] = s0v; (sb_ ? S.s1x : S.s1)[nb] = s1v; }
                         nb++;
                         chk = 0;
                         qh = gi + 1;
                     }
-                    if (lane == 0) { S.nb = nb; S.fail = fail; }
-                }
-                __syncthreads();
-                SUPP_T(1);
-                const int nb = S.nb;
-                {
-                    // kBatch / NW trials per wave, NW lanes per trial each counting every NW-th point (the lanes of
-                    // a point phase read the same point: an LDS broadcast)
-                    constexpr int NW = NT / 64;
-                    const int c = wave * (kBatch / NW) + lane / NW, qq = lane % NW;
-                    int cnt = 0;
-                    if (c < nb) {
-                        float L[6];
-                        line_from_samples(Q[S.s0[c]], Q[S.s1[c]], L);
-                        float ld[3] = {L[3], L[4], L[5]};
-                        normalize4(ld);
-#pragma unroll 1
-                        for (int i = qq; i < n; i += NW) cnt += line_sqd(L, ld, Q[i]) <= thr;
-                    }
-#pragma unroll
-                    for (int o = 1; o < NW; o <<= 1) cnt += __shfl_xor(cnt, o);
-                    if (qq == 0 && c < nb) S.cnt[c] = cnt;
-                }
-                __syncthreads();
-                SUPP_T(2);
-                if (wave == 0) {
-                    // computeModel's bookkeeping over the round's trials, in parallel (lane c = trial c): a
-                    // trial improves the model when its count beats the best so far (exclusive prefix max);
-                    // k changes only there, so the k each trial's `iterations < k` test sees is the k of the
-                    // last improvement before it; the loop stops at the first failed test, or after trial
-                    // 1000 - iterations (max_iterations_)
+                    if (lane == 0) { S.nbb[sb_] = nb; S.failb[sb_] = fail; }
+                };
+                // wave 0: computeModel's bookkeeping over the round's trials in buffer sb_, in parallel (lane c = trial
+                // c): a trial improves the model when its count beats the best so far (exclusive prefix max); k changes
+                // only there, so the k each trial's `iterations < k` test sees is the k of the last improvement before
+                // it; the loop stops at the first failed test, or after trial 1000 - iterations (max_iterations_)
+                auto decide = [&](int sb_, int nb) __attribute__((always_inline)) {
                     const int it0 = S.iterations, best0 = S.best;
                     const double k0 = S.k;
                     const bool act = lane < nb;
                     const int cn = act ? S.cnt[lane] : INT_MIN;
                     int pm = cn, lr;
-#pragma unroll
+    #pragma unroll
                     for (int off = 1; off < 64; off <<= 1) {
                         const int y = __shfl_up(pm, off);
                         if (lane >= off) pm = max(pm, y);
@@ -448,7 +585,7 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
                         kc = log_prob / log(pno);
                     }
                     lr = rec ? lane : -1;
-#pragma unroll
+    #pragma unroll
                     for (int off = 1; off < 64; off <<= 1) {
                         const int y = __shfl_up(lr, off);
                         if (lane >= off) lr = max(lr, y);
@@ -471,20 +608,58 @@ __global__ __launch_bounds__(NT, NT == 256 ? SPSLAM_SUPP_MINB : 1) void supp_lin
                         const int L = 63 - __clzll(rm);
                         kf = __shfl(kc, L);
                         if (lane == L) {
-                            S.best = cn; S.best_s0 = S.s0[L]; S.best_s1 = S.s1[L]; S.have = 1; S.k = kc;
+                            S.best = cn; S.best_s0 = (sb_ ? S.s0x : S.s0)[L]; S.best_s1 = (sb_ ? S.s1x : S.s1)[L];
+                            S.have = 1; S.k = kc;
                         }
                     }
-                    if (!done && (S.fail || !((double)it < kf))) done = true;
+                    if (!done && (S.failb[sb_] || !((double)it < kf))) done = true;
                     if (lane == 0) {
                         S.iterations = it;
                         S.done = done;
                     }
-                }
+                };
+                // the next round's samples (wave 0) drawn while the other waves count this round's inliers: the
+                // draws do not depend on the counts, and a round the bookkeeping does not reach is discarded (the
+                // reference discards its RNG too); the next round starts at trial iterations + this round's trials,
+                // which is where the bookkeeping continues whenever it does not stop
+                if (wave == 0 && !S.done) sample(0, 0);
                 __syncthreads();
-                SUPP_T(3);
+                SUPP_T(1);
+                int cur = 0;
+                while (!S.done) {
+                    const int nb = S.nbb[cur];
+                    if (wave == 0) {
+                        if (!S.failb[cur]) sample(cur ^ 1, S.iterations + nb);
+                        else if (lane == 0) { S.nbb[cur ^ 1] = 0; S.failb[cur ^ 1] = 1; }
+                    } else {
+                        // NW - 1 counting waves: NW - 1 lanes per trial, each counting every (NW - 1)-th point; the
+                        // partial counts are integers, so their LDS additions give the same total in any order
+                        constexpr int LP = NT / 64 - 1;
+                        const int u = t - 64, c = u / LP, qq = u - c * LP;
+                        if (c < nb) {
+                            float L[6];
+                            line_from_samples(Q[(cur ? S.s0x : S.s0)[c]], Q[(cur ? S.s1x : S.s1)[c]], L);
+                            float ld[3] = {L[3], L[4], L[5]};
+                            normalize4(ld);
+                            int cnt = 0;
+#pragma unroll 1
+                            for (int i = qq; i < n; i += LP) cnt += line_sqd(L, ld, Q[i]) <= thr;
+                            atomicAdd(&S.cnt[c], cnt);
+                        }
+                    }
+                    __syncthreads();
+                    SUPP_T(2);
+                    if (wave == 0) {
+                        decide(cur, nb);
+                        S.cnt[lane] = 0;  // (each lane read its own count above)
+                    }
+                    __syncthreads();
+                    SUPP_T(3);
 #ifdef SPSLAM_SUPP_PROF
-                if (t == 0) pr[6]++;
+                    if (t == 0) pr[6]++;
 #endif
+                    cur ^= 1;
+                }
             }
             // ---------------- inliers, optimizeModelCoefficients, refined inliers
             int n_inl = 0;
