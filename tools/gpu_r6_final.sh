@@ -8,10 +8,10 @@ cd ${GRAFT_REPO_ROOT:-.}
 mkdir -p gpurun_out
 case $1 in
   A)
-    bash tools/gpu_run.sh r6f tests smoke || exit 1
-    timeout -k 10 600 python bench.py > gpurun_out/r6f_bench_c2.json 2> gpurun_out/r6f_bench_c2.err || exit 1
-    cut -c1-300 gpurun_out/r6f_bench_c2.json
-    bash tools/gpu_run.sh r6f prof:c2 pmc:c2 || exit 1 ;;
+    bash tools/gpu_run.sh ${TAG:-r6f} tests smoke || exit 1
+    timeout -k 10 600 python bench.py > gpurun_out/${TAG:-r6f}_bench_c2.json 2> gpurun_out/${TAG:-r6f}_bench_c2.err || exit 1
+    cut -c1-300 gpurun_out/${TAG:-r6f}_bench_c2.json
+    bash tools/gpu_run.sh ${TAG:-r6f} prof:c2 pmc:c2 || exit 1 ;;
   B)
     for c in ${CONFIGS:-c3 c1 c4 c5}; do
       # (a heartbeat line a minute: C5's CPU baseline and ATE legs run minutes without output)
