@@ -56,6 +56,10 @@ constexpr int kSegThreads = SPSLAM_SEG_THREADS;
 constexpr int kSegWaves = kSegThreads / 64;
 constexpr int kMaxBig = 255;          // components > MinSize per frame (u8 tags)
 constexpr int kMaxRowWords = 8;       // W <= 512
+#ifndef SPSLAM_SEG_COV_AHEAD
+#define SPSLAM_SEG_COV_AHEAD 4
+#endif
+constexpr int kPD = SPSLAM_SEG_COV_AHEAD;  // phase G: member coordinate chunks in flight per wave
 constexpr int kLdsBytes = 160 * 1024;
 
 struct SegShared {
@@ -1050,15 +1054,7 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
         const int n = S.big_size[j], o = S.big_off[j];
         float* st = &S.stage[wave][0][0];
         float acc = 0.f;
-        // member indices two chunks ahead, coordinates one chunk ahead
-        auto idx_at = [&](int c0) { return c0 + lane < n ? mem_at(o + c0 + lane) : -1; };
-        int icur = idx_at(0), inext = idx_at(64);
-        float px = 0.f, py = 0.f, pz = 0.f;
-        if (icur >= 0) { px = X[icur]; py = Y[icur]; pz = Z[icur]; }
-        for (int c0 = 0; c0 < n; c0 += 64) {
-            const int i2 = idx_at(c0 + 128);
-            float nx = 0.f, ny = 0.f, nz = 0.f;
-            if (inext >= 0) { nx = X[inext]; ny = Y[inext]; nz = Z[inext]; }
+        auto chunk = [&](int c0, float px, float py, float pz) __attribute__((always_inline)) {
             const int cnt = min(64, n - c0), pad = (cnt + 3) & ~3;
             if (lane < cnt) {
                 st[0 * 64 + lane] = px * px; st[1 * 64 + lane] = px * py; st[2 * 64 + lane] = px * pz;
@@ -1090,8 +1086,45 @@ __global__ __launch_bounds__(kSegThreads) void plane_segment_kernel(
                 }
             }
             wave_sync();
-            px = nx; py = ny; pz = nz;
-            inext = i2;
+        };
+        if constexpr (K <= 4) {
+            // coordinates kPD chunks ahead (a chunk's adds take ~0.3 us, a cloud load's round trip several times that:
+            // with one chunk ahead the walk waited on every chunk's loads), member indices (LDS) one chunk further
+            auto idx_at = [&](int c0) { return c0 + lane < n ? mem_at(o + c0 + lane) : -1; };
+            float cx[kPD], cy[kPD], cz[kPD];
+#pragma unroll
+            for (int d = 0; d < kPD; d++) {
+                const int id = idx_at(64 * d);
+                cx[d] = 0.f; cy[d] = 0.f; cz[d] = 0.f;
+                if (id >= 0) { cx[d] = X[id]; cy[d] = Y[id]; cz[d] = Z[id]; }
+            }
+            int inext = idx_at(64 * kPD);
+            for (int c00 = 0; c00 < n; c00 += 64 * kPD)
+#pragma unroll
+            for (int d = 0; d < kPD; d++) {
+                const int c0 = c00 + 64 * d;
+                if (c0 >= n) break;  // (uniform)
+                const float px = cx[d], py = cy[d], pz = cz[d];
+                cx[d] = 0.f; cy[d] = 0.f; cz[d] = 0.f;
+                if (inext >= 0) { cx[d] = X[inext]; cy[d] = Y[inext]; cz[d] = Z[inext]; }
+                inext = idx_at(c0 + 64 * (kPD + 1));
+                chunk(c0, px, py, pz);
+            }
+        } else {
+            // member indices two chunks ahead, coordinates one chunk ahead (the 512-wide instance: more lookahead
+            // spills there)
+            auto idx_at = [&](int c0) { return c0 + lane < n ? mem_at(o + c0 + lane) : -1; };
+            int icur = idx_at(0), inext = idx_at(64);
+            float px = 0.f, py = 0.f, pz = 0.f;
+            if (icur >= 0) { px = X[icur]; py = Y[icur]; pz = Z[icur]; }
+            for (int c0 = 0; c0 < n; c0 += 64) {
+                const int i2 = idx_at(c0 + 128);
+                float nx = 0.f, ny = 0.f, nz = 0.f;
+                if (inext >= 0) { nx = X[inext]; ny = Y[inext]; nz = Z[inext]; }
+                chunk(c0, px, py, pz);
+                px = nx; py = ny; pz = nz;
+                inext = i2;
+            }
         }
         if (lane < 9) acc /= (float)n;
         float a[9];
