@@ -15,11 +15,11 @@ case $1 in
   B)
     for c in ${CONFIGS:-c3 c1 c4 c5}; do
       # (a heartbeat line a minute: C5's CPU baseline and ATE legs run minutes without output)
-      timeout -k 10 900 python bench.py --config $c > gpurun_out/r6f_bench_$c.json 2> gpurun_out/r6f_bench_$c.err &
+      timeout -k 10 900 python bench.py --config $c > gpurun_out/${TAG:-r6f}_bench_$c.json 2> gpurun_out/${TAG:-r6f}_bench_$c.err &
       pid=$!
       while kill -0 $pid 2> /dev/null; do sleep 60; echo "   $c running $(date +%T)"; done
       wait $pid || exit 1
-      cut -c1-200 gpurun_out/r6f_bench_$c.json
+      cut -c1-200 gpurun_out/${TAG:-r6f}_bench_$c.json
     done ;;
 esac
 echo "== done $(date +%T)"
